@@ -1,0 +1,185 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: ALS batch-layer ratings/sec on MI355X (BASELINE.json).
+
+``python bench.py --gpus N --steps K --warmup W``; for N > 1 launch one rank per GPU with
+``torch.distributed.run`` (RCCL over xGMI).  A *step* is one full ALS iteration of the batch
+layer's trainer -- item half-step + user half-step: all-reduce of the partial Gramians,
+the fused HIP gather/MFMA-Gramian/Cholesky solve of every owned row, and the all-gather of
+the new bf16 factor shard -- over the whole synthetic ratings matrix.
+
+Config (BASELINE.json "ALS rank=64 bf16 on 25M synthetic ratings, 1 MI355X"): implicit ALS,
+rank 64, lambda 0.001, alpha 1 (reference defaults except rank), bf16 factors with fp32
+accumulation and fp32 solves.  Weak scaling: every rank owns 25M ratings of its own 162,541
+users (MovieLens-25M-like shape) over a shared catalogue of 59,047 items with skewed
+popularity; the all-to-all that repartitions ratings by item happens once, before timing.
+
+Prints ONE JSON line (rank 0).  ``value`` = total ratings processed per second over all
+ranks = (global nnz * K) / max-over-ranks(time of K steps).  Extra fields report the
+speed-layer fold-in latency for a 10k-event micro-batch (the second half of the metric).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def _gen_ratings(n_local_users: int, n_items: int, nnz: int, rank: int, seed: int, device):
+    """Unique (user, item, strength) triples for this rank's users, skewed activity/popularity."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed * 7919 + rank)
+    u_lo = rank * n_local_users
+    have = torch.empty(0, dtype=torch.int64, device=device)
+    want = nnz
+    while have.numel() < want:
+        m = int((want - have.numel()) * 1.25) + 1024
+        u = (n_local_users * torch.rand(m, generator=g, device=device).pow(1.3)).to(torch.int64)
+        i = (n_items * torch.rand(m, generator=g, device=device).pow(2.5)).to(torch.int64)
+        u = u.clamp_(0, n_local_users - 1)
+        i = i.clamp_(0, n_items - 1)
+        have = torch.unique(torch.cat([have, u * n_items + i]))
+    keep = torch.randperm(have.numel(), generator=g, device=device)[:want]
+    key = have[keep]
+    users = torch.div(key, n_items, rounding_mode="floor") + u_lo
+    items = key % n_items
+    strength = torch.randint(1, 11, (want,), generator=g, device=device).to(torch.float32) * 0.5
+    return users, items, strength
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--rank-k", type=int, default=64, help="ALS rank (features)")
+    ap.add_argument("--ratings-per-gpu", type=int, default=25_000_000)
+    ap.add_argument("--users-per-gpu", type=int, default=162_541)
+    ap.add_argument("--items", type=int, default=59_047)
+    ap.add_argument("--implicit", type=int, default=1)
+    ap.add_argument("--speed-events", type=int, default=10_000)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--device", default="auto")
+    args = ap.parse_args(argv)
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oryx_amd.parallel import dist
+    from oryx_amd.models.als.trainer import ALSTrainer
+    from oryx_amd.ops import als as als_ops
+    from oryx_amd.utils import mathx
+
+    ctx = dist.init_from_env(device=args.device)
+    if ctx.world_size != args.gpus and ctx.is_main:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, ctx.world_size),
+              file=sys.stderr)
+    dev = ctx.device
+    W = ctx.world_size
+    n_users = args.users_per_gpu * W
+    users, items, strength = _gen_ratings(args.users_per_gpu, args.items, args.ratings_per_gpu,
+                                          ctx.rank, args.seed, dev)
+    trainer = ALSTrainer(args.rank_k, lam=0.001, alpha=1.0, implicit=bool(args.implicit),
+                         ctx=ctx, seed=args.seed)
+    trainer.prepare(users, items, strength, n_users, args.items)
+    del users, items, strength
+    trainer.init_factors()
+    nnz_local = torch.tensor([float(trainer.local_nnz)], dtype=torch.float64, device=dev)
+    dist.all_reduce_sum(nnz_local, ctx)
+    global_nnz = int(nnz_local.item())
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        trainer.iterate(1)
+    sync()
+    dist.barrier(ctx)
+    sync()
+    t0 = time.perf_counter()
+    trainer.iterate(args.steps)
+    sync()
+    dist.barrier(ctx)
+    sync()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if ctx.is_distributed:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / max(1, args.steps)
+    ratings_per_sec = global_nnz * args.steps / elapsed
+
+    # ---- speed layer: fold-in latency of one micro-batch of new events (rank 0's GPU)
+    speed_ms = None
+    if ctx.is_main and args.speed_events > 0:
+        k = args.rank_k
+        Xf = trainer.X[:, :k]
+        Yf = trainer.Y[:, :k]
+        g = torch.Generator(device=dev)
+        g.manual_seed(99)
+        B = args.speed_events
+        ui = torch.randint(0, Xf.shape[0], (B,), generator=g, device=dev)
+        ii = torch.randint(0, Yf.shape[0], (B,), generator=g, device=dev)
+        vals = torch.rand(B, generator=g, device=dev) * 4 + 0.5
+        present = torch.ones(B, dtype=torch.bool, device=dev)
+        times = []
+        for rep in range(4):
+            sync()
+            t1 = time.perf_counter()
+            # Gramians of the live factors + host RRQR solvers, then batched fold-in both ways
+            xtx = als_ops.gramian(Xf).double().cpu().numpy()
+            yty = als_ops.gramian(Yf).double().cpu().numpy()
+            yinv = torch.from_numpy(mathx.get_solver(yty).inverse()).to(dev)
+            xinv = torch.from_numpy(mathx.get_solver(xtx).inverse()).to(dev)
+            xu = Xf[ui]
+            yi = Yf[ii]
+            nx, vx = als_ops.fold_in(yinv, vals, xu, present, yi, True)
+            ny, vy = als_ops.fold_in(xinv, vals, yi, present, xu, True)
+            out = torch.cat([nx, ny]).cpu()
+            sync()
+            times.append((time.perf_counter() - t1) * 1e3)
+        speed_ms = min(times[1:])
+
+    if ctx.is_main:
+        rec = {
+            "metric": "ALS batch-layer ratings/sec + speed-layer model-update latency, 1/2/4/8 MI355X",
+            "value": ratings_per_sec,
+            "unit": "ratings/s",
+            "n_gpus": W,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (power-law users x items, unique pairs, strengths 0.5..5), "
+                    "random-init unit-Gaussian factors",
+            "config": {
+                "model": "ALS implicit rank=%d lambda=0.001 alpha=1 (MLlib normal equations)"
+                         % args.rank_k,
+                "global_batch": global_nnz,
+                "seq_len": None,
+                "parallelism": "dp%d (user/item row shards, RCCL all-reduce YtY + all-gather "
+                               "factors)" % W,
+                "ratings_per_gpu": args.ratings_per_gpu,
+                "users": n_users,
+                "items": args.items,
+                "step": "1 ALS iteration (items+users half-steps)",
+            },
+            "speed_layer_update_ms": speed_ms,
+            "speed_layer_events": args.speed_events,
+            "solve_failures": trainer.failures,
+        }
+        print(json.dumps(rec), flush=True)
+    if ctx.is_distributed:
+        dist.barrier(ctx)
+        torch.distributed.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,598 @@
+// oryx_log.cpp -- framework-owned append-only log (the Kafka/ZooKeeper replacement).
+//
+// The reference moves every inter-layer message over Kafka 0.8 topics (input: keyed,
+// 4 partitions; update: 1 partition, replayed from the beginning by speed/serving) and keeps
+// consumer-group offsets in ZooKeeper ([lambda]/TopicProducerImpl.java:32-84,
+// [kafka]/KafkaUtils.java:57-161, deploy/bin/oryx-run.sh:330-344).  Nothing like that exists
+// on an MI355X node, so this is a small native log with the same semantics:
+//
+//   <root>/<topic>/meta                     partitions, max message bytes, segment bytes
+//   <root>/<topic>/<p>/<base-offset>.log    segment files of framed records
+//   <root>/<topic>/.offsets/<group>         committed "partition offset" lines
+//
+// Record frame (little endian):  u32 magic | u32 crc32(payload) | u64 offset | i64 ts_ms |
+//                                u32 key_len (0xFFFFFFFF = null) | u32 value_len | key | value
+// Appends from any process are serialised with flock() on the partition directory's lock
+// file and written with one write() so readers in other processes never see torn frames
+// (a frame is only consumed once its full length and CRC check out).  Readers tail segment
+// files by position, so consumers in other processes need no shared memory.
+//
+// C ABI for ctypes; every call releases nothing (ctypes drops the GIL around the call).
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <dirent.h>
+#include <fcntl.h>
+#include <mutex>
+#include <string>
+#include <sys/file.h>
+#include <sys/stat.h>
+#include <sys/types.h>
+#include <thread>
+#include <unistd.h>
+#include <vector>
+
+namespace {
+
+constexpr uint32_t kMagic = 0x4F52594Cu;  // "ORYL"
+constexpr size_t kHeader = 4 + 4 + 8 + 8 + 4 + 4;
+constexpr uint32_t kNullKey = 0xFFFFFFFFu;
+
+uint32_t crc_table[256];
+std::once_flag crc_once;
+
+void init_crc() {
+  for (uint32_t i = 0; i < 256; ++i) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+    crc_table[i] = c;
+  }
+}
+
+uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc = 0) {
+  std::call_once(crc_once, init_crc);
+  crc = ~crc;
+  for (size_t i = 0; i < n; ++i) crc = crc_table[(crc ^ p[i]) & 0xFF] ^ (crc >> 8);
+  return ~crc;
+}
+
+thread_local std::string g_err;
+
+int fail(const std::string& msg) {
+  g_err = msg + (errno ? std::string(": ") + strerror(errno) : std::string());
+  return -1;
+}
+
+bool mkdirs(const std::string& path) {
+  if (path.empty()) return true;
+  struct stat st;
+  if (stat(path.c_str(), &st) == 0) return S_ISDIR(st.st_mode);
+  size_t slash = path.find_last_of('/');
+  if (slash != std::string::npos && slash > 0 && !mkdirs(path.substr(0, slash))) return false;
+  return mkdir(path.c_str(), 0755) == 0 || errno == EEXIST;
+}
+
+int64_t now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(
+             std::chrono::system_clock::now().time_since_epoch()).count();
+}
+
+std::vector<int64_t> list_segments(const std::string& dir) {
+  std::vector<int64_t> bases;
+  DIR* d = opendir(dir.c_str());
+  if (!d) return bases;
+  while (struct dirent* e = readdir(d)) {
+    std::string n = e->d_name;
+    if (n.size() > 4 && n.compare(n.size() - 4, 4, ".log") == 0) {
+      char* end = nullptr;
+      long long v = strtoll(n.c_str(), &end, 10);
+      if (end && std::string(end) == ".log") bases.push_back(v);
+    }
+  }
+  closedir(d);
+  std::sort(bases.begin(), bases.end());
+  return bases;
+}
+
+std::string seg_name(const std::string& dir, int64_t base) {
+  char buf[32];
+  snprintf(buf, sizeof(buf), "%020lld.log", (long long)base);
+  return dir + "/" + buf;
+}
+
+// MurmurHash2 (the hash Kafka's default partitioner uses), positive modulo partitions.
+uint32_t murmur2(const uint8_t* data, int len) {
+  const uint32_t seed = 0x9747b28c, m = 0x5bd1e995;
+  const int r = 24;
+  uint32_t h = seed ^ (uint32_t)len;
+  int len4 = len / 4;
+  for (int i = 0; i < len4; ++i) {
+    int i4 = i * 4;
+    uint32_t k = (data[i4 + 0] & 0xff) + ((data[i4 + 1] & 0xff) << 8) +
+                 ((data[i4 + 2] & 0xff) << 16) + ((uint32_t)(data[i4 + 3] & 0xff) << 24);
+    k *= m; k ^= k >> r; k *= m; h *= m; h ^= k;
+  }
+  switch (len % 4) {
+    case 3: h ^= (uint32_t)(data[(len & ~3) + 2] & 0xff) << 16; [[fallthrough]];
+    case 2: h ^= (uint32_t)(data[(len & ~3) + 1] & 0xff) << 8; [[fallthrough]];
+    case 1: h ^= (uint32_t)(data[len & ~3] & 0xff); h *= m;
+  }
+  h ^= h >> 13; h *= m; h ^= h >> 15;
+  return h;
+}
+
+struct Partition {
+  std::string dir;
+  int lock_fd = -1;
+  // cached tail of the active segment (validated under the lock on every append)
+  int64_t c_base = -1, c_pos = 0, c_next = 0;
+};
+
+struct Topic {
+  std::string root, name, dir;
+  int partitions = 1;
+  int64_t max_message = 16777216;
+  int64_t segment_bytes = 64ll << 20;
+  std::vector<Partition> parts;
+  std::mutex mu;
+  uint32_t rr = 0;
+};
+
+bool read_meta(Topic* t) {
+  FILE* f = fopen((t->dir + "/meta").c_str(), "r");
+  if (!f) return false;
+  int p = 0;
+  long long mm = 0, sb = 0;
+  int n = fscanf(f, "partitions=%d\nmax-message=%lld\nsegment-bytes=%lld", &p, &mm, &sb);
+  fclose(f);
+  if (n < 1 || p <= 0) return false;
+  t->partitions = p;
+  if (n >= 2 && mm > 0) t->max_message = mm;
+  if (n >= 3 && sb > 0) t->segment_bytes = sb;
+  return true;
+}
+
+bool write_meta(Topic* t) {
+  std::string tmp = t->dir + "/.meta.tmp." + std::to_string(getpid());
+  FILE* f = fopen(tmp.c_str(), "w");
+  if (!f) return false;
+  fprintf(f, "partitions=%d\nmax-message=%lld\nsegment-bytes=%lld\n", t->partitions,
+          (long long)t->max_message, (long long)t->segment_bytes);
+  fflush(f);
+  fsync(fileno(f));
+  fclose(f);
+  // first creator wins: link() fails if meta already exists
+  if (link(tmp.c_str(), (t->dir + "/meta").c_str()) != 0) {
+    unlink(tmp.c_str());
+    return read_meta(t);
+  }
+  unlink(tmp.c_str());
+  return true;
+}
+
+// Scan a segment from byte position `pos`; returns the next offset and fills `end_pos` with
+// the position after the last complete frame.
+int64_t scan_segment(const std::string& path, int64_t base, int64_t* end_pos,
+                     int64_t start_pos = 0, int64_t start_next = -1) {
+  int fd = open(path.c_str(), O_RDONLY);
+  if (fd < 0) { *end_pos = 0; return base; }
+  int64_t pos = start_pos, next = start_next >= 0 ? start_next : base;
+  uint8_t hdr[kHeader];
+  std::vector<uint8_t> payload;
+  for (;;) {
+    ssize_t r = pread(fd, hdr, kHeader, pos);
+    if (r != (ssize_t)kHeader) break;
+    uint32_t magic, crc, klen, vlen;
+    uint64_t off;
+    memcpy(&magic, hdr, 4); memcpy(&crc, hdr + 4, 4); memcpy(&off, hdr + 8, 8);
+    memcpy(&klen, hdr + 24, 4); memcpy(&vlen, hdr + 28, 4);
+    if (magic != kMagic) break;
+    size_t plen = (klen == kNullKey ? 0 : klen) + (size_t)vlen;
+    payload.resize(plen + 16);
+    memcpy(payload.data(), hdr + 8, 16);
+    if (plen && pread(fd, payload.data() + 16, plen, pos + kHeader) != (ssize_t)plen) break;
+    if (crc32(payload.data(), plen + 16) != crc) break;
+    pos += kHeader + plen;
+    next = (int64_t)off + 1;
+  }
+  close(fd);
+  *end_pos = pos;
+  return next;
+}
+
+struct Reader {
+  Topic* topic;
+  int part;
+  int64_t seg_base = -1;
+  int64_t pos = 0;
+  int64_t next_offset = 0;
+  int fd = -1;
+};
+
+// Position a reader at `offset` (clamped to [begin, end]).
+void reader_seek(Reader* r, int64_t offset) {
+  const std::string& dir = r->topic->parts[r->part].dir;
+  std::vector<int64_t> segs = list_segments(dir);
+  if (r->fd >= 0) { close(r->fd); r->fd = -1; }
+  if (segs.empty()) { r->seg_base = 0; r->pos = 0; r->next_offset = 0; return; }
+  if (offset < segs.front()) offset = segs.front();
+  size_t idx = 0;
+  for (size_t i = 0; i < segs.size(); ++i) if (segs[i] <= offset) idx = i;
+  r->seg_base = segs[idx];
+  r->pos = 0;
+  r->next_offset = segs[idx];
+  r->fd = open(seg_name(dir, segs[idx]).c_str(), O_RDONLY);
+  // skip frames before offset
+  uint8_t hdr[kHeader];
+  while (r->fd >= 0 && r->next_offset < offset) {
+    if (pread(r->fd, hdr, kHeader, r->pos) != (ssize_t)kHeader) break;
+    uint32_t magic, klen, vlen;
+    uint64_t off;
+    memcpy(&magic, hdr, 4); memcpy(&off, hdr + 8, 8); memcpy(&klen, hdr + 24, 4);
+    memcpy(&vlen, hdr + 28, 4);
+    if (magic != kMagic) break;
+    int64_t plen = (klen == kNullKey ? 0 : klen) + (int64_t)vlen;
+    struct stat st;
+    if (fstat(r->fd, &st) != 0 || st.st_size < r->pos + (int64_t)kHeader + plen) break;
+    r->pos += kHeader + plen;
+    r->next_offset = (int64_t)off + 1;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* oryx_log_last_error() { return g_err.c_str(); }
+
+// Opens (creating when `create_partitions` > 0) a topic.  Returns a handle or nullptr.
+void* oryx_log_open(const char* root, const char* topic, int create_partitions,
+                    long long max_message, long long segment_bytes) {
+  errno = 0;
+  auto* t = new Topic();
+  t->root = root;
+  t->name = topic;
+  t->dir = std::string(root) + "/" + topic;
+  if (!read_meta(t)) {
+    if (create_partitions <= 0) {
+      g_err = "topic does not exist: " + t->name;
+      delete t;
+      return nullptr;
+    }
+    if (!mkdirs(t->dir)) { fail("mkdir " + t->dir); delete t; return nullptr; }
+    t->partitions = create_partitions;
+    if (max_message > 0) t->max_message = max_message;
+    if (segment_bytes > 0) t->segment_bytes = segment_bytes;
+    if (!write_meta(t)) { fail("write meta"); delete t; return nullptr; }
+  }
+  t->parts.resize(t->partitions);
+  for (int p = 0; p < t->partitions; ++p) {
+    t->parts[p].dir = t->dir + "/" + std::to_string(p);
+    if (!mkdirs(t->parts[p].dir)) { fail("mkdir partition"); delete t; return nullptr; }
+    t->parts[p].lock_fd = open((t->parts[p].dir + "/.lock").c_str(), O_RDWR | O_CREAT, 0644);
+  }
+  return t;
+}
+
+int oryx_log_exists(const char* root, const char* topic) {
+  std::string meta = std::string(root) + "/" + topic + "/meta";
+  struct stat st;
+  return stat(meta.c_str(), &st) == 0 ? 1 : 0;
+}
+
+void oryx_log_close(void* h) {
+  auto* t = static_cast<Topic*>(h);
+  if (!t) return;
+  for (auto& p : t->parts) if (p.lock_fd >= 0) close(p.lock_fd);
+  delete t;
+}
+
+int oryx_log_num_partitions(void* h) { return static_cast<Topic*>(h)->partitions; }
+long long oryx_log_max_message(void* h) { return static_cast<Topic*>(h)->max_message; }
+
+int oryx_log_partition_for(void* h, const char* key, int key_len) {
+  auto* t = static_cast<Topic*>(h);
+  if (key_len < 0 || !key) {
+    std::lock_guard<std::mutex> g(t->mu);
+    return (int)(t->rr++ % (uint32_t)t->partitions);
+  }
+  return (int)((murmur2((const uint8_t*)key, key_len) & 0x7fffffffu) % (uint32_t)t->partitions);
+}
+
+// Appends `n` records packed as [i32 key_len(-1=null)][i64 value_len][key][value]... to one
+// partition (-1: per record by key / round robin).  Returns the last offset written, or -1.
+// Each record's offset is written to out_offsets when non-null.
+long long oryx_log_append_batch(void* h, int partition, const char* buf, long long buf_len,
+                                int n, long long ts_ms, int do_fsync, long long* out_offsets) {
+  auto* t = static_cast<Topic*>(h);
+  errno = 0;
+  if (ts_ms < 0) ts_ms = now_ms();
+  // Group records by destination partition, preserving order within a partition.
+  std::vector<std::vector<std::pair<const char*, int>>> groups(t->partitions);
+  std::vector<std::vector<int>> idx(t->partitions);
+  const char* p = buf;
+  const char* end = buf + buf_len;
+  std::vector<int> rec_part(n);
+  std::vector<const char*> rec_ptr(n);
+  for (int i = 0; i < n; ++i) {
+    if (p + 12 > end) { g_err = "truncated batch"; return -1; }
+    int32_t klen; int64_t vlen;
+    memcpy(&klen, p, 4); memcpy(&vlen, p + 4, 8);
+    const char* key = p + 12;
+    int64_t rec_bytes = 12 + (klen < 0 ? 0 : klen) + vlen;
+    if (p + rec_bytes > end) { g_err = "truncated batch"; return -1; }
+    if (vlen + (klen < 0 ? 0 : klen) > t->max_message) {
+      g_err = "message of " + std::to_string(vlen) + " bytes exceeds max message size " +
+              std::to_string(t->max_message);
+      return -2;
+    }
+    int part = partition >= 0 ? partition : oryx_log_partition_for(h, klen < 0 ? nullptr : key, klen);
+    if (part >= t->partitions) { g_err = "bad partition"; return -1; }
+    rec_part[i] = part;
+    rec_ptr[i] = p;
+    idx[part].push_back(i);
+    p += rec_bytes;
+  }
+  long long last = -1;
+  for (int part = 0; part < t->partitions; ++part) {
+    if (idx[part].empty()) continue;
+    Partition& P = t->parts[part];
+    if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_EX);
+    std::vector<int64_t> segs = list_segments(P.dir);
+    int64_t base = segs.empty() ? 0 : segs.back();
+    int64_t end_pos = 0;
+    int64_t next = 0;
+    if (!segs.empty()) {
+      if (P.c_base == base)
+        next = scan_segment(seg_name(P.dir, base), base, &end_pos, P.c_pos, P.c_next);
+      else
+        next = scan_segment(seg_name(P.dir, base), base, &end_pos);
+    }
+    std::string path = seg_name(P.dir, base);
+    if (!segs.empty() && end_pos >= t->segment_bytes) {
+      base = next;
+      path = seg_name(P.dir, base);
+      end_pos = 0;
+    }
+    int fd = open(path.c_str(), O_WRONLY | O_CREAT, 0644);
+    if (fd < 0) { if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN); return fail("open segment"); }
+    // truncate any torn tail left by a crashed writer
+    struct stat st;
+    if (fstat(fd, &st) == 0 && st.st_size > end_pos) { if (ftruncate(fd, end_pos) != 0) {} }
+    std::vector<uint8_t> out;
+    for (int i : idx[part]) {
+      const char* r = rec_ptr[i];
+      int32_t klen; int64_t vlen;
+      memcpy(&klen, r, 4); memcpy(&vlen, r + 4, 8);
+      uint32_t uk = klen < 0 ? kNullKey : (uint32_t)klen;
+      uint32_t uv = (uint32_t)vlen;
+      size_t plen = (klen < 0 ? 0 : klen) + (size_t)vlen;
+      size_t at = out.size();
+      out.resize(at + kHeader + plen);
+      uint8_t* f = out.data() + at;
+      uint64_t off = (uint64_t)next;
+      int64_t ts = ts_ms;
+      memcpy(f, &kMagic, 4);
+      memcpy(f + 8, &off, 8);
+      memcpy(f + 16, &ts, 8);
+      memcpy(f + 24, &uk, 4);
+      memcpy(f + 28, &uv, 4);
+      memcpy(f + kHeader, r + 12, plen);
+      uint32_t crc = crc32(f + kHeader, plen, crc32(f + 8, 16));
+      memcpy(f + 4, &crc, 4);
+      if (out_offsets) out_offsets[i] = next;
+      last = next;
+      ++next;
+    }
+    ssize_t w = pwrite(fd, out.data(), out.size(), end_pos);
+    if (w != (ssize_t)out.size()) {
+      close(fd);
+      if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN);
+      return fail("write");
+    }
+    if (do_fsync) fsync(fd);
+    close(fd);
+    P.c_base = base;
+    P.c_pos = end_pos + (int64_t)out.size();
+    P.c_next = next;
+    if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN);
+  }
+  return last;
+}
+
+long long oryx_log_begin_offset(void* h, int partition) {
+  auto* t = static_cast<Topic*>(h);
+  std::vector<int64_t> segs = list_segments(t->parts[partition].dir);
+  return segs.empty() ? 0 : segs.front();
+}
+
+long long oryx_log_end_offset(void* h, int partition) {
+  auto* t = static_cast<Topic*>(h);
+  const std::string& dir = t->parts[partition].dir;
+  std::vector<int64_t> segs = list_segments(dir);
+  if (segs.empty()) return 0;
+  int64_t end_pos;
+  return scan_segment(seg_name(dir, segs.back()), segs.back(), &end_pos);
+}
+
+// Deletes whole segments whose files were last modified before `older_than_ms` (keeping the
+// active segment).  Returns the number of segments deleted.
+int oryx_log_retain(void* h, long long older_than_ms) {
+  auto* t = static_cast<Topic*>(h);
+  int deleted = 0;
+  for (auto& P : t->parts) {
+    if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_EX);
+    std::vector<int64_t> segs = list_segments(P.dir);
+    for (size_t i = 0; i + 1 < segs.size(); ++i) {
+      std::string path = seg_name(P.dir, segs[i]);
+      struct stat st;
+      if (stat(path.c_str(), &st) == 0 &&
+          (int64_t)st.st_mtime * 1000 < older_than_ms) {
+        if (unlink(path.c_str()) == 0) ++deleted;
+      } else {
+        break;
+      }
+    }
+    if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN);
+  }
+  return deleted;
+}
+
+void* oryx_reader_open(void* h, int partition, long long offset) {
+  auto* t = static_cast<Topic*>(h);
+  if (partition < 0 || partition >= t->partitions) { g_err = "bad partition"; return nullptr; }
+  auto* r = new Reader();
+  r->topic = t;
+  r->part = partition;
+  reader_seek(r, offset < 0 ? oryx_log_end_offset(h, partition) : offset);
+  return r;
+}
+
+void oryx_reader_close(void* rh) {
+  auto* r = static_cast<Reader*>(rh);
+  if (!r) return;
+  if (r->fd >= 0) close(r->fd);
+  delete r;
+}
+
+long long oryx_reader_position(void* rh) { return static_cast<Reader*>(rh)->next_offset; }
+
+void oryx_reader_seek(void* rh, long long offset) { reader_seek(static_cast<Reader*>(rh), offset); }
+
+// Reads up to `max_records` complete records into `out` as
+// [i64 offset][i64 ts][i32 key_len(-1 null)][i32 value_len][key][value]...
+// Waits up to timeout_ms for the first record.  Returns the number of records read, -1 on
+// error, or -(needed bytes)-16 when the next record alone does not fit in `out`.
+long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_records,
+                           int timeout_ms, long long* out_used) {
+  auto* r = static_cast<Reader*>(rh);
+  const std::string& dir = r->topic->parts[r->part].dir;
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  long long used = 0;
+  int count = 0;
+  uint8_t hdr[kHeader];
+  std::vector<uint8_t> payload;
+  int sleep_us = 200;
+  for (;;) {
+    if (r->fd < 0) {
+      reader_seek(r, r->next_offset);
+    }
+    bool progressed = false;
+    while (r->fd >= 0 && count < max_records) {
+      if (pread(r->fd, hdr, kHeader, r->pos) != (ssize_t)kHeader) break;
+      uint32_t magic, crc, klen, vlen;
+      uint64_t off;
+      int64_t ts;
+      memcpy(&magic, hdr, 4); memcpy(&crc, hdr + 4, 4); memcpy(&off, hdr + 8, 8);
+      memcpy(&ts, hdr + 16, 8); memcpy(&klen, hdr + 24, 4); memcpy(&vlen, hdr + 28, 4);
+      if (magic != kMagic) break;
+      size_t kl = klen == kNullKey ? 0 : klen;
+      size_t plen = kl + vlen;
+      payload.resize(16 + plen);
+      memcpy(payload.data(), hdr + 8, 16);
+      if (plen && pread(r->fd, payload.data() + 16, plen, r->pos + kHeader) != (ssize_t)plen) break;
+      if (crc32(payload.data(), 16 + plen) != crc) break;  // torn / in-progress write
+      long long need = 24 + (long long)plen;
+      if (used + need > out_cap) {
+        if (count == 0) { *out_used = 0; return -need - 16; }
+        *out_used = used;
+        return count;
+      }
+      char* o = out + used;
+      int64_t o_off = (int64_t)off;
+      int32_t o_kl = klen == kNullKey ? -1 : (int32_t)klen;
+      int32_t o_vl = (int32_t)vlen;
+      memcpy(o, &o_off, 8); memcpy(o + 8, &ts, 8); memcpy(o + 16, &o_kl, 4);
+      memcpy(o + 20, &o_vl, 4); memcpy(o + 24, payload.data() + 16, plen);
+      used += need;
+      r->pos += kHeader + plen;
+      r->next_offset = (int64_t)off + 1;
+      ++count;
+      progressed = true;
+    }
+    if (count >= max_records) break;
+    if (!progressed) {
+      // maybe the writer rolled to a new segment
+      std::vector<int64_t> segs = list_segments(dir);
+      bool rolled = false;
+      for (int64_t b : segs) {
+        if (b > r->seg_base && b <= r->next_offset) {
+          if (r->fd >= 0) close(r->fd);
+          r->seg_base = b;
+          r->pos = 0;
+          r->fd = open(seg_name(dir, b).c_str(), O_RDONLY);
+          rolled = true;
+          break;
+        }
+      }
+      if (rolled) continue;
+      if (count > 0 || std::chrono::steady_clock::now() >= deadline) break;
+      std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
+      sleep_us = std::min(sleep_us * 2, 20000);
+    } else if (count > 0) {
+      break;  // deliver what we have
+    }
+  }
+  *out_used = used;
+  return count;
+}
+
+// ---- consumer-group offsets (ZooKeeper replacement) ----
+
+static std::string offsets_path(const char* root, const char* topic, const char* group) {
+  return std::string(root) + "/" + topic + "/.offsets/" + group;
+}
+
+// Writes `n` (partition, offset) pairs atomically (tmp + fsync + rename).
+int oryx_offsets_set(const char* root, const char* topic, const char* group, int n,
+                     const int* partitions, const long long* offsets) {
+  errno = 0;
+  std::string path = offsets_path(root, topic, group);
+  if (!mkdirs(path.substr(0, path.find_last_of('/')))) return fail("mkdir offsets");
+  // merge with existing
+  std::vector<long long> cur;
+  {
+    FILE* f = fopen(path.c_str(), "r");
+    if (f) {
+      int p; long long o;
+      while (fscanf(f, "%d %lld", &p, &o) == 2) {
+        if (p >= 0 && p < 1 << 20) {
+          if ((int)cur.size() <= p) cur.resize(p + 1, -1);
+          cur[p] = o;
+        }
+      }
+      fclose(f);
+    }
+  }
+  for (int i = 0; i < n; ++i) {
+    if ((int)cur.size() <= partitions[i]) cur.resize(partitions[i] + 1, -1);
+    cur[partitions[i]] = offsets[i];
+  }
+  std::string tmp = path + ".tmp." + std::to_string(getpid());
+  FILE* f = fopen(tmp.c_str(), "w");
+  if (!f) return fail("open offsets tmp");
+  for (size_t p = 0; p < cur.size(); ++p)
+    if (cur[p] >= 0) fprintf(f, "%zu %lld\n", p, cur[p]);
+  fflush(f);
+  fsync(fileno(f));
+  fclose(f);
+  if (rename(tmp.c_str(), path.c_str()) != 0) return fail("rename offsets");
+  return 0;
+}
+
+// Returns the committed offset of one partition, or -1 if none.
+long long oryx_offsets_get(const char* root, const char* topic, const char* group,
+                           int partition) {
+  FILE* f = fopen(offsets_path(root, topic, group).c_str(), "r");
+  if (!f) return -1;
+  int p; long long o, res = -1;
+  while (fscanf(f, "%d %lld", &p, &o) == 2) if (p == partition) res = o;
+  fclose(f);
+  return res;
+}
+
+}  // extern "C"

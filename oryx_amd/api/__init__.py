@@ -1,0 +1,196 @@
+"""Public API for app authors (the reference's ``framework/oryx-api``).
+
+Interfaces mirror ``[api]``:
+
+* :class:`KeyMessage` (``[api]/KeyMessage.java:28``, ``KeyMessageImpl.java:27-70``)
+* :class:`TopicProducer` (``[api]/TopicProducer.java:29-56``)
+* :class:`BatchLayerUpdate` (``[api]/batch/BatchLayerUpdate.java:38-59``)
+* :class:`SpeedModelManager`, :class:`SpeedModel` (``[api]/speed/SpeedModelManager.java:37-67``,
+  ``[api]/speed/SpeedModel.java:23-30``)
+* :class:`ServingModelManager`, :class:`AbstractServingModelManager`, :class:`ServingModel`
+  (``[api]/serving/ServingModelManager.java:35-75``,
+  ``[api]/serving/AbstractServingModelManager.java:26-48``, ``[api]/serving/ServingModel.java:23-30``)
+* :class:`OryxServingException` (``[api]/serving/OryxServingException.java:26-55``)
+* :class:`HasCSV` (``[api]/serving/HasCSV.java:25``)
+
+Data handed to batch updates is a :class:`Dataset` of (key, message) string pairs (the RDD
+equivalent).  The Scala adapter classes of the reference have no counterpart: Python classes
+implement these ABCs directly.
+"""
+
+from __future__ import annotations
+
+import abc
+from dataclasses import dataclass
+from typing import Any, Generic, Iterable, Iterator, List, Optional, Sequence, Tuple, TypeVar
+
+K = TypeVar("K")
+M = TypeVar("M")
+U = TypeVar("U")
+
+__all__ = ["KeyMessage", "TopicProducer", "BatchLayerUpdate", "SpeedModelManager", "SpeedModel",
+           "ServingModelManager", "AbstractServingModelManager", "ServingModel",
+           "OryxServingException", "HasCSV", "Dataset"]
+
+
+@dataclass(frozen=True)
+class KeyMessage(Generic[K, M]):
+    key: Optional[K]
+    message: M
+
+    def get_key(self):
+        return self.key
+
+    def get_message(self):
+        return self.message
+
+
+class TopicProducer(abc.ABC, Generic[K, M]):
+    """Sends keyed messages to a topic."""
+
+    @abc.abstractmethod
+    def get_update_broker(self) -> str: ...
+
+    @abc.abstractmethod
+    def get_topic(self) -> str: ...
+
+    @abc.abstractmethod
+    def send(self, key: Optional[K], message: M) -> None: ...
+
+    def send_many(self, pairs: Iterable[Tuple[Optional[K], M]]) -> None:
+        for k, m in pairs:
+            self.send(k, m)
+
+    def close(self) -> None:
+        pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+
+class Dataset:
+    """An immutable, in-memory collection of (key, message) pairs for one batch interval.
+
+    Plays the role of the reference's ``JavaPairRDD<K,M>``: batch updates receive the
+    interval's new data and all past data.  Heavy numeric work happens after parsing, on
+    device tensors, so a plain list is the right container here.
+    """
+
+    __slots__ = ("_pairs",)
+
+    def __init__(self, pairs: Iterable[Tuple[Any, Any]] = ()):
+        self._pairs = list(pairs)
+
+    def __len__(self):
+        return len(self._pairs)
+
+    def __iter__(self) -> Iterator[Tuple[Any, Any]]:
+        return iter(self._pairs)
+
+    def is_empty(self) -> bool:
+        return not self._pairs
+
+    def count(self) -> int:
+        return len(self._pairs)
+
+    def keys(self) -> List[Any]:
+        return [k for k, _ in self._pairs]
+
+    def values(self) -> List[Any]:
+        return [m for _, m in self._pairs]
+
+    def union(self, other: "Dataset") -> "Dataset":
+        return Dataset(self._pairs + list(other))
+
+    def filter(self, fn) -> "Dataset":
+        return Dataset(p for p in self._pairs if fn(p))
+
+    def map_values(self, fn) -> "Dataset":
+        return Dataset((k, fn(m)) for k, m in self._pairs)
+
+    def collect(self) -> List[Tuple[Any, Any]]:
+        return list(self._pairs)
+
+
+class BatchLayerUpdate(abc.ABC, Generic[K, M, U]):
+    """Called once per batch interval with new and past data."""
+
+    @abc.abstractmethod
+    def run_update(self, context: Any, timestamp: int, new_data: Dataset,
+                   past_data: Optional[Dataset], model_dir: str,
+                   model_update_topic: Optional[TopicProducer]) -> None: ...
+
+
+class SpeedModel(abc.ABC):
+    @abc.abstractmethod
+    def get_fraction_loaded(self) -> float: ...
+
+
+class SpeedModelManager(abc.ABC, Generic[K, M, U]):
+    """Consumes the update topic into an in-memory model; turns new input into updates."""
+
+    @abc.abstractmethod
+    def consume(self, updates: Iterator[KeyMessage], context: Any = None) -> None: ...
+
+    @abc.abstractmethod
+    def build_updates(self, new_data: Dataset) -> Iterable[U]: ...
+
+    def close(self) -> None:
+        pass
+
+
+class ServingModel(abc.ABC):
+    @abc.abstractmethod
+    def get_fraction_loaded(self) -> float: ...
+
+
+class ServingModelManager(abc.ABC, Generic[U]):
+    @abc.abstractmethod
+    def consume(self, updates: Iterator[KeyMessage], context: Any = None) -> None: ...
+
+    @abc.abstractmethod
+    def get_config(self): ...
+
+    @abc.abstractmethod
+    def get_model(self) -> Optional[ServingModel]: ...
+
+    @abc.abstractmethod
+    def is_read_only(self) -> bool: ...
+
+    def close(self) -> None:
+        pass
+
+
+class AbstractServingModelManager(ServingModelManager[U]):
+    """Stores the config and reads ``oryx.serving.api.read-only``."""
+
+    def __init__(self, config):
+        self._config = config
+        self._read_only = config.get_bool("oryx.serving.api.read-only")
+
+    def get_config(self):
+        return self._config
+
+    def is_read_only(self) -> bool:
+        return self._read_only
+
+
+class OryxServingException(Exception):
+    """An HTTP status + message raised from a serving resource."""
+
+    def __init__(self, status: int, message: Optional[str] = None):
+        super().__init__(message or "")
+        self.status = int(status)
+        self.message = message
+
+    def get_status_code(self) -> int:
+        return self.status
+
+
+class HasCSV(abc.ABC):
+    @abc.abstractmethod
+    def to_csv(self) -> str: ...

@@ -1,0 +1,163 @@
+"""Loading of the in-tree native libraries (built by :mod:`oryx_amd._build`).
+
+``runtime()`` returns the host C++ runtime (log transport etc.); ``kernels()`` the HIP kernel
+library.  The kernel library must be loaded after ``torch`` so it binds to the same HIP
+runtime instance (torch ships ``libamdhip64.so.7``; the dynamic linker reuses it by soname).
+
+On a GPU box the HIP path is mandatory: :func:`require_kernels` raises if the library is
+missing or fails to load (``oryx.gpu.require-native``), so a silent eager fallback can never
+masquerade as the native path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from . import _build
+
+__all__ = ["runtime", "kernels", "require_kernels", "kernels_available", "stream_ptr"]
+
+_lock = threading.Lock()
+_runtime = None
+_kernels = None
+_kernels_error = None
+
+c_vp = ctypes.c_void_p
+c_i = ctypes.c_int
+c_ll = ctypes.c_longlong
+c_f = ctypes.c_float
+c_cp = ctypes.c_char_p
+
+
+def _sig(lib, name, restype, argtypes):
+    fn = getattr(lib, name)
+    fn.restype = restype
+    fn.argtypes = argtypes
+    return fn
+
+
+def _load_runtime():
+    path = _build.RUNTIME_SO
+    if not os.path.exists(path) or _build._stale(path, _runtime_sources()):
+        try:
+            _build.build_runtime()
+        except Exception:
+            if not os.path.exists(path):
+                raise
+    lib = ctypes.CDLL(path)
+    _sig(lib, "oryx_log_last_error", c_cp, [])
+    _sig(lib, "oryx_log_open", c_vp, [c_cp, c_cp, c_i, c_ll, c_ll])
+    _sig(lib, "oryx_log_exists", c_i, [c_cp, c_cp])
+    _sig(lib, "oryx_log_close", None, [c_vp])
+    _sig(lib, "oryx_log_num_partitions", c_i, [c_vp])
+    _sig(lib, "oryx_log_max_message", c_ll, [c_vp])
+    _sig(lib, "oryx_log_partition_for", c_i, [c_vp, c_cp, c_i])
+    _sig(lib, "oryx_log_append_batch", c_ll, [c_vp, c_i, c_cp, c_ll, c_i, c_ll, c_i, c_vp])
+    _sig(lib, "oryx_log_begin_offset", c_ll, [c_vp, c_i])
+    _sig(lib, "oryx_log_end_offset", c_ll, [c_vp, c_i])
+    _sig(lib, "oryx_log_retain", c_i, [c_vp, c_ll])
+    _sig(lib, "oryx_reader_open", c_vp, [c_vp, c_i, c_ll])
+    _sig(lib, "oryx_reader_close", None, [c_vp])
+    _sig(lib, "oryx_reader_position", c_ll, [c_vp])
+    _sig(lib, "oryx_reader_seek", None, [c_vp, c_ll])
+    _sig(lib, "oryx_reader_poll", c_ll, [c_vp, c_vp, c_ll, c_i, c_i, ctypes.POINTER(c_ll)])
+    _sig(lib, "oryx_offsets_set", c_i, [c_cp, c_cp, c_cp, c_i, ctypes.POINTER(c_i),
+                                         ctypes.POINTER(c_ll)])
+    _sig(lib, "oryx_offsets_get", c_ll, [c_cp, c_cp, c_cp, c_i])
+    _register_runtime_extras(lib)
+    return lib
+
+
+def _register_runtime_extras(lib):
+    # Optional symbols of later runtime modules
+    for name, res, args in [
+        ("oryx_parse_ratings", c_ll, [c_cp, c_ll, c_vp, c_vp, c_vp, c_vp, c_ll, c_i]),
+        ("oryx_dict_new", c_vp, []),
+        ("oryx_dict_free", None, [c_vp]),
+        ("oryx_dict_size", c_ll, [c_vp]),
+        ("oryx_dict_encode", c_ll, [c_vp, c_cp, c_ll, c_i, c_vp]),
+        ("oryx_dict_get", c_ll, [c_vp, c_cp, c_ll]),
+        ("oryx_dict_key", c_ll, [c_vp, c_ll, c_cp, c_ll]),
+    ]:
+        if hasattr(lib, name):
+            _sig(lib, name, res, args)
+
+
+def _runtime_sources():
+    import glob
+    return glob.glob(os.path.join(_build.CSRC, "runtime", "*"))
+
+
+def runtime():
+    global _runtime
+    if _runtime is None:
+        with _lock:
+            if _runtime is None:
+                _runtime = _load_runtime()
+    return _runtime
+
+
+def _load_kernels():
+    import torch  # noqa: F401  (bind to torch's HIP runtime first)
+    path = _build.KERNELS_SO
+    if not os.path.exists(path):
+        _build.build_kernels()
+    lib = ctypes.CDLL(path)
+    _sig(lib, "oryx_kernels_version", c_i, [])
+    _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
+                                      c_i, c_f, c_f, c_i, c_vp, c_vp])
+    _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])
+    for name, res, args in [
+        ("oryx_topk_scores", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_i, c_vp, c_vp,
+                                   c_vp, c_vp]),
+        ("oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp]),
+        ("oryx_kmeans_accumulate", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
+                                         c_vp, c_vp]),
+        ("oryx_rdf_histogram", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i, c_i,
+                                     c_i, c_vp, c_vp]),
+        ("oryx_tree_traverse", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_i,
+                                     c_i, c_i, c_vp, c_vp]),
+        ("oryx_lsh_hash", c_i, [c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp]),
+    ]:
+        if hasattr(lib, name):
+            _sig(lib, name, res, args)
+    return lib
+
+
+def kernels():
+    global _kernels, _kernels_error
+    if _kernels is None and _kernels_error is None:
+        with _lock:
+            if _kernels is None and _kernels_error is None:
+                try:
+                    _kernels = _load_kernels()
+                except Exception as e:  # recorded; require_kernels() re-raises
+                    _kernels_error = e
+    if _kernels is None:
+        raise RuntimeError("oryx_amd HIP kernels unavailable: %r" % (_kernels_error,))
+    return _kernels
+
+
+def kernels_available() -> bool:
+    try:
+        kernels()
+        return True
+    except Exception:
+        return False
+
+
+def require_kernels():
+    """Fail loudly when the HIP kernels cannot be used on a GPU device."""
+    return kernels()
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError("%s failed (native error %d)" % (what, rc))

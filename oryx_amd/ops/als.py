@@ -1,0 +1,254 @@
+"""ALS device ops: CSR construction, Gramian, fused normal-equation solve.
+
+The hot op is :func:`solve_rows` -- for each row of a CSR ratings matrix, gather the opposite
+factor rows, form the per-row Gramian and solve the ALS normal equations.  On a GPU this
+calls the hand-written CDNA4 kernel ``oryx_als_solve`` (``csrc/kernels/als.hip``: MFMA
+segmented Gramian + in-register Cholesky); on CPU (tests, the ``local[*]`` plumbing config)
+an exact fp32 PyTorch reference of the same math runs instead.
+
+Normal equations (Spark MLlib's ALS, which the reference invokes at
+``[mllib]/als/ALSUpdate.java:116-124``):
+
+* implicit: ``(YtY + sum c1 y yT + lambda*n+ I) x = sum_{r>0} (1+c1) y``, ``c1 = alpha*|r|``
+* explicit: ``(sum y yT + lambda*n I) x = sum r y``
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from .. import native
+
+__all__ = ["CSR", "build_csr", "padded_rank", "gramian", "solve_rows", "solve_rows_reference",
+           "to_bf16_padded", "pair_dots", "KERNEL_MAX_KP"]
+
+KERNEL_MAX_KP = 128
+_KERNEL_KPS = (16, 32, 48, 64, 80, 96, 112, 128)
+
+
+def padded_rank(k: int) -> int:
+    """Rank padded to the kernel's tile granularity (16; 16..64 and 80..128 are supported)."""
+    kp = max(16, int(math.ceil(k / 16.0)) * 16)
+    return kp
+
+
+@dataclass
+class CSR:
+    """Row-compressed ratings: ``row_ptr`` int64 [n_rows+1], ``cols`` int32, ``vals`` fp32.
+
+    ``order`` lists rows with at least one rating, longest first (the kernel's work queue).
+    """
+
+    row_ptr: torch.Tensor
+    cols: torch.Tensor
+    vals: torch.Tensor
+    n_rows: int
+    n_cols: int
+    order: torch.Tensor
+
+    @property
+    def nnz(self) -> int:
+        return int(self.cols.numel())
+
+    def to(self, device) -> "CSR":
+        return CSR(self.row_ptr.to(device), self.cols.to(device), self.vals.to(device),
+                   self.n_rows, self.n_cols, self.order.to(device))
+
+
+def build_csr(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_rows: int,
+              n_cols: int, row_offset: int = 0) -> CSR:
+    """CSR of (row, col, val) triples (rows are global ids; ``row_offset`` makes them local).
+
+    Triples must already be unique per (row, col).  Runs on the tensors' device.
+    """
+    device = rows.device
+    r = rows.to(torch.int64) - row_offset
+    key = r * int(n_cols) + cols.to(torch.int64)
+    key_sorted, perm = torch.sort(key)
+    r_sorted = torch.div(key_sorted, int(n_cols), rounding_mode="floor")
+    c_sorted = (key_sorted - r_sorted * int(n_cols)).to(torch.int32)
+    v_sorted = vals.to(torch.float32)[perm]
+    counts = torch.bincount(r_sorted, minlength=n_rows)
+    row_ptr = torch.zeros(n_rows + 1, dtype=torch.int64, device=device)
+    torch.cumsum(counts, 0, out=row_ptr[1:])
+    nz_rows = torch.nonzero(counts, as_tuple=False).flatten()
+    order = nz_rows[torch.argsort(counts[nz_rows], descending=True, stable=True)]
+    return CSR(row_ptr, c_sorted.contiguous(), v_sorted.contiguous(), int(n_rows), int(n_cols),
+               order.to(torch.int32).contiguous())
+
+
+def to_bf16_padded(x: torch.Tensor, kp: int) -> torch.Tensor:
+    if x.shape[1] == kp:
+        return x.to(torch.bfloat16).contiguous()
+    out = torch.zeros((x.shape[0], kp), dtype=torch.bfloat16, device=x.device)
+    out[:, :x.shape[1]] = x
+    return out
+
+
+def gramian(x: torch.Tensor) -> torch.Tensor:
+    """``XᵀX`` in fp32 (a plain library GEMM: hipBLASLt on GPU)."""
+    x = x.to(torch.float32)
+    return x.t().matmul(x)
+
+
+def _use_kernel(device: torch.device, kp: int) -> bool:
+    return device.type == "cuda" and kp in _KERNEL_KPS
+
+
+def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_out: torch.Tensor,
+               xb_out: Optional[torch.Tensor], k: int, lam: float, alpha: float,
+               implicit: bool, y_f32: Optional[torch.Tensor] = None,
+               fail_count: Optional[torch.Tensor] = None) -> None:
+    """Solve every non-empty row of ``csr`` into ``x_out`` (fp32 [n_rows, kp]) / ``xb_out``.
+
+    ``y_bf16``: the opposite factors, bf16 [n_cols, kp] zero-padded.  ``yty``: fp32 [kp, kp]
+    Gramian of the opposite factors (implicit), ignored for explicit feedback.
+    """
+    kp = y_bf16.shape[1]
+    device = y_bf16.device
+    if _use_kernel(device, kp):
+        lib = native.require_kernels()
+        if yty is None or not implicit:
+            yty = torch.zeros((kp, kp), dtype=torch.float32, device=device)
+        yty = yty.to(torch.float32).contiguous()
+        assert x_out.dtype == torch.float32 and x_out.shape[1] == kp and x_out.is_contiguous()
+        assert csr.row_ptr.dtype == torch.int64 and csr.cols.dtype == torch.int32
+        assert y_bf16.dtype == torch.bfloat16 and y_bf16.is_contiguous()
+        assert x_out.shape[0] >= csr.n_rows and y_bf16.shape[0] >= csr.n_cols
+        if xb_out is not None:
+            assert xb_out.dtype == torch.bfloat16 and xb_out.shape == x_out.shape
+        rc = lib.oryx_als_solve(csr.row_ptr.data_ptr(), csr.order.data_ptr(),
+                                csr.cols.data_ptr(), csr.vals.data_ptr(), y_bf16.data_ptr(),
+                                yty.data_ptr(), x_out.data_ptr(),
+                                xb_out.data_ptr() if xb_out is not None else None,
+                                int(csr.order.numel()), int(k), int(kp), float(lam),
+                                float(alpha), int(bool(implicit)),
+                                fail_count.data_ptr() if fail_count is not None else None,
+                                native.stream_ptr(device))
+        native.check(rc, "oryx_als_solve")
+        return
+    # exact reference path (CPU, or ranks beyond the kernel's range)
+    src = y_f32 if y_f32 is not None else y_bf16.to(torch.float32)
+    sol = solve_rows_reference(csr, src, yty, k, lam, alpha, implicit)
+    rows = csr.order.to(torch.int64)
+    x_out[rows] = sol[rows].to(x_out.dtype)
+    if xb_out is not None:
+        xb_out[rows] = sol[rows].to(torch.bfloat16)
+
+
+def solve_rows_reference(csr: CSR, y: torch.Tensor, yty: Optional[torch.Tensor], k: int,
+                         lam: float, alpha: float, implicit: bool,
+                         chunk_rows: int = 8192) -> torch.Tensor:
+    """fp32 PyTorch reference of the kernel's math; returns [n_rows, kp] (zeros for empty rows)."""
+    device = y.device
+    kp = y.shape[1]
+    y = y.to(torch.float32)
+    out = torch.zeros((csr.n_rows, kp), dtype=torch.float32, device=device)
+    if csr.nnz == 0:
+        return out
+    row_ptr = csr.row_ptr
+    counts = (row_ptr[1:] - row_ptr[:-1])
+    row_of = torch.repeat_interleave(torch.arange(csr.n_rows, device=device), counts)
+    r = csr.vals.to(torch.float32)
+    if implicit:
+        wa = alpha * r.abs()
+        wb = torch.where(r > 0, 1.0 + wa, torch.zeros_like(r))
+        cnt = (r > 0).to(torch.float32)
+    else:
+        wa = torch.ones_like(r)
+        wb = r
+        cnt = torch.ones_like(r)
+    eye = torch.eye(kp, device=device)
+    pad_diag = torch.zeros(kp, device=device)
+    pad_diag[k:] = 1.0
+    for lo in range(0, csr.n_rows, chunk_rows):
+        hi = min(csr.n_rows, lo + chunk_rows)
+        s, e = int(row_ptr[lo]), int(row_ptr[hi])
+        if s == e:
+            continue
+        ro = row_of[s:e] - lo
+        yy = y[csr.cols[s:e].to(torch.int64)]
+        n = hi - lo
+        A = torch.zeros((n, kp, kp), device=device)
+        A.index_add_(0, ro, (wa[s:e, None, None] * yy[:, :, None]) * yy[:, None, :])
+        b = torch.zeros((n, kp), device=device)
+        b.index_add_(0, ro, wb[s:e, None] * yy)
+        c = torch.zeros(n, device=device)
+        c.index_add_(0, ro, cnt[s:e])
+        if implicit and yty is not None:
+            A = A + yty.to(torch.float32)[None]
+        diag = lam * c[:, None] * torch.cat([torch.ones(k, device=device),
+                                             torch.zeros(kp - k, device=device)])[None]
+        A = A + torch.diag_embed(diag + pad_diag[None])
+        nonempty = counts[lo:hi] > 0
+        if nonempty.any():
+            idx = torch.nonzero(nonempty).flatten()
+            L, info = torch.linalg.cholesky_ex(A[idx])
+            if bool((info != 0).any()):
+                sol = torch.linalg.lstsq(A[idx], b[idx].unsqueeze(-1)).solution.squeeze(-1)
+            else:
+                sol = torch.cholesky_solve(b[idx].unsqueeze(-1), L).squeeze(-1)
+            out[lo + idx] = sol
+    return out
+
+
+def pair_dots(x: torch.Tensor, y: torch.Tensor, us: torch.Tensor, items: torch.Tensor
+              ) -> torch.Tensor:
+    """``dot(x[us[j]], y[items[j]])`` for each pair (evaluation predictions)."""
+    if x.device.type == "cuda" and x.shape[1] % 16 == 0 and x.dtype == torch.float32 \
+            and y.dtype == torch.float32 and native.kernels_available():
+        lib = native.kernels()
+        out = torch.empty(us.numel(), dtype=torch.float32, device=x.device)
+        u32 = us.to(torch.int32).contiguous()
+        i32 = items.to(torch.int32).contiguous()
+        rc = lib.oryx_pair_dots(x.contiguous().data_ptr(), y.contiguous().data_ptr(),
+                                u32.data_ptr(), i32.data_ptr(), int(us.numel()), int(x.shape[1]),
+                                out.data_ptr(), native.stream_ptr(x.device))
+        native.check(rc, "oryx_pair_dots")
+        return out
+    return (x[us.to(torch.int64)] * y[items.to(torch.int64)]).sum(1)
+
+
+def target_qui(implicit: bool, value: torch.Tensor, current: torch.Tensor) -> torch.Tensor:
+    """Vectorised ``ALSUtils.computeTargetQui`` (``[app-common]/als/ALSUtils.java:37-59``).
+
+    NaN marks "no change".  Computed in float64 like the reference.
+    """
+    value = value.to(torch.float64)
+    current = current.to(torch.float64)
+    if not implicit:
+        return value.clone()
+    nan = torch.full_like(value, float("nan"))
+    pos = (value > 0) & (current < 1.0)
+    neg = (value < 0) & (current > 0.0)
+    pos_t = current + (value / (1.0 + value)) * (1.0 - current.clamp_min(0.0))
+    neg_t = current + (value / (value - 1.0)) * (-current.clamp_max(1.0))
+    return torch.where(pos, pos_t, torch.where(neg, neg_t, nan))
+
+
+def fold_in(solver_inv: torch.Tensor, values: torch.Tensor, xu: torch.Tensor,
+            xu_present: torch.Tensor, yi: torch.Tensor, implicit: bool):
+    """Batched ``ALSUtils.computeUpdatedXu`` (``[app-common]/als/ALSUtils.java:74-106``).
+
+    For B events at once: ``Qui = xu.yi`` (0.5 "don't know" target base when xu is absent),
+    ``dXu = inv(YtY) (dQui * yi)`` as one [B,k]x[k,k] GEMM, ``newXu = xu + dXu``.
+    Returns (new vectors fp32 [B,k], valid mask [B]); invalid rows had no target.
+    """
+    xu64 = xu.to(torch.float64)
+    yi64 = yi.to(torch.float64)
+    # the reference computes dot() with float products accumulated in double
+    qui = (xu.to(torch.float32) * yi.to(torch.float32)).to(torch.float64).sum(1)
+    qui = torch.where(xu_present, qui, torch.zeros_like(qui))
+    base = torch.where(xu_present, qui, torch.full_like(qui, 0.5))
+    tgt = target_qui(implicit, values, base)
+    valid = ~torch.isnan(tgt)
+    dq = torch.where(valid, tgt - qui, torch.zeros_like(tgt))
+    rhs = (yi.to(torch.float32) * dq.to(torch.float32)[:, None]).to(torch.float64)
+    dx = rhs.matmul(solver_inv.to(torch.float64).t())
+    dx32 = dx.to(torch.float32)
+    new = torch.where(xu_present[:, None], (xu.to(torch.float32) + dx32), dx32)
+    return new, valid

@@ -1,0 +1,185 @@
+"""One process per GPU over ``torch.distributed`` (RCCL on ROCm via the ``nccl`` backend).
+
+Every Spark shuffle the reference relies on becomes one of a few
+collectives here: all-reduce of partial Gramians / centroid sums / split histograms, and
+all-gather of factor-matrix row shards.  Single-process runs (world size 1) skip the
+collectives entirely.  CPU multi-process tests use the ``gloo`` backend.
+
+xGMI note: each MI355X has 7 point-to-point links; RCCL's multi-channel ring/tree algorithms
+already stripe large all-gathers over all links, so factor exchanges are issued as ONE large
+``all_gather_into_tensor`` per half-step (bucketed only when exceeding ``bucket_bytes``)
+rather than many small ones, and small latency-bound reductions (k x k Gramians) are
+batched into a single all-reduce.
+"""
+
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as tdist
+
+__all__ = ["DistContext", "init_from_env", "get_context", "shard_range", "padded_shard_size",
+           "all_gather_rows", "all_reduce_sum", "broadcast_object", "barrier"]
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: Optional[str] = None
+    group: Optional[object] = None
+
+    @property
+    def is_distributed(self) -> bool:
+        return self.world_size > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+_context: Optional[DistContext] = None
+
+
+def _pick_device(local_rank: int, device: Optional[str]) -> torch.device:
+    if device and device not in ("auto", ""):
+        if device == "cuda":
+            return torch.device("cuda", local_rank)
+        return torch.device(device)
+    if torch.cuda.is_available():
+        return torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    return torch.device("cpu")
+
+
+def init_from_env(device: Optional[str] = None, backend: Optional[str] = None,
+                  timeout_s: float = 600.0) -> DistContext:
+    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
+    global _context
+    if _context is not None:
+        return _context
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = _pick_device(local_rank, device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    ctx = DistContext(rank, world, local_rank, dev)
+    if world > 1:
+        if backend is None:
+            backend = "nccl" if dev.type == "cuda" else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if not tdist.is_initialized():
+            kwargs = dict(backend=backend, rank=rank, world_size=world,
+                          timeout=datetime.timedelta(seconds=timeout_s))
+            if backend == "nccl":
+                kwargs["device_id"] = dev
+            tdist.init_process_group(**kwargs)
+        ctx.backend = backend
+    _context = ctx
+    return ctx
+
+
+def get_context() -> DistContext:
+    return _context if _context is not None else DistContext()
+
+
+def set_context(ctx: Optional[DistContext]) -> None:
+    global _context
+    _context = ctx
+
+
+def padded_shard_size(n: int, world: int) -> int:
+    return (n + world - 1) // world if world > 1 else n
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous [lo, hi) of ``n`` rows owned by ``rank`` (equal padded shards)."""
+    s = padded_shard_size(n, world)
+    lo = min(n, rank * s)
+    hi = min(n, lo + s)
+    return lo, hi
+
+
+def all_gather_rows(local: torch.Tensor, n_total: int, ctx: DistContext,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Concatenate equal-size row shards from every rank (shards padded to the same size)."""
+    if not ctx.is_distributed:
+        if out is not None:
+            out[:local.shape[0]].copy_(local)
+            return out
+        return local
+    s = padded_shard_size(n_total, ctx.world_size)
+    if local.shape[0] != s:
+        pad = torch.zeros((s,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        pad[:local.shape[0]] = local
+        local = pad
+    full = out if out is not None and out.shape[0] == s * ctx.world_size else torch.empty(
+        (s * ctx.world_size,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if ctx.backend == "gloo":
+        parts = list(full.chunk(ctx.world_size, 0))
+        tdist.all_gather(parts, local.contiguous())
+    else:
+        tdist.all_gather_into_tensor(full, local.contiguous())
+    return full
+
+
+def all_reduce_sum(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:
+    if ctx.is_distributed:
+        tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
+    return t
+
+
+def broadcast_object(obj, ctx: DistContext, src: int = 0):
+    if not ctx.is_distributed:
+        return obj
+    lst = [obj]
+    tdist.broadcast_object_list(lst, src=src)
+    return lst[0]
+
+
+def barrier(ctx: DistContext) -> None:
+    if ctx.is_distributed:
+        if ctx.backend == "nccl":
+            tdist.barrier(device_ids=[ctx.device.index])
+        else:
+            tdist.barrier()
+
+
+def all_to_all_rows(send: torch.Tensor, send_counts: Sequence[int], ctx: DistContext
+                    ) -> torch.Tensor:
+    """Variable-size all-to-all of rows (the shuffle that repartitions ratings by item)."""
+    if not ctx.is_distributed:
+        return send
+    counts = torch.tensor(list(send_counts), dtype=torch.int64, device=send.device)
+    recv_counts = torch.empty_like(counts)
+    if ctx.backend == "gloo":
+        # gloo has no all_to_all: emulate with all_gather of counts and padded payloads
+        allc = [torch.empty_like(counts) for _ in range(ctx.world_size)]
+        tdist.all_gather(allc, counts)
+        recv_counts = torch.stack([c[ctx.rank] for c in allc])
+        maxn = int(torch.stack(allc).max())
+        chunks = list(torch.split(send, list(send_counts)))
+        outs = []
+        for src in range(ctx.world_size):
+            for dst in range(ctx.world_size):
+                n = int(allc[src][dst])
+                buf = torch.zeros((maxn,) + tuple(send.shape[1:]), dtype=send.dtype,
+                                  device=send.device)
+                if src == ctx.rank:
+                    buf[:n] = chunks[dst]
+                tdist.broadcast(buf, src=src)
+                if dst == ctx.rank:
+                    outs.append(buf[:n].clone())
+        return torch.cat(outs) if outs else send[:0]
+    tdist.all_to_all_single(recv_counts, counts)
+    recv = torch.empty((int(recv_counts.sum()),) + tuple(send.shape[1:]), dtype=send.dtype,
+                       device=send.device)
+    tdist.all_to_all_single(recv, send.contiguous(), output_split_sizes=recv_counts.tolist(),
+                            input_split_sizes=list(send_counts))
+    return recv

@@ -1,0 +1,310 @@
+"""Python bindings for the native append-only log (``csrc/runtime/oryx_log.cpp``).
+
+Provides Kafka-like primitives used by every layer:
+
+* :class:`Topic` -- open/create a topic (partitions, max message size), append single or
+  batched keyed records, begin/end offsets, retention;
+* :class:`PartitionReader` / :class:`TopicConsumer` -- tail one or all partitions from an
+  offset (``earliest`` / ``latest`` / committed group offset);
+* :func:`get_offsets` / :func:`set_offsets` -- consumer-group offset store
+  (the ZooKeeper role of ``[kafka]/KafkaUtils.java:123-161``);
+* :func:`maybe_create_topic`, :func:`topic_exists`, :func:`delete_topic`
+  (``[kafka]/KafkaUtils.java:57-115``).
+
+Brokers: the reference's ``host:port`` broker strings are accepted; records go to the log
+root directory ``oryx.transport.log-dir`` unless a broker is written ``log:/some/dir``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import shutil
+import struct
+import threading
+import time
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+
+from .. import native
+
+__all__ = ["Topic", "PartitionReader", "TopicConsumer", "Record", "get_offsets", "set_offsets",
+           "maybe_create_topic", "topic_exists", "delete_topic", "log_root_for",
+           "MessageTooLargeError", "DEFAULT_LOG_ROOT"]
+
+DEFAULT_LOG_ROOT = os.environ.get("ORYX_LOG_DIR", "/tmp/Oryx/log")
+
+
+class MessageTooLargeError(ValueError):
+    pass
+
+
+def _lib():
+    return native.runtime()
+
+
+def log_root_for(broker: Optional[str], config=None) -> str:
+    """Resolve a broker string to a log directory."""
+    if broker and broker.startswith("log:"):
+        return broker[4:]
+    if config is not None and config.has_path("oryx.transport.log-dir"):
+        from ..utils.ioutils import to_local_path
+        return to_local_path(config.get_string("oryx.transport.log-dir"))
+    return DEFAULT_LOG_ROOT
+
+
+def _b(s: Optional[str]) -> Optional[bytes]:
+    if s is None:
+        return None
+    return s.encode("utf-8") if isinstance(s, str) else bytes(s)
+
+
+def topic_exists(root: str, topic: str) -> bool:
+    return bool(_lib().oryx_log_exists(_b(root), _b(topic)))
+
+
+def maybe_create_topic(root: str, topic: str, partitions: int = 1,
+                       max_message: int = 16777216, segment_bytes: int = 64 << 20) -> None:
+    if not topic_exists(root, topic):
+        Topic(root, topic, create_partitions=partitions, max_message=max_message,
+              segment_bytes=segment_bytes).close()
+
+
+def delete_topic(root: str, topic: str) -> None:
+    path = os.path.join(root, topic)
+    if os.path.isdir(path):
+        shutil.rmtree(path, ignore_errors=True)
+
+
+class Record(Tuple):
+    pass
+
+
+_HDR = struct.Struct("<qqii")
+
+
+class Topic:
+    """A handle on one topic of the log."""
+
+    def __init__(self, root: str, name: str, create_partitions: int = 0,
+                 max_message: int = 16777216, segment_bytes: int = 64 << 20):
+        self.root = root
+        self.name = name
+        lib = _lib()
+        self._h = lib.oryx_log_open(_b(root), _b(name), int(create_partitions),
+                                    int(max_message), int(segment_bytes))
+        if not self._h:
+            raise FileNotFoundError(lib.oryx_log_last_error().decode())
+        self.partitions = lib.oryx_log_num_partitions(self._h)
+        self.max_message = lib.oryx_log_max_message(self._h)
+        self._lock = threading.Lock()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self) -> None:
+        with self._lock:
+            if self._h:
+                _lib().oryx_log_close(self._h)
+                self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def partition_for(self, key: Optional[str]) -> int:
+        kb = _b(key)
+        return _lib().oryx_log_partition_for(self._h, kb, -1 if kb is None else len(kb))
+
+    def append(self, key: Optional[str], value: str, partition: int = -1,
+               timestamp_ms: int = -1, fsync: bool = False) -> int:
+        return self.append_batch([(key, value)], partition, timestamp_ms, fsync)
+
+    def append_batch(self, records: Sequence[Tuple[Optional[str], str]], partition: int = -1,
+                     timestamp_ms: int = -1, fsync: bool = False) -> int:
+        """Append many (key, value) records with one native call; returns the last offset."""
+        if not records:
+            return -1
+        parts = []
+        for k, v in records:
+            kb = _b(k)
+            vb = _b(v)
+            parts.append(struct.pack("<iq", -1 if kb is None else len(kb), len(vb)))
+            if kb is not None:
+                parts.append(kb)
+            parts.append(vb)
+        buf = b"".join(parts)
+        res = _lib().oryx_log_append_batch(self._h, int(partition), buf, len(buf),
+                                           len(records), int(timestamp_ms), int(bool(fsync)),
+                                           None)
+        if res == -2:
+            raise MessageTooLargeError(_lib().oryx_log_last_error().decode())
+        if res < 0:
+            raise IOError(_lib().oryx_log_last_error().decode())
+        return res
+
+    def begin_offset(self, partition: int) -> int:
+        return _lib().oryx_log_begin_offset(self._h, partition)
+
+    def end_offset(self, partition: int) -> int:
+        return _lib().oryx_log_end_offset(self._h, partition)
+
+    def end_offsets(self) -> List[int]:
+        return [self.end_offset(p) for p in range(self.partitions)]
+
+    def retain(self, max_age_ms: int) -> int:
+        cutoff = int(time.time() * 1000) - int(max_age_ms)
+        return _lib().oryx_log_retain(self._h, cutoff)
+
+    def reader(self, partition: int, offset: int) -> "PartitionReader":
+        return PartitionReader(self, partition, offset)
+
+
+class PartitionReader:
+    """Tails one partition from an offset (``-1`` = current end)."""
+
+    def __init__(self, topic: Topic, partition: int, offset: int):
+        self.topic = topic
+        self.partition = partition
+        self._r = _lib().oryx_reader_open(topic.handle, partition, int(offset))
+        if not self._r:
+            raise IOError(_lib().oryx_log_last_error().decode())
+        self._cap = 1 << 20
+        self._buf = ctypes.create_string_buffer(self._cap)
+        self._used = ctypes.c_longlong(0)
+
+    @property
+    def position(self) -> int:
+        return _lib().oryx_reader_position(self._r)
+
+    def seek(self, offset: int) -> None:
+        _lib().oryx_reader_seek(self._r, int(offset))
+
+    def poll(self, max_records: int = 4096, timeout_ms: int = 100
+             ) -> List[Tuple[int, int, Optional[str], str]]:
+        """Returns up to ``max_records`` (offset, timestamp_ms, key, value) tuples."""
+        lib = _lib()
+        while True:
+            n = lib.oryx_reader_poll(self._r, self._buf, self._cap, int(max_records),
+                                     int(timeout_ms), ctypes.byref(self._used))
+            if n < -1:
+                need = -n - 16
+                self._cap = max(self._cap * 2, need + 1024)
+                self._buf = ctypes.create_string_buffer(self._cap)
+                continue
+            if n < 0:
+                raise IOError(lib.oryx_log_last_error().decode())
+            break
+        out = []
+        raw = self._buf.raw[:self._used.value] if n else b""
+        pos = 0
+        for _ in range(n):
+            off, ts, kl, vl = _HDR.unpack_from(raw, pos)
+            pos += 24
+            if kl >= 0:
+                key = raw[pos:pos + kl].decode("utf-8")
+                pos += kl
+            else:
+                key = None
+            val = raw[pos:pos + vl].decode("utf-8")
+            pos += vl
+            out.append((off, ts, key, val))
+        return out
+
+    def close(self) -> None:
+        if self._r:
+            _lib().oryx_reader_close(self._r)
+            self._r = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def get_offsets(root: str, topic: str, group: str, partitions: int) -> Dict[int, int]:
+    out = {}
+    lib = _lib()
+    for p in range(partitions):
+        o = lib.oryx_offsets_get(_b(root), _b(topic), _b(group), p)
+        if o >= 0:
+            out[p] = o
+    return out
+
+
+def set_offsets(root: str, topic: str, group: str, offsets: Dict[int, int]) -> None:
+    if not offsets:
+        return
+    n = len(offsets)
+    parts = (ctypes.c_int * n)(*offsets.keys())
+    offs = (ctypes.c_longlong * n)(*offsets.values())
+    if _lib().oryx_offsets_set(_b(root), _b(topic), _b(group), n, parts, offs) != 0:
+        raise IOError(_lib().oryx_log_last_error().decode())
+
+
+class TopicConsumer:
+    """Consumes all partitions of a topic, round-robin.
+
+    ``start``: ``"earliest"`` (replay from the beginning, as speed/serving do for the update
+    topic), ``"latest"``, or a dict partition->offset (resume); a ``group`` makes
+    :meth:`commit` persist offsets.
+    """
+
+    def __init__(self, topic: Topic, start="latest", group: Optional[str] = None):
+        self.topic = topic
+        self.group = group
+        self.readers: List[PartitionReader] = []
+        for p in range(topic.partitions):
+            if isinstance(start, dict):
+                off = start.get(p, topic.end_offset(p))
+            elif start == "earliest":
+                off = topic.begin_offset(p)
+            else:
+                off = topic.end_offset(p)
+            self.readers.append(PartitionReader(topic, p, off))
+        self._closed = False
+
+    def positions(self) -> Dict[int, int]:
+        return {r.partition: r.position for r in self.readers}
+
+    def poll(self, max_records: int = 4096, timeout_ms: int = 100
+             ) -> List[Tuple[int, int, int, Optional[str], str]]:
+        """(partition, offset, ts, key, value) tuples; waits up to timeout for any record."""
+        out = []
+        deadline = time.monotonic() + timeout_ms / 1000.0
+        while True:
+            for r in self.readers:
+                for rec in r.poll(max_records, 0):
+                    out.append((r.partition,) + rec)
+            if out or time.monotonic() >= deadline or self._closed:
+                return out
+            if len(self.readers) == 1:
+                rem = max(0, int((deadline - time.monotonic()) * 1000))
+                for rec in self.readers[0].poll(max_records, rem):
+                    out.append((0,) + rec)
+                return out
+            time.sleep(0.002)
+
+    def __iter__(self) -> Iterator[Tuple[Optional[str], str]]:
+        while not self._closed:
+            for _, _, _, k, v in self.poll():
+                yield k, v
+
+    def commit(self) -> None:
+        if self.group:
+            set_offsets(self.topic.root, self.topic.name, self.group, self.positions())
+
+    def close(self) -> None:
+        self._closed = True
+        for r in self.readers:
+            r.close()

@@ -1,0 +1,115 @@
+"""Numerics of the fused ALS solve kernel (csrc/kernels/als.hip) vs the fp32 PyTorch reference."""
+
+import pytest
+import torch
+
+from oryx_amd.ops import als as als_ops
+
+
+def _problem(n_rows, n_cols, nnz, k, seed, device, neg=False):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    key = torch.unique(torch.randint(0, n_rows * n_cols, (nnz,), generator=g))
+    rows, cols = key // n_cols, key % n_cols
+    vals = torch.randint(1, 10, (key.numel(),), generator=g).float() * 0.5
+    if neg:
+        vals = torch.where(torch.rand(key.numel(), generator=g) < 0.2, -vals, vals)
+    csr = als_ops.build_csr(rows, cols, vals, n_rows, n_cols).to(device)
+    kp = als_ops.padded_rank(k)
+    y = torch.zeros(n_cols, kp)
+    y[:, :k] = torch.randn(n_cols, k, generator=g) * 0.3
+    return csr, y.to(device), kp
+
+
+def test_build_csr_cpu():
+    rows = torch.tensor([2, 0, 2, 1, 0])
+    cols = torch.tensor([1, 3, 0, 2, 0])
+    vals = torch.tensor([1., 2., 3., 4., 5.])
+    csr = als_ops.build_csr(rows, cols, vals, 4, 4)
+    assert csr.row_ptr.tolist() == [0, 2, 3, 5, 5]
+    assert csr.cols.tolist() == [0, 3, 2, 0, 1]
+    assert csr.vals.tolist() == [5., 2., 4., 3., 1.]
+    assert sorted(csr.order.tolist()) == [0, 1, 2]
+
+
+def test_reference_matches_dense_solve_cpu():
+    csr, y, kp = _problem(20, 15, 120, 5, 0, "cpu")
+    yty = als_ops.gramian(y)
+    sol = als_ops.solve_rows_reference(csr, y, yty, 5, 0.1, 2.0, True)
+    # dense check of one row
+    u = int(csr.order[0])
+    s, e = int(csr.row_ptr[u]), int(csr.row_ptr[u + 1])
+    A = yty.clone().double()
+    b = torch.zeros(kp, dtype=torch.float64)
+    npos = 0
+    for j in range(s, e):
+        r = float(csr.vals[j]); yv = y[int(csr.cols[j])].double()
+        c1 = 2.0 * abs(r)
+        A += c1 * torch.outer(yv, yv)
+        if r > 0:
+            b += (1 + c1) * yv
+            npos += 1
+    A += torch.diag(torch.tensor([0.1 * npos] * 5 + [1.0] * (kp - 5), dtype=torch.float64))
+    x = torch.linalg.solve(A, b)
+    assert torch.allclose(sol[u].double(), x, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [10, 16, 32, 40, 64, 72, 100, 128])
+@pytest.mark.parametrize("implicit", [True, False])
+def test_kernel_vs_reference(cuda, k, implicit):
+    csr, y, kp = _problem(700, 400, 30000, k, k, cuda, neg=implicit)
+    yb = y.to(torch.bfloat16)
+    yty = als_ops.gramian(yb.float()) if implicit else None
+    x = torch.zeros(700, kp, device=cuda)
+    xb = torch.zeros(700, kp, device=cuda, dtype=torch.bfloat16)
+    fails = torch.zeros(1, dtype=torch.int32, device=cuda)
+    lam = 0.05
+    als_ops.solve_rows(csr, yb, yty, x, xb, k, lam, 1.5, implicit, fail_count=fails)
+    torch.cuda.synchronize()
+    ref = als_ops.solve_rows_reference(csr, yb.float(), yty, k, lam, 1.5, implicit)
+    rows = csr.order.long()
+    err = (x[rows] - ref[rows]).abs().max().item()
+    scale = ref[rows].abs().max().item()
+    assert int(fails.item()) == 0
+    assert err <= 2e-2 * max(scale, 1.0), (err, scale)
+    # padded features stay exactly zero
+    if kp > k:
+        assert x[:, k:].abs().max().item() == 0.0
+    assert torch.allclose(xb.float(), x, atol=1e-2 * max(scale, 1.0), rtol=1e-2)
+
+
+@pytest.mark.gpu
+def test_kernel_long_and_empty_rows(cuda):
+    # a few very long rows (> 32-rating chunks many times) and many empty rows
+    g = torch.Generator(device="cpu").manual_seed(3)
+    n_rows, n_cols, k = 50, 3000, 64
+    rows = torch.cat([torch.zeros(2500, dtype=torch.long), torch.full((700,), 7),
+                      torch.randint(10, 20, (300,))])
+    cols = torch.cat([torch.randperm(3000, generator=g)[:2500], torch.randperm(3000, generator=g)[:700],
+                      torch.randint(0, 3000, (300,), generator=g)])
+    key = torch.unique(rows * n_cols + cols)
+    rows, cols = key // n_cols, key % n_cols
+    vals = torch.rand(key.numel(), generator=g) * 3 + 0.5
+    csr = als_ops.build_csr(rows, cols, vals, n_rows, n_cols).to(cuda)
+    y = torch.randn(n_cols, k, generator=g) * 0.2
+    yb = y.to(cuda, torch.bfloat16)
+    yty = als_ops.gramian(yb.float())
+    x = torch.full((n_rows, k), 7.0, device=cuda)
+    als_ops.solve_rows(csr, yb, yty, x, None, k, 0.01, 1.0, True)
+    ref = als_ops.solve_rows_reference(csr, yb.float(), yty, k, 0.01, 1.0, True)
+    nz = csr.order.long()
+    assert (x[nz] - ref[nz]).abs().max().item() < 2e-2 * max(1.0, ref.abs().max().item())
+    empty = torch.ones(n_rows, dtype=torch.bool, device=cuda)
+    empty[nz] = False
+    assert (x[empty] == 7.0).all()  # untouched
+
+
+@pytest.mark.gpu
+def test_pair_dots(cuda):
+    x = torch.randn(100, 32, device=cuda)
+    y = torch.randn(80, 32, device=cuda)
+    us = torch.randint(0, 100, (1000,), device=cuda)
+    it = torch.randint(0, 80, (1000,), device=cuda)
+    out = als_ops.pair_dots(x, y, us, it)
+    ref = (x[us] * y[it]).sum(1)
+    assert torch.allclose(out, ref, atol=1e-4, rtol=1e-4)
