@@ -1,0 +1,252 @@
+"""ALS shared pieces: fold-in math and feature-vector stores.
+
+* :func:`compute_target_qui` / :func:`compute_updated_xu` -- scalar host versions of
+  ``ALSUtils`` (``[app-common]/als/ALSUtils.java:37-106``), bit-faithful to the reference's
+  float/double mix (used by ``/recommendToAnonymous`` etc.; the speed layer uses the batched
+  device form in :func:`oryx_amd.ops.als.fold_in`).
+* :class:`FeatureVectors` -- ``id -> vector`` store with "recent IDs" and Gramian
+  (``[app-common]/als/FeatureVectors.java:36-161``), backed by a growable matrix: a numpy host
+  mirror (O(1) lookups without device syncs) plus, when a device is given, a device-resident
+  copy in HBM that is refreshed lazily in one batched H2D copy per query burst.  Removed rows
+  are zeroed and recycled.  The device copy is what the GPU top-N scan reads.
+"""
+
+from __future__ import annotations
+
+import math
+import threading
+from typing import Callable, Collection, Dict, Iterable, List, Optional, Sequence, Set
+
+import numpy as np
+import torch
+
+from ...utils import lang, mathx
+
+__all__ = ["compute_target_qui", "compute_updated_xu", "FeatureVectors"]
+
+
+def compute_target_qui(implicit: bool, value: float, current_value: float) -> float:
+    if implicit:
+        if value > 0.0 and current_value < 1.0:
+            diff = 1.0 - max(0.0, current_value)
+            return current_value + (value / (1.0 + value)) * diff
+        if value < 0.0 and current_value > 0.0:
+            diff = -min(1.0, current_value)
+            return current_value + (value / (value - 1.0)) * diff
+        return float("nan")
+    return value
+
+
+def compute_updated_xu(solver, value: float, xu: Optional[np.ndarray], yi: Optional[np.ndarray],
+                       implicit: bool) -> Optional[np.ndarray]:
+    if yi is None:
+        return None
+    qui = 0.0 if xu is None else mathx.dot(xu, yi)
+    target = compute_target_qui(implicit, value, 0.5 if xu is None else qui)
+    if math.isnan(target):
+        return None
+    dqui = target - qui
+    dqui_yi = (np.asarray(yi, dtype=np.float32) * np.float32(dqui)).astype(np.float32)
+    dxu = solver.solve_f_to_f(dqui_yi)
+    if xu is None:
+        return dxu
+    return (np.asarray(xu, dtype=np.float32) + dxu).astype(np.float32)
+
+
+class FeatureVectors:
+    """Thread-safe ``id -> float32[k]`` store; optional device mirror for GPU scans."""
+
+    def __init__(self, features: int, device: Optional[torch.device] = None,
+                 initial_capacity: int = 1024, partitioner: Optional[Callable] = None):
+        self.k = int(features)
+        self.device = device
+        self._lock = lang.AutoReadWriteLock()
+        self._index: Dict[str, int] = {}
+        self._ids: List[Optional[str]] = []
+        self._free: List[int] = []
+        self._recent: Set[str] = set()
+        cap = max(16, int(initial_capacity))
+        self._host = np.zeros((cap, self.k), dtype=np.float32)
+        self._host_valid = np.zeros(cap, dtype=bool)
+        self._n_rows = 0                      # high-water mark of used rows
+        self._dirty: Set[int] = set()
+        self._dirty_all = False
+        self._dev = None                      # fp32 [cap, k]
+        self._dev_valid = None                # bool [cap]
+        self._dev_norm = None                 # fp32 [cap]
+        self._dev_lock = threading.Lock()
+        self.partitioner = partitioner        # rows -> partition ids (device LSH)
+        self._dev_part = None
+        self.version = 0
+
+    # ---------------------------------------------------------------- basic map API
+    def size(self) -> int:
+        return len(self._index)
+
+    def __len__(self):
+        return self.size()
+
+    def __contains__(self, id_: str) -> bool:
+        return id_ in self._index
+
+    def get_vector(self, id_: str) -> Optional[np.ndarray]:
+        with self._lock.read():
+            row = self._index.get(id_)
+            if row is None:
+                return None
+            return self._host[row].copy()
+
+    def row_of(self, id_: str) -> Optional[int]:
+        return self._index.get(id_)
+
+    def id_of_row(self, row: int) -> Optional[str]:
+        return self._ids[row] if row < len(self._ids) else None
+
+    def _alloc_row(self) -> int:
+        if self._free:
+            return self._free.pop()
+        row = self._n_rows
+        if row >= self._host.shape[0]:
+            cap = self._host.shape[0] * 2
+            host = np.zeros((cap, self.k), dtype=np.float32)
+            host[:self._host.shape[0]] = self._host
+            valid = np.zeros(cap, dtype=bool)
+            valid[:self._host_valid.shape[0]] = self._host_valid
+            self._host, self._host_valid = host, valid
+            self._dirty_all = True
+        self._n_rows += 1
+        self._ids.append(None)
+        return row
+
+    def set_vector(self, id_: str, vector) -> None:
+        v = np.asarray(vector, dtype=np.float32)
+        if v.shape != (self.k,):
+            raise ValueError("vector length %s != features %d" % (v.shape, self.k))
+        with self._lock.write():
+            row = self._index.get(id_)
+            if row is None:
+                row = self._alloc_row()
+                self._index[id_] = row
+                self._ids[row] = id_
+                self._recent.add(id_)
+            self._host[row] = v
+            self._host_valid[row] = True
+            self._dirty.add(row)
+            self.version += 1
+
+    def set_vectors(self, ids: Sequence[str], matrix: np.ndarray) -> None:
+        matrix = np.asarray(matrix, dtype=np.float32)
+        with self._lock.write():
+            for id_, v in zip(ids, matrix):
+                row = self._index.get(id_)
+                if row is None:
+                    row = self._alloc_row()
+                    self._index[id_] = row
+                    self._ids[row] = id_
+                    self._recent.add(id_)
+                self._host[row] = v
+                self._host_valid[row] = True
+                self._dirty.add(row)
+            self.version += 1
+
+    def remove_vector(self, id_: str) -> None:
+        with self._lock.write():
+            self._remove_locked(id_)
+
+    def _remove_locked(self, id_: str) -> None:
+        row = self._index.pop(id_, None)
+        self._recent.discard(id_)
+        if row is not None:
+            self._host[row] = 0.0
+            self._host_valid[row] = False
+            self._ids[row] = None
+            self._free.append(row)
+            self._dirty.add(row)
+            self.version += 1
+
+    def add_all_ids_to(self, out: Set[str]) -> None:
+        with self._lock.read():
+            out.update(self._index.keys())
+
+    def remove_all_ids_from(self, out: Set[str]) -> None:
+        with self._lock.read():
+            out.difference_update(self._index.keys())
+
+    def add_all_recent_to(self, out: Set[str]) -> None:
+        with self._lock.read():
+            out.update(self._recent)
+
+    def all_ids(self) -> List[str]:
+        with self._lock.read():
+            return list(self._index.keys())
+
+    def retain_recent_and_ids(self, new_model_ids: Collection[str]) -> None:
+        keep = new_model_ids if isinstance(new_model_ids, (set, frozenset)) else set(new_model_ids)
+        with self._lock.write():
+            for id_ in [i for i in self._index if i not in keep and i not in self._recent]:
+                self._remove_locked(id_)
+            self._recent.clear()
+
+    def for_each(self, fn: Callable[[str, np.ndarray], None]) -> None:
+        with self._lock.read():
+            for id_, row in self._index.items():
+                fn(id_, self._host[row])
+
+    def get_vtv(self) -> Optional[np.ndarray]:
+        """Gramian VᵀV (float64) on the device when present, else on the host."""
+        if self.size() == 0:
+            return None
+        if self.device is not None and self.device.type == "cuda":
+            mat, _, _ = self.device_view()
+            return mat.t().matmul(mat).double().cpu().numpy()
+        with self._lock.read():
+            m = self._host[:self._n_rows][self._host_valid[:self._n_rows]]
+            return mathx.transpose_times_self(m)
+
+    # ---------------------------------------------------------------- device mirror
+    def device_view(self):
+        """(matrix fp32 [n, k], valid bool [n], norms fp32 [n]) on the device, refreshed."""
+        if self.device is None:
+            raise RuntimeError("no device mirror")
+        with self._dev_lock:
+            with self._lock.read():
+                n = self._n_rows
+                need_full = (self._dev is None or self._dirty_all or
+                             self._dev.shape[0] < self._host.shape[0])
+                if need_full:
+                    cap = self._host.shape[0]
+                    self._dev = torch.from_numpy(self._host.copy()).to(self.device)
+                    self._dev_valid = torch.from_numpy(self._host_valid.copy()).to(self.device)
+                    self._dev_norm = self._dev.norm(dim=1)
+                    self._dirty.clear()
+                    self._dirty_all = False
+                    dirty_rows = None
+                elif self._dirty:
+                    rows = np.fromiter(self._dirty, dtype=np.int64, count=len(self._dirty))
+                    vals = torch.from_numpy(self._host[rows]).to(self.device, non_blocking=False)
+                    valid = torch.from_numpy(self._host_valid[rows]).to(self.device)
+                    self._dirty.clear()
+                    dirty_rows = torch.from_numpy(rows).to(self.device)
+                    self._dev.index_copy_(0, dirty_rows, vals)
+                    self._dev_valid.index_copy_(0, dirty_rows, valid)
+                    self._dev_norm.index_copy_(0, dirty_rows, vals.norm(dim=1))
+                else:
+                    dirty_rows = torch.empty(0, dtype=torch.int64, device=self.device)
+                if self.partitioner is not None:
+                    if need_full or self._dev_part is None:
+                        self._dev_part = self.partitioner(self._dev)
+                    elif dirty_rows is not None and dirty_rows.numel():
+                        self._dev_part[dirty_rows] = self.partitioner(self._dev[dirty_rows])
+            return self._dev[:n], self._dev_valid[:n], self._dev_norm[:n]
+
+    def device_partitions(self) -> Optional[torch.Tensor]:
+        if self._dev_part is None:
+            return None
+        return self._dev_part[:self._n_rows]
+
+    def host_rows(self, ids: Iterable[str]) -> List[int]:
+        idx = self._index
+        return [r for r in (idx.get(i) for i in ids) if r is not None]
+
+    def __repr__(self):
+        return "FeatureVectors[size:%d]" % self.size()

@@ -1,0 +1,419 @@
+"""ALS serving model: GPU-resident item factors, host user factors, known items, top-N.
+
+Equivalent of ``ALSServingModel`` / ``ALSServingModelManager`` / ``LocalitySensitiveHash`` /
+``TopNConsumer`` (``[serving-app]/als/model/ALSServingModel.java:58-496``,
+``ALSServingModelManager.java:63-154``, ``LocalitySensitiveHash.java:26-188``,
+``TopNConsumer.java:55-74``) re-designed for MI355X:
+
+* Y (items) lives in HBM as one fp32 matrix (``FeatureVectors`` device mirror) with a norms
+  vector; ``UP`` rows are applied to a host mirror and flushed to the device in one batched
+  copy before the next query, so a model load of millions of rows costs a few copies;
+* top-N is a full scan on the GPU: ``scores = Y q`` (one GEMV, or a GEMM for micro-batched
+  queries), known items / filtered rows masked to -inf, then ``topk``; cosine similarity
+  divides by the norms vector.  This replaces the reference's thread-pool scan of LSH
+  partitions.  LSH is kept for semantic parity when ``oryx.als.sample-rate < 1``: each item's
+  hash bucket is computed on the device at flush time and non-candidate buckets are masked;
+* YᵀY for anonymous fold-in is a device GEMM, cached until Y changes.
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+import threading
+from typing import Collection, Dict, Iterable, Iterator, List, Optional, Sequence, Set, Tuple
+
+import numpy as np
+import torch
+
+from ...api import AbstractServingModelManager, KeyMessage, ServingModel
+from ...utils import mathx, pmml as pmmlu, rng, text
+from ...utils.lang import AutoReadWriteLock
+from .common import FeatureVectors
+from .rescorer import Rescorer, RescorerProvider, load_rescorer_providers
+
+__all__ = ["ALSServingModel", "ALSServingModelManager", "LocalitySensitiveHash",
+           "RESCORE_FULL_POOL"]
+
+log = logging.getLogger(__name__)
+
+RESCORE_FULL_POOL = 1 << 17
+
+
+def _binom(n: int, k: int) -> int:
+    return math.comb(n, k)
+
+
+class LocalitySensitiveHash:
+    MAX_HASHES = 16
+
+    def __init__(self, sample_rate: float, num_features: int, num_cores: Optional[int] = None):
+        import os
+        if num_cores is None:
+            num_cores = os.cpu_count() or 1
+        num_hashes = 0
+        bits_differing = 0
+        while num_hashes < self.MAX_HASHES:
+            bits_differing = 0
+            num_partitions_to_try = 1
+            while bits_differing < num_hashes and num_partitions_to_try < num_cores:
+                bits_differing += 1
+                num_partitions_to_try += _binom(num_hashes, bits_differing)
+            if bits_differing == num_hashes and num_partitions_to_try < num_cores:
+                num_hashes += 1
+                continue
+            if num_partitions_to_try <= sample_rate * (1 << num_hashes):
+                break
+            num_hashes += 1
+        log.info("LSH with %d hashes, querying partitions with up to %d bits differing",
+                 num_hashes, bits_differing)
+        self.max_bits_differing = bits_differing
+        gen = rng.get_random()
+        vectors: List[np.ndarray] = []
+        for i in range(num_hashes):
+            best_total, next_best, since_best = math.inf, None, 0
+            while since_best < 1000:
+                cand = mathx.random_vector_f(num_features, gen)
+                score = self._total_abs_cos(vectors, cand)
+                if score < best_total:
+                    next_best = cand
+                    if score == 0.0:
+                        break
+                    best_total = score
+                    since_best = 0
+                else:
+                    since_best += 1
+            vectors.append(next_best)
+        self.hash_vectors = np.array(vectors, dtype=np.float32).reshape(num_hashes, num_features)
+        # candidate prototype: all 2^n ints ordered by popcount
+        n = num_hashes
+        proto = sorted(range(1 << n), key=lambda i: (bin(i).count("1"), i))
+        # the reference fills each popcount class in increasing order
+        self._prototype = np.array(proto, dtype=np.int64)
+        self._all = np.arange(1 << n, dtype=np.int64)
+        self._dev_vectors: Dict[str, torch.Tensor] = {}
+
+    @staticmethod
+    def _total_abs_cos(existing, new) -> float:
+        new_norm = mathx.norm(new)
+        s = 0.0
+        for e in existing:
+            s += abs(mathx.dot(e, new)) / mathx.norm(e) / new_norm
+        return s
+
+    def get_num_hashes(self) -> int:
+        return self.hash_vectors.shape[0]
+
+    def get_num_partitions(self) -> int:
+        return 1 << self.get_num_hashes()
+
+    def get_max_bits_differing(self) -> int:
+        return self.max_bits_differing
+
+    def get_index_for(self, vector) -> int:
+        index = 0
+        for i, h in enumerate(self.hash_vectors):
+            if mathx.dot(h, vector) > 0.0:
+                index |= 1 << i
+        return index
+
+    def get_candidate_indices(self, vector) -> np.ndarray:
+        main = self.get_index_for(vector)
+        n = self.get_num_hashes()
+        if n == self.max_bits_differing:
+            return self._all
+        if self.max_bits_differing == 0:
+            return np.array([main], dtype=np.int64)
+        how_many = sum(_binom(n, i) for i in range(self.max_bits_differing + 1))
+        return self._prototype[:how_many] ^ main
+
+    def device_partitioner(self, device):
+        """rows [m, k] fp32 (device) -> bucket index per row, computed as sign bits of H v."""
+        n = self.get_num_hashes()
+        if n == 0:
+            return None
+        key = str(device)
+        if key not in self._dev_vectors:
+            self._dev_vectors[key] = torch.from_numpy(self.hash_vectors).to(device)
+        H = self._dev_vectors[key]
+        weights = (1 << torch.arange(n, device=device, dtype=torch.int64))
+
+        def part(rows: torch.Tensor) -> torch.Tensor:
+            bits = (rows.matmul(H.t()) > 0).to(torch.int64)
+            return (bits * weights).sum(1)
+        return part
+
+
+class ALSServingModel(ServingModel):
+    def __init__(self, features: int, implicit: bool, sample_rate: float = 1.0,
+                 rescorer_provider: Optional[RescorerProvider] = None,
+                 device: Optional[torch.device] = None):
+        if features <= 0 or not (0.0 < sample_rate <= 1.0):
+            raise ValueError("bad features / sample rate")
+        if device is None:
+            device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+        self.device = device
+        # one GPU scans every candidate bucket at once: size the LSH for the sample rate alone
+        self.lsh = LocalitySensitiveHash(sample_rate, features, num_cores=1)
+        self.features = features
+        self.implicit = implicit
+        self.rescorer_provider = rescorer_provider
+        self.X = FeatureVectors(features, None)
+        self.Y = FeatureVectors(features, device,
+                                partitioner=self.lsh.device_partitioner(device))
+        self._known: Dict[str, Set[str]] = {}
+        self._known_lock = AutoReadWriteLock()
+        self._expected_users: Set[str] = set()
+        self._expected_items: Set[str] = set()
+        self._expected_lock = threading.Lock()
+        self._yty_solver = None
+        self._yty_version = -1
+
+    # ---------------------------------------------------------------- accessors
+    def get_features(self) -> int:
+        return self.features
+
+    def is_implicit(self) -> bool:
+        return self.implicit
+
+    def get_rescorer_provider(self) -> Optional[RescorerProvider]:
+        return self.rescorer_provider
+
+    def get_user_vector(self, user: str) -> Optional[np.ndarray]:
+        return self.X.get_vector(user)
+
+    def get_item_vector(self, item: str) -> Optional[np.ndarray]:
+        return self.Y.get_vector(item)
+
+    def set_user_vector(self, user: str, vector) -> None:
+        if len(vector) != self.features:
+            raise ValueError("wrong vector length")
+        self.X.set_vector(user, vector)
+        with self._expected_lock:
+            self._expected_users.discard(user)
+
+    def set_item_vector(self, item: str, vector) -> None:
+        if len(vector) != self.features:
+            raise ValueError("wrong vector length")
+        self.Y.set_vector(item, vector)
+        with self._expected_lock:
+            self._expected_items.discard(item)
+
+    def get_known_items(self, user: str) -> Set[str]:
+        with self._known_lock.read():
+            s = self._known.get(user)
+            return set(s) if s else set()
+
+    def add_known_items(self, user: str, items: Iterable[str]) -> None:
+        with self._known_lock.write():
+            s = self._known.get(user)
+            if s is None:
+                s = self._known[user] = set()
+            s.update(items)
+
+    def get_user_counts(self) -> Dict[str, int]:
+        with self._known_lock.read():
+            return {u: len(s) for u, s in self._known.items()}
+
+    def get_item_counts(self) -> Dict[str, int]:
+        counts: Dict[str, int] = {}
+        with self._known_lock.read():
+            for s in self._known.values():
+                for i in s:
+                    counts[i] = counts.get(i, 0) + 1
+        return counts
+
+    def get_known_item_vectors_for_user(self, user: str):
+        if self.get_user_vector(user) is None:
+            return None
+        known = self.get_known_items(user)
+        if not known:
+            return None
+        out = []
+        for item in known:
+            v = self.get_item_vector(item)
+            if v is not None:
+                out.append((item, v))
+        return out or None
+
+    def get_all_user_ids(self) -> List[str]:
+        return self.X.all_ids()
+
+    def get_all_item_ids(self) -> List[str]:
+        return self.Y.all_ids()
+
+    def get_num_users(self) -> int:
+        return self.X.size()
+
+    def get_num_items(self) -> int:
+        return self.Y.size()
+
+    # ---------------------------------------------------------------- top-N on the GPU
+    def top_n(self, target: np.ndarray, how_many: int, cosine: bool = False,
+              exclude: Optional[Collection[str]] = None,
+              rescorer: Optional[Rescorer] = None) -> List[Tuple[str, float]]:
+        """Best ``how_many`` items by ``dot(y, target)`` (or ``/|y|`` when ``cosine``).
+
+        ``exclude``: item IDs never returned.  ``rescorer``: filter + rescore on the host over
+        a candidate pool of the best raw scores (all items when the catalogue is small).
+        """
+        if how_many <= 0 or self.Y.size() == 0:
+            return []
+        mat, valid, norms = self.Y.device_view()
+        n = mat.shape[0]
+        if n == 0:
+            return []
+        q = torch.as_tensor(np.asarray(target, dtype=np.float32), device=mat.device)
+        scores = mat.matmul(q)
+        if cosine:
+            scores = scores / norms
+        neg_inf = torch.tensor(float("-inf"), device=mat.device)
+        scores = torch.where(valid, scores, neg_inf)
+        parts = self.Y.device_partitions()
+        if parts is not None and self.lsh.get_max_bits_differing() < self.lsh.get_num_hashes():
+            cand = torch.zeros(self.lsh.get_num_partitions(), dtype=torch.bool,
+                               device=mat.device)
+            cand[torch.from_numpy(self.lsh.get_candidate_indices(target)).to(mat.device)] = True
+            scores = torch.where(cand[parts], scores, neg_inf)
+        if exclude:
+            rows = self.Y.host_rows(exclude)
+            if rows:
+                scores[torch.as_tensor(rows, device=mat.device)] = float("-inf")
+        n_valid = self.Y.size()
+        if rescorer is None:
+            m = min(how_many, n)
+            vals, idx = torch.topk(scores, m)
+            vals, idx = vals.cpu().numpy(), idx.cpu().numpy()
+            out = []
+            for v, i in zip(vals, idx):
+                if v == float("-inf"):
+                    break
+                id_ = self.Y.id_of_row(int(i))
+                if id_ is not None:
+                    out.append((id_, float(v)))
+            return out
+        pool = n if n_valid <= RESCORE_FULL_POOL else min(n, max(how_many * 16, 4096))
+        vals, idx = torch.topk(scores, pool)
+        vals, idx = vals.cpu().numpy(), idx.cpu().numpy()
+        heap: List[Tuple[float, str]] = []
+        for v, i in zip(vals, idx):
+            if v == float("-inf"):
+                break
+            id_ = self.Y.id_of_row(int(i))
+            if id_ is None or rescorer.is_filtered(id_):
+                continue
+            s = rescorer.rescore(id_, float(v))
+            if not (s > float("-inf")) or math.isnan(s):
+                continue
+            heap.append((s, id_))
+        heap.sort(key=lambda t: -t[0])
+        return [(i, s) for s, i in heap[:how_many]]
+
+    def get_yty_solver(self):
+        ver = self.Y.version
+        if self._yty_solver is not None and self._yty_version == ver:
+            return self._yty_solver
+        vtv = self.Y.get_vtv()
+        solver = mathx.get_solver(vtv)
+        self._yty_solver, self._yty_version = solver, ver
+        return solver
+
+    # ---------------------------------------------------------------- model-update pruning
+    def retain_recent_and_user_ids(self, users: Collection[str]) -> None:
+        self.X.retain_recent_and_ids(users)
+        with self._expected_lock:
+            self._expected_users = set(users)
+            self.X.remove_all_ids_from(self._expected_users)
+
+    def retain_recent_and_item_ids(self, items: Collection[str]) -> None:
+        self.Y.retain_recent_and_ids(items)
+        with self._expected_lock:
+            self._expected_items = set(items)
+            self.Y.remove_all_ids_from(self._expected_items)
+
+    def retain_recent_and_known_items(self, users: Collection[str], items: Collection[str]
+                                      ) -> None:
+        recent_users: Set[str] = set()
+        self.X.add_all_recent_to(recent_users)
+        with self._known_lock.write():
+            for u in [u for u in self._known if u not in users and u not in recent_users]:
+                del self._known[u]
+        recent_items: Set[str] = set()
+        self.Y.add_all_recent_to(recent_items)
+        with self._known_lock.write():
+            for s in self._known.values():
+                drop = [i for i in s if i not in items and i not in recent_items]
+                s.difference_update(drop)
+
+    def get_fraction_loaded(self) -> float:
+        with self._expected_lock:
+            expected = len(self._expected_users) + len(self._expected_items)
+        if expected == 0:
+            return 1.0
+        loaded = float(self.get_num_users() + self.get_num_items())
+        return loaded / (loaded + expected)
+
+    def __repr__(self):
+        return ("ALSServingModel[features:%d, implicit:%s, X:(%d users), Y:(%d items), "
+                "fractionLoaded:%s, device:%s]" % (self.features, self.implicit,
+                                                   self.get_num_users(), self.get_num_items(),
+                                                   self.get_fraction_loaded(), self.device))
+
+
+class ALSServingModelManager(AbstractServingModelManager):
+    def __init__(self, config):
+        super().__init__(config)
+        self.sample_rate = config.get_double("oryx.als.sample-rate")
+        self.rescorer_provider = load_rescorer_providers(
+            config.get_string("oryx.als.rescorer-provider-class")
+            if config.has_path("oryx.als.rescorer-provider-class") else None)
+        if not (0.0 < self.sample_rate <= 1.0):
+            raise ValueError("sample-rate must be in (0,1]")
+        self.model: Optional[ALSServingModel] = None
+
+    def consume(self, updates: Iterator[KeyMessage], context=None) -> None:
+        countdown = 10000
+        for km in updates:
+            key, message = km.key, km.message
+            if key is None:
+                raise ValueError("Bad message: %r" % (km,))
+            if key == "UP":
+                if self.model is None:
+                    continue
+                update = text.read_json(message)
+                id_ = str(update[1])
+                vector = np.asarray(update[2], dtype=np.float32)
+                which = update[0]
+                if which == "X":
+                    self.model.set_user_vector(id_, vector)
+                    if len(update) > 3:
+                        self.model.add_known_items(id_, [str(x) for x in update[3]])
+                elif which == "Y":
+                    self.model.set_item_vector(id_, vector)
+                else:
+                    raise ValueError("Bad message: %r" % (km,))
+                countdown -= 1
+                if countdown <= 0:
+                    log.info("%s", self.model)
+                    countdown = 10000
+            elif key in ("MODEL", "MODEL-REF"):
+                log.info("Loading new model")
+                pmml = pmmlu.read_pmml_from_update_key_message(key, message)
+                features = int(pmml.get_extension_value("features"))
+                implicit = pmml.get_extension_value("implicit").lower() == "true"
+                if self.model is None or features != self.model.get_features():
+                    log.warning("No previous model, or # features has changed; creating new one")
+                    self.model = ALSServingModel(features, implicit, self.sample_rate,
+                                                 self.rescorer_provider)
+                log.info("Updating model")
+                xids = set(pmml.get_extension_content("XIDs") or [])
+                yids = set(pmml.get_extension_content("YIDs") or [])
+                self.model.retain_recent_and_known_items(xids, yids)
+                self.model.retain_recent_and_user_ids(xids)
+                self.model.retain_recent_and_item_ids(yids)
+                log.info("Model updated: %s", self.model)
+            else:
+                raise ValueError("Bad message: %r" % (km,))
+
+    def get_model(self) -> Optional[ALSServingModel]:
+        return self.model

@@ -1,0 +1,218 @@
+"""The serving layer: HTTP API over an in-memory (GPU-resident) model fed by the update topic.
+
+Equivalent of ``ServingLayer`` + ``ModelManagerListener`` (``[lserving]/ServingLayer.java:88-339``,
+``[lserving]/ModelManagerListener.java:103-224``):
+
+* loads ``oryx.serving.model-manager-class`` by name (reference Java names are aliased);
+* unless ``oryx.serving.api.read-only``, opens an async producer on the input topic
+  (``/ingest``, ``/pref``, ``/add``, ``/train`` write there);
+* starts a consumer thread that replays the update topic **from the beginning** into
+  ``manager.consume`` and keeps tailing it;
+* serves the resources of ``oryx.serving.application-resources`` (plus ``/ready``,
+  ``/error``, ``/metrics``) on ``oryx.serving.api.port`` -- or HTTPS on ``secure-port`` when a
+  key/cert is configured -- with optional DIGEST auth and a context path.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+import ssl
+import threading
+import time
+from typing import Iterator, List, Optional
+
+from ..api import KeyMessage, ServingModelManager
+from ..metrics import Registry
+from ..transport import log as tlog
+from ..transport.producer import LogTopicProducer, topic_root
+from ..utils import config as cfg
+from ..utils import ioutils, lang
+from . import http
+from .resources import INPUT_PRODUCER_KEY, MODEL_MANAGER_KEY
+
+__all__ = ["ServingLayer", "UpdateIterator", "resource_modules"]
+
+log = logging.getLogger(__name__)
+
+
+class UpdateIterator:
+    """Blocking iterator of :class:`KeyMessage` over a topic, until closed."""
+
+    def __init__(self, consumer: tlog.TopicConsumer, poll_ms: int = 100):
+        self.consumer = consumer
+        self.poll_ms = poll_ms
+        self.closed = False
+        self._pending: List = []
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> KeyMessage:
+        while not self._pending:
+            if self.closed:
+                raise StopIteration
+            recs = self.consumer.poll(8192, self.poll_ms)
+            self._pending = [KeyMessage(k, v) for _, _, _, k, v in recs]
+            self._pending.reverse()
+        return self._pending.pop()
+
+    def has_buffered(self) -> bool:
+        return bool(self._pending)
+
+    def close(self) -> None:
+        self.closed = True
+
+
+def resource_modules(config) -> List[str]:
+    mods = ["oryx_amd.serving.resources"]
+    names = cfg.get_optional_string(config, "oryx.serving.application-resources")
+    if names:
+        for n in names.split(","):
+            n = n.strip()
+            if n:
+                mods.append(lang.JAVA_CLASS_ALIASES.get(n, n))
+    else:
+        mgr = cfg.get_optional_string(config, "oryx.serving.model-manager-class")
+        if mgr:
+            mgr = lang.JAVA_CLASS_ALIASES.get(mgr, mgr)
+            pkg = mgr.rsplit(".", 2)[0]
+            mods.append(pkg + ".resources")
+    out = []
+    for m in mods:
+        if m not in out:
+            out.append(m)
+    return out
+
+
+class ServingLayer:
+    def __init__(self, config, manager: Optional[ServingModelManager] = None,
+                 input_producer=None, host: str = "0.0.0.0"):
+        self.config = config
+        self.host = host
+        self.read_only = config.get_bool("oryx.serving.api.read-only")
+        self.port = config.get_int("oryx.serving.api.port")
+        self.secure_port = config.get_int("oryx.serving.api.secure-port")
+        self.user_name = cfg.get_optional_string(config, "oryx.serving.api.user-name")
+        self.password = cfg.get_optional_string(config, "oryx.serving.api.password")
+        self.keystore_file = cfg.get_optional_string(config, "oryx.serving.api.keystore-file")
+        self.key_file = cfg.get_optional_string(config, "oryx.serving.api.key-file")
+        self.keystore_password = cfg.get_optional_string(config,
+                                                         "oryx.serving.api.keystore-password")
+        self.context_path = config.get_string("oryx.serving.api.context-path")
+        self.update_topic = config.get_string("oryx.update-topic.message.topic")
+        self.update_broker = config.get_string("oryx.update-topic.broker")
+        self.input_topic = config.get_string("oryx.input-topic.message.topic")
+        self.input_broker = config.get_string("oryx.input-topic.broker")
+        self.max_message = config.get_int("oryx.update-topic.message.max-size")
+        self._manager = manager
+        self._input_producer = input_producer
+        self._server: Optional[http.OryxHTTPServer] = None
+        self._consumer_thread: Optional[threading.Thread] = None
+        self._updates: Optional[UpdateIterator] = None
+        self._consumer: Optional[tlog.TopicConsumer] = None
+        self._closed = threading.Event()
+        self.metrics = Registry()
+        self.context: dict = {"config": config, "metrics": self.metrics}
+
+    # ---------------------------------------------------------------- lifecycle
+    def _load_manager(self) -> ServingModelManager:
+        name = self.config.get_string("oryx.serving.model-manager-class")
+        return lang.load_instance_of(name, None, self.config)
+
+    def start(self) -> "ServingLayer":
+        log.info("Starting serving layer")
+        if self._manager is None:
+            self._manager = self._load_manager()
+        self.context[MODEL_MANAGER_KEY] = self._manager
+        no_init = self.config.get_bool("oryx.serving.no-init-topics")
+        if not self.read_only:
+            if self._input_producer is None:
+                partitions = self.config.get_int("oryx.input-topic.partitions")
+                self._input_producer = LogTopicProducer(self.input_broker, self.input_topic,
+                                                        self.config, async_=True,
+                                                        create_partitions=partitions)
+            self.context[INPUT_PRODUCER_KEY] = self._input_producer
+        if not no_init:
+            self._start_update_consumer()
+        router = http.Router(http.collect_routes(resource_modules(self.config)),
+                             self.context_path)
+        ssl_ctx = self._ssl_context()
+        auth = None
+        if self.user_name and self.password:
+            auth = http.DigestAuth(self.user_name, self.password)
+        port = self.secure_port if ssl_ctx is not None else self.port
+        self._server = http.OryxHTTPServer(self.host, port, router, self.context, ssl_ctx, auth,
+                                           self.metrics)
+        self._server.start_background()
+        log.info("Serving layer listening on %s:%d%s", self.host, self._server.port,
+                 " (HTTPS)" if ssl_ctx else "")
+        lang.close_at_shutdown(self)
+        return self
+
+    def _ssl_context(self) -> Optional[ssl.SSLContext]:
+        cert = self.keystore_file
+        if not cert:
+            return None
+        cert = ioutils.to_local_path(cert)
+        key = ioutils.to_local_path(self.key_file) if self.key_file else None
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+        ctx.load_cert_chain(cert, key, password=self.keystore_password)
+        return ctx
+
+    def _start_update_consumer(self) -> None:
+        root = topic_root(self.update_broker, self.config)
+        tlog.maybe_create_topic(root, self.update_topic, 1, self.max_message)
+        topic = tlog.Topic(root, self.update_topic)
+        self._consumer = tlog.TopicConsumer(topic, start="earliest")
+        self._updates = UpdateIterator(self._consumer)
+
+        def run():
+            try:
+                self._manager.consume(self._updates, None)
+            except Exception:
+                log.exception("Error while consuming updates")
+                self.close()
+
+        self._consumer_thread = threading.Thread(target=run,
+                                                 name="OryxServingLayerUpdateConsumerThread",
+                                                 daemon=True)
+        self._consumer_thread.start()
+
+    @property
+    def actual_port(self) -> int:
+        return self._server.port if self._server else -1
+
+    @property
+    def manager(self) -> Optional[ServingModelManager]:
+        return self._manager
+
+    def await_termination(self, timeout: Optional[float] = None) -> None:
+        self._closed.wait(timeout)
+
+    def close(self) -> None:
+        if self._closed.is_set():
+            return
+        self._closed.set()
+        log.info("Shutting down serving layer")
+        if self._server is not None:
+            self._server.shutdown()
+            self._server.server_close()
+        if self._updates is not None:
+            self._updates.close()
+        if self._consumer_thread is not None:
+            self._consumer_thread.join(timeout=10)
+        if self._consumer is not None:
+            self._consumer.close()
+        if self._manager is not None:
+            self._manager.close()
+        if self._input_producer is not None:
+            self._input_producer.close()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
