@@ -1,0 +1,247 @@
+// oryx_ingest.cpp -- native data loading for the batch/speed layers.
+//
+// The reference parses input lines inside Spark tasks ([app-common]/common/fn/MLFunctions.java:39-65,
+// [mllib]/als/ALSUpdate.java:260-290) and maps string IDs to ints by parse-or-MD5-hash with a
+// reverse lookup collected to the driver (C4 in SURVEY.md section 2.5).  Here one C++ pass turns a
+// buffer of "user,item[,strength[,timestamp]]" lines (or JSON arrays) into dense dictionary
+// codes, strengths (NaN = delete) and timestamps, ready to upload as device tensors; the
+// dictionaries are collision-free (no hashing of IDs) and persist across intervals.
+// Also: shortest-round-trip float formatting of factor rows for JSON update messages.
+
+#include <charconv>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+struct Dict {
+  std::unordered_map<std::string, int64_t> map;
+  std::vector<std::string> keys;
+  std::mutex mu;
+  int64_t encode(std::string_view s) {
+    auto it = map.find(std::string(s));
+    if (it != map.end()) return it->second;
+    int64_t code = (int64_t)keys.size();
+    keys.emplace_back(s);
+    map.emplace(keys.back(), code);
+    return code;
+  }
+};
+
+// Parse one CSV field starting at p (RFC 4180 quotes, backslash escapes).  Returns end position.
+const char* csv_field(const char* p, const char* end, std::string& out) {
+  out.clear();
+  if (p < end && *p == '"') {
+    ++p;
+    while (p < end) {
+      char c = *p;
+      if (c == '\\' && p + 1 < end) { out.push_back(p[1]); p += 2; continue; }
+      if (c == '"') {
+        if (p + 1 < end && p[1] == '"') { out.push_back('"'); p += 2; continue; }
+        ++p;
+        break;
+      }
+      out.push_back(c);
+      ++p;
+    }
+    while (p < end && *p != ',') out.push_back(*p++);
+  } else {
+    while (p < end && *p != ',') {
+      if (*p == '\\' && p + 1 < end) { out.push_back(p[1]); p += 2; continue; }
+      out.push_back(*p++);
+    }
+  }
+  return p;
+}
+
+// Minimal JSON array-of-primitives parser: ["a", 1, "2.5", 123] -> tokens as strings.
+bool json_fields(const char* p, const char* end, std::vector<std::string>& toks) {
+  toks.clear();
+  if (p >= end || *p != '[') return false;
+  ++p;
+  std::string cur;
+  while (p < end) {
+    while (p < end && (*p == ' ' || *p == '\t' || *p == ',')) ++p;
+    if (p >= end) return false;
+    if (*p == ']') return true;
+    cur.clear();
+    if (*p == '"') {
+      ++p;
+      while (p < end && *p != '"') {
+        if (*p == '\\' && p + 1 < end) {
+          char e = p[1];
+          cur.push_back(e == 'n' ? '\n' : e == 't' ? '\t' : e);
+          p += 2;
+          continue;
+        }
+        cur.push_back(*p++);
+      }
+      ++p;
+    } else {
+      while (p < end && *p != ',' && *p != ']' && *p != ' ') cur.push_back(*p++);
+      if (cur == "null") cur.clear();
+    }
+    toks.push_back(cur);
+  }
+  return false;
+}
+
+bool parse_double(const std::string& s, double* out) {
+  if (s.empty()) return false;
+  const char* b = s.data();
+  const char* e = b + s.size();
+  while (b < e && (*b == ' ' || *b == '+')) ++b;
+  auto r = std::from_chars(b, e, *out);
+  return r.ec == std::errc() && r.ptr == e;
+}
+
+}  // namespace
+
+extern "C" {
+
+void* oryx_dict_new() { return new Dict(); }
+void oryx_dict_free(void* d) { delete static_cast<Dict*>(d); }
+long long oryx_dict_size(void* d) { return (long long)static_cast<Dict*>(d)->keys.size(); }
+
+// Encodes n strings packed back to back (lengths in lens) -> codes.  Returns n.
+long long oryx_dict_encode(void* dh, const char* buf, long long buf_len, int n, long long* codes) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  // buf holds n NUL-terminated strings
+  const char* p = buf;
+  const char* end = buf + buf_len;
+  for (int i = 0; i < n && p < end; ++i) {
+    size_t len = strnlen(p, end - p);
+    codes[i] = d->encode(std::string_view(p, len));
+    p += len + 1;
+  }
+  return n;
+}
+
+long long oryx_dict_get(void* dh, const char* s, long long len) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  auto it = d->map.find(std::string(s, (size_t)len));
+  return it == d->map.end() ? -1 : it->second;
+}
+
+// Copies key `code` into out (cap bytes); returns its length (or -1).
+long long oryx_dict_key(void* dh, long long code, char* out, long long cap) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  if (code < 0 || code >= (long long)d->keys.size()) return -1;
+  const std::string& k = d->keys[code];
+  if ((long long)k.size() <= cap) memcpy(out, k.data(), k.size());
+  return (long long)k.size();
+}
+
+// Parses newline-separated rating lines.  users/items: dictionaries; outputs per parsed row:
+// user code, item code, strength (NaN when the field is empty = delete; 1 when missing),
+// timestamp (default_ts when missing).  Returns rows parsed, or -(line number + 1) of the
+// first malformed line when strict.
+long long oryx_parse_ratings(const char* buf, long long len, void* users, void* items,
+                             long long* out_u, long long* out_i, double* out_s,
+                             long long* out_ts, long long max_rows, long long default_ts,
+                             int strict) {
+  Dict* du = static_cast<Dict*>(users);
+  Dict* di = static_cast<Dict*>(items);
+  std::lock_guard<std::mutex> gu(du->mu);
+  std::unique_lock<std::mutex> gi(di->mu, std::defer_lock);
+  if (di != du) gi.lock();
+  const char* p = buf;
+  const char* end = buf + len;
+  long long rows = 0, line_no = 0;
+  std::vector<std::string> toks;
+  std::string field;
+  while (p < end && rows < max_rows) {
+    const char* nl = static_cast<const char*>(memchr(p, '\n', end - p));
+    const char* le = nl ? nl : end;
+    const char* lend = le;
+    if (lend > p && lend[-1] == '\r') --lend;
+    if (lend > p) {
+      toks.clear();
+      if (*p == '[' && lend[-1] == ']') {
+        if (!json_fields(p, lend, toks)) toks.clear();
+      } else {
+        const char* q = p;
+        while (true) {
+          q = csv_field(q, lend, field);
+          toks.push_back(field);
+          if (q >= lend) break;
+          ++q;  // comma
+          if (q >= lend) { toks.emplace_back(); break; }
+        }
+      }
+      bool ok = toks.size() >= 2;
+      double s = 1.0;
+      long long ts = default_ts;
+      if (ok && toks.size() >= 3) {
+        if (toks[2].empty()) s = std::numeric_limits<double>::quiet_NaN();
+        else ok = parse_double(toks[2], &s);
+      }
+      if (ok && toks.size() >= 4 && !toks[3].empty()) {
+        double t;
+        ok = parse_double(toks[3], &t);
+        ts = (long long)t;
+      }
+      if (ok) {
+        out_u[rows] = du->encode(toks[0]);
+        out_i[rows] = di->encode(toks[1]);
+        out_s[rows] = s;
+        out_ts[rows] = ts;
+        ++rows;
+      } else if (strict) {
+        return -(line_no + 1);
+      }
+    }
+    ++line_no;
+    p = nl ? nl + 1 : end;
+  }
+  return rows;
+}
+
+// Formats rows of a float matrix as JSON arrays "[v0,v1,...]" with shortest round-trip
+// float32 text, back to back in out; row_ends[r] = end offset of row r.  Returns bytes used
+// or -1 when out is too small.
+long long oryx_format_float_rows(const float* mat, long long n, int k, long long stride,
+                                 char* out, long long cap, long long* row_ends) {
+  long long pos = 0;
+  char tmp[32];
+  for (long long r = 0; r < n; ++r) {
+    const float* row = mat + r * stride;
+    if (pos + 2 + (long long)k * 16 > cap) return -1;
+    out[pos++] = '[';
+    for (int j = 0; j < k; ++j) {
+      if (j) out[pos++] = ',';
+      float v = row[j];
+      if (std::isnan(v)) { memcpy(out + pos, "NaN", 3); pos += 3; continue; }
+      if (std::isinf(v)) {
+        const char* s = v > 0 ? "Infinity" : "-Infinity";
+        size_t l = strlen(s);
+        memcpy(out + pos, s, l);
+        pos += l;
+        continue;
+      }
+      auto res = std::to_chars(tmp, tmp + sizeof(tmp), v);
+      size_t l = res.ptr - tmp;
+      // Java-style: always show a decimal point for integral values ("1.0")
+      bool has_dot = false;
+      for (size_t q = 0; q < l; ++q) if (tmp[q] == '.' || tmp[q] == 'e') { has_dot = true; break; }
+      memcpy(out + pos, tmp, l);
+      pos += l;
+      if (!has_dot) { out[pos++] = '.'; out[pos++] = '0'; }
+    }
+    out[pos++] = ']';
+    row_ends[r] = pos;
+  }
+  return pos;
+}
+
+}  // extern "C"

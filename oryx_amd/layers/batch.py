@@ -1,0 +1,172 @@
+"""The batch layer: periodic full retraining over all history.
+
+Equivalent of ``BatchLayer`` + ``BatchUpdateFunction`` + ``SaveToHDFSFunction`` +
+``DeleteOldDataFn`` + ``UpdateOffsetsFn`` (``[lambda]/batch/BatchLayer.java:58-184``,
+``[lambda]/batch/BatchUpdateFunction.java:86-171``, ``SaveToHDFSFunction.java:59-76``,
+``[lambda]/DeleteOldDataFn.java:42-76``, ``[lambda]/UpdateOffsetsFn.java:56-67``).  Every
+``generation-interval-sec``:
+
+1. drain the input topic since the last interval (the interval's new data);
+2. if non-empty: read all past data (``data-dir/*/part-*``), open a *synchronous* producer on
+   the update topic and call the update class's ``run_update`` (the update runs before the
+   save, so past data never includes the current interval);
+3. save the new data as ``data-dir/oryx-<ms>.data/part-00000`` (JSON lines ``[key,message]``);
+4. commit input offsets (when ``oryx.id`` is set);
+5. delete data (and model) dirs older than ``max-age-data-hours`` (``max-age-model-hours``).
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import os
+import re
+import time
+from typing import List, Optional, Tuple
+
+from ..api import BatchLayerUpdate, Dataset
+from ..transport.producer import LogTopicProducer
+from ..utils import config as cfg
+from ..utils import ioutils, lang
+from .common import AbstractLayer, IntervalTimer, drain
+
+__all__ = ["BatchLayer", "save_interval_data", "read_past_data", "delete_old_data"]
+
+log = logging.getLogger(__name__)
+
+_TS_RE = re.compile(r"-(\d+)\.")
+
+
+def save_interval_data(data_dir: str, timestamp: int, records) -> Optional[str]:
+    if not records:
+        return None
+    d = os.path.join(ioutils.to_local_path(data_dir), "oryx-%d.data" % timestamp)
+    tmp = d + ".tmp"
+    os.makedirs(tmp, exist_ok=True)
+    with open(os.path.join(tmp, "part-00000"), "w", encoding="utf-8") as f:
+        for k, m in records:
+            f.write(json.dumps([k, m], separators=(",", ":")))
+            f.write("\n")
+    os.replace(tmp, d)
+    return d
+
+
+def read_past_data(data_dir: str) -> Dataset:
+    pairs: List[Tuple[Optional[str], str]] = []
+    for path in ioutils.list_files(data_dir, "*/part-*"):
+        if ".tmp" in os.path.dirname(path):
+            continue
+        with open(path, "r", encoding="utf-8") as f:
+            for line in f:
+                if line.strip():
+                    k, m = json.loads(line)
+                    pairs.append((k, m))
+    return Dataset(pairs)
+
+
+def delete_old_data(directory: str, max_age_hours: int, pattern: re.Pattern = _TS_RE,
+                    now_ms: Optional[int] = None) -> List[str]:
+    """Delete subdirectories whose embedded timestamp is older than ``max_age_hours``."""
+    if max_age_hours < 0:
+        return []
+    now = int(time.time() * 1000) if now_ms is None else now_ms
+    cutoff = now - max_age_hours * 3600 * 1000
+    deleted = []
+    root = ioutils.to_local_path(directory)
+    if not os.path.isdir(root):
+        return deleted
+    for name in os.listdir(root):
+        m = pattern.search(name)
+        if not m:
+            continue
+        if int(m.group(1)) < cutoff:
+            ioutils.delete_recursively(os.path.join(root, name))
+            deleted.append(name)
+    return deleted
+
+
+class BatchLayer(AbstractLayer):
+    layer_name = "BatchLayer"
+    config_group = "batch"
+
+    def __init__(self, config, update: Optional[BatchLayerUpdate] = None):
+        super().__init__(config)
+        self.data_dir = config.get_string("oryx.batch.storage.data-dir")
+        self.model_dir = config.get_string("oryx.batch.storage.model-dir")
+        self.max_data_age_hours = config.get_int("oryx.batch.storage.max-age-data-hours")
+        self.max_model_age_hours = config.get_int("oryx.batch.storage.max-age-model-hours")
+        self.update_class = cfg.get_optional_string(config, "oryx.batch.update-class")
+        self._update = update
+        self._timer: Optional[IntervalTimer] = None
+        self.intervals_run = 0
+
+    def load_update_instance(self) -> BatchLayerUpdate:
+        if self._update is not None:
+            return self._update
+        if not self.update_class:
+            raise ValueError("oryx.batch.update-class is not set")
+        return lang.load_instance_of(self.update_class, None, self.config)
+
+    def start(self) -> "BatchLayer":
+        ioutils.mkdirs(self.data_dir)
+        ioutils.mkdirs(self.model_dir)
+        self._update = self.load_update_instance()
+        self._context = self.layer_context()
+        self.build_input_consumer()
+        self._timer = IntervalTimer(self.generation_interval_sec, self.run_interval,
+                                    "OryxBatchLayer")
+        self._timer.start()
+        lang.close_at_shutdown(self)
+        log.info("Batch layer started (interval %ds)", self.generation_interval_sec)
+        return self
+
+    def run_interval(self, timestamp: Optional[int] = None) -> None:
+        """One generation (also callable directly, e.g. from the CLI or tests)."""
+        if self._input_consumer is None:
+            self._update = self.load_update_instance()
+            self._context = self.layer_context()
+            self.build_input_consumer()
+        ts = int(time.time() * 1000) if timestamp is None else timestamp
+        records = drain(self._input_consumer)
+        if records:
+            log.info("Beginning update at %d with %d new records", ts, len(records))
+            new_data = Dataset(records)
+            past = read_past_data(self.data_dir)
+            producer = None
+            if self.update_topic and self.update_broker:
+                producer = LogTopicProducer(self.update_broker, self.update_topic, self.config,
+                                            async_=False, max_message=self.max_message)
+            try:
+                self._update.run_update(self._context, ts, new_data,
+                                        past if len(past) else None, self.model_dir, producer)
+            finally:
+                if producer is not None:
+                    producer.close()
+            save_interval_data(self.data_dir, ts, records)
+        self.commit_input_offsets()
+        if self.max_data_age_hours >= 0:
+            delete_old_data(self.data_dir, self.max_data_age_hours)
+        if self.max_model_age_hours >= 0:
+            delete_old_data(self.model_dir, self.max_model_age_hours,
+                            pattern=re.compile(r"^(\d+)$"))
+        self.intervals_run += 1
+
+    def await_termination(self, timeout: Optional[float] = None) -> None:
+        t0 = time.time()
+        while self._timer is not None and self._timer.is_alive():
+            if timeout is not None and time.time() - t0 > timeout:
+                return
+            time.sleep(0.5)
+
+    def close(self) -> None:
+        if self._timer is not None:
+            self._timer.stop()
+            self._timer = None
+        self.close_input()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.close()
+        return False

@@ -1,0 +1,162 @@
+"""Shared batch/speed layer plumbing (the reference's ``AbstractSparkLayer``).
+
+``[lambda]/AbstractSparkLayer.java:77-252``: instance id (random when ``oryx.id`` is unset),
+consumer group ``OryxGroup-<Layer>-<id>``, the input-topic consumer that resumes from the
+committed group offsets when an id is configured (missing partitions fall back to the
+latest offset; without an id reading starts at the latest offset -- at-most-once), and the
+generation interval.  Spark Streaming's micro-batch scheduler becomes :class:`IntervalTimer`.
+"""
+
+from __future__ import annotations
+
+import logging
+import threading
+import time
+import uuid
+from dataclasses import dataclass
+from typing import Any, List, Optional, Tuple
+
+from ..api import Dataset
+from ..parallel import dist
+from ..transport import log as tlog
+from ..transport.producer import topic_root
+from ..utils import config as cfg
+from ..utils import lang
+
+__all__ = ["AbstractLayer", "LayerContext", "IntervalTimer", "drain"]
+
+log = logging.getLogger(__name__)
+
+
+@dataclass
+class LayerContext:
+    """What a layer hands to app code (in place of a JavaSparkContext)."""
+
+    config: Any
+    dist: dist.DistContext
+    layer: str = ""
+
+    @property
+    def device(self):
+        return self.dist.device
+
+
+def drain(consumer: tlog.TopicConsumer, max_records: int = 1 << 24,
+          end_offsets: Optional[List[int]] = None) -> List[Tuple[Optional[str], str]]:
+    """Everything currently available (up to the end offsets at call time)."""
+    topic = consumer.topic
+    ends = end_offsets or topic.end_offsets()
+    out: List[Tuple[Optional[str], str]] = []
+    for r in consumer.readers:
+        target = ends[r.partition]
+        while r.position < target and len(out) < max_records:
+            recs = r.poll(min(65536, target - r.position), 50)
+            if not recs:
+                break
+            for off, _, k, v in recs:
+                if off >= target:
+                    r.seek(off)
+                    break
+                out.append((k, v))
+    return out
+
+
+class IntervalTimer:
+    """Calls ``fn(timestamp_ms)`` every ``interval_s`` on a daemon thread until stopped."""
+
+    def __init__(self, interval_s: float, fn, name: str):
+        self.interval_s = float(interval_s)
+        self.fn = fn
+        self.name = name
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self.error: Optional[BaseException] = None
+
+    def start(self) -> None:
+        self._thread = threading.Thread(target=self._run, name=self.name, daemon=True)
+        self._thread.start()
+
+    def _run(self) -> None:
+        next_t = time.time() + self.interval_s
+        while not self._stop.is_set():
+            if self._stop.wait(max(0.0, next_t - time.time())):
+                break
+            ts = int(time.time() * 1000)
+            try:
+                self.fn(ts)
+            except BaseException as e:
+                log.exception("Error in %s interval", self.name)
+                self.error = e
+            next_t += self.interval_s
+            if next_t < time.time():
+                next_t = time.time() + self.interval_s
+
+    def stop(self, timeout: float = 60.0) -> None:
+        self._stop.set()
+        if self._thread is not None and self._thread is not threading.current_thread():
+            self._thread.join(timeout)
+
+    def is_alive(self) -> bool:
+        return self._thread is not None and self._thread.is_alive()
+
+
+class AbstractLayer:
+    layer_name = "Layer"
+    config_group = "batch"
+
+    def __init__(self, config):
+        self.config = config
+        log.info("Configuration:\n%s", cfg.pretty_print(config))
+        oid = cfg.get_optional_string(config, "oryx.id")
+        self.id = oid if oid else self.generate_random_id()
+        self.has_id = oid is not None
+        self.input_topic = config.get_string("oryx.input-topic.message.topic")
+        self.input_broker = config.get_string("oryx.input-topic.broker")
+        self.update_topic = cfg.get_optional_string(config, "oryx.update-topic.message.topic")
+        self.update_broker = cfg.get_optional_string(config, "oryx.update-topic.broker")
+        self.max_message = config.get_int("oryx.update-topic.message.max-size")
+        self.input_partitions = config.get_int("oryx.input-topic.partitions")
+        self.generation_interval_sec = config.get_int(
+            "oryx.%s.streaming.generation-interval-sec" % self.config_group)
+        if self.generation_interval_sec <= 0:
+            raise ValueError("generation-interval-sec must be > 0")
+        self.group_id = "OryxGroup-%s-%s" % (self.layer_name, self.id)
+        self.input_root = topic_root(self.input_broker, config)
+        self.update_root = topic_root(self.update_broker, config) if self.update_broker else None
+        self._input_consumer: Optional[tlog.TopicConsumer] = None
+        self._input_topic: Optional[tlog.Topic] = None
+
+    @staticmethod
+    def generate_random_id() -> str:
+        return uuid.uuid4().hex[:16]
+
+    def layer_context(self) -> LayerContext:
+        dev = cfg.get_optional_string(self.config, "oryx.gpu.device") or "auto"
+        return LayerContext(self.config, dist.init_from_env(device=dev), self.layer_name)
+
+    def build_input_consumer(self) -> tlog.TopicConsumer:
+        tlog.maybe_create_topic(self.input_root, self.input_topic, self.input_partitions)
+        topic = tlog.Topic(self.input_root, self.input_topic)
+        self._input_topic = topic
+        start = "latest"
+        if self.has_id:
+            offsets = tlog.get_offsets(self.input_root, self.input_topic, self.group_id,
+                                       topic.partitions)
+            latest = topic.end_offsets()
+            start = {p: offsets.get(p, latest[p]) for p in range(topic.partitions)}
+            log.info("Resuming %s from offsets %s", self.group_id, start)
+        self._input_consumer = tlog.TopicConsumer(topic, start=start, group=self.group_id)
+        return self._input_consumer
+
+    def commit_input_offsets(self) -> None:
+        """``UpdateOffsetsFn``: persist the consumed offsets when the layer has an id."""
+        if self.has_id and self._input_consumer is not None:
+            self._input_consumer.commit()
+
+    def close_input(self) -> None:
+        if self._input_consumer is not None:
+            self._input_consumer.close()
+            self._input_consumer = None
+        if self._input_topic is not None:
+            self._input_topic.close()
+            self._input_topic = None

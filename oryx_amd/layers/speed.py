@@ -1,0 +1,137 @@
+"""The speed layer: incremental model updates within seconds of new input.
+
+Equivalent of ``SpeedLayer`` + ``SpeedLayerUpdate`` (``[lambda]/speed/SpeedLayer.java:94-200``,
+``[lambda]/speed/SpeedLayerUpdate.java:51-64``):
+
+* thread A replays the update topic from the beginning into ``manager.consume`` (so the
+  speed model follows every batch ``MODEL`` and every ``UP``, including its own);
+* every ``generation-interval-sec`` the interval's new input is handed to
+  ``manager.build_updates``; each returned update is published as ``UP`` with an async
+  producer, then input offsets are committed.
+
+GPU managers (ALS/k-means/RDF) run their fold-in on a dedicated HIP stream so the interval's
+device work overlaps the update-consumer thread's host work.
+"""
+
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from typing import Optional
+
+from ..api import Dataset, SpeedModelManager
+from ..serving.layer import UpdateIterator
+from ..transport import log as tlog
+from ..transport.producer import LogTopicProducer
+from ..utils import config as cfg
+from ..utils import lang
+from .common import AbstractLayer, IntervalTimer, drain
+
+__all__ = ["SpeedLayer"]
+
+log = logging.getLogger(__name__)
+
+
+class SpeedLayer(AbstractLayer):
+    layer_name = "SpeedLayer"
+    config_group = "speed"
+
+    def __init__(self, config, manager: Optional[SpeedModelManager] = None):
+        super().__init__(config)
+        self.manager_class = cfg.get_optional_string(config, "oryx.speed.model-manager-class")
+        self._manager = manager
+        self._timer: Optional[IntervalTimer] = None
+        self._consumer_thread: Optional[threading.Thread] = None
+        self._updates: Optional[UpdateIterator] = None
+        self._update_consumer: Optional[tlog.TopicConsumer] = None
+        self._producer: Optional[LogTopicProducer] = None
+        self.intervals_run = 0
+        self.updates_sent = 0
+
+    def load_manager_instance(self) -> SpeedModelManager:
+        if self._manager is not None:
+            return self._manager
+        if not self.manager_class:
+            raise ValueError("oryx.speed.model-manager-class is not set")
+        return lang.load_instance_of(self.manager_class, None, self.config)
+
+    @property
+    def manager(self) -> Optional[SpeedModelManager]:
+        return self._manager
+
+    def start(self, start_timer: bool = True) -> "SpeedLayer":
+        self._manager = self.load_manager_instance()
+        self._context = self.layer_context()
+        tlog.maybe_create_topic(self.update_root, self.update_topic, 1, self.max_message)
+        topic = tlog.Topic(self.update_root, self.update_topic)
+        self._update_consumer = tlog.TopicConsumer(topic, start="earliest")
+        self._updates = UpdateIterator(self._update_consumer)
+
+        def consume():
+            try:
+                self._manager.consume(self._updates, self._context)
+            except Exception:
+                log.exception("Error while consuming updates")
+                self.close()
+
+        self._consumer_thread = threading.Thread(target=consume,
+                                                 name="OryxSpeedLayerUpdateConsumerThread",
+                                                 daemon=True)
+        self._consumer_thread.start()
+        self.build_input_consumer()
+        self._producer = LogTopicProducer(self.update_broker, self.update_topic, self.config,
+                                          async_=True, max_message=self.max_message)
+        if start_timer:
+            self._timer = IntervalTimer(self.generation_interval_sec, self.run_interval,
+                                        "OryxSpeedLayer")
+            self._timer.start()
+        lang.close_at_shutdown(self)
+        return self
+
+    def run_interval(self, timestamp: Optional[int] = None) -> int:
+        records = drain(self._input_consumer)
+        sent = 0
+        if records:
+            updates = self._manager.build_updates(Dataset(records))
+            if updates:
+                self._producer.send_many(("UP", u) for u in updates)
+                sent = len(updates) if hasattr(updates, "__len__") else 0
+            self._producer.flush()
+        self.commit_input_offsets()
+        self.intervals_run += 1
+        self.updates_sent += sent
+        return sent
+
+    def await_termination(self, timeout: Optional[float] = None) -> None:
+        t0 = time.time()
+        while self._timer is not None and self._timer.is_alive():
+            if timeout is not None and time.time() - t0 > timeout:
+                return
+            time.sleep(0.5)
+
+    def close(self) -> None:
+        if self._timer is not None:
+            self._timer.stop()
+            self._timer = None
+        if self._updates is not None:
+            self._updates.close()
+        if self._consumer_thread is not None and \
+                self._consumer_thread is not threading.current_thread():
+            self._consumer_thread.join(timeout=10)
+        if self._update_consumer is not None:
+            self._update_consumer.close()
+            self._update_consumer = None
+        if self._producer is not None:
+            self._producer.close()
+            self._producer = None
+        if self._manager is not None:
+            self._manager.close()
+        self.close_input()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.close()
+        return False

@@ -1,0 +1,240 @@
+"""ALS speed layer: batched GPU fold-in of new interactions into the current factors.
+
+Equivalent of ``ALSSpeedModel`` / ``ALSSpeedModelManager``
+(``[speed-app]/als/ALSSpeedModel.java:35-151``, ``ALSSpeedModelManager.java:65-215``):
+
+* ``consume``: ``MODEL`` creates/keeps a model and prunes to ``XIDs``/``YIDs`` (recent IDs
+  survive); ``UP`` sets X/Y rows (from the batch layer and from this layer's own output);
+* ``build_updates``: nothing until ``fraction_loaded >= oryx.speed.min-model-load-fraction``;
+  then the interval's input is time-ordered and aggregated like the batch layer, the
+  Gramians XᵀX / YᵀY are formed on the device and inverted (RRQR with the reference's
+  singularity check -- a singular Gramian skips the interval), and ALL events are folded in
+  at once: two ``[B,k]x[k,k]`` GEMMs on a dedicated HIP stream instead of B independent
+  k x k solves.  Each event yields ``["X",u,vec,[i]]`` and ``["Y",i,vec,[u]]``.
+"""
+
+from __future__ import annotations
+
+import json
+import logging
+import threading
+from typing import Iterable, Iterator, List, Optional, Set
+
+import numpy as np
+import torch
+
+from ... import ingest
+from ...api import Dataset, KeyMessage, SpeedModel, SpeedModelManager
+from ...ops import als as als_ops
+from ...utils import mathx, pmml as pmmlu, text
+from .batch import aggregate_scores
+from .common import FeatureVectors
+
+__all__ = ["ALSSpeedModel", "ALSSpeedModelManager"]
+
+log = logging.getLogger(__name__)
+
+
+def _default_device():
+    return torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+
+
+class ALSSpeedModel(SpeedModel):
+    def __init__(self, features: int, implicit: bool, device=None):
+        if features <= 0:
+            raise ValueError("features must be > 0")
+        self.device = device or _default_device()
+        self.features = features
+        self.implicit = implicit
+        self.X = FeatureVectors(features, self.device)
+        self.Y = FeatureVectors(features, self.device)
+        self._expected_users: Set[str] = set()
+        self._expected_items: Set[str] = set()
+        self._lock = threading.Lock()
+
+    def get_features(self) -> int:
+        return self.features
+
+    def is_implicit(self) -> bool:
+        return self.implicit
+
+    def get_user_vector(self, user):
+        return self.X.get_vector(user)
+
+    def get_item_vector(self, item):
+        return self.Y.get_vector(item)
+
+    def set_user_vector(self, user, vector) -> None:
+        if len(vector) != self.features:
+            raise ValueError("wrong vector length")
+        self.X.set_vector(user, vector)
+        with self._lock:
+            self._expected_users.discard(user)
+
+    def set_item_vector(self, item, vector) -> None:
+        if len(vector) != self.features:
+            raise ValueError("wrong vector length")
+        self.Y.set_vector(item, vector)
+        with self._lock:
+            self._expected_items.discard(item)
+
+    def retain_recent_and_user_ids(self, users) -> None:
+        self.X.retain_recent_and_ids(users)
+        with self._lock:
+            self._expected_users = set(users)
+            self.X.remove_all_ids_from(self._expected_users)
+
+    def retain_recent_and_item_ids(self, items) -> None:
+        self.Y.retain_recent_and_ids(items)
+        with self._lock:
+            self._expected_items = set(items)
+            self.Y.remove_all_ids_from(self._expected_items)
+
+    def get_xtx_solver(self):
+        return mathx.get_solver(self.X.get_vtv())
+
+    def get_yty_solver(self):
+        return mathx.get_solver(self.Y.get_vtv())
+
+    def get_fraction_loaded(self) -> float:
+        with self._lock:
+            expected = len(self._expected_users) + len(self._expected_items)
+        if expected == 0:
+            return 1.0
+        loaded = float(self.X.size() + self.Y.size())
+        return loaded / (loaded + expected)
+
+    def __repr__(self):
+        return "ALSSpeedModel[features:%d, implicit:%s, X:(%d users), Y:(%d items), " \
+               "fractionLoaded:%s]" % (self.features, self.implicit, self.X.size(),
+                                       self.Y.size(), self.get_fraction_loaded())
+
+
+class ALSSpeedModelManager(SpeedModelManager):
+    def __init__(self, config):
+        self.no_known_items = config.get_bool("oryx.als.no-known-items")
+        self.min_model_load_fraction = config.get_double("oryx.speed.min-model-load-fraction")
+        if not (0.0 <= self.min_model_load_fraction <= 1.0):
+            raise ValueError("bad min-model-load-fraction")
+        self.model: Optional[ALSSpeedModel] = None
+        self._stream = None
+
+    def consume(self, updates: Iterator[KeyMessage], context=None) -> None:
+        countdown = 10000
+        for km in updates:
+            key, message = km.key, km.message
+            if key is None:
+                raise ValueError("Bad message: %r" % (km,))
+            if key == "UP":
+                if self.model is None:
+                    continue
+                update = text.read_json(message)
+                id_ = str(update[1])
+                vec = np.asarray(update[2], dtype=np.float32)
+                if update[0] == "X":
+                    self.model.set_user_vector(id_, vec)
+                elif update[0] == "Y":
+                    self.model.set_item_vector(id_, vec)
+                else:
+                    raise ValueError("Bad message: %r" % (km,))
+                countdown -= 1
+                if countdown <= 0:
+                    log.info("%s", self.model)
+                    countdown = 10000
+            elif key in ("MODEL", "MODEL-REF"):
+                log.info("Loading new model")
+                pmml = pmmlu.read_pmml_from_update_key_message(key, message)
+                features = int(pmml.get_extension_value("features"))
+                implicit = pmml.get_extension_value("implicit").lower() == "true"
+                if self.model is None or features != self.model.get_features():
+                    log.warning("No previous model, or # features has changed; creating new one")
+                    self.model = ALSSpeedModel(features, implicit)
+                xids = set(pmml.get_extension_content("XIDs") or [])
+                yids = set(pmml.get_extension_content("YIDs") or [])
+                self.model.retain_recent_and_user_ids(xids)
+                self.model.retain_recent_and_item_ids(yids)
+                log.info("Model updated: %s", self.model)
+            else:
+                raise ValueError("Bad message: %r" % (km,))
+
+    def _device_stream(self, device):
+        if device.type != "cuda":
+            return None
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=device)
+        return self._stream
+
+    def build_updates(self, new_data: Dataset) -> List[str]:
+        model = self.model
+        if model is None or model.get_fraction_loaded() < self.min_model_load_fraction:
+            return []
+        users, items = ingest.IdDict(), ingest.IdDict()
+        u, i, s, ts = ingest.parse_ratings(new_data.values(), users, items, default_ts=0)
+        u, i, s = aggregate_scores(u, i, s, ts, model.is_implicit())
+        if len(u) == 0:
+            return []
+        try:
+            xtx = model.get_xtx_solver()
+            yty = model.get_yty_solver()
+        except mathx.SingularMatrixSolverException:
+            return []
+        if xtx is None or yty is None:
+            return []
+        uk, ik = users.keys(), items.keys()
+        u_ids = [uk[j] for j in u.tolist()]
+        i_ids = [ik[j] for j in i.tolist()]
+        dev = model.device
+        stream = self._device_stream(dev)
+        ctx = torch.cuda.stream(stream) if stream is not None else _null_ctx()
+        with ctx:
+            xmat, _, _ = model.X.device_view()
+            ymat, _, _ = model.Y.device_view()
+            xrows = np.array([model.X.row_of(a) if model.X.row_of(a) is not None else -1
+                              for a in u_ids], dtype=np.int64)
+            yrows = np.array([model.Y.row_of(b) if model.Y.row_of(b) is not None else -1
+                              for b in i_ids], dtype=np.int64)
+            xr = torch.from_numpy(np.maximum(xrows, 0)).to(dev)
+            yr = torch.from_numpy(np.maximum(yrows, 0)).to(dev)
+            xpres = torch.from_numpy(xrows >= 0).to(dev)
+            ypres = torch.from_numpy(yrows >= 0).to(dev)
+            xu = torch.where(xpres[:, None], xmat[xr] if len(xmat) else
+                             torch.zeros(len(xr), model.features, device=dev),
+                             torch.zeros((), device=dev))
+            yi = torch.where(ypres[:, None], ymat[yr] if len(ymat) else
+                             torch.zeros(len(yr), model.features, device=dev),
+                             torch.zeros((), device=dev))
+            vals = torch.from_numpy(s).to(dev)
+            yinv = torch.from_numpy(yty.inverse()).to(dev)
+            xinv = torch.from_numpy(xtx.inverse()).to(dev)
+            new_x, valid_x = als_ops.fold_in(yinv, vals, xu, xpres, yi, model.is_implicit())
+            new_y, valid_y = als_ops.fold_in(xinv, vals, yi, ypres, xu, model.is_implicit())
+            # Yi absent -> no X update; Xu absent -> no Y update (computeUpdatedXu(null) = null)
+            valid_x = valid_x & ypres
+            valid_y = valid_y & xpres
+            nx, vx = new_x.cpu().numpy(), valid_x.cpu().numpy()
+            ny, vy = new_y.cpu().numpy(), valid_y.cpu().numpy()
+        x_rows = ingest.format_float_rows(nx)
+        y_rows = ingest.format_float_rows(ny)
+        out: List[str] = []
+        for j in range(len(u_ids)):
+            if vx[j]:
+                out.append(self._to_update_json("X", u_ids[j], x_rows[j], i_ids[j]))
+            if vy[j]:
+                out.append(self._to_update_json("Y", i_ids[j], y_rows[j], u_ids[j]))
+        return out
+
+    def _to_update_json(self, matrix: str, id_: str, vec_json: str, other: str) -> str:
+        if self.no_known_items:
+            return '["%s",%s,%s]' % (matrix, json.dumps(id_), vec_json)
+        return '["%s",%s,%s,[%s]]' % (matrix, json.dumps(id_), vec_json, json.dumps(other))
+
+    def close(self) -> None:
+        pass
+
+
+class _null_ctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False

@@ -111,7 +111,7 @@ class ALSTrainer:
         """Random unit-norm Gaussian rows (MLlib's init), or warm-start from given factors."""
         ctx, dev, k, kp = self.ctx, self.device, self.k, self.kp
         gen = torch.Generator(device="cpu")
-        gen.manual_seed(self.seed * 1000003 + ctx.rank)
+        gen.manual_seed((self.seed * 1000003 + ctx.rank) & ((1 << 62) - 1))
         nu, ni = self.u_hi - self.u_lo, self.i_hi - self.i_lo
         self.X = torch.zeros((self.su, kp), dtype=torch.float32, device=dev)
         self.Y = torch.zeros((self.si, kp), dtype=torch.float32, device=dev)

@@ -71,18 +71,16 @@ def _load_runtime():
 
 
 def _register_runtime_extras(lib):
-    # Optional symbols of later runtime modules
-    for name, res, args in [
-        ("oryx_parse_ratings", c_ll, [c_cp, c_ll, c_vp, c_vp, c_vp, c_vp, c_ll, c_i]),
-        ("oryx_dict_new", c_vp, []),
-        ("oryx_dict_free", None, [c_vp]),
-        ("oryx_dict_size", c_ll, [c_vp]),
-        ("oryx_dict_encode", c_ll, [c_vp, c_cp, c_ll, c_i, c_vp]),
-        ("oryx_dict_get", c_ll, [c_vp, c_cp, c_ll]),
-        ("oryx_dict_key", c_ll, [c_vp, c_ll, c_cp, c_ll]),
-    ]:
-        if hasattr(lib, name):
-            _sig(lib, name, res, args)
+    c_dp = ctypes.POINTER(ctypes.c_double)
+    _sig(lib, "oryx_dict_new", c_vp, [])
+    _sig(lib, "oryx_dict_free", None, [c_vp])
+    _sig(lib, "oryx_dict_size", c_ll, [c_vp])
+    _sig(lib, "oryx_dict_encode", c_ll, [c_vp, c_cp, c_ll, c_i, c_vp])
+    _sig(lib, "oryx_dict_get", c_ll, [c_vp, c_cp, c_ll])
+    _sig(lib, "oryx_dict_key", c_ll, [c_vp, c_ll, c_vp, c_ll])
+    _sig(lib, "oryx_parse_ratings", c_ll, [c_cp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                           c_ll, c_ll, c_i])
+    _sig(lib, "oryx_format_float_rows", c_ll, [c_vp, c_ll, c_i, c_ll, c_vp, c_ll, c_vp])
 
 
 def _runtime_sources():

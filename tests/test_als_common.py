@@ -1,0 +1,137 @@
+"""ALSUtilsTest / FeatureVectorsTest / ALSUpdateTest / speed fold-in ports."""
+
+import math
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from oryx_amd.models.als import common
+from oryx_amd.models.als.batch import aggregate_scores, decay_rating, known_items
+from oryx_amd.models.als.common import FeatureVectors, compute_target_qui, compute_updated_xu
+from oryx_amd.ops import als as als_ops
+from oryx_amd.utils import mathx
+
+
+def test_implicit_qui():
+    for v, c in ((0.0, 1.0), (0.0, 0.0), (0.0, -1.0), (0.5, 1.0), (-0.5, 0.0)):
+        assert math.isnan(compute_target_qui(True, v, c))
+    assert compute_target_qui(True, 1.0, 0.5) == 0.75
+    assert compute_target_qui(True, -1.0, 0.5) == 0.25
+    for d in (-1.0, 0.0, 0.5, 1.0, 2.0):
+        assert compute_target_qui(False, d, 0.0) == d
+
+
+def _solver():
+    rows = [[1.0, 2.0], [3.0, 0.0], [0.0, 1.0]]
+    return mathx.get_solver(mathx.transpose_times_self(rows))
+
+
+def test_compute_updated_xu():
+    s = _solver()
+    assert compute_updated_xu(s, 1.0, None, None, True) is None
+    np.testing.assert_allclose(compute_updated_xu(s, 1.0, None, np.array([2.0, 1.0]), True),
+                               [0.13043478, 0.097826086], rtol=1e-6)
+    np.testing.assert_allclose(compute_updated_xu(s, 0.5, None, np.array([2.0, 1.0]), True),
+                               [0.11594203, 0.08695652], rtol=1e-6)
+    np.testing.assert_allclose(compute_updated_xu(s, 1.0, np.array([0.1, 0.1]),
+                                                  np.array([2.0, 1.0]), True),
+                               [0.16086957, 0.14565217], rtol=1e-6)
+
+
+def test_batched_fold_in_matches_scalar():
+    s = _solver()
+    inv = torch.from_numpy(s.inverse())
+    xu = torch.tensor([[0.0, 0.0], [0.0, 0.0], [0.1, 0.1], [0.5, 0.9]])
+    pres = torch.tensor([False, False, True, True])
+    yi = torch.tensor([[2.0, 1.0], [2.0, 1.0], [2.0, 1.0], [1.0, 1.0]])
+    vals = torch.tensor([1.0, 0.5, 1.0, 1.0])
+    new, valid = als_ops.fold_in(inv, vals, xu, pres, yi, True)
+    for j in range(4):
+        ref = compute_updated_xu(s, float(vals[j]), xu[j].numpy() if pres[j] else None,
+                                 yi[j].numpy(), True)
+        if ref is None:
+            assert not valid[j]
+        else:
+            assert valid[j]
+            np.testing.assert_allclose(new[j].numpy(), ref, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("device", ["cpu"])
+def test_feature_vectors(device):
+    fv = FeatureVectors(1, torch.device(device))
+    assert fv.size() == 0
+    fv.set_vector("foo", [1.0])
+    assert fv.size() == 1 and fv.get_vector("foo").tolist() == [1.0]
+    fv.remove_vector("foo")
+    assert fv.size() == 0 and fv.get_vector("foo") is None
+    fv3 = FeatureVectors(3, torch.device(device))
+    fv3.set_vector("foo", [1.0, 2.0, 4.0])
+    fv3.set_vector("bar", [1.5, -1.0, 0.0])
+    np.testing.assert_allclose(fv3.get_vtv(), [[3.25, 0.5, 4.0], [0.5, 5.0, 8.0],
+                                               [4.0, 8.0, 16.0]])
+    out = []
+    fv3.for_each(lambda i, v: out.append("%s%s" % (i, v[0])))
+    assert sorted(out) == ["bar1.5", "foo1.0"]
+    fv = FeatureVectors(1)
+    fv.set_vector("foo", [1.0])
+    fv.retain_recent_and_ids({"foo"})
+    assert fv.size() == 1
+    fv.retain_recent_and_ids({"bar"})
+    assert fv.size() == 0
+    fv.set_vector("foo", [1.0])
+    ids = set()
+    fv.add_all_ids_to(ids)
+    assert ids == {"foo"}
+    fv.remove_all_ids_from(ids)
+    assert not ids
+    rec = set()
+    fv.add_all_recent_to(rec)
+    assert rec == {"foo"}
+    fv.retain_recent_and_ids({"foo"})
+    rec.clear()
+    fv.add_all_recent_to(rec)
+    assert not rec
+
+
+def test_feature_vectors_concurrent_and_device_mirror():
+    fv = FeatureVectors(2, torch.device("cpu"))
+    counter = iter(range(10 ** 9))
+    lock = threading.Lock()
+
+    def work():
+        for _ in range(2000):
+            with lock:
+                c = next(counter)
+            fv.set_vector(str(c), [float(c), 1.0])
+
+    ts = [threading.Thread(target=work) for _ in range(8)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert fv.size() == 16000
+    mat, valid, norms = fv.device_view()
+    assert int(valid.sum()) == 16000
+    fv.remove_vector("5")
+    mat, valid, _ = fv.device_view()
+    assert int(valid.sum()) == 15999
+    assert mat.sum(0)[1].item() == 15999.0
+
+
+def test_decay():
+    assert decay_rating(2.0, 1000, 1000, 0.5) == 2.0
+    assert abs(decay_rating(2.0, 0, 86400000, 0.5) - 1.0) < 1e-12
+    assert abs(decay_rating(2.0, 0, 2 * 86400000, 0.5) - 0.5) < 1e-12
+
+
+def test_aggregate_and_known_items():
+    u = np.array([0, 0, 0, 1, 1, 2, 2])
+    i = np.array([0, 0, 0, 1, 1, 2, 2])
+    s = np.array([1, 2, np.nan, 3, 4, np.nan, 5.0])
+    ts = np.array([1, 2, 3, 1, 2, 1, 2])
+    uu, ii, ss = aggregate_scores(u, i, s, ts, True)
+    assert uu.tolist() == [1, 2] and ss.tolist() == [7.0, 5.0]
+    uu, ii, ss = aggregate_scores(u, i, s, ts, False)
+    assert ss.tolist() == [4.0, 5.0]
+    k = known_items(["a,x,1,1", "a,y,1,2", "a,x,,3", "b,z,1,4", "c,w,1,5", "c,w,,6"])
+    assert k == {"a": {"y"}, "b": {"z"}, "c": set()}

@@ -1,0 +1,171 @@
+"""End-to-end lambda loop on CPU: input log -> batch layer (ALSUpdate) -> update log ->
+speed layer fold-in and serving layer over real HTTP (ALSUpdateIT / ALSSpeedIT /
+ALSServingModelManagerIT equivalents)."""
+
+import json
+import os
+import time
+import urllib.request
+
+import numpy as np
+import pytest
+
+from oryx_amd.layers.batch import BatchLayer, delete_old_data, read_past_data
+from oryx_amd.layers.speed import SpeedLayer
+from oryx_amd.serving.layer import ServingLayer
+from oryx_amd.transport import log as tlog
+from oryx_amd.transport.producer import LogTopicProducer
+from oryx_amd.utils import config as cfg
+from oryx_amd.utils import ioutils, pmml as pmmlu
+
+
+def _config(tmp_path, **extra):
+    overlay = {
+        "oryx.id": '"test"',
+        "oryx.transport.log-dir": '"%s"' % (tmp_path / "log"),
+        "oryx.batch.storage.data-dir": '"file:%s/"' % (tmp_path / "data"),
+        "oryx.batch.storage.model-dir": '"file:%s/"' % (tmp_path / "model"),
+        "oryx.batch.update-class": "com.cloudera.oryx.app.batch.mllib.als.ALSUpdate",
+        "oryx.speed.model-manager-class": "com.cloudera.oryx.app.speed.als.ALSSpeedModelManager",
+        "oryx.serving.model-manager-class":
+            "com.cloudera.oryx.app.serving.als.model.ALSServingModelManager",
+        "oryx.serving.application-resources":
+            '"com.cloudera.oryx.app.serving,com.cloudera.oryx.app.serving.als"',
+        "oryx.serving.api.port": 0,
+        "oryx.als.hyperparams.features": 4,
+        "oryx.als.iterations": 4,
+        "oryx.ml.eval.test-fraction": 0.2,
+        "oryx.gpu.device": '"cpu"',
+    }
+    overlay.update(extra)
+    return cfg.overlay_on(overlay, cfg.get_default())
+
+
+def _random_input(n_users=40, n_items=30, n=800, seed=0):
+    g = np.random.default_rng(seed)
+    lines = []
+    t0 = 1_600_000_000_000
+    for j in range(n):
+        u, i = int(g.integers(n_users)), int(g.integers(n_items))
+        lines.append("U%d,I%d,%d,%d" % (u, i, int(g.integers(1, 5)), t0 + j * 1000))
+    return lines
+
+
+def _read_updates(root, topic="OryxUpdate"):
+    t = tlog.Topic(root, topic)
+    c = tlog.TopicConsumer(t, start="earliest")
+    out = []
+    while True:
+        recs = c.poll(100000, 50)
+        if not recs:
+            break
+        out.extend((k, v) for _, _, _, k, v in recs)
+    c.close()
+    t.close()
+    return out
+
+
+def test_batch_layer_als_end_to_end(tmp_path):
+    config = _config(tmp_path)
+    root = str(tmp_path / "log")
+    tlog.maybe_create_topic(root, "OryxInput", 4)
+    tlog.maybe_create_topic(root, "OryxUpdate", 1)
+    batch = BatchLayer(config)
+    batch.run_interval()        # positions consumer at the (empty) end; nothing to do
+    prod = LogTopicProducer("localhost:9092", "OryxInput", config, async_=False)
+    lines = _random_input()
+    for j, line in enumerate(lines):
+        prod.send(str(j), line)
+    batch.run_interval()
+    updates = _read_updates(root)
+    assert updates[0][0] == "MODEL"
+    pmml = pmmlu.from_string(updates[0][1])
+    names = [e.get("name") for e in pmml.extensions()]
+    assert names == ["X", "Y", "features", "lambda", "implicit", "alpha", "XIDs", "YIDs"]
+    xids = set(pmml.get_extension_content("XIDs"))
+    yids = set(pmml.get_extension_content("YIDs"))
+    ups = [json.loads(m) for k, m in updates[1:] if k == "UP"]
+    assert {u[1] for u in ups if u[0] == "Y"} == yids
+    assert {u[1] for u in ups if u[0] == "X"} == xids
+    # Y rows are published before X rows
+    first_x = min(n for n, u in enumerate(ups) if u[0] == "X")
+    assert all(u[0] == "Y" for u in ups[:first_x])
+    for u in ups:
+        assert len(u[2]) == 4
+        if u[0] == "X":
+            assert isinstance(u[3], list)
+    # data persisted, offsets committed
+    past = read_past_data(config.get_string("oryx.batch.storage.data-dir"))
+    assert len(past) == len(lines)
+    off = tlog.get_offsets(root, "OryxInput", "OryxGroup-BatchLayer-test", 4)
+    assert sum(off.values()) == len(lines)
+    # model dir: one generation with model.pmml + X/ Y/
+    model_dir = ioutils.to_local_path(config.get_string("oryx.batch.storage.model-dir"))
+    gens = [d for d in os.listdir(model_dir) if d.isdigit()]
+    assert len(gens) == 1
+    assert os.path.exists(os.path.join(model_dir, gens[0], "model.pmml"))
+    assert os.path.exists(os.path.join(model_dir, gens[0], "X", "part-00000.gz"))
+    # second generation: IDs are a superset of the previous generation's
+    for j, line in enumerate(_random_input(seed=1, n=200)):
+        prod.send(str(j), line)
+    batch.run_interval()
+    updates2 = _read_updates(root)
+    models = [m for k, m in updates2 if k == "MODEL"]
+    assert len(models) == 2
+    assert set(pmmlu.from_string(models[1]).get_extension_content("XIDs")) >= xids
+    batch.close()
+
+    # ---- serving layer over HTTP replays the update topic
+    serving = ServingLayer(config, host="127.0.0.1").start()
+    try:
+        port = serving.actual_port
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            try:
+                with urllib.request.urlopen("http://127.0.0.1:%d/ready" % port) as r:
+                    if r.status == 200:
+                        break
+            except Exception:
+                time.sleep(0.2)
+        uid = sorted(xids)[0]
+        req = urllib.request.Request("http://127.0.0.1:%d/recommend/%s?howMany=3" % (port, uid),
+                                     headers={"Accept": "application/json"})
+        with urllib.request.urlopen(req) as r:
+            recs = json.loads(r.read())
+        assert 1 <= len(recs) <= 3 and all("id" in x and "value" in x for x in recs)
+        req = urllib.request.Request("http://127.0.0.1:%d/ingest" % port, data=b"U1,I2,3\n",
+                                     method="POST", headers={"Content-Type": "text/plain"})
+        with urllib.request.urlopen(req) as r:
+            assert r.status == 204
+        with urllib.request.urlopen("http://127.0.0.1:%d/metrics" % port) as r:
+            assert b"oryx_http_requests_total" in r.read()
+    finally:
+        serving.close()
+
+    # ---- speed layer folds in new input
+    speed = SpeedLayer(config).start(start_timer=False)
+    try:
+        deadline = time.time() + 30
+        while time.time() < deadline and (speed.manager.model is None or
+                                          speed.manager.model.get_fraction_loaded() < 1.0):
+            time.sleep(0.1)
+        assert speed.manager.model is not None
+        known_u = sorted(xids)[0]
+        known_i = sorted(yids)[0]
+        prod.send("x", "%s,%s,2,%d" % (known_u, known_i, int(time.time() * 1000)))
+        prod.send("y", "newuser,%s,1,%d" % (known_i, int(time.time() * 1000)))
+        n = speed.run_interval()
+        assert n >= 2
+    finally:
+        speed.close()
+        prod.close()
+
+
+def test_delete_old_data(tmp_path):
+    d = tmp_path / "data"
+    now = int(time.time() * 1000)
+    for ts in (now - 10 * 3600 * 1000, now - 3600 * 1000, now):
+        (d / ("oryx-%d.data" % ts)).mkdir(parents=True)
+    deleted = delete_old_data(str(d), 5)
+    assert len(deleted) == 1
+    assert len(os.listdir(d)) == 2
