@@ -182,8 +182,10 @@ class ALSUpdate(MLUpdate):
         trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx,
                              seed=rng.next_seed())
         t0 = time.perf_counter()
-        trainer.prepare(torch.from_numpy(remap_u[u]), torch.from_numpy(remap_i[i]),
-                        torch.from_numpy(s.astype(np.float32)), len(used_u), len(used_i))
+        # every rank holds the same aggregated triples; each contributes a disjoint slice
+        part = slice(ctx.rank, None, ctx.world_size)
+        trainer.prepare(torch.from_numpy(remap_u[u][part]), torch.from_numpy(remap_i[i][part]),
+                        torch.from_numpy(s[part].astype(np.float32)), len(used_u), len(used_i))
         f = trainer.train(self.iterations)
         X = f.X.cpu().numpy()
         Y = f.Y.cpu().numpy()

@@ -1,0 +1,99 @@
+"""k-means speed layer: assign new points, running-mean update of the touched clusters.
+
+Equivalent of ``KMeansSpeedModel`` / ``KMeansSpeedModelManager``
+(``[speed-app]/kmeans/KMeansSpeedModel.java:31-63``,
+``[speed-app]/kmeans/KMeansSpeedModelManager.java:58-125``):
+
+* ``consume``: ``MODEL``/``MODEL-REF`` -> validate against the schema and load the clusters;
+  ``UP`` is ignored (the layer hears its own updates);
+* ``build_updates``: the interval's points are assigned in one batched device pass, the
+  per-cluster (sum, count) reduced with ``index_add``, and each touched cluster is updated with
+  ``ClusterInfo.update(mean, count)``; output ``[clusterID,[center...],count]`` per cluster, in
+  ascending cluster position.
+"""
+
+from __future__ import annotations
+
+import logging
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ...api import Dataset, SpeedModel, SpeedModelManager
+from ...utils import pmml as pmmlu, text
+from ..schema import InputSchema
+from .common import ClusterSet, parse_feature_matrix, read_clusters, validate_pmml_vs_schema
+
+__all__ = ["KMeansSpeedModel", "KMeansSpeedModelManager"]
+
+log = logging.getLogger(__name__)
+
+
+def _default_device():
+    return torch.device("cuda") if torch.cuda.is_available() else None
+
+
+class KMeansSpeedModel(SpeedModel):
+    def __init__(self, clusters, device=None):
+        self.clusters = ClusterSet(clusters, device if device is not None else _default_device())
+
+    def get_cluster(self, index: int):
+        return self.clusters.get(index)
+
+    def set_cluster(self, index: int, info) -> None:
+        self.clusters.set(index, info)
+
+    def closest_cluster(self, vector):
+        return self.clusters.nearest(vector)[0]
+
+    def get_fraction_loaded(self) -> float:
+        return 1.0
+
+    def __repr__(self):
+        return "KMeansSpeedModel[numClusters=%d]" % len(self.clusters)
+
+
+class KMeansSpeedModelManager(SpeedModelManager):
+    def __init__(self, config):
+        self.input_schema = InputSchema(config)
+        self.model: Optional[KMeansSpeedModel] = None
+
+    def consume(self, updates, context=None) -> None:
+        for km in updates:
+            key, message = km.key, km.message
+            if key is None:
+                raise ValueError("Bad message: %r" % (km,))
+            if key == "UP":
+                continue
+            if key in ("MODEL", "MODEL-REF"):
+                log.info("Loading new model")
+                pmml = pmmlu.read_pmml_from_update_key_message(key, message)
+                validate_pmml_vs_schema(pmml, self.input_schema)
+                self.model = KMeansSpeedModel(read_clusters(pmml))
+                log.info("New model loaded: %s", self.model)
+            else:
+                raise ValueError("Bad message: %r" % (km,))
+
+    def build_updates(self, new_data: Dataset) -> List[str]:
+        model = self.model
+        if model is None:
+            return []
+        x = parse_feature_matrix(new_data.values(), self.input_schema)
+        if len(x) == 0:
+            return []
+        idx, _ = model.clusters.nearest_batch(x)
+        k = len(model.clusters)
+        sums = np.zeros((k, x.shape[1]), dtype=np.float64)
+        np.add.at(sums, idx, x)
+        counts = np.bincount(idx, minlength=k)
+        out = []
+        for pos in np.nonzero(counts)[0].tolist():
+            info = model.get_cluster(pos)
+            info.update(sums[pos] / counts[pos], int(counts[pos]))
+            model.set_cluster(pos, info)
+            out.append(text.join_json([info.id, [float(v) for v in info.center], info.count]))
+        return out
+
+    def close(self) -> None:
+        pass

@@ -110,9 +110,9 @@ def _load_kernels():
     for name, res, args in [
         ("oryx_topk_scores", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_i, c_vp, c_vp,
                                    c_vp, c_vp]),
-        ("oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp]),
+        ("oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp, c_vp]),
         ("oryx_kmeans_accumulate", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
-                                         c_vp, c_vp]),
+                                         c_vp]),
         ("oryx_rdf_histogram", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i, c_i,
                                      c_i, c_vp, c_vp]),
         ("oryx_tree_traverse", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_i,

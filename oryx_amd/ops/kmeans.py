@@ -1,0 +1,295 @@
+"""k-means device ops: nearest-center assignment, centroid accumulation, k-means|| + Lloyd.
+
+Replaces Spark MLlib ``KMeans.train`` (invoked at ``[mllib]/kmeans/KMeansUpdate.java:116-117``;
+SURVEY.md K8/K9/K11, C10/C11).  On a GPU the assignment is the fused HIP kernel
+``oryx_kmeans_assign`` (bf16 MFMA distance GEMM + argmin, ``csrc/kernels/kmeans.hip``) and the
+centroid sums use ``oryx_kmeans_accumulate`` (row-coalesced fp32 atomics); across ranks the
+K x d sums and K counts are all-reduced (one RCCL call per Lloyd iteration).  On CPU an exact
+fp32 PyTorch path runs the same algorithm.
+
+Algorithm (MLlib semantics): k-means|| initialisation (``initializationSteps`` rounds of
+oversampling proportional to D^2 with ``l = 2k``, candidates weighted by assignment counts,
+then weighted k-means++ on the candidates), or "random" (k distinct random points); Lloyd
+iterations until every center moves less than ``epsilon`` or ``max_iterations``; empty
+clusters keep their previous center; best of ``runs`` by cost.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from .. import native
+from ..parallel import dist
+
+__all__ = ["assign", "accumulate", "kmeans_train", "KMeansResult", "pairwise_distances"]
+
+_CHUNK = 1 << 20
+
+
+def _pad_to(n: int, m: int) -> int:
+    return ((n + m - 1) // m) * m
+
+
+class DeviceCenters:
+    """Centers prepared for the assignment kernel (bf16, padded, norms with +inf padding)."""
+
+    def __init__(self, centers: torch.Tensor):
+        self.k, self.d = centers.shape
+        dev = centers.device
+        self.d_pad = _pad_to(max(self.d, 32), 32)
+        self.k_pad = _pad_to(max(self.k, 64), 64)
+        cb = torch.zeros((self.k_pad, self.d_pad), dtype=torch.bfloat16, device=dev)
+        cb[:self.k, :self.d] = centers
+        self.cb = cb
+        cn = torch.full((self.k_pad,), float("inf"), dtype=torch.float32, device=dev)
+        cn[:self.k] = cb[:self.k].float().pow(2).sum(1)
+        self.cnorm = cn
+
+
+def _kernel_ok(x: torch.Tensor) -> bool:
+    return x.device.type == "cuda" and _pad_to(max(x.shape[1], 32), 32) <= 512
+
+
+def assign(x: torch.Tensor, centers: torch.Tensor, exact: bool = False
+           ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(index int64 [n], squared distance fp32 [n]) of the nearest center for each row.
+
+    GPU + not ``exact``: bf16 MFMA kernel.  Otherwise fp32 chunked matmul + argmin.
+    """
+    n = x.shape[0]
+    if n == 0:
+        return (torch.zeros(0, dtype=torch.int64, device=x.device),
+                torch.zeros(0, dtype=torch.float32, device=x.device))
+    if _kernel_ok(x) and not exact:
+        lib = native.require_kernels()
+        dc = DeviceCenters(centers.float())
+        out_a = torch.empty(n, dtype=torch.int32, device=x.device)
+        out_d = torch.empty(n, dtype=torch.float32, device=x.device)
+        for lo in range(0, n, _CHUNK * 16):
+            hi = min(n, lo + _CHUNK * 16)
+            xb = torch.zeros((hi - lo, dc.d_pad), dtype=torch.bfloat16, device=x.device)
+            xb[:, :dc.d] = x[lo:hi]
+            xn = xb.float().pow(2).sum(1)
+            rc = lib.oryx_kmeans_assign(xb.data_ptr(), xn.data_ptr(), dc.cb.data_ptr(), hi - lo,
+                                        dc.d_pad, dc.k_pad, dc.cnorm.data_ptr(),
+                                        out_a[lo:hi].data_ptr(), out_d[lo:hi].data_ptr(),
+                                        native.stream_ptr(x.device))
+            native.check(rc, "oryx_kmeans_assign")
+        return out_a.to(torch.int64), out_d
+    c = centers.to(x.device, torch.float32)
+    cn = c.pow(2).sum(1)
+    idx = torch.empty(n, dtype=torch.int64, device=x.device)
+    dd = torch.empty(n, dtype=torch.float32, device=x.device)
+    for lo in range(0, n, _CHUNK):
+        hi = min(n, lo + _CHUNK)
+        xc = x[lo:hi].to(torch.float32)
+        d2 = (xc.pow(2).sum(1, keepdim=True) + cn[None, :] - 2.0 * xc.matmul(c.t())).clamp_min_(0)
+        v, i = d2.min(1)
+        idx[lo:hi] = i
+        dd[lo:hi] = v
+    return idx, dd
+
+
+def accumulate(x: torch.Tensor, idx: torch.Tensor, k: int,
+               mind: Optional[torch.Tensor] = None):
+    """(sums fp32 [k, d], counts int64 [k], dist stats fp64 [k, 2] = (sum d, sum d^2) or None)."""
+    n, d = x.shape
+    dev = x.device
+    sums = torch.zeros((k, d), dtype=torch.float32, device=dev)
+    stats = torch.zeros((k, 2), dtype=torch.float64, device=dev) if mind is not None else None
+    if dev.type == "cuda" and native.kernels_available():
+        lib = native.kernels()
+        counts = torch.zeros(k, dtype=torch.int64, device=dev)
+        xf = x.to(torch.float32).contiguous()
+        ia = idx.to(torch.int32).contiguous()
+        md = mind.to(torch.float32).contiguous() if mind is not None else None
+        rc = lib.oryx_kmeans_accumulate(xf.data_ptr(), ia.data_ptr(),
+                                        md.data_ptr() if md is not None else None, n, d, d,
+                                        sums.data_ptr(), counts.data_ptr(),
+                                        stats.data_ptr() if stats is not None else None,
+                                        native.stream_ptr(dev))
+        native.check(rc, "oryx_kmeans_accumulate")
+        return sums, counts, stats
+    sums.index_add_(0, idx, x.to(torch.float32))
+    counts = torch.bincount(idx, minlength=k).to(torch.int64)
+    if stats is not None:
+        dd = mind.double().clamp_min(0).sqrt()
+        stats[:, 0].index_add_(0, idx, dd)
+        stats[:, 1].index_add_(0, idx, dd * dd)
+    return sums, counts, stats
+
+
+def pairwise_distances(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Euclidean distances [len(a), len(b)] in float64 (evaluation metrics)."""
+    a = a.double()
+    b = b.double()
+    d2 = a.pow(2).sum(1, keepdim=True) + b.pow(2).sum(1)[None] - 2.0 * a.matmul(b.t())
+    return d2.clamp_min_(0).sqrt_()
+
+
+@dataclass
+class KMeansResult:
+    centers: torch.Tensor   # fp32 [k, d]
+    counts: torch.Tensor    # int64 [k]
+    cost: float
+    iterations: int
+
+
+def _global_count(n: int, ctx) -> int:
+    if not ctx.is_distributed:
+        return n
+    t = torch.tensor([float(n)], dtype=torch.float64, device=ctx.device)
+    dist.all_reduce_sum(t, ctx)
+    return int(t.item())
+
+
+def _gather_rows(rows: torch.Tensor, ctx) -> torch.Tensor:
+    """All ranks' variable-size row sets concatenated (small candidate sets)."""
+    if not ctx.is_distributed:
+        return rows
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
+    sizes = [torch.zeros_like(n) for _ in range(ctx.world_size)]
+    torch.distributed.all_gather(sizes, n)
+    mx = int(max(int(s) for s in sizes))
+    pad = torch.zeros((mx,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=rows.device)
+    pad[:rows.shape[0]] = rows
+    parts = [torch.zeros_like(pad) for _ in range(ctx.world_size)]
+    torch.distributed.all_gather(parts, pad)
+    return torch.cat([p[:int(s)] for p, s in zip(parts, sizes)])
+
+
+def _kmeanspp_weighted(cands: torch.Tensor, weights: torch.Tensor, k: int,
+                       gen: torch.Generator) -> torch.Tensor:
+    """Weighted k-means++ on a (small) candidate set, on the host in float64."""
+    c = cands.double().cpu()
+    w = weights.double().cpu()
+    n = c.shape[0]
+    if n <= k:
+        return c.float()
+    first = int(torch.multinomial(w / w.sum(), 1, generator=gen))
+    chosen = [first]
+    d2 = ((c - c[first]) ** 2).sum(1)
+    for _ in range(1, k):
+        p = w * d2
+        s = float(p.sum())
+        if s <= 0:
+            nxt = int(torch.randint(0, n, (1,), generator=gen))
+        else:
+            nxt = int(torch.multinomial(p / s, 1, generator=gen))
+        chosen.append(nxt)
+        d2 = torch.minimum(d2, ((c - c[nxt]) ** 2).sum(1))
+    return c[chosen].float()
+
+
+def _init_random(x, k, gen, ctx):
+    n = x.shape[0]
+    m = min(n, k)
+    idx = torch.randperm(n, generator=gen)[:m].to(x.device)
+    cands = _gather_rows(x[idx].float(), ctx)
+    perm = torch.randperm(cands.shape[0], generator=gen)[:k]
+    c = cands[perm.to(cands.device)]
+    if ctx.is_distributed:
+        torch.distributed.broadcast(c, src=0)
+    return c
+
+
+def _init_parallel(x, k, gen, ctx, steps: int = 5):
+    """k-means|| (Bahmani et al.), as MLlib's ``K_MEANS_PARALLEL``."""
+    n = x.shape[0]
+    dev = x.device
+    # first center: a uniformly random point (rank 0's choice broadcast)
+    i0 = int(torch.randint(0, max(1, n), (1,), generator=gen))
+    c0 = x[i0:i0 + 1].float() if n else torch.zeros((1, x.shape[1]), device=dev)
+    if ctx.is_distributed:
+        torch.distributed.broadcast(c0, src=0)
+    centers = c0
+    _, d2 = assign(x, centers, exact=True)
+    l = 2.0 * k
+    for _ in range(steps):
+        phi = d2.double().sum()
+        if ctx.is_distributed:
+            dist.all_reduce_sum(phi, ctx)
+        if float(phi) <= 0:
+            break
+        p = (l * d2.double() / phi).clamp_max(1.0)
+        r = torch.rand(n, generator=gen, dtype=torch.float64).to(dev)
+        picked = x[(r < p)].float()
+        new = _gather_rows(picked, ctx)
+        if new.shape[0] == 0:
+            continue
+        centers = torch.cat([centers, new])
+        _, dn = assign(x, new, exact=True)
+        d2 = torch.minimum(d2, dn)
+    idx, _ = assign(x, centers, exact=True)
+    w = torch.bincount(idx, minlength=centers.shape[0]).double()
+    if ctx.is_distributed:
+        dist.all_reduce_sum(w, ctx)
+    chosen = _kmeanspp_weighted(centers, w, k, gen).to(dev)
+    if ctx.is_distributed:
+        torch.distributed.broadcast(chosen, src=0)
+    return chosen
+
+
+def _farthest_points(x: torch.Tensor, d2: torch.Tensor, m: int, ctx) -> torch.Tensor:
+    """The ``m`` points (over all ranks) with the largest distance to their center."""
+    t = min(m, x.shape[0])
+    v, i = torch.topk(d2, t) if t else (d2[:0], d2[:0].long())
+    cand = torch.cat([v[:, None].float(), x[i].float()], 1)
+    cand = _gather_rows(cand, ctx)
+    if cand.shape[0] == 0:
+        return cand[:, 1:]
+    order = torch.argsort(cand[:, 0], descending=True, stable=True)[:m]
+    return cand[order, 1:]
+
+
+def kmeans_train(x: torch.Tensor, k: int, max_iterations: int, runs: int = 1,
+                 init: str = "k-means||", seed: int = 0, epsilon: float = 1e-4,
+                 ctx: Optional[dist.DistContext] = None) -> KMeansResult:
+    """Train k-means on this rank's rows ``x`` (the union over ranks is the data)."""
+    ctx = ctx or dist.DistContext(device=x.device)
+    best: Optional[KMeansResult] = None
+    for run in range(max(1, runs)):
+        gen = torch.Generator()
+        gen.manual_seed((seed * 7919 + run * 104729 + ctx.rank) & ((1 << 62) - 1))
+        if init in ("random",):
+            centers = _init_random(x, k, gen, ctx)
+        else:
+            centers = _init_parallel(x, k, gen, ctx)
+        kk = centers.shape[0]
+        it = 0
+        for it in range(1, max_iterations + 1):
+            idx, d2 = assign(x, centers)
+            sums, counts, _ = accumulate(x, idx, kk)
+            if ctx.is_distributed:
+                dist.all_reduce_sum(sums, ctx)
+                dist.all_reduce_sum(counts, ctx)
+            nonempty = counts > 0
+            new = centers.clone()
+            new[nonempty] = sums[nonempty] / counts[nonempty, None].float()
+            n_empty = int((~nonempty).sum())
+            if n_empty:
+                # re-seed empty clusters at the points farthest from their centers
+                far = _farthest_points(x, d2, n_empty, ctx)
+                if far.shape[0] == n_empty:
+                    new[~nonempty] = far
+                    moved = float("inf")
+            if not n_empty or far.shape[0] != n_empty:
+                moved = (new - centers).pow(2).sum(1).max().item() if kk else 0.0
+            centers = new
+            if moved <= epsilon * epsilon:
+                break
+        idx, d2 = assign(x, centers, exact=True)
+        cost = d2.double().sum()
+        counts = torch.bincount(idx, minlength=kk).to(torch.int64)
+        if ctx.is_distributed:
+            dist.all_reduce_sum(cost, ctx)
+            dist.all_reduce_sum(counts, ctx)
+        res = KMeansResult(centers, counts, float(cost), it)
+        if best is None or res.cost < best.cost:
+            best = res
+    return best

@@ -219,9 +219,17 @@ def route(method: str, template: str, produces=DEFAULT_PRODUCES, consumes=None):
 def collect_routes(module_names: Iterable[str]) -> List[Route]:
     import importlib
     routes: List[Route] = []
-    for name in module_names:
+    seen = set()
+    pending = list(module_names)
+    while pending:
+        name = pending.pop(0)
+        if name in seen:
+            continue
+        seen.add(name)
         mod = importlib.import_module(name)
         routes.extend(_ROUTES.get(mod.__name__, []))
+        # an app package may pull in a generic one (e.g. kmeans -> clustering endpoints)
+        pending.extend(getattr(mod, "INCLUDE_RESOURCES", ()))
     return routes
 
 

@@ -172,8 +172,8 @@ JAVA_CLASS_ALIASES = {
     "com.cloudera.oryx.app.serving.als": "oryx_amd.models.als.resources",
     "com.cloudera.oryx.app.serving.kmeans": "oryx_amd.models.kmeans.resources",
     "com.cloudera.oryx.app.serving.rdf": "oryx_amd.models.rdf.resources",
-    "com.cloudera.oryx.app.serving.clustering": "oryx_amd.models.kmeans.resources",
-    "com.cloudera.oryx.app.serving.classreg": "oryx_amd.models.rdf.resources",
+    "com.cloudera.oryx.app.serving.clustering": "oryx_amd.serving.clustering",
+    "com.cloudera.oryx.app.serving.classreg": "oryx_amd.serving.classreg",
     "com.cloudera.oryx.example.serving": "oryx_amd.models.example.resources",
 }
 

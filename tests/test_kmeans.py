@@ -1,0 +1,445 @@
+"""k-means app tests: ports of the reference's KMeansEvalIT / KMeansPMMLUtilsTest /
+ClusterInfoTest / KMeansUtilsTest / kmeans serving tests (T[mllib]/kmeans, T[app-common]/kmeans,
+T[serving-app]/kmeans) with their golden values, plus trainer, speed and distributed checks."""
+
+import math
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oryx_amd.api import Dataset, KeyMessage
+from oryx_amd.models import app_pmml
+from oryx_amd.models.kmeans import evaluation as ev
+from oryx_amd.models.kmeans.batch import KMeansUpdate
+from oryx_amd.models.kmeans.common import (ClusterInfo, closest_cluster, check_unique_ids,
+                                           clustering_model_pmml, features_from_tokens,
+                                           parse_feature_matrix, read_clusters,
+                                           validate_pmml_vs_schema)
+from oryx_amd.models.kmeans.serving import KMeansServingModel, KMeansServingModelManager
+from oryx_amd.models.kmeans.speed import KMeansSpeedModelManager
+from oryx_amd.models.schema import CategoricalValueEncodings, InputSchema
+from oryx_amd.ops import kmeans as km
+from oryx_amd.transport.producer import MockTopicProducer
+from oryx_amd.utils import config as cfg
+from oryx_amd.utils import pmml as pm
+
+from .serving_harness import Client
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _conf(**kv):
+    return cfg.overlay_on({k.replace("__", "."): v for k, v in kv.items()}, cfg.get_default())
+
+
+def _schema(**kv):
+    return InputSchema(_conf(**kv))
+
+
+def dummy_pmml():
+    """KMeansPMMLUtilsTest.buildDummyClusteringModel: x,y; clusters (1,0)x1, (2,-1)x2, (-1,0)x3."""
+    schema = _schema(**{"oryx__input-schema__feature-names": '["x","y"]',
+                        "oryx__input-schema__categorical-features": "[]"})
+    return clustering_model_pmml(schema, np.array([[1.0, 0.0], [2.0, -1.0], [-1.0, 0.0]]),
+                                 [1, 2, 3])
+
+
+EVAL_POINTS = np.array([[1.0, 0.0], [2.0, -2.0], [2.0, 0.0], [-2.0, 0.0], [-0.5, -1.0],
+                        [-0.5, 1.0]])
+
+
+# ---------------------------------------------------------------- schema
+
+def test_schema_num_features_and_predictors():
+    s = _schema(**{"oryx__input-schema__num-features": 4,
+                   "oryx__input-schema__categorical-features": "[]",
+                   "oryx__input-schema__ignored-features": "[0,2]"})
+    assert s.get_feature_names() == ["0", "1", "2", "3"]
+    assert s.get_num_predictors() == 2
+    assert not s.is_active(0) and s.is_active(1) and s.is_numeric("3")
+    assert s.feature_to_predictor_index(3) == 1
+    assert s.predictor_to_feature_index(0) == 1
+    with pytest.raises(ValueError):
+        s.feature_to_predictor_index(0)
+
+
+def test_schema_target_and_categorical():
+    s = _schema(**{"oryx__input-schema__feature-names": '["a","b","c","d"]',
+                   "oryx__input-schema__id-features": '["a"]',
+                   "oryx__input-schema__numeric-features": '["b"]',
+                   "oryx__input-schema__target-feature": "d"})
+    assert s.is_id("a") and s.is_categorical("c") and s.is_categorical("d")
+    assert s.has_target() and s.get_target_feature_index() == 3 and s.is_classification()
+    assert s.get_num_predictors() == 2
+    assert s.predictor_feature_indices == [1, 2]
+
+
+def test_schema_errors():
+    with pytest.raises(ValueError):
+        _schema()   # neither feature-names nor num-features
+    with pytest.raises(ValueError):
+        _schema(**{"oryx__input-schema__num-features": 2})   # no numeric/categorical set
+    with pytest.raises(ValueError):
+        _schema(**{"oryx__input-schema__feature-names": '["a","a"]',
+                   "oryx__input-schema__categorical-features": "[]"})
+
+
+def test_categorical_encodings_and_dictionary():
+    enc = CategoricalValueEncodings({1: ["x", "y", "z"]})
+    assert enc.get_value_encoding_map(1) == {"x": 0, "y": 1, "z": 2}
+    assert enc.get_encoding_value_map(1)[2] == "z"
+    assert enc.get_value_count(1) == 3 and enc.get_category_counts() == {1: 3}
+    s = _schema(**{"oryx__input-schema__feature-names": '["n","c"]',
+                   "oryx__input-schema__categorical-features": '["c"]'})
+    dd = app_pmml.build_data_dictionary(s, enc)
+    back = app_pmml.build_categorical_value_encodings(dd)
+    assert back.get_value_encoding_map(1) == enc.get_value_encoding_map(1)
+    ms = app_pmml.build_mining_schema(s, [0.25, 0.75])
+    fields = ms.findall(pm.q("MiningField"))
+    assert [f.get("importance") for f in fields] == ["0.25", "0.75"]
+
+
+# ---------------------------------------------------------------- common
+
+def test_cluster_info_update():
+    info = ClusterInfo(0, [-1.0, 2.0], 2)
+    assert repr(info) == "0 [-1.0, 2.0] 2"
+    info.update([-1.0, -1.0], 1)
+    assert repr(info) == "0 [-1.0, 1.0] 3"
+    info.update([0.0, 0.0], 3)
+    assert repr(info) == "0 [-0.5, 0.5] 6"
+
+
+def test_closest_cluster():
+    clusters = [ClusterInfo(2, [1.0, 2.0], 1), ClusterInfo(4, [0.0, -2.0], 1),
+                ClusterInfo(1, [3.0, 1.0], 1)]
+    c, d = closest_cluster(clusters, [0.0, -2.0])
+    assert c.id == 4 and d == 0.0
+    c, d = closest_cluster(clusters, [6.0, 5.0])
+    assert c.id == 1 and d == 5.0
+    with pytest.raises(ValueError):
+        closest_cluster([], [1.0])
+
+
+def test_features_from_tokens_and_matrix():
+    s = _schema(**{"oryx__input-schema__num-features": 4,
+                   "oryx__input-schema__categorical-features": "[]",
+                   "oryx__input-schema__ignored-features": "[0,2]"})
+    assert features_from_tokens(["1.0", "2.0", "0.0", "-3.5"], s).tolist() == [2.0, -3.5]
+    m = parse_feature_matrix(["1,2,3,4", "[5,6,7,8]", '"9",10,11,12'], s)
+    assert m.tolist() == [[2.0, 4.0], [6.0, 8.0], [10.0, 12.0]]
+
+
+def test_unique_ids():
+    check_unique_ids([ClusterInfo(2, [1.0], 1), ClusterInfo(4, [0.0], 1)])
+    with pytest.raises(ValueError):
+        check_unique_ids([ClusterInfo(2, [1.0], 1), ClusterInfo(2, [0.0], 1)])
+
+
+def test_pmml_round_trip_and_validate():
+    doc = dummy_pmml()
+    back = pm.from_string(pm.to_string(doc))
+    s = _schema(**{"oryx__input-schema__feature-names": '["x","y"]',
+                   "oryx__input-schema__num-features": 2,
+                   "oryx__input-schema__categorical-features": "[]"})
+    validate_pmml_vs_schema(back, s)
+    clusters = read_clusters(back)
+    assert len(clusters) == 3 and len(clusters[0].center) == 2 and clusters[1].count == 2
+    model = back.models()[0]
+    assert model.get("modelClass") == "centerBased"
+    assert model.find(pm.q("ComparisonMeasure")).get("kind") == "distance"
+    bad = _schema(**{"oryx__input-schema__feature-names": '["x","z"]',
+                     "oryx__input-schema__categorical-features": "[]"})
+    with pytest.raises(ValueError):
+        validate_pmml_vs_schema(back, bad)
+
+
+# ---------------------------------------------------------------- evaluation (KMeansEvalIT)
+
+def test_eval_golden_values():
+    clusters = read_clusters(dummy_pmml())
+    dev = torch.device("cpu")
+    assert ev.dunn_index(clusters, EVAL_POINTS, dev) == pytest.approx(1.3110480733464633,
+                                                                       abs=1e-12)
+    assert ev.davies_bouldin_index(clusters, EVAL_POINTS, dev) == pytest.approx(
+        0.9702216688254247, abs=1e-12)
+    assert ev.silhouette_coefficient(clusters, EVAL_POINTS, dev) == pytest.approx(
+        0.30648167401009796, abs=1e-12)
+    assert ev.sum_squared_error(clusters, EVAL_POINTS, dev) == pytest.approx(5.5, abs=1e-12)
+    assert len(ev.fetch_sample_data(EVAL_POINTS)) == 6
+
+
+def test_silhouette_helper():
+    assert ev.silhouette_of(-0.8, 0.2) == 5.0
+    assert ev.silhouette_of(0.8, -0.2) == -1.25
+    assert ev.silhouette_of(1.5, 1.5) == 0.0
+    assert ev.silhouette_of(1.5, float("inf")) == 1.0
+    assert ev.silhouette_of(float("inf"), 1.5) == -1.0
+
+
+def test_silhouette_tiled_matches_direct():
+    g = np.random.default_rng(3)
+    pts = np.concatenate([g.normal(c, 0.5, (150, 3)) for c in (-3, 0, 3)])
+    clusters = [ClusterInfo(i, [c] * 3, 1) for i, c in enumerate((-3.0, 0.0, 3.0))]
+    fast = ev.silhouette_coefficient(clusters, pts, torch.device("cpu"))
+    # direct O(n^2) reference
+    assign = np.argmin(((pts[:, None] - np.array([[c] * 3 for c in (-3, 0, 3)])[None]) ** 2)
+                       .sum(2), 1)
+    d = np.sqrt(((pts[:, None] - pts[None]) ** 2).sum(2))
+    tot = 0.0
+    for p in range(len(pts)):
+        own = assign == assign[p]
+        a = d[p, own].sum() / (own.sum() - 1)
+        b = min(d[p, assign == o].mean() for o in range(3) if o != assign[p])
+        tot += ev.silhouette_of(a, b)
+    assert fast == pytest.approx(tot / len(pts), abs=1e-9)
+
+
+# ---------------------------------------------------------------- trainer
+
+def _blobs(n_per=400, seed=0):
+    g = np.random.default_rng(seed)
+    cents = np.array([[0, 0, 0, 0], [8, 8, 0, 0], [-8, 8, 3, 0], [0, -9, -3, 4]], float)
+    pts = np.concatenate([g.normal(c, 0.6, (n_per, 4)) for c in cents])
+    return pts, cents
+
+
+def test_kmeans_train_recovers_blobs():
+    pts, cents = _blobs()
+    res = km.kmeans_train(torch.from_numpy(pts).float(), 4, 30, runs=2, seed=1)
+    got = res.centers.numpy()
+    for c in cents:
+        assert np.min(np.linalg.norm(got - c, axis=1)) < 0.3
+    assert res.counts.sum().item() == len(pts) and (res.counts > 0).all()
+
+
+def test_kmeans_random_init_is_lloyd_fixed_point():
+    pts, _ = _blobs()
+    x = torch.from_numpy(pts).float()
+    res = km.kmeans_train(x, 4, 50, runs=3, init="random", seed=1)
+    idx, d2 = km.assign(x, res.centers, exact=True)
+    sums, counts, _ = km.accumulate(x, idx, 4)
+    assert torch.allclose(sums / counts[:, None], res.centers, atol=1e-3)
+    assert res.cost == pytest.approx(float(d2.double().sum()), rel=1e-6)
+
+
+def test_kmeans_reseeds_empty_clusters():
+    # 3 distinct points, k=3 but random init may duplicate: every cluster must end non-empty
+    x = torch.tensor([[0.0, 0.0]] * 5 + [[10.0, 0.0]] * 5 + [[0.0, 10.0]] * 5)
+    res = km.kmeans_train(x, 3, 10, runs=1, init="random", seed=2)
+    assert sorted(res.counts.tolist()) == [5, 5, 5]
+
+
+def _update_config(tmp_path, strategy="SILHOUETTE"):
+    return _conf(**{"oryx__input-schema__num-features": 4,
+                    "oryx__input-schema__categorical-features": "[]",
+                    "oryx__kmeans__hyperparams__k": 4,
+                    "oryx__kmeans__iterations": 10,
+                    "oryx__kmeans__runs": 1,
+                    "oryx__kmeans__evaluation-strategy": strategy,
+                    "oryx__ml__eval__test-fraction": 0.2,
+                    "oryx__ml__eval__candidates": 2,
+                    "oryx__ml__eval__parallelism": 1})
+
+
+@pytest.mark.parametrize("strategy", ["SILHOUETTE", "SSE", "DUNN", "DAVIES_BOULDIN"])
+def test_kmeans_update_publishes_model(tmp_path, strategy):
+    pts, _ = _blobs(n_per=100)
+    lines = [",".join(repr(float(v)) for v in p) for p in pts]
+    upd = KMeansUpdate(_update_config(tmp_path, strategy))
+    MockTopicProducer.clear()
+    prod = MockTopicProducer()
+    upd.run_update(None, 1000, Dataset([(None, l) for l in lines]), None,
+                   str(tmp_path / "model"), prod)
+    msgs = MockTopicProducer.get_key_messages()
+    assert len(msgs) == 1 and msgs[0][0] == "MODEL"
+    doc = pm.from_string(msgs[0][1])
+    model = doc.models()[0]
+    assert model.get("numberOfClusters") == "4"
+    assert len(model.findall(pm.q("ClusteringField"))) == 4
+    clusters = read_clusters(doc)
+    assert len(clusters) == 4 and all(c.count > 0 for c in clusters)
+    assert len(clusters[0].center) == 4
+
+
+def test_kmeans_update_rejects_categorical():
+    c = _conf(**{"oryx__input-schema__num-features": 2,
+                 "oryx__input-schema__categorical-features": '["1"]'})
+    with pytest.raises(ValueError):
+        KMeansUpdate(c)
+
+
+# ---------------------------------------------------------------- speed
+
+def test_speed_manager_running_mean():
+    conf = _conf(**{"oryx__input-schema__feature-names": '["x","y"]',
+                    "oryx__input-schema__categorical-features": "[]"})
+    mgr = KMeansSpeedModelManager(conf)
+    assert mgr.build_updates(Dataset([(None, "1,1")])) == []
+    mgr.consume(iter([KeyMessage("MODEL", pm.to_string(dummy_pmml())),
+                      KeyMessage("UP", "ignored")]))
+    ups = mgr.build_updates(Dataset([(None, "1,1"), (None, "3,-1"), (None, "-3,0")]))
+    import json
+    got = [json.loads(u) for u in ups]
+    # (1,1) -> cluster 0 (1,0) count 1: mean (1,1) -> center (1,0.5), count 2
+    # (3,-1) -> cluster 1 (2,-1) count 2 -> center (2+1/3, -1), count 3
+    # (-3,0) -> cluster 2 (-1,0) count 3 -> center (-1.5, 0), count 4
+    assert got[0] == [0, [1.0, 0.5], 2]
+    assert got[1][0] == 1 and got[1][2] == 3
+    assert got[1][1] == pytest.approx([2 + 1 / 3, -1.0])
+    assert got[2] == [2, [-1.5, 0.0], 4]
+
+
+# ---------------------------------------------------------------- serving
+
+def _test_model():
+    s = _schema(**{"oryx__input-schema__num-features": 2,
+                   "oryx__input-schema__categorical-features": "[]"})
+    return KMeansServingModel([ClusterInfo(2, [1.0, 0.0], 1), ClusterInfo(3, [2.0, -1.0], 1),
+                               ClusterInfo(4, [-1.0, 0.0], 1)], s)
+
+
+def _client(read_only=False):
+    return Client(["oryx_amd.models.kmeans.resources"], _test_model(), read_only=read_only)
+
+
+def test_serving_assign():
+    c = _client()
+    assert int(c.get_text("/assign/1,0")) == 2
+    assert int(c.get_text("/assign/10,-1.0")) == 3
+    r = c.request("POST", "/assign", body="-1.5,0.5\n-1,0")
+    assert r.status == 200 and r.body.decode() == "4\n4\n"
+    assert c.status("GET", "/assign/1,0,3") == 400
+
+
+def test_serving_distance_to_nearest():
+    c = _client()
+    assert float(c.get_text("/distanceToNearest/1,0")) == 0.0
+    assert float(c.get_text("/distanceToNearest/10,-1.0")) == 8.0
+
+
+def test_serving_add_and_read_only():
+    data = "1.0,0.0,20.0\n1.0,-4.0,30.0\n0.0,0.0,40.0\n0.0,-4.0,50.0"
+    c = _client()
+    assert c.status("POST", "/add", body=data) == 204
+    assert [m for _, m in MockTopicProducer.get_key_messages()] == data.split("\n")
+    MockTopicProducer.clear()
+    assert c.status("POST", "/add/1.0,0.0,20.0") == 204
+    assert [m for _, m in MockTopicProducer.get_key_messages()] == ["1.0,0.0,20.0"]
+    ro = _client(read_only=True)
+    assert ro.status("POST", "/add", body=data) == 403
+
+
+def test_serving_console_and_ready():
+    c = _client()
+    r = c.get("/index.html")
+    assert r.status == 200 and b"<html" in r.body.lower()
+    assert c.status("GET", "/ready") == 200
+
+
+def test_serving_manager_consume():
+    conf = _conf(**{"oryx__input-schema__feature-names": '["x","y"]',
+                    "oryx__input-schema__categorical-features": "[]"})
+    mgr = KMeansServingModelManager(conf)
+    mgr.consume(iter([KeyMessage("UP", "[0,[1.0,1.0],5]")]))
+    assert mgr.get_model() is None
+    mgr.consume(iter([KeyMessage("MODEL", pm.to_string(dummy_pmml())),
+                      KeyMessage("UP", "[1,[5.0,5.0],7]")]))
+    m = mgr.get_model()
+    assert m.get_num_clusters() == 3
+    assert m.get_cluster(1).center.tolist() == [5.0, 5.0] and m.get_cluster(1).count == 7
+    assert m.nearest_cluster_id(["4.5", "4"]) == 1
+    assert m.nearest_cluster_ids([["4.5", "4"], ["-1", "0"]]) == [1, 2]
+
+
+# ---------------------------------------------------------------- distributed (gloo)
+
+def test_kmeans_distributed_gloo(tmp_path):
+    """world 2 over gloo: each rank holds half the points; the centers recover the blobs."""
+    script = tmp_path / "run.py"
+    script.write_text(f"""
+import sys, torch, numpy as np
+sys.path.insert(0, {ROOT!r})
+from oryx_amd.parallel import dist
+from oryx_amd.ops import kmeans as km
+ctx = dist.init_from_env(device='cpu')
+g = np.random.default_rng(0)
+cents = np.array([[0, 0], [9, 9], [-9, 9]], float)
+pts = np.concatenate([g.normal(c, 0.5, (300, 2)) for c in cents])
+x = torch.from_numpy(pts[ctx.rank::ctx.world_size]).float()
+res = km.kmeans_train(x, 3, 20, runs=1, seed=4, ctx=ctx)
+if ctx.rank == 0:
+    torch.save({{'c': res.centers, 'n': res.counts}}, sys.argv[1])
+""")
+    out = tmp_path / "w2.pt"
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29633", str(script), str(out)]
+    subprocess.run(cmd, check=True, env=env, timeout=180, capture_output=True)
+    r = torch.load(out)
+    got = r["c"].numpy()
+    for c in ([0, 0], [9, 9], [-9, 9]):
+        assert np.min(np.linalg.norm(got - np.array(c), axis=1)) < 0.3
+    assert int(r["n"].sum()) == 900
+
+
+# ---------------------------------------------------------------- GPU kernels
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,k", [(2, 3), (20, 64), (64, 100), (100, 257), (256, 50),
+                                 (500, 130)])
+def test_assign_kernel_matches_fp32(cuda, d, k):
+    g = torch.Generator().manual_seed(d * 1000 + k)
+    x = torch.randn(5000, d, generator=g)
+    c = torch.randn(k, d, generator=g)
+    idx, dist = km.assign(x.to(cuda), c.to(cuda))
+    # reference on the same bf16-rounded inputs, fp32 math
+    xb, cb = x.bfloat16().float(), c.bfloat16().float()
+    d2 = ((xb[:, None, :] - cb[None]) ** 2).sum(2)
+    ref_v, ref_i = d2.min(1)
+    got_i = idx.cpu()
+    got_v = dist.cpu()
+    # argmin agrees except within fp32-rounding near-ties
+    chosen = d2.gather(1, got_i[:, None])[:, 0]
+    assert torch.all(chosen <= ref_v + 1e-3 * (1 + ref_v))
+    assert (got_i == ref_i).float().mean() > 0.995
+    assert torch.allclose(got_v, ref_v, rtol=1e-3, atol=1e-3 * d)
+
+
+@pytest.mark.gpu
+def test_accumulate_kernel_matches_reference(cuda):
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(20000, 37, generator=g)
+    idx = torch.randint(0, 11, (20000,), generator=g)
+    mind = torch.rand(20000, generator=g)
+    sums, counts, stats = km.accumulate(x.to(cuda), idx.to(cuda), 11, mind.to(cuda))
+    rs = torch.zeros(11, 37).index_add_(0, idx, x)
+    rc = torch.bincount(idx, minlength=11)
+    dd = mind.double().sqrt()
+    assert torch.allclose(sums.cpu(), rs, atol=1e-3)
+    assert torch.equal(counts.cpu(), rc)
+    assert torch.allclose(stats[:, 0].cpu(), torch.zeros(11, dtype=torch.float64)
+                          .index_add_(0, idx, dd), rtol=1e-9)
+
+
+@pytest.mark.gpu
+def test_kmeans_train_gpu(cuda):
+    pts, cents = _blobs(n_per=2000)
+    res = km.kmeans_train(torch.from_numpy(pts).float().to(cuda), 4, 30, runs=1, seed=1)
+    got = res.centers.cpu().numpy()
+    for c in cents:
+        assert np.min(np.linalg.norm(got - c, axis=1)) < 0.3
+
+
+@pytest.mark.gpu
+def test_eval_metrics_gpu_match_cpu(cuda):
+    pts, cents = _blobs(n_per=500)
+    clusters = [ClusterInfo(i, c, 1) for i, c in enumerate(cents)]
+    for fn in (ev.sum_squared_error, ev.dunn_index, ev.davies_bouldin_index,
+               ev.silhouette_coefficient):
+        assert fn(clusters, pts, cuda) == pytest.approx(fn(clusters, pts, torch.device("cpu")),
+                                                        rel=1e-9)
