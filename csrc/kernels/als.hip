@@ -44,7 +44,14 @@ struct AlsParams {
   float alpha;
   int implicit;
   int* fail_count;         // nullable: incremented when a pivot is not positive
+  // split long rows: work item w with long_slot[w] >= 0 takes its Gramian, b and count from
+  // ws[slot] (summed beforehand by als_partial over fixed-size segments of the row)
+  const int32_t* long_slot;  // [n_work] (nullable)
+  const float* ws;           // [n_long][ws_stride(KP)]
 };
+
+// workspace record of one split row: full symmetric A [KP*KP], b [KP], count, padded to 16 B
+__host__ __device__ constexpr int ws_stride(int kp) { return (kp * kp + kp + 1 + 3) / 4 * 4; }
 
 __device__ __forceinline__ void als_weights(float r, float alpha, int implicit, float& wa,
                                             float& wb, float& cnt) {
@@ -69,110 +76,238 @@ constexpr int TS = 40;  // LDS row stride (bf16 elements) of the transposed chun
 
 // ------------------------------------------------------------------ wave-per-row kernel
 
+// Gathered chunk image in LDS: 32 rating rows x KP bf16, row-major (KP*2 bytes per row),
+// written lane-linearly (lane l of staging instruction `it` owns 16-byte slot it*64 + l).  The
+// 16-byte chunks of row r are rotated by rot(r) so that the ds_read_b64_tr_b16 operand reads
+// (4 ratings x 16 features per 16-lane group) are bank-conflict free (KP 32/64/96/128) or
+// 2-way (others); the rotation is applied on the GLOBAL side: slot (r, sc) holds feature
+// chunk (sc + rot(r)) % PPR.  Constants found by exhaustive search over the bank model.
 template <int KP>
-struct WaveSmem {
-  static constexpr int AS = KP + 1;
-  static constexpr int T_BYTES = KP * TS * 2;
-  static constexpr int A_BYTES = KP * AS * 4;
-  static constexpr int RAW = T_BYTES > A_BYTES ? T_BYTES : A_BYTES;
-  // + 32 floats of b weights + 64 floats of the broadcast L column
-  static constexpr int BYTES = (RAW + 15) / 16 * 16 + 128 + 256;
+struct ChunkImage {
+  static constexpr int PPR = KP / 8;              // 16-byte chunks per row
+  static constexpr int NPL = KP / 16;             // staging slots per lane (32*PPR/64)
+  static constexpr int BYTES = 32 * KP * 2;
+  static constexpr int SM = KP == 64 ? 1 : KP == 128 ? 2 : 0;
+  static constexpr int ST = KP == 64 ? 2 : KP == 128 ? 4 : (KP == 32 || KP == 96) ? 1 : 0;
+  __device__ static constexpr int rot(int r) { return (r * SM + (r >> 2) * ST) % PPR; }
 };
 
 template <int KP>
-__global__ __launch_bounds__(256) void als_solve_wave(AlsParams p) {
+struct WaveSmem {
+  static constexpr int AS = KP + 1;
+  static constexpr int G_BYTES = ChunkImage<KP>::BYTES;
+  static constexpr int A_BYTES = KP * AS * 4;
+  static constexpr int RAW = G_BYTES > A_BYTES ? G_BYTES : A_BYTES;
+  // + 64 floats of per-rating weights (wa | wb) + 64 floats of the broadcast L column
+  static constexpr int BYTES = (RAW + 15) / 16 * 16 + 256 + 256;
+};
+
+// Accumulate ratings [beg, end) of one row, one wave:
+//   acc   += lower 16x16 tiles of sum_r wa_r y_r y_r^T   (v_mfma_f32_16x16x32_bf16)
+//   bpart[pi] += sum over this lane's 8 ratings of wb_r * y_r[pi*16 + (lane&15)]
+//   cnt_acc   += #positive ratings (lanes < 32)
+// Software-pipelined one chunk deep: while the MFMAs of chunk c run, the 16-byte gathers of
+// chunk c+1 and the (col, value) metadata of chunk c+2 are in flight in registers.  All
+// gathers of a chunk are issued back to back (lanes past the row end re-read a valid row and
+// get zero weights), then written lane-linearly into the chunk image and read back
+// transposed with ds_read_b64_tr_b16 as the MFMA fragments.
+template <int KP, bool INIT_YTY>
+__device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg, int64_t end,
+                                                char* G, float* Wab,
+                                                f32x4 (&acc)[(KP / 16) * (KP / 16 + 1) / 2],
+                                                float (&bpart)[KP / 16], float& cnt_acc) {
+  using CI = ChunkImage<KP>;
+  constexpr int M = KP / 16;
+  constexpr int PPR = CI::PPR;
+  constexpr int NPL = CI::NPL;
+  // INIT_YTY: the accumulators start at this lane's fragment of YtY (zeros for explicit
+  // feedback), so A = YtY + sum c1 y yT comes out of the MFMA chain; the YtY loads are issued
+  // after the first chunk's gathers so both latencies overlap
+  auto init_yty = [&](int ln) {
+    const int gg = ln >> 4, ff = ln & 15;
+    int t = 0;
+#pragma unroll
+    for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+      for (int qi = 0; qi <= pi; ++qi, ++t)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          acc[t][v] = p.YtY[(pi * 16 + gg * 4 + v) * KP + qi * 16 + ff];
+  };
+  if (beg >= end) {
+    if (INIT_YTY) init_yty(threadIdx.x & 63);
+    return;
+  }
+  // opaque lane id: keeps the per-lane geometry below from being hoisted out of the caller's
+  // row loop (it would stay live through the register-heavy Cholesky phase)
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  const int g = lane >> 4, fl = lane & 15;
+  // per-lane staging geometry (constant over chunks)
+  int srow[NPL], soff[NPL];
+#pragma unroll
+  for (int it = 0; it < NPL; ++it) {
+    const int sl = it * 64 + lane, r = sl / PPR, sc = sl % PPR;
+    srow[it] = r;
+    soff[it] = ((sc + CI::rot(r)) % PPR) * 8;
+  }
+  // transposed-read byte offsets: operand pi, half h; lane 4q+p of group g reads row
+  // 8g+4h+q, features pi*16 + 4p .. +3
+  const int q = fl >> 2, pp = fl & 3;
+  auto tr_addr = [&](int pi, int h) -> int {
+    const int row = 8 * g + 4 * h + q;
+    const int pc = 2 * pi + (pp >> 1);
+    const int sc = (pc - CI::rot(row) + PPR) % PPR;
+    return row * KP * 2 + sc * 16 + (pp & 1) * 8;
+  };
+  auto load_meta = [&](int64_t c, int (&cols)[NPL], float& val) {
+#pragma unroll
+    for (int it = 0; it < NPL; ++it) {
+      const int64_t ri = c + srow[it] < end ? c + srow[it] : end - 1;
+      cols[it] = p.col_idx[ri];
+    }
+    const int64_t vi = c + (lane & 31) < end ? c + (lane & 31) : end - 1;
+    val = p.vals[vi];
+  };
+  i32x4 stg[NPL];
+  auto gather = [&](const int (&cols)[NPL]) {
+#pragma unroll
+    for (int it = 0; it < NPL; ++it)
+      stg[it] = *reinterpret_cast<const i32x4*>(p.Y + (int64_t)cols[it] * KP + soff[it]);
+  };
+
+  // two metadata sets used ping-pong (chunk parity) so that no register copies force an
+  // early wait on the in-flight prefetch loads
+  int cols0[NPL], cols1[NPL];
+  float val0, val1 = 0.f;
+  auto chunk = [&](int64_t c0, int (&cur_cols)[NPL], float& cur_val, int (&nxt_cols)[NPL]) {
+    const int n = (int)min((int64_t)32, end - c0);
+    float wa = 0.f, wb = 0.f, cn = 0.f;
+    if (lane < n) als_weights(cur_val, p.alpha, p.implicit, wa, wb, cn);
+    cnt_acc += cn;
+    if (lane < 32) {
+      Wab[lane] = wa;
+      Wab[32 + lane] = wb;
+    }
+#pragma unroll
+    for (int it = 0; it < NPL; ++it)
+      *reinterpret_cast<i32x4*>(G + (it * 64 + lane) * 16) = stg[it];
+    wave_sync();
+    if (c0 + 32 < end) {              // wave-uniform: prefetch chunk c+1, metadata of c+2
+      gather(nxt_cols);
+      if (c0 + 64 < end) load_meta(c0 + 64, cur_cols, cur_val);
+    }
+    const f32x4* wv = reinterpret_cast<const f32x4*>(Wab);
+    const f32x4 wa0 = wv[2 * g], wa1 = wv[2 * g + 1];
+    const f32x4 wb0 = wv[8 + 2 * g], wb1 = wv[8 + 2 * g + 1];
+    bf16x8 fa[M], fb[M];
+#pragma unroll
+    for (int pi = 0; pi < M; ++pi) {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 0)));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 1)));
+      const bf16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      fb[pi] = v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        fa[pi][j] = (__bf16)((float)v[j] * wa0[j]);
+        fa[pi][4 + j] = (__bf16)((float)v[4 + j] * wa1[j]);
+      }
+    }
+    {
+      int t = 0;
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+        for (int qi = 0; qi <= pi; ++qi, ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[pi], fb[qi], acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int pi = 0; pi < M; ++pi) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bpart[pi] += wb0[j] * (float)fb[pi][j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bpart[pi] += wb1[j] * (float)fb[pi][4 + j];
+    }
+    wave_sync();
+  };
+
+  load_meta(beg, cols0, val0);
+  gather(cols0);
+  if (beg + 32 < end) load_meta(beg + 32, cols1, val1);
+  if (INIT_YTY) init_yty(lane);
+  for (int64_t c0 = beg; c0 < end; c0 += 64) {
+    chunk(c0, cols0, val0, cols1);
+    if (c0 + 32 < end) chunk(c0 + 32, cols1, val1, cols0);
+  }
+}
+
+// sum the per-lane b partials over the 4 lane groups; lane f then takes feature f (+64h)
+template <int M>
+__device__ __forceinline__ void reduce_bpart(float (&bpart)[M]) {
+#pragma unroll
+  for (int pi = 0; pi < M; ++pi) {
+    bpart[pi] += __shfl_xor(bpart[pi], 16, 64);
+    bpart[pi] += __shfl_xor(bpart[pi], 32, 64);
+  }
+}
+
+template <int M>
+__device__ __forceinline__ float pick_bpart(const float (&bpart)[M], int sel) {
+  float r = bpart[0];
+#pragma unroll
+  for (int pi = 1; pi < M; ++pi) r = sel == pi ? bpart[pi] : r;
+  return r;
+}
+
+// PROF: accumulate per-phase shader-clock cycles of every row into prof[0..6] (analysis
+// builds only; see scripts/als_phase_profile.py)
+template <int KP, bool PROF = false>
+__global__ __launch_bounds__(256) void als_solve_wave(AlsParams p, unsigned long long* prof) {
   constexpr int M = KP / 16;
   constexpr int NT = M * (M + 1) / 2;
   constexpr int AS = WaveSmem<KP>::AS;
-  constexpr int PPR = KP / 8;         // 16-byte pieces per factor row
-  constexpr int PIECES = 32 * PPR;    // pieces per 32-rating chunk
-  static_assert(PIECES % 64 == 0, "KP must be a multiple of 16");
   __shared__ __attribute__((aligned(16))) char smem[4 * WaveSmem<KP>::BYTES];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   char* my = smem + wave * WaveSmem<KP>::BYTES;
-  __bf16* T = reinterpret_cast<__bf16*>(my);
+  char* G = my;
   float* A = reinterpret_cast<float*>(my);
-  float* Wb = reinterpret_cast<float*>(my + WaveSmem<KP>::BYTES - 384);
+  float* Wab = reinterpret_cast<float*>(my + WaveSmem<KP>::BYTES - 512);
   float* Lb = reinterpret_cast<float*>(my + WaveSmem<KP>::BYTES - 256);
   const int g = lane >> 4, fl = lane & 15;
   const int total_waves = gridDim.x * 4;
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
 
   for (int w = blockIdx.x * 4 + wave; w < p.n_work; w += total_waves) {
     const int row = p.row_ids ? p.row_ids[w] : w;
     const int64_t beg = p.row_ptr[row], end = p.row_ptr[row + 1];
+    const int slot = p.long_slot ? p.long_slot[w] : -1;
+    unsigned long long tp = PROF ? __builtin_amdgcn_s_memtime() : 0;
+#define ORYX_PHASE(ix)                                                   \
+  if (PROF) {                                                            \
+    const unsigned long long tn = __builtin_amdgcn_s_memtime();          \
+    ph[ix] += tn - tp;                                                   \
+    tp = tn;                                                             \
+  }
     f32x4 acc[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float bacc = 0.f, cnt_acc = 0.f;
-
-    for (int64_t c0 = beg; c0 < end; c0 += 32) {
-      const int n = (int)min((int64_t)32, end - c0);
-      int col = 0;
-      float wa = 0.f, wb = 0.f, cn = 0.f;
-      if (lane < n) {
-        col = p.col_idx[c0 + lane];
-        als_weights(p.vals[c0 + lane], p.alpha, p.implicit, wa, wb, cn);
-      }
-      cnt_acc += cn;
-      if (lane < 32) Wb[lane] = wb;
-      // gather 32 factor rows, transposed into T[feature][rating]
+    float bacc, cnt_acc = 0.f;
+    {
+      // split rows were accumulated by als_partial: skip their ratings here
+      float bpart[M];
 #pragma unroll
-      for (int it = 0; it < PIECES / 64; ++it) {
-        const int pid = it * 64 + lane;
-        const int r = pid / PPR, pc = pid % PPR;
-        const int cr = oryx_shfl_i(col, r);
-        bf16x8 v;
-        if (r < n) {
-          v = *reinterpret_cast<const bf16x8*>(p.Y + (int64_t)cr * KP + pc * 8);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) T[(pc * 8 + j) * TS + r] = v[j];
-      }
-      wave_sync();
-      // per-lane Gramian weights of this lane's 8 ratings
-      float wsc[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) wsc[j] = oryx_shfl(wa, 8 * g + j);
-      bf16x8 fa[M], fb[M];
-#pragma unroll
-      for (int pi = 0; pi < M; ++pi) {
-        const bf16x8 raw = *reinterpret_cast<const bf16x8*>(T + (pi * 16 + fl) * TS + 8 * g);
-        fb[pi] = raw;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) fa[pi][j] = (__bf16)((float)raw[j] * wsc[j]);
-      }
-      {
-        int t = 0;
-#pragma unroll
-        for (int pi = 0; pi < M; ++pi)
-#pragma unroll
-          for (int qi = 0; qi <= pi; ++qi, ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[pi], fb[qi], acc[t], 0, 0, 0);
-      }
-      // b += sum_r wb_r * y_r  (lane f owns feature f; wb broadcast from LDS)
-      {
-        const int f = lane < KP ? lane : KP - 1;
-        const bf16x8* trow = reinterpret_cast<const bf16x8*>(T + f * TS);
-        const f32x4* wbv = reinterpret_cast<const f32x4*>(Wb);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bf16x8 v = trow[q];
-          const f32x4 w0 = wbv[2 * q], w1 = wbv[2 * q + 1];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) bacc += w0[j] * (float)v[j];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) bacc += w1[j] * (float)v[4 + j];
-        }
-      }
-      wave_sync();
+      for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
+      wave_accumulate<KP, false>(p, beg, slot < 0 ? end : beg, G, Wab, acc, bpart, cnt_acc);
+      reduce_bpart<M>(bpart);
+      bacc = pick_bpart<M>(bpart, g);
     }
-
-    const float cnt = wave_sum(cnt_acc);
+    ORYX_PHASE(0)
+    float cnt = wave_sum(cnt_acc);
     // scatter the lower tiles (and their mirror) into A[KP][AS]
     {
       int t = 0;
@@ -187,67 +322,87 @@ __global__ __launch_bounds__(256) void als_solve_wave(AlsParams p) {
             if (pi != qi) A[j * AS + i] = acc[t][v];
           }
     }
+    if (slot >= 0) {
+      // add the split row's partial sums; lane-private opaque pointers so no per-i
+      // addresses get hoisted into SGPRs
+      const float* src = p.ws + (int64_t)slot * ws_stride(KP) + (lane < KP ? lane : 0);
+      asm volatile("" : "+v"(src));
+      float* dstc = A + (lane < KP ? lane : 0);
+      asm volatile("" : "+v"(dstc));
+      wave_sync();
+#pragma unroll 8
+      for (int i = 0; i < KP; ++i) dstc[i * AS] += src[i * KP];
+      bacc = src[KP * KP];
+      cnt = oryx_readlane(src[KP * KP + KP - (lane < KP ? lane : 0)], 0);
+    }
     wave_sync();
+    ORYX_PHASE(1)
     // lane c owns column c
     const int c = lane < KP ? lane : 0;
     const float diag = c < p.k ? p.lambda * cnt : 1.f;
     float a[KP];
     int cc = c;
     asm volatile("" : "+v"(cc));
-    // YtY is always present (zeros for explicit feedback); the opaque per-row pointer keeps
-    // the compiler from hoisting KP 64-bit addresses out of the row loop
-    const float* ycol = p.YtY + cc;
-    asm volatile("" : "+v"(ycol));
+    // + YtY column c = row c (symmetric): 16-byte loads off one opaque per-row base (YtY is
+    // always present: zeros for explicit feedback)
+    const f32x4* yrow = reinterpret_cast<const f32x4*>(p.YtY + cc * KP);
+    asm volatile("" : "+v"(yrow));
 #pragma unroll
-    for (int i = 0; i < KP; ++i) {
-      a[i] = A[i * AS + c] + ycol[i * KP] + (i == cc ? diag : 0.f);
-      if ((i & 15) == 15) __builtin_amdgcn_sched_barrier(0);
+    for (int i4 = 0; i4 < KP / 4; ++i4) {
+      const f32x4 yv = yrow[i4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = 4 * i4 + q;
+        a[i] = A[i * AS + c] + yv[q] + (i == cc ? diag : 0.f);
+      }
+      if ((i4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
+    ORYX_PHASE(2)
     // Cholesky A = L L^T in registers: after step j lane c holds L[c][j] in a[j]
-    // (lane j keeps the pivot d_j in a[j])
+    // (lane j keeps the pivot d_j in a[j] and 1/d_j in dinv).  The column of L that the
+    // rank-1 update needs is broadcast with v_readlane (one SGPR per row i, consumed by one
+    // FMA) -- no LDS round trip on the step's critical path.
     bool bad = false;
     // opaque copy of the lane id: stops the compiler hoisting 2*KP lane masks out of the row
     // loop (which would exhaust SGPRs)
     int ln = lane;
     asm volatile("" : "+v"(ln));
+    float dinv = 0.f;
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
       float s = oryx_readlane(a[j], j);
       bad |= !(s > 0.f);
       s = s > 1e-30f ? s : 1e-30f;
-      const float d = __builtin_sqrtf(s);
-      const float inv = __builtin_amdgcn_rcpf(d);
+      // one v_rsq_f32 (~1 ulp) instead of the IEEE sqrt expansion + reciprocal
+      const float inv = __builtin_amdgcn_rsqf(s);
+      const float d = s * inv;
       float l = a[j] * inv;
       l = ln < j ? 0.f : (ln == j ? d : l);
+      dinv = ln == j ? inv : dinv;
       a[j] = l;
-      // broadcast column j of L through LDS (same-address reads are conflict-free)
-      Lb[lane] = l;
-      wave_sync();
 #pragma unroll
-      for (int i4 = ((j + 1) / 4) * 4; i4 < KP; i4 += 4) {
-        const f32x4 lv = *reinterpret_cast<const f32x4*>(Lb + i4);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (i4 + q > j) a[i4 + q] -= lv[q] * l;
+      for (int i = j + 1; i < KP; ++i) {
+        a[i] -= oryx_readlane(l, i) * l;
+        if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
       }
       // pin the updated trailing column values here: without this LLVM sinks the rank-1
       // updates into a left-looking form that keeps every broadcast L column live (spills)
 #pragma unroll
       for (int i = j + 1; i < KP; ++i) asm volatile("" : "+v"(a[i]));
-      wave_sync();
     }
+    ORYX_PHASE(3)
     if (bad && lane == 0 && p.fail_count) atomicAdd(p.fail_count, 1);
     // forward: L z = b
     float zv = lane < KP ? bacc : 0.f, z_own = 0.f;
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
-      const float zj = oryx_readlane(zv, j) / oryx_readlane(a[j], j);
+      const float zj = oryx_readlane(zv * dinv, j);   // lane j scales by its own 1/d_j
       z_own = ln == j ? zj : z_own;
       zv -= a[j] * zj;
-      __builtin_amdgcn_sched_barrier(0);
     }
-    // back: L^T x = z, reading row j of L (and its pivot) from LDS
-    wave_sync();
+    ORYX_PHASE(4)
+    // back: L^T x = z.  Step j needs row j of L in every lane (lane c: L[j][c]); the rows go
+    // through LDS once and are read back independently of the solve chain.
     if (lane < KP) {
 #pragma unroll
       for (int i = 0; i < KP; ++i) A[lane * AS + i] = a[i];
@@ -256,16 +411,108 @@ __global__ __launch_bounds__(256) void als_solve_wave(AlsParams p) {
     float xv = z_own, x_own = 0.f;
 #pragma unroll
     for (int j = KP - 1; j >= 0; --j) {
-      const float xj = oryx_readlane(xv, j) / A[j * AS + j];
+      const float xj = oryx_readlane(xv * dinv, j);
       x_own = ln == j ? xj : x_own;
       xv -= A[j * AS + c] * xj;
-      __builtin_amdgcn_sched_barrier(0);
+      if ((j & 7) == 0) __builtin_amdgcn_sched_barrier(0);
     }
     if (lane < KP) {
       p.X[(int64_t)row * KP + lane] = x_own;
       if (p.Xb) p.Xb[(int64_t)row * KP + lane] = (__bf16)x_own;
     }
     wave_sync();
+    ORYX_PHASE(5)
+#undef ORYX_PHASE
+  }
+  if (PROF && lane == 0)
+    for (int i = 0; i < 6; ++i) atomicAdd(prof + i, ph[i]);
+}
+
+// Debug/verification: the raw normal equations (Gramian without YtY/lambda, b, count) of the
+// single row [beg, end), as accumulated by wave_accumulate.  One wave.
+template <int KP>
+__global__ __launch_bounds__(64) void als_debug_gram(AlsParams p, int64_t beg, int64_t end,
+                                                     float* __restrict__ out) {
+  constexpr int M = KP / 16;
+  constexpr int NT = M * (M + 1) / 2;
+  __shared__ __attribute__((aligned(16))) char smem[ChunkImage<KP>::BYTES + 256];
+  const int lane = threadIdx.x, g = lane >> 4, fl = lane & 15;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bpart[M];
+#pragma unroll
+  for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
+  float cnt_acc = 0.f;
+  wave_accumulate<KP, false>(p, beg, end, smem,
+                             reinterpret_cast<float*>(smem + ChunkImage<KP>::BYTES), acc, bpart,
+                             cnt_acc);
+  reduce_bpart<M>(bpart);
+  const float cnt = wave_sum(cnt_acc);
+  int t = 0;
+#pragma unroll
+  for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+    for (int qi = 0; qi <= pi; ++qi, ++t)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int i = pi * 16 + g * 4 + v, j = qi * 16 + fl;
+        out[i * KP + j] = acc[t][v];
+        out[j * KP + i] = acc[t][v];
+      }
+  if (lane < KP) out[KP * KP + lane] = pick_bpart<M>(bpart, g);
+  if (lane + 64 < KP) out[KP * KP + 64 + lane] = pick_bpart<M>(bpart, g + 4);
+  if (lane == 0) out[KP * KP + KP] = cnt;
+}
+
+// ------------------------------------------------------------------ split long rows
+
+// One wave per segment (row, slot, beg, end) of a long row: accumulate the segment's partial
+// Gramian / b / count and add them into the row's workspace record with fp32 atomics (one
+// 256-byte run per atomic instruction).  Runs before the solve kernel, which then takes long
+// rows' normal equations from the workspace: a row with 1e5 ratings is spread over ~100
+// waves instead of serialising on one (the tail of the popular-item half-step).
+template <int KP>
+__global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* __restrict__ segs,
+                                                  int n_seg, float* __restrict__ ws) {
+  constexpr int M = KP / 16;
+  constexpr int NT = M * (M + 1) / 2;
+  constexpr int BYTES = ChunkImage<KP>::BYTES + 256;
+  __shared__ __attribute__((aligned(16))) char smem[4 * BYTES];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  char* G = smem + wave * BYTES;
+  float* Wab = reinterpret_cast<float*>(G + ChunkImage<KP>::BYTES);
+  const int g = lane >> 4, fl = lane & 15;
+  for (int sgi = blockIdx.x * 4 + wave; sgi < n_seg; sgi += gridDim.x * 4) {
+    const int64_t slot = segs[4 * sgi + 1], beg = segs[4 * sgi + 2], end = segs[4 * sgi + 3];
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bpart[M];
+#pragma unroll
+    for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
+    float cnt_acc = 0.f;
+    wave_accumulate<KP, false>(p, beg, end, G, Wab, acc, bpart, cnt_acc);
+    reduce_bpart<M>(bpart);
+    const float cnt = wave_sum(cnt_acc);
+    float* dst = ws + slot * ws_stride(KP);
+    int t = 0;
+#pragma unroll
+    for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+      for (int qi = 0; qi <= pi; ++qi, ++t)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int i = pi * 16 + g * 4 + v, j = qi * 16 + fl;
+          atomicAdd(dst + i * KP + j, acc[t][v]);
+          if (pi != qi) atomicAdd(dst + j * KP + i, acc[t][v]);
+        }
+    // after the reduction lane (g, fl) holds b[pi*16 + fl] for every pi: lane l adds
+    // features l and l + 64
+    if (lane < KP) atomicAdd(dst + KP * KP + lane, pick_bpart<M>(bpart, g));
+    if (lane + 64 < KP) atomicAdd(dst + KP * KP + 64 + lane, pick_bpart<M>(bpart, g + 4));
+    if (lane == 0) atomicAdd(dst + KP * KP + KP, cnt);
   }
 }
 
@@ -315,7 +562,9 @@ __global__ __launch_bounds__(256) void als_solve_block(AlsParams p) {
     for (int s = 0; s < TPW; ++s) acc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
     float bacc = 0.f, cnt_acc = 0.f;
 
-    for (int64_t c0 = beg; c0 < end; c0 += 32) {
+    const int slot = p.long_slot ? p.long_slot[w] : -1;
+    const int64_t stop = slot < 0 ? end : beg;  // split rows come from the workspace
+    for (int64_t c0 = beg; c0 < stop; c0 += 32) {
       const int n = (int)min((int64_t)32, end - c0);
       __syncthreads();
       if (tid < 32) {
@@ -383,6 +632,12 @@ __global__ __launch_bounds__(256) void als_solve_block(AlsParams p) {
       if (lane == 0) s_cnt = c;
     }
     if (tid < KP) s_b[tid] = bacc;
+    if (slot >= 0) {
+      const float* src = p.ws + (int64_t)slot * ws_stride(KP);
+      for (int idx = tid; idx < KP * KP; idx += 256) A[(idx / KP) * AS + idx % KP] = src[idx];
+      if (tid < KP) s_b[tid] = src[KP * KP + tid];
+      if (tid == 0) s_cnt = src[KP * KP + KP];
+    }
     __syncthreads();
     const float reg = p.lambda * s_cnt;
     for (int idx = tid; idx < KP * KP; idx += 256) {
@@ -463,21 +718,50 @@ __global__ __launch_bounds__(256) void pair_dots(const float* __restrict__ X,
 
 extern "C" {
 
+// long_slot [n_work] (nullable) marks split rows; segs [n_seg][4] = (row, slot, beg, end);
+// ws: workspace of n_long * ws_stride(kp) floats (zeroed here).
 int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t* col_idx,
                    const float* vals, const void* Y, const float* YtY, float* X, void* Xb,
                    int n_work, int k, int kp, float lambda, float alpha, int implicit,
-                   int* fail_count, void* stream) {
+                   int* fail_count, const int32_t* long_slot, const int64_t* segs, int n_seg,
+                   int n_long, float* ws, void* stream) {
   if (n_work <= 0) return ORYX_OK;
+  if (n_seg > 0 && (!long_slot || !segs || !ws || n_long <= 0)) return ORYX_EINVAL;
   AlsParams p{row_ptr, row_ids, col_idx, vals, reinterpret_cast<const __bf16*>(Y), YtY, X,
-              reinterpret_cast<__bf16*>(Xb), n_work, k, lambda, alpha, implicit, fail_count};
+              reinterpret_cast<__bf16*>(Xb), n_work, k, lambda, alpha, implicit, fail_count,
+              n_seg > 0 ? long_slot : nullptr, ws};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int max_blocks = 256 * 16;
+  if (n_seg > 0) {
+    if (hipMemsetAsync(ws, 0, sizeof(float) * (size_t)n_long * ws_stride(kp), s) != hipSuccess)
+      return ORYX_ELAUNCH;
+    int blocks = (n_seg + 3) / 4;
+    if (blocks > max_blocks) blocks = max_blocks;
+    switch (kp) {
+#define PART_CASE(KPV)                                                                    \
+  case KPV:                                                                               \
+    hipLaunchKernelGGL(als_partial<KPV>, dim3(blocks), dim3(256), 0, s, p, segs, n_seg, ws); \
+    break;
+      PART_CASE(16)
+      PART_CASE(32)
+      PART_CASE(48)
+      PART_CASE(64)
+      PART_CASE(80)
+      PART_CASE(96)
+      PART_CASE(112)
+      PART_CASE(128)
+#undef PART_CASE
+      default:
+        return ORYX_EINVAL;
+    }
+  }
   switch (kp) {
 #define WAVE_CASE(KPV)                                                                \
   case KPV: {                                                                         \
     int blocks = (n_work + 3) / 4;                                                    \
     if (blocks > max_blocks) blocks = max_blocks;                                     \
-    hipLaunchKernelGGL(als_solve_wave<KPV>, dim3(blocks), dim3(256), 0, s, p);       \
+    hipLaunchKernelGGL((als_solve_wave<KPV, false>), dim3(blocks), dim3(256), 0, s, p,  \
+                       nullptr);                                                 \
     break;                                                                            \
   }
     WAVE_CASE(16)
@@ -513,6 +797,50 @@ int oryx_pair_dots(const float* X, const float* Y, const int32_t* us, const int3
   return oryx_check_launch();
 }
 
-int oryx_kernels_version() { return 1; }
+// analysis: als_solve_wave<64> with per-phase cycle counters (prof: 6 u64, zeroed by caller)
+int oryx_als_solve_profile64(const int64_t* row_ptr, const int32_t* row_ids,
+                             const int32_t* col_idx, const float* vals, const void* Y,
+                             const float* YtY, float* X, int n_work, int k, float lambda,
+                             float alpha, int implicit, unsigned long long* prof, void* stream) {
+  if (n_work <= 0) return ORYX_OK;
+  AlsParams p{row_ptr, row_ids, col_idx, vals, reinterpret_cast<const __bf16*>(Y), YtY, X,
+              nullptr, n_work, k, lambda, alpha, implicit, nullptr, nullptr, nullptr};
+  int blocks = (n_work + 3) / 4;
+  if (blocks > 256 * 16) blocks = 256 * 16;
+  hipLaunchKernelGGL((als_solve_wave<64, true>), dim3(blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), p, prof);
+  return oryx_check_launch();
+}
+
+int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const float* vals,
+                        const void* Y, int kp, float alpha, int implicit, long long beg,
+                        long long end, float* out, void* stream) {
+  AlsParams p{row_ptr, nullptr, col_idx, vals, reinterpret_cast<const __bf16*>(Y), nullptr,
+              nullptr, nullptr, 1, kp, 0.f, alpha, implicit, nullptr, nullptr, nullptr};
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (kp) {
+#define DBG_CASE(KPV)                                                                       \
+  case KPV:                                                                                 \
+    hipLaunchKernelGGL(als_debug_gram<KPV>, dim3(1), dim3(64), 0, s, p, (int64_t)beg,       \
+                       (int64_t)end, out);                                                  \
+    break;
+    DBG_CASE(16)
+    DBG_CASE(32)
+    DBG_CASE(48)
+    DBG_CASE(64)
+    DBG_CASE(80)
+    DBG_CASE(96)
+    DBG_CASE(112)
+    DBG_CASE(128)
+#undef DBG_CASE
+    default:
+      return ORYX_EINVAL;
+  }
+  return oryx_check_launch();
+}
+
+int oryx_kernels_version() { return 2; }
+
+int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 
 }  // extern "C"

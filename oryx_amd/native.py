@@ -105,7 +105,15 @@ def _load_kernels():
     lib = ctypes.CDLL(path)
     _sig(lib, "oryx_kernels_version", c_i, [])
     _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
-                                      c_i, c_f, c_f, c_i, c_vp, c_vp])
+                                      c_i, c_f, c_f, c_i, c_vp, c_vp, c_vp, c_i, c_i, c_vp,
+                                      c_vp])
+    _sig(lib, "oryx_als_ws_stride", c_i, [c_i])
+    _sig(lib, "oryx_als_solve_profile64", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i,
+                                                c_i, c_f, c_f, c_i, c_vp, c_vp])
+    _sig(lib, "oryx_gramian_ws_floats", c_i, [c_i])
+    _sig(lib, "oryx_als_debug_gram", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_f, c_i, c_ll, c_ll,
+                                           c_vp, c_vp])
+    _sig(lib, "oryx_gramian_f32", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])
     for name, res, args in [
         ("oryx_topk_scores", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_i, c_vp, c_vp,

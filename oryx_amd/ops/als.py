@@ -49,18 +49,70 @@ class CSR:
     n_rows: int
     n_cols: int
     order: torch.Tensor
+    # rows longer than the split threshold are accumulated in segments by several waves:
+    # long_slot [n_work] int32 (-1 = not split), segs [n_seg, 4] int64 (row, slot, beg, end)
+    long_slot: Optional[torch.Tensor] = None
+    segs: Optional[torch.Tensor] = None
+    n_long: int = 0
+    _ws: Optional[torch.Tensor] = None
 
     @property
     def nnz(self) -> int:
         return int(self.cols.numel())
 
+    @property
+    def n_seg(self) -> int:
+        return 0 if self.segs is None else int(self.segs.shape[0])
+
     def to(self, device) -> "CSR":
+        mv = (lambda t: None if t is None else t.to(device))
         return CSR(self.row_ptr.to(device), self.cols.to(device), self.vals.to(device),
-                   self.n_rows, self.n_cols, self.order.to(device))
+                   self.n_rows, self.n_cols, self.order.to(device), mv(self.long_slot),
+                   mv(self.segs), self.n_long)
+
+    def workspace(self, kp: int) -> Optional[torch.Tensor]:
+        """fp32 scratch for the split rows' partial normal equations (kernel zeroes it)."""
+        if self.n_seg == 0:
+            return None
+        need = self.n_long * ws_stride(kp)
+        if self._ws is None or self._ws.numel() < need or self._ws.device != self.row_ptr.device:
+            self._ws = torch.empty(need, dtype=torch.float32, device=self.row_ptr.device)
+        return self._ws
+
+
+SPLIT_THRESHOLD = 2048   # rows with more ratings than this are split ...
+SPLIT_SEGMENT = 1024     # ... into segments of this many ratings (one wave each)
+
+
+def ws_stride(kp: int) -> int:
+    """Floats per split-row workspace record: A [kp*kp], b [kp], count; 16-byte aligned."""
+    return (kp * kp + kp + 1 + 3) // 4 * 4
+
+
+def _split_long_rows(row_ptr: torch.Tensor, order: torch.Tensor, counts: torch.Tensor,
+                     threshold: int, seg: int):
+    lens = counts[order]
+    n_long = int((lens > threshold).sum())   # order is longest-first: long rows lead
+    if n_long == 0:
+        return None, None, 0
+    dev = order.device
+    long_rows = order[:n_long].to(torch.int64)
+    nseg = (lens[:n_long] + seg - 1) // seg
+    seg_slot = torch.repeat_interleave(torch.arange(n_long, device=dev), nseg)
+    first = torch.cumsum(nseg, 0) - nseg
+    j = torch.arange(int(nseg.sum()), device=dev) - first[seg_slot]
+    seg_row = long_rows[seg_slot]
+    beg = row_ptr[seg_row] + j * seg
+    end = torch.minimum(beg + seg, row_ptr[seg_row + 1])
+    segs = torch.stack([seg_row, seg_slot, beg, end], 1).contiguous()
+    long_slot = torch.full((order.numel(),), -1, dtype=torch.int32, device=dev)
+    long_slot[:n_long] = torch.arange(n_long, dtype=torch.int32, device=dev)
+    return long_slot, segs, n_long
 
 
 def build_csr(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_rows: int,
-              n_cols: int, row_offset: int = 0) -> CSR:
+              n_cols: int, row_offset: int = 0, split_threshold: int = SPLIT_THRESHOLD,
+              split_segment: int = SPLIT_SEGMENT) -> CSR:
     """CSR of (row, col, val) triples (rows are global ids; ``row_offset`` makes them local).
 
     Triples must already be unique per (row, col).  Runs on the tensors' device.
@@ -77,8 +129,10 @@ def build_csr(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_rows
     torch.cumsum(counts, 0, out=row_ptr[1:])
     nz_rows = torch.nonzero(counts, as_tuple=False).flatten()
     order = nz_rows[torch.argsort(counts[nz_rows], descending=True, stable=True)]
+    long_slot, segs, n_long = _split_long_rows(row_ptr, order, counts, split_threshold,
+                                               split_segment)
     return CSR(row_ptr, c_sorted.contiguous(), v_sorted.contiguous(), int(n_rows), int(n_cols),
-               order.to(torch.int32).contiguous())
+               order.to(torch.int32).contiguous(), long_slot, segs, n_long)
 
 
 def to_bf16_padded(x: torch.Tensor, kp: int) -> torch.Tensor:
@@ -89,9 +143,32 @@ def to_bf16_padded(x: torch.Tensor, kp: int) -> torch.Tensor:
     return out
 
 
+_GRAM_WS = {}
+
+
 def gramian(x: torch.Tensor) -> torch.Tensor:
-    """``XᵀX`` in fp32 (a plain library GEMM: hipBLASLt on GPU)."""
+    """``XᵀX`` in fp32.
+
+    On the GPU (width a multiple of 16, <= 128) this is the split-K fp32-MFMA kernel
+    ``oryx_gramian_f32`` (csrc/kernels/gramian.hip): ~10 us for 162k x 64, where a library
+    GEMM tiles the tiny 64 x 64 output over a handful of CUs.  Elsewhere a plain matmul.
+    """
     x = x.to(torch.float32)
+    kp = x.shape[1] if x.dim() == 2 else 0
+    if (x.device.type == "cuda" and kp % 16 == 0 and 0 < kp <= 128 and x.shape[0] > 0
+            and x.stride(1) == 1 and native.kernels_available()):
+        lib = native.kernels()
+        need = lib.oryx_gramian_ws_floats(kp)
+        key = (x.device, kp)
+        ws = _GRAM_WS.get(key)
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(need, dtype=torch.float32, device=x.device)
+            _GRAM_WS[key] = ws
+        out = torch.empty((kp, kp), dtype=torch.float32, device=x.device)
+        rc = lib.oryx_gramian_f32(x.data_ptr(), x.shape[0], x.stride(0), kp, out.data_ptr(),
+                                  ws.data_ptr(), native.stream_ptr(x.device))
+        native.check(rc, "oryx_gramian_f32")
+        return out
     return x.t().matmul(x)
 
 
@@ -121,6 +198,10 @@ def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_ou
         assert x_out.shape[0] >= csr.n_rows and y_bf16.shape[0] >= csr.n_cols
         if xb_out is not None:
             assert xb_out.dtype == torch.bfloat16 and xb_out.shape == x_out.shape
+        ws = csr.workspace(kp)
+        if ws is not None:
+            assert lib.oryx_als_ws_stride(kp) == ws_stride(kp)
+            assert csr.long_slot.numel() == csr.order.numel() and csr.segs.shape[1] == 4
         rc = lib.oryx_als_solve(csr.row_ptr.data_ptr(), csr.order.data_ptr(),
                                 csr.cols.data_ptr(), csr.vals.data_ptr(), y_bf16.data_ptr(),
                                 yty.data_ptr(), x_out.data_ptr(),
@@ -128,6 +209,10 @@ def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_ou
                                 int(csr.order.numel()), int(k), int(kp), float(lam),
                                 float(alpha), int(bool(implicit)),
                                 fail_count.data_ptr() if fail_count is not None else None,
+                                csr.long_slot.data_ptr() if csr.n_seg else None,
+                                csr.segs.data_ptr() if csr.n_seg else None,
+                                csr.n_seg, csr.n_long,
+                                ws.data_ptr() if ws is not None else None,
                                 native.stream_ptr(device))
         native.check(rc, "oryx_als_solve")
         return

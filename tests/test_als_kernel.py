@@ -113,3 +113,59 @@ def test_pair_dots(cuda):
     out = als_ops.pair_dots(x, y, us, it)
     ref = (x[us] * y[it]).sum(1)
     assert torch.allclose(out, ref, atol=1e-4, rtol=1e-4)
+
+
+def test_split_long_rows_layout_cpu():
+    # rows of length 10, 5, 3 with threshold 4 / segment 4 -> rows 0 and 1 split
+    rows = torch.tensor([0] * 10 + [1] * 5 + [2] * 3)
+    cols = torch.cat([torch.arange(10), torch.arange(5), torch.arange(3)])
+    csr = als_ops.build_csr(rows, cols, torch.ones(18), 3, 10, split_threshold=4,
+                            split_segment=4)
+    assert csr.n_long == 2 and csr.order.tolist() == [0, 1, 2]
+    assert csr.long_slot.tolist() == [0, 1, -1]
+    assert csr.segs.tolist() == [[0, 0, 0, 4], [0, 0, 4, 8], [0, 0, 8, 10],
+                                 [1, 1, 10, 14], [1, 1, 14, 15]]
+    none = als_ops.build_csr(rows, cols, torch.ones(18), 3, 10)
+    assert none.n_seg == 0 and none.long_slot is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [16, 64, 100])
+def test_kernel_split_rows_match_unsplit(cuda, k):
+    """Long rows accumulated in segments by several waves (als_partial) == one wave per row."""
+    g = torch.Generator().manual_seed(k)
+    n_rows, n_cols = 300, 3000
+    # a few very long rows plus many short ones
+    key = torch.unique(torch.cat([
+        torch.randint(0, 3 * n_cols, (6000,), generator=g),
+        torch.randint(0, n_rows * n_cols, (20000,), generator=g)]))
+    rows, cols = key // n_cols, key % n_cols
+    vals = torch.randint(1, 10, (key.numel(),), generator=g).float() * 0.5
+    kp = als_ops.padded_rank(k)
+    y = torch.zeros(n_cols, kp)
+    y[:, :k] = torch.randn(n_cols, k, generator=g) * 0.3
+    yb = y.to(cuda).to(torch.bfloat16)
+    yty = als_ops.gramian(yb.float())
+    outs = []
+    for thr in (1 << 30, 200):
+        csr = als_ops.build_csr(rows, cols, vals, n_rows, n_cols, split_threshold=thr,
+                                split_segment=96).to(cuda)
+        assert (csr.n_long > 0) == (thr == 200)
+        x = torch.zeros(n_rows, kp, device=cuda)
+        als_ops.solve_rows(csr, yb, yty, x, None, k, 0.05, 1.0, True)
+        outs.append(x)
+    torch.cuda.synchronize()
+    scale = outs[0].abs().max().item()
+    assert (outs[0] - outs[1]).abs().max().item() <= 1e-3 * max(scale, 1.0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,kp", [(1, 16), (1000, 16), (162541, 64), (70001, 128), (5, 48),
+                                  (33333, 80)])
+def test_gramian_kernel(cuda, n, kp):
+    g = torch.Generator().manual_seed(n + kp)
+    x = torch.randn(n, kp, generator=g)
+    got = als_ops.gramian(x.to(cuda)).cpu()
+    ref = (x.double().t() @ x.double()).float()
+    assert torch.allclose(got, ref, rtol=1e-4, atol=1e-3 * max(1.0, n ** 0.5))
+    assert torch.equal(got, got.t())
