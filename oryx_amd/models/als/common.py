@@ -134,19 +134,58 @@ class FeatureVectors:
             self._dirty.add(row)
             self.version += 1
 
+    def _ensure_capacity(self, rows: int) -> None:
+        cap = self._host.shape[0]
+        if rows <= cap:
+            return
+        while cap < rows:
+            cap *= 2
+        host = np.zeros((cap, self.k), dtype=np.float32)
+        host[:self._host.shape[0]] = self._host
+        valid = np.zeros(cap, dtype=bool)
+        valid[:self._host_valid.shape[0]] = self._host_valid
+        self._host, self._host_valid = host, valid
+        self._dirty_all = True
+
     def set_vectors(self, ids: Sequence[str], matrix: np.ndarray) -> None:
+        """Bulk insert/update (model loading): new IDs get one contiguous block of rows."""
         matrix = np.asarray(matrix, dtype=np.float32)
+        if matrix.ndim != 2 or matrix.shape[1] != self.k or len(ids) != matrix.shape[0]:
+            raise ValueError("bad matrix shape %s for %d ids" % (matrix.shape, len(ids)))
         with self._lock.write():
-            for id_, v in zip(ids, matrix):
-                row = self._index.get(id_)
-                if row is None:
-                    row = self._alloc_row()
-                    self._index[id_] = row
-                    self._ids[row] = id_
-                    self._recent.add(id_)
-                self._host[row] = v
-                self._host_valid[row] = True
-                self._dirty.add(row)
+            index = self._index
+            rows = np.fromiter((index.get(i, -1) for i in ids), dtype=np.int64, count=len(ids))
+            new_pos = np.nonzero(rows < 0)[0]
+            if len(new_pos):
+                new_ids = [ids[j] for j in new_pos.tolist()]
+                if len(set(new_ids)) != len(new_ids):
+                    # duplicates within the batch: fall back to the one-by-one path
+                    for id_, v in zip(ids, matrix):
+                        row = index.get(id_)
+                        if row is None:
+                            row = self._alloc_row()
+                            index[id_] = row
+                            self._ids[row] = id_
+                            self._recent.add(id_)
+                        self._host[row] = v
+                        self._host_valid[row] = True
+                        self._dirty.add(row)
+                    self.version += 1
+                    return
+                start = self._n_rows
+                self._ensure_capacity(start + len(new_ids))
+                new_rows = np.arange(start, start + len(new_ids), dtype=np.int64)
+                index.update(zip(new_ids, new_rows.tolist()))
+                self._ids.extend(new_ids)
+                self._recent.update(new_ids)
+                self._n_rows = start + len(new_ids)
+                rows[new_pos] = new_rows
+            self._host[rows] = matrix
+            self._host_valid[rows] = True
+            if len(rows) > max(1024, self._n_rows // 8):
+                self._dirty_all = True
+            else:
+                self._dirty.update(rows.tolist())
             self.version += 1
 
     def remove_vector(self, id_: str) -> None:

@@ -435,6 +435,9 @@ class _Handler(http.server.BaseHTTPRequestHandler):
     protocol_version = "HTTP/1.1"
     server_version = "Oryx"
     sys_version = ""
+    # TCP_NODELAY: with keep-alive, Nagle + the client's delayed ACK would add ~40 ms to
+    # every response
+    disable_nagle_algorithm = True
 
     def log_message(self, fmt, *args):
         log.debug("%s - %s", self.address_string(), fmt % args)
@@ -471,9 +474,11 @@ class _Handler(http.server.BaseHTTPRequestHandler):
         for k, v in headers_out.items():
             self.send_header(k, v)
         self.send_header("Content-Length", str(len(payload)))
-        self.end_headers()
+        # status line, headers and body leave in ONE write
+        self._headers_buffer.append(b"\r\n")
         if self.command != "HEAD" and payload:
-            self.wfile.write(payload)
+            self._headers_buffer.append(payload)
+        self.flush_headers()
         if srv.metrics is not None:
             srv.metrics.observe_request(parsed.path, resp.status, time.perf_counter() - t0)
 
