@@ -1,0 +1,215 @@
+"""RDF batch-layer update: parse -> encode -> GPU random forest -> PMML -> publish.
+
+Equivalent of ``RDFUpdate`` (``[mllib]/rdf/RDFUpdate.java:97-558``) and ``Evaluation``
+(``[mllib]/rdf/Evaluation.java:32-53``):
+
+* config ``oryx.rdf.num-trees`` and hyperparameters ``max-split-candidates``, ``max-depth``,
+  ``impurity``; the input schema must have a target (categorical -> classification);
+* categorical values are encoded in order of first appearance over the training data;
+* training: :func:`oryx_amd.ops.rdf.train_forest` (HIP histogram + routing kernels);
+* PMML: TreeModel (one tree) or MiningModel with one segment per tree; node record counts
+  and feature importances (share of decision-node visits per predictor) come from pushing all
+  training examples through the trees, as the reference does;
+* evaluation: accuracy (classification) or -RMSE (regression) of the forest on the test set,
+  scored on the device over the flattened trees.
+"""
+
+from __future__ import annotations
+
+import logging
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ...ml import hyperparams as hp
+from ...ml.mlupdate import MLUpdate
+from ...ops import rdf as rdf_ops
+from ...parallel import dist
+from ...utils import rng, text
+from ..classreg import CategoricalPrediction, NumericPrediction
+from ..schema import CategoricalValueEncodings, InputSchema
+from . import pmml as rdf_pmml
+from .pmml import TreeSpecNode
+
+__all__ = ["RDFUpdate", "parse_examples", "distinct_values", "evaluate_forest"]
+
+log = logging.getLogger(__name__)
+
+
+def distinct_values(rows: Sequence[Sequence[str]], schema: InputSchema) -> Dict[int, List[str]]:
+    """Categorical feature index -> distinct values in order of first appearance."""
+    cats = [i for i in range(schema.get_num_features()) if schema.is_categorical(i)]
+    seen: Dict[int, Dict[str, None]] = {i: {} for i in cats}
+    for r in rows:
+        for i in cats:
+            seen[i].setdefault(r[i], None)
+    return {i: list(v.keys()) for i, v in seen.items()}
+
+
+def parse_examples(rows: Sequence[Sequence[str]], schema: InputSchema,
+                   encodings: CategoricalValueEncodings, require_target: bool = True
+                   ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """(predictors float64 [n, P], target float64 [n] (NaN if missing), all-features
+    float64 [n, F] with categorical encodings (for scoring))."""
+    n = len(rows)
+    F = schema.get_num_features()
+    full = np.zeros((n, F), dtype=np.float64)
+    for fi in range(F):
+        if schema.is_numeric(fi):
+            col = [r[fi] for r in rows]
+            if schema.is_target(fi):
+                full[:, fi] = [float(v) if v != "" else np.nan for v in col]
+            else:
+                full[:, fi] = np.asarray(col, dtype=np.float64) if n else 0.0
+        elif schema.is_categorical(fi):
+            m = encodings.get_value_encoding_map(fi)
+            if schema.is_target(fi):
+                full[:, fi] = [m[r[fi]] if r[fi] != "" else np.nan for r in rows]
+            else:
+                full[:, fi] = [m[r[fi]] for r in rows]
+    pred_idx = schema.predictor_feature_indices
+    X = full[:, pred_idx]
+    target = full[:, schema.get_target_feature_index()] if schema.has_target() else \
+        np.full(n, np.nan)
+    if require_target and n and np.isnan(target).any():
+        raise ValueError("missing target value")
+    return X, target, full
+
+
+def _to_spec(node: rdf_ops.TrainedNode, data: rdf_ops.BinnedData, schema: InputSchema,
+             classification: bool) -> TreeSpecNode:
+    spec = TreeSpecNode(node.id, node.count)
+    if node.feature < 0:
+        if classification:
+            spec.class_counts = node.stats
+        else:
+            w = node.stats[0]
+            spec.mean = node.stats[1] / w if w > 0 else 0.0
+        return spec
+    spec.feature = schema.predictor_to_feature_index(node.feature)
+    if node.bin < 0:
+        spec.left_categories = [int(e) for e in node.cat_left]
+    else:
+        spec.threshold = float(data.thresholds[node.feature][node.bin])
+    spec.left = _to_spec(node.left, data, schema, classification)
+    spec.right = _to_spec(node.right, data, schema, classification)
+    spec.default_right = node.right.count > node.left.count
+    return spec
+
+
+def evaluate_forest(forest, encodings, schema: InputSchema, full: np.ndarray,
+                    target: np.ndarray, device) -> float:
+    """Accuracy (classification) or RMSE (regression) of the forest on the given examples."""
+    if len(full) == 0:
+        return 0.0 if schema.is_classification() else float("nan")
+    C = encodings.get_value_count(schema.get_target_feature_index()) \
+        if schema.is_classification() else 0
+    flat = rdf_ops.flatten_forest(forest, device, C)
+    X = torch.from_numpy(full).to(device)
+    leaves = rdf_ops.forest_leaves(flat, X)                          # [n, T]
+    vals = flat.leaf_value[leaves]                                    # [n, T, C|1]
+    w = flat.weights[None, :, None]
+    vote = (vals * w).sum(1) / flat.weights.sum()
+    tgt = torch.from_numpy(target).to(device)
+    if schema.is_classification():
+        pred = vote.argmax(1)
+        return float((pred == tgt.long()).double().mean())
+    return float(torch.sqrt(((vote[:, 0] - tgt) ** 2).mean()))
+
+
+class RDFUpdate(MLUpdate):
+    def __init__(self, config):
+        super().__init__(config)
+        self.num_trees = config.get_int("oryx.rdf.num-trees")
+        if self.num_trees < 1:
+            raise ValueError("num-trees must be >= 1")
+        self.hyper_param_values = [
+            hp.from_config(config, "oryx.rdf.hyperparams.max-split-candidates"),
+            hp.from_config(config, "oryx.rdf.hyperparams.max-depth"),
+            hp.from_config(config, "oryx.rdf.hyperparams.impurity"),
+        ]
+        self.input_schema = InputSchema(config)
+        if not self.input_schema.has_target():
+            raise ValueError("RDF needs a target feature")
+
+    def get_hyper_parameter_values(self):
+        return self.hyper_param_values
+
+    def _ctx(self, context) -> dist.DistContext:
+        if isinstance(context, dist.DistContext):
+            return context
+        c = getattr(context, "dist", None)
+        return c if c is not None else dist.get_context()
+
+    def build_model(self, context, train_data, hyper_parameters, candidate_path):
+        max_split_candidates = int(hyper_parameters[0])
+        max_depth = int(hyper_parameters[1])
+        impurity = str(hyper_parameters[2])
+        if max_split_candidates < 2:
+            raise ValueError("max-split-candidates must be at least 2")
+        if max_depth <= 0:
+            raise ValueError("max-depth must be at least 1")
+        schema = self.input_schema
+        rows = [text.parse_input_line(l) for l in train_data]
+        if not rows:
+            return None
+        encodings = CategoricalValueEncodings(distinct_values(rows, schema))
+        X, target, _ = parse_examples(rows, schema, encodings)
+        ctx = self._ctx(context)
+        P = schema.get_num_predictors()
+        categorical = [schema.is_categorical(schema.predictor_to_feature_index(p))
+                       for p in range(P)]
+        arities = [encodings.get_value_count(schema.predictor_to_feature_index(p))
+                   if categorical[p] else 0 for p in range(P)]
+        seed = rng.next_seed()
+        t0 = time.perf_counter()
+        # every rank holds the same parsed rows; each trains on a disjoint slice and the level
+        # histograms are all-reduced
+        sl = slice(ctx.rank, None, ctx.world_size)
+        data = rdf_ops.bin_features(X[sl], categorical, arities, max_split_candidates,
+                                    ctx.device, seed=seed, threshold_source=X)
+        classification = schema.is_classification()
+        C = encodings.get_value_count(schema.get_target_feature_index()) if classification \
+            else 0
+        tgt = torch.from_numpy(target[sl])
+        trained = rdf_ops.train_forest(data, tgt, C, self.num_trees, max_depth, impurity,
+                                       seed=seed, ctx=ctx)
+        log.info("RDF %d trees depth %d on %d examples x %d predictors: %.3fs", self.num_trees,
+                 max_depth, len(rows), P, time.perf_counter() - t0)
+        if not ctx.is_main:
+            return None
+        total = trained.predictor_counts.sum()
+        if total <= 0:
+            importances = np.zeros(P)
+        else:
+            importances = trained.predictor_counts / total
+        roots = [_to_spec(r, data, schema, classification) for r in trained.roots]
+        return rdf_pmml.forest_to_pmml(roots, schema, encodings, importances, max_depth,
+                                       max_split_candidates, impurity)
+
+    def evaluate(self, context, model, model_parent_path, test_data, train_data):
+        rdf_pmml.validate_pmml_vs_schema(model, self.input_schema)
+        forest, encodings = rdf_pmml.read(model)
+        rows = [text.parse_input_line(l) for l in test_data]
+        try:
+            _, target, full = parse_examples(rows, self.input_schema, encodings)
+        except KeyError:
+            # a categorical value never seen in training: score example by example
+            rows = [r for r in rows if self._known(r, encodings)]
+            _, target, full = parse_examples(rows, self.input_schema, encodings)
+        ev = evaluate_forest(forest, encodings, self.input_schema, full, target,
+                             self._ctx(context).device)
+        if self.input_schema.is_classification():
+            log.info("Accuracy: %s", ev)
+            return ev
+        log.info("RMSE: %s", ev)
+        return -ev
+
+    def _known(self, row, encodings) -> bool:
+        s = self.input_schema
+        for i in range(s.get_num_features()):
+            if s.is_categorical(i) and row[i] not in encodings.get_value_encoding_map(i):
+                return False
+        return True

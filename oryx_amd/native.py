@@ -115,20 +115,21 @@ def _load_kernels():
                                            c_vp, c_vp])
     _sig(lib, "oryx_gramian_f32", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])
-    for name, res, args in [
-        ("oryx_topk_scores", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_i, c_vp, c_vp,
-                                   c_vp, c_vp]),
-        ("oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp, c_vp]),
-        ("oryx_kmeans_accumulate", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
-                                         c_vp]),
-        ("oryx_rdf_histogram", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i, c_i,
-                                     c_i, c_vp, c_vp]),
-        ("oryx_tree_traverse", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_i,
-                                     c_i, c_i, c_vp, c_vp]),
-        ("oryx_lsh_hash", c_i, [c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp]),
-    ]:
-        if hasattr(lib, name):
-            _sig(lib, name, res, args)
+    _sig(lib, "oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
+                                          c_vp])
+    _sig(lib, "oryx_kmeans_accumulate", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp,
+                                              c_vp, c_vp])
+    # Xb, bin_bytes, n, P, label, y, S, cls, weight, T, node_of, node_lo, nodes, feats, Fs, B,
+    # hist, stream
+    _sig(lib, "oryx_rdf_histogram", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i, c_vp, c_i,
+                                          c_vp, c_i, c_i, c_vp, c_i, c_i, c_vp, c_vp])
+    # Xb, bin_bytes, n, P, T, node_of, nodes, split_feat, split_bin, cat_left, B, child_base,
+    # visits, stream
+    _sig(lib, "oryx_rdf_route", c_i, [c_vp, c_i, c_ll, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp,
+                                      c_i, c_vp, c_vp, c_vp])
+    # X, n, F, T, roots, feat, thr, cat_off, cat_bits, cat_len, left, right, leaf, stream
+    _sig(lib, "oryx_rdf_forest_leaf", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            c_vp, c_vp, c_vp, c_vp, c_vp])
     return lib
 
 

@@ -290,7 +290,8 @@ def pair_dots(x: torch.Tensor, y: torch.Tensor, us: torch.Tensor, items: torch.T
         out = torch.empty(us.numel(), dtype=torch.float32, device=x.device)
         u32 = us.to(torch.int32).contiguous()
         i32 = items.to(torch.int32).contiguous()
-        rc = lib.oryx_pair_dots(x.contiguous().data_ptr(), y.contiguous().data_ptr(),
+        xc, yc = x.contiguous(), y.contiguous()     # alive until the launch
+        rc = lib.oryx_pair_dots(xc.data_ptr(), yc.data_ptr(),
                                 u32.data_ptr(), i32.data_ptr(), int(us.numel()), int(x.shape[1]),
                                 out.data_ptr(), native.stream_ptr(x.device))
         native.check(rc, "oryx_pair_dots")

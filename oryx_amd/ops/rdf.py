@@ -1,0 +1,511 @@
+"""Random-decision-forest training and scoring on the device.
+
+Replaces Spark MLlib ``RandomForest.trainClassifier/trainRegressor`` as invoked at
+``[mllib]/rdf/RDFUpdate.java:140-158`` plus the node/feature example counting of
+``RDFUpdate.treeNodeExampleCounts`` / ``predictorExampleCounts`` (``:269-333``); SURVEY.md
+K12-K14.  The algorithm is MLlib's histogram (binned) level-wise random forest:
+
+* continuous predictors are binned on quantile thresholds of a sample (<= max-split-candidates
+  bins; features with fewer distinct values split between every value), categorical predictors
+  use their encodings as bins;
+* every tree gets Poisson(1) bootstrap weights (one tree: no bootstrap) and, at every node, a
+  random feature subset ("auto": all features for one tree, sqrt(P) for classification, P/3 for
+  regression);
+* level by level, ALL trees at once: the HIP histogram kernel (``oryx_rdf_histogram``,
+  csrc/kernels/rdf.hip) aggregates label statistics per (tree, node, feature, bin); the best
+  split per node (max impurity decrease: gini / entropy / variance; categorical bins ordered by
+  label centroid) is chosen with batched tensor ops; ``oryx_rdf_route`` moves every row one
+  level down and counts node visits;
+* a node becomes a leaf at max depth, when pure, with < 2 weighted examples, or when no split
+  improves impurity.
+
+Multi-GPU: histograms are additive, so ranks holding disjoint row slices all-reduce each
+level's histogram (one RCCL call per level) and choose identical splits.
+
+On CPU the same algorithm runs with ``index_add`` (tests / the ``local[*]`` plumbing path).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import native
+from ..parallel import dist
+
+__all__ = ["BinnedData", "bin_features", "train_forest", "TrainedForest", "FlatForest",
+           "flatten_forest", "forest_leaves"]
+
+_HIST_BUDGET = 1 << 26          # floats per histogram pass (256 MB)
+
+
+@dataclass
+class BinnedData:
+    Xb: torch.Tensor                 # [n, P] uint8 or int16 bins
+    n_bins: List[int]                # per predictor
+    thresholds: List[Optional[np.ndarray]]   # numeric predictors: bin b is x <= thr[b]
+    categorical: List[bool]
+    B: int                           # max bins over predictors
+
+    @property
+    def bin_bytes(self) -> int:
+        return self.Xb.element_size()
+
+
+def _quantile_thresholds(col: np.ndarray, max_bins: int) -> np.ndarray:
+    u = np.unique(col)
+    if len(u) <= max_bins:
+        return u[:-1].astype(np.float64)
+    qs = np.quantile(col, np.arange(1, max_bins) / max_bins, method="lower")
+    thr = np.unique(qs)
+    # never put the maximum as a threshold (nothing could go right of it)
+    return thr[thr < u[-1]].astype(np.float64)
+
+
+def bin_features(X, categorical: Sequence[bool], arities: Sequence[int], max_bins: int,
+                 device, seed: int = 0, sample_size: Optional[int] = None,
+                 threshold_source=None) -> BinnedData:
+    """``X``: float64 [n, P] predictors (categorical as encodings).  Returns device bins.
+
+    ``threshold_source``: the rows the split thresholds are computed from (default ``X``);
+    ranks that bin disjoint slices of one data set pass the full data so that every rank
+    gets identical bins.
+    """
+    X = np.asarray(X, dtype=np.float64)
+    n, P = X.shape
+    src = X if threshold_source is None else np.asarray(threshold_source, dtype=np.float64)
+    rng = np.random.default_rng(seed)
+    ns = sample_size or max(10000, max_bins * max_bins)
+    sample = src if len(src) <= ns else src[rng.choice(len(src), ns, replace=False)]
+    thresholds: List[Optional[np.ndarray]] = []
+    n_bins: List[int] = []
+    for f in range(P):
+        if categorical[f]:
+            thresholds.append(None)
+            n_bins.append(max(1, int(arities[f])))
+        else:
+            thr = _quantile_thresholds(sample[:, f], max_bins)
+            thresholds.append(thr)
+            n_bins.append(len(thr) + 1)
+    B = max(n_bins) if n_bins else 1
+    dtype = torch.uint8 if B <= 256 else torch.int16
+    Xb = torch.empty((n, P), dtype=dtype, device=device)
+    for f in range(P):
+        col = torch.from_numpy(np.ascontiguousarray(X[:, f])).to(device)
+        if categorical[f]:
+            b = col.to(torch.int64)
+        else:
+            thr = torch.from_numpy(thresholds[f]).to(device)
+            # number of thresholds strictly below x: x <= thr[b] <=> bin <= b
+            b = torch.searchsorted(thr, col, right=False) if len(thr) else \
+                torch.zeros(n, dtype=torch.int64, device=device)
+        Xb[:, f] = b.to(dtype)
+    return BinnedData(Xb, n_bins, thresholds, list(categorical), B)
+
+
+# ---------------------------------------------------------------- impurity
+
+def _impurity(stats: torch.Tensor, kind: str) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(impurity, weight) of label statistics [..., S]."""
+    if kind == "variance":
+        w = stats[..., 0]
+        safe = w.clamp_min(1e-30)
+        mean = stats[..., 1] / safe
+        imp = (stats[..., 2] / safe - mean * mean).clamp_min(0)
+        return imp, w
+    w = stats.sum(-1)
+    p = stats / w.clamp_min(1e-30).unsqueeze(-1)
+    if kind == "gini":
+        imp = 1.0 - (p * p).sum(-1)
+    else:   # entropy (log base 2, as MLlib)
+        imp = -(p * torch.log2(p.clamp_min(1e-30))).sum(-1)
+    return imp, w
+
+
+@dataclass
+class LevelSplits:
+    feat: torch.Tensor       # [T, N] predictor index or -1 (leaf)
+    bin: torch.Tensor        # [T, N] numeric: last bin going left; -1 categorical
+    cat_left: Optional[torch.Tensor]   # [T, N, B] uint8
+    totals: torch.Tensor     # [T, N, S] label statistics of the node (weighted)
+    gain: torch.Tensor       # [T, N]
+
+
+def _choose_splits(hist: torch.Tensor, feats: torch.Tensor, data: BinnedData, kind: str,
+                   force_leaf: bool) -> LevelSplits:
+    T, N, Fs, B, S = hist.shape
+    dev = hist.device
+    totals = hist[:, :, 0].sum(2)                                   # [T, N, S]
+    parent_imp, w = _impurity(totals, kind)                         # [T, N]
+    if B < 2:
+        none = torch.full((T, N), -1, dtype=torch.int64, device=dev)
+        return LevelSplits(none, none.clone(), None, totals, torch.zeros((T, N), device=dev))
+    cat_flag = torch.tensor(data.categorical, device=dev)[feats]    # [T, N, Fs]
+    h = hist
+    order = None
+    if bool(cat_flag.any()):
+        # categorical bins ordered by label centroid (regression: mean; classification:
+        # share of the node's majority class); empty bins last
+        if kind == "variance":
+            cen = h[..., 1] / h[..., 0].clamp_min(1e-30)
+            empty = h[..., 0] <= 0
+        else:
+            maj = totals.argmax(-1)                                 # [T, N]
+            cnt = h.sum(-1)
+            sel = h.gather(-1, maj[:, :, None, None, None].expand(T, N, Fs, B, 1))[..., 0]
+            cen = sel / cnt.clamp_min(1e-30)
+            empty = cnt <= 0
+        cen = torch.where(empty, torch.full_like(cen, float("inf")), cen)
+        ident = torch.arange(B, device=dev).expand(T, N, Fs, B)
+        order = torch.where(cat_flag[..., None], torch.argsort(cen, dim=-1, stable=True), ident)
+        h = h.gather(3, order[..., None].expand(T, N, Fs, B, S))
+    left = torch.cumsum(h, dim=3)[:, :, :, :-1]                     # split after position k
+    right = totals[:, :, None, None, :] - left
+    imp_l, w_l = _impurity(left, kind)
+    imp_r, w_r = _impurity(right, kind)
+    wt = w[:, :, None, None].clamp_min(1e-30)
+    gain = parent_imp[:, :, None, None] - (w_l * imp_l + w_r * imp_r) / wt
+    valid = (w_l >= 1.0) & (w_r >= 1.0)
+    gain = torch.where(valid, gain, torch.full_like(gain, float("-inf")))
+    flat = gain.reshape(T, N, Fs * (B - 1))
+    best, arg = flat.max(-1)
+    j = arg // (B - 1)
+    k = arg % (B - 1)
+    leaf = (best <= 1e-12) | (w < 2.0) | (parent_imp <= 1e-12) | torch.isinf(best)
+    if force_leaf:
+        leaf = torch.ones_like(leaf)
+    feat = torch.where(leaf, torch.full_like(j, -1), feats.gather(2, j[..., None])[..., 0])
+    is_cat = cat_flag.gather(2, j[..., None])[..., 0] & ~leaf
+    sbin = torch.where(is_cat | leaf, torch.full_like(k, -1), k)
+    cat_left = None
+    if bool(is_cat.any()):
+        # left set = the first k+1 categories in centroid order
+        o = order.gather(2, j[:, :, None, None].expand(T, N, 1, B))[:, :, 0]   # [T, N, B]
+        pos_in_order = torch.empty_like(o)
+        pos_in_order.scatter_(2, o, torch.arange(B, device=dev).expand(T, N, B))
+        cat_left = ((pos_in_order <= k[..., None]) & is_cat[..., None]).to(torch.uint8)
+    return LevelSplits(feat, sbin, cat_left, totals, torch.where(leaf, torch.zeros_like(best),
+                                                                 best))
+
+
+# ---------------------------------------------------------------- histogram / route
+
+def _histogram(data: BinnedData, label, y, S, cls, weight, node_of, lo, nodes, feats, B):
+    T = node_of.shape[0]
+    Fs = feats.shape[2]
+    dev = node_of.device
+    hist = torch.zeros((T, nodes, Fs, B, S), dtype=torch.float32, device=dev)
+    n, P = data.Xb.shape
+    if dev.type == "cuda":
+        lib = native.require_kernels()
+        rc = lib.oryx_rdf_histogram(
+            data.Xb.data_ptr(), data.bin_bytes, n, P,
+            label.data_ptr() if cls else None, None if cls else y.data_ptr(), S, int(cls),
+            weight.data_ptr() if weight is not None else None, T, node_of.data_ptr(), lo,
+            nodes, feats.contiguous().data_ptr(), Fs, B, hist.data_ptr(),
+            native.stream_ptr(dev))
+        native.check(rc, "oryx_rdf_histogram")
+        return hist
+    flat = hist.view(-1)
+    for t in range(T):
+        nd = node_of[t] - lo
+        m = (nd >= 0) & (nd < nodes)
+        if weight is not None:
+            m &= weight[t] > 0
+        rows = torch.nonzero(m).flatten()
+        if rows.numel() == 0:
+            continue
+        nd = nd[rows].long()
+        w = weight[t][rows].float() if weight is not None else torch.ones(rows.numel())
+        fsel = feats[t][nd]                                          # [m, Fs]
+        bins = data.Xb[rows[:, None], fsel].long()                   # [m, Fs]
+        jj = torch.arange(Fs)[None, :]
+        base = ((((t * nodes + nd[:, None]) * Fs + jj) * B + bins) * S)   # [m, Fs]
+        if cls:
+            idx = base + label[rows].long()[:, None]
+            flat.index_add_(0, idx.flatten(), w[:, None].expand(-1, Fs).flatten())
+        else:
+            yy = y[rows].float()
+            for s_, v in enumerate((w, w * yy, w * yy * yy)):
+                flat.index_add_(0, (base + s_).flatten(), v[:, None].expand(-1, Fs).flatten())
+    return hist
+
+
+def _route(data: BinnedData, node_of, nodes, split: LevelSplits, child_base, B):
+    T, n = node_of.shape
+    dev = node_of.device
+    visits = torch.zeros((T, nodes), dtype=torch.int64, device=dev)
+    if dev.type == "cuda":
+        lib = native.require_kernels()
+        # keep every converted operand alive until the launch: a temporary freed mid-call
+        # could be recycled (and overwritten) by the next conversion before the kernel runs
+        cl = split.cat_left.contiguous() if split.cat_left is not None else None
+        sf = split.feat.int().contiguous()
+        sb = split.bin.int().contiguous()
+        cb = child_base.int().contiguous()
+        rc = lib.oryx_rdf_route(data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.shape[1], T,
+                                node_of.data_ptr(), nodes, sf.data_ptr(), sb.data_ptr(),
+                                cl.data_ptr() if cl is not None else None, B, cb.data_ptr(),
+                                visits.data_ptr(), native.stream_ptr(dev))
+        native.check(rc, "oryx_rdf_route")
+        return visits
+    for t in range(T):
+        nd = node_of[t]
+        act = nd >= 0
+        rows = torch.nonzero(act).flatten()
+        ndr = nd[rows].long()
+        visits[t] += torch.bincount(ndr, minlength=nodes)
+        f = split.feat[t][ndr]
+        leafm = f < 0
+        fb = data.Xb[rows, f.clamp_min(0)].long()
+        if split.cat_left is not None:
+            catm = split.bin[t][ndr] < 0
+            go_left_cat = split.cat_left[t][ndr, fb] > 0
+            right = torch.where(catm, ~go_left_cat, fb > split.bin[t][ndr])
+        else:
+            right = fb > split.bin[t][ndr]
+        new = child_base[t][ndr] + right.long()
+        new = torch.where(leafm, torch.full_like(new, -1), new)
+        node_of[t][rows] = new.to(node_of.dtype)
+    return visits
+
+
+# ---------------------------------------------------------------- training
+
+@dataclass
+class TrainedNode:
+    id: str
+    count: int = 0                  # unweighted training examples reaching the node
+    stats: Optional[np.ndarray] = None     # weighted label statistics
+    feature: int = -1               # predictor index, -1 = leaf
+    bin: int = -1
+    cat_left: Optional[np.ndarray] = None  # categorical: encodings going left
+    left: Optional["TrainedNode"] = None
+    right: Optional["TrainedNode"] = None
+
+
+@dataclass
+class TrainedForest:
+    roots: List[TrainedNode]
+    predictor_counts: np.ndarray    # visits of decision nodes, by predictor (importances)
+    classification: bool
+
+
+def _feature_subset_size(P: int, num_trees: int, classification: bool) -> int:
+    if num_trees == 1:
+        return P
+    if classification:
+        return min(P, max(1, int(math.ceil(math.sqrt(P)))))
+    return min(P, max(1, int(math.ceil(P / 3.0))))
+
+
+def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_trees: int,
+                 max_depth: int, impurity: str, seed: int = 0,
+                 ctx: Optional[dist.DistContext] = None,
+                 feature_subset: Optional[int] = None) -> TrainedForest:
+    """``target``: int class encodings (``num_classes`` > 0) or float values (regression)."""
+    classification = num_classes > 0
+    kind = impurity if classification else "variance"
+    if classification and kind not in ("gini", "entropy"):
+        raise ValueError("impurity must be gini or entropy for classification")
+    dev = data.Xb.device
+    n, P = data.Xb.shape
+    T = int(num_trees)
+    B = data.B
+    S = num_classes if classification else 3
+    ctx = ctx or dist.DistContext(device=dev)
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed & ((1 << 62) - 1))
+    label = target.to(dev, torch.int32).contiguous() if classification else None
+    y = None if classification else target.to(dev, torch.float32).contiguous()
+    if T > 1:
+        gd = torch.Generator(device=dev)
+        gd.manual_seed((seed * 31 + ctx.rank + 7) & ((1 << 62) - 1))
+        weight = torch.poisson(torch.ones((T, n), device=dev), generator=gd).clamp_(max=255) \
+            .to(torch.uint8)
+    else:
+        weight = None
+    Fs = feature_subset or _feature_subset_size(P, T, classification)
+    node_of = torch.zeros((T, n), dtype=torch.int32, device=dev)
+    roots = [TrainedNode("r") for _ in range(T)]
+    level_nodes: List[List[Optional[TrainedNode]]] = [[r] for r in roots]
+    predictor_counts = np.zeros(P, dtype=np.float64)
+    nodes = 1
+    for depth in range(max_depth + 1):
+        if Fs < P:
+            feats = torch.argsort(torch.rand((T, nodes, P), generator=g), dim=-1)[..., :Fs]
+        else:
+            feats = torch.arange(P).expand(T, nodes, P)
+        feats = feats.to(torch.int32).to(dev).contiguous()
+        # histogram in node chunks that fit the budget
+        chunk = max(1, _HIST_BUDGET // max(1, T * Fs * B * S))
+        splits = []
+        for lo in range(0, nodes, chunk):
+            hi = min(nodes, lo + chunk)
+            hist = _histogram(data, label, y, S, classification, weight, node_of, lo, hi - lo,
+                              feats[:, lo:hi], B)
+            if ctx.is_distributed:
+                dist.all_reduce_sum(hist, ctx)
+            splits.append(_choose_splits(hist, feats[:, lo:hi], data, kind,
+                                         force_leaf=depth == max_depth))
+        split = LevelSplits(
+            torch.cat([s.feat for s in splits], 1), torch.cat([s.bin for s in splits], 1),
+            None if all(s.cat_left is None for s in splits) else torch.cat(
+                [s.cat_left if s.cat_left is not None else
+                 torch.zeros((T, s.feat.shape[1], B), dtype=torch.uint8, device=dev)
+                 for s in splits], 1),
+            torch.cat([s.totals for s in splits], 1), torch.cat([s.gain for s in splits], 1))
+        is_split = split.feat >= 0
+        rank = torch.cumsum(is_split.int(), 1) - is_split.int()
+        child_base = torch.where(is_split, 2 * rank, torch.full_like(rank, -1))
+        visits = _route(data, node_of, nodes, split, child_base, B)
+        if ctx.is_distributed:
+            dist.all_reduce_sum(visits, ctx)
+        feat_h = split.feat.cpu().numpy()
+        bin_h = split.bin.cpu().numpy()
+        tot_h = split.totals.double().cpu().numpy()
+        vis_h = visits.cpu().numpy()
+        cat_h = split.cat_left.cpu().numpy() if split.cat_left is not None else None
+        next_nodes = 0
+        new_level: List[List[Optional[TrainedNode]]] = []
+        for t in range(T):
+            row: List[Optional[TrainedNode]] = []
+            for slot, node in enumerate(level_nodes[t]):
+                if node is None:
+                    continue
+                node.count = int(vis_h[t, slot])
+                node.stats = tot_h[t, slot]
+                f = int(feat_h[t, slot])
+                if f >= 0:
+                    node.feature = f
+                    node.bin = int(bin_h[t, slot])
+                    if node.bin < 0:
+                        node.cat_left = np.nonzero(cat_h[t, slot])[0]
+                    node.left = TrainedNode(node.id + "-")
+                    node.right = TrainedNode(node.id + "+")
+                    row.extend([node.left, node.right])
+                    predictor_counts[f] += node.count
+            new_level.append(row)
+            next_nodes = max(next_nodes, len(row))
+        level_nodes = new_level
+        nodes = next_nodes
+        if nodes == 0:
+            break
+    return TrainedForest(roots, predictor_counts, classification)
+
+
+# ---------------------------------------------------------------- scoring (flattened)
+
+@dataclass
+class FlatForest:
+    roots: torch.Tensor
+    feat: torch.Tensor
+    thr: torch.Tensor
+    cat_off: torch.Tensor
+    cat_bits: torch.Tensor
+    cat_len: torch.Tensor
+    left: torch.Tensor
+    right: torch.Tensor
+    leaf_value: torch.Tensor         # [nodes, C] probabilities or [nodes, 1] means
+    weights: torch.Tensor
+    nodes: list                      # node objects by flat index (terminal lookups)
+
+
+def flatten_forest(forest, device, num_classes: int) -> FlatForest:
+    """Flatten a :class:`~oryx_amd.models.rdf.tree.DecisionForest` for device scoring."""
+    from ..models.rdf.tree import CategoricalDecision
+    feat, thr, cat_off, cat_len, left, right, vals, objs = [], [], [], [], [], [], [], []
+    bits: List[int] = []
+    roots = []
+    for tree in forest.get_trees():
+        base = len(feat)
+        order = []
+        stack = [tree.get_root()]
+        while stack:
+            nd = stack.pop()
+            order.append(nd)
+            if not nd.is_terminal():
+                stack.append(nd.right)
+                stack.append(nd.left)
+        index = {id(nd): base + i for i, nd in enumerate(order)}
+        roots.append(base)
+        for nd in order:
+            objs.append(nd)
+            if nd.is_terminal():
+                feat.append(-1)
+                thr.append(0.0)
+                cat_off.append(-1)
+                cat_len.append(0)
+                left.append(-1)
+                right.append(-1)
+                p = nd.get_prediction()
+                if num_classes > 0:
+                    vals.append(np.asarray(p.get_category_probabilities(), dtype=np.float64))
+                else:
+                    vals.append(np.array([p.get_prediction()], dtype=np.float64))
+            else:
+                d = nd.decision
+                feat.append(d.get_feature_number())
+                left.append(index[id(nd.left)])
+                right.append(index[id(nd.right)])
+                if isinstance(d, CategoricalDecision):
+                    ln = (max(d.active) + 1) if d.active else 0
+                    cat_off.append(len(bits))
+                    cat_len.append(ln)
+                    bits.extend(1 if e in d.active else 0 for e in range(ln))
+                    thr.append(0.0)
+                else:
+                    cat_off.append(-1)
+                    cat_len.append(0)
+                    thr.append(d.get_threshold())
+                vals.append(np.zeros(max(1, num_classes), dtype=np.float64))
+    width = max(1, num_classes)
+    leaf_value = np.zeros((len(vals), width), dtype=np.float64)
+    for i, v in enumerate(vals):
+        leaf_value[i, :len(v)] = v
+    it = lambda a: torch.tensor(a, dtype=torch.int32, device=device)
+    return FlatForest(it(roots), it(feat), torch.tensor(thr, dtype=torch.float64, device=device),
+                      it(cat_off), torch.tensor(bits + [0], dtype=torch.uint8, device=device),
+                      it(cat_len), it(left), it(right),
+                      torch.from_numpy(leaf_value).to(device),
+                      torch.from_numpy(np.asarray(forest.get_weights(), dtype=np.float64))
+                      .to(device), objs)
+
+
+def forest_leaves(flat: FlatForest, X: torch.Tensor) -> torch.Tensor:
+    """Leaf flat-index [n, T] of every example in every tree (X: float64 [n, F])."""
+    X = X.to(torch.float64).contiguous()
+    n, F = X.shape
+    T = flat.roots.numel()
+    dev = X.device
+    if dev.type == "cuda":
+        lib = native.require_kernels()
+        out = torch.empty((n, T), dtype=torch.int32, device=dev)
+        rc = lib.oryx_rdf_forest_leaf(X.data_ptr(), n, F, T, flat.roots.data_ptr(),
+                                      flat.feat.data_ptr(), flat.thr.data_ptr(),
+                                      flat.cat_off.data_ptr(), flat.cat_bits.data_ptr(),
+                                      flat.cat_len.data_ptr(), flat.left.data_ptr(),
+                                      flat.right.data_ptr(), out.data_ptr(),
+                                      native.stream_ptr(dev))
+        native.check(rc, "oryx_rdf_forest_leaf")
+        return out.long()
+    node = flat.roots.long()[None, :].expand(n, T).clone()
+    rows = torch.arange(n)[:, None].expand(n, T)
+    for _ in range(4096):
+        f = flat.feat.long()[node]
+        active = f >= 0
+        if not bool(active.any()):
+            break
+        x = X[rows, f.clamp_min(0)]
+        co = flat.cat_off.long()[node]
+        enc = x.long()
+        in_range = (enc >= 0) & (enc < flat.cat_len.long()[node])
+        bit = flat.cat_bits.long()[(co + enc.clamp_min(0)).clamp(0, flat.cat_bits.numel() - 1)]
+        pos = torch.where(co >= 0, in_range & (bit > 0), x >= flat.thr[node])
+        nxt = torch.where(pos, flat.right.long()[node], flat.left.long()[node])
+        node = torch.where(active, nxt, node)
+    return node

@@ -1,0 +1,414 @@
+"""RDF app tests: ports of the reference's decision/tree/forest/prediction tests
+(T[app-common]/rdf/**, T[app-common]/classreg/**), the RDF PMML codec tests
+(RDFPMMLUtilsTest), the serving endpoint tests with TestRDF{Regression,Classification}
+ModelFactory golden values (T[serving-app]/rdf/*Test.java), plus trainer/speed checks."""
+
+import json
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oryx_amd.api import Dataset, KeyMessage
+from oryx_amd.models.classreg import (CategoricalFeature, CategoricalPrediction, Example,
+                                      NumericFeature, NumericPrediction, data_to_example,
+                                      vote_on_feature)
+from oryx_amd.models.rdf import pmml as rdf_pmml
+from oryx_amd.models.rdf.batch import RDFUpdate, evaluate_forest, parse_examples
+from oryx_amd.models.rdf.serving import RDFServingModel, RDFServingModelManager
+from oryx_amd.models.rdf.speed import RDFSpeedModelManager
+from oryx_amd.models.rdf.tree import (CategoricalDecision, DecisionForest, DecisionNode,
+                                      DecisionTree, NumericDecision, TerminalNode, TreePath)
+from oryx_amd.models.schema import CategoricalValueEncodings, InputSchema
+from oryx_amd.ops import rdf as rdf_ops
+from oryx_amd.transport.producer import MockTopicProducer
+from oryx_amd.utils import config as cfg
+from oryx_amd.utils import pmml as pm
+
+from .serving_harness import Client
+
+
+def _conf(**kv):
+    return cfg.overlay_on({k.replace("__", "."): v for k, v in kv.items()}, cfg.get_default())
+
+
+def _schema(**kv):
+    return InputSchema(_conf(**kv))
+
+
+# ---------------------------------------------------------------- decisions / trees
+
+def test_numeric_decision():
+    d = NumericDecision(0, -3.1, True)
+    assert not d.is_positive(Example(None, NumericFeature(-3.5)))
+    assert d.is_positive(Example(None, NumericFeature(-3.1)))
+    assert d.is_positive(Example(None, NumericFeature(3.1)))
+    assert d.is_positive(Example(None, [None]))
+    assert repr(NumericDecision(0, 0.5, True)) == "(#0 >= 0.5)"
+    assert NumericDecision(0, 0.5, True) == NumericDecision(0, 0.5, False)
+    assert NumericDecision(0, 0.5, True) != NumericDecision(1, 0.5, True)
+
+
+def test_categorical_decision():
+    d = CategoricalDecision(0, {2, 5}, True)
+    for i in range(10):
+        assert d.is_positive(Example(None, CategoricalFeature.for_encoding(i))) == (i in (2, 5))
+    assert d.is_positive(Example(None, [None]))
+    assert repr(d) == "(#0 ∈ [2,5])"
+
+
+def build_test_tree():
+    rnn = TerminalNode("r--", NumericPrediction(0.0, 1))
+    rnp = TerminalNode("r-+", NumericPrediction(1.0, 1))
+    rn = DecisionNode("r-", NumericDecision(0, -1.0, False), rnn, rnp)
+    rp = TerminalNode("r+", NumericPrediction(2.0, 1))
+    return DecisionTree(DecisionNode("r", NumericDecision(0, 1.0, False), rn, rp))
+
+
+def test_decision_tree():
+    tree = build_test_tree()
+    assert tree.predict(Example(None, NumericFeature(0.5))).get_prediction() == 1.0
+    assert tree.find_terminal(Example(None, NumericFeature(0.5))).get_prediction() \
+        .get_prediction() == 1.0
+    assert tree.find_by_id("r-+").get_prediction().get_prediction() == 1.0
+    s = repr(tree)
+    assert s.startswith("(#0 >= 1.0)") and "(#0 >= -1.0)" in s
+    forest = DecisionForest([build_test_tree(), build_test_tree()], [1.0, 2.0], None)
+    assert forest.predict(Example(None, NumericFeature(0.5))).get_prediction() == 1.0
+    assert repr(forest).startswith("(#0 >= 1.0)")
+
+
+def test_tree_path():
+    lrl = TreePath.EMPTY.extend_left().extend_right().extend_left()
+    lrr = TreePath.EMPTY.extend_left().extend_right().extend_right()
+    lr = TreePath.EMPTY.extend_left().extend_right()
+    r = TreePath.EMPTY.extend_right()
+    assert repr(lrl) == "010" and repr(lrr) == "011" and repr(TreePath.EMPTY) == ""
+    assert lrl == TreePath.EMPTY.extend_left().extend_right().extend_left()
+    assert sorted([lrl, r, lr, lrr]) == [lrl, lr, lrr, r]
+
+
+def test_predictions_and_vote():
+    v = vote_on_feature([NumericPrediction(1.0, 1), NumericPrediction(3.0, 2),
+                         NumericPrediction(6.0, 3)], [1.0, 1.0, 1.0])
+    assert v.get_prediction() == pytest.approx(10.0 / 3.0)
+    c = vote_on_feature([CategoricalPrediction([1, 2, 3]), CategoricalPrediction([10, 30, 50])],
+                        [1.0, 2.0])
+    np.testing.assert_allclose(c.get_category_probabilities(),
+                               [(1 / 6 + 2 * 10 / 90) / 3, (2 / 6 + 2 * 30 / 90) / 3,
+                                (3 / 6 + 2 * 50 / 90) / 3])
+    p = CategoricalPrediction([1, 2, 3])
+    assert p.get_most_probable_category_encoding() == 2 and p.get_count() == 6
+    p.update(0, 10)
+    assert p.get_most_probable_category_encoding() == 0 and p.get_count() == 16
+    n = NumericPrediction(1.0, 1)
+    n.update(3.0, 3)
+    assert n.get_prediction() == 2.5 and n.get_count() == 4
+
+
+def test_data_to_example():
+    s = _schema(**{"oryx__input-schema__feature-names": '["a","b","c"]',
+                   "oryx__input-schema__categorical-features": '["a","c"]',
+                   "oryx__input-schema__target-feature": "c"})
+    enc = CategoricalValueEncodings({0: ["x", "y"], 2: ["p", "q"]})
+    e = data_to_example(["y", "1.5", "q"], s, enc)
+    assert e.get_feature(0) == CategoricalFeature.for_encoding(1)
+    assert e.get_feature(1) == NumericFeature(1.5)
+    assert e.get_feature(2) is None and e.get_target() == CategoricalFeature.for_encoding(1)
+    assert data_to_example(["x", "2", ""], s, enc).get_target() is None
+
+
+# ---------------------------------------------------------------- PMML codec
+
+def _dummy_classification_pmml(num_trees=1):
+    s = _schema(**{"oryx__input-schema__feature-names": '["color","fruit"]',
+                   "oryx__input-schema__numeric-features": "[]",
+                   "oryx__input-schema__target-feature": "fruit"})
+    enc = CategoricalValueEncodings({0: ["yellow", "red"], 1: ["banana", "apple"]})
+    roots = []
+    for _ in range(num_trees):
+        root = rdf_pmml.TreeSpecNode("r", 2.0)
+        root.feature = 0
+        root.left_categories = [1]           # red goes left -> "isNotIn red" on the right
+        root.left = rdf_pmml.TreeSpecNode("r-", 1.0)
+        root.left.class_counts = np.array([0.0, 1.0])
+        root.right = rdf_pmml.TreeSpecNode("r+", 1.0)
+        root.right.class_counts = np.array([1.0, 0.0])
+        roots.append(root)
+    return s, enc, rdf_pmml.forest_to_pmml(roots, s, enc, [0.5], 3, 10, "gini")
+
+
+def test_pmml_classification_round_trip():
+    s, enc, doc = _dummy_classification_pmml()
+    doc = pm.from_string(pm.to_string(doc))
+    rdf_pmml.validate_pmml_vs_schema(doc, s)
+    forest, enc2 = rdf_pmml.read(doc)
+    assert len(forest.get_trees()) == 1 and forest.get_weights().tolist() == [1.0]
+    assert forest.get_feature_importances().tolist() == [0.5, 0.0]
+    assert enc2.get_value_count(0) == 2 and enc2.get_value_count(1) == 2
+    root = forest.get_trees()[0].get_root()
+    assert isinstance(root.decision, CategoricalDecision) and root.decision.active == {0}
+    red = Example(None, CategoricalFeature.for_encoding(1), None)
+    assert forest.predict(red).get_most_probable_category_encoding() == 1   # apple
+    assert doc.get_extension_value("impurity") == "gini"
+    s3, enc3, doc3 = _dummy_classification_pmml(3)
+    assert len(rdf_pmml.read(doc3)[0].get_trees()) == 3
+
+
+def test_pmml_regression_greater_than_ulp():
+    s = _schema(**{"oryx__input-schema__feature-names": '["foo","bar"]',
+                   "oryx__input-schema__categorical-features": "[]",
+                   "oryx__input-schema__target-feature": "bar"})
+    enc = CategoricalValueEncodings({})
+    root = rdf_pmml.TreeSpecNode("r", 2.0)
+    root.feature, root.threshold = 0, 3.14
+    root.left = rdf_pmml.TreeSpecNode("r-", 1.0)
+    root.left.mean = -2.0
+    root.right = rdf_pmml.TreeSpecNode("r+", 1.0)
+    root.right.mean = 2.0
+    doc = rdf_pmml.forest_to_pmml([root], s, enc, [1.0], 1, 2, "variance")
+    rdf_pmml.validate_pmml_vs_schema(doc, s)
+    forest, enc2 = rdf_pmml.read(doc)
+    assert enc2.get_category_counts() == {}
+    d = forest.get_trees()[0].get_root().decision
+    assert d.get_threshold() == 3.14 + math.ulp(3.14)
+    assert forest.predict(Example(None, NumericFeature(3.14), None)).get_prediction() == -2.0
+    assert forest.predict(Example(None, NumericFeature(3.15), None)).get_prediction() == 2.0
+    bad = _schema(**{"oryx__input-schema__feature-names": '["foo","bar"]',
+                     "oryx__input-schema__numeric-features": "[]",
+                     "oryx__input-schema__target-feature": "bar"})
+    with pytest.raises(ValueError):
+        rdf_pmml.validate_pmml_vs_schema(doc, bad)
+
+
+# ---------------------------------------------------------------- serving (golden values)
+
+def _forest(preds1, preds2):
+    enc_left = CategoricalDecision(0, {1}, True)
+    t1 = DecisionTree(DecisionNode("r", enc_left, TerminalNode("r-", preds1[0]),
+                                   TerminalNode("r+", preds1[1])))
+    t2 = DecisionTree(DecisionNode("r", NumericDecision(1, -3.0, False),
+                                   TerminalNode("r-", preds2[0]), TerminalNode("r+", preds2[1])))
+    return DecisionForest([t1, t2], [1.0, 2.0], [0.1, 0.3])
+
+
+def regression_model():
+    forest = _forest([NumericPrediction(1.0, 1), NumericPrediction(10.0, 1)],
+                     [NumericPrediction(100.0, 1), NumericPrediction(1000.0, 1)])
+    enc = CategoricalValueEncodings({0: ["A", "B", "C"]})
+    s = _schema(**{"oryx__input-schema__num-features": 3,
+                   "oryx__input-schema__categorical-features": '["0"]',
+                   "oryx__input-schema__target-feature": '"2"'})
+    return RDFServingModel(forest, enc, s)
+
+
+def classification_model():
+    forest = _forest([CategoricalPrediction([1, 2, 3]), CategoricalPrediction([10, 30, 50])],
+                     [CategoricalPrediction([100, 400, 900]),
+                      CategoricalPrediction([1000, 10000, 100000])])
+    enc = CategoricalValueEncodings({0: ["A", "B", "C"], 2: ["X", "Y", "Z"]})
+    s = _schema(**{"oryx__input-schema__num-features": 3,
+                   "oryx__input-schema__categorical-features": '["0","2"]',
+                   "oryx__input-schema__target-feature": '"2"'})
+    return RDFServingModel(forest, enc, s)
+
+
+def _client(model, read_only=False):
+    return Client(["oryx_amd.models.rdf.resources"], model, read_only=read_only)
+
+
+def test_serving_predict():
+    c = _client(regression_model())
+    assert float(c.get_text("/predict/B,0,")) == pytest.approx((10.0 + 2 * 1000.0) / 3)
+    assert float(c.get_text("/predict/A,-5,")) == pytest.approx((1.0 + 2.0 * 100.0) / 3.0)
+    r = c.request("POST", "/predict", body="A,-5,\nB,0,")
+    assert r.body.decode() == "67.0\n670.0\n"
+    assert c.status("GET", "/predict/B,0") == 400
+
+
+def test_serving_classification_distribution():
+    c = _client(classification_model())
+    recs = c.get_json("/classificationDistribution/B,0,")
+    assert [r["id"] for r in recs] == ["X", "Y", "Z"]
+    assert recs[0]["value"] == pytest.approx((10.0 / 90.0 + 2 * (1000.0 / 111000.0)) / 3)
+    assert recs[2]["value"] == pytest.approx((50.0 / 90.0 + 2 * (100000.0 / 111000.0)) / 3)
+    recs = c.get_json("/classificationDistribution/A,-5,")
+    assert recs[1]["value"] == pytest.approx((2.0 / 6.0 + 2 * (400.0 / 1400.0)) / 3)
+    assert c.get_text("/predict/A,-5,").strip() == "Z"
+
+
+def test_serving_feature_importance_and_train():
+    c = _client(regression_model())
+    assert c.get_json("/feature/importance") == [0.1, 0.3]
+    assert float(c.get_text("/feature/importance/1")) == 0.3
+    assert c.status("GET", "/feature/importance/5") == 400
+    data = "B,0,20\nB,-4,30\nA,0,40\nA,-4,50"
+    assert c.status("POST", "/train", body=data) == 204
+    assert [m for _, m in MockTopicProducer.get_key_messages()] == data.split("\n")
+    assert _client(regression_model(), read_only=True).status("POST", "/train",
+                                                              body=data) == 403
+
+
+def test_serving_manager_updates():
+    s, enc, doc = _dummy_classification_pmml()
+    conf = _conf(**{"oryx__input-schema__feature-names": '["color","fruit"]',
+                    "oryx__input-schema__numeric-features": "[]",
+                    "oryx__input-schema__target-feature": "fruit"})
+    mgr = RDFServingModelManager(conf)
+    mgr.consume(iter([KeyMessage("MODEL", pm.to_string(doc)),
+                      KeyMessage("UP", '[0,"r+",{"1":5}]')]))
+    leaf = mgr.get_model().get_forest().get_trees()[0].find_by_id("r+")
+    assert leaf.get_prediction().get_category_counts().tolist() == [1.0, 5.0]
+    assert mgr.get_model().predict(["yellow", ""]) == "apple"
+
+
+# ---------------------------------------------------------------- training
+
+def _numeric_data(n=3000, seed=0):
+    g = np.random.default_rng(seed)
+    X = g.uniform(-1, 1, (n, 4))
+    y = np.where(X[:, 0] + 0.5 * X[:, 1] > 0.2, 1, 0)
+    return X, y
+
+
+def test_train_single_tree_classification_cpu():
+    X, y = _numeric_data()
+    data = rdf_ops.bin_features(X, [False] * 4, [0] * 4, 32, torch.device("cpu"))
+    f = rdf_ops.train_forest(data, torch.from_numpy(y), 2, 1, 6, "gini", seed=1)
+    root = f.roots[0]
+    assert root.feature in (0, 1) and root.count == len(y)
+    # counts are consistent: children sum to parent
+    stack = [root]
+    while stack:
+        nd = stack.pop()
+        if nd.feature >= 0:
+            assert nd.left.count + nd.right.count == nd.count
+            stack += [nd.left, nd.right]
+    assert f.predictor_counts[0] > 0
+
+
+def _rdf_conf(classification=True, trees=5):
+    kv = {"oryx__input-schema__feature-names": '["a","b","c","d","t"]',
+          "oryx__input-schema__target-feature": "t",
+          "oryx__rdf__num-trees": trees,
+          "oryx__rdf__hyperparams__max-depth": 6,
+          "oryx__rdf__hyperparams__max-split-candidates": 32,
+          "oryx__ml__eval__test-fraction": 0.2,
+          "oryx__ml__eval__candidates": 1}
+    if classification:
+        kv["oryx__input-schema__categorical-features"] = '["d","t"]'
+        kv["oryx__rdf__hyperparams__impurity"] = "entropy"
+    else:
+        kv["oryx__input-schema__categorical-features"] = '["d"]'
+        kv["oryx__rdf__hyperparams__impurity"] = "variance"
+    return _conf(**kv)
+
+
+def _lines(n, classification, seed=3):
+    g = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        a, b, c = (float(v) for v in g.uniform(-1, 1, 3))
+        d = str(g.choice(["red", "green", "blue"]))
+        if classification:
+            t = "yes" if (a > 0.1) ^ (d == "blue") else "no"
+        else:
+            t = repr(round(3 * a - 2 * b + (4.0 if d == "red" else 0.0), 4))
+        out.append("%r,%r,%r,%s,%s" % (a, b, c, d, t))
+    return out
+
+
+@pytest.mark.parametrize("classification", [True, False])
+def test_rdf_update_end_to_end(classification, tmp_path):
+    conf = _rdf_conf(classification)
+    upd = RDFUpdate(conf)
+    lines = _lines(2500, classification)
+    MockTopicProducer.clear()
+    upd.run_update(None, 1, Dataset([(None, l) for l in lines]), None,
+                   str(tmp_path / "model"), MockTopicProducer())
+    (k, m), = MockTopicProducer.get_key_messages()
+    assert k == "MODEL"
+    doc = pm.from_string(m)
+    schema = InputSchema(conf)
+    rdf_pmml.validate_pmml_vs_schema(doc, schema)
+    forest, enc = rdf_pmml.read(doc)
+    assert len(forest.get_trees()) == 5
+    assert doc.models()[0].tag == pm.q("MiningModel")
+    imp = forest.get_feature_importances()
+    assert imp[4] == 0.0 and abs(imp.sum() - 1.0) < 1e-9
+    test = _lines(500, classification, seed=9)
+    rows = [l.split(",") for l in test]
+    _, target, full = parse_examples(rows, schema, enc)
+    ev = evaluate_forest(forest, enc, schema, full, target, torch.device("cpu"))
+    if classification:
+        assert ev > 0.9
+    else:
+        assert ev < 1.0
+    # host tree walk agrees with the flattened device-style walk
+    from oryx_amd.models.classreg import data_to_example
+    preds = [forest.predict(data_to_example(r, schema, enc)) for r in rows[:50]]
+    flat = rdf_ops.flatten_forest(forest, torch.device("cpu"),
+                                  enc.get_value_count(4) if classification else 0)
+    leaves = rdf_ops.forest_leaves(flat, torch.from_numpy(full[:50]))
+    for e in range(50):
+        for t in range(5):
+            assert flat.nodes[int(leaves[e, t])] is forest.get_trees()[t].find_terminal(
+                data_to_example(rows[e], schema, enc))
+
+
+def test_speed_manager_leaf_updates():
+    conf = _rdf_conf(False, trees=2)
+    upd = RDFUpdate(conf)
+    MockTopicProducer.clear()
+    upd.run_update(None, 1, Dataset([(None, l) for l in _lines(800, False)]), None, "/tmp/rdfm",
+                   MockTopicProducer())
+    (k, m), = MockTopicProducer.get_key_messages()
+    mgr = RDFSpeedModelManager(conf)
+    mgr.consume(iter([KeyMessage(k, m)]))
+    ups = [json.loads(u) for u in mgr.build_updates(Dataset([(None, l)
+                                                             for l in _lines(20, False, 5)]))]
+    assert ups and all(len(u) == 4 for u in ups)
+    assert sum(u[3] for u in ups if u[0] == 0) == 20
+    serving = RDFServingModelManager(conf)
+    serving.consume(iter([KeyMessage(k, m)] + [KeyMessage("UP", json.dumps(u)) for u in ups]))
+
+
+# ---------------------------------------------------------------- GPU kernels
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("classification", [True, False])
+def test_gpu_training_matches_cpu(cuda, classification):
+    X, y = _numeric_data(20000, seed=4)
+    yr = X[:, 0] * 2 - X[:, 2]
+    res = {}
+    for dev in (torch.device("cpu"), cuda):
+        data = rdf_ops.bin_features(X, [False] * 4, [0] * 4, 32, dev, seed=2)
+        tgt = torch.from_numpy(y if classification else yr)
+        f = rdf_ops.train_forest(data, tgt, 2 if classification else 0, 1, 5,
+                                 "gini" if classification else "variance", seed=3)
+        res[dev.type] = f
+    # single tree, no bootstrap, all features: identical structure (up to fp32 ties)
+    a, b = res["cpu"].roots[0], res["cuda"].roots[0]
+    assert (a.feature, a.bin, a.count) == (b.feature, b.bin, b.count)
+    assert (a.left.feature, a.left.bin) == (b.left.feature, b.left.bin)
+    np.testing.assert_allclose(res["cpu"].predictor_counts, res["cuda"].predictor_counts)
+
+
+@pytest.mark.gpu
+def test_gpu_forest_leaves_match_cpu(cuda):
+    conf = _rdf_conf(True, trees=4)
+    upd = RDFUpdate(conf)
+    MockTopicProducer.clear()
+    upd.run_update(None, 1, Dataset([(None, l) for l in _lines(3000, True)]), None, "/tmp/rdfg",
+                   MockTopicProducer())
+    (k, m), = MockTopicProducer.get_key_messages()
+    forest, enc = rdf_pmml.read(pm.from_string(m))
+    schema = InputSchema(conf)
+    rows = [l.split(",") for l in _lines(1000, True, seed=11)]
+    _, target, full = parse_examples(rows, schema, enc)
+    flat_c = rdf_ops.flatten_forest(forest, torch.device("cpu"), 2)
+    flat_g = rdf_ops.flatten_forest(forest, cuda, 2)
+    lc = rdf_ops.forest_leaves(flat_c, torch.from_numpy(full))
+    lg = rdf_ops.forest_leaves(flat_g, torch.from_numpy(full).to(cuda)).cpu()
+    assert torch.equal(lc, lg)
