@@ -27,7 +27,8 @@ from typing import List, Optional, Tuple
 from ..api import BatchLayerUpdate, Dataset
 from ..transport.producer import LogTopicProducer
 from ..utils import config as cfg
-from ..utils import ioutils, lang
+from ..parallel import dist
+from ..utils import ioutils, lang, rng
 from .common import AbstractLayer, IntervalTimer, drain
 
 __all__ = ["BatchLayer", "save_interval_data", "read_past_data", "delete_old_data"]
@@ -98,6 +99,8 @@ class BatchLayer(AbstractLayer):
         self.update_class = cfg.get_optional_string(config, "oryx.batch.update-class")
         self._update = update
         self._timer: Optional[IntervalTimer] = None
+        self._context = None
+        self._released = False
         self.intervals_run = 0
 
     def load_update_instance(self) -> BatchLayerUpdate:
@@ -128,6 +131,12 @@ class BatchLayer(AbstractLayer):
             self.build_input_consumer()
         ts = int(time.time() * 1000) if timestamp is None else timestamp
         records = drain(self._input_consumer)
+        dctx = self._context.dist if self._context is not None else None
+        seed = rng.next_seed()
+        if dctx is not None and dctx.is_distributed:
+            # announce the generation to the follower ranks (they join the collectives)
+            dist.broadcast_object({"ts": ts, "records": records, "seed": seed}, dctx,
+                                  control=True)
         if records:
             log.info("Beginning update at %d with %d new records", ts, len(records))
             new_data = Dataset(records)
@@ -137,8 +146,10 @@ class BatchLayer(AbstractLayer):
                 producer = LogTopicProducer(self.update_broker, self.update_topic, self.config,
                                             async_=False, max_message=self.max_message)
             try:
-                self._update.run_update(self._context, ts, new_data,
-                                        past if len(past) else None, self.model_dir, producer)
+                with rng.shared_seed_scope(seed):
+                    self._update.run_update(self._context, ts, new_data,
+                                            past if len(past) else None, self.model_dir,
+                                            producer)
             finally:
                 if producer is not None:
                     producer.close()
@@ -151,6 +162,26 @@ class BatchLayer(AbstractLayer):
                             pattern=re.compile(r"^(\d+)$"))
         self.intervals_run += 1
 
+    def run_follower(self) -> int:
+        """Non-zero ranks of a multi-GPU batch layer: wait for rank 0's announcements and run
+        the same update (reading past data from the shared data dir) so every collective in
+        the trainers has all participants.  Returns the number of generations joined."""
+        self._update = self.load_update_instance()
+        self._context = self.layer_context()
+        dctx = self._context.dist
+        joined = 0
+        while True:
+            msg = dist.broadcast_object(None, dctx, control=True)
+            if msg is None:
+                return joined
+            if not msg["records"]:
+                continue
+            past = read_past_data(self.data_dir)
+            with rng.shared_seed_scope(msg["seed"]):
+                self._update.run_update(self._context, msg["ts"], Dataset(msg["records"]),
+                                        past if len(past) else None, self.model_dir, None)
+            joined += 1
+
     def await_termination(self, timeout: Optional[float] = None) -> None:
         t0 = time.time()
         while self._timer is not None and self._timer.is_alive():
@@ -162,6 +193,10 @@ class BatchLayer(AbstractLayer):
         if self._timer is not None:
             self._timer.stop()
             self._timer = None
+        dctx = self._context.dist if getattr(self, "_context", None) is not None else None
+        if dctx is not None and dctx.is_distributed and dctx.is_main and not self._released:
+            self._released = True
+            dist.broadcast_object(None, dctx, control=True)     # release the followers
         self.close_input()
 
     def __enter__(self):

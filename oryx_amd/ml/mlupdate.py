@@ -25,6 +25,7 @@ import time
 from typing import Any, List, Optional, Sequence, Tuple
 
 from ..api import BatchLayerUpdate, Dataset, TopicProducer
+from ..parallel import dist
 from ..utils import ioutils, lang, pmml as pmmlu, rng
 from . import hyperparams as hp
 
@@ -95,6 +96,17 @@ class MLUpdate(BatchLayerUpdate):
         values = self.get_hyper_parameter_values()
         per_param = hp.choose_values_per_hyper_param(len(values), self.candidates)
         combos = hp.choose_hyper_parameter_combos(values, self.candidates, per_param)
+        dctx = self._dist_ctx(context)
+        # multi-rank: every candidate runs in its own shared-seed scope so all ranks make the
+        # same splits whatever rank 0 does in between (evaluation, publishing)
+        self._candidate_seed_base = rng.next_seed() if dctx.is_distributed else None
+        if dctx.is_distributed and not dctx.is_main:
+            for i in range(self.candidates):
+                with rng.shared_seed_scope(self._candidate_seed_base + i):
+                    train, _ = self._split_train_test(new_msgs, past_msgs)
+                    if train:
+                        self.build_model(context, train, combos[i % len(combos)], None)
+            return
 
         model_dir_local = ioutils.to_local_path(model_dir)
         candidates_path = os.path.join(model_dir_local, ".temporary",
@@ -128,13 +140,20 @@ class MLUpdate(BatchLayerUpdate):
             self.publish_additional_model_data(context, best_model, new_msgs, past_msgs,
                                                final_path, model_update_topic)
 
+    @staticmethod
+    def _dist_ctx(context):
+        c = context if isinstance(context, dist.DistContext) else getattr(context, "dist", None)
+        return c if c is not None else dist.get_context()
+
     def _find_best_candidate_path(self, context, new_msgs, past_msgs, combos,
                                   candidates_path) -> Optional[str]:
+        # collective-using trainers must not interleave across candidates on multiple ranks
+        par = 1 if self._dist_ctx(context).is_distributed else \
+            min(self.eval_parallelism, self.candidates)
         results = lang.collect_in_parallel(
             self.candidates,
             lambda i: self._build_and_eval(i, combos, context, new_msgs, past_msgs,
-                                           candidates_path),
-            min(self.eval_parallelism, self.candidates))
+                                           candidates_path), par)
         best_path, best_eval = None, float("-inf")
         for path, ev in results:
             if path is None or not os.path.exists(path):
@@ -148,6 +167,15 @@ class MLUpdate(BatchLayerUpdate):
         return best_path
 
     def _build_and_eval(self, i, combos, context, new_msgs, past_msgs, candidates_path):
+        base = getattr(self, "_candidate_seed_base", None)
+        if base is not None:
+            with rng.shared_seed_scope(base + i):
+                return self._build_and_eval_inner(i, combos, context, new_msgs, past_msgs,
+                                                  candidates_path)
+        return self._build_and_eval_inner(i, combos, context, new_msgs, past_msgs,
+                                          candidates_path)
+
+    def _build_and_eval_inner(self, i, combos, context, new_msgs, past_msgs, candidates_path):
         params = combos[i % len(combos)]
         candidate_path = os.path.join(candidates_path, str(i))
         log.info("Building candidate %d with params %s", i, params)

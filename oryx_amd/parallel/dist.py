@@ -34,6 +34,7 @@ class DistContext:
     device: torch.device = torch.device("cpu")
     backend: Optional[str] = None
     group: Optional[object] = None
+    control: Optional[object] = None
 
     @property
     def is_distributed(self) -> bool:
@@ -81,6 +82,10 @@ def init_from_env(device: Optional[str] = None, backend: Optional[str] = None,
                 kwargs["device_id"] = dev
             tdist.init_process_group(**kwargs)
         ctx.backend = backend
+        # control plane: a gloo group with a long timeout for the batch layer's per-interval
+        # work announcements (rank 0 may wait hours between generations)
+        ctx.control = tdist.new_group(backend="gloo",
+                                      timeout=datetime.timedelta(days=30))
     _context = ctx
     return ctx
 
@@ -135,11 +140,16 @@ def all_reduce_sum(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:
     return t
 
 
-def broadcast_object(obj, ctx: DistContext, src: int = 0):
+def broadcast_object(obj, ctx: DistContext, src: int = 0, control: bool = False):
+    """Broadcast a picklable object from ``src``; ``control=True`` uses the long-timeout gloo
+    control group (host-side announcements) instead of the default group."""
     if not ctx.is_distributed:
         return obj
     lst = [obj]
-    tdist.broadcast_object_list(lst, src=src)
+    if control and ctx.control is not None:
+        tdist.broadcast_object_list(lst, src=src, group=ctx.control)
+    else:
+        tdist.broadcast_object_list(lst, src=src)
     return lst[0]
 
 

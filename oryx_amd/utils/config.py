@@ -236,7 +236,13 @@ def _overlay_value(v) -> str:
         return "[" + ",".join(_overlay_value(x) for x in v) + "]"
     if isinstance(v, dict):
         return hocon.render(v, concise=True)
-    return str(v)
+    s = str(v)
+    # plain strings with characters HOCON forbids unquoted (e.g. "log:/tmp/x") are quoted
+    # for convenience; HOCON syntax the caller wrote on purpose ([..], {..}, "..") is kept
+    if isinstance(v, str) and s and s[0] not in '[{"' and \
+            any(ch in s for ch in ':=,#`^?!@*&\\'):
+        return '"' + s.replace("\\", "\\\\").replace('"', '\\"') + '"'
+    return s
 
 
 def overlay_on(overlay: Mapping[str, Any], underlying: Config) -> Config:

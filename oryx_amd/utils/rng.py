@@ -17,7 +17,7 @@ from typing import Optional
 import numpy as np
 
 __all__ = ["get_random", "get_random_seeded", "use_test_seed", "is_test_seed", "test_seed",
-           "torch_generator", "next_seed"]
+           "torch_generator", "next_seed", "shared_seed_scope"]
 
 
 def _parse_seed() -> int:
@@ -74,7 +74,32 @@ class RandomGenerator:
         return self._gen
 
 
+_scope = threading.local()
+
+
+class shared_seed_scope:
+    """Within the scope, the i-th :func:`get_random` call returns a generator seeded with
+    ``hash(seed, i)`` -- so ranks that execute the same code path under the same broadcast seed
+    draw identical random streams (identical train/test splits, hyperparameter combos, ...)."""
+
+    def __init__(self, seed: int):
+        self.seed = int(seed) & ((1 << 62) - 1)
+
+    def __enter__(self):
+        self._prev = getattr(_scope, "state", None)
+        _scope.state = [self.seed, 0]
+        return self
+
+    def __exit__(self, *exc):
+        _scope.state = self._prev
+        return False
+
+
 def get_random() -> RandomGenerator:
+    st = getattr(_scope, "state", None)
+    if st is not None:
+        st[1] += 1
+        return RandomGenerator((st[0] * 1000003 + st[1]) & ((1 << 64) - 1))
     if _use_test_seed:
         return RandomGenerator(_TEST_SEED)
     r = RandomGenerator()
