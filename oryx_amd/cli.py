@@ -37,10 +37,11 @@ log = logging.getLogger("oryx_amd.cli")
 _ALIASES = {"kafka-setup": "log-setup", "kafka-tail": "log-tail", "kafka-input": "log-input"}
 
 
-def _load_config(path: Optional[str]):
+def _load_config(path: Optional[str], set_env: bool = True):
     from .utils import config as cfg
     if path:
-        os.environ["ORYX_CONFIG_FILE"] = os.path.abspath(path)
+        if set_env:     # so that code calling cfg.get_default() in this process sees it too
+            os.environ["ORYX_CONFIG_FILE"] = os.path.abspath(path)
         return cfg.load_file(path)
     return cfg.get_default()
 

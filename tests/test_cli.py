@@ -20,7 +20,7 @@ def _conf_file(tmp_path):
 
 
 def test_log_setup_input_tail(tmp_path):
-    conf = cli._load_config(_conf_file(tmp_path))
+    conf = cli._load_config(_conf_file(tmp_path), set_env=False)
     out = io.StringIO()
     cli.cmd_log_setup(conf, out)
     assert "Created topic OryxInput" in out.getvalue()
@@ -37,7 +37,7 @@ def test_log_setup_input_tail(tmp_path):
 
 
 def test_config_props_redacts(tmp_path):
-    conf = cli._load_config(_conf_file(tmp_path))
+    conf = cli._load_config(_conf_file(tmp_path), set_env=False)
     out = io.StringIO()
     cli.cmd_config_props(conf, out)
     text = out.getvalue()
