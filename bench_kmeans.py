@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""k-means batch-layer benchmark on MI355X (BASELINE.json config "k-means k=1000 d=256 on
+100M points, 8xMI355X (MFMA distance + centroid all-reduce)").
+
+``python bench_kmeans.py --gpus N --steps K --warmup W`` (N > 1: one rank per GPU under
+``torch.distributed.run``).  A *step* is one Lloyd iteration of the batch layer's k-means
+trainer (``oryx_amd.ops.kmeans.lloyd_step``, the loop MLlib runs for the reference at
+``[mllib]/kmeans/KMeansUpdate.java:116-117``): the fused bf16-MFMA distance + argmin kernel
+over every point against all K centers, the fp32 centroid accumulation kernel, ONE RCCL
+all-reduce of the K x (d + 1) sums/counts, and the center move.
+
+Weak scaling: every rank owns 100M / 8 = 12.5M points (the 8-GPU config's per-GPU share), so
+N = 8 is exactly the BASELINE config.  Data: a synthetic Gaussian mixture (1000 true centers,
+d = 256, fp32 resident in HBM); centers start from a random sample (initialisation is not
+part of the step).  The reference publishes no batch-layer numbers, so
+``vs_baseline`` is null.  Prints ONE JSON line (rank 0): ``value`` = points processed per
+second over all ranks; ``tflops`` = the distance-GEMM work rate (2 * n * K * d per point set).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--points-per-gpu", type=int, default=12_500_000)
+    ap.add_argument("--dim", type=int, default=256)
+    ap.add_argument("--k", type=int, default=1000)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--device", default="auto")
+    args = ap.parse_args(argv)
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oryx_amd.parallel import dist
+    from oryx_amd.ops import kmeans as km
+
+    ctx = dist.init_from_env(device=args.device)
+    dev = ctx.device
+    W = ctx.world_size
+    n, d, k = args.points_per_gpu, args.dim, args.k
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed)            # the same true centers on every rank
+    true_c = torch.randn((k, d), generator=g, device=dev) * 4.0
+    g.manual_seed(args.seed * 7919 + ctx.rank + 1)
+    x = torch.empty((n, d), dtype=torch.float32, device=dev)
+    chunk = 1 << 20
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        lab = torch.randint(0, k, (hi - lo,), generator=g, device=dev)
+        x[lo:hi] = true_c[lab] + torch.randn((hi - lo, d), generator=g, device=dev)
+    pts = km.PointSet(x)
+    # initial centers: a random sample of rank 0's points, broadcast
+    idx = torch.randperm(n, generator=g, device=dev)[:k]
+    centers = x[idx].clone()
+    if ctx.is_distributed:
+        torch.distributed.broadcast(centers, src=0)
+    ws = None
+    if pts.xb is not None:
+        ws = (torch.empty(n, dtype=torch.int32, device=dev),
+              torch.empty(n, dtype=torch.float32, device=dev))
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        dist.barrier(ctx)
+
+    empties = 0
+    for _ in range(args.warmup):
+        centers, counts, _, ne = km.lloyd_step(pts, centers, ctx, ws)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        centers, counts, _, ne = km.lloyd_step(pts, centers, ctx, ws)
+        empties += ne
+    sync()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if ctx.is_distributed:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t.item())
+    total_points = n * W * args.steps
+    ms = elapsed / args.steps * 1e3
+    total_counts = int(counts.sum().item())
+    if ctx.is_main:
+        print(json.dumps({
+            "metric": "k-means Lloyd-iteration points/sec (batch layer), 1/2/4/8 MI355X",
+            "value": total_points / elapsed, "unit": "points/s", "n_gpus": W,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 (MFMA distances, fp32 accumulate/sums)",
+            "data": "synthetic Gaussian mixture (1000 true centers), random-sample init",
+            "config": {"model": "k-means k=%d d=%d" % (k, d), "global_batch": n * W,
+                       "seq_len": None, "parallelism": "dp%d (point shards, RCCL all-reduce "
+                       "of K x (d+1) sums/counts)" % W, "points_per_gpu": n,
+                       "step": "1 Lloyd iteration (assign + accumulate + all-reduce + move)"},
+            "tflops": 2.0 * n * W * k * d / (ms * 1e-3) / 1e12,
+            "counted_points": total_counts, "empty_clusters_seen": empties,
+        }), flush=True)
+    if ctx.is_distributed:
+        torch.distributed.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -9,10 +9,12 @@
 // row-major [n][P]); every (tree, row) pair whose node is still open adds its bootstrap weight
 // times the label statistics (class one-hot for classification; w, w*y, w*y^2 for regression)
 // into hist[t][node][j][bin][s] for the node's sampled features j.  When one tree's level
-// histogram fits in LDS the workgroup accumulates privately (ds_add_f32) and flushes non-zero
-// bins with one global atomic each -- the root levels, where every row of a tree hits the same
-// few thousand bins, would otherwise serialise on L2 atomics.  Deeper levels (many nodes, low
-// contention) go straight to global fp32 atomics.
+// histogram of a chunk of nodes fits in LDS (<= 128 KB) the workgroup accumulates privately
+// (ds_add_f32) and flushes non-zero bins with one global atomic each -- the root levels, where
+// every row of a tree hits the same few thousand bins, would otherwise serialise on L2 atomics,
+// and deep levels would issue one L2 atomic per (row, feature).  Levels wider than one chunk
+// run one block column per node chunk.  Only a node whose own histogram exceeds the budget
+// goes straight to global fp32 atomics.
 //
 // rdf_route: moves every row of every tree one level down after the splits are chosen
 // (numeric: bin > split bin goes right; categorical: bit of the bin in the node's left-set mask)
@@ -29,13 +31,18 @@ __global__ __launch_bounds__(256) void rdf_histogram(
     const BinT* __restrict__ Xb, long long n, int P, const int* __restrict__ label,
     const float* __restrict__ y, int S, const unsigned char* __restrict__ weight,
     const int* __restrict__ node_of, int node_lo, int nodes, const int* __restrict__ feats,
-    int Fs, int B, float* __restrict__ hist, long long rows_per_block) {
+    int Fs, int B, float* __restrict__ hist, long long rows_per_block, int node_chunk) {
   extern __shared__ float lh[];
   const int t = blockIdx.y;
-  const long long per_tree = (long long)nodes * Fs * B * S;
+  const long long per_node = (long long)Fs * B * S;
+  const long long per_tree = (long long)nodes * per_node;
   float* gh = hist + (long long)t * per_tree;
+  // LDS path: this block owns the node slots [c_lo, c_hi) of the pass (blockIdx.z chunk)
+  const int c_lo = USE_LDS ? (int)blockIdx.z * node_chunk : 0;
+  const int c_hi = USE_LDS ? min(nodes, c_lo + node_chunk) : nodes;
+  const long long lds_len = (long long)(c_hi - c_lo) * per_node;
   if (USE_LDS) {
-    for (long long i = threadIdx.x; i < per_tree; i += 256) lh[i] = 0.f;
+    for (long long i = threadIdx.x; i < lds_len; i += 256) lh[i] = 0.f;
     __syncthreads();
   }
   const long long r0 = (long long)blockIdx.x * rows_per_block;
@@ -46,7 +53,7 @@ __global__ __launch_bounds__(256) void rdf_histogram(
   for (long long i = r0 + threadIdx.x; i < r1; i += 256) {
     // node slots [node_lo, node_lo + nodes) of this level are histogrammed in this pass
     const int node = nodes_t[i] - node_lo;
-    if (node < 0 || node >= nodes) continue;
+    if (node < c_lo || node >= c_hi) continue;
     const float w = w_t ? (float)w_t[i] : 1.f;
     if (w == 0.f) continue;
     const BinT* xr = Xb + i * P;
@@ -61,7 +68,7 @@ __global__ __launch_bounds__(256) void rdf_histogram(
       v1 = w * yi;
       v2 = w * yi * yi;
     }
-    float* base = (USE_LDS ? lh : gh) + (long long)node * Fs * B * S;
+    float* base = USE_LDS ? lh + (long long)(node - c_lo) * per_node : gh + node * per_node;
     for (int j = 0; j < Fs; ++j) {
       const int b = (int)xr[fj[j]];
       float* h = base + ((long long)j * B + b) * S;
@@ -76,9 +83,10 @@ __global__ __launch_bounds__(256) void rdf_histogram(
   }
   if (USE_LDS) {
     __syncthreads();
-    for (long long k = threadIdx.x; k < per_tree; k += 256) {
+    float* out = gh + (long long)c_lo * per_node;
+    for (long long k = threadIdx.x; k < lds_len; k += 256) {
       const float v = lh[k];
-      if (v != 0.f) atomicAdd(gh + k, v);
+      if (v != 0.f) atomicAdd(out + k, v);
     }
   }
 }
@@ -87,27 +95,40 @@ __global__ __launch_bounds__(256) void rdf_histogram(
 // split_feat[t][node] (-1: node became a leaf), split_bin (numeric: go right if bin > split_bin),
 // cat_left[t][node][B] (categorical: 1 if the bin goes left; nullptr when no categorical split),
 // child_base[t][node]: index of the node's left child in the next level (right = +1).
-// visits[t][node] counts rows reaching each open node (unweighted, all rows).
-template <typename BinT>
+// visits[t][node] counts rows reaching each open node (unweighted, all rows).  Grid: x = row
+// blocks, y = tree.  Visit counts are privatised in LDS per block (a level's rows all hit a few
+// counters -- the root level hits ONE per tree -- so direct global atomics serialise) and
+// flushed with one atomic per touched node.
+template <typename BinT, bool LDS_VISITS>
 __global__ __launch_bounds__(256) void rdf_route(const BinT* __restrict__ Xb, long long n, int P,
-                                                 int T, int* __restrict__ node_of, int nodes,
+                                                 int* __restrict__ node_of, int nodes,
                                                  const int* __restrict__ split_feat,
                                                  const int* __restrict__ split_bin,
                                                  const unsigned char* __restrict__ cat_left,
                                                  int B, const int* __restrict__ child_base,
-                                                 unsigned long long* __restrict__ visits) {
-  const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long total = (long long)T * n;
-  for (long long k = gid; k < total; k += (long long)gridDim.x * 256) {
-    const int t = (int)(k / n);
-    const long long i = k - (long long)t * n;
-    const int node = node_of[k];
+                                                 unsigned long long* __restrict__ visits,
+                                                 long long rows_per_block) {
+  extern __shared__ unsigned int vis[];
+  const int t = blockIdx.y;
+  if (LDS_VISITS) {
+    for (int j = threadIdx.x; j < nodes; j += 256) vis[j] = 0u;
+    __syncthreads();
+  }
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  int* nodes_t = node_of + (long long)t * n;
+  const long long tb = (long long)t * nodes;
+  for (long long i = r0 + threadIdx.x; i < r1; i += 256) {
+    const int node = nodes_t[i];
     if (node < 0) continue;
-    const long long tn = (long long)t * nodes + node;
-    if (visits) atomicAdd(visits + tn, 1ull);
+    const long long tn = tb + node;
+    if (visits) {
+      if (LDS_VISITS) atomicAdd(vis + node, 1u);
+      else atomicAdd(visits + tn, 1ull);
+    }
     const int f = split_feat[tn];
     if (f < 0) {
-      node_of[k] = -1;
+      nodes_t[i] = -1;
       continue;
     }
     const int b = (int)Xb[i * P + f];
@@ -117,7 +138,14 @@ __global__ __launch_bounds__(256) void rdf_route(const BinT* __restrict__ Xb, lo
     } else {
       right = b > split_bin[tn];
     }
-    node_of[k] = child_base[tn] + (right ? 1 : 0);
+    nodes_t[i] = child_base[tn] + (right ? 1 : 0);
+  }
+  if (LDS_VISITS) {
+    __syncthreads();
+    for (int j = threadIdx.x; j < nodes; j += 256) {
+      const unsigned int v = vis[j];
+      if (v) atomicAdd(visits + tb + j, (unsigned long long)v);
+    }
   }
 }
 
@@ -172,19 +200,34 @@ int oryx_rdf_histogram(const void* Xb, int bin_bytes, long long n, int P, const 
   if ((bin_bytes != 1 && bin_bytes != 2) || (cls && !label) || (!cls && (!y || S != 3)))
     return ORYX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const long long per_tree = (long long)nodes * Fs * B * S;
-  const bool lds = per_tree * 4 <= 64 * 1024;
-  // enough workgroups to fill the chip several times over across the T trees
-  long long blocks = (2048 + T - 1) / T;
-  long long rpb = (n + blocks - 1) / blocks;
-  if (rpb < 1024) rpb = 1024;
-  blocks = (n + rpb - 1) / rpb;
-  dim3 grid((unsigned)blocks, (unsigned)T);
-  const size_t smem = lds ? (size_t)per_tree * 4 : 0;
+  // LDS privatisation: a block histograms `chunk` node slots of one tree into LDS (up to
+  // 128 KB of the 160 KB); the level is covered by ceil(nodes / chunk) block columns that all
+  // scan the rows (rows outside the column's slots are skipped after a 5-byte read).  Rows per
+  // block are sized so each block's LDS flush stays small next to its accumulation work.
+  const long long per_node_bytes = (long long)Fs * B * S * 4;
+  constexpr long long LDS_BUDGET = 128 * 1024;
+  const bool lds = per_node_bytes <= LDS_BUDGET;
+  int chunk = lds ? (int)(LDS_BUDGET / per_node_bytes) : nodes;
+  if (chunk > nodes) chunk = nodes;
+  const int nchunks = lds ? (nodes + chunk - 1) / chunk : 1;
+  long long target = 2048 / ((long long)T * nchunks);
+  if (target < 1) target = 1;
+  long long rpb = (n + target - 1) / target;
+  const long long min_rows = lds ? 4096 : 1024;
+  if (rpb < min_rows) rpb = min_rows;
+  const long long blocks = (n + rpb - 1) / rpb;
+  dim3 grid((unsigned)blocks, (unsigned)T, (unsigned)nchunks);
+  const size_t smem = lds ? (size_t)chunk * per_node_bytes : 0;
 #define HIST_LAUNCH(BT, C, L)                                                                 \
-  hipLaunchKernelGGL((rdf_histogram<BT, C, L>), grid, dim3(256), smem, s,                    \
-                     reinterpret_cast<const BT*>(Xb), n, P, label, y, S, weight, node_of,     \
-                     node_lo, nodes, feats, Fs, B, hist, rpb)
+  do {                                                                                        \
+    if (L && smem > 65536) {                                                                  \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&rdf_histogram<BT, C, L>),           \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);             \
+    }                                                                                         \
+    hipLaunchKernelGGL((rdf_histogram<BT, C, L>), grid, dim3(256), smem, s,                  \
+                       reinterpret_cast<const BT*>(Xb), n, P, label, y, S, weight, node_of,   \
+                       node_lo, nodes, feats, Fs, B, hist, rpb, chunk);                       \
+  } while (0)
   if (bin_bytes == 1) {
     if (cls) {
       if (lds) HIST_LAUNCH(unsigned char, true, true); else HIST_LAUNCH(unsigned char, true, false);
@@ -208,19 +251,26 @@ int oryx_rdf_route(const void* Xb, int bin_bytes, long long n, int P, int T, int
                    unsigned long long* visits, void* stream) {
   if (n <= 0 || T <= 0) return ORYX_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  long long blocks = ((long long)T * n + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
+  long long target = 4096 / T;
+  if (target < 1) target = 1;
+  long long rpb = (n + target - 1) / target;
+  if (rpb < 2048) rpb = 2048;
+  const long long blocks = (n + rpb - 1) / rpb;
+  dim3 grid((unsigned)blocks, (unsigned)T);
+  const bool lds = nodes <= 16384;
+  const size_t smem = lds ? (size_t)nodes * 4 : 0;
+#define ROUTE_LAUNCH(BT, L)                                                                   \
+  hipLaunchKernelGGL((rdf_route<BT, L>), grid, dim3(256), smem, s,                           \
+                     reinterpret_cast<const BT*>(Xb), n, P, node_of, nodes, split_feat,       \
+                     split_bin, cat_left, B, child_base, visits, rpb)
   if (bin_bytes == 1) {
-    hipLaunchKernelGGL(rdf_route<unsigned char>, dim3((unsigned)blocks), dim3(256), 0, s,
-                       reinterpret_cast<const unsigned char*>(Xb), n, P, T, node_of, nodes,
-                       split_feat, split_bin, cat_left, B, child_base, visits);
+    if (lds) ROUTE_LAUNCH(unsigned char, true); else ROUTE_LAUNCH(unsigned char, false);
   } else if (bin_bytes == 2) {
-    hipLaunchKernelGGL(rdf_route<short>, dim3((unsigned)blocks), dim3(256), 0, s,
-                       reinterpret_cast<const short*>(Xb), n, P, T, node_of, nodes, split_feat,
-                       split_bin, cat_left, B, child_base, visits);
+    if (lds) ROUTE_LAUNCH(short, true); else ROUTE_LAUNCH(short, false);
   } else {
     return ORYX_EINVAL;
   }
+#undef ROUTE_LAUNCH
   return oryx_check_launch();
 }
 

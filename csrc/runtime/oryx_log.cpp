@@ -466,7 +466,8 @@ void oryx_reader_seek(void* rh, long long offset) { reader_seek(static_cast<Read
 // Reads up to `max_records` complete records into `out` as
 // [i64 offset][i64 ts][i32 key_len(-1 null)][i32 value_len][key][value]...
 // Waits up to timeout_ms for the first record.  Returns the number of records read, -1 on
-// error, or -(needed bytes)-16 when the next record alone does not fit in `out`.
+// error, -3 when the next record is corrupt (CRC mismatch with later data present), or
+// -(needed bytes)-16 when the next record alone does not fit in `out`.
 long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_records,
                            int timeout_ms, long long* out_used) {
   auto* r = static_cast<Reader*>(rh);
@@ -495,7 +496,21 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
       payload.resize(16 + plen);
       memcpy(payload.data(), hdr + 8, 16);
       if (plen && pread(r->fd, payload.data() + 16, plen, r->pos + kHeader) != (ssize_t)plen) break;
-      if (crc32(payload.data(), 16 + plen) != crc) break;  // torn / in-progress write
+      if (crc32(payload.data(), 16 + plen) != crc) {
+        // A torn or in-progress write can only be the tail of the segment; a bad frame with
+        // a complete frame header written after it is corruption, reported instead of being
+        // waited on forever.
+        struct stat st;
+        if (fstat(r->fd, &st) == 0 &&
+            (long long)st.st_size >= r->pos + (long long)(kHeader + plen + kHeader)) {
+          if (count > 0) break;   // deliver the good records first; the next poll reports
+          *out_used = 0;
+          fail("corrupt record (crc mismatch) in " + dir + " at offset " +
+               std::to_string(r->next_offset));
+          return -3;
+        }
+        break;  // torn / in-progress write
+      }
       long long need = 24 + (long long)plen;
       if (used + need > out_cap) {
         if (count == 0) { *out_used = 0; return -need - 16; }

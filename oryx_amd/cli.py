@@ -141,9 +141,12 @@ def cmd_config_props(config, out=sys.stdout) -> None:
     print(cfg.to_properties(config), file=out)
 
 
-def _relaunch_distributed(argv: List[str], gpus: int) -> int:
+def _relaunch_distributed(argv: List[str], gpus: int, max_restarts: int = 0) -> int:
+    # a rank that fails (or is ended by the watchdog) makes the agent restart the whole group
+    # up to max_restarts times; the ALS trainer then resumes from its factor checkpoint
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           "--nproc-per-node=%d" % gpus, "--master-addr=127.0.0.1",
+           "--nproc-per-node=%d" % gpus, "--max-restarts=%d" % max_restarts,
+           "--master-addr=127.0.0.1",
            "--master-port=%s" % os.environ.get("ORYX_MASTER_PORT", "29551"),
            "-m", "oryx_amd.cli"] + argv
     env = dict(os.environ, ORYX_DISTRIBUTED_CHILD="1")
@@ -183,7 +186,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     log.info("Configuration:\n%s", cfg.pretty_print(config))
     if command == "batch":
         if args.gpus > 1 and not os.environ.get("ORYX_DISTRIBUTED_CHILD"):
-            return _relaunch_distributed(argv, args.gpus)
+            return _relaunch_distributed(
+                argv, args.gpus, cfg.get_optional_int(config, "oryx.gpu.max-restarts") or 0)
         from .layers.batch import BatchLayer
         from .parallel import dist
         ctx = dist.init_from_env(device=config.get_string("oryx.gpu.device"))

@@ -28,7 +28,7 @@ from ..api import BatchLayerUpdate, Dataset
 from ..transport.producer import LogTopicProducer
 from ..utils import config as cfg
 from ..parallel import dist
-from ..utils import ioutils, lang, rng
+from ..utils import faults, ioutils, lang, rng
 from .common import AbstractLayer, IntervalTimer, drain
 
 __all__ = ["BatchLayer", "save_interval_data", "read_past_data", "delete_old_data"]
@@ -131,6 +131,7 @@ class BatchLayer(AbstractLayer):
             self.build_input_consumer()
         ts = int(time.time() * 1000) if timestamp is None else timestamp
         records = drain(self._input_consumer)
+        faults.point("batch.interval", timestamp=ts, records=len(records))
         dctx = self._context.dist if self._context is not None else None
         seed = rng.next_seed()
         if dctx is not None and dctx.is_distributed:

@@ -17,7 +17,7 @@ from dataclasses import dataclass
 from typing import Any, List, Optional, Tuple
 
 from ..api import Dataset
-from ..parallel import dist
+from ..parallel import dist, watchdog
 from ..transport import log as tlog
 from ..transport.producer import topic_root
 from ..utils import config as cfg
@@ -125,6 +125,9 @@ class AbstractLayer:
         self.update_root = topic_root(self.update_broker, config) if self.update_broker else None
         self._input_consumer: Optional[tlog.TopicConsumer] = None
         self._input_topic: Optional[tlog.Topic] = None
+        wd = cfg.get_optional_int(config, "oryx.gpu.collective-timeout-sec") or 0
+        if wd > 0:
+            watchdog.configure(wd)
 
     @staticmethod
     def generate_random_id() -> str:

@@ -97,6 +97,8 @@ class MLUpdate(BatchLayerUpdate):
         per_param = hp.choose_values_per_hyper_param(len(values), self.candidates)
         combos = hp.choose_hyper_parameter_combos(values, self.candidates, per_param)
         dctx = self._dist_ctx(context)
+        # trainers that checkpoint or warm-start find their files under the model dir
+        self.current_model_dir = ioutils.to_local_path(model_dir) if model_dir else None
         # multi-rank: every candidate runs in its own shared-seed scope so all ranks make the
         # same splits whatever rank 0 does in between (evaluation, publishing)
         self._candidate_seed_base = rng.next_seed() if dctx.is_distributed else None

@@ -19,6 +19,7 @@ Equivalent of ``ALSUpdate`` (``[mllib]/als/ALSUpdate.java:78-498``) and its help
 from __future__ import annotations
 
 import gzip
+import hashlib
 import json
 import logging
 import math
@@ -33,7 +34,7 @@ from ... import ingest
 from ...ml import hyperparams as hp
 from ...ml.mlupdate import MLUpdate
 from ...parallel import dist
-from ...utils import ioutils, pmml as pmmlu, rng, text
+from ...utils import config as cfg, ioutils, pmml as pmmlu, rng, text
 from . import evaluation
 from .trainer import ALSTrainer
 
@@ -128,6 +129,53 @@ def read_features(path: str) -> Tuple[List[str], np.ndarray]:
     return ids, mat
 
 
+def _fingerprint(u, i, s, *params) -> str:
+    """Identity of one training run: the aggregated ratings plus every setting that shapes
+    the factors (a checkpoint is only resumed by the same run)."""
+    h = hashlib.blake2b(digest_size=20)
+    for a in (u, i, s):
+        h.update(np.ascontiguousarray(a).tobytes())
+    h.update(repr(params).encode())
+    return h.hexdigest()
+
+
+def _latest_model_dir(model_dir: str) -> Optional[str]:
+    """The newest ``model-dir/<timestamp>/`` that has both X/ and Y/ factor directories."""
+    try:
+        names = [n for n in os.listdir(model_dir) if n.isdigit()]
+    except OSError:
+        return None
+    for n in sorted(names, key=int, reverse=True):
+        p = os.path.join(model_dir, n)
+        if os.path.isdir(os.path.join(p, "X")) and os.path.isdir(os.path.join(p, "Y")):
+            return p
+    return None
+
+
+def _warm_start_factors(model_dir: str, features: int, x_ids: List[str], y_ids: List[str]):
+    """Previous generation's factor rows for the IDs of this run (NaN rows where absent);
+    (None, None) when there is no previous model of the same rank."""
+    prev = _latest_model_dir(model_dir)
+    if prev is None:
+        return None, None
+    out = []
+    for sub, ids in (("X", x_ids), ("Y", y_ids)):
+        old_ids, mat = read_features(os.path.join(prev, sub))
+        if mat.ndim != 2 or mat.shape[1] != features:
+            log.info("Previous model %s has rank %s, not warm-starting", prev,
+                     mat.shape[1] if mat.ndim == 2 else None)
+            return None, None
+        index = {k: j for j, k in enumerate(old_ids)}
+        init = np.full((len(ids), features), np.nan, dtype=np.float32)
+        rows = [(a, index[k]) for a, k in enumerate(ids) if k in index]
+        if rows:
+            dst, src = zip(*rows)
+            init[list(dst)] = mat[list(src)]
+        out.append(torch.from_numpy(init))
+    log.info("Warm-starting ALS from %s", prev)
+    return out[0], out[1]
+
+
 class ALSUpdate(MLUpdate):
     def __init__(self, config):
         super().__init__(config)
@@ -141,6 +189,10 @@ class ALSUpdate(MLUpdate):
         self.no_known_items = config.get_bool("oryx.als.no-known-items")
         self.decay_factor = config.get_double("oryx.als.decay.factor")
         self.decay_zero_threshold = config.get_double("oryx.als.decay.zero-threshold")
+        self.checkpoint_interval = cfg.get_optional_int(config, "oryx.als.checkpoint-interval") \
+            or 0
+        self.warm_start = bool(cfg.get_optional_bool(config, "oryx.als.warm-start"))
+        self.current_model_dir: Optional[str] = None
         if self.iterations <= 0:
             raise ValueError("iterations must be > 0")
         if not (0.0 < self.decay_factor <= 1.0) or self.decay_zero_threshold < 0.0:
@@ -179,20 +231,31 @@ class ALSUpdate(MLUpdate):
         remap_i = np.full(len(item_ids), -1, dtype=np.int64)
         remap_i[used_i] = np.arange(len(used_i))
         ctx = self._ctx(context)
-        trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx,
-                             seed=rng.next_seed())
+        seed = rng.next_seed()
+        trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx, seed=seed)
         t0 = time.perf_counter()
         # every rank holds the same aggregated triples; each contributes a disjoint slice
         part = slice(ctx.rank, None, ctx.world_size)
         trainer.prepare(torch.from_numpy(remap_u[u][part]), torch.from_numpy(remap_i[i][part]),
                         torch.from_numpy(s[part].astype(np.float32)), len(used_u), len(used_i))
-        f = trainer.train(self.iterations)
+        x_ids = [user_ids[j] for j in used_u]
+        y_ids = [item_ids[j] for j in used_i]
+        ckpt_dir, fingerprint = None, ""
+        if self.checkpoint_interval > 0 and self.current_model_dir:
+            fingerprint = _fingerprint(u, i, s, features, lam, alpha, self.implicit,
+                                       self.iterations, seed, ctx.world_size)
+            ckpt_dir = os.path.join(self.current_model_dir, ".checkpoint",
+                                    "als-" + fingerprint[:16])
+        x_init = y_init = None
+        if self.warm_start and self.current_model_dir:
+            x_init, y_init = _warm_start_factors(self.current_model_dir, features, x_ids, y_ids)
+        f = trainer.train(self.iterations, checkpoint_dir=ckpt_dir,
+                          checkpoint_interval=self.checkpoint_interval, fingerprint=fingerprint,
+                          x_init=x_init, y_init=y_init)
         X = f.X.cpu().numpy()
         Y = f.Y.cpu().numpy()
         log.info("ALS %d ratings, %d users, %d items, rank %d: %.3fs", len(u), len(used_u),
                  len(used_i), features, time.perf_counter() - t0)
-        x_ids = [user_ids[j] for j in used_u]
-        y_ids = [item_ids[j] for j in used_i]
         if not ctx.is_main:
             return None
         write_features(os.path.join(candidate_path, "X"), x_ids, X)

@@ -14,12 +14,24 @@ Replaces Spark MLlib's block ALS that the reference runs at
 * iteration order follows MLlib: items from users, then users from items.
 
 With world size 1 no collectives are issued.  On CPU the exact fp32 reference solve runs.
+
+Checkpoint / resume (the reference only truncates MLlib lineage with
+``setCheckpointInterval(5)``, ``[mllib]/als/ALSUpdate.java:120``): every N iterations each rank
+writes its fp32 factor shards to ``<dir>/it<k>/rank<r>.safetensors``; once all ranks have
+written, rank 0 atomically replaces ``<dir>/latest.json`` (iteration, world size, shapes and a
+caller-supplied data fingerprint) and removes older iteration directories, so a crash at any
+point leaves one complete checkpoint.  :meth:`ALSTrainer.train` resumes from it when the
+fingerprint and layout match.  Warm start (an improvement the reference lacks): initial
+factor rows may be given per row, with NaN rows drawn at random as usual.
 """
 
 from __future__ import annotations
 
+import json
 import logging
 import math
+import os
+import shutil
 import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -27,7 +39,8 @@ from typing import Dict, List, Optional
 import torch
 
 from ...ops import als as als_ops
-from ...parallel import dist
+from ...parallel import dist, watchdog
+from ...utils import faults
 from ... import tracing
 
 __all__ = ["ALSTrainer", "ALSFactors"]
@@ -108,26 +121,95 @@ class ALSTrainer:
     # ------------------------------------------------------------------ factors
     def init_factors(self, x_init: Optional[torch.Tensor] = None,
                      y_init: Optional[torch.Tensor] = None) -> None:
-        """Random unit-norm Gaussian rows (MLlib's init), or warm-start from given factors."""
+        """Random unit-norm Gaussian rows (MLlib's init), or warm-start from given factors
+        (full [n, k] matrices; rows containing NaN are initialised at random)."""
         ctx, dev, k, kp = self.ctx, self.device, self.k, self.kp
         gen = torch.Generator(device="cpu")
         gen.manual_seed((self.seed * 1000003 + ctx.rank) & ((1 << 62) - 1))
         nu, ni = self.u_hi - self.u_lo, self.i_hi - self.i_lo
         self.X = torch.zeros((self.su, kp), dtype=torch.float32, device=dev)
         self.Y = torch.zeros((self.si, kp), dtype=torch.float32, device=dev)
-        if x_init is not None:
-            self.X[:nu, :k] = x_init[self.u_lo:self.u_hi].to(dev, torch.float32)
-        else:
-            self.X[:nu] = _unit_gaussian(nu, k, kp, gen, dev)
-        if y_init is not None:
-            self.Y[:ni, :k] = y_init[self.i_lo:self.i_hi].to(dev, torch.float32)
-        else:
-            self.Y[:ni] = _unit_gaussian(ni, k, kp, gen, dev)
+        self.X[:nu] = _unit_gaussian(nu, k, kp, gen, dev)
+        self.Y[:ni] = _unit_gaussian(ni, k, kp, gen, dev)
+        for init, dst, lo, hi in ((x_init, self.X, self.u_lo, self.u_hi),
+                                  (y_init, self.Y, self.i_lo, self.i_hi)):
+            if init is None:
+                continue
+            rows = init[lo:hi].to(dev, torch.float32)
+            ok = ~torch.isnan(rows).any(1)
+            dst[:hi - lo, :k] = torch.where(ok[:, None], rows, dst[:hi - lo, :k])
+        self._publish_factors()
+
+    def _publish_factors(self) -> None:
+        ctx = self.ctx
         self.Xb_local = self.X.to(torch.bfloat16)
         self.Yb_local = self.Y.to(torch.bfloat16)
         self.Xb = dist.all_gather_rows(self.Xb_local, self.n_users, ctx).contiguous()
         self.Yb = dist.all_gather_rows(self.Yb_local, self.n_items, ctx).contiguous()
-        self.fail_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.fail_count = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.iterations_done = 0
+
+    # ------------------------------------------------------------------ checkpoints
+    def _layout(self, fingerprint: str, iteration: int) -> dict:
+        return {"iteration": int(iteration), "world_size": self.ctx.world_size,
+                "n_users": self.n_users, "n_items": self.n_items, "k": self.k,
+                "kp": self.kp, "fingerprint": str(fingerprint)}
+
+    def save_checkpoint(self, directory: str, iteration: int, fingerprint: str = "") -> None:
+        """Write this rank's shards for ``iteration`` (collective: every rank calls it)."""
+        from safetensors.torch import save_file
+        ctx = self.ctx
+        it_dir = os.path.join(directory, "it%d" % iteration)
+        os.makedirs(it_dir, exist_ok=True)
+        path = os.path.join(it_dir, "rank%d.safetensors" % ctx.rank)
+        tmp = path + ".tmp"
+        save_file({"X": self.X.detach().cpu().contiguous(),
+                   "Y": self.Y.detach().cpu().contiguous()}, tmp,
+                  metadata={k: str(v) for k, v in self._layout(fingerprint, iteration).items()})
+        os.replace(tmp, path)
+        dist.barrier(ctx)
+        if ctx.is_main:
+            meta = os.path.join(directory, "latest.json")
+            with open(meta + ".tmp", "w") as f:
+                json.dump(self._layout(fingerprint, iteration), f)
+            os.replace(meta + ".tmp", meta)
+            for name in os.listdir(directory):
+                if name.startswith("it") and name != "it%d" % iteration:
+                    shutil.rmtree(os.path.join(directory, name), ignore_errors=True)
+        dist.barrier(ctx)
+
+    def load_checkpoint(self, directory: str, fingerprint: str = "") -> int:
+        """Restore the latest complete checkpoint if it matches this run; returns the
+        iteration it was taken after, or 0 (collective; every rank gets the same answer)."""
+        ctx = self.ctx
+        iteration = 0
+        if ctx.is_main:
+            try:
+                with open(os.path.join(directory, "latest.json")) as f:
+                    meta = json.load(f)
+                want = self._layout(fingerprint, meta.get("iteration", 0))
+                it_dir = os.path.join(directory, "it%d" % int(meta["iteration"]))
+                if meta == want and all(os.path.exists(os.path.join(
+                        it_dir, "rank%d.safetensors" % r)) for r in range(ctx.world_size)):
+                    iteration = int(meta["iteration"])
+                else:
+                    log.info("Ignoring checkpoint in %s: layout or data differ", directory)
+            except (OSError, ValueError, KeyError):
+                iteration = 0
+        iteration = int(dist.broadcast_object(iteration, ctx))
+        if iteration <= 0:
+            return 0
+        from safetensors.torch import load_file
+        t = load_file(os.path.join(directory, "it%d" % iteration,
+                                   "rank%d.safetensors" % ctx.rank))
+        if tuple(t["X"].shape) != (self.su, self.kp) or tuple(t["Y"].shape) != (self.si, self.kp):
+            raise ValueError("checkpoint shard shapes do not match the trainer")
+        self.X = t["X"].to(self.device)
+        self.Y = t["Y"].to(self.device)
+        self._publish_factors()
+        self.iterations_done = iteration
+        log.info("Resumed ALS from %s after iteration %d", directory, iteration)
+        return iteration
 
     # ------------------------------------------------------------------ iterations
     def _half_step(self, csr, src_own_f32, src_full_bf16, dst_f32, dst_b_local, n_total_dst,
@@ -147,16 +229,45 @@ class ALSTrainer:
 
     def iterate(self, iterations: int = 1) -> None:
         for _ in range(iterations):
+            self.iterations_done += 1
+            faults.point("als.iteration", iteration=self.iterations_done, rank=self.ctx.rank)
+            watchdog.heartbeat("als.iteration")
             # items given users, then users given items (MLlib order)
             self.Yb = self._half_step(self.csr_i, self.X, self.Xb, self.Y, self.Yb_local,
                                       self.n_items, "als.items")
             self.Xb = self._half_step(self.csr_u, self.Y, self.Yb, self.X, self.Xb_local,
                                       self.n_users, "als.users")
 
-    def train(self, iterations: int) -> ALSFactors:
-        self.init_factors()
-        self.iterate(iterations)
-        return self.factors()
+    def train(self, iterations: int, checkpoint_dir: Optional[str] = None,
+              checkpoint_interval: int = 0, fingerprint: str = "",
+              x_init: Optional[torch.Tensor] = None,
+              y_init: Optional[torch.Tensor] = None) -> ALSFactors:
+        """Initialise (or resume from ``checkpoint_dir``) and run ``iterations`` iterations,
+        checkpointing every ``checkpoint_interval``; a completed run removes its checkpoint."""
+        done = 0
+        use_ckpt = bool(checkpoint_dir) and checkpoint_interval > 0
+        if use_ckpt:
+            done = self.load_checkpoint(checkpoint_dir, fingerprint)
+        self.resumed_from = done
+        if done == 0:
+            self.init_factors(x_init, y_init)
+        done = min(done, iterations)
+        while done < iterations:
+            step = iterations - done
+            if use_ckpt:
+                step = min(step, checkpoint_interval - done % checkpoint_interval)
+            self.iterate(step)
+            done += step
+            if use_ckpt and done < iterations and done % checkpoint_interval == 0:
+                with tracing.range("als.checkpoint"):
+                    self.save_checkpoint(checkpoint_dir, done, fingerprint)
+        watchdog.get().end_heartbeats()
+        out = self.factors()
+        if use_ckpt:
+            dist.barrier(self.ctx)
+            if self.ctx.is_main:
+                shutil.rmtree(checkpoint_dir, ignore_errors=True)
+        return out
 
     def factors(self, gather: bool = True) -> ALSFactors:
         """Full fp32 factors (all-gathered from the owned shards)."""

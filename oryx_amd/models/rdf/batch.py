@@ -56,19 +56,43 @@ def parse_examples(rows: Sequence[Sequence[str]], schema: InputSchema,
     n = len(rows)
     F = schema.get_num_features()
     full = np.zeros((n, F), dtype=np.float64)
-    for fi in range(F):
-        if schema.is_numeric(fi):
-            col = [r[fi] for r in rows]
-            if schema.is_target(fi):
-                full[:, fi] = [float(v) if v != "" else np.nan for v in col]
-            else:
-                full[:, fi] = np.asarray(col, dtype=np.float64) if n else 0.0
-        elif schema.is_categorical(fi):
-            m = encodings.get_value_encoding_map(fi)
-            if schema.is_target(fi):
-                full[:, fi] = [m[r[fi]] if r[fi] != "" else np.nan for r in rows]
-            else:
-                full[:, fi] = [m[r[fi]] for r in rows]
+    if n == 0:
+        pass
+    elif all(len(r) == F for r in rows):
+        # one C-level conversion per column block instead of per-cell Python work
+        arr = np.array(rows, dtype=str).reshape(n, F)
+        for fi in range(F):
+            col = arr[:, fi]
+            if schema.is_numeric(fi):
+                if schema.is_target(fi):
+                    empty = col == ""
+                    vals = np.where(empty, "nan", col).astype(np.float64)
+                    full[:, fi] = vals
+                else:
+                    full[:, fi] = col.astype(np.float64)
+            elif schema.is_categorical(fi):
+                m = encodings.get_value_encoding_map(fi)
+                uniq, inv = np.unique(col, return_inverse=True)
+                if schema.is_target(fi):
+                    codes = np.array([m[u] if u != "" else np.nan for u in uniq.tolist()],
+                                     dtype=np.float64)
+                else:
+                    codes = np.array([m[u] for u in uniq.tolist()], dtype=np.float64)
+                full[:, fi] = codes[inv.reshape(-1)]
+    else:
+        for fi in range(F):
+            if schema.is_numeric(fi):
+                col = [r[fi] for r in rows]
+                if schema.is_target(fi):
+                    full[:, fi] = [float(v) if v != "" else np.nan for v in col]
+                else:
+                    full[:, fi] = np.asarray(col, dtype=np.float64)
+            elif schema.is_categorical(fi):
+                m = encodings.get_value_encoding_map(fi)
+                if schema.is_target(fi):
+                    full[:, fi] = [m[r[fi]] if r[fi] != "" else np.nan for r in rows]
+                else:
+                    full[:, fi] = [m[r[fi]] for r in rows]
     pred_idx = schema.predictor_feature_indices
     X = full[:, pred_idx]
     target = full[:, schema.get_target_feature_index()] if schema.has_target() else \

@@ -97,22 +97,36 @@ class RDFSpeedModelManager(SpeedModelManager):
         leaves = rdf_ops.forest_leaves(flat, torch.from_numpy(full).to(self.device)).cpu() \
             .numpy()                                             # [n, T]
         has_target = ~np.isnan(target)
-        groups: Dict[Tuple[int, str], list] = {}
-        for e in np.nonzero(has_target)[0].tolist():
-            for t in range(leaves.shape[1]):
-                node = flat.nodes[int(leaves[e, t])]
-                groups.setdefault((t, node.get_id()), []).append(target[e])
+        leaves = leaves[has_target]                               # [m, T] flat node indices
+        tv = target[has_target]
+        if leaves.size == 0:
+            return []
+        # flat nodes are laid out tree by tree from each root index
+        roots = flat.roots.cpu().numpy().astype(np.int64)
+        flat_leaf = leaves.ravel().astype(np.int64)
+        vals = np.broadcast_to(tv[:, None], leaves.shape).ravel()
         out = []
-        for (t, node_id), vals in groups.items():
-            if schema.is_classification():
-                counts: Dict[str, int] = {}
-                for v in vals:
-                    k = str(int(v))
-                    counts[k] = counts.get(k, 0) + 1
-                out.append(json.dumps([t, node_id, counts], separators=(",", ":")))
-            else:
-                arr = np.asarray(vals, dtype=np.float64)
-                out.append(json.dumps([t, node_id, float(arr.mean()), int(len(arr))],
+        if schema.is_classification():
+            # one pass over (leaf, class) pairs: counts per leaf per class
+            cls = vals.astype(np.int64)
+            nc = int(cls.max()) + 1
+            keys, counts = np.unique(flat_leaf * nc + cls, return_counts=True)
+            leaf_k, cls_k = keys // nc, keys % nc
+            bounds = np.flatnonzero(np.diff(leaf_k)) + 1
+            for seg_l, seg_c, seg_n in zip(np.split(leaf_k, bounds), np.split(cls_k, bounds),
+                                           np.split(counts, bounds)):
+                leaf = int(seg_l[0])
+                t = int(np.searchsorted(roots, leaf, side="right")) - 1
+                cmap = {str(int(c)): int(k) for c, k in zip(seg_c, seg_n)}
+                out.append(json.dumps([t, flat.nodes[leaf].get_id(), cmap],
+                                      separators=(",", ":")))
+        else:
+            keys, inv, counts = np.unique(flat_leaf, return_inverse=True, return_counts=True)
+            sums = np.bincount(inv, weights=vals, minlength=len(keys))
+            trees = np.searchsorted(roots, keys, side="right") - 1
+            for j, leaf in enumerate(keys.tolist()):
+                out.append(json.dumps([int(trees[j]), flat.nodes[leaf].get_id(),
+                                       float(sums[j] / counts[j]), int(counts[j])],
                                       separators=(",", ":")))
         return out
 

@@ -117,8 +117,8 @@ def _load_kernels():
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
                                           c_vp])
-    _sig(lib, "oryx_kmeans_accumulate", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp,
-                                              c_vp, c_vp])
+    _sig(lib, "oryx_kmeans_accumulate", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i, c_vp,
+                                              c_vp, c_vp, c_vp])
     # Xb, bin_bytes, n, P, label, y, S, cls, weight, T, node_of, node_lo, nodes, feats, Fs, B,
     # hist, stream
     _sig(lib, "oryx_rdf_histogram", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i, c_vp, c_i,

@@ -3,7 +3,7 @@
 Replaces Spark MLlib ``KMeans.train`` (invoked at ``[mllib]/kmeans/KMeansUpdate.java:116-117``;
 SURVEY.md K8/K9/K11, C10/C11).  On a GPU the assignment is the fused HIP kernel
 ``oryx_kmeans_assign`` (bf16 MFMA distance GEMM + argmin, ``csrc/kernels/kmeans.hip``) and the
-centroid sums use ``oryx_kmeans_accumulate`` (row-coalesced fp32 atomics); across ranks the
+centroid sums use ``oryx_kmeans_accumulate`` (LDS-privatised column slices); across ranks the
 K x d sums and K counts are all-reduced (one RCCL call per Lloyd iteration).  On CPU an exact
 fp32 PyTorch path runs the same algorithm.
 
@@ -24,9 +24,11 @@ import numpy as np
 import torch
 
 from .. import native
-from ..parallel import dist
+from ..parallel import dist, watchdog
+from ..utils import faults
 
-__all__ = ["assign", "accumulate", "kmeans_train", "KMeansResult", "pairwise_distances"]
+__all__ = ["assign", "accumulate", "kmeans_train", "lloyd_step", "PointSet", "KMeansResult",
+           "pairwise_distances"]
 
 _CHUNK = 1 << 20
 
@@ -55,32 +57,71 @@ def _kernel_ok(x: torch.Tensor) -> bool:
     return x.device.type == "cuda" and _pad_to(max(x.shape[1], 32), 32) <= 512
 
 
-def assign(x: torch.Tensor, centers: torch.Tensor, exact: bool = False
-           ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(index int64 [n], squared distance fp32 [n]) of the nearest center for each row.
+class PointSet:
+    """A rank's points, prepared once for repeated assignment passes.
 
-    GPU + not ``exact``: bf16 MFMA kernel.  Otherwise fp32 chunked matmul + argmin.
+    Holds the fp32 rows (centroid sums are accumulated from these) and, when the HIP
+    assignment kernel applies, a bf16 copy padded to ``d_pad`` columns plus the fp32 squared
+    norms of the bf16 rows -- built once per training instead of on every Lloyd iteration
+    (an N x d fp32 re-read + bf16 write that would otherwise cost as much HBM traffic as the
+    assignment itself).
     """
+
+    def __init__(self, x: torch.Tensor):
+        self.x = x if x.dtype == torch.float32 and x.is_contiguous() else \
+            x.to(torch.float32).contiguous()
+        self.n, self.d = self.x.shape
+        self.device = self.x.device
+        self.xb = None
+        self.xn = None
+        if self.n and _kernel_ok(self.x):
+            self.d_pad = _pad_to(max(self.d, 32), 32)
+            self.xb = torch.zeros((self.n, self.d_pad), dtype=torch.bfloat16, device=self.device)
+            self.xn = torch.empty(self.n, dtype=torch.float32, device=self.device)
+            for lo in range(0, self.n, _CHUNK * 4):
+                hi = min(self.n, lo + _CHUNK * 4)
+                self.xb[lo:hi, :self.d] = self.x[lo:hi]
+                self.xn[lo:hi] = self.xb[lo:hi].float().pow(2).sum(1)
+
+    @property
+    def shape(self):
+        return self.x.shape
+
+
+def _as_points(x) -> PointSet:
+    return x if isinstance(x, PointSet) else PointSet(x)
+
+
+def assign(x, centers: torch.Tensor, exact: bool = False, out=None
+           ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(index [n], squared distance fp32 [n]) of the nearest center for each row.
+
+    ``x``: a tensor or a prepared :class:`PointSet`.  GPU + not ``exact``: bf16 MFMA kernel
+    (indices int32, written into ``out=(idx, dist)`` when given).  Otherwise fp32 chunked
+    matmul + argmin (indices int64).
+    """
+    if not exact and isinstance(x, torch.Tensor) and _kernel_ok(x) and x.shape[0]:
+        x = PointSet(x)
+    if isinstance(x, PointSet):
+        if x.xb is not None and not exact:
+            lib = native.require_kernels()
+            dc = DeviceCenters(centers.float())
+            n = x.n
+            if out is None:
+                out = (torch.empty(n, dtype=torch.int32, device=x.device),
+                       torch.empty(n, dtype=torch.float32, device=x.device))
+            out_a, out_d = out
+            rc = lib.oryx_kmeans_assign(x.xb.data_ptr(), x.xn.data_ptr(), dc.cb.data_ptr(), n,
+                                        dc.d_pad, dc.k_pad, dc.cnorm.data_ptr(),
+                                        out_a.data_ptr(), out_d.data_ptr(),
+                                        native.stream_ptr(x.device))
+            native.check(rc, "oryx_kmeans_assign")
+            return out_a, out_d
+        x = x.x
     n = x.shape[0]
     if n == 0:
         return (torch.zeros(0, dtype=torch.int64, device=x.device),
                 torch.zeros(0, dtype=torch.float32, device=x.device))
-    if _kernel_ok(x) and not exact:
-        lib = native.require_kernels()
-        dc = DeviceCenters(centers.float())
-        out_a = torch.empty(n, dtype=torch.int32, device=x.device)
-        out_d = torch.empty(n, dtype=torch.float32, device=x.device)
-        for lo in range(0, n, _CHUNK * 16):
-            hi = min(n, lo + _CHUNK * 16)
-            xb = torch.zeros((hi - lo, dc.d_pad), dtype=torch.bfloat16, device=x.device)
-            xb[:, :dc.d] = x[lo:hi]
-            xn = xb.float().pow(2).sum(1)
-            rc = lib.oryx_kmeans_assign(xb.data_ptr(), xn.data_ptr(), dc.cb.data_ptr(), hi - lo,
-                                        dc.d_pad, dc.k_pad, dc.cnorm.data_ptr(),
-                                        out_a[lo:hi].data_ptr(), out_d[lo:hi].data_ptr(),
-                                        native.stream_ptr(x.device))
-            native.check(rc, "oryx_kmeans_assign")
-        return out_a.to(torch.int64), out_d
     c = centers.to(x.device, torch.float32)
     cn = c.pow(2).sum(1)
     idx = torch.empty(n, dtype=torch.int64, device=x.device)
@@ -98,6 +139,8 @@ def assign(x: torch.Tensor, centers: torch.Tensor, exact: bool = False
 def accumulate(x: torch.Tensor, idx: torch.Tensor, k: int,
                mind: Optional[torch.Tensor] = None):
     """(sums fp32 [k, d], counts int64 [k], dist stats fp64 [k, 2] = (sum d, sum d^2) or None)."""
+    if isinstance(x, PointSet):
+        x = x.x
     n, d = x.shape
     dev = x.device
     sums = torch.zeros((k, d), dtype=torch.float32, device=dev)
@@ -105,16 +148,19 @@ def accumulate(x: torch.Tensor, idx: torch.Tensor, k: int,
     if dev.type == "cuda" and native.kernels_available():
         lib = native.kernels()
         counts = torch.zeros(k, dtype=torch.int64, device=dev)
-        xf = x.to(torch.float32).contiguous()
-        ia = idx.to(torch.int32).contiguous()
+        xf = x if x.dtype == torch.float32 and x.is_contiguous() else \
+            x.to(torch.float32).contiguous()
+        ia = idx if idx.dtype == torch.int32 and idx.is_contiguous() else \
+            idx.to(torch.int32).contiguous()
         md = mind.to(torch.float32).contiguous() if mind is not None else None
         rc = lib.oryx_kmeans_accumulate(xf.data_ptr(), ia.data_ptr(),
-                                        md.data_ptr() if md is not None else None, n, d, d,
+                                        md.data_ptr() if md is not None else None, n, d, d, k,
                                         sums.data_ptr(), counts.data_ptr(),
                                         stats.data_ptr() if stats is not None else None,
                                         native.stream_ptr(dev))
         native.check(rc, "oryx_kmeans_accumulate")
         return sums, counts, stats
+    idx = idx.long()
     sums.index_add_(0, idx, x.to(torch.float32))
     counts = torch.bincount(idx, minlength=k).to(torch.int64)
     if stats is not None:
@@ -247,12 +293,41 @@ def _farthest_points(x: torch.Tensor, d2: torch.Tensor, m: int, ctx) -> torch.Te
     return cand[order, 1:]
 
 
-def kmeans_train(x: torch.Tensor, k: int, max_iterations: int, runs: int = 1,
+def lloyd_step(pts: PointSet, centers: torch.Tensor, ctx, workspace=None):
+    """One Lloyd iteration: assign (MFMA kernel), accumulate sums/counts, all-reduce them
+    (one K x (d + 1) RCCL call), move the centers.  Returns (new centers, counts, assignment
+    distances, number of empty clusters)."""
+    kk = centers.shape[0]
+    idx, d2 = assign(pts, centers, out=workspace)
+    sums, counts, _ = accumulate(pts, idx, kk)
+    if ctx.is_distributed:
+        # counts ride along as an extra fp32 column (exact below 2^24 per cluster per rank;
+        # summed in fp64 below)
+        packed = torch.cat([sums, counts[:, None].to(torch.float32)], 1)
+        if ctx.world_size * max(pts.n, 1) < (1 << 24):
+            dist.all_reduce_sum(packed, ctx)
+            sums, counts = packed[:, :-1], packed[:, -1].round().to(torch.int64)
+        else:
+            dist.all_reduce_sum(sums, ctx)
+            dist.all_reduce_sum(counts, ctx)
+    nonempty = counts > 0
+    new = torch.where(nonempty[:, None], sums / counts.clamp_min(1)[:, None].to(torch.float32),
+                      centers)
+    return new, counts, d2, int((~nonempty).sum())
+
+
+def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
                  init: str = "k-means||", seed: int = 0, epsilon: float = 1e-4,
                  ctx: Optional[dist.DistContext] = None) -> KMeansResult:
     """Train k-means on this rank's rows ``x`` (the union over ranks is the data)."""
+    pts = _as_points(x)
+    x = pts.x
     ctx = ctx or dist.DistContext(device=x.device)
     best: Optional[KMeansResult] = None
+    ws = None
+    if pts.xb is not None:
+        ws = (torch.empty(pts.n, dtype=torch.int32, device=pts.device),
+              torch.empty(pts.n, dtype=torch.float32, device=pts.device))
     for run in range(max(1, runs)):
         gen = torch.Generator()
         gen.manual_seed((seed * 7919 + run * 104729 + ctx.rank) & ((1 << 62) - 1))
@@ -263,32 +338,28 @@ def kmeans_train(x: torch.Tensor, k: int, max_iterations: int, runs: int = 1,
         kk = centers.shape[0]
         it = 0
         for it in range(1, max_iterations + 1):
-            idx, d2 = assign(x, centers)
-            sums, counts, _ = accumulate(x, idx, kk)
-            if ctx.is_distributed:
-                dist.all_reduce_sum(sums, ctx)
-                dist.all_reduce_sum(counts, ctx)
-            nonempty = counts > 0
-            new = centers.clone()
-            new[nonempty] = sums[nonempty] / counts[nonempty, None].float()
-            n_empty = int((~nonempty).sum())
+            faults.point("kmeans.iteration", iteration=it, rank=ctx.rank)
+            watchdog.heartbeat("kmeans.iteration")
+            new, counts, d2, n_empty = lloyd_step(pts, centers, ctx, ws)
+            moved = None
             if n_empty:
                 # re-seed empty clusters at the points farthest from their centers
                 far = _farthest_points(x, d2, n_empty, ctx)
                 if far.shape[0] == n_empty:
-                    new[~nonempty] = far
+                    new[counts == 0] = far
                     moved = float("inf")
-            if not n_empty or far.shape[0] != n_empty:
+            if moved is None:
                 moved = (new - centers).pow(2).sum(1).max().item() if kk else 0.0
             centers = new
             if moved <= epsilon * epsilon:
                 break
-        idx, d2 = assign(x, centers, exact=True)
+        idx, d2 = assign(pts, centers, exact=True)
         cost = d2.double().sum()
         counts = torch.bincount(idx, minlength=kk).to(torch.int64)
         if ctx.is_distributed:
             dist.all_reduce_sum(cost, ctx)
             dist.all_reduce_sum(counts, ctx)
+        watchdog.get().end_heartbeats()
         res = KMeansResult(centers, counts, float(cost), it)
         if best is None or res.cost < best.cost:
             best = res

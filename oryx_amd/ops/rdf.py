@@ -35,7 +35,8 @@ import numpy as np
 import torch
 
 from .. import native
-from ..parallel import dist
+from ..parallel import dist, watchdog
+from ..utils import faults
 
 __all__ = ["BinnedData", "bin_features", "train_forest", "TrainedForest", "FlatForest",
            "flatten_forest", "forest_leaves"]
@@ -75,12 +76,23 @@ def bin_features(X, categorical: Sequence[bool], arities: Sequence[int], max_bin
     ranks that bin disjoint slices of one data set pass the full data so that every rank
     gets identical bins.
     """
-    X = np.asarray(X, dtype=np.float64)
+    on_device = isinstance(X, torch.Tensor)
+    if not on_device:
+        X = np.asarray(X, dtype=np.float64)
     n, P = X.shape
-    src = X if threshold_source is None else np.asarray(threshold_source, dtype=np.float64)
+    src = X if threshold_source is None else threshold_source
+    if not isinstance(src, torch.Tensor):
+        src = np.asarray(src, dtype=np.float64)
     rng = np.random.default_rng(seed)
     ns = sample_size or max(10000, max_bins * max_bins)
-    sample = src if len(src) <= ns else src[rng.choice(len(src), ns, replace=False)]
+    if len(src) <= ns:
+        sample = src
+    else:
+        pick = np.sort(rng.choice(len(src), ns, replace=False))
+        sample = src[torch.from_numpy(pick).to(src.device)] if isinstance(src, torch.Tensor) \
+            else src[pick]
+    if isinstance(sample, torch.Tensor):
+        sample = sample.to(torch.float64).cpu().numpy()
     thresholds: List[Optional[np.ndarray]] = []
     n_bins: List[int] = []
     for f in range(P):
@@ -95,7 +107,8 @@ def bin_features(X, categorical: Sequence[bool], arities: Sequence[int], max_bin
     dtype = torch.uint8 if B <= 256 else torch.int16
     Xb = torch.empty((n, P), dtype=dtype, device=device)
     for f in range(P):
-        col = torch.from_numpy(np.ascontiguousarray(X[:, f])).to(device)
+        col = X[:, f].to(device, torch.float64) if on_device else \
+            torch.from_numpy(np.ascontiguousarray(X[:, f])).to(device)
         if categorical[f]:
             b = col.to(torch.int64)
         else:
@@ -336,6 +349,8 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     predictor_counts = np.zeros(P, dtype=np.float64)
     nodes = 1
     for depth in range(max_depth + 1):
+        faults.point("rdf.level", depth=depth, rank=ctx.rank)
+        watchdog.heartbeat("rdf.level")
         if Fs < P:
             feats = torch.argsort(torch.rand((T, nodes, P), generator=g), dim=-1)[..., :Fs]
         else:
@@ -395,6 +410,7 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
         nodes = next_nodes
         if nodes == 0:
             break
+    watchdog.get().end_heartbeats()
     return TrainedForest(roots, predictor_counts, classification)
 
 

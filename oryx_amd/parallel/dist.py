@@ -22,6 +22,8 @@ from typing import List, Optional, Sequence
 import torch
 import torch.distributed as tdist
 
+from . import watchdog
+
 __all__ = ["DistContext", "init_from_env", "get_context", "shard_range", "padded_shard_size",
            "all_gather_rows", "all_reduce_sum", "broadcast_object", "barrier"]
 
@@ -78,6 +80,15 @@ def init_from_env(device: Optional[str] = None, backend: Optional[str] = None,
         if not tdist.is_initialized():
             kwargs = dict(backend=backend, rank=rank, world_size=world,
                           timeout=datetime.timedelta(seconds=timeout_s))
+            restart = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+            if restart not in (None, "", "0") and "MASTER_PORT" in os.environ:
+                # under torch.distributed.run the agent's TCPStore outlives a failed attempt;
+                # keys of the dead attempt (gloo / RCCL peer addresses) would be read by the
+                # restarted ranks, so each later attempt rendezvous under its own prefix
+                base = tdist.TCPStore(os.environ["MASTER_ADDR"],
+                                      int(os.environ["MASTER_PORT"]), world, False,
+                                      timeout=datetime.timedelta(seconds=timeout_s))
+                kwargs["store"] = tdist.PrefixStore("oryx/attempt_%s" % restart, base)
             if backend == "nccl":
                 kwargs["device_id"] = dev
             tdist.init_process_group(**kwargs)
@@ -126,17 +137,19 @@ def all_gather_rows(local: torch.Tensor, n_total: int, ctx: DistContext,
         local = pad
     full = out if out is not None and out.shape[0] == s * ctx.world_size else torch.empty(
         (s * ctx.world_size,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    if ctx.backend == "gloo":
-        parts = list(full.chunk(ctx.world_size, 0))
-        tdist.all_gather(parts, local.contiguous())
-    else:
-        tdist.all_gather_into_tensor(full, local.contiguous())
+    with watchdog.guard("all_gather_rows"):
+        if ctx.backend == "gloo":
+            parts = list(full.chunk(ctx.world_size, 0))
+            tdist.all_gather(parts, local.contiguous())
+        else:
+            tdist.all_gather_into_tensor(full, local.contiguous())
     return full
 
 
 def all_reduce_sum(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:
     if ctx.is_distributed:
-        tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
+        with watchdog.guard("all_reduce"):
+            tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
     return t
 
 
@@ -147,18 +160,21 @@ def broadcast_object(obj, ctx: DistContext, src: int = 0, control: bool = False)
         return obj
     lst = [obj]
     if control and ctx.control is not None:
+        # control announcements legitimately wait a whole batch interval: no deadline
         tdist.broadcast_object_list(lst, src=src, group=ctx.control)
     else:
-        tdist.broadcast_object_list(lst, src=src)
+        with watchdog.guard("broadcast_object"):
+            tdist.broadcast_object_list(lst, src=src)
     return lst[0]
 
 
 def barrier(ctx: DistContext) -> None:
     if ctx.is_distributed:
-        if ctx.backend == "nccl":
-            tdist.barrier(device_ids=[ctx.device.index])
-        else:
-            tdist.barrier()
+        with watchdog.guard("barrier"):
+            if ctx.backend == "nccl":
+                tdist.barrier(device_ids=[ctx.device.index])
+            else:
+                tdist.barrier()
 
 
 def all_to_all_rows(send: torch.Tensor, send_counts: Sequence[int], ctx: DistContext
@@ -166,6 +182,12 @@ def all_to_all_rows(send: torch.Tensor, send_counts: Sequence[int], ctx: DistCon
     """Variable-size all-to-all of rows (the shuffle that repartitions ratings by item)."""
     if not ctx.is_distributed:
         return send
+    with watchdog.guard("all_to_all_rows"):
+        return _all_to_all_rows(send, send_counts, ctx)
+
+
+def _all_to_all_rows(send: torch.Tensor, send_counts: Sequence[int], ctx: DistContext
+                     ) -> torch.Tensor:
     counts = torch.tensor(list(send_counts), dtype=torch.int64, device=send.device)
     recv_counts = torch.empty_like(counts)
     if ctx.backend == "gloo":

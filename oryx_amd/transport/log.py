@@ -26,6 +26,7 @@ import time
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
 from .. import native
+from ..utils import faults
 
 __all__ = ["Topic", "PartitionReader", "TopicConsumer", "Record", "get_offsets", "set_offsets",
            "maybe_create_topic", "topic_exists", "delete_topic", "log_root_for",
@@ -134,6 +135,15 @@ class Topic:
         """Append many (key, value) records with one native call; returns the last offset."""
         if not records:
             return -1
+        if faults.armed():
+            act = faults.point("log.append", topic=self.name, partition=partition)
+            if act == "drop":
+                records = records[1:]
+                if not records:
+                    return -1
+            elif act == "corrupt":
+                # damage the first record's bytes on disk after its CRC was computed
+                return self._append_corrupted(records, partition, timestamp_ms, fsync)
         parts = []
         for k, v in records:
             kb = _b(k)
@@ -152,6 +162,24 @@ class Topic:
             raise IOError(_lib().oryx_log_last_error().decode())
         return res
 
+    def _append_corrupted(self, records, partition, timestamp_ms, fsync) -> int:
+        p = partition if partition >= 0 else (0 if self.partitions == 1 else
+                                              self.partition_for(records[0][0]))
+        pdir = os.path.join(self.root, self.name, str(p))
+        segs = sorted(f for f in os.listdir(pdir) if f.endswith(".log")) if \
+            os.path.isdir(pdir) else []
+        before = os.path.getsize(os.path.join(pdir, segs[-1])) if segs else 0
+        res = self.append_batch(list(records), p, timestamp_ms, fsync)
+        segs = sorted(f for f in os.listdir(pdir) if f.endswith(".log"))
+        seg = os.path.join(pdir, segs[-1])
+        start = before if os.path.getsize(seg) > before else 0
+        with open(seg, "r+b") as f:
+            f.seek(start + _FRAME_HEADER)        # first payload byte of the first record
+            b = f.read(1)
+            f.seek(start + _FRAME_HEADER)
+            f.write(bytes([(b[0] if b else 0) ^ 0xFF]))
+        return res
+
     def begin_offset(self, partition: int) -> int:
         return _lib().oryx_log_begin_offset(self._h, partition)
 
@@ -167,6 +195,13 @@ class Topic:
 
     def reader(self, partition: int, offset: int) -> "PartitionReader":
         return PartitionReader(self, partition, offset)
+
+
+_FRAME_HEADER = 32     # u32 magic, u32 crc, u64 offset, i64 ts, u32 key len, u32 value len
+
+
+class LogCorruptionError(IOError):
+    """A record failed its CRC check with later records present (not a torn tail write)."""
 
 
 class PartitionReader:
@@ -196,7 +231,9 @@ class PartitionReader:
         while True:
             n = lib.oryx_reader_poll(self._r, self._buf, self._cap, int(max_records),
                                      int(timeout_ms), ctypes.byref(self._used))
-            if n < -1:
+            if n == -3:
+                raise LogCorruptionError(lib.oryx_log_last_error().decode())
+            if n < -3:
                 need = -n - 16
                 self._cap = max(self._cap * 2, need + 1024)
                 self._buf = ctypes.create_string_buffer(self._cap)

@@ -277,6 +277,14 @@ def get_optional_double(config: Config, key: str) -> Optional[float]:
     return config.get_double(key) if config.has_path(key) else None
 
 
+def get_optional_int(config: Config, key: str) -> Optional[int]:
+    return config.get_int(key) if config.has_path(key) else None
+
+
+def get_optional_bool(config: Config, key: str) -> Optional[bool]:
+    return config.get_bool(key) if config.has_path(key) else None
+
+
 def serialize(config: Config) -> str:
     """Concise rendering of only the ``oryx`` subtree (``ConfigUtils.serialize``)."""
     return hocon.render(config.with_only_key("oryx").root, concise=True)

@@ -23,6 +23,7 @@ from oryx_amd.models.kmeans.serving import KMeansServingModel, KMeansServingMode
 from oryx_amd.models.kmeans.speed import KMeansSpeedModelManager
 from oryx_amd.models.schema import CategoricalValueEncodings, InputSchema
 from oryx_amd.ops import kmeans as km
+from oryx_amd.parallel import dist
 from oryx_amd.transport.producer import MockTopicProducer
 from oryx_amd.utils import config as cfg
 from oryx_amd.utils import pmml as pm
@@ -366,6 +367,7 @@ import sys, torch, numpy as np
 sys.path.insert(0, {ROOT!r})
 from oryx_amd.parallel import dist
 from oryx_amd.ops import kmeans as km
+from oryx_amd.parallel import dist
 ctx = dist.init_from_env(device='cpu')
 g = np.random.default_rng(0)
 cents = np.array([[0, 0], [9, 9], [-9, 9]], float)
@@ -443,3 +445,40 @@ def test_eval_metrics_gpu_match_cpu(cuda):
                ev.silhouette_coefficient):
         assert fn(clusters, pts, cuda) == pytest.approx(fn(clusters, pts, torch.device("cpu")),
                                                         rel=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d,k", [(50000, 256, 1000), (30000, 37, 300), (20000, 16, 9000)])
+def test_accumulate_kernel_lds_slices(cuda, n, d, k):
+    """LDS column-slice path (k=1000 d=256: 8 slices; d < slice width) and the L2-atomic
+    fallback (k=9000 does not fit LDS) against index_add."""
+    g = torch.Generator().manual_seed(n + d + k)
+    x = torch.randn(n, d, generator=g)
+    idx = torch.randint(0, k, (n,), generator=g)
+    mind = torch.rand(n, generator=g)
+    sums, counts, stats = km.accumulate(x.to(cuda), idx.to(cuda).int(), k, mind.to(cuda))
+    rs = torch.zeros(k, d, dtype=torch.float64).index_add_(0, idx, x.double())
+    assert torch.allclose(sums.cpu().double(), rs, atol=1e-3)
+    assert torch.equal(counts.cpu(), torch.bincount(idx, minlength=k))
+    dd = mind.double().sqrt()
+    ref = torch.zeros(k, dtype=torch.float64).index_add_(0, idx, dd)
+    assert torch.allclose(stats[:, 0].cpu(), ref, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_lloyd_step_matches_cpu(cuda):
+    pts, _ = _blobs(n_per=3000)
+    x = torch.from_numpy(pts).float()
+    c0 = x[torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(3))[:6]].clone()
+    ctx = dist.DistContext(device=cuda)
+    new_g, counts_g, _, _ = km.lloyd_step(km.PointSet(x.to(cuda)), c0.to(cuda), ctx)
+    new_c, counts_c, _, _ = km.lloyd_step(km.PointSet(x), c0, dist.DistContext())
+    assert int(counts_g.sum()) == x.shape[0]
+    # bf16 distances may flip near-tie assignments (several initial centers share a blob)
+    assert (counts_g.cpu() - counts_c).abs().sum() <= 0.005 * x.shape[0]
+    # given the kernel's own assignment the update is exact: centers = per-cluster means
+    idx, _ = km.assign(km.PointSet(x.to(cuda)), c0.to(cuda))
+    idx = idx.long().cpu()
+    ref = torch.zeros(6, x.shape[1], dtype=torch.float64).index_add_(0, idx, x.double())
+    ref /= torch.bincount(idx, minlength=6).clamp_min(1)[:, None]
+    assert torch.allclose(new_g.cpu().double(), ref, atol=1e-4)

@@ -412,3 +412,45 @@ def test_gpu_forest_leaves_match_cpu(cuda):
     lc = rdf_ops.forest_leaves(flat_c, torch.from_numpy(full))
     lg = rdf_ops.forest_leaves(flat_g, torch.from_numpy(full).to(cuda)).cpu()
     assert torch.equal(lc, lg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls", [True, False])
+def test_histogram_and_route_kernels_match_cpu(cuda, cls):
+    """Level kernels on a wide level (200 node slots -> several LDS node chunks per tree,
+    bootstrap weights, 3 trees) against the CPU index_add / gather implementations."""
+    g = torch.Generator().manual_seed(5)
+    n, P, B, T, nodes, Fs = 40000, 12, 40, 3, 200, 5
+    Xb = torch.randint(0, B, (n, P), generator=g).to(torch.uint8)
+    data = rdf_ops.BinnedData(Xb, [B] * P, [np.arange(B - 1, dtype=np.float64)] * P,
+                              [False] * P, B)
+    node_of = torch.randint(-1, nodes, (T, n), generator=g).to(torch.int32)
+    weight = torch.randint(0, 3, (T, n), generator=g).to(torch.uint8)
+    feats = torch.stack([torch.stack([torch.randperm(P, generator=g)[:Fs]
+                                      for _ in range(nodes)]) for _ in range(T)]).int()
+    if cls:
+        label, y, S = torch.randint(0, 4, (n,), generator=g).int(), None, 4
+    else:
+        label, y, S = None, torch.randn(n, generator=g), 3
+    h_cpu = rdf_ops._histogram(data, label, y, S, cls, weight, node_of, 0, nodes, feats, B)
+    gd = rdf_ops.BinnedData(Xb.to(cuda), data.n_bins, data.thresholds, data.categorical, B)
+    h_gpu = rdf_ops._histogram(gd, label.to(cuda) if cls else None,
+                               None if cls else y.to(cuda), S, cls, weight.to(cuda),
+                               node_of.to(cuda), 0, nodes, feats.to(cuda), B)
+    assert torch.allclose(h_gpu.cpu(), h_cpu, rtol=1e-4, atol=1e-3)
+    # routing: half the nodes split on a random feature/bin, the rest become leaves
+    sf = torch.where(torch.rand(T, nodes, generator=g) < 0.5,
+                     torch.randint(0, P, (T, nodes), generator=g), torch.full((T, nodes), -1))
+    sb = torch.randint(0, B, (T, nodes), generator=g)
+    is_split = sf >= 0
+    rank = torch.cumsum(is_split.int(), 1) - is_split.int()
+    cb = torch.where(is_split, 2 * rank, torch.full_like(rank, -1))
+    split = rdf_ops.LevelSplits(sf, sb, None, torch.zeros(T, nodes, S), torch.zeros(T, nodes))
+    no_c = node_of.clone()
+    v_cpu = rdf_ops._route(data, no_c, nodes, split, cb, B)
+    no_g = node_of.to(cuda)
+    split_g = rdf_ops.LevelSplits(sf.to(cuda), sb.to(cuda), None, split.totals.to(cuda),
+                                  split.gain.to(cuda))
+    v_gpu = rdf_ops._route(gd, no_g, nodes, split_g, cb.to(cuda), B)
+    assert torch.equal(v_gpu.cpu(), v_cpu)
+    assert torch.equal(no_g.cpu(), no_c)
