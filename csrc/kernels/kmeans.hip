@@ -61,18 +61,17 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
       }
     }
   }
-  // per-lane best for rows (rt, g*4 + v)
+  // per-lane best for rows (rt, g*4 + v).  argmin_c |x|^2 + |c|^2 - 2 x.c = argmax_c
+  // (x.c - |c|^2 / 2): the accumulator starts at -|c|^2 / 2 (the lane's center), so the
+  // epilogue is one compare and two selects per value; |x|^2 only enters the final distance.
   float best[ROW_TILES][4];
   int besti[ROW_TILES][4];
-  float xn[ROW_TILES][4];
 #pragma unroll
   for (int rt = 0; rt < ROW_TILES; ++rt)
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      best[rt][v] = INFINITY;
+      best[rt][v] = -INFINITY;
       besti[rt][v] = 0;
-      const long long r = row0 + rt * 16 + g * 4 + v;
-      xn[rt][v] = r < n ? xnorm[r] : 0.f;
     }
 
   const int ntiles = k_pad / BN;
@@ -120,10 +119,11 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
 #pragma unroll
     for (int ct = 0; ct < BN / 16; ++ct) {
       if (ct + 1 < BN / 16) read_b(ct + 1, bfr[(ct + 1) & 1]);
-      const float cn = cnorm[t * BN + ct * 16 + fl];
+      const int c = t * BN + ct * 16 + fl;
+      const float h = -0.5f * cnorm[c];       // +inf padding rows -> -inf, never chosen
       f32x4 acc[ROW_TILES];
 #pragma unroll
-      for (int rt = 0; rt < ROW_TILES; ++rt) acc[rt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int rt = 0; rt < ROW_TILES; ++rt) acc[rt] = f32x4{h, h, h, h};
 #pragma unroll
       for (int s = 0; s < DK; ++s) {
 #pragma unroll
@@ -132,14 +132,12 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
                                                             0, 0, 0);
       }
       // C/D layout: col = fl (center), row = g*4 + v (point)
-      const int c = t * BN + ct * 16 + fl;
 #pragma unroll
       for (int rt = 0; rt < ROW_TILES; ++rt)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const float d = xn[rt][v] + cn - 2.f * acc[rt][v];
-          if (d < best[rt][v]) {
-            best[rt][v] = d;
+          if (acc[rt][v] > best[rt][v]) {
+            best[rt][v] = acc[rt][v];
             besti[rt][v] = c;
           }
         }
@@ -161,15 +159,16 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
       for (int off = 1; off < 16; off <<= 1) {
         const float ov = __shfl_xor(bv, off, 64);
         const int oi = __shfl_xor(bi, off, 64);
-        if (ov < bv || (ov == bv && oi < bi)) {
+        if (ov > bv || (ov == bv && oi < bi)) {
           bv = ov;
           bi = oi;
         }
       }
       const long long r = row0 + rt * 16 + g * 4 + v;
       if (fl == 0 && r < n) {
+        const float d = xnorm[r] - 2.f * bv;
         assign[r] = bi;
-        mind[r] = bv > 0.f ? bv : 0.f;
+        mind[r] = d > 0.f ? d : 0.f;
       }
     }
 }
@@ -316,6 +315,195 @@ __global__ __launch_bounds__(1024) void kmeans_accumulate_lds_kernel(
   }
 }
 
+// ---- sort-based accumulation (counting sort by cluster + segmented row sums) ----
+// LDS float atomics run at a fraction of a lane per cycle, so with K = 1000 and d = 256 the
+// 3.2G (row, column) adds of one Lloyd step dominate.  Instead: (1) per-block cluster
+// histograms, (2) per-cluster prefix offsets over blocks, (3) scatter of row ids into cluster
+// order (integer LDS cursors, one per row), (4) one workgroup per (cluster, piece of
+// PIECE rows) summing its rows -- a 1 KB coalesced row read per step, fp32 register
+// accumulation, one global atomic per column per piece.  X is read once, in row order per
+// cluster; counts come out of the scan exactly (no atomics).
+constexpr int SORT_BLOCKS = 512;
+constexpr int PIECE = 2048;
+
+__global__ __launch_bounds__(256) void km_block_hist(const int* __restrict__ assign, long long n,
+                                                     int k, long long rpb,
+                                                     unsigned int* __restrict__ bh) {
+  extern __shared__ unsigned int h[];
+  for (int i = threadIdx.x; i < k; i += 256) h[i] = 0u;
+  __syncthreads();
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const long long r1 = r0 + rpb < n ? r0 + rpb : n;
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256) atomicAdd(h + assign[r], 1u);
+  __syncthreads();
+  unsigned int* out = bh + (long long)blockIdx.x * k;
+  for (int i = threadIdx.x; i < k; i += 256) out[i] = h[i];
+}
+
+// per cluster: running sum over blocks (bh becomes the block's start within the cluster);
+// 16 block rows are loaded per step so the loop is not one HBM round trip per block
+__global__ __launch_bounds__(256) void km_cluster_scan(unsigned int* __restrict__ bh, int nb,
+                                                       int k,
+                                                       unsigned long long* __restrict__ counts) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= k) return;
+  unsigned int run = 0;
+  constexpr int V = 16;
+  for (int b0 = 0; b0 < nb; b0 += V) {
+    unsigned int v[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u) v[u] = b0 + u < nb ? bh[(long long)(b0 + u) * k + c] : 0u;
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+      if (b0 + u < nb) bh[(long long)(b0 + u) * k + c] = run;
+      run += v[u];
+    }
+  }
+  counts[c] = run;
+}
+
+// one block: exclusive scan of counts -> off[c]; pieces_prefix[c] = pieces before cluster c
+__global__ __launch_bounds__(1024) void km_offsets(const unsigned long long* __restrict__ counts,
+                                                   int k, long long* __restrict__ off,
+                                                   int* __restrict__ pieces) {
+  __shared__ long long s_off[1024];
+  __shared__ int s_pc[1024];
+  __shared__ long long carry_off;
+  __shared__ int carry_pc;
+  if (threadIdx.x == 0) {
+    carry_off = 0;
+    carry_pc = 0;
+  }
+  __syncthreads();
+  for (int base = 0; base < k; base += 1024) {
+    const int c = base + threadIdx.x;
+    const long long cnt = c < k ? (long long)counts[c] : 0;
+    s_off[threadIdx.x] = cnt;
+    s_pc[threadIdx.x] = (int)((cnt + PIECE - 1) / PIECE);
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {      // Hillis-Steele inclusive scan
+      long long a = 0;
+      int b = 0;
+      if (threadIdx.x >= d) {
+        a = s_off[threadIdx.x - d];
+        b = s_pc[threadIdx.x - d];
+      }
+      __syncthreads();
+      s_off[threadIdx.x] += a;
+      s_pc[threadIdx.x] += b;
+      __syncthreads();
+    }
+    if (c < k) {
+      off[c] = carry_off + s_off[threadIdx.x] - cnt;
+      pieces[c] = carry_pc + s_pc[threadIdx.x] - (int)((cnt + PIECE - 1) / PIECE);
+    }
+    __syncthreads();
+    if (threadIdx.x == 1023) {
+      carry_off += s_off[1023];
+      carry_pc += s_pc[1023];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) pieces[k] = carry_pc;
+}
+
+__global__ __launch_bounds__(256) void km_scatter(const int* __restrict__ assign, long long n,
+                                                  int k, long long rpb,
+                                                  const unsigned int* __restrict__ bh,
+                                                  const long long* __restrict__ off,
+                                                  int* __restrict__ perm) {
+  extern __shared__ unsigned int cur[];
+  const unsigned int* start = bh + (long long)blockIdx.x * k;
+  for (int i = threadIdx.x; i < k; i += 256) cur[i] = start[i];
+  __syncthreads();
+  const long long r0 = (long long)blockIdx.x * rpb;
+  const long long r1 = r0 + rpb < n ? r0 + rpb : n;
+  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
+    const int c = assign[r];
+    const unsigned int slot = atomicAdd(cur + c, 1u);
+    perm[off[c] + slot] = (int)r;
+  }
+}
+
+// block = one piece of one cluster; T threads per row (power of two >= d, <= 256), 256 / T
+// rows in flight, U rows unrolled per thread so the row loads overlap
+template <bool STATS>
+__global__ __launch_bounds__(256) void km_segment_sum(
+    const float* __restrict__ X, const float* __restrict__ mind, int d, int ld, int k,
+    const int* __restrict__ perm, const unsigned long long* __restrict__ counts,
+    const long long* __restrict__ off, const int* __restrict__ pieces, int tpr,
+    float* __restrict__ sums, double* __restrict__ dstats) {
+  __shared__ float red[256];
+  __shared__ double dred[256];
+  const int total = pieces[k];
+  const int p = blockIdx.x;
+  if (p >= total) return;
+  // cluster of this piece: last c with pieces[c] <= p
+  int lo = 0, hi = k - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (pieces[mid] <= p) lo = mid; else hi = mid - 1;
+  }
+  const int c = lo;
+  const long long cnt = (long long)counts[c];
+  const long long i0 = (long long)(p - pieces[c]) * PIECE;
+  const long long i1 = i0 + PIECE < cnt ? i0 + PIECE : cnt;
+  const int* rows = perm + off[c];
+  const int rpp = 256 / tpr;
+  const int sub = threadIdx.x / tpr, col = threadIdx.x % tpr;
+  constexpr int U = 8;
+  for (int cb = 0; cb < d; cb += tpr) {
+    const int j = cb + col;
+    float acc = 0.f;
+    double dacc = 0.0;
+    for (long long i = i0 + sub; i < i1; i += (long long)U * rpp) {
+      int r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long ii = i + (long long)u * rpp;
+        r[u] = ii < i1 ? rows[ii] : -1;
+      }
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        v[u] = (r[u] >= 0 && j < d) ? X[(long long)r[u] * ld + j] : 0.f;
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc += v[u];
+      if (STATS && cb == 0 && col == 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (r[u] >= 0) dacc += sqrt((double)mind[r[u]]);
+      }
+    }
+    red[threadIdx.x] = acc;
+    if (STATS && cb == 0) dred[threadIdx.x] = dacc;
+    __syncthreads();
+    if (sub == 0) {
+      float s = 0.f;
+      for (int q = 0; q < rpp; ++q) s += red[q * tpr + col];
+      if (j < d && s != 0.f) atomicAdd(sums + (long long)c * d + j, s);
+    }
+    if (STATS && cb == 0 && threadIdx.x == 0) {
+      double s = 0.0;
+      for (int q = 0; q < rpp; ++q) s += dred[q * tpr];
+      atomicAdd(dstats + 2 * c, s);
+    }
+    __syncthreads();
+  }
+  // sum of squared distances (= sum of mind) in a second light pass over the piece's rows
+  if (STATS) {
+    double s2 = 0.0;
+    for (long long i = i0 + threadIdx.x; i < i1; i += 256) s2 += (double)mind[rows[i]];
+    dred[threadIdx.x] = s2;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (threadIdx.x < w) dred[threadIdx.x] += dred[threadIdx.x + w];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicAdd(dstats + 2 * c + 1, dred[0]);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -435,6 +623,49 @@ int oryx_kmeans_accumulate(const float* X, const int* assign, const float* mind,
   const int blocks = (int)((waves + 3) / 4);
   hipLaunchKernelGGL(kmeans_accumulate_kernel, dim3(blocks), dim3(256), 0, s, X, assign, mind,
                      n, d, ld, sums, counts, dstats);
+  return oryx_check_launch();
+}
+
+// Workspace bytes for oryx_kmeans_accumulate_sorted.
+long long oryx_kmeans_sorted_ws_bytes(long long n, int k) {
+  return (long long)SORT_BLOCKS * k * 4 + (long long)k * 8 + (long long)(k + 1) * 4 + n * 4 + 64;
+}
+
+// Sort-based accumulation (see km_segment_sum): sums fp32 [k][d] and dstats f64 [k][2] must be
+// zeroed; counts u64 [k] is written (not accumulated).  ws: oryx_kmeans_sorted_ws_bytes.
+int oryx_kmeans_accumulate_sorted(const float* X, const int* assign, const float* mind,
+                                  long long n, int d, int ld, int k, float* sums,
+                                  unsigned long long* counts, double* dstats, void* ws,
+                                  void* stream) {
+  if (n <= 0) return ORYX_OK;
+  if (k <= 0 || (long long)k * 4 > 64 * 1024 || n >= (1ll << 31)) return ORYX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  char* w = reinterpret_cast<char*>(ws);
+  unsigned int* bh = reinterpret_cast<unsigned int*>(w);
+  w += (long long)SORT_BLOCKS * k * 4;
+  long long* off = reinterpret_cast<long long*>(w);
+  w += (long long)k * 8;
+  int* pieces = reinterpret_cast<int*>(w);
+  w += (long long)(k + 1) * 4;
+  int* perm = reinterpret_cast<int*>(w);
+  const long long rpb = (n + SORT_BLOCKS - 1) / SORT_BLOCKS;
+  const size_t hsm = (size_t)k * 4;
+  hipLaunchKernelGGL(km_block_hist, dim3(SORT_BLOCKS), dim3(256), hsm, s, assign, n, k, rpb, bh);
+  hipLaunchKernelGGL(km_cluster_scan, dim3((k + 255) / 256), dim3(256), 0, s, bh, SORT_BLOCKS, k,
+                     counts);
+  hipLaunchKernelGGL(km_offsets, dim3(1), dim3(1024), 0, s, counts, k, off, pieces);
+  hipLaunchKernelGGL(km_scatter, dim3(SORT_BLOCKS), dim3(256), hsm, s, assign, n, k, rpb, bh, off,
+                     perm);
+  int tpr = 1;
+  while (tpr < d && tpr < 256) tpr <<= 1;
+  if (tpr < 1) tpr = 1;
+  const long long max_pieces = (n + PIECE - 1) / PIECE + k;
+  if (dstats)
+    hipLaunchKernelGGL(km_segment_sum<true>, dim3((unsigned)max_pieces), dim3(256), 0, s, X,
+                       mind, d, ld, k, perm, counts, off, pieces, tpr, sums, dstats);
+  else
+    hipLaunchKernelGGL(km_segment_sum<false>, dim3((unsigned)max_pieces), dim3(256), 0, s, X,
+                       mind, d, ld, k, perm, counts, off, pieces, tpr, sums, dstats);
   return oryx_check_launch();
 }
 

@@ -27,6 +27,7 @@
 #include <cstring>
 #include <dirent.h>
 #include <fcntl.h>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <sys/file.h>
@@ -128,6 +129,10 @@ uint32_t murmur2(const uint8_t* data, int len) {
 struct Partition {
   std::string dir;
   int lock_fd = -1;
+  // flock() excludes other processes (and other handles); threads sharing this handle also
+  // share the lock's open file description, for which flock is a no-op, so appends through
+  // one handle are serialised by this mutex as well
+  std::shared_ptr<std::mutex> mu = std::make_shared<std::mutex>();
   // cached tail of the active segment (validated under the lock on every append)
   int64_t c_base = -1, c_pos = 0, c_next = 0;
 };
@@ -341,6 +346,7 @@ long long oryx_log_append_batch(void* h, int partition, const char* buf, long lo
   for (int part = 0; part < t->partitions; ++part) {
     if (idx[part].empty()) continue;
     Partition& P = t->parts[part];
+    std::lock_guard<std::mutex> in_process(*P.mu);
     if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_EX);
     std::vector<int64_t> segs = list_segments(P.dir);
     int64_t base = segs.empty() ? 0 : segs.back();

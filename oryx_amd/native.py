@@ -117,6 +117,9 @@ def _load_kernels():
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
                                           c_vp])
+    _sig(lib, "oryx_kmeans_sorted_ws_bytes", c_ll, [c_ll, c_i])
+    _sig(lib, "oryx_kmeans_accumulate_sorted", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i,
+                                                     c_vp, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_accumulate", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i, c_vp,
                                               c_vp, c_vp, c_vp])
     # Xb, bin_bytes, n, P, label, y, S, cls, weight, T, node_of, node_lo, nodes, feats, Fs, B,

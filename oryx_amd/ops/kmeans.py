@@ -17,6 +17,7 @@ clusters keep their previous center; best of ``runs`` by cost.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -31,6 +32,8 @@ __all__ = ["assign", "accumulate", "kmeans_train", "lloyd_step", "PointSet", "KM
            "pairwise_distances"]
 
 _CHUNK = 1 << 20
+# GPU centroid accumulation: sort-based (default) or LDS-atomic (ORYX_KMEANS_ACCUM=atomic)
+_SORTED = os.environ.get("ORYX_KMEANS_ACCUM", "sorted") != "atomic"
 
 
 def _pad_to(n: int, m: int) -> int:
@@ -153,10 +156,19 @@ def accumulate(x: torch.Tensor, idx: torch.Tensor, k: int,
         ia = idx if idx.dtype == torch.int32 and idx.is_contiguous() else \
             idx.to(torch.int32).contiguous()
         md = mind.to(torch.float32).contiguous() if mind is not None else None
-        rc = lib.oryx_kmeans_accumulate(xf.data_ptr(), ia.data_ptr(),
-                                        md.data_ptr() if md is not None else None, n, d, d, k,
-                                        sums.data_ptr(), counts.data_ptr(),
-                                        stats.data_ptr() if stats is not None else None,
+        mdp = md.data_ptr() if md is not None else None
+        stp = stats.data_ptr() if stats is not None else None
+        if _SORTED and 0 < k <= 16384 and n < (1 << 31):
+            # counting sort by cluster + segmented row sums (no float atomics per element)
+            ws = torch.empty(int(lib.oryx_kmeans_sorted_ws_bytes(n, k)), dtype=torch.uint8,
+                             device=dev)
+            rc = lib.oryx_kmeans_accumulate_sorted(xf.data_ptr(), ia.data_ptr(), mdp, n, d, d,
+                                                   k, sums.data_ptr(), counts.data_ptr(), stp,
+                                                   ws.data_ptr(), native.stream_ptr(dev))
+            native.check(rc, "oryx_kmeans_accumulate_sorted")
+            return sums, counts, stats
+        rc = lib.oryx_kmeans_accumulate(xf.data_ptr(), ia.data_ptr(), mdp, n, d, d, k,
+                                        sums.data_ptr(), counts.data_ptr(), stp,
                                         native.stream_ptr(dev))
         native.check(rc, "oryx_kmeans_accumulate")
         return sums, counts, stats

@@ -448,10 +448,14 @@ def test_eval_metrics_gpu_match_cpu(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,d,k", [(50000, 256, 1000), (30000, 37, 300), (20000, 16, 9000)])
-def test_accumulate_kernel_lds_slices(cuda, n, d, k):
-    """LDS column-slice path (k=1000 d=256: 8 slices; d < slice width) and the L2-atomic
+@pytest.mark.parametrize("sorted_path", [True, False])
+@pytest.mark.parametrize("n,d,k", [(50000, 256, 1000), (30000, 37, 300), (20000, 16, 9000),
+                                   (70000, 300, 5)])
+def test_accumulate_kernel_lds_slices(cuda, n, d, k, sorted_path, monkeypatch):
+    """Sort-based segmented sums (clusters split into 2048-row pieces; d > 256 columns), the
+    LDS column-slice path (k=1000 d=256: 8 slices; d < slice width) and the L2-atomic
     fallback (k=9000 does not fit LDS) against index_add."""
+    monkeypatch.setattr(km, "_SORTED", sorted_path)
     g = torch.Generator().manual_seed(n + d + k)
     x = torch.randn(n, d, generator=g)
     idx = torch.randint(0, k, (n,), generator=g)
