@@ -626,6 +626,33 @@ int oryx_kmeans_accumulate(const float* X, const int* assign, const float* mind,
   return oryx_check_launch();
 }
 
+// Generic counting sort: perm lists 0..n-1 grouped by key (keys in [0, k), k * 4 bytes of
+// LDS, so k <= 16384); counts[k] = group sizes; group c occupies [off[c], off[c] + counts[c])
+// with off returned in ws (first k * 8 bytes after the block histograms; see
+// oryx_counting_sort_offsets).  Order within a group is unspecified.  ws:
+// oryx_kmeans_sorted_ws_bytes(n, k) bytes.
+int oryx_counting_sort(const int* keys, long long n, int k, int* perm, unsigned long long* counts,
+                       void* ws, void* stream) {
+  if (n <= 0) return ORYX_OK;
+  if (k <= 0 || k > 16384 || n >= (1ll << 31)) return ORYX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  char* w = reinterpret_cast<char*>(ws);
+  unsigned int* bh = reinterpret_cast<unsigned int*>(w);
+  w += (long long)SORT_BLOCKS * k * 4;
+  long long* off = reinterpret_cast<long long*>(w);
+  w += (long long)k * 8;
+  int* pieces = reinterpret_cast<int*>(w);
+  const long long rpb = (n + SORT_BLOCKS - 1) / SORT_BLOCKS;
+  const size_t hsm = (size_t)k * 4;
+  hipLaunchKernelGGL(km_block_hist, dim3(SORT_BLOCKS), dim3(256), hsm, s, keys, n, k, rpb, bh);
+  hipLaunchKernelGGL(km_cluster_scan, dim3((k + 255) / 256), dim3(256), 0, s, bh, SORT_BLOCKS, k,
+                     counts);
+  hipLaunchKernelGGL(km_offsets, dim3(1), dim3(1024), 0, s, counts, k, off, pieces);
+  hipLaunchKernelGGL(km_scatter, dim3(SORT_BLOCKS), dim3(256), hsm, s, keys, n, k, rpb, bh, off,
+                     perm);
+  return oryx_check_launch();
+}
+
 // Workspace bytes for oryx_kmeans_accumulate_sorted.
 long long oryx_kmeans_sorted_ws_bytes(long long n, int k) {
   return (long long)SORT_BLOCKS * k * 4 + (long long)k * 8 + (long long)(k + 1) * 4 + n * 4 + 64;

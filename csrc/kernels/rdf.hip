@@ -149,6 +149,85 @@ __global__ __launch_bounds__(256) void rdf_route(const BinT* __restrict__ Xb, lo
   }
 }
 
+// Segmented level histogram: rows are kept grouped by (tree, node) -- a counting sort of the
+// routed rows after every level (oryx_counting_sort) -- so a workgroup owns one PIECE of one
+// node's rows: it reads only those rows (row ids through the permutation), accumulates the
+// node's Fs x B x S histogram in LDS (8 KB for 10 features x 100 bins x 2 classes, so many
+// workgroups share a CU), and flushes it once.  Versus scanning every row once per node chunk
+// (rdf_histogram) the deep levels do no skipped-row work and the LDS image stays small.
+// perm: indices into the flattened [T][n] row space (nullptr: identity), pieces: per piece
+// (tree, node slot relative to node_lo, begin, end) positions into perm.
+template <typename BinT, bool CLS, bool USE_LDS>
+__global__ __launch_bounds__(256) void rdf_histogram_pieces(
+    const BinT* __restrict__ Xb, long long n, int P, const int* __restrict__ label,
+    const float* __restrict__ y, int S, const unsigned char* __restrict__ weight,
+    const int* __restrict__ perm, const int* __restrict__ piece_tree,
+    const int* __restrict__ piece_node, const long long* __restrict__ piece_lo,
+    const long long* __restrict__ piece_hi, int nodes, const int* __restrict__ feats, int Fs,
+    int B, float* __restrict__ hist) {
+  extern __shared__ float lh[];
+  const int pc = blockIdx.x;
+  const int t = piece_tree[pc];
+  const int node = piece_node[pc];
+  const long long per_node = (long long)Fs * B * S;
+  float* gh = hist + ((long long)t * nodes + node) * per_node;
+  float* base = USE_LDS ? lh : gh;
+  if (USE_LDS) {
+    for (long long i = threadIdx.x; i < per_node; i += 256) lh[i] = 0.f;
+    __syncthreads();
+  }
+  const int* fj = feats + ((long long)t * nodes + node) * Fs;
+  const long long p0 = piece_lo[pc], p1 = piece_hi[pc];
+  const long long toff = (long long)t * n;
+  constexpr int U = 4;
+  for (long long q = p0 + threadIdx.x; q < p1; q += 256 * U) {
+    long long row[U];
+    float w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long qq = q + (long long)u * 256;
+      row[u] = qq < p1 ? (perm ? (long long)perm[qq] - toff : qq - toff) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      w[u] = row[u] >= 0 ? (weight ? (float)weight[toff + row[u]] : 1.f) : 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (w[u] == 0.f) continue;
+      const long long i = row[u];
+      int s0;
+      float v0 = w[u], v1 = 0.f, v2 = 0.f;
+      if (CLS) {
+        s0 = label[i];
+      } else {
+        s0 = 0;
+        const float yi = y[i];
+        v1 = v0 * yi;
+        v2 = v0 * yi * yi;
+      }
+      const BinT* xr = Xb + i * P;
+      for (int j = 0; j < Fs; ++j) {
+        const int b = (int)xr[fj[j]];
+        float* h = base + ((long long)j * B + b) * S;
+        if (CLS) {
+          atomicAdd(h + s0, v0);
+        } else {
+          atomicAdd(h, v0);
+          atomicAdd(h + 1, v1);
+          atomicAdd(h + 2, v2);
+        }
+      }
+    }
+  }
+  if (USE_LDS) {
+    __syncthreads();
+    for (long long k = threadIdx.x; k < per_node; k += 256) {
+      const float v = lh[k];
+      if (v != 0.f) atomicAdd(gh + k, v);
+    }
+  }
+}
+
 // Flattened forest scoring: per (example, tree) walk from the tree's root to a leaf.
 // feat[node] (-1 leaf), thr[node] (numeric: x >= thr goes right, i.e. the positive child),
 // cat_off[node] (>= 0: categorical, bit table at cat_bits[cat_off + encoding]),
@@ -271,6 +350,42 @@ int oryx_rdf_route(const void* Xb, int bin_bytes, long long n, int P, int T, int
     return ORYX_EINVAL;
   }
 #undef ROUTE_LAUNCH
+  return oryx_check_launch();
+}
+
+int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
+                              const int* label, const float* y, int S, int cls,
+                              const unsigned char* weight, const int* perm,
+                              const int* piece_tree, const int* piece_node,
+                              const long long* piece_lo, const long long* piece_hi,
+                              int n_pieces, int nodes, const int* feats, int Fs, int B,
+                              float* hist, void* stream) {
+  if (n_pieces <= 0) return ORYX_OK;
+  if ((bin_bytes != 1 && bin_bytes != 2) || (cls && !label) || (!cls && (!y || S != 3)))
+    return ORYX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const long long per_node_bytes = (long long)Fs * B * S * 4;
+  const bool lds = per_node_bytes <= 64 * 1024;
+  const size_t smem = lds ? (size_t)per_node_bytes : 0;
+#define PIECE_LAUNCH(BT, C, L)                                                                \
+  hipLaunchKernelGGL((rdf_histogram_pieces<BT, C, L>), dim3((unsigned)n_pieces), dim3(256),  \
+                     smem, s, reinterpret_cast<const BT*>(Xb), n, P, label, y, S, weight,     \
+                     perm, piece_tree, piece_node, piece_lo, piece_hi, nodes, feats, Fs, B,   \
+                     hist)
+  if (bin_bytes == 1) {
+    if (cls) {
+      if (lds) PIECE_LAUNCH(unsigned char, true, true); else PIECE_LAUNCH(unsigned char, true, false);
+    } else {
+      if (lds) PIECE_LAUNCH(unsigned char, false, true); else PIECE_LAUNCH(unsigned char, false, false);
+    }
+  } else {
+    if (cls) {
+      if (lds) PIECE_LAUNCH(short, true, true); else PIECE_LAUNCH(short, true, false);
+    } else {
+      if (lds) PIECE_LAUNCH(short, false, true); else PIECE_LAUNCH(short, false, false);
+    }
+  }
+#undef PIECE_LAUNCH
   return oryx_check_launch();
 }
 

@@ -117,6 +117,10 @@ def _load_kernels():
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
                                           c_vp])
+    _sig(lib, "oryx_counting_sort", c_i, [c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_rdf_histogram_pieces", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i,
+                                                 c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
+                                                 c_vp, c_i, c_i, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_sorted_ws_bytes", c_ll, [c_ll, c_i])
     _sig(lib, "oryx_kmeans_accumulate_sorted", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i,
                                                      c_vp, c_vp, c_vp, c_vp, c_vp])

@@ -28,6 +28,7 @@ On CPU the same algorithm runs with ``index_add`` (tests / the ``local[*]`` plum
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -42,6 +43,9 @@ __all__ = ["BinnedData", "bin_features", "train_forest", "TrainedForest", "FlatF
            "flatten_forest", "forest_leaves"]
 
 _HIST_BUDGET = 1 << 26          # floats per histogram pass (256 MB)
+# GPU level histograms from rows grouped by node (counting sort per level); ORYX_RDF_GROUPED=0
+# selects the scan-all-rows kernel
+_GROUPED = os.environ.get("ORYX_RDF_GROUPED", "1") != "0"
 
 
 @dataclass
@@ -248,6 +252,94 @@ def _histogram(data: BinnedData, label, y, S, cls, weight, node_of, lo, nodes, f
     return hist
 
 
+_PIECE = 4096          # rows per workgroup in the segmented histogram
+_SORT_MAX_KEYS = 16384
+
+
+class RowGroups:
+    """Rows of every tree grouped by their open node at the current level (GPU path): a
+    permutation of the flattened [T][n] row space plus per-(tree, node) counts/offsets."""
+
+    def __init__(self, perm: Optional[torch.Tensor], counts: np.ndarray, width: int, n: int):
+        self.perm = perm                      # int32 [T*n] (None: identity, one node per tree)
+        self.counts = counts                  # int64 [T, width]
+        self.width = width
+        self.n = n
+        flat = counts.reshape(-1)
+        self.offsets = (np.cumsum(flat) - flat).reshape(counts.shape)
+
+    @staticmethod
+    def root(T: int, n: int) -> "RowGroups":
+        g = RowGroups(None, np.full((T, 1), n, dtype=np.int64), 1, n)
+        g.offsets = (np.arange(T, dtype=np.int64) * n)[:, None]
+        return g
+
+    @staticmethod
+    def from_nodes(node_of: torch.Tensor, width: int) -> Optional["RowGroups"]:
+        """Counting sort of the rows by (tree, node); None when the key space is too wide."""
+        T, n = node_of.shape
+        k = T * width + 1                     # last key: rows that reached a leaf
+        if k > _SORT_MAX_KEYS or T * n >= (1 << 31):
+            return None
+        dev = node_of.device
+        lib = native.require_kernels()
+        tt = torch.arange(T, device=dev, dtype=torch.int32)[:, None] * width
+        keys = torch.where(node_of >= 0, node_of + tt, torch.full_like(node_of, k - 1))
+        keys = keys.reshape(-1).contiguous()
+        perm = torch.empty(T * n, dtype=torch.int32, device=dev)
+        counts = torch.empty(k, dtype=torch.int64, device=dev)
+        ws = torch.empty(int(lib.oryx_kmeans_sorted_ws_bytes(T * n, k)), dtype=torch.uint8,
+                         device=dev)
+        rc = lib.oryx_counting_sort(keys.data_ptr(), T * n, k, perm.data_ptr(),
+                                    counts.data_ptr(), ws.data_ptr(), native.stream_ptr(dev))
+        native.check(rc, "oryx_counting_sort")
+        c = counts.cpu().numpy()[:-1].reshape(T, width)
+        return RowGroups(perm, c, width, n)
+
+    def pieces(self, lo: int, hi: int, dev):
+        """(tree, node - lo, begin, end) of every PIECE-row slice of nodes [lo, hi)."""
+        cnt = self.counts[:, lo:hi]
+        off = self.offsets[:, lo:hi]
+        npc = (cnt + _PIECE - 1) // _PIECE
+        tot = int(npc.sum())
+        if tot == 0:
+            return None
+        T, W = cnt.shape
+        t_idx = np.repeat(np.repeat(np.arange(T), W), npc.reshape(-1))
+        n_idx = np.repeat(np.tile(np.arange(W), T), npc.reshape(-1))
+        first = np.repeat(np.cumsum(npc.reshape(-1)) - npc.reshape(-1), npc.reshape(-1))
+        k = np.arange(tot) - first
+        begin = np.repeat(off.reshape(-1), npc.reshape(-1)) + k * _PIECE
+        end = np.minimum(begin + _PIECE, np.repeat((off + cnt).reshape(-1), npc.reshape(-1)))
+        to = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a.astype(dt))).to(dev)
+        return (to(t_idx, np.int32), to(n_idx, np.int32), to(begin, np.int64),
+                to(end, np.int64), tot)
+
+
+def _histogram_groups(data: BinnedData, label, y, S, cls, weight, groups: RowGroups, lo, nodes,
+                      feats, B, T):
+    """Level histogram of node slots [lo, lo + nodes) from grouped rows (GPU)."""
+    Fs = feats.shape[2]
+    dev = data.Xb.device
+    hist = torch.zeros((T, nodes, Fs, B, S), dtype=torch.float32, device=dev)
+    pc = groups.pieces(lo, lo + nodes, dev)
+    if pc is None:
+        return hist
+    pt, pn, pb, pe, tot = pc
+    n, P = data.Xb.shape
+    lib = native.require_kernels()
+    fe = feats.contiguous()
+    rc = lib.oryx_rdf_histogram_pieces(
+        data.Xb.data_ptr(), data.bin_bytes, n, P, label.data_ptr() if cls else None,
+        None if cls else y.data_ptr(), S, int(cls),
+        weight.data_ptr() if weight is not None else None,
+        groups.perm.data_ptr() if groups.perm is not None else None,
+        pt.data_ptr(), pn.data_ptr(), pb.data_ptr(), pe.data_ptr(), tot, nodes, fe.data_ptr(),
+        Fs, B, hist.data_ptr(), native.stream_ptr(dev))
+    native.check(rc, "oryx_rdf_histogram_pieces")
+    return hist
+
+
 def _route(data: BinnedData, node_of, nodes, split: LevelSplits, child_base, B):
     T, n = node_of.shape
     dev = node_of.device
@@ -348,7 +440,10 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     level_nodes: List[List[Optional[TrainedNode]]] = [[r] for r in roots]
     predictor_counts = np.zeros(P, dtype=np.float64)
     nodes = 1
+    groups = RowGroups.root(T, n) if dev.type == "cuda" and _GROUPED else None
     for depth in range(max_depth + 1):
+        if depth > 0 and groups is not None:
+            groups = RowGroups.from_nodes(node_of, nodes)
         faults.point("rdf.level", depth=depth, rank=ctx.rank)
         watchdog.heartbeat("rdf.level")
         if Fs < P:
@@ -361,8 +456,12 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
         splits = []
         for lo in range(0, nodes, chunk):
             hi = min(nodes, lo + chunk)
-            hist = _histogram(data, label, y, S, classification, weight, node_of, lo, hi - lo,
-                              feats[:, lo:hi], B)
+            if groups is not None:
+                hist = _histogram_groups(data, label, y, S, classification, weight, groups, lo,
+                                         hi - lo, feats[:, lo:hi], B, T)
+            else:
+                hist = _histogram(data, label, y, S, classification, weight, node_of, lo,
+                                  hi - lo, feats[:, lo:hi], B)
             if ctx.is_distributed:
                 dist.all_reduce_sum(hist, ctx)
             splits.append(_choose_splits(hist, feats[:, lo:hi], data, kind,

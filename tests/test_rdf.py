@@ -438,6 +438,24 @@ def test_histogram_and_route_kernels_match_cpu(cuda, cls):
                                None if cls else y.to(cuda), S, cls, weight.to(cuda),
                                node_of.to(cuda), 0, nodes, feats.to(cuda), B)
     assert torch.allclose(h_gpu.cpu(), h_cpu, rtol=1e-4, atol=1e-3)
+    # grouped rows (counting sort by (tree, node)) through the segmented kernel, in two node
+    # chunks
+    groups = rdf_ops.RowGroups.from_nodes(node_of.to(cuda), nodes)
+    assert groups is not None
+    assert int(groups.counts.sum()) == int((node_of >= 0).sum())
+    h_grp = torch.cat([rdf_ops._histogram_groups(
+        gd, label.to(cuda) if cls else None, None if cls else y.to(cuda), S, cls,
+        weight.to(cuda), groups, lo, hi - lo, feats[:, lo:hi].to(cuda), B, T)
+        for lo, hi in ((0, 77), (77, nodes))], 1)
+    assert torch.allclose(h_grp.cpu(), h_cpu, rtol=1e-4, atol=1e-3)
+    root = rdf_ops.RowGroups.root(T, n)
+    h_root = rdf_ops._histogram_groups(gd, label.to(cuda) if cls else None,
+                                       None if cls else y.to(cuda), S, cls, weight.to(cuda),
+                                       root, 0, 1, feats[:, :1].to(cuda), B, T)
+    h_root_cpu = rdf_ops._histogram(data, label, y, S, cls, weight,
+                                    torch.zeros((T, n), dtype=torch.int32), 0, 1, feats[:, :1],
+                                    B)
+    assert torch.allclose(h_root.cpu(), h_root_cpu, rtol=1e-4, atol=1e-2)
     # routing: half the nodes split on a random feature/bin, the rest become leaves
     sf = torch.where(torch.rand(T, nodes, generator=g) < 0.5,
                      torch.randint(0, P, (T, nodes), generator=g), torch.full((T, nodes), -1))
