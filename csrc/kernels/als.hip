@@ -27,6 +27,10 @@
 
 #include "common.h"
 
+#ifndef ORYX_ALS_CHOL_LDS
+#define ORYX_ALS_CHOL_LDS 1
+#endif
+
 namespace {
 
 struct AlsParams {
@@ -368,6 +372,14 @@ __global__ __launch_bounds__(256) void als_solve_wave(AlsParams p, unsigned long
     int ln = lane;
     asm volatile("" : "+v"(ln));
     float dinv = 0.f;
+#if ORYX_ALS_CHOL_LDS
+    // the column of L goes through LDS: one ds_write_b32 per step, then broadcast
+    // ds_read_b128 (all lanes read the same 16 bytes) of the trailing entries -- the rank-1
+    // update's FMAs take VGPR operands instead of one v_readlane (+ SGPR hazard) each.  A's
+    // LDS image is dead during the factorization, so its first row is the broadcast buffer.
+    typedef __attribute__((address_space(3))) float lds_float;
+    lds_float* bc = (lds_float*)(A);
+#endif
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
       float s = oryx_readlane(a[j], j);
@@ -380,11 +392,29 @@ __global__ __launch_bounds__(256) void als_solve_wave(AlsParams p, unsigned long
       l = ln < j ? 0.f : (ln == j ? d : l);
       dinv = ln == j ? inv : dinv;
       a[j] = l;
+#if ORYX_ALS_CHOL_LDS
+      if (j + 1 < KP) {
+        bc[c] = l;      // lanes >= KP (KP < 64) rewrite slot 0, which is never read back
+        // each updated entry passes through an empty asm: otherwise the SLP vectoriser fuses
+        // the straight-line updates into vector ops on a[] and the array lands in scratch
+        // all broadcast reads first (16-byte, in flight together), then the FMAs
+        f32x4 bv[KP / 4];
+#pragma unroll
+        for (int i4 = (j + 1) / 4; i4 < KP / 4; ++i4)
+          bv[i4] = *reinterpret_cast<const __attribute__((address_space(3))) f32x4*>(bc + 4 * i4);
+#pragma unroll
+        for (int i = j + 1; i < KP; ++i) {
+          a[i] -= bv[i / 4][i % 4] * l;
+          asm volatile("" : "+v"(a[i]));
+        }
+      }
+#else
 #pragma unroll
       for (int i = j + 1; i < KP; ++i) {
         a[i] -= oryx_readlane(l, i) * l;
         if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
       }
+#endif
       // pin the updated trailing column values here: without this LLVM sinks the rank-1
       // updates into a left-looking form that keeps every broadcast L column live (spills)
 #pragma unroll

@@ -275,16 +275,22 @@ class RowGroups:
         return g
 
     @staticmethod
-    def from_nodes(node_of: torch.Tensor, width: int) -> Optional["RowGroups"]:
-        """Counting sort of the rows by (tree, node); None when the key space is too wide."""
+    def from_nodes(node_of: torch.Tensor, width: int,
+                   weight: Optional[torch.Tensor] = None) -> Optional["RowGroups"]:
+        """Counting sort of the rows by (tree, node); None when the key space is too wide.
+        Rows that reached a leaf, and rows a tree's bootstrap left out (weight 0: they only
+        count as node visits, which routing tallies over all rows), go to a last, unused key."""
         T, n = node_of.shape
-        k = T * width + 1                     # last key: rows that reached a leaf
+        k = T * width + 1
         if k > _SORT_MAX_KEYS or T * n >= (1 << 31):
             return None
         dev = node_of.device
         lib = native.require_kernels()
         tt = torch.arange(T, device=dev, dtype=torch.int32)[:, None] * width
-        keys = torch.where(node_of >= 0, node_of + tt, torch.full_like(node_of, k - 1))
+        live = node_of >= 0
+        if weight is not None:
+            live &= weight > 0
+        keys = torch.where(live, node_of + tt, torch.full_like(node_of, k - 1))
         keys = keys.reshape(-1).contiguous()
         perm = torch.empty(T * n, dtype=torch.int32, device=dev)
         counts = torch.empty(k, dtype=torch.int64, device=dev)
@@ -443,7 +449,7 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     groups = RowGroups.root(T, n) if dev.type == "cuda" and _GROUPED else None
     for depth in range(max_depth + 1):
         if depth > 0 and groups is not None:
-            groups = RowGroups.from_nodes(node_of, nodes)
+            groups = RowGroups.from_nodes(node_of, nodes, weight)
         faults.point("rdf.level", depth=depth, rank=ctx.rank)
         watchdog.heartbeat("rdf.level")
         if Fs < P:

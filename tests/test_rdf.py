@@ -440,9 +440,9 @@ def test_histogram_and_route_kernels_match_cpu(cuda, cls):
     assert torch.allclose(h_gpu.cpu(), h_cpu, rtol=1e-4, atol=1e-3)
     # grouped rows (counting sort by (tree, node)) through the segmented kernel, in two node
     # chunks
-    groups = rdf_ops.RowGroups.from_nodes(node_of.to(cuda), nodes)
+    groups = rdf_ops.RowGroups.from_nodes(node_of.to(cuda), nodes, weight.to(cuda))
     assert groups is not None
-    assert int(groups.counts.sum()) == int((node_of >= 0).sum())
+    assert int(groups.counts.sum()) == int(((node_of >= 0) & (weight > 0)).sum())
     h_grp = torch.cat([rdf_ops._histogram_groups(
         gd, label.to(cuda) if cls else None, None if cls else y.to(cuda), S, cls,
         weight.to(cuda), groups, lo, hi - lo, feats[:, lo:hi].to(cuda), B, T)
