@@ -24,6 +24,7 @@ import re
 import time
 from typing import List, Optional, Tuple
 
+from .. import tracing
 from ..api import BatchLayerUpdate, Dataset
 from ..transport.producer import LogTopicProducer
 from ..utils import config as cfg
@@ -97,6 +98,8 @@ class BatchLayer(AbstractLayer):
         self.max_data_age_hours = config.get_int("oryx.batch.storage.max-age-data-hours")
         self.max_model_age_hours = config.get_int("oryx.batch.storage.max-age-model-hours")
         self.update_class = cfg.get_optional_string(config, "oryx.batch.update-class")
+        # per-interval JSON lines (new; the reference only logs)
+        self.timings_file = cfg.get_optional_string(config, "oryx.metrics.timings-file")
         self._update = update
         self._timer: Optional[IntervalTimer] = None
         self._context = None
@@ -130,6 +133,7 @@ class BatchLayer(AbstractLayer):
             self._context = self.layer_context()
             self.build_input_consumer()
         ts = int(time.time() * 1000) if timestamp is None else timestamp
+        t_start = time.perf_counter()
         records = drain(self._input_consumer)
         faults.point("batch.interval", timestamp=ts, records=len(records))
         dctx = self._context.dist if self._context is not None else None
@@ -156,6 +160,12 @@ class BatchLayer(AbstractLayer):
                     producer.close()
             save_interval_data(self.data_dir, ts, records)
         self.commit_input_offsets()
+        rec = {"event": "batch_interval", "layer_id": self.id, "timestamp": ts,
+               "records": len(records), "seconds": time.perf_counter() - t_start}
+        tracing.record(rec)
+        if self.timings_file:
+            with open(self.timings_file, "a") as f:
+                f.write(json.dumps(rec) + "\n")
         if self.max_data_age_hours >= 0:
             delete_old_data(self.data_dir, self.max_data_age_hours)
         if self.max_model_age_hours >= 0:

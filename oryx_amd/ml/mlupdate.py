@@ -19,12 +19,14 @@ serialises them) or sequentially across all ranks.
 from __future__ import annotations
 
 import abc
+import json
 import logging
 import os
 import time
 from typing import Any, List, Optional, Sequence, Tuple
 
 from ..api import BatchLayerUpdate, Dataset, TopicProducer
+from .. import tracing
 from ..parallel import dist
 from ..utils import ioutils, lang, pmml as pmmlu, rng
 from . import hyperparams as hp
@@ -34,6 +36,7 @@ __all__ = ["MLUpdate", "MODEL_FILE_NAME"]
 log = logging.getLogger(__name__)
 
 MODEL_FILE_NAME = "model.pmml"
+TIMINGS_FILE_NAME = "timings.json"
 
 
 class MLUpdate(BatchLayerUpdate):
@@ -183,10 +186,15 @@ class MLUpdate(BatchLayerUpdate):
         log.info("Building candidate %d with params %s", i, params)
         train, test = self._split_train_test(new_msgs, past_msgs)
         ev = float("nan")
+        timing = {"candidate": i, "params": [str(p) for p in params], "train": len(train),
+                  "test": len(test)}
         if not train:
             log.info("No train data to build a model")
         else:
-            model = self.build_model(context, train, params, candidate_path)
+            t0 = time.perf_counter()
+            with tracing.range("mlupdate.build"):
+                model = self.build_model(context, train, params, candidate_path)
+            timing["build_s"] = time.perf_counter() - t0
             if model is None:
                 log.info("Unable to build a model")
             else:
@@ -198,9 +206,22 @@ class MLUpdate(BatchLayerUpdate):
                     log.info("No test data available to evaluate model")
                 else:
                     log.info("Evaluating model")
-                    ev = float(self.evaluate(context, model, candidate_path, test, train))
+                    t1 = time.perf_counter()
+                    with tracing.range("mlupdate.evaluate"):
+                        ev = float(self.evaluate(context, model, candidate_path, test, train))
+                    timing["evaluate_s"] = time.perf_counter() - t1
+                timing.update(self.build_timings(candidate_path))
+                # per-candidate timing record next to the model (moves with the winner)
+                with open(os.path.join(candidate_path, TIMINGS_FILE_NAME), "w") as f:
+                    json.dump(dict(timing, eval=ev if ev == ev else None), f)
+        timing["eval"] = ev if ev == ev else None
+        tracing.record(dict(timing, event="candidate"))
         log.info("Model eval for params %s: %s (%s)", params, ev, candidate_path)
         return candidate_path, ev
+
+    def build_timings(self, candidate_path: str) -> dict:
+        """App-specific timing details of the last build (e.g. ALS iteration ms, ratings/s)."""
+        return {}
 
     def _split_train_test(self, new_msgs, past_msgs):
         if self.test_fraction <= 0.0:

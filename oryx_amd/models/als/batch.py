@@ -198,6 +198,7 @@ class ALSUpdate(MLUpdate):
         if not (0.0 < self.decay_factor <= 1.0) or self.decay_zero_threshold < 0.0:
             raise ValueError("bad decay settings")
         self._cache: Dict[str, dict] = {}
+        self._timings: Dict[str, dict] = {}
 
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
@@ -271,7 +272,16 @@ class ALSUpdate(MLUpdate):
         pmml.add_extension_content("XIDs", x_ids)
         pmml.add_extension_content("YIDs", y_ids)
         self._cache[candidate_path] = {"x_ids": x_ids, "y_ids": y_ids, "X": X, "Y": Y}
+        its = trainer.timings.get("iteration_ms", [])
+        self._timings[candidate_path] = {
+            "ratings": int(len(u)), "users": len(used_u), "items": len(used_i),
+            "prepare_s": trainer.timings.get("prepare_s"), "iteration_ms": its,
+            "resumed_from_iteration": getattr(trainer, "resumed_from", 0),
+            "ratings_per_s": (len(u) * 1e3 / (sum(its) / len(its))) if its else None}
         return pmml
+
+    def build_timings(self, candidate_path: str) -> dict:
+        return self._timings.pop(candidate_path, {})
 
     # ---------------------------------------------------------------- evaluate
     def _load(self, model_parent_path: str, pmml) -> dict:

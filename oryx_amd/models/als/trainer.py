@@ -256,7 +256,12 @@ class ALSTrainer:
             step = iterations - done
             if use_ckpt:
                 step = min(step, checkpoint_interval - done % checkpoint_interval)
+            t_it = time.perf_counter()
             self.iterate(step)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.timings.setdefault("iteration_ms", []).extend(
+                [(time.perf_counter() - t_it) * 1e3 / step] * step)
             done += step
             if use_ckpt and done < iterations and done % checkpoint_interval == 0:
                 with tracing.range("als.checkpoint"):

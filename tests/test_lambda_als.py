@@ -66,7 +66,7 @@ def _read_updates(root, topic="OryxUpdate"):
 
 
 def test_batch_layer_als_end_to_end(tmp_path):
-    config = _config(tmp_path)
+    config = _config(tmp_path, **{"oryx.metrics.timings-file": '"%s"' % (tmp_path / "t.jsonl")})
     root = str(tmp_path / "log")
     tlog.maybe_create_topic(root, "OryxInput", 4)
     tlog.maybe_create_topic(root, "OryxUpdate", 1)
@@ -105,6 +105,13 @@ def test_batch_layer_als_end_to_end(tmp_path):
     assert len(gens) == 1
     assert os.path.exists(os.path.join(model_dir, gens[0], "model.pmml"))
     assert os.path.exists(os.path.join(model_dir, gens[0], "X", "part-00000.gz"))
+    recs = [json.loads(l) for l in open(tmp_path / "t.jsonl")]
+    assert [r["records"] for r in recs] == [0, len(lines)]
+    assert recs[1]["seconds"] > 0
+    # per-candidate timing record moved with the winning model
+    tim = json.load(open(os.path.join(model_dir, gens[0], "timings.json")))
+    assert tim["ratings"] > 0 and len(tim["iteration_ms"]) == config.get_int("oryx.als.iterations")
+    assert tim["build_s"] > 0 and tim["ratings_per_s"] > 0
     # second generation: IDs are a superset of the previous generation's
     for j, line in enumerate(_random_input(seed=1, n=200)):
         prod.send(str(j), line)
