@@ -59,21 +59,25 @@ def test_faults_from_environment(tmp_path):
 
 def test_watchdog_guard_and_heartbeat():
     fired = []
-    wd = watchdog.Watchdog(0.3, on_expire=fired.append, poll_s=0.05)
+    wd = watchdog.Watchdog(1.0, on_expire=fired.append, poll_s=0.05)
     with wd.guard("fast"):
         pass
-    time.sleep(0.5)
+    time.sleep(1.3)
     assert not fired
     with wd.guard("stuck collective"):
-        time.sleep(1.0)
+        t0 = time.time()
+        while not fired and time.time() - t0 < 10:
+            time.sleep(0.05)
     assert fired and "stuck collective" in fired[0]
     fired2 = []
-    wd2 = watchdog.Watchdog(0.3, on_expire=fired2.append, poll_s=0.05)
-    for _ in range(5):
+    wd2 = watchdog.Watchdog(1.0, on_expire=fired2.append, poll_s=0.05)
+    for _ in range(8):
         wd2.heartbeat("loop")
         time.sleep(0.1)
     assert not fired2
-    time.sleep(0.8)
+    t0 = time.time()
+    while not fired2 and time.time() - t0 < 10:
+        time.sleep(0.05)
     assert fired2 and "loop" in fired2[0]
     off = watchdog.Watchdog(0)
     with off.guard("x"):
