@@ -461,6 +461,220 @@ __global__ __launch_bounds__(256) void als_solve_wave(AlsParams p, unsigned long
     for (int i = 0; i < 6; ++i) atomicAdd(prof + i, ph[i]);
 }
 
+// ------------------------------------------------------------------ panel-Cholesky kernel
+
+// LDS of one wave in als_solve_panel: the lower block-column panels of L (panel p = rows
+// 16p..KP-1 x columns 16p..16p+15, LS floats per row), aliased with the gather's chunk image,
+// plus the per-rating weights.  LS = 20: lane-per-row ds_read_b128, the accumulator-layout
+// scatter and the MFMA-fragment reads are all bank-conflict free.  KP=64: 12.8 KB per wave
+// (the register-Cholesky kernel keeps a 64x65 fp32 image, 17 KB).
+template <int KP>
+struct PanelSmem {
+  static constexpr int M = KP / 16;
+  static constexpr int LS = 20;
+  static constexpr int ROWS = 16 * M * (M + 1) / 2;
+  static constexpr int L_BYTES = ROWS * LS * 4;
+  static constexpr int G_BYTES = ChunkImage<KP>::BYTES;
+  static constexpr int RAW = L_BYTES > G_BYTES ? L_BYTES : G_BYTES;
+  static constexpr int BYTES = (RAW + 15) / 16 * 16 + 256;
+  // first LDS row of panel p: sum_{q<p} (KP - 16 q)
+  __host__ __device__ static constexpr int base(int p) { return 16 * (p * M - p * (p - 1) / 2); }
+};
+
+// One wave per row, KP <= 64.  The normal-equation matrix never leaves the MFMA accumulators
+// until it is factored:
+//   * A = YtY + sum_i c_i y_i y_i^T accumulates on v_mfma_f32_16x16x32_bf16 starting from YtY
+//     (wave_accumulate<KP, true>); lambda*n_u goes onto the diagonal in accumulator layout;
+//   * right-looking blocked Cholesky over 16-column panels.  Panel p's tiles go to LDS once
+//     and come back lane-per-row (lane r holds A[r][16p..16p+15]); its 16 columns are
+//     eliminated in registers (the in-panel broadcasts are v_readlane of the panel's own
+//     diagonal-block rows: <= 15 per step instead of one per trailing row), the forward solve
+//     L z = b rides along as an augmented column (lane r holds b_r), and the trailing tiles
+//     (i, j > p) are updated on v_mfma_f32_16x16x4_f32 straight in the accumulators;
+//   * back substitution L^T x = z reads the LDS panels (off the dependency chain).
+// Per row (KP=64): 480 in-panel FMAs per lane + 40 small MFMAs, versus 2016 FMAs per lane for
+// the all-register column Cholesky of als_solve_wave.
+template <int KP, bool PROF = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void als_solve_panel(AlsParams p, unsigned long long* prof) {
+  using PS = PanelSmem<KP>;
+  constexpr int M = KP / 16;
+  constexpr int NT = M * (M + 1) / 2;
+  constexpr int LS = PS::LS;
+  __shared__ __attribute__((aligned(16))) char smem[4 * PS::BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  char* my = smem + wave * PS::BYTES;
+  float* Lp = reinterpret_cast<float*>(my);
+  float* Wab = reinterpret_cast<float*>(my + PS::BYTES - 256);
+  const int g = lane >> 4, fl = lane & 15;
+  const int total_waves = gridDim.x * 4;
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+
+  for (int w = blockIdx.x * 4 + wave; w < p.n_work; w += total_waves) {
+    const int row = p.row_ids ? p.row_ids[w] : w;
+    const int64_t beg = p.row_ptr[row], end = p.row_ptr[row + 1];
+    const int slot = p.long_slot ? p.long_slot[w] : -1;
+    unsigned long long tp = PROF ? __builtin_amdgcn_s_memtime() : 0;
+#define ORYX_PHASE(ix)                                                   \
+  if (PROF) {                                                            \
+    const unsigned long long tn = __builtin_amdgcn_s_memtime();          \
+    ph[ix] += tn - tp;                                                   \
+    tp = tn;                                                             \
+  }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bz, cnt_acc = 0.f;
+    {
+      float bpart[M];
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
+      // acc = sum over the row's ratings (split rows: nothing here, partials from ws below)
+      wave_accumulate<KP, false>(p, beg, slot < 0 ? end : beg, my, Wab, acc, bpart, cnt_acc);
+      reduce_bpart<M>(bpart);
+      bz = pick_bpart<M>(bpart, g);   // lane l (< KP): b[l]
+    }
+    float cnt = wave_sum(cnt_acc);
+    const float* wsrow = nullptr;
+    if (slot >= 0) {
+      const float* src = p.ws + (int64_t)slot * ws_stride(KP);
+      bz = src[KP * KP + (lane < KP ? lane : 0)];
+      cnt = src[KP * KP + KP];
+      wsrow = src;
+    }
+    ORYX_PHASE(0)
+    float dinv = 0.f;
+    // opaque lane id (keeps per-step lane masks from being hoisted into SGPR pairs)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+#pragma unroll
+    for (int pp = 0; pp < M; ++pp) {
+      float* P = Lp + PS::base(pp) * LS;
+      // panel tiles (i, pp), i >= pp: accumulator layout -> LDS rows 16pp.. of the panel
+#pragma unroll
+      for (int i = pp; i < M; ++i) {
+        const int t = i * (i + 1) / 2 + pp;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) P[(16 * (i - pp) + 4 * g + v) * LS + fl] = acc[t][v];
+      }
+      wave_sync();
+      const bool inp = ln >= 16 * pp && ln < KP;
+      const int prow = inp ? ln - 16 * pp : 0;
+      // + YtY (and a split row's partial sums) and lambda * n_u, added to each panel as it is
+      // loaded: all are plain additions to A, and tile (i, j)'s share is only needed once
+      // panel j is factored (the trailing updates before that just subtract from it)
+      const int rr = ln < KP ? ln : 0;
+      const f32x4* yr = reinterpret_cast<const f32x4*>(p.YtY + rr * KP + 16 * pp);
+      f32x4 yv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) yv[q] = yr[q];
+      if (wsrow) {
+        const f32x4* wr = reinterpret_cast<const f32x4*>(wsrow + rr * KP + 16 * pp);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) yv[q] += wr[q];
+      }
+      float pr[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(P + prow * LS + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pr[4 * q + e] = v[e] + yv[q][e];
+      }
+      {
+        int rel = ln - 16 * pp;
+        asm volatile("" : "+v"(rel));
+        const float dg = ln < p.k ? p.lambda * cnt : 1.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) pr[j] += rel == j ? dg : 0.f;
+      }
+      ORYX_PHASE(2)
+      // eliminate the panel's 16 columns; lane r ends with L[r][16pp + j] in pr[j]
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int J = 16 * pp + j;
+        // lane-relative index made opaque per step: the lane masks are formed here, not
+        // hoisted to the top of the row (3 x KP live SGPR pairs -> spills into VGPR lanes)
+        int rel = ln - J;
+        asm volatile("" : "+v"(rel));
+        float s = oryx_readlane(pr[j], J);
+        // not positive (or NaN) -> clamped to 1e-30; detected from 1/d below (per-step
+        // boolean flags get sunk to the end of the row and pin all 64 pivots in SGPRs)
+        s = s > 1e-30f ? s : 1e-30f;
+        const float inv = __builtin_amdgcn_rsqf(s);
+        const float d = s * inv;
+        float l = pr[j] * inv;
+        l = rel < 0 ? 0.f : (rel == 0 ? d : l);
+        dinv = rel == 0 ? inv : dinv;
+        pr[j] = l;
+        // forward solve on the augmented column: z_J = b_J / d_J
+        const float zJ = oryx_readlane(bz, J) * inv;
+        bz = rel == 0 ? zJ : (rel > 0 ? bz - l * zJ : bz);
+#pragma unroll
+        for (int jj = j + 1; jj < 16; ++jj) {
+          pr[jj] -= l * oryx_readlane(l, 16 * pp + jj);
+          asm volatile("" : "+v"(pr[jj]));
+        }
+      }
+      if (inp) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(P + prow * LS + 4 * q) =
+              f32x4{pr[4 * q], pr[4 * q + 1], pr[4 * q + 2], pr[4 * q + 3]};
+      }
+      wave_sync();
+      ORYX_PHASE(3)
+      // trailing update: A(i, jt) -= L(i, pp) L(jt, pp)^T for i >= jt > pp, on fp32 MFMA
+      if (pp + 1 < M) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          float fr[M];
+#pragma unroll
+          for (int i = pp + 1; i < M; ++i) fr[i] = P[(16 * (i - pp) + fl) * LS + 4 * kk + g];
+#pragma unroll
+          for (int i = pp + 1; i < M; ++i)
+#pragma unroll
+            for (int jt = pp + 1; jt <= i; ++jt) {
+              const int t = i * (i + 1) / 2 + jt;
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(-fr[i], fr[jt], acc[t], 0, 0, 0);
+            }
+        }
+      }
+      ORYX_PHASE(4)
+    }
+    // a clamped pivot gives 1/d = 1e15
+    const bool bad = __any(lane < KP && !(dinv < 9.9e14f));
+    if (bad && lane == 0 && p.fail_count) atomicAdd(p.fail_count, 1);
+    // back substitution L^T x = z: step J takes L[J][c] (lane c) from panel c/16
+    const int c = lane < KP ? lane : 0;
+    const int pc = c >> 4;
+    typedef __attribute__((address_space(3))) float lds_float;
+    const lds_float* lcol = (const lds_float*)(Lp + (PS::base(pc) - 16 * pc) * LS + (c & 15));
+    float xv = bz, x_own = 0.f;
+#pragma unroll
+    for (int J = KP - 1; J >= 0; --J) {
+      int rel = ln - J;
+      asm volatile("" : "+v"(rel));
+      const float lv = lcol[J * LS];
+      const float xj = oryx_readlane(xv * dinv, J);
+      x_own = rel == 0 ? xj : x_own;
+      // lanes c > J are finished (x_own captured); for c in a later panel than row J the read
+      // lands on another panel's rows (in bounds, value irrelevant), so no mask is needed
+      xv -= lv * xj;
+      if ((J & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+    if (lane < KP) {
+      p.X[(int64_t)row * KP + lane] = x_own;
+      if (p.Xb) p.Xb[(int64_t)row * KP + lane] = (__bf16)x_own;
+    }
+    wave_sync();
+    ORYX_PHASE(5)
+#undef ORYX_PHASE
+  }
+  if (PROF && lane == 0)
+    for (int i = 0; i < 6; ++i) atomicAdd(prof + i, ph[i]);
+}
+
 // Debug/verification: the raw normal equations (Gramian without YtY/lambda, b, count) of the
 // single row [beg, end), as accumulated by wave_accumulate.  One wave.
 template <int KP>
@@ -749,7 +963,16 @@ __global__ __launch_bounds__(256) void pair_dots(const float* __restrict__ X,
 
 }  // namespace
 
+// KP <= 64 solve kernel: 0 = als_solve_panel (default), 1 = als_solve_wave (register Cholesky)
+static int g_als_variant = 0;
+
 extern "C" {
+
+int oryx_als_set_variant(int v) {
+  if (v < 0 || v > 1) return ORYX_EINVAL;
+  g_als_variant = v;
+  return ORYX_OK;
+}
 
 // long_slot [n_work] (nullable) marks split rows; segs [n_seg][4] = (row, slot, beg, end);
 // ws: workspace of n_long * ws_stride(kp) floats (zeroed here).
@@ -793,8 +1016,12 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
   case KPV: {                                                                         \
     int blocks = (n_work + 3) / 4;                                                    \
     if (blocks > max_blocks) blocks = max_blocks;                                     \
-    hipLaunchKernelGGL((als_solve_wave<KPV, false>), dim3(blocks), dim3(256), 0, s, p,  \
-                       nullptr);                                                 \
+    if (g_als_variant == 0)                                                           \
+      hipLaunchKernelGGL((als_solve_panel<KPV, false>), dim3(blocks), dim3(256), 0, s, p, \
+                         nullptr);                                                    \
+    else                                                                              \
+      hipLaunchKernelGGL((als_solve_wave<KPV, false>), dim3(blocks), dim3(256), 0, s, p, \
+                         nullptr);                                                    \
     break;                                                                            \
   }
     WAVE_CASE(16)
@@ -840,8 +1067,12 @@ int oryx_als_solve_profile64(const int64_t* row_ptr, const int32_t* row_ids,
               nullptr, n_work, k, lambda, alpha, implicit, nullptr, nullptr, nullptr};
   int blocks = (n_work + 3) / 4;
   if (blocks > 256 * 16) blocks = 256 * 16;
-  hipLaunchKernelGGL((als_solve_wave<64, true>), dim3(blocks), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), p, prof);
+  if (g_als_variant == 0)
+    hipLaunchKernelGGL((als_solve_panel<64, true>), dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), p, prof);
+  else
+    hipLaunchKernelGGL((als_solve_wave<64, true>), dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), p, prof);
   return oryx_check_launch();
 }
 
@@ -872,7 +1103,7 @@ int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const fl
   return oryx_check_launch();
 }
 
-int oryx_kernels_version() { return 2; }
+int oryx_kernels_version() { return 3; }
 
 int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 

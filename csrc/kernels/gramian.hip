@@ -71,17 +71,41 @@ __global__ __launch_bounds__(256) void gramian_partial(const float* __restrict__
   for (int i = tid; i < KP * KP; i += 256) dst[i] = red[i];
 }
 
-__global__ __launch_bounds__(256) void gramian_reduce(const float* __restrict__ part, int nblk,
-                                                      int kp, float* __restrict__ out) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= kp * kp) return;
-  const int i = idx / kp, j = idx % kp;
-  // entries of the lower triangle (16x16 diagonal tiles are computed in full: use (i, j) with
-  // i >= j for both (i, j) and (j, i))
-  const int src = i >= j ? idx : j * kp + i;
+// Second pass: 64 output entries per workgroup, 16 waves.  Wave w sums partials w, w+16, ...
+// (eight loads in flight per lane, each a coalesced 256-byte run), then wave 0 adds the 16
+// wave sums in a fixed order: deterministic, and ~kp*kp/64 workgroups x 16 waves instead of
+// kp*kp/256 threads each walking all partials serially (122 us -> a few us at kp=64).
+// Only entries with i >= j are reduced (the 16x16 diagonal tiles hold both halves, the
+// strictly-upper off-diagonal tiles are zero); each is written to (i, j) and (j, i).
+__global__ __launch_bounds__(1024) void gramian_reduce(const float* __restrict__ part, int nblk,
+                                                       int kp, float* __restrict__ out) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int idx = blockIdx.x * 64 + lane;
+  const int kk = kp * kp;
+  const int src = idx < kk ? idx : 0;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += part[(long long)b * kp * kp + src];
-  out[idx] = s;
+  int b = wave;
+  for (; b + 7 * 16 < nblk; b += 8 * 16) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(long long)(b + u * 16) * kk + src];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; b < nblk; b += 16) s += part[(long long)b * kk + src];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && idx < kk) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    const int i = idx / kp, j = idx % kp;
+    if (i >= j) {
+      out[idx] = t;
+      if (i != j) out[j * kp + i] = t;
+    }
+  }
 }
 
 }  // namespace
@@ -117,7 +141,7 @@ int oryx_gramian_f32(const float* X, long long n, int ld, int kp, float* out, fl
     default:
       return ORYX_EINVAL;
   }
-  hipLaunchKernelGGL(gramian_reduce, dim3((kp * kp + 255) / 256), dim3(256), 0, s, ws,
+  hipLaunchKernelGGL(gramian_reduce, dim3((kp * kp + 63) / 64), dim3(1024), 0, s, ws,
                      (int)blocks, kp, out);
   return oryx_check_launch();
 }

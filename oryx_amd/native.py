@@ -104,6 +104,9 @@ def _load_kernels():
         _build.build_kernels()
     lib = ctypes.CDLL(path)
     _sig(lib, "oryx_kernels_version", c_i, [])
+    # ORYX_ALS_VARIANT=1 selects the register-Cholesky KP<=64 solve (als_solve_wave) for A/B runs
+    _sig(lib, "oryx_als_set_variant", c_i, [c_i])
+    lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "0")))
     _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                       c_i, c_f, c_f, c_i, c_vp, c_vp, c_vp, c_i, c_i, c_vp,
                                       c_vp])
