@@ -29,6 +29,10 @@
 
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
+#ifndef ORYX_ALS_PANEL_WAVES
+#define ORYX_ALS_PANEL_WAVES 3
+#endif
+
 #ifndef ORYX_ALS_CHOL_LDS
 #define ORYX_ALS_CHOL_LDS 1
 #endif
@@ -495,7 +499,7 @@ struct PanelSmem {
 // Per row (KP=64): 480 in-panel FMAs per lane + 40 small MFMAs, versus 2016 FMAs per lane for
 // the all-register column Cholesky of als_solve_wave.
 template <int KP, bool PROF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void als_solve_panel(AlsParams p, unsigned long long* prof) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORYX_ALS_PANEL_WAVES, ORYX_ALS_PANEL_WAVES))) void als_solve_panel(AlsParams p, unsigned long long* prof) {
   using PS = PanelSmem<KP>;
   constexpr int M = KP / 16;
   constexpr int NT = M * (M + 1) / 2;
@@ -544,10 +548,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       wsrow = src;
     }
     ORYX_PHASE(0)
-    float dinv = 0.f;
+    float dinv = 0.f, z_own = 0.f;
     // opaque lane id (keeps per-step lane masks from being hoisted into SGPR pairs)
     int ln = lane;
     asm volatile("" : "+v"(ln));
+    typedef __attribute__((address_space(3))) float lds_float;
+    typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+    lds_float* bcl = (lds_float*)Wab;   // 64 floats: the weights' slot, free after the gather
 #pragma unroll
     for (int pp = 0; pp < M; ++pp) {
       float* P = Lp + PS::base(pp) * LS;
@@ -589,31 +596,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         for (int j = 0; j < 16; ++j) pr[j] += rel == j ? dg : 0.f;
       }
       ORYX_PHASE(2)
-      // eliminate the panel's 16 columns; lane r ends with L[r][16pp + j] in pr[j]
+      // eliminate the panel's 16 columns; lane r > J ends with L[r][J] in pr[J - 16pp], lane J
+      // with d_J (lanes below J hold values that are never read: the trailing update uses rows
+      // below the diagonal block, and back substitution only lanes c < J of row J)
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int J = 16 * pp + j;
-        // lane-relative index made opaque per step: the lane masks are formed here, not
-        // hoisted to the top of the row (3 x KP live SGPR pairs -> spills into VGPR lanes)
-        int rel = ln - J;
-        asm volatile("" : "+v"(rel));
         float s = oryx_readlane(pr[j], J);
         // not positive (or NaN) -> clamped to 1e-30; detected from 1/d below (per-step
         // boolean flags get sunk to the end of the row and pin all 64 pivots in SGPRs)
         s = s > 1e-30f ? s : 1e-30f;
         const float inv = __builtin_amdgcn_rsqf(s);
-        const float d = s * inv;
-        float l = pr[j] * inv;
-        l = rel < 0 ? 0.f : (rel == 0 ? d : l);
-        dinv = rel == 0 ? inv : dinv;
+        const float l = pr[j] * inv;   // lane J: s / sqrt(s) = d_J
         pr[j] = l;
-        // forward solve on the augmented column: z_J = b_J / d_J
+        // forward solve on the augmented column: z_J = b_J / d_J; lanes <= J keep junk in bz
+        // from here on (z_J is captured in z_own)
         const float zJ = oryx_readlane(bz, J) * inv;
-        bz = rel == 0 ? zJ : (rel > 0 ? bz - l * zJ : bz);
+        bz -= l * zJ;
+        // lane-relative index made opaque per step so the mask is formed here, not hoisted
+        int rel = ln - J;
+        asm volatile("" : "+v"(rel));
+        dinv = rel == 0 ? inv : dinv;
+        z_own = rel == 0 ? zJ : z_own;
+        // materialise both selects now: otherwise LLVM sinks the 64-deep select chains to their
+        // use in the back substitution and keeps every step's 1/d and z live (spills)
+        asm volatile("" : "+v"(dinv), "+v"(z_own), "+v"(bz));
+        if (j < 15) {
+          // column J of the diagonal block to every lane: one ds_write_b32 per lane (own
+          // slot), broadcast ds_read_b128 of the 16-entry block, packed FMAs
+          bcl[ln] = l;
+          wave_sync();
+          f32x4 bq[4];
 #pragma unroll
-        for (int jj = j + 1; jj < 16; ++jj) {
-          pr[jj] -= l * oryx_readlane(l, 16 * pp + jj);
-          asm volatile("" : "+v"(pr[jj]));
+          for (int q = (j + 1) / 4; q < 4; ++q)
+            bq[q] = *reinterpret_cast<const lds_f32x4*>(bcl + 16 * pp + 4 * q);
+#pragma unroll
+          for (int jj = j + 1; jj < 16; ++jj) {
+            pr[jj] -= l * bq[jj / 4][jj % 4];
+            asm volatile("" : "+v"(pr[jj]));
+          }
+          wave_sync();
         }
       }
       if (inp) {
@@ -648,9 +670,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     // back substitution L^T x = z: step J takes L[J][c] (lane c) from panel c/16
     const int c = lane < KP ? lane : 0;
     const int pc = c >> 4;
-    typedef __attribute__((address_space(3))) float lds_float;
     const lds_float* lcol = (const lds_float*)(Lp + (PS::base(pc) - 16 * pc) * LS + (c & 15));
-    float xv = bz, x_own = 0.f;
+    float xv = z_own, x_own = 0.f;
 #pragma unroll
     for (int J = KP - 1; J >= 0; --J) {
       int rel = ln - J;
