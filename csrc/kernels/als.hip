@@ -254,6 +254,143 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
   }
 }
 
+// Same accumulation with THREE chunks of gathers in flight (register rings of 3 by chunk
+// index mod 3).  Issue order inside chunk c, after its image is in LDS:
+// [cols(c+5), val(c+3), gathers(c+3)].  vmcnt retires in issue order, so every load a later
+// wait needs is issued before the gather groups that should stay in flight past that wait:
+// when chunk c+1 starts, gathers(c+1), val(c+1) and cols(c+4) are all older than
+// gathers(c+2) and gathers(c+3), which stay in flight.
+template <int KP>
+__device__ __forceinline__ void wave_accumulate3(const AlsParams& p, int64_t beg, int64_t end,
+                                                 char* G, float* Wab,
+                                                 f32x4 (&acc)[(KP / 16) * (KP / 16 + 1) / 2],
+                                                 float (&bpart)[KP / 16], float& cnt_acc) {
+  using CI = ChunkImage<KP>;
+  constexpr int M = KP / 16;
+  constexpr int PPR = CI::PPR;
+  constexpr int NPL = CI::NPL;
+  if (beg >= end) return;
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  const int g = lane >> 4, fl = lane & 15;
+  int srow[NPL], soff[NPL];
+#pragma unroll
+  for (int it = 0; it < NPL; ++it) {
+    const int sl = it * 64 + lane, r = sl / PPR, sc = sl % PPR;
+    srow[it] = r;
+    soff[it] = ((sc + CI::rot(r)) % PPR) * 8;
+  }
+  const int q = fl >> 2, pp = fl & 3;
+  auto tr_addr = [&](int pi, int h) -> int {
+    const int row = 8 * g + 4 * h + q;
+    const int pc = 2 * pi + (pp >> 1);
+    const int sc = (pc - CI::rot(row) + PPR) % PPR;
+    return row * KP * 2 + sc * 16 + (pp & 1) * 8;
+  };
+  const int64_t nch = (end - beg + 31) / 32;
+  auto load_cols = [&](int64_t ch, int (&cols)[NPL]) {
+    const int64_t c = beg + ch * 32;
+#pragma unroll
+    for (int it = 0; it < NPL; ++it) {
+      const int64_t ri = c + srow[it] < end ? c + srow[it] : end - 1;
+      cols[it] = p.col_idx[ri];
+    }
+  };
+  auto load_val = [&](int64_t ch, float& val) {
+    const int64_t c = beg + ch * 32;
+    const int64_t vi = c + (lane & 31) < end ? c + (lane & 31) : end - 1;
+    val = p.vals[vi];
+  };
+  auto gather = [&](const int (&cols)[NPL], i32x4 (&stg)[NPL]) {
+#pragma unroll
+    for (int it = 0; it < NPL; ++it)
+      stg[it] = *reinterpret_cast<const i32x4*>(p.Y + (int64_t)cols[it] * KP + soff[it]);
+  };
+  i32x4 stg0[NPL], stg1[NPL], stg2[NPL];
+  int cols0[NPL], cols1[NPL], cols2[NPL];
+  float val0 = 0.f, val1 = 0.f, val2 = 0.f;
+
+  // chunk ch: stg / val hold its data, cols_g the metadata of chunk ch+3 (gathered into stg
+  // once its image is in LDS), cols_l the free slot that receives cols(ch+5)
+  auto chunk = [&](int64_t ch, i32x4 (&stg)[NPL], float& val, int (&cols_g)[NPL],
+                   int (&cols_l)[NPL]) {
+    const int64_t c0 = beg + ch * 32;
+    const int n = (int)min((int64_t)32, end - c0);
+    float wa = 0.f, wb = 0.f, cn = 0.f;
+    if (lane < n) als_weights(val, p.alpha, p.implicit, wa, wb, cn);
+    cnt_acc += cn;
+    if (lane < 32) {
+      Wab[lane] = wa;
+      Wab[32 + lane] = wb;
+    }
+#pragma unroll
+    for (int it = 0; it < NPL; ++it)
+      *reinterpret_cast<i32x4*>(G + (it * 64 + lane) * 16) = stg[it];
+    wave_sync();
+    if (ch + 5 < nch) load_cols(ch + 5, cols_l);
+    if (ch + 3 < nch) {
+      load_val(ch + 3, val);
+      gather(cols_g, stg);
+    }
+    const f32x4* wv = reinterpret_cast<const f32x4*>(Wab);
+    const f32x4 wa0 = wv[2 * g], wa1 = wv[2 * g + 1];
+    const f32x4 wb0 = wv[8 + 2 * g], wb1 = wv[8 + 2 * g + 1];
+    bf16x8 fa[M], fb[M];
+#pragma unroll
+    for (int pi = 0; pi < M; ++pi) {
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 0)));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 1)));
+      const bf16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      fb[pi] = v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        fa[pi][j] = (__bf16)((float)v[j] * wa0[j]);
+        fa[pi][4 + j] = (__bf16)((float)v[4 + j] * wa1[j]);
+      }
+    }
+    {
+      int t = 0;
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+        for (int qi = 0; qi <= pi; ++qi, ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[pi], fb[qi], acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int pi = 0; pi < M; ++pi) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bpart[pi] += wb0[j] * (float)fb[pi][j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bpart[pi] += wb1[j] * (float)fb[pi][4 + j];
+    }
+    wave_sync();
+  };
+
+  // prologue: [cols(0..2), val(0)] G(0) [cols(3), val(1)] G(1) [cols(4), val(2)] G(2)
+  load_cols(0, cols0);
+  if (nch > 1) load_cols(1, cols1);
+  if (nch > 2) load_cols(2, cols2);
+  load_val(0, val0);
+  gather(cols0, stg0);
+  if (nch > 3) load_cols(3, cols0);
+  if (nch > 1) {
+    load_val(1, val1);
+    gather(cols1, stg1);
+  }
+  if (nch > 4) load_cols(4, cols1);
+  if (nch > 2) {
+    load_val(2, val2);
+    gather(cols2, stg2);
+  }
+  for (int64_t ch = 0; ch < nch; ch += 3) {
+    chunk(ch, stg0, val0, cols0, cols2);
+    if (ch + 1 < nch) chunk(ch + 1, stg1, val1, cols1, cols0);
+    if (ch + 2 < nch) chunk(ch + 2, stg2, val2, cols2, cols1);
+  }
+}
+
 // sum the per-lane b partials over the 4 lane groups; lane f then takes feature f (+64h)
 template <int M>
 __device__ __forceinline__ void reduce_bpart(float (&bpart)[M]) {
@@ -498,8 +635,8 @@ struct PanelSmem {
 //   * back substitution L^T x = z reads the LDS panels (off the dependency chain).
 // Per row (KP=64): 480 in-panel FMAs per lane + 40 small MFMAs, versus 2016 FMAs per lane for
 // the all-register column Cholesky of als_solve_wave.
-template <int KP, bool PROF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORYX_ALS_PANEL_WAVES, ORYX_ALS_PANEL_WAVES))) void als_solve_panel(AlsParams p, unsigned long long* prof) {
+template <int KP, bool PROF = false, bool DEEP = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : ORYX_ALS_PANEL_WAVES, DEEP ? 2 : ORYX_ALS_PANEL_WAVES))) void als_solve_panel(AlsParams p, unsigned long long* prof) {
   using PS = PanelSmem<KP>;
   constexpr int M = KP / 16;
   constexpr int NT = M * (M + 1) / 2;
@@ -535,7 +672,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORYX_ALS_PA
 #pragma unroll
       for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
       // acc = sum over the row's ratings (split rows: nothing here, partials from ws below)
-      wave_accumulate<KP, false>(p, beg, slot < 0 ? end : beg, my, Wab, acc, bpart, cnt_acc);
+      if (DEEP)
+        wave_accumulate3<KP>(p, beg, slot < 0 ? end : beg, my, Wab, acc, bpart, cnt_acc);
+      else
+        wave_accumulate<KP, false>(p, beg, slot < 0 ? end : beg, my, Wab, acc, bpart, cnt_acc);
       reduce_bpart<M>(bpart);
       bz = pick_bpart<M>(bpart, g);   // lane l (< KP): b[l]
     }
@@ -984,13 +1124,15 @@ __global__ __launch_bounds__(256) void pair_dots(const float* __restrict__ X,
 
 }  // namespace
 
-// KP <= 64 solve kernel: 0 = als_solve_panel (default), 1 = als_solve_wave (register Cholesky)
-static int g_als_variant = 0;
+// KP <= 64 solve kernel: 2 = als_solve_panel with three chunks of gathers in flight at 2 waves
+// per SIMD (default), 0 = als_solve_panel with one chunk in flight at 3 waves per SIMD,
+// 1 = als_solve_wave (register column Cholesky)
+static int g_als_variant = 2;
 
 extern "C" {
 
 int oryx_als_set_variant(int v) {
-  if (v < 0 || v > 1) return ORYX_EINVAL;
+  if (v < 0 || v > 2) return ORYX_EINVAL;
   g_als_variant = v;
   return ORYX_OK;
 }
@@ -1040,6 +1182,9 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
     if (g_als_variant == 0)                                                           \
       hipLaunchKernelGGL((als_solve_panel<KPV, false>), dim3(blocks), dim3(256), 0, s, p, \
                          nullptr);                                                    \
+    else if (g_als_variant == 2)                                                      \
+      hipLaunchKernelGGL((als_solve_panel<KPV, false, true>), dim3(blocks), dim3(256), 0, \
+                         s, p, nullptr);                                              \
     else                                                                              \
       hipLaunchKernelGGL((als_solve_wave<KPV, false>), dim3(blocks), dim3(256), 0, s, p, \
                          nullptr);                                                    \
@@ -1090,6 +1235,9 @@ int oryx_als_solve_profile64(const int64_t* row_ptr, const int32_t* row_ids,
   if (blocks > 256 * 16) blocks = 256 * 16;
   if (g_als_variant == 0)
     hipLaunchKernelGGL((als_solve_panel<64, true>), dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), p, prof);
+  else if (g_als_variant == 2)
+    hipLaunchKernelGGL((als_solve_panel<64, true, true>), dim3(blocks), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), p, prof);
   else
     hipLaunchKernelGGL((als_solve_wave<64, true>), dim3(blocks), dim3(256), 0,

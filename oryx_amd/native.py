@@ -104,9 +104,10 @@ def _load_kernels():
         _build.build_kernels()
     lib = ctypes.CDLL(path)
     _sig(lib, "oryx_kernels_version", c_i, [])
-    # ORYX_ALS_VARIANT=1 selects the register-Cholesky KP<=64 solve (als_solve_wave) for A/B runs
+    # ORYX_ALS_VARIANT selects the KP<=64 solve kernel for A/B runs (csrc/kernels/als.hip:
+    # 2 = panel Cholesky + 3-deep gather ring (default), 0 = panel + 1-deep, 1 = register)
     _sig(lib, "oryx_als_set_variant", c_i, [c_i])
-    lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "0")))
+    lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "2")))
     _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                       c_i, c_f, c_f, c_i, c_vp, c_vp, c_vp, c_i, c_i, c_vp,
                                       c_vp])
