@@ -29,6 +29,11 @@
 
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
+// 1: the next row's first chunk gathers are issued during this row's factorization
+#ifndef ORYX_ALS_XROW_PREFETCH
+#define ORYX_ALS_XROW_PREFETCH 0
+#endif
+
 #ifndef ORYX_ALS_PANEL_WAVES
 #define ORYX_ALS_PANEL_WAVES 3
 #endif
@@ -255,65 +260,96 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
 }
 
 // Same accumulation with THREE chunks of gathers in flight (register rings of 3 by chunk
-// index mod 3).  Issue order inside chunk c, after its image is in LDS:
+// index mod 3), kept as state across rows so that the next row's first three chunks are
+// issued (prefetch) before the current row is factored: the factorization's VALU work hides
+// the next row's gather latency.  Issue order inside chunk c, after its image is in LDS:
 // [cols(c+5), val(c+3), gathers(c+3)].  vmcnt retires in issue order, so every load a later
 // wait needs is issued before the gather groups that should stay in flight past that wait:
 // when chunk c+1 starts, gathers(c+1), val(c+1) and cols(c+4) are all older than
-// gathers(c+2) and gathers(c+3), which stay in flight.
+// gathers(c+2) and gathers(c+3), which stay in flight.  (The factorization therefore takes
+// YtY from LDS, not global memory: a global load there would drain the prefetch.)
 template <int KP>
-__device__ __forceinline__ void wave_accumulate3(const AlsParams& p, int64_t beg, int64_t end,
-                                                 char* G, float* Wab,
-                                                 f32x4 (&acc)[(KP / 16) * (KP / 16 + 1) / 2],
-                                                 float (&bpart)[KP / 16], float& cnt_acc) {
+struct GatherRing {
   using CI = ChunkImage<KP>;
-  constexpr int M = KP / 16;
-  constexpr int PPR = CI::PPR;
-  constexpr int NPL = CI::NPL;
-  if (beg >= end) return;
-  int lane = threadIdx.x & 63;
-  asm volatile("" : "+v"(lane));
-  const int g = lane >> 4, fl = lane & 15;
+  static constexpr int M = KP / 16;
+  static constexpr int PPR = CI::PPR;
+  static constexpr int NPL = CI::NPL;
+  int lane, g, fl, q4, p4;
   int srow[NPL], soff[NPL];
+  int64_t beg = 0, end = 0, nch = 0;
+  i32x4 stg0[NPL], stg1[NPL], stg2[NPL];
+  int cols0[NPL], cols1[NPL], cols2[NPL];
+  float val0 = 0.f, val1 = 0.f, val2 = 0.f;
+
+  __device__ __forceinline__ void init() {
+    lane = threadIdx.x & 63;
+    g = lane >> 4;
+    fl = lane & 15;
+    q4 = fl >> 2;
+    p4 = fl & 3;
 #pragma unroll
-  for (int it = 0; it < NPL; ++it) {
-    const int sl = it * 64 + lane, r = sl / PPR, sc = sl % PPR;
-    srow[it] = r;
-    soff[it] = ((sc + CI::rot(r)) % PPR) * 8;
+    for (int it = 0; it < NPL; ++it) {
+      const int sl = it * 64 + lane, r = sl / PPR, sc = sl % PPR;
+      srow[it] = r;
+      soff[it] = ((sc + CI::rot(r)) % PPR) * 8;
+    }
   }
-  const int q = fl >> 2, pp = fl & 3;
-  auto tr_addr = [&](int pi, int h) -> int {
-    const int row = 8 * g + 4 * h + q;
-    const int pc = 2 * pi + (pp >> 1);
+  // transposed-read byte offsets: operand pi, half h; lane 4q+p of group g reads row
+  // 8g+4h+q, features pi*16 + 4p .. +3
+  __device__ __forceinline__ int tr_addr(int pi, int h) const {
+    const int row = 8 * g + 4 * h + q4;
+    const int pc = 2 * pi + (p4 >> 1);
     const int sc = (pc - CI::rot(row) + PPR) % PPR;
-    return row * KP * 2 + sc * 16 + (pp & 1) * 8;
-  };
-  const int64_t nch = (end - beg + 31) / 32;
-  auto load_cols = [&](int64_t ch, int (&cols)[NPL]) {
+    return row * KP * 2 + sc * 16 + (p4 & 1) * 8;
+  }
+  __device__ __forceinline__ void load_cols(const AlsParams& p, int64_t ch, int (&cols)[NPL]) {
     const int64_t c = beg + ch * 32;
 #pragma unroll
     for (int it = 0; it < NPL; ++it) {
       const int64_t ri = c + srow[it] < end ? c + srow[it] : end - 1;
       cols[it] = p.col_idx[ri];
     }
-  };
-  auto load_val = [&](int64_t ch, float& val) {
+  }
+  __device__ __forceinline__ void load_val(const AlsParams& p, int64_t ch, float& val) {
     const int64_t c = beg + ch * 32;
     const int64_t vi = c + (lane & 31) < end ? c + (lane & 31) : end - 1;
     val = p.vals[vi];
-  };
-  auto gather = [&](const int (&cols)[NPL], i32x4 (&stg)[NPL]) {
+  }
+  __device__ __forceinline__ void gather(const AlsParams& p, const int (&cols)[NPL],
+                                         i32x4 (&stg)[NPL]) {
 #pragma unroll
     for (int it = 0; it < NPL; ++it)
       stg[it] = *reinterpret_cast<const i32x4*>(p.Y + (int64_t)cols[it] * KP + soff[it]);
-  };
-  i32x4 stg0[NPL], stg1[NPL], stg2[NPL];
-  int cols0[NPL], cols1[NPL], cols2[NPL];
-  float val0 = 0.f, val1 = 0.f, val2 = 0.f;
-
+  }
+  // issue the first three chunks of ratings [b, e) in two stages, so the second stage (the
+  // gathers, which need the column indices) can come once the indices have arrived:
+  // stage 1 [cols(0..2), val(0..2)], stage 2 G(0) [cols(3)] G(1) [cols(4)] G(2)
+  __device__ __forceinline__ void prefetch_meta(const AlsParams& p, int64_t b, int64_t e) {
+    beg = b;
+    end = e;
+    nch = e > b ? (e - b + 31) / 32 : 0;
+    if (nch == 0) return;
+    load_cols(p, 0, cols0);
+    if (nch > 1) load_cols(p, 1, cols1);
+    if (nch > 2) load_cols(p, 2, cols2);
+    load_val(p, 0, val0);
+    if (nch > 1) load_val(p, 1, val1);
+    if (nch > 2) load_val(p, 2, val2);
+  }
+  __device__ __forceinline__ void prefetch_gather(const AlsParams& p) {
+    if (nch == 0) return;
+    gather(p, cols0, stg0);
+    if (nch > 3) load_cols(p, 3, cols0);
+    if (nch > 1) gather(p, cols1, stg1);
+    if (nch > 4) load_cols(p, 4, cols1);
+    if (nch > 2) gather(p, cols2, stg2);
+  }
   // chunk ch: stg / val hold its data, cols_g the metadata of chunk ch+3 (gathered into stg
   // once its image is in LDS), cols_l the free slot that receives cols(ch+5)
-  auto chunk = [&](int64_t ch, i32x4 (&stg)[NPL], float& val, int (&cols_g)[NPL],
-                   int (&cols_l)[NPL]) {
+  __device__ __forceinline__ void chunk(const AlsParams& p, int64_t ch, i32x4 (&stg)[NPL],
+                                        float& val, int (&cols_g)[NPL], int (&cols_l)[NPL],
+                                        char* G, float* Wab, f32x4 (&acc)[M * (M + 1) / 2],
+                                        float (&bpart)[M], float& cnt_acc) {
     const int64_t c0 = beg + ch * 32;
     const int n = (int)min((int64_t)32, end - c0);
     float wa = 0.f, wb = 0.f, cn = 0.f;
@@ -327,10 +363,10 @@ __device__ __forceinline__ void wave_accumulate3(const AlsParams& p, int64_t beg
     for (int it = 0; it < NPL; ++it)
       *reinterpret_cast<i32x4*>(G + (it * 64 + lane) * 16) = stg[it];
     wave_sync();
-    if (ch + 5 < nch) load_cols(ch + 5, cols_l);
+    if (ch + 5 < nch) load_cols(p, ch + 5, cols_l);
     if (ch + 3 < nch) {
-      load_val(ch + 3, val);
-      gather(cols_g, stg);
+      load_val(p, ch + 3, val);
+      gather(p, cols_g, stg);
     }
     const f32x4* wv = reinterpret_cast<const f32x4*>(Wab);
     const f32x4 wa0 = wv[2 * g], wa1 = wv[2 * g + 1];
@@ -366,30 +402,18 @@ __device__ __forceinline__ void wave_accumulate3(const AlsParams& p, int64_t beg
       for (int j = 0; j < 4; ++j) bpart[pi] += wb1[j] * (float)fb[pi][4 + j];
     }
     wave_sync();
-  };
-
-  // prologue: [cols(0..2), val(0)] G(0) [cols(3), val(1)] G(1) [cols(4), val(2)] G(2)
-  load_cols(0, cols0);
-  if (nch > 1) load_cols(1, cols1);
-  if (nch > 2) load_cols(2, cols2);
-  load_val(0, val0);
-  gather(cols0, stg0);
-  if (nch > 3) load_cols(3, cols0);
-  if (nch > 1) {
-    load_val(1, val1);
-    gather(cols1, stg1);
   }
-  if (nch > 4) load_cols(4, cols1);
-  if (nch > 2) {
-    load_val(2, val2);
-    gather(cols2, stg2);
+  // consume every chunk of the prefetched ratings
+  __device__ __forceinline__ void run(const AlsParams& p, char* G, float* Wab,
+                                      f32x4 (&acc)[M * (M + 1) / 2], float (&bpart)[M],
+                                      float& cnt_acc) {
+    for (int64_t ch = 0; ch < nch; ch += 3) {
+      chunk(p, ch, stg0, val0, cols0, cols2, G, Wab, acc, bpart, cnt_acc);
+      if (ch + 1 < nch) chunk(p, ch + 1, stg1, val1, cols1, cols0, G, Wab, acc, bpart, cnt_acc);
+      if (ch + 2 < nch) chunk(p, ch + 2, stg2, val2, cols2, cols1, G, Wab, acc, bpart, cnt_acc);
+    }
   }
-  for (int64_t ch = 0; ch < nch; ch += 3) {
-    chunk(ch, stg0, val0, cols0, cols2);
-    if (ch + 1 < nch) chunk(ch + 1, stg1, val1, cols1, cols0);
-    if (ch + 2 < nch) chunk(ch + 2, stg2, val2, cols2, cols1);
-  }
-}
+};
 
 // sum the per-lane b partials over the 4 lane groups; lane f then takes feature f (+64h)
 template <int M>
@@ -642,6 +666,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
   constexpr int NT = M * (M + 1) / 2;
   constexpr int LS = PS::LS;
   __shared__ __attribute__((aligned(16))) char smem[4 * PS::BYTES];
+  // DEEP: the block's copy of YtY, row stride KP + 4 floats (lane-per-row 16-byte reads are
+  // bank-conflict free); global loads during the factorization would drain the prefetch
+  constexpr int YS = KP + 4;
+  __shared__ __attribute__((aligned(16))) float ytys[DEEP ? KP * YS : 4];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -651,6 +679,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
   const int g = lane >> 4, fl = lane & 15;
   const int total_waves = gridDim.x * 4;
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+  GatherRing<KP> ring;
+  if (DEEP) {
+    for (int i = threadIdx.x; i < KP * KP / 4; i += 256) {
+      const int r = (4 * i) / KP, c = (4 * i) % KP;
+      *reinterpret_cast<f32x4*>(ytys + r * YS + c) =
+          reinterpret_cast<const f32x4*>(p.YtY)[i];
+    }
+    __syncthreads();
+    ring.init();
+    const int w0 = blockIdx.x * 4 + wave;
+    if (ORYX_ALS_XROW_PREFETCH && w0 < p.n_work) {
+      const int row0 = p.row_ids ? p.row_ids[w0] : w0;
+      const int slot0 = p.long_slot ? p.long_slot[w0] : -1;
+      const int64_t b0 = p.row_ptr[row0];
+      ring.prefetch_meta(p, b0, slot0 < 0 ? p.row_ptr[row0 + 1] : b0);
+      ring.prefetch_gather(p);
+    }
+  }
 
   for (int w = blockIdx.x * 4 + wave; w < p.n_work; w += total_waves) {
     const int row = p.row_ids ? p.row_ids[w] : w;
@@ -672,9 +718,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
 #pragma unroll
       for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
       // acc = sum over the row's ratings (split rows: nothing here, partials from ws below)
-      if (DEEP)
-        wave_accumulate3<KP>(p, beg, slot < 0 ? end : beg, my, Wab, acc, bpart, cnt_acc);
-      else
+      if (DEEP) {
+        if (!ORYX_ALS_XROW_PREFETCH) {
+          ring.prefetch_meta(p, beg, slot < 0 ? end : beg);
+          ring.prefetch_gather(p);
+        }
+        ring.run(p, my, Wab, acc, bpart, cnt_acc);
+        // the next row's metadata now, its first three chunk gathers after this row's first
+        // panel: they are in flight while this row is factored
+        const int wn = w + total_waves;
+        if (ORYX_ALS_XROW_PREFETCH && wn < p.n_work) {
+          const int rown = p.row_ids ? p.row_ids[wn] : wn;
+          const int slotn = p.long_slot ? p.long_slot[wn] : -1;
+          const int64_t bn = p.row_ptr[rown];
+          ring.prefetch_meta(p, bn, slotn < 0 ? p.row_ptr[rown + 1] : bn);
+        } else {
+          ring.nch = 0;
+        }
+      } else
         wave_accumulate<KP, false>(p, beg, slot < 0 ? end : beg, my, Wab, acc, bpart, cnt_acc);
       reduce_bpart<M>(bpart);
       bz = pick_bpart<M>(bpart, g);   // lane l (< KP): b[l]
@@ -712,10 +773,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
       // loaded: all are plain additions to A, and tile (i, j)'s share is only needed once
       // panel j is factored (the trailing updates before that just subtract from it)
       const int rr = ln < KP ? ln : 0;
-      const f32x4* yr = reinterpret_cast<const f32x4*>(p.YtY + rr * KP + 16 * pp);
       f32x4 yv[4];
+      if (DEEP) {
+        const lds_f32x4* yr = reinterpret_cast<const lds_f32x4*>(
+            (const lds_float*)ytys + rr * YS + 16 * pp);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) yv[q] = yr[q];
+        for (int q = 0; q < 4; ++q) yv[q] = yr[q];
+      } else {
+        const f32x4* yr = reinterpret_cast<const f32x4*>(p.YtY + rr * KP + 16 * pp);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) yv[q] = yr[q];
+      }
       if (wsrow) {
         const f32x4* wr = reinterpret_cast<const f32x4*>(wsrow + rr * KP + 16 * pp);
 #pragma unroll
@@ -738,14 +806,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
       ORYX_PHASE(2)
       // eliminate the panel's 16 columns; lane r > J ends with L[r][J] in pr[J - 16pp], lane J
       // with d_J (lanes below J hold values that are never read: the trailing update uses rows
-      // below the diagonal block, and back substitution only lanes c < J of row J)
+      // below the diagonal block, and back substitution only lanes c < J of row J).
+      // Critical path per step: pivot -> rsq -> l -> readlane L[J+1][J] -> update column j+1
+      // -> next pivot, all in registers; the other columns (j+2..15) take column J through an
+      // LDS broadcast whose round trip overlaps the next step's pivot work.  A wave's LDS
+      // accesses complete in order and the slot array aliases, so no fence is needed between
+      // a step's broadcast write, its reads, and the next step's write.
+      float sp = oryx_readlane(pr[0], 16 * pp);
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int J = 16 * pp + j;
-        float s = oryx_readlane(pr[j], J);
         // not positive (or NaN) -> clamped to 1e-30; detected from 1/d below (per-step
         // boolean flags get sunk to the end of the row and pin all 64 pivots in SGPRs)
-        s = s > 1e-30f ? s : 1e-30f;
+        const float s = sp > 1e-30f ? sp : 1e-30f;
         const float inv = __builtin_amdgcn_rsqf(s);
         const float l = pr[j] * inv;   // lane J: s / sqrt(s) = d_J
         pr[j] = l;
@@ -762,20 +835,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
         // use in the back substitution and keeps every step's 1/d and z live (spills)
         asm volatile("" : "+v"(dinv), "+v"(z_own), "+v"(bz));
         if (j < 15) {
-          // column J of the diagonal block to every lane: one ds_write_b32 per lane (own
-          // slot), broadcast ds_read_b128 of the 16-entry block, packed FMAs
-          bcl[ln] = l;
-          wave_sync();
-          f32x4 bq[4];
+          if (j < 14) bcl[ln] = l;
+          const float a1 = oryx_readlane(l, J + 1);   // L[J+1][J]
+          pr[j + 1] -= l * a1;
+          asm volatile("" : "+v"(pr[j + 1]));
+          sp = oryx_readlane(pr[j + 1], J + 1);
+          if (j < 14) {
+            f32x4 bq[4];
 #pragma unroll
-          for (int q = (j + 1) / 4; q < 4; ++q)
-            bq[q] = *reinterpret_cast<const lds_f32x4*>(bcl + 16 * pp + 4 * q);
+            for (int q = (j + 2) / 4; q < 4; ++q)
+              bq[q] = *reinterpret_cast<const lds_f32x4*>(bcl + 16 * pp + 4 * q);
 #pragma unroll
-          for (int jj = j + 1; jj < 16; ++jj) {
-            pr[jj] -= l * bq[jj / 4][jj % 4];
-            asm volatile("" : "+v"(pr[jj]));
+            for (int jj = j + 2; jj < 16; ++jj) {
+              pr[jj] -= l * bq[jj / 4][jj % 4];
+              asm volatile("" : "+v"(pr[jj]));
+            }
           }
-          wave_sync();
         }
       }
       if (inp) {
@@ -802,6 +877,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
             }
         }
       }
+      if (DEEP && ORYX_ALS_XROW_PREFETCH && pp == 0) ring.prefetch_gather(p);
       ORYX_PHASE(4)
     }
     // a clamped pivot gives 1/d = 1e15
