@@ -27,6 +27,26 @@
 
 #include "common.h"
 
+#include <type_traits>
+
+// compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>) (or descending); the body
+// sees its index as a constant, so register arrays indexed by it never fall back to scratch
+// (#pragma unroll gives up on very large bodies)
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (N > 0) {
+    static_for<N - 1>(f);
+    f(std::integral_constant<int, N - 1>{});
+  }
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for_desc(F&& f) {
+  if constexpr (N > 0) {
+    f(std::integral_constant<int, N - 1>{});
+    static_for_desc<N - 1>(f);
+  }
+}
+
 typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 // 1: the next row's first chunk gathers are issued during this row's factorization
@@ -1000,6 +1020,269 @@ __global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* _
   }
 }
 
+// ------------------------------------------------------------------ wide panel kernel (KP 80..128)
+
+// One wave per row for 64 < KP <= 128: lane r owns rows r and r + 64 in the panel phases.
+//   * A = YtY + sum c_i y_i y_i^T accumulates in 36 (KP=128) 16x16 MFMA tiles that start at YtY
+//     (wave_accumulate<KP, true>); lambda * n_u goes onto the diagonal in accumulator layout;
+//   * right-looking blocked Cholesky over 16-column panels, as in als_solve_panel, with the
+//     trailing tiles updated on v_mfma_f32_16x16x4_f32; each factored panel's L tiles are
+//     written back into the accumulators it came from, so the whole factor stays in registers
+//     and LDS only ever holds one panel (10 KB at KP=128 instead of 46 KB for all of them);
+//   * the forward solve rides along as an augmented column; pivots' 1/d and z go to LDS;
+//   * blocked back substitution from the last panel: panel p comes back to LDS once, 64
+//     lanes form sum_{J in later blocks} L[J][c] x_J for its 16 columns (4 row groups, two
+//     cross-lane adds), then a 16-step triangular solve finishes the block.
+template <int KP>
+struct WideSmem {
+  static constexpr int LS = 20;
+  static constexpr int PB = KP * LS * 4;
+  static constexpr int GB = ChunkImage<KP>::BYTES;
+  static constexpr int RAW = PB > GB ? PB : GB;
+  // + broadcast slots (128), 1/d (128), z (128), x (128), weights (64)
+  static constexpr int BYTES = (RAW + 15) / 16 * 16 + (4 * 128 + 64) * 4;
+};
+
+template <int KP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void als_solve_wide(
+    AlsParams p) {
+  using WS = WideSmem<KP>;
+  constexpr int M = KP / 16;
+  constexpr int NT = M * (M + 1) / 2;
+  constexpr int LS = WS::LS;
+  typedef __attribute__((address_space(3))) float lds_float;
+  typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+  __shared__ __attribute__((aligned(16))) char smem[4 * WS::BYTES];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  char* my = smem + wave * WS::BYTES;
+  float* P = reinterpret_cast<float*>(my);
+  lds_float* bcl = (lds_float*)(my + (WS::RAW + 15) / 16 * 16);
+  lds_float* invs = bcl + 128;
+  lds_float* zs = bcl + 256;
+  lds_float* xs = bcl + 384;
+  float* Wab = reinterpret_cast<float*>(my + (WS::RAW + 15) / 16 * 16 + 512 * 4);
+  const int g = lane >> 4, fl = lane & 15;
+  const int total_waves = gridDim.x * 4;
+
+  for (int w = blockIdx.x * 4 + wave; w < p.n_work; w += total_waves) {
+    const int row = p.row_ids ? p.row_ids[w] : w;
+    const int64_t beg = p.row_ptr[row], end = p.row_ptr[row + 1];
+    const int slot = p.long_slot ? p.long_slot[w] : -1;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float bz0, bz1, cnt_acc = 0.f;
+    {
+      float bpart[M];
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
+      wave_accumulate<KP, false>(p, beg, slot < 0 ? end : beg, my, Wab, acc, bpart, cnt_acc);
+      reduce_bpart<M>(bpart);
+      // lane (g, fl) holds b[pi*16 + fl] for every pi: rows lane and lane + 64
+      bz0 = pick_bpart<M>(bpart, g);
+      bz1 = pick_bpart<M>(bpart, g + 4);
+    }
+    float cnt = wave_sum(cnt_acc);
+    const float* wsrow = nullptr;
+    if (slot >= 0) {
+      const float* src = p.ws + (int64_t)slot * ws_stride(KP);
+      bz0 = src[KP * KP + lane];
+      bz1 = src[KP * KP + (lane + 64 < KP ? lane + 64 : 0)];
+      cnt = src[KP * KP + KP];
+      wsrow = src;
+    }
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+
+    static_for<M>([&](auto PPc) {
+      constexpr int pp = decltype(PPc)::value;
+      // panel tiles (i, pp), i >= pp -> LDS rows (r - 16pp)
+#pragma unroll
+      for (int i = pp; i < M; ++i) {
+        const int t = i * (i + 1) / 2 + pp;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) P[(16 * (i - pp) + 4 * g + v) * LS + fl] = acc[t][v];
+      }
+      wave_sync();
+      // lane rows ln (set 0) and ln + 64 (set 1); rows outside [16pp, KP) read row 16pp (junk)
+      const int r0 = ln >= 16 * pp ? ln - 16 * pp : 0;
+      const int r1 = ln + 64 >= 16 * pp && ln + 64 < KP ? ln + 64 - 16 * pp : 0;
+      // + YtY (and a split row's partial sums) and lambda * n_u, added as each panel is loaded
+      // (plain additions to A; tile (i, j)'s share is only needed once panel j is factored)
+      const int ra = ln, rb = ln + 64 < KP ? ln + 64 : 0;
+      f32x4 ya[4], yb[4];
+      {
+        const f32x4* y0 = reinterpret_cast<const f32x4*>(p.YtY + ra * KP + 16 * pp);
+        const f32x4* y1 = reinterpret_cast<const f32x4*>(p.YtY + rb * KP + 16 * pp);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          ya[q] = y0[q];
+          yb[q] = y1[q];
+        }
+        if (wsrow) {
+          const f32x4* w0 = reinterpret_cast<const f32x4*>(wsrow + ra * KP + 16 * pp);
+          const f32x4* w1 = reinterpret_cast<const f32x4*>(wsrow + rb * KP + 16 * pp);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            ya[q] += w0[q];
+            yb[q] += w1[q];
+          }
+        }
+      }
+      float pa[16], pb[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 va = *reinterpret_cast<const f32x4*>(P + r0 * LS + 4 * q);
+        const f32x4 vb = *reinterpret_cast<const f32x4*>(P + r1 * LS + 4 * q);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pa[4 * q + e] = va[e] + ya[q][e];
+          pb[4 * q + e] = vb[e] + yb[q][e];
+        }
+      }
+      {
+        int rel = ln - 16 * pp;
+        asm volatile("" : "+v"(rel));
+        const float dga = ln < p.k ? p.lambda * cnt : 1.f;
+        const float dgb = ln + 64 < p.k ? p.lambda * cnt : 1.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          pa[j] += rel == j ? dga : 0.f;
+          pb[j] += rel + 64 == j ? dgb : 0.f;
+        }
+      }
+      // the panel's diagonal block lives in set 0 (pp < 4) or set 1 (pp >= 4)
+      const bool hi = pp >= 4;
+      float sp = hi ? oryx_readlane(pb[0], 16 * pp - 64) : oryx_readlane(pa[0], 16 * pp);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int J = 16 * pp + j;
+        const float s = sp > 1e-30f ? sp : 1e-30f;
+        const float inv = __builtin_amdgcn_rsqf(s);
+        const float la = pa[j] * inv, lb = pb[j] * inv;   // row J's lane: d_J
+        pa[j] = la;
+        pb[j] = lb;
+        const float zJ = (hi ? oryx_readlane(bz1, J - 64) : oryx_readlane(bz0, J)) * inv;
+        bz0 -= la * zJ;
+        bz1 -= lb * zJ;
+        if (lane == 0) {
+          invs[J] = inv;
+          zs[J] = zJ;
+        }
+        asm volatile("" : "+v"(bz0), "+v"(bz1));
+        if (j < 15) {
+          const float lJ = hi ? lb : la;     // column J of the diagonal-block rows
+          if (j < 14) bcl[ln] = lJ;
+          const float a1 = oryx_readlane(lJ, (J + 1) & 63);   // L[J+1][J]
+          pa[j + 1] -= la * a1;
+          pb[j + 1] -= lb * a1;
+          asm volatile("" : "+v"(pa[j + 1]), "+v"(pb[j + 1]));
+          sp = hi ? oryx_readlane(pb[j + 1], J + 1 - 64) : oryx_readlane(pa[j + 1], J + 1);
+          if (j < 14) {
+            const int base = (16 * pp) & 63;
+            f32x4 bq[4];
+#pragma unroll
+            for (int q = (j + 2) / 4; q < 4; ++q)
+              bq[q] = *reinterpret_cast<const lds_f32x4*>(bcl + base + 4 * q);
+#pragma unroll
+            for (int jj = j + 2; jj < 16; ++jj) {
+              pa[jj] -= la * bq[jj / 4][jj % 4];
+              pb[jj] -= lb * bq[jj / 4][jj % 4];
+              asm volatile("" : "+v"(pa[jj]), "+v"(pb[jj]));
+            }
+          }
+        }
+      }
+      // factored panel back to LDS (rows >= 16pp of each set)
+      if (ln >= 16 * pp) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(P + r0 * LS + 4 * q) =
+              f32x4{pa[4 * q], pa[4 * q + 1], pa[4 * q + 2], pa[4 * q + 3]};
+      }
+      if (ln + 64 >= 16 * pp && ln + 64 < KP) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          *reinterpret_cast<f32x4*>(P + r1 * LS + 4 * q) =
+              f32x4{pb[4 * q], pb[4 * q + 1], pb[4 * q + 2], pb[4 * q + 3]};
+      }
+      wave_sync();
+      // trailing update A(i, jt) -= L(i, pp) L(jt, pp)^T on fp32 MFMA
+      if (pp + 1 < M) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          float fr[M];
+#pragma unroll
+          for (int i = pp + 1; i < M; ++i) fr[i] = P[(16 * (i - pp) + fl) * LS + 4 * kk + g];
+#pragma unroll
+          for (int i = pp + 1; i < M; ++i)
+#pragma unroll
+            for (int jt = pp + 1; jt <= i; ++jt) {
+              const int t = i * (i + 1) / 2 + jt;
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(-fr[i], fr[jt], acc[t], 0, 0, 0);
+            }
+        }
+      }
+      // L(i, pp) tiles back into the accumulators they came from (kept for the solve)
+#pragma unroll
+      for (int i = pp; i < M; ++i) {
+        const int t = i * (i + 1) / 2 + pp;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[t][v] = P[(16 * (i - pp) + 4 * g + v) * LS + fl];
+      }
+      wave_sync();
+    });
+    {
+      // a clamped pivot gives 1/d = 1e15
+      const float d0 = invs[lane], d1 = lane + 64 < KP ? invs[lane + 64] : 0.f;
+      if (__any(!(d0 < 9.9e14f) || !(d1 < 9.9e14f)) && lane == 0 && p.fail_count)
+        atomicAdd(p.fail_count, 1);
+    }
+    // blocked back substitution L^T x = z, last panel first
+    static_for_desc<M>([&](auto PPc) {
+      constexpr int pp = decltype(PPc)::value;
+#pragma unroll
+      for (int i = pp; i < M; ++i) {
+        const int t = i * (i + 1) / 2 + pp;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) P[(16 * (i - pp) + 4 * g + v) * LS + fl] = acc[t][v];
+      }
+      wave_sync();
+      // rhs_c = z_c - sum_{J >= 16(pp+1)} L[J][c] x_J; lane (g, fl): column 16pp + fl, rows
+      // J = 16(pp+1) + 4m + g
+      float part = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4 * (M - 1 - pp); ++m) {
+        const int jr = 16 + 4 * m;   // panel-local row of J - g
+        part += P[(jr + g) * LS + fl] * xs[16 * (pp + 1) + 4 * m + g];
+      }
+      part += __shfl_xor(part, 16, 64);
+      part += __shfl_xor(part, 32, 64);
+      float rhs = zs[16 * pp + fl] - part;   // every g-group holds the same 16 values
+#pragma unroll
+      for (int cc = 15; cc >= 0; --cc) {
+        const int c = 16 * pp + cc;
+        const float x = oryx_readlane(rhs, cc) * invs[c];
+        if (lane == 0) xs[c] = x;
+        rhs -= P[cc * LS + fl] * x;     // row c of the panel, column 16pp + fl (fl < cc used)
+      }
+      wave_sync();
+    });
+    if (lane < KP) {
+      const float x0 = xs[lane];
+      p.X[(int64_t)row * KP + lane] = x0;
+      if (p.Xb) p.Xb[(int64_t)row * KP + lane] = (__bf16)x0;
+    }
+    if (lane + 64 < KP) {
+      const float x1 = xs[lane + 64];
+      p.X[(int64_t)row * KP + lane + 64] = x1;
+      if (p.Xb) p.Xb[(int64_t)row * KP + lane + 64] = (__bf16)x1;
+    }
+    wave_sync();
+  }
+}
+
 // ------------------------------------------------------------------ block-per-row kernel
 
 template <int KP>
@@ -1204,12 +1487,20 @@ __global__ __launch_bounds__(256) void pair_dots(const float* __restrict__ X,
 // per SIMD (default), 0 = als_solve_panel with one chunk in flight at 3 waves per SIMD,
 // 1 = als_solve_wave (register column Cholesky)
 static int g_als_variant = 2;
+// 64 < KP <= 128: 0 = als_solve_wide (default), 1 = als_solve_block (LDS Cholesky)
+static int g_als_wide_variant = 0;
 
 extern "C" {
 
 int oryx_als_set_variant(int v) {
   if (v < 0 || v > 2) return ORYX_EINVAL;
   g_als_variant = v;
+  return ORYX_OK;
+}
+
+int oryx_als_set_wide_variant(int v) {
+  if (v < 0 || v > 1) return ORYX_EINVAL;
+  g_als_wide_variant = v;
   return ORYX_OK;
 }
 
@@ -1273,8 +1564,14 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
 #undef WAVE_CASE
 #define BLOCK_CASE(KPV)                                                               \
   case KPV: {                                                                         \
-    int blocks = n_work < max_blocks ? n_work : max_blocks;                           \
-    hipLaunchKernelGGL(als_solve_block<KPV>, dim3(blocks), dim3(256), 0, s, p);      \
+    if (g_als_wide_variant == 0) {                                                    \
+      int blocks = (n_work + 3) / 4;                                                  \
+      if (blocks > max_blocks) blocks = max_blocks;                                   \
+      hipLaunchKernelGGL(als_solve_wide<KPV>, dim3(blocks), dim3(256), 0, s, p);     \
+    } else {                                                                          \
+      int blocks = n_work < max_blocks ? n_work : max_blocks;                         \
+      hipLaunchKernelGGL(als_solve_block<KPV>, dim3(blocks), dim3(256), 0, s, p);    \
+    }                                                                                 \
     break;                                                                            \
   }
     BLOCK_CASE(80)
