@@ -16,6 +16,7 @@ Normal equations (Spark MLlib's ALS, which the reference invokes at
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Optional, Tuple
 
@@ -80,8 +81,24 @@ class CSR:
         return self._ws
 
 
-SPLIT_THRESHOLD = 2048   # rows with more ratings than this are split ...
-SPLIT_SEGMENT = 1024     # ... into segments of this many ratings (one wave each)
+# Rows longer than the split threshold are cut into segments (one wave each, partial normal
+# equations added with fp32 atomics) so one popular row does not set the kernel's tail.  The
+# threshold adapts to the data: max(SPLIT_MIN, SPLIT_MEAN_FACTOR x mean row length), segments
+# half of it -- at 1 GPU (items: mean 423 ratings) that is 4096/2048, which measured 13 %
+# faster than 2048/1024 (fewer atomics); with 8 GPUs' item shards (mean ~3.4k) typical rows
+# stay whole.  ORYX_ALS_SPLIT="thr,seg" fixes both (tuning runs).
+SPLIT_MIN = 4096
+SPLIT_MEAN_FACTOR = 4
+_SPLIT_ENV = os.environ.get("ORYX_ALS_SPLIT")
+
+
+def split_params(nnz: int, n_nonempty: int) -> Tuple[int, int]:
+    if _SPLIT_ENV:
+        thr, seg = (int(v) for v in _SPLIT_ENV.split(","))
+        return thr, seg
+    mean = nnz / max(1, n_nonempty)
+    thr = max(SPLIT_MIN, int(SPLIT_MEAN_FACTOR * mean))
+    return thr, max(256, thr // 2)
 
 
 def ws_stride(kp: int) -> int:
@@ -111,8 +128,8 @@ def _split_long_rows(row_ptr: torch.Tensor, order: torch.Tensor, counts: torch.T
 
 
 def build_csr(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_rows: int,
-              n_cols: int, row_offset: int = 0, split_threshold: int = SPLIT_THRESHOLD,
-              split_segment: int = SPLIT_SEGMENT) -> CSR:
+              n_cols: int, row_offset: int = 0, split_threshold: Optional[int] = None,
+              split_segment: Optional[int] = None) -> CSR:
     """CSR of (row, col, val) triples (rows are global ids; ``row_offset`` makes them local).
 
     Triples must already be unique per (row, col).  Runs on the tensors' device.
@@ -129,8 +146,12 @@ def build_csr(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_rows
     torch.cumsum(counts, 0, out=row_ptr[1:])
     nz_rows = torch.nonzero(counts, as_tuple=False).flatten()
     order = nz_rows[torch.argsort(counts[nz_rows], descending=True, stable=True)]
-    long_slot, segs, n_long = _split_long_rows(row_ptr, order, counts, split_threshold,
-                                               split_segment)
+    thr, seg = split_params(int(key.numel()), int(nz_rows.numel()))
+    if split_threshold is not None:
+        thr = split_threshold
+    if split_segment is not None:
+        seg = split_segment
+    long_slot, segs, n_long = _split_long_rows(row_ptr, order, counts, thr, seg)
     return CSR(row_ptr, c_sorted.contiguous(), v_sorted.contiguous(), int(n_rows), int(n_cols),
                order.to(torch.int32).contiguous(), long_slot, segs, n_long)
 

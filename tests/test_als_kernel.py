@@ -169,3 +169,11 @@ def test_gramian_kernel(cuda, n, kp):
     ref = (x.double().t() @ x.double()).float()
     assert torch.allclose(got, ref, rtol=1e-4, atol=1e-3 * max(1.0, n ** 0.5))
     assert torch.equal(got, got.t())
+
+
+def test_split_params_adapt_to_mean_row_length():
+    # 1 GPU item CSR of the bench (mean 423 ratings/row) -> 4096/2048; an 8-GPU item shard
+    # (mean ~3.4k) raises the threshold so typical rows stay on one wave
+    assert als_ops.split_params(25_000_000, 59_047) == (4096, 2048)
+    thr, seg = als_ops.split_params(25_000_000, 7_381)
+    assert thr == 4 * int(25_000_000 / 7_381) and seg == thr // 2
