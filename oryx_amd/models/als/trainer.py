@@ -9,8 +9,12 @@ Replaces Spark MLlib's block ALS that the reference runs at
 * every rank keeps a replicated bf16 copy of both factor matrices (the gather operand of the
   fused solve kernel) and an fp32 master copy of its own row shard;
 * per half-step: partial Gramians of the owned fp32 shard are all-reduced (k x k, one call),
-  the fused HIP kernel solves the owned rows, and the new bf16 shard is all-gathered
-  (one RCCL all-gather per half-step, striped over the xGMI links);
+  then the owned rows are solved in ``gather_chunks`` row ranges; as soon as a range is
+  solved its bf16 rows are all-gathered asynchronously (RCCL, striped over the xGMI links)
+  while the fused HIP kernel solves the next range, so only the last range's exchange is
+  exposed.  The replicated bf16 factor matrices are laid out chunk-major
+  ([chunk][rank][row], see :class:`RowLayout`) so that each range's all-gather writes one
+  contiguous block; the CSR column indices are remapped to that layout once, in prepare();
 * iteration order follows MLlib: items from users, then users from items.
 
 With world size 1 no collectives are issued.  On CPU the exact fp32 reference solve runs.
@@ -54,6 +58,55 @@ class ALSFactors:
     Y: torch.Tensor   # fp32 [n_items, k]
 
 
+class RowLayout:
+    """Row order of a replicated factor matrix gathered in chunks.
+
+    ``n`` rows are sharded over ``W`` ranks in equal padded shards of ``s`` rows; each shard is
+    cut into ``C`` ranges of ``cr`` rows.  Gathered row of global id ``r*s + l`` (rank r, local
+    l = c*cr + o): ``(c*W + r)*cr + o``.  With C = 1 this is the plain rank-major layout and
+    with W = 1 it is the identity.
+    """
+
+    def __init__(self, n: int, world: int, chunks: int):
+        self.n, self.W = int(n), int(world)
+        self.s = dist.padded_shard_size(self.n, self.W)
+        self.C = max(1, min(int(chunks), self.s)) if self.s > 0 else 1
+        self.cr = max(1, -(-self.s // self.C))
+
+    @property
+    def local_rows(self) -> int:
+        return self.C * self.cr
+
+    @property
+    def rows(self) -> int:
+        return self.C * self.W * self.cr
+
+    def remap(self, ids: torch.Tensor) -> torch.Tensor:
+        ids = ids.to(torch.int64)
+        r = torch.div(ids, self.s, rounding_mode="floor")
+        loc = ids - r * self.s
+        c = torch.div(loc, self.cr, rounding_mode="floor")
+        return (c * self.W + r) * self.cr + (loc - c * self.cr)
+
+    def gather(self, local: torch.Tensor, ctx: dist.DistContext, overlap_with=None):
+        """All-gather ``local`` ([local_rows, ...]) into the gathered layout; ``overlap_with``
+        (callable c -> None) runs before each range's exchange is started."""
+        out = torch.empty((self.rows,) + tuple(local.shape[1:]), dtype=local.dtype,
+                          device=local.device)
+        handles = []
+        for c in range(self.C):
+            if overlap_with is not None:
+                overlap_with(c)
+            handles.append(dist.all_gather_rows_async(
+                local[c * self.cr:(c + 1) * self.cr],
+                out[c * self.W * self.cr:(c + 1) * self.W * self.cr], ctx))
+        with watchdog.guard("all_gather_rows"):
+            for h in handles:
+                if h is not None:
+                    h.wait()
+        return out
+
+
 def _unit_gaussian(n: int, k: int, kp: int, gen: torch.Generator, device) -> torch.Tensor:
     v = torch.randn((n, k), generator=gen, dtype=torch.float32, device="cpu")
     v = v / v.norm(dim=1, keepdim=True).clamp_min(1e-12)
@@ -64,7 +117,8 @@ def _unit_gaussian(n: int, k: int, kp: int, gen: torch.Generator, device) -> tor
 
 class ALSTrainer:
     def __init__(self, features: int, lam: float, alpha: float, implicit: bool,
-                 ctx: Optional[dist.DistContext] = None, seed: int = 0):
+                 ctx: Optional[dist.DistContext] = None, seed: int = 0,
+                 gather_chunks: Optional[int] = None):
         self.k = int(features)
         self.kp = als_ops.padded_rank(self.k)
         self.lam = float(lam)
@@ -75,6 +129,10 @@ class ALSTrainer:
         self.seed = int(seed)
         self.timings: Dict[str, float] = {}
         self.fail_count = None
+        # row ranges per half-step whose factor exchange overlaps the next range's solve
+        self._explicit_chunks = bool(gather_chunks)
+        self.gather_chunks = int(gather_chunks) if gather_chunks else (
+            4 if self.ctx.is_distributed else 1)
 
     # ------------------------------------------------------------------ data
     def prepare(self, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tensor,
@@ -97,14 +155,41 @@ class ALSTrainer:
         t0 = time.perf_counter()
         by_user = self._route(users, items, ratings, users // self.su)
         by_item = self._route(users, items, ratings, items // self.si)
-        self.csr_u = als_ops.build_csr(by_user[0], by_user[1], by_user[2], self.u_hi - self.u_lo,
-                                       self.n_items, row_offset=self.u_lo)
-        self.csr_i = als_ops.build_csr(by_item[1], by_item[0], by_item[2], self.i_hi - self.i_lo,
-                                       self.n_users, row_offset=self.i_lo)
+        self.lay_u = RowLayout(self.n_users, W, self._chunks_for(self.n_users))
+        self.lay_i = RowLayout(self.n_items, W, self._chunks_for(self.n_items))
+        # column ids index the gathered (chunk-major) copy of the opposite factors
+        self.csr_u = als_ops.build_csr(by_user[0], self.lay_i.remap(by_user[1]), by_user[2],
+                                       self.u_hi - self.u_lo, self.lay_i.rows,
+                                       row_offset=self.u_lo)
+        self.csr_i = als_ops.build_csr(by_item[1], self.lay_u.remap(by_item[0]), by_item[2],
+                                       self.i_hi - self.i_lo, self.lay_u.rows,
+                                       row_offset=self.i_lo)
+        self.csr_u_parts = self._row_parts(self.csr_u, self.lay_u)
+        self.csr_i_parts = self._row_parts(self.csr_i, self.lay_i)
         self.local_nnz = self.csr_u.nnz
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         self.timings["prepare_s"] = time.perf_counter() - t0
+
+    # a factor matrix is exchanged in ranges only when the exchange is worth hiding and each
+    # range still fills the GPU (small ranges leave CUs idle in every launch's tail)
+    OVERLAP_MIN_BYTES = 16 << 20
+    OVERLAP_MIN_ROWS = 8192
+
+    def _chunks_for(self, n_total: int) -> int:
+        c = self.gather_chunks
+        if c <= 1 or self._explicit_chunks:
+            return max(1, c)
+        shard = dist.padded_shard_size(n_total, self.ctx.world_size)
+        if n_total * self.kp * 2 < self.OVERLAP_MIN_BYTES or shard // c < self.OVERLAP_MIN_ROWS:
+            return 1
+        return c
+
+    @staticmethod
+    def _row_parts(csr: als_ops.CSR, lay: RowLayout) -> List[als_ops.CSR]:
+        if lay.C == 1:
+            return [csr]
+        return [csr.row_range(c * lay.cr, (c + 1) * lay.cr) for c in range(lay.C)]
 
     def _route(self, users, items, ratings, owner):
         ctx = self.ctx
@@ -127,8 +212,9 @@ class ALSTrainer:
         gen = torch.Generator(device="cpu")
         gen.manual_seed((self.seed * 1000003 + ctx.rank) & ((1 << 62) - 1))
         nu, ni = self.u_hi - self.u_lo, self.i_hi - self.i_lo
-        self.X = torch.zeros((self.su, kp), dtype=torch.float32, device=dev)
-        self.Y = torch.zeros((self.si, kp), dtype=torch.float32, device=dev)
+        # local shards padded to whole gather ranges (rows past the shard stay zero)
+        self.X = torch.zeros((self.lay_u.local_rows, kp), dtype=torch.float32, device=dev)
+        self.Y = torch.zeros((self.lay_i.local_rows, kp), dtype=torch.float32, device=dev)
         self.X[:nu] = _unit_gaussian(nu, k, kp, gen, dev)
         self.Y[:ni] = _unit_gaussian(ni, k, kp, gen, dev)
         for init, dst, lo, hi in ((x_init, self.X, self.u_lo, self.u_hi),
@@ -144,8 +230,8 @@ class ALSTrainer:
         ctx = self.ctx
         self.Xb_local = self.X.to(torch.bfloat16)
         self.Yb_local = self.Y.to(torch.bfloat16)
-        self.Xb = dist.all_gather_rows(self.Xb_local, self.n_users, ctx).contiguous()
-        self.Yb = dist.all_gather_rows(self.Yb_local, self.n_items, ctx).contiguous()
+        self.Xb = self.lay_u.gather(self.Xb_local, ctx)
+        self.Yb = self.lay_i.gather(self.Yb_local, ctx)
         self.fail_count = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.iterations_done = 0
 
@@ -153,7 +239,8 @@ class ALSTrainer:
     def _layout(self, fingerprint: str, iteration: int) -> dict:
         return {"iteration": int(iteration), "world_size": self.ctx.world_size,
                 "n_users": self.n_users, "n_items": self.n_items, "k": self.k,
-                "kp": self.kp, "fingerprint": str(fingerprint)}
+                "kp": self.kp, "chunks": [self.lay_u.C, self.lay_i.C],
+                "fingerprint": str(fingerprint)}
 
     def save_checkpoint(self, directory: str, iteration: int, fingerprint: str = "") -> None:
         """Write this rank's shards for ``iteration`` (collective: every rank calls it)."""
@@ -202,7 +289,8 @@ class ALSTrainer:
         from safetensors.torch import load_file
         t = load_file(os.path.join(directory, "it%d" % iteration,
                                    "rank%d.safetensors" % ctx.rank))
-        if tuple(t["X"].shape) != (self.su, self.kp) or tuple(t["Y"].shape) != (self.si, self.kp):
+        if tuple(t["X"].shape) != (self.lay_u.local_rows, self.kp) or \
+                tuple(t["Y"].shape) != (self.lay_i.local_rows, self.kp):
             raise ValueError("checkpoint shard shapes do not match the trainer")
         self.X = t["X"].to(self.device)
         self.Y = t["Y"].to(self.device)
@@ -212,20 +300,22 @@ class ALSTrainer:
         return iteration
 
     # ------------------------------------------------------------------ iterations
-    def _half_step(self, csr, src_own_f32, src_full_bf16, dst_f32, dst_b_local, n_total_dst,
-                   name):
+    def _half_step(self, parts, src_own_f32, src_full_bf16, dst_f32, dst_b_local, lay, name):
         ctx = self.ctx
         yty = None
         if self.implicit:
             with tracing.range(name + ".gramian"):
                 yty = als_ops.gramian(src_own_f32)
                 dist.all_reduce_sum(yty, ctx)
-        with tracing.range(name + ".solve"):
-            als_ops.solve_rows(csr, src_full_bf16, yty, dst_f32, dst_b_local, self.k, self.lam,
-                               self.alpha, self.implicit, fail_count=self.fail_count)
-        with tracing.range(name + ".allgather"):
-            full = dist.all_gather_rows(dst_b_local, n_total_dst, ctx)
-        return full
+
+        def solve(c):
+            with tracing.range(name + ".solve"):
+                als_ops.solve_rows(parts[c], src_full_bf16, yty, dst_f32, dst_b_local, self.k,
+                                   self.lam, self.alpha, self.implicit,
+                                   fail_count=self.fail_count)
+        # range c's bf16 rows are exchanged while range c+1 is solved
+        with tracing.range(name + ".solve+allgather"):
+            return lay.gather(dst_b_local, ctx, overlap_with=solve)
 
     def iterate(self, iterations: int = 1) -> None:
         for _ in range(iterations):
@@ -233,10 +323,10 @@ class ALSTrainer:
             faults.point("als.iteration", iteration=self.iterations_done, rank=self.ctx.rank)
             watchdog.heartbeat("als.iteration")
             # items given users, then users given items (MLlib order)
-            self.Yb = self._half_step(self.csr_i, self.X, self.Xb, self.Y, self.Yb_local,
-                                      self.n_items, "als.items")
-            self.Xb = self._half_step(self.csr_u, self.Y, self.Yb, self.X, self.Xb_local,
-                                      self.n_users, "als.users")
+            self.Yb = self._half_step(self.csr_i_parts, self.X, self.Xb, self.Y, self.Yb_local,
+                                      self.lay_i, "als.items")
+            self.Xb = self._half_step(self.csr_u_parts, self.Y, self.Yb, self.X, self.Xb_local,
+                                      self.lay_u, "als.users")
 
     def train(self, iterations: int, checkpoint_dir: Optional[str] = None,
               checkpoint_interval: int = 0, fingerprint: str = "",
@@ -277,8 +367,8 @@ class ALSTrainer:
     def factors(self, gather: bool = True) -> ALSFactors:
         """Full fp32 factors (all-gathered from the owned shards)."""
         ctx = self.ctx
-        X = dist.all_gather_rows(self.X, self.n_users, ctx)[:self.n_users, :self.k]
-        Y = dist.all_gather_rows(self.Y, self.n_items, ctx)[:self.n_items, :self.k]
+        X = dist.all_gather_rows(self.X[:self.su], self.n_users, ctx)[:self.n_users, :self.k]
+        Y = dist.all_gather_rows(self.Y[:self.si], self.n_items, ctx)[:self.n_items, :self.k]
         return ALSFactors(X.contiguous(), Y.contiguous())
 
     @property

@@ -71,6 +71,22 @@ class CSR:
                    self.n_rows, self.n_cols, self.order.to(device), mv(self.long_slot),
                    mv(self.segs), self.n_long)
 
+    def row_range(self, lo: int, hi: int) -> "CSR":
+        """A view solving only rows [lo, hi): same arrays, its own work list and long-row
+        split (the shared workspace is re-zeroed by every launch, which is stream-ordered)."""
+        o = self.order.to(torch.int64)
+        order = o[(o >= lo) & (o < hi)]
+        counts = self.row_ptr[1:] - self.row_ptr[:-1]
+        long_slot, segs, n_long = (None, None, 0)
+        if self.long_slot is not None and order.numel():
+            # rows split in the full CSR stay split (same threshold: the shortest split row)
+            split_rows = o[:self.n_long]
+            thr = int(counts[split_rows].min()) - 1
+            seg = int((self.segs[:, 3] - self.segs[:, 2]).max())
+            long_slot, segs, n_long = _split_long_rows(self.row_ptr, order, counts, thr, seg)
+        return CSR(self.row_ptr, self.cols, self.vals, self.n_rows, self.n_cols,
+                   order.to(torch.int32).contiguous(), long_slot, segs, n_long)
+
     def workspace(self, kp: int) -> Optional[torch.Tensor]:
         """fp32 scratch for the split rows' partial normal equations (kernel zeroes it)."""
         if self.n_seg == 0:

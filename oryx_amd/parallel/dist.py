@@ -25,7 +25,8 @@ import torch.distributed as tdist
 from . import watchdog
 
 __all__ = ["DistContext", "init_from_env", "get_context", "shard_range", "padded_shard_size",
-           "all_gather_rows", "all_reduce_sum", "broadcast_object", "barrier"]
+           "all_gather_rows", "all_gather_rows_async", "all_reduce_sum", "broadcast_object",
+           "barrier"]
 
 
 @dataclass
@@ -144,6 +145,23 @@ def all_gather_rows(local: torch.Tensor, n_total: int, ctx: DistContext,
         else:
             tdist.all_gather_into_tensor(full, local.contiguous())
     return full
+
+
+def all_gather_rows_async(local: torch.Tensor, out: torch.Tensor, ctx: DistContext):
+    """Start an all-gather of one equal-size row block per rank into ``out`` (rank-major,
+    ``world_size * local.shape[0]`` rows); returns a work handle (``wait()``) or None.
+
+    With RCCL the collective runs on the communicator's stream after the kernels already
+    queued on the current stream (the producer of ``local``), so compute launched afterwards
+    overlaps it; ``wait()`` makes the current stream wait for it.
+    """
+    if not ctx.is_distributed:
+        out.copy_(local)
+        return None
+    if ctx.backend == "gloo":
+        parts = list(out.chunk(ctx.world_size, 0))
+        return tdist.all_gather(parts, local.contiguous(), async_op=True)
+    return tdist.all_gather_into_tensor(out, local.contiguous(), async_op=True)
 
 
 def all_reduce_sum(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:

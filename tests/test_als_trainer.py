@@ -44,7 +44,8 @@ def test_trainer_implicit_ranks_known_items_higher():
 
 
 def test_distributed_matches_single_process_gloo(tmp_path):
-    """world_size 2 over gloo (all-to-all shuffle, all-reduce YtY, all-gather) == world 1."""
+    """world_size 2 over gloo (all-to-all shuffle, all-reduce YtY, all-gather; also with the
+    factor exchange split into 3 asynchronous ranges) == world 1."""
     script = tmp_path / "run.py"
     script.write_text(f"""
 import sys, torch
@@ -58,7 +59,8 @@ u, i = key // 50, key % 50
 r = torch.randint(1, 6, (key.numel(),), generator=g).float()
 # every rank holds a different slice of the data
 sl = slice(ctx.rank, None, ctx.world_size)
-tr = ALSTrainer(5, lam=0.05, alpha=1.0, implicit=True, ctx=ctx, seed=3)
+tr = ALSTrainer(5, lam=0.05, alpha=1.0, implicit=True, ctx=ctx, seed=3,
+                gather_chunks=int(sys.argv[2]))
 tr.prepare(u[sl], i[sl], r[sl], 64, 50)
 # deterministic identical init regardless of world size
 gi = torch.Generator().manual_seed(11)
@@ -70,16 +72,18 @@ if ctx.rank == 0:
     torch.save({{'X': f.X, 'Y': f.Y}}, sys.argv[1])
 """)
     outs = []
-    for world in (1, 2):
-        out = tmp_path / f"w{world}.pt"
+    for world, chunks in ((1, 1), (2, 1), (2, 3)):
+        out = tmp_path / f"w{world}c{chunks}.pt"
         env = dict(os.environ, OMP_NUM_THREADS="1")
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                f"--nproc-per-node={world}", "--master-addr=127.0.0.1",
-               f"--master-port={29600 + world}", str(script), str(out)]
+               f"--master-port={29600 + world + 10 * chunks}", str(script), str(out),
+               str(chunks)]
         subprocess.run(cmd, check=True, env=env, timeout=180, capture_output=True)
         outs.append(torch.load(out))
-    assert torch.allclose(outs[0]["X"], outs[1]["X"], atol=1e-4)
-    assert torch.allclose(outs[0]["Y"], outs[1]["Y"], atol=1e-4)
+    for o in outs[1:]:
+        assert torch.allclose(outs[0]["X"], o["X"], atol=1e-4)
+        assert torch.allclose(outs[0]["Y"], o["Y"], atol=1e-4)
 
 
 @pytest.mark.gpu
@@ -98,3 +102,51 @@ def test_trainer_gpu_matches_cpu_reference(cuda):
     a, b = res["cpu"], res[str(cuda)]
     scale = a.X.abs().max().item()
     assert (a.X - b.X.cpu()).abs().max().item() < 5e-2 * max(1, scale)
+
+
+def test_row_layout_is_a_bijection():
+    from oryx_amd.models.als.trainer import RowLayout
+    for n, W, C in ((10, 1, 1), (10, 1, 3), (1000, 8, 4), (7, 2, 5), (1, 4, 4)):
+        lay = RowLayout(n, W, C)
+        ids = torch.arange(W * lay.s)
+        g = lay.remap(ids)
+        assert g.unique().numel() == ids.numel() and int(g.max()) < lay.rows
+        if C == 1 and W == 1:
+            assert torch.equal(g, ids)
+        # range c of rank r is one contiguous block of the gathered layout
+        r, loc = ids // lay.s, ids % lay.s
+        c = loc // lay.cr
+        assert torch.equal(g // lay.cr, c * W + r)
+
+
+@pytest.mark.parametrize("chunks", [2, 3])
+def test_chunked_gather_matches_single_range_cpu(chunks):
+    u, i, r = _data(seed=6)
+    res = []
+    for c in (1, chunks):
+        tr = ALSTrainer(6, lam=0.05, alpha=1.0, implicit=True, ctx=dist.DistContext(), seed=2,
+                        gather_chunks=c)
+        tr.prepare(u, i, r, 60, 40)
+        gi = torch.Generator().manual_seed(3)
+        tr.init_factors(torch.randn(60, 6, generator=gi), torch.randn(40, 6, generator=gi))
+        tr.iterate(2)
+        res.append(tr.factors())
+    assert torch.allclose(res[0].X, res[1].X, atol=1e-5)
+    assert torch.allclose(res[0].Y, res[1].Y, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_chunked_gather_gpu(cuda):
+    u, i, r = _data(seed=7, n_u=3000, n_i=900, nnz=60000)
+    res = []
+    for c in (1, 3):
+        tr = ALSTrainer(32, lam=0.05, alpha=1.0, implicit=True,
+                        ctx=dist.DistContext(device=cuda), seed=2, gather_chunks=c)
+        tr.prepare(u, i, r, 3000, 900)
+        gi = torch.Generator().manual_seed(3)
+        tr.init_factors(torch.randn(3000, 32, generator=gi) * 0.3,
+                        torch.randn(900, 32, generator=gi) * 0.3)
+        tr.iterate(2)
+        res.append(tr.factors())
+    assert torch.allclose(res[0].X, res[1].X, atol=1e-4)
+    assert torch.allclose(res[0].Y, res[1].Y, atol=1e-4)
