@@ -1,0 +1,471 @@
+"""Framework-tier unit tests with the reference's golden values.
+
+Ports of the reference's ``framework/oryx-common`` and ``framework/oryx-ml`` unit tests:
+TextUtilsTest, VectorMathTest, LinearSystemSolverTest, DoubleWeightedMeanTest, ConfigUtilsTest,
+ConfigToPropertiesTest, PMMLUtilsTest, RandomManagerTest, HyperParamsTest, AutoLockTest,
+AutoReadWriteLockTest, ExecUtilsTest, ClassUtilsTest, IOUtilsTest (paths under
+``/root/reference/framework/*/src/test/java/com/cloudera/oryx/``).
+"""
+
+import math
+import os
+import threading
+import xml.etree.ElementTree as ET
+
+import numpy as np
+import pytest
+
+from oryx_amd.ml import hyperparams as hp
+from oryx_amd.utils import config as cfg
+from oryx_amd.utils import ioutils, lang, mathx, pmml, rng, text
+
+FLOAT_EPS = 1e-5
+
+
+# ---------------------------------------------------------------- TextUtilsTest
+
+def test_parse_json_array():
+    assert text.parse_json_array('["a","1","foo"]') == ["a", "1", "foo"]
+    assert text.parse_json_array('["a","1","foo",""]') == ["a", "1", "foo", ""]
+    assert text.parse_json_array('["2.3"]') == ["2.3"]
+    assert text.parse_json_array("[]") == []
+
+
+def test_parse_delimited():
+    pd = text.parse_delimited
+    assert pd("a,1,foo", ",") == ["a", "1", "foo"]
+    assert pd("a,1,foo,", ",") == ["a", "1", "foo", ""]
+    assert pd("2.3", ",") == ["2.3"]
+    assert pd('"""a"""', ",") == ['"a"']
+    assert pd('"""" """"""', " ") == ['"', '""']
+    assert pd("", ",") == [""]
+    assert pd("a\t1,\t,foo", "\t") == ["a", "1,", ",foo"]
+    assert pd("a 1 foo ", " ") == ["a", "1", "foo", ""]
+    assert pd('-1.0 a"\\ "b', " ") == ["-1.0", 'a" "b']
+    assert pd('-1.0 "a\\"b\\"c"', " ") == ["-1.0", 'a"b"c']
+
+
+def test_parse_pmml_delimited():
+    p = text.parse_pmml_delimited
+    assert p("1 22 3") == ["1", "22", "3"]
+    assert p('ab  "a b"   "with \\"quotes\\" " ') == ["ab", "a b", 'with "quotes" ']
+    assert p('"\\" \\""') == ['" "']
+    assert p(' " c\\" d \\"e " " c\\" d \\"e " ') == [' c" d "e ', ' c" d "e ']
+
+
+def test_join_delimited():
+    jd = text.join_delimited
+    assert jd(["1", "2", "3"], ",") == "1,2,3"
+    assert jd(["a,b"], ",") == '"a,b"'
+    assert jd(['"a"'], ",") == '"""a"""'
+    assert jd(["1", "2", "3"], " ") == "1 2 3"
+    assert jd(["1 ", "2 ", "3"], " ") == '"1 " "2 " 3'
+    assert jd(['"a"'], " ") == '"""a"""'
+    assert jd(['"', '""'], " ") == '"""" """"""'
+    assert jd([], "\t") == ""
+
+
+def test_join_pmml_delimited():
+    assert text.join_pmml_delimited(["ab", "a b", 'with "quotes" ']) == \
+        'ab "a b" "with \\"quotes\\" "'
+    assert text.join_pmml_delimited(["1", "22", "3"]) == "1 22 3"
+    assert text.join_pmml_delimited([' c" d "e ', ' c" d "e ']) == \
+        '" c\\" d \\"e " " c\\" d \\"e "'
+    assert text.join_pmml_delimited_numbers([-1.0, 2.01, 3.5]) == "-1.0 2.01 3.5"
+
+
+def test_join_json_and_read_json():
+    assert text.join_json(["1", "2", "3"]) == '["1","2","3"]'
+    assert text.join_json(["1 ", "2 ", "3"]) == '["1 ","2 ","3"]'
+    assert text.join_json([]) == "[]"
+    assert text.join_json(["A", ["foo", 2], "B"]) == '["A",["foo",2],"B"]'
+    assert text.join_json(["A", {"1": "bar", "foo": 2}, "B"]) == '["A",{"1":"bar","foo":2},"B"]'
+    assert text.read_json("3") == 3
+    assert text.read_json('["foo", "bar"]') == ["foo", "bar"]
+    assert text.read_json("[1,2]") == [1, 2]
+
+
+def test_java_number_rendering():
+    # Float.toString / Double.toString conventions used on the wire (Preference.java:71-83)
+    assert text.java_float_str(1.0) == "1.0"
+    assert text.java_float_str(0.1) == "0.1"
+    assert text.java_double_str(1e-5) == "1.0E-5"
+    assert text.java_double_str(12345678.0) == "1.2345678E7"
+    assert text.java_double_str(100.0) == "100.0"
+
+
+# ---------------------------------------------------------------- VectorMathTest
+
+VEC1 = np.array([1.0, 0.5, -3.5], dtype=np.float32)
+VEC2 = np.array([0.0, -10.3, -3.0], dtype=np.float32)
+
+
+def test_vector_math():
+    assert mathx.dot(VEC1, VEC2) == pytest.approx(5.35, abs=FLOAT_EPS)
+    a = np.array([1.0e-24], dtype=np.float32)
+    assert mathx.dot(a, a) == pytest.approx(1.0e-24 * 1.0e-24, rel=1e-6)
+    assert mathx.norm(np.array([0.0], dtype=np.float32)) == 0.0
+    assert mathx.norm(VEC1) == pytest.approx(3.674234614174767, abs=FLOAT_EPS)
+    assert mathx.norm(VEC2) == pytest.approx(10.72800074571213, abs=FLOAT_EPS)
+    np.testing.assert_array_equal(mathx.parse_vector(["-1.0", "2.01", "3.5"]),
+                                  [-1.0, 2.01, 3.5])
+
+
+def test_transpose_times_self():
+    vecs = [np.array(v, dtype=np.float32) for v in
+            ([1.3, -2.0, 3.0], [2.0, 0.0, 5.0], [0.0, -1.5, 5.5])]
+    ata = mathx.transpose_times_self(vecs)
+    expected = np.array([[5.69, -2.6, 13.9], [-2.6, 6.25, -14.25], [13.9, -14.25, 64.25]])
+    np.testing.assert_allclose(ata, expected, atol=FLOAT_EPS)
+    assert mathx.transpose_times_self(None) is None
+    assert mathx.transpose_times_self([]) is None
+
+
+def test_random_vector():
+    r = rng.get_random()
+    v1 = mathx.random_vector_f(10, r)
+    v2 = mathx.random_vector_f(10, r)
+    assert len(v1) == 10 and len(v2) == 10
+    assert not np.array_equal(v1, v2)
+
+
+# ---------------------------------------------------------------- LinearSystemSolverTest
+
+def test_solver():
+    assert mathx.get_solver(None) is None
+    a = np.array([[1.3, -2.0, 3.0], [2.0, 0.0, 5.0], [0.0, -1.5, 5.5]])
+    solver = mathx.get_solver(a)
+    y = solver.solve_f_to_f(np.array([1.0, 2.0, 6.5], dtype=np.float32))
+    np.testing.assert_allclose(y, [-1.956044, 0.0021978023, 1.1824176], rtol=1e-5)
+
+
+def test_is_non_singular():
+    assert mathx.is_non_singular(np.array([[1.3, -2.0, 3.0], [2.0, 0.0, 5.0],
+                                           [0.0, -1.5, 5.5]]))
+    assert not mathx.is_non_singular(np.array([[1.3, -2.0, 3.0], [2.6, -4.0, 6.0],
+                                               [0.0, -1.5, 5.5]]))
+    assert mathx.is_non_singular(np.array([[1.3e-20, -2.0e-20, 3.0e-20], [2.0e-20, 0.0, 5.0e-20],
+                                           [0.0, -1.5e-20, 5.5e-20]]))
+
+
+def test_apparent_rank():
+    with pytest.raises(mathx.SingularMatrixSolverException) as e:
+        mathx.get_solver(np.array([[1.3001, -2.0, 3.0], [2.6, -4.0001, 6.0001],
+                                   [0.0, -1.5, 5.5]]))
+    assert e.value.apparent_rank == 2
+    with pytest.raises(mathx.SingularMatrixSolverException) as e:
+        mathx.get_solver(np.array([[1.3001, -2.0, 3.0], [2.6, -4.0001, 6.0001],
+                                   [1.3, -2.0002, 3.0002]]))
+    assert e.value.apparent_rank == 1
+
+
+# ---------------------------------------------------------------- DoubleWeightedMeanTest
+
+def test_double_weighted_mean():
+    m = mathx.DoubleWeightedMean()
+    assert m.get_n() == 0 and math.isnan(m.result)
+    m.increment(1.5)
+    assert m.get_n() == 1 and m.result == 1.5 and repr(m) == "1.5"
+    m = mathx.DoubleWeightedMean()
+    m.increment(0.2, 4.0)
+    m.increment(-0.1, 2.0)
+    assert m.get_n() == 2 and m.result == pytest.approx(0.1, abs=1e-15)
+    m2 = mathx.DoubleWeightedMean()
+    m2.increment(-0.1, 2.1)
+    m2.increment(0.1, 2.1)
+    assert m2.result == pytest.approx(0.0, abs=1e-15)
+    m3 = mathx.DoubleWeightedMean()
+    for i in range(1, 6):
+        m3.increment(1.0 / (i + 1), i)
+    assert m3.get_n() == 5
+    assert m3.result == pytest.approx((1 / 2 + 2 / 3 + 3 / 4 + 4 / 5 + 5 / 6) / 15.0, rel=1e-12)
+    copy = m.copy()
+    assert copy == m and hash(copy) == hash(m)
+    m.clear()
+    assert m == mathx.DoubleWeightedMean()
+    with pytest.raises(ValueError):
+        m.increment(1.0, -1.0)
+
+
+# ---------------------------------------------------------------- ConfigUtilsTest
+
+def test_default_config():
+    c = cfg.get_default()
+    # the reference defaults to "yarn-client" (a Spark master); there is no Spark here and the
+    # key only names where batch work runs, so the default is the local node
+    assert c.get_string("oryx.batch.streaming.master") == "local[*]"
+    assert c.get_int("oryx.batch.streaming.generation-interval-sec") == 21600
+    assert c.get_int("oryx.speed.streaming.generation-interval-sec") == 10
+    assert c.get_int("oryx.update-topic.message.max-size") == 16777216
+
+
+def test_serialize_round_trip():
+    s = cfg.serialize(cfg.get_default())
+    assert "update-class" in s
+    d = cfg.deserialize(s)
+    assert d.get_string("oryx.serving.api.port") == \
+        cfg.get_default().get_string("oryx.serving.api.port")
+
+
+def test_optional_and_overlay():
+    d = cfg.get_default()
+    assert cfg.get_optional_string(d, "nonexistent") is None
+    assert cfg.get_optional_string_list(d, "nonexistent") is None
+    assert cfg.get_optional_double(d, "nonexistent") is None
+    c = cfg.overlay_on({"foo": "bar", "a.b": 3, "l": [1, 2]}, d)
+    assert c.get_string("foo") == "bar"
+    assert c.get_int("a.b") == 3
+    assert c.get_string_list("l") == ["1", "2"]
+    # overlay wins, defaults remain
+    assert c.get_string("oryx.batch.streaming.master") == "local[*]"
+
+
+def test_set_path(tmp_path):
+    m = {}
+    cfg.set_path(m, "cwd", ".")
+    cfg.set_path(m, "temp", str(tmp_path))
+    assert m["cwd"] == '"file:%s/"' % os.path.realpath(".")
+    assert m["temp"] == '"file:%s/"' % os.path.realpath(str(tmp_path))
+    c = cfg.overlay_on(m, cfg.get_default())
+    assert c.get_string("temp").startswith("file:/")
+
+
+def test_pretty_print_and_redact():
+    pretty = cfg.pretty_print(cfg.get_default())
+    assert "batch" in pretty and "local[*]" in pretty
+    assert "password" in pretty and "*****" in pretty
+    red = cfg.redact("  password=foo \nPassword=foo\nPASSWORD = foo\n"
+                     " the-password= foo \nThe-Password =foo")
+    assert "foo" not in red
+    for frag in ("*****", "password=", "Password=", "PASSWORD = ", "the-password= ",
+                 "The-Password ="):
+        assert frag in red
+
+
+def test_config_to_properties():
+    lines = cfg.to_properties(cfg.get_default()).splitlines()
+    assert "oryx.serving.api.secure-port=443" in lines
+    assert "oryx.id=null" not in lines
+    assert all(line.startswith("oryx.") for line in lines)
+
+
+def test_hocon_features():
+    c = cfg.parse_string("""
+        a = 1
+        b = ${a}
+        c { d = "x", e = [1, 2, 3] }
+        c.f = ${c.d}"y"
+        g = ${?NOT_SET_ANYWHERE_ORYX}
+    """, fallback_defaults=False)
+    assert c.get_int("b") == 1
+    assert c.get_string("c.f") == "xy"
+    assert c.get_list("c.e") == [1, 2, 3]
+    assert not c.has_path("g")
+
+
+# ---------------------------------------------------------------- PMMLUtilsTest
+
+def test_pmml_skeleton_and_round_trip(tmp_path):
+    doc = pmml.build_skeleton_pmml()
+    app = doc.header.find(pmml.q("Application"))
+    assert app.get("name") == "Oryx"
+    assert doc.header.find(pmml.q("Timestamp")) is not None
+    model = ET.Element(pmml.q("TreeModel"), {"functionName": "classification"})
+    ET.SubElement(model, pmml.q("Node"), {"recordCount": "123.0"})
+    doc.add(model)
+    path = str(tmp_path / "model.pmml")
+    pmml.write(doc, path)
+    doc2 = pmml.read(path)
+    models = doc2.models()
+    assert len(models) == 1 and models[0].tag == pmml.q("TreeModel")
+    assert models[0].find(pmml.q("Node")).get("recordCount") == "123.0"
+    doc3 = pmml.from_string(pmml.to_string(doc))
+    assert doc3.version == "4.2.1"
+    assert doc3.models()[0].get("functionName") == "classification"
+
+
+def test_pmml_extensions():
+    doc = pmml.build_skeleton_pmml()
+    doc.add_extension("features", 2)
+    doc.add_extension_content("XIDs", ["a", "b c"])
+    doc2 = pmml.from_string(pmml.to_string(doc))
+    assert doc2.get_extension_value("features") == "2"
+    assert doc2.get_extension_content("XIDs") == ["a", "b c"]
+    assert doc2.get_extension_value("missing") is None
+
+
+# ---------------------------------------------------------------- RandomManagerTest
+
+def test_random_manager_test_seed():
+    rng.use_test_seed()
+    a = rng.get_random().next_double()
+    rng.use_test_seed()
+    b = rng.get_random().next_double()
+    assert a == b
+    r = rng.get_random()
+    assert 0 <= r.next_int(10) < 10
+    vals = {r.next_double() for _ in range(5)}
+    assert len(vals) == 5
+
+
+# ---------------------------------------------------------------- HyperParamsTest
+
+def _vals(h, n):
+    v = h.get_trial_values(n)
+    assert repr(h)
+    return v
+
+
+def test_hyperparams_continuous():
+    assert _vals(hp.fixed(3.0), 1) == [3.0]
+    assert _vals(hp.fixed(3.0), 3) == [3.0]
+    assert _vals(hp.range_of(3.0, 5.0), 1) == [4.0]
+    assert _vals(hp.range_of(3.0, 5.0), 2) == [3.0, 5.0]
+    np.testing.assert_allclose(_vals(hp.range_of(3.0, 5.0), 4),
+                               [3.0, 3.6666666666666667, 4.3333333333333333, 5.0])
+    assert _vals(hp.range_of(0.0, 1.0), 3) == [0.0, 0.5, 1.0]
+    assert _vals(hp.range_of(-1.0, 1.0), 5) == [-1.0, -0.5, 0.0, 0.5, 1.0]
+    np.testing.assert_allclose(_vals(hp.range_of(-1.0, 1.0), 4),
+                               [-1.0, -0.3333333333333333, 0.3333333333333333, 1.0])
+    assert _vals(hp.around(-3.0, 0.1), 1) == [-3.0]
+    np.testing.assert_allclose(_vals(hp.around(-3.0, 0.1), 2), [-3.05, -2.95])
+    np.testing.assert_allclose(_vals(hp.around(-3.0, 0.1), 3), [-3.1, -3.0, -2.9])
+
+
+def test_hyperparams_discrete():
+    assert _vals(hp.fixed(3), 1) == [3]
+    assert _vals(hp.fixed(3), 3) == [3]
+    assert _vals(hp.range_of(3, 4), 1) == [3]
+    assert _vals(hp.range_of(3, 5), 1) == [4]
+    assert _vals(hp.range_of(3, 5), 2) == [3, 5]
+    assert _vals(hp.range_of(3, 5), 3) == [3, 4, 5]
+    assert _vals(hp.range_of(3, 5), 4) == [3, 4, 5]
+    assert _vals(hp.range_of(0, 1), 3) == [0, 1]
+    assert _vals(hp.range_of(-1, 1), 5) == [-1, 0, 1]
+    assert _vals(hp.range_of(0, 10), 3) == [0, 5, 10]
+    assert _vals(hp.around(-3, 1), 1) == [-3]
+    assert _vals(hp.around(-3, 1), 2) == [-3, -2]
+    assert _vals(hp.around(-3, 1), 3) == [-4, -3, -2]
+    assert _vals(hp.around(-3, 10), 2) == [-8, 2]
+    assert _vals(hp.around(-3, 10), 3) == [-13, -3, 7]
+    u = hp.unordered_from_values(["foo", "bar"])
+    assert _vals(u, 1) == ["foo"]
+    assert _vals(u, 2) == ["foo", "bar"]
+    assert _vals(u, 3) == ["foo", "bar"]
+
+
+def test_hyperparam_combos():
+    params = [hp.fixed(1.0), hp.range_of(2, 10), hp.around(5.0, 0.5)]
+    combos = hp.choose_hyper_parameter_combos(params, 50, 2)
+    assert len(combos) == 4
+    for c in ([1.0, 2, 4.75], [1.0, 10, 4.75], [1.0, 2, 5.25], [1.0, 10, 5.25]):
+        assert c in combos
+    # fewer wanted than exist: a random subset of the grid.  (The reference's
+    # chooseHyperParameterCombos computes a permutation and then ignores it, always taking
+    # the first howMany combos -- SURVEY.md 2.7 quirk 1; this framework samples as intended.)
+    two = hp.choose_hyper_parameter_combos(params, 2, 2)
+    assert len(two) == 2 and two[0] != two[1]
+    assert all(c in combos for c in two)
+    assert hp.choose_hyper_parameter_combos([], 1, 0) == [[]]
+
+
+def test_hyperparams_from_config():
+    c = cfg.overlay_on({"a": 1, "b": 2.7, "c": "[3,4]", "d": "[5.3,6.6]", "e": '["x","y"]'},
+                       cfg.get_default())
+    assert _vals(hp.from_config(c, "a"), 1) == [1]
+    assert _vals(hp.from_config(c, "b"), 1) == [2.7]
+    assert _vals(hp.from_config(c, "c"), 2) == [3, 4]
+    assert _vals(hp.from_config(c, "d"), 2) == [5.3, 6.6]
+    assert _vals(hp.from_config(c, "e"), 2) == ["x", "y"]
+
+
+def test_choose_values_per_hyperparam():
+    cv = hp.choose_values_per_hyper_param
+    assert cv(0, 1) == 0
+    assert cv(1, 1) == 1
+    assert cv(1, 3) == 3
+    assert cv(2, 1) == 1
+    assert cv(2, 2) == 2
+    assert cv(2, 4) == 2
+    assert cv(3, 1) == 1
+    assert cv(3, 7) == 2
+    assert cv(3, 8) == 2
+
+
+# ---------------------------------------------------------------- lang: locks, exec, classes
+
+def test_auto_lock_and_rw_lock():
+    lock = lang.AutoLock()
+    with lock:
+        with lock.auto_lock():   # re-entrant, as the reference's ReentrantLock
+            pass
+    rw = lang.AutoReadWriteLock()
+    state = []
+    with rw.read():
+        with rw.read():          # shared readers
+            state.append(1)
+    with rw.write():
+        with rw.read():          # a writer may also read
+            state.append(2)
+    assert state == [1, 2]
+    # a writer waits for the readers
+    order = []
+    entered = threading.Event()
+
+    def reader():
+        with rw.read():
+            entered.set()
+            threading.Event().wait(0.2)
+            order.append("r")
+
+    t = threading.Thread(target=reader)
+    t.start()
+    entered.wait(5)
+    with rw.write():
+        order.append("w")
+    t.join()
+    assert order == ["r", "w"]
+
+
+def test_exec_utils():
+    hits = []
+    lang.do_in_parallel(8, lambda i: hits.append(i), parallelism=3)
+    assert sorted(hits) == list(range(8))
+    out = lang.collect_in_parallel(5, lambda i: i * i, parallelism=2)
+    assert out == [0, 1, 4, 9, 16]
+    with pytest.raises(ZeroDivisionError):
+        lang.collect_in_parallel(3, lambda i: 1 // (i - 1), parallelism=3)
+
+
+def test_class_utils():
+    cls = lang.load_class("oryx_amd.utils.mathx.DoubleWeightedMean")
+    assert cls is mathx.DoubleWeightedMean
+    assert lang.class_exists("oryx_amd.utils.mathx.Solver")
+    assert not lang.class_exists("oryx_amd.utils.mathx.NoSuchThing")
+    inst = lang.load_instance_of("oryx_amd.utils.mathx.DoubleWeightedMean")
+    assert isinstance(inst, mathx.DoubleWeightedMean)
+    # the reference's Java class names resolve to this framework's classes
+    assert lang.class_exists("com.cloudera.oryx.app.batch.mllib.als.ALSUpdate")
+
+
+# ---------------------------------------------------------------- IOUtilsTest
+
+def test_io_utils(tmp_path):
+    d = tmp_path / "a" / "b"
+    ioutils.mkdirs(str(d))
+    (d / "part-00000").write_text("x")
+    (d / "other").write_text("y")
+    assert [os.path.basename(p) for p in ioutils.list_files(str(d), "part-*")] == ["part-00000"]
+    uri = ioutils.to_uri(str(d))
+    assert uri.startswith("file:")
+    assert ioutils.to_local_path(uri).rstrip("/") == str(d)
+    f = str(tmp_path / "t.txt")
+    ioutils.write_text(f, "hello\n")
+    assert ioutils.read_text(f) == "hello\n"
+    ioutils.atomic_write_text(str(tmp_path / "atomic.txt"), "v1")
+    ioutils.atomic_write_text(str(tmp_path / "atomic.txt"), "v2")
+    assert (tmp_path / "atomic.txt").read_text() == "v2"
+    ioutils.delete_recursively(str(tmp_path / "a"))
+    assert not ioutils.exists(str(tmp_path / "a"))
+    port = ioutils.choose_free_port()
+    assert 0 < port < 65536
