@@ -91,6 +91,11 @@ class RowLayout:
     def gather(self, local: torch.Tensor, ctx: dist.DistContext, overlap_with=None):
         """All-gather ``local`` ([local_rows, ...]) into the gathered layout; ``overlap_with``
         (callable c -> None) runs before each range's exchange is started."""
+        if not ctx.is_distributed and self.C == 1:
+            # one process, one range: the local shard IS the gathered matrix (no copy)
+            if overlap_with is not None:
+                overlap_with(0)
+            return local
         out = torch.empty((self.rows,) + tuple(local.shape[1:]), dtype=local.dtype,
                           device=local.device)
         handles = []
