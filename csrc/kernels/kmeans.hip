@@ -173,6 +173,155 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
     }
 }
 
+// kmeans_assign_wide: the same argmin with the roles of the MFMA operands swapped, so that
+// each wave covers 64 points with one (best, argbest) pair per lane and point tile:
+//   * points are the B operand (column = lane & 15) of v_mfma_f32_16x16x32_bf16, held in
+//     registers for the whole kernel (4 tiles x DK k-steps); centers are the A operand
+//     (row = 4 (lane >> 4) + v), so each lane scans 4 centers of one point per 16x16 tile;
+//   * 64 points per wave halves the LDS operand reads per MFMA against 32-point waves, and the
+//     per-point state is 8 registers instead of 32, which keeps two waves per SIMD;
+//   * center tiles (64 rows) are copied global -> LDS by global_load_lds_dwordx4 (no staging
+//     registers), double-buffered; the LDS image is written linearly and the 16-byte units of
+//     each row are XOR-swizzled by (row & 7) through the per-lane SOURCE address, so the
+//     fragment ds_read_b128 of 8 consecutive rows hits 8 distinct bank groups;
+//   * |c|^2 of the tile rides along in LDS (a 4-byte glds by wave 0), the accumulator starts
+//     at -|c|^2 / 2 and the argmax of x.c - |c|^2 / 2 is the nearest center.
+// Requires d_pad = 32 DK with 2 <= DK <= 8 (each LDS row has at least 8 units).
+template <int DK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void
+kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict__ xnorm,
+                          const __bf16* __restrict__ C, const float* __restrict__ cnorm,
+                          long long n, int k_pad, int* __restrict__ assign,
+                          float* __restrict__ mind) {
+  constexpr int DPAD = DK * 32;
+  constexpr int RU = DPAD / 8;             // 16-byte units per center row
+  constexpr int CT = 64;                   // centers per LDS stage
+  constexpr int STAGE = CT * DPAD * 2;     // bytes of one center tile
+  constexpr int BUF = STAGE + CT * 4;      // + |c|^2 of the tile
+  constexpr int PT = 4;                    // 16-point tiles per wave
+  constexpr int GPW = RU / 4;              // 1 KB glds chunks per wave per stage
+  typedef __attribute__((address_space(3))) void lds_void;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, fl = lane & 15;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const long long p0 = (long long)bid * (4 * PT * 16) + wave * PT * 16;
+  const int ntiles = k_pad / CT;
+
+  // glds source for this lane: chunk (i * 4 + wave), unit u = chunk * 64 + lane of the tile
+  // image; row = u / RU, stored unit us = u % RU holds source unit us ^ (row & 7).  Chunk i
+  // of the wave is 4 * 64 / RU = 256 / RU rows further down, a multiple of 8, so the swizzle
+  // term is the same for every i.
+  const int u0 = wave * 64 + lane;
+  const int srow = u0 / RU, sus = u0 % RU;
+  const long long src_off = (long long)srow * DPAD + (long long)((sus ^ (srow & 7)) * 8);
+  auto issue_tile = [&](int t, int buf) {
+    char* dst = smem + buf * BUF;
+    const __bf16* src = C + (long long)t * CT * DPAD + src_off;
+#pragma unroll
+    for (int i = 0; i < GPW; ++i)
+      __builtin_amdgcn_global_load_lds(src + (long long)i * (256 / RU) * DPAD,
+                                       (lds_void*)(dst + (i * 4 + wave) * 1024), 16, 0, 0);
+    if (wave == 0)
+      __builtin_amdgcn_global_load_lds(cnorm + (long long)t * CT + lane,
+                                       (lds_void*)(dst + STAGE), 4, 0, 0);
+  };
+  issue_tile(0, 0);
+
+  // points: B fragment (k = ks*32 + 8g + j, column = point fl of tile pt)
+  bf16x8 b[PT][DK];
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) {
+    const long long r = p0 + pt * 16 + fl;
+#pragma unroll
+    for (int s = 0; s < DK; ++s) {
+      if (r < n) {
+        b[pt][s] = *reinterpret_cast<const bf16x8*>(X + r * DPAD + s * 32 + 8 * g);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[pt][s][j] = (__bf16)0.f;
+      }
+    }
+  }
+  float best[PT];
+  int besti[PT];
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) {
+    best[pt] = -INFINITY;
+    besti[pt] = 0;
+  }
+  // A fragment of center group ct, k-step ks: row ct*16 + fl, unit 4 ks + g stored at
+  // (4 ks + g) ^ (fl & 7) = 4 (ks ^ sb) + (g ^ (fl & 3)) with sb = (fl >> 2) & 1: one lane base
+  // for even and one for odd ks, everything else an immediate offset.
+  const int sb = (fl >> 2) & 1;
+  const int lrow = fl * RU * 16 + 16 * (g ^ (fl & 3));
+  const int off_e = lrow + 64 * sb, off_o = lrow + 64 * (1 - sb);
+
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) issue_tile(t + 1, buf ^ 1);
+    const char* base = smem + buf * BUF;
+    const float* cn = reinterpret_cast<const float*>(base + STAGE);
+    bf16x8 a[2][DK];
+    auto read_a = [&](int ct, bf16x8* dst) {
+#pragma unroll
+      for (int s = 0; s < DK; ++s)
+        dst[s] = *reinterpret_cast<const bf16x8*>(base + ((s & 1) ? off_o : off_e) +
+                                                  ct * 16 * RU * 16 + 128 * (s >> 1));
+    };
+    read_a(0, a[0]);
+#pragma unroll
+    for (int ct = 0; ct < CT / 16; ++ct) {
+      if (ct + 1 < CT / 16) read_a(ct + 1, a[(ct + 1) & 1]);
+      const f32x4 c4 = *reinterpret_cast<const f32x4*>(cn + ct * 16 + 4 * g);
+      const f32x4 h = c4 * -0.5f;            // +inf padding rows -> -inf, never chosen
+      f32x4 acc[PT];
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) acc[pt] = h;
+#pragma unroll
+      for (int s = 0; s < DK; ++s)
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt)
+          acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct & 1][s], b[pt][s], acc[pt], 0, 0,
+                                                            0);
+      const int c0 = t * CT + ct * 16 + 4 * g;
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt)
+          if (acc[pt][v] > best[pt]) {
+            best[pt] = acc[pt][v];
+            besti[pt] = c0 + v;
+          }
+    }
+    if (t + 1 < ntiles) __syncthreads();  // tile t+1 landed (each wave drained its glds) and
+                                          // every wave is done reading tile t's buffer
+  }
+  // reduce over the 4 lane groups holding the same point; ties -> lowest center index
+#pragma unroll
+  for (int pt = 0; pt < PT; ++pt) {
+    float bv = best[pt];
+    int bi = besti[pt];
+#pragma unroll
+    for (int off = 16; off < 64; off <<= 1) {
+      const float ov = __shfl_xor(bv, off, 64);
+      const int oi = __shfl_xor(bi, off, 64);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    const long long r = p0 + pt * 16 + fl;
+    if (g == 0 && r < n) {
+      const float d = xnorm[r] - 2.f * bv;
+      assign[r] = bi;
+      mind[r] = d > 0.f ? d : 0.f;
+    }
+  }
+}
+
 // one wave per row: sums[assign[r]] += x[r] (fp32 atomics, 256 contiguous bytes per instr)
 __global__ __launch_bounds__(256) void kmeans_accumulate_kernel(
     const float* __restrict__ X, const int* __restrict__ assign, const float* __restrict__ mind,
@@ -538,7 +687,33 @@ int oryx_kmeans_assign(const void* X, const float* xnorm, const void* C, long lo
   // traffic per MFMA relative to RT = 2 but drops to one wave per SIMD; measured at d = 256,
   // K = 1000 it ran 7% slower (10.2 vs 9.5 ms per 12.5M points), so RT = 2 is the default and
   // ORYX_KMEANS_RT=4 selects the wide tiles
-  static const int rt_pref = getenv("ORYX_KMEANS_RT") ? atoi(getenv("ORYX_KMEANS_RT")) : 2;
+  static const int rt_pref = getenv("ORYX_KMEANS_RT") ? atoi(getenv("ORYX_KMEANS_RT")) : 0;
+#define WIDE_CASE(DKV)                                                                        \
+  case DKV: {                                                                                 \
+    const int smem = 2 * (64 * DKV * 64 + 256);                                               \
+    const long long blocks = (n + 255) / 256;                                                 \
+    static bool attr_set = false;                                                             \
+    if (!attr_set && smem > 65536) {                                                          \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_assign_wide_kernel<DKV>),    \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, smem);                  \
+      attr_set = true;                                                                        \
+    }                                                                                         \
+    hipLaunchKernelGGL((kmeans_assign_wide_kernel<DKV>), dim3((unsigned)blocks), dim3(256),  \
+                       smem, s, x, xnorm, c, cnorm, n, k_pad, assign, mind);                  \
+    return oryx_check_launch();                                                               \
+  }
+  // default: the 64-point-per-wave kernel where its LDS swizzle applies (d_pad 64/128/256);
+  // ORYX_KMEANS_RT=2 or 4 selects the 32- or 64-point A-operand kernel
+  if (rt_pref == 0) {
+    switch (dk) {
+      WIDE_CASE(2)
+      WIDE_CASE(4)
+      WIDE_CASE(8)
+      default:
+        break;
+    }
+  }
+#undef WIDE_CASE
   if (rt_pref != 4 && dk <= 8) {
     switch (dk) {
       ASSIGN_CASE(1, 2)

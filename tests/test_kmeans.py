@@ -392,7 +392,7 @@ if ctx.rank == 0:
 # ---------------------------------------------------------------- GPU kernels
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,k", [(2, 3), (20, 64), (64, 100), (100, 257), (256, 50),
+@pytest.mark.parametrize("d,k", [(2, 3), (20, 64), (64, 100), (100, 257), (256, 50), (256, 1000),
                                  (500, 130)])
 def test_assign_kernel_matches_fp32(cuda, d, k):
     g = torch.Generator().manual_seed(d * 1000 + k)
