@@ -182,13 +182,42 @@ __global__ __launch_bounds__(256) void kmeans_assign_kernel(
 //     per-point state is 8 registers instead of 32, which keeps two waves per SIMD;
 //   * center tiles (64 rows) are copied global -> LDS by global_load_lds_dwordx4 (no staging
 //     registers), double-buffered; the LDS image is written linearly and the 16-byte units of
-//     each row are XOR-swizzled by (row & 7) through the per-lane SOURCE address, so the
-//     fragment ds_read_b128 of 8 consecutive rows hits 8 distinct bank groups;
+//     each row are XOR-swizzled through the per-lane SOURCE address so that each lane group
+//     of the fragment ds_read_b128 is bank-conflict free (see swz below);
 //   * |c|^2 of the tile rides along in LDS (a 4-byte glds by wave 0), the accumulator starts
 //     at -|c|^2 / 2 and the argmax of x.c - |c|^2 / 2 is the nearest center.
+template <int RU>
+__host__ __device__ constexpr int km_swz(int r) {
+  return RU >= 16 ? (r & 15) : ((r >> 1) & 7);
+}
+
+__device__ __forceinline__ float km_pack(float x, unsigned v) {
+  return __uint_as_float((__float_as_uint(x) & ~3u) | v);
+}
+
+__device__ __forceinline__ float km_max3(float a, float b, float c) {
+  float m;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(a), "v"(b), "v"(c));
+  return m;
+}
+
+// Packed epilogue of one 16-center group and point tile: each value gets its row-in-group v (0..3) in the
+// two low mantissa bits (a 2^-21 relative perturbation), so the running best is two v_max3
+// per 4 values and only the group index needs a compare + select.
+__device__ __forceinline__ void km_epilogue_one(const f32x4& ac, int ctg, float& bestp,
+                                                int& bestct) {
+  float m = km_max3(bestp, km_pack(ac[0], 0), km_pack(ac[1], 1));
+  m = km_max3(m, km_pack(ac[2], 2), km_pack(ac[3], 3));
+  bestct = __float_as_uint(m) != __float_as_uint(bestp) ? ctg : bestct;
+  bestp = m;
+}
+
 // Requires d_pad = 32 DK with 2 <= DK <= 8 (each LDS row has at least 8 units).
-template <int DK>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void
+// PK selects the packed, software-pipelined epilogue (the group-ct epilogue runs while the
+// MFMAs of group ct+1 are in flight, on a second accumulator set; the A fragments are
+// refilled in place, one k-step at a time).
+template <int DK, int NW, bool PK>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void
 kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict__ xnorm,
                           const __bf16* __restrict__ C, const float* __restrict__ cnorm,
                           long long n, int k_pad, int* __restrict__ assign,
@@ -199,30 +228,37 @@ kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict_
   constexpr int STAGE = CT * DPAD * 2;     // bytes of one center tile
   constexpr int BUF = STAGE + CT * 4;      // + |c|^2 of the tile
   constexpr int PT = 4;                    // 16-point tiles per wave
-  constexpr int GPW = RU / 4;              // 1 KB glds chunks per wave per stage
+  constexpr int GPW = RU / NW;             // 1 KB glds chunks per wave per stage
+  static_assert(GPW * NW == RU && RU % 8 == 0 && RU <= 32, "glds chunking");
   typedef __attribute__((address_space(3))) void lds_void;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, fl = lane & 15;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  const long long p0 = (long long)bid * (4 * PT * 16) + wave * PT * 16;
+  const long long p0 = (long long)bid * (NW * PT * 16) + wave * PT * 16;
   const int ntiles = k_pad / CT;
 
-  // glds source for this lane: chunk (i * 4 + wave), unit u = chunk * 64 + lane of the tile
-  // image; row = u / RU, stored unit us = u % RU holds source unit us ^ (row & 7).  Chunk i
-  // of the wave is 4 * 64 / RU = 256 / RU rows further down, a multiple of 8, so the swizzle
-  // term is the same for every i.
+  // LDS image of a tile: linear, row r's 16-byte unit q stored at unit q ^ swz(r).  The
+  // ds_read_b128 lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same + 32) read
+  // rows fl of unit 4 ks + g; with swz = row & 15 (rows of >= 16 units) or (row >> 1) & 7
+  // (8-unit rows, two rows per 256 B) every group covers the 16 bank quads of a 256-byte LDS
+  // cycle exactly once.  glds writes lane-linearly, so the permutation goes on the source:
+  // chunk (i * NW + wave) = units u = chunk * 64 + lane, row u / RU, source unit
+  // (u % RU) ^ swz(row).
   const int u0 = wave * 64 + lane;
   const int srow = u0 / RU, sus = u0 % RU;
-  const long long src_off = (long long)srow * DPAD + (long long)((sus ^ (srow & 7)) * 8);
+  constexpr int RSTEP = NW * 64 / RU;      // rows between a wave's consecutive chunks
   auto issue_tile = [&](int t, int buf) {
     char* dst = smem + buf * BUF;
-    const __bf16* src = C + (long long)t * CT * DPAD + src_off;
+    const __bf16* src = C + (long long)t * CT * DPAD;
 #pragma unroll
-    for (int i = 0; i < GPW; ++i)
-      __builtin_amdgcn_global_load_lds(src + (long long)i * (256 / RU) * DPAD,
-                                       (lds_void*)(dst + (i * 4 + wave) * 1024), 16, 0, 0);
+    for (int i = 0; i < GPW; ++i) {
+      // swz(r) spelled out: a call out of this lambda drops the kernel's host stub (hipcc 7.2)
+      const int r = srow + i * RSTEP;
+      __builtin_amdgcn_global_load_lds(src + r * DPAD + (sus ^ (RU >= 16 ? (r & 15) : ((r >> 1) & 7))) * 8,
+                                       (lds_void*)(dst + (i * NW + wave) * 1024), 16, 0, 0);
+    }
     if (wave == 0)
       __builtin_amdgcn_global_load_lds(cnorm + (long long)t * CT + lane,
                                        (lds_void*)(dst + STAGE), 4, 0, 0);
@@ -251,14 +287,97 @@ kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict_
     best[pt] = -INFINITY;
     besti[pt] = 0;
   }
-  // A fragment of center group ct, k-step ks: row ct*16 + fl, unit 4 ks + g stored at
-  // (4 ks + g) ^ (fl & 7) = 4 (ks ^ sb) + (g ^ (fl & 3)) with sb = (fl >> 2) & 1: one lane base
-  // for even and one for odd ks, everything else an immediate offset.
-  const int sb = (fl >> 2) & 1;
-  const int lrow = fl * RU * 16 + 16 * (g ^ (fl & 3));
-  const int off_e = lrow + 64 * sb, off_o = lrow + 64 * (1 - sb);
+  // A fragment of center group ct, k-step ks: row ct*16 + fl (swz(row) = swz(fl)), unit
+  // 4 ks + g.  The swizzle only touches the low 4 unit bits, so ks >> 2 is an immediate
+  // offset and ks & 3 selects one of (at most) 4 lane bases.
+  int aoff[DK < 4 ? DK : 4];
+#pragma unroll
+  for (int m = 0; m < (DK < 4 ? DK : 4); ++m)
+    aoff[m] = fl * RU * 16 + 16 * ((4 * m + g) ^ km_swz<RU>(fl));
 
   __syncthreads();
+  if constexpr (PK) {
+    float bestp[PT];
+    int bestct[PT];
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) {
+      bestp[pt] = -3.0e38f;
+      bestct[pt] = 0;
+    }
+    f32x4 acc[2][PT];
+    bf16x8 a[DK];
+    for (int t = 0; t < ntiles; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < ntiles) issue_tile(t + 1, buf ^ 1);
+      const char* base = smem + buf * BUF;
+      const float* cn = reinterpret_cast<const float*>(base + STAGE);
+      auto a_addr = [&](int ct, int s) {
+        return reinterpret_cast<const bf16x8*>(base + aoff[s & 3] + ct * 16 * RU * 16 +
+                                               256 * (s >> 2));
+      };
+#pragma unroll
+      for (int s = 0; s < DK; ++s) a[s] = *a_addr(0, s);
+      // |c|^2 of group ct + 1 is read during group ct (an LDS read right before the first
+      // MFMA of each group would expose its latency once per group)
+      f32x4 c4n = *reinterpret_cast<const f32x4*>(cn + 4 * g);
+#pragma unroll
+      for (int ct = 0; ct < CT / 16; ++ct) {
+        const f32x4 c4 = c4n;
+        if (ct + 1 < CT / 16) c4n = *reinterpret_cast<const f32x4*>(cn + (ct + 1) * 16 + 4 * g);
+        // padding rows (|c|^2 = +inf) start at -5e29: finite, so the packed bits stay a number
+        f32x4 h;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) h[v] = -0.5f * fminf(c4[v], 1.0e30f);
+#pragma unroll
+        for (int pt = 0; pt < PT; ++pt) acc[ct & 1][pt] = h;
+        // the previous group's epilogue (other accumulator set) is spread over the k-steps,
+        // point tile pt at step pt % DK, and a scheduling barrier closes each step so the
+        // refill reads and the epilogue stay where they are put
+        const bool prev = ct > 0 || t > 0;
+        const int pset = (ct + 1) & 1;
+        const int pctg = t * (CT / 16) + ct - 1;
+#pragma unroll
+        for (int s = 0; s < DK; ++s) {
+#pragma unroll
+          for (int pt = 0; pt < PT; ++pt)
+            acc[ct & 1][pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], b[pt][s],
+                                                                      acc[ct & 1][pt], 0, 0, 0);
+          if (ct + 1 < CT / 16) a[s] = *a_addr(ct + 1, s);
+          if (prev) {
+#pragma unroll
+            for (int pt = 0; pt < PT; ++pt)
+              if (pt % DK == s) km_epilogue_one(acc[pset][pt], pctg, bestp[pt], bestct[pt]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      if (t + 1 < ntiles) __syncthreads();
+    }
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt)
+      km_epilogue_one(acc[1][pt], ntiles * (CT / 16) - 1, bestp[pt], bestct[pt]);
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt) {
+      float bv = bestp[pt];
+      int bi = bestct[pt] * 16 + 4 * g + (int)(__float_as_uint(bv) & 3u);
+#pragma unroll
+      for (int off = 16; off < 64; off <<= 1) {
+        const float ov = __shfl_xor(bv, off, 64);
+        const int oi = __shfl_xor(bi, off, 64);
+        if (ov > bv || (ov == bv && oi < bi)) {
+          bv = ov;
+          bi = oi;
+        }
+      }
+      const long long r = p0 + pt * 16 + fl;
+      if (g == 0 && r < n) {
+        const float d = xnorm[r] - 2.f * bv;
+        assign[r] = bi;
+        mind[r] = d > 0.f ? d : 0.f;
+      }
+    }
+    return;
+  }
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) issue_tile(t + 1, buf ^ 1);
@@ -268,8 +387,8 @@ kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict_
     auto read_a = [&](int ct, bf16x8* dst) {
 #pragma unroll
       for (int s = 0; s < DK; ++s)
-        dst[s] = *reinterpret_cast<const bf16x8*>(base + ((s & 1) ? off_o : off_e) +
-                                                  ct * 16 * RU * 16 + 128 * (s >> 1));
+        dst[s] = *reinterpret_cast<const bf16x8*>(base + aoff[s & 3] + ct * 16 * RU * 16 +
+                                                  256 * (s >> 2));
     };
     read_a(0, a[0]);
 #pragma unroll
@@ -688,31 +807,49 @@ int oryx_kmeans_assign(const void* X, const float* xnorm, const void* C, long lo
   // K = 1000 it ran 7% slower (10.2 vs 9.5 ms per 12.5M points), so RT = 2 is the default and
   // ORYX_KMEANS_RT=4 selects the wide tiles
   static const int rt_pref = getenv("ORYX_KMEANS_RT") ? atoi(getenv("ORYX_KMEANS_RT")) : 0;
-#define WIDE_CASE(DKV)                                                                        \
+#define WIDE_CASE(DKV, NWV, PKV)                                                              \
   case DKV: {                                                                                 \
     const int smem = 2 * (64 * DKV * 64 + 256);                                               \
-    const long long blocks = (n + 255) / 256;                                                 \
+    const long long blocks = (n + NWV * 64 - 1) / (NWV * 64);                                 \
     static bool attr_set = false;                                                             \
     if (!attr_set && smem > 65536) {                                                          \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_assign_wide_kernel<DKV>),    \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_assign_wide_kernel<DKV, NWV, PKV>), \
                           hipFuncAttributeMaxDynamicSharedMemorySize, smem);                  \
       attr_set = true;                                                                        \
     }                                                                                         \
-    hipLaunchKernelGGL((kmeans_assign_wide_kernel<DKV>), dim3((unsigned)blocks), dim3(256),  \
-                       smem, s, x, xnorm, c, cnorm, n, k_pad, assign, mind);                  \
+    hipLaunchKernelGGL((kmeans_assign_wide_kernel<DKV, NWV, PKV>), dim3((unsigned)blocks),    \
+                       dim3(NWV * 64), smem, s, x, xnorm, c, cnorm, n, k_pad, assign, mind);  \
     return oryx_check_launch();                                                               \
   }
   // default: the 64-point-per-wave kernel where its LDS swizzle applies (d_pad 64/128/256);
-  // ORYX_KMEANS_RT=2 or 4 selects the 32- or 64-point A-operand kernel
+  // ORYX_KMEANS_RT=2 or 4 selects the 32- or 64-point A-operand kernel.  ORYX_KMEANS_WAVES=8
+  // runs 8-wave blocks (512 points share each center tile: half the L2 -> LDS traffic, one
+  // block per CU)
+  static const int nw_pref = getenv("ORYX_KMEANS_WAVES") ? atoi(getenv("ORYX_KMEANS_WAVES")) : 4;
+  // ORYX_KMEANS_EPI=0 selects the unpacked compare/select epilogue
+  static const bool pk = !(getenv("ORYX_KMEANS_EPI") && atoi(getenv("ORYX_KMEANS_EPI")) == 0);
+#define WIDE_SWITCH(NWV, PKV)                                                                 \
+  switch (dk) {                                                                               \
+    WIDE_CASE(2, NWV, PKV)                                                                    \
+    WIDE_CASE(4, NWV, PKV)                                                                    \
+    WIDE_CASE(8, NWV, PKV)                                                                    \
+    default:                                                                                  \
+      break;                                                                                  \
+  }
   if (rt_pref == 0) {
-    switch (dk) {
-      WIDE_CASE(2)
-      WIDE_CASE(4)
-      WIDE_CASE(8)
-      default:
-        break;
+    if (nw_pref == 8) {
+      if (pk) {
+        WIDE_SWITCH(8, true)
+      } else {
+        WIDE_SWITCH(8, false)
+      }
+    } else if (pk) {
+      WIDE_SWITCH(4, true)
+    } else {
+      WIDE_SWITCH(4, false)
     }
   }
+#undef WIDE_SWITCH
 #undef WIDE_CASE
   if (rt_pref != 4 && dk <= 8) {
     switch (dk) {

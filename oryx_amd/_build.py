@@ -97,8 +97,24 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
         if verbose:
             print(" ".join(cmd), flush=True)
         _run(cmd)
+        _check_no_missing_stubs(tmp)
         os.replace(tmp, KERNELS_SO)
     return KERNELS_SO
+
+
+def _check_no_missing_stubs(so: str) -> None:
+    """A kernel template whose host-side instantiation hipcc silently dropped links into a
+    library with an undefined internal symbol that only fails at dlopen on the GPU box;
+    catch it here instead."""
+    try:
+        out = subprocess.run(["nm", "-u", so], capture_output=True, text=True, timeout=60).stdout
+    except (OSError, subprocess.SubprocessError):
+        return
+    missing = [ln.split()[-1] for ln in out.splitlines() if "_GLOBAL__N_" in ln]
+    if missing:
+        os.unlink(so)
+        raise RuntimeError("native build: undefined internal kernel symbols (host stubs not "
+                           "emitted): %s" % ", ".join(missing[:4]))
 
 
 def build(force: bool = False, verbose: bool = False) -> List[str]:
