@@ -265,21 +265,20 @@ kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict_
   };
   issue_tile(0, 0);
 
-  // points: B fragment (k = ks*32 + 8g + j, column = point fl of tile pt)
+  // points: B fragment (k = ks*32 + 8g + j, column = point fl of tile pt); rows past n are
+  // clamped to row n-1 (their results are never stored)
   bf16x8 b[PT][DK];
+  const __bf16* xrow[PT];
 #pragma unroll
   for (int pt = 0; pt < PT; ++pt) {
     const long long r = p0 + pt * 16 + fl;
-#pragma unroll
-    for (int s = 0; s < DK; ++s) {
-      if (r < n) {
-        b[pt][s] = *reinterpret_cast<const bf16x8*>(X + r * DPAD + s * 32 + 8 * g);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) b[pt][s][j] = (__bf16)0.f;
-      }
-    }
+    xrow[pt] = X + (r < n ? r : n - 1) * DPAD + 8 * g;
   }
+#pragma unroll
+  for (int s = 0; s < DK; ++s)
+#pragma unroll
+    for (int pt = 0; pt < PT; ++pt)
+      b[pt][s] = *reinterpret_cast<const bf16x8*>(xrow[pt] + s * 32);
   float best[PT];
   int besti[PT];
 #pragma unroll

@@ -149,6 +149,54 @@ __global__ __launch_bounds__(256) void rdf_route(const BinT* __restrict__ Xb, lo
   }
 }
 
+// Route without visit counting (the grouped path takes node visits from the per-level
+// counting sort): one thread per row walks ALL trees, so the row's bytes come from HBM once
+// per level and the other trees' reads of it hit L1/L2, instead of every tree streaming the
+// whole bin matrix (grid y = tree in rdf_route).
+template <typename BinT>
+__global__ __launch_bounds__(256) void rdf_route_rows(const BinT* __restrict__ Xb, long long n,
+                                                      int P, int T, int* __restrict__ node_of,
+                                                      int nodes,
+                                                      const int* __restrict__ split_feat,
+                                                      const int* __restrict__ split_bin,
+                                                      const unsigned char* __restrict__ cat_left,
+                                                      int B, const int* __restrict__ child_base) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const BinT* xr = Xb + i * P;
+    // trees in groups of 8 with each dependent load step issued for the whole group: three
+    // memory round trips per 8 trees instead of three per tree
+    for (int t0 = 0; t0 < T; t0 += 8) {
+      int node[8], f[8], sb[8], cb[8], b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        node[u] = t0 + u < T ? node_of[(long long)(t0 + u) * n + i] : -1;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const long long tn = (long long)(t0 + u) * nodes + node[u];
+        f[u] = node[u] >= 0 ? split_feat[tn] : -1;
+        sb[u] = node[u] >= 0 ? split_bin[tn] : 0;
+        cb[u] = node[u] >= 0 ? child_base[tn] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) b[u] = f[u] >= 0 ? (int)xr[f[u]] : 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (node[u] < 0) continue;
+        int* slot = node_of + (long long)(t0 + u) * n + i;
+        if (f[u] < 0) {
+          *slot = -1;
+          continue;
+        }
+        const long long tn = (long long)(t0 + u) * nodes + node[u];
+        const bool right =
+            (cat_left && sb[u] < 0) ? cat_left[tn * B + b[u]] == 0 : b[u] > sb[u];
+        *slot = cb[u] + (right ? 1 : 0);
+      }
+    }
+  }
+}
+
 // Segmented level histogram: rows are kept grouped by (tree, node) -- a counting sort of the
 // routed rows after every level (oryx_counting_sort) -- so a workgroup owns one PIECE of one
 // node's rows: it reads only those rows (row ids through the permutation), accumulates the
@@ -225,6 +273,120 @@ __global__ __launch_bounds__(256) void rdf_histogram_pieces(
       const float v = lh[k];
       if (v != 0.f) atomicAdd(gh + k, v);
     }
+  }
+}
+
+// Row-staged variant (byte bins): the Fs single-byte loads per row of rdf_histogram_pieces
+// each touch 64 different cache lines per wave instruction (the rows come through the
+// permutation), so the texture-address path, not HBM, bounds it.  Here every wave copies its
+// 64 rows whole into its own LDS slice first -- one dword load instruction covers two rows
+// (lanes 0-31 and 32-63, lane & 31 = dword of the row), i.e. a handful of cache lines -- and
+// each lane then reads its row's Fs feature bytes from LDS.  Waves stage and consume only
+// their own rows, so no workgroup barrier is needed until the histogram flush.  A row takes
+// RSW dwords of LDS (odd, so the 64 lanes' byte reads fall on distinct banks); a row that
+// starts off a dword boundary (P % 4 != 0) is copied from the aligned dword below it and read
+// at byte offset (i * P) & 3.
+template <bool CLS>
+__global__ __launch_bounds__(256) void rdf_histogram_staged(
+    const unsigned char* __restrict__ Xb, long long n, int P, const int* __restrict__ label,
+    const float* __restrict__ y, int S, const unsigned char* __restrict__ weight,
+    const int* __restrict__ perm, const int* __restrict__ piece_tree,
+    const int* __restrict__ piece_node, const long long* __restrict__ piece_lo,
+    const long long* __restrict__ piece_hi, int nodes, const int* __restrict__ feats, int Fs,
+    int B, float* __restrict__ hist, int NDW, int RSW) {
+  extern __shared__ __attribute__((aligned(16))) float lsm[];
+  const int per_node = Fs * B * S;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float* lh = lsm;                                                        // [per_node]
+  unsigned int* rows = reinterpret_cast<unsigned int*>(lsm + per_node) + wave * 64 * RSW;
+  const unsigned char* rowb = reinterpret_cast<const unsigned char*>(rows);
+  const int pc = blockIdx.x;
+  const int t = piece_tree[pc];
+  const int node = piece_node[pc];
+  float* gh = hist + ((long long)t * nodes + node) * per_node;
+  for (int i = tid; i < per_node; i += 256) lh[i] = 0.f;   // 0.f and 0u share the bits
+  __syncthreads();
+  const int* fj = feats + ((long long)t * nodes + node) * Fs;
+  const long long p0 = piece_lo[pc], p1 = piece_hi[pc];
+  const long long toff = (long long)t * n;
+  const unsigned int* Xw = reinterpret_cast<const unsigned int*>(Xb);
+  // word indices fit 32 bits (the launcher checks n * P < 2^34); the partial last word, if
+  // any, is assembled once from its bytes
+  const long long nbytes = n * P;
+  const unsigned int nfull = (unsigned int)(nbytes >> 2);
+  unsigned int tailw = 0;
+  for (int b = 0; b < (int)(nbytes & 3); ++b)
+    tailw |= (unsigned int)Xb[(long long)nfull * 4 + b] << (8 * b);
+  const int half = lane >> 5, wl = lane & 31;
+  for (long long q0 = p0 + wave * 64; q0 < p1; q0 += 256) {
+    const long long q = q0 + lane;
+    const long long i = q < p1 ? (perm ? (long long)perm[q] - toff : q - toff) : -1;
+    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
+    int s0 = 0;
+    if (i >= 0) {
+      v0 = weight ? (float)weight[toff + i] : 1.f;
+      if (CLS) {
+        s0 = label[i];
+      } else {
+        const float yi = y[i];
+        v1 = v0 * yi;
+        v2 = v0 * yi * yi;
+      }
+    }
+    const int nr = (int)((p1 - q0) < 64 ? (p1 - q0) : 64);
+    // stage: step it copies rows 2 it (lanes 0-31) and 2 it + 1 (lanes 32-63), dword
+    // wp * 32 + (lane & 31) of each; all 32 steps' loads are issued before the first LDS
+    // store, so the wave has up to 32 row loads in flight instead of one round trip per step
+    const unsigned int wb = i >= 0 ? (unsigned int)((i * P) >> 2) : 0u;   // first word of row
+    // row word bases of the 64 rows, shuffled with every lane active (a bpermute reads 0
+    // from a lane that is switched off)
+    unsigned int wbr[32];
+#pragma unroll
+    for (int it = 0; it < 32; ++it) wbr[it] = (unsigned int)__shfl((int)wb, 2 * it + half, 64);
+    for (int wp = 0; wp * 32 < NDW; ++wp) {
+      const int w = wp * 32 + wl;
+      if (w < NDW) {
+        // rows past the batch end load row 0 into their (unused) slots: no per-step predicate.
+        // Only words wi <= nfull can hold bytes of a row, so the index is clamped to the last
+        // full word and the partial one comes from tailw.
+        unsigned int v[32];
+#pragma unroll
+        for (int it = 0; it < 32; ++it) {
+          const unsigned int wi = wbr[it] + (unsigned int)w;
+          v[it] = Xw[wi < nfull ? wi : nfull - 1];
+          if (wi == nfull) v[it] = tailw;
+        }
+#pragma unroll
+        for (int it = 0; it < 32; ++it) rows[(2 * it + half) * RSW + w] = v[it];
+      }
+    }
+    // this wave's LDS writes before its reads (LDS executes one wave's accesses in order;
+    // the fence only stops the compiler from reordering them)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const unsigned int wcnt = (unsigned int)v0;
+    if (v0 != 0.f) {
+      const unsigned char* xr = rowb + lane * RSW * 4 + (int)((i * P) & 3);
+      for (int j = 0; j < Fs; ++j) {
+        const int b = xr[fj[j]];
+        float* h = lh + (j * B + b) * S;
+        if (CLS) {
+          // integer counts (bootstrap weights are small integers): ds_add_u32, exact
+          atomicAdd(reinterpret_cast<unsigned int*>(h) + s0, wcnt);
+        } else {
+          atomicAdd(h, v0);
+          atomicAdd(h + 1, v1);
+          atomicAdd(h + 2, v2);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  __syncthreads();
+  for (int k = tid; k < per_node; k += 256) {
+    const float v = CLS ? (float)reinterpret_cast<const unsigned int*>(lh)[k] : lh[k];
+    if (v != 0.f) atomicAdd(gh + k, v);
   }
 }
 
@@ -330,6 +492,21 @@ int oryx_rdf_route(const void* Xb, int bin_bytes, long long n, int P, int T, int
                    unsigned long long* visits, void* stream) {
   if (n <= 0 || T <= 0) return ORYX_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!visits) {
+    long long blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (bin_bytes == 1)
+      hipLaunchKernelGGL((rdf_route_rows<unsigned char>), dim3((unsigned)blocks), dim3(256), 0, s,
+                         reinterpret_cast<const unsigned char*>(Xb), n, P, T, node_of, nodes,
+                         split_feat, split_bin, cat_left, B, child_base);
+    else if (bin_bytes == 2)
+      hipLaunchKernelGGL((rdf_route_rows<short>), dim3((unsigned)blocks), dim3(256), 0, s,
+                         reinterpret_cast<const short*>(Xb), n, P, T, node_of, nodes, split_feat,
+                         split_bin, cat_left, B, child_base);
+    else
+      return ORYX_EINVAL;
+    return oryx_check_launch();
+  }
   long long target = 4096 / T;
   if (target < 1) target = 1;
   long long rpb = (n + target - 1) / target;
@@ -365,6 +542,28 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
     return ORYX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const long long per_node_bytes = (long long)Fs * B * S * 4;
+  // row-staged kernel for byte bins when histogram + 256 staged rows fit in 64 KB of LDS
+  // (ORYX_RDF_HIST=0 selects the direct-gather kernel)
+  static const bool staged_ok =
+      !(getenv("ORYX_RDF_HIST") && atoi(getenv("ORYX_RDF_HIST")) == 0);
+  if (staged_ok && bin_bytes == 1 && n * (long long)P < (1LL << 34) && n * (long long)P >= 4) {
+    const int ndw = (P + 3) / 4 + 1;                 // dwords covering any row alignment
+    const int rsw = ndw | 1;
+    const long long smem_st = per_node_bytes + 256LL * rsw * 4;
+    if (smem_st <= 64 * 1024) {
+      if (cls)
+        hipLaunchKernelGGL((rdf_histogram_staged<true>), dim3((unsigned)n_pieces), dim3(256),
+                           smem_st, s, reinterpret_cast<const unsigned char*>(Xb), n, P, label,
+                           y, S, weight, perm, piece_tree, piece_node, piece_lo, piece_hi,
+                           nodes, feats, Fs, B, hist, ndw, rsw);
+      else
+        hipLaunchKernelGGL((rdf_histogram_staged<false>), dim3((unsigned)n_pieces), dim3(256),
+                           smem_st, s, reinterpret_cast<const unsigned char*>(Xb), n, P, label,
+                           y, S, weight, perm, piece_tree, piece_node, piece_lo, piece_hi,
+                           nodes, feats, Fs, B, hist, ndw, rsw);
+      return oryx_check_launch();
+    }
+  }
   const bool lds = per_node_bytes <= 64 * 1024;
   const size_t smem = lds ? (size_t)per_node_bytes : 0;
 #define PIECE_LAUNCH(BT, C, L)                                                                \

@@ -15,7 +15,7 @@ K12-K14.  The algorithm is MLlib's histogram (binned) level-wise random forest:
   csrc/kernels/rdf.hip) aggregates label statistics per (tree, node, feature, bin); the best
   split per node (max impurity decrease: gini / entropy / variance; categorical bins ordered by
   label centroid) is chosen with batched tensor ops; ``oryx_rdf_route`` moves every row one
-  level down and counts node visits;
+  level down (and counts node visits unless the level's counting sort already did);
 * a node becomes a leaf at max depth, when pure, with < 2 weighted examples, or when no split
   improves impurity.
 
@@ -260,17 +260,22 @@ class RowGroups:
     """Rows of every tree grouped by their open node at the current level (GPU path): a
     permutation of the flattened [T][n] row space plus per-(tree, node) counts/offsets."""
 
-    def __init__(self, perm: Optional[torch.Tensor], counts: np.ndarray, width: int, n: int):
+    def __init__(self, perm: Optional[torch.Tensor], counts: np.ndarray, width: int, n: int,
+                 visits: Optional[np.ndarray] = None):
         self.perm = perm                      # int32 [T*n] (None: identity, one node per tree)
-        self.counts = counts                  # int64 [T, width]
+        self.counts = counts                  # int64 [T, width]: rows with weight > 0
         self.width = width
         self.n = n
+        # int64 [T, width]: every row at the node, bootstrap weight 0 included (the PMML
+        # recordCount / importance input that routing would otherwise count)
+        self.visits = visits
         flat = counts.reshape(-1)
         self.offsets = (np.cumsum(flat) - flat).reshape(counts.shape)
 
     @staticmethod
     def root(T: int, n: int) -> "RowGroups":
-        g = RowGroups(None, np.full((T, 1), n, dtype=np.int64), 1, n)
+        g = RowGroups(None, np.full((T, 1), n, dtype=np.int64), 1, n,
+                      np.full((T, 1), n, dtype=np.int64))
         g.offsets = (np.arange(T, dtype=np.int64) * n)[:, None]
         return g
 
@@ -278,19 +283,18 @@ class RowGroups:
     def from_nodes(node_of: torch.Tensor, width: int,
                    weight: Optional[torch.Tensor] = None) -> Optional["RowGroups"]:
         """Counting sort of the rows by (tree, node); None when the key space is too wide.
-        Rows that reached a leaf, and rows a tree's bootstrap left out (weight 0: they only
-        count as node visits, which routing tallies over all rows), go to a last, unused key."""
+        Rows a tree's bootstrap left out (weight 0) only count as node visits: they get a
+        second key per node after all live keys, and rows that reached a leaf a last, unused
+        key, so one sort yields both the live groups and the visit counts."""
         T, n = node_of.shape
-        k = T * width + 1
+        k = 2 * T * width + 1
         if k > _SORT_MAX_KEYS or T * n >= (1 << 31):
             return None
         dev = node_of.device
         lib = native.require_kernels()
         tt = torch.arange(T, device=dev, dtype=torch.int32)[:, None] * width
-        live = node_of >= 0
-        if weight is not None:
-            live &= weight > 0
-        keys = torch.where(live, node_of + tt, torch.full_like(node_of, k - 1))
+        off = tt if weight is None else tt + (weight == 0).to(torch.int32) * (T * width)
+        keys = torch.where(node_of >= 0, node_of + off, torch.full_like(node_of, k - 1))
         keys = keys.reshape(-1).contiguous()
         perm = torch.empty(T * n, dtype=torch.int32, device=dev)
         counts = torch.empty(k, dtype=torch.int64, device=dev)
@@ -299,8 +303,9 @@ class RowGroups:
         rc = lib.oryx_counting_sort(keys.data_ptr(), T * n, k, perm.data_ptr(),
                                     counts.data_ptr(), ws.data_ptr(), native.stream_ptr(dev))
         native.check(rc, "oryx_counting_sort")
-        c = counts.cpu().numpy()[:-1].reshape(T, width)
-        return RowGroups(perm, c, width, n)
+        c = counts.cpu().numpy()[:-1]
+        live = c[:T * width].reshape(T, width)
+        return RowGroups(perm, live, width, n, live + c[T * width:].reshape(T, width))
 
     def pieces(self, lo: int, hi: int, dev):
         """(tree, node - lo, begin, end) of every PIECE-row slice of nodes [lo, hi)."""
@@ -346,10 +351,14 @@ def _histogram_groups(data: BinnedData, label, y, S, cls, weight, groups: RowGro
     return hist
 
 
-def _route(data: BinnedData, node_of, nodes, split: LevelSplits, child_base, B):
+def _route(data: BinnedData, node_of, nodes, split: LevelSplits, child_base, B,
+           count_visits: bool = True):
+    """Move every open row one level down; returns the per-node visit counts (None on the
+    GPU when ``count_visits`` is off: the grouped path already has them)."""
     T, n = node_of.shape
     dev = node_of.device
-    visits = torch.zeros((T, nodes), dtype=torch.int64, device=dev)
+    visits = torch.zeros((T, nodes), dtype=torch.int64, device=dev) \
+        if count_visits or dev.type != "cuda" else None
     if dev.type == "cuda":
         lib = native.require_kernels()
         # keep every converted operand alive until the launch: a temporary freed mid-call
@@ -361,7 +370,8 @@ def _route(data: BinnedData, node_of, nodes, split: LevelSplits, child_base, B):
         rc = lib.oryx_rdf_route(data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.shape[1], T,
                                 node_of.data_ptr(), nodes, sf.data_ptr(), sb.data_ptr(),
                                 cl.data_ptr() if cl is not None else None, B, cb.data_ptr(),
-                                visits.data_ptr(), native.stream_ptr(dev))
+                                visits.data_ptr() if visits is not None else None,
+                                native.stream_ptr(dev))
         native.check(rc, "oryx_rdf_route")
         return visits
     for t in range(T):
@@ -482,7 +492,11 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
         is_split = split.feat >= 0
         rank = torch.cumsum(is_split.int(), 1) - is_split.int()
         child_base = torch.where(is_split, 2 * rank, torch.full_like(rank, -1))
-        visits = _route(data, node_of, nodes, split, child_base, B)
+        if groups is not None and groups.visits is not None:
+            _route(data, node_of, nodes, split, child_base, B, count_visits=False)
+            visits = torch.from_numpy(np.ascontiguousarray(groups.visits[:, :nodes])).to(dev)
+        else:
+            visits = _route(data, node_of, nodes, split, child_base, B)
         if ctx.is_distributed:
             dist.all_reduce_sum(visits, ctx)
         feat_h = split.feat.cpu().numpy()

@@ -416,11 +416,13 @@ def test_gpu_forest_leaves_match_cpu(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cls", [True, False])
-def test_histogram_and_route_kernels_match_cpu(cuda, cls):
+@pytest.mark.parametrize("n,P", [(40000, 12), (40001, 13)])
+def test_histogram_and_route_kernels_match_cpu(cuda, cls, n, P):
     """Level kernels on a wide level (200 node slots -> several LDS node chunks per tree,
-    bootstrap weights, 3 trees) against the CPU index_add / gather implementations."""
+    bootstrap weights, 3 trees) against the CPU index_add / gather implementations.  P = 13
+    puts rows off dword boundaries and leaves a partial dword at the end of the bins."""
     g = torch.Generator().manual_seed(5)
-    n, P, B, T, nodes, Fs = 40000, 12, 40, 3, 200, 5
+    B, T, nodes, Fs = 40, 3, 200, 5
     Xb = torch.randint(0, B, (n, P), generator=g).to(torch.uint8)
     data = rdf_ops.BinnedData(Xb, [B] * P, [np.arange(B - 1, dtype=np.float64)] * P,
                               [False] * P, B)
@@ -472,3 +474,10 @@ def test_histogram_and_route_kernels_match_cpu(cuda, cls):
     v_gpu = rdf_ops._route(gd, no_g, nodes, split_g, cb.to(cuda), B)
     assert torch.equal(v_gpu.cpu(), v_cpu)
     assert torch.equal(no_g.cpu(), no_c)
+    # all-trees-per-row route (no visit counters) moves rows identically, and the counting
+    # sort's visit counts (weight-0 rows included) equal the routing tallies
+    no_r = node_of.to(cuda)
+    assert rdf_ops._route(gd, no_r, nodes, split_g, cb.to(cuda), B, count_visits=False) is None
+    assert torch.equal(no_r.cpu(), no_c)
+    assert groups.visits is not None
+    assert np.array_equal(groups.visits, v_cpu.numpy())
