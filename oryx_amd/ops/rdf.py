@@ -60,6 +60,15 @@ class BinnedData:
     def bin_bytes(self) -> int:
         return self.Xb.element_size()
 
+    def cat_flags(self) -> torch.Tensor:
+        """Device copy of ``categorical`` (made once: a host list -> device tensor per level
+        is a blocking copy)."""
+        cf = getattr(self, "_cat_dev", None)
+        if cf is None or cf.device != self.Xb.device:
+            cf = torch.tensor(self.categorical, device=self.Xb.device)
+            object.__setattr__(self, "_cat_dev", cf)
+        return cf
+
 
 def _quantile_thresholds(col: np.ndarray, max_bins: int) -> np.ndarray:
     u = np.unique(col)
@@ -161,10 +170,11 @@ def _choose_splits(hist: torch.Tensor, feats: torch.Tensor, data: BinnedData, ki
     if B < 2:
         none = torch.full((T, N), -1, dtype=torch.int64, device=dev)
         return LevelSplits(none, none.clone(), None, totals, torch.zeros((T, N), device=dev))
-    cat_flag = torch.tensor(data.categorical, device=dev)[feats]    # [T, N, Fs]
+    any_cat = any(data.categorical)                                 # host: no device sync
+    cat_flag = data.cat_flags()[feats]                              # [T, N, Fs]
     h = hist
     order = None
-    if bool(cat_flag.any()):
+    if any_cat:
         # categorical bins ordered by label centroid (regression: mean; classification:
         # share of the node's majority class); empty bins last
         if kind == "variance":
@@ -199,7 +209,7 @@ def _choose_splits(hist: torch.Tensor, feats: torch.Tensor, data: BinnedData, ki
     is_cat = cat_flag.gather(2, j[..., None])[..., 0] & ~leaf
     sbin = torch.where(is_cat | leaf, torch.full_like(k, -1), k)
     cat_left = None
-    if bool(is_cat.any()):
+    if any_cat:
         # left set = the first k+1 categories in centroid order
         o = order.gather(2, j[:, :, None, None].expand(T, N, 1, B))[:, :, 0]   # [T, N, B]
         pos_in_order = torch.empty_like(o)
@@ -499,11 +509,20 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
             visits = _route(data, node_of, nodes, split, child_base, B)
         if ctx.is_distributed:
             dist.all_reduce_sum(visits, ctx)
-        feat_h = split.feat.cpu().numpy()
-        bin_h = split.bin.cpu().numpy()
-        tot_h = split.totals.double().cpu().numpy()
-        vis_h = visits.cpu().numpy()
-        cat_h = split.cat_left.cpu().numpy() if split.cat_left is not None else None
+        # one device -> host transfer (one sync) for everything the host tree needs
+        parts = [split.feat.double().reshape(T, -1), split.bin.double().reshape(T, -1),
+                 split.totals.double().reshape(T, -1), visits.double().reshape(T, -1)]
+        if split.cat_left is not None:
+            parts.append(split.cat_left.double().reshape(T, -1))
+        host = torch.cat(parts, 1).cpu().numpy()
+        w = [p_.shape[1] for p_ in parts]
+        cut = np.cumsum([0] + w)
+        feat_h = host[:, cut[0]:cut[1]].astype(np.int64)
+        bin_h = host[:, cut[1]:cut[2]].astype(np.int64)
+        tot_h = host[:, cut[2]:cut[3]].reshape(split.totals.shape)
+        vis_h = host[:, cut[3]:cut[4]].astype(np.int64)
+        cat_h = host[:, cut[4]:cut[5]].reshape(split.cat_left.shape).astype(np.uint8) \
+            if split.cat_left is not None else None
         next_nodes = 0
         new_level: List[List[Optional[TrainedNode]]] = []
         for t in range(T):
