@@ -16,6 +16,7 @@ Equivalent of ``RDFUpdate`` (``[mllib]/rdf/RDFUpdate.java:97-558``) and ``Evalua
 
 from __future__ import annotations
 
+import io
 import logging
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -46,6 +47,58 @@ def distinct_values(rows: Sequence[Sequence[str]], schema: InputSchema) -> Dict[
         for i in cats:
             seen[i].setdefault(r[i], None)
     return {i: list(v.keys()) for i, v in seen.items()}
+
+
+def parse_csv_block(lines: Sequence[str], schema: InputSchema,
+                    encodings: CategoricalValueEncodings):
+    """Fast path of ``parse_input_line`` + :func:`parse_examples` for a block of plain CSV
+    lines (no JSON arrays, no quoting): one C-level CSV parse (pandas) with numeric columns
+    read straight to float64.  Returns ``(X, target, full)`` or None when the block does not
+    qualify (the caller then takes the general path)."""
+    try:
+        import pandas as pd
+    except ImportError:                                     # pragma: no cover
+        return None
+    if not lines:
+        return None
+    blob = "\n".join(lines)
+    if '"' in blob or "\\" in blob or "[" in blob:
+        return None
+    F = schema.get_num_features()
+    dtypes = {fi: (np.float64 if schema.is_numeric(fi) else str) for fi in range(F)}
+    try:
+        df = pd.read_csv(io.StringIO(blob), header=None, dtype=dtypes, names=list(range(F)),
+                         keep_default_na=False, na_values={fi: [""] for fi in range(F)
+                                                           if schema.is_numeric(fi)},
+                         engine="c")
+    except (ValueError, pd.errors.ParserError):
+        return None
+    if len(df) != len(lines) or df.shape[1] != F:
+        return None
+    n = len(df)
+    full = np.zeros((n, F), dtype=np.float64)
+    for fi in range(F):
+        col = df[fi]
+        if schema.is_numeric(fi):
+            v = col.to_numpy(dtype=np.float64)
+            if np.isnan(v).any() and not schema.is_target(fi):
+                return None                                  # empty predictor: general path
+            full[:, fi] = v
+        elif schema.is_categorical(fi):
+            m = encodings.get_value_encoding_map(fi)
+            uniq, inv = np.unique(col.to_numpy(dtype=str), return_inverse=True)
+            try:
+                codes = np.array([m[u] if u != "" else np.nan for u in uniq.tolist()],
+                                 dtype=np.float64)
+            except KeyError:
+                return None                                  # unknown value: general path
+            if not schema.is_target(fi) and np.isnan(codes).any():
+                return None
+            full[:, fi] = codes[inv.reshape(-1)]
+    X = full[:, schema.predictor_feature_indices]
+    target = full[:, schema.get_target_feature_index()] if schema.has_target() else \
+        np.full(n, np.nan)
+    return X, target, full
 
 
 def parse_examples(rows: Sequence[Sequence[str]], schema: InputSchema,

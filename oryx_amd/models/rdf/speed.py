@@ -23,7 +23,7 @@ from ...ops import rdf as rdf_ops
 from ...utils import pmml as pmmlu, text
 from ..schema import InputSchema
 from . import pmml as rdf_pmml
-from .batch import parse_examples
+from .batch import parse_csv_block, parse_examples
 
 __all__ = ["RDFSpeedModel", "RDFSpeedModelManager"]
 
@@ -87,10 +87,14 @@ class RDFSpeedModelManager(SpeedModelManager):
         if model is None:
             return []
         schema = self.input_schema
-        rows = [text.parse_input_line(v) for v in new_data.values()]
-        if not rows:
+        values = list(new_data.values())
+        if not values:
             return []
-        _, target, full = parse_examples(rows, schema, model.encodings, require_target=False)
+        parsed = parse_csv_block(values, schema, model.encodings)
+        if parsed is None:
+            rows = [text.parse_input_line(v) for v in values]
+            parsed = parse_examples(rows, schema, model.encodings, require_target=False)
+        _, target, full = parsed
         C = model.encodings.get_value_count(schema.get_target_feature_index()) \
             if schema.is_classification() else 0
         flat = model.flat(self.device, C)
@@ -106,28 +110,29 @@ class RDFSpeedModelManager(SpeedModelManager):
         flat_leaf = leaves.ravel().astype(np.int64)
         vals = np.broadcast_to(tv[:, None], leaves.shape).ravel()
         out = []
+        # node ids of the touched leaves, looked up once per distinct leaf
         if schema.is_classification():
             # one pass over (leaf, class) pairs: counts per leaf per class
             cls = vals.astype(np.int64)
             nc = int(cls.max()) + 1
             keys, counts = np.unique(flat_leaf * nc + cls, return_counts=True)
             leaf_k, cls_k = keys // nc, keys % nc
-            bounds = np.flatnonzero(np.diff(leaf_k)) + 1
-            for seg_l, seg_c, seg_n in zip(np.split(leaf_k, bounds), np.split(cls_k, bounds),
-                                           np.split(counts, bounds)):
-                leaf = int(seg_l[0])
-                t = int(np.searchsorted(roots, leaf, side="right")) - 1
-                cmap = {str(int(c)): int(k) for c, k in zip(seg_c, seg_n)}
-                out.append(json.dumps([t, flat.nodes[leaf].get_id(), cmap],
-                                      separators=(",", ":")))
+            starts = np.flatnonzero(np.r_[True, np.diff(leaf_k) != 0])
+            ends = np.r_[starts[1:], len(leaf_k)]
+            trees = (np.searchsorted(roots, leaf_k[starts], side="right") - 1).tolist()
+            leaf_l, cls_l, cnt_l = leaf_k.tolist(), cls_k.tolist(), counts.tolist()
+            for j, (a, b) in enumerate(zip(starts.tolist(), ends.tolist())):
+                cmap = ",".join('"%d":%d' % (cls_l[q], cnt_l[q]) for q in range(a, b))
+                out.append('[%d,%s,{%s}]' % (trees[j], json.dumps(flat.nodes[leaf_l[a]].get_id()),
+                                             cmap))
         else:
             keys, inv, counts = np.unique(flat_leaf, return_inverse=True, return_counts=True)
             sums = np.bincount(inv, weights=vals, minlength=len(keys))
-            trees = np.searchsorted(roots, keys, side="right") - 1
+            trees = (np.searchsorted(roots, keys, side="right") - 1).tolist()
+            means = (sums / counts).tolist()
             for j, leaf in enumerate(keys.tolist()):
-                out.append(json.dumps([int(trees[j]), flat.nodes[leaf].get_id(),
-                                       float(sums[j] / counts[j]), int(counts[j])],
-                                      separators=(",", ":")))
+                out.append(json.dumps([trees[j], flat.nodes[leaf].get_id(), means[j],
+                                       int(counts[j])], separators=(",", ":")))
         return out
 
     def close(self) -> None:

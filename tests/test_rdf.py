@@ -481,3 +481,27 @@ def test_histogram_and_route_kernels_match_cpu(cuda, cls, n, P):
     assert torch.equal(no_r.cpu(), no_c)
     assert groups.visits is not None
     assert np.array_equal(groups.visits, v_cpu.numpy())
+
+
+def test_csv_block_fast_path_matches_general_parse():
+    """parse_csv_block (pandas C parser) returns exactly what parse_input_line +
+    parse_examples return, declines blocks it cannot take (quotes, JSON arrays, unknown
+    categories), and keeps an empty target as NaN."""
+    from oryx_amd.models.rdf.batch import parse_csv_block
+    from oryx_amd.utils import text
+    schema = InputSchema(cfg.overlay_on({
+        "oryx.input-schema.feature-names": '["a","b","c","t"]',
+        "oryx.input-schema.categorical-features": '["b","t"]',
+        "oryx.input-schema.target-feature": '"t"'}, cfg.get_default()))
+    enc = CategoricalValueEncodings({1: ["x", "y"], 3: ["no", "yes"]})
+    lines = ["1.5,x,-2,yes", "0.25,y,3e2,no", "7,x,0,", "-1,y,1.125,yes"]
+    got = parse_csv_block(lines, schema, enc)
+    want = parse_examples([text.parse_input_line(v) for v in lines], schema, enc,
+                          require_target=False)
+    assert got is not None
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+    assert np.isnan(got[1][2])
+    assert parse_csv_block(['1,"x",2,yes'], schema, enc) is None
+    assert parse_csv_block(['[1,"x",2,"yes"]'], schema, enc) is None
+    assert parse_csv_block(["1,z,2,yes"], schema, enc) is None
