@@ -197,6 +197,27 @@ __global__ __launch_bounds__(256) void rdf_route_rows(const BinT* __restrict__ X
   }
 }
 
+// Counting-sort keys of one level (RowGroups.from_nodes): open rows with bootstrap weight
+// > 0 -> t * width + node, weight-0 open rows -> T * width + t * width + node (visits only),
+// rows in leaves -> 2 T width.  One pass instead of four elementwise tensor ops.
+__global__ __launch_bounds__(256) void rdf_sort_keys(const int* __restrict__ node_of,
+                                                     const unsigned char* __restrict__ weight,
+                                                     int T, long long n, int width,
+                                                     int* __restrict__ keys) {
+  const int t = blockIdx.y;                                   // grid y = tree: no division
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    const long long k = (long long)t * n + i;
+    const int node = node_of[k];
+    int key = 2 * T * width;
+    if (node >= 0) {
+      key = t * width + node;
+      if (weight && weight[k] == 0) key += T * width;
+    }
+    keys[k] = key;
+  }
+}
+
 // Segmented level histogram: rows are kept grouped by (tree, node) -- a counting sort of the
 // routed rows after every level (oryx_counting_sort) -- so a workgroup owns one PIECE of one
 // node's rows: it reads only those rows (row ids through the permutation), accumulates the
@@ -585,6 +606,16 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
     }
   }
 #undef PIECE_LAUNCH
+  return oryx_check_launch();
+}
+
+int oryx_rdf_sort_keys(const int* node_of, const unsigned char* weight, int T, long long n,
+                       int width, int* keys, void* stream) {
+  if (T <= 0 || n <= 0) return ORYX_OK;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(rdf_sort_keys, dim3((unsigned)blocks, (unsigned)T), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), node_of, weight, T, n, width, keys);
   return oryx_check_launch();
 }
 

@@ -139,6 +139,7 @@ def _load_kernels():
                                           c_vp, c_i, c_i, c_vp, c_i, c_i, c_vp, c_vp])
     # Xb, bin_bytes, n, P, T, node_of, nodes, split_feat, split_bin, cat_left, B, child_base,
     # visits, stream
+    _sig(lib, "oryx_rdf_sort_keys", c_i, [c_vp, c_vp, c_i, c_ll, c_i, c_vp, c_vp])
     _sig(lib, "oryx_rdf_route", c_i, [c_vp, c_i, c_ll, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp,
                                       c_i, c_vp, c_vp, c_vp])
     # X, n, F, T, roots, feat, thr, cat_off, cat_bits, cat_len, left, right, leaf, stream

@@ -302,10 +302,12 @@ class RowGroups:
             return None
         dev = node_of.device
         lib = native.require_kernels()
-        tt = torch.arange(T, device=dev, dtype=torch.int32)[:, None] * width
-        off = tt if weight is None else tt + (weight == 0).to(torch.int32) * (T * width)
-        keys = torch.where(node_of >= 0, node_of + off, torch.full_like(node_of, k - 1))
-        keys = keys.reshape(-1).contiguous()
+        keys = torch.empty(T * n, dtype=torch.int32, device=dev)
+        w = weight.contiguous() if weight is not None else None
+        rc = lib.oryx_rdf_sort_keys(node_of.contiguous().data_ptr(),
+                                    w.data_ptr() if w is not None else None, T, n, width,
+                                    keys.data_ptr(), native.stream_ptr(dev))
+        native.check(rc, "oryx_rdf_sort_keys")
         perm = torch.empty(T * n, dtype=torch.int32, device=dev)
         counts = torch.empty(k, dtype=torch.int64, device=dev)
         ws = torch.empty(int(lib.oryx_kmeans_sorted_ws_bytes(T * n, k)), dtype=torch.uint8,
@@ -456,8 +458,12 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     if T > 1:
         gd = torch.Generator(device=dev)
         gd.manual_seed((seed * 31 + ctx.rank + 7) & ((1 << 62) - 1))
-        weight = torch.poisson(torch.ones((T, n), device=dev), generator=gd).clamp_(max=255) \
-            .to(torch.uint8)
+        # Poisson(1) bootstrap counts by inverse CDF of one uniform per (tree, row): same
+        # distribution as torch.poisson (the rejection sampler), a fraction of its time
+        k = torch.arange(24, dtype=torch.float64)
+        cdf = torch.cumsum(torch.exp(-1.0 - torch.lgamma(k + 1.0)), 0)[:-1].to(torch.float32)
+        u = torch.rand((T, n), generator=gd, device=dev)
+        weight = torch.bucketize(u, cdf.to(dev), right=True).to(torch.uint8)
     else:
         weight = None
     Fs = feature_subset or _feature_subset_size(P, T, classification)
