@@ -319,15 +319,18 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
   const int per_node = Fs * B * S;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float* lh = lsm;                                                        // [per_node]
-  unsigned int* rows = reinterpret_cast<unsigned int*>(lsm + per_node) + wave * 64 * RSW;
+  int* fjs = reinterpret_cast<int*>(lsm + per_node);                      // [Fs]
+  unsigned int* rows = reinterpret_cast<unsigned int*>(lsm + per_node + ((Fs + 3) & ~3)) +
+                       wave * 64 * RSW;
   const unsigned char* rowb = reinterpret_cast<const unsigned char*>(rows);
   const int pc = blockIdx.x;
   const int t = piece_tree[pc];
   const int node = piece_node[pc];
   float* gh = hist + ((long long)t * nodes + node) * per_node;
   for (int i = tid; i < per_node; i += 256) lh[i] = 0.f;   // 0.f and 0u share the bits
-  __syncthreads();
   const int* fj = feats + ((long long)t * nodes + node) * Fs;
+  for (int j = tid; j < Fs; j += 256) fjs[j] = fj[j];
+  __syncthreads();
   const long long p0 = piece_lo[pc], p1 = piece_hi[pc];
   const long long toff = (long long)t * n;
   const unsigned int* Xw = reinterpret_cast<const unsigned int*>(Xb);
@@ -339,21 +342,30 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
   for (int b = 0; b < (int)(nbytes & 3); ++b)
     tailw |= (unsigned int)Xb[(long long)nfull * 4 + b] << (8 * b);
   const int half = lane >> 5, wl = lane & 31;
+  // software pipeline over the wave's 64-row batches: the next batch's row ids are loaded
+  // with this batch's row bytes, and its weights / labels while this batch's bytes go
+  // through LDS, so each batch waits on one memory round trip instead of three
+  long long i = -1;
+  {
+    const long long q = p0 + wave * 64 + lane;
+    if (q < p1) i = perm ? (long long)perm[q] - toff : q - toff;
+  }
+  unsigned int wgt = 0;
+  float ylab = 0.f;
+  int lab = 0;
+  if (i >= 0) {
+    wgt = weight ? weight[toff + i] : 1u;
+    if (CLS) lab = label[i]; else ylab = y[i];
+  }
   for (long long q0 = p0 + wave * 64; q0 < p1; q0 += 256) {
-    const long long q = q0 + lane;
-    const long long i = q < p1 ? (perm ? (long long)perm[q] - toff : q - toff) : -1;
-    float v0 = 0.f, v1 = 0.f, v2 = 0.f;
-    int s0 = 0;
-    if (i >= 0) {
-      v0 = weight ? (float)weight[toff + i] : 1.f;
-      if (CLS) {
-        s0 = label[i];
-      } else {
-        const float yi = y[i];
-        v1 = v0 * yi;
-        v2 = v0 * yi * yi;
-      }
+    long long inext = -1;
+    {
+      const long long q = q0 + 256 + lane;
+      if (q < p1) inext = perm ? (long long)perm[q] - toff : q - toff;
     }
+    const float v0 = (float)wgt;
+    const int s0 = lab;
+    const float v1 = v0 * ylab, v2 = v0 * ylab * ylab;
     const int nr = (int)((p1 - q0) < 64 ? (p1 - q0) : 64);
     // stage: step it copies rows 2 it (lanes 0-31) and 2 it + 1 (lanes 32-63), dword
     // wp * 32 + (lane & 31) of each; all 32 steps' loads are issued before the first LDS
@@ -385,19 +397,35 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
     // the fence only stops the compiler from reordering them)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // next batch's weights / labels, in flight during this batch's LDS work
+    const long long icur = i;
+    i = inext;
+    wgt = 0;
+    if (i >= 0) {
+      wgt = weight ? weight[toff + i] : 1u;
+      if (CLS) lab = label[i]; else ylab = y[i];
+    }
     const unsigned int wcnt = (unsigned int)v0;
     if (v0 != 0.f) {
-      const unsigned char* xr = rowb + lane * RSW * 4 + (int)((i * P) & 3);
-      for (int j = 0; j < Fs; ++j) {
-        const int b = xr[fj[j]];
-        float* h = lh + (j * B + b) * S;
-        if (CLS) {
-          // integer counts (bootstrap weights are small integers): ds_add_u32, exact
-          atomicAdd(reinterpret_cast<unsigned int*>(h) + s0, wcnt);
-        } else {
-          atomicAdd(h, v0);
-          atomicAdd(h + 1, v1);
-          atomicAdd(h + 2, v2);
+      const unsigned char* xr = rowb + lane * RSW * 4 + (int)((icur * P) & 3);
+      // features in groups of 8: the 8 byte reads are issued before the 8 atomics (the
+      // feature indices come from LDS, copied there once per workgroup)
+      for (int j0 = 0; j0 < Fs; j0 += 8) {
+        int b[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) b[u] = j0 + u < Fs ? xr[fjs[j0 + u]] : 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (j0 + u >= Fs) break;
+          float* h = lh + ((j0 + u) * B + b[u]) * S;
+          if (CLS) {
+            // integer counts (bootstrap weights are small integers): ds_add_u32, exact
+            atomicAdd(reinterpret_cast<unsigned int*>(h) + s0, wcnt);
+          } else {
+            atomicAdd(h, v0);
+            atomicAdd(h + 1, v1);
+            atomicAdd(h + 2, v2);
+          }
         }
       }
     }
@@ -570,7 +598,7 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
   if (staged_ok && bin_bytes == 1 && n * (long long)P < (1LL << 34) && n * (long long)P >= 4) {
     const int ndw = (P + 3) / 4 + 1;                 // dwords covering any row alignment
     const int rsw = ndw | 1;
-    const long long smem_st = per_node_bytes + 256LL * rsw * 4;
+    const long long smem_st = per_node_bytes + ((Fs + 3) & ~3) * 4LL + 256LL * rsw * 4;
     if (smem_st <= 64 * 1024) {
       if (cls)
         hipLaunchKernelGGL((rdf_histogram_staged<true>), dim3((unsigned)n_pieces), dim3(256),

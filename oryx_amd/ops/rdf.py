@@ -262,7 +262,7 @@ def _histogram(data: BinnedData, label, y, S, cls, weight, node_of, lo, nodes, f
     return hist
 
 
-_PIECE = 4096          # rows per workgroup in the segmented histogram
+_PIECE = int(os.environ.get("ORYX_RDF_PIECE", "16384"))   # rows per histogram workgroup
 _SORT_MAX_KEYS = 16384
 
 

@@ -5,9 +5,9 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_rdf.py tests/test_kmeans.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t_rdf.log 2>&1 || { tail -30 gpurun_out/t_rdf.log; exit 1; }
 tail -2 gpurun_out/t_rdf.log
-for h in ${HISTS:-1 0}; do
-  ORYX_RDF_HIST=$h timeout -k 10 400 python bench_rdf.py --steps 2 --warmup 1 --speed-events 2000 > gpurun_out/brdf$h.log 2>&1 || { tail -30 gpurun_out/brdf$h.log; exit 1; }
-  echo "hist=$h $(tail -1 gpurun_out/brdf$h.log | cut -c1-400)"
+for h in ${HISTS:-1 0}; do for pc in ${PIECES:-16384}; do
+  ORYX_RDF_PIECE=$pc ORYX_RDF_HIST=$h timeout -k 10 400 python bench_rdf.py --steps 2 --warmup 1 --speed-events 2000 > gpurun_out/brdf$h.log 2>&1 || { tail -30 gpurun_out/brdf$h.log; exit 1; }
+  echo "hist=$h piece=$pc $(tail -1 gpurun_out/brdf$h.log | cut -c1-300)"; done
 done
 if [[ ${PROF:-1} == 1 ]]; then
   cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

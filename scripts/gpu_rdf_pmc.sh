@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 rm -rf gpurun_out/pmc_rdf
-timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM -d gpurun_out/pmc_rdf -o run --output-format csv -- python3 bench_rdf.py --steps 1 --warmup 0 --speed-events 100 > gpurun_out/pmc_rdf.log 2>&1 || { tail -20 gpurun_out/pmc_rdf.log; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS -d gpurun_out/pmc_rdf -o run --output-format csv -- python3 bench_rdf.py --steps 1 --warmup 0 --speed-events 100 > gpurun_out/pmc_rdf.log 2>&1 || { tail -20 gpurun_out/pmc_rdf.log; exit 1; }
 python3 - <<'PY'
 import csv, collections
 rows = list(csv.DictReader(open('gpurun_out/pmc_rdf/run_counter_collection.csv')))
