@@ -679,7 +679,7 @@ struct PanelSmem {
 //   * back substitution L^T x = z reads the LDS panels (off the dependency chain).
 // Per row (KP=64): 480 in-panel FMAs per lane + 40 small MFMAs, versus 2016 FMAs per lane for
 // the all-register column Cholesky of als_solve_wave.
-template <int KP, bool PROF = false, bool DEEP = false>
+template <int KP, bool PROF = false, bool DEEP = false, int PRIO = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : ORYX_ALS_PANEL_WAVES, DEEP ? 2 : ORYX_ALS_PANEL_WAVES))) void als_solve_panel(AlsParams p, unsigned long long* prof) {
   using PS = PanelSmem<KP>;
   constexpr int M = KP / 16;
@@ -769,6 +769,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
       wsrow = src;
     }
     ORYX_PHASE(0)
+    // PRIO > 0: the serial factorisation runs at raised issue priority, so when the SIMD's
+    // other wave is gathering, this wave's dependent chain is not left waiting behind it
+    if (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
     float dinv = 0.f, z_own = 0.f;
     // opaque lane id (keeps per-step lane masks from being hoisted into SGPR pairs)
     int ln = lane;
@@ -925,6 +928,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
       if (p.Xb) p.Xb[(int64_t)row * KP + lane] = (__bf16)x_own;
     }
     wave_sync();
+    if (PRIO > 0) __builtin_amdgcn_s_setprio(0);
     ORYX_PHASE(5)
 #undef ORYX_PHASE
   }
@@ -1484,16 +1488,17 @@ __global__ __launch_bounds__(256) void pair_dots(const float* __restrict__ X,
 }  // namespace
 
 // KP <= 64 solve kernel: 2 = als_solve_panel with three chunks of gathers in flight at 2 waves
-// per SIMD (default), 0 = als_solve_panel with one chunk in flight at 3 waves per SIMD,
-// 1 = als_solve_wave (register column Cholesky)
-static int g_als_variant = 2;
+// per SIMD, 0 = als_solve_panel with one chunk in flight at 3 waves per SIMD, 1 =
+// als_solve_wave (register column Cholesky), 3 (default) / 4 = variant 2 with the
+// factorisation at raised issue priority (s_setprio 2 / 3: 2-6% faster half-steps than 2)
+static int g_als_variant = 3;
 // 64 < KP <= 128: 0 = als_solve_wide (default), 1 = als_solve_block (LDS Cholesky)
 static int g_als_wide_variant = 0;
 
 extern "C" {
 
 int oryx_als_set_variant(int v) {
-  if (v < 0 || v > 2) return ORYX_EINVAL;
+  if (v < 0 || v > 4) return ORYX_EINVAL;
   g_als_variant = v;
   return ORYX_OK;
 }
@@ -1552,6 +1557,12 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
     else if (g_als_variant == 2)                                                      \
       hipLaunchKernelGGL((als_solve_panel<KPV, false, true>), dim3(blocks), dim3(256), 0, \
                          s, p, nullptr);                                              \
+    else if (g_als_variant == 3)                                                      \
+      hipLaunchKernelGGL((als_solve_panel<KPV, false, true, 2>), dim3(blocks), dim3(256), \
+                         0, s, p, nullptr);                                           \
+    else if (g_als_variant == 4)                                                      \
+      hipLaunchKernelGGL((als_solve_panel<KPV, false, true, 3>), dim3(blocks), dim3(256), \
+                         0, s, p, nullptr);                                           \
     else                                                                              \
       hipLaunchKernelGGL((als_solve_wave<KPV, false>), dim3(blocks), dim3(256), 0, s, p, \
                          nullptr);                                                    \
@@ -1611,6 +1622,12 @@ int oryx_als_solve_profile64(const int64_t* row_ptr, const int32_t* row_ids,
                        reinterpret_cast<hipStream_t>(stream), p, prof);
   else if (g_als_variant == 2)
     hipLaunchKernelGGL((als_solve_panel<64, true, true>), dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), p, prof);
+  else if (g_als_variant == 3)
+    hipLaunchKernelGGL((als_solve_panel<64, true, true, 2>), dim3(blocks), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), p, prof);
+  else if (g_als_variant == 4)
+    hipLaunchKernelGGL((als_solve_panel<64, true, true, 3>), dim3(blocks), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), p, prof);
   else
     hipLaunchKernelGGL((als_solve_wave<64, true>), dim3(blocks), dim3(256), 0,

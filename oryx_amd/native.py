@@ -107,7 +107,7 @@ def _load_kernels():
     # ORYX_ALS_VARIANT selects the KP<=64 solve kernel for A/B runs (csrc/kernels/als.hip:
     # 2 = panel Cholesky + 3-deep gather ring (default), 0 = panel + 1-deep, 1 = register)
     _sig(lib, "oryx_als_set_variant", c_i, [c_i])
-    lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "2")))
+    lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "3")))
     # ORYX_ALS_WIDE_VARIANT: 64 < k <= 128 solve (0 = als_solve_wide, 1 = als_solve_block)
     _sig(lib, "oryx_als_set_wide_variant", c_i, [c_i])
     lib.oryx_als_set_wide_variant(int(os.environ.get("ORYX_ALS_WIDE_VARIANT", "0")))

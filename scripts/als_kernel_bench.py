@@ -45,7 +45,7 @@ def main():
             ts.append(a.elapsed_time(b))
         return statistics.median(ts)
 
-    out = {"k": args.rank_k, "variant": os.environ.get("ORYX_ALS_VARIANT", "2")}
+    out = {"k": args.rank_k, "variant": os.environ.get("ORYX_ALS_VARIANT", "3")}
     yty_x = als_ops.gramian(tr.X)
     yty_y = als_ops.gramian(tr.Y)
     out["gramian_users_ms"] = timed(lambda: als_ops.gramian(tr.X))

@@ -14,7 +14,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-if os.environ.get("ORYX_ALS_VARIANT", "2") == "1":   # als_solve_wave (register Cholesky)
+if os.environ.get("ORYX_ALS_VARIANT", "3") == "1":   # als_solve_wave (register Cholesky)
     PHASES = ["gather+mfma", "scatter/ws", "load A+YtY", "cholesky", "forward", "back+store"]
 else:                                               # als_solve_panel (default)
     PHASES = ["gather+mfma+b", "-", "panel to/from LDS (+YtY, diag)",
