@@ -1,0 +1,63 @@
+"""The driver's bench.py contract on CPU (gloo): one JSON line from rank 0 with the metric and
+config BASELINE.json names, the whole-job value, and world size 2 through
+torch.distributed.run on 127.0.0.1."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--device", "cpu", "--ratings-per-gpu", "20000", "--users-per-gpu", "500", "--items",
+         "300", "--rank-k", "16", "--steps", "1", "--warmup", "1", "--speed-events", "100"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_lines(out):
+    return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+
+
+def _check(rec, n):
+    baseline = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert rec["metric"] == baseline["metric"]
+    for key in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in rec, key
+    assert rec["n_gpus"] == n and rec["steps"] == 1 and rec["warmup"] == 1
+    assert rec["value"] > 0 and rec["ms_per_step"] > 0
+    assert rec["higher_is_better"] is True and rec["scaling"] == "weak"
+    # whole-job aggregate: ratings of all ranks over the timed step
+    assert abs(rec["value"] - rec["config"]["global_batch"] / (rec["ms_per_step"] * 1e-3)) \
+        <= 1e-6 * rec["value"]
+    assert rec["config"]["global_batch"] == 20000 * n
+
+
+@pytest.mark.timeout(600)
+def test_bench_single_process_cpu():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + SMALL,
+                         capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    recs = _json_lines(out.stdout)
+    assert len(recs) == 1
+    _check(recs[0], 1)
+
+
+@pytest.mark.timeout(600)
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    recs = _json_lines(out.stdout)
+    assert len(recs) == 1                       # rank 0 only
+    _check(recs[0], 2)
