@@ -292,6 +292,15 @@ class RowGroups:
     @staticmethod
     def from_nodes(node_of: torch.Tensor, width: int,
                    weight: Optional[torch.Tensor] = None) -> Optional["RowGroups"]:
+        finish = RowGroups.launch_from_nodes(node_of, width, weight)
+        return finish() if finish is not None else None
+
+    @staticmethod
+    def launch_from_nodes(node_of: torch.Tensor, width: int,
+                          weight: Optional[torch.Tensor] = None):
+        """Queue the level's counting sort on the device and return ``finish()`` (which waits
+        for the counts and builds the RowGroups), or None when the key space is too wide; the
+        host can do other work between the two."""
         """Counting sort of the rows by (tree, node); None when the key space is too wide.
         Rows a tree's bootstrap left out (weight 0) only count as node visits: they get a
         second key per node after all live keys, and rows that reached a leaf a last, unused
@@ -315,9 +324,12 @@ class RowGroups:
         rc = lib.oryx_counting_sort(keys.data_ptr(), T * n, k, perm.data_ptr(),
                                     counts.data_ptr(), ws.data_ptr(), native.stream_ptr(dev))
         native.check(rc, "oryx_counting_sort")
-        c = counts.cpu().numpy()[:-1]
-        live = c[:T * width].reshape(T, width)
-        return RowGroups(perm, live, width, n, live + c[T * width:].reshape(T, width))
+
+        def finish() -> "RowGroups":
+            c = counts.cpu().numpy()[:-1]
+            live = c[:T * width].reshape(T, width)
+            return RowGroups(perm, live, width, n, live + c[T * width:].reshape(T, width))
+        return finish
 
     def pieces(self, lo: int, hi: int, dev):
         """(tree, node - lo, begin, end) of every PIECE-row slice of nodes [lo, hi)."""
@@ -474,8 +486,6 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     nodes = 1
     groups = RowGroups.root(T, n) if dev.type == "cuda" and _GROUPED else None
     for depth in range(max_depth + 1):
-        if depth > 0 and groups is not None:
-            groups = RowGroups.from_nodes(node_of, nodes, weight)
         faults.point("rdf.level", depth=depth, rank=ctx.rank)
         watchdog.heartbeat("rdf.level")
         if Fs < P:
@@ -529,6 +539,13 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
         vis_h = host[:, cut[3]:cut[4]].astype(np.int64)
         cat_h = host[:, cut[4]:cut[5]].reshape(split.cat_left.shape).astype(np.uint8) \
             if split.cat_left is not None else None
+        # next level's width from the split flags (padding slots of narrower trees are leaves),
+        # so its counting sort is queued on the device before the host builds this level's
+        # nodes below (the GPU sorts while Python allocates)
+        width_next = int(2 * (feat_h >= 0).sum(1).max()) if feat_h.size else 0
+        finish_groups = None
+        if groups is not None and width_next > 0:
+            finish_groups = RowGroups.launch_from_nodes(node_of, width_next, weight)
         next_nodes = 0
         new_level: List[List[Optional[TrainedNode]]] = []
         for t in range(T):
@@ -551,9 +568,12 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
             new_level.append(row)
             next_nodes = max(next_nodes, len(row))
         level_nodes = new_level
+        assert next_nodes == width_next, (next_nodes, width_next)
         nodes = next_nodes
         if nodes == 0:
             break
+        if groups is not None:
+            groups = finish_groups() if finish_groups is not None else None
     watchdog.get().end_heartbeats()
     return TrainedForest(roots, predictor_counts, classification)
 
