@@ -592,6 +592,7 @@ __global__ __launch_bounds__(1024) void kmeans_accumulate_lds_kernel(
 // cluster; counts come out of the scan exactly (no atomics).
 constexpr int SORT_BLOCKS = 512;
 constexpr int PIECE = 2048;
+constexpr int SORT_U = 8;
 
 __global__ __launch_bounds__(256) void km_block_hist(const int* __restrict__ assign, long long n,
                                                      int k, long long rpb,
@@ -601,7 +602,19 @@ __global__ __launch_bounds__(256) void km_block_hist(const int* __restrict__ ass
   __syncthreads();
   const long long r0 = (long long)blockIdx.x * rpb;
   const long long r1 = r0 + rpb < n ? r0 + rpb : n;
-  for (long long r = r0 + threadIdx.x; r < r1; r += 256) atomicAdd(h + assign[r], 1u);
+  // SORT_U coalesced key loads issued before their LDS atomics, so a wave keeps SORT_U loads in
+  // flight instead of one HBM round trip per key
+  for (long long rb = r0 + threadIdx.x; rb < r1; rb += 256ll * SORT_U) {
+    int c[SORT_U];
+#pragma unroll
+    for (int u = 0; u < SORT_U; ++u) {
+      const long long r = rb + 256ll * u;
+      c[u] = r < r1 ? assign[r] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < SORT_U; ++u)
+      if (c[u] >= 0) atomicAdd(h + c[u], 1u);
+  }
   __syncthreads();
   unsigned int* out = bh + (long long)blockIdx.x * k;
   for (int i = threadIdx.x; i < k; i += 256) out[i] = h[i];
@@ -679,16 +692,24 @@ __global__ __launch_bounds__(256) void km_scatter(const int* __restrict__ assign
                                                   const unsigned int* __restrict__ bh,
                                                   const long long* __restrict__ off,
                                                   int* __restrict__ perm) {
+  // cursors hold absolute output positions (off[c] + this block's start; n < 2^31), so the
+  // store needs no dependent global load of off[c]
   extern __shared__ unsigned int cur[];
   const unsigned int* start = bh + (long long)blockIdx.x * k;
-  for (int i = threadIdx.x; i < k; i += 256) cur[i] = start[i];
+  for (int i = threadIdx.x; i < k; i += 256) cur[i] = (unsigned int)off[i] + start[i];
   __syncthreads();
   const long long r0 = (long long)blockIdx.x * rpb;
   const long long r1 = r0 + rpb < n ? r0 + rpb : n;
-  for (long long r = r0 + threadIdx.x; r < r1; r += 256) {
-    const int c = assign[r];
-    const unsigned int slot = atomicAdd(cur + c, 1u);
-    perm[off[c] + slot] = (int)r;
+  for (long long rb = r0 + threadIdx.x; rb < r1; rb += 256ll * SORT_U) {
+    int c[SORT_U];
+#pragma unroll
+    for (int u = 0; u < SORT_U; ++u) {
+      const long long r = rb + 256ll * u;
+      c[u] = r < r1 ? assign[r] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < SORT_U; ++u)
+      if (c[u] >= 0) perm[atomicAdd(cur + c[u], 1u)] = (int)(rb + 256ll * u);
   }
 }
 

@@ -99,8 +99,9 @@ def runtime():
 
 def _load_kernels():
     import torch  # noqa: F401  (bind to torch's HIP runtime first)
-    path = _build.KERNELS_SO
-    if not os.path.exists(path):
+    # ORYX_KERNELS_SO: load another build of the kernel library (same-box A/B of kernel changes)
+    path = os.environ.get("ORYX_KERNELS_SO") or _build.KERNELS_SO
+    if path == _build.KERNELS_SO and not os.path.exists(path):
         _build.build_kernels()
     lib = ctypes.CDLL(path)
     _sig(lib, "oryx_kernels_version", c_i, [])

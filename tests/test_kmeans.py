@@ -486,3 +486,28 @@ def test_lloyd_step_matches_cpu(cuda):
     ref = torch.zeros(6, x.shape[1], dtype=torch.float64).index_add_(0, idx, x.double())
     ref /= torch.bincount(idx, minlength=6).clamp_min(1)[:, None]
     assert torch.allclose(new_g.cpu().double(), ref, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k", [(1, 1), (1000, 3), (300_001, 1000), (2_000_003, 5121)])
+def test_counting_sort_kernel_groups_every_row(cuda, n, k):
+    """oryx_counting_sort (used by the k-means sorted accumulate and the RDF level grouping)
+    against torch: counts equal bincount, every row appears once, each group holds its key."""
+    from oryx_amd import native
+    lib = native.require_kernels()
+    g = torch.Generator().manual_seed(n + k)
+    keys = (k * torch.rand(n, generator=g).pow(2)).to(torch.int32).clamp_(0, k - 1)
+    keys_d = keys.to(cuda)
+    perm = torch.empty(n, dtype=torch.int32, device=cuda)
+    counts = torch.empty(k, dtype=torch.int64, device=cuda)
+    ws = torch.empty(int(lib.oryx_kmeans_sorted_ws_bytes(n, k)), dtype=torch.uint8, device=cuda)
+    native.check(lib.oryx_counting_sort(keys_d.data_ptr(), n, k, perm.data_ptr(),
+                                        counts.data_ptr(), ws.data_ptr(),
+                                        native.stream_ptr(cuda)), "oryx_counting_sort")
+    torch.cuda.synchronize()
+    ref_counts = torch.bincount(keys.long(), minlength=k)
+    assert torch.equal(counts.cpu(), ref_counts)
+    p = perm.cpu().long()
+    assert torch.equal(torch.sort(p).values, torch.arange(n))
+    grouped = keys.long()[p]
+    assert torch.equal(grouped, torch.repeat_interleave(torch.arange(k), ref_counts))
