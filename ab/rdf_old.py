@@ -485,50 +485,14 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     predictor_counts = np.zeros(P, dtype=np.float64)
     nodes = 1
     groups = RowGroups.root(T, n) if dev.type == "cuda" and _GROUPED else None
-
-    def sample_feats(width: int) -> torch.Tensor:
-        # Fs smallest of P uniforms per node, in order: the same subsets as a full argsort
-        # prefix, at a third of the host time
-        if Fs < P:
-            f = torch.topk(torch.rand((T, width, P), generator=g), Fs, dim=-1, largest=False,
-                           sorted=True).indices
-        else:
-            f = torch.arange(P).expand(T, width, P)
-        return f.to(torch.int32).to(dev).contiguous()
-
-    def build_level(level_nodes, feat_h, bin_h, tot_h, vis_h, cat_h, width_next):
-        new_level: List[List[Optional[TrainedNode]]] = []
-        next_nodes = 0
-        for t in range(T):
-            row: List[Optional[TrainedNode]] = []
-            for slot, node in enumerate(level_nodes[t]):
-                if node is None:
-                    continue
-                node.count = int(vis_h[t, slot])
-                node.stats = tot_h[t, slot]
-                f = int(feat_h[t, slot])
-                if f >= 0:
-                    node.feature = f
-                    node.bin = int(bin_h[t, slot])
-                    if node.bin < 0:
-                        node.cat_left = np.nonzero(cat_h[t, slot])[0]
-                    node.left = TrainedNode(node.id + "-")
-                    node.right = TrainedNode(node.id + "+")
-                    row.extend([node.left, node.right])
-                    predictor_counts[f] += node.count
-            new_level.append(row)
-            next_nodes = max(next_nodes, len(row))
-        assert next_nodes == width_next, (next_nodes, width_next)
-        return new_level
-
-    # The host tree of level d is built after level d + 1's device work is queued (the
-    # GPU builds histograms while Python allocates nodes); next-level feature subsets are
-    # drawn while the device runs the level's counting sort.
-    pending = None
-    feats = sample_feats(nodes)
     for depth in range(max_depth + 1):
         faults.point("rdf.level", depth=depth, rank=ctx.rank)
         watchdog.heartbeat("rdf.level")
+        if Fs < P:
+            feats = torch.argsort(torch.rand((T, nodes, P), generator=g), dim=-1)[..., :Fs]
+        else:
+            feats = torch.arange(P).expand(T, nodes, P)
+        feats = feats.to(torch.int32).to(dev).contiguous()
         # histogram in node chunks that fit the budget
         chunk = max(1, _HIST_BUDGET // max(1, T * Fs * B * S))
         splits = []
@@ -561,9 +525,6 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
             visits = _route(data, node_of, nodes, split, child_base, B)
         if ctx.is_distributed:
             dist.all_reduce_sum(visits, ctx)
-        if pending is not None:
-            level_nodes = build_level(*pending)
-            pending = None
         # one device -> host transfer (one sync) for everything the host tree needs
         parts = [split.feat.double().reshape(T, -1), split.bin.double().reshape(T, -1),
                  split.totals.double().reshape(T, -1), visits.double().reshape(T, -1)]
@@ -579,20 +540,40 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
         cat_h = host[:, cut[4]:cut[5]].reshape(split.cat_left.shape).astype(np.uint8) \
             if split.cat_left is not None else None
         # next level's width from the split flags (padding slots of narrower trees are leaves),
-        # so its counting sort is queued on the device before anything else on the host
+        # so its counting sort is queued on the device before the host builds this level's
+        # nodes below (the GPU sorts while Python allocates)
         width_next = int(2 * (feat_h >= 0).sum(1).max()) if feat_h.size else 0
         finish_groups = None
         if groups is not None and width_next > 0:
             finish_groups = RowGroups.launch_from_nodes(node_of, width_next, weight)
-        pending = (level_nodes, feat_h, bin_h, tot_h, vis_h, cat_h, width_next)
-        nodes = width_next
+        next_nodes = 0
+        new_level: List[List[Optional[TrainedNode]]] = []
+        for t in range(T):
+            row: List[Optional[TrainedNode]] = []
+            for slot, node in enumerate(level_nodes[t]):
+                if node is None:
+                    continue
+                node.count = int(vis_h[t, slot])
+                node.stats = tot_h[t, slot]
+                f = int(feat_h[t, slot])
+                if f >= 0:
+                    node.feature = f
+                    node.bin = int(bin_h[t, slot])
+                    if node.bin < 0:
+                        node.cat_left = np.nonzero(cat_h[t, slot])[0]
+                    node.left = TrainedNode(node.id + "-")
+                    node.right = TrainedNode(node.id + "+")
+                    row.extend([node.left, node.right])
+                    predictor_counts[f] += node.count
+            new_level.append(row)
+            next_nodes = max(next_nodes, len(row))
+        level_nodes = new_level
+        assert next_nodes == width_next, (next_nodes, width_next)
+        nodes = next_nodes
         if nodes == 0:
             break
-        feats = sample_feats(nodes)
         if groups is not None:
             groups = finish_groups() if finish_groups is not None else None
-    if pending is not None:
-        build_level(*pending)
     watchdog.get().end_heartbeats()
     return TrainedForest(roots, predictor_counts, classification)
 
