@@ -51,31 +51,48 @@ def _gen_ratings(n_local_users: int, n_items: int, nnz: int, rank: int, seed: in
     return users, items, strength
 
 
+# BASELINE.json configs this bench covers (weak scaling: per-GPU shares of the named totals)
+PRESETS = {
+    # "ALS rank=64 bf16 on 25M synthetic ratings, 1 MI355X"
+    "c2": dict(rank_k=64, ratings_per_gpu=25_000_000, users_per_gpu=162_541, items=59_047),
+    # "ALS rank=128 on 1B synthetic ratings, 8xMI355X": 125M ratings of 1.25M users per GPU
+    # over a shared 500k-item catalogue (1B ratings / 10M users at 8 GPUs)
+    "c3": dict(rank_k=128, ratings_per_gpu=125_000_000, users_per_gpu=1_250_000,
+               items=500_000),
+}
+
+
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--rank-k", type=int, default=64, help="ALS rank (features)")
-    ap.add_argument("--ratings-per-gpu", type=int, default=25_000_000)
-    ap.add_argument("--users-per-gpu", type=int, default=162_541)
-    ap.add_argument("--items", type=int, default=59_047)
+    ap.add_argument("--preset", choices=sorted(PRESETS), default="c2")
+    ap.add_argument("--rank-k", type=int, default=None, help="ALS rank (features)")
+    ap.add_argument("--ratings-per-gpu", type=int, default=None)
+    ap.add_argument("--users-per-gpu", type=int, default=None)
+    ap.add_argument("--items", type=int, default=None)
     ap.add_argument("--implicit", type=int, default=1)
     ap.add_argument("--speed-events", type=int, default=10_000)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--device", default="auto")
     args = ap.parse_args(argv)
+    for key, val in PRESETS[args.preset].items():
+        if getattr(args, key) is None:
+            setattr(args, key, val)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oryx_amd.parallel import launch
+    rc = launch.relaunch_if_needed(os.path.abspath(__file__), argv, args.gpus)
+    if rc is not None:
+        return rc
     from oryx_amd.parallel import dist
     from oryx_amd.models.als.trainer import ALSTrainer
     from oryx_amd.ops import als as als_ops
     from oryx_amd.utils import mathx
 
     ctx = dist.init_from_env(device=args.device)
-    if ctx.world_size != args.gpus and ctx.is_main:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, ctx.world_size),
-              file=sys.stderr)
     dev = ctx.device
     W = ctx.world_size
     n_users = args.users_per_gpu * W
@@ -143,6 +160,11 @@ def main(argv=None) -> int:
             times.append((time.perf_counter() - t1) * 1e3)
         speed_ms = min(times[1:])
 
+    info = dist.run_info(ctx)
+    peak = torch.tensor([float(torch.cuda.max_memory_allocated(dev)) if dev.type == "cuda"
+                         else 0.0], dtype=torch.float64, device=dev)
+    if ctx.is_distributed:
+        torch.distributed.all_reduce(peak, op=torch.distributed.ReduceOp.MAX)
     if ctx.is_main:
         rec = {
             "metric": "ALS batch-layer ratings/sec + speed-layer model-update latency, 1/2/4/8 MI355X",
@@ -169,7 +191,12 @@ def main(argv=None) -> int:
                 "users": n_users,
                 "items": args.items,
                 "step": "1 ALS iteration (items+users half-steps)",
+                "preset": args.preset,
             },
+            "world_size": info["world_size"],
+            "backend": info["backend"],
+            "rank_devices": [r.get("current_device", r["device"]) for r in info["ranks"]],
+            "peak_hbm_gib_per_rank": float(peak.item()) / 2**30,
             "speed_layer_update_ms": speed_ms,
             "speed_layer_events": args.speed_events,
             "solve_failures": trainer.failures,

@@ -29,6 +29,7 @@ import torch
 
 
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -41,6 +42,10 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oryx_amd.parallel import launch
+    rc = launch.relaunch_if_needed(os.path.abspath(__file__), argv, args.gpus)
+    if rc is not None:
+        return rc
     from oryx_amd.parallel import dist
     from oryx_amd.ops import kmeans as km
 
@@ -92,8 +97,11 @@ def main(argv=None) -> int:
     total_points = n * W * args.steps
     ms = elapsed / args.steps * 1e3
     total_counts = int(counts.sum().item())
+    info = dist.run_info(ctx)
     if ctx.is_main:
         print(json.dumps({
+            "world_size": info["world_size"], "backend": info["backend"],
+            "rank_devices": [r.get("current_device", r["device"]) for r in info["ranks"]],
             "metric": "k-means Lloyd-iteration points/sec (batch layer), 1/2/4/8 MI355X",
             "value": total_points / elapsed, "unit": "points/s", "n_gpus": W,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,

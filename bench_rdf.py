@@ -63,6 +63,7 @@ def _speed_latency(trained, data, schema_cfg, events: int, P: int, dev) -> float
 
 
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -78,6 +79,10 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oryx_amd.parallel import launch
+    rc = launch.relaunch_if_needed(os.path.abspath(__file__), argv, args.gpus)
+    if rc is not None:
+        return rc
     from oryx_amd.parallel import dist
     from oryx_amd.ops import rdf as rdf_ops
     from oryx_amd.utils import config as cfg
@@ -128,6 +133,7 @@ def main(argv=None) -> int:
         return 1 + (count_nodes(nd.left) + count_nodes(nd.right) if nd.feature >= 0 else 0)
 
     speed_ms = None
+    info = dist.run_info(ctx)
     if ctx.is_main:
         names = ",".join('"%d"' % i for i in range(P + 1))
         schema_cfg = cfg.overlay_on({
@@ -149,6 +155,8 @@ def main(argv=None) -> int:
                 "parallelism": "dp%d (example shards, RCCL all-reduce of level histograms)" % W,
                 "examples_per_gpu": n, "features": P,
                 "step": "1 full forest (all levels of all trees)"},
+            "world_size": info["world_size"], "backend": info["backend"],
+            "rank_devices": [r.get("current_device", r["device"]) for r in info["ranks"]],
             "nodes": sum(count_nodes(r) for r in trained.roots),
             "speed_layer_update_ms": speed_ms, "speed_layer_events": args.speed_events,
         }), flush=True)

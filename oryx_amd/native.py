@@ -24,6 +24,10 @@ _runtime = None
 _kernels = None
 _kernels_error = None
 
+# must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
+# kernel entry point's signature or semantics change
+KERNELS_ABI_VERSION = 4
+
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
 c_ll = ctypes.c_longlong
@@ -101,10 +105,17 @@ def _load_kernels():
     import torch  # noqa: F401  (bind to torch's HIP runtime first)
     # ORYX_KERNELS_SO: load another build of the kernel library (same-box A/B of kernel changes)
     path = os.environ.get("ORYX_KERNELS_SO") or _build.KERNELS_SO
-    if path == _build.KERNELS_SO and not os.path.exists(path):
+    if path == _build.KERNELS_SO:
+        # incremental: a no-op when the library is newer than every kernel source, so a
+        # library left over from before a kernel change is never loaded silently
         _build.build_kernels()
     lib = ctypes.CDLL(path)
     _sig(lib, "oryx_kernels_version", c_i, [])
+    got = lib.oryx_kernels_version()
+    if got != KERNELS_ABI_VERSION:
+        raise RuntimeError("%s has kernel ABI version %d, this package expects %d (stale "
+                           "build: rebuild with python -m oryx_amd._build --force)"
+                           % (path, got, KERNELS_ABI_VERSION))
     # ORYX_ALS_VARIANT selects the KP<=64 solve kernel for A/B runs (csrc/kernels/als.hip:
     # 2 = panel Cholesky + 3-deep gather ring (default), 0 = panel + 1-deep, 1 = register)
     _sig(lib, "oryx_als_set_variant", c_i, [c_i])

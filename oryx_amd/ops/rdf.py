@@ -165,6 +165,8 @@ def _choose_splits(hist: torch.Tensor, feats: torch.Tensor, data: BinnedData, ki
                    force_leaf: bool) -> LevelSplits:
     T, N, Fs, B, S = hist.shape
     dev = hist.device
+    if kind == "variance":
+        hist = hist.double()        # cumsum / E[y^2] - mean^2 in fp64 (MLlib's aggregator)
     totals = hist[:, :, 0].sum(2)                                   # [T, N, S]
     parent_imp, w = _impurity(totals, kind)                         # [T, N]
     if B < 2:
@@ -466,7 +468,18 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     g = torch.Generator(device="cpu")
     g.manual_seed(seed & ((1 << 62) - 1))
     label = target.to(dev, torch.int32).contiguous() if classification else None
-    y = None if classification else target.to(dev, torch.float32).contiguous()
+    y = None
+    y_shift = 0.0
+    if not classification:
+        # regression statistics (sum w, sum wy, sum wy^2) are accumulated in fp32 on the
+        # device: centre the targets on their global mean first so that E[y^2] - mean^2 does
+        # not cancel for targets with a large offset (the split search then runs in fp64)
+        yd = target.to(dev, torch.float64)
+        s = torch.stack([yd.sum(), torch.tensor(float(n), dtype=torch.float64, device=dev)])
+        if ctx.is_distributed:
+            dist.all_reduce_sum(s, ctx)
+        y_shift = float(s[0] / s[1].clamp_min(1.0))
+        y = (yd - y_shift).to(torch.float32).contiguous()
     if T > 1:
         gd = torch.Generator(device=dev)
         gd.manual_seed((seed * 31 + ctx.rank + 7) & ((1 << 62) - 1))
@@ -575,6 +588,11 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
         feat_h = host[:, cut[0]:cut[1]].astype(np.int64)
         bin_h = host[:, cut[1]:cut[2]].astype(np.int64)
         tot_h = host[:, cut[2]:cut[3]].reshape(split.totals.shape)
+        if y_shift:
+            # un-centre the node statistics: sum w(y'+m)^2 and sum w(y'+m)
+            w_, s1 = tot_h[..., 0].copy(), tot_h[..., 1].copy()
+            tot_h[..., 2] += 2.0 * y_shift * s1 + y_shift * y_shift * w_
+            tot_h[..., 1] += y_shift * w_
         vis_h = host[:, cut[3]:cut[4]].astype(np.int64)
         cat_h = host[:, cut[4]:cut[5]].reshape(split.cat_left.shape).astype(np.uint8) \
             if split.cat_left is not None else None

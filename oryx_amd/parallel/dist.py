@@ -26,7 +26,7 @@ from . import watchdog
 
 __all__ = ["DistContext", "init_from_env", "get_context", "shard_range", "padded_shard_size",
            "all_gather_rows", "all_gather_rows_async", "all_reduce_sum", "broadcast_object",
-           "barrier"]
+           "barrier", "run_info"]
 
 
 @dataclass
@@ -38,10 +38,13 @@ class DistContext:
     backend: Optional[str] = None
     group: Optional[object] = None
     control: Optional[object] = None
+    # ORYX_FORCE_COLLECTIVES=1: a world of one still initialises the process group and runs
+    # every collective (exercises the RCCL code paths on a single GPU)
+    forced: bool = False
 
     @property
     def is_distributed(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.forced
 
     @property
     def is_main(self) -> bool:
@@ -74,10 +77,13 @@ def init_from_env(device: Optional[str] = None, backend: Optional[str] = None,
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     ctx = DistContext(rank, world, local_rank, dev)
-    if world > 1:
+    ctx.forced = world == 1 and os.environ.get("ORYX_FORCE_COLLECTIVES") == "1"
+    if world > 1 or ctx.forced:
         if backend is None:
             backend = "nccl" if dev.type == "cuda" else "gloo"
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if ctx.forced:
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         if not tdist.is_initialized():
             kwargs = dict(backend=backend, rank=rank, world_size=world,
                           timeout=datetime.timedelta(seconds=timeout_s))
@@ -100,6 +106,29 @@ def init_from_env(device: Optional[str] = None, backend: Optional[str] = None,
                                       timeout=datetime.timedelta(days=30))
     _context = ctx
     return ctx
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_info(ctx: DistContext) -> dict:
+    """World size, backend and every rank's device (gathered over the control group); the
+    bench JSON carries it so a scaling point can be checked for its actual rank layout."""
+    me = {"rank": ctx.rank, "device": str(ctx.device)}
+    if ctx.device.type == "cuda":
+        me["current_device"] = torch.cuda.current_device()
+    if ctx.is_distributed and tdist.is_initialized():
+        allv = [None] * tdist.get_world_size()
+        tdist.all_gather_object(allv, me, group=ctx.control)
+        ws = tdist.get_world_size()
+        backend = tdist.get_backend()
+    else:
+        allv, ws, backend = [me], 1, None
+    return {"world_size": ws, "backend": backend, "ranks": allv}
 
 
 def get_context() -> DistContext:

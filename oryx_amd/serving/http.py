@@ -380,24 +380,34 @@ class Router:
 # ---------------------------------------------------------------- auth
 
 class DigestAuth:
-    """HTTP DIGEST authentication (RFC 2617, MD5, qop=auth) against one user/password."""
+    """HTTP DIGEST authentication (RFC 2617, MD5, qop=auth) against one user/password.
 
-    def __init__(self, user: str, password: str, realm: str = "Oryx"):
+    The response is bound to the request target (the ``uri`` parameter must equal it), nonces
+    expire after ``nonce_ttl_s`` (answered with ``stale=true`` so clients retry without
+    prompting) and each nonce's ``nc`` must strictly increase, so a captured Authorization
+    header can neither be replayed nor pointed at another endpoint.
+    """
+
+    def __init__(self, user: str, password: str, realm: str = "Oryx",
+                 nonce_ttl_s: float = 300.0):
         self.user = user
         self.password = password
         self.realm = realm
-        self._nonces: Dict[str, float] = {}
+        self.nonce_ttl_s = float(nonce_ttl_s)
+        self._nonces: Dict[str, list] = {}      # nonce -> [issued_at, last nc]
         self._lock = threading.Lock()
 
-    def challenge(self) -> str:
+    def challenge(self, stale: bool = False) -> str:
         nonce = secrets.token_hex(16)
+        now = time.time()
         with self._lock:
-            self._nonces[nonce] = time.time()
-            if len(self._nonces) > 10000:
-                cutoff = time.time() - 600
-                self._nonces = {n: t for n, t in self._nonces.items() if t > cutoff}
-        return 'Digest realm="%s", qop="auth", nonce="%s", opaque="%s"' % (
-            self.realm, nonce, hashlib.md5(self.realm.encode()).hexdigest())
+            self._nonces[nonce] = [now, 0]
+            if len(self._nonces) > 1024:
+                cutoff = now - self.nonce_ttl_s
+                self._nonces = {n: v for n, v in self._nonces.items() if v[0] > cutoff}
+        return 'Digest realm="%s", qop="auth", nonce="%s", opaque="%s"%s' % (
+            self.realm, nonce, hashlib.md5(self.realm.encode()).hexdigest(),
+            ", stale=true" if stale else "")
 
     @staticmethod
     def _parse(header: str) -> Dict[str, str]:
@@ -406,24 +416,42 @@ class DigestAuth:
             out[m.group(1).lower()] = m.group(2) if m.group(2) is not None else m.group(3)
         return out
 
-    def check(self, method: str, header: Optional[str]) -> bool:
+    def verify(self, method: str, target: str, header: Optional[str]) -> str:
+        """``"ok"``, ``"stale"`` (right credentials, expired nonce) or ``"denied"``."""
         if not header or not header.lower().startswith("digest "):
-            return False
+            return "denied"
         p = self._parse(header[7:])
         if p.get("username") != self.user or p.get("realm") != self.realm:
-            return False
-        with self._lock:
-            if p.get("nonce") not in self._nonces:
-                return False
+            return "denied"
+        if p.get("uri", "") != target:
+            return "denied"
         ha1 = hashlib.md5(("%s:%s:%s" % (self.user, self.realm, self.password)).encode()).hexdigest()
         ha2 = hashlib.md5(("%s:%s" % (method, p.get("uri", ""))).encode()).hexdigest()
-        if p.get("qop"):
-            expected = hashlib.md5(("%s:%s:%s:%s:%s:%s" % (
-                ha1, p.get("nonce"), p.get("nc"), p.get("cnonce"), p.get("qop"), ha2)).encode()
-            ).hexdigest()
-        else:
-            expected = hashlib.md5(("%s:%s:%s" % (ha1, p.get("nonce"), ha2)).encode()).hexdigest()
-        return secrets.compare_digest(expected, p.get("response", ""))
+        if p.get("qop") != "auth":
+            return "denied"
+        expected = hashlib.md5(("%s:%s:%s:%s:%s:%s" % (
+            ha1, p.get("nonce"), p.get("nc"), p.get("cnonce"), p.get("qop"), ha2)).encode()
+        ).hexdigest()
+        if not secrets.compare_digest(expected, p.get("response", "")):
+            return "denied"
+        try:
+            nc = int(p.get("nc", ""), 16)
+        except ValueError:
+            return "denied"
+        with self._lock:
+            entry = self._nonces.get(p.get("nonce"))
+            if entry is None:
+                return "stale"
+            if time.time() - entry[0] > self.nonce_ttl_s:
+                del self._nonces[p.get("nonce")]
+                return "stale"
+            if nc <= entry[1]:
+                return "denied"                  # replayed (or reordered) request
+            entry[1] = nc
+        return "ok"
+
+    def check(self, method: str, header: Optional[str], target: str = "") -> bool:
+        return self.verify(method, target, header) == "ok"
 
 
 # ---------------------------------------------------------------- server
@@ -453,9 +481,11 @@ class _Handler(http.server.BaseHTTPRequestHandler):
         query = urllib.parse.parse_qs(parsed.query, keep_blank_values=True)
         headers = {k.lower(): v for k, v in self.headers.items()}
         req = Request(self.command, parsed.path, query, headers, body, srv.app_context)
-        if srv.auth is not None and not srv.auth.check(self.command, headers.get("authorization")):
+        verdict = "ok" if srv.auth is None else srv.auth.verify(
+            self.command, self.path, headers.get("authorization"))
+        if verdict != "ok":
             resp = Response(401, b"401 Unauthorized\n", TEXT,
-                            {"WWW-Authenticate": srv.auth.challenge()})
+                            {"WWW-Authenticate": srv.auth.challenge(stale=verdict == "stale")})
         else:
             resp = srv.router.dispatch(req)
         payload = resp.body

@@ -38,6 +38,7 @@ def _check(rec, n):
     assert abs(rec["value"] - rec["config"]["global_batch"] / (rec["ms_per_step"] * 1e-3)) \
         <= 1e-6 * rec["value"]
     assert rec["config"]["global_batch"] == 20000 * n
+    assert rec["world_size"] == n and len(rec["rank_devices"]) == n
 
 
 @pytest.mark.timeout(600)
@@ -61,3 +62,39 @@ def test_bench_two_ranks_gloo():
     recs = _json_lines(out.stdout)
     assert len(recs) == 1                       # rank 0 only
     _check(recs[0], 2)
+
+
+@pytest.mark.timeout(600)
+def test_bench_self_launches_ranks():
+    """``python bench.py --gpus 2`` with no external launcher starts 2 ranks itself."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL,
+                         capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    recs = _json_lines(out.stdout)
+    assert len(recs) == 1
+    _check(recs[0], 2)
+    assert recs[0]["backend"] == "gloo"
+
+
+def test_bench_rejects_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL,
+                         capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert out.returncode == 2
+    assert "WORLD_SIZE" in out.stderr
+
+
+@pytest.mark.timeout(600)
+def test_bench_forced_collectives_world_one():
+    """World of one with ORYX_FORCE_COLLECTIVES=1 runs every collective code path."""
+    env = dict(os.environ, ORYX_FORCE_COLLECTIVES="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + SMALL,
+                         capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = _json_lines(out.stdout)[0]
+    _check(rec, 1)
+    assert rec["backend"] == "gloo"

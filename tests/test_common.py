@@ -469,3 +469,11 @@ def test_io_utils(tmp_path):
     assert not ioutils.exists(str(tmp_path / "a"))
     port = ioutils.choose_free_port()
     assert 0 < port < 65536
+
+
+def test_kernel_abi_version_matches_source():
+    import re
+    from oryx_amd import native, _build
+    src = open(os.path.join(_build.CSRC, "kernels", "als.hip")).read()
+    m = re.search(r"int oryx_kernels_version\(\) \{ return (\d+); \}", src)
+    assert m and int(m.group(1)) == native.KERNELS_ABI_VERSION

@@ -505,3 +505,31 @@ def test_csv_block_fast_path_matches_general_parse():
     assert parse_csv_block(['1,"x",2,yes'], schema, enc) is None
     assert parse_csv_block(['[1,"x",2,"yes"]'], schema, enc) is None
     assert parse_csv_block(["1,z,2,yes"], schema, enc) is None
+
+
+def test_regression_split_with_large_target_offset():
+    """Targets 1e4 + N(0,1) with a step of 1 at x0 = 0.3: the root split must be the one a
+    float64 host search over the same bins picks (no E[y^2] - mean^2 cancellation)."""
+    g = np.random.default_rng(11)
+    n = 20000
+    X = g.uniform(-1, 1, (n, 3))
+    y = 1e4 + g.standard_normal(n) + (X[:, 0] > 0.3) * 1.0
+    data = rdf_ops.bin_features(X, [False] * 3, [0] * 3, 32, torch.device("cpu"))
+    f = rdf_ops.train_forest(data, torch.from_numpy(y), 0, 1, 1, "variance", seed=1)
+    root = f.roots[0]
+    # brute-force float64 variance-reduction search over the bins
+    Xb = data.Xb.numpy().astype(np.int64)
+    best = (-np.inf, None, None)
+    tot_var = y.var() * n
+    for j in range(3):
+        for b in range(data.B - 1):
+            left = Xb[:, j] <= b
+            nl = left.sum()
+            if nl == 0 or nl == n:
+                continue
+            gain = tot_var - (y[left].var() * nl + y[~left].var() * (n - nl))
+            if gain > best[0]:
+                best = (gain, j, b)
+    assert (root.feature, root.bin) == (best[1], best[2])
+    # leaf statistics are reported un-centred
+    assert abs(root.stats[1] / root.stats[0] - y.mean()) < 1e-6

@@ -191,3 +191,36 @@ def test_https_and_digest_auth(tmp_path):
             urllib.request.urlopen("http://127.0.0.1:%d/ready" % lay.actual_port, timeout=5)
     finally:
         lay.close()
+
+
+def _digest_header(auth, method, uri, nonce, nc, password="pass", user="oryx"):
+    import hashlib
+    ha1 = hashlib.md5(("%s:%s:%s" % (user, auth.realm, password)).encode()).hexdigest()
+    ha2 = hashlib.md5(("%s:%s" % (method, uri)).encode()).hexdigest()
+    ncs = "%08x" % nc
+    resp = hashlib.md5(("%s:%s:%s:%s:%s:%s" % (ha1, nonce, ncs, "abc", "auth", ha2)).encode()
+                       ).hexdigest()
+    return ('Digest username="%s", realm="%s", nonce="%s", uri="%s", qop=auth, nc=%s, '
+            'cnonce="abc", response="%s"' % (user, auth.realm, nonce, uri, ncs, resp))
+
+
+def test_digest_auth_replay_uri_and_expiry():
+    import re as _re
+    from oryx_amd.serving.http import DigestAuth
+    auth = DigestAuth("oryx", "pass", nonce_ttl_s=60)
+    nonce = _re.search(r'nonce="([0-9a-f]+)"', auth.challenge()).group(1)
+    h1 = _digest_header(auth, "GET", "/recommend/U0", nonce, 1)
+    assert auth.verify("GET", "/recommend/U0", h1) == "ok"
+    # the same header again (captured and replayed): nc did not increase
+    assert auth.verify("GET", "/recommend/U0", h1) == "denied"
+    # a valid header pointed at another endpoint
+    h2 = _digest_header(auth, "POST", "/ingest", nonce, 2)
+    assert auth.verify("POST", "/pref/U0/I0", h2) == "denied"
+    assert auth.verify("POST", "/ingest", h2) == "ok"
+    # wrong password
+    assert auth.verify("GET", "/x", _digest_header(auth, "GET", "/x", nonce, 9, "bad")) == "denied"
+    # expired nonce: stale (client re-authenticates with a fresh nonce)
+    auth._nonces[nonce][0] -= 3600
+    h3 = _digest_header(auth, "GET", "/recommend/U0", nonce, 3)
+    assert auth.verify("GET", "/recommend/U0", h3) == "stale"
+    assert "stale=true" in auth.challenge(stale=True)
