@@ -54,11 +54,13 @@ def _gen_ratings(n_local_users: int, n_items: int, nnz: int, rank: int, seed: in
 # BASELINE.json configs this bench covers (weak scaling: per-GPU shares of the named totals)
 PRESETS = {
     # "ALS rank=64 bf16 on 25M synthetic ratings, 1 MI355X"
-    "c2": dict(rank_k=64, ratings_per_gpu=25_000_000, users_per_gpu=162_541, items=59_047),
+    "c2": dict(rank_k=64, ratings_per_gpu=25_000_000, users_per_gpu=162_541, items=59_047,
+               precision="bf16"),
     # "ALS rank=128 on 1B synthetic ratings, 8xMI355X": 125M ratings of 1.25M users per GPU
     # over a shared 500k-item catalogue (1B ratings / 10M users at 8 GPUs)
+    # (no dtype named: MLlib's fp32 factors, carried as bf16 hi|lo pairs)
     "c3": dict(rank_k=128, ratings_per_gpu=125_000_000, users_per_gpu=1_250_000,
-               items=500_000),
+               items=500_000, precision="fp32"),
 }
 
 
@@ -73,6 +75,8 @@ def main(argv=None) -> int:
     ap.add_argument("--ratings-per-gpu", type=int, default=None)
     ap.add_argument("--users-per-gpu", type=int, default=None)
     ap.add_argument("--items", type=int, default=None)
+    ap.add_argument("--precision", choices=["bf16", "fp32"], default=None,
+                    help="factor operand precision (fp32 = bf16 hi|lo split operands)")
     ap.add_argument("--implicit", type=int, default=1)
     ap.add_argument("--speed-events", type=int, default=10_000)
     ap.add_argument("--seed", type=int, default=1234)
@@ -99,7 +103,7 @@ def main(argv=None) -> int:
     users, items, strength = _gen_ratings(args.users_per_gpu, args.items, args.ratings_per_gpu,
                                           ctx.rank, args.seed, dev)
     trainer = ALSTrainer(args.rank_k, lam=0.001, alpha=1.0, implicit=bool(args.implicit),
-                         ctx=ctx, seed=args.seed)
+                         ctx=ctx, seed=args.seed, precision=args.precision)
     trainer.prepare(users, items, strength, n_users, args.items)
     del users, items, strength
     trainer.init_factors()
@@ -177,7 +181,7 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": args.precision,
             "data": "synthetic (power-law users x items, unique pairs, strengths 0.5..5), "
                     "random-init unit-Gaussian factors",
             "config": {

@@ -3,16 +3,19 @@
 100M points, 8xMI355X (MFMA distance + centroid all-reduce)").
 
 ``python bench_kmeans.py --gpus N --steps K --warmup W`` (N > 1: one rank per GPU under
-``torch.distributed.run``).  A *step* is one Lloyd iteration of the batch layer's k-means
-trainer (``oryx_amd.ops.kmeans.lloyd_step``, the loop MLlib runs for the reference at
-``[mllib]/kmeans/KMeansUpdate.java:116-117``): the fused bf16-MFMA distance + argmin kernel
-over every point against all K centers, the fp32 centroid accumulation kernel, ONE RCCL
-all-reduce of the K x (d + 1) sums/counts, and the center move.
+``torch.distributed.run``; without an external launcher the script starts them itself).  A
+*step* is one Lloyd iteration of the batch layer's k-means trainer
+(``oryx_amd.ops.kmeans.lloyd_step``, the loop MLlib runs for the reference at
+``[mllib]/kmeans/KMeansUpdate.java:116-117``): the fused MFMA distance + argmin kernel over
+every point against all K centers (``--precision fp32``, the default since the BASELINE config
+names no reduced dtype: the certified kernel whose ambiguous points are re-decided in fp32,
+i.e. the fp32 argmin; ``bf16``: the plain bf16 argmin), the fp32 centroid accumulation
+kernel, ONE RCCL all-reduce of the K x (d + 1) sums/counts, and the center move.
 
 Weak scaling: every rank owns 100M / 8 = 12.5M points (the 8-GPU config's per-GPU share), so
 N = 8 is exactly the BASELINE config.  Data: a synthetic Gaussian mixture (1000 true centers,
-d = 256, fp32 resident in HBM); centers start from a random sample (initialisation is not
-part of the step).  The reference publishes no batch-layer numbers, so
+d = 256, fp32 resident in HBM); centers start from k-means|| (the app's default init, timed
+separately as ``init_ms``; ``--init sample`` starts from a random sample instead).  The reference publishes no batch-layer numbers, so
 ``vs_baseline`` is null.  Prints ONE JSON line (rank 0): ``value`` = points processed per
 second over all ranks; ``tflops`` = the distance-GEMM work rate (2 * n * K * d per point set).
 """
@@ -39,6 +42,8 @@ def main(argv=None) -> int:
     ap.add_argument("--k", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--init", choices=["k-means||", "sample"], default="k-means||")
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -65,11 +70,23 @@ def main(argv=None) -> int:
         lab = torch.randint(0, k, (hi - lo,), generator=g, device=dev)
         x[lo:hi] = true_c[lab] + torch.randn((hi - lo, d), generator=g, device=dev)
     pts = km.PointSet(x)
-    # initial centers: a random sample of rank 0's points, broadcast
-    idx = torch.randperm(n, generator=g, device=dev)[:k]
-    centers = x[idx].clone()
-    if ctx.is_distributed:
-        torch.distributed.broadcast(centers, src=0)
+    init_ms = None
+    if args.init == "sample":
+        # initial centers: a random sample of rank 0's points, broadcast
+        idx = torch.randperm(n, generator=g, device=dev)[:k]
+        centers = x[idx].clone()
+        if ctx.is_distributed:
+            torch.distributed.broadcast(centers, src=0)
+    else:
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        dist.barrier(ctx)
+        t_init = time.perf_counter()
+        centers = km.init_centers(pts, k, "k-means||", seed=args.seed, ctx=ctx,
+                                  precision=args.precision)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        init_ms = (time.perf_counter() - t_init) * 1e3
     ws = None
     if pts.xb is not None:
         ws = (torch.empty(n, dtype=torch.int32, device=dev),
@@ -82,11 +99,12 @@ def main(argv=None) -> int:
 
     empties = 0
     for _ in range(args.warmup):
-        centers, counts, _, ne = km.lloyd_step(pts, centers, ctx, ws)
+        centers, counts, _, ne = km.lloyd_step(pts, centers, ctx, ws, args.precision)
     sync()
+    km.CERT_STATS.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        centers, counts, _, ne = km.lloyd_step(pts, centers, ctx, ws)
+        centers, counts, _, ne = km.lloyd_step(pts, centers, ctx, ws, args.precision)
         empties += ne
     sync()
     elapsed = time.perf_counter() - t0
@@ -97,6 +115,8 @@ def main(argv=None) -> int:
     total_points = n * W * args.steps
     ms = elapsed / args.steps * 1e3
     total_counts = int(counts.sum().item())
+    st = km.CERT_STATS.get(dev)
+    rescored = None if st is None else [v / args.steps for v in st.tolist()]
     info = dist.run_info(ctx)
     if ctx.is_main:
         print(json.dumps({
@@ -106,14 +126,18 @@ def main(argv=None) -> int:
             "value": total_points / elapsed, "unit": "points/s", "n_gpus": W,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16 (MFMA distances, fp32 accumulate/sums)",
-            "data": "synthetic Gaussian mixture (1000 true centers), random-sample init",
+            "dtype": args.precision,
+            "dtype_detail": ("fp32 argmin: bf16 MFMA scan certified by rounding bounds, "
+                             "ambiguous points re-decided from fp32 rows" if args.precision ==
+                             "fp32" else "bf16 MFMA distances") + ", fp32 sums",
+            "data": "synthetic Gaussian mixture (1000 true centers), %s init" % args.init,
             "config": {"model": "k-means k=%d d=%d" % (k, d), "global_batch": n * W,
                        "seq_len": None, "parallelism": "dp%d (point shards, RCCL all-reduce "
                        "of K x (d+1) sums/counts)" % W, "points_per_gpu": n,
                        "step": "1 Lloyd iteration (assign + accumulate + all-reduce + move)"},
             "tflops": 2.0 * n * W * k * d / (ms * 1e-3) / 1e12,
             "counted_points": total_counts, "empty_clusters_seen": empties,
+            "init_ms": init_ms, "rescored_points_per_step": rescored,
         }), flush=True)
     if ctx.is_distributed:
         torch.distributed.destroy_process_group()

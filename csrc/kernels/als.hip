@@ -85,6 +85,28 @@ struct AlsParams {
   const float* ws;           // [n_long][ws_stride(KP)]
 };
 
+// fp32 factor mode (SPLIT kernels): every factor row is stored as 2*KP bf16, the hi part
+// bf16(y) followed by the lo part bf16(y - hi), so hi + lo = y to ~2^-17 relative; the Gramian
+// takes s_hi*y_hi + s_lo*y_hi + s_hi*y_lo (s = c*y in fp32, split the same way).  Y, Xb and the
+// gathered operands then have a row stride of 2*KP.
+template <bool SPLIT, int KP>
+__device__ __forceinline__ void store_xb(__bf16* Xb, int64_t row, int c, float x) {
+  const __bf16 h = (__bf16)x;
+  if constexpr (SPLIT) {
+    Xb[row * 2 * KP + c] = h;
+    Xb[row * 2 * KP + KP + c] = (__bf16)(x - (float)h);
+  } else {
+    Xb[row * KP + c] = h;
+  }
+}
+
+// c_i * y_i is split into bf16 hi + lo before the MFMA (one extra MFMA per tile) so that the
+// confidence weight keeps fp32 precision; only y_i itself is rounded (bf16 factor mode)
+#ifndef ORYX_ALS_EXACT_C
+#define ORYX_ALS_EXACT_C 1
+#endif
+constexpr bool kExactC = ORYX_ALS_EXACT_C != 0;
+
 // workspace record of one split row: full symmetric A [KP*KP], b [KP], count, padded to 16 B
 __host__ __device__ constexpr int ws_stride(int kp) { return (kp * kp + kp + 1 + 3) / 4 * 4; }
 
@@ -127,10 +149,10 @@ struct ChunkImage {
   __device__ static constexpr int rot(int r) { return (r * SM + (r >> 2) * ST) % PPR; }
 };
 
-template <int KP>
+template <int KP, bool SPLIT = false>
 struct WaveSmem {
   static constexpr int AS = KP + 1;
-  static constexpr int G_BYTES = ChunkImage<KP>::BYTES;
+  static constexpr int G_BYTES = ChunkImage<KP>::BYTES * (SPLIT ? 2 : 1);
   static constexpr int A_BYTES = KP * AS * 4;
   static constexpr int RAW = G_BYTES > A_BYTES ? G_BYTES : A_BYTES;
   // + 64 floats of per-rating weights (wa | wb) + 64 floats of the broadcast L column
@@ -146,7 +168,7 @@ struct WaveSmem {
 // gathers of a chunk are issued back to back (lanes past the row end re-read a valid row and
 // get zero weights), then written lane-linearly into the chunk image and read back
 // transposed with ds_read_b64_tr_b16 as the MFMA fragments.
-template <int KP, bool INIT_YTY>
+template <int KP, bool INIT_YTY, bool SPLIT = false>
 __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg, int64_t end,
                                                 char* G, float* Wab,
                                                 f32x4 (&acc)[(KP / 16) * (KP / 16 + 1) / 2],
@@ -205,10 +227,15 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
     val = p.vals[vi];
   };
   i32x4 stg[NPL];
+  i32x4 stgl[SPLIT ? NPL : 1];
+  constexpr int YS = SPLIT ? 2 * KP : KP;
   auto gather = [&](const int (&cols)[NPL]) {
 #pragma unroll
-    for (int it = 0; it < NPL; ++it)
-      stg[it] = *reinterpret_cast<const i32x4*>(p.Y + (int64_t)cols[it] * KP + soff[it]);
+    for (int it = 0; it < NPL; ++it) {
+      const __bf16* yr = p.Y + (int64_t)cols[it] * YS + soff[it];
+      stg[it] = *reinterpret_cast<const i32x4*>(yr);
+      if constexpr (SPLIT) stgl[it] = *reinterpret_cast<const i32x4*>(yr + KP);
+    }
   };
 
   // two metadata sets used ping-pong (chunk parity) so that no register copies force an
@@ -225,8 +252,11 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
       Wab[32 + lane] = wb;
     }
 #pragma unroll
-    for (int it = 0; it < NPL; ++it)
+    for (int it = 0; it < NPL; ++it) {
       *reinterpret_cast<i32x4*>(G + (it * 64 + lane) * 16) = stg[it];
+      if constexpr (SPLIT)
+        *reinterpret_cast<i32x4*>(G + CI::BYTES + (it * 64 + lane) * 16) = stgl[it];
+    }
     wave_sync();
     if (c0 + 32 < end) {              // wave-uniform: prefetch chunk c+1, metadata of c+2
       gather(nxt_cols);
@@ -235,7 +265,8 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
     const f32x4* wv = reinterpret_cast<const f32x4*>(Wab);
     const f32x4 wa0 = wv[2 * g], wa1 = wv[2 * g + 1];
     const f32x4 wb0 = wv[8 + 2 * g], wb1 = wv[8 + 2 * g + 1];
-    bf16x8 fa[M], fb[M];
+    constexpr bool LO = SPLIT || kExactC;
+    bf16x8 fb[M], fbl[SPLIT ? M : 1];
 #pragma unroll
     for (int pi = 0; pi < M; ++pi) {
       typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -243,28 +274,51 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
           (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 0)));
       const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
           (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 1)));
-      const bf16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      fb[pi] = v;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        fa[pi][j] = (__bf16)((float)v[j] * wa0[j]);
-        fa[pi][4 + j] = (__bf16)((float)v[4 + j] * wa1[j]);
+      fb[pi] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      if constexpr (SPLIT) {
+        const bf16x4 lo2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) bf16x4*)(G + CI::BYTES + tr_addr(pi, 0)));
+        const bf16x4 hi2 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) bf16x4*)(G + CI::BYTES + tr_addr(pi, 1)));
+        fbl[pi] = __builtin_shufflevector(lo2, hi2, 0, 1, 2, 3, 4, 5, 6, 7);
       }
     }
     {
+      // A operand of row block pi made just before its MFMAs (two fragments live, not 2M)
       int t = 0;
 #pragma unroll
-      for (int pi = 0; pi < M; ++pi)
+      for (int pi = 0; pi < M; ++pi) {
+        bf16x8 fa, fal;
 #pragma unroll
-        for (int qi = 0; qi <= pi; ++qi, ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[pi], fb[qi], acc[t], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) {
+          float yv = (float)fb[pi][j];
+          if constexpr (SPLIT) yv += (float)fbl[pi][j];
+          const float sv = yv * (j < 4 ? wa0[j] : wa1[j - 4]);
+          fa[j] = (__bf16)sv;
+          if constexpr (LO) fal[j] = (__bf16)(sv - (float)fa[j]);
+        }
+#pragma unroll
+        for (int qi = 0; qi <= pi; ++qi, ++t) {
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[qi], acc[t], 0, 0, 0);
+          if constexpr (LO)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fal, fb[qi], acc[t], 0, 0, 0);
+          if constexpr (SPLIT)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fbl[qi], acc[t], 0, 0, 0);
+        }
+      }
     }
 #pragma unroll
     for (int pi = 0; pi < M; ++pi) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bpart[pi] += wb0[j] * (float)fb[pi][j];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bpart[pi] += wb1[j] * (float)fb[pi][4 + j];
+      for (int j = 0; j < 4; ++j) {
+        float y0 = (float)fb[pi][j], y1 = (float)fb[pi][4 + j];
+        if constexpr (SPLIT) {
+          y0 += (float)fbl[pi][j];
+          y1 += (float)fbl[pi][4 + j];
+        }
+        bpart[pi] += wb0[j] * y0;
+        bpart[pi] += wb1[j] * y1;
+      }
     }
     wave_sync();
   };
@@ -391,28 +445,34 @@ struct GatherRing {
     const f32x4* wv = reinterpret_cast<const f32x4*>(Wab);
     const f32x4 wa0 = wv[2 * g], wa1 = wv[2 * g + 1];
     const f32x4 wb0 = wv[8 + 2 * g], wb1 = wv[8 + 2 * g + 1];
-    bf16x8 fa[M], fb[M];
+    bf16x8 fb[M];
 #pragma unroll
     for (int pi = 0; pi < M; ++pi) {
       const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
           (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 0)));
       const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
           (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 1)));
-      const bf16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      fb[pi] = v;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        fa[pi][j] = (__bf16)((float)v[j] * wa0[j]);
-        fa[pi][4 + j] = (__bf16)((float)v[4 + j] * wa1[j]);
-      }
+      fb[pi] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     }
     {
+      // A operand of row block pi made just before its MFMAs (two fragments live, not 2M)
       int t = 0;
 #pragma unroll
-      for (int pi = 0; pi < M; ++pi)
+      for (int pi = 0; pi < M; ++pi) {
+        bf16x8 fa, fal;
 #pragma unroll
-        for (int qi = 0; qi <= pi; ++qi, ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[pi], fb[qi], acc[t], 0, 0, 0);
+        for (int j = 0; j < 8; ++j) {
+          const float sv = (float)fb[pi][j] * (j < 4 ? wa0[j] : wa1[j - 4]);
+          fa[j] = (__bf16)sv;
+          if constexpr (kExactC) fal[j] = (__bf16)(sv - (float)fa[j]);
+        }
+#pragma unroll
+        for (int qi = 0; qi <= pi; ++qi, ++t) {
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[qi], acc[t], 0, 0, 0);
+          if constexpr (kExactC)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fal, fb[qi], acc[t], 0, 0, 0);
+        }
+      }
     }
 #pragma unroll
     for (int pi = 0; pi < M; ++pi) {
@@ -455,20 +515,21 @@ __device__ __forceinline__ float pick_bpart(const float (&bpart)[M], int sel) {
 
 // PROF: accumulate per-phase shader-clock cycles of every row into prof[0..6] (analysis
 // builds only; see scripts/als_phase_profile.py)
-template <int KP, bool PROF = false>
+template <int KP, bool PROF = false, bool SPLIT = false>
 __global__ __launch_bounds__(256) void als_solve_wave(AlsParams p, unsigned long long* prof) {
+  using WSM = WaveSmem<KP, SPLIT>;
   constexpr int M = KP / 16;
   constexpr int NT = M * (M + 1) / 2;
-  constexpr int AS = WaveSmem<KP>::AS;
-  __shared__ __attribute__((aligned(16))) char smem[4 * WaveSmem<KP>::BYTES];
+  constexpr int AS = WSM::AS;
+  __shared__ __attribute__((aligned(16))) char smem[4 * WSM::BYTES];
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  char* my = smem + wave * WaveSmem<KP>::BYTES;
+  char* my = smem + wave * WSM::BYTES;
   char* G = my;
   float* A = reinterpret_cast<float*>(my);
-  float* Wab = reinterpret_cast<float*>(my + WaveSmem<KP>::BYTES - 512);
-  float* Lb = reinterpret_cast<float*>(my + WaveSmem<KP>::BYTES - 256);
+  float* Wab = reinterpret_cast<float*>(my + WSM::BYTES - 512);
+  float* Lb = reinterpret_cast<float*>(my + WSM::BYTES - 256);
   const int g = lane >> 4, fl = lane & 15;
   const int total_waves = gridDim.x * 4;
   unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
@@ -493,7 +554,8 @@ __global__ __launch_bounds__(256) void als_solve_wave(AlsParams p, unsigned long
       float bpart[M];
 #pragma unroll
       for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
-      wave_accumulate<KP, false>(p, beg, slot < 0 ? end : beg, G, Wab, acc, bpart, cnt_acc);
+      wave_accumulate<KP, false, SPLIT>(p, beg, slot < 0 ? end : beg, G, Wab, acc, bpart,
+                                        cnt_acc);
       reduce_bpart<M>(bpart);
       bacc = pick_bpart<M>(bpart, g);
     }
@@ -636,7 +698,7 @@ __global__ __launch_bounds__(256) void als_solve_wave(AlsParams p, unsigned long
     }
     if (lane < KP) {
       p.X[(int64_t)row * KP + lane] = x_own;
-      if (p.Xb) p.Xb[(int64_t)row * KP + lane] = (__bf16)x_own;
+      if (p.Xb) store_xb<SPLIT, KP>(p.Xb, row, lane, x_own);
     }
     wave_sync();
     ORYX_PHASE(5)
@@ -925,7 +987,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
     }
     if (lane < KP) {
       p.X[(int64_t)row * KP + lane] = x_own;
-      if (p.Xb) p.Xb[(int64_t)row * KP + lane] = (__bf16)x_own;
+      if (p.Xb) store_xb<false, KP>(p.Xb, row, lane, x_own);
     }
     wave_sync();
     if (PRIO > 0) __builtin_amdgcn_s_setprio(0);
@@ -938,12 +1000,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
 
 // Debug/verification: the raw normal equations (Gramian without YtY/lambda, b, count) of the
 // single row [beg, end), as accumulated by wave_accumulate.  One wave.
-template <int KP>
+template <int KP, bool SPLIT = false>
 __global__ __launch_bounds__(64) void als_debug_gram(AlsParams p, int64_t beg, int64_t end,
                                                      float* __restrict__ out) {
   constexpr int M = KP / 16;
   constexpr int NT = M * (M + 1) / 2;
-  __shared__ __attribute__((aligned(16))) char smem[ChunkImage<KP>::BYTES + 256];
+  constexpr int GB = ChunkImage<KP>::BYTES * (SPLIT ? 2 : 1);
+  __shared__ __attribute__((aligned(16))) char smem[GB + 256];
   const int lane = threadIdx.x, g = lane >> 4, fl = lane & 15;
   f32x4 acc[NT];
 #pragma unroll
@@ -952,9 +1015,8 @@ __global__ __launch_bounds__(64) void als_debug_gram(AlsParams p, int64_t beg, i
 #pragma unroll
   for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
   float cnt_acc = 0.f;
-  wave_accumulate<KP, false>(p, beg, end, smem,
-                             reinterpret_cast<float*>(smem + ChunkImage<KP>::BYTES), acc, bpart,
-                             cnt_acc);
+  wave_accumulate<KP, false, SPLIT>(p, beg, end, smem, reinterpret_cast<float*>(smem + GB), acc,
+                                    bpart, cnt_acc);
   reduce_bpart<M>(bpart);
   const float cnt = wave_sum(cnt_acc);
   int t = 0;
@@ -980,17 +1042,18 @@ __global__ __launch_bounds__(64) void als_debug_gram(AlsParams p, int64_t beg, i
 // 256-byte run per atomic instruction).  Runs before the solve kernel, which then takes long
 // rows' normal equations from the workspace: a row with 1e5 ratings is spread over ~100
 // waves instead of serialising on one (the tail of the popular-item half-step).
-template <int KP>
+template <int KP, bool SPLIT = false>
 __global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* __restrict__ segs,
                                                   int n_seg, float* __restrict__ ws) {
   constexpr int M = KP / 16;
   constexpr int NT = M * (M + 1) / 2;
-  constexpr int BYTES = ChunkImage<KP>::BYTES + 256;
+  constexpr int GB = ChunkImage<KP>::BYTES * (SPLIT ? 2 : 1);
+  constexpr int BYTES = GB + 256;
   __shared__ __attribute__((aligned(16))) char smem[4 * BYTES];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   char* G = smem + wave * BYTES;
-  float* Wab = reinterpret_cast<float*>(G + ChunkImage<KP>::BYTES);
+  float* Wab = reinterpret_cast<float*>(G + GB);
   const int g = lane >> 4, fl = lane & 15;
   for (int sgi = blockIdx.x * 4 + wave; sgi < n_seg; sgi += gridDim.x * 4) {
     const int64_t slot = segs[4 * sgi + 1], beg = segs[4 * sgi + 2], end = segs[4 * sgi + 3];
@@ -1001,7 +1064,7 @@ __global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* _
 #pragma unroll
     for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
     float cnt_acc = 0.f;
-    wave_accumulate<KP, false>(p, beg, end, G, Wab, acc, bpart, cnt_acc);
+    wave_accumulate<KP, false, SPLIT>(p, beg, end, G, Wab, acc, bpart, cnt_acc);
     reduce_bpart<M>(bpart);
     const float cnt = wave_sum(cnt_acc);
     float* dst = ws + slot * ws_stride(KP);
@@ -1037,20 +1100,20 @@ __global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* _
 //   * blocked back substitution from the last panel: panel p comes back to LDS once, 64
 //     lanes form sum_{J in later blocks} L[J][c] x_J for its 16 columns (4 row groups, two
 //     cross-lane adds), then a 16-step triangular solve finishes the block.
-template <int KP>
+template <int KP, bool SPLIT = false>
 struct WideSmem {
   static constexpr int LS = 20;
   static constexpr int PB = KP * LS * 4;
-  static constexpr int GB = ChunkImage<KP>::BYTES;
+  static constexpr int GB = ChunkImage<KP>::BYTES * (SPLIT ? 2 : 1);
   static constexpr int RAW = PB > GB ? PB : GB;
   // + broadcast slots (128), 1/d (128), z (128), x (128), weights (64)
   static constexpr int BYTES = (RAW + 15) / 16 * 16 + (4 * 128 + 64) * 4;
 };
 
-template <int KP>
+template <int KP, bool SPLIT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void als_solve_wide(
     AlsParams p) {
-  using WS = WideSmem<KP>;
+  using WS = WideSmem<KP, SPLIT>;
   constexpr int M = KP / 16;
   constexpr int NT = M * (M + 1) / 2;
   constexpr int LS = WS::LS;
@@ -1081,7 +1144,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       float bpart[M];
 #pragma unroll
       for (int pi = 0; pi < M; ++pi) bpart[pi] = 0.f;
-      wave_accumulate<KP, false>(p, beg, slot < 0 ? end : beg, my, Wab, acc, bpart, cnt_acc);
+      wave_accumulate<KP, false, SPLIT>(p, beg, slot < 0 ? end : beg, my, Wab, acc, bpart,
+                                        cnt_acc);
       reduce_bpart<M>(bpart);
       // lane (g, fl) holds b[pi*16 + fl] for every pi: rows lane and lane + 64
       bz0 = pick_bpart<M>(bpart, g);
@@ -1276,12 +1340,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (lane < KP) {
       const float x0 = xs[lane];
       p.X[(int64_t)row * KP + lane] = x0;
-      if (p.Xb) p.Xb[(int64_t)row * KP + lane] = (__bf16)x0;
+      if (p.Xb) store_xb<SPLIT, KP>(p.Xb, row, lane, x0);
     }
     if (lane + 64 < KP) {
       const float x1 = xs[lane + 64];
       p.X[(int64_t)row * KP + lane + 64] = x1;
-      if (p.Xb) p.Xb[(int64_t)row * KP + lane + 64] = (__bf16)x1;
+      if (p.Xb) store_xb<SPLIT, KP>(p.Xb, row, lane + 64, x1);
     }
     wave_sync();
   }
@@ -1372,10 +1436,16 @@ __global__ __launch_bounds__(256) void als_solve_block(AlsParams p) {
         if (tpi[s] < 0) continue;
         const bf16x8 ra = *reinterpret_cast<const bf16x8*>(T + (tpi[s] * 16 + fl) * TS + 8 * g);
         const bf16x8 rb = *reinterpret_cast<const bf16x8*>(T + (tqi[s] * 16 + fl) * TS + 8 * g);
-        bf16x8 fa;
+        bf16x8 fa, fal;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) fa[j] = (__bf16)((float)ra[j] * wsc[j]);
+        for (int j = 0; j < 8; ++j) {
+          const float sv = (float)ra[j] * wsc[j];
+          fa[j] = (__bf16)sv;
+          fal[j] = (__bf16)(sv - (float)fa[j]);
+        }
         acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, rb, acc[s], 0, 0, 0);
+        if constexpr (kExactC)
+          acc[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fal, rb, acc[s], 0, 0, 0);
       }
       if (tid < KP) {
         const bf16x8* trow = reinterpret_cast<const bf16x8*>(T + tid * TS);
@@ -1515,7 +1585,7 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
                    const float* vals, const void* Y, const float* YtY, float* X, void* Xb,
                    int n_work, int k, int kp, float lambda, float alpha, int implicit,
                    int* fail_count, const int32_t* long_slot, const int64_t* segs, int n_seg,
-                   int n_long, float* ws, void* stream) {
+                   int n_long, float* ws, int split, void* stream) {
   if (n_work <= 0) return ORYX_OK;
   if (n_seg > 0 && (!long_slot || !segs || !ws || n_long <= 0)) return ORYX_EINVAL;
   AlsParams p{row_ptr, row_ids, col_idx, vals, reinterpret_cast<const __bf16*>(Y), YtY, X,
@@ -1531,7 +1601,12 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
     switch (kp) {
 #define PART_CASE(KPV)                                                                    \
   case KPV:                                                                               \
-    hipLaunchKernelGGL(als_partial<KPV>, dim3(blocks), dim3(256), 0, s, p, segs, n_seg, ws); \
+    if (split)                                                                            \
+      hipLaunchKernelGGL((als_partial<KPV, true>), dim3(blocks), dim3(256), 0, s, p, segs,  \
+                         n_seg, ws);                                                      \
+    else                                                                                  \
+      hipLaunchKernelGGL((als_partial<KPV, false>), dim3(blocks), dim3(256), 0, s, p, segs, \
+                         n_seg, ws);                                                      \
     break;
       PART_CASE(16)
       PART_CASE(32)
@@ -1551,7 +1626,10 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
   case KPV: {                                                                         \
     int blocks = (n_work + 3) / 4;                                                    \
     if (blocks > max_blocks) blocks = max_blocks;                                     \
-    if (g_als_variant == 0)                                                           \
+    if (split)                                                                        \
+      hipLaunchKernelGGL((als_solve_wave<KPV, false, true>), dim3(blocks), dim3(256), 0, \
+                         s, p, nullptr);                                              \
+    else if (g_als_variant == 0)                                                      \
       hipLaunchKernelGGL((als_solve_panel<KPV, false>), dim3(blocks), dim3(256), 0, s, p, \
                          nullptr);                                                    \
     else if (g_als_variant == 2)                                                      \
@@ -1575,10 +1653,13 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
 #undef WAVE_CASE
 #define BLOCK_CASE(KPV)                                                               \
   case KPV: {                                                                         \
-    if (g_als_wide_variant == 0) {                                                    \
+    if (split || g_als_wide_variant == 0) {                                           \
       int blocks = (n_work + 3) / 4;                                                  \
       if (blocks > max_blocks) blocks = max_blocks;                                   \
-      hipLaunchKernelGGL(als_solve_wide<KPV>, dim3(blocks), dim3(256), 0, s, p);     \
+      if (split)                                                                      \
+        hipLaunchKernelGGL((als_solve_wide<KPV, true>), dim3(blocks), dim3(256), 0, s, p); \
+      else                                                                            \
+        hipLaunchKernelGGL((als_solve_wide<KPV, false>), dim3(blocks), dim3(256), 0, s, p); \
     } else {                                                                          \
       int blocks = n_work < max_blocks ? n_work : max_blocks;                         \
       hipLaunchKernelGGL(als_solve_block<KPV>, dim3(blocks), dim3(256), 0, s, p);    \
@@ -1637,15 +1718,19 @@ int oryx_als_solve_profile64(const int64_t* row_ptr, const int32_t* row_ids,
 
 int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const float* vals,
                         const void* Y, int kp, float alpha, int implicit, long long beg,
-                        long long end, float* out, void* stream) {
+                        long long end, float* out, int split, void* stream) {
   AlsParams p{row_ptr, nullptr, col_idx, vals, reinterpret_cast<const __bf16*>(Y), nullptr,
               nullptr, nullptr, 1, kp, 0.f, alpha, implicit, nullptr, nullptr, nullptr};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (kp) {
 #define DBG_CASE(KPV)                                                                       \
   case KPV:                                                                                 \
-    hipLaunchKernelGGL(als_debug_gram<KPV>, dim3(1), dim3(64), 0, s, p, (int64_t)beg,       \
-                       (int64_t)end, out);                                                  \
+    if (split)                                                                              \
+      hipLaunchKernelGGL((als_debug_gram<KPV, true>), dim3(1), dim3(64), 0, s, p,           \
+                         (int64_t)beg, (int64_t)end, out);                                  \
+    else                                                                                    \
+      hipLaunchKernelGGL((als_debug_gram<KPV, false>), dim3(1), dim3(64), 0, s, p,          \
+                         (int64_t)beg, (int64_t)end, out);                                  \
     break;
     DBG_CASE(16)
     DBG_CASE(32)
@@ -1662,7 +1747,7 @@ int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const fl
   return oryx_check_launch();
 }
 
-int oryx_kernels_version() { return 4; }
+int oryx_kernels_version() { return 6; }
 
 int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 

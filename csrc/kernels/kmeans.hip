@@ -212,22 +212,53 @@ __device__ __forceinline__ void km_epilogue_one(const f32x4& ac, int ctg, float&
   bestp = m;
 }
 
+// Certified assignment (fp32 parity; see kmeans_assign_wide_kernel<..., TOP3 = true>): the
+// full center index rides in the low `bits` mantissa bits of each packed value and every lane
+// keeps its three best packed values in order; inserting p into (b1 >= b2 >= b3) is three
+// ops: b3 = med3(b2, b3, p), b2 = med3(b1, b2, p), b1 = max(b1, p).
+struct CertParams {
+  int* idx2;               // [n] second-best center
+  unsigned char* flags;    // [n] 0 = top-1 certified, 1 = rescore top-2, 2 = full rescan
+  unsigned mask;           // (1 << bits) - 1
+  float u;                 // bf16 rounding bound (relative, per operand)
+  float eta_scale;         // packing + accumulation slack, times (|x| + cmax)^2
+  float cmax;              // max |c| over the real centers
+};
+
+__device__ __forceinline__ float km_packi(float x, unsigned idx, unsigned mask) {
+  return __uint_as_float((__float_as_uint(x) & ~mask) | idx);
+}
+
+__device__ __forceinline__ void km_insert3(float p, float& b1, float& b2, float& b3) {
+  b3 = __builtin_amdgcn_fmed3f(b2, b3, p);
+  b2 = __builtin_amdgcn_fmed3f(b1, b2, p);
+  b1 = fmaxf(b1, p);
+}
+
+__device__ __forceinline__ void km_epilogue_top3(const f32x4& ac, int ctg, int g, unsigned mask,
+                                                 float& b1, float& b2, float& b3) {
+  const unsigned base = (unsigned)(ctg * 16 + 4 * g);
+#pragma unroll
+  for (int v = 0; v < 4; ++v) km_insert3(km_packi(ac[v], base + v, mask), b1, b2, b3);
+}
+
 // Requires d_pad = 32 DK with 2 <= DK <= 8 (each LDS row has at least 8 units).
 // PK selects the packed, software-pipelined epilogue (the group-ct epilogue runs while the
 // MFMAs of group ct+1 are in flight, on a second accumulator set; the A fragments are
 // refilled in place, one k-step at a time).
-template <int DK, int NW, bool PK>
+template <int DK, int NW, bool PK, bool TOP3 = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void
 kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict__ xnorm,
                           const __bf16* __restrict__ C, const float* __restrict__ cnorm,
                           long long n, int k_pad, int* __restrict__ assign,
-                          float* __restrict__ mind) {
+                          float* __restrict__ mind, CertParams cert) {
   constexpr int DPAD = DK * 32;
   constexpr int RU = DPAD / 8;             // 16-byte units per center row
   constexpr int CT = 64;                   // centers per LDS stage
   constexpr int STAGE = CT * DPAD * 2;     // bytes of one center tile
   constexpr int BUF = STAGE + CT * 4;      // + |c|^2 of the tile
-  constexpr int PT = 4;                    // 16-point tiles per wave
+  // 16-point tiles per wave (the certified kernel's top-3 state costs a tile at d_pad 256)
+  constexpr int PT = TOP3 && DK == 8 ? 3 : 4;
   constexpr int GPW = RU / NW;             // 1 KB glds chunks per wave per stage
   static_assert(GPW * NW == RU && RU % 8 == 0 && RU <= 32, "glds chunking");
   typedef __attribute__((address_space(3))) void lds_void;
@@ -298,11 +329,22 @@ kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict_
   if constexpr (PK) {
     float bestp[PT];
     int bestct[PT];
+    float t2[TOP3 ? PT : 1], t3[TOP3 ? PT : 1];
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt) {
       bestp[pt] = -3.0e38f;
       bestct[pt] = 0;
+      if constexpr (TOP3) {
+        t2[pt] = -3.0e38f;
+        t3[pt] = -3.0e38f;
+      }
     }
+    auto epi = [&](const f32x4& ac, int ctg, int pt) {
+      if constexpr (TOP3)
+        km_epilogue_top3(ac, ctg, g, cert.mask, bestp[pt], t2[pt], t3[pt]);
+      else
+        km_epilogue_one(ac, ctg, bestp[pt], bestct[pt]);
+    };
     f32x4 acc[2][PT];
     bf16x8 a[DK];
     for (int t = 0; t < ntiles; ++t) {
@@ -345,7 +387,7 @@ kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict_
           if (prev) {
 #pragma unroll
             for (int pt = 0; pt < PT; ++pt)
-              if (pt % DK == s) km_epilogue_one(acc[pset][pt], pctg, bestp[pt], bestct[pt]);
+              if (pt % DK == s) epi(acc[pset][pt], pctg, pt);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -353,8 +395,42 @@ kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict_
       if (t + 1 < ntiles) __syncthreads();
     }
 #pragma unroll
-    for (int pt = 0; pt < PT; ++pt)
-      km_epilogue_one(acc[1][pt], ntiles * (CT / 16) - 1, bestp[pt], bestct[pt]);
+    for (int pt = 0; pt < PT; ++pt) epi(acc[1][pt], ntiles * (CT / 16) - 1, pt);
+    if constexpr (TOP3) {
+#pragma unroll
+      for (int pt = 0; pt < PT; ++pt) {
+        float b1 = bestp[pt], b2 = t2[pt], b3 = t3[pt];
+#pragma unroll
+        for (int off = 16; off < 64; off <<= 1) {
+          const float o1 = __shfl_xor(b1, off, 64);
+          const float o2 = __shfl_xor(b2, off, 64);
+          const float o3 = __shfl_xor(b3, off, 64);
+          km_insert3(o1, b1, b2, b3);
+          km_insert3(o2, b1, b2, b3);
+          km_insert3(o3, b1, b2, b3);
+        }
+        const long long r = p0 + pt * 16 + fl;
+        if (g == 0 && r < n) {
+          const float xn = xnorm[r];
+          const float d1 = xn - 2.f * b1, d2 = xn - 2.f * b2, d3 = xn - 2.f * b3;
+          // true distances lie in [lower(d~), upper(d~)] (bf16 operand rounding delta,
+          // packing / accumulation slack eta); both bounds are monotone in d~
+          const float xr = sqrtf(fmaxf(xn, 0.f)) + cert.cmax;
+          const float delta = cert.u * xr, eta = cert.eta_scale * xr * xr;
+          auto lower = [&](float t) {
+            const float q = fmaxf(sqrtf(fmaxf(t, 0.f)) - delta, 0.f);
+            return q * q - eta;
+          };
+          const float up1 = sqrtf(fmaxf(d1, 0.f)) + delta;
+          const float upper1 = up1 * up1 + eta;
+          assign[r] = (int)(__float_as_uint(b1) & cert.mask);
+          cert.idx2[r] = (int)(__float_as_uint(b2) & cert.mask);
+          cert.flags[r] = lower(d2) > upper1 ? 0 : (lower(d3) > upper1 ? 1 : 2);
+          mind[r] = d1 > 0.f ? d1 : 0.f;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int pt = 0; pt < PT; ++pt) {
       float bv = bestp[pt];
@@ -792,6 +868,80 @@ __global__ __launch_bounds__(256) void km_segment_sum(
   }
 }
 
+// Exact fp32 re-check of the points the certified assignment could not decide: one wave per
+// 64 points, flagged points handled one at a time by the whole wave.  flag 1: squared
+// distances sum (x - c)^2 to the two bf16 candidates (each lane a strided slice of the
+// dimensions); flag 2: every center (lane j scans centers j, j + 64, ...).  Ties go to the
+// lower center index.  stats[0] / stats[1] count flag-1 / flag-2 points (nullable).
+__global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, int ldx, int d,
+                                                  const float* __restrict__ C, int k, long long n,
+                                                  int* __restrict__ assign,
+                                                  const int* __restrict__ idx2,
+                                                  const unsigned char* __restrict__ flags,
+                                                  float* __restrict__ mind,
+                                                  unsigned long long* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const long long nw = (long long)gridDim.x * 4;
+  for (long long w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); w * 64 < n; w += nw) {
+    const long long r0 = w * 64;
+    const int f = r0 + lane < n ? flags[r0 + lane] : 0;
+    unsigned long long m = __ballot(f != 0);
+    while (m) {
+      const int j = __builtin_ctzll(m);
+      m &= m - 1;
+      const long long r = r0 + j;
+      const int fj = __builtin_amdgcn_readlane(f, j);
+      const float* xr = X + r * ldx;
+      float bd;
+      int bi;
+      if (fj == 1) {
+        const int i1 = assign[r], i2 = idx2[r];
+        float s1 = 0.f, s2 = 0.f;
+        for (int t = lane; t < d; t += 64) {
+          const float xv = xr[t];
+          const float a = xv - C[(long long)i1 * d + t], b = xv - C[(long long)i2 * d + t];
+          s1 += a * a;
+          s2 += b * b;
+        }
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        const bool first = s1 < s2 || (s1 == s2 && i1 < i2);
+        bd = first ? s1 : s2;
+        bi = first ? i1 : i2;
+      } else {
+        bd = INFINITY;
+        bi = 0x7fffffff;
+        for (int c = lane; c < k; c += 64) {
+          const float* cr = C + (long long)c * d;
+          float sc = 0.f;
+          for (int t = 0; t < d; ++t) {
+            const float a = xr[t] - cr[t];
+            sc += a * a;
+          }
+          if (sc < bd) {
+            bd = sc;
+            bi = c;
+          }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          const float od = __shfl_xor(bd, off, 64);
+          const int oi = __shfl_xor(bi, off, 64);
+          if (od < bd || (od == bd && oi < bi)) {
+            bd = od;
+            bi = oi;
+          }
+        }
+      }
+      if (lane == 0) {
+        assign[r] = bi;
+        mind[r] = bd;
+        if (stats) atomicAdd(stats + (fj == 1 ? 0 : 1), 1ull);
+      }
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -838,7 +988,8 @@ int oryx_kmeans_assign(const void* X, const float* xnorm, const void* C, long lo
       attr_set = true;                                                                        \
     }                                                                                         \
     hipLaunchKernelGGL((kmeans_assign_wide_kernel<DKV, NWV, PKV>), dim3((unsigned)blocks),    \
-                       dim3(NWV * 64), smem, s, x, xnorm, c, cnorm, n, k_pad, assign, mind);  \
+                       dim3(NWV * 64), smem, s, x, xnorm, c, cnorm, n, k_pad, assign, mind,   \
+                       CertParams{});                                                         \
     return oryx_check_launch();                                                               \
   }
   // default: the 64-point-per-wave kernel where its LDS swizzle applies (d_pad 64/128/256);
@@ -902,6 +1053,64 @@ int oryx_kmeans_assign(const void* X, const float* xnorm, const void* C, long lo
       return ORYX_EINVAL;
   }
 #undef ASSIGN_CASE
+  return oryx_check_launch();
+}
+
+// Certified fp32-parity assignment: the bf16 MFMA kernel keeps each point's three best
+// centers and flags the points whose bf16 ranking is not provably the fp32 one; km_rescore
+// then decides those exactly from the fp32 rows (Xf [n][ldx], Cf [k][d]).  Only d_pad 64 /
+// 128 / 256 (the 64-point-per-wave kernel) and k_pad <= 65536.  idx2 / flags: [n] scratch.
+int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, long long n,
+                            int d_pad, int k_pad, const float* cnorm, const float* Xf, int ldx,
+                            int d, const float* Cf, int k, float cmax, int* assign, float* mind,
+                            int* idx2, unsigned char* flags, unsigned long long* stats,
+                            void* stream) {
+  if (n <= 0) return ORYX_OK;
+  const int dk = d_pad / 32;
+  if (d_pad % 32 || k_pad % 64 || k_pad > 65536 || (dk != 2 && dk != 4 && dk != 8) || k <= 0 ||
+      k > k_pad || d > d_pad)
+    return ORYX_EINVAL;
+  int bits = 2;
+  while ((1 << bits) < k_pad) ++bits;
+  CertParams cp;
+  cp.idx2 = idx2;
+  cp.flags = flags;
+  cp.mask = (1u << bits) - 1u;
+  cp.u = 1.0f / 256.0f;   // 2x the bf16 round-to-nearest bound: covers |x| from the bf16 row
+  cp.eta_scale = ldexpf(1.0f, bits - 22) + (float)d_pad * ldexpf(1.0f, -22) + 1e-6f;
+  cp.cmax = cmax;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const __bf16* x = reinterpret_cast<const __bf16*>(X);
+  const __bf16* c = reinterpret_cast<const __bf16*>(C);
+#define CERT_CASE(DKV)                                                                        \
+  case DKV: {                                                                                 \
+    const int smem = 2 * (64 * DKV * 64 + 256);                                               \
+    constexpr int PPB = 4 * 16 * (DKV == 8 ? 3 : 4);                                          \
+    const long long blocks = (n + PPB - 1) / PPB;                                             \
+    static bool attr_set = false;                                                             \
+    if (!attr_set && smem > 65536) {                                                          \
+      hipFuncSetAttribute(                                                                    \
+          reinterpret_cast<const void*>(&kmeans_assign_wide_kernel<DKV, 4, true, true>),      \
+          hipFuncAttributeMaxDynamicSharedMemorySize, smem);                                  \
+      attr_set = true;                                                                        \
+    }                                                                                         \
+    hipLaunchKernelGGL((kmeans_assign_wide_kernel<DKV, 4, true, true>), dim3((unsigned)blocks), \
+                       dim3(256), smem, s, x, xnorm, c, cnorm, n, k_pad, assign, mind, cp);   \
+    break;                                                                                    \
+  }
+  switch (dk) {
+    CERT_CASE(2)
+    CERT_CASE(4)
+    CERT_CASE(8)
+    default:
+      return ORYX_EINVAL;
+  }
+#undef CERT_CASE
+  long long waves = (n + 63) / 64;
+  long long blocks = (waves + 3) / 4;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(km_rescore, dim3((unsigned)blocks), dim3(256), 0, s, Xf, ldx, d, Cf, k, n,
+                     assign, idx2, flags, mind, stats);
   return oryx_check_launch();
 }
 

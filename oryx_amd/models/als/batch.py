@@ -189,6 +189,7 @@ class ALSUpdate(MLUpdate):
         self.no_known_items = config.get_bool("oryx.als.no-known-items")
         self.decay_factor = config.get_double("oryx.als.decay.factor")
         self.decay_zero_threshold = config.get_double("oryx.als.decay.zero-threshold")
+        self.precision = cfg.get_optional_string(config, "oryx.gpu.dtype") or "fp32"
         self.checkpoint_interval = cfg.get_optional_int(config, "oryx.als.checkpoint-interval") \
             or 0
         self.warm_start = bool(cfg.get_optional_bool(config, "oryx.als.warm-start"))
@@ -233,7 +234,8 @@ class ALSUpdate(MLUpdate):
         remap_i[used_i] = np.arange(len(used_i))
         ctx = self._ctx(context)
         seed = rng.next_seed()
-        trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx, seed=seed)
+        trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx, seed=seed,
+                             precision=self.precision)
         t0 = time.perf_counter()
         # every rank holds the same aggregated triples; each contributes a disjoint slice
         part = slice(ctx.rank, None, ctx.world_size)

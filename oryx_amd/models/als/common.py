@@ -46,7 +46,8 @@ def compute_updated_xu(solver, value: float, xu: Optional[np.ndarray], yi: Optio
     if math.isnan(target):
         return None
     dqui = target - qui
-    dqui_yi = (np.asarray(yi, dtype=np.float32) * np.float32(dqui)).astype(np.float32)
+    # Java: float[] dQuiYi ... dQuiYi[i] *= dQui (double): product in double, one rounding
+    dqui_yi = (np.asarray(yi, dtype=np.float32).astype(np.float64) * dqui).astype(np.float32)
     dxu = solver.solve_f_to_f(dqui_yi)
     if xu is None:
         return dxu

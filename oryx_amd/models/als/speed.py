@@ -203,7 +203,8 @@ class ALSSpeedModelManager(SpeedModelManager):
             yi = torch.where(ypres[:, None], ymat[yr] if len(ymat) else
                              torch.zeros(len(yr), model.features, device=dev),
                              torch.zeros((), device=dev))
-            vals = torch.from_numpy(s).to(dev)
+            # the reference folds in strength.floatValue() (ALSSpeedModelManager.java:170)
+            vals = torch.from_numpy(np.asarray(s, dtype=np.float32).astype(np.float64)).to(dev)
             yinv = torch.from_numpy(yty.inverse()).to(dev)
             xinv = torch.from_numpy(xtx.inverse()).to(dev)
             new_x, valid_x = als_ops.fold_in(yinv, vals, xu, xpres, yi, model.is_implicit())

@@ -19,6 +19,12 @@ Replaces Spark MLlib's block ALS that the reference runs at
 
 With world size 1 no collectives are issued.  On CPU the exact fp32 reference solve runs.
 
+Factor precision: ``"bf16"`` replicates bf16 factors (the BASELINE rank-64 bf16 config);
+``"fp32"`` replicates every factor row as bf16 hi|lo pairs (``ops.als.to_split_bf16``: the
+same bytes as fp32, ~2^-17 relative) and the solve kernels form the Gramian from
+hi*hi + hi*lo + lo*hi MFMA products -- MLlib's fp32 factors at bf16 MFMA rates.  Confidence
+weights c_i stay fp32 in both modes (c_i * y_i is itself split into hi + lo).
+
 Checkpoint / resume (the reference only truncates MLlib lineage with
 ``setCheckpointInterval(5)``, ``[mllib]/als/ALSUpdate.java:120``): every N iterations each rank
 writes its fp32 factor shards to ``<dir>/it<k>/rank<r>.safetensors``; once all ranks have
@@ -123,7 +129,11 @@ def _unit_gaussian(n: int, k: int, kp: int, gen: torch.Generator, device) -> tor
 class ALSTrainer:
     def __init__(self, features: int, lam: float, alpha: float, implicit: bool,
                  ctx: Optional[dist.DistContext] = None, seed: int = 0,
-                 gather_chunks: Optional[int] = None):
+                 gather_chunks: Optional[int] = None, precision: str = "bf16"):
+        if precision not in ("bf16", "fp32"):
+            raise ValueError("precision must be bf16 or fp32, not %r" % (precision,))
+        self.precision = precision
+        self.split = precision == "fp32"
         self.k = int(features)
         self.kp = als_ops.padded_rank(self.k)
         self.lam = float(lam)
@@ -186,7 +196,7 @@ class ALSTrainer:
         if c <= 1 or self._explicit_chunks:
             return max(1, c)
         shard = dist.padded_shard_size(n_total, self.ctx.world_size)
-        if n_total * self.kp * 2 < self.OVERLAP_MIN_BYTES or shard // c < self.OVERLAP_MIN_ROWS:
+        if n_total * self.kp * (4 if self.split else 2) < self.OVERLAP_MIN_BYTES or shard // c < self.OVERLAP_MIN_ROWS:
             return 1
         return c
 
@@ -233,12 +243,15 @@ class ALSTrainer:
 
     def _publish_factors(self) -> None:
         ctx = self.ctx
-        self.Xb_local = self.X.to(torch.bfloat16)
-        self.Yb_local = self.Y.to(torch.bfloat16)
+        self.Xb_local = self._operand(self.X)
+        self.Yb_local = self._operand(self.Y)
         self.Xb = self.lay_u.gather(self.Xb_local, ctx)
         self.Yb = self.lay_i.gather(self.Yb_local, ctx)
         self.fail_count = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.iterations_done = 0
+
+    def _operand(self, x: torch.Tensor) -> torch.Tensor:
+        return als_ops.to_split_bf16(x) if self.split else x.to(torch.bfloat16)
 
     # ------------------------------------------------------------------ checkpoints
     def _layout(self, fingerprint: str, iteration: int) -> dict:
@@ -317,7 +330,7 @@ class ALSTrainer:
             with tracing.range(name + ".solve"):
                 als_ops.solve_rows(parts[c], src_full_bf16, yty, dst_f32, dst_b_local, self.k,
                                    self.lam, self.alpha, self.implicit,
-                                   fail_count=self.fail_count)
+                                   fail_count=self.fail_count, split=self.split)
         # range c's bf16 rows are exchanged while range c+1 is solved
         with tracing.range(name + ".solve+allgather"):
             return lay.gather(dst_b_local, ctx, overlap_with=solve)

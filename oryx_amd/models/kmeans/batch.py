@@ -50,6 +50,8 @@ class KMeansUpdate(MLUpdate):
         self.max_iterations = config.get_int("oryx.kmeans.iterations")
         self.hyper_param_values = [hp.from_config(config, "oryx.kmeans.hyperparams.k")]
         self.input_schema = InputSchema(config)
+        from ...utils import config as cfg
+        self.precision = cfg.get_optional_string(config, "oryx.gpu.dtype") or "fp32"
         if self.max_iterations <= 0 or self.number_of_runs <= 0:
             raise ValueError("iterations and runs must be > 0")
         if self.initialization_strategy not in _INIT_STRATEGIES:
@@ -84,7 +86,7 @@ class KMeansUpdate(MLUpdate):
         local = torch.from_numpy(x[ctx.rank::ctx.world_size].astype(np.float32)).to(ctx.device)
         res = km_ops.kmeans_train(local, k, self.max_iterations, self.number_of_runs,
                                   self.initialization_strategy, seed=rng.next_seed(),
-                                  ctx=ctx)
+                                  ctx=ctx, precision=self.precision)
         centers = res.centers.double().cpu().numpy()
         sizes = res.counts.cpu().numpy()
         log.info("k-means k=%d on %d points x %d: cost %.6g, %d iterations, %.3fs", k, len(x),

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 4
+KERNELS_ABI_VERSION = 6
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -123,19 +123,25 @@ def _load_kernels():
     # ORYX_ALS_WIDE_VARIANT: 64 < k <= 128 solve (0 = als_solve_wide, 1 = als_solve_block)
     _sig(lib, "oryx_als_set_wide_variant", c_i, [c_i])
     lib.oryx_als_set_wide_variant(int(os.environ.get("ORYX_ALS_WIDE_VARIANT", "0")))
+    # ..., n_long, ws, split (fp32 factors as bf16 hi|lo rows of 2*kp), stream
     _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                       c_i, c_f, c_f, c_i, c_vp, c_vp, c_vp, c_i, c_i, c_vp,
-                                      c_vp])
+                                      c_i, c_vp])
     _sig(lib, "oryx_als_ws_stride", c_i, [c_i])
     _sig(lib, "oryx_als_solve_profile64", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i,
                                                 c_i, c_f, c_f, c_i, c_vp, c_vp])
     _sig(lib, "oryx_gramian_ws_floats", c_i, [c_i])
     _sig(lib, "oryx_als_debug_gram", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_f, c_i, c_ll, c_ll,
-                                           c_vp, c_vp])
+                                           c_vp, c_i, c_vp])
     _sig(lib, "oryx_gramian_f32", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
                                           c_vp])
+    # X, xnorm, C, n, d_pad, k_pad, cnorm, Xf, ldx, d, Cf, k, cmax, assign, mind, idx2, flags,
+    # stats, stream
+    _sig(lib, "oryx_kmeans_assign_cert", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_i,
+                                               c_i, c_vp, c_i, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                               c_vp])
     _sig(lib, "oryx_counting_sort", c_i, [c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_rdf_histogram_pieces", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i,
                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,

@@ -25,7 +25,7 @@ import torch
 from .. import native
 
 __all__ = ["CSR", "build_csr", "padded_rank", "gramian", "solve_rows", "solve_rows_reference",
-           "to_bf16_padded", "pair_dots", "KERNEL_MAX_KP"]
+           "to_bf16_padded", "to_split_bf16", "from_split_bf16", "pair_dots", "KERNEL_MAX_KP"]
 
 KERNEL_MAX_KP = 128
 _KERNEL_KPS = (16, 32, 48, 64, 80, 96, 112, 128)
@@ -172,6 +172,25 @@ def build_csr(rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, n_rows
                order.to(torch.int32).contiguous(), long_slot, segs, n_long)
 
 
+def to_split_bf16(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [n, kp] -> bf16 [n, 2*kp]: ``hi = bf16(x)`` then ``lo = bf16(x - hi)``.
+
+    The fp32-factor operand of the solve kernels (``store_xb`` / the SPLIT kernels in
+    csrc/kernels/als.hip): ``hi + lo`` equals ``x`` to ~2^-17 relative, so the Gramian keeps
+    close to fp32 precision while every load stays a bf16 MFMA operand.  Same bytes per row as
+    fp32.
+    """
+    x = x.to(torch.float32)
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.to(torch.float32)).to(torch.bfloat16)
+    return torch.cat([hi, lo], 1).contiguous()
+
+
+def from_split_bf16(xs: torch.Tensor) -> torch.Tensor:
+    kp = xs.shape[1] // 2
+    return xs[:, :kp].to(torch.float32) + xs[:, kp:].to(torch.float32)
+
+
 def to_bf16_padded(x: torch.Tensor, kp: int) -> torch.Tensor:
     if x.shape[1] == kp:
         return x.to(torch.bfloat16).contiguous()
@@ -216,14 +235,17 @@ def _use_kernel(device: torch.device, kp: int) -> bool:
 def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_out: torch.Tensor,
                xb_out: Optional[torch.Tensor], k: int, lam: float, alpha: float,
                implicit: bool, y_f32: Optional[torch.Tensor] = None,
-               fail_count: Optional[torch.Tensor] = None) -> None:
+               fail_count: Optional[torch.Tensor] = None, split: bool = False) -> None:
     """Solve every non-empty row of ``csr`` into ``x_out`` (fp32 [n_rows, kp]) / ``xb_out``.
 
     ``y_bf16``: the opposite factors, bf16 [n_cols, kp] zero-padded.  ``yty``: fp32 [kp, kp]
     Gramian of the opposite factors (implicit), ignored for explicit feedback.
+    ``split``: fp32-factor mode -- ``y_bf16`` and ``xb_out`` are [n, 2*kp] hi|lo rows
+    (:func:`to_split_bf16`).
     """
-    kp = y_bf16.shape[1]
+    kp = x_out.shape[1]
     device = y_bf16.device
+    assert y_bf16.shape[1] == (2 * kp if split else kp), (y_bf16.shape, kp, split)
     if _use_kernel(device, kp):
         lib = native.require_kernels()
         if yty is None or not implicit:
@@ -234,7 +256,8 @@ def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_ou
         assert y_bf16.dtype == torch.bfloat16 and y_bf16.is_contiguous()
         assert x_out.shape[0] >= csr.n_rows and y_bf16.shape[0] >= csr.n_cols
         if xb_out is not None:
-            assert xb_out.dtype == torch.bfloat16 and xb_out.shape == x_out.shape
+            assert xb_out.dtype == torch.bfloat16 and xb_out.is_contiguous()
+            assert xb_out.shape == (x_out.shape[0], y_bf16.shape[1])
         ws = csr.workspace(kp)
         if ws is not None:
             assert lib.oryx_als_ws_stride(kp) == ws_stride(kp)
@@ -250,42 +273,46 @@ def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_ou
                                 csr.segs.data_ptr() if csr.n_seg else None,
                                 csr.n_seg, csr.n_long,
                                 ws.data_ptr() if ws is not None else None,
-                                native.stream_ptr(device))
+                                int(bool(split)), native.stream_ptr(device))
         native.check(rc, "oryx_als_solve")
         return
     # exact reference path (CPU, or ranks beyond the kernel's range)
-    src = y_f32 if y_f32 is not None else y_bf16.to(torch.float32)
+    if y_f32 is not None:
+        src = y_f32
+    else:
+        src = from_split_bf16(y_bf16) if split else y_bf16.to(torch.float32)
     sol = solve_rows_reference(csr, src, yty, k, lam, alpha, implicit)
     rows = csr.order.to(torch.int64)
     x_out[rows] = sol[rows].to(x_out.dtype)
     if xb_out is not None:
-        xb_out[rows] = sol[rows].to(torch.bfloat16)
+        xb_out[rows] = to_split_bf16(sol[rows]) if split else sol[rows].to(torch.bfloat16)
 
 
 def solve_rows_reference(csr: CSR, y: torch.Tensor, yty: Optional[torch.Tensor], k: int,
                          lam: float, alpha: float, implicit: bool,
                          chunk_rows: int = 8192) -> torch.Tensor:
-    """fp32 PyTorch reference of the kernel's math; returns [n_rows, kp] (zeros for empty rows)."""
+    """PyTorch reference of the kernel's math in fp32 (or fp64 when ``y`` is float64);
+    returns [n_rows, kp] (zeros for empty rows)."""
     device = y.device
     kp = y.shape[1]
-    y = y.to(torch.float32)
-    out = torch.zeros((csr.n_rows, kp), dtype=torch.float32, device=device)
+    dt = torch.float64 if y.dtype == torch.float64 else torch.float32
+    y = y.to(dt)
+    out = torch.zeros((csr.n_rows, kp), dtype=dt, device=device)
     if csr.nnz == 0:
         return out
     row_ptr = csr.row_ptr
     counts = (row_ptr[1:] - row_ptr[:-1])
     row_of = torch.repeat_interleave(torch.arange(csr.n_rows, device=device), counts)
-    r = csr.vals.to(torch.float32)
+    r = csr.vals.to(dt)
     if implicit:
         wa = alpha * r.abs()
         wb = torch.where(r > 0, 1.0 + wa, torch.zeros_like(r))
-        cnt = (r > 0).to(torch.float32)
+        cnt = (r > 0).to(dt)
     else:
         wa = torch.ones_like(r)
         wb = r
         cnt = torch.ones_like(r)
-    eye = torch.eye(kp, device=device)
-    pad_diag = torch.zeros(kp, device=device)
+    pad_diag = torch.zeros(kp, device=device, dtype=dt)
     pad_diag[k:] = 1.0
     for lo in range(0, csr.n_rows, chunk_rows):
         hi = min(csr.n_rows, lo + chunk_rows)
@@ -295,16 +322,16 @@ def solve_rows_reference(csr: CSR, y: torch.Tensor, yty: Optional[torch.Tensor],
         ro = row_of[s:e] - lo
         yy = y[csr.cols[s:e].to(torch.int64)]
         n = hi - lo
-        A = torch.zeros((n, kp, kp), device=device)
+        A = torch.zeros((n, kp, kp), device=device, dtype=dt)
         A.index_add_(0, ro, (wa[s:e, None, None] * yy[:, :, None]) * yy[:, None, :])
-        b = torch.zeros((n, kp), device=device)
+        b = torch.zeros((n, kp), device=device, dtype=dt)
         b.index_add_(0, ro, wb[s:e, None] * yy)
-        c = torch.zeros(n, device=device)
+        c = torch.zeros(n, device=device, dtype=dt)
         c.index_add_(0, ro, cnt[s:e])
         if implicit and yty is not None:
-            A = A + yty.to(torch.float32)[None]
-        diag = lam * c[:, None] * torch.cat([torch.ones(k, device=device),
-                                             torch.zeros(kp - k, device=device)])[None]
+            A = A + yty.to(dt)[None]
+        diag = lam * c[:, None] * torch.cat([torch.ones(k, device=device, dtype=dt),
+                                             torch.zeros(kp - k, device=device, dtype=dt)])[None]
         A = A + torch.diag_embed(diag + pad_diag[None])
         nonempty = counts[lo:hi] > 0
         if nonempty.any():
@@ -370,7 +397,9 @@ def fold_in(solver_inv: torch.Tensor, values: torch.Tensor, xu: torch.Tensor,
     tgt = target_qui(implicit, values, base)
     valid = ~torch.isnan(tgt)
     dq = torch.where(valid, tgt - qui, torch.zeros_like(tgt))
-    rhs = (yi.to(torch.float32) * dq.to(torch.float32)[:, None]).to(torch.float64)
+    # Java's dQuiYi[i] *= dQui: float times double, evaluated and rounded once in double
+    rhs = (yi.to(torch.float32).to(torch.float64) * dq[:, None]).to(torch.float32).to(
+        torch.float64)
     dx = rhs.matmul(solver_inv.to(torch.float64).t())
     dx32 = dx.to(torch.float32)
     new = torch.where(xu_present[:, None], (xu.to(torch.float32) + dx32), dx32)

@@ -7,6 +7,13 @@ centroid sums use ``oryx_kmeans_accumulate`` (LDS-privatised column slices); acr
 K x d sums and K counts are all-reduced (one RCCL call per Lloyd iteration).  On CPU an exact
 fp32 PyTorch path runs the same algorithm.
 
+Precision: ``"fp32"`` (default; MLlib computes distances in double on fp32-parsed points)
+uses the certified kernel ``oryx_kmeans_assign_cert``: the bf16 MFMA scan keeps each point's
+three best centers and flags every point whose bf16 ranking is not provably the fp32 ranking
+(rounding bounds on the bf16 operands), and ``km_rescore`` decides exactly those from the
+fp32 rows -- the same argmin as an fp32 scan outside the fp32 rounding band, at close to the
+bf16 kernel's cost.  ``"bf16"`` takes the bf16 argmin as is.
+
 Algorithm (MLlib semantics): k-means|| initialisation (``initializationSteps`` rounds of
 oversampling proportional to D^2 with ``l = 2k``, candidates weighted by assignment counts,
 then weighted k-means++ on the candidates), or "random" (k distinct random points); Lloyd
@@ -29,9 +36,13 @@ from ..parallel import dist, watchdog
 from ..utils import faults
 
 __all__ = ["assign", "accumulate", "kmeans_train", "lloyd_step", "PointSet", "KMeansResult",
-           "pairwise_distances"]
+           "pairwise_distances", "init_centers"]
 
 _CHUNK = 1 << 20
+# operand precision of the assignment when the caller does not name one (oryx.gpu.dtype)
+DEFAULT_PRECISION = "fp32"
+# cumulative (rescored top-2, full rescans) point counts of the certified kernel, per device
+CERT_STATS = {}
 # GPU centroid accumulation: sort-based (default) or LDS-atomic (ORYX_KMEANS_ACCUM=atomic)
 _SORTED = os.environ.get("ORYX_KMEANS_ACCUM", "sorted") != "atomic"
 
@@ -54,6 +65,14 @@ class DeviceCenters:
         cn = torch.full((self.k_pad,), float("inf"), dtype=torch.float32, device=dev)
         cn[:self.k] = cb[:self.k].float().pow(2).sum(1)
         self.cnorm = cn
+        self.cf = centers.to(torch.float32).contiguous()
+        self._cmax = None
+
+    @property
+    def cmax(self) -> float:
+        if self._cmax is None:
+            self._cmax = float(self.cf.norm(dim=1).max()) if self.k else 0.0
+        return self._cmax
 
 
 def _kernel_ok(x: torch.Tensor) -> bool:
@@ -85,6 +104,14 @@ class PointSet:
                 hi = min(self.n, lo + _CHUNK * 4)
                 self.xb[lo:hi, :self.d] = self.x[lo:hi]
                 self.xn[lo:hi] = self.xb[lo:hi].float().pow(2).sum(1)
+        self._cert = None
+
+    def cert_workspace(self):
+        """(second-best index int32 [n], flags uint8 [n]) scratch of the certified kernel."""
+        if self._cert is None:
+            self._cert = (torch.empty(self.n, dtype=torch.int32, device=self.device),
+                          torch.empty(self.n, dtype=torch.uint8, device=self.device))
+        return self._cert
 
     @property
     def shape(self):
@@ -95,14 +122,21 @@ def _as_points(x) -> PointSet:
     return x if isinstance(x, PointSet) else PointSet(x)
 
 
-def assign(x, centers: torch.Tensor, exact: bool = False, out=None
-           ) -> Tuple[torch.Tensor, torch.Tensor]:
+def _cert_ok(pts: "PointSet", k_pad: int) -> bool:
+    return pts.d_pad in (64, 128, 256) and k_pad <= 65536
+
+
+def assign(x, centers: torch.Tensor, exact: bool = False, out=None,
+           precision: Optional[str] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """(index [n], squared distance fp32 [n]) of the nearest center for each row.
 
-    ``x``: a tensor or a prepared :class:`PointSet`.  GPU + not ``exact``: bf16 MFMA kernel
-    (indices int32, written into ``out=(idx, dist)`` when given).  Otherwise fp32 chunked
-    matmul + argmin (indices int64).
+    ``x``: a tensor or a prepared :class:`PointSet`.  GPU + not ``exact``: the MFMA kernels
+    (indices int32, written into ``out=(idx, dist)`` when given) -- certified fp32 argmin when
+    ``precision`` is "fp32" (rows the kernel re-checked carry exact fp32 distances, the others
+    the bf16 estimate), bf16 argmin when "bf16".  Otherwise fp32 chunked matmul + argmin
+    (indices int64).
     """
+    precision = precision or DEFAULT_PRECISION
     if not exact and isinstance(x, torch.Tensor) and _kernel_ok(x) and x.shape[0]:
         x = PointSet(x)
     if isinstance(x, PointSet):
@@ -114,13 +148,30 @@ def assign(x, centers: torch.Tensor, exact: bool = False, out=None
                 out = (torch.empty(n, dtype=torch.int32, device=x.device),
                        torch.empty(n, dtype=torch.float32, device=x.device))
             out_a, out_d = out
-            rc = lib.oryx_kmeans_assign(x.xb.data_ptr(), x.xn.data_ptr(), dc.cb.data_ptr(), n,
-                                        dc.d_pad, dc.k_pad, dc.cnorm.data_ptr(),
-                                        out_a.data_ptr(), out_d.data_ptr(),
-                                        native.stream_ptr(x.device))
-            native.check(rc, "oryx_kmeans_assign")
-            return out_a, out_d
-        x = x.x
+            if precision == "fp32" and not _cert_ok(x, dc.k_pad):
+                x = x.x          # no certified kernel for this shape: exact fp32 scan below
+            elif precision == "fp32":
+                idx2, flags = x.cert_workspace()
+                st = CERT_STATS.get(x.device)
+                if st is None:
+                    st = CERT_STATS[x.device] = torch.zeros(2, dtype=torch.int64,
+                                                            device=x.device)
+                rc = lib.oryx_kmeans_assign_cert(
+                    x.xb.data_ptr(), x.xn.data_ptr(), dc.cb.data_ptr(), n, dc.d_pad, dc.k_pad,
+                    dc.cnorm.data_ptr(), x.x.data_ptr(), x.x.stride(0), x.d, dc.cf.data_ptr(),
+                    dc.k, dc.cmax, out_a.data_ptr(), out_d.data_ptr(), idx2.data_ptr(),
+                    flags.data_ptr(), st.data_ptr(), native.stream_ptr(x.device))
+                native.check(rc, "oryx_kmeans_assign_cert")
+                return out_a, out_d
+            else:
+                rc = lib.oryx_kmeans_assign(x.xb.data_ptr(), x.xn.data_ptr(),
+                                            dc.cb.data_ptr(), n, dc.d_pad, dc.k_pad,
+                                            dc.cnorm.data_ptr(), out_a.data_ptr(),
+                                            out_d.data_ptr(), native.stream_ptr(x.device))
+                native.check(rc, "oryx_kmeans_assign")
+                return out_a, out_d
+        if isinstance(x, PointSet):
+            x = x.x
     n = x.shape[0]
     if n == 0:
         return (torch.zeros(0, dtype=torch.int64, device=x.device),
@@ -256,8 +307,11 @@ def _init_random(x, k, gen, ctx):
     return c
 
 
-def _init_parallel(x, k, gen, ctx, steps: int = 5):
-    """k-means|| (Bahmani et al.), as MLlib's ``K_MEANS_PARALLEL``."""
+def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = None):
+    """k-means|| (Bahmani et al.), as MLlib's ``K_MEANS_PARALLEL``; the D^2 passes run on the
+    assignment kernels (``precision`` as for Lloyd)."""
+    pts = _as_points(pts)
+    x = pts.x
     n = x.shape[0]
     dev = x.device
     # first center: a uniformly random point (rank 0's choice broadcast)
@@ -266,7 +320,8 @@ def _init_parallel(x, k, gen, ctx, steps: int = 5):
     if ctx.is_distributed:
         torch.distributed.broadcast(c0, src=0)
     centers = c0
-    _, d2 = assign(x, centers, exact=True)
+    _, d2 = assign(pts, centers, precision=precision)
+    d2 = d2.clone()
     l = 2.0 * k
     for _ in range(steps):
         phi = d2.double().sum()
@@ -281,10 +336,10 @@ def _init_parallel(x, k, gen, ctx, steps: int = 5):
         if new.shape[0] == 0:
             continue
         centers = torch.cat([centers, new])
-        _, dn = assign(x, new, exact=True)
+        _, dn = assign(pts, new, precision=precision)
         d2 = torch.minimum(d2, dn)
-    idx, _ = assign(x, centers, exact=True)
-    w = torch.bincount(idx, minlength=centers.shape[0]).double()
+    idx, _ = assign(pts, centers, precision=precision)
+    w = torch.bincount(idx.long(), minlength=centers.shape[0]).double()
     if ctx.is_distributed:
         dist.all_reduce_sum(w, ctx)
     chosen = _kmeanspp_weighted(centers, w, k, gen).to(dev)
@@ -305,12 +360,25 @@ def _farthest_points(x: torch.Tensor, d2: torch.Tensor, m: int, ctx) -> torch.Te
     return cand[order, 1:]
 
 
-def lloyd_step(pts: PointSet, centers: torch.Tensor, ctx, workspace=None):
+def init_centers(pts, k: int, init: str = "k-means||", seed: int = 0, run: int = 0,
+                 ctx: Optional[dist.DistContext] = None, precision: Optional[str] = None):
+    """The initial centers of one run (the generator seeding of :func:`kmeans_train`)."""
+    pts = _as_points(pts)
+    ctx = ctx or dist.DistContext(device=pts.device)
+    gen = torch.Generator()
+    gen.manual_seed((seed * 7919 + run * 104729 + ctx.rank) & ((1 << 62) - 1))
+    if init == "random":
+        return _init_random(pts.x, k, gen, ctx)
+    return _init_parallel(pts, k, gen, ctx, precision=precision)
+
+
+def lloyd_step(pts: PointSet, centers: torch.Tensor, ctx, workspace=None,
+               precision: Optional[str] = None):
     """One Lloyd iteration: assign (MFMA kernel), accumulate sums/counts, all-reduce them
     (one K x (d + 1) RCCL call), move the centers.  Returns (new centers, counts, assignment
     distances, number of empty clusters)."""
     kk = centers.shape[0]
-    idx, d2 = assign(pts, centers, out=workspace)
+    idx, d2 = assign(pts, centers, out=workspace, precision=precision)
     sums, counts, _ = accumulate(pts, idx, kk)
     if ctx.is_distributed:
         # counts ride along as an extra fp32 column (exact below 2^24 per cluster per rank;
@@ -330,7 +398,8 @@ def lloyd_step(pts: PointSet, centers: torch.Tensor, ctx, workspace=None):
 
 def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
                  init: str = "k-means||", seed: int = 0, epsilon: float = 1e-4,
-                 ctx: Optional[dist.DistContext] = None) -> KMeansResult:
+                 ctx: Optional[dist.DistContext] = None,
+                 precision: Optional[str] = None) -> KMeansResult:
     """Train k-means on this rank's rows ``x`` (the union over ranks is the data)."""
     pts = _as_points(x)
     x = pts.x
@@ -346,13 +415,13 @@ def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
         if init in ("random",):
             centers = _init_random(x, k, gen, ctx)
         else:
-            centers = _init_parallel(x, k, gen, ctx)
+            centers = _init_parallel(pts, k, gen, ctx, precision=precision)
         kk = centers.shape[0]
         it = 0
         for it in range(1, max_iterations + 1):
             faults.point("kmeans.iteration", iteration=it, rank=ctx.rank)
             watchdog.heartbeat("kmeans.iteration")
-            new, counts, d2, n_empty = lloyd_step(pts, centers, ctx, ws)
+            new, counts, d2, n_empty = lloyd_step(pts, centers, ctx, ws, precision)
             moved = None
             if n_empty:
                 # re-seed empty clusters at the points farthest from their centers

@@ -53,10 +53,17 @@ def test_reference_matches_dense_solve_cpu():
     assert torch.allclose(sol[u].double(), x, atol=1e-4, rtol=1e-4)
 
 
+def _row_rel_err(x, ref, rows):
+    d = (x[rows].double() - ref[rows].double()).norm(dim=1)
+    return d / ref[rows].double().norm(dim=1).clamp_min(1e-12)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", [10, 16, 32, 40, 64, 72, 100, 128])
 @pytest.mark.parametrize("implicit", [True, False])
 def test_kernel_vs_reference(cuda, k, implicit):
+    """bf16 factor mode: on the same bf16-rounded factors the kernel is as accurate as an fp32
+    solve -- per-row relative error vs fp64 within 1e-3, or within 4x torch fp32's own error."""
     csr, y, kp = _problem(700, 400, 30000, k, k, cuda, neg=implicit)
     yb = y.to(torch.bfloat16)
     yty = als_ops.gramian(yb.float()) if implicit else None
@@ -66,16 +73,64 @@ def test_kernel_vs_reference(cuda, k, implicit):
     lam = 0.05
     als_ops.solve_rows(csr, yb, yty, x, xb, k, lam, 1.5, implicit, fail_count=fails)
     torch.cuda.synchronize()
-    ref = als_ops.solve_rows_reference(csr, yb.float(), yty, k, lam, 1.5, implicit)
     rows = csr.order.long()
-    err = (x[rows] - ref[rows]).abs().max().item()
-    scale = ref[rows].abs().max().item()
+    ref64 = als_ops.solve_rows_reference(csr, yb.double(), yty, k, lam, 1.5, implicit)
+    ref32 = als_ops.solve_rows_reference(csr, yb.float(), yty, k, lam, 1.5, implicit)
+    e_kernel = _row_rel_err(x, ref64, rows)
+    e_torch = _row_rel_err(ref32, ref64, rows)
     assert int(fails.item()) == 0
-    assert err <= 2e-2 * max(scale, 1.0), (err, scale)
+    assert bool((e_kernel <= torch.clamp(4 * e_torch, min=1e-3)).all()), (
+        e_kernel.max().item(), e_torch.max().item())
     # padded features stay exactly zero
     if kp > k:
         assert x[:, k:].abs().max().item() == 0.0
-    assert torch.allclose(xb.float(), x, atol=1e-2 * max(scale, 1.0), rtol=1e-2)
+    assert torch.equal(xb, x.to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [10, 48, 64, 100, 128])
+@pytest.mark.parametrize("implicit", [True, False])
+@pytest.mark.parametrize("split_rows", [False, True])
+def test_kernel_fp32_factors_vs_fp64(cuda, k, implicit, split_rows):
+    """fp32 factor mode (bf16 hi|lo operands, SPLIT kernels) on TRUE fp32 factors: per-row
+    relative error vs an fp64 solve <= 1e-3 and within 4x of a torch fp32 solve's error."""
+    csr, y, kp = _problem(700, 400, 30000, k, 100 + k, "cpu", neg=implicit)
+    if split_rows:
+        rows_, cols_ = csr.row_ptr, csr.cols      # rebuild with long rows cut into segments
+        counts = rows_[1:] - rows_[:-1]
+        r = torch.repeat_interleave(torch.arange(700), counts)
+        csr = als_ops.build_csr(r, cols_, csr.vals, 700, 400, split_threshold=20,
+                                split_segment=16)
+        assert csr.n_long > 0
+    csr = csr.to(cuda)
+    y = y.to(cuda)
+    ys = als_ops.to_split_bf16(y)
+    yty = als_ops.gramian(y) if implicit else None
+    x = torch.zeros(700, kp, device=cuda)
+    xs = torch.zeros(700, 2 * kp, device=cuda, dtype=torch.bfloat16)
+    fails = torch.zeros(1, dtype=torch.int32, device=cuda)
+    als_ops.solve_rows(csr, ys, yty, x, xs, k, 0.05, 1.5, implicit, fail_count=fails, split=True)
+    torch.cuda.synchronize()
+    rows = csr.order.long()
+    ref64 = als_ops.solve_rows_reference(csr, y.double(), yty, k, 0.05, 1.5, implicit)
+    ref32 = als_ops.solve_rows_reference(csr, y, yty, k, 0.05, 1.5, implicit)
+    e_kernel = _row_rel_err(x, ref64, rows)
+    e_torch = _row_rel_err(ref32, ref64, rows)
+    assert int(fails.item()) == 0
+    assert e_kernel.max().item() <= 1e-3, e_kernel.max().item()
+    assert bool((e_kernel <= torch.clamp(4 * e_torch, min=1e-5)).all()), (
+        e_kernel.max().item(), e_torch.max().item())
+    # the split output round-trips to the fp32 solution
+    back = als_ops.from_split_bf16(xs)
+    assert ((back - x).abs() <= 1e-5 * x.abs() + 1e-30).all()
+
+
+def test_split_bf16_round_trip_cpu():
+    x = torch.randn(1000, 64) * torch.logspace(-3, 3, 64)[None]
+    xs = als_ops.to_split_bf16(x)
+    assert xs.shape == (1000, 128) and xs.dtype == torch.bfloat16
+    rel = ((als_ops.from_split_bf16(xs) - x).abs() / x.abs().clamp_min(1e-30)).max().item()
+    assert rel < 2 ** -15
 
 
 @pytest.mark.gpu
@@ -177,3 +232,13 @@ def test_split_params_adapt_to_mean_row_length():
     assert als_ops.split_params(25_000_000, 59_047) == (4096, 2048)
     thr, seg = als_ops.split_params(25_000_000, 7_381)
     assert thr == 4 * int(25_000_000 / 7_381) and seg == thr // 2
+
+
+def test_reference_solve_fp64_cpu():
+    for implicit in (True, False):
+        csr, y, kp = _problem(30, 20, 200, 6, 1, "cpu", neg=implicit)
+        yty = als_ops.gramian(y) if implicit else None
+        s32 = als_ops.solve_rows_reference(csr, y, yty, 6, 0.1, 2.0, implicit)
+        s64 = als_ops.solve_rows_reference(csr, y.double(), yty, 6, 0.1, 2.0, implicit)
+        assert s64.dtype == torch.float64
+        assert torch.allclose(s32.double(), s64, atol=1e-4, rtol=1e-4)

@@ -150,3 +150,43 @@ def test_chunked_gather_gpu(cuda):
         res.append(tr.factors())
     assert torch.allclose(res[0].X, res[1].X, atol=1e-4)
     assert torch.allclose(res[0].Y, res[1].Y, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [16, 100])
+def test_trainer_gpu_fp32_factors_match_cpu(cuda, k):
+    """fp32 factor precision (bf16 hi|lo SPLIT kernels) tracks the CPU fp32 trainer closely
+    after two iterations (the bf16 mode's tolerance is 50x looser)."""
+    u, i, r = _data(seed=5, n_u=400, n_i=250, nnz=12000)
+    res = {}
+    for dev in ("cpu", cuda):
+        tr = ALSTrainer(k, lam=0.05, alpha=1.0, implicit=True,
+                        ctx=dist.DistContext(device=torch.device(dev)), seed=1,
+                        precision="fp32")
+        tr.prepare(u, i, r, 400, 250)
+        gi = torch.Generator().manual_seed(11)
+        tr.init_factors(torch.randn(400, k, generator=gi) * 0.3,
+                        torch.randn(250, k, generator=gi) * 0.3)
+        tr.iterate(2)
+        res[str(dev)] = tr.factors()
+    a, b = res["cpu"], res[str(cuda)]
+    for m in ("X", "Y"):
+        ref, got = getattr(a, m).double(), getattr(b, m).cpu().double()
+        rel = (got - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-12)
+        assert rel.max().item() < 1e-3, (m, rel.max().item())
+
+
+def test_trainer_fp32_precision_cpu():
+    u, i, r = _data(seed=8)
+    out = []
+    for prec in ("bf16", "fp32"):
+        tr = ALSTrainer(6, lam=0.05, alpha=1.0, implicit=True, ctx=dist.DistContext(), seed=2,
+                        precision=prec)
+        tr.prepare(u, i, r, 60, 40)
+        gi = torch.Generator().manual_seed(3)
+        tr.init_factors(torch.randn(60, 6, generator=gi), torch.randn(40, 6, generator=gi))
+        tr.iterate(2)
+        out.append(tr.factors())
+        assert tr.Xb_local.shape[1] == (2 if prec == "fp32" else 1) * tr.kp
+    # the CPU path solves from the operand copy: fp32 mode from ~fp32 factors
+    assert not torch.equal(out[0].X, out[1].X)

@@ -394,11 +394,11 @@ if ctx.rank == 0:
 @pytest.mark.gpu
 @pytest.mark.parametrize("d,k", [(2, 3), (20, 64), (64, 100), (100, 257), (256, 50), (256, 1000),
                                  (500, 130)])
-def test_assign_kernel_matches_fp32(cuda, d, k):
+def test_assign_kernel_bf16_matches_fp32_on_rounded_inputs(cuda, d, k):
     g = torch.Generator().manual_seed(d * 1000 + k)
     x = torch.randn(5000, d, generator=g)
     c = torch.randn(k, d, generator=g)
-    idx, dist = km.assign(x.to(cuda), c.to(cuda))
+    idx, dist = km.assign(x.to(cuda), c.to(cuda), precision="bf16")
     # reference on the same bf16-rounded inputs, fp32 math
     xb, cb = x.bfloat16().float(), c.bfloat16().float()
     d2 = ((xb[:, None, :] - cb[None]) ** 2).sum(2)
@@ -406,10 +406,77 @@ def test_assign_kernel_matches_fp32(cuda, d, k):
     got_i = idx.cpu()
     got_v = dist.cpu()
     # argmin agrees except within fp32-rounding near-ties
-    chosen = d2.gather(1, got_i[:, None])[:, 0]
+    chosen = d2.gather(1, got_i[:, None].long())[:, 0]
     assert torch.all(chosen <= ref_v + 1e-3 * (1 + ref_v))
     assert (got_i == ref_i).float().mean() > 0.995
     assert torch.allclose(got_v, ref_v, rtol=1e-3, atol=1e-3 * d)
+
+
+def _fp64_d2(x, c):
+    x, c = x.double(), c.double()
+    return ((x[:, None, :] - c[None]) ** 2).sum(2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,k", [(2, 3), (64, 100), (100, 257), (128, 64), (256, 50),
+                                 (256, 1000), (500, 130)])
+def test_assign_fp32_is_exact_argmin_on_true_data(cuda, d, k):
+    """fp32 precision (certified kernel + fp32 rescore, or the exact scan for shapes without
+    it) on UN-rounded fp32 data: the chosen center is an fp64 argmin up to the fp32 tie band
+    (3e-5 relative), and all but a handful of points pick exactly the fp64 argmin."""
+    g = torch.Generator().manual_seed(d * 7 + k)
+    x = torch.randn(6000, d, generator=g)
+    c = torch.randn(k, d, generator=g)
+    idx, dist = km.assign(x.to(cuda), c.to(cuda), precision="fp32")
+    d64 = _fp64_d2(x, c)
+    ref_v, ref_i = d64.min(1)
+    got_i = idx.cpu().long()
+    chosen = d64.gather(1, got_i[:, None])[:, 0]
+    assert torch.all(chosen <= ref_v * (1 + 3e-5) + 1e-9), (chosen - ref_v).max()
+    assert (got_i == ref_i).float().mean() >= 0.999
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [64, 256])
+def test_assign_fp32_resolves_bf16_near_ties(cuda, d):
+    """Centers 3 apart in a cloud of radius ~16 (bf16 cannot separate them for most points):
+    two-way ties (rescored top-2) and three-way ties (full rescan) still get the fp64 argmin,
+    where the bf16 argmin is wrong for a measurable share of the points."""
+    g = torch.Generator().manual_seed(d)
+    base = torch.randn(d, generator=g) * 8
+    cents = torch.stack([base + 0.02 * torch.randn(d, generator=g) for _ in range(3)] +
+                        [torch.randn(d, generator=g) * 8 for _ in range(61)])
+    x = base + torch.randn(20000, d, generator=g)
+    d64 = _fp64_d2(x, cents)
+    ref_v, ref_i = d64.min(1)
+    from oryx_amd.ops import kmeans as kmo
+    kmo.CERT_STATS.clear()
+    idx, _ = km.assign(x.to(cuda), cents.to(cuda), precision="fp32")
+    got_i = idx.cpu().long()
+    chosen = d64.gather(1, got_i[:, None])[:, 0]
+    assert torch.all(chosen <= ref_v * (1 + 3e-5) + 1e-9)
+    st = kmo.CERT_STATS[torch.device(cuda)].cpu().tolist()
+    assert st[0] + st[1] > 0, st          # the rescore kernel decided some points
+    bidx, _ = km.assign(x.to(cuda), cents.to(cuda), precision="bf16")
+    wrong_bf16 = (bidx.cpu().long() != ref_i).float().mean().item()
+    assert (got_i == ref_i).float().mean().item() > 1 - 1e-3
+    assert wrong_bf16 > 1e-3, wrong_bf16   # the data really defeats a plain bf16 argmin
+
+
+@pytest.mark.gpu
+def test_lloyd_sse_fp32_vs_bf16(cuda):
+    """End-metric drift: SSE of fp32-certified Lloyd matches the fp64-checked CPU run; the bf16
+    run's SSE is reported against it (within 0.5%)."""
+    g = torch.Generator().manual_seed(5)
+    true_c = torch.randn(12, 64, generator=g) * 3
+    x = true_c[torch.randint(0, 12, (30000,), generator=g)] + torch.randn(30000, 64, generator=g)
+    out = {}
+    for prec, dev in (("fp32", cuda), ("bf16", cuda), ("fp32", "cpu")):
+        res = km.kmeans_train(x.to(dev), 16, 15, runs=1, seed=3, init="random",
+                              ctx=dist.DistContext(device=torch.device(dev)), precision=prec)
+        out[(prec, str(dev))] = res.cost
+    assert out[("fp32", str(cuda))] == pytest.approx(out[("fp32", "cpu")], rel=1e-5)
+    assert out[("bf16", str(cuda))] == pytest.approx(out[("fp32", "cpu")], rel=5e-3)
 
 
 @pytest.mark.gpu
@@ -475,13 +542,18 @@ def test_lloyd_step_matches_cpu(cuda):
     x = torch.from_numpy(pts).float()
     c0 = x[torch.randperm(x.shape[0], generator=torch.Generator().manual_seed(3))[:6]].clone()
     ctx = dist.DistContext(device=cuda)
-    new_g, counts_g, _, _ = km.lloyd_step(km.PointSet(x.to(cuda)), c0.to(cuda), ctx)
+    new_g, counts_g, _, _ = km.lloyd_step(km.PointSet(x.to(cuda)), c0.to(cuda), ctx,
+                                          precision="bf16")
     new_c, counts_c, _, _ = km.lloyd_step(km.PointSet(x), c0, dist.DistContext())
     assert int(counts_g.sum()) == x.shape[0]
     # bf16 distances may flip near-tie assignments (several initial centers share a blob)
     assert (counts_g.cpu() - counts_c).abs().sum() <= 0.005 * x.shape[0]
+    # fp32 precision: the same counts as the fp32 CPU step up to fp32 near-ties
+    _, counts_f, _, _ = km.lloyd_step(km.PointSet(x.to(cuda)), c0.to(cuda), ctx,
+                                      precision="fp32")
+    assert (counts_f.cpu() - counts_c).abs().sum() <= 2
     # given the kernel's own assignment the update is exact: centers = per-cluster means
-    idx, _ = km.assign(km.PointSet(x.to(cuda)), c0.to(cuda))
+    idx, _ = km.assign(km.PointSet(x.to(cuda)), c0.to(cuda), precision="bf16")
     idx = idx.long().cpu()
     ref = torch.zeros(6, x.shape[1], dtype=torch.float64).index_add_(0, idx, x.double())
     ref /= torch.bincount(idx, minlength=6).clamp_min(1)[:, None]
