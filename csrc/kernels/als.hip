@@ -100,10 +100,12 @@ __device__ __forceinline__ void store_xb(__bf16* Xb, int64_t row, int c, float x
   }
 }
 
-// c_i * y_i is split into bf16 hi + lo before the MFMA (one extra MFMA per tile) so that the
-// confidence weight keeps fp32 precision; only y_i itself is rounded (bf16 factor mode)
+// bf16 factor mode: the MFMA A operand is bf16(c_i * y_i) (bf16 operands, fp32 accumulation;
+// modelled exactly by solve_rows_reference(..., bf16_operands=True)).  ORYX_ALS_EXACT_C=1
+// builds split c_i * y_i into bf16 hi + lo there too (one extra MFMA per tile, ~18% slower
+// half-steps at rank 64); the fp32 factor mode (SPLIT kernels) always splits it.
 #ifndef ORYX_ALS_EXACT_C
-#define ORYX_ALS_EXACT_C 1
+#define ORYX_ALS_EXACT_C 0
 #endif
 constexpr bool kExactC = ORYX_ALS_EXACT_C != 0;
 
@@ -266,6 +268,40 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
     const f32x4 wa0 = wv[2 * g], wa1 = wv[2 * g + 1];
     const f32x4 wb0 = wv[8 + 2 * g], wb1 = wv[8 + 2 * g + 1];
     constexpr bool LO = SPLIT || kExactC;
+    if constexpr (!LO) {
+      // bf16 factor mode: A fragments bf16(c * y) for all row blocks, then the MFMAs
+      bf16x8 fa[M], fb[M];
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi) {
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 0)));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 1)));
+        const bf16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        fb[pi] = v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          fa[pi][j] = (__bf16)((float)v[j] * wa0[j]);
+          fa[pi][4 + j] = (__bf16)((float)v[4 + j] * wa1[j]);
+        }
+      }
+      int t = 0;
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+        for (int qi = 0; qi <= pi; ++qi, ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[pi], fb[qi], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bpart[pi] += wb0[j] * (float)fb[pi][j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bpart[pi] += wb1[j] * (float)fb[pi][4 + j];
+      }
+      wave_sync();
+      return;
+    }
     bf16x8 fb[M], fbl[SPLIT ? M : 1];
 #pragma unroll
     for (int pi = 0; pi < M; ++pi) {
@@ -445,16 +481,16 @@ struct GatherRing {
     const f32x4* wv = reinterpret_cast<const f32x4*>(Wab);
     const f32x4 wa0 = wv[2 * g], wa1 = wv[2 * g + 1];
     const f32x4 wb0 = wv[8 + 2 * g], wb1 = wv[8 + 2 * g + 1];
-    bf16x8 fb[M];
+    if constexpr (kExactC) {
+      bf16x8 fb[M];
 #pragma unroll
-    for (int pi = 0; pi < M; ++pi) {
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-          (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 0)));
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-          (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 1)));
-      fb[pi] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-    {
+      for (int pi = 0; pi < M; ++pi) {
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 0)));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 1)));
+        fb[pi] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
       // A operand of row block pi made just before its MFMAs (two fragments live, not 2M)
       int t = 0;
 #pragma unroll
@@ -464,15 +500,46 @@ struct GatherRing {
         for (int j = 0; j < 8; ++j) {
           const float sv = (float)fb[pi][j] * (j < 4 ? wa0[j] : wa1[j - 4]);
           fa[j] = (__bf16)sv;
-          if constexpr (kExactC) fal[j] = (__bf16)(sv - (float)fa[j]);
+          fal[j] = (__bf16)(sv - (float)fa[j]);
         }
 #pragma unroll
         for (int qi = 0; qi <= pi; ++qi, ++t) {
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[qi], acc[t], 0, 0, 0);
-          if constexpr (kExactC)
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fal, fb[qi], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fal, fb[qi], acc[t], 0, 0, 0);
         }
       }
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bpart[pi] += wb0[j] * (float)fb[pi][j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bpart[pi] += wb1[j] * (float)fb[pi][4 + j];
+      }
+      wave_sync();
+      return;
+    }
+    bf16x8 fa[M], fb[M];
+#pragma unroll
+    for (int pi = 0; pi < M; ++pi) {
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 0)));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+          (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 1)));
+      const bf16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      fb[pi] = v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        fa[pi][j] = (__bf16)((float)v[j] * wa0[j]);
+        fa[pi][4 + j] = (__bf16)((float)v[4 + j] * wa1[j]);
+      }
+    }
+    {
+      int t = 0;
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+        for (int qi = 0; qi <= pi; ++qi, ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[pi], fb[qi], acc[t], 0, 0, 0);
     }
 #pragma unroll
     for (int pi = 0; pi < M; ++pi) {
@@ -987,7 +1054,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DEEP ? 2 : 
     }
     if (lane < KP) {
       p.X[(int64_t)row * KP + lane] = x_own;
-      if (p.Xb) store_xb<false, KP>(p.Xb, row, lane, x_own);
+      if (p.Xb) p.Xb[(int64_t)row * KP + lane] = (__bf16)x_own;
     }
     wave_sync();
     if (PRIO > 0) __builtin_amdgcn_s_setprio(0);

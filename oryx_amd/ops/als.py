@@ -290,9 +290,13 @@ def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_ou
 
 def solve_rows_reference(csr: CSR, y: torch.Tensor, yty: Optional[torch.Tensor], k: int,
                          lam: float, alpha: float, implicit: bool,
-                         chunk_rows: int = 8192) -> torch.Tensor:
+                         chunk_rows: int = 8192, bf16_operands: bool = False) -> torch.Tensor:
     """PyTorch reference of the kernel's math in fp32 (or fp64 when ``y`` is float64);
-    returns [n_rows, kp] (zeros for empty rows)."""
+    returns [n_rows, kp] (zeros for empty rows).
+
+    ``bf16_operands``: model the bf16 factor mode's MFMA operands exactly -- the Gramian
+    terms are ``bf16(c_i * y_i) * y_i`` (``y`` itself should already be bf16-rounded).
+    """
     device = y.device
     kp = y.shape[1]
     dt = torch.float64 if y.dtype == torch.float64 else torch.float32
@@ -323,7 +327,10 @@ def solve_rows_reference(csr: CSR, y: torch.Tensor, yty: Optional[torch.Tensor],
         yy = y[csr.cols[s:e].to(torch.int64)]
         n = hi - lo
         A = torch.zeros((n, kp, kp), device=device, dtype=dt)
-        A.index_add_(0, ro, (wa[s:e, None, None] * yy[:, :, None]) * yy[:, None, :])
+        cy = wa[s:e, None] * yy
+        if bf16_operands:
+            cy = cy.to(torch.float32).to(torch.bfloat16).to(dt)
+        A.index_add_(0, ro, cy[:, :, None] * yy[:, None, :])
         b = torch.zeros((n, kp), device=device, dtype=dt)
         b.index_add_(0, ro, wb[s:e, None] * yy)
         c = torch.zeros(n, device=device, dtype=dt)

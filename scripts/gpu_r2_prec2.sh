@@ -1,5 +1,5 @@
 #!/bin/bash
-# Precision round 2: ALS + k-means GPU numerics tests, exact-c A/B, fp32 ALS rank-128 and the
+# Precision round 2: ALS + k-means GPU numerics tests, the rank-64 bf16 bench, fp32 ALS rank-128 and the
 # certified fp32 k-means bench (vs bf16) on the BASELINE shapes.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -7,12 +7,8 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_als_kernel.py tests/test_als_trainer.py tests/test_kmeans.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_prec.log 2>&1 || { tail -40 gpurun_out/pytest_prec.log; exit 1; }
 tail -2 gpurun_out/pytest_prec.log
-for i in 1 2; do for v in new old; do
-  if [[ $v == old ]]; then export ORYX_KERNELS_SO=$PWD/ab/liboryx_kernels_noexact.so; else unset ORYX_KERNELS_SO; fi
-  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --speed-events 0 > gpurun_out/ab_als_$v.log 2>&1 || { tail -20 gpurun_out/ab_als_$v.log; exit 1; }
-  echo "als64 $v $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_als_$v.log)"
-done; done
-unset ORYX_KERNELS_SO
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --speed-events 0 > gpurun_out/bench64.log 2>&1 || { tail -20 gpurun_out/bench64.log; exit 1; }
+echo "als64 bf16 $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench64.log)"
 timeout -k 10 300 python bench.py --rank-k 128 --precision fp32 --steps 10 --warmup 3 --speed-events 0 > gpurun_out/bench128_fp32.log 2>&1 || { tail -20 gpurun_out/bench128_fp32.log; exit 1; }
 echo "als128 fp32 25M $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/bench128_fp32.log)"
 timeout -k 10 300 python bench.py --rank-k 128 --precision bf16 --steps 10 --warmup 3 --speed-events 0 > gpurun_out/bench128_bf16.log 2>&1 || { tail -20 gpurun_out/bench128_bf16.log; exit 1; }
