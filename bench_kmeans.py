@@ -82,8 +82,7 @@ def main(argv=None) -> int:
             torch.cuda.synchronize(dev)
         dist.barrier(ctx)
         t_init = time.perf_counter()
-        centers = km.init_centers(pts, k, "k-means||", seed=args.seed, ctx=ctx,
-                                  precision=args.precision)
+        centers = km.init_centers(pts, k, "k-means||", seed=args.seed, ctx=ctx)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         init_ms = (time.perf_counter() - t_init) * 1e3

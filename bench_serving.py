@@ -57,52 +57,45 @@ print(json.dumps({"n": n, "wall": time.perf_counter() - t0, "lat": lat, "errors"
 """
 
 
-def build_model(items: int, users: int, features: int, sample_rate: float, seed: int):
-    import torch
-    from oryx_amd.models.als.serving import ALSServingModel
+def make_data(items: int, users: int, features: int, seed: int):
+    """Item / user factor matrices, ids and Poisson(20) known items (LoadTestALSModelFactory)."""
     rng = np.random.default_rng(seed)
-    model = ALSServingModel(features, True, sample_rate)
-    chunk = 1 << 20
-    for lo in range(0, items, chunk):
-        hi = min(items, lo + chunk)
-        model.Y.set_vectors(["I%d" % i for i in range(lo, hi)],
-                            rng.standard_normal((hi - lo, features), dtype=np.float32))
-    for lo in range(0, users, chunk):
-        hi = min(users, lo + chunk)
-        model.X.set_vectors(["U%d" % i for i in range(lo, hi)],
-                            rng.standard_normal((hi - lo, features), dtype=np.float32))
+    Y = rng.standard_normal((items, features), dtype=np.float32)
+    X = rng.standard_normal((users, features), dtype=np.float32)
+    item_ids = ["I%d" % i for i in range(items)]
+    user_ids = ["U%d" % i for i in range(users)]
     counts = rng.poisson(20, users)
     known = rng.integers(0, items, int(counts.sum()))
+    return Y, X, item_ids, user_ids, counts, known
+
+
+def build_model(data, features: int, sample_rate: float, max_batch: int = 16):
+    import torch
+    from oryx_amd.models.als.serving import ALSServingModel
+    Y, X, item_ids, user_ids, counts, known = data
+    model = ALSServingModel(features, True, sample_rate, max_batch=max_batch)
+    chunk = 1 << 21
+    for lo in range(0, len(item_ids), chunk):
+        model.Y.set_vectors(item_ids[lo:lo + chunk], Y[lo:lo + chunk])
+    for lo in range(0, len(user_ids), chunk):
+        model.X.set_vectors(user_ids[lo:lo + chunk], X[lo:lo + chunk])
     pos = 0
-    for u in range(users):
-        c = int(counts[u])
-        model.add_known_items("U%d" % u, ["I%d" % i for i in known[pos:pos + c].tolist()])
+    for u, c in enumerate(counts.tolist()):
+        model.add_known_items(user_ids[u], [item_ids[i] for i in known[pos:pos + c].tolist()])
         pos += c
     model.Y.device_view()          # push the matrix to HBM before timing
+    if model.index is not None:
+        model.index.refresh()      # and build the bucket-sorted scan index
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     return model
 
 
-def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument("--items", type=int, default=1_000_000)
-    ap.add_argument("--users", type=int, default=100_000)
-    ap.add_argument("--features", type=int, default=50)
-    ap.add_argument("--sample-rate", type=float, default=0.3)
-    ap.add_argument("--workers", type=int, default=2)
-    ap.add_argument("--requests", type=int, default=500, help="per worker")
-    ap.add_argument("--warmup", type=int, default=50, help="per worker, untimed")
-    ap.add_argument("--seed", type=int, default=7)
-    args = ap.parse_args(argv)
-
+def serve_and_measure(model, users: int, workers: int, requests: int, warmup: int,
+                      seed: int):
     from oryx_amd.api import AbstractServingModelManager
     from oryx_amd.serving.layer import ServingLayer
     from oryx_amd.utils import config as cfg
-
-    t0 = time.perf_counter()
-    model = build_model(args.items, args.users, args.features, args.sample_rate, args.seed)
-    build_s = time.perf_counter() - t0
 
     class _Manager(AbstractServingModelManager):
         def consume(self, updates, context=None):
@@ -123,17 +116,16 @@ def main(argv=None) -> int:
     port = layer.actual_port
 
     def run(n):
-        procs = [subprocess.Popen([sys.executable, "-c", CLIENT, str(port), str(args.users),
-                                   str(n), str(args.seed * 100 + w)],
+        procs = [subprocess.Popen([sys.executable, "-c", CLIENT, str(port), str(users),
+                                   str(n), str(seed * 100 + w)],
                                   stdout=subprocess.PIPE, text=True)
-                 for w in range(args.workers)]
-        t = time.perf_counter()
+                 for w in range(workers)]
         outs = [json.loads(p.communicate()[0]) for p in procs]
-        return outs, time.perf_counter() - t
+        return outs
 
     try:
-        run(args.warmup)
-        outs, wall = run(args.requests)
+        run(warmup)
+        outs = run(requests)
     finally:
         layer.close()
     lat = np.concatenate([o["lat"] for o in outs])
@@ -141,23 +133,72 @@ def main(argv=None) -> int:
     errors = sum(o["errors"] for o in outs)
     # wall clock of the slowest client (process start-up excluded)
     client_wall = max(o["wall"] for o in outs)
-    qps = total / client_wall
-    key = (args.features, int(round(args.items / 1e6)), args.sample_rate)
+    return total / client_wall, lat, total, errors
+
+
+def record(model, args_like, qps, lat, total, errors, build_s, workers, sample_rate, items,
+           features):
+    key = (features, int(round(items / 1e6)), sample_rate)
     pub = PUBLISHED.get(key)
-    rec = {
+    b = model.batcher
+    return {
         "metric": "/recommend throughput (LoadBenchmark equivalent)",
         "value": qps, "unit": "req/s", "higher_is_better": True,
         "mean_latency_ms": float(lat.mean()), "p50_ms": float(np.percentile(lat, 50)),
         "p99_ms": float(np.percentile(lat, 99)),
-        "items": args.items, "users": args.users, "features": args.features,
-        "sample_rate": args.sample_rate, "workers": args.workers, "requests": total,
+        "items": items, "users": args_like.users, "features": features,
+        "sample_rate": sample_rate, "workers": workers, "requests": total,
         "errors": errors, "model_build_s": build_s,
+        "scan": "fused HIP top-N (topn.hip)" if b is not None else "torch",
+        "mean_batch": (b.requests / b.batches) if b is not None and b.batches else None,
         "published_reference": {"qps": pub[0], "latency_ms": pub[1],
                                 "hardware": "32-core Xeon 2.3GHz Haswell, JDK 8"} if pub else None,
         "vs_reference_qps": (qps / pub[0]) if pub else None,
+        "vs_reference_latency": (pub[1] / float(lat.mean())) if pub else None,
         "data": "synthetic random Gaussian factors, Poisson(20) known items per user",
     }
-    print(json.dumps(rec), flush=True)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--items", type=int, default=1_000_000)
+    ap.add_argument("--users", type=int, default=500_000)
+    ap.add_argument("--features", type=int, default=50)
+    ap.add_argument("--sample-rate", type=float, default=0.3)
+    ap.add_argument("--workers", default="2", help="comma list of concurrent clients")
+    ap.add_argument("--requests", type=int, default=500, help="per worker")
+    ap.add_argument("--warmup", type=int, default=50, help="per worker, untimed")
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--sweep", action="store_true",
+                    help="every published row: features 50/250 x items 1/5/20M x sample rate "
+                         "0.3/1.0 at each --workers count (one JSON line each)")
+    ap.add_argument("--max-batch", type=int, default=16)
+    args = ap.parse_args(argv)
+    workers = [int(w) for w in str(args.workers).split(",")]
+    if args.sweep:
+        grid = [(f, m) for f in (50, 250) for m in (1_000_000, 5_000_000, 20_000_000)]
+        rates = (0.3, 1.0)
+    else:
+        grid = [(args.features, args.items)]
+        rates = (args.sample_rate,)
+    for features, items in grid:
+        data = make_data(items, args.users, features, args.seed)
+        for rate in rates:
+            t0 = time.perf_counter()
+            model = build_model(data, features, rate, args.max_batch)
+            build_s = time.perf_counter() - t0
+            for w in workers:
+                if model.batcher is not None:
+                    model.batcher.batches = model.batcher.requests = 0
+                qps, lat, total, errors = serve_and_measure(model, args.users, w,
+                                                            args.requests, args.warmup,
+                                                            args.seed)
+                print(json.dumps(record(model, args, qps, lat, total, errors, build_s, w, rate,
+                                        items, features)), flush=True)
+            if model.batcher is not None:
+                model.batcher.close()
+            del model
+        del data
     return 0
 
 

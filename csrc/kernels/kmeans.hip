@@ -869,10 +869,11 @@ __global__ __launch_bounds__(256) void km_segment_sum(
 }
 
 // Exact fp32 re-check of the points the certified assignment could not decide: one wave per
-// 64 points, flagged points handled one at a time by the whole wave.  flag 1: squared
-// distances sum (x - c)^2 to the two bf16 candidates (each lane a strided slice of the
-// dimensions); flag 2: every center (lane j scans centers j, j + 64, ...).  Ties go to the
-// lower center index.  stats[0] / stats[1] count flag-1 / flag-2 points (nullable).
+// 64 points, flagged points handled one at a time by the whole wave, lanes over the
+// dimensions (the point's row stays in registers, center rows are read coalesced).  flag 1:
+// squared distances sum (x - c)^2 to the two bf16 candidates; flag 2: every center, four at a
+// time (one 4-value butterfly reduction per group).  Ties go to the lower center index.
+// stats[0] / stats[1] count flag-1 / flag-2 points (nullable).  d <= 512.
 __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, int ldx, int d,
                                                   const float* __restrict__ C, int k, long long n,
                                                   int* __restrict__ assign,
@@ -892,34 +893,50 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
       const long long r = r0 + j;
       const int fj = __builtin_amdgcn_readlane(f, j);
       const float* xr = X + r * ldx;
+      float xv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[e] = lane + 64 * e < d ? xr[lane + 64 * e] : 0.f;
+      auto dist2 = [&](int c) {
+        const float* cr = C + (long long)c * d;
+        float sc = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float cv = lane + 64 * e < d ? cr[lane + 64 * e] : 0.f;
+          const float a = xv[e] - cv;
+          sc += a * a;
+        }
+        return sc;
+      };
       float bd;
       int bi;
       if (fj == 1) {
         const int i1 = assign[r], i2 = idx2[r];
-        float s1 = 0.f, s2 = 0.f;
-        for (int t = lane; t < d; t += 64) {
-          const float xv = xr[t];
-          const float a = xv - C[(long long)i1 * d + t], b = xv - C[(long long)i2 * d + t];
-          s1 += a * a;
-          s2 += b * b;
-        }
-        s1 = wave_sum(s1);
-        s2 = wave_sum(s2);
+        const float s1 = wave_sum(dist2(i1)), s2 = wave_sum(dist2(i2));
         const bool first = s1 < s2 || (s1 == s2 && i1 < i2);
         bd = first ? s1 : s2;
         bi = first ? i1 : i2;
       } else {
         bd = INFINITY;
         bi = 0x7fffffff;
-        for (int c = lane; c < k; c += 64) {
-          const float* cr = C + (long long)c * d;
-          float sc = 0.f;
-          for (int t = 0; t < d; ++t) {
-            const float a = xr[t] - cr[t];
-            sc += a * a;
-          }
-          if (sc < bd) {
-            bd = sc;
+        for (int c0 = 0; c0 < k; c0 += 4) {
+          float p4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) p4[u] = c0 + u < k ? dist2(c0 + u) : 0.f;
+          // reduce four partial sums at once: after the xor-32 / xor-16 steps lane group
+          // (lane >> 4) holds center c0 + (lane >> 4); then a 16-lane sum
+          const bool up32 = lane & 32, up16 = lane & 16;
+          float a0 = up32 ? p4[2] : p4[0], a1 = up32 ? p4[3] : p4[1];
+          const float b0 = up32 ? p4[0] : p4[2], b1 = up32 ? p4[1] : p4[3];
+          a0 += __shfl_xor(b0, 32, 64);
+          a1 += __shfl_xor(b1, 32, 64);
+          float v = up16 ? a1 : a0;
+          const float o = up16 ? a0 : a1;
+          v += __shfl_xor(o, 16, 64);
+#pragma unroll
+          for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+          const int c = c0 + ((lane >> 5) << 1) + ((lane >> 4) & 1);
+          if (c < k && (v < bd || (v == bd && c < bi))) {
+            bd = v;
             bi = c;
           }
         }
@@ -1068,7 +1085,7 @@ int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, lo
   if (n <= 0) return ORYX_OK;
   const int dk = d_pad / 32;
   if (d_pad % 32 || k_pad % 64 || k_pad > 65536 || (dk != 2 && dk != 4 && dk != 8) || k <= 0 ||
-      k > k_pad || d > d_pad)
+      k > k_pad || d > d_pad || d > 512)
     return ORYX_EINVAL;
   int bits = 2;
   while ((1 << bits) < k_pad) ++bits;
@@ -1076,7 +1093,9 @@ int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, lo
   cp.idx2 = idx2;
   cp.flags = flags;
   cp.mask = (1u << bits) - 1u;
-  cp.u = 1.0f / 256.0f;   // 2x the bf16 round-to-nearest bound: covers |x| from the bf16 row
+  // bf16 round-to-nearest unit roundoff 2^-8 (8-bit significand), 1% slack for |x| being
+  // taken from the bf16 row
+  cp.u = 1.01f / 256.0f;
   cp.eta_scale = ldexpf(1.0f, bits - 22) + (float)d_pad * ldexpf(1.0f, -22) + 1e-6f;
   cp.cmax = cmax;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);

@@ -79,6 +79,8 @@ class FeatureVectors:
         self.partitioner = partitioner        # rows -> partition ids (device LSH)
         self._dev_part = None
         self.version = 0
+        # rows changed since the last take_index_dirty() (serving ItemIndex); None = all
+        self._idx_dirty: Optional[Set[int]] = None
 
     # ---------------------------------------------------------------- basic map API
     def size(self) -> int:
@@ -115,6 +117,7 @@ class FeatureVectors:
             valid[:self._host_valid.shape[0]] = self._host_valid
             self._host, self._host_valid = host, valid
             self._dirty_all = True
+            self._idx_dirty = None
         self._n_rows += 1
         self._ids.append(None)
         return row
@@ -133,7 +136,18 @@ class FeatureVectors:
             self._host[row] = v
             self._host_valid[row] = True
             self._dirty.add(row)
+            if self._idx_dirty is not None:
+                self._idx_dirty.add(row)
             self.version += 1
+
+    def take_index_dirty(self) -> Optional[np.ndarray]:
+        """Rows changed since the previous call (None: everything may have changed)."""
+        with self._lock.write():
+            d = self._idx_dirty
+            self._idx_dirty = set()
+        if d is None:
+            return None
+        return np.fromiter(d, dtype=np.int64, count=len(d))
 
     def _ensure_capacity(self, rows: int) -> None:
         cap = self._host.shape[0]
@@ -147,6 +161,7 @@ class FeatureVectors:
         valid[:self._host_valid.shape[0]] = self._host_valid
         self._host, self._host_valid = host, valid
         self._dirty_all = True
+        self._idx_dirty = None
 
     def set_vectors(self, ids: Sequence[str], matrix: np.ndarray) -> None:
         """Bulk insert/update (model loading): new IDs get one contiguous block of rows."""
@@ -171,6 +186,7 @@ class FeatureVectors:
                         self._host[row] = v
                         self._host_valid[row] = True
                         self._dirty.add(row)
+                    self._idx_dirty = None
                     self.version += 1
                     return
                 start = self._n_rows
@@ -185,8 +201,11 @@ class FeatureVectors:
             self._host_valid[rows] = True
             if len(rows) > max(1024, self._n_rows // 8):
                 self._dirty_all = True
+                self._idx_dirty = None
             else:
                 self._dirty.update(rows.tolist())
+                if self._idx_dirty is not None:
+                    self._idx_dirty.update(rows.tolist())
             self.version += 1
 
     def remove_vector(self, id_: str) -> None:
@@ -202,6 +221,8 @@ class FeatureVectors:
             self._ids[row] = None
             self._free.append(row)
             self._dirty.add(row)
+            if self._idx_dirty is not None:
+                self._idx_dirty.add(row)
             self.version += 1
 
     def add_all_ids_to(self, out: Set[str]) -> None:

@@ -5,14 +5,16 @@ Equivalent of ``ALSServingModel`` / ``ALSServingModelManager`` / ``LocalitySensi
 ``ALSServingModelManager.java:63-154``, ``LocalitySensitiveHash.java:26-188``,
 ``TopNConsumer.java:55-74``) re-designed for MI355X:
 
-* Y (items) lives in HBM as one fp32 matrix (``FeatureVectors`` device mirror) with a norms
-  vector; ``UP`` rows are applied to a host mirror and flushed to the device in one batched
-  copy before the next query, so a model load of millions of rows costs a few copies;
-* top-N is a full scan on the GPU: ``scores = Y q`` (one GEMV, or a GEMM for micro-batched
-  queries), known items / filtered rows masked to -inf, then ``topk``; cosine similarity
-  divides by the norms vector.  This replaces the reference's thread-pool scan of LSH
-  partitions.  LSH is kept for semantic parity when ``oryx.als.sample-rate < 1``: each item's
-  hash bucket is computed on the device at flush time and non-candidate buckets are masked;
+* Y (items) lives in HBM as one fp32 matrix (``FeatureVectors`` device mirror); ``UP`` rows
+  are applied to a host mirror and flushed to the device in one batched copy before the next
+  query, so a model load of millions of rows costs a few copies;
+* top-N runs on the fused HIP scan (:mod:`oryx_amd.ops.topn`, ``csrc/kernels/topn.hip``) over
+  a bucket-sorted copy of Y: a query reads only its LSH candidate buckets (``oryx.als.
+  sample-rate``), known / excluded items and the candidate-bucket mask are applied in the
+  kernel's epilogue, and each wave keeps a top-64 per query in LDS.  Concurrent requests are
+  micro-batched (``oryx.serving.max-batch``, ``batch-wait-sec``): one launch scores up to 16
+  queries in one pass over the item rows.  Requests with a rescorer (host callbacks) or more
+  than 64 results take the unfused torch path (scores, masks, ``topk``);
 * YᵀY for anonymous fold-in is a device GEMM, cached until Y changes.
 """
 
@@ -27,6 +29,7 @@ import numpy as np
 import torch
 
 from ...api import AbstractServingModelManager, KeyMessage, ServingModel
+from ...ops import topn as topn_ops
 from ...utils import mathx, pmml as pmmlu, rng, text
 from ...utils.lang import AutoReadWriteLock
 from .common import FeatureVectors
@@ -38,6 +41,76 @@ __all__ = ["ALSServingModel", "ALSServingModelManager", "LocalitySensitiveHash",
 log = logging.getLogger(__name__)
 
 RESCORE_FULL_POOL = 1 << 17
+
+
+class TopNBatcher:
+    """Micro-batches concurrent top-N requests into shared kernel launches.
+
+    Requests queue up while a launch runs; the worker takes everything queued (up to
+    ``max_batch``), optionally waiting ``wait_s`` for more, and answers each request's event.
+    With ``max_batch <= 1`` requests run inline on the caller's thread.
+    """
+
+    def __init__(self, index: "topn_ops.ItemIndex", max_batch: int, wait_s: float):
+        self.index = index
+        self.max_batch = max(1, int(max_batch))
+        self.wait_s = max(0.0, float(wait_s))
+        self._cv = threading.Condition()
+        self._queue: List[list] = []
+        self._thread = None
+        self._closed = False
+        self.batches = 0
+        self.requests = 0
+
+    def submit(self, q: "topn_ops.TopNQuery"):
+        if self.max_batch <= 1:
+            return self.index.scan([q])[0]
+        slot = [q, None, None, threading.Event()]
+        with self._cv:
+            if self._thread is None:
+                self._thread = threading.Thread(target=self._run, name="OryxTopNBatcher",
+                                                daemon=True)
+                self._thread.start()
+            self._queue.append(slot)
+            self._cv.notify()
+        slot[3].wait()
+        if slot[2] is not None:
+            raise slot[2]
+        return slot[1]
+
+    def _run(self) -> None:
+        import time
+        while True:
+            with self._cv:
+                while not self._queue and not self._closed:
+                    self._cv.wait()
+                if self._closed and not self._queue:
+                    return
+                if self.wait_s > 0 and len(self._queue) < self.max_batch:
+                    deadline = time.monotonic() + self.wait_s
+                    while len(self._queue) < self.max_batch:
+                        left = deadline - time.monotonic()
+                        if left <= 0:
+                            break
+                        self._cv.wait(left)
+                batch = self._queue[:self.max_batch]
+                del self._queue[:len(batch)]
+            try:
+                res = self.index.scan([b[0] for b in batch])
+                for b, r in zip(batch, res):
+                    b[1] = r
+            except Exception as e:   # answered to every waiting request
+                for b in batch:
+                    b[2] = e
+            self.batches += 1
+            self.requests += len(batch)
+            for b in batch:
+                b[3].set()
+
+    def close(self) -> None:
+        with self._cv:
+            self._closed = True
+            self._cv.notify_all()
 
 
 def _binom(n: int, k: int) -> int:
@@ -147,7 +220,8 @@ class LocalitySensitiveHash:
 class ALSServingModel(ServingModel):
     def __init__(self, features: int, implicit: bool, sample_rate: float = 1.0,
                  rescorer_provider: Optional[RescorerProvider] = None,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, max_batch: int = 16,
+                 batch_wait_s: float = 0.0):
         if features <= 0 or not (0.0 < sample_rate <= 1.0):
             raise ValueError("bad features / sample rate")
         if device is None:
@@ -168,6 +242,11 @@ class ALSServingModel(ServingModel):
         self._expected_lock = threading.Lock()
         self._yty_solver = None
         self._yty_version = -1
+        self.index = None
+        self.batcher = None
+        if topn_ops.kernel_ok(device, features):
+            self.index = topn_ops.ItemIndex(self.Y, self.lsh.get_num_partitions())
+            self.batcher = TopNBatcher(self.index, max_batch, batch_wait_s)
 
     # ---------------------------------------------------------------- accessors
     def get_features(self) -> int:
@@ -259,6 +338,18 @@ class ALSServingModel(ServingModel):
         """
         if how_many <= 0 or self.Y.size() == 0:
             return []
+        lsh_on = self.lsh.get_max_bits_differing() < self.lsh.get_num_hashes()
+        if self.batcher is not None and rescorer is None and how_many <= topn_ops.MAX_HOW_MANY:
+            cands = self.lsh.get_candidate_indices(target) if lsh_on else None
+            ex = self.Y.host_rows(exclude) if exclude else None
+            rows, scores = self.batcher.submit(topn_ops.TopNQuery(
+                np.asarray(target, dtype=np.float32), how_many, cosine, cands, ex))
+            out = []
+            for r, v in zip(rows.tolist(), scores.tolist()):
+                id_ = self.Y.id_of_row(r)
+                if id_ is not None:
+                    out.append((id_, float(v)))
+            return out
         mat, valid, norms = self.Y.device_view()
         n = mat.shape[0]
         if n == 0:
@@ -270,7 +361,7 @@ class ALSServingModel(ServingModel):
         neg_inf = torch.tensor(float("-inf"), device=mat.device)
         scores = torch.where(valid, scores, neg_inf)
         parts = self.Y.device_partitions()
-        if parts is not None and self.lsh.get_max_bits_differing() < self.lsh.get_num_hashes():
+        if parts is not None and lsh_on:
             cand = torch.zeros(self.lsh.get_num_partitions(), dtype=torch.bool,
                                device=mat.device)
             cand[torch.from_numpy(self.lsh.get_candidate_indices(target)).to(mat.device)] = True
@@ -364,6 +455,11 @@ class ALSServingModelManager(AbstractServingModelManager):
     def __init__(self, config):
         super().__init__(config)
         self.sample_rate = config.get_double("oryx.als.sample-rate")
+        from ...utils import config as cfg
+        self.max_batch = cfg.get_optional_int(config, "oryx.serving.max-batch") or 16
+        wait = config.get_double("oryx.serving.batch-wait-sec") \
+            if config.has_path("oryx.serving.batch-wait-sec") else 0.0
+        self.batch_wait_s = float(wait)
         self.rescorer_provider = load_rescorer_providers(
             config.get_string("oryx.als.rescorer-provider-class")
             if config.has_path("oryx.als.rescorer-provider-class") else None)
@@ -404,7 +500,9 @@ class ALSServingModelManager(AbstractServingModelManager):
                 if self.model is None or features != self.model.get_features():
                     log.warning("No previous model, or # features has changed; creating new one")
                     self.model = ALSServingModel(features, implicit, self.sample_rate,
-                                                 self.rescorer_provider)
+                                                 self.rescorer_provider,
+                                                 max_batch=self.max_batch,
+                                                 batch_wait_s=self.batch_wait_s)
                 log.info("Updating model")
                 xids = set(pmml.get_extension_content("XIDs") or [])
                 yids = set(pmml.get_extension_content("YIDs") or [])

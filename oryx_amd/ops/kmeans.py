@@ -307,9 +307,11 @@ def _init_random(x, k, gen, ctx):
     return c
 
 
-def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = None):
+def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = "bf16"):
     """k-means|| (Bahmani et al.), as MLlib's ``K_MEANS_PARALLEL``; the D^2 passes run on the
-    assignment kernels (``precision`` as for Lloyd)."""
+    bf16 assignment kernel by default: they only set sampling probabilities and candidate
+    weights, and certifying near-ties against ~2k freshly sampled data points would re-decide
+    most of them."""
     pts = _as_points(pts)
     x = pts.x
     n = x.shape[0]
@@ -369,7 +371,7 @@ def init_centers(pts, k: int, init: str = "k-means||", seed: int = 0, run: int =
     gen.manual_seed((seed * 7919 + run * 104729 + ctx.rank) & ((1 << 62) - 1))
     if init == "random":
         return _init_random(pts.x, k, gen, ctx)
-    return _init_parallel(pts, k, gen, ctx, precision=precision)
+    return _init_parallel(pts, k, gen, ctx, precision=precision or "bf16")
 
 
 def lloyd_step(pts: PointSet, centers: torch.Tensor, ctx, workspace=None,
@@ -415,7 +417,7 @@ def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
         if init in ("random",):
             centers = _init_random(x, k, gen, ctx)
         else:
-            centers = _init_parallel(pts, k, gen, ctx, precision=precision)
+            centers = _init_parallel(pts, k, gen, ctx)
         kk = centers.shape[0]
         it = 0
         for it in range(1, max_iterations + 1):

@@ -329,3 +329,118 @@ def test_recommend_gpu(cuda):
     assert recs[0]["id"] == "I1" and abs(recs[0]["value"] - 0.4653969) < FE
     r = c.get_json("/similarity/I0/I4/I6")
     assert abs(r[2]["value"] - 0.5571406537227921) < 1e-5
+
+
+# ---------------------------------------------------------------- fused top-N scan (GPU)
+
+def _brute(Y, valid, q, how_many, cosine=False, allowed=None, exclude=()):
+    s = Y.double() @ torch.as_tensor(q, dtype=torch.float64)
+    if cosine:
+        s = s / Y.double().norm(dim=1).clamp_min(1e-30)
+    s[~valid] = float("-inf")
+    if allowed is not None:
+        s[~allowed] = float("-inf")
+    for r in exclude:
+        s[r] = float("-inf")
+    v, i = torch.topk(s, how_many)
+    keep = torch.isfinite(v)
+    return i[keep].numpy(), v[keep].numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n", [(10, 5000), (50, 100_003), (250, 40_000)])
+@pytest.mark.parametrize("cosine", [False, True])
+def test_topn_kernel_matches_bruteforce(cuda, k, n, cosine):
+    from oryx_amd.models.als.common import FeatureVectors
+    from oryx_amd.ops import topn
+    g = np.random.default_rng(k + n)
+    fv = FeatureVectors(k, cuda)
+    Y = g.standard_normal((n, k)).astype(np.float32)
+    fv.set_vectors(["I%d" % i for i in range(n)], Y)
+    idx = topn.ItemIndex(fv, 1)
+    qs = [topn.TopNQuery(g.standard_normal(k).astype(np.float32), hm, cosine,
+                         exclude_rows=g.integers(0, n, 30).tolist())
+          for hm in (1, 10, 64, 7, 33)]
+    res = idx.scan(qs)
+    Yt = torch.from_numpy(Y)
+    valid = torch.ones(n, dtype=torch.bool)
+    for q, (rows, scores) in zip(qs, res):
+        br, bs = _brute(Yt, valid, q.target, q.how_many, cosine, exclude=q.exclude_rows)
+        assert len(rows) == len(br)
+        # same score sequence (fp32 vs fp64 rounding), same items up to near-ties
+        assert np.allclose(scores, bs, rtol=1e-5, atol=1e-5)
+        assert (rows == br).mean() > 0.9
+        assert not set(rows.tolist()) & set(q.exclude_rows)
+
+
+@pytest.mark.gpu
+def test_topn_kernel_lsh_candidates_and_batches(cuda):
+    """Bucket-sorted index: per-query candidate buckets prune exactly like a brute-force mask;
+    17 queries split over two launches; in-place updates and a re-sort keep it exact."""
+    from oryx_amd.models.als.common import FeatureVectors
+    from oryx_amd.ops import topn
+    g = np.random.default_rng(3)
+    k, n, nb = 32, 60_000, 64
+    H = torch.from_numpy(g.standard_normal((6, k)).astype(np.float32)).to(cuda)
+    w = (1 << torch.arange(6, device=cuda))
+    part = lambda rows: ((rows @ H.t()) > 0).long().mul(w).sum(1)
+    fv = FeatureVectors(k, cuda, partitioner=part)
+    Y = g.standard_normal((n, k)).astype(np.float32)
+    fv.set_vectors(["I%d" % i for i in range(n)], Y)
+    idx = topn.ItemIndex(fv, nb)
+    bucket = part(torch.from_numpy(Y).to(cuda)).cpu()
+    for step in range(3):
+        qs = []
+        for j in range(17):
+            c = np.sort(g.choice(nb, 20, replace=False))
+            qs.append(topn.TopNQuery(g.standard_normal(k).astype(np.float32), 10,
+                                     candidates=c))
+        res = idx.scan(qs)
+        Yt = torch.from_numpy(Y)
+        valid = torch.ones(n, dtype=torch.bool)
+        for q, (rows, scores) in zip(qs, res):
+            allowed = torch.from_numpy(np.isin(bucket.numpy(), q.candidates))
+            br, bs = _brute(Yt, valid, q.target, 10, allowed=allowed)
+            assert np.allclose(scores, bs, rtol=1e-5, atol=1e-5)
+            assert set(rows.tolist()) <= set(np.nonzero(allowed.numpy())[0].tolist())
+        # updates: small in-place changes (same bucket) then a large change (re-sort)
+        if step == 0:
+            ch = g.choice(n, 100, replace=False)
+            Y[ch] *= 1.5            # same sign pattern -> same bucket
+            for r in ch:
+                fv.set_vector("I%d" % r, Y[r])
+            before = idx.rebuilds
+        elif step == 1:
+            assert idx.rebuilds == before      # applied in place
+            ch = g.choice(n, 5000, replace=False)
+            Y[ch] = g.standard_normal((5000, k)).astype(np.float32)
+            fv.set_vectors(["I%d" % r for r in ch], Y[ch])
+            bucket = part(torch.from_numpy(Y).to(cuda)).cpu()
+
+
+@pytest.mark.gpu
+def test_serving_model_topn_uses_kernel_and_batcher(cuda):
+    import threading
+    from oryx_amd.models.als.serving import ALSServingModel
+    g = np.random.default_rng(5)
+    k, n = 20, 20000
+    m = ALSServingModel(k, True, 1.0, device=torch.device(cuda), max_batch=16)
+    assert m.index is not None
+    Y = g.standard_normal((n, k)).astype(np.float32)
+    m.Y.set_vectors(["I%d" % i for i in range(n)], Y)
+    targets = [g.standard_normal(k).astype(np.float32) for _ in range(40)]
+    out = [None] * 40
+
+    def work(j):
+        out[j] = m.top_n(targets[j], 5, exclude={"I1", "I2"})
+    ts = [threading.Thread(target=work, args=(j,)) for j in range(40)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for j in range(40):
+        s = Y @ targets[j]
+        s[[1, 2]] = -np.inf
+        best = np.argsort(-s)[:5]
+        assert [i for i, _ in out[j]] == ["I%d" % b for b in best]
+    assert m.batcher.requests == 40 and m.batcher.batches <= 40
