@@ -235,11 +235,19 @@ __device__ __forceinline__ void km_insert3(float p, float& b1, float& b2, float&
   b1 = fmaxf(b1, p);
 }
 
+// Most groups hold nothing above the lane's third best once the scan is under way: a group
+// max (two ops) and a wave vote skip the three-op insertions unless some lane needs them.
 __device__ __forceinline__ void km_epilogue_top3(const f32x4& ac, int ctg, int g, unsigned mask,
                                                  float& b1, float& b2, float& b3) {
   const unsigned base = (unsigned)(ctg * 16 + 4 * g);
+  float p[4];
 #pragma unroll
-  for (int v = 0; v < 4; ++v) km_insert3(km_packi(ac[v], base + v, mask), b1, b2, b3);
+  for (int v = 0; v < 4; ++v) p[v] = km_packi(ac[v], base + v, mask);
+  const float m = fmaxf(km_max3(p[0], p[1], p[2]), p[3]);
+  if (__builtin_expect(__any(m > b3), 0)) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) km_insert3(p[v], b1, b2, b3);
+  }
 }
 
 // Requires d_pad = 32 DK with 2 <= DK <= 8 (each LDS row has at least 8 units).
@@ -257,8 +265,7 @@ kmeans_assign_wide_kernel(const __bf16* __restrict__ X, const float* __restrict_
   constexpr int CT = 64;                   // centers per LDS stage
   constexpr int STAGE = CT * DPAD * 2;     // bytes of one center tile
   constexpr int BUF = STAGE + CT * 4;      // + |c|^2 of the tile
-  // 16-point tiles per wave (the certified kernel's top-3 state costs a tile at d_pad 256)
-  constexpr int PT = TOP3 && DK == 8 ? 3 : 4;
+  constexpr int PT = 4;                    // 16-point tiles per wave
   constexpr int GPW = RU / NW;             // 1 KB glds chunks per wave per stage
   static_assert(GPW * NW == RU && RU % 8 == 0 && RU <= 32, "glds chunking");
   typedef __attribute__((address_space(3))) void lds_void;
@@ -1104,7 +1111,7 @@ int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, lo
 #define CERT_CASE(DKV)                                                                        \
   case DKV: {                                                                                 \
     const int smem = 2 * (64 * DKV * 64 + 256);                                               \
-    constexpr int PPB = 4 * 16 * (DKV == 8 ? 3 : 4);                                          \
+    constexpr int PPB = 4 * 16 * 4;                                                           \
     const long long blocks = (n + PPB - 1) / PPB;                                             \
     static bool attr_set = false;                                                             \
     if (!attr_set && smem > 65536) {                                                          \

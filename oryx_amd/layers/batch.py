@@ -13,6 +13,16 @@ Equivalent of ``BatchLayer`` + ``BatchUpdateFunction`` + ``SaveToHDFSFunction`` 
 3. save the new data as ``data-dir/oryx-<ms>.data/part-00000`` (JSON lines ``[key,message]``);
 4. commit input offsets (when ``oryx.id`` is set);
 5. delete data (and model) dirs older than ``max-age-data-hours`` (``max-age-model-hours``).
+
+Sharded data path (one rank per GPU; update classes with ``sharded_data = True``, i.e. the ALS,
+k-means and RDF apps): rank 0 announces only the generation (timestamp, seed and the input
+offset range of every partition); each rank reads ITS share of every partition's offset range
+straight from the log, reads only its share of the past part files, runs the update on its
+share (the apps exchange what they need by key with all-to-alls -- the reference's Spark
+shuffles) and writes its own ``part-<rank>`` file, like the reference's per-partition
+``SaveToHDFSFunction`` / ``BatchUpdateFunction`` (``[lambda]/batch/SaveToHDFSFunction.java:
+59-76``, ``BatchUpdateFunction.java:103-130``).  No record crosses ranks in the layer.
+Other update classes get the interval's records from rank 0 (broadcast) as before.
 """
 
 from __future__ import annotations
@@ -32,7 +42,8 @@ from ..parallel import dist
 from ..utils import faults, ioutils, lang, rng
 from .common import AbstractLayer, IntervalTimer, drain
 
-__all__ = ["BatchLayer", "save_interval_data", "read_past_data", "delete_old_data"]
+__all__ = ["BatchLayer", "save_interval_data", "read_past_data", "delete_old_data",
+           "read_log_share", "save_interval_part"]
 
 log = logging.getLogger(__name__)
 
@@ -53,10 +64,35 @@ def save_interval_data(data_dir: str, timestamp: int, records) -> Optional[str]:
     return d
 
 
-def read_past_data(data_dir: str) -> Dataset:
+def save_interval_part(data_dir: str, timestamp: int, records, rank: int) -> str:
+    """This rank's share of an interval: ``oryx-<ts>.data.tmp/part-<rank>`` (the directory is
+    renamed into place by rank 0 once every rank has written)."""
+    d = os.path.join(ioutils.to_local_path(data_dir), "oryx-%d.data.tmp" % timestamp)
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, "part-%05d" % rank)
+    with open(path + ".w", "w", encoding="utf-8") as f:
+        for k, m in records:
+            f.write(json.dumps([k, m], separators=(",", ":")))
+            f.write("\n")
+    os.replace(path + ".w", path)
+    return d
+
+
+def _finish_interval_dir(data_dir: str, timestamp: int) -> None:
+    root = ioutils.to_local_path(data_dir)
+    tmp = os.path.join(root, "oryx-%d.data.tmp" % timestamp)
+    if os.path.isdir(tmp):
+        os.replace(tmp, os.path.join(root, "oryx-%d.data" % timestamp))
+
+
+def read_past_data(data_dir: str, rank: int = 0, world: int = 1) -> Dataset:
+    """All past records, or with ``world > 1`` this rank's share: part file j of the sorted
+    listing belongs to rank ``j % world``."""
     pairs: List[Tuple[Optional[str], str]] = []
-    for path in ioutils.list_files(data_dir, "*/part-*"):
-        if ".tmp" in os.path.dirname(path):
+    paths = [p for p in sorted(ioutils.list_files(data_dir, "*/part-*"))
+             if ".tmp" not in os.path.dirname(p) and not p.endswith(".w")]
+    for j, path in enumerate(paths):
+        if j % world != rank:
             continue
         with open(path, "r", encoding="utf-8") as f:
             for line in f:
@@ -64,6 +100,35 @@ def read_past_data(data_dir: str) -> Dataset:
                     k, m = json.loads(line)
                     pairs.append((k, m))
     return Dataset(pairs)
+
+
+def read_log_share(root: str, topic_name: str, starts: List[int], ends: List[int], rank: int,
+                   world: int) -> List[Tuple[Optional[str], str]]:
+    """Records of this rank's contiguous share of every partition's [start, end) range."""
+    from ..transport import log as tlog
+    out: List[Tuple[Optional[str], str]] = []
+    topic = tlog.Topic(root, topic_name)
+    try:
+        for p, (lo, hi) in enumerate(zip(starts, ends)):
+            n = hi - lo
+            a, b = lo + n * rank // world, lo + n * (rank + 1) // world
+            if b <= a:
+                continue
+            r = topic.reader(p, a)
+            try:
+                while r.position < b:
+                    recs = r.poll(min(65536, b - r.position), 100)
+                    if not recs:
+                        break
+                    for off, _, k, v in recs:
+                        if off >= b:
+                            break
+                        out.append((k, v))
+            finally:
+                r.close()
+    finally:
+        topic.close()
+    return out
 
 
 def delete_old_data(directory: str, max_age_hours: int, pattern: re.Pattern = _TS_RE,
@@ -126,6 +191,11 @@ class BatchLayer(AbstractLayer):
         log.info("Batch layer started (interval %ds)", self.generation_interval_sec)
         return self
 
+    def _sharded(self) -> bool:
+        dctx = self._context.dist if self._context is not None else None
+        return bool(dctx is not None and dctx.is_distributed and
+                    getattr(self._update, "sharded_data", False))
+
     def run_interval(self, timestamp: Optional[int] = None) -> None:
         """One generation (also callable directly, e.g. from the CLI or tests)."""
         if self._input_consumer is None:
@@ -134,6 +204,9 @@ class BatchLayer(AbstractLayer):
             self.build_input_consumer()
         ts = int(time.time() * 1000) if timestamp is None else timestamp
         t_start = time.perf_counter()
+        if self._sharded():
+            self._run_sharded_main(ts, t_start)
+            return
         records = drain(self._input_consumer)
         faults.point("batch.interval", timestamp=ts, records=len(records))
         dctx = self._context.dist if self._context is not None else None
@@ -173,6 +246,63 @@ class BatchLayer(AbstractLayer):
                             pattern=re.compile(r"^(\d+)$"))
         self.intervals_run += 1
 
+    # ------------------------------------------------------------------ sharded generations
+    def _run_sharded_main(self, ts: int, t_start: float) -> None:
+        cons = self._input_consumer
+        ends = cons.topic.end_offsets()
+        starts = [r.position for r in sorted(cons.readers, key=lambda r: r.partition)]
+        seed = rng.next_seed()
+        msg = {"ts": ts, "seed": seed, "starts": starts, "ends": ends, "sharded": True}
+        dist.broadcast_object(msg, self._context.dist, control=True)
+        n = self._run_sharded(msg)
+        for r in cons.readers:
+            r.seek(ends[r.partition])
+        self.commit_input_offsets()
+        rec = {"event": "batch_interval", "layer_id": self.id, "timestamp": ts,
+               "records": n, "seconds": time.perf_counter() - t_start, "sharded": True}
+        tracing.record(rec)
+        if self.timings_file:
+            with open(self.timings_file, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+        if self.max_data_age_hours >= 0:
+            delete_old_data(self.data_dir, self.max_data_age_hours)
+        if self.max_model_age_hours >= 0:
+            delete_old_data(self.model_dir, self.max_model_age_hours,
+                            pattern=re.compile(r"^(\d+)$"))
+        self.intervals_run += 1
+
+    def _run_sharded(self, msg) -> int:
+        """Every rank: read its share, update, save its part; returns the interval's total
+        record count (all ranks)."""
+        dctx = self._context.dist
+        total = sum(e - s for s, e in zip(msg["starts"], msg["ends"]))
+        if total <= 0:
+            return 0
+        ts = msg["ts"]
+        records = read_log_share(self.input_root, self.input_topic, msg["starts"], msg["ends"],
+                                 dctx.rank, dctx.world_size)
+        faults.point("batch.interval", timestamp=ts, records=len(records))
+        log.info("Rank %d: update at %d with %d of %d new records", dctx.rank, ts,
+                 len(records), total)
+        past = read_past_data(self.data_dir, dctx.rank, dctx.world_size)
+        producer = None
+        if self.update_topic and self.update_broker:
+            producer = LogTopicProducer(self.update_broker, self.update_topic, self.config,
+                                        async_=False, max_message=self.max_message)
+        try:
+            with rng.shared_seed_scope(msg["seed"]):
+                self._update.run_update(self._context, ts, Dataset(records),
+                                        past if len(past) else None, self.model_dir, producer)
+        finally:
+            if producer is not None:
+                producer.close()
+        save_interval_part(self.data_dir, ts, records, dctx.rank)
+        dist.barrier(dctx)
+        if dctx.is_main:
+            _finish_interval_dir(self.data_dir, ts)
+        dist.barrier(dctx)
+        return total
+
     def run_follower(self) -> int:
         """Non-zero ranks of a multi-GPU batch layer: wait for rank 0's announcements and run
         the same update (reading past data from the shared data dir) so every collective in
@@ -185,6 +315,10 @@ class BatchLayer(AbstractLayer):
             msg = dist.broadcast_object(None, dctx, control=True)
             if msg is None:
                 return joined
+            if msg.get("sharded"):
+                if self._run_sharded(msg):
+                    joined += 1
+                continue
             if not msg["records"]:
                 continue
             past = read_past_data(self.data_dir)

@@ -14,6 +14,12 @@ Equivalent of ``MLUpdate`` (``[ml]/MLUpdate.java:59-372``):
 Data is a :class:`~oryx_amd.api.Dataset` of (key, message) pairs; apps see message lists.
 GPU candidates run concurrently on one device from separate threads (the device queue
 serialises them) or sequentially across all ranks.
+
+Sharded apps (``sharded_data = True``) on several ranks: each rank holds only its share of the
+data; every rank runs the whole candidate loop (split, build, evaluate -- the apps' collective
+versions, so every rank gets the same eval and picks the same winner), rank 0 writes the
+candidate files, promotes the winner and sends ``MODEL``, and every rank publishes its own
+share of the additional model data (the reference publishes per partition from executors).
 """
 
 from __future__ import annotations
@@ -40,8 +46,13 @@ TIMINGS_FILE_NAME = "timings.json"
 
 
 class MLUpdate(BatchLayerUpdate):
+    # True when build_model / evaluate / publish_additional_model_data accept this rank's share
+    # of the data and do their own cross-rank exchanges
+    sharded_data = False
+
     def __init__(self, config):
         self.config = config
+        self.dist_ctx = None
         self.test_fraction = config.get_double("oryx.ml.eval.test-fraction")
         candidates = config.get_int("oryx.ml.eval.candidates")
         self.eval_parallelism = config.get_int("oryx.ml.eval.parallelism")
@@ -100,8 +111,13 @@ class MLUpdate(BatchLayerUpdate):
         per_param = hp.choose_values_per_hyper_param(len(values), self.candidates)
         combos = hp.choose_hyper_parameter_combos(values, self.candidates, per_param)
         dctx = self._dist_ctx(context)
+        self.dist_ctx = dctx
         # trainers that checkpoint or warm-start find their files under the model dir
         self.current_model_dir = ioutils.to_local_path(model_dir) if model_dir else None
+        if dctx.is_distributed and self.sharded_data:
+            self._run_update_sharded(context, new_msgs, past_msgs, combos, model_dir,
+                                     model_update_topic, dctx)
+            return
         # multi-rank: every candidate runs in its own shared-seed scope so all ranks make the
         # same splits whatever rank 0 does in between (evaluation, publishing)
         self._candidate_seed_base = rng.next_seed() if dctx.is_distributed else None
@@ -145,6 +161,56 @@ class MLUpdate(BatchLayerUpdate):
             self.publish_additional_model_data(context, best_model, new_msgs, past_msgs,
                                                final_path, model_update_topic)
 
+    def _run_update_sharded(self, context, new_msgs, past_msgs, combos, model_dir,
+                            model_update_topic, dctx) -> None:
+        main = dctx.is_main
+        model_dir_local = ioutils.to_local_path(model_dir)
+        stamp = dist.broadcast_object(int(time.time() * 1000) if main else None, dctx)
+        candidates_path = os.path.join(model_dir_local, ".temporary", str(stamp))
+        if main:
+            os.makedirs(candidates_path, exist_ok=True)
+        results = [self._build_and_eval(i, combos, context, new_msgs, past_msgs,
+                                        candidates_path) for i in range(self.candidates)]
+        best_i, best_eval = None, float("-inf")
+        for i, (path, ev) in enumerate(results):
+            if path is None:
+                continue
+            if ev == ev:
+                if ev > best_eval:
+                    best_eval, best_i = ev, i
+            elif best_i is None and self.test_fraction == 0.0:
+                best_i = i
+        final_path = os.path.join(model_dir_local, str(stamp + 1))
+        if main:
+            if best_i is None:
+                log.info("Unable to build any model")
+            else:
+                os.replace(results[best_i][0], final_path)
+            ioutils.delete_recursively(candidates_path)
+        dist.barrier(dctx)
+        if model_update_topic is None or best_i is None:
+            if model_update_topic is None:
+                log.info("No update topic configured, not publishing models to a topic")
+            return
+        best_model_path = os.path.join(final_path, MODEL_FILE_NAME)
+        best_model = pmmlu.read(best_model_path)
+        if main:
+            if os.path.getsize(best_model_path) <= self.max_message_size:
+                model_update_topic.send("MODEL", pmmlu.to_string(best_model))
+            else:
+                model_update_topic.send("MODEL-REF", ioutils.to_uri(best_model_path))
+        dist.barrier(dctx)
+        if self.can_publish_additional_model_data():
+            self.publish_additional_model_data(context, best_model, new_msgs, past_msgs,
+                                               final_path, model_update_topic)
+
+    def _global_count(self, n: int) -> int:
+        d = self.dist_ctx
+        if d is None or not d.is_distributed or not self.sharded_data:
+            return n
+        from ..parallel import shuffle
+        return int(sum(shuffle.all_gather_int(n, d)))
+
     @staticmethod
     def _dist_ctx(context):
         c = context if isinstance(context, dist.DistContext) else getattr(context, "dist", None)
@@ -186,9 +252,13 @@ class MLUpdate(BatchLayerUpdate):
         log.info("Building candidate %d with params %s", i, params)
         train, test = self._split_train_test(new_msgs, past_msgs)
         ev = float("nan")
-        timing = {"candidate": i, "params": [str(p) for p in params], "train": len(train),
-                  "test": len(test)}
-        if not train:
+        n_train, n_test = self._global_count(len(train)), self._global_count(len(test))
+        timing = {"candidate": i, "params": [str(p) for p in params], "train": n_train,
+                  "test": n_test}
+        # sharded: every rank builds / evaluates (collectives), rank 0 writes the files
+        writer = not (self.sharded_data and self.dist_ctx is not None and
+                      self.dist_ctx.is_distributed and not self.dist_ctx.is_main)
+        if not n_train:
             log.info("No train data to build a model")
         else:
             t0 = time.perf_counter()
@@ -197,12 +267,15 @@ class MLUpdate(BatchLayerUpdate):
             timing["build_s"] = time.perf_counter() - t0
             if model is None:
                 log.info("Unable to build a model")
+                if not writer:
+                    return None, ev
             else:
-                os.makedirs(candidate_path, exist_ok=True)
-                model_path = os.path.join(candidate_path, MODEL_FILE_NAME)
-                log.info("Writing model to %s", model_path)
-                pmmlu.write(model, model_path)
-                if not test:
+                if writer:
+                    os.makedirs(candidate_path, exist_ok=True)
+                    model_path = os.path.join(candidate_path, MODEL_FILE_NAME)
+                    log.info("Writing model to %s", model_path)
+                    pmmlu.write(model, model_path)
+                if not n_test:
                     log.info("No test data available to evaluate model")
                 else:
                     log.info("Evaluating model")
@@ -212,8 +285,9 @@ class MLUpdate(BatchLayerUpdate):
                     timing["evaluate_s"] = time.perf_counter() - t1
                 timing.update(self.build_timings(candidate_path))
                 # per-candidate timing record next to the model (moves with the winner)
-                with open(os.path.join(candidate_path, TIMINGS_FILE_NAME), "w") as f:
-                    json.dump(dict(timing, eval=ev if ev == ev else None), f)
+                if writer:
+                    with open(os.path.join(candidate_path, TIMINGS_FILE_NAME), "w") as f:
+                        json.dump(dict(timing, eval=ev if ev == ev else None), f)
         timing["eval"] = ev if ev == ev else None
         tracing.record(dict(timing, event="candidate"))
         log.info("Model eval for params %s: %s (%s)", params, ev, candidate_path)

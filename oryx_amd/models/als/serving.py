@@ -59,6 +59,8 @@ class TopNBatcher:
         self._queue: List[list] = []
         self._thread = None
         self._closed = False
+        self._contended = False
+        self._last_scan_s = 0.0
         self.batches = 0
         self.requests = 0
 
@@ -86,8 +88,13 @@ class TopNBatcher:
                     self._cv.wait()
                 if self._closed and not self._queue:
                     return
-                if self.wait_s > 0 and len(self._queue) < self.max_batch:
-                    deadline = time.monotonic() + self.wait_s
+                # wait for stragglers when asked to, or when requests queued up while the
+                # previous launch ran (concurrent clients): a tenth of that launch's time
+                wait = self.wait_s
+                if self._contended and self._last_scan_s > 0:
+                    wait = max(wait, min(0.1 * self._last_scan_s, 0.005))
+                if wait > 0 and len(self._queue) < self.max_batch:
+                    deadline = time.monotonic() + wait
                     while len(self._queue) < self.max_batch:
                         left = deadline - time.monotonic()
                         if left <= 0:
@@ -95,6 +102,7 @@ class TopNBatcher:
                         self._cv.wait(left)
                 batch = self._queue[:self.max_batch]
                 del self._queue[:len(batch)]
+            t_scan = time.monotonic()
             try:
                 res = self.index.scan([b[0] for b in batch])
                 for b, r in zip(batch, res):
@@ -102,8 +110,11 @@ class TopNBatcher:
             except Exception as e:   # answered to every waiting request
                 for b in batch:
                     b[2] = e
+            self._last_scan_s = time.monotonic() - t_scan
             self.batches += 1
             self.requests += len(batch)
+            with self._cv:
+                self._contended = bool(self._queue) or len(batch) > 1
             for b in batch:
                 b[3].set()
 
