@@ -14,6 +14,17 @@ Equivalent of ``ALSUpdate`` (``[mllib]/als/ALSUpdate.java:78-498``) and its help
   ``XIDs``, ``YIDs``;
 * evaluation: AUC (implicit; per-user positives vs sampled negatives) or -RMSE, on device;
 * publishing: ``UP`` ``["Y",id,vec]`` rows first, then ``["X",id,vec,[known items]]``.
+
+Sharded (several ranks, :mod:`oryx_amd.layers.batch` sharded generations): each rank parses
+only its share of the lines; user / item strings get global codes from a distributed
+dictionary (:func:`oryx_amd.parallel.shuffle.unify_ids`, owner = crc32 % W -- the
+reference's parse-or-hash + reverse map, collision-free); events are routed to their user's
+owner for the time-ordered aggregation (the reference's ``reduceByKey`` shuffle,
+``[mllib]/als/ALSUpdate.java:332-352``); the trainer re-partitions by item itself.  The test
+split boundary uses the global timestamp range; AUC / RMSE are per-rank partial sums
+all-reduced (``Evaluation.java:49-136``); each rank publishes its share of the Y rows, then of
+the X rows with the known items of the users it owns (``EnqueueFeatureVecsFn`` per
+partition).
 """
 
 from __future__ import annotations
@@ -33,7 +44,7 @@ import torch
 from ... import ingest
 from ...ml import hyperparams as hp
 from ...ml.mlupdate import MLUpdate
-from ...parallel import dist
+from ...parallel import dist, shuffle
 from ...utils import config as cfg, ioutils, pmml as pmmlu, rng, text
 from . import evaluation
 from .trainer import ALSTrainer
@@ -177,6 +188,8 @@ def _warm_start_factors(model_dir: str, features: int, x_ids: List[str], y_ids: 
 
 
 class ALSUpdate(MLUpdate):
+    sharded_data = True
+
     def __init__(self, config):
         super().__init__(config)
         self.iterations = config.get_int("oryx.als.iterations")
@@ -211,12 +224,19 @@ class ALSUpdate(MLUpdate):
         c = getattr(context, "dist", None)
         return c if c is not None else dist.get_context()
 
+    def _sharded(self, context) -> bool:
+        return self._ctx(context).is_distributed and self.dist_ctx is not None and \
+            self.dist_ctx.is_distributed
+
     def build_model(self, context, train_data, hyper_parameters, candidate_path):
         features = int(hyper_parameters[0])
         lam = float(hyper_parameters[1])
         alpha = float(hyper_parameters[2])
         if features <= 0 or lam < 0.0 or alpha <= 0.0:
             raise ValueError("bad hyperparameters %s" % (hyper_parameters,))
+        if self._sharded(context):
+            return self._build_sharded(context, train_data, features, lam, alpha,
+                                       candidate_path)
         users, items = ingest.IdDict(), ingest.IdDict()
         u, i, s, ts = parse_ratings(train_data, users, items, self.decay_factor,
                                     self.decay_zero_threshold)
@@ -282,6 +302,154 @@ class ALSUpdate(MLUpdate):
             "ratings_per_s": (len(u) * 1e3 / (sum(its) / len(its))) if its else None}
         return pmml
 
+    # ---------------------------------------------------------------- sharded path
+    def _parse_global(self, lines, ctx):
+        """This rank's lines -> (global user code, global item code, strength, ts) plus the
+        dictionaries' owner tables."""
+        users, items = ingest.IdDict(), ingest.IdDict()
+        u, i, s, ts = parse_ratings(lines, users, items, self.decay_factor,
+                                    self.decay_zero_threshold)
+        ucode, utab = shuffle.unify_ids(users.keys(), ctx)
+        icode, itab = shuffle.unify_ids(items.keys(), ctx)
+        gu = ucode[u] if len(u) else u
+        gi = icode[i] if len(i) else i
+        return gu, gi, s, ts, utab, itab
+
+    def _build_sharded(self, context, lines, features, lam, alpha, candidate_path):
+        ctx = self._ctx(context)
+        W = ctx.world_size
+        t_parse = time.perf_counter()
+        gu, gi, s, ts, utab, itab = self._parse_global(lines, ctx)
+        # events of one user on one rank, for the time-ordered aggregation
+        gu, gi, s, ts = shuffle.route(gu % W, ctx, gu, gi, s, ts)
+        au, ai, av = aggregate_scores(gu, gi, s, ts, self.implicit)
+        used_u = np.zeros(utab.total, dtype=np.int32)
+        used_i = np.zeros(itab.total, dtype=np.int32)
+        used_u[au] = 1
+        used_i[ai] = 1
+        used_u = shuffle.all_reduce_np(used_u, ctx) > 0
+        used_i = shuffle.all_reduce_np(used_i, ctx) > 0
+        nu, ni = int(used_u.sum()), int(used_i.sum())
+        n_ratings = int(sum(shuffle.all_gather_int(len(au), ctx)))
+        parse_s = time.perf_counter() - t_parse
+        if n_ratings == 0:
+            log.info("No ratings after aggregation")
+            return None
+        dense_u = np.cumsum(used_u) - 1
+        dense_i = np.cumsum(used_i) - 1
+        seed = rng.next_seed()
+        trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx, seed=seed,
+                             precision=self.precision)
+        t0 = time.perf_counter()
+        trainer.prepare(torch.from_numpy(dense_u[au]), torch.from_numpy(dense_i[ai]),
+                        torch.from_numpy(av.astype(np.float32)), nu, ni)
+        x_ids = shuffle.gather_strings(utab, ctx, keep=used_u)
+        y_ids = shuffle.gather_strings(itab, ctx, keep=used_i)
+        x_init = y_init = None
+        if self.warm_start and self.current_model_dir:
+            x_init, y_init = _warm_start_factors(self.current_model_dir, features, x_ids, y_ids)
+        f = trainer.train(self.iterations, x_init=x_init, y_init=y_init)
+        X = f.X.cpu().numpy()
+        Y = f.Y.cpu().numpy()
+        log.info("ALS (sharded, %d ranks) %d ratings, %d users, %d items, rank %d: %.3fs", W,
+                 n_ratings, nu, ni, features, time.perf_counter() - t0)
+        if ctx.is_main:
+            write_features(os.path.join(candidate_path, "X"), x_ids, X)
+            write_features(os.path.join(candidate_path, "Y"), y_ids, Y)
+        pmml = pmmlu.build_skeleton_pmml()
+        pmml.add_extension("X", "X/")
+        pmml.add_extension("Y", "Y/")
+        pmml.add_extension("features", features)
+        pmml.add_extension("lambda", lam)
+        pmml.add_extension("implicit", self.implicit)
+        if self.implicit:
+            pmml.add_extension("alpha", alpha)
+        pmml.add_extension_content("XIDs", x_ids)
+        pmml.add_extension_content("YIDs", y_ids)
+        # every rank keeps what evaluation needs: factors, its dictionary share, dense maps
+        self._cache[candidate_path] = {
+            "x_ids": x_ids, "y_ids": y_ids, "X": X, "Y": Y, "utab": utab, "itab": itab,
+            "dense_u": np.where(used_u, dense_u, -1), "dense_i": np.where(used_i, dense_i, -1)}
+        its = trainer.timings.get("iteration_ms", [])
+        self._timings[candidate_path] = {
+            "ratings": n_ratings, "users": nu, "items": ni, "ranks": W,
+            "parse_shuffle_aggregate_s": parse_s,
+            "prepare_s": trainer.timings.get("prepare_s"), "iteration_ms": its,
+            "ratings_per_s": (n_ratings * 1e3 / (sum(its) / len(its))) if its else None}
+        return pmml
+
+    def _evaluate_sharded(self, context, model_parent_path, test_data):
+        ctx = self._ctx(context)
+        f = self._cache.pop(model_parent_path)
+        users, items = ingest.IdDict(), ingest.IdDict()
+        u, i, s, ts = parse_ratings(test_data, users, items, self.decay_factor,
+                                    self.decay_zero_threshold)
+        ucode = shuffle.lookup(users.keys(), f["utab"], ctx, mapping=f["dense_u"])
+        icode = shuffle.lookup(items.keys(), f["itab"], ctx, mapping=f["dense_i"])
+        # unknown test IDs keep a private negative code per string so aggregation still
+        # separates them (they are dropped afterwards)
+        gu = np.where(ucode[u] >= 0, ucode[u], -1 - u) if len(u) else u
+        gi = np.where(icode[i] >= 0, icode[i], -1 - i) if len(i) else i
+        W = ctx.world_size
+        owner = np.where(gu >= 0, gu % W, ctx.rank)
+        gu, gi, s, ts = shuffle.route(owner, ctx, gu, gi, s, ts)
+        # aggregate on compact codes (unknown IDs carry negative placeholders)
+        uu, uinv = np.unique(gu, return_inverse=True)
+        ii, iinv = np.unique(gi, return_inverse=True)
+        au, ai, av = aggregate_scores(uinv.astype(np.int64), iinv.astype(np.int64), s, ts,
+                                      self.implicit)
+        au, ai = (uu[au], ii[ai]) if len(au) else (au, ai)
+        device = ctx.device
+        X = torch.from_numpy(f["X"]).to(device)
+        Y = torch.from_numpy(f["Y"]).to(device)
+        mu = np.where(au >= 0, au, -1)
+        mi = np.where(ai >= 0, ai, -1)
+        if self.implicit:
+            known = (mu >= 0) & (mi >= 0)
+            items_all = np.unique(np.concatenate(shuffle.all_gather_var(
+                np.unique(mi[known]).astype(np.int64), ctx)))
+            tot, cnt = evaluation.auc_parts(X, Y, mu, mi, items_all, device=device)
+            tc = shuffle.all_reduce_np(np.array([tot, cnt], dtype=np.float64), ctx)
+            auc = float(tc[0] / tc[1]) if tc[1] > 0 else float("nan")
+            log.info("AUC: %s", auc)
+            return auc
+        se, n = evaluation.squared_error_parts(X, Y, mu, mi, av, device=device)
+        tc = shuffle.all_reduce_np(np.array([se, n], dtype=np.float64), ctx)
+        rmse = math.sqrt(tc[0] / tc[1]) if tc[1] > 0 else float("nan")
+        log.info("RMSE: %s", rmse)
+        return -rmse
+
+    def _publish_sharded(self, context, pmml, new_data, past_data, model_parent_path, topic):
+        ctx = self._ctx(context)
+        W, R = ctx.world_size, ctx.rank
+        x_ids, X = read_features(os.path.join(model_parent_path, pmml.get_extension_value("X")))
+        y_ids, Y = read_features(os.path.join(model_parent_path, pmml.get_extension_value("Y")))
+        mine = np.arange(R, len(y_ids), W)
+        log.info("Rank %d sending %d item / Y rows as model updates", R, len(mine))
+        rows = ingest.format_float_rows(Y[mine]) if len(mine) else []
+        topic.send_many(("UP", '["Y",%s,%s]' % (json.dumps(y_ids[j]), r))
+                        for j, r in zip(mine.tolist(), rows))
+        dist.barrier(ctx)
+        # users owned by this rank (crc32 owner of the ID) with their known items
+        all_lines = list(new_data) + list(past_data or [])
+        if self.no_known_items:
+            owned = np.nonzero(shuffle.owner_of_strings(x_ids, W) == R)[0]
+            xr = ingest.format_float_rows(X[owned]) if len(owned) else []
+            topic.send_many(("UP", '["X",%s,%s]' % (json.dumps(x_ids[j]), r))
+                            for j, r in zip(owned.tolist(), xr))
+        else:
+            known = _known_items_sharded(all_lines, ctx)
+            xmap = {k: j for j, k in enumerate(x_ids)}
+            sel = [(xmap[uid], uid) for uid in known if uid in xmap]
+            sel.sort()
+            idx = np.array([j for j, _ in sel], dtype=np.int64)
+            xr = ingest.format_float_rows(X[idx]) if len(idx) else []
+            log.info("Rank %d sending %d user / X rows as model updates", R, len(idx))
+            topic.send_many(("UP", '["X",%s,%s,%s]' % (json.dumps(uid), r,
+                                                        json.dumps(sorted(known[uid]))))
+                            for (_, uid), r in zip(sel, xr))
+        dist.barrier(ctx)
+
     def build_timings(self, candidate_path: str) -> dict:
         return self._timings.pop(candidate_path, {})
 
@@ -297,6 +465,8 @@ class ALSUpdate(MLUpdate):
         return {"x_ids": x_ids, "y_ids": y_ids, "X": X, "Y": Y}
 
     def evaluate(self, context, model, model_parent_path, test_data, train_data):
+        if self._sharded(context):
+            return self._evaluate_sharded(context, model_parent_path, test_data)
         f = self._load(model_parent_path, model)
         users, items = ingest.IdDict(), ingest.IdDict()
         u, i, s, ts = parse_ratings(test_data, users, items, self.decay_factor,
@@ -325,6 +495,10 @@ class ALSUpdate(MLUpdate):
 
     def publish_additional_model_data(self, context, pmml, new_data, past_data,
                                       model_parent_path, model_update_topic):
+        if self._sharded(context):
+            self._publish_sharded(context, pmml, new_data, past_data, model_parent_path,
+                                  model_update_topic)
+            return
         all_data = list(new_data) + list(past_data or [])
         x_ids, X = read_features(os.path.join(model_parent_path, pmml.get_extension_value("X")))
         y_ids, Y = read_features(os.path.join(model_parent_path, pmml.get_extension_value("Y")))
@@ -351,9 +525,20 @@ class ALSUpdate(MLUpdate):
     # ---------------------------------------------------------------- split
     def split_new_data_to_train_test(self, new_data):
         ts = _timestamps(new_data)
-        if len(ts) == 0:
+        sharded = self.dist_ctx is not None and self.dist_ctx.is_distributed
+        if sharded:
+            # the boundary comes from the global timestamp range of the new data
+            big = np.iinfo(np.int64).max
+            mm = shuffle.all_reduce_np(np.array([-(int(ts.min()) if len(ts) else big),
+                                                 int(ts.max()) if len(ts) else -big],
+                                                dtype=np.int64), self.dist_ctx, op="max")
+            if mm[1] == -big:
+                return list(new_data), []
+            lo, hi = int(-mm[0]), int(mm[1])
+        elif len(ts) == 0:
             return list(new_data), []
-        lo, hi = int(ts.min()), int(ts.max())
+        else:
+            lo, hi = int(ts.min()), int(ts.max())
         log.info("New data timestamp range: %d - %d", lo, hi)
         boundary = int(hi - self.get_test_fraction() * (hi - lo))
         log.info("Splitting at timestamp %d", boundary)
@@ -369,6 +554,37 @@ class ALSUpdate(MLUpdate):
                     continue
                 (train if int(t[0]) < boundary else test).append(line)
         return train, test
+
+
+def _known_items_sharded(lines: Sequence[str], ctx) -> Dict[str, set]:
+    """Known items of the users this rank owns (crc32 owner), from every rank's lines."""
+    users, items = ingest.IdDict(), ingest.IdDict()
+    u, i, s, ts = ingest.parse_ratings(lines, users, items, default_ts=0)
+    uk, ik = users.keys(), items.keys()
+    W = ctx.world_size
+    # ship (user, item, strength, ts) rows to the user's owner as dictionary codes of a
+    # global table, then decide per pair by the last event
+    ucode, utab = shuffle.unify_ids(uk, ctx)
+    icode, itab = shuffle.unify_ids(ik, ctx)
+    gu = ucode[u] if len(u) else u
+    gi = icode[i] if len(i) else i
+    owner = shuffle.owner_of_strings(uk, W)[u] if len(u) else u
+    gu, gi, s, ts = shuffle.route(owner, ctx, gu, gi, s, ts)
+    ustr = shuffle.gather_strings(utab, ctx)
+    istr = shuffle.gather_strings(itab, ctx)
+    out: Dict[str, set] = {ustr[a]: set() for a in np.unique(gu).tolist()}
+    if len(gu) == 0:
+        return out
+    n_i = int(gi.max()) + 1
+    key = gu * n_i + gi
+    order = np.lexsort((np.arange(len(key)), ts, key))
+    key_s, s_s = key[order], s[order]
+    last = np.r_[key_s[1:] != key_s[:-1], True]
+    keep = last & ~np.isnan(s_s)
+    kk = key_s[keep]
+    for a, b in zip((kk // n_i).tolist(), (kk % n_i).tolist()):
+        out[ustr[a]].add(istr[b])
+    return out
 
 
 def known_items(lines: Sequence[str]) -> Dict[str, set]:

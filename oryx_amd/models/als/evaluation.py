@@ -14,6 +14,7 @@
 from __future__ import annotations
 
 import math
+from typing import Optional, Tuple
 
 import numpy as np
 import torch
@@ -44,15 +45,39 @@ def rmse(X: torch.Tensor, Y: torch.Tensor, u: np.ndarray, i: np.ndarray, r: np.n
     return float(torch.sqrt(((pred - rr) ** 2).mean()).item())
 
 
+def squared_error_parts(X: torch.Tensor, Y: torch.Tensor, u: np.ndarray, i: np.ndarray,
+                        r: np.ndarray, device=None) -> Tuple[float, int]:
+    """(sum of squared errors, count) over the pairs with known IDs (sharded RMSE)."""
+    ok = (u >= 0) & (i >= 0)
+    if not ok.any():
+        return 0.0, 0
+    dev = X.device
+    uu = torch.from_numpy(u[ok]).to(dev)
+    ii = torch.from_numpy(i[ok]).to(dev)
+    rr = torch.from_numpy(r[ok].astype(np.float64)).to(dev)
+    pred = (X[uu].double() * Y[ii].double()).sum(1)
+    return float(((pred - rr) ** 2).sum().item()), int(ok.sum())
+
+
 def area_under_curve(X: torch.Tensor, Y: torch.Tensor, u: np.ndarray, i: np.ndarray,
                      device=None, seed=None) -> float:
+    tot, cnt = auc_parts(X, Y, u, i, None, device=device, seed=seed)
+    return tot / cnt if cnt else float("nan")
+
+
+def auc_parts(X: torch.Tensor, Y: torch.Tensor, u: np.ndarray, i: np.ndarray,
+              all_items: Optional[np.ndarray], device=None, seed=None) -> Tuple[float, int]:
+    """(sum of per-user AUCs, number of users) -- the mean over users is the reference's AUC
+    (``[mllib]/als/Evaluation.java:70-136``); ``all_items`` is the negative-sampling universe
+    (default: the distinct items of these pairs; sharded callers pass the global set)."""
     ok = (u >= 0) & (i >= 0)
     u, i = u[ok], i[ok]
     if len(u) == 0:
-        return float("nan")
+        return 0.0, 0
     dev = X.device
     gen = rng.get_random().generator if seed is None else np.random.default_rng(seed)
-    all_items = np.unique(i)
+    if all_items is None:
+        all_items = np.unique(i)
     n_items = len(all_items)
     # positives per user
     order = np.argsort(u, kind="stable")
@@ -79,7 +104,7 @@ def area_under_curve(X: torch.Tensor, Y: torch.Tensor, u: np.ndarray, i: np.ndar
                 neg_i.append(item)
                 got += 1
     if not neg_u:
-        return float("nan")
+        return 0.0, 0
     nu = np.asarray(neg_u, dtype=np.int64)
     ni = np.asarray(neg_i, dtype=np.int64)
     tu = torch.from_numpy(np.concatenate([u_s, nu])).to(dev)
@@ -109,4 +134,4 @@ def area_under_curve(X: torch.Tensor, Y: torch.Tensor, u: np.ndarray, i: np.ndar
         0, seg_id, (~sp).double())
     valid = (n_pos > 0) & (n_neg > 0)
     auc_u = correct[valid] / (n_pos[valid] * n_neg[valid])
-    return float(auc_u.mean().item()) if auc_u.numel() else float("nan")
+    return float(auc_u.sum().item()), int(auc_u.numel())

@@ -42,6 +42,8 @@ _INIT_STRATEGIES = ("k-means||", "random")
 
 
 class KMeansUpdate(MLUpdate):
+    sharded_data = True
+
     def __init__(self, config):
         super().__init__(config)
         self.initialization_strategy = config.get_string("oryx.kmeans.initialization-strategy")
@@ -73,17 +75,29 @@ class KMeansUpdate(MLUpdate):
         c = getattr(context, "dist", None)
         return c if c is not None else dist.get_context()
 
+    def _sharded(self, ctx) -> bool:
+        return ctx.is_distributed and self.dist_ctx is not None and self.dist_ctx.is_distributed
+
     def build_model(self, context, train_data, hyper_parameters, candidate_path):
         k = int(hyper_parameters[0])
         if k <= 1:
             raise ValueError("k must be > 1")
         ctx = self._ctx(context)
         x = parse_feature_matrix(list(train_data), self.input_schema)
-        if len(x) == 0:
+        sharded = self._sharded(ctx)
+        if sharded:
+            from ...parallel import shuffle
+            if sum(shuffle.all_gather_int(len(x), ctx)) == 0:
+                return None
+            if len(x) == 0:
+                x = np.zeros((0, self.input_schema.get_num_predictors()), dtype=np.float64)
+        elif len(x) == 0:
             return None
         t0 = time.perf_counter()
-        # each rank takes a disjoint slice of the (identical) parsed records
-        local = torch.from_numpy(x[ctx.rank::ctx.world_size].astype(np.float32)).to(ctx.device)
+        # sharded: this rank's share of the records; otherwise every rank parsed everything
+        # and takes a disjoint slice
+        rows = x if sharded else x[ctx.rank::ctx.world_size]
+        local = torch.from_numpy(rows.astype(np.float32)).to(ctx.device)
         res = km_ops.kmeans_train(local, k, self.max_iterations, self.number_of_runs,
                                   self.initialization_strategy, seed=rng.next_seed(),
                                   ctx=ctx, precision=self.precision)
@@ -91,7 +105,7 @@ class KMeansUpdate(MLUpdate):
         sizes = res.counts.cpu().numpy()
         log.info("k-means k=%d on %d points x %d: cost %.6g, %d iterations, %.3fs", k, len(x),
                  x.shape[1], res.cost, res.iterations, time.perf_counter() - t0)
-        if not ctx.is_main:
+        if not ctx.is_main and not sharded:
             return None
         return clustering_model_pmml(self.input_schema, centers, sizes)
 
@@ -100,6 +114,12 @@ class KMeansUpdate(MLUpdate):
         x = parse_feature_matrix(list(train_data) + list(test_data), self.input_schema)
         clusters = read_clusters(model)
         ctx = self._ctx(context)
-        ev = evaluation.evaluate(self.evaluation_strategy, clusters, x, device=ctx.device)
+        if self._sharded(ctx):
+            if len(x) == 0:
+                x = np.zeros((0, len(clusters[0].center)), dtype=np.float64)
+            ev = evaluation.evaluate_sharded(self.evaluation_strategy, clusters, x, ctx,
+                                             device=ctx.device)
+        else:
+            ev = evaluation.evaluate(self.evaluation_strategy, clusters, x, device=ctx.device)
         log.info("k-means eval (%s): %s", self.evaluation_strategy, ev)
         return ev

@@ -10,6 +10,12 @@ The per-point nearest-center assignment and the per-cluster (count, sum d, sum d
 run as batched float64 tensor ops on the device; the silhouette's O(S^2) pairwise distances
 are computed tile by tile and reduced per cluster with one GEMM against the cluster one-hot
 matrix (sum_j d(p, j) for every cluster at once), never materialising S x S.
+
+Sharded (:func:`evaluate_sharded`): every rank assigns its own points with the certified fp32
+MFMA kernel (large GPU shares) or the float64 scan, takes float64 distances to the chosen
+centers, and the K x 3 cluster metrics are all-reduced; Davies-Bouldin and Dunn then come from
+one K x K center-distance matrix; the silhouette sample is drawn per rank (the same keep
+probability everywhere) and gathered, and rank 0's value is broadcast.
 """
 
 from __future__ import annotations
@@ -25,7 +31,8 @@ from .common import ClusterInfo
 
 __all__ = ["ClusterMetric", "fetch_cluster_metrics", "sum_squared_error", "davies_bouldin_index",
            "dunn_index", "silhouette_coefficient", "silhouette_of", "fetch_sample_data",
-           "MAX_SAMPLE_SIZE", "EVAL_STRATEGIES", "evaluate"]
+           "MAX_SAMPLE_SIZE", "EVAL_STRATEGIES", "evaluate", "evaluate_sharded",
+           "local_cluster_stats"]
 
 MAX_SAMPLE_SIZE = 100000
 EVAL_STRATEGIES = ("SSE", "DAVIES_BOULDIN", "DUNN", "SILHOUETTE")
@@ -99,34 +106,15 @@ def _center_dist(a: ClusterInfo, b: ClusterInfo) -> float:
 
 
 def davies_bouldin_index(clusters, data, device=None) -> float:
-    """Mean over clusters i of max_j (s_i + s_j) / d(c_i, c_j) (not symmetric in i, j)."""
-    metrics = fetch_cluster_metrics(clusters, data, device)
+    """Mean over clusters i of max_j (s_i + s_j) / d(c_i, c_j) (not symmetric in i, j); one
+    K x K center-distance matrix instead of the reference's double loop."""
     by_id = sorted(clusters, key=lambda c: c.id)
-    vals = []
-    for ci in by_id:
-        if ci.id not in metrics:
-            continue
-        si = metrics[ci.id].get_mean_dist()
-        best = 0.0
-        for cj in by_id:
-            if cj.id == ci.id or cj.id not in metrics:
-                continue
-            r = (si + metrics[cj.id].get_mean_dist()) / _center_dist(ci, cj)
-            best = max(best, r)
-        vals.append(best)
-    return sum(vals) / len(vals) if vals else 0.0
+    return _db_from(by_id, fetch_cluster_metrics(by_id, data, device))
 
 
 def dunn_index(clusters, data, device=None) -> float:
     """min inter-center distance / max mean intra-cluster distance."""
-    metrics = fetch_cluster_metrics(clusters, data, device)
-    max_intra = max((m.get_mean_dist() for m in metrics.values()), default=float("nan"))
-    min_inter = float("inf")
-    cl = list(clusters)
-    for i in range(len(cl)):
-        for j in range(i + 1, len(cl)):
-            min_inter = min(min_inter, _center_dist(cl[i], cl[j]))
-    return min_inter / max_intra
+    return _dunn_from(list(clusters), fetch_cluster_metrics(clusters, data, device))
 
 
 def silhouette_of(ai: float, bi: float) -> float:
@@ -184,6 +172,86 @@ def silhouette_coefficient(clusters, data, device=None, max_sample: int = MAX_SA
         sil = torch.where(own_size > 1, sil, torch.zeros_like(sil))
         total += sil.sum()
     return float(total) / s
+
+
+def _metrics_from_arrays(clusters, cnt, s1, s2) -> Dict[int, ClusterMetric]:
+    return {clusters[j].id: ClusterMetric(int(cnt[j]), float(s1[j]), float(s2[j]))
+            for j in range(len(clusters)) if cnt[j] > 0}
+
+
+def local_cluster_stats(clusters, x: np.ndarray, device=None) -> np.ndarray:
+    """[K, 3] float64 (count, sum d, sum d^2) of this rank's points ``x``."""
+    dev = _device(device)
+    k = len(clusters)
+    out = np.zeros((k, 3), dtype=np.float64)
+    if len(x) == 0:
+        return out
+    c = _centers(clusters, dev)
+    xt = torch.as_tensor(np.asarray(x, dtype=np.float64)).to(dev)
+    if dev.type == "cuda" and len(x) >= 65536:
+        from ...ops import kmeans as km_ops
+        idx, _ = km_ops.assign(xt.float(), c.float(), precision="fp32")
+        idx = idx.long()
+        dist = (xt - c[idx]).pow(2).sum(1).sqrt()
+    else:
+        idx, dist = _assign(xt, c)
+    out[:, 0] = torch.bincount(idx, minlength=k).double().cpu().numpy()
+    out[:, 1] = torch.zeros(k, dtype=torch.float64, device=dev).index_add_(
+        0, idx, dist).cpu().numpy()
+    out[:, 2] = torch.zeros(k, dtype=torch.float64, device=dev).index_add_(
+        0, idx, dist * dist).cpu().numpy()
+    return out
+
+
+def _db_from(clusters, metrics) -> float:
+    ids = [c.id for c in clusters]
+    present = np.array([i in metrics for i in ids])
+    if not present.any():
+        return 0.0
+    cen = np.stack([c.center for c in clusters]).astype(np.float64)
+    mean = np.array([metrics[i].get_mean_dist() if i in metrics else 0.0 for i in ids])
+    dd = np.sqrt(((cen[:, None, :] - cen[None]) ** 2).sum(2))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = (mean[:, None] + mean[None, :]) / dd
+    r[~present[:, None] | ~present[None, :]] = 0.0
+    np.fill_diagonal(r, 0.0)
+    r = np.where(np.isfinite(r), r, 0.0)
+    return float(r.max(1)[present].mean())
+
+
+def _dunn_from(clusters, metrics) -> float:
+    max_intra = max((m.get_mean_dist() for m in metrics.values()), default=float("nan"))
+    cen = np.stack([c.center for c in clusters]).astype(np.float64)
+    dd = np.sqrt(((cen[:, None, :] - cen[None]) ** 2).sum(2))
+    iu = np.triu_indices(len(clusters), 1)
+    min_inter = float(dd[iu].min()) if len(iu[0]) else float("inf")
+    return min_inter / max_intra
+
+
+def evaluate_sharded(strategy: str, clusters, x_local: np.ndarray, ctx, device=None) -> float:
+    """Like :func:`evaluate` over the union of every rank's ``x_local`` (collective)."""
+    from ...parallel import shuffle, dist as dist_
+    if strategy == "SILHOUETTE":
+        n_all = sum(shuffle.all_gather_int(len(x_local), ctx))
+        p = min(1.0, MAX_SAMPLE_SIZE / max(1, n_all))
+        keep = rng.get_random().generator.random(len(x_local)) < p
+        samp = np.asarray(x_local, dtype=np.float64)[keep]
+        d = np.asarray(x_local).shape[1] if np.asarray(x_local).ndim == 2 else \
+            len(clusters[0].center)
+        parts = shuffle.all_gather_var(samp.reshape(-1), ctx)
+        sample = np.concatenate(parts).reshape(-1, d)
+        val = silhouette_coefficient(clusters, sample, device, max_sample=len(sample) + 1) \
+            if ctx.is_main else 0.0
+        return float(dist_.broadcast_object(val, ctx))
+    stats = shuffle.all_reduce_np(local_cluster_stats(clusters, x_local, device), ctx)
+    metrics = _metrics_from_arrays(clusters, stats[:, 0], stats[:, 1], stats[:, 2])
+    if strategy == "SSE":
+        return -math.fsum(m.sum_squared_dist for m in metrics.values())
+    if strategy == "DAVIES_BOULDIN":
+        return -_db_from(clusters, metrics)
+    if strategy == "DUNN":
+        return _dunn_from(clusters, metrics)
+    raise ValueError("Unknown evaluation strategy " + strategy)
 
 
 def evaluate(strategy: str, clusters, data, device=None) -> float:

@@ -78,3 +78,106 @@ def test_two_rank_batch_generation(tmp_path):
     # exactly one generation dir was published
     dirs = [d for d in os.listdir(tmp_path / "model") if not d.startswith(".")]
     assert len(dirs) == 1
+
+
+ALS_SCRIPT = r"""
+import json, os, sys
+sys.path.insert(0, ROOT)
+import numpy as np
+from oryx_amd.layers.batch import BatchLayer
+from oryx_amd.parallel import dist
+from oryx_amd.transport.producer import LogTopicProducer
+from oryx_amd.utils import config as cfg
+
+tmp = sys.argv[1]
+conf = cfg.overlay_on({
+    "oryx.batch.update-class": "com.cloudera.oryx.app.batch.mllib.als.ALSUpdate",
+    "oryx.input-topic.broker": "log:" + tmp + "/log",
+    "oryx.update-topic.broker": "log:" + tmp + "/log",
+    "oryx.input-topic.partitions": 3,
+    "oryx.batch.storage.data-dir": tmp + "/data",
+    "oryx.batch.storage.model-dir": tmp + "/model",
+    "oryx.als.hyperparams.features": 4,
+    "oryx.als.iterations": 3,
+    "oryx.als.implicit": "true",
+    "oryx.ml.eval.candidates": 2,
+    "oryx.ml.eval.test-fraction": 0.2,
+    "oryx.gpu.device": "cpu",
+}, cfg.get_default())
+ctx = dist.init_from_env(device="cpu")
+layer = BatchLayer(conf)
+if ctx.is_main:
+    layer._context = layer.layer_context()
+    layer._update = layer.load_update_instance()
+    layer.build_input_consumer()
+    g = np.random.default_rng(1)
+    for gen in range(2):
+        lines = ["U%d,I%d,%d,%d" % (g.integers(0, 40), g.integers(0, 25), g.integers(1, 5),
+                                    1000 * gen + j) for j in range(600)]
+        prod = LogTopicProducer("log:" + tmp + "/log", "OryxInput", conf, async_=False)
+        prod.send_many([(None, l) for l in lines])
+        prod.close()
+        with open(os.path.join(tmp, "input%d.txt" % gen), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        layer.run_interval(1000 + gen)
+    layer.close()
+    out = {"rank": 0}
+else:
+    out = {"rank": 1, "joined": layer.run_follower()}
+with open(os.path.join(tmp, "rank%d.json" % ctx.rank), "w") as f:
+    json.dump(out, f)
+"""
+
+
+def test_two_rank_sharded_als_generations(tmp_path):
+    """ALS on 2 gloo ranks with sharded generations: each rank reads its own share of the 3
+    input partitions (the part files are disjoint and cover the input), the second generation
+    reads past data per rank, one MODEL per generation, Y rows then X rows with known items
+    from both ranks."""
+    import json
+    script = tmp_path / "run.py"
+    script.write_text(ALS_SCRIPT.replace("ROOT", repr(ROOT)))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29643", str(script), str(tmp_path)]
+    r = subprocess.run(cmd, env=env, timeout=600, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert json.loads((tmp_path / "rank1.json").read_text())["joined"] == 2
+    for gen in range(2):
+        d = tmp_path / "data" / ("oryx-%d.data" % (1000 + gen))
+        parts = sorted(os.listdir(d))
+        assert parts == ["part-00000", "part-00001"]
+        got = [[json.loads(l)[1] for l in open(d / p)] for p in parts]
+        assert got[0] and got[1]
+        inp = open(tmp_path / ("input%d.txt" % gen)).read().split()
+        assert sorted(got[0] + got[1]) == sorted(inp)
+    from oryx_amd.transport import log as tlog
+    topic = tlog.Topic(str(tmp_path / "log"), "OryxUpdate")
+    c = tlog.TopicConsumer(topic, "earliest")
+    msgs = []
+    while True:
+        batch = [(k, m) for _, _, _, k, m in c.poll(10000, 200)]
+        if not batch:
+            break
+        msgs.extend(batch)
+    c.close()
+    keys = [k for k, _ in msgs]
+    assert keys.count("MODEL") == 2
+    # the second generation: every item and user of both generations, Y before X
+    second = msgs[keys.index("MODEL", keys.index("MODEL") + 1) + 1:]
+    ups = [json.loads(m) for k, m in second if k == "UP"]
+    kinds = [u[0] for u in ups]
+    assert kinds == sorted(kinds, key=lambda t: t != "Y")
+    lines = open(tmp_path / "input0.txt").read().split() + \
+        open(tmp_path / "input1.txt").read().split()
+    users = {l.split(",")[0] for l in lines}
+    items = {l.split(",")[1] for l in lines}
+    assert {u[1] for u in ups if u[0] == "Y"} == items
+    xs = {u[1]: set(u[3]) for u in ups if u[0] == "X"}
+    assert set(xs) == users
+    # known items = every (user, item) pair seen (no deletes in this data)
+    want = {}
+    for l in lines:
+        a, b = l.split(",")[:2]
+        want.setdefault(a, set()).add(b)
+    assert xs == want

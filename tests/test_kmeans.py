@@ -583,3 +583,66 @@ def test_counting_sort_kernel_groups_every_row(cuda, n, k):
     assert torch.equal(torch.sort(p).values, torch.arange(n))
     grouped = keys.long()[p]
     assert torch.equal(grouped, torch.repeat_interleave(torch.arange(k), ref_counts))
+
+
+def test_vectorised_db_dunn_match_loops():
+    """The K x K matrix forms of Davies-Bouldin / Dunn equal the reference's double loops."""
+    pts, cents = _blobs(n_per=300)
+    g = np.random.default_rng(4)
+    clusters = [ClusterInfo(i, c + g.normal(0, 0.2, 4), 1) for i, c in enumerate(cents)]
+    m = ev.fetch_cluster_metrics(clusters, pts, "cpu")
+    vals = []
+    for ci in clusters:
+        si = m[ci.id].get_mean_dist()
+        vals.append(max((si + m[cj.id].get_mean_dist()) / np.linalg.norm(ci.center - cj.center)
+                        for cj in clusters if cj.id != ci.id))
+    assert ev.davies_bouldin_index(clusters, pts, "cpu") == pytest.approx(np.mean(vals), 1e-12)
+    inter = min(np.linalg.norm(a.center - b.center) for a in clusters for b in clusters
+                if a.id < b.id)
+    intra = max(x.get_mean_dist() for x in m.values())
+    assert ev.dunn_index(clusters, pts, "cpu") == pytest.approx(inter / intra, 1e-12)
+
+
+EVAL_SCRIPT = r"""
+import json, os, sys
+sys.path.insert(0, ROOT)
+import numpy as np
+from oryx_amd.models.kmeans import evaluation as ev
+from oryx_amd.models.kmeans.common import ClusterInfo
+from oryx_amd.parallel import dist
+from oryx_amd.utils import rng
+ctx = dist.init_from_env(device="cpu")
+g = np.random.default_rng(0)
+cents = np.array([[0, 0, 0], [6, 6, 0], [-6, 6, 2]], float)
+pts = np.concatenate([g.normal(c, 0.7, (400, 3)) for c in cents])
+clusters = [ClusterInfo(i, c, 1) for i, c in enumerate(cents)]
+mine = pts[ctx.rank::ctx.world_size]
+out = {}
+for s in ("SSE", "DAVIES_BOULDIN", "DUNN"):
+    out[s] = ev.evaluate_sharded(s, clusters, mine, ctx, device="cpu")
+    out[s + "_1"] = ev.evaluate(s, clusters, pts, device="cpu")
+with rng.shared_seed_scope(5):
+    out["SIL"] = ev.evaluate_sharded("SILHOUETTE", clusters, mine, ctx, device="cpu")
+out["SIL_1"] = ev.evaluate("SILHOUETTE", clusters, pts, device="cpu")
+with open(os.path.join(sys.argv[1], "r%d.json" % ctx.rank), "w") as f:
+    json.dump(out, f)
+"""
+
+
+def test_sharded_eval_metrics_equal_single_process(tmp_path):
+    """World-2 (gloo) cluster metrics over point shards == world-1 over all points."""
+    import json, os, subprocess, sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "ev.py"
+    script.write_text(EVAL_SCRIPT.replace("ROOT", repr(root)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", "--master-port=29647", str(script), str(tmp_path)]
+    r = subprocess.run(cmd, env=dict(os.environ, OMP_NUM_THREADS="1"), timeout=300,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    a = json.loads((tmp_path / "r0.json").read_text())
+    b = json.loads((tmp_path / "r1.json").read_text())
+    for s in ("SSE", "DAVIES_BOULDIN", "DUNN"):
+        assert a[s] == pytest.approx(a[s + "_1"], rel=1e-12) and a[s] == b[s]
+    # 1200 points < the 100k cap: the sample is everything on both sides
+    assert a["SIL"] == pytest.approx(a["SIL_1"], rel=1e-9) and a["SIL"] == b["SIL"]
