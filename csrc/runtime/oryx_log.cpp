@@ -562,6 +562,89 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
   return count;
 }
 
+// Bulk text read for the batch layer's drains: every record from the reader's position up
+// to `end_offset` (exclusive) appended to `out` as `value '\n'`, reading the segment files in
+// 4 MB blocks (one pread per block instead of two per record).  Returns the number of
+// records consumed (fewer than asked when `out` is full: call again), or -3 on a corrupt
+// frame.  *flags gets bit 0 when a record had a key and bit 1 when a value contained a
+// newline (the caller then uses the per-record path for those semantics).
+long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long long out_cap,
+                                long long* out_used, int* flags) {
+  auto* r = static_cast<Reader*>(rh);
+  const std::string& dir = r->topic->parts[r->part].dir;
+  constexpr size_t kBlock = 4u << 20;
+  std::vector<uint8_t> buf(kBlock);
+  long long used = 0, count = 0;
+  *flags = 0;
+  if (r->fd < 0) reader_seek(r, r->next_offset);
+  while (r->next_offset < end_offset) {
+    if (r->fd < 0) break;
+    ssize_t got = pread(r->fd, buf.data(), buf.size(), r->pos);
+    size_t at = 0;
+    bool need_more = false;
+    while (got > 0 && at + kHeader <= (size_t)got && r->next_offset < end_offset) {
+      const uint8_t* h = buf.data() + at;
+      uint32_t magic, crc, klen, vlen;
+      uint64_t off;
+      memcpy(&magic, h, 4); memcpy(&crc, h + 4, 4); memcpy(&off, h + 8, 8);
+      memcpy(&klen, h + 24, 4); memcpy(&vlen, h + 28, 4);
+      if (magic != kMagic) { got = 0; break; }
+      size_t kl = klen == kNullKey ? 0 : klen;
+      size_t plen = kl + vlen;
+      if (at + kHeader + plen > (size_t)got) {
+        // frame straddles the block: re-read from its start (grow for huge frames)
+        if (kHeader + plen > buf.size()) buf.resize(kHeader + plen);
+        need_more = true;
+        break;
+      }
+      // crc covers offset | ts | key | value (the 16 header bytes at +8 and the payload)
+      uint32_t c = crc32(h + 8, 16);
+      c = crc32(h + kHeader, plen, c);
+      if (c != crc) {
+        *out_used = used;
+        fail("corrupt record (crc mismatch) in " + dir + " at offset " +
+             std::to_string(r->next_offset));
+        return -3;
+      }
+      if ((long long)off >= end_offset) { r->next_offset = end_offset; break; }
+      if (used + (long long)vlen + 1 > out_cap) {
+        *out_used = used;
+        return count;
+      }
+      if (klen != kNullKey) *flags |= 1;
+      const uint8_t* v = h + kHeader + kl;
+      if (memchr(v, '\n', vlen)) *flags |= 2;
+      memcpy(out + used, v, vlen);
+      out[used + vlen] = '\n';
+      used += vlen + 1;
+      at += kHeader + plen;
+      r->pos += kHeader + plen;
+      r->next_offset = (int64_t)off + 1;
+      ++count;
+    }
+    if (r->next_offset >= end_offset) break;
+    if (need_more) continue;
+    if (at == 0) {
+      // end of this segment file: move to the next one (records up to end_offset exist)
+      std::vector<int64_t> segs = list_segments(dir);
+      bool rolled = false;
+      for (int64_t b : segs) {
+        if (b > r->seg_base && b <= r->next_offset) {
+          close(r->fd);
+          r->seg_base = b;
+          r->pos = 0;
+          r->fd = open(seg_name(dir, b).c_str(), O_RDONLY);
+          rolled = true;
+          break;
+        }
+      }
+      if (!rolled) break;   // not written yet: deliver what there is
+    }
+  }
+  *out_used = used;
+  return count;
+}
+
 // ---- consumer-group offsets (ZooKeeper replacement) ----
 
 static std::string offsets_path(const char* root, const char* topic, const char* group) {

@@ -77,43 +77,76 @@ class Dataset:
 
     Plays the role of the reference's ``JavaPairRDD<K,M>``: batch updates receive the
     interval's new data and all past data.  Heavy numeric work happens after parsing, on
-    device tensors, so a plain list is the right container here.
+    device tensors, so a plain list is the right container here.  Data read in bulk from the
+    log or from text part files has no keys: it is held as the message list alone
+    (:meth:`from_values`), and pairs are only materialised if someone iterates them.
     """
 
-    __slots__ = ("_pairs",)
+    __slots__ = ("_pairs", "_values")
 
     def __init__(self, pairs: Iterable[Tuple[Any, Any]] = ()):
         self._pairs = list(pairs)
+        self._values = None
+
+    @classmethod
+    def from_values(cls, values: List[Any]) -> "Dataset":
+        """Messages with null keys (the list is kept, not copied)."""
+        d = cls.__new__(cls)
+        d._pairs = None
+        d._values = values
+        return d
+
+    def _p(self) -> List[Tuple[Any, Any]]:
+        if self._pairs is None:
+            self._pairs = [(None, v) for v in self._values]
+        return self._pairs
+
+    @property
+    def keyless(self) -> bool:
+        """True when every key is null and the messages are held as one list."""
+        return self._values is not None
 
     def __len__(self):
-        return len(self._pairs)
+        return len(self._values) if self._values is not None else len(self._pairs)
 
     def __iter__(self) -> Iterator[Tuple[Any, Any]]:
-        return iter(self._pairs)
+        return iter(self._p())
+
+    def __getstate__(self):
+        return (self._pairs if self._values is None else None, self._values)
+
+    def __setstate__(self, state):
+        self._pairs, self._values = state
 
     def is_empty(self) -> bool:
-        return not self._pairs
+        return len(self) == 0
 
     def count(self) -> int:
-        return len(self._pairs)
+        return len(self)
 
     def keys(self) -> List[Any]:
+        if self._values is not None:
+            return [None] * len(self._values)
         return [k for k, _ in self._pairs]
 
     def values(self) -> List[Any]:
+        if self._values is not None:
+            return self._values
         return [m for _, m in self._pairs]
 
     def union(self, other: "Dataset") -> "Dataset":
-        return Dataset(self._pairs + list(other))
+        if self.keyless and isinstance(other, Dataset) and other.keyless:
+            return Dataset.from_values(self._values + other._values)
+        return Dataset(self._p() + list(other))
 
     def filter(self, fn) -> "Dataset":
-        return Dataset(p for p in self._pairs if fn(p))
+        return Dataset(p for p in self._p() if fn(p))
 
     def map_values(self, fn) -> "Dataset":
-        return Dataset((k, fn(m)) for k, m in self._pairs)
+        return Dataset((k, fn(m)) for k, m in self._p())
 
     def collect(self) -> List[Tuple[Any, Any]]:
-        return list(self._pairs)
+        return list(self._p())
 
 
 class BatchLayerUpdate(abc.ABC, Generic[K, M, U]):

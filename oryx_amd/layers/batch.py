@@ -10,7 +10,9 @@ Equivalent of ``BatchLayer`` + ``BatchUpdateFunction`` + ``SaveToHDFSFunction`` 
 2. if non-empty: read all past data (``data-dir/*/part-*``), open a *synchronous* producer on
    the update topic and call the update class's ``run_update`` (the update runs before the
    save, so past data never includes the current interval);
-3. save the new data as ``data-dir/oryx-<ms>.data/part-00000`` (JSON lines ``[key,message]``);
+3. save the new data as ``data-dir/oryx-<ms>.data/part-00000.txt`` (the messages, one per
+   line, when no record has a key -- the common case, read back without per-record
+   decoding) or ``part-00000`` (JSON lines ``[key,message]``);
 4. commit input offsets (when ``oryx.id`` is set);
 5. delete data (and model) dirs older than ``max-age-data-hours`` (``max-age-model-hours``).
 
@@ -40,7 +42,7 @@ from ..transport.producer import LogTopicProducer
 from ..utils import config as cfg
 from ..parallel import dist
 from ..utils import faults, ioutils, lang, rng
-from .common import AbstractLayer, IntervalTimer, drain
+from .common import AbstractLayer, IntervalTimer, drain_dataset
 
 __all__ = ["BatchLayer", "save_interval_data", "read_past_data", "delete_old_data",
            "read_log_share", "save_interval_part"]
@@ -50,16 +52,33 @@ log = logging.getLogger(__name__)
 _TS_RE = re.compile(r"-(\d+)\.")
 
 
+def _write_part(path_no_ext: str, records) -> str:
+    """Write one part file; keyless single-line messages as plain text (``.txt``)."""
+    if isinstance(records, Dataset) and records.keyless:
+        vals = records.values()
+        text = "\n".join(vals)
+        if text.count("\n") == len(vals) - 1:
+            path = path_no_ext + ".txt"
+            with open(path + ".w", "w", encoding="utf-8") as f:
+                f.write(text)
+                f.write("\n")
+            os.replace(path + ".w", path)
+            return path
+    with open(path_no_ext + ".w", "w", encoding="utf-8") as f:
+        for k, m in records:
+            f.write(json.dumps([k, m], separators=(",", ":")))
+            f.write("\n")
+    os.replace(path_no_ext + ".w", path_no_ext)
+    return path_no_ext
+
+
 def save_interval_data(data_dir: str, timestamp: int, records) -> Optional[str]:
-    if not records:
+    if not records or not len(records):
         return None
     d = os.path.join(ioutils.to_local_path(data_dir), "oryx-%d.data" % timestamp)
     tmp = d + ".tmp"
     os.makedirs(tmp, exist_ok=True)
-    with open(os.path.join(tmp, "part-00000"), "w", encoding="utf-8") as f:
-        for k, m in records:
-            f.write(json.dumps([k, m], separators=(",", ":")))
-            f.write("\n")
+    _write_part(os.path.join(tmp, "part-00000"), records)
     os.replace(tmp, d)
     return d
 
@@ -69,12 +88,7 @@ def save_interval_part(data_dir: str, timestamp: int, records, rank: int) -> str
     renamed into place by rank 0 once every rank has written)."""
     d = os.path.join(ioutils.to_local_path(data_dir), "oryx-%d.data.tmp" % timestamp)
     os.makedirs(d, exist_ok=True)
-    path = os.path.join(d, "part-%05d" % rank)
-    with open(path + ".w", "w", encoding="utf-8") as f:
-        for k, m in records:
-            f.write(json.dumps([k, m], separators=(",", ":")))
-            f.write("\n")
-    os.replace(path + ".w", path)
+    _write_part(os.path.join(d, "part-%05d" % rank), records)
     return d
 
 
@@ -89,24 +103,34 @@ def read_past_data(data_dir: str, rank: int = 0, world: int = 1) -> Dataset:
     """All past records, or with ``world > 1`` this rank's share: part file j of the sorted
     listing belongs to rank ``j % world``."""
     pairs: List[Tuple[Optional[str], str]] = []
+    values: List[str] = []
     paths = [p for p in sorted(ioutils.list_files(data_dir, "*/part-*"))
              if ".tmp" not in os.path.dirname(p) and not p.endswith(".w")]
     for j, path in enumerate(paths):
         if j % world != rank:
             continue
         with open(path, "r", encoding="utf-8") as f:
+            if path.endswith(".txt"):
+                vals = f.read().split("\n")
+                if vals and vals[-1] == "":
+                    vals.pop()
+                values.extend(vals)
+                continue
             for line in f:
                 if line.strip():
                     k, m = json.loads(line)
                     pairs.append((k, m))
-    return Dataset(pairs)
+    if not pairs:
+        return Dataset.from_values(values)
+    return Dataset([(None, v) for v in values] + pairs)
 
 
 def read_log_share(root: str, topic_name: str, starts: List[int], ends: List[int], rank: int,
-                   world: int) -> List[Tuple[Optional[str], str]]:
+                   world: int) -> Dataset:
     """Records of this rank's contiguous share of every partition's [start, end) range."""
     from ..transport import log as tlog
     out: List[Tuple[Optional[str], str]] = []
+    values: List[str] = []
     topic = tlog.Topic(root, topic_name)
     try:
         for p, (lo, hi) in enumerate(zip(starts, ends)):
@@ -116,6 +140,10 @@ def read_log_share(root: str, topic_name: str, starts: List[int], ends: List[int
                 continue
             r = topic.reader(p, a)
             try:
+                vals, _ = r.read_text(b)
+                if vals is not None:
+                    values.extend(vals)
+                    continue
                 while r.position < b:
                     recs = r.poll(min(65536, b - r.position), 100)
                     if not recs:
@@ -128,7 +156,9 @@ def read_log_share(root: str, topic_name: str, starts: List[int], ends: List[int
                 r.close()
     finally:
         topic.close()
-    return out
+    if not out:
+        return Dataset.from_values(values)
+    return Dataset([(None, v) for v in values] + out)
 
 
 def delete_old_data(directory: str, max_age_hours: int, pattern: re.Pattern = _TS_RE,
@@ -170,6 +200,7 @@ class BatchLayer(AbstractLayer):
         self._context = None
         self._released = False
         self.intervals_run = 0
+        self.last_phases = {}
 
     def load_update_instance(self) -> BatchLayerUpdate:
         if self._update is not None:
@@ -207,7 +238,8 @@ class BatchLayer(AbstractLayer):
         if self._sharded():
             self._run_sharded_main(ts, t_start)
             return
-        records = drain(self._input_consumer)
+        records = drain_dataset(self._input_consumer)
+        ph = self.last_phases = {"drain": time.perf_counter() - t_start}
         faults.point("batch.interval", timestamp=ts, records=len(records))
         dctx = self._context.dist if self._context is not None else None
         seed = rng.next_seed()
@@ -215,14 +247,17 @@ class BatchLayer(AbstractLayer):
             # announce the generation to the follower ranks (they join the collectives)
             dist.broadcast_object({"ts": ts, "records": records, "seed": seed}, dctx,
                                   control=True)
-        if records:
+        if len(records):
             log.info("Beginning update at %d with %d new records", ts, len(records))
-            new_data = Dataset(records)
+            new_data = records
+            tp = time.perf_counter()
             past = read_past_data(self.data_dir)
+            ph["read_past"] = time.perf_counter() - tp
             producer = None
             if self.update_topic and self.update_broker:
                 producer = LogTopicProducer(self.update_broker, self.update_topic, self.config,
                                             async_=False, max_message=self.max_message)
+            tp = time.perf_counter()
             try:
                 with rng.shared_seed_scope(seed):
                     self._update.run_update(self._context, ts, new_data,
@@ -231,7 +266,10 @@ class BatchLayer(AbstractLayer):
             finally:
                 if producer is not None:
                     producer.close()
+            ph["update"] = time.perf_counter() - tp
+            tp = time.perf_counter()
             save_interval_data(self.data_dir, ts, records)
+            ph["save_data"] = time.perf_counter() - tp
         self.commit_input_offsets()
         rec = {"event": "batch_interval", "layer_id": self.id, "timestamp": ts,
                "records": len(records), "seconds": time.perf_counter() - t_start}
@@ -291,7 +329,7 @@ class BatchLayer(AbstractLayer):
                                         async_=False, max_message=self.max_message)
         try:
             with rng.shared_seed_scope(msg["seed"]):
-                self._update.run_update(self._context, ts, Dataset(records),
+                self._update.run_update(self._context, ts, records,
                                         past if len(past) else None, self.model_dir, producer)
         finally:
             if producer is not None:
@@ -319,11 +357,13 @@ class BatchLayer(AbstractLayer):
                 if self._run_sharded(msg):
                     joined += 1
                 continue
-            if not msg["records"]:
+            if not len(msg["records"]):
                 continue
             past = read_past_data(self.data_dir)
+            recs = msg["records"]
             with rng.shared_seed_scope(msg["seed"]):
-                self._update.run_update(self._context, msg["ts"], Dataset(msg["records"]),
+                self._update.run_update(self._context, msg["ts"],
+                                        recs if isinstance(recs, Dataset) else Dataset(recs),
                                         past if len(past) else None, self.model_dir, None)
             joined += 1
 

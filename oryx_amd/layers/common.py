@@ -23,7 +23,7 @@ from ..transport.producer import topic_root
 from ..utils import config as cfg
 from ..utils import lang
 
-__all__ = ["AbstractLayer", "LayerContext", "IntervalTimer", "drain"]
+__all__ = ["AbstractLayer", "LayerContext", "IntervalTimer", "drain", "drain_dataset"]
 
 log = logging.getLogger(__name__)
 
@@ -39,6 +39,34 @@ class LayerContext:
     @property
     def device(self):
         return self.dist.device
+
+
+def drain_dataset(consumer: tlog.TopicConsumer,
+                  end_offsets: Optional[List[int]] = None) -> Dataset:
+    """Everything currently available as a :class:`Dataset`: partitions are read in bulk
+    natively (messages only) unless a record has a key or a multi-line value."""
+    topic = consumer.topic
+    ends = end_offsets or topic.end_offsets()
+    values: List[str] = []
+    pairs: List[Tuple[Optional[str], str]] = []
+    for r in consumer.readers:
+        target = ends[r.partition]
+        vals, _ = r.read_text(target)
+        if vals is not None:
+            values.extend(vals)
+            continue
+        while r.position < target:
+            recs = r.poll(min(65536, target - r.position), 50)
+            if not recs:
+                break
+            for off, _, k, v in recs:
+                if off >= target:
+                    r.seek(off)
+                    break
+                pairs.append((k, v))
+    if not pairs:
+        return Dataset.from_values(values)
+    return Dataset([(None, v) for v in values] + pairs)
 
 
 def drain(consumer: tlog.TopicConsumer, max_records: int = 1 << 24,

@@ -26,7 +26,7 @@ from ..transport import log as tlog
 from ..transport.producer import LogTopicProducer
 from ..utils import config as cfg
 from ..utils import lang
-from .common import AbstractLayer, IntervalTimer, drain
+from .common import AbstractLayer, IntervalTimer, drain_dataset
 
 __all__ = ["SpeedLayer"]
 
@@ -90,10 +90,10 @@ class SpeedLayer(AbstractLayer):
         return self
 
     def run_interval(self, timestamp: Optional[int] = None) -> int:
-        records = drain(self._input_consumer)
+        records = drain_dataset(self._input_consumer)
         sent = 0
-        if records:
-            updates = self._manager.build_updates(Dataset(records))
+        if len(records):
+            updates = self._manager.build_updates(records)
             if updates:
                 self._producer.send_many(("UP", u) for u in updates)
                 sent = len(updates) if hasattr(updates, "__len__") else 0

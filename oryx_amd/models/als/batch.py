@@ -213,6 +213,8 @@ class ALSUpdate(MLUpdate):
             raise ValueError("bad decay settings")
         self._cache: Dict[str, dict] = {}
         self._timings: Dict[str, dict] = {}
+        # cumulative seconds per phase of build / publish (bench_batch.py reads them)
+        self.phase_seconds: Dict[str, float] = {}
 
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
@@ -237,10 +239,15 @@ class ALSUpdate(MLUpdate):
         if self._sharded(context):
             return self._build_sharded(context, train_data, features, lam, alpha,
                                        candidate_path)
+        ph = self.phase_seconds
+        tp = time.perf_counter()
         users, items = ingest.IdDict(), ingest.IdDict()
         u, i, s, ts = parse_ratings(train_data, users, items, self.decay_factor,
                                     self.decay_zero_threshold)
+        ph["parse"] = ph.get("parse", 0.0) + time.perf_counter() - tp
+        tp = time.perf_counter()
         u, i, s = aggregate_scores(u, i, s, ts, self.implicit)
+        ph["aggregate"] = ph.get("aggregate", 0.0) + time.perf_counter() - tp
         if len(u) == 0:
             log.info("No ratings after aggregation")
             return None
@@ -272,17 +279,22 @@ class ALSUpdate(MLUpdate):
         x_init = y_init = None
         if self.warm_start and self.current_model_dir:
             x_init, y_init = _warm_start_factors(self.current_model_dir, features, x_ids, y_ids)
+        ph["csr_prepare"] = ph.get("csr_prepare", 0.0) + (trainer.timings.get("prepare_s") or 0)
+        tp = time.perf_counter()
         f = trainer.train(self.iterations, checkpoint_dir=ckpt_dir,
                           checkpoint_interval=self.checkpoint_interval, fingerprint=fingerprint,
                           x_init=x_init, y_init=y_init)
         X = f.X.cpu().numpy()
         Y = f.Y.cpu().numpy()
+        ph["train"] = ph.get("train", 0.0) + time.perf_counter() - tp
         log.info("ALS %d ratings, %d users, %d items, rank %d: %.3fs", len(u), len(used_u),
                  len(used_i), features, time.perf_counter() - t0)
         if not ctx.is_main:
             return None
+        tp = time.perf_counter()
         write_features(os.path.join(candidate_path, "X"), x_ids, X)
         write_features(os.path.join(candidate_path, "Y"), y_ids, Y)
+        ph["write_factors"] = ph.get("write_factors", 0.0) + time.perf_counter() - tp
         pmml = pmmlu.build_skeleton_pmml()
         pmml.add_extension("X", "X/")
         pmml.add_extension("Y", "Y/")
@@ -495,10 +507,19 @@ class ALSUpdate(MLUpdate):
 
     def publish_additional_model_data(self, context, pmml, new_data, past_data,
                                       model_parent_path, model_update_topic):
-        if self._sharded(context):
-            self._publish_sharded(context, pmml, new_data, past_data, model_parent_path,
-                                  model_update_topic)
-            return
+        tp = time.perf_counter()
+        try:
+            if self._sharded(context):
+                self._publish_sharded(context, pmml, new_data, past_data, model_parent_path,
+                                      model_update_topic)
+            else:
+                self._publish_local(pmml, new_data, past_data, model_parent_path,
+                                    model_update_topic)
+        finally:
+            self.phase_seconds["publish_up"] = self.phase_seconds.get("publish_up", 0.0) + \
+                time.perf_counter() - tp
+
+    def _publish_local(self, pmml, new_data, past_data, model_parent_path, model_update_topic):
         all_data = list(new_data) + list(past_data or [])
         x_ids, X = read_features(os.path.join(model_parent_path, pmml.get_extension_value("X")))
         y_ids, Y = read_features(os.path.join(model_parent_path, pmml.get_extension_value("Y")))

@@ -66,6 +66,8 @@ def _load_runtime():
     _sig(lib, "oryx_reader_close", None, [c_vp])
     _sig(lib, "oryx_reader_position", c_ll, [c_vp])
     _sig(lib, "oryx_reader_seek", None, [c_vp, c_ll])
+    _sig(lib, "oryx_reader_read_text", c_ll, [c_vp, c_ll, c_vp, c_ll, ctypes.POINTER(c_ll),
+                                              ctypes.POINTER(c_i)])
     _sig(lib, "oryx_reader_poll", c_ll, [c_vp, c_vp, c_ll, c_i, c_i, ctypes.POINTER(c_ll)])
     _sig(lib, "oryx_offsets_set", c_i, [c_cp, c_cp, c_cp, c_i, ctypes.POINTER(c_i),
                                          ctypes.POINTER(c_ll)])

@@ -257,6 +257,45 @@ class PartitionReader:
             out.append((off, ts, key, val))
         return out
 
+    def read_text(self, end_offset: int) -> Tuple[Optional[List[str]], int]:
+        """Values of every record up to ``end_offset`` (exclusive) in one bulk native read.
+
+        Returns (values, records read); values is None when a record has a key or a value
+        contains a newline (the position is then back where it started: use :meth:`poll`).
+        """
+        lib = _lib()
+        start = self.position
+        chunks: List[bytes] = []
+        total = 0
+        cap = 64 << 20
+        buf = ctypes.create_string_buffer(cap)
+        used = ctypes.c_longlong(0)
+        flags = ctypes.c_int(0)
+        while self.position < end_offset:
+            n = lib.oryx_reader_read_text(self._r, int(end_offset), buf, cap,
+                                          ctypes.byref(used), ctypes.byref(flags))
+            if n == -3:
+                raise LogCorruptionError(lib.oryx_log_last_error().decode())
+            if n < 0:
+                raise IOError(lib.oryx_log_last_error().decode())
+            if flags.value:
+                self.seek(start)
+                return None, 0
+            if n == 0:
+                if used.value == 0 and cap < (1 << 30):
+                    cap *= 4           # one record larger than the buffer
+                    buf = ctypes.create_string_buffer(cap)
+                    continue
+                break
+            chunks.append(buf.raw[:used.value])
+            total += n
+        if not chunks:
+            return [], 0
+        text = b"".join(chunks).decode("utf-8")
+        vals = text.split("\n")
+        vals.pop()                     # trailing separator
+        return vals, total
+
     def close(self) -> None:
         if self._r:
             _lib().oryx_reader_close(self._r)

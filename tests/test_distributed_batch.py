@@ -146,8 +146,9 @@ def test_two_rank_sharded_als_generations(tmp_path):
     for gen in range(2):
         d = tmp_path / "data" / ("oryx-%d.data" % (1000 + gen))
         parts = sorted(os.listdir(d))
-        assert parts == ["part-00000", "part-00001"]
-        got = [[json.loads(l)[1] for l in open(d / p)] for p in parts]
+        # keyless single-line input: plain-text part files
+        assert parts == ["part-00000.txt", "part-00001.txt"]
+        got = [open(d / p).read().split() for p in parts]
         assert got[0] and got[1]
         inp = open(tmp_path / ("input%d.txt" % gen)).read().split()
         assert sorted(got[0] + got[1]) == sorted(inp)
