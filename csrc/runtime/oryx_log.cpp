@@ -135,6 +135,10 @@ struct Partition {
   std::shared_ptr<std::mutex> mu = std::make_shared<std::mutex>();
   // cached tail of the active segment (validated under the lock on every append)
   int64_t c_base = -1, c_pos = 0, c_next = 0;
+  // where oryx_log_end_offset's last scan stopped (it resumes from there)
+  std::shared_ptr<std::mutex> end_mu_p = std::make_shared<std::mutex>();
+  std::mutex& end_mu = *end_mu_p;
+  int64_t e_base = -1, e_pos = 0, e_next = 0;
 };
 
 struct Topic {
@@ -186,23 +190,39 @@ int64_t scan_segment(const std::string& path, int64_t base, int64_t* end_pos,
   int fd = open(path.c_str(), O_RDONLY);
   if (fd < 0) { *end_pos = 0; return base; }
   int64_t pos = start_pos, next = start_next >= 0 ? start_next : base;
-  uint8_t hdr[kHeader];
-  std::vector<uint8_t> payload;
+  // 4 MB block reads; a frame straddling a block is re-read from its start
+  std::vector<uint8_t> buf(4u << 20);
   for (;;) {
-    ssize_t r = pread(fd, hdr, kHeader, pos);
-    if (r != (ssize_t)kHeader) break;
-    uint32_t magic, crc, klen, vlen;
-    uint64_t off;
-    memcpy(&magic, hdr, 4); memcpy(&crc, hdr + 4, 4); memcpy(&off, hdr + 8, 8);
-    memcpy(&klen, hdr + 24, 4); memcpy(&vlen, hdr + 28, 4);
-    if (magic != kMagic) break;
-    size_t plen = (klen == kNullKey ? 0 : klen) + (size_t)vlen;
-    payload.resize(plen + 16);
-    memcpy(payload.data(), hdr + 8, 16);
-    if (plen && pread(fd, payload.data() + 16, plen, pos + kHeader) != (ssize_t)plen) break;
-    if (crc32(payload.data(), plen + 16) != crc) break;
-    pos += kHeader + plen;
-    next = (int64_t)off + 1;
+    ssize_t got = pread(fd, buf.data(), buf.size(), pos);
+    if (got < (ssize_t)kHeader) break;
+    size_t at = 0;
+    bool bad = false, straddle = false;
+    while (at + kHeader <= (size_t)got) {
+      const uint8_t* h = buf.data() + at;
+      uint32_t magic, crc, klen, vlen;
+      uint64_t off;
+      memcpy(&magic, h, 4); memcpy(&crc, h + 4, 4); memcpy(&off, h + 8, 8);
+      memcpy(&klen, h + 24, 4); memcpy(&vlen, h + 28, 4);
+      if (magic != kMagic) { bad = true; break; }
+      size_t plen = (klen == kNullKey ? 0 : klen) + (size_t)vlen;
+      if (at + kHeader + plen > (size_t)got) {
+        if (kHeader + plen > buf.size()) buf.resize(kHeader + plen);
+        straddle = true;
+        break;
+      }
+      uint32_t c = crc32(h + 8, 16);
+      c = crc32(h + kHeader, plen, c);
+      if (c != crc) { bad = true; break; }
+      at += kHeader + plen;
+      next = (int64_t)off + 1;
+    }
+    pos += (int64_t)at;
+    if (bad) break;
+    if (!straddle && at == 0) break;
+    if (!straddle && (size_t)got < buf.size()) {
+      // short read: the rest (if any) is a torn tail
+      if (at + kHeader > (size_t)got) break;
+    }
   }
   close(fd);
   *end_pos = pos;
@@ -418,11 +438,22 @@ long long oryx_log_begin_offset(void* h, int partition) {
 
 long long oryx_log_end_offset(void* h, int partition) {
   auto* t = static_cast<Topic*>(h);
-  const std::string& dir = t->parts[partition].dir;
+  auto& P = t->parts[partition];
+  const std::string& dir = P.dir;
   std::vector<int64_t> segs = list_segments(dir);
   if (segs.empty()) return 0;
   int64_t end_pos;
-  return scan_segment(seg_name(dir, segs.back()), segs.back(), &end_pos);
+  int64_t next;
+  // resume the scan where the previous call ended (valid frames only ever get appended)
+  std::lock_guard<std::mutex> g(P.end_mu);
+  if (P.e_base == segs.back())
+    next = scan_segment(seg_name(dir, segs.back()), segs.back(), &end_pos, P.e_pos, P.e_next);
+  else
+    next = scan_segment(seg_name(dir, segs.back()), segs.back(), &end_pos);
+  P.e_base = segs.back();
+  P.e_pos = end_pos;
+  P.e_next = next;
+  return next;
 }
 
 // Deletes whole segments whose files were last modified before `older_than_ms` (keeping the

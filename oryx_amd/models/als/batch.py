@@ -533,14 +533,13 @@ class ALSUpdate(MLUpdate):
             model_update_topic.send_many(("UP", '["X",%s,%s]' % (json.dumps(u), r))
                                          for u, r in zip(x_ids, x_rows))
         else:
-            known = known_items(all_data)
+            known = known_items_json(all_data)
             msgs = []
             for uid, r in zip(x_ids, x_rows):
                 ks = known.get(uid)
                 if ks is None:
                     continue  # join: users without any event are not sent
-                msgs.append(("UP", '["X",%s,%s,%s]' % (json.dumps(uid), r,
-                                                        json.dumps(sorted(ks)))))
+                msgs.append(("UP", '["X",%s,%s,%s]' % (json.dumps(uid), r, ks)))
             model_update_topic.send_many(msgs)
 
     # ---------------------------------------------------------------- split
@@ -605,6 +604,38 @@ def _known_items_sharded(lines: Sequence[str], ctx) -> Dict[str, set]:
     kk = key_s[keep]
     for a, b in zip((kk // n_i).tolist(), (kk % n_i).tolist()):
         out[ustr[a]].add(istr[b])
+    return out
+
+
+def known_items_json(lines: Sequence[str]) -> Dict[str, str]:
+    """User -> JSON array text of its known items (sorted by ID), as :func:`known_items`
+    but grouped with array ops: one JSON-encoded name per item, one join per user."""
+    users, items = ingest.IdDict(), ingest.IdDict()
+    u, i, s, ts = ingest.parse_ratings(lines, users, items, default_ts=0)
+    if len(u) == 0:
+        return {}
+    uk, ik = users.keys(), items.keys()
+    n_i = len(ik)
+    key = u * n_i + i
+    order = np.lexsort((np.arange(len(key)), ts, key))
+    key_s, s_s = key[order], s[order]
+    last = np.r_[key_s[1:] != key_s[:-1], True]
+    keep = last & ~np.isnan(s_s)
+    kk = key_s[keep]
+    uu, ii = kk // n_i, kk % n_i
+    # within a user, items in ID-string order
+    name_rank = np.empty(n_i, dtype=np.int64)
+    name_rank[np.argsort(np.array(ik, dtype=object), kind="stable")] = np.arange(n_i)
+    o2 = np.lexsort((name_rank[ii], uu))
+    uu, ii = uu[o2], ii[o2]
+    enc = [json.dumps(n) for n in ik]
+    out: Dict[str, str] = {uk[a]: "[]" for a in np.unique(u).tolist()}
+    if len(uu):
+        cuts = np.flatnonzero(np.r_[True, uu[1:] != uu[:-1]])
+        ends = np.r_[cuts[1:], len(uu)]
+        il = ii.tolist()
+        for a, lo, hi in zip(uu[cuts].tolist(), cuts.tolist(), ends.tolist()):
+            out[uk[a]] = "[" + ",".join([enc[j] for j in il[lo:hi]]) + "]"
     return out
 
 

@@ -135,3 +135,15 @@ def test_aggregate_and_known_items():
     assert ss.tolist() == [4.0, 5.0]
     k = known_items(["a,x,1,1", "a,y,1,2", "a,x,,3", "b,z,1,4", "c,w,1,5", "c,w,,6"])
     assert k == {"a": {"y"}, "b": {"z"}, "c": set()}
+
+
+def test_known_items_json_matches_sets():
+    import json
+    from oryx_amd.models.als.batch import known_items, known_items_json
+    lines = ["a,x,1,1", "a,y,1,2", "a,x,,3", "b,z,1,4", "c,w,1,5", "c,w,,6", "b,\"q\\\\r\",2,7",
+             "d,b10,1,1", "d,b9,1,2", "d,a,1,3"]
+    sets = known_items(lines)
+    js = known_items_json(lines)
+    assert set(js) == set(sets)
+    for u in sets:
+        assert json.loads(js[u]) == sorted(sets[u])
