@@ -95,6 +95,45 @@ def aggregate_scores(u: np.ndarray, i: np.ndarray, s: np.ndarray, ts: np.ndarray
     return (gk // n_i).astype(np.int64), (gk % n_i).astype(np.int64), out[keep]
 
 
+def aggregate_scores_device(u: np.ndarray, i: np.ndarray, s: np.ndarray, ts: np.ndarray,
+                            implicit: bool, device) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """:func:`aggregate_scores` on the device: two stable sorts (time, then (user, item)) and
+    segmented scans instead of a host lexsort -- same results."""
+    if len(u) == 0:
+        return u, i, s
+    dev = torch.device(device)
+    n_i = int(i.max()) + 1
+    key = torch.from_numpy(u.astype(np.int64) * n_i + i.astype(np.int64)).to(dev)
+    tt = torch.from_numpy(np.ascontiguousarray(ts, dtype=np.int64)).to(dev)
+    vv = torch.from_numpy(np.ascontiguousarray(s, dtype=np.float64)).to(dev)
+    # arrival order breaks time ties: stable sort by time, then stable sort by key
+    o1 = torch.sort(tt, stable=True).indices
+    o2 = torch.sort(key[o1], stable=True).indices
+    order = o1[o2]
+    key_s, s_s = key[order], vv[order]
+    n = key_s.numel()
+    first = torch.ones(n, dtype=torch.bool, device=dev)
+    first[1:] = key_s[1:] != key_s[:-1]
+    starts = torch.nonzero(first, as_tuple=False).flatten()
+    ends = torch.cat([starts[1:], torch.tensor([n], device=dev)])
+    if implicit:
+        isnan = torch.isnan(s_s)
+        idx = torch.where(isnan, torch.arange(n, device=dev), torch.full((n,), -1, device=dev))
+        last_nan = torch.cummax(idx, 0).values
+        grp_last_nan = last_nan[ends - 1]
+        grp_start = torch.maximum(starts, grp_last_nan + 1)
+        vals = torch.where(isnan, torch.zeros_like(s_s), s_s)
+        csum = torch.cat([torch.zeros(1, dtype=vals.dtype, device=dev), torch.cumsum(vals, 0)])
+        out = csum[ends] - csum[grp_start.clamp_max(n)]
+        out = torch.where(grp_last_nan == ends - 1, torch.full_like(out, float("nan")), out)
+    else:
+        out = s_s[ends - 1]
+    keep = ~torch.isnan(out)
+    gk = key_s[starts][keep]
+    gu = torch.div(gk, n_i, rounding_mode="floor")
+    return (gu.cpu().numpy(), (gk - gu * n_i).cpu().numpy(), out[keep].cpu().numpy())
+
+
 def parse_ratings(lines: Sequence[str], users: ingest.IdDict, items: ingest.IdDict,
                   decay_factor: float = 1.0, zero_threshold: float = 0.0,
                   now_ms: Optional[int] = None):
@@ -246,7 +285,11 @@ class ALSUpdate(MLUpdate):
                                     self.decay_zero_threshold)
         ph["parse"] = ph.get("parse", 0.0) + time.perf_counter() - tp
         tp = time.perf_counter()
-        u, i, s = aggregate_scores(u, i, s, ts, self.implicit)
+        dev = self._ctx(context).device
+        if dev.type == "cuda":
+            u, i, s = aggregate_scores_device(u, i, s, ts, self.implicit, dev)
+        else:
+            u, i, s = aggregate_scores(u, i, s, ts, self.implicit)
         ph["aggregate"] = ph.get("aggregate", 0.0) + time.perf_counter() - tp
         if len(u) == 0:
             log.info("No ratings after aggregation")
@@ -334,7 +377,10 @@ class ALSUpdate(MLUpdate):
         gu, gi, s, ts, utab, itab = self._parse_global(lines, ctx)
         # events of one user on one rank, for the time-ordered aggregation
         gu, gi, s, ts = shuffle.route(gu % W, ctx, gu, gi, s, ts)
-        au, ai, av = aggregate_scores(gu, gi, s, ts, self.implicit)
+        if ctx.device.type == "cuda":
+            au, ai, av = aggregate_scores_device(gu, gi, s, ts, self.implicit, ctx.device)
+        else:
+            au, ai, av = aggregate_scores(gu, gi, s, ts, self.implicit)
         used_u = np.zeros(utab.total, dtype=np.int32)
         used_i = np.zeros(itab.total, dtype=np.int32)
         used_u[au] = 1

@@ -204,6 +204,9 @@ class LogCorruptionError(IOError):
     """A record failed its CRC check with later records present (not a torn tail write)."""
 
 
+_TLS = threading.local()
+
+
 class PartitionReader:
     """Tails one partition from an offset (``-1`` = current end)."""
 
@@ -267,8 +270,12 @@ class PartitionReader:
         start = self.position
         chunks: List[bytes] = []
         total = 0
-        cap = 64 << 20
-        buf = ctypes.create_string_buffer(cap)
+        # one reusable 16 MB buffer per thread (zeroing a fresh one per call costs more than
+        # the read); a record larger than that gets a private one
+        buf = getattr(_TLS, "text_buf", None)
+        if buf is None:
+            buf = _TLS.text_buf = ctypes.create_string_buffer(16 << 20)
+        cap = len(buf)
         used = ctypes.c_longlong(0)
         flags = ctypes.c_int(0)
         while self.position < end_offset:
@@ -287,7 +294,7 @@ class PartitionReader:
                     buf = ctypes.create_string_buffer(cap)
                     continue
                 break
-            chunks.append(buf.raw[:used.value])
+            chunks.append(ctypes.string_at(buf, used.value))
             total += n
         if not chunks:
             return [], 0

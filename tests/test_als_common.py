@@ -147,3 +147,38 @@ def test_known_items_json_matches_sets():
     assert set(js) == set(sets)
     for u in sets:
         assert json.loads(js[u]) == sorted(sets[u])
+
+
+def test_device_aggregation_matches_host():
+    import numpy as np
+    from oryx_amd.models.als.batch import aggregate_scores, aggregate_scores_device
+    g = np.random.default_rng(3)
+    n = 20000
+    u = g.integers(0, 50, n)
+    i = g.integers(0, 40, n)
+    s = g.integers(1, 5, n).astype(np.float64)
+    s[g.random(n) < 0.1] = np.nan
+    ts = g.integers(0, 1000, n)         # many time ties: arrival order decides
+    for implicit in (True, False):
+        a = aggregate_scores(u, i, s, ts, implicit)
+        b = aggregate_scores_device(u, i, s, ts, implicit, "cpu")
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y) or np.allclose(x, y, rtol=1e-12, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_device_aggregation_matches_host_gpu(cuda):
+    import numpy as np
+    from oryx_amd.models.als.batch import aggregate_scores, aggregate_scores_device
+    g = np.random.default_rng(4)
+    n = 200000
+    u = g.integers(0, 500, n)
+    i = g.integers(0, 400, n)
+    s = g.integers(1, 5, n).astype(np.float64)
+    s[g.random(n) < 0.1] = np.nan
+    ts = g.integers(0, 1000, n)
+    for implicit in (True, False):
+        a = aggregate_scores(u, i, s, ts, implicit)
+        b = aggregate_scores_device(u, i, s, ts, implicit, cuda)
+        for x, y in zip(a, b):
+            assert np.allclose(x, y, rtol=1e-12, equal_nan=True)
