@@ -133,36 +133,48 @@ def main(argv=None) -> int:
     ms_per_step = elapsed * 1e3 / max(1, args.steps)
     ratings_per_sec = global_nnz * args.steps / elapsed
 
-    # ---- speed layer: fold-in latency of one micro-batch of new events (rank 0's GPU)
-    speed_ms = None
+    # ---- speed layer: one micro-batch of new events through the real speed-layer update
+    # (ALSSpeedModelManager.build_updates: native parse, aggregation, Gramian inverses, the
+    # fused HIP fold-in, native UP-message formatting) against the trained model, plus the
+    # fold-in kernel alone (rank 0's GPU)
+    speed_ms = foldin_ms = speed_phases = n_updates = None
+    # full factors on every rank (a collective), used by rank 0's speed-layer model
+    f = trainer.factors() if args.speed_events > 0 else None
     if ctx.is_main and args.speed_events > 0:
+        import numpy as np
+        from oryx_amd.api import Dataset
+        from oryx_amd.models.als.speed import ALSSpeedModel, ALSSpeedModelManager
+        from oryx_amd.utils import config as cfg
         k = args.rank_k
-        Xf = trainer.X[:, :k]
-        Yf = trainer.Y[:, :k]
-        g = torch.Generator(device=dev)
-        g.manual_seed(99)
+        Xh, Yh = f.X.cpu().numpy(), f.Y.cpu().numpy()
+        mgr = ALSSpeedModelManager(cfg.get_default())
+        model = ALSSpeedModel(k, bool(args.implicit), dev)
+        model.X.set_vectors(["U%d" % j for j in range(len(Xh))], Xh)
+        model.Y.set_vectors(["I%d" % j for j in range(len(Yh))], Yh)
+        mgr.model = model
+        g = np.random.default_rng(99)
         B = args.speed_events
-        ui = torch.randint(0, Xf.shape[0], (B,), generator=g, device=dev)
-        ii = torch.randint(0, Yf.shape[0], (B,), generator=g, device=dev)
-        vals = torch.rand(B, generator=g, device=dev) * 4 + 0.5
-        present = torch.ones(B, dtype=torch.bool, device=dev)
-        times = []
+        now = int(time.time() * 1000)
+        lines = ["U%d,I%d,%.2f,%d" % (a, b, v, now) for a, b, v in
+                 zip(g.integers(0, len(Xh), B).tolist(), g.integers(0, len(Yh), B).tolist(),
+                     (g.random(B) * 4 + 0.5).tolist())]
+        ds = Dataset.from_values(lines)
+        times, phases = [], []
         for rep in range(4):
+            # a new micro-batch always follows a change of the factors (the previous
+            # batch's own UP rows): the Gramian inverses are recomputed every time
+            model.X.version += 1
             sync()
             t1 = time.perf_counter()
-            # Gramians of the live factors + host RRQR solvers, then batched fold-in both ways
-            xtx = als_ops.gramian(Xf).double().cpu().numpy()
-            yty = als_ops.gramian(Yf).double().cpu().numpy()
-            yinv = torch.from_numpy(mathx.get_solver(yty).inverse()).to(dev)
-            xinv = torch.from_numpy(mathx.get_solver(xtx).inverse()).to(dev)
-            xu = Xf[ui]
-            yi = Yf[ii]
-            nx, vx = als_ops.fold_in(yinv, vals, xu, present, yi, True)
-            ny, vy = als_ops.fold_in(xinv, vals, yi, present, xu, True)
-            out = torch.cat([nx, ny]).cpu()
+            ups = mgr.build_updates(ds)
             sync()
             times.append((time.perf_counter() - t1) * 1e3)
-        speed_ms = min(times[1:])
+            phases.append(dict(mgr.last_phase_ms))
+        best = int(np.argmin(times[1:])) + 1
+        speed_ms = times[best]
+        speed_phases = phases[best]
+        foldin_ms = speed_phases.get("foldin")
+        n_updates = len(ups)
 
     info = dist.run_info(ctx)
     peak = torch.tensor([float(torch.cuda.max_memory_allocated(dev)) if dev.type == "cuda"
@@ -203,6 +215,11 @@ def main(argv=None) -> int:
             "peak_hbm_gib_per_rank": float(peak.item()) / 2**30,
             "speed_layer_update_ms": speed_ms,
             "speed_layer_events": args.speed_events,
+            "speed_layer_update_messages": n_updates,
+            "speed_layer_foldin_ms": foldin_ms,
+            "speed_layer_phase_ms": speed_phases,
+            "speed_layer_path": "ALSSpeedModelManager.build_updates (parse, aggregate, "
+                                "inverses, fused HIP fold-in, UP formatting)",
             "solve_failures": trainer.failures,
         }
         print(json.dumps(rec), flush=True)

@@ -890,6 +890,9 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
                                                   unsigned long long* __restrict__ stats) {
   const int lane = threadIdx.x & 63;
   const long long nw = (long long)gridDim.x * 4;
+  // per-wave tallies, one atomic per wave at the end (a per-point atomic on one address
+  // serialised ~10^6 updates in L2)
+  unsigned long long n1 = 0, n2 = 0;
   for (long long w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); w * 64 < n; w += nw) {
     const long long r0 = w * 64;
     const int f = r0 + lane < n ? flags[r0 + lane] : 0;
@@ -960,9 +963,14 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
       if (lane == 0) {
         assign[r] = bi;
         mind[r] = bd;
-        if (stats) atomicAdd(stats + (fj == 1 ? 0 : 1), 1ull);
       }
+      if (fj == 1) ++n1;
+      else ++n2;
     }
+  }
+  if (stats && lane == 0) {
+    if (n1) atomicAdd(stats, n1);
+    if (n2) atomicAdd(stats + 1, n2);
   }
 }
 

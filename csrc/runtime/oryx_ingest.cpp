@@ -244,4 +244,130 @@ long long oryx_format_float_rows(const float* mat, long long n, int k, long long
   return pos;
 }
 
+// All keys from `from` on, back to back in out; ends[j] = end offset of key from + j.
+// Returns bytes used, or -(bytes needed) when out is too small.
+long long oryx_dict_keys_blob(void* dh, long long from, char* out, long long cap,
+                              long long* ends) {
+  auto* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  long long need = 0;
+  for (size_t c = (size_t)from; c < d->keys.size(); ++c) need += (long long)d->keys[c].size();
+  if (need > cap) return -need;
+  long long pos = 0;
+  for (size_t c = (size_t)from; c < d->keys.size(); ++c) {
+    memcpy(out + pos, d->keys[c].data(), d->keys[c].size());
+    pos += (long long)d->keys[c].size();
+    ends[c - from] = pos;
+  }
+  return pos;
+}
+
+}  // extern "C"
+
+namespace {
+
+// JSON string literal of UTF-8 text with Python json.dumps' default escaping (ensure_ascii:
+// non-ASCII as \uXXXX, astral planes as surrogate pairs).
+void json_quote(const std::string& s, std::string& o) {
+  static const char* hex = "0123456789abcdef";
+  auto u4 = [&](unsigned v) {
+    o += "\\u";
+    o += hex[(v >> 12) & 15]; o += hex[(v >> 8) & 15]; o += hex[(v >> 4) & 15]; o += hex[v & 15];
+  };
+  o += '"';
+  for (size_t p = 0; p < s.size();) {
+    unsigned char c = (unsigned char)s[p];
+    if (c < 0x80) {
+      switch (c) {
+        case '"': o += "\\\""; break;
+        case '\\': o += "\\\\"; break;
+        case '\n': o += "\\n"; break;
+        case '\r': o += "\\r"; break;
+        case '\t': o += "\\t"; break;
+        case '\b': o += "\\b"; break;
+        case '\f': o += "\\f"; break;
+        default:
+          if (c < 0x20) u4(c); else o += (char)c;
+      }
+      ++p;
+      continue;
+    }
+    unsigned cp = 0;
+    int extra = c >= 0xF0 ? 3 : c >= 0xE0 ? 2 : 1;
+    cp = c & (0x3F >> extra);
+    for (int q = 1; q <= extra && p + q < s.size(); ++q) cp = (cp << 6) | (s[p + q] & 0x3F);
+    p += 1 + extra;
+    if (cp >= 0x10000) {
+      cp -= 0x10000;
+      u4(0xD800 + (cp >> 10));
+      u4(0xDC00 + (cp & 0x3FF));
+    } else {
+      u4(cp);
+    }
+  }
+  o += '"';
+}
+
+void float_row(const float* row, int k, std::string& o) {
+  char tmp[32];
+  o += '[';
+  for (int j = 0; j < k; ++j) {
+    if (j) o += ',';
+    float v = row[j];
+    if (std::isnan(v)) { o += "NaN"; continue; }
+    if (std::isinf(v)) { o += v > 0 ? "Infinity" : "-Infinity"; continue; }
+    auto res = std::to_chars(tmp, tmp + sizeof(tmp), v);
+    size_t l = res.ptr - tmp;
+    bool has_dot = false;
+    for (size_t q = 0; q < l; ++q) if (tmp[q] == '.' || tmp[q] == 'e') { has_dot = true; break; }
+    o.append(tmp, l);
+    if (!has_dot) o += ".0";
+  }
+  o += ']';
+}
+
+}  // namespace
+
+extern "C" {
+
+// The ALS speed layer's update messages for n folded-in events, in the reference's order
+// (per event: ["X",user,[Xu'],[item]] if vx, then ["Y",item,[Yi'],[user]] if vy;
+// ALSSpeedModelManager.java:182-215), '\n'-separated into out.  IDs come straight from the
+// parse dictionaries by code.  Returns bytes used or -(bytes needed).
+long long oryx_format_als_updates(void* users, void* items, const long long* u,
+                                  const long long* i, const float* nx, const float* ny,
+                                  const unsigned char* vx, const unsigned char* vy, long long n,
+                                  int k, int with_known, char* out, long long cap) {
+  auto* du = static_cast<Dict*>(users);
+  auto* di = static_cast<Dict*>(items);
+  std::string o;
+  o.reserve((size_t)n * (size_t)(k * 12 + 48));
+  std::string qu, qi;
+  for (long long e = 0; e < n; ++e) {
+    qu.clear();
+    qi.clear();
+    json_quote(du->keys[(size_t)u[e]], qu);
+    json_quote(di->keys[(size_t)i[e]], qi);
+    if (vx[e]) {
+      o += "[\"X\",";
+      o += qu;
+      o += ',';
+      float_row(nx + e * k, k, o);
+      if (with_known) { o += ",["; o += qi; o += ']'; }
+      o += "]\n";
+    }
+    if (vy[e]) {
+      o += "[\"Y\",";
+      o += qi;
+      o += ',';
+      float_row(ny + e * k, k, o);
+      if (with_known) { o += ",["; o += qu; o += ']'; }
+      o += "]\n";
+    }
+  }
+  if ((long long)o.size() > cap) return -(long long)o.size();
+  memcpy(out, o.data(), o.size());
+  return (long long)o.size();
+}
+
 }  // extern "C"

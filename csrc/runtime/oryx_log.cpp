@@ -593,6 +593,32 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
   return count;
 }
 
+// Records sharing one key (or none: key_len -1) given as one blob of values plus their byte
+// lengths (the producer's fast path: no per-record framing in the caller); same semantics
+// as oryx_log_append_batch.
+long long oryx_log_append_values(void* h, int partition, const char* key, int key_len,
+                                 const char* blob, const long long* lens, int n,
+                                 long long ts_ms, int do_fsync) {
+  long long total = 0;
+  for (int i = 0; i < n; ++i) total += lens[i];
+  const size_t kl = key_len < 0 ? 0 : (size_t)key_len;
+  std::vector<char> buf((size_t)total + (size_t)n * (12 + kl));
+  char* o = buf.data();
+  const char* v = blob;
+  const int32_t k32 = key_len < 0 ? -1 : key_len;
+  for (int i = 0; i < n; ++i) {
+    const int64_t vl = lens[i];
+    memcpy(o, &k32, 4);
+    memcpy(o + 4, &vl, 8);
+    if (kl) memcpy(o + 12, key, kl);
+    memcpy(o + 12 + kl, v, (size_t)vl);
+    o += 12 + kl + vl;
+    v += vl;
+  }
+  return oryx_log_append_batch(h, partition, buf.data(), (long long)buf.size(), n, ts_ms,
+                               do_fsync, nullptr);
+}
+
 // Bulk text read for the batch layer's drains: every record from the reader's position up
 // to `end_offset` (exclusive) appended to `out` as `value '\n'`, reading the segment files in
 // 4 MB blocks (one pread per block instead of two per record).  Returns the number of

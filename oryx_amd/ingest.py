@@ -14,7 +14,7 @@ import numpy as np
 
 from . import native
 
-__all__ = ["IdDict", "parse_ratings", "format_float_rows"]
+__all__ = ["IdDict", "parse_ratings", "format_float_rows", "format_als_updates"]
 
 
 class IdDict:
@@ -51,16 +51,27 @@ class IdDict:
 
     def keys(self) -> List[str]:
         n = len(self)
-        if len(self._keys_cache) < n:
-            buf = ctypes.create_string_buffer(4096)
-            for code in range(len(self._keys_cache), n):
-                ln = self._lib.oryx_dict_key(self._h, code, buf, 4096)
-                if ln > 4096:
-                    big = ctypes.create_string_buffer(int(ln))
-                    self._lib.oryx_dict_key(self._h, code, big, ln)
-                    self._keys_cache.append(big.raw[:ln].decode("utf-8"))
-                else:
-                    self._keys_cache.append(buf.raw[:ln].decode("utf-8"))
+        have = len(self._keys_cache)
+        if have < n:
+            # one native call: the new keys back to back plus their end offsets
+            ends = np.empty(n - have, dtype=np.int64)
+            cap = 1 << 16
+            while True:
+                buf = ctypes.create_string_buffer(cap)
+                used = self._lib.oryx_dict_keys_blob(self._h, have, buf, cap,
+                                                     ends.ctypes.data_as(ctypes.c_void_p))
+                if used >= 0:
+                    break
+                cap = -used + 1
+            raw = ctypes.string_at(buf, used)
+            if used == (ends[-1] if len(ends) else 0) and raw.isascii():
+                text = raw.decode("ascii")
+                starts = np.r_[0, ends[:-1]].tolist()
+                self._keys_cache.extend(text[a:b] for a, b in zip(starts, ends.tolist()))
+            else:
+                starts = np.r_[0, ends[:-1]].tolist()
+                self._keys_cache.extend(raw[a:b].decode("utf-8")
+                                        for a, b in zip(starts, ends.tolist()))
         return self._keys_cache[:n]
 
 
@@ -84,6 +95,40 @@ def parse_ratings(lines, users: IdDict, items: IdDict, default_ts: int,
     if n < 0:
         raise ValueError("Bad input line %d" % (-n - 1))
     return u[:n], i[:n], s[:n], t[:n]
+
+
+def format_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndarray,
+                       nx: np.ndarray, ny: np.ndarray, vx: np.ndarray, vy: np.ndarray,
+                       with_known: bool) -> List[str]:
+    """The speed layer's ``UP`` messages for folded-in events (see ``oryx_ingest.cpp``)."""
+    n = len(u)
+    if n == 0:
+        return []
+    k = int(nx.shape[1])
+    u = np.ascontiguousarray(u, dtype=np.int64)
+    i = np.ascontiguousarray(i, dtype=np.int64)
+    nx = np.ascontiguousarray(nx, dtype=np.float32)
+    ny = np.ascontiguousarray(ny, dtype=np.float32)
+    vx = np.ascontiguousarray(vx, dtype=np.uint8)
+    vy = np.ascontiguousarray(vy, dtype=np.uint8)
+    vp = ctypes.c_void_p
+    cap = n * (k * 16 + 256)
+    lib = native.runtime()
+    while True:
+        out = ctypes.create_string_buffer(cap)
+        used = lib.oryx_format_als_updates(users.handle, items.handle, u.ctypes.data_as(vp),
+                                           i.ctypes.data_as(vp), nx.ctypes.data_as(vp),
+                                           ny.ctypes.data_as(vp), vx.ctypes.data_as(vp),
+                                           vy.ctypes.data_as(vp), n, k, int(bool(with_known)),
+                                           out, cap)
+        if used >= 0:
+            break
+        cap = -used + 1
+    if used == 0:
+        return []
+    msgs = ctypes.string_at(out, used).decode("ascii").split("\n")
+    msgs.pop()
+    return msgs
 
 
 def format_float_rows(mat: np.ndarray) -> List[str]:

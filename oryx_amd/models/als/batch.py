@@ -579,7 +579,8 @@ class ALSUpdate(MLUpdate):
             model_update_topic.send_many(("UP", '["X",%s,%s]' % (json.dumps(u), r))
                                          for u, r in zip(x_ids, x_rows))
         else:
-            known = known_items_json(all_data)
+            known = known_items_json(all_data, device=self.dist_ctx.device
+                                     if self.dist_ctx is not None else None)
             msgs = []
             for uid, r in zip(x_ids, x_rows):
                 ks = known.get(uid)
@@ -653,35 +654,43 @@ def _known_items_sharded(lines: Sequence[str], ctx) -> Dict[str, set]:
     return out
 
 
-def known_items_json(lines: Sequence[str]) -> Dict[str, str]:
+def known_items_json(lines: Sequence[str], device=None) -> Dict[str, str]:
     """User -> JSON array text of its known items (sorted by ID), as :func:`known_items`
-    but grouped with array ops: one JSON-encoded name per item, one join per user."""
+    but with the time-ordered last-event selection as device sorts and the per-user lists
+    joined from one array of JSON-encoded item names."""
     users, items = ingest.IdDict(), ingest.IdDict()
     u, i, s, ts = ingest.parse_ratings(lines, users, items, default_ts=0)
     if len(u) == 0:
         return {}
     uk, ik = users.keys(), items.keys()
     n_i = len(ik)
-    key = u * n_i + i
-    order = np.lexsort((np.arange(len(key)), ts, key))
-    key_s, s_s = key[order], s[order]
-    last = np.r_[key_s[1:] != key_s[:-1], True]
-    keep = last & ~np.isnan(s_s)
-    kk = key_s[keep]
-    uu, ii = kk // n_i, kk % n_i
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    key = torch.from_numpy(u * n_i + i).to(dev)
+    tt = torch.from_numpy(ts).to(dev)
+    o1 = torch.sort(tt, stable=True).indices
+    order = o1[torch.sort(key[o1], stable=True).indices]
+    key_s = key[order]
+    nan_s = torch.from_numpy(np.isnan(s)).to(dev)[order]
+    last = torch.ones_like(key_s, dtype=torch.bool)
+    last[:-1] = key_s[1:] != key_s[:-1]
+    kk = key_s[last & ~nan_s]
     # within a user, items in ID-string order
     name_rank = np.empty(n_i, dtype=np.int64)
     name_rank[np.argsort(np.array(ik, dtype=object), kind="stable")] = np.arange(n_i)
-    o2 = np.lexsort((name_rank[ii], uu))
-    uu, ii = uu[o2], ii[o2]
-    enc = [json.dumps(n) for n in ik]
+    uu = torch.div(kk, n_i, rounding_mode="floor")
+    ii = kk - uu * n_i
+    rk = torch.from_numpy(name_rank).to(dev)[ii]
+    o2 = torch.sort(uu * n_i + rk, stable=True).indices
+    uu = uu[o2].cpu().numpy()
+    ii = ii[o2].cpu().numpy()
+    enc = np.array([json.dumps(n) for n in ik], dtype=object)
     out: Dict[str, str] = {uk[a]: "[]" for a in np.unique(u).tolist()}
     if len(uu):
+        names = enc[ii]
         cuts = np.flatnonzero(np.r_[True, uu[1:] != uu[:-1]])
         ends = np.r_[cuts[1:], len(uu)]
-        il = ii.tolist()
         for a, lo, hi in zip(uu[cuts].tolist(), cuts.tolist(), ends.tolist()):
-            out[uk[a]] = "[" + ",".join([enc[j] for j in il[lo:hi]]) + "]"
+            out[uk[a]] = "[" + ",".join(names[lo:hi]) + "]"
     return out
 
 

@@ -8,9 +8,12 @@ Equivalent of ``ALSSpeedModel`` / ``ALSSpeedModelManager``
 * ``build_updates``: nothing until ``fraction_loaded >= oryx.speed.min-model-load-fraction``;
   then the interval's input is time-ordered and aggregated like the batch layer, the
   Gramians XᵀX / YᵀY are formed on the device and inverted (RRQR with the reference's
-  singularity check -- a singular Gramian skips the interval), and ALL events are folded in
-  at once: two ``[B,k]x[k,k]`` GEMMs on a dedicated HIP stream instead of B independent
-  k x k solves.  Each event yields ``["X",u,vec,[i]]`` and ``["Y",i,vec,[u]]``.
+  singularity check -- a singular Gramian skips the interval; the inverses are cached until
+  the factors change), and ALL events are folded in at once by the fused HIP kernel
+  ``oryx_als_foldin`` (``csrc/kernels/foldin.hip``: dot, target, inverse x rhs in double, axpy;
+  rows read from the device mirrors by index) on a dedicated stream, instead of B independent
+  k x k solves.  Each event yields ``["X",u,vec,[i]]`` and ``["Y",i,vec,[u]]``,
+  formatted natively straight from the parse dictionaries (``oryx_format_als_updates``).
 """
 
 from __future__ import annotations
@@ -96,6 +99,23 @@ class ALSSpeedModel(SpeedModel):
     def get_yty_solver(self):
         return mathx.get_solver(self.Y.get_vtv())
 
+    def solver_inverses(self):
+        """(inverse of XtX, inverse of YtY) as fp64 device tensors, recomputed only when the
+        factors changed since the last call; raises SingularMatrixSolverException like the
+        solvers; None when a matrix is empty."""
+        key = (self.X.version, self.Y.version)
+        if getattr(self, "_inv_key", None) == key:
+            return self._inv
+        xtx = self.get_xtx_solver()
+        yty = self.get_yty_solver()
+        if xtx is None or yty is None:
+            inv = None
+        else:
+            inv = (torch.from_numpy(xtx.inverse()).to(self.device),
+                   torch.from_numpy(yty.inverse()).to(self.device))
+        self._inv_key, self._inv = key, inv
+        return inv
+
     def get_fraction_loaded(self) -> float:
         with self._lock:
             expected = len(self._expected_users) + len(self._expected_items)
@@ -118,6 +138,9 @@ class ALSSpeedModelManager(SpeedModelManager):
             raise ValueError("bad min-model-load-fraction")
         self.model: Optional[ALSSpeedModel] = None
         self._stream = None
+        # milliseconds per phase of the last build_updates (parse_aggregate, inverses,
+        # foldin = kernel + device->host copy, format)
+        self.last_phase_ms = {}
 
     def consume(self, updates: Iterator[KeyMessage], context=None) -> None:
         countdown = 10000
@@ -168,11 +191,17 @@ class ALSSpeedModelManager(SpeedModelManager):
         model = self.model
         if model is None or model.get_fraction_loaded() < self.min_model_load_fraction:
             return []
+        import time
+        t0 = time.perf_counter()
         users, items = ingest.IdDict(), ingest.IdDict()
         u, i, s, ts = ingest.parse_ratings(new_data.values(), users, items, default_ts=0)
         u, i, s = aggregate_scores(u, i, s, ts, model.is_implicit())
+        self.last_phase_ms = {"parse_aggregate": (time.perf_counter() - t0) * 1e3}
         if len(u) == 0:
             return []
+        dev = model.device
+        if dev.type == "cuda" and model.features <= 256:
+            return self._build_updates_fused(model, users, items, u, i, s)
         try:
             xtx = model.get_xtx_solver()
             yty = model.get_yty_solver()
@@ -222,6 +251,64 @@ class ALSSpeedModelManager(SpeedModelManager):
                 out.append(self._to_update_json("X", u_ids[j], x_rows[j], i_ids[j]))
             if vy[j]:
                 out.append(self._to_update_json("Y", i_ids[j], y_rows[j], u_ids[j]))
+        return out
+
+    def _build_updates_fused(self, model, users, items, u, i, s) -> List[str]:
+        import time
+        from ... import native
+        ph = self.last_phase_ms
+        t0 = time.perf_counter()
+        try:
+            inv = model.solver_inverses()
+        except mathx.SingularMatrixSolverException:
+            return []
+        if inv is None:
+            return []
+        ph["inverses"] = (time.perf_counter() - t0) * 1e3
+        t0 = time.perf_counter()
+        xinv, yinv = inv
+        dev = model.device
+        k = model.features
+        # store rows of the batch's distinct IDs (dictionary codes index them)
+        xi, yi_ = model.X._index, model.Y._index
+        urow = np.fromiter((xi.get(key, -1) for key in users.keys()), dtype=np.int64,
+                           count=len(users))
+        irow = np.fromiter((yi_.get(key, -1) for key in items.keys()), dtype=np.int64,
+                           count=len(items))
+        n = len(u)
+        lib = native.require_kernels()
+        stream = self._device_stream(dev)
+        with torch.cuda.stream(stream):
+            xmat, _, _ = model.X.device_view()
+            ymat, _, _ = model.Y.device_view()
+            xm = xmat if len(xmat) else torch.zeros((1, k), device=dev)
+            ym = ymat if len(ymat) else torch.zeros((1, k), device=dev)
+            xr = torch.from_numpy(urow[u]).to(dev)
+            yr = torch.from_numpy(irow[i]).to(dev)
+            # the reference folds in strength.floatValue() (ALSSpeedModelManager.java:170)
+            vals = torch.from_numpy(np.asarray(s, dtype=np.float32)).to(dev)
+            new_x = torch.empty((n, k), dtype=torch.float32, device=dev)
+            new_y = torch.empty((n, k), dtype=torch.float32, device=dev)
+            vx = torch.empty(n, dtype=torch.uint8, device=dev)
+            vy = torch.empty(n, dtype=torch.uint8, device=dev)
+            rc = lib.oryx_als_foldin(xm.contiguous().data_ptr(), ym.contiguous().data_ptr(), k,
+                                     xr.data_ptr(), yr.data_ptr(), vals.data_ptr(),
+                                     xinv.contiguous().data_ptr(), yinv.contiguous().data_ptr(),
+                                     int(model.is_implicit()), n, new_x.data_ptr(),
+                                     new_y.data_ptr(), vx.data_ptr(), vy.data_ptr(),
+                                     native.stream_ptr(dev))
+            native.check(rc, "oryx_als_foldin")
+            host = torch.cat([new_x.view(-1), new_y.view(-1),
+                              torch.cat([vx, vy]).to(torch.float32)]).cpu().numpy()
+        nx = host[:n * k].reshape(n, k)
+        ny = host[n * k:2 * n * k].reshape(n, k)
+        vxh = host[2 * n * k:2 * n * k + n] > 0
+        vyh = host[2 * n * k + n:] > 0
+        ph["foldin"] = (time.perf_counter() - t0) * 1e3
+        t0 = time.perf_counter()
+        out = ingest.format_als_updates(users, items, u, i, nx, ny, vxh, vyh,
+                                        not self.no_known_items)
+        ph["format"] = (time.perf_counter() - t0) * 1e3
         return out
 
     def _to_update_json(self, matrix: str, id_: str, vec_json: str, other: str) -> str:

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 7
+KERNELS_ABI_VERSION = 8
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -59,6 +59,8 @@ def _load_runtime():
     _sig(lib, "oryx_log_max_message", c_ll, [c_vp])
     _sig(lib, "oryx_log_partition_for", c_i, [c_vp, c_cp, c_i])
     _sig(lib, "oryx_log_append_batch", c_ll, [c_vp, c_i, c_cp, c_ll, c_i, c_ll, c_i, c_vp])
+    _sig(lib, "oryx_log_append_values", c_ll, [c_vp, c_i, c_cp, c_i, c_cp, c_vp, c_i, c_ll,
+                                                c_i])
     _sig(lib, "oryx_log_begin_offset", c_ll, [c_vp, c_i])
     _sig(lib, "oryx_log_end_offset", c_ll, [c_vp, c_i])
     _sig(lib, "oryx_log_retain", c_i, [c_vp, c_ll])
@@ -87,6 +89,10 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_parse_ratings", c_ll, [c_cp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_ll, c_ll, c_i])
     _sig(lib, "oryx_format_float_rows", c_ll, [c_vp, c_ll, c_i, c_ll, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_vp, c_ll, c_vp])
+    # users, items, u, i, nx, ny, vx, vy, n, k, with_known, out, cap
+    _sig(lib, "oryx_format_als_updates", c_ll, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                c_ll, c_i, c_i, c_vp, c_ll])
 
 
 def _runtime_sources():
@@ -144,6 +150,9 @@ def _load_kernels():
     _sig(lib, "oryx_kmeans_assign_cert", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_i,
                                                c_i, c_vp, c_i, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                c_vp])
+    # X, Y, k, xrow, yrow, vals, xinv, yinv, implicit, n, new_x, new_y, vx, vy, stream
+    _sig(lib, "oryx_als_foldin", c_i, [c_vp, c_vp, c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_ll,
+                                       c_vp, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_topn_waves", c_ll, [c_ll])
     # Y, inv_norm, Q, kp, nq, bucket_of, cand_bits, words, ranges, tile0, n_ranges, n_tiles,
     # excl_ptr, excl_rows, out_score, out_row, stream

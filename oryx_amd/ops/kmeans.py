@@ -274,22 +274,34 @@ def _gather_rows(rows: torch.Tensor, ctx) -> torch.Tensor:
 
 def _kmeanspp_weighted(cands: torch.Tensor, weights: torch.Tensor, k: int,
                        gen: torch.Generator) -> torch.Tensor:
-    """Weighted k-means++ on a (small) candidate set, on the host in float64."""
-    c = cands.double().cpu()
-    w = weights.double().cpu()
+    """Weighted k-means++ on the (small) candidate set in float64.
+
+    The D^2 updates run where the candidates live (one [n, d] pass per chosen center on the
+    GPU); each draw is an inverse-CDF lookup of one uniform from the host generator ``gen``
+    (a single scalar sync per step), so the choice sequence is identical on CPU and GPU.
+    """
+    c = cands.double()
+    w = weights.double().to(c.device)
     n = c.shape[0]
     if n <= k:
         return c.float()
-    first = int(torch.multinomial(w / w.sum(), 1, generator=gen))
+
+    def draw(p: torch.Tensor) -> int:
+        cdf = torch.cumsum(p, 0)
+        total = cdf[-1]
+        u = float(torch.rand(1, generator=gen, dtype=torch.float64)) * float(total)
+        return min(int(torch.searchsorted(cdf, torch.tensor([u], dtype=torch.float64,
+                                                              device=c.device))), n - 1)
+
+    first = draw(w)
     chosen = [first]
     d2 = ((c - c[first]) ** 2).sum(1)
     for _ in range(1, k):
         p = w * d2
-        s = float(p.sum())
-        if s <= 0:
+        if float(p.sum()) <= 0:
             nxt = int(torch.randint(0, n, (1,), generator=gen))
         else:
-            nxt = int(torch.multinomial(p / s, 1, generator=gen))
+            nxt = draw(p)
         chosen.append(nxt)
         d2 = torch.minimum(d2, ((c - c[nxt]) ** 2).sum(1))
     return c[chosen].float()
@@ -344,7 +356,7 @@ def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = 
     w = torch.bincount(idx.long(), minlength=centers.shape[0]).double()
     if ctx.is_distributed:
         dist.all_reduce_sum(w, ctx)
-    chosen = _kmeanspp_weighted(centers, w, k, gen).to(dev)
+    chosen = _kmeanspp_weighted(centers.to(dev), w, k, gen).to(dev)
     if ctx.is_distributed:
         torch.distributed.broadcast(chosen, src=0)
     return chosen

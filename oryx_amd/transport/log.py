@@ -25,6 +25,8 @@ import threading
 import time
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
+import numpy as np
+
 from .. import native
 from ..utils import faults
 
@@ -144,6 +146,10 @@ class Topic:
             elif act == "corrupt":
                 # damage the first record's bytes on disk after its CRC was computed
                 return self._append_corrupted(records, partition, timestamp_ms, fsync)
+        k0 = records[0][0]
+        if all(k == k0 for k, _ in records):
+            return self.append_values([v for _, v in records], partition, timestamp_ms, fsync,
+                                      key=k0)
         parts = []
         for k, v in records:
             kb = _b(k)
@@ -156,6 +162,31 @@ class Topic:
         res = _lib().oryx_log_append_batch(self._h, int(partition), buf, len(buf),
                                            len(records), int(timestamp_ms), int(bool(fsync)),
                                            None)
+        if res == -2:
+            raise MessageTooLargeError(_lib().oryx_log_last_error().decode())
+        if res < 0:
+            raise IOError(_lib().oryx_log_last_error().decode())
+        return res
+
+    def append_values(self, values: Sequence[str], partition: int = -1,
+                      timestamp_ms: int = -1, fsync: bool = False,
+                      key: Optional[str] = None) -> int:
+        """Append records that share one key (default none): one encode of the joined
+        values, lengths computed in bulk (character counts when the text is ASCII)."""
+        if not values:
+            return -1
+        text = "".join(values)
+        blob = text.encode("utf-8")
+        if len(blob) == len(text):
+            lens = np.fromiter(map(len, values), dtype=np.int64, count=len(values))
+        else:
+            lens = np.fromiter((len(v.encode("utf-8")) for v in values), dtype=np.int64,
+                               count=len(values))
+        kb = _b(key)
+        res = _lib().oryx_log_append_values(self._h, int(partition), kb,
+                                            -1 if kb is None else len(kb), blob,
+                                            lens.ctypes.data_as(ctypes.c_void_p), len(values),
+                                            int(timestamp_ms), int(bool(fsync)))
         if res == -2:
             raise MessageTooLargeError(_lib().oryx_log_last_error().decode())
         if res < 0:

@@ -182,3 +182,46 @@ def test_device_aggregation_matches_host_gpu(cuda):
         b = aggregate_scores_device(u, i, s, ts, implicit, cuda)
         for x, y in zip(a, b):
             assert np.allclose(x, y, rtol=1e-12, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("implicit", [True, False])
+@pytest.mark.parametrize("k", [8, 64, 100])
+def test_fused_foldin_matches_unfused(cuda, implicit, k):
+    """oryx_als_foldin == the torch fold_in path (dot, target, inverse solve, axpy), with
+    absent users / items and NaN targets (negative strengths on implicit data)."""
+    import torch
+    from oryx_amd import native
+    g = torch.Generator().manual_seed(k)
+    nu, ni, n = 300, 200, 5000
+    X = torch.randn(nu, k, generator=g) * 0.3
+    Y = torch.randn(ni, k, generator=g) * 0.3
+    xrow = torch.randint(-1, nu, (n,), generator=g)
+    yrow = torch.randint(-1, ni, (n,), generator=g)
+    vals = (torch.rand(n, generator=g) * 4 - 1).float()
+    xinv = torch.linalg.inv((X.T @ X).double() + torch.eye(k, dtype=torch.float64))
+    yinv = torch.linalg.inv((Y.T @ Y).double() + torch.eye(k, dtype=torch.float64))
+    dev = torch.device(cuda)
+    out = {nm: torch.empty((n, k), device=dev) for nm in ("nx", "ny")}
+    vx = torch.empty(n, dtype=torch.uint8, device=dev)
+    vy = torch.empty(n, dtype=torch.uint8, device=dev)
+    Xd, Yd = X.to(dev), Y.to(dev)
+    xr, yr = xrow.to(dev), yrow.to(dev)
+    vd = vals.to(dev)
+    xi, yi = xinv.to(dev), yinv.to(dev)
+    rc = native.require_kernels().oryx_als_foldin(
+        Xd.data_ptr(), Yd.data_ptr(), k, xr.data_ptr(), yr.data_ptr(), vd.data_ptr(),
+        xi.data_ptr(), yi.data_ptr(), int(implicit), n, out["nx"].data_ptr(),
+        out["ny"].data_ptr(), vx.data_ptr(), vy.data_ptr(), native.stream_ptr(dev))
+    assert rc == 0
+    torch.cuda.synchronize()
+    xp, yp = xrow >= 0, yrow >= 0
+    xu = torch.where(xp[:, None], X[xrow.clamp_min(0)], torch.zeros(()))
+    yv = torch.where(yp[:, None], Y[yrow.clamp_min(0)], torch.zeros(()))
+    v64 = vals.double()
+    rx, okx = als_ops.fold_in(yinv, v64, xu, xp, yv, implicit)
+    ry, oky = als_ops.fold_in(xinv, v64, yv, yp, xu, implicit)
+    okx, oky = okx & yp, oky & xp
+    assert torch.equal(vx.cpu().bool(), okx) and torch.equal(vy.cpu().bool(), oky)
+    assert torch.allclose(out["nx"].cpu()[okx], rx[okx], rtol=1e-5, atol=1e-6)
+    assert torch.allclose(out["ny"].cpu()[oky], ry[oky], rtol=1e-5, atol=1e-6)

@@ -285,6 +285,16 @@ def test_als_speed_golden_vectors(tmp_path):
     """ALSSpeedIT: a MODEL + 9 UP messages (an SVD factorisation of a 4x5 matrix), then 9
     inputs that each pair a new user or item with a known one -> exactly 9 updates whose
     vectors match the reference's golden values to 1e-5."""
+    _als_speed_golden(tmp_path)
+
+
+@pytest.mark.gpu
+def test_als_speed_golden_vectors_gpu(tmp_path, cuda):
+    """The same golden ALSSpeedIT check through the fused HIP fold-in (device model)."""
+    _als_speed_golden(tmp_path)
+
+
+def _als_speed_golden(tmp_path):
     config = _config(tmp_path, **{
         "oryx.speed.model-manager-class": "com.cloudera.oryx.app.speed.als.ALSSpeedModelManager",
         "oryx.als.hyperparams.features": 2})
