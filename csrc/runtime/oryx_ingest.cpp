@@ -330,6 +330,167 @@ void float_row(const float* row, int k, std::string& o) {
 
 extern "C" {
 
+// ---- bulk parsing of ALS model-update messages (the serving / speed model load) ----
+
+struct JsonCursor {
+  const char* p;
+  const char* end;
+  void ws() { while (p < end && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p; }
+  bool eat(char c) { ws(); if (p < end && *p == c) { ++p; return true; } return false; }
+  // a JSON string (escapes decoded to UTF-8) or a bare number / literal as text
+  bool token(std::string& out) {
+    ws();
+    out.clear();
+    if (p >= end) return false;
+    if (*p != '"') {
+      const char* b = p;
+      while (p < end && *p != ',' && *p != ']' && *p != ' ') ++p;
+      out.assign(b, p - b);
+      return p > b;
+    }
+    ++p;
+    while (p < end && *p != '"') {
+      char c = *p++;
+      if (c != '\\') { out += c; continue; }
+      if (p >= end) return false;
+      char e = *p++;
+      switch (e) {
+        case '"': out += '"'; break;
+        case '\\': out += '\\'; break;
+        case '/': out += '/'; break;
+        case 'b': out += '\b'; break;
+        case 'f': out += '\f'; break;
+        case 'n': out += '\n'; break;
+        case 'r': out += '\r'; break;
+        case 't': out += '\t'; break;
+        case 'u': {
+          auto hex4 = [&](unsigned& v) {
+            if (end - p < 4) return false;
+            v = 0;
+            for (int q = 0; q < 4; ++q) {
+              char h = p[q];
+              v <<= 4;
+              if (h >= '0' && h <= '9') v |= h - '0';
+              else if (h >= 'a' && h <= 'f') v |= h - 'a' + 10;
+              else if (h >= 'A' && h <= 'F') v |= h - 'A' + 10;
+              else return false;
+            }
+            p += 4;
+            return true;
+          };
+          unsigned cp;
+          if (!hex4(cp)) return false;
+          if (cp >= 0xD800 && cp < 0xDC00 && end - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+            p += 2;
+            unsigned lo;
+            if (!hex4(lo)) return false;
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+          }
+          if (cp < 0x80) out += (char)cp;
+          else if (cp < 0x800) { out += (char)(0xC0 | (cp >> 6)); out += (char)(0x80 | (cp & 63)); }
+          else if (cp < 0x10000) {
+            out += (char)(0xE0 | (cp >> 12)); out += (char)(0x80 | ((cp >> 6) & 63));
+            out += (char)(0x80 | (cp & 63));
+          } else {
+            out += (char)(0xF0 | (cp >> 18)); out += (char)(0x80 | ((cp >> 12) & 63));
+            out += (char)(0x80 | ((cp >> 6) & 63)); out += (char)(0x80 | (cp & 63));
+          }
+          break;
+        }
+        default: return false;
+      }
+    }
+    if (p >= end) return false;
+    ++p;
+    return true;
+  }
+};
+
+}  // extern "C"
+
+namespace {
+thread_local std::string g_up_ids, g_up_known;
+}
+
+extern "C" {
+
+// Parses n messages ["X"|"Y", id, [k floats], optional [ids...]] (back to back in buf, ends
+// = message end offsets).  kinds[j] = 0 (X) / 1 (Y) / 2 (unparseable: the caller falls back);
+// vecs [n][k]; id_ends[j] / known_cnt[j] index the id and known-item texts, fetched with
+// oryx_up_texts (ids, then known items, each back to back; known_ends per item).  Returns the
+// total number of known items.
+long long oryx_parse_up_batch(const char* buf, const long long* ends, long long n, int k,
+                              unsigned char* kinds, float* vecs, long long* id_ends,
+                              long long* known_cnt) {
+  g_up_ids.clear();
+  g_up_known.clear();
+  std::string tok;
+  long long start = 0, total_known = 0;
+  for (long long j = 0; j < n; ++j) {
+    JsonCursor c{buf + start, buf + ends[j]};
+    start = ends[j];
+    kinds[j] = 2;
+    known_cnt[j] = 0;
+    const size_t id_mark = g_up_ids.size(), known_mark = g_up_known.size();
+    bool ok = c.eat('[') && c.token(tok) && (tok == "X" || tok == "Y");
+    unsigned char kind = ok && tok == "Y" ? 1 : 0;
+    ok = ok && c.eat(',') && c.token(tok);
+    if (ok) g_up_ids += tok;
+    ok = ok && c.eat(',') && c.eat('[');
+    float* v = vecs + j * k;
+    for (int f = 0; ok && f < k; ++f) {
+      if (f && !c.eat(',')) { ok = false; break; }
+      c.ws();
+      const char* b = c.p;
+      while (c.p < c.end && *c.p != ',' && *c.p != ']' && *c.p != ' ') ++c.p;
+      auto r = std::from_chars(b, c.p, v[f]);
+      if (r.ec != std::errc() || r.ptr != c.p) {
+        std::string t(b, c.p - b);   // NaN / Infinity spellings
+        if (t == "NaN") v[f] = std::numeric_limits<float>::quiet_NaN();
+        else if (t == "Infinity") v[f] = std::numeric_limits<float>::infinity();
+        else if (t == "-Infinity") v[f] = -std::numeric_limits<float>::infinity();
+        else ok = false;
+      }
+    }
+    ok = ok && c.eat(']');
+    long long cnt = 0;
+    if (ok && c.eat(',')) {
+      ok = c.eat('[');
+      if (ok && !c.eat(']')) {
+        do {
+          if (!c.token(tok)) { ok = false; break; }
+          g_up_known += tok;
+          g_up_known += '\0';
+          ++cnt;
+        } while (c.eat(','));
+        ok = ok && c.eat(']');
+      }
+    }
+    ok = ok && c.eat(']');
+    if (!ok) {
+      g_up_ids.resize(id_mark);
+      g_up_known.resize(known_mark);
+      id_ends[j] = (long long)g_up_ids.size();
+      continue;
+    }
+    kinds[j] = kind;
+    id_ends[j] = (long long)g_up_ids.size();
+    known_cnt[j] = cnt;
+    total_known += cnt;
+  }
+  return total_known;
+}
+
+// The id texts (back to back) and the known-item texts ('\0'-terminated) of the last
+// oryx_parse_up_batch call; returns -(bytes needed) when a buffer is too small.
+long long oryx_up_texts(char* ids, long long ids_cap, char* known, long long known_cap) {
+  if ((long long)g_up_ids.size() > ids_cap || (long long)g_up_known.size() > known_cap)
+    return -(long long)(g_up_ids.size() + g_up_known.size());
+  memcpy(ids, g_up_ids.data(), g_up_ids.size());
+  memcpy(known, g_up_known.data(), g_up_known.size());
+  return (long long)g_up_ids.size();
+}
+
 // The ALS speed layer's update messages for n folded-in events, in the reference's order
 // (per event: ["X",user,[Xu'],[item]] if vx, then ["Y",item,[Yi'],[user]] if vy;
 // ALSSpeedModelManager.java:182-215), '\n'-separated into out.  IDs come straight from the

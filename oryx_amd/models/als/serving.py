@@ -289,6 +289,17 @@ class ALSServingModel(ServingModel):
         with self._expected_lock:
             self._expected_items.discard(item)
 
+    def set_user_vectors(self, ids: Sequence[str], mat: np.ndarray) -> None:
+        """Bulk :meth:`set_user_vector` (model loads)."""
+        self.X.set_vectors(ids, mat)
+        with self._expected_lock:
+            self._expected_users.difference_update(ids)
+
+    def set_item_vectors(self, ids: Sequence[str], mat: np.ndarray) -> None:
+        self.Y.set_vectors(ids, mat)
+        with self._expected_lock:
+            self._expected_items.difference_update(ids)
+
     def get_known_items(self, user: str) -> Set[str]:
         with self._known_lock.read():
             s = self._known.get(user)
@@ -462,6 +473,39 @@ class ALSServingModel(ServingModel):
                                                    self.get_fraction_loaded(), self.device))
 
 
+def apply_up_batch(model, messages: List[str]) -> None:
+    """Apply ``UP`` rows in bulk: ``ingest.parse_up_batch`` then one ``set_vectors`` per
+    matrix (the later row wins for a repeated ID), known items added per user; messages the
+    native parser rejects go through the per-message path (and raise as it does)."""
+    from ... import ingest
+    kinds, ids, vecs, known = ingest.parse_up_batch(messages, model.get_features())
+    for kind, setter in ((0, "set_user_vectors"), (1, "set_item_vectors")):
+        sel = np.nonzero(kinds == kind)[0]
+        if not len(sel):
+            continue
+        # last occurrence of each ID wins
+        last = {}
+        for j in sel.tolist():
+            last[ids[j]] = j
+        rows = np.fromiter(last.values(), dtype=np.int64, count=len(last))
+        getattr(model, setter)([ids[j] for j in rows.tolist()], vecs[rows])
+        if kind == 0 and hasattr(model, "add_known_items"):
+            for j in sel.tolist():
+                if known[j]:
+                    model.add_known_items(ids[j], known[j])
+    for j in np.nonzero(kinds == 2)[0].tolist():
+        update = text.read_json(messages[j])
+        vector = np.asarray(update[2], dtype=np.float32)
+        if update[0] == "X":
+            model.set_user_vector(str(update[1]), vector)
+            if len(update) > 3 and hasattr(model, "add_known_items"):
+                model.add_known_items(str(update[1]), [str(x) for x in update[3]])
+        elif update[0] == "Y":
+            model.set_item_vector(str(update[1]), vector)
+        else:
+            raise ValueError("Bad message: %r" % (messages[j],))
+
+
 class ALSServingModelManager(AbstractServingModelManager):
     def __init__(self, config):
         super().__init__(config)
@@ -487,6 +531,17 @@ class ALSServingModelManager(AbstractServingModelManager):
             if key == "UP":
                 if self.model is None:
                     continue
+                take = getattr(updates, "take_buffered", None)
+                if take is not None:
+                    # a run of UP rows already fetched: one native parse, bulk row updates
+                    batch = [message] + [m.message for m in take(lambda m: m.key == "UP")]
+                    if len(batch) > 1:
+                        apply_up_batch(self.model, batch)
+                        countdown -= len(batch)
+                        if countdown <= 0:
+                            log.info("%s", self.model)
+                            countdown = 10000
+                        continue
                 update = text.read_json(message)
                 id_ = str(update[1])
                 vector = np.asarray(update[2], dtype=np.float32)

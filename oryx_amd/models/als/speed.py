@@ -81,6 +81,16 @@ class ALSSpeedModel(SpeedModel):
         with self._lock:
             self._expected_items.discard(item)
 
+    def set_user_vectors(self, ids, mat) -> None:
+        self.X.set_vectors(ids, mat)
+        with self._lock:
+            self._expected_users.difference_update(ids)
+
+    def set_item_vectors(self, ids, mat) -> None:
+        self.Y.set_vectors(ids, mat)
+        with self._lock:
+            self._expected_items.difference_update(ids)
+
     def retain_recent_and_user_ids(self, users) -> None:
         self.X.retain_recent_and_ids(users)
         with self._lock:
@@ -151,6 +161,17 @@ class ALSSpeedModelManager(SpeedModelManager):
             if key == "UP":
                 if self.model is None:
                     continue
+                take = getattr(updates, "take_buffered", None)
+                if take is not None:
+                    batch = [message] + [m.message for m in take(lambda m: m.key == "UP")]
+                    if len(batch) > 1:
+                        from .serving import apply_up_batch
+                        apply_up_batch(self.model, batch)
+                        countdown -= len(batch)
+                        if countdown <= 0:
+                            log.info("%s", self.model)
+                            countdown = 10000
+                        continue
                 update = text.read_json(message)
                 id_ = str(update[1])
                 vec = np.asarray(update[2], dtype=np.float32)

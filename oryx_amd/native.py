@@ -90,6 +90,8 @@ def _register_runtime_extras(lib):
                                            c_ll, c_ll, c_i])
     _sig(lib, "oryx_format_float_rows", c_ll, [c_vp, c_ll, c_i, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_parse_up_batch", c_ll, [c_cp, c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_up_texts", c_ll, [c_vp, c_ll, c_vp, c_ll])
     # users, items, u, i, nx, ny, vx, vy, n, k, with_known, out, cap
     _sig(lib, "oryx_format_als_updates", c_ll, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                 c_ll, c_i, c_i, c_vp, c_ll])

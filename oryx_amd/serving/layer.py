@@ -60,6 +60,22 @@ class UpdateIterator:
     def has_buffered(self) -> bool:
         return bool(self._pending)
 
+    def take_buffered(self, pred, max_n: int = 1 << 16) -> List[KeyMessage]:
+        """Already-fetched messages from the front while ``pred`` holds (no blocking) -- lets
+        a manager apply a run of ``UP`` rows as one batch."""
+        out: List[KeyMessage] = []
+        if not self._pending and not self.closed:
+            recs = self.consumer.poll(8192, 0)
+            self._pending = [KeyMessage(k, v) for _, _, _, k, v in recs]
+            self._pending.reverse()
+        while self._pending and len(out) < max_n and pred(self._pending[-1]):
+            out.append(self._pending.pop())
+            if not self._pending and len(out) < max_n and not self.closed:
+                recs = self.consumer.poll(8192, 0)
+                self._pending = [KeyMessage(k, v) for _, _, _, k, v in recs]
+                self._pending.reverse()
+        return out
+
     def close(self) -> None:
         self.closed = True
 

@@ -444,3 +444,38 @@ def test_serving_model_topn_uses_kernel_and_batcher(cuda):
         best = np.argsort(-s)[:5]
         assert [i for i, _ in out[j]] == ["I%d" % b for b in best]
     assert m.batcher.requests == 40 and m.batcher.batches <= 40
+
+
+def test_bulk_up_batch_matches_per_message(tmp_path):
+    """apply_up_batch (native parse, bulk set_vectors) == applying each UP message alone,
+    including repeated IDs (last wins), known items, non-string IDs and a fallback row."""
+    import json as _json
+    from oryx_amd.models.als.serving import ALSServingModel, apply_up_batch
+    g = np.random.default_rng(2)
+    msgs = []
+    for j in range(300):
+        v = g.standard_normal(3).astype(np.float32).tolist()
+        if j % 3 == 0:
+            msgs.append(_json.dumps(["Y", "I%d" % (j % 40), v]))
+        else:
+            msgs.append(_json.dumps(["X", "U%d" % (j % 25), v, ["I%d" % (j % 7)]]))
+    msgs.append('["X", 77, [1, 2, 3]]')
+    msgs.append('["Y","I\\u00e9",[0.5,0.25,-1.0]]')
+    a = ALSServingModel(3, True, device=torch.device("cpu"))
+    b = ALSServingModel(3, True, device=torch.device("cpu"))
+    apply_up_batch(a, msgs)
+    for m in msgs:
+        u = _json.loads(m)
+        if u[0] == "X":
+            b.set_user_vector(str(u[1]), np.asarray(u[2], dtype=np.float32))
+            if len(u) > 3:
+                b.add_known_items(str(u[1]), [str(x) for x in u[3]])
+        else:
+            b.set_item_vector(str(u[1]), np.asarray(u[2], dtype=np.float32))
+    assert sorted(a.get_all_user_ids()) == sorted(b.get_all_user_ids())
+    assert sorted(a.get_all_item_ids()) == sorted(b.get_all_item_ids())
+    for uid in b.get_all_user_ids():
+        np.testing.assert_array_equal(a.get_user_vector(uid), b.get_user_vector(uid))
+        assert a.get_known_items(uid) == b.get_known_items(uid)
+    for iid in b.get_all_item_ids():
+        np.testing.assert_array_equal(a.get_item_vector(iid), b.get_item_vector(iid))
