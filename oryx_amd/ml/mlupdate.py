@@ -13,7 +13,9 @@ Equivalent of ``MLUpdate`` (``[ml]/MLUpdate.java:59-372``):
 
 Data is a :class:`~oryx_amd.api.Dataset` of (key, message) pairs; apps see message lists.
 GPU candidates run concurrently on one device from separate threads (the device queue
-serialises them) or sequentially across all ranks.
+serialises them); on several ranks with ``oryx.ml.eval.parallelism`` > 1 the ranks split into
+disjoint process groups that train different candidates at once (``_run_update_grouped``),
+otherwise candidates run one after another across all ranks.
 
 Sharded apps (``sharded_data = True``) on several ranks: each rank holds only its share of the
 data; every rank runs the whole candidate loop (split, build, evaluate -- the apps' collective
@@ -43,6 +45,18 @@ log = logging.getLogger(__name__)
 
 MODEL_FILE_NAME = "model.pmml"
 TIMINGS_FILE_NAME = "timings.json"
+
+
+def _with_dist(context, ctx: dist.DistContext):
+    """``context`` with its distributed context replaced by ``ctx`` (a subgroup)."""
+    if context is None or isinstance(context, dist.DistContext):
+        return ctx
+    if hasattr(context, "dist"):
+        import copy
+        c = copy.copy(context)
+        c.dist = ctx
+        return c
+    return ctx
 
 
 class MLUpdate(BatchLayerUpdate):
@@ -114,6 +128,11 @@ class MLUpdate(BatchLayerUpdate):
         self.dist_ctx = dctx
         # trainers that checkpoint or warm-start find their files under the model dir
         self.current_model_dir = ioutils.to_local_path(model_dir) if model_dir else None
+        n_groups = min(self.eval_parallelism, self.candidates, dctx.world_size)
+        if dctx.is_distributed and n_groups > 1:
+            self._run_update_grouped(context, new_msgs, past_msgs, combos, model_dir,
+                                     model_update_topic, dctx, n_groups)
+            return
         if dctx.is_distributed and self.sharded_data:
             self._run_update_sharded(context, new_msgs, past_msgs, combos, model_dir,
                                      model_update_topic, dctx)
@@ -145,6 +164,106 @@ class MLUpdate(BatchLayerUpdate):
         if model_update_topic is None:
             log.info("No update topic configured, not publishing models to a topic")
             return
+        self._publish_final(context, final_path, new_msgs, past_msgs, model_update_topic)
+
+    def _run_update_sharded(self, context, new_msgs, past_msgs, combos, model_dir,
+                            model_update_topic, dctx) -> None:
+        main = dctx.is_main
+        model_dir_local = ioutils.to_local_path(model_dir)
+        stamp = dist.broadcast_object(int(time.time() * 1000) if main else None, dctx)
+        candidates_path = os.path.join(model_dir_local, ".temporary", str(stamp))
+        if main:
+            os.makedirs(candidates_path, exist_ok=True)
+        results = [self._build_and_eval(i, combos, context, new_msgs, past_msgs,
+                                        candidates_path) for i in range(self.candidates)]
+        self._promote_and_publish(context, results, new_msgs, past_msgs, model_dir_local,
+                                  candidates_path, stamp, model_update_topic, dctx)
+
+    def _pick_best(self, results) -> Optional[int]:
+        best_i, best_eval = None, float("-inf")
+        for i, (path, ev) in enumerate(results):
+            if path is None:
+                continue
+            if ev == ev:
+                if ev > best_eval:
+                    best_eval, best_i = ev, i
+            elif best_i is None and self.test_fraction == 0.0:
+                best_i = i
+        return best_i
+
+    def _run_update_grouped(self, context, new_msgs, past_msgs, combos, model_dir,
+                            model_update_topic, dctx, n_groups) -> None:
+        """Candidate parallelism across GPUs (``MLUpdate.java:251-261`` runs candidates with
+        ``collectInParallel``): the ranks split into ``n_groups`` disjoint process groups and
+        group g builds and evaluates candidates g, g + G, ... with its own collectives, so
+        G candidates train at once on disjoint GPUs.  Sharded apps first replicate the data
+        into every group (member m of each group receives the shares of the ranks r with
+        r mod group-size == m).  Each group's first rank writes its candidates' files; the
+        (path, eval) results are exchanged over the control plane and every rank picks the
+        same winner, which is promoted and published as in the single-group flow."""
+        g, sub = dist.split_groups(dctx, n_groups)
+        G = dctx.world_size // sub.world_size
+        model_dir_local = ioutils.to_local_path(model_dir)
+        stamp = dist.broadcast_object(int(time.time() * 1000) if dctx.is_main else None, dctx)
+        seed_base = dist.broadcast_object(rng.next_seed() if dctx.is_main else None, dctx)
+        candidates_path = os.path.join(model_dir_local, ".temporary", str(stamp))
+        if dctx.is_main:
+            os.makedirs(candidates_path, exist_ok=True)
+        dist.barrier(dctx)
+        if self.sharded_data:
+            from ..parallel import shuffle
+            my_new = shuffle.replicate_to_groups(list(new_msgs), dctx, sub.world_size)
+            my_past = shuffle.replicate_to_groups(list(past_msgs), dctx, sub.world_size) \
+                if past_msgs is not None else None
+        else:
+            my_new, my_past = new_msgs, past_msgs
+        sub_context = _with_dist(context, sub)
+        self.dist_ctx = sub
+        mine = {}
+        try:
+            for i in range(g, self.candidates, G):
+                with rng.shared_seed_scope(seed_base + i):
+                    if self.sharded_data or sub.is_main or not sub.is_distributed:
+                        mine[i] = self._build_and_eval_inner(i, combos, sub_context, my_new,
+                                                             my_past, candidates_path)
+                    else:
+                        # non-sharded followers only join the group's collective build
+                        train, _ = self._split_train_test(my_new, my_past)
+                        if train:
+                            self.build_model(sub_context, train, combos[i % len(combos)], None)
+        finally:
+            self.dist_ctx = dctx
+        reported = mine if sub.is_main else {}
+        gathered = [None] * dctx.world_size
+        import torch.distributed as tdist
+        tdist.all_gather_object(gathered, reported, group=dctx.control)
+        merged = {}
+        for d in gathered:
+            merged.update(d or {})
+        results = [merged.get(i, (None, float("nan"))) for i in range(self.candidates)]
+        log.info("Candidate results over %d groups: %s", G, [ev for _, ev in results])
+        if self.sharded_data:
+            self._promote_and_publish(context, results, new_msgs, past_msgs, model_dir_local,
+                                      candidates_path, stamp, model_update_topic, dctx)
+            return
+        # non-sharded apps publish from rank 0 with its full copy of the data
+        best_i = self._pick_best(results)
+        final_path = os.path.join(model_dir_local, str(stamp + 1))
+        if dctx.is_main:
+            if best_i is None:
+                log.info("Unable to build any model")
+            else:
+                os.replace(results[best_i][0], final_path)
+            ioutils.delete_recursively(candidates_path)
+        dist.barrier(dctx)
+        if not dctx.is_main or best_i is None:
+            return
+        if model_update_topic is None:
+            log.info("No update topic configured, not publishing models to a topic")
+            return
+        self._publish_final(context, final_path, new_msgs, past_msgs, model_update_topic)
+
+    def _publish_final(self, context, final_path, new_msgs, past_msgs, model_update_topic):
         best_model_path = os.path.join(final_path, MODEL_FILE_NAME)
         if not os.path.exists(best_model_path):
             return
@@ -161,25 +280,12 @@ class MLUpdate(BatchLayerUpdate):
             self.publish_additional_model_data(context, best_model, new_msgs, past_msgs,
                                                final_path, model_update_topic)
 
-    def _run_update_sharded(self, context, new_msgs, past_msgs, combos, model_dir,
-                            model_update_topic, dctx) -> None:
+    def _promote_and_publish(self, context, results, new_msgs, past_msgs, model_dir_local,
+                             candidates_path, stamp, model_update_topic, dctx) -> None:
+        """Sharded flow after the candidates: rank 0 promotes the winner and sends ``MODEL``;
+        every rank publishes its share of the additional model data."""
         main = dctx.is_main
-        model_dir_local = ioutils.to_local_path(model_dir)
-        stamp = dist.broadcast_object(int(time.time() * 1000) if main else None, dctx)
-        candidates_path = os.path.join(model_dir_local, ".temporary", str(stamp))
-        if main:
-            os.makedirs(candidates_path, exist_ok=True)
-        results = [self._build_and_eval(i, combos, context, new_msgs, past_msgs,
-                                        candidates_path) for i in range(self.candidates)]
-        best_i, best_eval = None, float("-inf")
-        for i, (path, ev) in enumerate(results):
-            if path is None:
-                continue
-            if ev == ev:
-                if ev > best_eval:
-                    best_eval, best_i = ev, i
-            elif best_i is None and self.test_fraction == 0.0:
-                best_i = i
+        best_i = self._pick_best(results)
         final_path = os.path.join(model_dir_local, str(stamp + 1))
         if main:
             if best_i is None:

@@ -263,12 +263,12 @@ def _gather_rows(rows: torch.Tensor, ctx) -> torch.Tensor:
         return rows
     n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
     sizes = [torch.zeros_like(n) for _ in range(ctx.world_size)]
-    torch.distributed.all_gather(sizes, n)
+    dist.all_gather_list(sizes, n, ctx)
     mx = int(max(int(s) for s in sizes))
     pad = torch.zeros((mx,) + tuple(rows.shape[1:]), dtype=rows.dtype, device=rows.device)
     pad[:rows.shape[0]] = rows
     parts = [torch.zeros_like(pad) for _ in range(ctx.world_size)]
-    torch.distributed.all_gather(parts, pad)
+    dist.all_gather_list(parts, pad, ctx)
     return torch.cat([p[:int(s)] for p, s in zip(parts, sizes)])
 
 
@@ -315,7 +315,7 @@ def _init_random(x, k, gen, ctx):
     perm = torch.randperm(cands.shape[0], generator=gen)[:k]
     c = cands[perm.to(cands.device)]
     if ctx.is_distributed:
-        torch.distributed.broadcast(c, src=0)
+        dist.broadcast_tensor(c, ctx)
     return c
 
 
@@ -332,7 +332,7 @@ def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = 
     i0 = int(torch.randint(0, max(1, n), (1,), generator=gen))
     c0 = x[i0:i0 + 1].float() if n else torch.zeros((1, x.shape[1]), device=dev)
     if ctx.is_distributed:
-        torch.distributed.broadcast(c0, src=0)
+        dist.broadcast_tensor(c0, ctx)
     centers = c0
     _, d2 = assign(pts, centers, precision=precision)
     d2 = d2.clone()
@@ -358,7 +358,7 @@ def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = 
         dist.all_reduce_sum(w, ctx)
     chosen = _kmeanspp_weighted(centers.to(dev), w, k, gen).to(dev)
     if ctx.is_distributed:
-        torch.distributed.broadcast(chosen, src=0)
+        dist.broadcast_tensor(chosen, ctx)
     return chosen
 
 

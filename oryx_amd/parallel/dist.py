@@ -26,7 +26,8 @@ from . import watchdog
 
 __all__ = ["DistContext", "init_from_env", "get_context", "shard_range", "padded_shard_size",
            "all_gather_rows", "all_gather_rows_async", "all_reduce_sum", "broadcast_object",
-           "barrier", "run_info"]
+           "barrier", "run_info", "split_groups", "broadcast_tensor", "all_gather_list",
+           "global_rank"]
 
 
 @dataclass
@@ -36,8 +37,11 @@ class DistContext:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: Optional[str] = None
-    group: Optional[object] = None
+    group: Optional[object] = None          # None: the default (world) group
     control: Optional[object] = None
+    # global ranks of this context's members when it is a subgroup (rank / world_size are
+    # then positions within it); None for the world
+    group_ranks: Optional[List[int]] = None
     # ORYX_FORCE_COLLECTIVES=1: a world of one still initialises the process group and runs
     # every collective (exercises the RCCL code paths on a single GPU)
     forced: bool = False
@@ -170,9 +174,9 @@ def all_gather_rows(local: torch.Tensor, n_total: int, ctx: DistContext,
     with watchdog.guard("all_gather_rows"):
         if ctx.backend == "gloo":
             parts = list(full.chunk(ctx.world_size, 0))
-            tdist.all_gather(parts, local.contiguous())
+            tdist.all_gather(parts, local.contiguous(), group=ctx.group)
         else:
-            tdist.all_gather_into_tensor(full, local.contiguous())
+            tdist.all_gather_into_tensor(full, local.contiguous(), group=ctx.group)
     return full
 
 
@@ -189,15 +193,38 @@ def all_gather_rows_async(local: torch.Tensor, out: torch.Tensor, ctx: DistConte
         return None
     if ctx.backend == "gloo":
         parts = list(out.chunk(ctx.world_size, 0))
-        return tdist.all_gather(parts, local.contiguous(), async_op=True)
-    return tdist.all_gather_into_tensor(out, local.contiguous(), async_op=True)
+        return tdist.all_gather(parts, local.contiguous(), async_op=True, group=ctx.group)
+    return tdist.all_gather_into_tensor(out, local.contiguous(), async_op=True,
+                                        group=ctx.group)
 
 
 def all_reduce_sum(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:
     if ctx.is_distributed:
         with watchdog.guard("all_reduce"):
-            tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
+            tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=ctx.group)
     return t
+
+
+def global_rank(ctx: DistContext, rank: int) -> int:
+    """The global rank of member ``rank`` of ``ctx``'s group."""
+    return ctx.group_ranks[rank] if ctx.group_ranks is not None else rank
+
+
+def broadcast_tensor(t: torch.Tensor, ctx: DistContext, src: int = 0) -> torch.Tensor:
+    """In-place broadcast of ``t`` from group member ``src``."""
+    if ctx.is_distributed:
+        with watchdog.guard("broadcast"):
+            tdist.broadcast(t, src=global_rank(ctx, src), group=ctx.group)
+    return t
+
+
+def all_gather_list(parts: List[torch.Tensor], t: torch.Tensor, ctx: DistContext) -> None:
+    """``parts[r]`` <- member r's ``t`` (equal shapes)."""
+    if not ctx.is_distributed:
+        parts[0].copy_(t)
+        return
+    with watchdog.guard("all_gather"):
+        tdist.all_gather(parts, t, group=ctx.group)
 
 
 def broadcast_object(obj, ctx: DistContext, src: int = 0, control: bool = False):
@@ -208,10 +235,10 @@ def broadcast_object(obj, ctx: DistContext, src: int = 0, control: bool = False)
     lst = [obj]
     if control and ctx.control is not None:
         # control announcements legitimately wait a whole batch interval: no deadline
-        tdist.broadcast_object_list(lst, src=src, group=ctx.control)
+        tdist.broadcast_object_list(lst, src=global_rank(ctx, src), group=ctx.control)
     else:
         with watchdog.guard("broadcast_object"):
-            tdist.broadcast_object_list(lst, src=src)
+            tdist.broadcast_object_list(lst, src=global_rank(ctx, src), group=ctx.group)
     return lst[0]
 
 
@@ -219,9 +246,9 @@ def barrier(ctx: DistContext) -> None:
     if ctx.is_distributed:
         with watchdog.guard("barrier"):
             if ctx.backend == "nccl":
-                tdist.barrier(device_ids=[ctx.device.index])
+                tdist.barrier(group=ctx.group, device_ids=[ctx.device.index])
             else:
-                tdist.barrier()
+                tdist.barrier(group=ctx.group)
 
 
 def all_to_all_rows(send: torch.Tensor, send_counts: Sequence[int], ctx: DistContext
@@ -240,7 +267,7 @@ def _all_to_all_rows(send: torch.Tensor, send_counts: Sequence[int], ctx: DistCo
     if ctx.backend == "gloo":
         # gloo has no all_to_all: emulate with all_gather of counts and padded payloads
         allc = [torch.empty_like(counts) for _ in range(ctx.world_size)]
-        tdist.all_gather(allc, counts)
+        tdist.all_gather(allc, counts, group=ctx.group)
         recv_counts = torch.stack([c[ctx.rank] for c in allc])
         maxn = int(torch.stack(allc).max())
         chunks = list(torch.split(send, list(send_counts)))
@@ -252,13 +279,54 @@ def _all_to_all_rows(send: torch.Tensor, send_counts: Sequence[int], ctx: DistCo
                                   device=send.device)
                 if src == ctx.rank:
                     buf[:n] = chunks[dst]
-                tdist.broadcast(buf, src=src)
+                tdist.broadcast(buf, src=global_rank(ctx, src), group=ctx.group)
                 if dst == ctx.rank:
                     outs.append(buf[:n].clone())
         return torch.cat(outs) if outs else send[:0]
-    tdist.all_to_all_single(recv_counts, counts)
+    tdist.all_to_all_single(recv_counts, counts, group=ctx.group)
     recv = torch.empty((int(recv_counts.sum()),) + tuple(send.shape[1:]), dtype=send.dtype,
                        device=send.device)
     tdist.all_to_all_single(recv, send.contiguous(), output_split_sizes=recv_counts.tolist(),
-                            input_split_sizes=list(send_counts))
+                            input_split_sizes=list(send_counts), group=ctx.group)
     return recv
+
+
+_subgroups: dict = {}
+
+
+def split_groups(ctx: DistContext, n_groups: int):
+    """Partition the world into ``n_groups`` disjoint, equal, contiguous blocks of ranks
+    (``n_groups`` is lowered to the largest divisor of the world size not above it) and
+    return (this rank's block index, a :class:`DistContext` over that block).
+
+    Every rank must call this with the same ``n_groups`` (group creation is collective); the
+    process groups are created once per block layout and reused.  A block of one rank is an
+    ordinary single-process context (no collectives).  Contiguous blocks keep each block's
+    ranks on neighbouring GPUs.
+    """
+    W = ctx.world_size
+    n = max(1, min(int(n_groups), W))
+    while W % n:
+        n -= 1
+    if not ctx.is_distributed or n == 1:
+        return 0, ctx
+    size = W // n
+    key = (W, n)
+    if key not in _subgroups:
+        made = []
+        for g in range(n):
+            ranks = list(range(g * size, (g + 1) * size))
+            # new_group is collective over the world even for groups a rank is not in
+            pg = tdist.new_group(ranks=ranks, backend=ctx.backend)
+            ctl = tdist.new_group(ranks=ranks, backend="gloo",
+                                  timeout=datetime.timedelta(days=30))
+            made.append((ranks, pg, ctl))
+        _subgroups[key] = made
+    g = ctx.rank // size
+    ranks, pg, ctl = _subgroups[key][g]
+    if size == 1:
+        return g, DistContext(rank=0, world_size=1, local_rank=ctx.local_rank,
+                              device=ctx.device, group_ranks=ranks)
+    return g, DistContext(rank=ctx.rank - ranks[0], world_size=size, local_rank=ctx.local_rank,
+                          device=ctx.device, backend=ctx.backend, group=pg, control=ctl,
+                          group_ranks=ranks)

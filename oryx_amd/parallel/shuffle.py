@@ -98,6 +98,24 @@ def _route_strings(keys: Sequence[str], owner: np.ndarray, ctx) -> List[str]:
     return _blob_to_strings(got_blob.astype(np.uint8), got_lens)
 
 
+def replicate_to_groups(lines: Sequence[str], ctx: dist.DistContext,
+                        group_size: int) -> List[str]:
+    """Re-shard strings for candidate groups (:func:`dist.split_groups` blocks of
+    ``group_size`` contiguous ranks): this rank's lines go to member ``rank % group_size`` of
+    EVERY group, so each group together holds the whole data set once.  Returns the lines
+    this rank receives (source-rank order)."""
+    W = ctx.world_size
+    if not ctx.is_distributed or group_size >= W:
+        return list(lines)
+    G = W // group_size
+    m = ctx.rank % group_size
+    dests = np.array([g * group_size + m for g in range(G)], dtype=np.int64)
+    n = len(lines)
+    keys = list(lines) * G
+    owner = np.repeat(dests, n)
+    return _route_strings(keys, owner, ctx)
+
+
 class IdTable:
     """The owner side of a global dictionary: this rank's strings and their global codes."""
 
@@ -168,7 +186,7 @@ def all_gather_np(a: np.ndarray, ctx) -> np.ndarray:
     dev = _dev(ctx)
     t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     parts = [torch.empty_like(t) for _ in range(ctx.world_size)]
-    tdist.all_gather(parts, t)
+    dist.all_gather_list(parts, t, ctx)
     return torch.stack(parts).cpu().numpy()
 
 
@@ -212,7 +230,7 @@ def all_reduce_np(a: np.ndarray, ctx, op: str = "sum") -> np.ndarray:
     dev = _dev(ctx)
     t = torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     red = {"sum": tdist.ReduceOp.SUM, "max": tdist.ReduceOp.MAX, "min": tdist.ReduceOp.MIN}[op]
-    tdist.all_reduce(t, op=red)
+    tdist.all_reduce(t, op=red, group=ctx.group)
     return t.cpu().numpy()
 
 

@@ -18,3 +18,5 @@ tail -1 gpurun_out/bench_km_fp32.log | cut -c1-300; grep -o '"init_ms.*' gpurun_
 rm -rf gpurun_out/prof64
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof64 -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 > gpurun_out/prof64.log 2>&1 || { tail -20 gpurun_out/prof64.log; exit 1; }
 find gpurun_out/prof64 -name "*kernel_stats.csv" | head -1 | xargs -I{} head -12 {}
+timeout -k 10 600 python -u bench_serving.py --time-to-ready --items 1000000 --users 100000 --features 250 > gpurun_out/ttr.log 2>&1 || { tail -20 gpurun_out/ttr.log; exit 1; }
+tail -1 gpurun_out/ttr.log

@@ -182,3 +182,119 @@ def test_two_rank_sharded_als_generations(tmp_path):
         a, b = l.split(",")[:2]
         want.setdefault(a, set()).add(b)
     assert xs == want
+
+
+GROUP_SCRIPT = r"""
+import json, os, sys
+sys.path.insert(0, ROOT)
+import numpy as np
+from oryx_amd.layers.batch import BatchLayer
+from oryx_amd.parallel import dist
+from oryx_amd.transport.producer import LogTopicProducer
+from oryx_amd.utils import config as cfg
+
+tmp, app = sys.argv[1], sys.argv[2]
+base = {
+    "oryx.input-topic.broker": "log:" + tmp + "/log",
+    "oryx.update-topic.broker": "log:" + tmp + "/log",
+    "oryx.input-topic.partitions": 4,
+    "oryx.batch.storage.data-dir": tmp + "/data",
+    "oryx.batch.storage.model-dir": tmp + "/model",
+    "oryx.ml.eval.candidates": 2,
+    "oryx.ml.eval.parallelism": 2,
+    "oryx.gpu.device": "cpu",
+}
+if app == "als":
+    base.update({"oryx.batch.update-class": "com.cloudera.oryx.app.batch.mllib.als.ALSUpdate",
+                 "oryx.als.hyperparams.features": "[3,5]", "oryx.als.iterations": 3,
+                 "oryx.als.implicit": "true", "oryx.ml.eval.test-fraction": 0.2})
+else:
+    base.update({"oryx.batch.update-class": "com.cloudera.oryx.app.batch.mllib.rdf.RDFUpdate",
+                 "oryx.input-schema.num-features": 3,
+                 "oryx.input-schema.categorical-features": "[]",
+                 "oryx.input-schema.target-feature": "\"2\"",
+                 "oryx.rdf.num-trees": 3, "oryx.rdf.hyperparams.max-depth": "[2,4]",
+                 "oryx.ml.eval.test-fraction": 0.2})
+conf = cfg.overlay_on(base, cfg.get_default())
+ctx = dist.init_from_env(device="cpu")
+layer = BatchLayer(conf)
+if ctx.is_main:
+    layer._context = layer.layer_context()
+    layer._update = layer.load_update_instance()
+    layer.build_input_consumer()
+    g = np.random.default_rng(3)
+    if app == "als":
+        lines = ["U%d,I%d,%d,%d" % (g.integers(0, 60), g.integers(0, 30), g.integers(1, 5), j)
+                 for j in range(1500)]
+    else:
+        x = g.normal(0, 1, (800, 2))
+        lines = ["%r,%r,%r" % (float(a), float(b), float(3 * a - b)) for a, b in x]
+    prod = LogTopicProducer("log:" + tmp + "/log", "OryxInput", conf, async_=False)
+    prod.send_many([(None, l) for l in lines])
+    prod.close()
+    layer.run_interval(1000)
+    layer.close()
+    out = {"rank": 0}
+else:
+    out = {"rank": ctx.rank, "joined": layer.run_follower()}
+with open(os.path.join(tmp, "rank%d.json" % ctx.rank), "w") as f:
+    json.dump(out, f)
+"""
+
+
+def _run_grouped(tmp_path, app, nproc, port):
+    import json
+    script = tmp_path / "run.py"
+    script.write_text(GROUP_SCRIPT.replace("ROOT", repr(ROOT)))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % nproc, "--master-addr=127.0.0.1",
+           "--master-port=%d" % port, str(script), str(tmp_path), app]
+    r = subprocess.run(cmd, env=env, timeout=600, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for k in range(1, nproc):
+        assert json.loads((tmp_path / ("rank%d.json" % k)).read_text())["joined"] == 1
+    from oryx_amd.transport import log as tlog
+    topic = tlog.Topic(str(tmp_path / "log"), "OryxUpdate")
+    c = tlog.TopicConsumer(topic, "earliest")
+    msgs = []
+    while True:
+        batch = [(k, m) for _, _, _, k, m in c.poll(10000, 200)]
+        if not batch:
+            break
+        msgs.extend(batch)
+    c.close()
+    dirs = [d for d in os.listdir(tmp_path / "model") if not d.startswith(".")]
+    assert len(dirs) == 1
+    timing = json.loads((tmp_path / "model" / dirs[0] / "timings.json").read_text())
+    return msgs, timing
+
+
+def test_candidate_groups_sharded_als_four_ranks(tmp_path):
+    """Candidate parallelism on disjoint process groups (MLUpdate.java:251-261
+    collectInParallel): 4 gloo ranks split into 2 groups of 2, each group trains one ALS
+    candidate with its own collectives on the data replicated into it; one MODEL is
+    published and every user and item gets an UP row."""
+    msgs, timing = _run_grouped(tmp_path, "als", 4, 29651)
+    keys = [k for k, _ in msgs]
+    assert keys.count("MODEL") == 1
+    assert timing["ranks"] == 2          # the winner was trained by a 2-rank group
+    assert timing["eval"] is not None
+    import json
+    ups = [json.loads(m) for k, m in msgs if k == "UP"]
+    assert len({u[1] for u in ups if u[0] == "Y"}) == 30
+    assert len({u[1] for u in ups if u[0] == "X"}) == 60
+
+
+def test_candidate_groups_rdf_two_ranks(tmp_path):
+    """A non-sharded app (RDF) with 2 ranks and parallelism 2: each rank builds one candidate
+    alone; the better of the two is published once."""
+    msgs, timing = _run_grouped(tmp_path, "rdf", 2, 29653)
+    assert [k for k, _ in msgs] == ["MODEL"]
+    assert timing["eval"] is not None
+
+
+def test_replicate_to_groups_layout():
+    """Member m of every group receives the lines of the ranks r with r % size == m."""
+    from oryx_amd.parallel import dist, shuffle
+    assert shuffle.replicate_to_groups(["a", "b"], dist.DistContext(), 1) == ["a", "b"]
