@@ -19,6 +19,8 @@
 #include <unordered_map>
 #include <vector>
 
+#include "fastfloat.h"
+
 namespace {
 
 struct Dict {
@@ -208,38 +210,39 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
 }
 
 // Formats rows of a float matrix as JSON arrays "[v0,v1,...]" with shortest round-trip
-// float32 text, back to back in out; row_ends[r] = end offset of row r.  Returns bytes used
-// or -1 when out is too small.
+// float32 text (fastfloat.h), back to back in out; row_ends[r] = end offset of row r.  Rows are
+// split over the native threads (each formats its range into its own buffer, then the parts
+// are copied in order).  Returns bytes used or -1 when out is too small.
 long long oryx_format_float_rows(const float* mat, long long n, int k, long long stride,
                                  char* out, long long cap, long long* row_ends) {
-  long long pos = 0;
-  char tmp[32];
-  for (long long r = 0; r < n; ++r) {
-    const float* row = mat + r * stride;
-    if (pos + 2 + (long long)k * 16 > cap) return -1;
-    out[pos++] = '[';
-    for (int j = 0; j < k; ++j) {
-      if (j) out[pos++] = ',';
-      float v = row[j];
-      if (std::isnan(v)) { memcpy(out + pos, "NaN", 3); pos += 3; continue; }
-      if (std::isinf(v)) {
-        const char* s = v > 0 ? "Infinity" : "-Infinity";
-        size_t l = strlen(s);
-        memcpy(out + pos, s, l);
-        pos += l;
-        continue;
+  const int T = oryx_ff::native_threads();
+  std::vector<std::string> part((size_t)T);
+  std::vector<long long> lo_of((size_t)T + 1, n);
+  const int P = oryx_ff::parallel_ranges(n, 512, [&](long long lo, long long hi, int t) {
+    lo_of[(size_t)t] = lo;
+    std::string& o = part[(size_t)t];
+    o.resize((size_t)(hi - lo) * (size_t)(2 + 18 * (long long)k));
+    char* w = &o[0];
+    for (long long r = lo; r < hi; ++r) {
+      const float* row = mat + r * stride;
+      *w++ = '[';
+      for (int j = 0; j < k; ++j) {
+        if (j) *w++ = ',';
+        w = oryx_ff::write_float_json(row[j], w);
       }
-      auto res = std::to_chars(tmp, tmp + sizeof(tmp), v);
-      size_t l = res.ptr - tmp;
-      // Java-style: always show a decimal point for integral values ("1.0")
-      bool has_dot = false;
-      for (size_t q = 0; q < l; ++q) if (tmp[q] == '.' || tmp[q] == 'e') { has_dot = true; break; }
-      memcpy(out + pos, tmp, l);
-      pos += l;
-      if (!has_dot) { out[pos++] = '.'; out[pos++] = '0'; }
+      *w++ = ']';
+      row_ends[r] = w - o.data();   // local end; rebased below
     }
-    out[pos++] = ']';
-    row_ends[r] = pos;
+    o.resize((size_t)(w - o.data()));
+  });
+  long long pos = 0;
+  for (int t = 0; t < P; ++t) {
+    const long long lo = lo_of[(size_t)t], hi = t + 1 < P ? lo_of[(size_t)t + 1] : n;
+    const std::string& o = part[(size_t)t];
+    if (pos + (long long)o.size() > cap) return -1;
+    std::memcpy(out + pos, o.data(), o.size());
+    for (long long r = lo; r < hi; ++r) row_ends[r] += pos;
+    pos += (long long)o.size();
   }
   return pos;
 }
@@ -309,21 +312,16 @@ void json_quote(const std::string& s, std::string& o) {
 }
 
 void float_row(const float* row, int k, std::string& o) {
-  char tmp[32];
-  o += '[';
+  const size_t at = o.size();
+  o.resize(at + 2 + 18 * (size_t)k);
+  char* w = &o[at];
+  *w++ = '[';
   for (int j = 0; j < k; ++j) {
-    if (j) o += ',';
-    float v = row[j];
-    if (std::isnan(v)) { o += "NaN"; continue; }
-    if (std::isinf(v)) { o += v > 0 ? "Infinity" : "-Infinity"; continue; }
-    auto res = std::to_chars(tmp, tmp + sizeof(tmp), v);
-    size_t l = res.ptr - tmp;
-    bool has_dot = false;
-    for (size_t q = 0; q < l; ++q) if (tmp[q] == '.' || tmp[q] == 'e') { has_dot = true; break; }
-    o.append(tmp, l);
-    if (!has_dot) o += ".0";
+    if (j) *w++ = ',';
+    w = oryx_ff::write_float_json(row[j], w);
   }
-  o += ']';
+  *w++ = ']';
+  o.resize((size_t)(w - o.data()));
 }
 
 }  // namespace
@@ -410,75 +408,154 @@ struct JsonCursor {
 
 namespace {
 thread_local std::string g_up_ids, g_up_known;
+
+// One ["X"|"Y", id, [k floats], optional [ids...]] message: returns 0 (X) / 1 (Y) / 2 (not
+// parseable: nothing appended).  The id text is appended to ids, known ids ('\0'-terminated)
+// to known; cnt = number of known ids, -1 when the list is absent.
+int parse_one_up(const char* b, const char* e, int k, float* v, std::string& ids,
+                 std::string& known, long long& cnt, std::string& tok) {
+  JsonCursor c{b, e};
+  cnt = -1;
+  const size_t id_mark = ids.size(), known_mark = known.size();
+  bool ok = c.eat('[') && c.token(tok) && (tok == "X" || tok == "Y");
+  const int kind = ok && tok == "Y" ? 1 : 0;
+  ok = ok && c.eat(',') && c.token(tok);
+  if (ok) ids += tok;
+  ok = ok && c.eat(',') && c.eat('[');
+  for (int f = 0; ok && f < k; ++f) {
+    if (f && !c.eat(',')) { ok = false; break; }
+    c.ws();
+    const char* fb = c.p;
+    while (c.p < c.end && *c.p != ',' && *c.p != ']' && *c.p != ' ') ++c.p;
+    if (!oryx_ff::parse_float(fb, c.p, v[f])) {
+      const std::string_view t(fb, (size_t)(c.p - fb));   // NaN / Infinity spellings
+      if (t == "NaN") v[f] = std::numeric_limits<float>::quiet_NaN();
+      else if (t == "Infinity") v[f] = std::numeric_limits<float>::infinity();
+      else if (t == "-Infinity") v[f] = -std::numeric_limits<float>::infinity();
+      else ok = false;
+    }
+  }
+  ok = ok && c.eat(']');
+  if (ok && c.eat(',')) {
+    cnt = 0;
+    ok = c.eat('[');
+    if (ok && !c.eat(']')) {
+      do {
+        if (!c.token(tok)) { ok = false; break; }
+        known += tok;
+        known += '\0';
+        ++cnt;
+      } while (c.eat(','));
+      ok = ok && c.eat(']');
+    }
+  }
+  ok = ok && c.eat(']');
+  if (!ok) {
+    ids.resize(id_mark);
+    known.resize(known_mark);
+    cnt = -1;
+    return 2;
+  }
+  return kind;
 }
+
+// Parses messages [begin[j], end[j]) for j < n over the native threads into the thread-local
+// texts of the calling thread (id_ends are global offsets into them).  With stop_at_bad, the
+// result is cut before the first unparseable message; returns the number of messages kept.
+long long parse_up_spans(const char* buf, const long long* begin, const long long* end,
+                         long long n, int k, unsigned char* kinds, float* vecs,
+                         long long* id_ends, long long* known_cnt, bool stop_at_bad) {
+  g_up_ids.clear();
+  g_up_known.clear();
+  const int T = oryx_ff::native_threads();
+  std::vector<std::string> ids((size_t)T), known((size_t)T);
+  std::vector<long long> lo_of((size_t)T + 1, n);
+  const int P = oryx_ff::parallel_ranges(n, 128, [&](long long lo, long long hi, int t) {
+    lo_of[(size_t)t] = lo;
+    std::string tok;
+    std::string& id = ids[(size_t)t];
+    std::string& kn = known[(size_t)t];
+    for (long long j = lo; j < hi; ++j) {
+      kinds[j] = (unsigned char)parse_one_up(buf + begin[j], buf + end[j], k, vecs + j * k, id,
+                                             kn, known_cnt[j], tok);
+      id_ends[j] = (long long)id.size();   // local; rebased below
+    }
+  });
+  long long keep = n;
+  if (stop_at_bad)
+    for (long long j = 0; j < n; ++j)
+      if (kinds[j] == 2) { keep = j; break; }
+  size_t id_total = 0, kn_total = 0;
+  for (int t = 0; t < P; ++t) { id_total += ids[(size_t)t].size(); kn_total += known[(size_t)t].size(); }
+  g_up_ids.reserve(id_total);
+  g_up_known.reserve(kn_total);
+  for (int t = 0; t < P; ++t) {
+    const long long lo = lo_of[(size_t)t], hi = t + 1 < P ? lo_of[(size_t)t + 1] : n;
+    const long long base = (long long)g_up_ids.size();
+    for (long long j = lo; j < hi; ++j) id_ends[j] += base;
+    g_up_ids += ids[(size_t)t];
+    g_up_known += known[(size_t)t];
+  }
+  if (keep < n) {
+    // drop what follows the first bad message from the texts
+    g_up_ids.resize(keep ? (size_t)id_ends[keep - 1] : 0);
+    size_t kb = 0;
+    for (long long j = 0; j < keep; ++j)
+      if (known_cnt[j] > 0) {
+        for (long long q = 0; q < known_cnt[j]; ++q) kb = g_up_known.find('\0', kb) + 1;
+      }
+    g_up_known.resize(kb);
+  }
+  return keep;
+}
+}  // namespace
 
 extern "C" {
 
-// Parses n messages ["X"|"Y", id, [k floats], optional [ids...]] (back to back in buf, ends
-// = message end offsets).  kinds[j] = 0 (X) / 1 (Y) / 2 (unparseable: the caller falls back);
-// vecs [n][k]; id_ends[j] / known_cnt[j] index the id and known-item texts, fetched with
-// oryx_up_texts (ids, then known items, each back to back; known_ends per item).  Returns the
-// total number of known items.
+// Parses n messages (back to back in buf, ends = message end offsets).  kinds[j] = 0 (X) /
+// 1 (Y) / 2 (unparseable: the caller falls back); vecs [n][k]; id_ends[j] indexes the id
+// texts, known_cnt[j] = number of known ids (-1: no list); the texts are fetched with
+// oryx_up_texts (ids back to back, then known items '\0'-terminated).  Returns the total
+// number of known items.
 long long oryx_parse_up_batch(const char* buf, const long long* ends, long long n, int k,
                               unsigned char* kinds, float* vecs, long long* id_ends,
                               long long* known_cnt) {
-  g_up_ids.clear();
-  g_up_known.clear();
-  std::string tok;
-  long long start = 0, total_known = 0;
-  for (long long j = 0; j < n; ++j) {
-    JsonCursor c{buf + start, buf + ends[j]};
-    start = ends[j];
-    kinds[j] = 2;
-    known_cnt[j] = 0;
-    const size_t id_mark = g_up_ids.size(), known_mark = g_up_known.size();
-    bool ok = c.eat('[') && c.token(tok) && (tok == "X" || tok == "Y");
-    unsigned char kind = ok && tok == "Y" ? 1 : 0;
-    ok = ok && c.eat(',') && c.token(tok);
-    if (ok) g_up_ids += tok;
-    ok = ok && c.eat(',') && c.eat('[');
-    float* v = vecs + j * k;
-    for (int f = 0; ok && f < k; ++f) {
-      if (f && !c.eat(',')) { ok = false; break; }
-      c.ws();
-      const char* b = c.p;
-      while (c.p < c.end && *c.p != ',' && *c.p != ']' && *c.p != ' ') ++c.p;
-      auto r = std::from_chars(b, c.p, v[f]);
-      if (r.ec != std::errc() || r.ptr != c.p) {
-        std::string t(b, c.p - b);   // NaN / Infinity spellings
-        if (t == "NaN") v[f] = std::numeric_limits<float>::quiet_NaN();
-        else if (t == "Infinity") v[f] = std::numeric_limits<float>::infinity();
-        else if (t == "-Infinity") v[f] = -std::numeric_limits<float>::infinity();
-        else ok = false;
-      }
-    }
-    ok = ok && c.eat(']');
-    long long cnt = 0;
-    if (ok && c.eat(',')) {
-      ok = c.eat('[');
-      if (ok && !c.eat(']')) {
-        do {
-          if (!c.token(tok)) { ok = false; break; }
-          g_up_known += tok;
-          g_up_known += '\0';
-          ++cnt;
-        } while (c.eat(','));
-        ok = ok && c.eat(']');
-      }
-    }
-    ok = ok && c.eat(']');
-    if (!ok) {
-      g_up_ids.resize(id_mark);
-      g_up_known.resize(known_mark);
-      id_ends[j] = (long long)g_up_ids.size();
-      continue;
-    }
-    kinds[j] = kind;
-    id_ends[j] = (long long)g_up_ids.size();
-    known_cnt[j] = cnt;
-    total_known += cnt;
+  std::vector<long long> begin((size_t)n);
+  for (long long j = 0; j < n; ++j) begin[(size_t)j] = j ? ends[j - 1] : 0;
+  parse_up_spans(buf, begin.data(), ends, n, k, kinds, vecs, id_ends, known_cnt, false);
+  long long total = 0;
+  for (long long j = 0; j < n; ++j) if (known_cnt[j] > 0) total += known_cnt[j];
+  return total;
+}
+
+// The leading run of "UP" records of a raw poll buffer (oryx_reader_poll layout: per record
+// i64 offset, i64 timestamp, i32 key length (-1: none), i32 value length, key, value), parsed
+// as oryx_parse_up_batch does, stopping before the first record that is not a parseable UP.
+// At most max_n records; *consumed_bytes = buffer offset after the run.  Returns the run
+// length (0 when the first record is not one).
+long long oryx_parse_up_records(const char* raw, long long used, long long nrec, int k,
+                                long long max_n, unsigned char* kinds, float* vecs,
+                                long long* id_ends, long long* known_cnt,
+                                long long* consumed_bytes) {
+  std::vector<long long> begin, end, after;
+  long long pos = 0;
+  for (long long r = 0; r < nrec && r < max_n; ++r) {
+    if (pos + 24 > used) break;
+    int32_t kl, vl;
+    std::memcpy(&kl, raw + pos + 16, 4);
+    std::memcpy(&vl, raw + pos + 20, 4);
+    const long long kpos = pos + 24;
+    if (kl != 2 || raw[kpos] != 'U' || raw[kpos + 1] != 'P') break;
+    begin.push_back(kpos + 2);
+    end.push_back(kpos + 2 + vl);
+    pos = kpos + 2 + vl;
+    after.push_back(pos);
   }
-  return total_known;
+  const long long n = (long long)begin.size();
+  const long long keep = n ? parse_up_spans(raw, begin.data(), end.data(), n, k, kinds, vecs,
+                                            id_ends, known_cnt, true) : 0;
+  *consumed_bytes = keep ? after[(size_t)keep - 1] : 0;
+  return keep;
 }
 
 // The id texts (back to back) and the known-item texts ('\0'-terminated) of the last
@@ -491,6 +568,59 @@ long long oryx_up_texts(char* ids, long long ids_cap, char* known, long long kno
   return (long long)g_up_ids.size();
 }
 
+}  // extern "C"
+
+namespace {
+
+// One event's messages: ["X",user,row,[item]] if vx, then ["Y",item,row,[user]] if vy.
+void als_update_messages(Dict* du, Dict* di, long long ue, long long ie, const char* xrow,
+                         size_t xlen, const char* yrow, size_t ylen, bool vx, bool vy,
+                         bool with_known, std::string& o, std::string& qu, std::string& qi) {
+  qu.clear();
+  qi.clear();
+  json_quote(du->keys[(size_t)ue], qu);
+  json_quote(di->keys[(size_t)ie], qi);
+  if (vx) {
+    o += "[\"X\",";
+    o += qu;
+    o += ',';
+    o.append(xrow, xlen);
+    if (with_known) { o += ",["; o += qi; o += ']'; }
+    o += "]\n";
+  }
+  if (vy) {
+    o += "[\"Y\",";
+    o += qi;
+    o += ',';
+    o.append(yrow, ylen);
+    if (with_known) { o += ",["; o += qu; o += ']'; }
+    o += "]\n";
+  }
+}
+
+// Runs the per-event formatter over the native threads and joins the parts into out.
+template <class Fn>
+long long join_event_parts(long long n, char* out, long long cap, Fn&& fn) {
+  const int T = oryx_ff::native_threads();
+  std::vector<std::string> part((size_t)T);
+  const int P = oryx_ff::parallel_ranges(n, 256, [&](long long lo, long long hi, int t) {
+    fn(lo, hi, part[(size_t)t]);
+  });
+  long long need = 0;
+  for (int t = 0; t < P; ++t) need += (long long)part[(size_t)t].size();
+  if (need > cap) return -need;
+  long long pos = 0;
+  for (int t = 0; t < P; ++t) {
+    std::memcpy(out + pos, part[(size_t)t].data(), part[(size_t)t].size());
+    pos += (long long)part[(size_t)t].size();
+  }
+  return pos;
+}
+
+}  // namespace
+
+extern "C" {
+
 // The ALS speed layer's update messages for n folded-in events, in the reference's order
 // (per event: ["X",user,[Xu'],[item]] if vx, then ["Y",item,[Yi'],[user]] if vy;
 // ALSSpeedModelManager.java:182-215), '\n'-separated into out.  IDs come straight from the
@@ -501,34 +631,39 @@ long long oryx_format_als_updates(void* users, void* items, const long long* u,
                                   int k, int with_known, char* out, long long cap) {
   auto* du = static_cast<Dict*>(users);
   auto* di = static_cast<Dict*>(items);
-  std::string o;
-  o.reserve((size_t)n * (size_t)(k * 12 + 48));
-  std::string qu, qi;
-  for (long long e = 0; e < n; ++e) {
-    qu.clear();
-    qi.clear();
-    json_quote(du->keys[(size_t)u[e]], qu);
-    json_quote(di->keys[(size_t)i[e]], qi);
-    if (vx[e]) {
-      o += "[\"X\",";
-      o += qu;
-      o += ',';
-      float_row(nx + e * k, k, o);
-      if (with_known) { o += ",["; o += qi; o += ']'; }
-      o += "]\n";
+  return join_event_parts(n, out, cap, [&](long long lo, long long hi, std::string& o) {
+    o.reserve((size_t)(hi - lo) * (size_t)(k * 24 + 96));
+    std::string qu, qi, xr, yr;
+    for (long long e = lo; e < hi; ++e) {
+      xr.clear();
+      yr.clear();
+      if (vx[e]) float_row(nx + e * k, k, xr);
+      if (vy[e]) float_row(ny + e * k, k, yr);
+      als_update_messages(du, di, u[e], i[e], xr.data(), xr.size(), yr.data(), yr.size(),
+                          vx[e] != 0, vy[e] != 0, with_known != 0, o, qu, qi);
     }
-    if (vy[e]) {
-      o += "[\"Y\",";
-      o += qi;
-      o += ',';
-      float_row(ny + e * k, k, o);
-      if (with_known) { o += ",["; o += qu; o += ']'; }
-      o += "]\n";
+  });
+}
+
+// As oryx_format_als_updates with the rows already formatted (e.g. on the GPU): row e of
+// X is xtext[xends[e-1], xends[e]) (xends[-1] = 0), likewise Y.
+long long oryx_assemble_als_updates(void* users, void* items, const long long* u,
+                                    const long long* i, const char* xtext,
+                                    const long long* xends, const char* ytext,
+                                    const long long* yends, const unsigned char* vx,
+                                    const unsigned char* vy, long long n, int with_known,
+                                    char* out, long long cap) {
+  auto* du = static_cast<Dict*>(users);
+  auto* di = static_cast<Dict*>(items);
+  return join_event_parts(n, out, cap, [&](long long lo, long long hi, std::string& o) {
+    std::string qu, qi;
+    for (long long e = lo; e < hi; ++e) {
+      const long long xs = e ? xends[e - 1] : 0, ys = e ? yends[e - 1] : 0;
+      als_update_messages(du, di, u[e], i[e], xtext + xs, (size_t)(xends[e] - xs),
+                          ytext + ys, (size_t)(yends[e] - ys), vx[e] != 0, vy[e] != 0,
+                          with_known != 0, o, qu, qi);
     }
-  }
-  if ((long long)o.size() > cap) return -(long long)o.size();
-  memcpy(out, o.data(), o.size());
-  return (long long)o.size();
+  });
 }
 
 }  // extern "C"

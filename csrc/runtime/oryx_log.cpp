@@ -43,21 +43,39 @@ constexpr uint32_t kMagic = 0x4F52594Cu;  // "ORYL"
 constexpr size_t kHeader = 4 + 4 + 8 + 8 + 4 + 4;
 constexpr uint32_t kNullKey = 0xFFFFFFFFu;
 
-uint32_t crc_table[256];
+// CRC-32 (IEEE, zlib's polynomial), slicing-by-8: eight table lookups per 8 input bytes
+// (~1 byte/cycle instead of ~0.2 for the bytewise loop) -- every poll and bulk read checks
+// every record, and model loads read gigabytes of update messages.
+uint32_t crc_tab[8][256];
 std::once_flag crc_once;
 
 void init_crc() {
   for (uint32_t i = 0; i < 256; ++i) {
     uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
-    crc_table[i] = c;
+    crc_tab[0][i] = c;
   }
+  for (uint32_t i = 0; i < 256; ++i)
+    for (int t = 1; t < 8; ++t)
+      crc_tab[t][i] = (crc_tab[t - 1][i] >> 8) ^ crc_tab[0][crc_tab[t - 1][i] & 0xFF];
 }
 
 uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc = 0) {
   std::call_once(crc_once, init_crc);
   crc = ~crc;
-  for (size_t i = 0; i < n; ++i) crc = crc_table[(crc ^ p[i]) & 0xFF] ^ (crc >> 8);
+  while (n >= 8) {
+    uint32_t lo, hi;
+    memcpy(&lo, p, 4);
+    memcpy(&hi, p + 4, 4);
+    lo ^= crc;
+    crc = crc_tab[7][lo & 0xFF] ^ crc_tab[6][(lo >> 8) & 0xFF] ^
+          crc_tab[5][(lo >> 16) & 0xFF] ^ crc_tab[4][lo >> 24] ^
+          crc_tab[3][hi & 0xFF] ^ crc_tab[2][(hi >> 8) & 0xFF] ^
+          crc_tab[1][(hi >> 16) & 0xFF] ^ crc_tab[0][hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) crc = crc_tab[0][(crc ^ *p++) & 0xFF] ^ (crc >> 8);
   return ~crc;
 }
 
@@ -236,13 +254,37 @@ struct Reader {
   int64_t pos = 0;
   int64_t next_offset = 0;
   int fd = -1;
+  // read-ahead block of the current segment file: polls parse frames out of it instead of
+  // two preads per record (invalidated whenever fd changes or a frame is incomplete/bad)
+  std::vector<uint8_t> blk;
+  int64_t blk_pos = -1;
+  size_t blk_len = 0;
 };
+
+// Pointer to bytes [pos, pos + n) of the reader's segment (through the read-ahead block), or
+// nullptr when the file does not hold them (yet).
+const uint8_t* reader_bytes(Reader* r, int64_t pos, size_t n) {
+  if (r->blk_pos >= 0 && pos >= r->blk_pos &&
+      (size_t)(pos - r->blk_pos) + n <= r->blk_len)
+    return r->blk.data() + (pos - r->blk_pos);
+  const size_t want = n > (1u << 20) ? n : (1u << 20);
+  if (r->blk.size() < want) r->blk.resize(want);
+  const ssize_t got = pread(r->fd, r->blk.data(), want, pos);
+  r->blk_pos = pos;
+  r->blk_len = got > 0 ? (size_t)got : 0;
+  if (r->blk_len < n) {
+    r->blk_pos = -1;
+    return nullptr;
+  }
+  return r->blk.data();
+}
 
 // Position a reader at `offset` (clamped to [begin, end]).
 void reader_seek(Reader* r, int64_t offset) {
   const std::string& dir = r->topic->parts[r->part].dir;
   std::vector<int64_t> segs = list_segments(dir);
   if (r->fd >= 0) { close(r->fd); r->fd = -1; }
+  r->blk_pos = -1;
   if (segs.empty()) { r->seg_base = 0; r->pos = 0; r->next_offset = 0; return; }
   if (offset < segs.front()) offset = segs.front();
   size_t idx = 0;
@@ -512,8 +554,6 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
   auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
   long long used = 0;
   int count = 0;
-  uint8_t hdr[kHeader];
-  std::vector<uint8_t> payload;
   int sleep_us = 200;
   for (;;) {
     if (r->fd < 0) {
@@ -521,19 +561,23 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
     }
     bool progressed = false;
     while (r->fd >= 0 && count < max_records) {
-      if (pread(r->fd, hdr, kHeader, r->pos) != (ssize_t)kHeader) break;
+      const uint8_t* h = reader_bytes(r, r->pos, kHeader);
+      if (!h) break;
       uint32_t magic, crc, klen, vlen;
       uint64_t off;
       int64_t ts;
-      memcpy(&magic, hdr, 4); memcpy(&crc, hdr + 4, 4); memcpy(&off, hdr + 8, 8);
-      memcpy(&ts, hdr + 16, 8); memcpy(&klen, hdr + 24, 4); memcpy(&vlen, hdr + 28, 4);
-      if (magic != kMagic) break;
+      memcpy(&magic, h, 4); memcpy(&crc, h + 4, 4); memcpy(&off, h + 8, 8);
+      memcpy(&ts, h + 16, 8); memcpy(&klen, h + 24, 4); memcpy(&vlen, h + 28, 4);
+      if (magic != kMagic) { r->blk_pos = -1; break; }
       size_t kl = klen == kNullKey ? 0 : klen;
       size_t plen = kl + vlen;
-      payload.resize(16 + plen);
-      memcpy(payload.data(), hdr + 8, 16);
-      if (plen && pread(r->fd, payload.data() + 16, plen, r->pos + kHeader) != (ssize_t)plen) break;
-      if (crc32(payload.data(), 16 + plen) != crc) {
+      // the whole frame, so header and payload are contiguous in the block
+      const uint8_t* f = reader_bytes(r, r->pos, kHeader + plen);
+      if (!f) break;
+      const uint8_t* pl = f + kHeader;
+      uint32_t c = crc32(f + 8, 16);
+      if (crc32(pl, plen, c) != crc) {
+        r->blk_pos = -1;
         // A torn or in-progress write can only be the tail of the segment; a bad frame with
         // a complete frame header written after it is corruption, reported instead of being
         // waited on forever.
@@ -559,7 +603,7 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
       int32_t o_kl = klen == kNullKey ? -1 : (int32_t)klen;
       int32_t o_vl = (int32_t)vlen;
       memcpy(o, &o_off, 8); memcpy(o + 8, &ts, 8); memcpy(o + 16, &o_kl, 4);
-      memcpy(o + 20, &o_vl, 4); memcpy(o + 24, payload.data() + 16, plen);
+      memcpy(o + 20, &o_vl, 4); memcpy(o + 24, pl, plen);
       used += need;
       r->pos += kHeader + plen;
       r->next_offset = (int64_t)off + 1;
@@ -574,6 +618,7 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
       for (int64_t b : segs) {
         if (b > r->seg_base && b <= r->next_offset) {
           if (r->fd >= 0) close(r->fd);
+          r->blk_pos = -1;
           r->seg_base = b;
           r->pos = 0;
           r->fd = open(seg_name(dir, b).c_str(), O_RDONLY);

@@ -102,8 +102,8 @@ def parse_up_batch(messages: Sequence[str], k: int):
     """Bulk-parse ALS ``UP`` messages ``["X"|"Y", id, [k floats], [known ids]?]``.
 
     Returns (kinds uint8 [n] -- 0 X, 1 Y, 2 unparseable --, ids list, vectors fp32 [n, k],
-    known lists per message (None when absent)).  One native pass instead of a JSON parse
-    per message (the serving / speed model load of millions of rows).
+    known lists per message (None when absent)).  One native pass (threaded) instead of a
+    JSON parse per message (the serving / speed model load of millions of rows).
     """
     n = len(messages)
     enc = [m.encode("utf-8") for m in messages]
@@ -114,37 +114,69 @@ def parse_up_batch(messages: Sequence[str], k: int):
     id_ends = np.empty(n, dtype=np.int64)
     kcnt = np.empty(n, dtype=np.int64)
     vp = ctypes.c_void_p
-    lib = native.runtime()
-    lib.oryx_parse_up_batch(blob, ends.ctypes.data_as(vp), n, int(k), kinds.ctypes.data_as(vp),
-                            vecs.ctypes.data_as(vp), id_ends.ctypes.data_as(vp),
-                            kcnt.ctypes.data_as(vp))
-    ids_cap = int(id_ends[-1]) if n else 0
-    known_cap = max(16, len(blob))
-    ib = ctypes.create_string_buffer(max(1, ids_cap))
-    kb = ctypes.create_string_buffer(known_cap)
-    got = lib.oryx_up_texts(ib, max(1, ids_cap), kb, known_cap)
+    native.runtime().oryx_parse_up_batch(blob, ends.ctypes.data_as(vp), n, int(k),
+                                         kinds.ctypes.data_as(vp), vecs.ctypes.data_as(vp),
+                                         id_ends.ctypes.data_as(vp), kcnt.ctypes.data_as(vp))
+    ids, known = _up_texts(id_ends, kcnt, len(blob))
+    return kinds, ids, vecs, known
+
+
+def parse_up_records(raw_ptr: int, used: int, nrec: int, k: int, max_n: int):
+    """The leading run of ``UP`` records of a raw log poll buffer (see
+    ``oryx_parse_up_records``): returns (count, consumed bytes, kinds, ids, vectors, known) --
+    count 0 when the first record is not a parseable ``UP``."""
+    m = min(nrec, max_n)
+    kinds = np.empty(m, dtype=np.uint8)
+    vecs = np.empty((m, k), dtype=np.float32)
+    id_ends = np.empty(m, dtype=np.int64)
+    kcnt = np.empty(m, dtype=np.int64)
+    consumed = ctypes.c_longlong(0)
+    vp = ctypes.c_void_p
+    got = native.runtime().oryx_parse_up_records(
+        ctypes.c_void_p(raw_ptr), int(used), int(nrec), int(k), int(max_n),
+        kinds.ctypes.data_as(vp), vecs.ctypes.data_as(vp), id_ends.ctypes.data_as(vp),
+        kcnt.ctypes.data_as(vp), ctypes.byref(consumed))
+    if got <= 0:
+        return 0, 0, None, None, None, None
+    ids, known = _up_texts(id_ends[:got], kcnt[:got], int(used))
+    return got, consumed.value, kinds[:got], ids, vecs[:got], known
+
+
+def _up_texts(id_ends: np.ndarray, kcnt: np.ndarray, bound: int):
+    """IDs and known-item lists of the last native UP parse (thread-local texts)."""
+    n = len(id_ends)
+    ids_cap = max(1, int(id_ends[-1]) if n else 0)
+    known_cap = max(16, bound)
+    ib = np.empty(ids_cap, dtype=np.uint8)
+    kb = np.empty(known_cap, dtype=np.uint8)
+    vp = ctypes.c_void_p
+    got = native.runtime().oryx_up_texts(ib.ctypes.data_as(vp), ids_cap,
+                                         kb.ctypes.data_as(vp), known_cap)
     if got < 0:
         raise RuntimeError("UP batch texts exceed their buffers")
-    raw_ids = ctypes.string_at(ib, ids_cap).decode("utf-8")
-    starts = np.r_[0, id_ends[:-1]].tolist()
-    ids = [raw_ids[a:b] for a, b in zip(starts, id_ends.tolist())] if raw_ids.isascii() else \
-        [ctypes.string_at(ib, ids_cap)[a:b].decode("utf-8") for a, b in zip(starts,
-                                                                            id_ends.tolist())]
-    total = int(kcnt.sum())
+    raw = ib[:int(id_ends[-1]) if n else 0].tobytes()
+    starts = np.r_[0, id_ends[:-1]].tolist() if n else []
+    if raw.isascii():
+        text = raw.decode("ascii")
+        ids = [text[a:b] for a, b in zip(starts, id_ends.tolist())]
+    else:
+        ids = [raw[a:b].decode("utf-8") for a, b in zip(starts, id_ends.tolist())]
     known: List[Optional[List[str]]] = [None] * n
+    pos_c = kcnt > 0
+    total = int(kcnt[pos_c].sum()) if n else 0
     if total:
-        flat = ctypes.string_at(kb, known_cap).split(b"\0")[:total]
-        flat = [x.decode("utf-8") for x in flat]
+        flat = [x.decode("utf-8") for x in kb.tobytes().split(b"\0", total)[:total]]
         pos = 0
         for j, c in enumerate(kcnt.tolist()):
-            if c:
+            if c > 0:
                 known[j] = flat[pos:pos + c]
                 pos += c
-    # a present-but-empty known list ("[...],[]]") is an empty list, not None
-    for j, e in enumerate(enc):
-        if known[j] is None and kinds[j] != 2 and e.rstrip().endswith(b"[]]"):
+            elif c == 0:
+                known[j] = []
+    else:
+        for j in np.nonzero(kcnt == 0)[0].tolist():
             known[j] = []
-    return kinds, ids, vecs, known
+    return ids, known
 
 
 def format_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndarray,
@@ -162,41 +194,75 @@ def format_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndarra
     vx = np.ascontiguousarray(vx, dtype=np.uint8)
     vy = np.ascontiguousarray(vy, dtype=np.uint8)
     vp = ctypes.c_void_p
-    cap = n * (k * 16 + 256)
     lib = native.runtime()
+    return _run_message_writer(n * (k * 20 + 256), lambda out, cap: lib.oryx_format_als_updates(
+        users.handle, items.handle, u.ctypes.data_as(vp), i.ctypes.data_as(vp),
+        nx.ctypes.data_as(vp), ny.ctypes.data_as(vp), vx.ctypes.data_as(vp),
+        vy.ctypes.data_as(vp), n, k, int(bool(with_known)), out, cap))
+
+
+def assemble_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndarray,
+                         xrows, yrows, vx: np.ndarray, vy: np.ndarray,
+                         with_known: bool) -> List[str]:
+    """As :func:`format_als_updates` with the factor rows already formatted
+    (:class:`~oryx_amd.ops.textfmt.RowText`, e.g. by the GPU formatter)."""
+    n = len(u)
+    if n == 0:
+        return []
+    u = np.ascontiguousarray(u, dtype=np.int64)
+    i = np.ascontiguousarray(i, dtype=np.int64)
+    vx = np.ascontiguousarray(vx, dtype=np.uint8)
+    vy = np.ascontiguousarray(vy, dtype=np.uint8)
+    xe = np.ascontiguousarray(xrows.ends, dtype=np.int64)
+    ye = np.ascontiguousarray(yrows.ends, dtype=np.int64)
+    vp = ctypes.c_void_p
+    lib = native.runtime()
+    cap = len(xrows.blob) + len(yrows.blob) + n * 256
+    return _run_message_writer(cap, lambda out, c: lib.oryx_assemble_als_updates(
+        users.handle, items.handle, u.ctypes.data_as(vp), i.ctypes.data_as(vp), xrows.blob,
+        xe.ctypes.data_as(vp), yrows.blob, ye.ctypes.data_as(vp), vx.ctypes.data_as(vp),
+        vy.ctypes.data_as(vp), n, int(bool(with_known)), out, c))
+
+
+def _run_message_writer(cap: int, call) -> List[str]:
+    """Runs a native '\\n'-separated message writer (retrying once with the size it asks
+    for) and splits its output."""
     while True:
-        out = ctypes.create_string_buffer(cap)
-        used = lib.oryx_format_als_updates(users.handle, items.handle, u.ctypes.data_as(vp),
-                                           i.ctypes.data_as(vp), nx.ctypes.data_as(vp),
-                                           ny.ctypes.data_as(vp), vx.ctypes.data_as(vp),
-                                           vy.ctypes.data_as(vp), n, k, int(bool(with_known)),
-                                           out, cap)
+        out = np.empty(cap, dtype=np.uint8)
+        used = call(out.ctypes.data_as(ctypes.c_void_p), cap)
         if used >= 0:
             break
         cap = -used + 1
     if used == 0:
         return []
-    msgs = ctypes.string_at(out, used).decode("ascii").split("\n")
+    msgs = out[:used].tobytes().decode("ascii").split("\n")
     msgs.pop()
     return msgs
 
 
-def format_float_rows(mat: np.ndarray) -> List[str]:
-    """JSON array text of each row, shortest float32 round-trip digits (Jackson-like)."""
+def format_float_rows_blob(mat: np.ndarray):
+    """JSON array text of each row (shortest float32 round-trip digits, Jackson-like) as one
+    :class:`~oryx_amd.ops.textfmt.RowText` (native, threaded)."""
+    from .ops.textfmt import RowText
     mat = np.ascontiguousarray(mat, dtype=np.float32)
     n, k = mat.shape
-    cap = n * (2 + k * 17) + 16
-    out = ctypes.create_string_buffer(cap)
+    if n == 0:
+        return RowText(b"", np.zeros(0, dtype=np.int64))
+    cap = n * (2 + k * 18) + 16
+    out = np.empty(cap, dtype=np.uint8)
     ends = np.empty(n, dtype=np.int64)
     vp = ctypes.c_void_p
-    used = native.runtime().oryx_format_float_rows(mat.ctypes.data_as(vp), n, k, k, out, cap,
+    used = native.runtime().oryx_format_float_rows(mat.ctypes.data_as(vp), n, k, k,
+                                                   out.ctypes.data_as(vp), cap,
                                                    ends.ctypes.data_as(vp))
     if used < 0:
         raise RuntimeError("format buffer too small")
-    raw = out.raw[:used].decode("ascii")
-    res = []
-    start = 0
-    for e in ends.tolist():
-        res.append(raw[start:e])
-        start = e
-    return res
+    return RowText(out[:used].tobytes(), ends)
+
+
+def format_float_rows(mat: np.ndarray) -> List[str]:
+    """JSON array text of each row, shortest float32 round-trip digits (Jackson-like)."""
+    mat = np.asarray(mat, dtype=np.float32)
+    if mat.shape[0] == 0:
+        return []
+    return format_float_rows_blob(mat).rows()

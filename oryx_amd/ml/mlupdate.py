@@ -67,6 +67,7 @@ class MLUpdate(BatchLayerUpdate):
     def __init__(self, config):
         self.config = config
         self.dist_ctx = None
+        self.promoted_from: Optional[str] = None
         self.test_fraction = config.get_double("oryx.ml.eval.test-fraction")
         candidates = config.get_int("oryx.ml.eval.candidates")
         self.eval_parallelism = config.get_int("oryx.ml.eval.parallelism")
@@ -155,6 +156,8 @@ class MLUpdate(BatchLayerUpdate):
         best = self._find_best_candidate_path(context, new_msgs, past_msgs, combos,
                                               candidates_path)
         final_path = os.path.join(model_dir_local, str(int(time.time() * 1000)))
+        # apps may keep what they built in memory, keyed by candidate path
+        self.promoted_from = best
         if best is None:
             log.info("Unable to build any model")
         else:
@@ -249,6 +252,7 @@ class MLUpdate(BatchLayerUpdate):
         # non-sharded apps publish from rank 0 with its full copy of the data
         best_i = self._pick_best(results)
         final_path = os.path.join(model_dir_local, str(stamp + 1))
+        self.promoted_from = results[best_i][0] if best_i is not None else None
         if dctx.is_main:
             if best_i is None:
                 log.info("Unable to build any model")
@@ -287,6 +291,7 @@ class MLUpdate(BatchLayerUpdate):
         main = dctx.is_main
         best_i = self._pick_best(results)
         final_path = os.path.join(model_dir_local, str(stamp + 1))
+        self.promoted_from = results[best_i][0] if best_i is not None else None
         if main:
             if best_i is None:
                 log.info("Unable to build any model")

@@ -45,6 +45,7 @@ from ... import ingest
 from ...ml import hyperparams as hp
 from ...ml.mlupdate import MLUpdate
 from ...parallel import dist, shuffle
+from ...ops import textfmt
 from ...utils import config as cfg, ioutils, pmml as pmmlu, rng, text
 from . import evaluation
 from .trainer import ALSTrainer
@@ -134,11 +135,23 @@ def aggregate_scores_device(u: np.ndarray, i: np.ndarray, s: np.ndarray, ts: np.
     return (gu.cpu().numpy(), (gk - gu * n_i).cpu().numpy(), out[keep].cpu().numpy())
 
 
+_NO_TS = -(1 << 62)     # parse marker of a line without a timestamp
+
+
 def parse_ratings(lines: Sequence[str], users: ingest.IdDict, items: ingest.IdDict,
                   decay_factor: float = 1.0, zero_threshold: float = 0.0,
-                  now_ms: Optional[int] = None):
+                  now_ms: Optional[int] = None, raw_out: Optional[list] = None):
+    """Parse + decay + zero-threshold.  ``raw_out`` (a list) receives the undecayed parse
+    with lines lacking a timestamp at 0 -- what :func:`known_items_json_parsed` needs -- so
+    the publish step can skip a second parse of the same data."""
     now = int(time.time() * 1000) if now_ms is None else now_ms
-    u, i, s, ts = ingest.parse_ratings(lines, users, items, default_ts=now)
+    if raw_out is not None:
+        u, i, s, ts0 = ingest.parse_ratings(lines, users, items, default_ts=_NO_TS)
+        missing = ts0 == _NO_TS
+        raw_out.extend([u, i, s, np.where(missing, 0, ts0)])
+        ts = np.where(missing, now, ts0)
+    else:
+        u, i, s, ts = ingest.parse_ratings(lines, users, items, default_ts=now)
     if decay_factor < 1.0:
         days = np.maximum(0, now - ts) / 86400000.0
         s = np.where(ts >= now, s, s * np.power(decay_factor, days))
@@ -154,14 +167,18 @@ def _timestamps(lines: Sequence[str]) -> np.ndarray:
     return ts
 
 
-def write_features(path: str, ids: List[str], mat: np.ndarray) -> None:
-    """``X/`` or ``Y/`` directory with one gzip part of ``[id,[floats]]`` JSON lines."""
+def write_features(path: str, ids: List[str], mat) -> None:
+    """``X/`` or ``Y/`` directory with one gzip part of ``[id,[floats]]`` JSON lines (the
+    reference's Spark text output with the gzip codec); ``mat`` is a float matrix or its
+    pre-formatted :class:`~oryx_amd.ops.textfmt.RowText`."""
     os.makedirs(path, exist_ok=True)
-    rows = ingest.format_float_rows(mat)
-    with gzip.open(os.path.join(path, "part-00000.gz"), "wt", encoding="utf-8",
-                   compresslevel=1) as f:
-        for id_, row in zip(ids, rows):
-            f.write("[%s,%s]\n" % (json.dumps(id_), row))
+    rows = mat if isinstance(mat, textfmt.RowText) else textfmt.format_rows(mat)
+    text = rows.blob.decode("ascii")
+    starts = [0] + rows.ends[:-1].tolist()
+    data = "".join("[%s,%s]\n" % (json.dumps(id_), text[a:b])
+                   for id_, a, b in zip(ids, starts, rows.ends.tolist())).encode("utf-8")
+    with open(os.path.join(path, "part-00000.gz"), "wb") as f:
+        f.write(gzip.compress(data, compresslevel=1))
 
 
 def read_features(path: str) -> Tuple[List[str], np.ndarray]:
@@ -251,12 +268,34 @@ class ALSUpdate(MLUpdate):
         if not (0.0 < self.decay_factor <= 1.0) or self.decay_zero_threshold < 0.0:
             raise ValueError("bad decay settings")
         self._cache: Dict[str, dict] = {}
+        # the build's undecayed parse of the complete data set, reused by the publish step
+        self._raw_parse: Optional[dict] = None
         self._timings: Dict[str, dict] = {}
         # cumulative seconds per phase of build / publish (bench_batch.py reads them)
         self.phase_seconds: Dict[str, float] = {}
 
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
+
+    def _raw_parse_slot(self, lines, users, items) -> Optional[list]:
+        """A list for parse_ratings' raw output when the training lines are the complete data
+        set (test fraction 0: MLUpdate trains on new + past data, exactly what the publish
+        step joins known items from); None otherwise."""
+        if self.get_test_fraction() != 0.0 or not lines:
+            self._raw_parse = None
+            return None
+        out: list = []
+        self._raw_parse = {"n": len(lines), "first": lines[0], "last": lines[-1],
+                           "users": users, "items": items, "arrays": out}
+        return out
+
+    def _raw_parse_for(self, lines):
+        """(users, items, u, i, s, ts) of the memoised parse when it is of ``lines``."""
+        m = self._raw_parse
+        if m is None or not lines or len(m["arrays"]) != 4 or m["n"] != len(lines) or \
+                m["first"] != lines[0] or m["last"] != lines[-1]:
+            return None
+        return (m["users"], m["items"]) + tuple(m["arrays"])
 
     # ---------------------------------------------------------------- build
     def _ctx(self, context) -> dist.DistContext:
@@ -282,7 +321,8 @@ class ALSUpdate(MLUpdate):
         tp = time.perf_counter()
         users, items = ingest.IdDict(), ingest.IdDict()
         u, i, s, ts = parse_ratings(train_data, users, items, self.decay_factor,
-                                    self.decay_zero_threshold)
+                                    self.decay_zero_threshold, raw_out=self._raw_parse_slot(
+                                        train_data, users, items))
         ph["parse"] = ph.get("parse", 0.0) + time.perf_counter() - tp
         tp = time.perf_counter()
         dev = self._ctx(context).device
@@ -330,13 +370,19 @@ class ALSUpdate(MLUpdate):
         X = f.X.cpu().numpy()
         Y = f.Y.cpu().numpy()
         ph["train"] = ph.get("train", 0.0) + time.perf_counter() - tp
+        tp = time.perf_counter()
+        # the rows' JSON text, formatted where the factors live (GPU: textfmt.hip); reused by
+        # the X/ Y/ files and the UP messages
+        x_rows = textfmt.format_rows(f.X) if ctx.is_main else None
+        y_rows = textfmt.format_rows(f.Y) if ctx.is_main else None
+        ph["format_rows"] = ph.get("format_rows", 0.0) + time.perf_counter() - tp
         log.info("ALS %d ratings, %d users, %d items, rank %d: %.3fs", len(u), len(used_u),
                  len(used_i), features, time.perf_counter() - t0)
         if not ctx.is_main:
             return None
         tp = time.perf_counter()
-        write_features(os.path.join(candidate_path, "X"), x_ids, X)
-        write_features(os.path.join(candidate_path, "Y"), y_ids, Y)
+        write_features(os.path.join(candidate_path, "X"), x_ids, x_rows)
+        write_features(os.path.join(candidate_path, "Y"), y_ids, y_rows)
         ph["write_factors"] = ph.get("write_factors", 0.0) + time.perf_counter() - tp
         pmml = pmmlu.build_skeleton_pmml()
         pmml.add_extension("X", "X/")
@@ -348,7 +394,8 @@ class ALSUpdate(MLUpdate):
             pmml.add_extension("alpha", alpha)
         pmml.add_extension_content("XIDs", x_ids)
         pmml.add_extension_content("YIDs", y_ids)
-        self._cache[candidate_path] = {"x_ids": x_ids, "y_ids": y_ids, "X": X, "Y": Y}
+        self._cache[candidate_path] = {"x_ids": x_ids, "y_ids": y_ids, "X": X, "Y": Y,
+                                       "x_rows": x_rows, "y_rows": y_rows}
         its = trainer.timings.get("iteration_ms", [])
         self._timings[candidate_path] = {
             "ratings": int(len(u)), "users": len(used_u), "items": len(used_i),
@@ -409,11 +456,12 @@ class ALSUpdate(MLUpdate):
         f = trainer.train(self.iterations, x_init=x_init, y_init=y_init)
         X = f.X.cpu().numpy()
         Y = f.Y.cpu().numpy()
+        x_rows, y_rows = textfmt.format_rows(f.X), textfmt.format_rows(f.Y)
         log.info("ALS (sharded, %d ranks) %d ratings, %d users, %d items, rank %d: %.3fs", W,
                  n_ratings, nu, ni, features, time.perf_counter() - t0)
         if ctx.is_main:
-            write_features(os.path.join(candidate_path, "X"), x_ids, X)
-            write_features(os.path.join(candidate_path, "Y"), y_ids, Y)
+            write_features(os.path.join(candidate_path, "X"), x_ids, x_rows)
+            write_features(os.path.join(candidate_path, "Y"), y_ids, y_rows)
         pmml = pmmlu.build_skeleton_pmml()
         pmml.add_extension("X", "X/")
         pmml.add_extension("Y", "Y/")
@@ -427,6 +475,7 @@ class ALSUpdate(MLUpdate):
         # every rank keeps what evaluation needs: factors, its dictionary share, dense maps
         self._cache[candidate_path] = {
             "x_ids": x_ids, "y_ids": y_ids, "X": X, "Y": Y, "utab": utab, "itab": itab,
+            "x_rows": x_rows, "y_rows": y_rows,
             "dense_u": np.where(used_u, dense_u, -1), "dense_i": np.where(used_i, dense_i, -1)}
         its = trainer.timings.get("iteration_ms", [])
         self._timings[candidate_path] = {
@@ -438,7 +487,7 @@ class ALSUpdate(MLUpdate):
 
     def _evaluate_sharded(self, context, model_parent_path, test_data):
         ctx = self._ctx(context)
-        f = self._cache.pop(model_parent_path)
+        f = self._cache[model_parent_path]
         users, items = ingest.IdDict(), ingest.IdDict()
         u, i, s, ts = parse_ratings(test_data, users, items, self.decay_factor,
                                     self.decay_zero_threshold)
@@ -480,11 +529,10 @@ class ALSUpdate(MLUpdate):
     def _publish_sharded(self, context, pmml, new_data, past_data, model_parent_path, topic):
         ctx = self._ctx(context)
         W, R = ctx.world_size, ctx.rank
-        x_ids, X = read_features(os.path.join(model_parent_path, pmml.get_extension_value("X")))
-        y_ids, Y = read_features(os.path.join(model_parent_path, pmml.get_extension_value("Y")))
+        x_ids, x_rows, y_ids, y_rows = self._published_rows(pmml, model_parent_path)
         mine = np.arange(R, len(y_ids), W)
         log.info("Rank %d sending %d item / Y rows as model updates", R, len(mine))
-        rows = ingest.format_float_rows(Y[mine]) if len(mine) else []
+        rows = y_rows.take(mine).rows() if len(mine) else []
         topic.send_many(("UP", '["Y",%s,%s]' % (json.dumps(y_ids[j]), r))
                         for j, r in zip(mine.tolist(), rows))
         dist.barrier(ctx)
@@ -492,7 +540,7 @@ class ALSUpdate(MLUpdate):
         all_lines = list(new_data) + list(past_data or [])
         if self.no_known_items:
             owned = np.nonzero(shuffle.owner_of_strings(x_ids, W) == R)[0]
-            xr = ingest.format_float_rows(X[owned]) if len(owned) else []
+            xr = x_rows.take(owned).rows() if len(owned) else []
             topic.send_many(("UP", '["X",%s,%s]' % (json.dumps(x_ids[j]), r))
                             for j, r in zip(owned.tolist(), xr))
         else:
@@ -501,7 +549,7 @@ class ALSUpdate(MLUpdate):
             sel = [(xmap[uid], uid) for uid in known if uid in xmap]
             sel.sort()
             idx = np.array([j for j, _ in sel], dtype=np.int64)
-            xr = ingest.format_float_rows(X[idx]) if len(idx) else []
+            xr = x_rows.take(idx).rows() if len(idx) else []
             log.info("Rank %d sending %d user / X rows as model updates", R, len(idx))
             topic.send_many(("UP", '["X",%s,%s,%s]' % (json.dumps(uid), r,
                                                         json.dumps(sorted(known[uid]))))
@@ -513,7 +561,7 @@ class ALSUpdate(MLUpdate):
 
     # ---------------------------------------------------------------- evaluate
     def _load(self, model_parent_path: str, pmml) -> dict:
-        cached = self._cache.pop(model_parent_path, None)
+        cached = self._cache.get(model_parent_path)
         if cached is not None:
             return cached
         x_ids, X = read_features(os.path.join(model_parent_path,
@@ -564,23 +612,38 @@ class ALSUpdate(MLUpdate):
         finally:
             self.phase_seconds["publish_up"] = self.phase_seconds.get("publish_up", 0.0) + \
                 time.perf_counter() - tp
+            # the generation is done: drop the candidates' factors and the parse memo
+            self._cache.clear()
+            self._raw_parse = None
+
+    def _published_rows(self, pmml, model_parent_path):
+        """(x_ids, X rows text, y_ids, Y rows text) of the promoted model: from the build's
+        cache when the winner was built in this process, else read back from its files."""
+        src = getattr(self, "promoted_from", None)
+        f = self._cache.get(src) if src else None
+        if f is not None and f.get("x_rows") is not None:
+            return f["x_ids"], f["x_rows"], f["y_ids"], f["y_rows"]
+        x_ids, X = read_features(os.path.join(model_parent_path, pmml.get_extension_value("X")))
+        y_ids, Y = read_features(os.path.join(model_parent_path, pmml.get_extension_value("Y")))
+        return x_ids, textfmt.format_rows(X), y_ids, textfmt.format_rows(Y)
 
     def _publish_local(self, pmml, new_data, past_data, model_parent_path, model_update_topic):
         all_data = list(new_data) + list(past_data or [])
-        x_ids, X = read_features(os.path.join(model_parent_path, pmml.get_extension_value("X")))
-        y_ids, Y = read_features(os.path.join(model_parent_path, pmml.get_extension_value("Y")))
+        x_ids, x_text, y_ids, y_text = self._published_rows(pmml, model_parent_path)
         log.info("Sending item / Y data as model updates")
-        y_rows = ingest.format_float_rows(Y) if len(y_ids) else []
+        y_rows = y_text.rows() if len(y_ids) else []
         model_update_topic.send_many(("UP", '["Y",%s,%s]' % (json.dumps(i), r))
                                      for i, r in zip(y_ids, y_rows))
         log.info("Sending user / X data as model updates")
-        x_rows = ingest.format_float_rows(X) if len(x_ids) else []
+        x_rows = x_text.rows() if len(x_ids) else []
         if self.no_known_items:
             model_update_topic.send_many(("UP", '["X",%s,%s]' % (json.dumps(u), r))
                                          for u, r in zip(x_ids, x_rows))
         else:
-            known = known_items_json(all_data, device=self.dist_ctx.device
-                                     if self.dist_ctx is not None else None)
+            parsed = self._raw_parse_for(all_data)
+            dev = self.dist_ctx.device if self.dist_ctx is not None else None
+            known = known_items_json(all_data, device=dev) if parsed is None else \
+                known_items_json_parsed(*parsed, device=dev)
             msgs = []
             for uid, r in zip(x_ids, x_rows):
                 ks = known.get(uid)
@@ -660,6 +723,11 @@ def known_items_json(lines: Sequence[str], device=None) -> Dict[str, str]:
     joined from one array of JSON-encoded item names."""
     users, items = ingest.IdDict(), ingest.IdDict()
     u, i, s, ts = ingest.parse_ratings(lines, users, items, default_ts=0)
+    return known_items_json_parsed(users, items, u, i, s, ts, device)
+
+
+def known_items_json_parsed(users, items, u, i, s, ts, device=None) -> Dict[str, str]:
+    """:func:`known_items_json` from already parsed events (lines without a timestamp at 0)."""
     if len(u) == 0:
         return {}
     uk, ik = users.keys(), items.keys()

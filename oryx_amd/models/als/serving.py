@@ -312,6 +312,17 @@ class ALSServingModel(ServingModel):
                 s = self._known[user] = set()
             s.update(items)
 
+    def add_known_items_many(self, pairs) -> None:
+        """Bulk :meth:`add_known_items` over (user, items) pairs under one lock (loads)."""
+        with self._known_lock.write():
+            known = self._known
+            for user, items in pairs:
+                s = known.get(user)
+                if s is None:
+                    known[user] = set(items)
+                else:
+                    s.update(items)
+
     def get_user_counts(self) -> Dict[str, int]:
         with self._known_lock.read():
             return {u: len(s) for u, s in self._known.items()}
@@ -479,6 +490,27 @@ def apply_up_batch(model, messages: List[str]) -> None:
     native parser rejects go through the per-message path (and raise as it does)."""
     from ... import ingest
     kinds, ids, vecs, known = ingest.parse_up_batch(messages, model.get_features())
+    apply_up_parsed(model, kinds, ids, vecs, known, messages)
+
+
+def drain_up_blocks(model, updates) -> int:
+    """Apply the ``UP`` runs the update iterator can parse straight from the log
+    (:meth:`~oryx_amd.serving.layer.UpdateIterator.take_up_block`) until a different message
+    or the end of what is available; returns rows applied."""
+    take = getattr(updates, "take_up_block", None)
+    done = 0
+    while take is not None:
+        blk = take(model.get_features())
+        if blk is None:
+            break
+        apply_up_parsed(model, *blk)
+        done += len(blk[0])
+    return done
+
+
+def apply_up_parsed(model, kinds, ids, vecs, known, messages=None) -> None:
+    """Apply parsed ``UP`` rows (see :func:`apply_up_batch`); kind-2 rows are re-parsed from
+    ``messages`` on the per-message path."""
     for kind, setter in ((0, "set_user_vectors"), (1, "set_item_vectors")):
         sel = np.nonzero(kinds == kind)[0]
         if not len(sel):
@@ -489,11 +521,16 @@ def apply_up_batch(model, messages: List[str]) -> None:
             last[ids[j]] = j
         rows = np.fromiter(last.values(), dtype=np.int64, count=len(last))
         getattr(model, setter)([ids[j] for j in rows.tolist()], vecs[rows])
-        if kind == 0 and hasattr(model, "add_known_items"):
+        if kind == 0 and hasattr(model, "add_known_items_many"):
+            model.add_known_items_many((ids[j], known[j]) for j in sel.tolist() if known[j])
+        elif kind == 0 and hasattr(model, "add_known_items"):
             for j in sel.tolist():
                 if known[j]:
                     model.add_known_items(ids[j], known[j])
-    for j in np.nonzero(kinds == 2)[0].tolist():
+    bad = np.nonzero(kinds == 2)[0].tolist()
+    if bad and messages is None:
+        raise ValueError("unparseable UP rows without their messages")
+    for j in bad:
         update = text.read_json(messages[j])
         vector = np.asarray(update[2], dtype=np.float32)
         if update[0] == "X":
@@ -534,14 +571,16 @@ class ALSServingModelManager(AbstractServingModelManager):
                 take = getattr(updates, "take_buffered", None)
                 if take is not None:
                     # a run of UP rows already fetched: one native parse, bulk row updates
-                    batch = [message] + [m.message for m in take(lambda m: m.key == "UP")]
-                    if len(batch) > 1:
-                        apply_up_batch(self.model, batch)
-                        countdown -= len(batch)
-                        if countdown <= 0:
-                            log.info("%s", self.model)
-                            countdown = 10000
-                        continue
+                    # the decoded UP rows already fetched, then the rest of the run parsed
+                    # natively from the log buffer
+                    batch = [message] + [m.message for m in take(lambda m: m.key == "UP",
+                                                                 poll=False)]
+                    apply_up_batch(self.model, batch)
+                    countdown -= len(batch) + drain_up_blocks(self.model, updates)
+                    if countdown <= 0:
+                        log.info("%s", self.model)
+                        countdown = 10000
+                    continue
                 update = text.read_json(message)
                 id_ = str(update[1])
                 vector = np.asarray(update[2], dtype=np.float32)

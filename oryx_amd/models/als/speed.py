@@ -13,7 +13,9 @@ Equivalent of ``ALSSpeedModel`` / ``ALSSpeedModelManager``
   ``oryx_als_foldin`` (``csrc/kernels/foldin.hip``: dot, target, inverse x rhs in double, axpy;
   rows read from the device mirrors by index) on a dedicated stream, instead of B independent
   k x k solves.  Each event yields ``["X",u,vec,[i]]`` and ``["Y",i,vec,[u]]``,
-  formatted natively straight from the parse dictionaries (``oryx_format_als_updates``).
+  whose factor rows are formatted to JSON text on the device (``csrc/kernels/textfmt.hip``)
+  and assembled natively with the IDs from the parse dictionaries
+  (``oryx_assemble_als_updates``).
 """
 
 from __future__ import annotations
@@ -28,7 +30,7 @@ import torch
 
 from ... import ingest
 from ...api import Dataset, KeyMessage, SpeedModel, SpeedModelManager
-from ...ops import als as als_ops
+from ...ops import als as als_ops, textfmt
 from ...utils import mathx, pmml as pmmlu, text
 from .batch import aggregate_scores
 from .common import FeatureVectors
@@ -163,15 +165,15 @@ class ALSSpeedModelManager(SpeedModelManager):
                     continue
                 take = getattr(updates, "take_buffered", None)
                 if take is not None:
-                    batch = [message] + [m.message for m in take(lambda m: m.key == "UP")]
-                    if len(batch) > 1:
-                        from .serving import apply_up_batch
-                        apply_up_batch(self.model, batch)
-                        countdown -= len(batch)
-                        if countdown <= 0:
-                            log.info("%s", self.model)
-                            countdown = 10000
-                        continue
+                    from .serving import apply_up_batch, drain_up_blocks
+                    batch = [message] + [m.message for m in take(lambda m: m.key == "UP",
+                                                                 poll=False)]
+                    apply_up_batch(self.model, batch)
+                    countdown -= len(batch) + drain_up_blocks(self.model, updates)
+                    if countdown <= 0:
+                        log.info("%s", self.model)
+                        countdown = 10000
+                    continue
                 update = text.read_json(message)
                 id_ = str(update[1])
                 vec = np.asarray(update[2], dtype=np.float32)
@@ -319,16 +321,15 @@ class ALSSpeedModelManager(SpeedModelManager):
                                      new_y.data_ptr(), vx.data_ptr(), vy.data_ptr(),
                                      native.stream_ptr(dev))
             native.check(rc, "oryx_als_foldin")
-            host = torch.cat([new_x.view(-1), new_y.view(-1),
-                              torch.cat([vx, vy]).to(torch.float32)]).cpu().numpy()
-        nx = host[:n * k].reshape(n, k)
-        ny = host[n * k:2 * n * k].reshape(n, k)
-        vxh = host[2 * n * k:2 * n * k + n] > 0
-        vyh = host[2 * n * k + n:] > 0
-        ph["foldin"] = (time.perf_counter() - t0) * 1e3
-        t0 = time.perf_counter()
-        out = ingest.format_als_updates(users, items, u, i, nx, ny, vxh, vyh,
-                                        not self.no_known_items)
+            valid = torch.cat([vx, vy]).cpu().numpy()
+            ph["foldin"] = (time.perf_counter() - t0) * 1e3
+            t0 = time.perf_counter()
+            # the updated rows become JSON text on the device (csrc/kernels/textfmt.hip);
+            # only the text crosses to the host
+            xrows = textfmt.format_rows(new_x)
+            yrows = textfmt.format_rows(new_y)
+        out = ingest.assemble_als_updates(users, items, u, i, xrows, yrows, valid[:n] > 0,
+                                          valid[n:] > 0, not self.no_known_items)
         ph["format"] = (time.perf_counter() - t0) * 1e3
         return out
 

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 8
+KERNELS_ABI_VERSION = 9
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -92,9 +92,15 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_parse_up_batch", c_ll, [c_cp, c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_up_texts", c_ll, [c_vp, c_ll, c_vp, c_ll])
+    # raw, used, nrec, k, max_n, kinds, vecs, id_ends, known_cnt, consumed_bytes
+    _sig(lib, "oryx_parse_up_records", c_ll, [c_vp, c_ll, c_ll, c_i, c_ll, c_vp, c_vp, c_vp,
+                                              c_vp, c_vp])
     # users, items, u, i, nx, ny, vx, vy, n, k, with_known, out, cap
     _sig(lib, "oryx_format_als_updates", c_ll, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                 c_ll, c_i, c_i, c_vp, c_ll])
+    # users, items, u, i, xtext, xends, ytext, yends, vx, vy, n, with_known, out, cap
+    _sig(lib, "oryx_assemble_als_updates", c_ll, [c_vp, c_vp, c_vp, c_vp, c_cp, c_vp, c_cp,
+                                                  c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_ll])
 
 
 def _runtime_sources():
@@ -155,6 +161,9 @@ def _load_kernels():
     # X, Y, k, xrow, yrow, vals, xinv, yinv, implicit, n, new_x, new_y, vx, vy, stream
     _sig(lib, "oryx_als_foldin", c_i, [c_vp, c_vp, c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_ll,
                                        c_vp, c_vp, c_vp, c_vp, c_vp])
+    # M, n, k, ld, row_len, stream / M, n, k, ld, row_end, row_len, out, stream
+    _sig(lib, "oryx_format_rows_len", c_i, [c_vp, c_ll, c_i, c_ll, c_vp, c_vp])
+    _sig(lib, "oryx_format_rows_text", c_i, [c_vp, c_ll, c_i, c_ll, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_topn_waves", c_ll, [c_ll])
     # Y, inv_norm, Q, kp, nq, bucket_of, cand_bits, words, ranges, tile0, n_ranges, n_tiles,
     # excl_ptr, excl_rows, out_score, out_row, stream

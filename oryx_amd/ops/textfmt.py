@@ -1,0 +1,90 @@
+"""Factor rows -> JSON array text, formatted where the rows live.
+
+Model updates carry factor rows as JSON arrays of shortest round-trip floats (the reference
+writes them with ``TextUtils.joinJSON``: ``[app-common]/als/ALSUtils`` callers in
+``ALSUpdate.publishAdditionalModelData`` and ``ALSSpeedModelManager.java:182-215``).  Rows on
+the GPU are converted by ``csrc/kernels/textfmt.hip`` (one wave per row, two launches) and only
+the text crosses to the host; host rows use the native formatter of
+``csrc/runtime/fastfloat.h``.  Both produce identical bytes.
+
+:class:`RowText` holds the rows back to back (``blob``) with their end offsets; ``row(j)`` /
+``rows()`` give Python strings, and the native message assemblers take the blob directly.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List
+
+import numpy as np
+import torch
+
+from .. import native
+
+__all__ = ["RowText", "format_rows"]
+
+
+@dataclass
+class RowText:
+    blob: bytes                 # ASCII, rows back to back
+    ends: np.ndarray            # int64 [n]: end offset of row j
+
+    def __len__(self) -> int:
+        return len(self.ends)
+
+    def rows(self) -> List[str]:
+        text = self.blob.decode("ascii")
+        out, start = [], 0
+        for e in self.ends.tolist():
+            out.append(text[start:e])
+            start = e
+        return out
+
+    def take(self, idx: np.ndarray) -> "RowText":
+        """The rows ``idx`` (in that order) as a new :class:`RowText`."""
+        idx = np.asarray(idx, dtype=np.int64)
+        if len(idx) == 0:
+            return RowText(b"", np.zeros(0, dtype=np.int64))
+        starts = np.r_[0, self.ends[:-1]]
+        buf = np.frombuffer(self.blob, dtype=np.uint8)
+        lens = self.ends[idx] - starts[idx]
+        parts = [buf[s:s + l] for s, l in zip(starts[idx].tolist(), lens.tolist())]
+        return RowText(np.concatenate(parts).tobytes(), np.cumsum(lens))
+
+
+def format_rows(mat) -> RowText:
+    """JSON array text of every row of a 2-D float32 matrix (device tensor -> HIP kernels,
+    host array / CPU tensor -> native host formatter)."""
+    if isinstance(mat, torch.Tensor) and mat.device.type == "cuda":
+        return _format_device(mat)
+    if isinstance(mat, torch.Tensor):
+        mat = mat.detach().numpy()
+    from .. import ingest
+    return ingest.format_float_rows_blob(np.asarray(mat, dtype=np.float32))
+
+
+def _format_device(mat: torch.Tensor) -> RowText:
+    m = mat.detach()
+    if m.dtype != torch.float32:
+        m = m.float()
+    if m.dim() != 2:
+        raise ValueError("need a 2-D matrix")
+    if m.stride(1) != 1:
+        m = m.contiguous()
+    n, k = m.shape
+    if n == 0:
+        return RowText(b"", np.zeros(0, dtype=np.int64))
+    lib = native.require_kernels()
+    dev = m.device
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = native.stream_ptr(dev)
+    native.check(lib.oryx_format_rows_len(m.data_ptr(), n, k, m.stride(0), lens.data_ptr(),
+                                          stream), "oryx_format_rows_len")
+    ends = torch.cumsum(lens, 0, dtype=torch.int64)
+    total = int(ends[-1])
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    native.check(lib.oryx_format_rows_text(m.data_ptr(), n, k, m.stride(0), ends.data_ptr(),
+                                           lens.data_ptr(), out.data_ptr(), stream),
+                 "oryx_format_rows_text")
+    blob = out.cpu().numpy().tobytes()
+    return RowText(blob, ends.cpu().numpy())

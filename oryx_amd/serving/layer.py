@@ -44,6 +44,7 @@ class UpdateIterator:
         self.poll_ms = poll_ms
         self.closed = False
         self._pending: List = []
+        self._rr = 0
 
     def __iter__(self):
         return self
@@ -60,10 +61,16 @@ class UpdateIterator:
     def has_buffered(self) -> bool:
         return bool(self._pending)
 
-    def take_buffered(self, pred, max_n: int = 1 << 16) -> List[KeyMessage]:
+    def take_buffered(self, pred, max_n: int = 1 << 16, poll: bool = True
+                      ) -> List[KeyMessage]:
         """Already-fetched messages from the front while ``pred`` holds (no blocking) -- lets
-        a manager apply a run of ``UP`` rows as one batch."""
+        a manager apply a run of ``UP`` rows as one batch; ``poll`` also fetches (without
+        waiting) what the log already holds while the run continues."""
         out: List[KeyMessage] = []
+        if not poll:
+            while self._pending and len(out) < max_n and pred(self._pending[-1]):
+                out.append(self._pending.pop())
+            return out
         if not self._pending and not self.closed:
             recs = self.consumer.poll(8192, 0)
             self._pending = [KeyMessage(k, v) for _, _, _, k, v in recs]
@@ -75,6 +82,31 @@ class UpdateIterator:
                 self._pending = [KeyMessage(k, v) for _, _, _, k, v in recs]
                 self._pending.reverse()
         return out
+
+    def take_up_block(self, k: int, max_n: int = 1 << 15):
+        """The next run of ``UP`` records parsed natively straight from the log's raw poll
+        buffer -- no per-message Python objects -- as (kinds, ids, vectors [n, k], known
+        lists); None when nothing is buffered-free to read or the next record is not a
+        parseable ``UP`` (the records after the run are queued as ordinary messages).  Only
+        used when no already-decoded messages are pending, so the order is kept."""
+        if self._pending or self.closed:
+            return None
+        from .. import ingest
+        readers = self.consumer.readers
+        for step in range(len(readers)):
+            r = readers[(self._rr + step) % len(readers)]
+            n = r.poll_raw(max_n, 0, min_buffer=64 << 20)
+            if not n:
+                continue
+            self._rr = (self._rr + step + 1) % len(readers)
+            addr, used = r.raw_buffer()
+            got, consumed, kinds, ids, vecs, known = ingest.parse_up_records(addr, used, n, k,
+                                                                              n)
+            rest = r.decode_raw(consumed, n - got)
+            self._pending = [KeyMessage(key, v) for _, _, key, v in rest]
+            self._pending.reverse()
+            return (kinds, ids, vecs, known) if got else None
+        return None
 
     def close(self) -> None:
         self.closed = True

@@ -261,7 +261,19 @@ class PartitionReader:
     def poll(self, max_records: int = 4096, timeout_ms: int = 100
              ) -> List[Tuple[int, int, Optional[str], str]]:
         """Returns up to ``max_records`` (offset, timestamp_ms, key, value) tuples."""
+        n = self.poll_raw(max_records, timeout_ms)
+        return self.decode_raw(0, n)
+
+    def poll_raw(self, max_records: int = 4096, timeout_ms: int = 100,
+                 min_buffer: int = 0) -> int:
+        """Reads up to ``max_records`` records into this reader's raw buffer (layout: per
+        record i64 offset, i64 timestamp, i32 key length, i32 value length, key, value) and
+        returns how many; :meth:`raw_buffer` / :meth:`decode_raw` read them.  ``min_buffer``
+        grows the buffer first (bulk loads fetch many large records per call)."""
         lib = _lib()
+        if min_buffer > self._cap:
+            self._cap = int(min_buffer)
+            self._buf = ctypes.create_string_buffer(self._cap)
         while True:
             n = lib.oryx_reader_poll(self._r, self._buf, self._cap, int(max_records),
                                      int(timeout_ms), ctypes.byref(self._used))
@@ -274,10 +286,21 @@ class PartitionReader:
                 continue
             if n < 0:
                 raise IOError(lib.oryx_log_last_error().decode())
-            break
+            return n
+
+    def raw_buffer(self) -> Tuple[int, int]:
+        """(address, bytes used) of the last :meth:`poll_raw`."""
+        return ctypes.addressof(self._buf), self._used.value
+
+    def decode_raw(self, start: int, count: int) -> List[Tuple[int, int, Optional[str], str]]:
+        """``count`` records of the raw buffer from byte ``start`` as (offset, timestamp_ms,
+        key, value) tuples."""
         out = []
-        raw = self._buf.raw[:self._used.value] if n else b""
+        if not count:
+            return out
+        raw = ctypes.string_at(ctypes.addressof(self._buf) + start, self._used.value - start)
         pos = 0
+        n = count
         for _ in range(n):
             off, ts, kl, vl = _HDR.unpack_from(raw, pos)
             pos += 24

@@ -479,3 +479,64 @@ def test_bulk_up_batch_matches_per_message(tmp_path):
         assert a.get_known_items(uid) == b.get_known_items(uid)
     for iid in b.get_all_item_ids():
         np.testing.assert_array_equal(a.get_item_vector(iid), b.get_item_vector(iid))
+
+
+def test_up_blocks_from_log_keep_order(tmp_path):
+    """The serving manager's load path parses runs of UP records straight from the log's raw
+    poll buffer (UpdateIterator.take_up_block): a MODEL in the middle of the stream is still
+    seen in order, a later UP overrides an earlier one (also one written by hand with spaces
+    and integer values), and known items arrive with their users."""
+    import json as _json
+    from oryx_amd.models.als.serving import ALSServingModelManager
+    from oryx_amd.serving.layer import UpdateIterator
+    from oryx_amd.transport import log as tlog
+    from oryx_amd.utils import config as cfg, pmml as pmmlu
+    root = str(tmp_path / "log")
+    tlog.maybe_create_topic(root, "U", 1, max_message=1 << 24)
+    topic = tlog.Topic(root, "U")
+    doc = pmmlu.build_skeleton_pmml()
+    for k_, v_ in (("X", "X/"), ("Y", "Y/"), ("features", 2), ("lambda", 0.001),
+                   ("implicit", True), ("alpha", 1.0)):
+        doc.add_extension(k_, v_)
+    doc.add_extension_content("XIDs", ["U%d" % j for j in range(50)])
+    doc.add_extension_content("YIDs", ["I%d" % j for j in range(3000)])
+    model = pmmlu.to_string(doc)
+    recs = [("MODEL", model)]
+    recs += [("UP", _json.dumps(["Y", "I%d" % j, [float(j), 1.0]])) for j in range(3000)]
+    recs += [("UP", _json.dumps(["X", "U%d" % j, [1.0, float(j)], ["I%d" % j]]))
+             for j in range(50)]
+    recs.append(("MODEL", model))          # same features: the model is kept
+    recs += [("UP", _json.dumps(["Y", "I%d" % j, [-1.0, -2.0]])) for j in range(10)]
+    recs.append(("UP", '["Y", "I11", [7, 8]]'))
+    topic.append_batch(recs)
+    conf = cfg.overlay_on({"oryx.update-topic.message.max-size": 1 << 24}, cfg.get_default())
+    mgr = ALSServingModelManager(conf)
+    cons = tlog.TopicConsumer(topic, "earliest")
+    it = UpdateIterator(cons, poll_ms=0)
+    end = topic.end_offset(0)
+
+    class Bounded:
+        def __iter__(self):
+            return self
+
+        def __next__(self):
+            if not it._pending and cons.readers[0].position >= end:
+                raise StopIteration
+            return next(it)
+
+        def take_buffered(self, *a, **kw):
+            return it.take_buffered(*a, **kw)
+
+        def take_up_block(self, *a, **kw):
+            return it.take_up_block(*a, **kw)
+
+    mgr.consume(Bounded())
+    m = mgr.get_model()
+    assert m.get_num_items() == 3000 and m.get_num_users() == 50
+    np.testing.assert_array_equal(m.get_item_vector("I3"), [-1.0, -2.0])
+    np.testing.assert_array_equal(m.get_item_vector("I11"), [7.0, 8.0])
+    np.testing.assert_array_equal(m.get_item_vector("I2999"), [2999.0, 1.0])
+    np.testing.assert_array_equal(m.get_user_vector("U7"), [1.0, 7.0])
+    assert m.get_known_items("U7") == {"I7"}
+    cons.close()
+    topic.close()

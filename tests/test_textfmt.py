@@ -1,0 +1,90 @@
+"""Factor-row text codecs: the host shortest-float formatter / parser (csrc/runtime/
+fastfloat.h) against std::to_chars / std::from_chars, the Python RowText helpers, and the GPU
+formatter (csrc/kernels/textfmt.hip) byte-for-byte against the host one."""
+
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _special_matrix(rows=300, k=67, seed=0):
+    g = np.random.default_rng(seed)
+    x = g.normal(size=(rows, k)).astype(np.float32)
+    x[1] = g.normal(scale=1e4, size=k)
+    x[2] = g.normal(scale=1e-6, size=k)
+    bits = g.integers(0, 2 ** 32, size=k, dtype=np.uint64).astype(np.uint32)
+    x[3] = bits.view(np.float32)
+    x[4, :12] = [0.0, -0.0, 1.0, -1.0, 100.0, 33871888.0, 1e-7, 3.4e38, 1.4e-45, 123456.7,
+                 np.inf, -np.inf]
+    x[5, :3] = [np.nan, 0.1, 1e10]
+    return x
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
+def test_fastfloat_matches_std_charconv(tmp_path):
+    exe = str(tmp_path / "ffc")
+    subprocess.run(["g++", "-O2", "-std=c++17", os.path.join(ROOT, "csrc", "runtime", "tests",
+                                                              "fastfloat_check.cpp"), "-o", exe],
+                   check=True, timeout=300)
+    r = subprocess.run([exe, "99991"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+
+
+def test_host_rows_round_trip_exactly():
+    from oryx_amd import ingest
+    x = _special_matrix()
+    rows = ingest.format_float_rows(x)
+    for j, text in enumerate(rows):
+        vals = json.loads(text.replace("NaN", '"nan"').replace("-Infinity", '"-inf"')
+                          .replace("Infinity", '"inf"'))
+        back = np.array([float(v) for v in vals], dtype=np.float32)
+        assert np.array_equal(back.view(np.uint32)[~np.isnan(back)],
+                              x[j].view(np.uint32)[~np.isnan(x[j])]), text
+    assert rows[4].startswith("[0.0,-0.0,1.0,-1.0,100.0,33871888.0,1e-07,3.4e+38,1e-45,")
+    assert rows[5].startswith("[NaN,0.1,1e+10,")
+
+
+def test_row_text_take_and_rows():
+    from oryx_amd.ops import textfmt
+    x = np.arange(12, dtype=np.float32).reshape(4, 3) / 4
+    rt = textfmt.format_rows(x)
+    assert rt.rows() == ["[0.0,0.25,0.5]", "[0.75,1.0,1.25]", "[1.5,1.75,2.0]",
+                         "[2.25,2.5,2.75]"]
+    sub = rt.take(np.array([2, 0]))
+    assert sub.rows() == ["[1.5,1.75,2.0]", "[0.0,0.25,0.5]"]
+
+
+def test_parse_up_batch_reads_formatted_rows_exactly():
+    """The native UP parser (fast-path float parse) recovers the exact floats."""
+    from oryx_amd import ingest
+    x = _special_matrix(rows=50, k=20)
+    x = np.where(np.isfinite(x), x, 1.0).astype(np.float32)
+    rows = ingest.format_float_rows(x)
+    msgs = ['["Y","i%d",%s]' % (j, r) for j, r in enumerate(rows)]
+    kinds, ids, vecs, known = ingest.parse_up_batch(msgs, 20)
+    assert (kinds == 1).all()
+    assert np.array_equal(vecs.view(np.uint32), x.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_gpu_formatter_matches_host_bytes():
+    from oryx_amd import native
+    from oryx_amd.ops import textfmt
+    assert native.kernels_available()
+    for k in (1, 7, 64, 67, 130, 250):
+        x = _special_matrix(rows=257, k=k, seed=k)
+        host = textfmt.format_rows(x)
+        dev = textfmt.format_rows(torch.from_numpy(x).cuda())
+        assert np.array_equal(host.ends, dev.ends), k
+        assert host.blob == dev.blob, k
+    # a strided view (leading dimension > k)
+    big = torch.from_numpy(_special_matrix(rows=64, k=80)).cuda()
+    view = big[:, :50]
+    assert textfmt.format_rows(view).blob == textfmt.format_rows(view.cpu().numpy()).blob
