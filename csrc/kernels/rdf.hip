@@ -233,9 +233,10 @@ __global__ __launch_bounds__(256) void rdf_histogram_pieces(
     const int* __restrict__ perm, const int* __restrict__ piece_tree,
     const int* __restrict__ piece_node, const long long* __restrict__ piece_lo,
     const long long* __restrict__ piece_hi, int nodes, const int* __restrict__ feats, int Fs,
-    int B, float* __restrict__ hist) {
+    int B, float* __restrict__ hist, const int* __restrict__ n_live) {
   extern __shared__ float lh[];
   const int pc = blockIdx.x;
+  if (n_live && pc >= *n_live) return;     // grid sized by an upper bound (device pieces)
   const int t = piece_tree[pc];
   const int node = piece_node[pc];
   const long long per_node = (long long)Fs * B * S;
@@ -314,8 +315,9 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
     const int* __restrict__ perm, const int* __restrict__ piece_tree,
     const int* __restrict__ piece_node, const long long* __restrict__ piece_lo,
     const long long* __restrict__ piece_hi, int nodes, const int* __restrict__ feats, int Fs,
-    int B, float* __restrict__ hist, int NDW, int RSW) {
+    int B, float* __restrict__ hist, int NDW, int RSW, const int* __restrict__ n_live) {
   extern __shared__ __attribute__((aligned(16))) float lsm[];
+  if (n_live && (int)blockIdx.x >= *n_live) return;   // grid sized by an upper bound
   const int per_node = Fs * B * S;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float* lh = lsm;                                                        // [per_node]
@@ -474,9 +476,247 @@ __global__ __launch_bounds__(256) void rdf_forest_leaf(
   }
 }
 
+// Device-side piece list of one level (no host round trip): slot c = t * W + node of the
+// level's counting sort has counts[c] live rows at offset sum(counts[< c]); the slots with
+// node in [lo, hi) are cut into ceil(counts / piece) pieces, written in slot order.  One
+// 1024-thread block scans the (<= 16384) slots; *n_live receives the piece count, which the
+// histogram kernels (grid = an upper bound) read to retire their surplus workgroups.
+__global__ __launch_bounds__(1024) void rdf_expand_pieces(
+    const long long* __restrict__ counts, int T, int W, int lo, int hi, long long piece,
+    int max_pieces, int* __restrict__ ptree, int* __restrict__ pnode,
+    long long* __restrict__ pbeg, long long* __restrict__ pend, int* __restrict__ n_live) {
+  __shared__ long long s_cnt[1024], s_np[1024];
+  const int tid = threadIdx.x;
+  const int nslot = T * W;
+  const int per = (nslot + 1023) / 1024;
+  const int c0 = tid * per;
+  long long my_cnt = 0, my_np = 0;
+  for (int c = c0; c < c0 + per && c < nslot; ++c) {
+    my_cnt += counts[c];
+    const int node = c % W;
+    if (node >= lo && node < hi) my_np += (counts[c] + piece - 1) / piece;
+  }
+  s_cnt[tid] = my_cnt;
+  s_np[tid] = my_np;
+  __syncthreads();
+  // inclusive Hillis-Steele scans of both arrays
+  for (int off = 1; off < 1024; off <<= 1) {
+    const long long a = tid >= off ? s_cnt[tid - off] : 0;
+    const long long b = tid >= off ? s_np[tid - off] : 0;
+    __syncthreads();
+    s_cnt[tid] += a;
+    s_np[tid] += b;
+    __syncthreads();
+  }
+  long long off_rows = s_cnt[tid] - my_cnt, off_p = s_np[tid] - my_np;
+  for (int c = c0; c < c0 + per && c < nslot; ++c) {
+    const long long cnt = counts[c];
+    const int node = c % W;
+    if (node >= lo && node < hi) {
+      const long long np = (cnt + piece - 1) / piece;
+      for (long long k = 0; k < np && off_p + k < max_pieces; ++k) {
+        const long long b = off_rows + k * piece;
+        ptree[off_p + k] = c / W;
+        pnode[off_p + k] = node - lo;
+        pbeg[off_p + k] = b;
+        pend[off_p + k] = b + piece < off_rows + cnt ? b + piece : off_rows + cnt;
+      }
+      off_p += np;
+    }
+    off_rows += cnt;
+  }
+  if (tid == 1023) *n_live = (int)(s_np[1023] < max_pieces ? s_np[1023] : max_pieces);
+}
+
+// impurity of label statistics st[0..S) (classification counts; regression w, sum wy,
+// sum wy^2), weight in *w.  kind: 0 gini, 1 entropy (log2), 2 variance.
+__device__ double rdf_impurity(const double* st, int S, int kind, double* w) {
+  if (kind == 2) {
+    *w = st[0];
+    const double safe = st[0] > 1e-30 ? st[0] : 1e-30;
+    const double mean = st[1] / safe;
+    const double v = st[2] / safe - mean * mean;
+    return v > 0.0 ? v : 0.0;
+  }
+  double tot = 0.0;
+  for (int s = 0; s < S; ++s) tot += st[s];
+  *w = tot;
+  const double inv = 1.0 / (tot > 1e-30 ? tot : 1e-30);
+  double acc = 0.0;
+  for (int s = 0; s < S; ++s) {
+    const double pr = st[s] * inv;
+    if (kind == 0) acc += pr * pr;
+    else acc -= pr * log2(pr > 1e-30 ? pr : 1e-30);
+  }
+  return kind == 0 ? 1.0 - acc : acc;
+}
+
+constexpr int RDF_MAX_S = 32;   // label statistics per bin the split kernel keeps in registers
+
+// label centroid of bin b (regression: mean; classification: share of class maj); +inf when
+// the bin is empty
+__device__ __forceinline__ double rdf_centroid(const float* hf, int b, int S, int kind, int maj) {
+  if (kind == 2) {
+    const double cnt = (double)hf[(long long)b * S];
+    return cnt > 0.0 ? (double)hf[(long long)b * S + 1] / cnt : INFINITY;
+  }
+  double c2 = 0.0;
+  for (int s = 0; s < S; ++s) c2 += (double)hf[(long long)b * S + s];
+  return c2 > 0.0 ? (double)hf[(long long)b * S + maj] / c2 : INFINITY;
+}
+
+// ord[r] = the bin of rank r in centroid order (ties by bin index, empty bins last)
+__device__ void rdf_cat_order(const float* hf, int B, int S, int kind, int maj,
+                              unsigned short* ord) {
+  for (int b = 0; b < B; ++b) {
+    const double cb = rdf_centroid(hf, b, S, kind, maj);
+    int r = 0;
+    for (int o = 0; o < B; ++o) {
+      const double co = rdf_centroid(hf, o, S, kind, maj);
+      r += (co < cb || (co == cb && o < b)) ? 1 : 0;
+    }
+    ord[r] = (unsigned short)b;
+  }
+}
+
+// Best split of every (tree, node) of a level -- the per-level search MLlib runs over its
+// aggregated bins (RandomForest.findBestSplits via RDFUpdate.java:143-165), as one kernel:
+// one wave per node, one lane per candidate feature (lane, lane + 64, ...).  A lane walks its
+// feature's bins in order (categorical features: bins ordered by label centroid -- regression
+// mean, classification share of the node's majority class -- empty bins last, ranks computed
+// in the lane and kept in LDS), carries the left statistics as a prefix sum in fp64, and
+// scores every split position by the impurity decrease (w_l imp_l + w_r imp_r over the node
+// weight; both sides need weight >= 1).  The wave keeps the best (gain, then the lowest
+// feature-slot x position index); the node becomes a leaf at max depth, when pure, with < 2
+// weighted examples, or without a positive gain.  hist [T][W][Fs][B][S] fp32, feats
+// [T][W][Fs]; outputs feat / bin [T][W] (-1: leaf; bin -1 for a categorical split),
+// totals [T][W][S] fp64, gain [T][W], cat_left [T][W][B] (nullable when no predictor is
+// categorical).
+__global__ __launch_bounds__(64) void rdf_best_split(
+    const float* __restrict__ hist, const int* __restrict__ feats,
+    const unsigned char* __restrict__ is_cat, int T, int W, int Fs, int B, int S, int kind,
+    int force_leaf, int* __restrict__ out_feat, int* __restrict__ out_bin,
+    double* __restrict__ out_tot, float* __restrict__ out_gain,
+    unsigned char* __restrict__ cat_left) {
+  extern __shared__ unsigned short s_ord[];   // [64][B] categorical orders (when used)
+  const int lane = threadIdx.x;
+  const long long node = blockIdx.x;          // t * W + slot
+  const float* h = hist + node * (long long)Fs * B * S;
+  const int* fj = feats + node * Fs;
+  // node totals = sum over the bins of feature slot 0
+  double tot[RDF_MAX_S];
+  for (int s = 0; s < S; ++s) tot[s] = 0.0;
+  for (int b = lane; b < B; b += 64)
+    for (int s = 0; s < S; ++s) tot[s] += (double)h[(long long)b * S + s];
+  for (int s = 0; s < S; ++s) {
+    double v = tot[s];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    tot[s] = v;
+  }
+  double wn;
+  const double parent = rdf_impurity(tot, S, kind, &wn);
+  int maj = 0;
+  if (kind != 2)
+    for (int s = 1; s < S; ++s) if (tot[s] > tot[maj]) maj = s;
+  double best = -INFINITY;
+  long long best_idx = 0x7FFFFFFFFFFFFFFFLL;
+  const bool leaf_node = force_leaf || wn < 2.0 || parent <= 1e-12 || B < 2;
+  unsigned short* ord = s_ord + lane * B;
+  if (!leaf_node) {
+    for (int jj = lane; jj < Fs; jj += 64) {
+      const int f = fj[jj];
+      const float* hf = h + (long long)jj * B * S;
+      const bool cat = is_cat && is_cat[f];
+      if (cat) rdf_cat_order(hf, B, S, kind, maj, ord);
+      double left[RDF_MAX_S], right[RDF_MAX_S];
+      for (int s = 0; s < S; ++s) left[s] = 0.0;
+      for (int k = 0; k + 1 < B; ++k) {
+        const int b = cat ? ord[k] : k;
+        for (int s = 0; s < S; ++s) {
+          left[s] += (double)hf[(long long)b * S + s];
+          right[s] = tot[s] - left[s];
+        }
+        double wl, wr;
+        const double il = rdf_impurity(left, S, kind, &wl);
+        const double ir = rdf_impurity(right, S, kind, &wr);
+        if (wl >= 1.0 && wr >= 1.0) {
+          const double wt = wn > 1e-30 ? wn : 1e-30;
+          const double gain = parent - (wl * il + wr * ir) / wt;
+          const long long idx = (long long)jj * (B - 1) + k;
+          if (gain > best || (gain == best && idx < best_idx)) {
+            best = gain;
+            best_idx = idx;
+          }
+        }
+      }
+    }
+  }
+  // wave arg-max (gain, then lowest index)
+  for (int off = 32; off > 0; off >>= 1) {
+    const double og = __shfl_xor(best, off, 64);
+    const long long oi = __shfl_xor(best_idx, off, 64);
+    if (og > best || (og == best && oi < best_idx)) {
+      best = og;
+      best_idx = oi;
+    }
+  }
+  const bool leaf = leaf_node || !(best > 1e-12) || isinf(best);
+  const int jbest = leaf ? 0 : (int)(best_idx / (B - 1));
+  const int kbest = leaf ? 0 : (int)(best_idx % (B - 1));
+  const int fbest = leaf ? -1 : fj[jbest];
+  const bool cbest = !leaf && is_cat && is_cat[fbest];
+  if (lane == 0) {
+    out_feat[node] = fbest;
+    out_bin[node] = (leaf || cbest) ? -1 : kbest;
+    out_gain[node] = leaf ? 0.f : (float)best;
+  }
+  for (int s = lane; s < S; s += 64) out_tot[node * S + s] = tot[s];
+  if (cat_left) {
+    unsigned char* cl = cat_left + node * (long long)B;
+    if (!cbest) {
+      for (int b = lane; b < B; b += 64) cl[b] = 0;
+    } else {
+      // the winning feature's order (recomputed: a lane's slot holds its last feature's):
+      // the first kbest + 1 bins in centroid order go left
+      if (lane == 0) rdf_cat_order(h + (long long)jbest * B * S, B, S, kind, maj, s_ord);
+      for (int b = lane; b < B; b += 64) cl[b] = 0;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int r = lane; r <= kbest; r += 64) cl[s_ord[r]] = 1;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int oryx_rdf_expand_pieces(const long long* counts, int T, int W, int lo, int hi,
+                           long long piece, int max_pieces, int* ptree, int* pnode,
+                           long long* pbeg, long long* pend, int* n_live, void* stream) {
+  if (T <= 0 || W <= 0 || T * W > 16384 || piece <= 0) return ORYX_EINVAL;
+  hipLaunchKernelGGL(rdf_expand_pieces, dim3(1), dim3(1024), 0,
+                     reinterpret_cast<hipStream_t>(stream), counts, T, W, lo, hi, piece,
+                     max_pieces, ptree, pnode, pbeg, pend, n_live);
+  return oryx_check_launch();
+}
+
+// hist [T][W][Fs][B][S] fp32 -> best split per (tree, node); see rdf_best_split.
+int oryx_rdf_best_split(const float* hist, const int* feats, const unsigned char* is_cat, int T,
+                        int W, int Fs, int B, int S, int kind, int force_leaf, int* out_feat,
+                        int* out_bin, double* out_tot, float* out_gain,
+                        unsigned char* cat_left, void* stream) {
+  if (T <= 0 || W <= 0) return ORYX_OK;
+  if (S < 1 || S > RDF_MAX_S || B < 1 || kind < 0 || kind > 2) return ORYX_EINVAL;
+  const size_t smem = is_cat ? (size_t)64 * B * sizeof(unsigned short) : 0;
+  if (smem > 64 * 1024) return ORYX_EINVAL;
+  hipLaunchKernelGGL(rdf_best_split, dim3((unsigned)(T * W)), dim3(64), smem,
+                     reinterpret_cast<hipStream_t>(stream), hist, feats, is_cat, T, W, Fs, B, S,
+                     kind, force_leaf, out_feat, out_bin, out_tot, out_gain, cat_left);
+  return oryx_check_launch();
+}
+
 
 // bin_bytes: 1 (uint8 bins) or 2 (int16 bins); cls: 1 classification (label, S classes),
 // 0 regression (y, S == 3).  hist must be zeroed: [T][nodes][Fs][B][S] fp32.
@@ -585,7 +825,7 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
                               const int* piece_tree, const int* piece_node,
                               const long long* piece_lo, const long long* piece_hi,
                               int n_pieces, int nodes, const int* feats, int Fs, int B,
-                              float* hist, void* stream) {
+                              float* hist, const int* n_live, void* stream) {
   if (n_pieces <= 0) return ORYX_OK;
   if ((bin_bytes != 1 && bin_bytes != 2) || (cls && !label) || (!cls && (!y || S != 3)))
     return ORYX_EINVAL;
@@ -604,12 +844,12 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
         hipLaunchKernelGGL((rdf_histogram_staged<true>), dim3((unsigned)n_pieces), dim3(256),
                            smem_st, s, reinterpret_cast<const unsigned char*>(Xb), n, P, label,
                            y, S, weight, perm, piece_tree, piece_node, piece_lo, piece_hi,
-                           nodes, feats, Fs, B, hist, ndw, rsw);
+                           nodes, feats, Fs, B, hist, ndw, rsw, n_live);
       else
         hipLaunchKernelGGL((rdf_histogram_staged<false>), dim3((unsigned)n_pieces), dim3(256),
                            smem_st, s, reinterpret_cast<const unsigned char*>(Xb), n, P, label,
                            y, S, weight, perm, piece_tree, piece_node, piece_lo, piece_hi,
-                           nodes, feats, Fs, B, hist, ndw, rsw);
+                           nodes, feats, Fs, B, hist, ndw, rsw, n_live);
       return oryx_check_launch();
     }
   }
@@ -619,7 +859,7 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
   hipLaunchKernelGGL((rdf_histogram_pieces<BT, C, L>), dim3((unsigned)n_pieces), dim3(256),  \
                      smem, s, reinterpret_cast<const BT*>(Xb), n, P, label, y, S, weight,     \
                      perm, piece_tree, piece_node, piece_lo, piece_hi, nodes, feats, Fs, B,   \
-                     hist)
+                     hist, n_live)
   if (bin_bytes == 1) {
     if (cls) {
       if (lds) PIECE_LAUNCH(unsigned char, true, true); else PIECE_LAUNCH(unsigned char, true, false);

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 9
+KERNELS_ABI_VERSION = 10
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -170,9 +170,17 @@ def _load_kernels():
     _sig(lib, "oryx_topn_scan", c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_vp, c_vp, c_i, c_vp, c_vp,
                                       c_i, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_counting_sort", c_i, [c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])
+    # ..., hist, n_live (device piece count, nullable), stream
     _sig(lib, "oryx_rdf_histogram_pieces", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i,
                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
-                                                 c_vp, c_i, c_i, c_vp, c_vp])
+                                                 c_vp, c_i, c_i, c_vp, c_vp, c_vp])
+    # counts, T, W, lo, hi, piece, max_pieces, ptree, pnode, pbeg, pend, n_live, stream
+    _sig(lib, "oryx_rdf_expand_pieces", c_i, [c_vp, c_i, c_i, c_i, c_i, c_ll, c_i, c_vp, c_vp,
+                                              c_vp, c_vp, c_vp, c_vp])
+    # hist, feats, is_cat, T, W, Fs, B, S, kind, force_leaf, feat, bin, tot, gain, cat_left,
+    # stream
+    _sig(lib, "oryx_rdf_best_split", c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
+                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_sorted_ws_bytes", c_ll, [c_ll, c_i])
     _sig(lib, "oryx_kmeans_accumulate_sorted", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i,
                                                      c_vp, c_vp, c_vp, c_vp, c_vp])

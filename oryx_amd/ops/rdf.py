@@ -221,6 +221,39 @@ def _choose_splits(hist: torch.Tensor, feats: torch.Tensor, data: BinnedData, ki
                                                                  best))
 
 
+_KIND = {"gini": 0, "entropy": 1, "variance": 2}
+
+
+def _split_kernel_ok(data: BinnedData, S: int) -> bool:
+    return S <= 32 and (not any(data.categorical) or 64 * data.B * 2 <= 64 * 1024)
+
+
+def _choose_splits_kernel(hist: torch.Tensor, feats: torch.Tensor, data: BinnedData, kind: str,
+                          force_leaf: bool) -> LevelSplits:
+    """:func:`_choose_splits` as one HIP kernel (``rdf_best_split``: a wave per node, a lane
+    per candidate feature, fp64 prefix sums and gains) instead of ~25 tensor ops over
+    [T, N, Fs, B, S] temporaries."""
+    T, N, Fs, B, S = hist.shape
+    dev = hist.device
+    lib = native.require_kernels()
+    h = hist.contiguous()
+    fe = feats.contiguous()
+    cat = data.cat_flags().to(torch.uint8) if any(data.categorical) else None
+    feat = torch.empty((T, N), dtype=torch.int32, device=dev)
+    sbin = torch.empty((T, N), dtype=torch.int32, device=dev)
+    tot = torch.empty((T, N, S), dtype=torch.float64, device=dev)
+    gain = torch.empty((T, N), dtype=torch.float32, device=dev)
+    cl = torch.empty((T, N, B), dtype=torch.uint8, device=dev) if cat is not None else None
+    rc = lib.oryx_rdf_best_split(h.data_ptr(), fe.data_ptr(),
+                                 cat.data_ptr() if cat is not None else None, T, N, Fs, B, S,
+                                 _KIND[kind], int(bool(force_leaf)), feat.data_ptr(),
+                                 sbin.data_ptr(), tot.data_ptr(), gain.data_ptr(),
+                                 cl.data_ptr() if cl is not None else None,
+                                 native.stream_ptr(dev))
+    native.check(rc, "oryx_rdf_best_split")
+    return LevelSplits(feat.long(), sbin.long(), cl, tot, gain)
+
+
 # ---------------------------------------------------------------- histogram / route
 
 def _histogram(data: BinnedData, label, y, S, cls, weight, node_of, lo, nodes, feats, B):
@@ -331,6 +364,12 @@ class RowGroups:
             c = counts.cpu().numpy()[:-1]
             live = c[:T * width].reshape(T, width)
             return RowGroups(perm, live, width, n, live + c[T * width:].reshape(T, width))
+
+        def device():
+            """(perm, live counts [T*width], visits [T, width]) left on the device."""
+            live = counts[:T * width]
+            return perm, live, (live + counts[T * width:2 * T * width]).view(T, width)
+        finish.device = device
         return finish
 
     def pieces(self, lo: int, hi: int, dev):
@@ -372,7 +411,7 @@ def _histogram_groups(data: BinnedData, label, y, S, cls, weight, groups: RowGro
         weight.data_ptr() if weight is not None else None,
         groups.perm.data_ptr() if groups.perm is not None else None,
         pt.data_ptr(), pn.data_ptr(), pb.data_ptr(), pe.data_ptr(), tot, nodes, fe.data_ptr(),
-        Fs, B, hist.data_ptr(), native.stream_ptr(dev))
+        Fs, B, hist.data_ptr(), None, native.stream_ptr(dev))
     native.check(rc, "oryx_rdf_histogram_pieces")
     return hist
 
@@ -492,6 +531,10 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     else:
         weight = None
     Fs = feature_subset or _feature_subset_size(P, T, classification)
+    if dev.type == "cuda" and _GROUPED and _DEVICE_LOOP and T * (1 << max_depth) <= 8191 and \
+            n * T < (1 << 31) and _split_kernel_ok(data, S):
+        return _train_device(data, label, y, y_shift, S, classification, kind, weight, T, Fs,
+                             max_depth, seed, ctx)
     node_of = torch.zeros((T, n), dtype=torch.int32, device=dev)
     roots = [TrainedNode("r") for _ in range(T)]
     level_nodes: List[List[Optional[TrainedNode]]] = [[r] for r in roots]
@@ -611,6 +654,155 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
             groups = finish_groups() if finish_groups is not None else None
     if pending is not None:
         build_level(*pending)
+    watchdog.get().end_heartbeats()
+    return TrainedForest(roots, predictor_counts, classification)
+
+
+_DEVICE_LOOP = os.environ.get("ORYX_RDF_DEVICE_LOOP", "1") != "0"
+
+
+def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classification: bool,
+                  kind: str, weight, T: int, Fs: int, max_depth: int, seed: int,
+                  ctx: dist.DistContext) -> TrainedForest:
+    """The level loop with no host round trip inside it (GPU, forests whose widest level fits
+    the counting sort's key space).  Level d has 2^d node slots per tree (slots past a tree's
+    real nodes stay empty: no rows, so no pieces, and they come out as leaves); per level the
+    device runs: feature subsets (device RNG), the piece list from the previous level's
+    counting sort (``rdf_expand_pieces``), the grouped histogram (grid = an upper bound on
+    the pieces, surplus workgroups retire on the device-side count), the split search
+    (``rdf_best_split``), child numbering, routing and the next level's counting sort.  Each
+    level's splits / totals / visits go to pinned host memory asynchronously with an event;
+    the host builds level d's nodes while the device is already working on later levels."""
+    dev = data.Xb.device
+    n, P = data.Xb.shape
+    B = data.B
+    lib = native.require_kernels()
+    stream = native.stream_ptr(dev)
+    gf = torch.Generator(device=dev)
+    gf.manual_seed((seed * 977 + 13) & ((1 << 62) - 1))
+    node_of = torch.zeros((T, n), dtype=torch.int32, device=dev)
+    roots = [TrainedNode("r") for _ in range(T)]
+    level_nodes: List[List[Optional[TrainedNode]]] = [[r] for r in roots]
+    predictor_counts = np.zeros(P, dtype=np.float64)
+    # root: every row of a tree is one group (identity permutation)
+    counts = torch.full((T,), n, dtype=torch.int64, device=dev)
+    visits = torch.full((T, 1), n, dtype=torch.int64, device=dev)
+    perm = None
+    pending = []
+    any_cat = any(data.categorical)
+
+    def sample_feats(width: int) -> torch.Tensor:
+        if Fs < P:
+            r = torch.rand((T, width, P), generator=gf, device=dev)
+            return torch.topk(r, Fs, dim=-1, largest=False, sorted=True).indices \
+                .to(torch.int32).contiguous()
+        return torch.arange(P, dtype=torch.int32, device=dev).expand(T, width, P).contiguous()
+
+    def build(lv) -> None:
+        nonlocal level_nodes
+        lv["event"].synchronize()
+        feat_h = lv["feat"].numpy()
+        bin_h = lv["bin"].numpy()
+        tot_h = lv["tot"].numpy().copy()
+        vis_h = lv["vis"].numpy()
+        cat_h = lv["cat"].numpy() if lv["cat"] is not None else None
+        if y_shift:
+            w_, s1 = tot_h[..., 0].copy(), tot_h[..., 1].copy()
+            tot_h[..., 2] += 2.0 * y_shift * s1 + y_shift * y_shift * w_
+            tot_h[..., 1] += y_shift * w_
+        new_level: List[List[Optional[TrainedNode]]] = []
+        for t in range(T):
+            row: List[Optional[TrainedNode]] = []
+            for slot, node in enumerate(level_nodes[t]):
+                node.count = int(vis_h[t, slot])
+                node.stats = tot_h[t, slot]
+                f = int(feat_h[t, slot])
+                if f >= 0:
+                    node.feature = f
+                    node.bin = int(bin_h[t, slot])
+                    if node.bin < 0:
+                        node.cat_left = np.nonzero(cat_h[t, slot])[0]
+                    node.left = TrainedNode(node.id + "-")
+                    node.right = TrainedNode(node.id + "+")
+                    row.extend([node.left, node.right])
+                    predictor_counts[f] += node.count
+            new_level.append(row)
+        level_nodes = new_level
+
+    def to_host(t: torch.Tensor) -> torch.Tensor:
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        return h
+
+    W = 1
+    for depth in range(max_depth + 1):
+        faults.point("rdf.level", depth=depth, rank=ctx.rank)
+        watchdog.heartbeat("rdf.level")
+        feats = sample_feats(W)
+        chunk = max(1, _HIST_BUDGET // max(1, T * Fs * B * S))
+        parts = []
+        for lo in range(0, W, chunk):
+            hi = min(W, lo + chunk)
+            hist = torch.zeros((T, hi - lo, Fs, B, S), dtype=torch.float32, device=dev)
+            max_pieces = (T * n + _PIECE - 1) // _PIECE + T * (hi - lo)
+            ptree = torch.empty(max_pieces, dtype=torch.int32, device=dev)
+            pnode = torch.empty(max_pieces, dtype=torch.int32, device=dev)
+            pbeg = torch.empty(max_pieces, dtype=torch.int64, device=dev)
+            pend = torch.empty(max_pieces, dtype=torch.int64, device=dev)
+            n_live = torch.empty(1, dtype=torch.int32, device=dev)
+            native.check(lib.oryx_rdf_expand_pieces(
+                counts.data_ptr(), T, W, lo, hi, _PIECE, max_pieces, ptree.data_ptr(),
+                pnode.data_ptr(), pbeg.data_ptr(), pend.data_ptr(), n_live.data_ptr(), stream),
+                "oryx_rdf_expand_pieces")
+            fe = feats[:, lo:hi].contiguous()
+            native.check(lib.oryx_rdf_histogram_pieces(
+                data.Xb.data_ptr(), data.bin_bytes, n, P,
+                label.data_ptr() if classification else None,
+                None if classification else y.data_ptr(), S, int(classification),
+                weight.data_ptr() if weight is not None else None,
+                perm.data_ptr() if perm is not None else None, ptree.data_ptr(),
+                pnode.data_ptr(), pbeg.data_ptr(), pend.data_ptr(), max_pieces, hi - lo,
+                fe.data_ptr(), Fs, B, hist.data_ptr(), n_live.data_ptr(), stream),
+                "oryx_rdf_histogram_pieces")
+            if ctx.is_distributed:
+                dist.all_reduce_sum(hist, ctx)
+            parts.append(_choose_splits_kernel(hist, fe, data, kind,
+                                               force_leaf=depth == max_depth))
+            del hist
+        if len(parts) == 1:
+            split = parts[0]
+        else:
+            split = LevelSplits(torch.cat([q.feat for q in parts], 1),
+                                torch.cat([q.bin for q in parts], 1),
+                                torch.cat([q.cat_left for q in parts], 1) if any_cat else None,
+                                torch.cat([q.totals for q in parts], 1),
+                                torch.cat([q.gain for q in parts], 1))
+        is_split = split.feat >= 0
+        rank = torch.cumsum(is_split.int(), 1) - is_split.int()
+        child_base = torch.where(is_split, 2 * rank, torch.full_like(rank, -1))
+        if depth < max_depth:
+            _route(data, node_of, W, split, child_base, B, count_visits=False)
+        vis = visits
+        if ctx.is_distributed:
+            vis = vis.clone()
+            dist.all_reduce_sum(vis, ctx)
+        lv = {"feat": to_host(split.feat.int()), "bin": to_host(split.bin.int()),
+              "tot": to_host(split.totals), "vis": to_host(vis),
+              "cat": to_host(split.cat_left) if split.cat_left is not None else None,
+              "event": torch.cuda.Event()}
+        lv["event"].record()
+        if depth < max_depth:
+            # next level: 2W slots, rows grouped by (tree, node) with one counting sort
+            W2 = 2 * W
+            finish = RowGroups.launch_from_nodes(node_of, W2, weight)
+            perm, counts, visits = finish.device()
+            W = W2
+        # the previous level's nodes are built while this level's work runs
+        while pending:
+            build(pending.pop(0))
+        pending.append(lv)
+    while pending:
+        build(pending.pop(0))
     watchdog.get().end_heartbeats()
     return TrainedForest(roots, predictor_counts, classification)
 

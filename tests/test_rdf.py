@@ -533,3 +533,78 @@ def test_regression_split_with_large_target_offset():
     assert (root.feature, root.bin) == (best[1], best[2])
     # leaf statistics are reported un-centred
     assert abs(root.stats[1] / root.stats[0] - y.mean()) < 1e-6
+
+
+def _random_level(T, N, Fs, B, S, P, cls, seed, rows=300):
+    """Level histograms of random rows (float weights, so no exact gain ties): every feature
+    slot of a node bins the same rows, so all slots share the node totals."""
+    g = torch.Generator().manual_seed(seed)
+    hist = torch.zeros((T, N, Fs, B, S), dtype=torch.float64)
+    for t in range(T):
+        for nd in range(N):
+            w = torch.rand(rows, generator=g, dtype=torch.float64) * 2
+            if cls:
+                lab = torch.randint(0, S, (rows,), generator=g)
+                stat = torch.zeros((rows, S), dtype=torch.float64)
+                stat[torch.arange(rows), lab] = w
+            else:
+                yv = torch.randn(rows, generator=g, dtype=torch.float64) + \
+                    torch.linspace(-1, 1, rows, dtype=torch.float64)
+                stat = torch.stack([w, w * yv, w * yv * yv], 1)
+            for j in range(Fs):
+                b = torch.randint(0, B, (rows,), generator=g)
+                hist[t, nd, j].index_add_(0, b, stat)
+    feats = torch.stack([torch.randperm(P, generator=g)[:Fs] for _ in range(T * N)]) \
+        .view(T, N, Fs).int()
+    return hist.float(), feats
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls,kind", [(True, "gini"), (True, "entropy"), (False, "variance")])
+@pytest.mark.parametrize("with_cat", [False, True])
+def test_split_kernel_matches_tensor_search(cuda, cls, kind, with_cat):
+    """rdf_best_split (one wave per node, fp64) against the tensor-op split search."""
+    T, N, Fs, B, S, P = 3, 9, 6, 11, 3, 10
+    hist, feats = _random_level(T, N, Fs, B, S, P, cls, seed=7 + int(with_cat))
+    cat = [with_cat and (f % 3 == 0) for f in range(P)]
+    data = rdf_ops.BinnedData(torch.zeros((1, P), dtype=torch.uint8, device=cuda), [B] * P,
+                              [None] * P, cat, B)
+    # the reference search on the same fp32 statistics, evaluated in fp64
+    ref = rdf_ops._choose_splits(hist.double().to(cuda), feats.to(cuda), data, kind, False)
+    got = rdf_ops._choose_splits_kernel(hist.to(cuda), feats.to(cuda), data, kind, False)
+    assert torch.equal(got.feat.cpu(), ref.feat.cpu())
+    assert torch.equal(got.bin.cpu(), ref.bin.cpu())
+    np.testing.assert_allclose(got.totals.cpu().numpy(), ref.totals.double().cpu().numpy())
+    if with_cat:
+        assert torch.equal(got.cat_left.cpu(), ref.cat_left.cpu())
+    leaf = rdf_ops._choose_splits_kernel(hist.to(cuda), feats.to(cuda), data, kind, True)
+    assert (leaf.feat == -1).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("classification", [True, False])
+def test_device_level_loop_matches_host_loop(cuda, classification, monkeypatch):
+    """The sync-free level loop (device pieces, split kernel, pipelined host tree build)
+    grows the same single full-feature tree as the host-driven loop."""
+    X, y = _numeric_data(30000, seed=6)
+    yr = X[:, 0] * 2 - X[:, 2] + 0.1 * X[:, 1]
+    data = rdf_ops.bin_features(X, [False] * 4, [0] * 4, 32, cuda, seed=2)
+    tgt = torch.from_numpy(y if classification else yr)
+    kind = "entropy" if classification else "variance"
+    out = {}
+    for flag in (False, True):
+        monkeypatch.setattr(rdf_ops, "_DEVICE_LOOP", flag)
+        out[flag] = rdf_ops.train_forest(data, tgt, 2 if classification else 0, 1, 6, kind,
+                                         seed=3)
+
+    def walk(nd):
+        yield (nd.id, nd.feature, nd.bin, nd.count)
+        if nd.feature >= 0:
+            yield from walk(nd.left)
+            yield from walk(nd.right)
+    assert list(walk(out[False].roots[0])) == list(walk(out[True].roots[0]))
+    np.testing.assert_allclose(out[False].predictor_counts, out[True].predictor_counts)
+    # a bootstrapped multi-tree forest through the device loop: every tree has a root split
+    monkeypatch.setattr(rdf_ops, "_DEVICE_LOOP", True)
+    f = rdf_ops.train_forest(data, tgt, 2 if classification else 0, 6, 5, kind, seed=4)
+    assert all(r.feature >= 0 and r.count == 30000 for r in f.roots)

@@ -21,9 +21,10 @@ def _special_matrix(rows=300, k=67, seed=0):
     x[2] = g.normal(scale=1e-6, size=k)
     bits = g.integers(0, 2 ** 32, size=k, dtype=np.uint64).astype(np.uint32)
     x[3] = bits.view(np.float32)
-    x[4, :12] = [0.0, -0.0, 1.0, -1.0, 100.0, 33871888.0, 1e-7, 3.4e38, 1.4e-45, 123456.7,
-                 np.inf, -np.inf]
-    x[5, :3] = [np.nan, 0.1, 1e10]
+    sp = [0.0, -0.0, 1.0, -1.0, 100.0, 33871888.0, 1e-7, 3.4e38, 1.4e-45, 123456.7, np.inf,
+          -np.inf]
+    x[4, :min(k, 12)] = sp[:min(k, 12)]
+    x[5, :min(k, 3)] = [np.nan, 0.1, 1e10][:min(k, 3)]
     return x
 
 
