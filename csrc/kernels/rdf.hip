@@ -528,6 +528,48 @@ __global__ __launch_bounds__(1024) void rdf_expand_pieces(
   if (tid == 1023) *n_live = (int)(s_np[1023] < max_pieces ? s_np[1023] : max_pieces);
 }
 
+// Fused forest scoring + weighted vote (K14 + K15): one thread per example walks every tree
+// (the same traversal as rdf_forest_leaf) and accumulates w_t * leaf_value[leaf] into its own
+// output row, then divides by the weight sum -- the [n, T, C] gather of per-tree leaf values
+// never exists.  vote [n][C] (regression: C = 1, the weighted mean).
+__global__ __launch_bounds__(256) void rdf_forest_vote(
+    const double* __restrict__ X, long long n, int F, int T, const int* __restrict__ roots,
+    const int* __restrict__ feat, const double* __restrict__ thr, const int* __restrict__ cat_off,
+    const unsigned char* __restrict__ cat_bits, const int* __restrict__ cat_len,
+    const int* __restrict__ left, const int* __restrict__ right,
+    const double* __restrict__ leaf_value, int C, const double* __restrict__ weights,
+    double* __restrict__ vote) {
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < n;
+       e += (long long)gridDim.x * 256) {
+    const double* x = X + e * F;
+    double* out = vote + e * C;
+    for (int c = 0; c < C; ++c) out[c] = 0.0;
+    double wsum = 0.0;
+    for (int t = 0; t < T; ++t) {
+      int node = roots[t];
+      for (int guard = 0; guard < 4096; ++guard) {
+        const int f = feat[node];
+        if (f < 0) break;
+        bool pos;
+        const int co = cat_off[node];
+        if (co >= 0) {
+          const int enc = (int)x[f];
+          pos = enc >= 0 && enc < cat_len[node] && cat_bits[co + enc] != 0;
+        } else {
+          pos = x[f] >= thr[node];
+        }
+        node = pos ? right[node] : left[node];
+      }
+      const double w = weights[t];
+      wsum += w;
+      const double* lv = leaf_value + (long long)node * C;
+      for (int c = 0; c < C; ++c) out[c] += w * lv[c];
+    }
+    const double inv = wsum != 0.0 ? 1.0 / wsum : 0.0;
+    for (int c = 0; c < C; ++c) out[c] *= inv;
+  }
+}
+
 // impurity of label statistics st[0..S) (classification counts; regression w, sum wy,
 // sum wy^2), weight in *w.  kind: 0 gini, 1 entropy (log2), 2 variance.
 __device__ double rdf_impurity(const double* st, int S, int kind, double* w) {
@@ -691,6 +733,21 @@ __global__ __launch_bounds__(64) void rdf_best_split(
 }  // namespace
 
 extern "C" {
+
+int oryx_rdf_forest_vote(const double* X, long long n, int F, int T, const int* roots,
+                         const int* feat, const double* thr, const int* cat_off,
+                         const unsigned char* cat_bits, const int* cat_len, const int* left,
+                         const int* right, const double* leaf_value, int C,
+                         const double* weights, double* vote, void* stream) {
+  if (n <= 0 || T <= 0) return ORYX_OK;
+  if (C < 1) return ORYX_EINVAL;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(rdf_forest_vote, dim3((unsigned)blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), X, n, F, T, roots, feat, thr,
+                     cat_off, cat_bits, cat_len, left, right, leaf_value, C, weights, vote);
+  return oryx_check_launch();
+}
 
 int oryx_rdf_expand_pieces(const long long* counts, int T, int W, int lo, int hi,
                            long long piece, int max_pieces, int* ptree, int* pnode,

@@ -185,10 +185,7 @@ def evaluate_forest(forest, encodings, schema: InputSchema, full: np.ndarray,
         if schema.is_classification() else 0
     flat = rdf_ops.flatten_forest(forest, device, C)
     X = torch.from_numpy(full).to(device)
-    leaves = rdf_ops.forest_leaves(flat, X)                          # [n, T]
-    vals = flat.leaf_value[leaves]                                    # [n, T, C|1]
-    w = flat.weights[None, :, None]
-    vote = (vals * w).sum(1) / flat.weights.sum()
+    vote = rdf_ops.forest_vote(flat, X)                               # [n, C|1]
     tgt = torch.from_numpy(target).to(device)
     if schema.is_classification():
         pred = vote.argmax(1)

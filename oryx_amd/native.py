@@ -174,6 +174,10 @@ def _load_kernels():
     _sig(lib, "oryx_rdf_histogram_pieces", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i,
                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                                  c_vp, c_i, c_i, c_vp, c_vp, c_vp])
+    # X, n, F, T, roots, feat, thr, cat_off, cat_bits, cat_len, left, right, leaf_value, C,
+    # weights, vote, stream
+    _sig(lib, "oryx_rdf_forest_vote", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            c_vp, c_vp, c_vp, c_vp, c_i, c_vp, c_vp, c_vp])
     # counts, T, W, lo, hi, piece, max_pieces, ptree, pnode, pbeg, pend, n_live, stream
     _sig(lib, "oryx_rdf_expand_pieces", c_i, [c_vp, c_i, c_i, c_i, c_i, c_ll, c_i, c_vp, c_vp,
                                               c_vp, c_vp, c_vp, c_vp])

@@ -40,7 +40,7 @@ from ..parallel import dist, watchdog
 from ..utils import faults
 
 __all__ = ["BinnedData", "bin_features", "train_forest", "TrainedForest", "FlatForest",
-           "flatten_forest", "forest_leaves"]
+           "flatten_forest", "forest_leaves", "forest_vote"]
 
 _HIST_BUDGET = 1 << 26          # floats per histogram pass (256 MB)
 # GPU level histograms from rows grouped by node (counting sort per level); ORYX_RDF_GROUPED=0
@@ -883,6 +883,34 @@ def flatten_forest(forest, device, num_classes: int) -> FlatForest:
                       torch.from_numpy(leaf_value).to(device),
                       torch.from_numpy(np.asarray(forest.get_weights(), dtype=np.float64))
                       .to(device), objs)
+
+
+def forest_vote(flat: FlatForest, X: torch.Tensor) -> torch.Tensor:
+    """Weighted vote of the forest per example: [n, C] mean class probabilities
+    (classification) or [n, 1] weighted mean prediction (regression).  GPU: one fused
+    traversal + vote kernel (``rdf_forest_vote``); CPU: leaves then a gather."""
+    X = X.to(torch.float64).contiguous()
+    n, F = X.shape
+    T = flat.roots.numel()
+    C = int(flat.leaf_value.shape[1])
+    dev = X.device
+    if dev.type == "cuda":
+        lib = native.require_kernels()
+        out = torch.empty((n, C), dtype=torch.float64, device=dev)
+        lv = flat.leaf_value.contiguous()
+        wt = flat.weights.to(torch.float64).contiguous()
+        rc = lib.oryx_rdf_forest_vote(X.data_ptr(), n, F, T, flat.roots.data_ptr(),
+                                      flat.feat.data_ptr(), flat.thr.data_ptr(),
+                                      flat.cat_off.data_ptr(), flat.cat_bits.data_ptr(),
+                                      flat.cat_len.data_ptr(), flat.left.data_ptr(),
+                                      flat.right.data_ptr(), lv.data_ptr(), C, wt.data_ptr(),
+                                      out.data_ptr(), native.stream_ptr(dev))
+        native.check(rc, "oryx_rdf_forest_vote")
+        return out
+    leaves = forest_leaves(flat, X)
+    vals = flat.leaf_value[leaves]                                    # [n, T, C]
+    w = flat.weights[None, :, None]
+    return (vals * w).sum(1) / flat.weights.sum()
 
 
 def forest_leaves(flat: FlatForest, X: torch.Tensor) -> torch.Tensor:

@@ -412,6 +412,10 @@ def test_gpu_forest_leaves_match_cpu(cuda):
     lc = rdf_ops.forest_leaves(flat_c, torch.from_numpy(full))
     lg = rdf_ops.forest_leaves(flat_g, torch.from_numpy(full).to(cuda)).cpu()
     assert torch.equal(lc, lg)
+    # fused traversal + weighted vote (K15) == leaves then the gathered vote on the host
+    vc = rdf_ops.forest_vote(flat_c, torch.from_numpy(full))
+    vg = rdf_ops.forest_vote(flat_g, torch.from_numpy(full).to(cuda)).cpu()
+    torch.testing.assert_close(vg, vc, rtol=1e-12, atol=1e-12)
 
 
 @pytest.mark.gpu
