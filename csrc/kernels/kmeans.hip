@@ -974,6 +974,100 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
   }
 }
 
+// Silhouette coefficient of a sample (K10; SilhouetteCoefficient.java:39-147): for every
+// point i, a_i = mean distance to the other points of its cluster, b_i = smallest mean
+// distance to another cluster, s_i = (b - a) / max(a, b) (0 for singleton clusters).  The
+// sample is sorted by cluster, so the columns of one cluster are contiguous: a thread owns row
+// i and streams every column once, accumulating Euclidean distances (fp32 differences squared,
+// sqrt, fp64 sums) into a running per-cluster sum that is finalised into a / b whenever the
+// column's cluster changes -- no [s, s] distance matrix and no [s, k] per-cluster GEMM.  Column
+// tiles (32 columns x 64 dimensions) come through LDS as broadcast reads; the row's own
+// coordinates come from the transposed copy xT [d][s] (coalesced across the block's rows).
+// Output: per-block partial sums of s_i (fp64).
+constexpr int SIL_TC = 32, SIL_DC = 64;
+__global__ __launch_bounds__(256) void km_silhouette(
+    const float* __restrict__ x, const float* __restrict__ xT, const int* __restrict__ cl,
+    const int* __restrict__ csize, int s, int d, double* __restrict__ partial) {
+  __shared__ float tile[SIL_DC][SIL_TC];
+  __shared__ int tcl[SIL_TC];
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  const int i = blockIdx.x * 256 + tid;
+  const bool live = i < s;
+  const int own = live ? cl[i] : -1;
+  double a = 0.0, b = INFINITY;
+  int cur = -1;
+  double cur_sum = 0.0;
+  auto finish = [&](int c, double sum) {
+    if (c < 0) return;
+    if (c == own) {
+      a = sum;
+    } else {
+      const double m = sum / (double)csize[c];
+      b = m < b ? m : b;
+    }
+  };
+  for (int j0 = 0; j0 < s; j0 += SIL_TC) {
+    float acc[SIL_TC];
+#pragma unroll
+    for (int c = 0; c < SIL_TC; ++c) acc[c] = 0.f;
+    __syncthreads();
+    if (tid < SIL_TC) tcl[tid] = j0 + tid < s ? cl[j0 + tid] : -1;
+    for (int d0 = 0; d0 < d; d0 += SIL_DC) {
+      __syncthreads();
+      for (int e = tid; e < SIL_TC * SIL_DC; e += 256) {
+        const int c = e / SIL_DC, dd = e % SIL_DC;
+        const int j = j0 + c, dim = d0 + dd;
+        tile[dd][c] = (j < s && dim < d) ? x[(long long)j * d + dim] : 0.f;
+      }
+      __syncthreads();
+      const int dn = d - d0 < SIL_DC ? d - d0 : SIL_DC;
+      for (int dd = 0; dd < dn; ++dd) {
+        const float xi = live ? xT[(long long)(d0 + dd) * s + i] : 0.f;
+        const f32x4* tr = reinterpret_cast<const f32x4*>(&tile[dd][0]);
+#pragma unroll
+        for (int q = 0; q < SIL_TC / 4; ++q) {
+          const f32x4 v = tr[q];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float df = xi - v[e];
+            acc[4 * q + e] += df * df;
+          }
+        }
+      }
+    }
+    if (live) {
+#pragma unroll
+      for (int c = 0; c < SIL_TC; ++c) {
+        const int cc = tcl[c];
+        if (cc < 0) continue;
+        if (cc != cur) {
+          finish(cur, cur_sum);
+          cur = cc;
+          cur_sum = 0.0;
+        }
+        cur_sum += (double)sqrtf(acc[c]);
+      }
+    }
+  }
+  double sil = 0.0;
+  if (live) {
+    finish(cur, cur_sum);
+    const int n_own = csize[own];
+    if (n_own > 1) {
+      a /= (double)(n_own - 1);
+      sil = a < b ? 1.0 - a / b : (a > b ? b / a - 1.0 : 0.0);
+    }
+  }
+  red[tid] = sil;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) red[tid] += red[tid + off];
+    __syncthreads();
+  }
+  if (tid == 0) partial[blockIdx.x] = red[0];
+}
+
 }  // namespace
 
 extern "C" {
@@ -1268,6 +1362,18 @@ int oryx_kmeans_accumulate_sorted(const float* X, const int* assign, const float
   else
     hipLaunchKernelGGL(km_segment_sum<false>, dim3((unsigned)max_pieces), dim3(256), 0, s, X,
                        mind, d, ld, k, perm, counts, off, pieces, tpr, sums, dstats);
+  return oryx_check_launch();
+}
+
+// x [s][d] and xT [d][s] fp32 of the sample sorted by cluster id cl [s] (every id in
+// [0, k), csize[k] = points per cluster); partial [ceil(s / 256)] receives per-block sums of
+// the points' silhouettes.
+int oryx_kmeans_silhouette(const float* x, const float* xT, const int* cl, const int* csize,
+                           int s, int d, double* partial, void* stream) {
+  if (s <= 0) return ORYX_OK;
+  if (d <= 0) return ORYX_EINVAL;
+  hipLaunchKernelGGL(km_silhouette, dim3((unsigned)((s + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), x, xT, cl, csize, s, d, partial);
   return oryx_check_launch();
 }
 

@@ -158,6 +158,8 @@ def _load_kernels():
     _sig(lib, "oryx_kmeans_assign_cert", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_i,
                                                c_i, c_vp, c_i, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                c_vp])
+    # x, xT, cl, csize, s, d, partial, stream
+    _sig(lib, "oryx_kmeans_silhouette", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_vp, c_vp])
     # X, Y, k, xrow, yrow, vals, xinv, yinv, implicit, n, new_x, new_y, vx, vy, stream
     _sig(lib, "oryx_als_foldin", c_i, [c_vp, c_vp, c_i, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_ll,
                                        c_vp, c_vp, c_vp, c_vp, c_vp])

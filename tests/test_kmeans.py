@@ -646,3 +646,20 @@ def test_sharded_eval_metrics_equal_single_process(tmp_path):
         assert a[s] == pytest.approx(a[s + "_1"], rel=1e-12) and a[s] == b[s]
     # 1200 points < the 100k cap: the sample is everything on both sides
     assert a["SIL"] == pytest.approx(a["SIL_1"], rel=1e-9) and a["SIL"] == b["SIL"]
+
+
+@pytest.mark.gpu
+def test_silhouette_kernel_matches_host(cuda):
+    """km_silhouette (sorted sample, streamed distances, running per-cluster sums) against the
+    fp64 tensor path, on the golden points and on a wide sample with an empty cluster and a
+    singleton cluster."""
+    clusters = read_clusters(dummy_pmml())
+    assert ev.silhouette_coefficient(clusters, EVAL_POINTS, cuda) == pytest.approx(
+        0.30648167401009796, abs=1e-6)
+    g = np.random.default_rng(8)
+    cs = [g.normal(0, 4, 70) for _ in range(12)]
+    pts = np.concatenate([g.normal(c, 1.0, (300, 70)) for c in cs[:10]] + [cs[10][None]])
+    clusters = [ClusterInfo(i, c.tolist(), 1) for i, c in enumerate(cs)]
+    host = ev.silhouette_coefficient(clusters, pts, torch.device("cpu"))
+    dev = ev.silhouette_coefficient(clusters, pts, cuda)
+    assert dev == pytest.approx(host, rel=1e-5)
