@@ -598,9 +598,12 @@ void als_update_messages(Dict* du, Dict* di, long long ue, long long ie, const c
   }
 }
 
-// Runs the per-event formatter over the native threads and joins the parts into out.
+// Runs the per-event formatter over the native threads and joins the parts into out; with
+// msg_ends (capacity 2n), the end offset of every '\n'-terminated message (its '\n' excluded)
+// is written and *n_msgs set.
 template <class Fn>
-long long join_event_parts(long long n, char* out, long long cap, Fn&& fn) {
+long long join_event_parts(long long n, char* out, long long cap, long long* msg_ends,
+                           long long* n_msgs, Fn&& fn) {
   const int T = oryx_ff::native_threads();
   std::vector<std::string> part((size_t)T);
   const int P = oryx_ff::parallel_ranges(n, 256, [&](long long lo, long long hi, int t) {
@@ -609,11 +612,23 @@ long long join_event_parts(long long n, char* out, long long cap, Fn&& fn) {
   long long need = 0;
   for (int t = 0; t < P; ++t) need += (long long)part[(size_t)t].size();
   if (need > cap) return -need;
-  long long pos = 0;
+  long long pos = 0, m = 0;
   for (int t = 0; t < P; ++t) {
-    std::memcpy(out + pos, part[(size_t)t].data(), part[(size_t)t].size());
-    pos += (long long)part[(size_t)t].size();
+    const std::string& q = part[(size_t)t];
+    std::memcpy(out + pos, q.data(), q.size());
+    if (msg_ends) {
+      const char* b = q.data();
+      const char* e = b + q.size();
+      for (const char* c = b; c < e;) {
+        const char* nl = static_cast<const char*>(memchr(c, '\n', (size_t)(e - c)));
+        if (!nl) break;
+        msg_ends[m++] = pos + (nl - b);
+        c = nl + 1;
+      }
+    }
+    pos += (long long)q.size();
   }
+  if (n_msgs) *n_msgs = m;
   return pos;
 }
 
@@ -631,7 +646,8 @@ long long oryx_format_als_updates(void* users, void* items, const long long* u,
                                   int k, int with_known, char* out, long long cap) {
   auto* du = static_cast<Dict*>(users);
   auto* di = static_cast<Dict*>(items);
-  return join_event_parts(n, out, cap, [&](long long lo, long long hi, std::string& o) {
+  return join_event_parts(n, out, cap, nullptr, nullptr,
+                          [&](long long lo, long long hi, std::string& o) {
     o.reserve((size_t)(hi - lo) * (size_t)(k * 24 + 96));
     std::string qu, qi, xr, yr;
     for (long long e = lo; e < hi; ++e) {
@@ -646,24 +662,75 @@ long long oryx_format_als_updates(void* users, void* items, const long long* u,
 }
 
 // As oryx_format_als_updates with the rows already formatted (e.g. on the GPU): row e of
-// X is xtext[xends[e-1], xends[e]) (xends[-1] = 0), likewise Y.
+// X is xtext[xends[e-1], xends[e]) (xends[-1] = 0), likewise Y.  msg_ends (capacity 2n)
+// receives each message's end offset ('\n' excluded), *n_msgs their number.  Two threaded
+// passes: message sizes per event (the quoted IDs are the only unknowns), then every thread
+// writes its events straight into out at their prefix offsets.
 long long oryx_assemble_als_updates(void* users, void* items, const long long* u,
                                     const long long* i, const char* xtext,
                                     const long long* xends, const char* ytext,
                                     const long long* yends, const unsigned char* vx,
                                     const unsigned char* vy, long long n, int with_known,
-                                    char* out, long long cap) {
+                                    char* out, long long cap, long long* msg_ends,
+                                    long long* n_msgs) {
   auto* du = static_cast<Dict*>(users);
   auto* di = static_cast<Dict*>(items);
-  return join_event_parts(n, out, cap, [&](long long lo, long long hi, std::string& o) {
-    std::string qu, qi;
+  std::vector<long long> bytes((size_t)n + 1, 0), msgs((size_t)n + 1, 0);
+  // "[\"X\"," id "," row (",[" other "]")? "]\n"
+  oryx_ff::parallel_ranges(n, 256, [&](long long lo, long long hi, int) {
+    std::string q;
     for (long long e = lo; e < hi; ++e) {
+      q.clear();
+      json_quote(du->keys[(size_t)u[e]], q);
+      const long long lu = (long long)q.size();
+      q.clear();
+      json_quote(di->keys[(size_t)i[e]], q);
+      const long long li = (long long)q.size();
       const long long xs = e ? xends[e - 1] : 0, ys = e ? yends[e - 1] : 0;
-      als_update_messages(du, di, u[e], i[e], xtext + xs, (size_t)(xends[e] - xs),
-                          ytext + ys, (size_t)(yends[e] - ys), vx[e] != 0, vy[e] != 0,
-                          with_known != 0, o, qu, qi);
+      long long b = 0;
+      if (vx[e]) b += 5 + lu + 1 + (xends[e] - xs) + (with_known ? 3 + li : 0) + 2;
+      if (vy[e]) b += 5 + li + 1 + (yends[e] - ys) + (with_known ? 3 + lu : 0) + 2;
+      bytes[(size_t)e + 1] = b;
+      msgs[(size_t)e + 1] = (vx[e] ? 1 : 0) + (vy[e] ? 1 : 0);
     }
   });
+  for (long long e = 0; e < n; ++e) {
+    bytes[(size_t)e + 1] += bytes[(size_t)e];
+    msgs[(size_t)e + 1] += msgs[(size_t)e];
+  }
+  if (bytes[(size_t)n] > cap) return -bytes[(size_t)n];
+  oryx_ff::parallel_ranges(n, 256, [&](long long lo, long long hi, int) {
+    std::string qu, qi;
+    for (long long e = lo; e < hi; ++e) {
+      qu.clear();
+      qi.clear();
+      json_quote(du->keys[(size_t)u[e]], qu);
+      json_quote(di->keys[(size_t)i[e]], qi);
+      char* o = out + bytes[(size_t)e];
+      long long m = msgs[(size_t)e];
+      auto put = [&](const char* p, size_t len) { std::memcpy(o, p, len); o += len; };
+      auto one = [&](const char* kind, const std::string& self, const char* row, size_t rl,
+                     const std::string& other) {
+        put(kind, 5);
+        put(self.data(), self.size());
+        *o++ = ',';
+        put(row, rl);
+        if (with_known) {
+          put(",[", 2);
+          put(other.data(), other.size());
+          *o++ = ']';
+        }
+        *o++ = ']';
+        if (msg_ends) msg_ends[m++] = o - out;
+        *o++ = '\n';
+      };
+      const long long xs = e ? xends[e - 1] : 0, ys = e ? yends[e - 1] : 0;
+      if (vx[e]) one("[\"X\",", qu, xtext + xs, (size_t)(xends[e] - xs), qi);
+      if (vy[e]) one("[\"Y\",", qi, ytext + ys, (size_t)(yends[e] - ys), qu);
+    }
+  });
+  if (n_msgs) *n_msgs = msgs[(size_t)n];
+  return bytes[(size_t)n];
 }
 
 }  // extern "C"

@@ -641,9 +641,22 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
 // Records sharing one key (or none: key_len -1) given as one blob of values plus their byte
 // lengths (the producer's fast path: no per-record framing in the caller); same semantics
 // as oryx_log_append_batch.
+long long oryx_log_append_values_gap(void* h, int partition, const char* key, int key_len,
+                                     const char* blob, const long long* lens, int n, int gap,
+                                     long long ts_ms, int do_fsync);
+
 long long oryx_log_append_values(void* h, int partition, const char* key, int key_len,
                                  const char* blob, const long long* lens, int n,
                                  long long ts_ms, int do_fsync) {
+  return oryx_log_append_values_gap(h, partition, key, key_len, blob, lens, n, 0, ts_ms,
+                                    do_fsync);
+}
+
+// As oryx_log_append_values with `gap` separator bytes after every value in blob (e.g. the
+// '\n' between the messages of a native formatter's output).
+long long oryx_log_append_values_gap(void* h, int partition, const char* key, int key_len,
+                                     const char* blob, const long long* lens, int n, int gap,
+                                     long long ts_ms, int do_fsync) {
   long long total = 0;
   for (int i = 0; i < n; ++i) total += lens[i];
   const size_t kl = key_len < 0 ? 0 : (size_t)key_len;
@@ -658,7 +671,7 @@ long long oryx_log_append_values(void* h, int partition, const char* key, int ke
     if (kl) memcpy(o + 12, key, kl);
     memcpy(o + 12 + kl, v, (size_t)vl);
     o += 12 + kl + vl;
-    v += vl;
+    v += vl + gap;
   }
   return oryx_log_append_batch(h, partition, buf.data(), (long long)buf.size(), n, ts_ms,
                                do_fsync, nullptr);

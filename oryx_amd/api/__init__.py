@@ -21,6 +21,7 @@ implement these ABCs directly.
 from __future__ import annotations
 
 import abc
+import collections.abc
 from dataclasses import dataclass
 from typing import Any, Generic, Iterable, Iterator, List, Optional, Sequence, Tuple, TypeVar
 
@@ -28,8 +29,8 @@ K = TypeVar("K")
 M = TypeVar("M")
 U = TypeVar("U")
 
-__all__ = ["KeyMessage", "TopicProducer", "BatchLayerUpdate", "SpeedModelManager", "SpeedModel",
-           "ServingModelManager", "AbstractServingModelManager", "ServingModel",
+__all__ = ["KeyMessage", "MessageBlock", "TopicProducer", "BatchLayerUpdate",
+           "SpeedModelManager", "SpeedModel", "ServingModelManager", "AbstractServingModelManager", "ServingModel",
            "OryxServingException", "HasCSV", "Dataset"]
 
 
@@ -43,6 +44,58 @@ class KeyMessage(Generic[K, M]):
 
     def get_message(self):
         return self.message
+
+
+class MessageBlock(collections.abc.Sequence):
+    """A run of text messages held as one byte buffer plus end offsets (what the native /
+    GPU formatters produce) -- a read-only sequence of ``str`` that producers can append to
+    the log in one native call (:meth:`TopicProducer.send_block`) without materialising a
+    Python string per message.  ``ends[j]`` is the end of message j; message j starts after
+    the separator byte that follows message j - 1 (``sep`` = 1) or right at its end (0)."""
+
+    __slots__ = ("buf", "ends", "sep", "_cache")
+
+    def __init__(self, buf, ends, sep: int = 1):
+        import numpy as _np
+        self.buf = buf                       # bytes or uint8 numpy array
+        self.ends = _np.asarray(ends, dtype=_np.int64)
+        self.sep = int(sep)
+        self._cache = None
+
+    def starts(self):
+        import numpy as _np
+        if len(self.ends) == 0:
+            return self.ends
+        return _np.r_[0, self.ends[:-1] + self.sep]
+
+    def lengths(self):
+        return self.ends - self.starts()
+
+    def __len__(self) -> int:
+        return len(self.ends)
+
+    def _all(self) -> List[str]:
+        if self._cache is None:
+            text = str(memoryview(self.buf)[:int(self.ends[-1]) if len(self.ends) else 0],
+                       "utf-8")
+            st = self.starts().tolist()
+            self._cache = [text[a:b] for a, b in zip(st, self.ends.tolist())] \
+                if text.isascii() else [bytes(memoryview(self.buf)[a:b]).decode("utf-8")
+                                        for a, b in zip(st, self.ends.tolist())]
+        return self._cache
+
+    def __getitem__(self, j):
+        return self._all()[j]
+
+    def __iter__(self) -> Iterator[str]:
+        return iter(self._all())
+
+    def __eq__(self, other) -> bool:
+        return list(self) == list(other) if isinstance(other, (list, tuple, MessageBlock)) \
+            else NotImplemented
+
+    def __repr__(self) -> str:
+        return "MessageBlock(%d messages)" % len(self)
 
 
 class TopicProducer(abc.ABC, Generic[K, M]):
@@ -60,6 +113,10 @@ class TopicProducer(abc.ABC, Generic[K, M]):
     def send_many(self, pairs: Iterable[Tuple[Optional[K], M]]) -> None:
         for k, m in pairs:
             self.send(k, m)
+
+    def send_block(self, key: Optional[K], block: "MessageBlock") -> None:
+        """Send every message of ``block`` with ``key`` (in order)."""
+        self.send_many((key, m) for m in block)
 
     def close(self) -> None:
         pass

@@ -202,13 +202,14 @@ def format_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndarra
 
 
 def assemble_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndarray,
-                         xrows, yrows, vx: np.ndarray, vy: np.ndarray,
-                         with_known: bool) -> List[str]:
+                         xrows, yrows, vx: np.ndarray, vy: np.ndarray, with_known: bool):
     """As :func:`format_als_updates` with the factor rows already formatted
-    (:class:`~oryx_amd.ops.textfmt.RowText`, e.g. by the GPU formatter)."""
+    (:class:`~oryx_amd.ops.textfmt.RowText`, e.g. by the GPU formatter).  Returns a
+    :class:`~oryx_amd.api.MessageBlock` (one buffer; producers append it natively)."""
+    from .api import MessageBlock
     n = len(u)
     if n == 0:
-        return []
+        return MessageBlock(b"", np.zeros(0, dtype=np.int64))
     u = np.ascontiguousarray(u, dtype=np.int64)
     i = np.ascontiguousarray(i, dtype=np.int64)
     vx = np.ascontiguousarray(vx, dtype=np.uint8)
@@ -218,10 +219,39 @@ def assemble_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndar
     vp = ctypes.c_void_p
     lib = native.runtime()
     cap = len(xrows.blob) + len(yrows.blob) + n * 256
-    return _run_message_writer(cap, lambda out, c: lib.oryx_assemble_als_updates(
-        users.handle, items.handle, u.ctypes.data_as(vp), i.ctypes.data_as(vp), xrows.blob,
-        xe.ctypes.data_as(vp), yrows.blob, ye.ctypes.data_as(vp), vx.ctypes.data_as(vp),
-        vy.ctypes.data_as(vp), n, int(bool(with_known)), out, c))
+    ends = np.empty(2 * n, dtype=np.int64)
+    n_msgs = ctypes.c_longlong(0)
+    while True:
+        out = _host_buffer(cap)
+        used = lib.oryx_assemble_als_updates(
+            users.handle, items.handle, u.ctypes.data_as(vp), i.ctypes.data_as(vp),
+            _buf_ptr(xrows.blob), xe.ctypes.data_as(vp), _buf_ptr(yrows.blob),
+            ye.ctypes.data_as(vp), vx.ctypes.data_as(vp), vy.ctypes.data_as(vp), n,
+            int(bool(with_known)), out.ctypes.data_as(vp), cap, ends.ctypes.data_as(vp),
+            ctypes.byref(n_msgs))
+        if used >= 0:
+            break
+        cap = -used + 1
+    return MessageBlock(out[:used], ends[:n_msgs.value].copy())
+
+
+def _host_buffer(n: int) -> np.ndarray:
+    """A uint8 host buffer; on a GPU host from torch's caching pinned allocator, whose blocks
+    are reused (already-faulted pages) once the previous holder is gone."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return torch.empty(int(n), dtype=torch.uint8, pin_memory=True).numpy()
+    except RuntimeError:
+        pass
+    return np.empty(int(n), dtype=np.uint8)
+
+
+def _buf_ptr(b) -> ctypes.c_void_p:
+    """Address of a bytes object or uint8 numpy array (kept alive by the caller)."""
+    if isinstance(b, np.ndarray):
+        return ctypes.c_void_p(b.ctypes.data)
+    return ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p)
 
 
 def _run_message_writer(cap: int, call) -> List[str]:

@@ -20,7 +20,7 @@ import threading
 import time
 from typing import Optional
 
-from ..api import Dataset, SpeedModelManager
+from ..api import Dataset, MessageBlock, SpeedModelManager
 from ..serving.layer import UpdateIterator
 from ..transport import log as tlog
 from ..transport.producer import LogTopicProducer
@@ -94,7 +94,9 @@ class SpeedLayer(AbstractLayer):
         sent = 0
         if len(records):
             updates = self._manager.build_updates(records)
-            if updates:
+            if isinstance(updates, MessageBlock):
+                self._producer.send_block("UP", updates)
+            elif updates:
                 self._producer.send_many(("UP", u) for u in updates)
                 sent = len(updates) if hasattr(updates, "__len__") else 0
             self._producer.flush()

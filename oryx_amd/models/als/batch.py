@@ -173,7 +173,7 @@ def write_features(path: str, ids: List[str], mat) -> None:
     pre-formatted :class:`~oryx_amd.ops.textfmt.RowText`."""
     os.makedirs(path, exist_ok=True)
     rows = mat if isinstance(mat, textfmt.RowText) else textfmt.format_rows(mat)
-    text = rows.blob.decode("ascii")
+    text = str(memoryview(rows.blob), "ascii")
     starts = [0] + rows.ends[:-1].tolist()
     data = "".join("[%s,%s]\n" % (json.dumps(id_), text[a:b])
                    for id_, a, b in zip(ids, starts, rows.ends.tolist())).encode("utf-8")

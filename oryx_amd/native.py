@@ -61,6 +61,9 @@ def _load_runtime():
     _sig(lib, "oryx_log_append_batch", c_ll, [c_vp, c_i, c_cp, c_ll, c_i, c_ll, c_i, c_vp])
     _sig(lib, "oryx_log_append_values", c_ll, [c_vp, c_i, c_cp, c_i, c_cp, c_vp, c_i, c_ll,
                                                 c_i])
+    # h, partition, key, key_len, blob, lens, n, gap, ts, fsync
+    _sig(lib, "oryx_log_append_values_gap", c_ll, [c_vp, c_i, c_cp, c_i, c_vp, c_vp, c_i, c_i,
+                                                    c_ll, c_i])
     _sig(lib, "oryx_log_begin_offset", c_ll, [c_vp, c_i])
     _sig(lib, "oryx_log_end_offset", c_ll, [c_vp, c_i])
     _sig(lib, "oryx_log_retain", c_i, [c_vp, c_ll])
@@ -98,9 +101,11 @@ def _register_runtime_extras(lib):
     # users, items, u, i, nx, ny, vx, vy, n, k, with_known, out, cap
     _sig(lib, "oryx_format_als_updates", c_ll, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                 c_ll, c_i, c_i, c_vp, c_ll])
-    # users, items, u, i, xtext, xends, ytext, yends, vx, vy, n, with_known, out, cap
-    _sig(lib, "oryx_assemble_als_updates", c_ll, [c_vp, c_vp, c_vp, c_vp, c_cp, c_vp, c_cp,
-                                                  c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_ll])
+    # users, items, u, i, xtext, xends, ytext, yends, vx, vy, n, with_known, out, cap,
+    # msg_ends, n_msgs
+    _sig(lib, "oryx_assemble_als_updates", c_ll, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                  c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_ll,
+                                                  c_vp, c_vp])
 
 
 def _runtime_sources():

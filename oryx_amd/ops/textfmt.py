@@ -26,14 +26,14 @@ __all__ = ["RowText", "format_rows"]
 
 @dataclass
 class RowText:
-    blob: bytes                 # ASCII, rows back to back
+    blob: object                # ASCII bytes or uint8 array, rows back to back
     ends: np.ndarray            # int64 [n]: end offset of row j
 
     def __len__(self) -> int:
         return len(self.ends)
 
     def rows(self) -> List[str]:
-        text = self.blob.decode("ascii")
+        text = str(memoryview(self.blob), "ascii")
         out, start = [], 0
         for e in self.ends.tolist():
             out.append(text[start:e])
@@ -46,7 +46,8 @@ class RowText:
         if len(idx) == 0:
             return RowText(b"", np.zeros(0, dtype=np.int64))
         starts = np.r_[0, self.ends[:-1]]
-        buf = np.frombuffer(self.blob, dtype=np.uint8)
+        buf = self.blob if isinstance(self.blob, np.ndarray) else \
+            np.frombuffer(self.blob, dtype=np.uint8)
         lens = self.ends[idx] - starts[idx]
         parts = [buf[s:s + l] for s, l in zip(starts[idx].tolist(), lens.tolist())]
         return RowText(np.concatenate(parts).tobytes(), np.cumsum(lens))
@@ -86,5 +87,7 @@ def _format_device(mat: torch.Tensor) -> RowText:
     native.check(lib.oryx_format_rows_text(m.data_ptr(), n, k, m.stride(0), ends.data_ptr(),
                                            lens.data_ptr(), out.data_ptr(), stream),
                  "oryx_format_rows_text")
-    blob = out.cpu().numpy().tobytes()
-    return RowText(blob, ends.cpu().numpy())
+    # pinned staging (torch's caching host allocator): one DMA, no page faults per call
+    host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    host.copy_(out)
+    return RowText(host.numpy(), ends.cpu().numpy())

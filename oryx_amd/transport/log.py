@@ -193,6 +193,33 @@ class Topic:
             raise IOError(_lib().oryx_log_last_error().decode())
         return res
 
+    def append_block(self, block, key: Optional[str] = None, partition: int = -1,
+                     timestamp_ms: int = -1, fsync: bool = False) -> int:
+        """Append every message of a :class:`~oryx_amd.api.MessageBlock` with one key, straight
+        from its buffer (no per-message Python strings)."""
+        n = len(block)
+        if n == 0:
+            return -1
+        if faults.armed():
+            return self.append_values(list(block), partition, timestamp_ms, fsync, key=key)
+        lens = np.ascontiguousarray(block.lengths(), dtype=np.int64)
+        buf = block.buf
+        if isinstance(buf, np.ndarray):
+            ptr = ctypes.c_void_p(buf.ctypes.data)
+        else:
+            ptr = ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p)
+        kb = _b(key)
+        res = _lib().oryx_log_append_values_gap(self._h, int(partition), kb,
+                                                -1 if kb is None else len(kb), ptr,
+                                                lens.ctypes.data_as(ctypes.c_void_p), n,
+                                                int(block.sep), int(timestamp_ms),
+                                                int(bool(fsync)))
+        if res == -2:
+            raise MessageTooLargeError(_lib().oryx_log_last_error().decode())
+        if res < 0:
+            raise IOError(_lib().oryx_log_last_error().decode())
+        return res
+
     def _append_corrupted(self, records, partition, timestamp_ms, fsync) -> int:
         p = partition if partition >= 0 else (0 if self.partitions == 1 else
                                               self.partition_for(records[0][0]))

@@ -96,6 +96,18 @@ class LogTopicProducer(TopicProducer):
                 self._flusher.start()
             self._lock.notify()
 
+    def send_block(self, key: Optional[str], block) -> None:
+        """Messages queued before are appended first, then the block in one native call."""
+        if len(block) == 0:
+            return
+        self._drain()
+        try:
+            self._get_topic().append_block(block, key=key)
+        except tlog.MessageTooLargeError:
+            # per-message size errors: the per-record path drops just the oversized ones
+            self.send_many((key, m) for m in block)
+            self._drain()
+
     def _drain(self) -> None:
         with self._lock:
             batch, self._buf = self._buf, []
