@@ -141,16 +141,39 @@ def cmd_config_props(config, out=sys.stdout) -> None:
     print(cfg.to_properties(config), file=out)
 
 
-def _relaunch_distributed(argv: List[str], gpus: int, max_restarts: int = 0) -> int:
+def _relaunch_distributed(argv: List[str], gpus: int, max_restarts: int = 0,
+                          min_gpus: int = 1) -> int:
     # a rank that fails (or is ended by the watchdog) makes the agent restart the whole group
-    # up to max_restarts times; the ALS trainer then resumes from its factor checkpoint
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-           "--nproc-per-node=%d" % gpus, "--max-restarts=%d" % max_restarts,
-           "--master-addr=127.0.0.1",
-           "--master-port=%s" % os.environ.get("ORYX_MASTER_PORT", "29551"),
-           "-m", "oryx_amd.cli"] + argv
+    # up to max_restarts times; the ALS trainer then resumes from its factor checkpoint.  A
+    # rank that loses its GPU ends the group instead, and the supervisor relaunches it on a
+    # smaller world of the healthy GPUs (parallel/elastic.py)
+    from .parallel import elastic
+
+    def build(world: int) -> List[str]:
+        return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                "--nproc-per-node=%d" % world, "--max-restarts=%d" % max_restarts,
+                "--master-addr=127.0.0.1",
+                "--master-port=%s" % os.environ.get("ORYX_MASTER_PORT", "29551"),
+                "-m", "oryx_amd.cli"] + _with_gpus(argv, world)
     env = dict(os.environ, ORYX_DISTRIBUTED_CHILD="1")
-    return subprocess.call(cmd, env=env)
+    return elastic.supervise(build, gpus, min_world=min_gpus, env=env)
+
+
+def _with_gpus(argv: List[str], world: int) -> List[str]:
+    """``argv`` with its ``--gpus`` value replaced by ``world``."""
+    out, skip = [], False
+    for j, a in enumerate(argv):
+        if skip:
+            skip = False
+            continue
+        if a == "--gpus":
+            out += ["--gpus", str(world)]
+            skip = True
+        elif a.startswith("--gpus="):
+            out.append("--gpus=%d" % world)
+        else:
+            out.append(a)
+    return out
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -187,16 +210,22 @@ def main(argv: Optional[List[str]] = None) -> int:
     if command == "batch":
         if args.gpus > 1 and not os.environ.get("ORYX_DISTRIBUTED_CHILD"):
             return _relaunch_distributed(
-                argv, args.gpus, cfg.get_optional_int(config, "oryx.gpu.max-restarts") or 0)
+                argv, args.gpus, cfg.get_optional_int(config, "oryx.gpu.max-restarts") or 0,
+                cfg.get_optional_int(config, "oryx.gpu.elastic.min-gpus") or 1)
         from .layers.batch import BatchLayer
-        from .parallel import dist
-        ctx = dist.init_from_env(device=config.get_string("oryx.gpu.device"))
-        layer = BatchLayer(config)
-        if ctx.is_main:
-            layer.start()
-            _wait_forever(layer)
-        else:
-            layer.run_follower()
+        from .parallel import dist, elastic
+        try:
+            ctx = dist.init_from_env(device=config.get_string("oryx.gpu.device"))
+            layer = BatchLayer(config)
+            if ctx.is_main:
+                layer.start()
+                _wait_forever(layer)
+            else:
+                layer.run_follower()
+        except Exception as e:
+            if os.environ.get("ORYX_DISTRIBUTED_CHILD") and elastic.is_device_failure(e):
+                elastic.report_device_lost(str(e))
+            raise
         return 0
     if command == "speed":
         from .layers.speed import SpeedLayer

@@ -355,8 +355,10 @@ class ALSUpdate(MLUpdate):
         y_ids = [item_ids[j] for j in used_i]
         ckpt_dir, fingerprint = None, ""
         if self.checkpoint_interval > 0 and self.current_model_dir:
+            # neither the world size nor the init seed: a checkpoint holds global factors, and
+            # a group relaunched on fewer GPUs (parallel/elastic.py) resumes from it
             fingerprint = _fingerprint(u, i, s, features, lam, alpha, self.implicit,
-                                       self.iterations, seed, ctx.world_size)
+                                       self.iterations)
             ckpt_dir = os.path.join(self.current_model_dir, ".checkpoint",
                                     "als-" + fingerprint[:16])
         x_init = y_init = None

@@ -150,8 +150,9 @@ class ALSSpeedModelManager(SpeedModelManager):
             raise ValueError("bad min-model-load-fraction")
         self.model: Optional[ALSSpeedModel] = None
         self._stream = None
-        # milliseconds per phase of the last build_updates (parse_aggregate, inverses,
-        # foldin = kernel + device->host copy, format)
+        # milliseconds per phase of the last build_updates (parse_aggregate, inverses, lookup
+        # of the batch's IDs in the stores, foldin = kernel + validity flags to the host,
+        # format_rows = GPU row text + copy, assemble = native UP message assembly)
         self.last_phase_ms = {}
 
     def consume(self, updates: Iterator[KeyMessage], context=None) -> None:
@@ -298,6 +299,8 @@ class ALSSpeedModelManager(SpeedModelManager):
                            count=len(users))
         irow = np.fromiter((yi_.get(key, -1) for key in items.keys()), dtype=np.int64,
                            count=len(items))
+        ph["lookup"] = (time.perf_counter() - t0) * 1e3
+        t0 = time.perf_counter()
         n = len(u)
         lib = native.require_kernels()
         stream = self._device_stream(dev)
@@ -328,9 +331,11 @@ class ALSSpeedModelManager(SpeedModelManager):
             # only the text crosses to the host
             xrows = textfmt.format_rows(new_x)
             yrows = textfmt.format_rows(new_y)
+        ph["format_rows"] = (time.perf_counter() - t0) * 1e3
+        t0 = time.perf_counter()
         out = ingest.assemble_als_updates(users, items, u, i, xrows, yrows, valid[:n] > 0,
                                           valid[n:] > 0, not self.no_known_items)
-        ph["format"] = (time.perf_counter() - t0) * 1e3
+        ph["assemble"] = (time.perf_counter() - t0) * 1e3
         return out
 
     def _to_update_json(self, matrix: str, id_: str, vec_json: str, other: str) -> str:

@@ -254,29 +254,32 @@ class ALSTrainer:
         return als_ops.to_split_bf16(x) if self.split else x.to(torch.bfloat16)
 
     # ------------------------------------------------------------------ checkpoints
+    # A checkpoint holds the FULL fp32 factors in global row order (not per-rank shards), so
+    # it does not depend on the world size: a group that shrinks after losing a GPU (see
+    # parallel/elastic.py) resumes from it with a different row sharding.
     def _layout(self, fingerprint: str, iteration: int) -> dict:
-        return {"iteration": int(iteration), "world_size": self.ctx.world_size,
+        return {"iteration": int(iteration), "format": "global-v1",
                 "n_users": self.n_users, "n_items": self.n_items, "k": self.k,
-                "kp": self.kp, "chunks": [self.lay_u.C, self.lay_i.C],
                 "fingerprint": str(fingerprint)}
 
     def save_checkpoint(self, directory: str, iteration: int, fingerprint: str = "") -> None:
-        """Write this rank's shards for ``iteration`` (collective: every rank calls it)."""
+        """Write the factors after ``iteration`` (collective: every rank calls it; rank 0
+        writes one safetensors file and then ``latest.json``, both atomically)."""
         from safetensors.torch import save_file
         ctx = self.ctx
-        it_dir = os.path.join(directory, "it%d" % iteration)
-        os.makedirs(it_dir, exist_ok=True)
-        path = os.path.join(it_dir, "rank%d.safetensors" % ctx.rank)
-        tmp = path + ".tmp"
-        save_file({"X": self.X.detach().cpu().contiguous(),
-                   "Y": self.Y.detach().cpu().contiguous()}, tmp,
-                  metadata={k: str(v) for k, v in self._layout(fingerprint, iteration).items()})
-        os.replace(tmp, path)
-        dist.barrier(ctx)
+        f = self.factors()
         if ctx.is_main:
+            it_dir = os.path.join(directory, "it%d" % iteration)
+            os.makedirs(it_dir, exist_ok=True)
+            path = os.path.join(it_dir, "factors.safetensors")
+            save_file({"X": f.X.detach().cpu().contiguous(),
+                       "Y": f.Y.detach().cpu().contiguous()}, path + ".tmp",
+                      metadata={k: str(v) for k, v in
+                                self._layout(fingerprint, iteration).items()})
+            os.replace(path + ".tmp", path)
             meta = os.path.join(directory, "latest.json")
-            with open(meta + ".tmp", "w") as f:
-                json.dump(self._layout(fingerprint, iteration), f)
+            with open(meta + ".tmp", "w") as fh:
+                json.dump(self._layout(fingerprint, iteration), fh)
             os.replace(meta + ".tmp", meta)
             for name in os.listdir(directory):
                 if name.startswith("it") and name != "it%d" % iteration:
@@ -284,18 +287,19 @@ class ALSTrainer:
         dist.barrier(ctx)
 
     def load_checkpoint(self, directory: str, fingerprint: str = "") -> int:
-        """Restore the latest complete checkpoint if it matches this run; returns the
-        iteration it was taken after, or 0 (collective; every rank gets the same answer)."""
+        """Restore the latest complete checkpoint if it matches this run (any world size);
+        returns the iteration it was taken after, or 0 (collective; every rank gets the same
+        answer and takes its own rows of the global factors)."""
         ctx = self.ctx
         iteration = 0
         if ctx.is_main:
             try:
-                with open(os.path.join(directory, "latest.json")) as f:
-                    meta = json.load(f)
+                with open(os.path.join(directory, "latest.json")) as fh:
+                    meta = json.load(fh)
                 want = self._layout(fingerprint, meta.get("iteration", 0))
-                it_dir = os.path.join(directory, "it%d" % int(meta["iteration"]))
-                if meta == want and all(os.path.exists(os.path.join(
-                        it_dir, "rank%d.safetensors" % r)) for r in range(ctx.world_size)):
+                path = os.path.join(directory, "it%d" % int(meta["iteration"]),
+                                    "factors.safetensors")
+                if meta == want and os.path.exists(path):
                     iteration = int(meta["iteration"])
                 else:
                     log.info("Ignoring checkpoint in %s: layout or data differ", directory)
@@ -304,17 +308,25 @@ class ALSTrainer:
         iteration = int(dist.broadcast_object(iteration, ctx))
         if iteration <= 0:
             return 0
-        from safetensors.torch import load_file
-        t = load_file(os.path.join(directory, "it%d" % iteration,
-                                   "rank%d.safetensors" % ctx.rank))
-        if tuple(t["X"].shape) != (self.lay_u.local_rows, self.kp) or \
-                tuple(t["Y"].shape) != (self.lay_i.local_rows, self.kp):
-            raise ValueError("checkpoint shard shapes do not match the trainer")
-        self.X = t["X"].to(self.device)
-        self.Y = t["Y"].to(self.device)
+        from safetensors import safe_open
+        path = os.path.join(directory, "it%d" % iteration, "factors.safetensors")
+        with safe_open(path, framework="pt") as fh:
+            xs, ys = fh.get_slice("X"), fh.get_slice("Y")
+            if tuple(xs.get_shape()) != (self.n_users, self.k) or \
+                    tuple(ys.get_shape()) != (self.n_items, self.k):
+                raise ValueError("checkpoint factor shapes do not match the trainer")
+            xr = xs[self.u_lo:self.u_hi]
+            yr = ys[self.i_lo:self.i_hi]
+        X = torch.zeros((self.lay_u.local_rows, self.kp), dtype=torch.float32)
+        Y = torch.zeros((self.lay_i.local_rows, self.kp), dtype=torch.float32)
+        X[:xr.shape[0], :self.k] = xr
+        Y[:yr.shape[0], :self.k] = yr
+        self.X = X.to(self.device)
+        self.Y = Y.to(self.device)
         self._publish_factors()
         self.iterations_done = iteration
-        log.info("Resumed ALS from %s after iteration %d", directory, iteration)
+        log.info("Resumed ALS from %s after iteration %d (world size %d)", directory,
+                 iteration, ctx.world_size)
         return iteration
 
     # ------------------------------------------------------------------ iterations

@@ -6,6 +6,8 @@ point fires when its conditions match the call's attributes:
 * ``raise``   -- raise :class:`InjectedFault` (a crashed update / rank),
 * ``exit``    -- ``os._exit(code)`` with no cleanup (a killed rank; default code 43),
 * ``hang``    -- sleep ``seconds`` (a stuck collective / kernel; exercises the watchdog),
+* ``device_lost`` -- the rank's GPU is reported lost and the rank leaves the group (exit 87;
+  the shrink-world supervisor of ``parallel/elastic.py`` relaunches on fewer GPUs),
 * anything else (``corrupt``, ``drop``, ...) is returned to the call site, which applies it
   to the data it is handling (e.g. the log writer corrupts or drops a record).
 
@@ -132,6 +134,8 @@ def point(name: str, **attrs) -> Optional[str]:
     # restart attempt of an elastic (torch.distributed.run) group, so a spec can fire on the
     # first attempt only: "...@restart=0"
     attrs.setdefault("restart", os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+    # and of the shrink-world supervisor (parallel/elastic.py): "...@attempt=0"
+    attrs.setdefault("attempt", os.environ.get("ORYX_ELASTIC_ATTEMPT", "0"))
     hit = None
     with _lock:
         for f in _faults:
@@ -151,4 +155,7 @@ def point(name: str, **attrs) -> Optional[str]:
     if hit.action == "hang":
         time.sleep(hit.seconds)
         return None
+    if hit.action == "device_lost":
+        from ..parallel import elastic
+        elastic.report_device_lost("injected at %s %s" % (name, attrs))
     return hit.action

@@ -216,3 +216,81 @@ def test_elastic_restart_resumes_from_checkpoint(tmp_path):
     assert json.loads((clean / "resumed.json").read_text())["resumed_from"] == 0
     np.testing.assert_array_equal(np.load(faulty / "X.npy"), np.load(clean / "X.npy"))
     np.testing.assert_array_equal(np.load(faulty / "Y.npy"), np.load(clean / "Y.npy"))
+
+
+def test_next_world_and_device_failure_classification():
+    from oryx_amd.parallel import elastic
+    assert elastic.next_world(7, 8) == 4
+    assert elastic.next_world(3, 4) == 2
+    assert elastic.next_world(1, 2) == 1
+    assert elastic.next_world(0, 2) == 0
+    assert elastic.next_world(5, 8, min_world=8) == 0
+    assert elastic.is_device_failure(RuntimeError("HIP error: hipErrorLaunchFailure"))
+    assert not elastic.is_device_failure(ValueError("bad input"))
+
+
+SHRINK = r"""
+import json, os, sys
+sys.path.insert(0, ROOT)
+import numpy as np, torch
+from oryx_amd.models.als.trainer import ALSTrainer
+from oryx_amd.parallel import dist
+out_dir = sys.argv[1]
+ctx = dist.init_from_env(device="cpu")
+g = np.random.default_rng(0)
+key = g.choice(80 * 50, 1200, replace=False)
+u, i = key // 50, key % 50
+s = g.integers(1, 6, len(key)).astype(np.float32)
+part = slice(ctx.rank, None, ctx.world_size)
+t = ALSTrainer(5, 0.01, 1.0, True, ctx=ctx, seed=3)
+t.prepare(torch.from_numpy(u[part]), torch.from_numpy(i[part]), torch.from_numpy(s[part]), 80, 50)
+f = t.train(6, checkpoint_dir=os.path.join(out_dir, "ckpt"), checkpoint_interval=2,
+            fingerprint="shrink")
+if ctx.is_main:
+    np.save(os.path.join(out_dir, "X.npy"), f.X.numpy())
+    np.save(os.path.join(out_dir, "Y.npy"), f.Y.numpy())
+    with open(os.path.join(out_dir, "resumed.json"), "w") as fh:
+        json.dump({"resumed_from": t.resumed_from, "world": ctx.world_size,
+                   "attempt": os.environ.get("ORYX_ELASTIC_ATTEMPT")}, fh)
+"""
+
+
+def test_shrink_world_after_device_loss_resumes_from_checkpoint(tmp_path):
+    """Rank 3 of a 4-rank gloo group loses its 'GPU' (device_lost fault) in iteration 3: the
+    supervisor drops that device, relaunches the group on 2 ranks (the largest power of two
+    below 4 that the 3 healthy devices allow), and the trainer resumes from the world-size
+    independent iteration-2 checkpoint; the factors match an uninterrupted 4-rank run up to
+    the summation order of the last iterations."""
+    from oryx_amd.parallel import elastic
+    script = tmp_path / "run.py"
+    script.write_text(SHRINK.replace("ROOT", repr(ROOT)))
+    runs = {}
+    for name, faults_spec, port in (("clean", "", 29671),
+                                    ("faulty", "als.iteration:device_lost@iteration=3,rank=3,"
+                                               "attempt=0", 29673)):
+        out = tmp_path / name
+        out.mkdir()
+
+        def build(world, out=out, port=port):
+            return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                    "--nproc-per-node=%d" % world, "--max-restarts=0",
+                    "--master-addr=127.0.0.1", "--master-port=%d" % port, str(script),
+                    str(out)]
+        env = dict(os.environ, OMP_NUM_THREADS="1", ORYX_FAULTS=faults_spec)
+        rc = elastic.supervise(build, 4, env=env)
+        assert rc == 0, name
+        runs[name] = out
+    info = json.loads((runs["faulty"] / "resumed.json").read_text())
+    assert info == {"resumed_from": 2, "world": 2, "attempt": "1"}
+    # iterations 3-6 ran on 2 ranks instead of 4: same math, different fp32 summation order
+    for m in ("X.npy", "Y.npy"):
+        a, b = np.load(runs["faulty"] / m), np.load(runs["clean"] / m)
+        assert np.linalg.norm(a - b) / np.linalg.norm(b) < 2e-3, m
+        np.testing.assert_allclose(a, b, atol=5e-3)
+
+
+def test_cli_relaunch_rewrites_gpus():
+    from oryx_amd import cli
+    assert cli._with_gpus(["batch", "--gpus", "8", "--conf", "x"], 4) == \
+        ["batch", "--gpus", "4", "--conf", "x"]
+    assert cli._with_gpus(["batch", "--gpus=8"], 2) == ["batch", "--gpus=2"]
