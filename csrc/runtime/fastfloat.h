@@ -363,6 +363,62 @@ inline bool parse_float(const char* b, const char* e, float& out) {
   return r.ec == std::errc() && r.ptr == e;
 }
 
+// Parses [b, e) as a double: exact fast path for <= 19 significant digits, a mantissa that
+// fits 53 bits and |exp10| <= 22 (one correctly rounded operation), else std::from_chars.
+// Leading '+' and spaces are accepted (CSV strengths / timestamps).
+inline bool parse_double(const char* b, const char* e, double& out) {
+  static const double kP10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                  1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                  1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  while (b < e && (*b == ' ' || *b == '+')) ++b;
+  const char* p = b;
+  bool neg = false;
+  if (p < e && *p == '-') {
+    neg = true;
+    ++p;
+  }
+  uint64_t D = 0;
+  int nd = 0, exp10 = 0;
+  bool any = false, slow = false;
+  for (; p < e && (unsigned)(*p - '0') < 10u; ++p) {
+    any = true;
+    const unsigned dgt = (unsigned)(*p - '0');
+    if (D == 0 && dgt == 0) continue;
+    if (nd < 19) { D = D * 10 + dgt; ++nd; } else { ++exp10; if (dgt) slow = true; }
+  }
+  if (p < e && *p == '.') {
+    ++p;
+    for (; p < e && (unsigned)(*p - '0') < 10u; ++p) {
+      any = true;
+      const unsigned dgt = (unsigned)(*p - '0');
+      if (D == 0 && dgt == 0) { --exp10; continue; }
+      if (nd < 19) { D = D * 10 + dgt; ++nd; --exp10; } else if (dgt) slow = true;
+    }
+  }
+  if (!any) slow = true;
+  if (!slow && p < e && (*p == 'e' || *p == 'E')) {
+    ++p;
+    bool eneg = false;
+    if (p < e && (*p == '-' || *p == '+')) eneg = *p++ == '-';
+    if (p >= e || (unsigned)(*p - '0') >= 10u) {
+      slow = true;
+    } else {
+      int x = 0;
+      for (; p < e && (unsigned)(*p - '0') < 10u; ++p)
+        if (x < 100000) x = x * 10 + (*p - '0');
+      exp10 += eneg ? -x : x;
+    }
+  }
+  if (!slow && p == e && D <= (1ull << 53) && exp10 >= -22 && exp10 <= 22) {
+    double x = (double)D;
+    x = exp10 < 0 ? x / kP10[-exp10] : x * kP10[exp10];
+    out = neg ? -x : x;
+    return true;
+  }
+  auto r = std::from_chars(b, e, out);
+  return r.ec == std::errc() && r.ptr == e;
+}
+
 // Threads for the bulk text loops: ORYX_NATIVE_THREADS, else the hardware threads, at most 16.
 inline int native_threads() {
   static const int n = [] {

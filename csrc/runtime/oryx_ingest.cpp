@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <deque>
 #include <limits>
 #include <mutex>
 #include <string>
@@ -24,15 +25,17 @@
 namespace {
 
 struct Dict {
-  std::unordered_map<std::string, int64_t> map;
-  std::vector<std::string> keys;
+  // the map's keys are views of the strings in `keys` (a deque: elements never move), so a
+  // lookup needs no std::string
+  std::unordered_map<std::string_view, int64_t> map;
+  std::deque<std::string> keys;
   std::mutex mu;
   int64_t encode(std::string_view s) {
-    auto it = map.find(std::string(s));
+    auto it = map.find(s);
     if (it != map.end()) return it->second;
     int64_t code = (int64_t)keys.size();
     keys.emplace_back(s);
-    map.emplace(keys.back(), code);
+    map.emplace(std::string_view(keys.back()), code);
     return code;
   }
 };
@@ -130,7 +133,7 @@ long long oryx_dict_encode(void* dh, const char* buf, long long buf_len, int n, 
 long long oryx_dict_get(void* dh, const char* s, long long len) {
   Dict* d = static_cast<Dict*>(dh);
   std::lock_guard<std::mutex> g(d->mu);
-  auto it = d->map.find(std::string(s, (size_t)len));
+  auto it = d->map.find(std::string_view(s, (size_t)len));
   return it == d->map.end() ? -1 : it->second;
 }
 
@@ -144,10 +147,211 @@ long long oryx_dict_key(void* dh, long long code, char* out, long long cap) {
   return (long long)k.size();
 }
 
+}  // extern "C"
+
+namespace {
+
+// Open-addressing string -> int32 index for the parse hot loop (std::unordered_map costs a
+// node and a key indirection per lookup: two cache misses once the IDs number 1e5).  Keys of
+// up to 16 bytes are stored inline, longer ones as views (into the input buffer or owned
+// storage); the full 64-bit hash is compared first.
+class FlatIndex {
+ public:
+  FlatIndex() { rehash(1024); }
+  // value of key k, or -1
+  int32_t find(std::string_view k) const {
+    const uint64_t h = hash(k.data(), k.size());
+    const size_t m = slots_.size() - 1;
+    for (size_t j = (size_t)h & m;; j = (j + 1) & m) {
+      const Slot& sl = slots_[j];
+      if (sl.code < 0) return -1;
+      if (sl.h == h && sl.len == k.size() &&
+          std::memcmp(k.size() <= 16 ? sl.in : sl.ptr, k.data(), k.size()) == 0)
+        return sl.code;
+    }
+  }
+  // index of key k, inserting it with value `next` when absent (*inserted set)
+  int32_t find_or_add(std::string_view k, int32_t next, bool* inserted) {
+    const uint64_t h = hash(k.data(), k.size());
+    size_t m = slots_.size() - 1, j = (size_t)h & m;
+    while (true) {
+      Slot& sl = slots_[j];
+      if (sl.code < 0) {
+        if ((used_ + 1) * 2 > slots_.size()) {
+          rehash(slots_.size() * 2);
+          return find_or_add(k, next, inserted);
+        }
+        sl.h = h;
+        sl.len = (uint32_t)k.size();
+        sl.code = next;
+        if (k.size() <= 16) std::memcpy(sl.in, k.data(), k.size());
+        else sl.ptr = k.data();
+        ++used_;
+        *inserted = true;
+        return next;
+      }
+      if (sl.h == h && sl.len == k.size() &&
+          std::memcmp(k.size() <= 16 ? sl.in : sl.ptr, k.data(), k.size()) == 0) {
+        *inserted = false;
+        return sl.code;
+      }
+      j = (j + 1) & m;
+    }
+  }
+
+ private:
+  struct Slot {
+    uint64_t h = 0;
+    uint32_t len = 0;
+    int32_t code = -1;
+    union {
+      char in[16];
+      const char* ptr;
+    };
+    Slot() : in{} {}
+  };
+  static uint64_t mix(uint64_t a, uint64_t b) {
+    const unsigned __int128 r = (unsigned __int128)a * b;
+    return (uint64_t)r ^ (uint64_t)(r >> 64);
+  }
+  static uint64_t hash(const char* p, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    while (n >= 8) {
+      uint64_t v;
+      std::memcpy(&v, p, 8);
+      h = mix(h ^ v, 0xA0761D6478BD642Full);
+      p += 8;
+      n -= 8;
+    }
+    uint64_t v = 0;
+    std::memcpy(&v, p, n);
+    return mix(h ^ v, 0xE7037ED1A0B428DBull);
+  }
+  void rehash(size_t cap) {
+    std::vector<Slot> old;
+    old.swap(slots_);
+    slots_.assign(cap, Slot());
+    used_ = 0;
+    const size_t m = cap - 1;
+    for (const Slot& sl : old) {
+      if (sl.code < 0) continue;
+      size_t j = (size_t)sl.h & m;
+      while (slots_[j].code >= 0) j = (j + 1) & m;
+      slots_[j] = sl;
+      ++used_;
+    }
+  }
+  std::vector<Slot> slots_;
+  size_t used_ = 0;
+};
+
+// One chunk of rating lines parsed by one thread: IDs get chunk-local codes (first-appearance
+// order) from chunk-local maps of views; the caller merges the local dictionaries into the
+// global ones in chunk order, which reproduces the global first-appearance numbering.
+struct RatingChunk {
+  std::vector<int32_t> u, i;
+  std::vector<double> s;
+  std::vector<long long> ts;
+  FlatIndex umap, imap;
+  std::vector<std::string_view> ukeys, ikeys;
+  std::deque<std::string> owned;     // unescaped fields (quoted CSV / JSON lines)
+  long long lines = 0, bad_line = -1;
+
+  int32_t code(FlatIndex& m, std::vector<std::string_view>& keys, std::string_view k,
+               bool stable) {
+    if (!stable) {
+      // an unescaped token lives in a per-line buffer: index a stable copy, made only for a
+      // key not seen before
+      const int32_t c = m.find(k);
+      if (c >= 0) return c;
+      owned.emplace_back(k);
+      k = owned.back();
+    }
+    bool inserted;
+    const int32_t c = m.find_or_add(k, (int32_t)keys.size(), &inserted);
+    if (inserted) keys.push_back(k);
+    return c;
+  }
+
+  void parse(const char* p, const char* end, long long default_ts, bool strict) {
+    std::vector<std::string> toks;
+    std::string field;
+    std::string_view f[4];
+    while (p < end) {
+      const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
+      const char* le = nl ? nl : end;
+      const char* lend = le;
+      if (lend > p && lend[-1] == '\r') --lend;
+      if (lend > p) {
+        int nf = 0;
+        bool ok, stable;
+        double sv = 1.0;
+        long long tv = default_ts;
+        // fast path: plain CSV (no quotes / escapes): fields are views of the line
+        if (*p != '[' && !memchr(p, '"', (size_t)(lend - p)) &&
+            !memchr(p, '\\', (size_t)(lend - p))) {
+          const char* q = p;
+          while (nf < 4) {
+            const char* c = static_cast<const char*>(memchr(q, ',', (size_t)(lend - q)));
+            const char* fe = c ? c : lend;
+            f[nf++] = std::string_view(q, (size_t)(fe - q));
+            if (!c) break;
+            q = c + 1;
+          }
+          stable = true;
+        } else {
+          toks.clear();
+          if (*p == '[' && lend[-1] == ']') {
+            if (!json_fields(p, lend, toks)) toks.clear();
+          } else {
+            const char* q = p;
+            while (true) {
+              q = csv_field(q, lend, field);
+              toks.push_back(field);
+              if (q >= lend) break;
+              ++q;
+              if (q >= lend) { toks.emplace_back(); break; }
+            }
+          }
+          for (size_t t = 0; t < toks.size() && nf < 4; ++t) f[nf++] = toks[t];
+          stable = false;
+        }
+        ok = nf >= 2;
+        if (ok && nf >= 3) {
+          if (f[2].empty()) sv = std::numeric_limits<double>::quiet_NaN();
+          else ok = oryx_ff::parse_double(f[2].data(), f[2].data() + f[2].size(), sv);
+        }
+        if (ok && nf >= 4 && !f[3].empty()) {
+          double t;
+          ok = oryx_ff::parse_double(f[3].data(), f[3].data() + f[3].size(), t);
+          tv = (long long)t;
+        }
+        if (ok) {
+          u.push_back(code(umap, ukeys, f[0], stable));
+          i.push_back(code(imap, ikeys, f[1], stable));
+          s.push_back(sv);
+          ts.push_back(tv);
+        } else if (strict && bad_line < 0) {
+          bad_line = lines;
+          return;
+        }
+      }
+      ++lines;
+      p = nl ? nl + 1 : end;
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" {
+
 // Parses newline-separated rating lines.  users/items: dictionaries; outputs per parsed row:
 // user code, item code, strength (NaN when the field is empty = delete; 1 when missing),
 // timestamp (default_ts when missing).  Returns rows parsed, or -(line number + 1) of the
-// first malformed line when strict.
+// first malformed line when strict.  Large inputs are split at line boundaries over the
+// native threads (per-chunk dictionaries merged in chunk order: the codes are the same as a
+// sequential pass would give).
 long long oryx_parse_ratings(const char* buf, long long len, void* users, void* items,
                              long long* out_u, long long* out_i, double* out_s,
                              long long* out_ts, long long max_rows, long long default_ts,
@@ -157,56 +361,54 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
   std::lock_guard<std::mutex> gu(du->mu);
   std::unique_lock<std::mutex> gi(di->mu, std::defer_lock);
   if (di != du) gi.lock();
-  const char* p = buf;
-  const char* end = buf + len;
-  long long rows = 0, line_no = 0;
-  std::vector<std::string> toks;
-  std::string field;
-  while (p < end && rows < max_rows) {
-    const char* nl = static_cast<const char*>(memchr(p, '\n', end - p));
-    const char* le = nl ? nl : end;
-    const char* lend = le;
-    if (lend > p && lend[-1] == '\r') --lend;
-    if (lend > p) {
-      toks.clear();
-      if (*p == '[' && lend[-1] == ']') {
-        if (!json_fields(p, lend, toks)) toks.clear();
-      } else {
-        const char* q = p;
-        while (true) {
-          q = csv_field(q, lend, field);
-          toks.push_back(field);
-          if (q >= lend) break;
-          ++q;  // comma
-          if (q >= lend) { toks.emplace_back(); break; }
-        }
-      }
-      bool ok = toks.size() >= 2;
-      double s = 1.0;
-      long long ts = default_ts;
-      if (ok && toks.size() >= 3) {
-        if (toks[2].empty()) s = std::numeric_limits<double>::quiet_NaN();
-        else ok = parse_double(toks[2], &s);
-      }
-      if (ok && toks.size() >= 4 && !toks[3].empty()) {
-        double t;
-        ok = parse_double(toks[3], &t);
-        ts = (long long)t;
-      }
-      if (ok) {
-        out_u[rows] = du->encode(toks[0]);
-        out_i[rows] = di->encode(toks[1]);
-        out_s[rows] = s;
-        out_ts[rows] = ts;
-        ++rows;
-      } else if (strict) {
-        return -(line_no + 1);
+  // chunk boundaries at newlines
+  int P = len >= (8ll << 20) ? oryx_ff::native_threads() : 1;
+  std::vector<const char*> cut((size_t)P + 1);
+  cut[0] = buf;
+  cut[(size_t)P] = buf + len;
+  for (int t = 1; t < P; ++t) {
+    const char* c = buf + len * t / P;
+    if (c < cut[(size_t)t - 1]) c = cut[(size_t)t - 1];
+    const char* nl = static_cast<const char*>(memchr(c, '\n', (size_t)(buf + len - c)));
+    cut[(size_t)t] = nl ? nl + 1 : buf + len;
+  }
+  std::vector<RatingChunk> ch((size_t)P);
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t)
+      ch[(size_t)t].parse(cut[(size_t)t], cut[(size_t)t + 1], default_ts, strict != 0);
+  });
+  // strict: the first malformed line in input order
+  long long lines_before = 0;
+  for (int t = 0; t < P; ++t) {
+    if (ch[(size_t)t].bad_line >= 0) return -(lines_before + ch[(size_t)t].bad_line + 1);
+    lines_before += ch[(size_t)t].lines;
+  }
+  // merge the chunk dictionaries in order, then write the rows at their offsets
+  std::vector<std::vector<int64_t>> umap((size_t)P), imap((size_t)P);
+  std::vector<long long> off((size_t)P + 1, 0);
+  for (int t = 0; t < P; ++t) {
+    RatingChunk& c = ch[(size_t)t];
+    umap[(size_t)t].reserve(c.ukeys.size());
+    for (auto k : c.ukeys) umap[(size_t)t].push_back(du->encode(k));
+    imap[(size_t)t].reserve(c.ikeys.size());
+    for (auto k : c.ikeys) imap[(size_t)t].push_back(di->encode(k));
+    off[(size_t)t + 1] = off[(size_t)t] + (long long)c.u.size();
+  }
+  const long long total = off[(size_t)P] < max_rows ? off[(size_t)P] : max_rows;
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      const RatingChunk& c = ch[(size_t)t];
+      const long long o = off[(size_t)t];
+      const long long n = (long long)c.u.size();
+      for (long long r = 0; r < n && o + r < total; ++r) {
+        out_u[o + r] = umap[(size_t)t][(size_t)c.u[(size_t)r]];
+        out_i[o + r] = imap[(size_t)t][(size_t)c.i[(size_t)r]];
+        out_s[o + r] = c.s[(size_t)r];
+        out_ts[o + r] = c.ts[(size_t)r];
       }
     }
-    ++line_no;
-    p = nl ? nl + 1 : end;
-  }
-  return rows;
+  });
+  return total;
 }
 
 // Formats rows of a float matrix as JSON arrays "[v0,v1,...]" with shortest round-trip

@@ -477,3 +477,41 @@ def test_kernel_abi_version_matches_source():
     src = open(os.path.join(_build.CSRC, "kernels", "als.hip")).read()
     m = re.search(r"int oryx_kernels_version\(\) \{ return (\d+); \}", src)
     assert m and int(m.group(1)) == native.KERNELS_ABI_VERSION
+
+
+def test_parallel_ratings_parse_matches_sequential():
+    """Inputs of >= 8 MB are parsed by several native threads with chunk-local dictionaries
+    merged in order: codes, values and the strict-mode error line match a one-chunk parse."""
+    import numpy as np
+    from oryx_amd import ingest
+    g = np.random.default_rng(5)
+    n = 450_000
+    u = g.integers(0, 30000, n)
+    i = g.integers(0, 9000, n)
+    lines = []
+    for j in range(n):
+        r = j % 97
+        if r == 0:
+            lines.append('["u%d","i%d",2.5,%d]' % (u[j], i[j], j))
+        elif r == 1:
+            lines.append('"u%d","i,%d",,%d' % (u[j], i[j], j))
+        elif r == 2:
+            lines.append("u%d,i%d" % (u[j], i[j]))
+        else:
+            lines.append("u%d,i%d,%d.5,%d" % (u[j], i[j], j % 7, j))
+    blob = ("\n".join(lines)).encode()
+    assert len(blob) >= 8 << 20
+    big = ingest.IdDict(), ingest.IdDict()
+    out_big = ingest.parse_ratings(blob, big[0], big[1], default_ts=-1)
+    # the same lines in small pieces (each below the threading threshold), one dictionary
+    small = ingest.IdDict(), ingest.IdDict()
+    parts = [ingest.parse_ratings(lines[a:a + 100000], small[0], small[1], default_ts=-1)
+             for a in range(0, n, 100000)]
+    for k in range(4):
+        np.testing.assert_array_equal(out_big[k], np.concatenate([p[k] for p in parts]))
+    assert big[0].keys() == small[0].keys() and big[1].keys() == small[1].keys()
+    bad = list(lines)
+    bad[400_000] = "only-one-field"
+    with pytest.raises(ValueError, match="line 400000"):
+        ingest.parse_ratings(("\n".join(bad)).encode(), ingest.IdDict(), ingest.IdDict(),
+                             default_ts=0, strict=True)
