@@ -235,7 +235,9 @@ __global__ __launch_bounds__(256) void rdf_histogram_pieces(
     const long long* __restrict__ piece_hi, int nodes, const int* __restrict__ feats, int Fs,
     int B, float* __restrict__ hist, const int* __restrict__ n_live) {
   extern __shared__ float lh[];
-  const int pc = blockIdx.x;
+  // device pieces (n_live set) come sorted by their first row: the XCD-aware order puts the
+  // pieces of different trees over the same rows on one XCD, so those rows come from its L2
+  const int pc = n_live ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   if (n_live && pc >= *n_live) return;     // grid sized by an upper bound (device pieces)
   const int t = piece_tree[pc];
   const int node = piece_node[pc];
@@ -317,7 +319,9 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
     const long long* __restrict__ piece_hi, int nodes, const int* __restrict__ feats, int Fs,
     int B, float* __restrict__ hist, int NDW, int RSW, const int* __restrict__ n_live) {
   extern __shared__ __attribute__((aligned(16))) float lsm[];
-  if (n_live && (int)blockIdx.x >= *n_live) return;   // grid sized by an upper bound
+  // see rdf_histogram_pieces: sorted device pieces in XCD-aware order
+  const int pc = n_live ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  if (n_live && pc >= *n_live) return;   // grid sized by an upper bound
   const int per_node = Fs * B * S;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float* lh = lsm;                                                        // [per_node]
@@ -325,7 +329,7 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
   unsigned int* rows = reinterpret_cast<unsigned int*>(lsm + per_node + ((Fs + 3) & ~3)) +
                        wave * 64 * RSW;
   const unsigned char* rowb = reinterpret_cast<const unsigned char*>(rows);
-  const int pc = blockIdx.x;
+  // (pc: see above)
   const int t = piece_tree[pc];
   const int node = piece_node[pc];
   float* gh = hist + ((long long)t * nodes + node) * per_node;

@@ -462,7 +462,7 @@ def _route(data: BinnedData, node_of, nodes, split: LevelSplits, child_base, B,
 
 # ---------------------------------------------------------------- training
 
-@dataclass
+@dataclass(slots=True)
 class TrainedNode:
     id: str
     count: int = 0                  # unweighted training examples reaching the node
@@ -701,31 +701,36 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
     def build(lv) -> None:
         nonlocal level_nodes
         lv["event"].synchronize()
-        feat_h = lv["feat"].numpy()
-        bin_h = lv["bin"].numpy()
         tot_h = lv["tot"].numpy().copy()
-        vis_h = lv["vis"].numpy()
-        cat_h = lv["cat"].numpy() if lv["cat"] is not None else None
         if y_shift:
             w_, s1 = tot_h[..., 0].copy(), tot_h[..., 1].copy()
             tot_h[..., 2] += 2.0 * y_shift * s1 + y_shift * y_shift * w_
             tot_h[..., 1] += y_shift * w_
+        # Python lists (scalar access on numpy arrays costs more than the node itself)
+        feat_l = lv["feat"].numpy().tolist()
+        bin_l = lv["bin"].numpy().tolist()
+        vis_l = lv["vis"].numpy().tolist()
+        cat_h = lv["cat"].numpy() if lv["cat"] is not None else None
+        np.add.at(predictor_counts, lv["feat"].numpy()[lv["feat"].numpy() >= 0],
+                  lv["vis"].numpy()[lv["feat"].numpy() >= 0])
         new_level: List[List[Optional[TrainedNode]]] = []
         for t in range(T):
             row: List[Optional[TrainedNode]] = []
+            ft, bt, vt, st = feat_l[t], bin_l[t], vis_l[t], tot_h[t]
             for slot, node in enumerate(level_nodes[t]):
-                node.count = int(vis_h[t, slot])
-                node.stats = tot_h[t, slot]
-                f = int(feat_h[t, slot])
+                node.count = vt[slot]
+                node.stats = st[slot]
+                f = ft[slot]
                 if f >= 0:
                     node.feature = f
-                    node.bin = int(bin_h[t, slot])
+                    node.bin = bt[slot]
                     if node.bin < 0:
                         node.cat_left = np.nonzero(cat_h[t, slot])[0]
-                    node.left = TrainedNode(node.id + "-")
-                    node.right = TrainedNode(node.id + "+")
-                    row.extend([node.left, node.right])
-                    predictor_counts[f] += node.count
+                    nid = node.id
+                    node.left = left = TrainedNode(nid + "-")
+                    node.right = right = TrainedNode(nid + "+")
+                    row.append(left)
+                    row.append(right)
             new_level.append(row)
         level_nodes = new_level
 
@@ -754,6 +759,16 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
                 counts.data_ptr(), T, W, lo, hi, _PIECE, max_pieces, ptree.data_ptr(),
                 pnode.data_ptr(), pbeg.data_ptr(), pend.data_ptr(), n_live.data_ptr(), stream),
                 "oryx_rdf_expand_pieces")
+            # pieces in order of their first row (trees interleaved): the workgroups that run
+            # together read the same rows, which then come from L2 / MALL instead of HBM
+            live = torch.arange(max_pieces, device=dev) < n_live
+            first = pbeg.clamp(0, T * n - 1)
+            row0 = (perm[first].long() if perm is not None else first) % n
+            key = torch.where(live, row0 * T + ptree.long().clamp(0, T - 1),
+                              torch.full_like(row0, 1 << 62))
+            order = torch.argsort(key)
+            ptree, pnode = ptree[order].contiguous(), pnode[order].contiguous()
+            pbeg, pend = pbeg[order].contiguous(), pend[order].contiguous()
             fe = feats[:, lo:hi].contiguous()
             native.check(lib.oryx_rdf_histogram_pieces(
                 data.Xb.data_ptr(), data.bin_bytes, n, P,
