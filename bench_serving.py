@@ -261,6 +261,10 @@ def main(argv=None) -> int:
     ap.add_argument("--sweep", action="store_true",
                     help="every published row: features 50/250 x items 1/5/20M x sample rate "
                          "0.3/1.0 at each --workers count (one JSON line each)")
+    ap.add_argument("--sweep-features", default="50,250",
+                    help="--sweep: the feature counts to cover (comma list)")
+    ap.add_argument("--sweep-items", default="1000000,5000000,20000000",
+                    help="--sweep: the item counts to cover (comma list)")
     ap.add_argument("--max-batch", type=int, default=16)
     ap.add_argument("--time-to-ready", action="store_true",
                     help="measure the model load through the update topic instead")
@@ -271,7 +275,8 @@ def main(argv=None) -> int:
         return 0
     workers = [int(w) for w in str(args.workers).split(",")]
     if args.sweep:
-        grid = [(f, m) for f in (50, 250) for m in (1_000_000, 5_000_000, 20_000_000)]
+        grid = [(int(f), int(m)) for f in args.sweep_features.split(",")
+                for m in args.sweep_items.split(",")]
         rates = (0.3, 1.0)
     else:
         grid = [(args.features, args.items)]

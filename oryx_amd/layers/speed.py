@@ -96,6 +96,7 @@ class SpeedLayer(AbstractLayer):
             updates = self._manager.build_updates(records)
             if isinstance(updates, MessageBlock):
                 self._producer.send_block("UP", updates)
+                sent = len(updates)
             elif updates:
                 self._producer.send_many(("UP", u) for u in updates)
                 sent = len(updates) if hasattr(updates, "__len__") else 0
