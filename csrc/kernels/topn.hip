@@ -144,71 +144,33 @@ __global__ __launch_bounds__(WPB * 64) void topn_scan(TopnParams p) {
     }
     r = lo;
   }
-  // software pipeline, one tile deep: tile t + 1's item rows (and its norms / buckets) are
-  // loaded before tile t's MFMAs and epilogue run, so every wave keeps a tile of loads in
-  // flight instead of alternating load-wait-compute
-  auto tile_rows = [&](long long t, int& rr, long long& i0, long long& rend) {
-    while (t >= p.tile0[rr + 1]) ++rr;
-    const long long rbeg = p.ranges[2 * rr];
-    rend = p.ranges[2 * rr + 1];
-    i0 = rbeg + 16 * (t - p.tile0[rr]);
-  };
-  f32x4 abuf[S];
-  float nbuf[4];
-  int bbuf[4];
-  long long i0 = 0, rend = 0;
-  auto load = [&](long long ti0, long long trend, f32x4 (&a)[S], float (&nv)[4],
-                  int (&bv)[4]) {
-    const long long ia = ti0 + (lane & 15) < trend ? ti0 + (lane & 15) : trend - 1;
-    const float* yrow = p.Y + ia * KP + 4 * kg;
-#pragma unroll
-    for (int s = 0; s < S; ++s) a[s] = *reinterpret_cast<const f32x4*>(yrow + 16 * s);
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const long long it = ti0 + 4 * kg + v;
-      const long long ic = it < trend ? it : trend - 1;
-      nv[v] = p.inv_norm ? p.inv_norm[ic] : 1.f;
-      bv[v] = cbits ? p.bucket_of[ic] : 0;
-    }
-  };
-  if (t_beg < t_end) {
-    tile_rows(t_beg, r, i0, rend);
-    load(i0, rend, abuf, nbuf, bbuf);
-  }
   for (long long t = t_beg; t < t_end; ++t) {
-    const long long ci0 = i0, crend = rend;
-    f32x4 cur[S];
-    float cn[4];
-    int cb[4];
-#pragma unroll
-    for (int s = 0; s < S; ++s) cur[s] = abuf[s];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      cn[v] = nbuf[v];
-      cb[v] = bbuf[v];
-    }
-    if (t + 1 < t_end) {
-      tile_rows(t + 1, r, i0, rend);
-      load(i0, rend, abuf, nbuf, bbuf);
-    }
+    while (t >= p.tile0[r + 1]) ++r;
+    const long long rbeg = p.ranges[2 * r], rend = p.ranges[2 * r + 1];
+    const long long i0 = rbeg + 16 * (t - p.tile0[r]);
+    // A: item row i0 + (lane & 15), features 16 s + 4 kg .. + 3
+    const long long ia = i0 + (lane & 15) < rend ? i0 + (lane & 15) : rend - 1;
+    const float* yrow = p.Y + ia * KP + 4 * kg;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < S; ++s) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(yrow + 16 * s);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(cur[s][j], qb[s][j], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], qb[s][j], acc, 0, 0, 0);
     }
-    // C: lane holds items ci0 + 4 kg + v of query q
+    // C: lane holds items i0 + 4 kg + v of query q
     bool any = false;
     float v4[4];
     int r4[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const long long it = ci0 + 4 * kg + v;
-      float sv = acc[v] * cn[v];
-      bool ok = it < crend && q < p.nq;
+      const long long it = i0 + 4 * kg + v;
+      float sv = acc[v];
+      bool ok = it < rend && q < p.nq;
+      if (ok && p.inv_norm) sv *= p.inv_norm[it];
       if (ok && cbits) {
-        const int b = cb[v];
+        const int b = p.bucket_of[it];
         ok = (cbits[b >> 5] >> (b & 31)) & 1u;
       }
       ok = ok && sv > theta && !(sv != sv);

@@ -232,7 +232,7 @@ class ALSServingModel(ServingModel):
     def __init__(self, features: int, implicit: bool, sample_rate: float = 1.0,
                  rescorer_provider: Optional[RescorerProvider] = None,
                  device: Optional[torch.device] = None, max_batch: int = 16,
-                 batch_wait_s: float = 0.0):
+                 batch_wait_s: float = 0.0, scan_devices: Optional[Sequence] = None):
         if features <= 0 or not (0.0 < sample_rate <= 1.0):
             raise ValueError("bad features / sample rate")
         if device is None:
@@ -256,7 +256,12 @@ class ALSServingModel(ServingModel):
         self.index = None
         self.batcher = None
         if topn_ops.kernel_ok(device, features):
-            self.index = topn_ops.ItemIndex(self.Y, self.lsh.get_num_partitions())
+            if scan_devices is not None and len(scan_devices) > 1:
+                # item-sharded scan over several GPUs (oryx.serving.scan-gpus)
+                self.index = topn_ops.ShardedItemIndex(self.Y, self.lsh.get_num_partitions(),
+                                                       scan_devices)
+            else:
+                self.index = topn_ops.ItemIndex(self.Y, self.lsh.get_num_partitions())
             self.batcher = TopNBatcher(self.index, max_batch, batch_wait_s)
 
     # ---------------------------------------------------------------- accessors
@@ -557,6 +562,13 @@ class ALSServingModelManager(AbstractServingModelManager):
             if config.has_path("oryx.als.rescorer-provider-class") else None)
         if not (0.0 < self.sample_rate <= 1.0):
             raise ValueError("sample-rate must be in (0,1]")
+        # oryx.serving.scan-gpus > 1: the item matrix is sharded over that many GPUs for the
+        # top-N scan (ShardedItemIndex); 1 = one GPU (horizontal replicas scale out instead)
+        ng = cfg.get_optional_int(config, "oryx.serving.scan-gpus") or 1
+        self.scan_devices = None
+        if ng > 1 and torch.cuda.is_available():
+            avail = torch.cuda.device_count()
+            self.scan_devices = [torch.device("cuda", j % avail) for j in range(ng)]
         self.model: Optional[ALSServingModel] = None
 
     def consume(self, updates: Iterator[KeyMessage], context=None) -> None:
@@ -607,7 +619,8 @@ class ALSServingModelManager(AbstractServingModelManager):
                     self.model = ALSServingModel(features, implicit, self.sample_rate,
                                                  self.rescorer_provider,
                                                  max_batch=self.max_batch,
-                                                 batch_wait_s=self.batch_wait_s)
+                                                 batch_wait_s=self.batch_wait_s,
+                                                 scan_devices=self.scan_devices)
                 log.info("Updating model")
                 xids = set(pmml.get_extension_content("XIDs") or [])
                 yids = set(pmml.get_extension_content("YIDs") or [])

@@ -26,7 +26,8 @@ import torch
 
 from .. import native
 
-__all__ = ["ItemIndex", "TopNQuery", "MAX_BATCH", "MAX_HOW_MANY", "kernel_ok"]
+__all__ = ["ItemIndex", "ShardedItemIndex", "TopNQuery", "MAX_BATCH", "MAX_HOW_MANY",
+           "kernel_ok"]
 
 MAX_BATCH = 16          # queries per kernel launch
 MAX_HOW_MANY = 64       # candidates each wave keeps per query
@@ -55,13 +56,16 @@ class TopNQuery:
 
 
 class ItemIndex:
-    """Bucket-sorted device copy of an item store (see module docstring)."""
+    """Bucket-sorted device copy of an item store (see module docstring).  ``shard`` =
+    (d, N) keeps only the store rows r with r % N == d, on ``device`` (item sharding over
+    several GPUs: :class:`ShardedItemIndex`)."""
 
-    def __init__(self, store, num_buckets: int):
+    def __init__(self, store, num_buckets: int, device=None, shard: Tuple[int, int] = (0, 1)):
         self.store = store
         self.k = store.k
         self.kp = _kp(self.k)
-        self.device = store.device
+        self.device = torch.device(device) if device is not None else store.device
+        self.shard = (int(shard[0]), int(shard[1]))
         self.num_buckets = max(1, int(num_buckets))
         self.words = (self.num_buckets + 31) // 32
         self._lock = threading.Lock()
@@ -99,8 +103,11 @@ class ItemIndex:
         return parts[rows].to(torch.int64)
 
     def _rebuild(self, mat, valid, parts) -> None:
-        dev = mat.device
+        dev = self.device
         rows = torch.nonzero(valid, as_tuple=False).flatten()
+        d, nsh = self.shard
+        if nsh > 1:
+            rows = rows[rows % nsh == d]
         b = self._buckets(parts, rows)
         order = torch.argsort(b, stable=True)
         rows = rows[order]
@@ -108,7 +115,9 @@ class ItemIndex:
         n = int(rows.numel())
         ys = torch.zeros((max(n, 1), self.kp), dtype=torch.float32, device=dev)
         if n:
-            ys[:n, :self.k] = mat[rows]
+            ys[:n, :self.k] = mat[rows].to(dev)
+        rows = rows.to(dev)
+        b = b.to(dev)
         self.Ys = ys
         nrm = ys[:n].norm(dim=1) if n else torch.zeros(0, device=dev)
         self.inv_norm = torch.where(nrm > 0, 1.0 / nrm, torch.zeros_like(nrm))
@@ -130,19 +139,26 @@ class ItemIndex:
             return True
         if len(dirty) > max(4096, self.n // 16):
             return False
-        dev = mat.device
-        rows = torch.from_numpy(np.asarray(dirty, dtype=np.int64)).to(dev)
+        dev = self.device
+        d, nsh = self.shard
+        dirty = np.asarray(dirty, dtype=np.int64)
+        if nsh > 1:
+            dirty = dirty[dirty % nsh == d]
+            if len(dirty) == 0:
+                return True
+        src = torch.from_numpy(dirty).to(mat.device)
+        rows = src.to(dev)
         if int(rows.max()) >= self.pos_of_row.numel():
             return False
         pos = self.pos_of_row[rows]
-        ok = valid[rows]
+        ok = valid[src].to(dev)
         # new / removed rows or a changed bucket need a re-sort
         if bool(((pos < 0) | ~ok).any()):
             return False
-        nb = self._buckets(parts, rows)
+        nb = self._buckets(parts, src).to(dev)
         if bool((nb != self.bucket_of[pos].to(torch.int64)).any()):
             return False
-        self.Ys[pos, :self.k] = mat[rows]
+        self.Ys[pos, :self.k] = mat[src].to(dev)
         nrm = self.Ys[pos].norm(dim=1)
         self.inv_norm[pos] = torch.where(nrm > 0, 1.0 / nrm, torch.zeros_like(nrm))
         return True
@@ -261,3 +277,42 @@ class ItemIndex:
             keep = np.isfinite(vj) & (pj >= 0)
             out.append((self.row_of_pos_h[pj[keep]], vj[keep]))
         return out
+
+
+class ShardedItemIndex:
+    """Item-sharded top-N over several GPUs: store row r lives in shard
+    r % N on ``devices[r % N]``; a batch of queries is scanned by every shard at once (one
+    host thread per device, each launching its own fused scan) and the per-shard candidates
+    are merged on the host.  Same interface as :class:`ItemIndex` (``refresh`` / ``scan``)."""
+
+    def __init__(self, store, num_buckets: int, devices: Sequence):
+        import concurrent.futures
+        self.store = store
+        self.shards = [ItemIndex(store, num_buckets, device=dv, shard=(j, len(devices)))
+                       for j, dv in enumerate(devices)]
+        self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=len(devices),
+                                                           thread_name_prefix="oryx-topn")
+
+    @property
+    def n(self) -> int:
+        return sum(sh.n for sh in self.shards)
+
+    def refresh(self) -> None:
+        for f in [self._pool.submit(sh.refresh) for sh in self.shards]:
+            f.result()
+
+    def scan(self, queries: Sequence[TopNQuery]) -> List[Tuple[np.ndarray, np.ndarray]]:
+        parts = [f.result() for f in [self._pool.submit(sh.scan, queries)
+                                       for sh in self.shards]]
+        out = []
+        for j, q in enumerate(queries):
+            rows = np.concatenate([p[j][0] for p in parts])
+            sc = np.concatenate([p[j][1] for p in parts])
+            # descending by score, ties by row (the single-index order)
+            o = np.lexsort((rows, -sc))[:q.how_many]
+            out.append((rows[o], sc[o]))
+        return out
+
+    def close(self) -> None:
+        self._pool.shutdown(wait=False)
+

@@ -1,4 +1,4 @@
 #!/bin/bash
 set -o pipefail
 cd "$(dirname "$0")/.."
-bash scripts/gpu_r2_speed2.sh && bash scripts/gpu_r2_topn_ab.sh
+bash scripts/gpu_r2_speed2.sh

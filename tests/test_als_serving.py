@@ -446,6 +446,49 @@ def test_serving_model_topn_uses_kernel_and_batcher(cuda):
     assert m.batcher.requests == 40 and m.batcher.batches <= 40
 
 
+@pytest.mark.gpu
+def test_item_sharded_index_matches_single_index(cuda):
+    """C20: the item matrix split over 3 shards (rows r mod 3; on one GPU here -- the shards
+    only differ by device on a multi-GPU node), each scanned by its own fused kernel and
+    merged on the host, returns what one index returns, also after in-place updates and with
+    LSH candidates and excluded rows; the serving model takes it via scan_devices."""
+    from oryx_amd.models.als.common import FeatureVectors
+    from oryx_amd.models.als.serving import ALSServingModel
+    from oryx_amd.ops import topn
+    g = np.random.default_rng(12)
+    k, n, nb = 24, 50_000, 16
+    H = torch.from_numpy(g.standard_normal((4, k)).astype(np.float32)).to(cuda)
+    w = (1 << torch.arange(4, device=cuda))
+    part = lambda rows: ((rows @ H.t()) > 0).long().mul(w).sum(1)
+    fv = FeatureVectors(k, cuda, partitioner=part)
+    Y = g.standard_normal((n, k)).astype(np.float32)
+    fv.set_vectors(["I%d" % i for i in range(n)], Y)
+    one = topn.ItemIndex(fv, nb)
+    sharded = topn.ShardedItemIndex(fv, nb, [cuda, cuda, cuda])
+    for step in range(2):
+        qs = [topn.TopNQuery(g.standard_normal(k).astype(np.float32), hm, cos,
+                             candidates=np.sort(g.choice(nb, 6, replace=False)) if j % 2
+                             else None, exclude_rows=g.integers(0, n, 10).tolist())
+              for j, (hm, cos) in enumerate([(10, False), (64, True), (1, False), (33, True)])]
+        a, b = one.scan(qs), sharded.scan(qs)
+        for (ra, sa), (rb, sb) in zip(a, b):
+            np.testing.assert_allclose(sb, sa, rtol=1e-6, atol=1e-6)
+            assert (ra == rb).mean() > 0.95
+        if step == 0:
+            ch = g.choice(n, 50, replace=False)
+            Y[ch] *= 1.25
+            for r in ch:
+                fv.set_vector("I%d" % r, Y[r])
+    assert sharded.n == one.n
+    sharded.close()
+    m = ALSServingModel(k, True, 1.0, device=torch.device(cuda), scan_devices=[cuda, cuda])
+    assert isinstance(m.index, topn.ShardedItemIndex)
+    m.Y.set_vectors(["I%d" % i for i in range(n)], Y)
+    t = g.standard_normal(k).astype(np.float32)
+    best = np.argsort(-(Y @ t))[:5]
+    assert [i for i, _ in m.top_n(t, 5)] == ["I%d" % b for b in best]
+
+
 def test_bulk_up_batch_matches_per_message(tmp_path):
     """apply_up_batch (native parse, bulk set_vectors) == applying each UP message alone,
     including repeated IDs (last wins), known items, non-string IDs and a fallback row."""
