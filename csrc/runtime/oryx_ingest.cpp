@@ -411,6 +411,93 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
   return total;
 }
 
+// Plain CSV block -> a dense row-major double matrix (the classification / regression
+// examples of the RDF and k-means speed layers and batch inputs): F fields per line, numeric
+// columns (is_num[f] != 0) parsed with the exact fast-path double parser (empty -> NaN), the
+// other columns returned as (offset, length) spans into buf for the caller's category maps.
+// Lines are split over the native threads (newline counts first, then every chunk parses
+// straight into its rows).  Returns the row count, or -(line + 1) of the first line that is
+// not plain CSV with F fields or has an unparseable numeric field (the caller then takes the
+// general path).
+long long oryx_csv_numeric_block(const char* buf, long long len, int F,
+                                 const unsigned char* is_num, double* out, long long* span_off,
+                                 int* span_len, long long max_rows) {
+  const int P = len >= (4ll << 20) ? oryx_ff::native_threads() : 1;
+  std::vector<const char*> cut((size_t)P + 1);
+  cut[0] = buf;
+  cut[(size_t)P] = buf + len;
+  for (int t = 1; t < P; ++t) {
+    const char* c = buf + len * t / P;
+    if (c < cut[(size_t)t - 1]) c = cut[(size_t)t - 1];
+    const char* nl = static_cast<const char*>(memchr(c, '\n', (size_t)(buf + len - c)));
+    cut[(size_t)t] = nl ? nl + 1 : buf + len;
+  }
+  // rows per chunk (non-empty lines)
+  std::vector<long long> rows((size_t)P + 1, 0), bad((size_t)P, -1), lines((size_t)P, 0);
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      long long r = 0, l = 0;
+      for (const char* p = cut[(size_t)t]; p < cut[(size_t)t + 1];) {
+        const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(cut[(size_t)t + 1] - p)));
+        const char* le = nl ? nl : cut[(size_t)t + 1];
+        if (le > p && !(le - p == 1 && *p == '\r')) ++r;
+        ++l;
+        p = nl ? nl + 1 : cut[(size_t)t + 1];
+      }
+      rows[(size_t)t + 1] = r;
+      lines[(size_t)t] = l;
+    }
+  });
+  for (int t = 0; t < P; ++t) rows[(size_t)t + 1] += rows[(size_t)t];
+  if (rows[(size_t)P] > max_rows) return -1;
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      long long row = rows[(size_t)t], line = 0;
+      for (const char* p = cut[(size_t)t]; p < cut[(size_t)t + 1];) {
+        const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(cut[(size_t)t + 1] - p)));
+        const char* le = nl ? nl : cut[(size_t)t + 1];
+        const char* lend = le;
+        if (lend > p && lend[-1] == '\r') --lend;
+        if (lend > p) {
+          double* o = out + row * F;
+          const char* q = p;
+          int f = 0;
+          bool ok = true;
+          while (ok) {
+            const char* c = static_cast<const char*>(memchr(q, ',', (size_t)(lend - q)));
+            const char* fe = c ? c : lend;
+            if (f >= F || memchr(q, '"', (size_t)(fe - q))) { ok = false; break; }
+            if (is_num[f]) {
+              if (fe == q) o[f] = std::numeric_limits<double>::quiet_NaN();
+              else if (!oryx_ff::parse_double(q, fe, o[f])) ok = false;
+            } else {
+              o[f] = std::numeric_limits<double>::quiet_NaN();
+              span_off[row * F + f] = q - buf;
+              span_len[row * F + f] = (int)(fe - q);
+            }
+            ++f;
+            if (!c) break;
+            q = c + 1;
+          }
+          if (!ok || f != F) {
+            bad[(size_t)t] = line;
+            return;
+          }
+          ++row;
+        }
+        ++line;
+        p = nl ? nl + 1 : cut[(size_t)t + 1];
+      }
+    }
+  });
+  long long before = 0;
+  for (int t = 0; t < P; ++t) {
+    if (bad[(size_t)t] >= 0) return -(before + bad[(size_t)t] + 1);
+    before += lines[(size_t)t];
+  }
+  return rows[(size_t)P];
+}
+
 // Formats rows of a float matrix as JSON arrays "[v0,v1,...]" with shortest round-trip
 // float32 text (fastfloat.h), back to back in out; row_ends[r] = end offset of row r.  Rows are
 // split over the native threads (each formats its range into its own buffer, then the parts

@@ -55,16 +55,19 @@ def parse_csv_block(lines: Sequence[str], schema: InputSchema,
     lines (no JSON arrays, no quoting): one C-level CSV parse (pandas) with numeric columns
     read straight to float64.  Returns ``(X, target, full)`` or None when the block does not
     qualify (the caller then takes the general path)."""
-    try:
-        import pandas as pd
-    except ImportError:                                     # pragma: no cover
-        return None
     if not lines:
         return None
     blob = "\n".join(lines)
     if '"' in blob or "\\" in blob or "[" in blob:
         return None
     F = schema.get_num_features()
+    full = _native_csv_block(blob, len(lines), schema, encodings, F)
+    if full is not None:
+        return _split_full(full, schema)
+    try:
+        import pandas as pd
+    except ImportError:                                     # pragma: no cover
+        return None
     dtypes = {fi: (np.float64 if schema.is_numeric(fi) else str) for fi in range(F)}
     try:
         df = pd.read_csv(io.StringIO(blob), header=None, dtype=dtypes, names=list(range(F)),
@@ -95,10 +98,55 @@ def parse_csv_block(lines: Sequence[str], schema: InputSchema,
             if not schema.is_target(fi) and np.isnan(codes).any():
                 return None
             full[:, fi] = codes[inv.reshape(-1)]
+    return _split_full(full, schema)
+
+
+def _split_full(full: np.ndarray, schema: InputSchema):
     X = full[:, schema.predictor_feature_indices]
     target = full[:, schema.get_target_feature_index()] if schema.has_target() else \
-        np.full(n, np.nan)
+        np.full(len(full), np.nan)
     return X, target, full
+
+
+def _native_csv_block(blob: str, n: int, schema: InputSchema,
+                      encodings: CategoricalValueEncodings, F: int) -> Optional[np.ndarray]:
+    """The block through the native threaded CSV parser (``oryx_csv_numeric_block``: exact
+    fast-path doubles, categorical fields as spans mapped here); None when a line does not
+    qualify or a value is unknown (the pandas / general path then decides)."""
+    from ... import native
+    import ctypes
+    data = blob.encode("utf-8")
+    is_num = np.array([1 if schema.is_numeric(fi) else 0 for fi in range(F)], dtype=np.uint8)
+    full = np.empty((n, F), dtype=np.float64)
+    span_off = np.zeros((n, F), dtype=np.int64)
+    span_len = np.zeros((n, F), dtype=np.int32)
+    vp = ctypes.c_void_p
+    got = native.runtime().oryx_csv_numeric_block(
+        data, len(data), F, is_num.ctypes.data_as(vp), full.ctypes.data_as(vp),
+        span_off.ctypes.data_as(vp), span_len.ctypes.data_as(vp), n)
+    if got != n:
+        return None
+    for fi in range(F):
+        if schema.is_numeric(fi):
+            if not schema.is_target(fi) and np.isnan(full[:, fi]).any():
+                return None                                  # empty predictor: general path
+        elif schema.is_categorical(fi):
+            m = encodings.get_value_encoding_map(fi)
+            vals = [data[o:o + l] for o, l in zip(span_off[:, fi].tolist(),
+                                                 span_len[:, fi].tolist())]
+            uniq, inv = np.unique(np.array(vals, dtype=object).astype(bytes),
+                                  return_inverse=True)
+            try:
+                codes = np.array([m[u.decode("utf-8")] if u else np.nan
+                                  for u in uniq.tolist()], dtype=np.float64)
+            except KeyError:
+                return None                                  # unknown value: general path
+            if not schema.is_target(fi) and np.isnan(codes).any():
+                return None
+            full[:, fi] = codes[inv.reshape(-1)]
+        else:
+            full[:, fi] = 0.0
+    return full
 
 
 def parse_examples(rows: Sequence[Sequence[str]], schema: InputSchema,
