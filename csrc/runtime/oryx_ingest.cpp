@@ -411,6 +411,50 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
   return total;
 }
 
+// ---- id -> row maps mirroring a Python feature store (the speed layer's ID lookups) ----
+
+struct RowMap {
+  std::unordered_map<std::string, int64_t> map;
+};
+
+void* oryx_rowmap_new() { return new RowMap(); }
+void oryx_rowmap_free(void* h) { delete static_cast<RowMap*>(h); }
+long long oryx_rowmap_size(void* h) { return (long long)static_cast<RowMap*>(h)->map.size(); }
+
+// n ids back to back in blob (ends = end offsets) -> rows (set / overwrite).
+void oryx_rowmap_set(void* h, const char* blob, const long long* ends, const long long* rows,
+                     long long n) {
+  auto& m = static_cast<RowMap*>(h)->map;
+  m.reserve(m.size() + (size_t)n);
+  long long b = 0;
+  for (long long j = 0; j < n; ++j) {
+    m[std::string(blob + b, (size_t)(ends[j] - b))] = rows[j];
+    b = ends[j];
+  }
+}
+
+void oryx_rowmap_remove(void* h, const char* blob, const long long* ends, long long n) {
+  auto& m = static_cast<RowMap*>(h)->map;
+  long long b = 0;
+  for (long long j = 0; j < n; ++j) {
+    m.erase(std::string(blob + b, (size_t)(ends[j] - b)));
+    b = ends[j];
+  }
+}
+
+// out[c] = row of dictionary key c (-1 when absent) for every code of the dictionary.
+long long oryx_rowmap_translate(void* h, void* dh, long long* out) {
+  auto& m = static_cast<RowMap*>(h)->map;
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  const long long n = (long long)d->keys.size();
+  for (long long c = 0; c < n; ++c) {
+    auto it = m.find(d->keys[(size_t)c]);
+    out[c] = it == m.end() ? -1 : it->second;
+  }
+  return n;
+}
+
 // Plain CSV block -> a dense row-major double matrix (the classification / regression
 // examples of the RDF and k-means speed layers and batch inputs): F fields per line, numeric
 // columns (is_num[f] != 0) parsed with the exact fast-path double parser (empty -> NaN), the

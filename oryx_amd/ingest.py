@@ -98,6 +98,56 @@ def parse_ratings(lines, users: IdDict, items: IdDict, default_ts: int,
     return u[:n], i[:n], s[:n], t[:n]
 
 
+def _ids_blob(ids: Sequence[str]):
+    enc = [i.encode("utf-8") for i in ids]
+    ends = np.cumsum(np.fromiter((len(e) for e in enc), dtype=np.int64, count=len(enc)))
+    return b"".join(enc), ends
+
+
+class RowMap:
+    """Native ``id -> row`` map mirroring a feature store's index, so a batch's dictionary of
+    IDs translates to store rows in one call (no per-ID Python lookups)."""
+
+    def __init__(self):
+        self._lib = native.runtime()
+        self._h = self._lib.oryx_rowmap_new()
+
+    def __del__(self):
+        try:
+            if self._h:
+                self._lib.oryx_rowmap_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def __len__(self) -> int:
+        return int(self._lib.oryx_rowmap_size(self._h))
+
+    def set(self, ids: Sequence[str], rows) -> None:
+        if not len(ids):
+            return
+        blob, ends = _ids_blob(ids)
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        vp = ctypes.c_void_p
+        self._lib.oryx_rowmap_set(self._h, blob, ends.ctypes.data_as(vp),
+                                  rows.ctypes.data_as(vp), len(ids))
+
+    def remove(self, ids: Sequence[str]) -> None:
+        if not len(ids):
+            return
+        blob, ends = _ids_blob(ids)
+        self._lib.oryx_rowmap_remove(self._h, blob, ends.ctypes.data_as(ctypes.c_void_p),
+                                     len(ids))
+
+    def translate(self, d: "IdDict") -> np.ndarray:
+        """Row of every key of ``d`` in code order (-1: not in the map)."""
+        out = np.empty(len(d), dtype=np.int64)
+        if len(out):
+            self._lib.oryx_rowmap_translate(self._h, d.handle,
+                                            out.ctypes.data_as(ctypes.c_void_p))
+        return out
+
+
 def parse_up_batch(messages: Sequence[str], k: int):
     """Bulk-parse ALS ``UP`` messages ``["X"|"Y", id, [k floats], [known ids]?]``.
 

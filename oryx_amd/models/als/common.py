@@ -81,6 +81,10 @@ class FeatureVectors:
         self.version = 0
         # rows changed since the last take_index_dirty() (serving ItemIndex); None = all
         self._idx_dirty: Optional[Set[int]] = None
+        # native id -> row mirror (ingest.RowMap) for bulk lookups, built on first use and
+        # then kept current from a journal of id insertions / removals
+        self._rowmap = None
+        self._journal: Optional[list] = None
 
     # ---------------------------------------------------------------- basic map API
     def size(self) -> int:
@@ -133,6 +137,8 @@ class FeatureVectors:
                 self._index[id_] = row
                 self._ids[row] = id_
                 self._recent.add(id_)
+                if self._journal is not None:
+                    self._journal.append((True, id_, row))
             self._host[row] = v
             self._host_valid[row] = True
             self._dirty.add(row)
@@ -183,6 +189,8 @@ class FeatureVectors:
                             index[id_] = row
                             self._ids[row] = id_
                             self._recent.add(id_)
+                            if self._journal is not None:
+                                self._journal.append((True, id_, row))
                         self._host[row] = v
                         self._host_valid[row] = True
                         self._dirty.add(row)
@@ -193,6 +201,8 @@ class FeatureVectors:
                 self._ensure_capacity(start + len(new_ids))
                 new_rows = np.arange(start, start + len(new_ids), dtype=np.int64)
                 index.update(zip(new_ids, new_rows.tolist()))
+                if self._journal is not None:
+                    self._journal.append((True, new_ids, new_rows))
                 self._ids.extend(new_ids)
                 self._recent.update(new_ids)
                 self._n_rows = start + len(new_ids)
@@ -215,6 +225,8 @@ class FeatureVectors:
     def _remove_locked(self, id_: str) -> None:
         row = self._index.pop(id_, None)
         self._recent.discard(id_)
+        if row is not None and self._journal is not None:
+            self._journal.append((False, id_, row))
         if row is not None:
             self._host[row] = 0.0
             self._host_valid[row] = False
@@ -224,6 +236,41 @@ class FeatureVectors:
             if self._idx_dirty is not None:
                 self._idx_dirty.add(row)
             self.version += 1
+
+    def native_rows(self, d) -> np.ndarray:
+        """Rows of every key of the native dictionary ``d`` (``ingest.IdDict``) in code
+        order, -1 for IDs not in the store: one native translation instead of a Python dict
+        lookup per ID (the speed layer resolves a micro-batch's users / items this way)."""
+        from ... import ingest
+        with self._lock.write():
+            if self._rowmap is None:
+                self._rowmap = ingest.RowMap()
+                ids = list(self._index.keys())
+                self._rowmap.set(ids, np.fromiter(self._index.values(), dtype=np.int64,
+                                                  count=len(ids)))
+                self._journal = []
+            elif self._journal:
+                # replay in order, batching runs of the same kind
+                run_kind, run_ids, run_rows = None, [], []
+
+                def flush():
+                    if run_kind:
+                        self._rowmap.set(run_ids, np.asarray(run_rows, dtype=np.int64))
+                    elif run_kind is not None:
+                        self._rowmap.remove(run_ids)
+                for kind, ids, rows in self._journal:
+                    if kind != run_kind:
+                        flush()
+                        run_kind, run_ids, run_rows = kind, [], []
+                    if isinstance(ids, list):
+                        run_ids.extend(ids)
+                        run_rows.extend(np.asarray(rows).tolist())
+                    else:
+                        run_ids.append(ids)
+                        run_rows.append(int(rows))
+                flush()
+                self._journal = []
+            return self._rowmap.translate(d)
 
     def add_all_ids_to(self, out: Set[str]) -> None:
         with self._lock.read():

@@ -294,11 +294,8 @@ class ALSSpeedModelManager(SpeedModelManager):
         dev = model.device
         k = model.features
         # store rows of the batch's distinct IDs (dictionary codes index them)
-        xi, yi_ = model.X._index, model.Y._index
-        urow = np.fromiter((xi.get(key, -1) for key in users.keys()), dtype=np.int64,
-                           count=len(users))
-        irow = np.fromiter((yi_.get(key, -1) for key in items.keys()), dtype=np.int64,
-                           count=len(items))
+        urow = model.X.native_rows(users)
+        irow = model.Y.native_rows(items)
         ph["lookup"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
         n = len(u)

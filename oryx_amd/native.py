@@ -92,6 +92,12 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_parse_ratings", c_ll, [c_cp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_ll, c_ll, c_i])
     _sig(lib, "oryx_format_float_rows", c_ll, [c_vp, c_ll, c_i, c_ll, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_rowmap_new", c_vp, [])
+    _sig(lib, "oryx_rowmap_free", None, [c_vp])
+    _sig(lib, "oryx_rowmap_size", c_ll, [c_vp])
+    _sig(lib, "oryx_rowmap_set", None, [c_vp, c_vp, c_vp, c_vp, c_ll])
+    _sig(lib, "oryx_rowmap_remove", None, [c_vp, c_vp, c_vp, c_ll])
+    _sig(lib, "oryx_rowmap_translate", c_ll, [c_vp, c_vp, c_vp])
     # buf, len, F, is_num, out, span_off, span_len, max_rows
     _sig(lib, "oryx_csv_numeric_block", c_ll, [c_cp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp,
                                                c_ll])

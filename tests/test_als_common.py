@@ -225,3 +225,25 @@ def test_fused_foldin_matches_unfused(cuda, implicit, k):
     assert torch.equal(vx.cpu().bool(), okx) and torch.equal(vy.cpu().bool(), oky)
     assert torch.allclose(out["nx"].cpu()[okx], rx[okx], rtol=1e-5, atol=1e-6)
     assert torch.allclose(out["ny"].cpu()[oky], ry[oky], rtol=1e-5, atol=1e-6)
+
+
+def test_native_rows_follow_inserts_and_removals():
+    """FeatureVectors.native_rows (native id -> row mirror kept current from a journal)
+    agrees with the Python index through bulk loads, single inserts, removals and row reuse."""
+    import numpy as np
+    from oryx_amd import ingest
+    from oryx_amd.models.als.common import FeatureVectors
+    fv = FeatureVectors(3, None)
+    fv.set_vectors(["a%d" % j for j in range(100)], np.ones((100, 3), np.float32))
+    d = ingest.IdDict()
+    d.encode(["a5", "zz", "a99", "b1"])
+    assert fv.native_rows(d).tolist() == [fv.row_of("a5"), -1, fv.row_of("a99"), -1]
+    fv.set_vector("b1", [1, 2, 3])
+    fv.remove_vector("a5")
+    fv.set_vector("c7", [0, 0, 1])            # reuses a5's row
+    fv.set_vectors(["zz", "a99"], np.zeros((2, 3), np.float32))
+    fv.retain_recent_and_ids({"a99", "zz", "b1", "c7"})
+    d.encode(["c7"])
+    want = [fv.row_of(k) if fv.row_of(k) is not None else -1 for k in d.keys()]
+    assert fv.native_rows(d).tolist() == want
+    assert want[0] == -1 and want[-1] == fv.row_of("c7")
