@@ -237,8 +237,12 @@ __global__ __launch_bounds__(256) void rdf_histogram_pieces(
   extern __shared__ float lh[];
   // device pieces (n_live set) come sorted by their first row: the XCD-aware order puts the
   // pieces of different trees over the same rows on one XCD, so those rows come from its L2
-  const int pc = n_live ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-  if (n_live && pc >= *n_live) return;     // grid sized by an upper bound (device pieces)
+  // grid sized by an upper bound (device pieces): the surplus workgroups retire, and the
+  // XCD-aware order is taken over the LIVE pieces only -- remapping over the whole grid would
+  // leave the live pieces on the first XCDs and the last ones idle
+  const int nl = n_live ? *n_live : (int)gridDim.x;
+  if ((int)blockIdx.x >= nl) return;
+  const int pc = n_live ? xcd_remap(blockIdx.x, nl) : (int)blockIdx.x;
   const int t = piece_tree[pc];
   const int node = piece_node[pc];
   const long long per_node = (long long)Fs * B * S;
@@ -320,8 +324,9 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
     int B, float* __restrict__ hist, int NDW, int RSW, const int* __restrict__ n_live) {
   extern __shared__ __attribute__((aligned(16))) float lsm[];
   // see rdf_histogram_pieces: sorted device pieces in XCD-aware order
-  const int pc = n_live ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-  if (n_live && pc >= *n_live) return;   // grid sized by an upper bound
+  const int nl = n_live ? *n_live : (int)gridDim.x;   // see rdf_histogram_pieces
+  if ((int)blockIdx.x >= nl) return;
+  const int pc = n_live ? xcd_remap(blockIdx.x, nl) : (int)blockIdx.x;
   const int per_node = Fs * B * S;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   float* lh = lsm;                                                        // [per_node]

@@ -659,6 +659,8 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
 
 
 _DEVICE_LOOP = os.environ.get("ORYX_RDF_DEVICE_LOOP", "1") != "0"
+# device pieces ordered by first row (trees over the same rows on one XCD); 0: slot order
+_ROW_ORDER = os.environ.get("ORYX_RDF_ROW_ORDER", "1") != "0"
 
 
 def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classification: bool,
@@ -761,14 +763,15 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
                 "oryx_rdf_expand_pieces")
             # pieces in order of their first row (trees interleaved): the workgroups that run
             # together read the same rows, which then come from L2 / MALL instead of HBM
-            live = torch.arange(max_pieces, device=dev) < n_live
-            first = pbeg.clamp(0, T * n - 1)
-            row0 = (perm[first].long() if perm is not None else first) % n
-            key = torch.where(live, row0 * T + ptree.long().clamp(0, T - 1),
-                              torch.full_like(row0, 1 << 62))
-            order = torch.argsort(key)
-            ptree, pnode = ptree[order].contiguous(), pnode[order].contiguous()
-            pbeg, pend = pbeg[order].contiguous(), pend[order].contiguous()
+            if _ROW_ORDER:
+                live = torch.arange(max_pieces, device=dev) < n_live
+                first = pbeg.clamp(0, T * n - 1)
+                row0 = (perm[first].long() if perm is not None else first) % n
+                key = torch.where(live, row0 * T + ptree.long().clamp(0, T - 1),
+                                  torch.full_like(row0, 1 << 62))
+                order = torch.argsort(key)
+                ptree, pnode = ptree[order].contiguous(), pnode[order].contiguous()
+                pbeg, pend = pbeg[order].contiguous(), pend[order].contiguous()
             fe = feats[:, lo:hi].contiguous()
             native.check(lib.oryx_rdf_histogram_pieces(
                 data.Xb.data_ptr(), data.bin_bytes, n, P,
