@@ -8,7 +8,9 @@
 // dictionaries are collision-free (no hashing of IDs) and persist across intervals.
 // Also: shortest-round-trip float formatting of factor rows for JSON update messages.
 
+#include <algorithm>
 #include <charconv>
+#include <cstdio>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -19,6 +21,8 @@
 #include <string_view>
 #include <unordered_map>
 #include <vector>
+
+#include <zlib.h>
 
 #include "fastfloat.h"
 
@@ -604,14 +608,14 @@ namespace {
 
 // JSON string literal of UTF-8 text with Python json.dumps' default escaping (ensure_ascii:
 // non-ASCII as \uXXXX, astral planes as surrogate pairs).
-void json_quote(const std::string& s, std::string& o) {
+void json_quote(const char* s, size_t len, std::string& o) {
   static const char* hex = "0123456789abcdef";
   auto u4 = [&](unsigned v) {
     o += "\\u";
     o += hex[(v >> 12) & 15]; o += hex[(v >> 8) & 15]; o += hex[(v >> 4) & 15]; o += hex[v & 15];
   };
   o += '"';
-  for (size_t p = 0; p < s.size();) {
+  for (size_t p = 0; p < len;) {
     unsigned char c = (unsigned char)s[p];
     if (c < 0x80) {
       switch (c) {
@@ -631,7 +635,7 @@ void json_quote(const std::string& s, std::string& o) {
     unsigned cp = 0;
     int extra = c >= 0xF0 ? 3 : c >= 0xE0 ? 2 : 1;
     cp = c & (0x3F >> extra);
-    for (int q = 1; q <= extra && p + q < s.size(); ++q) cp = (cp << 6) | (s[p + q] & 0x3F);
+    for (int q = 1; q <= extra && p + q < len; ++q) cp = (cp << 6) | (s[p + q] & 0x3F);
     p += 1 + extra;
     if (cp >= 0x10000) {
       cp -= 0x10000;
@@ -643,6 +647,8 @@ void json_quote(const std::string& s, std::string& o) {
   }
   o += '"';
 }
+
+void json_quote(const std::string& s, std::string& o) { json_quote(s.data(), s.size(), o); }
 
 void float_row(const float* row, int k, std::string& o) {
   const size_t at = o.size();
@@ -1064,6 +1070,169 @@ long long oryx_assemble_als_updates(void* users, void* items, const long long* u
   });
   if (n_msgs) *n_msgs = msgs[(size_t)n];
   return bytes[(size_t)n];
+}
+
+}  // extern "C"
+
+namespace {
+
+// Span j of a blob with end offsets (ends[-1] = 0).
+struct Spans {
+  const char* blob;
+  const long long* ends;
+  const char* ptr(long long j) const { return blob + (j ? ends[j - 1] : 0); }
+  size_t len(long long j) const { return (size_t)(ends[j] - (j ? ends[j - 1] : 0)); }
+};
+
+}  // namespace
+
+extern "C" {
+
+// Model rows as update messages / part-file lines (ALSUpdate.publishAdditionalModelData,
+// ALSUpdate.java:183-235; the X/ Y/ text parts of saveFeaturesRDD):
+//   kind 'Y' (or 'X' without known): ["Y",id_e,row_e]
+//   kind 'X' with known:            ["X",id_e,row_e,known_{kidx[e]}]  (kidx[e] < 0: skipped,
+//                                    the reference's join drops users without events)
+//   kind 0:                          [id_e,row_e]
+// IDs are raw UTF-8 spans (quoted here as json.dumps does), rows and known arrays JSON text
+// spans.  '\n'-terminated into out; msg_ends receives each line's end ('\n' excluded) and
+// *n_msgs their number.  Two threaded passes (sizes, then direct writes at prefix offsets).
+// Returns bytes used or -(bytes needed).
+long long oryx_assemble_row_messages(int kind, const char* ids, const long long* id_ends,
+                                     const char* rows, const long long* row_ends, long long n,
+                                     const char* known, const long long* known_ends,
+                                     const long long* kidx, char* out, long long cap,
+                                     long long* msg_ends, long long* n_msgs) {
+  const Spans id{ids, id_ends}, row{rows, row_ends}, kn{known, known_ends};
+  const bool with_known = known != nullptr && kidx != nullptr;
+  const size_t head = kind ? 5 : 1;   // "[\"X\"," or "["
+  std::vector<long long> bytes((size_t)n + 1, 0), msgs((size_t)n + 1, 0);
+  oryx_ff::parallel_ranges(n, 1024, [&](long long lo, long long hi, int) {
+    std::string q;
+    for (long long e = lo; e < hi; ++e) {
+      if (with_known && kidx[e] < 0) continue;
+      q.clear();
+      json_quote(id.ptr(e), id.len(e), q);
+      long long b = (long long)(head + q.size() + 1 + row.len(e) + 2);
+      if (with_known) b += 1 + (long long)kn.len(kidx[e]);
+      bytes[(size_t)e + 1] = b;
+      msgs[(size_t)e + 1] = 1;
+    }
+  });
+  for (long long e = 0; e < n; ++e) {
+    bytes[(size_t)e + 1] += bytes[(size_t)e];
+    msgs[(size_t)e + 1] += msgs[(size_t)e];
+  }
+  if (bytes[(size_t)n] > cap) return -bytes[(size_t)n];
+  const char hdr[6] = {'[', '"', (char)kind, '"', ',', 0};
+  oryx_ff::parallel_ranges(n, 1024, [&](long long lo, long long hi, int) {
+    std::string q;
+    for (long long e = lo; e < hi; ++e) {
+      if (with_known && kidx[e] < 0) continue;
+      q.clear();
+      json_quote(id.ptr(e), id.len(e), q);
+      char* o = out + bytes[(size_t)e];
+      if (kind) { std::memcpy(o, hdr, 5); o += 5; } else { *o++ = '['; }
+      std::memcpy(o, q.data(), q.size());
+      o += q.size();
+      *o++ = ',';
+      std::memcpy(o, row.ptr(e), row.len(e));
+      o += row.len(e);
+      if (with_known) {
+        *o++ = ',';
+        std::memcpy(o, kn.ptr(kidx[e]), kn.len(kidx[e]));
+        o += kn.len(kidx[e]);
+      }
+      *o++ = ']';
+      if (msg_ends) msg_ends[msgs[(size_t)e]] = o - out;
+      *o++ = '\n';
+    }
+  });
+  if (n_msgs) *n_msgs = msgs[(size_t)n];
+  return bytes[(size_t)n];
+}
+
+// Known-item JSON arrays per user code (the X messages' last element): the (user, item)
+// code pairs come sorted by user; user c's array lists the quoted names (items dictionary)
+// of its items in the given order, "[]" for a user without pairs.  ends[c], c < n_users.
+// Returns bytes used or -(bytes needed).
+long long oryx_known_items_text(void* items, const long long* uu, const long long* ii,
+                                long long m, long long n_users, char* out, long long cap,
+                                long long* ends) {
+  auto* di = static_cast<Dict*>(items);
+  const long long n_items = (long long)di->keys.size();
+  std::vector<std::string> qname((size_t)n_items);
+  oryx_ff::parallel_ranges(n_items, 4096, [&](long long lo, long long hi, int) {
+    for (long long j = lo; j < hi; ++j) json_quote(di->keys[(size_t)j], qname[(size_t)j]);
+  });
+  // pair range of every user (uu ascending)
+  std::vector<long long> first((size_t)n_users + 1);
+  oryx_ff::parallel_ranges(n_users + 1, 4096, [&](long long lo, long long hi, int) {
+    for (long long c = lo; c < hi; ++c)
+      first[(size_t)c] = std::lower_bound(uu, uu + m, c) - uu;
+  });
+  std::vector<long long> bytes((size_t)n_users + 1, 0);
+  oryx_ff::parallel_ranges(n_users, 1024, [&](long long lo, long long hi, int) {
+    for (long long c = lo; c < hi; ++c) {
+      const long long a = first[(size_t)c], b = first[(size_t)c + 1];
+      long long sz = 2 + (b > a ? b - a - 1 : 0);
+      for (long long p = a; p < b; ++p) sz += (long long)qname[(size_t)ii[p]].size();
+      bytes[(size_t)c + 1] = sz;
+    }
+  });
+  for (long long c = 0; c < n_users; ++c) bytes[(size_t)c + 1] += bytes[(size_t)c];
+  if (bytes[(size_t)n_users] > cap) return -bytes[(size_t)n_users];
+  oryx_ff::parallel_ranges(n_users, 1024, [&](long long lo, long long hi, int) {
+    for (long long c = lo; c < hi; ++c) {
+      char* o = out + bytes[(size_t)c];
+      *o++ = '[';
+      for (long long p = first[(size_t)c]; p < first[(size_t)c + 1]; ++p) {
+        if (p > first[(size_t)c]) *o++ = ',';
+        const std::string& q = qname[(size_t)ii[p]];
+        std::memcpy(o, q.data(), q.size());
+        o += q.size();
+      }
+      *o++ = ']';
+      ends[c] = o - out;
+    }
+  });
+  return bytes[(size_t)n_users];
+}
+
+// buf[0, n) written to path as concatenated gzip members, one per 2 MB slice, compressed on
+// the native threads (a multi-member file is a single gzip stream to gzip / zlib / Hadoop
+// readers).  Returns 0, or -1 (file error) / -2 (zlib error).
+int oryx_write_gzip(const char* path, const char* buf, long long n, int level) {
+  const long long slice = 2ll << 20;
+  const long long ns = n > 0 ? (n + slice - 1) / slice : 1;
+  std::vector<std::string> part((size_t)ns);
+  std::vector<int> bad((size_t)ns, 0);
+  oryx_ff::parallel_ranges(ns, 1, [&](long long lo, long long hi, int) {
+    for (long long k = lo; k < hi; ++k) {
+      const long long a = k * slice, len = std::min(slice, n - a);
+      z_stream z{};
+      if (deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+        bad[(size_t)k] = 1;
+        continue;
+      }
+      std::string& o = part[(size_t)k];
+      o.resize(deflateBound(&z, (uLong)(len > 0 ? len : 0)) + 64);
+      z.next_in = reinterpret_cast<Bytef*>(const_cast<char*>(buf + (len > 0 ? a : 0)));
+      z.avail_in = (uInt)(len > 0 ? len : 0);
+      z.next_out = reinterpret_cast<Bytef*>(&o[0]);
+      z.avail_out = (uInt)o.size();
+      if (deflate(&z, Z_FINISH) != Z_STREAM_END) bad[(size_t)k] = 1;
+      o.resize(z.total_out);
+      deflateEnd(&z);
+    }
+  });
+  for (int b : bad)
+    if (b) return -2;
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return -1;
+  for (const std::string& o : part)
+    if (std::fwrite(o.data(), 1, o.size(), f) != o.size()) { std::fclose(f); return -1; }
+  return std::fclose(f) == 0 ? 0 : -1;
 }
 
 }  // extern "C"

@@ -285,6 +285,83 @@ def assemble_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndar
     return MessageBlock(out[:used], ends[:n_msgs.value].copy())
 
 
+def assemble_row_messages(kind: str, ids, rows, known=None, kidx=None):
+    """Model rows as newline-separated JSON lines in one :class:`~oryx_amd.api.MessageBlock`
+    (native, threaded): ``kind`` "Y" / "X" -> ``["Y",id,row]`` update messages (with
+    ``known`` spans and ``kidx``: ``["X",id,row,known[kidx[e]]]``, rows with ``kidx < 0``
+    skipped), "" -> ``[id,row]`` part-file lines.  ``ids``: list of str or (blob, ends);
+    ``rows`` / ``known``: :class:`~oryx_amd.ops.textfmt.RowText`."""
+    from .api import MessageBlock
+    id_blob, id_ends = ids if isinstance(ids, tuple) else _ids_blob(ids)
+    n = len(id_ends)
+    if n != len(rows):
+        raise ValueError("%d ids vs %d rows" % (n, len(rows)))
+    if n == 0:
+        return MessageBlock(b"", np.zeros(0, dtype=np.int64))
+    vp = ctypes.c_void_p
+    id_ends = np.ascontiguousarray(id_ends, dtype=np.int64)
+    re = np.ascontiguousarray(rows.ends, dtype=np.int64)
+    if known is not None:
+        ke = np.ascontiguousarray(known.ends, dtype=np.int64)
+        kidx = np.ascontiguousarray(kidx, dtype=np.int64)
+        if len(kidx) != n or (len(kidx) and int(kidx.max()) >= len(ke)):
+            raise ValueError("known index out of range")
+        kargs = (_buf_ptr(known.blob), ke.ctypes.data_as(vp), kidx.ctypes.data_as(vp))
+        extra = int(ke[-1]) if len(ke) else 0
+    else:
+        kargs = (None, None, None)
+        extra = 0
+    lib = native.runtime()
+    cap = len(id_blob) * 2 + len(rows.blob) + extra + n * 16
+    ends = np.empty(n, dtype=np.int64)
+    n_msgs = ctypes.c_longlong(0)
+    code = ord(kind) if kind else 0
+    while True:
+        out = _host_buffer(cap)
+        used = lib.oryx_assemble_row_messages(
+            code, _buf_ptr(id_blob), id_ends.ctypes.data_as(vp), _buf_ptr(rows.blob),
+            re.ctypes.data_as(vp), n, *kargs, out.ctypes.data_as(vp), cap,
+            ends.ctypes.data_as(vp), ctypes.byref(n_msgs))
+        if used >= 0:
+            break
+        cap = -used + 1
+    return MessageBlock(out[:used], ends[:n_msgs.value].copy())
+
+
+def known_items_text(items: IdDict, uu: np.ndarray, ii: np.ndarray, n_users: int):
+    """Per user code, the JSON array of its items' quoted names (``(uu, ii)`` code pairs
+    sorted by user, items in the order given); a :class:`~oryx_amd.ops.textfmt.RowText`."""
+    from .ops.textfmt import RowText
+    uu = np.ascontiguousarray(uu, dtype=np.int64)
+    ii = np.ascontiguousarray(ii, dtype=np.int64)
+    if len(uu) and (int(ii.min()) < 0 or int(ii.max()) >= len(items) or
+                    int(uu.min()) < 0 or int(uu.max()) >= n_users):
+        raise ValueError("code out of range")
+    vp = ctypes.c_void_p
+    lib = native.runtime()
+    ends = np.empty(n_users, dtype=np.int64)
+    cap = 2 * n_users + 16 * len(uu) + 64
+    while True:
+        out = np.empty(cap, dtype=np.uint8)
+        used = lib.oryx_known_items_text(items.handle, uu.ctypes.data_as(vp),
+                                         ii.ctypes.data_as(vp), len(uu), n_users,
+                                         out.ctypes.data_as(vp), cap, ends.ctypes.data_as(vp))
+        if used >= 0:
+            break
+        cap = -used + 1
+    return RowText(out[:used], ends)
+
+
+def write_gzip(path: str, buf, level: int = 1) -> None:
+    """``buf`` (bytes / uint8 array) to ``path`` as a multi-member gzip file, compressed on
+    the native threads."""
+    n = len(buf)
+    rc = native.runtime().oryx_write_gzip(path.encode(), _buf_ptr(buf) if n else None, n,
+                                          int(level))
+    if rc != 0:
+        raise OSError("cannot write %s (%s)" % (path, "zlib" if rc == -2 else "file error"))
+
+
 def _host_buffer(n: int) -> np.ndarray:
     """A uint8 host buffer; on a GPU host from torch's caching pinned allocator, whose blocks
     are reused (already-faulted pages) once the previous holder is gone."""

@@ -170,15 +170,12 @@ def _timestamps(lines: Sequence[str]) -> np.ndarray:
 def write_features(path: str, ids: List[str], mat) -> None:
     """``X/`` or ``Y/`` directory with one gzip part of ``[id,[floats]]`` JSON lines (the
     reference's Spark text output with the gzip codec); ``mat`` is a float matrix or its
-    pre-formatted :class:`~oryx_amd.ops.textfmt.RowText`."""
+    pre-formatted :class:`~oryx_amd.ops.textfmt.RowText`.  Lines are assembled and
+    compressed natively (multi-member gzip, one member per slice, threads)."""
     os.makedirs(path, exist_ok=True)
     rows = mat if isinstance(mat, textfmt.RowText) else textfmt.format_rows(mat)
-    text = str(memoryview(rows.blob), "ascii")
-    starts = [0] + rows.ends[:-1].tolist()
-    data = "".join("[%s,%s]\n" % (json.dumps(id_), text[a:b])
-                   for id_, a, b in zip(ids, starts, rows.ends.tolist())).encode("utf-8")
-    with open(os.path.join(path, "part-00000.gz"), "wb") as f:
-        f.write(gzip.compress(data, compresslevel=1))
+    block = ingest.assemble_row_messages("", list(ids), rows)
+    ingest.write_gzip(os.path.join(path, "part-00000.gz"), block.buf, level=1)
 
 
 def read_features(path: str) -> Tuple[List[str], np.ndarray]:
@@ -633,26 +630,32 @@ class ALSUpdate(MLUpdate):
         all_data = list(new_data) + list(past_data or [])
         x_ids, x_text, y_ids, y_text = self._published_rows(pmml, model_parent_path)
         log.info("Sending item / Y data as model updates")
-        y_rows = y_text.rows() if len(y_ids) else []
-        model_update_topic.send_many(("UP", '["Y",%s,%s]' % (json.dumps(i), r))
-                                     for i, r in zip(y_ids, y_rows))
+        if len(y_ids):
+            model_update_topic.send_block("UP", ingest.assemble_row_messages("Y", y_ids, y_text))
         log.info("Sending user / X data as model updates")
-        x_rows = x_text.rows() if len(x_ids) else []
+        if not len(x_ids):
+            return
         if self.no_known_items:
-            model_update_topic.send_many(("UP", '["X",%s,%s]' % (json.dumps(u), r))
-                                         for u, r in zip(x_ids, x_rows))
-        else:
-            parsed = self._raw_parse_for(all_data)
-            dev = self.dist_ctx.device if self.dist_ctx is not None else None
-            known = known_items_json(all_data, device=dev) if parsed is None else \
-                known_items_json_parsed(*parsed, device=dev)
-            msgs = []
-            for uid, r in zip(x_ids, x_rows):
-                ks = known.get(uid)
-                if ks is None:
-                    continue  # join: users without any event are not sent
-                msgs.append(("UP", '["X",%s,%s,%s]' % (json.dumps(uid), r, ks)))
-            model_update_topic.send_many(msgs)
+            model_update_topic.send_block("UP", ingest.assemble_row_messages("X", x_ids, x_text))
+            return
+        parsed = self._raw_parse_for(all_data)
+        dev = self.dist_ctx.device if self.dist_ctx is not None else None
+        if parsed is None:
+            users, items = ingest.IdDict(), ingest.IdDict()
+            parsed = (users, items) + tuple(
+                ingest.parse_ratings(all_data, users, items, default_ts=0))
+        users = parsed[0]
+        known, present = known_items_spans(*parsed, device=dev)
+        if known is None:
+            return
+        # join: users without any event are not sent
+        n_u = len(present)
+        code = users.encode(list(x_ids))
+        ok = code < n_u
+        ok[ok] = present[code[ok]]
+        kidx = np.where(ok, code, -1)
+        model_update_topic.send_block("UP", ingest.assemble_row_messages("X", x_ids, x_text,
+                                                                         known, kidx))
 
     # ---------------------------------------------------------------- split
     def split_new_data_to_train_test(self, new_data):
@@ -730,10 +733,23 @@ def known_items_json(lines: Sequence[str], device=None) -> Dict[str, str]:
 
 def known_items_json_parsed(users, items, u, i, s, ts, device=None) -> Dict[str, str]:
     """:func:`known_items_json` from already parsed events (lines without a timestamp at 0)."""
-    if len(u) == 0:
+    text, present = known_items_spans(users, items, u, i, s, ts, device)
+    if text is None:
         return {}
-    uk, ik = users.keys(), items.keys()
-    n_i = len(ik)
+    rows = text.rows()
+    uk = users.keys()
+    return {uk[a]: rows[a] for a in np.flatnonzero(present).tolist()}
+
+
+def known_items_spans(users, items, u, i, s, ts, device=None):
+    """Known items of every user code as JSON array text (``RowText`` indexed by user code,
+    item names in ID-string order) and the mask of users with any event; ``(None, None)``
+    without events.  The last event per (user, item) in time order decides: a NaN strength
+    (empty value) removes the item.  Sorting runs on ``device``, the text natively."""
+    if len(u) == 0:
+        return None, None
+    ik = items.keys()
+    n_i, n_u = len(ik), len(users)
     dev = torch.device(device) if device is not None else torch.device("cpu")
     key = torch.from_numpy(u * n_i + i).to(dev)
     tt = torch.from_numpy(ts).to(dev)
@@ -753,15 +769,9 @@ def known_items_json_parsed(users, items, u, i, s, ts, device=None) -> Dict[str,
     o2 = torch.sort(uu * n_i + rk, stable=True).indices
     uu = uu[o2].cpu().numpy()
     ii = ii[o2].cpu().numpy()
-    enc = np.array([json.dumps(n) for n in ik], dtype=object)
-    out: Dict[str, str] = {uk[a]: "[]" for a in np.unique(u).tolist()}
-    if len(uu):
-        names = enc[ii]
-        cuts = np.flatnonzero(np.r_[True, uu[1:] != uu[:-1]])
-        ends = np.r_[cuts[1:], len(uu)]
-        for a, lo, hi in zip(uu[cuts].tolist(), cuts.tolist(), ends.tolist()):
-            out[uk[a]] = "[" + ",".join(names[lo:hi]) + "]"
-    return out
+    present = np.zeros(n_u, dtype=bool)
+    present[u] = True
+    return ingest.known_items_text(items, uu, ii, n_u), present
 
 
 def known_items(lines: Sequence[str]) -> Dict[str, set]:

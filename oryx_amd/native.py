@@ -115,6 +115,12 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_assemble_als_updates", c_ll, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                                   c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_ll,
                                                   c_vp, c_vp])
+    # kind, ids, id_ends, rows, row_ends, n, known, known_ends, kidx, out, cap, msg_ends, n_msgs
+    _sig(lib, "oryx_assemble_row_messages", c_ll, [c_i, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp,
+                                                   c_vp, c_vp, c_vp, c_ll, c_vp, c_vp])
+    # items, uu, ii, m, n_users, out, cap, ends
+    _sig(lib, "oryx_known_items_text", c_ll, [c_vp, c_vp, c_vp, c_ll, c_ll, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_write_gzip", c_i, [c_cp, c_vp, c_ll, c_i])
 
 
 def _runtime_sources():

@@ -90,3 +90,51 @@ def test_gpu_formatter_matches_host_bytes():
     view = big[:, :50]
     assert bytes(textfmt.format_rows(view).blob) == \
         bytes(textfmt.format_rows(view.cpu().numpy()).blob)
+
+
+def test_assemble_row_messages_matches_python():
+    import json
+    from oryx_amd import ingest
+    from oryx_amd.ops.textfmt import format_rows
+    rng = np.random.default_rng(3)
+    mat = rng.standard_normal((50, 7)).astype(np.float32)
+    ids = ["u%d" % j for j in range(48)] + ['q"\\x\n', "\u00e9\U0001F600"]
+    rows = format_rows(mat)
+    r = rows.rows()
+    y = ingest.assemble_row_messages("Y", ids, rows)
+    assert list(y) == ['["Y",%s,%s]' % (json.dumps(a), b) for a, b in zip(ids, r)]
+    lines = ingest.assemble_row_messages("", ids, rows)
+    assert list(lines) == ["[%s,%s]" % (json.dumps(a), b) for a, b in zip(ids, r)]
+    # known arrays by index, -1 skips the row
+    from oryx_amd.ops.textfmt import RowText
+    kt = ['["a"]', "[]", '["b","c"]']
+    blob = "".join(kt).encode()
+    known = RowText(blob, np.cumsum([len(k) for k in kt]))
+    kidx = np.array([j % 4 - 1 for j in range(50)])
+    x = ingest.assemble_row_messages("X", ids, rows, known, kidx)
+    want = ['["X",%s,%s,%s]' % (json.dumps(a), b, kt[k]) for a, b, k in zip(ids, r, kidx)
+            if k >= 0]
+    assert list(x) == want
+
+
+def test_known_items_text_and_gzip(tmp_path):
+    import gzip
+    import json
+    from oryx_amd import ingest
+    items = ingest.IdDict()
+    items.encode(["i0", "i\u00e91", 'i"2'])
+    uu = np.array([0, 0, 2, 2, 2])
+    ii = np.array([1, 0, 2, 1, 0])
+    kt = ingest.known_items_text(items, uu, ii, 4).rows()
+    names = items.keys()
+    assert kt == ["[%s,%s]" % (json.dumps(names[1]), json.dumps(names[0])), "[]",
+                  "[" + ",".join(json.dumps(names[j]) for j in (2, 1, 0)) + "]", "[]"]
+    # several gzip members (slices of 8 MB) read back as one stream
+    data = np.random.default_rng(0).integers(32, 127, size=(20 << 20), dtype=np.uint8)
+    p = str(tmp_path / "x.gz")
+    ingest.write_gzip(p, data)
+    with gzip.open(p, "rb") as f:
+        assert f.read() == data.tobytes()
+    ingest.write_gzip(p, b"")
+    with gzip.open(p, "rb") as f:
+        assert f.read() == b""
