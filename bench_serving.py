@@ -171,10 +171,11 @@ def time_to_ready(items: int, users: int, features: int, seed: int) -> dict:
     from oryx_amd.serving.layer import ServingLayer
     from oryx_amd.transport import log as tlog
     from oryx_amd.utils import config as cfg, pmml as pmmlu
-    work = tempfile.mkdtemp(prefix="oryx_ttr_")
+    work = tempfile.mkdtemp(prefix="oryx_ttr_", dir=os.environ.get("ORYX_TTR_DIR"))
     try:
         Y, X, item_ids, user_ids, counts, known = make_data(items, users, features, seed)
         root = os.path.join(work, "log")
+        t_gen = time.perf_counter()
         tlog.maybe_create_topic(root, "OryxUpdate", 1, max_message=1 << 30)
         topic = tlog.Topic(root, "OryxUpdate")
         doc = pmmlu.build_skeleton_pmml()
@@ -187,21 +188,25 @@ def time_to_ready(items: int, users: int, features: int, seed: int) -> dict:
         doc.add_extension_content("XIDs", user_ids)
         doc.add_extension_content("YIDs", item_ids)
         topic.append_batch([("MODEL", pmmlu.to_string(doc))])
-        chunk = 1 << 18
+        # the batch layer's publish path: rows formatted and assembled natively, appended
+        # as blocks
+        chunk = 1 << 20
         for lo in range(0, items, chunk):
-            rows = ingest.format_float_rows(Y[lo:lo + chunk])
-            topic.append_values(['["Y","%s",%s]' % (item_ids[lo + j], r)
-                                 for j, r in enumerate(rows)], key="UP")
+            hi = min(items, lo + chunk)
+            topic.append_block(ingest.assemble_row_messages(
+                "Y", item_ids[lo:hi], ingest.format_float_rows_blob(Y[lo:hi])), key="UP")
         pos = np.r_[0, np.cumsum(counts)]
+        names = ingest.IdDict()
+        names.encode(["I%d" % i for i in range(items)])
         for lo in range(0, users, chunk):
-            rows = ingest.format_float_rows(X[lo:lo + chunk])
-            msgs = []
-            for j, r in enumerate(rows):
-                u = lo + j
-                ks = ",".join('"I%d"' % i for i in known[pos[u]:pos[u + 1]].tolist())
-                msgs.append('["X","%s",%s,[%s]]' % (user_ids[u], r, ks))
-            topic.append_values(msgs, key="UP")
+            hi = min(users, lo + chunk)
+            uu = np.repeat(np.arange(hi - lo), counts[lo:hi])
+            kt = ingest.known_items_text(names, uu, known[pos[lo]:pos[hi]], hi - lo)
+            topic.append_block(ingest.assemble_row_messages(
+                "X", user_ids[lo:hi], ingest.format_float_rows_blob(X[lo:hi]), kt,
+                np.arange(hi - lo)), key="UP")
         topic.close()
+        gen_s = time.perf_counter() - t_gen
         log_bytes = sum(os.path.getsize(os.path.join(dp, f)) for dp, _, fs in os.walk(root)
                         for f in fs)
         conf = cfg.overlay_on({
@@ -240,7 +245,7 @@ def time_to_ready(items: int, users: int, features: int, seed: int) -> dict:
             layer.close()
         return {"metric": "ALS serving model time-to-ready from the update topic",
                 "items": items, "users": users, "features": features,
-                "update_log_gb": log_bytes / 1e9, "ready_s": ready_s,
+                "update_log_gb": log_bytes / 1e9, "log_build_s": gen_s, "ready_s": ready_s,
                 "rows_per_s": (items + users) / ready_s,
                 "first_query_s": first_query_s, "model_hbm_gib": hbm,
                 "data": "synthetic Gaussian factors, Poisson(20) known items per user"}
