@@ -465,12 +465,15 @@ long long oryx_rowmap_translate(void* h, void* dh, long long* out) {
 // other columns returned as (offset, length) spans into buf for the caller's category maps.
 // Lines are split over the native threads (newline counts first, then every chunk parses
 // straight into its rows).  Returns the row count, or -(line + 1) of the first line that is
-// not plain CSV with F fields or has an unparseable numeric field (the caller then takes the
-// general path).
+// not plain CSV with F fields (a quote, a backslash or a leading '[' included) or has an
+// unparseable numeric field (the caller then takes the general path).
 long long oryx_csv_numeric_block(const char* buf, long long len, int F,
                                  const unsigned char* is_num, double* out, long long* span_off,
                                  int* span_len, long long max_rows) {
-  const int P = len >= (4ll << 20) ? oryx_ff::native_threads() : 1;
+  // threads for blocks past 256 KB (a 10k-event speed-layer batch is ~1 MB)
+  long long np_ = len >> 18;
+  if (np_ > oryx_ff::native_threads()) np_ = oryx_ff::native_threads();
+  const int P = np_ > 1 ? (int)np_ : 1;
   std::vector<const char*> cut((size_t)P + 1);
   cut[0] = buf;
   cut[(size_t)P] = buf + len;
@@ -510,7 +513,8 @@ long long oryx_csv_numeric_block(const char* buf, long long len, int F,
           double* o = out + row * F;
           const char* q = p;
           int f = 0;
-          bool ok = true;
+          // JSON-array lines and backslash escapes belong to the general parser
+          bool ok = *p != '[' && !memchr(p, '\\', (size_t)(lend - p));
           while (ok) {
             const char* c = static_cast<const char*>(memchr(q, ',', (size_t)(lend - q)));
             const char* fe = c ? c : lend;

@@ -58,12 +58,13 @@ def parse_csv_block(lines: Sequence[str], schema: InputSchema,
     if not lines:
         return None
     blob = "\n".join(lines)
-    if '"' in blob or "\\" in blob or "[" in blob:
-        return None
     F = schema.get_num_features()
+    # the native parser rejects quotes, backslashes and JSON-array lines itself
     full = _native_csv_block(blob, len(lines), schema, encodings, F)
     if full is not None:
         return _split_full(full, schema)
+    if '"' in blob or "\\" in blob or "[" in blob:
+        return None
     try:
         import pandas as pd
     except ImportError:                                     # pragma: no cover
@@ -102,7 +103,11 @@ def parse_csv_block(lines: Sequence[str], schema: InputSchema,
 
 
 def _split_full(full: np.ndarray, schema: InputSchema):
-    X = full[:, schema.predictor_feature_indices]
+    idx = list(schema.predictor_feature_indices)
+    if idx and idx == list(range(idx[0], idx[0] + len(idx))):
+        X = full[:, idx[0]:idx[0] + len(idx)]               # contiguous predictors: a view
+    else:
+        X = full[:, idx]
     target = full[:, schema.get_target_feature_index()] if schema.has_target() else \
         np.full(len(full), np.nan)
     return X, target, full
@@ -118,34 +123,46 @@ def _native_csv_block(blob: str, n: int, schema: InputSchema,
     data = blob.encode("utf-8")
     is_num = np.array([1 if schema.is_numeric(fi) else 0 for fi in range(F)], dtype=np.uint8)
     full = np.empty((n, F), dtype=np.float64)
-    span_off = np.zeros((n, F), dtype=np.int64)
-    span_len = np.zeros((n, F), dtype=np.int32)
+    # spans are written for every non-numeric field (numeric entries stay unused)
+    span_off = np.empty((n, F), dtype=np.int64)
+    span_len = np.empty((n, F), dtype=np.int32)
     vp = ctypes.c_void_p
     got = native.runtime().oryx_csv_numeric_block(
         data, len(data), F, is_num.ctypes.data_as(vp), full.ctypes.data_as(vp),
         span_off.ctypes.data_as(vp), span_len.ctypes.data_as(vp), n)
     if got != n:
         return None
+    num_pred = [fi for fi in range(F) if schema.is_numeric(fi) and not schema.is_target(fi)]
+    if num_pred and np.isnan(full).any(axis=0)[num_pred].any():
+        return None                                          # empty predictor: general path
+    buf = np.frombuffer(data, dtype=np.uint8)
     for fi in range(F):
         if schema.is_numeric(fi):
-            if not schema.is_target(fi) and np.isnan(full[:, fi]).any():
-                return None                                  # empty predictor: general path
-        elif schema.is_categorical(fi):
-            m = encodings.get_value_encoding_map(fi)
-            vals = [data[o:o + l] for o, l in zip(span_off[:, fi].tolist(),
-                                                 span_len[:, fi].tolist())]
-            uniq, inv = np.unique(np.array(vals, dtype=object).astype(bytes),
-                                  return_inverse=True)
-            try:
-                codes = np.array([m[u.decode("utf-8")] if u else np.nan
-                                  for u in uniq.tolist()], dtype=np.float64)
-            except KeyError:
-                return None                                  # unknown value: general path
-            if not schema.is_target(fi) and np.isnan(codes).any():
-                return None
-            full[:, fi] = codes[inv.reshape(-1)]
-        else:
+            continue
+        if not schema.is_categorical(fi):
             full[:, fi] = 0.0
+            continue
+        # the column's spans gathered into fixed-width byte strings (vectorised), one
+        # dictionary lookup per distinct value
+        off, ln = span_off[:, fi], span_len[:, fi]
+        L = int(ln.max()) if n else 0
+        if L > 0:
+            j = np.arange(L)
+            g = buf[np.minimum(off[:, None] + j, len(buf) - 1)]
+            g[j >= ln[:, None]] = 0
+            vals = np.ascontiguousarray(g).view("S%d" % L).ravel()
+        else:
+            vals = np.zeros(n, dtype="S1")
+        uniq, inv = np.unique(vals, return_inverse=True)
+        m = encodings.get_value_encoding_map(fi)
+        try:
+            codes = np.array([m[u.decode("utf-8")] if u else np.nan for u in uniq.tolist()],
+                             dtype=np.float64)
+        except (KeyError, UnicodeDecodeError):
+            return None                                      # unknown value: general path
+        if not schema.is_target(fi) and np.isnan(codes).any():
+            return None
+        full[:, fi] = codes[inv.reshape(-1)]
     return full
 
 
