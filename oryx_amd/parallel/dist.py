@@ -14,6 +14,7 @@ batched into a single all-reduce.
 
 from __future__ import annotations
 
+import atexit
 import datetime
 import os
 from dataclasses import dataclass
@@ -108,8 +109,20 @@ def init_from_env(device: Optional[str] = None, backend: Optional[str] = None,
         # work announcements (rank 0 may wait hours between generations)
         ctx.control = tdist.new_group(backend="gloo",
                                       timeout=datetime.timedelta(days=30))
+        # tear the groups down before interpreter exit: left to the process's static
+        # destructors, a gloo / RCCL group can be destroyed while its worker threads are
+        # still joinable (std::terminate, SIGABRT at exit)
+        atexit.register(_destroy_groups)
     _context = ctx
     return ctx
+
+
+def _destroy_groups() -> None:
+    try:
+        if tdist.is_initialized():
+            tdist.destroy_process_group()
+    except Exception:                                      # pragma: no cover - best effort
+        pass
 
 
 def _free_port() -> int:
