@@ -9,6 +9,7 @@
 // Also: shortest-round-trip float formatting of factor rows for JSON update messages.
 
 #include <algorithm>
+#include <array>
 #include <charconv>
 #include <cstdio>
 #include <cmath>
@@ -901,6 +902,72 @@ long long oryx_parse_up_records(const char* raw, long long used, long long nrec,
   return keep;
 }
 
+// Factor part-file lines ([id,[k floats]] per line, the X/ Y/ text parts written by
+// write_features / the reference's saveFeaturesRDD) -> vecs [n][k] and the id texts (fetched
+// with oryx_up_texts, as after oryx_parse_up_batch).  Lines are split over the native threads.
+// Empty lines are skipped.  Returns the number of rows, or -(line + 1) of the first line that
+// does not parse (the caller then takes the general path); at most max_n rows.
+long long oryx_parse_feature_lines(const char* buf, long long len, int k, long long max_n,
+                                   float* vecs, long long* id_ends) {
+  g_up_ids.clear();
+  g_up_known.clear();
+  std::vector<long long> begin, end;
+  for (const char* p = buf; p < buf + len;) {
+    const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(buf + len - p)));
+    const char* le = nl ? nl : buf + len;
+    const char* b = p;
+    while (b < le && (*b == ' ' || *b == '\r')) ++b;
+    if (b < le) {
+      if ((long long)begin.size() >= max_n) return -((long long)begin.size() + 1);
+      begin.push_back(p - buf);
+      end.push_back(le - buf);
+    }
+    p = nl ? nl + 1 : buf + len;
+  }
+  const long long n = (long long)begin.size();
+  const int T = oryx_ff::native_threads();
+  std::vector<std::string> ids((size_t)T);
+  std::vector<long long> lo_of((size_t)T + 1, n), bad((size_t)T, -1);
+  const int P = oryx_ff::parallel_ranges(n, 256, [&](long long lo, long long hi, int t) {
+    lo_of[(size_t)t] = lo;
+    std::string tok;
+    std::string& id = ids[(size_t)t];
+    for (long long j = lo; j < hi; ++j) {
+      JsonCursor c{buf + begin[(size_t)j], buf + end[(size_t)j]};
+      float* v = vecs + j * k;
+      bool ok = c.eat('[') && c.token(tok);
+      if (ok) id += tok;
+      ok = ok && c.eat(',') && c.eat('[');
+      for (int f = 0; ok && f < k; ++f) {
+        if (f && !c.eat(',')) { ok = false; break; }
+        c.ws();
+        const char* fb = c.p;
+        while (c.p < c.end && *c.p != ',' && *c.p != ']' && *c.p != ' ') ++c.p;
+        if (!oryx_ff::parse_float(fb, c.p, v[f])) {
+          const std::string_view t(fb, (size_t)(c.p - fb));
+          if (t == "NaN") v[f] = std::numeric_limits<float>::quiet_NaN();
+          else if (t == "Infinity") v[f] = std::numeric_limits<float>::infinity();
+          else if (t == "-Infinity") v[f] = -std::numeric_limits<float>::infinity();
+          else ok = false;
+        }
+      }
+      ok = ok && c.eat(']') && c.eat(']');
+      if (ok) { c.ws(); while (c.p < c.end && *c.p == '\r') ++c.p; ok = c.p == c.end; }
+      if (!ok) { bad[(size_t)t] = j; return; }
+      id_ends[j] = (long long)id.size();   // local; rebased below
+    }
+  });
+  for (int t = 0; t < P; ++t)
+    if (bad[(size_t)t] >= 0) return -(bad[(size_t)t] + 1);
+  for (int t = 0; t < P; ++t) {
+    const long long lo = lo_of[(size_t)t], hi = t + 1 < P ? lo_of[(size_t)t + 1] : n;
+    const long long base = (long long)g_up_ids.size();
+    for (long long j = lo; j < hi; ++j) id_ends[j] += base;
+    g_up_ids += ids[(size_t)t];
+  }
+  return n;
+}
+
 // The id texts (back to back) and the known-item texts ('\0'-terminated) of the last
 // oryx_parse_up_batch call; returns -(bytes needed) when a buffer is too small.
 long long oryx_up_texts(char* ids, long long ids_cap, char* known, long long known_cap) {
@@ -1205,7 +1272,10 @@ long long oryx_known_items_text(void* items, const long long* uu, const long lon
 
 // buf[0, n) written to path as concatenated gzip members, one per 2 MB slice, compressed on
 // the native threads (a multi-member file is a single gzip stream to gzip / zlib / Hadoop
-// readers).  Returns 0, or -1 (file error) / -2 (zlib error).
+// readers).  Every member's header carries an extra subfield "OX" (RFC 1952 FEXTRA, ignored
+// by other readers) with the member's total size and its uncompressed size, so that
+// oryx_gzip_indexed_inflate can find the members without inflating and decompress them in
+// parallel (the BGZF idea).  Returns 0, or -1 (file error) / -2 (zlib error).
 int oryx_write_gzip(const char* path, const char* buf, long long n, int level) {
   const long long slice = 2ll << 20;
   const long long ns = n > 0 ? (n + slice - 1) / slice : 1;
@@ -1213,21 +1283,33 @@ int oryx_write_gzip(const char* path, const char* buf, long long n, int level) {
   std::vector<int> bad((size_t)ns, 0);
   oryx_ff::parallel_ranges(ns, 1, [&](long long lo, long long hi, int) {
     for (long long k = lo; k < hi; ++k) {
-      const long long a = k * slice, len = std::min(slice, n - a);
+      const long long a = k * slice, len = n > 0 ? std::min(slice, n - a) : 0;
+      const Bytef* src = reinterpret_cast<const Bytef*>(buf + (len > 0 ? a : 0));
       z_stream z{};
-      if (deflateInit2(&z, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+      if (deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
         bad[(size_t)k] = 1;
         continue;
       }
       std::string& o = part[(size_t)k];
-      o.resize(deflateBound(&z, (uLong)(len > 0 ? len : 0)) + 64);
-      z.next_in = reinterpret_cast<Bytef*>(const_cast<char*>(buf + (len > 0 ? a : 0)));
-      z.avail_in = (uInt)(len > 0 ? len : 0);
-      z.next_out = reinterpret_cast<Bytef*>(&o[0]);
-      z.avail_out = (uInt)o.size();
+      const size_t H = 24;                     // 10 fixed + XLEN + "OX" subfield of 8 bytes
+      o.resize(H + deflateBound(&z, (uLong)len) + 8);
+      z.next_in = const_cast<Bytef*>(src);
+      z.avail_in = (uInt)len;
+      z.next_out = reinterpret_cast<Bytef*>(&o[H]);
+      z.avail_out = (uInt)(o.size() - H - 8);
       if (deflate(&z, Z_FINISH) != Z_STREAM_END) bad[(size_t)k] = 1;
-      o.resize(z.total_out);
+      const size_t body = z.total_out;
       deflateEnd(&z);
+      const uint32_t total = (uint32_t)(H + body + 8), isize = (uint32_t)len;
+      const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), src, (uInt)len);
+      unsigned char* h = reinterpret_cast<unsigned char*>(&o[0]);
+      const unsigned char fixed[16] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 255, 12, 0, 'O', 'X', 8, 0};
+      std::memcpy(h, fixed, 16);
+      std::memcpy(h + 16, &total, 4);
+      std::memcpy(h + 20, &isize, 4);
+      std::memcpy(h + H + body, &crc, 4);
+      std::memcpy(h + H + body + 4, &isize, 4);
+      o.resize(total);
     }
   });
   for (int b : bad)
@@ -1237,6 +1319,75 @@ int oryx_write_gzip(const char* path, const char* buf, long long n, int level) {
   for (const std::string& o : part)
     if (std::fwrite(o.data(), 1, o.size(), f) != o.size()) { std::fclose(f); return -1; }
   return std::fclose(f) == 0 ? 0 : -1;
+}
+
+namespace {
+
+// The members of an "OX"-indexed gzip file: (offset, total size, output offset, out size);
+// false when any member lacks the index (other writers).
+bool gzip_members(const unsigned char* b, long long n,
+                  std::vector<std::array<long long, 4>>& m) {
+  long long pos = 0, out = 0;
+  while (pos < n) {
+    if (n - pos < 24 || b[pos] != 0x1f || b[pos + 1] != 0x8b || b[pos + 2] != 8 ||
+        b[pos + 3] != 4)
+      return false;
+    const int xlen = b[pos + 10] | (b[pos + 11] << 8);
+    if (xlen != 12 || b[pos + 12] != 'O' || b[pos + 13] != 'X' || b[pos + 14] != 8 ||
+        b[pos + 15] != 0)
+      return false;
+    uint32_t total, isize;
+    std::memcpy(&total, b + pos + 16, 4);
+    std::memcpy(&isize, b + pos + 20, 4);
+    if (total < 32 || pos + total > n) return false;
+    m.push_back({pos, (long long)total, out, (long long)isize});
+    pos += total;
+    out += isize;
+  }
+  return !m.empty();
+}
+
+}  // namespace
+
+// Uncompressed size of an "OX"-indexed gzip file (see oryx_write_gzip), -1 when it is not one.
+long long oryx_gzip_indexed_size(const unsigned char* b, long long n) {
+  std::vector<std::array<long long, 4>> m;
+  if (!gzip_members(b, n, m)) return -1;
+  return m.back()[2] + m.back()[3];
+}
+
+// Inflates an "OX"-indexed gzip file into out (cap >= oryx_gzip_indexed_size), members on the
+// native threads, each checked against its CRC-32 and size.  Returns the size, -1 when the
+// file is not indexed, -2 on a corrupt member.
+long long oryx_gzip_indexed_inflate(const unsigned char* b, long long n, char* out,
+                                    long long cap) {
+  std::vector<std::array<long long, 4>> m;
+  if (!gzip_members(b, n, m)) return -1;
+  const long long size = m.back()[2] + m.back()[3];
+  if (size > cap) return -2;
+  std::vector<int> bad(m.size(), 0);
+  oryx_ff::parallel_ranges((long long)m.size(), 1, [&](long long lo, long long hi, int) {
+    for (long long k = lo; k < hi; ++k) {
+      const auto& e = m[(size_t)k];
+      z_stream z{};
+      if (inflateInit2(&z, -15) != Z_OK) { bad[(size_t)k] = 1; continue; }
+      z.next_in = const_cast<Bytef*>(b + e[0] + 24);
+      z.avail_in = (uInt)(e[1] - 24 - 8);
+      Bytef* dst = reinterpret_cast<Bytef*>(out + e[2]);
+      z.next_out = dst;
+      z.avail_out = (uInt)e[3];
+      const int rc = inflate(&z, Z_FINISH);
+      const bool ok = rc == Z_STREAM_END && (long long)z.total_out == e[3];
+      inflateEnd(&z);
+      uint32_t crc;
+      std::memcpy(&crc, b + e[0] + e[1] - 8, 4);
+      if (!ok || (uint32_t)crc32(crc32(0L, Z_NULL, 0), dst, (uInt)e[3]) != crc)
+        bad[(size_t)k] = 1;
+    }
+  });
+  for (int x : bad)
+    if (x) return -2;
+  return size;
 }
 
 }  // extern "C"

@@ -192,6 +192,25 @@ def parse_up_records(raw_ptr: int, used: int, nrec: int, k: int, max_n: int):
     return got, consumed.value, kinds[:got], ids, vecs[:got], known
 
 
+def parse_feature_lines(data: bytes, k: int):
+    """(ids, fp32 [n, k]) of factor part-file lines ``[id,[k floats]]`` (native, threaded),
+    or None when a line does not parse that way."""
+    if isinstance(data, np.ndarray):
+        n_max = int(np.count_nonzero(data == 10)) + 1
+    else:
+        n_max = data.count(b"\n") + 1
+    vecs = np.empty((n_max, k), dtype=np.float32)
+    id_ends = np.empty(n_max, dtype=np.int64)
+    vp = ctypes.c_void_p
+    n = native.runtime().oryx_parse_feature_lines(_buf_ptr(data), len(data), int(k), n_max,
+                                                  vecs.ctypes.data_as(vp),
+                                                  id_ends.ctypes.data_as(vp))
+    if n < 0:
+        return None
+    ids, _ = _up_texts(id_ends[:n], np.full(n, -1, dtype=np.int64), 16)
+    return ids, vecs[:n]
+
+
 def _up_texts(id_ends: np.ndarray, kcnt: np.ndarray, bound: int):
     """IDs and known-item lists of the last native UP parse (thread-local texts)."""
     n = len(id_ends)
@@ -360,6 +379,23 @@ def write_gzip(path: str, buf, level: int = 1) -> None:
                                           int(level))
     if rc != 0:
         raise OSError("cannot write %s (%s)" % (path, "zlib" if rc == -2 else "file error"))
+
+
+def read_gzip(raw: bytes):
+    """Decompressed contents of a gzip file (bytes, or a uint8 array for files written by
+    :func:`write_gzip`, whose indexed members are inflated natively in parallel and
+    CRC-checked); any other gzip goes through :mod:`gzip`."""
+    lib = native.runtime()
+    size = lib.oryx_gzip_indexed_size(raw, len(raw))
+    if size < 0:
+        import gzip
+        return gzip.decompress(raw)
+    out = np.empty(max(1, size), dtype=np.uint8)
+    got = lib.oryx_gzip_indexed_inflate(raw, len(raw), out.ctypes.data_as(ctypes.c_void_p),
+                                        size)
+    if got != size:
+        raise OSError("corrupt gzip member (CRC / size mismatch)")
+    return out[:size]
 
 
 def _host_buffer(n: int) -> np.ndarray:

@@ -179,18 +179,42 @@ def write_features(path: str, ids: List[str], mat) -> None:
 
 
 def read_features(path: str) -> Tuple[List[str], np.ndarray]:
-    ids, vecs = [], []
+    """The ``X/`` / ``Y/`` factor parts back as (ids, fp32 matrix): each part decompressed
+    whole and parsed natively (threaded), with a per-line JSON fallback for a part that is not
+    in the plain ``[id,[floats]]`` form."""
+    ids: List[str] = []
+    mats = []
     for part in sorted(ioutils.list_files(path, "part-*")):
-        with ioutils.open_text_maybe_gz(part) as f:
-            for line in f:
+        with open(part, "rb") as f:
+            raw = f.read()
+        if part.endswith(".gz"):
+            raw = ingest.read_gzip(raw)
+        head = bytes(raw[:1 << 16]).lstrip()
+        while b"\n" not in head and len(head) < len(raw):   # a first line past 64 KB
+            head = bytes(raw[:len(head) * 4 + (1 << 16)]).lstrip()
+        first = head.split(b"\n", 1)[0]
+        if not first.strip():
+            continue
+        got = None
+        try:
+            k = len(json.loads(first)[1])
+            got = ingest.parse_feature_lines(raw, k)
+        except (ValueError, IndexError, TypeError):
+            got = None
+        if got is None:
+            p_ids, vecs = [], []
+            for line in bytes(raw).decode("utf-8").splitlines():
                 line = line.strip()
-                if not line:
-                    continue
-                rec = json.loads(line)
-                ids.append(str(rec[0]))
-                vecs.append(rec[1])
-    mat = np.asarray(vecs, dtype=np.float32) if vecs else np.zeros((0, 0), np.float32)
-    return ids, mat
+                if line:
+                    rec = json.loads(line)
+                    p_ids.append(str(rec[0]))
+                    vecs.append(rec[1])
+            got = (p_ids, np.asarray(vecs, dtype=np.float32))
+        ids.extend(got[0])
+        mats.append(got[1])
+    if not ids:
+        return ids, np.zeros((0, 0), np.float32)
+    return ids, mats[0] if len(mats) == 1 else np.concatenate(mats)
 
 
 def _fingerprint(u, i, s, *params) -> str:

@@ -121,6 +121,10 @@ def _register_runtime_extras(lib):
     # items, uu, ii, m, n_users, out, cap, ends
     _sig(lib, "oryx_known_items_text", c_ll, [c_vp, c_vp, c_vp, c_ll, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_write_gzip", c_i, [c_cp, c_vp, c_ll, c_i])
+    _sig(lib, "oryx_gzip_indexed_size", c_ll, [c_vp, c_ll])
+    _sig(lib, "oryx_gzip_indexed_inflate", c_ll, [c_vp, c_ll, c_vp, c_ll])
+    # buf, len, k, max_n, vecs, id_ends
+    _sig(lib, "oryx_parse_feature_lines", c_ll, [c_vp, c_ll, c_i, c_ll, c_vp, c_vp])
 
 
 def _runtime_sources():

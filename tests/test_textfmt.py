@@ -138,3 +138,34 @@ def test_known_items_text_and_gzip(tmp_path):
     ingest.write_gzip(p, b"")
     with gzip.open(p, "rb") as f:
         assert f.read() == b""
+
+
+def test_indexed_gzip_and_feature_files_round_trip(tmp_path):
+    import gzip
+    import os
+    from oryx_amd import ingest
+    from oryx_amd.models.als.batch import read_features, write_features
+    rng = np.random.default_rng(5)
+    mat = rng.standard_normal((3000, 9)).astype(np.float32)
+    mat[4, 2] = np.nan
+    mat[5, 0] = np.inf
+    ids = ["id%d" % j for j in range(3000)]
+    ids[1] = 'q"é\\'
+    write_features(str(tmp_path / "X"), ids, mat)
+    raw = open(tmp_path / "X" / "part-00000.gz", "rb").read()
+    # the indexed members are a plain gzip stream to other readers, and inflate natively
+    assert bytes(ingest.read_gzip(raw)) == gzip.decompress(raw)
+    got_ids, got = read_features(str(tmp_path / "X"))
+    assert got_ids == ids
+    assert np.array_equal(got, mat, equal_nan=True)
+    # a part written by another gzip writer, with a bare-number id: the general paths
+    os.makedirs(tmp_path / "Y")
+    with gzip.open(tmp_path / "Y" / "part-00000.gz", "wt") as f:
+        f.write('[7,[1.5,-2]]\n\n["b",[3,4e-3]]\n')
+    assert read_features(str(tmp_path / "Y"))[0] == ["7", "b"]
+    assert np.allclose(read_features(str(tmp_path / "Y"))[1], [[1.5, -2], [3, 4e-3]])
+    # a damaged member is reported, not returned
+    bad = bytearray(raw)
+    bad[len(bad) // 2] ^= 0x55
+    with pytest.raises(Exception):
+        ingest.read_gzip(bytes(bad))
