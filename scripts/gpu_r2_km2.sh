@@ -9,5 +9,5 @@ for ro in 1 0; do
   echo "row_order=$ro"; tail -1 gpurun_out/bench_rdf_ro$ro.log | grep -o '"ms_per_step[^,]*\|"speed_layer_update_ms[^,]*'
 done
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rdf3 -o run -- python bench_rdf.py --steps 3 --warmup 1 > gpurun_out/prof_rdf3.log 2>&1 || { tail -20 gpurun_out/prof_rdf3.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_rdf3 -o run --output-format csv -- python3 bench_rdf.py --steps 3 --warmup 1 > gpurun_out/prof_rdf3.log 2>&1 || { tail -20 gpurun_out/prof_rdf3.log; exit 1; }
 bash scripts/gpu_r2_km.sh
