@@ -876,18 +876,19 @@ __global__ __launch_bounds__(256) void km_segment_sum(
 }
 
 // Exact fp32 re-check of the points the certified assignment could not decide: one wave per
-// 64 points, flagged points handled one at a time by the whole wave, lanes over the
-// dimensions (the point's row stays in registers, center rows are read coalesced).  flag 1:
-// squared distances sum (x - c)^2 to the two bf16 candidates; flag 2: every center, four at a
-// time (one 4-value butterfly reduction per group).  Ties go to the lower center index.
-// stats[0] / stats[1] count flag-1 / flag-2 points (nullable).  d <= 512.
+// 64 points.  flag 1 (two candidates): the point is handled by the whole wave, lanes over the
+// dimensions (the row stays in registers, center rows are read coalesced), squared distances
+// sum (x - c)^2 to the two bf16 candidates, ties to the lower center index.  flag 2 (the bf16
+// ranking certifies no short list): the point is appended to list2 ([0] = count, then rows)
+// for km_rescore_full.  stats[0] / stats[1] count flag-1 / flag-2 points (nullable).  d <= 512.
 __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, int ldx, int d,
                                                   const float* __restrict__ C, int k, long long n,
                                                   int* __restrict__ assign,
                                                   const int* __restrict__ idx2,
                                                   const unsigned char* __restrict__ flags,
                                                   float* __restrict__ mind,
-                                                  unsigned long long* __restrict__ stats) {
+                                                  unsigned long long* __restrict__ stats,
+                                                  int* __restrict__ list2) {
   const int lane = threadIdx.x & 63;
   const long long nw = (long long)gridDim.x * 4;
   // per-wave tallies, one atomic per wave at the end (a per-point atomic on one address
@@ -896,12 +897,20 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
   for (long long w = (long long)blockIdx.x * 4 + (threadIdx.x >> 6); w * 64 < n; w += nw) {
     const long long r0 = w * 64;
     const int f = r0 + lane < n ? flags[r0 + lane] : 0;
-    unsigned long long m = __ballot(f != 0);
+    // flag-2 points go to the list of km_rescore_full (one list atomic per wave)
+    const unsigned long long m2 = __ballot(f == 2);
+    if (m2) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(list2, (int)__popcll(m2));
+      base = __shfl(base, 0, 64);
+      if (f == 2) list2[1 + base + (int)__popcll(m2 & ((1ull << lane) - 1ull))] = (int)(r0 + lane);
+      n2 += __popcll(m2);
+    }
+    unsigned long long m = __ballot(f == 1);
     while (m) {
       const int j = __builtin_ctzll(m);
       m &= m - 1;
       const long long r = r0 + j;
-      const int fj = __builtin_amdgcn_readlane(f, j);
       const float* xr = X + r * ldx;
       float xv[8];
 #pragma unroll
@@ -917,60 +926,137 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
         }
         return sc;
       };
-      float bd;
-      int bi;
-      if (fj == 1) {
-        const int i1 = assign[r], i2 = idx2[r];
-        const float s1 = wave_sum(dist2(i1)), s2 = wave_sum(dist2(i2));
-        const bool first = s1 < s2 || (s1 == s2 && i1 < i2);
-        bd = first ? s1 : s2;
-        bi = first ? i1 : i2;
-      } else {
-        bd = INFINITY;
-        bi = 0x7fffffff;
-        for (int c0 = 0; c0 < k; c0 += 4) {
-          float p4[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) p4[u] = c0 + u < k ? dist2(c0 + u) : 0.f;
-          // reduce four partial sums at once: after the xor-32 / xor-16 steps lane group
-          // (lane >> 4) holds center c0 + (lane >> 4); then a 16-lane sum
-          const bool up32 = lane & 32, up16 = lane & 16;
-          float a0 = up32 ? p4[2] : p4[0], a1 = up32 ? p4[3] : p4[1];
-          const float b0 = up32 ? p4[0] : p4[2], b1 = up32 ? p4[1] : p4[3];
-          a0 += __shfl_xor(b0, 32, 64);
-          a1 += __shfl_xor(b1, 32, 64);
-          float v = up16 ? a1 : a0;
-          const float o = up16 ? a0 : a1;
-          v += __shfl_xor(o, 16, 64);
-#pragma unroll
-          for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-          const int c = c0 + ((lane >> 5) << 1) + ((lane >> 4) & 1);
-          if (c < k && (v < bd || (v == bd && c < bi))) {
-            bd = v;
-            bi = c;
-          }
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-          const float od = __shfl_xor(bd, off, 64);
-          const int oi = __shfl_xor(bi, off, 64);
-          if (od < bd || (od == bd && oi < bi)) {
-            bd = od;
-            bi = oi;
-          }
-        }
-      }
+      const int i1 = assign[r], i2 = idx2[r];
+      const float s1 = wave_sum(dist2(i1)), s2 = wave_sum(dist2(i2));
+      const bool first = s1 < s2 || (s1 == s2 && i1 < i2);
+      const float bd = first ? s1 : s2;
+      const int bi = first ? i1 : i2;
       if (lane == 0) {
         assign[r] = bi;
         mind[r] = bd;
       }
-      if (fj == 1) ++n1;
-      else ++n2;
+      ++n1;
     }
   }
   if (stats && lane == 0) {
     if (n1) atomicAdd(stats, n1);
     if (n2) atomicAdd(stats + 1, n2);
+  }
+}
+
+// Exact fp32 argmin over every center for the flag-2 points of km_rescore (list2: [0] =
+// count, then rows).  Per point the old path streamed all K center rows through one wave
+// (1 MB of L2 reads per point at K = 1000, d = 256); here a workgroup takes RP points at a
+// time with their rows staged in LDS (read as broadcasts), each lane owns one center of a
+// 64-center chunk and keeps that center's 64-dimension slice in registers, accumulating
+// (x - c)^2 in dimension order for all RP points -- K x d x 4 bytes of center traffic per RP
+// points and two VALU ops per (point, center, dimension).  (min, lowest index) per point is
+// reduced over lanes, then over the 4 waves through LDS.  Persistent grid: every workgroup
+// walks tiles of the list until the device-side count is exhausted.
+template <int RP>
+__global__ __launch_bounds__(256) void km_rescore_full(const float* __restrict__ X, int ldx,
+                                                       int d, const float* __restrict__ C,
+                                                       int k, const int* __restrict__ list2,
+                                                       int* __restrict__ assign,
+                                                       float* __restrict__ mind) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];     // [RP][dp] + reduction
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int dp = (d + 3) & ~3;
+  float* red_d = xs + RP * dp;                                   // [4][RP]
+  int* red_i = reinterpret_cast<int*>(red_d + 4 * RP);          // [4][RP]
+  const int cnt = list2[0];
+  for (int t0 = blockIdx.x * RP; t0 < cnt; t0 += gridDim.x * RP) {
+    const int np = cnt - t0 < RP ? cnt - t0 : RP;
+    __syncthreads();                                             // previous tile done
+    for (int i = tid; i < RP * dp; i += 256) {
+      const int p = i / dp, e = i - p * dp;
+      xs[i] = (p < np && e < d) ? X[(long long)list2[1 + t0 + p] * ldx + e] : 0.f;
+    }
+    __syncthreads();
+    float best[RP];
+    int bidx[RP];
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      best[p] = INFINITY;
+      bidx[p] = 0x7fffffff;
+    }
+    for (int c0 = wave * 64; c0 < k; c0 += 256) {
+      const int c = c0 + lane;
+      const bool live = c < k;
+      const float* cr = C + (long long)(live ? c : 0) * d;
+      float acc[RP];
+#pragma unroll
+      for (int p = 0; p < RP; ++p) acc[p] = 0.f;
+      for (int e0 = 0; e0 < dp; e0 += 64) {
+        float cv[64];
+#pragma unroll
+        for (int q = 0; q < 64; ++q) cv[q] = e0 + q < d ? cr[e0 + q] : 0.f;
+        const int q4n = (dp - e0) >= 64 ? 16 : (dp - e0) >> 2;
+#pragma unroll
+        for (int p = 0; p < RP; ++p) {
+          const float4* xp = reinterpret_cast<const float4*>(xs + p * dp + e0);
+          float a = acc[p];
+#pragma unroll
+          for (int q4 = 0; q4 < 16; ++q4) {
+            if (q4 < q4n) {
+              const float4 xv = xp[q4];
+              float t = xv.x - cv[4 * q4];
+              a = fmaf(t, t, a);
+              t = xv.y - cv[4 * q4 + 1];
+              a = fmaf(t, t, a);
+              t = xv.z - cv[4 * q4 + 2];
+              a = fmaf(t, t, a);
+              t = xv.w - cv[4 * q4 + 3];
+              a = fmaf(t, t, a);
+            }
+          }
+          acc[p] = a;
+        }
+      }
+      if (live) {
+#pragma unroll
+        for (int p = 0; p < RP; ++p)
+          if (acc[p] < best[p]) {                                // c grows: ties keep the lower
+            best[p] = acc[p];
+            bidx[p] = c;
+          }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+      float bd = best[p];
+      int bi = bidx[p];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        const float od = __shfl_xor(bd, off, 64);
+        const int oi = __shfl_xor(bi, off, 64);
+        if (od < bd || (od == bd && oi < bi)) {
+          bd = od;
+          bi = oi;
+        }
+      }
+      if (lane == 0) {
+        red_d[wave * RP + p] = bd;
+        red_i[wave * RP + p] = bi;
+      }
+    }
+    __syncthreads();
+    if (tid < np) {
+      float bd = red_d[tid];
+      int bi = red_i[tid];
+      for (int w = 1; w < 4; ++w) {
+        const float od = red_d[w * RP + tid];
+        const int oi = red_i[w * RP + tid];
+        if (od < bd || (od == bd && oi < bi)) {
+          bd = od;
+          bi = oi;
+        }
+      }
+      if (bi < 0 || bi >= k) bi = 0;                             // NaN row: no ordering
+      const int r = list2[1 + t0 + tid];
+      assign[r] = bi;
+      mind[r] = bd;
+    }
   }
 }
 
@@ -1184,14 +1270,16 @@ int oryx_kmeans_assign(const void* X, const float* xnorm, const void* C, long lo
 
 // Certified fp32-parity assignment: the bf16 MFMA kernel keeps each point's three best
 // centers and flags the points whose bf16 ranking is not provably the fp32 one; km_rescore
-// then decides those exactly from the fp32 rows (Xf [n][ldx], Cf [k][d]).  Only d_pad 64 /
-// 128 / 256 (the 64-point-per-wave kernel) and k_pad <= 65536.  idx2 / flags: [n] scratch.
+// then decides those exactly from the fp32 rows (Xf [n][ldx], Cf [k][d]), the flag-2 points
+// through km_rescore_full.  Only d_pad 64 / 128 / 256 (the 64-point-per-wave kernel) and
+// k_pad <= 65536.  idx2 / flags: [n] scratch; list2: [n + 1] int32 scratch.
 int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, long long n,
                             int d_pad, int k_pad, const float* cnorm, const float* Xf, int ldx,
                             int d, const float* Cf, int k, float cmax, int* assign, float* mind,
                             int* idx2, unsigned char* flags, unsigned long long* stats,
-                            void* stream) {
+                            int* list2, void* stream) {
   if (n <= 0) return ORYX_OK;
+  if (n >= 0x7fffffffLL) return ORYX_EINVAL;                   // list2 holds int32 rows
   const int dk = d_pad / 32;
   if (d_pad % 32 || k_pad % 64 || k_pad > 65536 || (dk != 2 && dk != 4 && dk != 8) || k <= 0 ||
       k > k_pad || d > d_pad || d > 512)
@@ -1237,8 +1325,22 @@ int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, lo
   long long waves = (n + 63) / 64;
   long long blocks = (waves + 3) / 4;
   if (blocks > 4096) blocks = 4096;
+  if (hipMemsetAsync(list2, 0, sizeof(int), s) != hipSuccess) return ORYX_ELAUNCH;
   hipLaunchKernelGGL(km_rescore, dim3((unsigned)blocks), dim3(256), 0, s, Xf, ldx, d, Cf, k, n,
-                     assign, idx2, flags, mind, stats);
+                     assign, idx2, flags, mind, stats, list2);
+  constexpr int RP = 32;
+  const int dp = (d + 3) & ~3;
+  const size_t smem = (size_t)RP * dp * 4 + 8 * RP * 4;
+  long long fblocks = (n + RP - 1) / RP;
+  if (fblocks > 1024) fblocks = 1024;
+  static bool full_attr = false;
+  if (!full_attr && smem > 65536) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&km_rescore_full<RP>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    full_attr = true;
+  }
+  hipLaunchKernelGGL((km_rescore_full<RP>), dim3((unsigned)fblocks), dim3(256), smem, s, Xf,
+                     ldx, d, Cf, k, list2, assign, mind);
   return oryx_check_launch();
 }
 

@@ -107,10 +107,12 @@ class PointSet:
         self._cert = None
 
     def cert_workspace(self):
-        """(second-best index int32 [n], flags uint8 [n]) scratch of the certified kernel."""
+        """(second-best index int32 [n], flags uint8 [n], full-rescan list int32 [n + 1])
+        scratch of the certified kernel."""
         if self._cert is None:
             self._cert = (torch.empty(self.n, dtype=torch.int32, device=self.device),
-                          torch.empty(self.n, dtype=torch.uint8, device=self.device))
+                          torch.empty(self.n, dtype=torch.uint8, device=self.device),
+                          torch.empty(self.n + 1, dtype=torch.int32, device=self.device))
         return self._cert
 
     @property
@@ -151,7 +153,7 @@ def assign(x, centers: torch.Tensor, exact: bool = False, out=None,
             if precision == "fp32" and not _cert_ok(x, dc.k_pad):
                 x = x.x          # no certified kernel for this shape: exact fp32 scan below
             elif precision == "fp32":
-                idx2, flags = x.cert_workspace()
+                idx2, flags, list2 = x.cert_workspace()
                 st = CERT_STATS.get(x.device)
                 if st is None:
                     st = CERT_STATS[x.device] = torch.zeros(2, dtype=torch.int64,
@@ -160,7 +162,8 @@ def assign(x, centers: torch.Tensor, exact: bool = False, out=None,
                     x.xb.data_ptr(), x.xn.data_ptr(), dc.cb.data_ptr(), n, dc.d_pad, dc.k_pad,
                     dc.cnorm.data_ptr(), x.x.data_ptr(), x.x.stride(0), x.d, dc.cf.data_ptr(),
                     dc.k, dc.cmax, out_a.data_ptr(), out_d.data_ptr(), idx2.data_ptr(),
-                    flags.data_ptr(), st.data_ptr(), native.stream_ptr(x.device))
+                    flags.data_ptr(), st.data_ptr(), list2.data_ptr(),
+                    native.stream_ptr(x.device))
                 native.check(rc, "oryx_kmeans_assign_cert")
                 return out_a, out_d
             else:
