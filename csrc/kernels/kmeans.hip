@@ -984,30 +984,30 @@ __global__ __launch_bounds__(256) void km_rescore_full(const float* __restrict__
       const int c = c0 + lane;
       const bool live = c < k;
       const float* cr = C + (long long)(live ? c : 0) * d;
-      float acc[RP];
+      // even / odd dimensions in the two halves of packed fp32 pairs (v_pk_add_f32 /
+      // v_pk_fma_f32: two lanes' worth of work per instruction), summed at the end
+      f32x2 acc[RP];
 #pragma unroll
-      for (int p = 0; p < RP; ++p) acc[p] = 0.f;
+      for (int p = 0; p < RP; ++p) acc[p] = f32x2{0.f, 0.f};
       for (int e0 = 0; e0 < dp; e0 += 64) {
-        float cv[64];
+        f32x2 cv[32];
 #pragma unroll
-        for (int q = 0; q < 64; ++q) cv[q] = e0 + q < d ? cr[e0 + q] : 0.f;
+        for (int q = 0; q < 32; ++q)
+          cv[q] = f32x2{e0 + 2 * q < d ? cr[e0 + 2 * q] : 0.f,
+                        e0 + 2 * q + 1 < d ? cr[e0 + 2 * q + 1] : 0.f};
         const int q4n = (dp - e0) >= 64 ? 16 : (dp - e0) >> 2;
 #pragma unroll
         for (int p = 0; p < RP; ++p) {
-          const float4* xp = reinterpret_cast<const float4*>(xs + p * dp + e0);
-          float a = acc[p];
+          const f32x4* xp = reinterpret_cast<const f32x4*>(xs + p * dp + e0);
+          f32x2 a = acc[p];
 #pragma unroll
           for (int q4 = 0; q4 < 16; ++q4) {
             if (q4 < q4n) {
-              const float4 xv = xp[q4];
-              float t = xv.x - cv[4 * q4];
-              a = fmaf(t, t, a);
-              t = xv.y - cv[4 * q4 + 1];
-              a = fmaf(t, t, a);
-              t = xv.z - cv[4 * q4 + 2];
-              a = fmaf(t, t, a);
-              t = xv.w - cv[4 * q4 + 3];
-              a = fmaf(t, t, a);
+              const f32x4 xv = xp[q4];
+              f32x2 t = f32x2{xv[0], xv[1]} - cv[2 * q4];
+              a = __builtin_elementwise_fma(t, t, a);
+              t = f32x2{xv[2], xv[3]} - cv[2 * q4 + 1];
+              a = __builtin_elementwise_fma(t, t, a);
             }
           }
           acc[p] = a;
@@ -1015,11 +1015,13 @@ __global__ __launch_bounds__(256) void km_rescore_full(const float* __restrict__
       }
       if (live) {
 #pragma unroll
-        for (int p = 0; p < RP; ++p)
-          if (acc[p] < best[p]) {                                // c grows: ties keep the lower
-            best[p] = acc[p];
+        for (int p = 0; p < RP; ++p) {
+          const float v = acc[p][0] + acc[p][1];
+          if (v < best[p]) {                                     // c grows: ties keep the lower
+            best[p] = v;
             bidx[p] = c;
           }
+        }
       }
     }
 #pragma unroll
@@ -1332,7 +1334,7 @@ int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, lo
   const int dp = (d + 3) & ~3;
   const size_t smem = (size_t)RP * dp * 4 + 8 * RP * 4;
   long long fblocks = (n + RP - 1) / RP;
-  if (fblocks > 1024) fblocks = 1024;
+  if (fblocks > 2048) fblocks = 2048;
   static bool full_attr = false;
   if (!full_attr && smem > 65536) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&km_rescore_full<RP>),
