@@ -989,12 +989,27 @@ __global__ __launch_bounds__(256) void km_rescore_full(const float* __restrict__
       f32x2 acc[RP];
 #pragma unroll
       for (int p = 0; p < RP; ++p) acc[p] = f32x2{0.f, 0.f};
+      // center slices: 16 dwordx4 loads per 64 dimensions when rows are 16-byte aligned
+      // (d % 4 == 0)
+      auto load_slice = [&](int e0, f32x2* cv) {
+        if ((d & 3) == 0) {
+          const f32x4* c4 = reinterpret_cast<const f32x4*>(cr + e0);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const f32x4 v = e0 + 4 * q < d ? c4[q] : f32x4{0.f, 0.f, 0.f, 0.f};
+            cv[2 * q] = f32x2{v[0], v[1]};
+            cv[2 * q + 1] = f32x2{v[2], v[3]};
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 32; ++q)
+            cv[q] = f32x2{e0 + 2 * q < d ? cr[e0 + 2 * q] : 0.f,
+                          e0 + 2 * q + 1 < d ? cr[e0 + 2 * q + 1] : 0.f};
+        }
+      };
       for (int e0 = 0; e0 < dp; e0 += 64) {
         f32x2 cv[32];
-#pragma unroll
-        for (int q = 0; q < 32; ++q)
-          cv[q] = f32x2{e0 + 2 * q < d ? cr[e0 + 2 * q] : 0.f,
-                        e0 + 2 * q + 1 < d ? cr[e0 + 2 * q + 1] : 0.f};
+        load_slice(e0, cv);
         const int q4n = (dp - e0) >= 64 ? 16 : (dp - e0) >> 2;
 #pragma unroll
         for (int p = 0; p < RP; ++p) {
