@@ -29,18 +29,114 @@
 
 namespace {
 
+// Open-addressing string -> int32 index for the parse hot loop (std::unordered_map costs a
+// node and a key indirection per lookup: two cache misses once the IDs number 1e5).  Keys of
+// up to 16 bytes are stored inline, longer ones as views (into the input buffer or owned
+// storage); the full 64-bit hash is compared first.
+class FlatIndex {
+ public:
+  FlatIndex() { rehash(1024); }
+  // value of key k, or -1
+  int32_t find(std::string_view k) const {
+    const uint64_t h = hash(k.data(), k.size());
+    const size_t m = slots_.size() - 1;
+    for (size_t j = (size_t)h & m;; j = (j + 1) & m) {
+      const Slot& sl = slots_[j];
+      if (sl.code < 0) return -1;
+      if (sl.h == h && sl.len == k.size() &&
+          std::memcmp(k.size() <= 16 ? sl.in : sl.ptr, k.data(), k.size()) == 0)
+        return sl.code;
+    }
+  }
+  // index of key k, inserting it with value `next` when absent (*inserted set)
+  int32_t find_or_add(std::string_view k, int32_t next, bool* inserted) {
+    const uint64_t h = hash(k.data(), k.size());
+    size_t m = slots_.size() - 1, j = (size_t)h & m;
+    while (true) {
+      Slot& sl = slots_[j];
+      if (sl.code < 0) {
+        if ((used_ + 1) * 2 > slots_.size()) {
+          rehash(slots_.size() * 2);
+          return find_or_add(k, next, inserted);
+        }
+        sl.h = h;
+        sl.len = (uint32_t)k.size();
+        sl.code = next;
+        if (k.size() <= 16) std::memcpy(sl.in, k.data(), k.size());
+        else sl.ptr = k.data();
+        ++used_;
+        *inserted = true;
+        return next;
+      }
+      if (sl.h == h && sl.len == k.size() &&
+          std::memcmp(k.size() <= 16 ? sl.in : sl.ptr, k.data(), k.size()) == 0) {
+        *inserted = false;
+        return sl.code;
+      }
+      j = (j + 1) & m;
+    }
+  }
+
+ private:
+  struct Slot {
+    uint64_t h = 0;
+    uint32_t len = 0;
+    int32_t code = -1;
+    union {
+      char in[16];
+      const char* ptr;
+    };
+    Slot() : in{} {}
+  };
+  static uint64_t mix(uint64_t a, uint64_t b) {
+    const unsigned __int128 r = (unsigned __int128)a * b;
+    return (uint64_t)r ^ (uint64_t)(r >> 64);
+  }
+  static uint64_t hash(const char* p, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    while (n >= 8) {
+      uint64_t v;
+      std::memcpy(&v, p, 8);
+      h = mix(h ^ v, 0xA0761D6478BD642Full);
+      p += 8;
+      n -= 8;
+    }
+    uint64_t v = 0;
+    std::memcpy(&v, p, n);
+    return mix(h ^ v, 0xE7037ED1A0B428DBull);
+  }
+  void rehash(size_t cap) {
+    std::vector<Slot> old;
+    old.swap(slots_);
+    slots_.assign(cap, Slot());
+    used_ = 0;
+    const size_t m = cap - 1;
+    for (const Slot& sl : old) {
+      if (sl.code < 0) continue;
+      size_t j = (size_t)sl.h & m;
+      while (slots_[j].code >= 0) j = (j + 1) & m;
+      slots_[j] = sl;
+      ++used_;
+    }
+  }
+  std::vector<Slot> slots_;
+  size_t used_ = 0;
+};
+
 struct Dict {
-  // the map's keys are views of the strings in `keys` (a deque: elements never move), so a
-  // lookup needs no std::string
-  std::unordered_map<std::string_view, int64_t> map;
+  // the index's long keys are views of the strings in `keys` (a deque: elements never move);
+  // open addressing (FlatIndex): a micro-batch's fresh dictionary of 10k IDs costs no node
+  // allocations, and lookups in a 1e6-ID dictionary one cache miss
+  FlatIndex map;
   std::deque<std::string> keys;
   std::mutex mu;
   int64_t encode(std::string_view s) {
-    auto it = map.find(s);
-    if (it != map.end()) return it->second;
-    int64_t code = (int64_t)keys.size();
+    const int32_t f = map.find(s);
+    if (f >= 0) return f;
+    const int32_t code = (int32_t)keys.size();
     keys.emplace_back(s);
-    map.emplace(std::string_view(keys.back()), code);
+    bool ins;
+    map.find_or_add(std::string_view(keys.back()), code, &ins);
     return code;
   }
 };
@@ -138,8 +234,7 @@ long long oryx_dict_encode(void* dh, const char* buf, long long buf_len, int n, 
 long long oryx_dict_get(void* dh, const char* s, long long len) {
   Dict* d = static_cast<Dict*>(dh);
   std::lock_guard<std::mutex> g(d->mu);
-  auto it = d->map.find(std::string_view(s, (size_t)len));
-  return it == d->map.end() ? -1 : it->second;
+  return d->map.find(std::string_view(s, (size_t)len));
 }
 
 // Copies key `code` into out (cap bytes); returns its length (or -1).
@@ -155,100 +250,6 @@ long long oryx_dict_key(void* dh, long long code, char* out, long long cap) {
 }  // extern "C"
 
 namespace {
-
-// Open-addressing string -> int32 index for the parse hot loop (std::unordered_map costs a
-// node and a key indirection per lookup: two cache misses once the IDs number 1e5).  Keys of
-// up to 16 bytes are stored inline, longer ones as views (into the input buffer or owned
-// storage); the full 64-bit hash is compared first.
-class FlatIndex {
- public:
-  FlatIndex() { rehash(1024); }
-  // value of key k, or -1
-  int32_t find(std::string_view k) const {
-    const uint64_t h = hash(k.data(), k.size());
-    const size_t m = slots_.size() - 1;
-    for (size_t j = (size_t)h & m;; j = (j + 1) & m) {
-      const Slot& sl = slots_[j];
-      if (sl.code < 0) return -1;
-      if (sl.h == h && sl.len == k.size() &&
-          std::memcmp(k.size() <= 16 ? sl.in : sl.ptr, k.data(), k.size()) == 0)
-        return sl.code;
-    }
-  }
-  // index of key k, inserting it with value `next` when absent (*inserted set)
-  int32_t find_or_add(std::string_view k, int32_t next, bool* inserted) {
-    const uint64_t h = hash(k.data(), k.size());
-    size_t m = slots_.size() - 1, j = (size_t)h & m;
-    while (true) {
-      Slot& sl = slots_[j];
-      if (sl.code < 0) {
-        if ((used_ + 1) * 2 > slots_.size()) {
-          rehash(slots_.size() * 2);
-          return find_or_add(k, next, inserted);
-        }
-        sl.h = h;
-        sl.len = (uint32_t)k.size();
-        sl.code = next;
-        if (k.size() <= 16) std::memcpy(sl.in, k.data(), k.size());
-        else sl.ptr = k.data();
-        ++used_;
-        *inserted = true;
-        return next;
-      }
-      if (sl.h == h && sl.len == k.size() &&
-          std::memcmp(k.size() <= 16 ? sl.in : sl.ptr, k.data(), k.size()) == 0) {
-        *inserted = false;
-        return sl.code;
-      }
-      j = (j + 1) & m;
-    }
-  }
-
- private:
-  struct Slot {
-    uint64_t h = 0;
-    uint32_t len = 0;
-    int32_t code = -1;
-    union {
-      char in[16];
-      const char* ptr;
-    };
-    Slot() : in{} {}
-  };
-  static uint64_t mix(uint64_t a, uint64_t b) {
-    const unsigned __int128 r = (unsigned __int128)a * b;
-    return (uint64_t)r ^ (uint64_t)(r >> 64);
-  }
-  static uint64_t hash(const char* p, size_t n) {
-    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
-    while (n >= 8) {
-      uint64_t v;
-      std::memcpy(&v, p, 8);
-      h = mix(h ^ v, 0xA0761D6478BD642Full);
-      p += 8;
-      n -= 8;
-    }
-    uint64_t v = 0;
-    std::memcpy(&v, p, n);
-    return mix(h ^ v, 0xE7037ED1A0B428DBull);
-  }
-  void rehash(size_t cap) {
-    std::vector<Slot> old;
-    old.swap(slots_);
-    slots_.assign(cap, Slot());
-    used_ = 0;
-    const size_t m = cap - 1;
-    for (const Slot& sl : old) {
-      if (sl.code < 0) continue;
-      size_t j = (size_t)sl.h & m;
-      while (slots_[j].code >= 0) j = (j + 1) & m;
-      slots_[j] = sl;
-      ++used_;
-    }
-  }
-  std::vector<Slot> slots_;
-  size_t used_ = 0;
-};
 
 // One chunk of rating lines parsed by one thread: IDs get chunk-local codes (first-appearance
 // order) from chunk-local maps of views; the caller merges the local dictionaries into the
@@ -418,45 +419,178 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
 
 // ---- id -> row maps mirroring a Python feature store (the speed layer's ID lookups) ----
 
+// Open addressing with linear probing and tombstones: a slot holds the 64-bit hash, the key
+// (inline up to 16 bytes, else an index into owned storage) and the row, so a lookup of a
+// short ID touches one cache line (std::unordered_map<std::string> took a bucket, a node and
+// the key's heap copy: ~370 ns per ID of a 10k-event micro-batch against a 162k-row store).
 struct RowMap {
-  std::unordered_map<std::string, int64_t> map;
+  struct Slot {
+    uint64_t h = 0;
+    uint32_t len = 0;
+    int32_t state = -1;     // -1 empty, -2 deleted, 0 live
+    int64_t row = 0;
+    union {
+      char in[16];
+      int64_t big;          // index into longs
+    };
+    Slot() : in{} {}
+  };
+  std::vector<Slot> slots = std::vector<Slot>(1024);
+  std::vector<std::string> longs;
+  size_t live = 0, used = 0;   // used: live + deleted slots
+
+  static uint64_t mix(uint64_t a, uint64_t b) {
+    const unsigned __int128 r = (unsigned __int128)a * b;
+    return (uint64_t)r ^ (uint64_t)(r >> 64);
+  }
+  static uint64_t hash(const char* p, size_t n) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ (uint64_t)n;
+    while (n >= 8) {
+      uint64_t v;
+      std::memcpy(&v, p, 8);
+      h = mix(h ^ v, 0xA0761D6478BD642Full);
+      p += 8;
+      n -= 8;
+    }
+    uint64_t v = 0;
+    std::memcpy(&v, p, n);
+    return mix(h ^ v, 0xE7037ED1A0B428DBull);
+  }
+  const char* key_of(const Slot& sl) const {
+    return sl.len <= 16 ? sl.in : longs[(size_t)sl.big].data();
+  }
+  bool same(const Slot& sl, uint64_t h, const char* k, size_t n) const {
+    return sl.state == 0 && sl.h == h && sl.len == n && std::memcmp(key_of(sl), k, n) == 0;
+  }
+  // slot of key k, or -1
+  int64_t find(const char* k, size_t n, uint64_t h) const {
+    const size_t m = slots.size() - 1;
+    for (size_t j = (size_t)h & m;; j = (j + 1) & m) {
+      const Slot& sl = slots[j];
+      if (sl.state == -1) return -1;
+      if (same(sl, h, k, n)) return (int64_t)j;
+    }
+  }
+  void rehash(size_t cap) {
+    std::vector<Slot> old;
+    old.swap(slots);
+    slots.assign(cap, Slot());
+    used = 0;
+    std::vector<std::string> kept;   // live long keys only
+    const size_t m = cap - 1;
+    for (const Slot& sl : old) {
+      if (sl.state != 0) continue;
+      size_t j = (size_t)sl.h & m;
+      while (slots[j].state != -1) j = (j + 1) & m;
+      slots[j] = sl;
+      if (sl.len > 16) {
+        slots[j].big = (int64_t)kept.size();
+        kept.push_back(std::move(longs[(size_t)sl.big]));
+      }
+      ++used;
+    }
+    longs.swap(kept);
+  }
+  void set(const char* k, size_t n, int64_t row) {
+    const uint64_t h = hash(k, n);
+    const int64_t f = find(k, n, h);
+    if (f >= 0) {
+      slots[(size_t)f].row = row;
+      return;
+    }
+    if ((used + 1) * 2 > slots.size()) {
+      size_t cap = 1024;
+      while (cap < (live + 1) * 4) cap *= 2;
+      rehash(cap);
+    }
+    const size_t m = slots.size() - 1;
+    size_t j = (size_t)h & m;
+    while (slots[j].state == 0) j = (j + 1) & m;
+    Slot& sl = slots[j];
+    if (sl.state == -1) ++used;
+    sl.h = h;
+    sl.len = (uint32_t)n;
+    sl.state = 0;
+    sl.row = row;
+    if (n <= 16) {
+      std::memcpy(sl.in, k, n);
+    } else {
+      sl.big = (int64_t)longs.size();
+      longs.emplace_back(k, n);
+    }
+    ++live;
+  }
+  void remove(const char* k, size_t n) {
+    const int64_t f = find(k, n, hash(k, n));
+    if (f < 0) return;
+    slots[(size_t)f].state = -2;    // a long key's storage is reclaimed at the next rehash
+    --live;
+    if (live == 0) {
+      slots.assign(1024, Slot());
+      longs.clear();
+      used = 0;
+    }
+  }
+  int64_t row_of(const char* k, size_t n, uint64_t h) const {
+    const int64_t f = find(k, n, h);
+    return f < 0 ? -1 : slots[(size_t)f].row;
+  }
+  void prefetch(uint64_t h) const { __builtin_prefetch(&slots[(size_t)h & (slots.size() - 1)]); }
 };
 
 void* oryx_rowmap_new() { return new RowMap(); }
 void oryx_rowmap_free(void* h) { delete static_cast<RowMap*>(h); }
-long long oryx_rowmap_size(void* h) { return (long long)static_cast<RowMap*>(h)->map.size(); }
+long long oryx_rowmap_size(void* h) { return (long long)static_cast<RowMap*>(h)->live; }
 
 // n ids back to back in blob (ends = end offsets) -> rows (set / overwrite).
 void oryx_rowmap_set(void* h, const char* blob, const long long* ends, const long long* rows,
                      long long n) {
-  auto& m = static_cast<RowMap*>(h)->map;
-  m.reserve(m.size() + (size_t)n);
+  RowMap* m = static_cast<RowMap*>(h);
   long long b = 0;
   for (long long j = 0; j < n; ++j) {
-    m[std::string(blob + b, (size_t)(ends[j] - b))] = rows[j];
+    m->set(blob + b, (size_t)(ends[j] - b), rows[j]);
     b = ends[j];
   }
 }
 
 void oryx_rowmap_remove(void* h, const char* blob, const long long* ends, long long n) {
-  auto& m = static_cast<RowMap*>(h)->map;
+  RowMap* m = static_cast<RowMap*>(h);
   long long b = 0;
   for (long long j = 0; j < n; ++j) {
-    m.erase(std::string(blob + b, (size_t)(ends[j] - b)));
+    m->remove(blob + b, (size_t)(ends[j] - b));
     b = ends[j];
   }
 }
 
 // out[c] = row of dictionary key c (-1 when absent) for every code of the dictionary.
 long long oryx_rowmap_translate(void* h, void* dh, long long* out) {
-  auto& m = static_cast<RowMap*>(h)->map;
+  const RowMap* m = static_cast<RowMap*>(h);
   Dict* d = static_cast<Dict*>(dh);
   std::lock_guard<std::mutex> g(d->mu);
   const long long n = (long long)d->keys.size();
-  for (long long c = 0; c < n; ++c) {
-    auto it = m.find(d->keys[(size_t)c]);
-    out[c] = it == m.end() ? -1 : it->second;
-  }
+  // a store of 1e5+ rows is a table of several MB: every probe is a cache miss, so hashes are
+  // computed D keys ahead and their slots prefetched (~10 misses in flight instead of one),
+  // and batches past 4k keys are split over the native threads
+  oryx_ff::parallel_ranges(n, 4096, [&](long long lo, long long hi, int) {
+    constexpr int D = 16;
+    uint64_t hs[D];
+    for (long long c = lo; c < hi && c < lo + D; ++c) {
+      const std::string& k = d->keys[(size_t)c];
+      hs[(c - lo) % D] = RowMap::hash(k.data(), k.size());
+      m->prefetch(hs[(c - lo) % D]);
+    }
+    for (long long c = lo; c < hi; ++c) {
+      const int q = (int)((c - lo) % D);
+      const uint64_t h = hs[q];
+      if (c + D < hi) {
+        const std::string& kn = d->keys[(size_t)(c + D)];
+        hs[q] = RowMap::hash(kn.data(), kn.size());
+        m->prefetch(hs[q]);
+      }
+      const std::string& k = d->keys[(size_t)c];
+      out[c] = m->row_of(k.data(), k.size(), h);
+    }
+  });
   return n;
 }
 

@@ -13,8 +13,8 @@
 // Record frame (little endian):  u32 magic | u32 crc32(payload) | u64 offset | i64 ts_ms |
 //                                u32 key_len (0xFFFFFFFF = null) | u32 value_len | key | value
 // Appends from any process are serialised with flock() on the partition directory's lock
-// file and written with one write() so readers in other processes never see torn frames
-// (a frame is only consumed once its full length and CRC check out).  Readers tail segment
+// file and written with one pwrite() (a block past 2 GB: consecutive ones); readers never
+// consume a torn frame (a frame is only consumed once its full length and CRC check out).  Readers tail segment
 // files by position, so consumers in other processes need no shared memory.
 //
 // C ABI for ctypes; every call releases nothing (ctypes drops the GIL around the call).
@@ -456,8 +456,17 @@ long long oryx_log_append_batch(void* h, int partition, const char* buf, long lo
       last = next;
       ++next;
     }
-    ssize_t w = pwrite(fd, out.data(), out.size(), end_pos);
-    if (w != (ssize_t)out.size()) {
+    // one pwrite per append; Linux caps a single write at 0x7ffff000 bytes, so a block past
+    // 2 GB goes out in pieces (a reader that gets ahead of them sees a short last frame and
+    // stops there, as it does for any append in progress)
+    size_t done = 0;
+    while (done < out.size()) {
+      const ssize_t w = pwrite(fd, out.data() + done, out.size() - done, end_pos + (off_t)done);
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) break;
+      done += (size_t)w;
+    }
+    if (done != out.size()) {
       close(fd);
       if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN);
       return fail("write");

@@ -7,11 +7,12 @@ mkdir -p gpurun_out
 ITEMS=${1:-20000000}
 df -h /tmp /dev/shm . 2>&1 | tee gpurun_out/ttr_df.txt
 free -g | tee -a gpurun_out/ttr_df.txt
-# the log needs ~2.8 KB per row: pick a filesystem with room for it
+# the log needs ~2.8 KB per row: pick a filesystem with room for it (the overlay /tmp
+# reported 79 GB free but failed a write part-way through the 20M-row log)
 DIR=$(python - "$ITEMS" <<'PY'
 import os, shutil, sys
 need = int(sys.argv[1]) * 2900 * 1.15
-for d in ("/tmp", "/dev/shm", os.getcwd()):
+for d in ("/dev/shm", "/tmp", os.getcwd()):
     try:
         if shutil.disk_usage(d).free > need:
             print(d); break
