@@ -262,6 +262,10 @@ struct RatingChunk {
   std::vector<std::string_view> ukeys, ikeys;
   std::deque<std::string> owned;     // unescaped fields (quoted CSV / JSON lines)
   long long lines = 0, bad_line = -1;
+  // single-chunk parse: codes straight from the global dictionaries (no chunk-local index
+  // and merge; both dictionaries are locked by the caller)
+  Dict* gu = nullptr;
+  Dict* gi = nullptr;
 
   int32_t code(FlatIndex& m, std::vector<std::string_view>& keys, std::string_view k,
                bool stable) {
@@ -333,8 +337,13 @@ struct RatingChunk {
           tv = (long long)t;
         }
         if (ok) {
-          u.push_back(code(umap, ukeys, f[0], stable));
-          i.push_back(code(imap, ikeys, f[1], stable));
+          if (gu) {
+            u.push_back((int32_t)gu->encode(f[0]));
+            i.push_back((int32_t)gi->encode(f[1]));
+          } else {
+            u.push_back(code(umap, ukeys, f[0], stable));
+            i.push_back(code(imap, ikeys, f[1], stable));
+          }
           s.push_back(sv);
           ts.push_back(tv);
         } else if (strict && bad_line < 0) {
@@ -379,6 +388,21 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
     cut[(size_t)t] = nl ? nl + 1 : buf + len;
   }
   std::vector<RatingChunk> ch((size_t)P);
+  if (P == 1) {
+    ch[0].gu = du;
+    ch[0].gi = di;
+    ch[0].parse(buf, buf + len, default_ts, strict != 0);
+    const RatingChunk& c = ch[0];
+    if (c.bad_line >= 0) return -(c.bad_line + 1);
+    const long long n = (long long)c.u.size() < max_rows ? (long long)c.u.size() : max_rows;
+    for (long long r = 0; r < n; ++r) {
+      out_u[r] = c.u[(size_t)r];
+      out_i[r] = c.i[(size_t)r];
+      out_s[r] = c.s[(size_t)r];
+      out_ts[r] = c.ts[(size_t)r];
+    }
+    return n;
+  }
   oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
     for (long long t = lo; t < hi; ++t)
       ch[(size_t)t].parse(cut[(size_t)t], cut[(size_t)t + 1], default_ts, strict != 0);

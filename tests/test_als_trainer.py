@@ -190,3 +190,52 @@ def test_trainer_fp32_precision_cpu():
         assert tr.Xb_local.shape[1] == (2 if prec == "fp32" else 1) * tr.kp
     # the CPU path solves from the operand copy: fp32 mode from ~fp32 factors
     assert not torch.equal(out[0].X, out[1].X)
+
+
+def _planted_implicit(seed=21, n_u=1500, n_i=600, rank=8):
+    """Implicit feedback planted from a rank-8 model: each user's positives are the top 5-40
+    items of U V^T + noise; 10% of every user's positives are held out."""
+    g = torch.Generator().manual_seed(seed)
+    U = torch.randn(n_u, rank, generator=g)
+    V = torch.randn(n_i, rank, generator=g)
+    S = U @ V.t() + 0.5 * torch.randn(n_u, n_i, generator=g)
+    m = torch.randint(5, 41, (n_u,), generator=g)
+    top = S.argsort(dim=1, descending=True)
+    tr_u, tr_i, tr_r, te_u, te_i = [], [], [], [], []
+    for a in range(n_u):
+        items = top[a, :int(m[a])]
+        hold = torch.rand(len(items), generator=g) < 0.1
+        tr_u.append(torch.full((int((~hold).sum()),), a))
+        tr_i.append(items[~hold])
+        tr_r.append(torch.randint(1, 6, (int((~hold).sum()),), generator=g).float())
+        te_u.append(torch.full((int(hold.sum()),), a))
+        te_i.append(items[hold])
+    cat = torch.cat
+    return cat(tr_u), cat(tr_i), cat(tr_r), cat(te_u).numpy(), cat(te_i).numpy(), n_u, n_i
+
+
+@pytest.mark.gpu
+def test_auc_drift_bf16_vs_fp32(cuda):
+    """End-metric drift of the factor precisions: held-out AUC (the reference's implicit
+    evaluation, Evaluation.java:70-136) of the GPU bf16 and fp32 modes vs the CPU fp32 trainer
+    from the same initial factors."""
+    import json
+    from oryx_amd.models.als.evaluation import area_under_curve
+    u, i, r, te_u, te_i, n_u, n_i = _planted_implicit()
+    k = 32
+    auc = {}
+    for name, dev, prec in (("cpu_fp32", "cpu", "fp32"), ("gpu_fp32", cuda, "fp32"),
+                            ("gpu_bf16", cuda, "bf16")):
+        tr = ALSTrainer(k, lam=0.01, alpha=1.0, implicit=True,
+                        ctx=dist.DistContext(device=torch.device(dev)), seed=1, precision=prec)
+        tr.prepare(u, i, r, n_u, n_i)
+        gi = torch.Generator().manual_seed(11)
+        tr.init_factors(torch.randn(n_u, k, generator=gi) * 0.1,
+                        torch.randn(n_i, k, generator=gi) * 0.1)
+        tr.iterate(10)
+        f = tr.factors()
+        auc[name] = area_under_curve(f.X.cpu(), f.Y.cpu(), te_u, te_i, seed=7)
+    print(json.dumps({"als_auc_drift": auc, "k": k, "iterations": 10}))
+    assert auc["cpu_fp32"] > 0.8, auc                    # the planted structure is learned
+    assert abs(auc["gpu_fp32"] - auc["cpu_fp32"]) < 2e-3, auc
+    assert abs(auc["gpu_bf16"] - auc["cpu_fp32"]) < 1e-2, auc
