@@ -320,11 +320,15 @@ class FeatureVectors:
             with self._lock.read():
                 n = self._n_rows
                 need_full = (self._dev is None or self._dirty_all or
-                             self._dev.shape[0] < self._host.shape[0])
+                             self._dev.shape[0] < max(n, 1))
                 if need_full:
-                    cap = self._host.shape[0]
-                    self._dev = torch.from_numpy(self._host.copy()).to(self.device)
-                    self._dev_valid = torch.from_numpy(self._host_valid.copy()).to(self.device)
+                    # the device copy tracks the used rows plus 1/8 headroom, not the host's
+                    # power-of-two capacity (a 20M-row store would otherwise hold 33.5M rows
+                    # of HBM); the read lock keeps writers out during the synchronous copies
+                    cap = min(self._host.shape[0], max(1024, n + n // 8))
+                    self._dev = torch.from_numpy(self._host[:cap]).to(self.device, copy=True)
+                    self._dev_valid = torch.from_numpy(self._host_valid[:cap]).to(self.device,
+                                                                                  copy=True)
                     self._dev_norm = self._dev.norm(dim=1)
                     self._dirty.clear()
                     self._dirty_all = False

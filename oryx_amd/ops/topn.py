@@ -114,8 +114,12 @@ class ItemIndex:
         b = b[order]
         n = int(rows.numel())
         ys = torch.zeros((max(n, 1), self.kp), dtype=torch.float32, device=dev)
-        if n:
-            ys[:n, :self.k] = mat[rows].to(dev)
+        # gathered in slices of 1M rows: a whole-matrix mat[rows] temporary would add another
+        # full copy of the item factors to the peak HBM of a rebuild (20 GB at 20M x 250)
+        step = 1 << 20
+        for lo in range(0, n, step):
+            hi = min(n, lo + step)
+            ys[lo:hi, :self.k] = mat[rows[lo:hi]].to(dev)
         rows = rows.to(dev)
         b = b.to(dev)
         self.Ys = ys
