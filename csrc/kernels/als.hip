@@ -202,14 +202,39 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));
   const int g = lane >> 4, fl = lane & 15;
-  // per-lane staging geometry (constant over chunks)
-  int srow[NPL], soff[NPL];
+  // per-lane staging geometry (constant over chunks).  KP > 64 (the one-wave-per-SIMD wide
+  // kernels at 512 registers): recomputed at each use from an opaque lane id -- a handful of
+  // integer ops -- instead of 2 x NPL registers held across the chunk loop (the fp32 rank-128
+  // kernel spilled them to scratch and reloaded them every chunk)
+  constexpr bool RECOMP = KP > 64;
+  int srow_[RECOMP ? 1 : NPL], soff_[RECOMP ? 1 : NPL];
+  if constexpr (!RECOMP) {
 #pragma unroll
-  for (int it = 0; it < NPL; ++it) {
-    const int sl = it * 64 + lane, r = sl / PPR, sc = sl % PPR;
-    srow[it] = r;
-    soff[it] = ((sc + CI::rot(r)) % PPR) * 8;
+    for (int it = 0; it < NPL; ++it) {
+      const int sl = it * 64 + lane, r = sl / PPR, sc = sl % PPR;
+      srow_[it] = r;
+      soff_[it] = ((sc + CI::rot(r)) % PPR) * 8;
+    }
   }
+  auto srow = [&](int it) -> int {
+    if constexpr (RECOMP) {
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      return (it * 64 + ln) / PPR;
+    } else {
+      return srow_[it];
+    }
+  };
+  auto soff = [&](int it) -> int {
+    if constexpr (RECOMP) {
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int sl = it * 64 + ln, r = sl / PPR, sc = sl % PPR;
+      return ((sc + CI::rot(r)) % PPR) * 8;
+    } else {
+      return soff_[it];
+    }
+  };
   // transposed-read byte offsets: operand pi, half h; lane 4q+p of group g reads row
   // 8g+4h+q, features pi*16 + 4p .. +3
   const int q = fl >> 2, pp = fl & 3;
@@ -222,7 +247,7 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
   auto load_meta = [&](int64_t c, int (&cols)[NPL], float& val) {
 #pragma unroll
     for (int it = 0; it < NPL; ++it) {
-      const int64_t ri = c + srow[it] < end ? c + srow[it] : end - 1;
+      const int64_t ri = c + srow(it) < end ? c + srow(it) : end - 1;
       cols[it] = p.col_idx[ri];
     }
     const int64_t vi = c + (lane & 31) < end ? c + (lane & 31) : end - 1;
@@ -234,7 +259,7 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
   auto gather = [&](const int (&cols)[NPL]) {
 #pragma unroll
     for (int it = 0; it < NPL; ++it) {
-      const __bf16* yr = p.Y + (int64_t)cols[it] * YS + soff[it];
+      const __bf16* yr = p.Y + (int64_t)cols[it] * YS + soff(it);
       stg[it] = *reinterpret_cast<const i32x4*>(yr);
       if constexpr (SPLIT) stgl[it] = *reinterpret_cast<const i32x4*>(yr + KP);
     }
@@ -1137,15 +1162,20 @@ __global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* _
     float* dst = ws + slot * ws_stride(KP);
     int t = 0;
 #pragma unroll
-    for (int pi = 0; pi < M; ++pi)
+    for (int pi = 0; pi < M; ++pi) {
+      // per-tile addresses formed here from opaque lane coordinates: hoisted out of the
+      // unrolled loops, the 2 x NT x 4 atomic addresses did not fit the register file at KP=128
+      int gg = g, ff = fl;
+      asm volatile("" : "+v"(gg), "+v"(ff));
 #pragma unroll
       for (int qi = 0; qi <= pi; ++qi, ++t)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const int i = pi * 16 + g * 4 + v, j = qi * 16 + fl;
+          const int i = pi * 16 + gg * 4 + v, j = qi * 16 + ff;
           atomicAdd(dst + i * KP + j, acc[t][v]);
           if (pi != qi) atomicAdd(dst + j * KP + i, acc[t][v]);
         }
+    }
     // after the reduction lane (g, fl) holds b[pi*16 + fl] for every pi: lane l adds
     // features l and l + 64
     if (lane < KP) atomicAdd(dst + KP * KP + lane, pick_bpart<M>(bpart, g));
