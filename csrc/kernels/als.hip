@@ -202,11 +202,11 @@ __device__ __forceinline__ void wave_accumulate(const AlsParams& p, int64_t beg,
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));
   const int g = lane >> 4, fl = lane & 15;
-  // per-lane staging geometry (constant over chunks).  KP > 64 (the one-wave-per-SIMD wide
+  // per-lane staging geometry (constant over chunks).  SPLIT and KP > 64 (the fp32 wide
   // kernels at 512 registers): recomputed at each use from an opaque lane id -- a handful of
   // integer ops -- instead of 2 x NPL registers held across the chunk loop (the fp32 rank-128
   // kernel spilled them to scratch and reloaded them every chunk)
-  constexpr bool RECOMP = KP > 64;
+  constexpr bool RECOMP = SPLIT && KP > 64;
   int srow_[RECOMP ? 1 : NPL], soff_[RECOMP ? 1 : NPL];
   if constexpr (!RECOMP) {
 #pragma unroll
