@@ -54,3 +54,11 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
 static inline int oryx_check_launch() {
   return hipGetLastError() == hipSuccess ? ORYX_OK : ORYX_ELAUNCH;
 }
+
+// Raises a kernel's dynamic-LDS limit (needed past 64 KB); false when the runtime refuses.
+template <class K>
+inline bool oryx_set_max_lds(K* kernel, int bytes) {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                             hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess;
+}
+

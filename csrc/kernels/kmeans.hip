@@ -1193,8 +1193,9 @@ int oryx_kmeans_assign(const void* X, const float* xnorm, const void* C, long lo
     const long long blocks = (n + BM - 1) / BM;                                               \
     static bool attr_set = false;                                                             \
     if (!attr_set && smem > 65536) {                                                          \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_assign_kernel<DKV, RT>),     \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, smem);                  \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_assign_kernel<DKV, RT>), \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess) \
+        return ORYX_ELAUNCH;                                                                  \
       attr_set = true;                                                                        \
     }                                                                                         \
     hipLaunchKernelGGL((kmeans_assign_kernel<DKV, RT>), dim3((unsigned)blocks), dim3(256),   \
@@ -1212,8 +1213,10 @@ int oryx_kmeans_assign(const void* X, const float* xnorm, const void* C, long lo
     const long long blocks = (n + NWV * 64 - 1) / (NWV * 64);                                 \
     static bool attr_set = false;                                                             \
     if (!attr_set && smem > 65536) {                                                          \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_assign_wide_kernel<DKV, NWV, PKV>), \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, smem);                  \
+      if (hipFuncSetAttribute(                                                                \
+              reinterpret_cast<const void*>(&kmeans_assign_wide_kernel<DKV, NWV, PKV>),       \
+              hipFuncAttributeMaxDynamicSharedMemorySize, smem) != hipSuccess)                \
+        return ORYX_ELAUNCH;                                                                  \
       attr_set = true;                                                                        \
     }                                                                                         \
     hipLaunchKernelGGL((kmeans_assign_wide_kernel<DKV, NWV, PKV>), dim3((unsigned)blocks),    \
@@ -1322,9 +1325,8 @@ int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, lo
     const long long blocks = (n + PPB - 1) / PPB;                                             \
     static bool attr_set = false;                                                             \
     if (!attr_set && smem > 65536) {                                                          \
-      hipFuncSetAttribute(                                                                    \
-          reinterpret_cast<const void*>(&kmeans_assign_wide_kernel<DKV, 4, true, true>),      \
-          hipFuncAttributeMaxDynamicSharedMemorySize, smem);                                  \
+      if (!oryx_set_max_lds(&kmeans_assign_wide_kernel<DKV, 4, true, true>, smem))            \
+        return ORYX_ELAUNCH;                                                                  \
       attr_set = true;                                                                        \
     }                                                                                         \
     hipLaunchKernelGGL((kmeans_assign_wide_kernel<DKV, 4, true, true>), dim3((unsigned)blocks), \
@@ -1352,8 +1354,7 @@ int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, lo
   if (fblocks > 2048) fblocks = 2048;
   static bool full_attr = false;
   if (!full_attr && smem > 65536) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&km_rescore_full<RP>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (!oryx_set_max_lds(&km_rescore_full<RP>, (int)smem)) return ORYX_ELAUNCH;
     full_attr = true;
   }
   hipLaunchKernelGGL((km_rescore_full<RP>), dim3((unsigned)fblocks), dim3(256), smem, s, Xf,
@@ -1392,10 +1393,8 @@ int oryx_kmeans_accumulate(const float* X, const int* assign, const float* mind,
                      (reinterpret_cast<unsigned long long>(X) % 16 == 0);
     static bool attr_set = false;
     if (!attr_set) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_accumulate_lds_kernel<true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&kmeans_accumulate_lds_kernel<false>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS);
+      if (!oryx_set_max_lds(&kmeans_accumulate_lds_kernel<true>, (int)LDS)) return ORYX_ELAUNCH;
+      if (!oryx_set_max_lds(&kmeans_accumulate_lds_kernel<false>, (int)LDS)) return ORYX_ELAUNCH;
       attr_set = true;
     }
     const dim3 grid((unsigned)blocks, (unsigned)slices);

@@ -817,8 +817,7 @@ int oryx_rdf_histogram(const void* Xb, int bin_bytes, long long n, int P, const 
 #define HIST_LAUNCH(BT, C, L)                                                                 \
   do {                                                                                        \
     if (L && smem > 65536) {                                                                  \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&rdf_histogram<BT, C, L>),           \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);             \
+      if (!oryx_set_max_lds(&rdf_histogram<BT, C, L>, (int)smem)) return ORYX_ELAUNCH;     \
     }                                                                                         \
     hipLaunchKernelGGL((rdf_histogram<BT, C, L>), grid, dim3(256), smem, s,                  \
                        reinterpret_cast<const BT*>(Xb), n, P, label, y, S, weight, node_of,   \
