@@ -901,7 +901,9 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
   static const bool staged_ok =
       !(getenv("ORYX_RDF_HIST") && atoi(getenv("ORYX_RDF_HIST")) == 0);
   if (staged_ok && bin_bytes == 1 && n * (long long)P < (1LL << 34) && n * (long long)P >= 4) {
-    const int ndw = (P + 3) / 4 + 1;                 // dwords covering any row alignment
+    // dwords covering any row alignment; a row pitch that is a multiple of 4 bytes (the
+    // padded pitch of ops/rdf.py) starts every row on a dword, so the pitch itself suffices
+    const int ndw = P % 4 == 0 ? P / 4 : (P + 3) / 4 + 1;
     const int rsw = ndw | 1;
     const long long smem_st = per_node_bytes + ((Fs + 3) & ~3) * 4LL + 256LL * rsw * 4;
     if (smem_st <= 64 * 1024) {
