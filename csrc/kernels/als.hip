@@ -1689,7 +1689,27 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
               reinterpret_cast<__bf16*>(Xb), n_work, k, lambda, alpha, implicit, fail_count,
               n_seg > 0 ? long_slot : nullptr, ws};
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int max_blocks = 256 * 16;
+  // grid caps (the waves loop over rows with a stride of 4 x grid).  The 2-wave-per-SIMD panel
+  // kernels run best as one resident generation, 2 blocks per CU: 512 blocks on MI355X
+  // measured 2.14-2.16 ms per rank-64 iteration against 2.18-2.19 ms at 4096
+  // (profiles/r2_als_grid_sweep.txt); the one-wave wide kernels and als_partial keep 4096
+  // (rank 128 fp32: 13.86 ms at 4096, 14.0 at 512).  ORYX_ALS_MAX_BLOCKS overrides both.
+  static const int env_blocks = [] {
+    const char* e = getenv("ORYX_ALS_MAX_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return v >= 64 && v <= 65536 ? v : 0;
+  }();
+  static const int resident_panel_blocks = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    return 2 * cus;
+  }();
+  const int max_blocks = env_blocks ? env_blocks : 256 * 16;
+  const bool deep = g_als_variant >= 2 && g_als_variant <= 4;
+  const int panel_blocks = env_blocks ? env_blocks : (deep ? resident_panel_blocks : 256 * 16);
   if (n_seg > 0) {
     if (hipMemsetAsync(ws, 0, sizeof(float) * (size_t)n_long * ws_stride(kp), s) != hipSuccess)
       return ORYX_ELAUNCH;
@@ -1722,7 +1742,8 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
 #define WAVE_CASE(KPV)                                                                \
   case KPV: {                                                                         \
     int blocks = (n_work + 3) / 4;                                                    \
-    if (blocks > max_blocks) blocks = max_blocks;                                     \
+    if (blocks > (split ? max_blocks : panel_blocks))                                 \
+      blocks = split ? max_blocks : panel_blocks;                                     \
     if (split)                                                                        \
       hipLaunchKernelGGL((als_solve_wave<KPV, false, true>), dim3(blocks), dim3(256), 0, \
                          s, p, nullptr);                                              \
