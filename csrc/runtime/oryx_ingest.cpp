@@ -36,6 +36,12 @@ namespace {
 class FlatIndex {
  public:
   FlatIndex() { rehash(1024); }
+  // grow once to hold about n keys (load <= 1/2) instead of doubling through every size
+  void reserve(size_t n) {
+    size_t cap = slots_.size();
+    while (cap < 2 * n) cap *= 2;
+    if (cap > slots_.size()) rehash(cap);
+  }
   // value of key k, or -1
   int32_t find(std::string_view k) const {
     const uint64_t h = hash(k.data(), k.size());
@@ -389,6 +395,12 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
   }
   std::vector<RatingChunk> ch((size_t)P);
   if (P == 1) {
+    // a fresh dictionary (the speed layer's per-interval ones) is sized for the batch up front:
+    // at most one new user and item per line (~24 bytes per line in practice; capped so an
+    // 8 MB block of few distinct IDs does not allocate a table for 350k)
+    const size_t est = std::min<size_t>((size_t)(len / 24) + 16, (size_t)1 << 17);
+    if (du->keys.empty()) du->map.reserve(est);
+    if (di != du && di->keys.empty()) di->map.reserve(est);
     ch[0].gu = du;
     ch[0].gi = di;
     ch[0].parse(buf, buf + len, default_ts, strict != 0);
