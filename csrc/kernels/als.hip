@@ -25,29 +25,7 @@
 //     grid-stride loop so long rows start early and short rows fill the tail.
 // Output is the fp32 solution plus an optional bf16 copy (the operand of the next half-step).
 
-#include "common.h"
-
-#include <type_traits>
-
-// compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>) (or descending); the body
-// sees its index as a constant, so register arrays indexed by it never fall back to scratch
-// (#pragma unroll gives up on very large bodies)
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (N > 0) {
-    static_for<N - 1>(f);
-    f(std::integral_constant<int, N - 1>{});
-  }
-}
-template <int N, typename F>
-__device__ __forceinline__ void static_for_desc(F&& f) {
-  if constexpr (N > 0) {
-    f(std::integral_constant<int, N - 1>{});
-    static_for_desc<N - 1>(f);
-  }
-}
-
-typedef __attribute__((ext_vector_type(2))) float f32x2;
+#include "als_common.h"
 
 // 1: the next row's first chunk gathers are issued during this row's factorization
 #ifndef ORYX_ALS_XROW_PREFETCH
@@ -64,42 +42,6 @@ typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 namespace {
 
-struct AlsParams {
-  const int64_t* row_ptr;  // [n_rows + 1]
-  const int32_t* row_ids;  // [n_work] (nullable: rows 0..n_work-1)
-  const int32_t* col_idx;  // [nnz]
-  const float* vals;       // [nnz]
-  const __bf16* Y;         // [n_cols][KP]
-  const float* YtY;        // [KP][KP] (zeros for explicit feedback)
-  float* X;                // [n_rows][KP]
-  __bf16* Xb;              // [n_rows][KP] (nullable)
-  int n_work;
-  int k;
-  float lambda;
-  float alpha;
-  int implicit;
-  int* fail_count;         // nullable: incremented when a pivot is not positive
-  // split long rows: work item w with long_slot[w] >= 0 takes its Gramian, b and count from
-  // ws[slot] (summed beforehand by als_partial over fixed-size segments of the row)
-  const int32_t* long_slot;  // [n_work] (nullable)
-  const float* ws;           // [n_long][ws_stride(KP)]
-};
-
-// fp32 factor mode (SPLIT kernels): every factor row is stored as 2*KP bf16, the hi part
-// bf16(y) followed by the lo part bf16(y - hi), so hi + lo = y to ~2^-17 relative; the Gramian
-// takes s_hi*y_hi + s_lo*y_hi + s_hi*y_lo (s = c*y in fp32, split the same way).  Y, Xb and the
-// gathered operands then have a row stride of 2*KP.
-template <bool SPLIT, int KP>
-__device__ __forceinline__ void store_xb(__bf16* Xb, int64_t row, int c, float x) {
-  const __bf16 h = (__bf16)x;
-  if constexpr (SPLIT) {
-    Xb[row * 2 * KP + c] = h;
-    Xb[row * 2 * KP + KP + c] = (__bf16)(x - (float)h);
-  } else {
-    Xb[row * KP + c] = h;
-  }
-}
-
 // bf16 factor mode: the MFMA A operand is bf16(c_i * y_i) (bf16 operands, fp32 accumulation;
 // modelled exactly by solve_rows_reference(..., bf16_operands=True)).  ORYX_ALS_EXACT_C=1
 // builds split c_i * y_i into bf16 hi + lo there too (one extra MFMA per tile, ~18% slower
@@ -109,47 +51,10 @@ __device__ __forceinline__ void store_xb(__bf16* Xb, int64_t row, int c, float x
 #endif
 constexpr bool kExactC = ORYX_ALS_EXACT_C != 0;
 
-// workspace record of one split row: full symmetric A [KP*KP], b [KP], count, padded to 16 B
-__host__ __device__ constexpr int ws_stride(int kp) { return (kp * kp + kp + 1 + 3) / 4 * 4; }
-
-__device__ __forceinline__ void als_weights(float r, float alpha, int implicit, float& wa,
-                                            float& wb, float& cnt) {
-  if (implicit) {
-    const float c1 = alpha * fabsf(r);
-    wa = c1;
-    wb = r > 0.f ? 1.f + c1 : 0.f;
-    cnt = r > 0.f ? 1.f : 0.f;
-  } else {
-    wa = 1.f;
-    wb = r;
-    cnt = 1.f;
-  }
-}
-
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
 constexpr int TS = 40;  // LDS row stride (bf16 elements) of the transposed chunk: 32 + 8 pad
 
 // ------------------------------------------------------------------ wave-per-row kernel
 
-// Gathered chunk image in LDS: 32 rating rows x KP bf16, row-major (KP*2 bytes per row),
-// written lane-linearly (lane l of staging instruction `it` owns 16-byte slot it*64 + l).  The
-// 16-byte chunks of row r are rotated by rot(r) so that the ds_read_b64_tr_b16 operand reads
-// (4 ratings x 16 features per 16-lane group) are bank-conflict free (KP 32/64/96/128) or
-// 2-way (others); the rotation is applied on the GLOBAL side: slot (r, sc) holds feature
-// chunk (sc + rot(r)) % PPR.  Constants found by exhaustive search over the bank model.
-template <int KP>
-struct ChunkImage {
-  static constexpr int PPR = KP / 8;              // 16-byte chunks per row
-  static constexpr int NPL = KP / 16;             // staging slots per lane (32*PPR/64)
-  static constexpr int BYTES = 32 * KP * 2;
-  static constexpr int SM = KP == 64 ? 1 : KP == 128 ? 2 : 0;
-  static constexpr int ST = KP == 64 ? 2 : KP == 128 ? 4 : (KP == 32 || KP == 96) ? 1 : 0;
-  __device__ static constexpr int rot(int r) { return (r * SM + (r >> 2) * ST) % PPR; }
-};
 
 template <int KP, bool SPLIT = false>
 struct WaveSmem {
@@ -587,23 +492,6 @@ struct GatherRing {
   }
 };
 
-// sum the per-lane b partials over the 4 lane groups; lane f then takes feature f (+64h)
-template <int M>
-__device__ __forceinline__ void reduce_bpart(float (&bpart)[M]) {
-#pragma unroll
-  for (int pi = 0; pi < M; ++pi) {
-    bpart[pi] += __shfl_xor(bpart[pi], 16, 64);
-    bpart[pi] += __shfl_xor(bpart[pi], 32, 64);
-  }
-}
-
-template <int M>
-__device__ __forceinline__ float pick_bpart(const float (&bpart)[M], int sel) {
-  float r = bpart[0];
-#pragma unroll
-  for (int pi = 1; pi < M; ++pi) r = sel == pi ? bpart[pi] : r;
-  return r;
-}
 
 // PROF: accumulate per-phase shader-clock cycles of every row into prof[0..6] (analysis
 // builds only; see scripts/als_phase_profile.py)
@@ -1654,7 +1542,8 @@ __global__ __launch_bounds__(256) void pair_dots(const float* __restrict__ X,
 
 }  // namespace
 
-// KP <= 64 solve kernel: 2 = als_solve_panel with three chunks of gathers in flight at 2 waves
+// KP <= 64 solve kernel: 5 = als_solve_batch (als_batch.hip: four rows per wave, batched
+// block-LDL^T), 2 = als_solve_panel with three chunks of gathers in flight at 2 waves
 // per SIMD, 0 = als_solve_panel with one chunk in flight at 3 waves per SIMD, 1 =
 // als_solve_wave (register column Cholesky), 3 (default) / 4 = variant 2 with the
 // factorisation at raised issue priority (s_setprio 2 / 3: 2-6% faster half-steps than 2)
@@ -1665,10 +1554,12 @@ static int g_als_wide_variant = 0;
 extern "C" {
 
 int oryx_als_set_variant(int v) {
-  if (v < 0 || v > 4) return ORYX_EINVAL;
+  if (v < 0 || v > 5) return ORYX_EINVAL;
   g_als_variant = v;
   return ORYX_OK;
 }
+
+int oryx_als_get_variant() { return g_als_variant; }
 
 int oryx_als_set_wide_variant(int v) {
   if (v < 0 || v > 1) return ORYX_EINVAL;
@@ -1737,6 +1628,13 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
       default:
         return ORYX_EINVAL;
     }
+  }
+  if (g_als_variant == 5 && !split && kp <= 64) {
+    // four rows per wave, one wave per SIMD: one resident block per CU
+    const int cus = resident_panel_blocks / 2;
+    if (const int rc = oryx_als::batch_solve_launch(p, kp, env_blocks ? env_blocks : cus, s))
+      return rc;
+    return ORYX_OK;
   }
   switch (kp) {
 #define WAVE_CASE(KPV)                                                                \
@@ -1865,7 +1763,7 @@ int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const fl
   return oryx_check_launch();
 }
 
-int oryx_kernels_version() { return 11; }
+int oryx_kernels_version() { return 12; }
 
 int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 

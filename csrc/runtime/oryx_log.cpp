@@ -211,7 +211,8 @@ int64_t scan_segment(const std::string& path, int64_t base, int64_t* end_pos,
   // 4 MB block reads; a frame straddling a block is re-read from its start
   std::vector<uint8_t> buf(4u << 20);
   for (;;) {
-    ssize_t got = pread(fd, buf.data(), buf.size(), pos);
+    const size_t cap = buf.size();
+    ssize_t got = pread(fd, buf.data(), cap, pos);
     if (got < (ssize_t)kHeader) break;
     size_t at = 0;
     bool bad = false, straddle = false;
@@ -236,11 +237,14 @@ int64_t scan_segment(const std::string& path, int64_t base, int64_t* end_pos,
     }
     pos += (int64_t)at;
     if (bad) break;
-    if (!straddle && at == 0) break;
-    if (!straddle && (size_t)got < buf.size()) {
-      // short read: the rest (if any) is a torn tail
-      if (at + kHeader > (size_t)got) break;
+    // a frame that runs past a short read ends where the file ends: a torn tail (a writer
+    // that died mid-append); only a full block (or one just grown for a large frame) is
+    // re-read from the frame's start
+    if (straddle) {
+      if ((size_t)got < cap) break;
+      continue;
     }
+    if (at == 0 || (size_t)got < cap) break;
   }
   close(fd);
   *end_pos = pos;
@@ -690,8 +694,9 @@ long long oryx_log_append_values_gap(void* h, int partition, const char* key, in
 // to `end_offset` (exclusive) appended to `out` as `value '\n'`, reading the segment files in
 // 4 MB blocks (one pread per block instead of two per record).  Returns the number of
 // records consumed (fewer than asked when `out` is full: call again), or -3 on a corrupt
-// frame.  *flags gets bit 0 when a record had a key and bit 1 when a value contained a
-// newline (the caller then uses the per-record path for those semantics).
+// frame.  *flags gets bit 0 when a record had a key and bit 1 when a value contained a newline
+// (the caller then uses the per-record path for those semantics), and bit 2 when the next
+// record alone is larger than out_cap (nothing delivered; *out_used is the size it needs).
 long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long long out_cap,
                                 long long* out_used, int* flags) {
   auto* r = static_cast<Reader*>(rh);
@@ -703,7 +708,8 @@ long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long 
   if (r->fd < 0) reader_seek(r, r->next_offset);
   while (r->next_offset < end_offset) {
     if (r->fd < 0) break;
-    ssize_t got = pread(r->fd, buf.data(), buf.size(), r->pos);
+    const size_t cap = buf.size();
+    ssize_t got = pread(r->fd, buf.data(), cap, r->pos);
     size_t at = 0;
     bool need_more = false;
     while (got > 0 && at + kHeader <= (size_t)got && r->next_offset < end_offset) {
@@ -732,7 +738,13 @@ long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long 
       }
       if ((long long)off >= end_offset) { r->next_offset = end_offset; break; }
       if (used + (long long)vlen + 1 > out_cap) {
-        *out_used = used;
+        // buffer full; with nothing delivered yet, report the size this record needs
+        if (count == 0) {
+          *flags |= 4;
+          *out_used = (long long)vlen + 1;
+        } else {
+          *out_used = used;
+        }
         return count;
       }
       if (klen != kNullKey) *flags |= 1;
@@ -747,7 +759,11 @@ long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long 
       ++count;
     }
     if (r->next_offset >= end_offset) break;
-    if (need_more) continue;
+    // a frame cut off by a short read is still being written (or torn): deliver what there is
+    if (need_more) {
+      if (got < (ssize_t)cap) break;
+      continue;
+    }
     if (at == 0) {
       // end of this segment file: move to the next one (records up to end_offset exist)
       std::vector<int64_t> segs = list_segments(dir);
@@ -758,6 +774,7 @@ long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long 
           r->seg_base = b;
           r->pos = 0;
           r->fd = open(seg_name(dir, b).c_str(), O_RDONLY);
+          r->blk_pos = -1;   // the poll read-ahead block holds the previous file's bytes
           rolled = true;
           break;
         }

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import math
 import threading
-from typing import Callable, Collection, Dict, Iterable, List, Optional, Sequence, Set
+from typing import Callable, Collection, Dict, Iterable, List, Optional, Sequence, Set, Tuple
 
 import numpy as np
 import torch
@@ -80,7 +80,10 @@ class FeatureVectors:
         self._dev_part = None
         self.version = 0
         # rows changed since the last take_index_dirty() (serving ItemIndex); None = all
-        self._idx_dirty: Optional[Set[int]] = None
+        # rows changed since each index consumer's last take_index_state (token -> rows; None:
+        # everything may have changed).  One set per consumer: two indexes over one store
+        # (e.g. a single-GPU and an item-sharded one) must not consume each other's changes
+        self._idx_dirty: Dict[int, Optional[Set[int]]] = {}
         # native id -> row mirror (ingest.RowMap) for bulk lookups, built on first use and
         # then kept current from a journal of id insertions / removals
         self._rowmap = None
@@ -121,7 +124,7 @@ class FeatureVectors:
             valid[:self._host_valid.shape[0]] = self._host_valid
             self._host, self._host_valid = host, valid
             self._dirty_all = True
-            self._idx_dirty = None
+            self._idx_mark_all()
         self._n_rows += 1
         self._ids.append(None)
         return row
@@ -142,18 +145,43 @@ class FeatureVectors:
             self._host[row] = v
             self._host_valid[row] = True
             self._dirty.add(row)
-            if self._idx_dirty is not None:
-                self._idx_dirty.add(row)
+            self._idx_mark((row,))
             self.version += 1
 
-    def take_index_dirty(self) -> Optional[np.ndarray]:
-        """Rows changed since the previous call (None: everything may have changed)."""
+    def _idx_mark(self, rows) -> None:
+        for d in self._idx_dirty.values():
+            if d is not None:
+                d.update(rows)
+
+    def _idx_mark_all(self) -> None:
+        for t in self._idx_dirty:
+            self._idx_dirty[t] = None
+
+    def register_index_consumer(self) -> int:
+        """A token for :meth:`take_index_state`; its first call reports everything."""
         with self._lock.write():
-            d = self._idx_dirty
-            self._idx_dirty = set()
+            token = len(self._idx_dirty) + 1
+            while token in self._idx_dirty:
+                token += 1
+            self._idx_dirty[token] = None
+            return token
+
+    def take_index_dirty(self, token: int = 0) -> Optional[np.ndarray]:
+        """Rows changed since the previous call (None: everything may have changed)."""
+        return self.take_index_state(token)[1]
+
+    def take_index_state(self, token: int = 0) -> Tuple[int, Optional[np.ndarray]]:
+        """(version, rows changed since this consumer's previous call), read together under
+        the write lock (None rows: everything may have changed).  A consumer that then takes
+        :meth:`device_view` sees at least these changes; a write landing in between shows up
+        again in the next call's rows, so re-applying it is all that can happen."""
+        with self._lock.write():
+            ver = self.version
+            d = self._idx_dirty.get(token)
+            self._idx_dirty[token] = set()
         if d is None:
-            return None
-        return np.fromiter(d, dtype=np.int64, count=len(d))
+            return ver, None
+        return ver, np.fromiter(d, dtype=np.int64, count=len(d))
 
     def _ensure_capacity(self, rows: int) -> None:
         cap = self._host.shape[0]
@@ -167,7 +195,7 @@ class FeatureVectors:
         valid[:self._host_valid.shape[0]] = self._host_valid
         self._host, self._host_valid = host, valid
         self._dirty_all = True
-        self._idx_dirty = None
+        self._idx_mark_all()
 
     def set_vectors(self, ids: Sequence[str], matrix: np.ndarray) -> None:
         """Bulk insert/update (model loading): new IDs get one contiguous block of rows."""
@@ -194,7 +222,7 @@ class FeatureVectors:
                         self._host[row] = v
                         self._host_valid[row] = True
                         self._dirty.add(row)
-                    self._idx_dirty = None
+                    self._idx_mark_all()
                     self.version += 1
                     return
                 start = self._n_rows
@@ -211,11 +239,10 @@ class FeatureVectors:
             self._host_valid[rows] = True
             if len(rows) > max(1024, self._n_rows // 8):
                 self._dirty_all = True
-                self._idx_dirty = None
+                self._idx_mark_all()
             else:
                 self._dirty.update(rows.tolist())
-                if self._idx_dirty is not None:
-                    self._idx_dirty.update(rows.tolist())
+                self._idx_mark(rows.tolist())
             self.version += 1
 
     def remove_vector(self, id_: str) -> None:
@@ -233,8 +260,7 @@ class FeatureVectors:
             self._ids[row] = None
             self._free.append(row)
             self._dirty.add(row)
-            if self._idx_dirty is not None:
-                self._idx_dirty.add(row)
+            self._idx_mark((row,))
             self.version += 1
 
     def native_rows(self, d) -> np.ndarray:

@@ -514,10 +514,27 @@ def drain_up_blocks(model, updates) -> int:
 
 
 def apply_up_parsed(model, kinds, ids, vecs, known, messages=None) -> None:
-    """Apply parsed ``UP`` rows (see :func:`apply_up_batch`); kind-2 rows are re-parsed from
-    ``messages`` on the per-message path."""
+    """Apply parsed ``UP`` rows (see :func:`apply_up_batch`) in message order; kind-2 rows
+    (the native parser's rejects) are re-parsed from ``messages`` on the per-message path.
+
+    The batch is cut at every kind-2 row, so an ID updated both by a rejected row and a parsed
+    row ends with whichever came last in the log, as on the per-message path."""
+    kinds = np.asarray(kinds)
+    bad = np.nonzero(kinds == 2)[0].tolist()
+    if bad and messages is None:
+        raise ValueError("unparseable UP rows without their messages")
+    lo = 0
+    for cut in bad + [len(kinds)]:
+        if cut > lo:
+            _apply_parsed_run(model, kinds, ids, vecs, known, lo, cut)
+        if cut < len(kinds):
+            _apply_up_message(model, messages[cut])
+        lo = cut + 1
+
+
+def _apply_parsed_run(model, kinds, ids, vecs, known, lo: int, hi: int) -> None:
     for kind, setter in ((0, "set_user_vectors"), (1, "set_item_vectors")):
-        sel = np.nonzero(kinds == kind)[0]
+        sel = lo + np.nonzero(kinds[lo:hi] == kind)[0]
         if not len(sel):
             continue
         # last occurrence of each ID wins
@@ -532,20 +549,19 @@ def apply_up_parsed(model, kinds, ids, vecs, known, messages=None) -> None:
             for j in sel.tolist():
                 if known[j]:
                     model.add_known_items(ids[j], known[j])
-    bad = np.nonzero(kinds == 2)[0].tolist()
-    if bad and messages is None:
-        raise ValueError("unparseable UP rows without their messages")
-    for j in bad:
-        update = text.read_json(messages[j])
-        vector = np.asarray(update[2], dtype=np.float32)
-        if update[0] == "X":
-            model.set_user_vector(str(update[1]), vector)
-            if len(update) > 3 and hasattr(model, "add_known_items"):
-                model.add_known_items(str(update[1]), [str(x) for x in update[3]])
-        elif update[0] == "Y":
-            model.set_item_vector(str(update[1]), vector)
-        else:
-            raise ValueError("Bad message: %r" % (messages[j],))
+
+
+def _apply_up_message(model, message) -> None:
+    update = text.read_json(message)
+    vector = np.asarray(update[2], dtype=np.float32)
+    if update[0] == "X":
+        model.set_user_vector(str(update[1]), vector)
+        if len(update) > 3 and hasattr(model, "add_known_items"):
+            model.add_known_items(str(update[1]), [str(x) for x in update[3]])
+    elif update[0] == "Y":
+        model.set_item_vector(str(update[1]), vector)
+    else:
+        raise ValueError("Bad message: %r" % (message,))
 
 
 class ALSServingModelManager(AbstractServingModelManager):

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 11
+KERNELS_ABI_VERSION = 12
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -157,8 +157,10 @@ def _load_kernels():
                            "build: rebuild with python -m oryx_amd._build --force)"
                            % (path, got, KERNELS_ABI_VERSION))
     # ORYX_ALS_VARIANT selects the KP<=64 solve kernel for A/B runs (csrc/kernels/als.hip:
-    # 2 = panel Cholesky + 3-deep gather ring (default), 0 = panel + 1-deep, 1 = register)
+    # 5 = four rows per wave, batched block LDL^T (als_batch.hip), 3 = panel Cholesky at
+    # raised priority, 2 = panel + 3-deep gather ring, 0 = panel + 1-deep, 1 = register)
     _sig(lib, "oryx_als_set_variant", c_i, [c_i])
+    _sig(lib, "oryx_als_get_variant", c_i, [])
     lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "3")))
     # ORYX_ALS_WIDE_VARIANT: 64 < k <= 128 solve (0 = als_solve_wide, 1 = als_solve_block)
     _sig(lib, "oryx_als_set_wide_variant", c_i, [c_i])

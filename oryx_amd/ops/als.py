@@ -15,6 +15,7 @@ Normal equations (Spark MLlib's ALS, which the reference invokes at
 
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from dataclasses import dataclass
@@ -226,6 +227,18 @@ def gramian(x: torch.Tensor) -> torch.Tensor:
         native.check(rc, "oryx_gramian_f32")
         return out
     return x.t().matmul(x)
+
+
+@contextlib.contextmanager
+def solve_variant(v: int):
+    """Temporarily select the KP <= 64 solve kernel (``ORYX_ALS_VARIANT`` values; A/B tests)."""
+    lib = native.require_kernels()
+    old = lib.oryx_als_get_variant()
+    native.check(lib.oryx_als_set_variant(int(v)), "oryx_als_set_variant")
+    try:
+        yield
+    finally:
+        lib.oryx_als_set_variant(old)
 
 
 def _use_kernel(device: torch.device, kp: int) -> bool:

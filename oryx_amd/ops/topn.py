@@ -60,8 +60,13 @@ class ItemIndex:
     (d, N) keeps only the store rows r with r % N == d, on ``device`` (item sharding over
     several GPUs: :class:`ShardedItemIndex`)."""
 
-    def __init__(self, store, num_buckets: int, device=None, shard: Tuple[int, int] = (0, 1)):
+    def __init__(self, store, num_buckets: int, device=None, shard: Tuple[int, int] = (0, 1),
+                 managed: bool = False):
         self.store = store
+        # managed: a ShardedItemIndex takes the store's changes once and hands every shard
+        # its share; the shard never consumes the store's dirty set itself
+        self._managed = bool(managed)
+        self._token = None if managed else store.register_index_consumer()
         self.k = store.k
         self.kp = _kp(self.k)
         self.device = torch.device(device) if device is not None else store.device
@@ -81,17 +86,22 @@ class ItemIndex:
         self.rebuilds = 0
 
     # ------------------------------------------------------------------ maintenance
-    def refresh(self) -> None:
+    def refresh(self, state: Optional[Tuple[int, Optional[np.ndarray]]] = None) -> None:
+        """Bring the index up to the store.  ``state`` = (version, changed rows) taken by the
+        owning :class:`ShardedItemIndex`; otherwise this index takes them itself -- version and
+        rows together, before the device view, so no write can fall between them."""
         st = self.store
-        if self.version == st.version and self.Ys is not None:
-            return
-        with self._lock:
-            if self.version == st.version and self.Ys is not None:
+        if state is None:
+            if self._managed or (self.version == st.version and self.Ys is not None):
                 return
+        with self._lock:
+            if state is None:
+                if self.version == st.version and self.Ys is not None:
+                    return
+                state = st.take_index_state(self._token)
+            ver, dirty = state
             mat, valid, _ = st.device_view()
             parts = st.device_partitions()
-            ver = st.version
-            dirty = st.take_index_dirty()
             if self.Ys is None or dirty is None or not self._update_in_place(mat, valid, parts,
                                                                              dirty):
                 self._rebuild(mat, valid, parts)
@@ -292,20 +302,36 @@ class ShardedItemIndex:
     def __init__(self, store, num_buckets: int, devices: Sequence):
         import concurrent.futures
         self.store = store
-        self.shards = [ItemIndex(store, num_buckets, device=dv, shard=(j, len(devices)))
+        self.shards = [ItemIndex(store, num_buckets, device=dv, shard=(j, len(devices)),
+                                 managed=True)
                        for j, dv in enumerate(devices)]
         self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=len(devices),
                                                            thread_name_prefix="oryx-topn")
+        self._lock = threading.Lock()
+        self.version = -1
+        self._token = store.register_index_consumer()
 
     @property
     def n(self) -> int:
         return sum(sh.n for sh in self.shards)
 
     def refresh(self) -> None:
-        for f in [self._pool.submit(sh.refresh) for sh in self.shards]:
-            f.result()
+        """Take the store's changes ONCE and give every shard the same (version, rows): each
+        keeps the rows r % N == d of them (a shard consuming the shared dirty set itself would
+        leave the others with nothing and stale rows)."""
+        st = self.store
+        if self.version == st.version and all(sh.Ys is not None for sh in self.shards):
+            return
+        with self._lock:
+            if self.version == st.version and all(sh.Ys is not None for sh in self.shards):
+                return
+            state = st.take_index_state(self._token)
+            for f in [self._pool.submit(sh.refresh, state) for sh in self.shards]:
+                f.result()
+            self.version = state[0]
 
     def scan(self, queries: Sequence[TopNQuery]) -> List[Tuple[np.ndarray, np.ndarray]]:
+        self.refresh()
         parts = [f.result() for f in [self._pool.submit(sh.scan, queries)
                                        for sh in self.shards]]
         out = []

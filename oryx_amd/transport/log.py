@@ -366,14 +366,16 @@ class PartitionReader:
                 raise LogCorruptionError(lib.oryx_log_last_error().decode())
             if n < 0:
                 raise IOError(lib.oryx_log_last_error().decode())
-            if flags.value:
+            if flags.value & 3:
                 self.seek(start)
                 return None, 0
+            if flags.value & 4:
+                # the next record alone is larger than the buffer: the native call reported
+                # the size it needs
+                cap = max(int(used.value), 2 * cap)
+                buf = ctypes.create_string_buffer(cap)
+                continue
             if n == 0:
-                if used.value == 0 and cap < (1 << 30):
-                    cap *= 4           # one record larger than the buffer
-                    buf = ctypes.create_string_buffer(cap)
-                    continue
                 break
             chunks.append(ctypes.string_at(buf, used.value))
             total += n

@@ -250,3 +250,66 @@ def test_reference_solve_fp64_cpu():
         s64 = als_ops.solve_rows_reference(csr, y.double(), yty, 6, 0.1, 2.0, implicit)
         assert s64.dtype == torch.float64
         assert torch.allclose(s32.double(), s64, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [10, 16, 32, 40, 48, 64])
+@pytest.mark.parametrize("implicit", [True, False])
+@pytest.mark.parametrize("split_rows", [False, True])
+def test_batched_kernel_vs_reference(cuda, k, implicit, split_rows):
+    """Variant 5 (als_batch.hip: four rows per wave, batched block LDL^T on DPP + fp32 MFMA)
+    against the fp64 model of the bf16 operand arithmetic, with the same bound as the panel
+    kernel; long rows split into als_partial segments go through the workspace path."""
+    n_rows = 701      # not a multiple of the 4-row batch: the tail batch is padded
+    csr, y, kp = _problem(n_rows, 400, 30000, k, 300 + k, "cpu", neg=implicit)
+    if split_rows:
+        counts = csr.row_ptr[1:] - csr.row_ptr[:-1]
+        r = torch.repeat_interleave(torch.arange(n_rows), counts)
+        csr = als_ops.build_csr(r, csr.cols, csr.vals, n_rows, 400, split_threshold=50,
+                                split_segment=24)
+        assert csr.n_long > 0
+    csr = csr.to(cuda)
+    yb = y.to(cuda).to(torch.bfloat16)
+    yty = als_ops.gramian(yb.float()) if implicit else None
+    x = torch.full((n_rows, kp), 7.0, device=cuda)
+    xb = torch.zeros(n_rows, kp, device=cuda, dtype=torch.bfloat16)
+    fails = torch.zeros(1, dtype=torch.int32, device=cuda)
+    with als_ops.solve_variant(5):
+        als_ops.solve_rows(csr, yb, yty, x, xb, k, 0.05, 1.5, implicit, fail_count=fails)
+    torch.cuda.synchronize()
+    rows = csr.order.long()
+    ref64 = als_ops.solve_rows_reference(csr, yb.double(), yty, k, 0.05, 1.5, implicit,
+                                         bf16_operands=True)
+    ref32 = als_ops.solve_rows_reference(csr, yb.float(), yty, k, 0.05, 1.5, implicit,
+                                         bf16_operands=True)
+    e_kernel = _row_rel_err(x, ref64, rows)
+    e_torch = _row_rel_err(ref32, ref64, rows)
+    assert int(fails.item()) == 0
+    assert bool((e_kernel <= torch.clamp(4 * e_torch, min=1e-3)).all()), (
+        e_kernel.max().item(), e_torch.max().item())
+    if kp > k:
+        assert x[rows, k:].abs().max().item() == 0.0
+    # rows without ratings are not touched
+    empty = torch.ones(n_rows, dtype=torch.bool, device=cuda)
+    empty[rows] = False
+    if bool(empty.any()):
+        assert bool((x[empty] == 7.0).all())
+    assert torch.equal(xb[rows], x[rows].to(torch.bfloat16))
+
+
+@pytest.mark.gpu
+def test_batched_kernel_flags_singular_rows(cuda):
+    """Explicit feedback with lambda = 0 and a single rating per row: rank-1 Gramians, so
+    every real row reports a failed pivot exactly once (the padded tail batch does not)."""
+    n_rows, n_cols, k = 9, 30, 16
+    rows = torch.arange(n_rows)
+    cols = torch.arange(n_rows) * 3
+    vals = torch.ones(n_rows)
+    csr = als_ops.build_csr(rows, cols, vals, n_rows, n_cols).to(cuda)
+    yb = (torch.randn(n_cols, 16) * 0.3).to(cuda).to(torch.bfloat16)
+    x = torch.zeros(n_rows, 16, device=cuda)
+    fails = torch.zeros(1, dtype=torch.int32, device=cuda)
+    with als_ops.solve_variant(5):
+        als_ops.solve_rows(csr, yb, None, x, None, k, 0.0, 1.0, False, fail_count=fails)
+    torch.cuda.synchronize()
+    assert int(fails.item()) == n_rows

@@ -479,6 +479,14 @@ def test_item_sharded_index_matches_single_index(cuda):
             Y[ch] *= 1.25
             for r in ch:
                 fv.set_vector("I%d" % r, Y[r])
+            # in-place item updates reach EVERY shard, whichever index refreshes first
+            sharded.refresh()
+            fresh = topn.ShardedItemIndex(fv, nb, [cuda, cuda, cuda])
+            fresh.refresh()
+            for sh, fr in zip(sharded.shards, fresh.shards):
+                assert sh.n == fr.n
+                torch.testing.assert_close(sh.Ys[:sh.n], fr.Ys[:fr.n])
+            fresh.close()
     assert sharded.n == one.n
     sharded.close()
     m = ALSServingModel(k, True, 1.0, device=torch.device(cuda), scan_devices=[cuda, cuda])
@@ -504,6 +512,11 @@ def test_bulk_up_batch_matches_per_message(tmp_path):
             msgs.append(_json.dumps(["X", "U%d" % (j % 25), v, ["I%d" % (j % 7)]]))
     msgs.append('["X", 77, [1, 2, 3]]')
     msgs.append('["Y","I\\u00e9",[0.5,0.25,-1.0]]')
+    # a rejected (non-string ID) row and a parsed row for the same ID: log order decides
+    msgs.append('["Y", 5, [9, 9, 9]]')
+    msgs.append('["Y", "5", [1.0, 1.0, 1.0]]')
+    msgs.append('["Y", "6", [1.0, 1.0, 1.0]]')
+    msgs.append('["Y", 6, [2, 2, 2]]')
     a = ALSServingModel(3, True, device=torch.device("cpu"))
     b = ALSServingModel(3, True, device=torch.device("cpu"))
     apply_up_batch(a, msgs)
@@ -522,6 +535,8 @@ def test_bulk_up_batch_matches_per_message(tmp_path):
         assert a.get_known_items(uid) == b.get_known_items(uid)
     for iid in b.get_all_item_ids():
         np.testing.assert_array_equal(a.get_item_vector(iid), b.get_item_vector(iid))
+    np.testing.assert_array_equal(a.get_item_vector("5"), [1.0, 1.0, 1.0])
+    np.testing.assert_array_equal(a.get_item_vector("6"), [2.0, 2.0, 2.0])
 
 
 def test_up_blocks_from_log_keep_order(tmp_path):

@@ -114,6 +114,82 @@ def test_offsets_get_set(tmp_path):
     assert tlog.get_offsets(root, "In", "other", 3) == {}
 
 
+def _segment_files(root, topic, part=0):
+    import glob
+    import os
+    d = os.path.join(root, topic)
+    files = [f for f in glob.glob(os.path.join(d, "**", "*"), recursive=True)
+             if os.path.isfile(f) and os.path.basename(f) not in ("meta", "lock")
+             and not os.path.basename(f).startswith(".")]
+    return sorted(files)
+
+
+@pytest.mark.timeout(60)
+def test_torn_tail_is_truncated_not_spun_on(tmp_path):
+    """A writer that died mid-append leaves a complete header with a short payload: the end
+    offset ignores it, the next append truncates it, and readers never see it."""
+    import os
+    root = str(tmp_path)
+    tlog.maybe_create_topic(root, "Torn", 1)
+    topic = tlog.Topic(root, "Torn")
+    for i in range(3):
+        topic.append(None, "value-%d" % i)
+    topic.append(None, "x" * 5000)          # the record that gets torn
+    seg = max(_segment_files(root, "Torn"), key=os.path.getsize)
+    size = os.path.getsize(seg)
+    with open(seg, "r+b") as fh:
+        fh.truncate(size - 2000)             # header intact, payload short
+    topic.close()
+    topic = tlog.Topic(root, "Torn")
+    assert topic.end_offset(0) == 3
+    assert topic.append(None, "after") == 3
+    assert topic.end_offset(0) == 4
+    recs = topic.reader(0, 0).poll(100, 100)
+    assert [r[3] for r in recs] == ["value-0", "value-1", "value-2", "after"]
+    vals, n = topic.reader(0, 0).read_text(4)
+    assert n == 4 and vals == ["value-0", "value-1", "value-2", "after"]
+    topic.close()
+
+
+@pytest.mark.timeout(60)
+def test_read_text_roll_then_poll_same_reader(tmp_path):
+    """read_text rolling into the next segment drops the poll read-ahead block, so a later
+    poll on the same reader continues in the new file instead of replaying the old one."""
+    root = str(tmp_path)
+    tlog.maybe_create_topic(root, "Roll", 1, segment_bytes=256)
+    topic = tlog.Topic(root, "Roll")
+    vals = ["rec-%03d-%s" % (i, "p" * 40) for i in range(40)]
+    for v in vals:
+        topic.append(None, v)
+    assert len(_segment_files(root, "Roll")) > 3
+    r = topic.reader(0, 0)
+    first = r.poll(1, 50)
+    assert first[0][3] == vals[0]
+    got, n = r.read_text(25)
+    assert n == 24 and got == vals[1:25]
+    rest = []
+    while True:
+        recs = r.poll(100, 50)
+        if not recs:
+            break
+        rest.extend(x[3] for x in recs)
+    assert rest == vals[25:]
+    topic.close()
+
+
+def test_read_text_grows_for_one_huge_record(tmp_path):
+    root = str(tmp_path)
+    tlog.maybe_create_topic(root, "Huge", 1, max_message=64 << 20)
+    topic = tlog.Topic(root, "Huge")
+    big = "z" * (20 << 20)                   # larger than the 16 MB text buffer
+    topic.append(None, "small")
+    topic.append(None, big)
+    topic.append(None, "tail")
+    vals, n = topic.reader(0, 0).read_text(3)
+    assert n == 3 and vals[0] == "small" and vals[1] == big and vals[2] == "tail"
+    topic.close()
+
+
 # ---------------------------------------------------------------- BatchLayerIT
 
 class MockBatchUpdate(BatchLayerUpdate):
