@@ -162,14 +162,20 @@ class ALSTrainer:
         W, R = ctx.world_size, ctx.rank
         self.su = dist.padded_shard_size(self.n_users, W)
         self.si = dist.padded_shard_size(self.n_items, W)
-        self.u_lo, self.u_hi = dist.shard_range(self.n_users, R, W)
-        self.i_lo, self.i_hi = dist.shard_range(self.n_items, R, W)
+        # ids are owned round-robin (id % W, like MLlib's hash partitioner), not in contiguous
+        # ranges: popularity is skewed towards some id ranges (the synthetic data: low item
+        # ids), and a contiguous item shard put 43% of all ratings on rank 0 at 8 GPUs.
+        # Internally a row lives at the padded global position owner * s + id // W; this rank's
+        # rows are [u_lo, u_hi) of that space.
+        self.u_lo, self.u_hi = R * self.su, R * self.su + self._owned(self.n_users)
+        self.i_lo, self.i_hi = R * self.si, R * self.si + self._owned(self.n_items)
         users = users.to(dev, torch.int64)
         items = items.to(dev, torch.int64)
         ratings = ratings.to(dev, torch.float32)
         t0 = time.perf_counter()
-        by_user = self._route(users, items, ratings, users // self.su)
-        by_item = self._route(users, items, ratings, items // self.si)
+        gu, gi = self._position(users, self.su), self._position(items, self.si)
+        by_user = self._route(gu, gi, ratings, users % W)
+        by_item = self._route(gu, gi, ratings, items % W)
         self.lay_u = RowLayout(self.n_users, W, self._chunks_for(self.n_users))
         self.lay_i = RowLayout(self.n_items, W, self._chunks_for(self.n_items))
         # column ids index the gathered (chunk-major) copy of the opposite factors
@@ -206,17 +212,39 @@ class ALSTrainer:
             return [csr]
         return [csr.row_range(c * lay.cr, (c + 1) * lay.cr) for c in range(lay.C)]
 
+    def _owned(self, n: int) -> int:
+        """Ids of [0, n) this rank owns (id % W == rank)."""
+        W, R = self.ctx.world_size, self.ctx.rank
+        return max(0, (n - R + W - 1) // W)
+
+    def _position(self, ids: torch.Tensor, s: int) -> torch.Tensor:
+        """Padded global row of each id: owner * s + id // W."""
+        W = self.ctx.world_size
+        if W == 1:
+            return ids
+        return (ids % W) * s + torch.div(ids, W, rounding_mode="floor")
+
+    def _original_order(self, full: torch.Tensor, n: int, s: int) -> torch.Tensor:
+        """Rows of a rank-major gathered matrix ([W * s, ...]) back in id order ([n, ...])."""
+        if self.ctx.world_size == 1:
+            return full[:n]
+        ids = torch.arange(n, device=full.device)
+        return full[self._position(ids, s)]
+
     def _route(self, users, items, ratings, owner):
+        """Send each (user row, item row, rating) to ``owner``: one variable-size all-to-all of
+        12-byte int32 triples (the rating travels as its fp32 bits)."""
         ctx = self.ctx
         if not ctx.is_distributed:
             return users, items, ratings
+        assert max(self.su, self.si) * ctx.world_size < 2 ** 31
         order = torch.argsort(owner, stable=True)
         counts = torch.bincount(owner, minlength=ctx.world_size).tolist()
-        packed = torch.stack([users[order].to(torch.float64), items[order].to(torch.float64),
-                              ratings[order].to(torch.float64)], 1)
+        packed = torch.stack([users[order].to(torch.int32), items[order].to(torch.int32),
+                              ratings[order].contiguous().view(torch.int32)], 1)
         recv = dist.all_to_all_rows(packed, counts, ctx)
         return (recv[:, 0].to(torch.int64), recv[:, 1].to(torch.int64),
-                recv[:, 2].to(torch.float32))
+                recv[:, 2].contiguous().view(torch.float32))
 
     # ------------------------------------------------------------------ factors
     def init_factors(self, x_init: Optional[torch.Tensor] = None,
@@ -236,7 +264,8 @@ class ALSTrainer:
                                   (y_init, self.Y, self.i_lo, self.i_hi)):
             if init is None:
                 continue
-            rows = init[lo:hi].to(dev, torch.float32)
+            rows = init[ctx.rank::ctx.world_size].to(dev, torch.float32)
+            assert rows.shape[0] == hi - lo
             ok = ~torch.isnan(rows).any(1)
             dst[:hi - lo, :k] = torch.where(ok[:, None], rows, dst[:hi - lo, :k])
         self._publish_factors()
@@ -315,8 +344,8 @@ class ALSTrainer:
             if tuple(xs.get_shape()) != (self.n_users, self.k) or \
                     tuple(ys.get_shape()) != (self.n_items, self.k):
                 raise ValueError("checkpoint factor shapes do not match the trainer")
-            xr = xs[self.u_lo:self.u_hi]
-            yr = ys[self.i_lo:self.i_hi]
+            xr = xs[:][ctx.rank::ctx.world_size]
+            yr = ys[:][ctx.rank::ctx.world_size]
         X = torch.zeros((self.lay_u.local_rows, self.kp), dtype=torch.float32)
         Y = torch.zeros((self.lay_i.local_rows, self.kp), dtype=torch.float32)
         X[:xr.shape[0], :self.k] = xr
@@ -397,8 +426,10 @@ class ALSTrainer:
     def factors(self, gather: bool = True) -> ALSFactors:
         """Full fp32 factors (all-gathered from the owned shards)."""
         ctx = self.ctx
-        X = dist.all_gather_rows(self.X[:self.su], self.n_users, ctx)[:self.n_users, :self.k]
-        Y = dist.all_gather_rows(self.Y[:self.si], self.n_items, ctx)[:self.n_items, :self.k]
+        X = dist.all_gather_rows(self.X[:self.su], self.n_users, ctx)
+        Y = dist.all_gather_rows(self.Y[:self.si], self.n_items, ctx)
+        X = self._original_order(X, self.n_users, self.su)[:, :self.k]
+        Y = self._original_order(Y, self.n_items, self.si)[:, :self.k]
         return ALSFactors(X.contiguous(), Y.contiguous())
 
     @property

@@ -45,7 +45,7 @@ def test_trainer_implicit_ranks_known_items_higher():
 
 def test_distributed_matches_single_process_gloo(tmp_path):
     """world_size 2 over gloo (all-to-all shuffle, all-reduce YtY, all-gather; also with the
-    factor exchange split into 3 asynchronous ranges) == world 1."""
+    factor exchange split into 3 asynchronous ranges; round-robin row ownership) == world 1."""
     script = tmp_path / "run.py"
     script.write_text(f"""
 import sys, torch
@@ -59,8 +59,10 @@ u, i = key // 50, key % 50
 r = torch.randint(1, 6, (key.numel(),), generator=g).float()
 # every rank holds a different slice of the data
 sl = slice(ctx.rank, None, ctx.world_size)
+# fp32 factor mode: with bf16 replicated factors a 1-ulp difference in the all-reduced YtY
+# (a different summation order per world size) can flip a bf16 rounding and grow to ~1e-4
 tr = ALSTrainer(5, lam=0.05, alpha=1.0, implicit=True, ctx=ctx, seed=3,
-                gather_chunks=int(sys.argv[2]))
+                gather_chunks=int(sys.argv[2]), precision="fp32")
 tr.prepare(u[sl], i[sl], r[sl], 64, 50)
 # deterministic identical init regardless of world size
 gi = torch.Generator().manual_seed(11)
