@@ -1547,7 +1547,7 @@ __global__ __launch_bounds__(256) void pair_dots(const float* __restrict__ X,
 // per SIMD, 0 = als_solve_panel with one chunk in flight at 3 waves per SIMD, 1 =
 // als_solve_wave (register column Cholesky), 3 (default) / 4 = variant 2 with the
 // factorisation at raised issue priority (s_setprio 2 / 3: 2-6% faster half-steps than 2)
-static int g_als_variant = 3;
+static int g_als_variant = 5;
 // 64 < KP <= 128: 0 = als_solve_wide (default), 1 = als_solve_block (LDS Cholesky)
 static int g_als_wide_variant = 0;
 
@@ -1730,6 +1730,13 @@ int oryx_als_solve_profile64(const int64_t* row_ptr, const int32_t* row_ids,
     hipLaunchKernelGGL((als_solve_wave<64, true>), dim3(blocks), dim3(256), 0,
                        reinterpret_cast<hipStream_t>(stream), p, prof);
   return oryx_check_launch();
+}
+
+// analysis: subsequent KP=64 variant-5 solves count per-phase cycles into prof[0..6]
+// (7 u64, zeroed by the caller; nullptr switches it off)
+int oryx_als_batch_profile(unsigned long long* prof) {
+  oryx_als::batch_set_profile(prof);
+  return ORYX_OK;
 }
 
 int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const float* vals,

@@ -30,6 +30,7 @@
 // One wave per SIMD (512 registers: four 10-tile accumulator sets + the gather ring).
 
 #include "als_common.h"
+#include "dpp_fmac.h"
 
 namespace {
 
@@ -62,17 +63,24 @@ struct BatchCfg {
   static constexpr int NT = M * (M + 1) / 2;
   static constexpr int IMG = ChunkImage<KP>::BYTES;
   static constexpr int DS = 20;   // scratch row stride in floats (ds_read_b128 rows conflict free)
-  static constexpr int SCR = 4 * 16 * DS * 4;
-  static constexpr int VEC = 4 * 16 * 4;
+  static constexpr int SCR = NM * 16 * DS * 4;
+  static constexpr int VEC = NM * 16 * 4;
   static constexpr int WAVE_BYTES = NM * IMG + NM * 256 + SCR + VEC;
   static constexpr int YTY_BYTES = NT * 64 * 16;
   static constexpr int BYTES = YTY_BYTES + 4 * WAVE_BYTES;
 };
 
-// D: chunks in flight per row (register ring depth); the wave keeps NM * D gathers in flight
-template <int KP, int NM, int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void als_solve_batch(
-    AlsParams p) {
+// D: chunks in flight per row (register ring depth); the wave keeps NM * D gathers in flight.
+// PROF: per-phase shader-clock cycles summed into prof[0..7] (analysis build,
+// scripts/als_phase_profile.py)
+// NM = 4: one wave per SIMD (512 registers), lane group g owns row g.  NM = 2: two waves per
+// SIMD (256 registers each), lane groups g and g + 2 both hold row g & 1 (the group-layout
+// work is duplicated, but the SIMD interleaves the two waves' VALU streams -- one wave alone
+// issues a VALU instruction every 4 cycles, two fill the SIMD-32's 2-cycle slots -- and one
+// wave's gather overlaps the other's MFMA-heavy solve).
+template <int KP, int NM, int D, bool PROF = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4 / NM, 4 / NM))) void
+als_solve_batch(AlsParams p, unsigned long long* prof) {
   using C = BatchCfg<KP, NM, D>;
   using CI = ChunkImage<KP>;
   constexpr int M = C::M;
@@ -80,7 +88,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int NPL = CI::NPL;
   constexpr int PPR = CI::PPR;
   constexpr int DS = C::DS;
-  static_assert(NM == 4, "lane group m owns row m of the batch");
+  static_assert(NM == 4 || NM == 2, "lane group g owns row g % NM of the batch");
   typedef __attribute__((address_space(3))) float lds_float;
   typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
   __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
@@ -88,11 +96,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, f = lane & 15;
+  const int mg = g & (NM - 1);   // the row of the batch this lane's group works on
   char* my = smem + C::YTY_BYTES + wave * C::WAVE_BYTES;
   char* img = my;
   float* wab = reinterpret_cast<float*>(my + NM * C::IMG);
   lds_float* scr = (lds_float*)(my + NM * C::IMG + NM * 256);
-  lds_float* vdis = scr + 4 * 16 * DS;
+  lds_float* vdis = scr + NM * 16 * DS;
 
   // YtY in accumulator order: tile t, lane l -> rows 16pi + 4(l>>4) + v, column 16qi + (l&15)
   {
@@ -131,6 +140,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   const int nb = (p.n_work + NM - 1) / NM;
   const int total_waves = gridDim.x * 4;
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tp = PROF ? __builtin_amdgcn_s_memtime() : 0;
+  auto phase = [&](int ix) {
+    if constexpr (PROF) {
+      const unsigned long long tn = __builtin_amdgcn_s_memtime();
+      ph[ix] += tn - tp;
+      tp = tn;
+    }
+  };
   for (int bi = blockIdx.x * 4 + wave; bi < nb; bi += total_waves) {
     int rows[NM], slot[NM];
     int64_t beg[NM], end[NM];
@@ -149,6 +167,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       nr = nch > nr ? nch : nr;
     });
 
+    phase(0);
     // ------------------------------------------------------------ gather + MFMA Gramian
     f32x4 acc[NM][NT];
     float bpart[NM][M], cnt[NM];
@@ -173,16 +192,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       cbase[m] = p.col_idx + b0;
       vbase[m] = p.vals + b0;
     });
+    // byte offset of rating o of row m, clamped into the row (a uniform base + 32-bit offset
+    // is one global_load with an SGPR base)
     auto clampo = [&](int m, int o) -> unsigned {
       o = o < len[m] ? o : len[m] - 1;
-      return (unsigned)(o < 0 ? 0 : o);
+      return (unsigned)(o < 0 ? 0 : o) * 4u;
     };
     auto ld_cols = [&](int m, int ch, int (&c)[NPL]) {
+      const char* b = reinterpret_cast<const char*>(cbase[m]);
 #pragma unroll
-      for (int it = 0; it < NPL; ++it) c[it] = cbase[m][clampo(m, 32 * ch + srow[it])];
+      for (int it = 0; it < NPL; ++it)
+        c[it] = *reinterpret_cast<const int*>(b + clampo(m, 32 * ch + srow[it]));
     };
     auto ld_val = [&](int m, int ch, float& v) {
-      v = vbase[m][clampo(m, 32 * ch + (lane & 31))];
+      v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(vbase[m]) +
+                                          clampo(m, 32 * ch + (lane & 31)));
     };
     const char* ybase = reinterpret_cast<const char*>(p.Y);
     auto gather = [&](const int (&c)[NPL], i32x4 (&st)[NPL]) {
@@ -214,30 +238,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       });
     }
     // consume chunk kk of row m from ring slot s (= kk % D); refill the slot with chunk kk + D
-    // (its columns were loaded a round earlier) and load the columns of chunk kk + 2D
+    // (its columns were loaded a round earlier) and load the columns of chunk kk + 2D.
+    // Branch-free on purpose: a conditional prefetch or a divergent block splits the round
+    // into basic blocks, and the waitcnt insertion then waits for nearly every load in flight
+    // (vmcnt(4)) before each prefetch -- the ring drained every chunk.  Past the row's end
+    // the loads are clamped to its last rating (one cached Y row) and the weights are zero.
+    const float alpha = p.alpha;
+    const bool implicit = p.implicit != 0;
     auto consume = [&](auto Mc, auto Sc, int kk) {
       constexpr int m = decltype(Mc)::value;
       constexpr int s = decltype(Sc)::value;
       const int left = len[m] - 32 * kk;
-      const int n = left < 0 ? 0 : (left > 32 ? 32 : left);
-      float wa = 0.f, wb = 0.f, cn = 0.f;
-      if (lane < n) als_weights(val[m][s], p.alpha, p.implicit, wa, wb, cn);
-      cnt[m] += cn;
+      const bool live = (lane & 31) < left;
+      const float r = val[m][s];
+      const float c1 = alpha * fabsf(r);
+      const bool pos = r > 0.f;
+      const float wa = live ? (implicit ? c1 : 1.f) : 0.f;
+      const float wb = live ? (implicit ? (pos ? 1.f + c1 : 0.f) : r) : 0.f;
+      cnt[m] += (live && (!implicit || pos) && lane < 32) ? 1.f : 0.f;
       float* W = wab + m * 64;
       char* G = img + m * C::IMG;
-      if (lane < 32) {
-        W[lane] = wa;
-        W[32 + lane] = wb;
-      }
+      // lanes l and l + 32 hold the same rating: both write the same value
+      W[lane & 31] = wa;
+      W[32 + (lane & 31)] = wb;
 #pragma unroll
       for (int it = 0; it < NPL; ++it)
         *reinterpret_cast<i32x4*>(G + (it * 64 + lane) * 16) = stg[m][s][it];
       wave_sync();
-      if (kk + D < nr) {   // wave-uniform
-        ld_val(m, kk + D, val[m][s]);
-        gather(cols[m][s], stg[m][s]);
-        ld_cols(m, kk + 2 * D, cols[m][s]);
-      }
+      ld_val(m, kk + D, val[m][s]);
+      gather(cols[m][s], stg[m][s]);
+      ld_cols(m, kk + 2 * D, cols[m][s]);
       const f32x4* wv = reinterpret_cast<const f32x4*>(W);
       const f32x4 wa0 = wv[2 * g], wa1 = wv[2 * g + 1];
       const f32x4 wb0 = wv[8 + 2 * g], wb1 = wv[8 + 2 * g + 1];
@@ -250,22 +280,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             (__attribute__((address_space(3))) bf16x4*)(G + tr_addr(pi, 1)));
         fb[pi] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
+      // upper tile (pi, qi) = y_(16pi+a) bf16(c y_(16qi+b)): the weighted operand is always
+      // the one of the larger feature index, so every entry equals the LOWER-triangle entry
+      // bf16(c y_r) y_c (r >= c) of the reference model (the bf16 rounding of c*y makes the
+      // accumulated Gramian slightly asymmetric; only its lower triangle is the matrix)
 #pragma unroll
-      for (int pi = 0; pi < M; ++pi) {
+      for (int qi = 0; qi < M; ++qi) {
         bf16x8 fa;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          fa[j] = (__bf16)((float)fb[pi][j] * wa0[j]);
-          fa[4 + j] = (__bf16)((float)fb[pi][4 + j] * wa1[j]);
+          fa[j] = (__bf16)((float)fb[qi][j] * wa0[j]);
+          fa[4 + j] = (__bf16)((float)fb[qi][4 + j] * wa1[j]);
         }
 #pragma unroll
-        for (int qi = pi; qi < M; ++qi)
+        for (int pi = 0; pi <= qi; ++pi)
           acc[m][tix<M>(pi, qi)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              fa, fb[qi], acc[m][tix<M>(pi, qi)], 0, 0, 0);
+              fb[pi], fa, acc[m][tix<M>(pi, qi)], 0, 0, 0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bpart[m][pi] += wb0[j] * (float)fb[pi][j];
+        for (int j = 0; j < 4; ++j) bpart[m][qi] += wb0[j] * (float)fb[qi][j];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bpart[m][pi] += wb1[j] * (float)fb[pi][4 + j];
+        for (int j = 0; j < 4; ++j) bpart[m][qi] += wb1[j] * (float)fb[qi][4 + j];
       }
       wave_sync();
     };
@@ -276,6 +310,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       });
     }
 
+    phase(1);
     // ------------------------------------------------------------ normal equations
     float cntw[NM];
     static_for<NM>([&](auto Mc) {
@@ -313,18 +348,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       float r = bpart[0][pi];
       static_for<NM - 1>([&](auto Mc) {
         constexpr int m = decltype(Mc)::value + 1;
-        r = g == m ? bpart[m][pi] : r;
+        r = mg == m ? bpart[m][pi] : r;
       });
       rhs[pi] = r;
     }
 
+    phase(2);
     // ------------------------------------------------------------ block LDL^T + forward
     float zp[M], disv[M];
     int bad = 0;
     static_for<M>([&](auto Pc) {
       constexpr int pp = decltype(Pc)::value;
       constexpr int td = tix<M>(pp, pp);
-      // diagonal tiles -> group layout (symmetric: lane (g, f) holds row f, columns 4g..4g+3)
+      // diagonal tiles -> group layout: lane (m, r) gets column r of the tile, whose entries
+      // c <= r are the lower-triangle row r (the elimination below reads nothing else)
 #pragma unroll
       for (int m = 0; m < NM; ++m)
         *reinterpret_cast<lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g) = acc[m][td];
@@ -332,7 +369,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       float a[16], e[16];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (g * 16 + f) * DS + 4 * q);
+        const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q);
 #pragma unroll
         for (int u = 0; u < 4; ++u) a[4 * q + u] = v[u];
       }
@@ -342,7 +379,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int c = 0; c < 16; ++c) e[c] = c == fr ? 1.f : 0.f;
       float dself = 1.f;
-      // [A | I] row operations, pivot row j broadcast inside each 16-lane row
+      // [A | I] row operations on the lower triangle only: row r -= m_r row j uses the pivot
+      // row's entries a_j[c] (c > j), which by symmetry are a_c[j] -- column j of lane c,
+      // broadcast inside each 16-lane row; the identity half takes lane j's row as it is
       static_for<16>([&](auto Jc) {
         constexpr int j = decltype(Jc)::value;
         float piv = rbc<j>(a[j]);
@@ -351,37 +390,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const float mr = a[j] * __builtin_amdgcn_rcpf(piv);
         int rl = f - j;
         asm volatile("" : "+v"(rl));
-        const float mlt = rl > 0 ? mr : 0.f;
+        const float nml = rl > 0 ? -mr : 0.f;   // -L[r][j] (rows r <= j untouched)
         dself = rl == 0 ? piv : dself;
-        // next pivot column first: it is the step's critical path
-        static_for<15 - j>([&](auto Cc) {
-          constexpr int c = j + 1 + decltype(Cc)::value;
-          a[c] -= mlt * rbc<j>(a[c]);
-          asm volatile("" : "+v"(a[c]));
-        });
-        static_for<j>([&](auto Cc) {
-          constexpr int c = decltype(Cc)::value;
-          e[c] -= mlt * rbc<j>(e[c]);
-          asm volatile("" : "+v"(e[c]));
-        });
+        // fused DPP FMAs (dpp_fmac.h); the next pivot column a[j+1] is the first of the group
+        dfa_range<j + 1, 15 - j>(a, a[j], nml);
+        dfb_range<j, 0, j>(nml, e);
         e[j] = rl > 0 ? -mr : e[j];
       });
+      phase(3);
       const float dis = __builtin_amdgcn_rsqf(dself);
       disv[pp] = dis;
       // forward: z_p = D^-1/2 Li r_p
-      float zz = 0.f;
-      static_for<16>([&](auto Cc) {
-        constexpr int c = decltype(Cc)::value;
-        zz += e[c] * rbc<c>(rhs[pp]);
-      });
-      const float z = zz * dis;
+      float z0 = 0.f, z1 = 0.f;
+      dfc_range<0, 16>(z0, z1, rhs[pp], e);
+      const float z = (z0 + z1) * dis;
       zp[pp] = z;
       // Li rows and D^-1/2 to LDS; back as Li^T in accumulator layout (lane (g, f): Li[f][4g+v])
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<lds_f32x4*>(scr + (g * 16 + f) * DS + 4 * q) =
+        *reinterpret_cast<lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q) =
             f32x4{e[4 * q], e[4 * q + 1], e[4 * q + 2], e[4 * q + 3]};
-      vdis[g * 16 + f] = dis;
+      vdis[mg * 16 + f] = dis;
       wave_sync();
       f32x4 Y[NM], d4[NM];
 #pragma unroll
@@ -429,21 +458,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         float col[16];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (g * 16 + f) * DS + 4 * q);
+          const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q);
 #pragma unroll
           for (int u = 0; u < 4; ++u) col[4 * q + u] = v[u];
         }
         wave_sync();
-        float o = 0.f;
-        static_for<16>([&](auto Cc) {
-          constexpr int c = decltype(Cc)::value;
-          o += col[c] * rbc<c>(z);
-        });
-        rhs[i] -= o;
+        float o0 = 0.f, o1 = 0.f;
+        dfc_range<0, 16>(o0, o1, z, col);
+        rhs[i] -= o0 + o1;
       });
       // keep Li^T (accumulator layout) for the back substitution in the dead diagonal tile
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[m][td] = Y[m];
+      phase(4);
     });
     {
       const unsigned long long bm = __ballot(bad != 0);
@@ -466,7 +493,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       wave_sync();
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (g * 16 + f) * DS + 4 * q);
+        const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q);
 #pragma unroll
         for (int u = 0; u < 4; ++u) out[4 * q + u] = v[u];
       }
@@ -482,12 +509,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int m = 0; m < NM; ++m) T[m] = acc[m][tix<M>(pp, i)];
         float row[16];
         rows_of(T, row);   // lane (m, r): K_i[r][0..15]
-        float o = 0.f;
-        static_for<16>([&](auto Ac) {
-          constexpr int a = decltype(Ac)::value;
-          o += row[a] * rbc<a>(xs[i]);
-        });
-        w -= o;
+        float o0 = 0.f, o1 = 0.f;
+        dfc_range<0, 16>(o0, o1, xs[i], row);
+        w -= o0 + o1;
       });
       const float yv = w * disv[pp];
       f32x4 T[NM];
@@ -495,12 +519,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int m = 0; m < NM; ++m) T[m] = acc[m][tix<M>(pp, pp)];
       float col[16];
       rows_of(T, col);   // lane (m, a): Li^T[a][c] = Li[c][a]
-      float x = 0.f;
-      static_for<16>([&](auto Cc) {
-        constexpr int c = decltype(Cc)::value;
-        x += col[c] * rbc<c>(yv);
-      });
-      xs[pp] = x;
+      float x0 = 0.f, x1 = 0.f;
+      dfc_range<0, 16>(x0, x1, yv, col);
+      xs[pp] = x0 + x1;
     });
 
     // lane (m, r) holds x_m[16 pp + r]
@@ -508,16 +529,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     bool ok = valid[0];
     static_for<NM - 1>([&](auto Mc) {
       constexpr int m = decltype(Mc)::value + 1;
-      orow = g == m ? rows[m] : orow;
-      ok = g == m ? valid[m] : ok;
+      orow = mg == m ? rows[m] : orow;
+      ok = mg == m ? valid[m] : ok;
     });
-    if (ok) {
+    if (ok && g < NM) {
 #pragma unroll
       for (int pp = 0; pp < M; ++pp) {
         p.X[(int64_t)orow * KP + 16 * pp + f] = xs[pp];
         if (p.Xb) p.Xb[(int64_t)orow * KP + 16 * pp + f] = (__bf16)xs[pp];
       }
     }
+    phase(5);
+    if constexpr (PROF) ph[6] += 1;
+  }
+  if constexpr (PROF) {
+    if (lane == 0)
+      for (int i = 0; i < 7; ++i) atomicAdd(prof + i, ph[i]);
   }
 }
 
@@ -528,17 +555,35 @@ namespace oryx_als {
 #ifndef ORYX_ALS_BATCH_DEPTH
 #define ORYX_ALS_BATCH_DEPTH 1
 #endif
+// rows per wave: 2 (two waves per SIMD, default) or 4 (one wave per SIMD)
+#ifndef ORYX_ALS_BATCH_NM
+#define ORYX_ALS_BATCH_NM 2
+#endif
+
+static unsigned long long* g_batch_prof = nullptr;
+
+void batch_set_profile(unsigned long long* prof) { g_batch_prof = prof; }
 
 int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s) {
-  const int nb = (p.n_work + 3) / 4;
+  constexpr int NM = ORYX_ALS_BATCH_NM;
+  constexpr int D = ORYX_ALS_BATCH_DEPTH;
+  // one resident generation: 4 / NM blocks of 4 waves per CU (max_blocks = CUs unless
+  // overridden by ORYX_ALS_MAX_BLOCKS)
+  const int nb = (p.n_work + NM - 1) / NM;
   int blocks = (nb + 3) / 4;
-  if (blocks > max_blocks) blocks = max_blocks;
+  const int cap = max_blocks * (4 / NM);
+  if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
+  if (g_batch_prof && kp == 64) {
+    hipLaunchKernelGGL((als_solve_batch<64, NM, D, true>), dim3(blocks), dim3(256), 0, s, p,
+                       g_batch_prof);
+    return oryx_check_launch();
+  }
   switch (kp) {
-#define BATCH_CASE(KPV)                                                                      \
-  case KPV:                                                                                  \
-    hipLaunchKernelGGL((als_solve_batch<KPV, 4, (KPV <= 32 ? 2 : ORYX_ALS_BATCH_DEPTH)>),      \
-                       dim3(blocks), dim3(256), 0, s, p);                                   \
+#define BATCH_CASE(KPV)                                                                       \
+  case KPV:                                                                                   \
+    hipLaunchKernelGGL((als_solve_batch<KPV, NM, D>), dim3(blocks), dim3(256), 0, s, p,      \
+                       nullptr);                                                             \
     break;
     BATCH_CASE(16)
     BATCH_CASE(32)

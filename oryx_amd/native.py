@@ -161,7 +161,8 @@ def _load_kernels():
     # raised priority, 2 = panel + 3-deep gather ring, 0 = panel + 1-deep, 1 = register)
     _sig(lib, "oryx_als_set_variant", c_i, [c_i])
     _sig(lib, "oryx_als_get_variant", c_i, [])
-    lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "3")))
+    _sig(lib, "oryx_als_batch_profile", c_i, [c_vp])
+    lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "5")))
     # ORYX_ALS_WIDE_VARIANT: 64 < k <= 128 solve (0 = als_solve_wide, 1 = als_solve_block)
     _sig(lib, "oryx_als_set_wide_variant", c_i, [c_i])
     lib.oryx_als_set_wide_variant(int(os.environ.get("ORYX_ALS_WIDE_VARIANT", "0")))

@@ -14,6 +14,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+BATCH_PHASES = ["batch setup", "gather+mfma (4 rows)", "normal equations", "LDL^T 16x16 blocks",
+                "K + trailing MFMA + rhs", "back substitution + store"]
 if os.environ.get("ORYX_ALS_VARIANT", "3") == "1":   # als_solve_wave (register Cholesky)
     PHASES = ["gather+mfma", "scatter/ws", "load A+YtY", "cholesky", "forward", "back+store"]
 else:                                               # als_solve_panel (default)
@@ -36,6 +38,28 @@ def main():
     tr.init_factors()
     lib = native.require_kernels()
     out = {}
+    if lib.oryx_als_get_variant() == 5:
+        # als_solve_batch<64, PROF>: the real half-step (split long rows included); cycles of
+        # one wave (= one SIMD) per batch of 4 rows
+        for name, csr, src_b, src_f, dst, dstb in (
+                ("items", tr.csr_i, tr.Xb, tr.X, tr.Y, tr.Yb_local),
+                ("users", tr.csr_u, tr.Yb, tr.Y, tr.X, tr.Xb_local)):
+            yty = als_ops.gramian(src_f)
+            prof = torch.zeros(8, dtype=torch.int64, device=dev)
+            lib.oryx_als_batch_profile(prof.data_ptr())
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            als_ops.solve_rows(csr, src_b, yty, dst, dstb, 64, 0.001, 1.0, True)
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3
+            lib.oryx_als_batch_profile(None)
+            p = prof.cpu().tolist()
+            nb = max(1, p[6])
+            out[name] = {"rows": int(csr.order.numel()), "batches": p[6], "nnz": csr.nnz,
+                         "ms": ms, "cycles_per_batch": {k: p[i] / nb
+                                                        for i, k in enumerate(BATCH_PHASES)}}
+        print(json.dumps(out, indent=1))
+        return
     for name, csr, src_b, src_f, dst in (("items", tr.csr_i, tr.Xb, tr.X, tr.Y),
                                          ("users", tr.csr_u, tr.Yb, tr.Y, tr.X)):
         yty = als_ops.gramian(src_f)
