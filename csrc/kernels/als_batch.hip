@@ -284,22 +284,34 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
       // the one of the larger feature index, so every entry equals the LOWER-triangle entry
       // bf16(c y_r) y_c (r >= c) of the reference model (the bf16 rounding of c*y makes the
       // accumulated Gramian slightly asymmetric; only its lower triangle is the matrix)
+      // weights as register pairs matching the fragment's bf16 pairs (ratings 8g+2i, +1)
+      const f32x2 wap[4] = {f32x2{wa0[0], wa0[1]}, f32x2{wa0[2], wa0[3]},
+                            f32x2{wa1[0], wa1[1]}, f32x2{wa1[2], wa1[3]}};
+      const f32x2 wbp[4] = {f32x2{wb0[0], wb0[1]}, f32x2{wb0[2], wb0[3]},
+                            f32x2{wb1[0], wb1[1]}, f32x2{wb1[2], wb1[3]}};
 #pragma unroll
       for (int qi = 0; qi < M; ++qi) {
-        bf16x8 fa;
+        // bf16(c y) per pair: unpack (shift / mask), v_pk_mul_f32, v_cvt_pk_bf16_f32; the same
+        // unpacked pair feeds b's v_pk_fma_f32
+        const i32x4 raw = __builtin_bit_cast(i32x4, fb[qi]);
+        i32x4 wraw;
+        f32x2 bacc = f32x2{0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          fa[j] = (__bf16)((float)fb[qi][j] * wa0[j]);
-          fa[4 + j] = (__bf16)((float)fb[qi][4 + j] * wa1[j]);
+        for (int i = 0; i < 4; ++i) {
+          const unsigned u = (unsigned)raw[i];
+          const f32x2 y = f32x2{__builtin_bit_cast(float, u << 16),
+                                __builtin_bit_cast(float, u & 0xffff0000u)};
+          const f32x2 cy = y * wap[i];
+          bacc = y * wbp[i] + bacc;
+          typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+          wraw[i] = __builtin_bit_cast(int, __builtin_convertvector(cy, bf16x2));
         }
+        const bf16x8 fa = __builtin_bit_cast(bf16x8, wraw);
+        bpart[m][qi] += bacc[0] + bacc[1];
 #pragma unroll
         for (int pi = 0; pi <= qi; ++pi)
           acc[m][tix<M>(pi, qi)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               fb[pi], fa, acc[m][tix<M>(pi, qi)], 0, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bpart[m][qi] += wb0[j] * (float)fb[qi][j];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bpart[m][qi] += wb1[j] * (float)fb[qi][4 + j];
       }
       wave_sync();
     };
