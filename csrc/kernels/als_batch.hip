@@ -51,6 +51,13 @@ __device__ __forceinline__ int64_t uni(int64_t v) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// scalar (s_load) read of a read-only array through the constant address space: the value
+// lands in SGPRs and is waited on lgkmcnt, never on the vmcnt of the gather ring
+template <typename T>
+__device__ __forceinline__ T sload(const T* base, int64_t i) {
+  return ((const __attribute__((address_space(4))) T*)base)[i];
+}
+
 // index of upper tile (pi, qi), pi <= qi, row-major over the upper triangle
 template <int M>
 __host__ __device__ constexpr int tix(int pi, int qi) {
@@ -149,21 +156,90 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
       tp = tn;
     }
   };
-  for (int bi = blockIdx.x * 4 + wave; bi < nb; bi += total_waves) {
-    int rows[NM], slot[NM];
-    int64_t beg[NM], end[NM];
-    bool valid[NM];
-    int nr = 0;
+  // Row metadata of a batch arrives in three dependent round trips (work list -> row_ptr ->
+  // column ids of the first chunks).  For the next batch they are issued in stages under this
+  // batch's solve (stage1 after the gather loop, stage2 after the first LDL^T, stage3 after the
+  // first panel), so a batch starts with its first gathers' column ids already in registers.
+  int rows_n[NM], slot_n[NM], len_n[NM];
+  int64_t b_n[NM], e_n[NM], beg_n[NM];
+  bool valid_n[NM];
+  int cols_n[NM][D][NPL];
+  float val_n[NM][D];
+  auto stage1 = [&](int b) {
     static_for<NM>([&](auto Mc) {
       constexpr int m = decltype(Mc)::value;
-      const int w = bi * NM + m;
-      valid[m] = w < p.n_work;
-      const int ww = valid[m] ? w : p.n_work - 1;   // tail: a real row, solved but not stored
-      rows[m] = uni(p.row_ids ? p.row_ids[ww] : ww);
-      slot[m] = uni((valid[m] && p.long_slot) ? p.long_slot[ww] : -1);
-      beg[m] = uni(p.row_ptr[rows[m]]);
-      end[m] = (slot[m] >= 0 || !valid[m]) ? beg[m] : uni(p.row_ptr[rows[m] + 1]);
-      const int nch = (int)((end[m] - beg[m] + 31) / 32);
+      const int w = b * NM + m;
+      valid_n[m] = w < p.n_work;
+      const int ww = valid_n[m] ? w : p.n_work - 1;   // tail: a real row, solved, not stored
+      rows_n[m] = p.row_ids ? sload(p.row_ids, ww) : ww;
+      slot_n[m] = (valid_n[m] && p.long_slot) ? sload(p.long_slot, ww) : -1;
+    });
+  };
+  auto stage2 = [&]() {
+    static_for<NM>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      b_n[m] = sload(p.row_ptr, rows_n[m]);
+      e_n[m] = sload(p.row_ptr, rows_n[m] + 1);
+    });
+  };
+  // byte offset of rating o of a row of length n, clamped into the row (a uniform base plus a
+  // 32-bit offset is one global_load with an SGPR base)
+  auto clampo = [&](int n, int o) -> unsigned {
+    o = o < n ? o : n - 1;
+    return (unsigned)(o < 0 ? 0 : o) * 4u;
+  };
+  auto ld_cols_at = [&](const int32_t* cb, int n, int ch, int (&c)[NPL]) {
+    const char* b = reinterpret_cast<const char*>(cb);
+#pragma unroll
+    for (int it = 0; it < NPL; ++it)
+      c[it] = *reinterpret_cast<const int*>(b + clampo(n, 32 * ch + srow[it]));
+  };
+  auto ld_val_at = [&](const float* vb, int n, int ch, float& v) {
+    v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(vb) +
+                                        clampo(n, 32 * ch + (lane & 31)));
+  };
+  auto stage3 = [&]() {
+    static_for<NM>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      beg_n[m] = b_n[m];
+      const int64_t en = (slot_n[m] >= 0 || !valid_n[m]) ? beg_n[m] : e_n[m];
+      len_n[m] = (int)(en - beg_n[m]);
+      const int64_t b0 = len_n[m] > 0 ? beg_n[m] : 0;
+      static_for<D>([&](auto Sc) {
+        constexpr int s = decltype(Sc)::value;
+        ld_cols_at(p.col_idx + b0, len_n[m], s, cols_n[m][s]);
+        ld_val_at(p.vals + b0, len_n[m], s, val_n[m][s]);
+      });
+    });
+  };
+  if (blockIdx.x * 4 + wave < nb) {
+    stage1(blockIdx.x * 4 + wave);
+    stage2();
+    stage3();
+  }
+
+  for (int bi = blockIdx.x * 4 + wave; bi < nb; bi += total_waves) {
+    // the next batch of this wave (the last one re-loads itself: the stages run
+    // unconditionally, so their results are dead during the gather loop -- a conditional stage
+    // would keep the previous values live through it and spill)
+    const int bnext = bi + total_waves < nb ? bi + total_waves : bi;
+    int rows[NM], slot[NM];
+    bool valid[NM];
+    int nr = 0;
+    // per-row uniform bases, per-lane 32-bit offsets
+    const int32_t* cbase[NM];
+    const float* vbase[NM];
+    int len[NM];
+    static_for<NM>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      rows[m] = rows_n[m];
+      slot[m] = slot_n[m];
+      valid[m] = valid_n[m];
+      len[m] = len_n[m];
+      const int64_t b0 = len[m] > 0 ? beg_n[m] : 0;
+      cbase[m] = p.col_idx + b0;
+      vbase[m] = p.vals + b0;
+      const int nch = (len[m] + 31) / 32;
       nr = nch > nr ? nch : nr;
     });
 
@@ -180,34 +256,8 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
       cnt[m] = 0.f;
     });
 
-    // per-row uniform bases, per-lane 32-bit offsets (global_load with an SGPR base): the
-    // ring's addresses cost one VGPR each instead of a 64-bit pair
-    const int32_t* cbase[NM];
-    const float* vbase[NM];
-    int len[NM];
-    static_for<NM>([&](auto Mc) {
-      constexpr int m = decltype(Mc)::value;
-      len[m] = (int)(end[m] - beg[m]);
-      const int64_t b0 = len[m] > 0 ? beg[m] : 0;
-      cbase[m] = p.col_idx + b0;
-      vbase[m] = p.vals + b0;
-    });
-    // byte offset of rating o of row m, clamped into the row (a uniform base + 32-bit offset
-    // is one global_load with an SGPR base)
-    auto clampo = [&](int m, int o) -> unsigned {
-      o = o < len[m] ? o : len[m] - 1;
-      return (unsigned)(o < 0 ? 0 : o) * 4u;
-    };
-    auto ld_cols = [&](int m, int ch, int (&c)[NPL]) {
-      const char* b = reinterpret_cast<const char*>(cbase[m]);
-#pragma unroll
-      for (int it = 0; it < NPL; ++it)
-        c[it] = *reinterpret_cast<const int*>(b + clampo(m, 32 * ch + srow[it]));
-    };
-    auto ld_val = [&](int m, int ch, float& v) {
-      v = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(vbase[m]) +
-                                          clampo(m, 32 * ch + (lane & 31)));
-    };
+    auto ld_cols = [&](int m, int ch, int (&c)[NPL]) { ld_cols_at(cbase[m], len[m], ch, c); };
+    auto ld_val = [&](int m, int ch, float& v) { ld_val_at(vbase[m], len[m], ch, v); };
     const char* ybase = reinterpret_cast<const char*>(p.Y);
     auto gather = [&](const int (&c)[NPL], i32x4 (&st)[NPL]) {
 #pragma unroll
@@ -216,18 +266,20 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
             ybase + ((unsigned)c[it] * (unsigned)(KP * 2) + (unsigned)(soff[it] * 2)));
     };
 
+    // ring: chunk s of every row; its column ids and values were prefetched (stage3)
     i32x4 stg[NM][D][NPL];
     int cols[NM][D][NPL];
     float val[NM][D];
-    if (nr > 0) {
-      static_for<NM>([&](auto Mc) {
-        constexpr int m = decltype(Mc)::value;
-        static_for<D>([&](auto Sc) {
-          constexpr int s = decltype(Sc)::value;
-          ld_cols(m, s, cols[m][s]);
-          ld_val(m, s, val[m][s]);
-        });
+    static_for<NM>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      static_for<D>([&](auto Sc) {
+        constexpr int s = decltype(Sc)::value;
+#pragma unroll
+        for (int it = 0; it < NPL; ++it) cols[m][s][it] = cols_n[m][s][it];
+        val[m][s] = val_n[m][s];
       });
+    });
+    if (nr > 0) {
       static_for<NM>([&](auto Mc) {
         constexpr int m = decltype(Mc)::value;
         static_for<D>([&](auto Sc) {
@@ -323,6 +375,7 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
     }
 
     phase(1);
+    stage1(bnext);
     // ------------------------------------------------------------ normal equations
     float cntw[NM];
     static_for<NM>([&](auto Mc) {
@@ -410,6 +463,7 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
         e[j] = rl > 0 ? -mr : e[j];
       });
       phase(3);
+      if constexpr (pp == 0) stage2();
       const float dis = __builtin_amdgcn_rsqf(dself);
       disv[pp] = dis;
       // forward: z_p = D^-1/2 Li r_p
@@ -482,6 +536,7 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
       // keep Li^T (accumulator layout) for the back substitution in the dead diagonal tile
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[m][td] = Y[m];
+      if constexpr (pp == (M > 1 ? 1 : 0)) stage3();
       phase(4);
     });
     {

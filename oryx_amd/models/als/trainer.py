@@ -144,6 +144,7 @@ class ALSTrainer:
         self.seed = int(seed)
         self.timings: Dict[str, float] = {}
         self.fail_count = None
+        self.events: Optional[list] = None
         # row ranges per half-step whose factor exchange overlaps the next range's solve
         self._explicit_chunks = bool(gather_chunks)
         self.gather_chunks = int(gather_chunks) if gather_chunks else (
@@ -359,22 +360,55 @@ class ALSTrainer:
         return iteration
 
     # ------------------------------------------------------------------ iterations
+    def _mark(self, label: str) -> None:
+        """Phase event for :meth:`phase_breakdown` (only while ``self.events`` is a list)."""
+        if self.events is not None and self.device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.events.append((label, ev))
+
     def _half_step(self, parts, src_own_f32, src_full_bf16, dst_f32, dst_b_local, lay, name):
         ctx = self.ctx
         yty = None
+        self._mark(name + ".start")
         if self.implicit:
             with tracing.range(name + ".gramian"):
                 yty = als_ops.gramian(src_own_f32)
                 dist.all_reduce_sum(yty, ctx)
+        self._mark(name + ".gramian")
 
         def solve(c):
             with tracing.range(name + ".solve"):
                 als_ops.solve_rows(parts[c], src_full_bf16, yty, dst_f32, dst_b_local, self.k,
                                    self.lam, self.alpha, self.implicit,
                                    fail_count=self.fail_count, split=self.split)
+            if c == lay.C - 1:
+                self._mark(name + ".solve")
         # range c's bf16 rows are exchanged while range c+1 is solved
         with tracing.range(name + ".solve+allgather"):
-            return lay.gather(dst_b_local, ctx, overlap_with=solve)
+            out = lay.gather(dst_b_local, ctx, overlap_with=solve)
+        self._mark(name + ".exchange")
+        return out
+
+    def phase_breakdown(self, iterations: int = 3) -> Dict[str, float]:
+        """Milliseconds per iteration (mean of ``iterations``) of each half-step's phases on this
+        rank's stream: Gramian + YtY all-reduce, the solve launches (ranges after the first
+        overlap the previous range's all-gather), and the exposed factor exchange after the
+        last solve."""
+        if self.device.type != "cuda":
+            return {}
+        self.events = []
+        self.iterate(iterations)
+        torch.cuda.synchronize(self.device)
+        ev, self.events = self.events, None
+        out: Dict[str, float] = {}
+        for (la, a), (lb, b) in zip(ev[:-1], ev[1:]):
+            half, phase = lb.rsplit(".", 1)
+            if phase == "start":
+                continue
+            key = "%s_%s_ms" % (half.split(".")[-1], phase)
+            out[key] = out.get(key, 0.0) + a.elapsed_time(b) / iterations
+        return out
 
     def iterate(self, iterations: int = 1) -> None:
         for _ in range(iterations):
