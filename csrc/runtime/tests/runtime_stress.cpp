@@ -20,6 +20,8 @@ void* oryx_log_open(const char*, const char*, int, long long, long long);
 void oryx_log_close(void*);
 long long oryx_log_append_batch(void*, int, const char*, long long, int, long long, int,
                                 long long*);
+long long oryx_log_append_values_gap(void*, int, const char*, int, const char*,
+                                     const long long*, int, int, long long, int);
 void* oryx_reader_open(void*, int, long long);
 void oryx_reader_close(void*);
 long long oryx_reader_poll(void*, char*, long long, int, int, long long*);
@@ -127,7 +129,56 @@ int main(int argc, char** argv) {
       oryx_dict_free(items);
     }
   });
+  // large blocks (frames built on several threads inside each append) from two writers
+  const int big_batches = 3, big_n = 5000;
+  void* b1 = oryx_log_open(root, "Big", 1, 1 << 20, 64ll << 20);
+  void* b2 = oryx_log_open(root, "Big", 1, 1 << 20, 64ll << 20);
+  for (int w = 0; w < 2; ++w) {
+    th.emplace_back([&, w] {
+      std::string blob;
+      std::vector<long long> lens;
+      for (int i = 0; i < big_n; ++i) {
+        std::string v = "w" + std::to_string(w) + ":" + std::to_string(i) + ":";
+        v.append(600, (char)('a' + i % 26));
+        lens.push_back((long long)v.size());
+        blob += v;
+        blob += '\n';
+      }
+      for (int b = 0; b < big_batches; ++b)
+        if (oryx_log_append_values_gap(w ? b2 : b1, -1, "UP", 2, blob.data(), lens.data(), big_n,
+                                       1, -1, 0) < 0)
+          ++errors;
+    });
+  }
   for (auto& x : th) x.join();
+  {
+    void* r = oryx_reader_open(b1, 0, 0);
+    std::vector<char> out(1 << 22);
+    long long used = 0, last = -1, got = 0;
+    for (int idle = 0; idle < 5;) {
+      const long long n = oryx_reader_poll(r, out.data(), (long long)out.size(), 4096, 20, &used);
+      if (n <= 0) {
+        ++idle;
+        continue;
+      }
+      long long pos = 0;
+      for (long long i = 0; i < n; ++i) {
+        long long off;
+        int kl, vl;
+        memcpy(&off, out.data() + pos, 8);
+        memcpy(&kl, out.data() + pos + 16, 4);
+        memcpy(&vl, out.data() + pos + 20, 4);
+        if (off != last + 1 || kl != 2 || vl < 600) ++errors;
+        last = off;
+        pos += 24 + (kl > 0 ? kl : 0) + vl;
+      }
+      got += n;
+    }
+    if (got != 2LL * big_batches * big_n) ++errors;
+    oryx_reader_close(r);
+  }
+  oryx_log_close(b1);
+  oryx_log_close(b2);
   oryx_log_close(t1);
   oryx_log_close(t2);
   for (int part = 0; part < P; ++part)
