@@ -114,10 +114,24 @@ class ALSSpeedModel(SpeedModel):
     def solver_inverses(self):
         """(inverse of XtX, inverse of YtY) as fp64 device tensors, recomputed only when the
         factors changed since the last call; raises SingularMatrixSolverException like the
-        solvers; None when a matrix is empty."""
+        solvers; None when a matrix is empty.
+
+        On a GPU both Gramians come from the fused fp32 MFMA kernel (``ops.als.gramian``) and
+        are inverted on the device by an fp64 Cholesky (one host sync for both).  The device
+        result is used only when it certifies what the reference's RRQR check
+        (``LinearSystemSolver.getSolver``, ``mathx.get_solver``) would accept: for SPD A every
+        |R_ii| of a pivoted QR is >= lambda_min(A) >= 1 / ||A^-1||_F, so
+        1 / ||A^-1||_F > ||A||_inf * ratio implies the RRQR test passes.  Anything else
+        (near-singular, empty) takes the host RRQR path, which keeps its exact semantics
+        (the exception and its apparent rank)."""
         key = (self.X.version, self.Y.version)
         if getattr(self, "_inv_key", None) == key:
             return self._inv
+        if self.device is not None and self.device.type == "cuda":
+            inv = self._device_inverses()
+            if inv is not None:
+                self._inv_key, self._inv = key, inv
+                return inv
         xtx = self.get_xtx_solver()
         yty = self.get_yty_solver()
         if xtx is None or yty is None:
@@ -127,6 +141,22 @@ class ALSSpeedModel(SpeedModel):
                    torch.from_numpy(yty.inverse()).to(self.device))
         self._inv_key, self._inv = key, inv
         return inv
+
+    def _device_inverses(self):
+        if self.X.size() == 0 or self.Y.size() == 0:
+            return None
+        invs, oks = [], []
+        for store in (self.X, self.Y):
+            mat, _, _ = store.device_view()
+            a = als_ops.gramian(mat).double()
+            chol, info = torch.linalg.cholesky_ex(a)
+            inv = torch.cholesky_inverse(chol)
+            thr = a.abs().sum(1).max() * mathx.SINGULARITY_THRESHOLD_RATIO
+            oks.append((info == 0) & torch.isfinite(inv).all() & (inv.norm() * thr < 1.0))
+            invs.append(inv)
+        if not bool(torch.stack(oks).all().item()):
+            return None
+        return invs[0], invs[1]
 
     def get_fraction_loaded(self) -> float:
         with self._lock:

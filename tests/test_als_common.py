@@ -247,3 +247,33 @@ def test_native_rows_follow_inserts_and_removals():
     want = [fv.row_of(k) if fv.row_of(k) is not None else -1 for k in d.keys()]
     assert fv.native_rows(d).tolist() == want
     assert want[0] == -1 and want[-1] == fv.row_of("c7")
+
+
+@pytest.mark.gpu
+def test_speed_device_inverses_match_host_rrqr(cuda):
+    """ALSSpeedModel.solver_inverses on a GPU (fused Gramian + fp64 device Cholesky) equals
+    the host RRQR inverses; a rank-deficient factor matrix still raises the reference's
+    SingularMatrixSolverException (the device certificate fails, the host path decides)."""
+    import numpy as np
+    import torch
+    from oryx_amd.models.als.speed import ALSSpeedModel
+    from oryx_amd.utils import mathx
+    g = np.random.default_rng(5)
+    k = 32
+    m = ALSSpeedModel(k, True, torch.device(cuda))
+    X = g.standard_normal((3000, k)).astype(np.float32)
+    Y = g.standard_normal((2000, k)).astype(np.float32)
+    m.X.set_vectors(["U%d" % j for j in range(len(X))], X)
+    m.Y.set_vectors(["I%d" % j for j in range(len(Y))], Y)
+    xi, yi = m.solver_inverses()
+    assert xi.device.type == "cuda" and xi.dtype == torch.float64
+    for inv, mat in ((xi, X), (yi, Y)):
+        ref = mathx.get_solver(mat.astype(np.float64).T @ mat.astype(np.float64)).inverse()
+        np.testing.assert_allclose(inv.cpu().numpy(), ref, rtol=1e-4, atol=1e-7)
+    bad = ALSSpeedModel(k, True, torch.device(cuda))
+    Yb = Y.copy()
+    Yb[:, 1] = Yb[:, 0]                       # rank k - 1
+    bad.X.set_vectors(["U%d" % j for j in range(len(X))], X)
+    bad.Y.set_vectors(["I%d" % j for j in range(len(Yb))], Yb)
+    with pytest.raises(mathx.SingularMatrixSolverException):
+        bad.solver_inverses()
