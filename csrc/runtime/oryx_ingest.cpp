@@ -1561,3 +1561,79 @@ long long oryx_gzip_indexed_inflate(const unsigned char* b, long long n, char* o
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ newline-delimited text
+// (oryx_amd.textlines.TextLines: messages held as one buffer, every line ending in '\n')
+
+extern "C" {
+
+// End offset (position of the '\n') of every line of buf[0, len), threaded over blocks cut at
+// newlines.  Returns the number of lines written to out_ends (at most max_lines).
+long long oryx_line_ends(const char* buf, long long len, long long* out_ends,
+                         long long max_lines) {
+  if (len <= 0) return 0;
+  const int P = len >= (16ll << 20) ? oryx_ff::native_threads() : 1;
+  std::vector<const char*> cut((size_t)P + 1);
+  cut[0] = buf;
+  cut[(size_t)P] = buf + len;
+  for (int t = 1; t < P; ++t) {
+    const char* c = buf + len * t / P;
+    if (c < cut[(size_t)t - 1]) c = cut[(size_t)t - 1];
+    const char* nl = static_cast<const char*>(memchr(c, '\n', (size_t)(buf + len - c)));
+    cut[(size_t)t] = nl ? nl + 1 : buf + len;
+  }
+  std::vector<long long> cnt((size_t)P, 0);
+  auto count = [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      long long c = 0;
+      for (const char* p = cut[(size_t)t]; p < cut[(size_t)t + 1];) {
+        const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(cut[(size_t)t + 1] - p)));
+        if (!nl) break;
+        ++c;
+        p = nl + 1;
+      }
+      cnt[(size_t)t] = c;
+    }
+  };
+  oryx_ff::parallel_ranges(P, 1, count);
+  std::vector<long long> first((size_t)P + 1, 0);
+  for (int t = 0; t < P; ++t) first[(size_t)t + 1] = first[(size_t)t] + cnt[(size_t)t];
+  const long long total = first[(size_t)P];
+  if (total > max_lines) return -total;
+  auto fill = [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      long long k = first[(size_t)t];
+      for (const char* p = cut[(size_t)t]; p < cut[(size_t)t + 1];) {
+        const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(cut[(size_t)t + 1] - p)));
+        if (!nl) break;
+        out_ends[k++] = (long long)(nl - buf);
+        p = nl + 1;
+      }
+    }
+  };
+  oryx_ff::parallel_ranges(P, 1, fill);
+  return total;
+}
+
+// Copies lines idx[0..n) (line j = buf[ends[j-1] + 1, ends[j]), ends[-1] = -1) into out, each
+// followed by '\n'; out must hold sum of their lengths + n bytes.  Returns bytes written.
+long long oryx_gather_lines(const char* buf, const long long* ends, const long long* idx,
+                            long long n, char* out) {
+  std::vector<long long> at((size_t)n + 1, 0);
+  for (long long k = 0; k < n; ++k) {
+    const long long j = idx[k];
+    const long long b = j ? ends[j - 1] + 1 : 0;
+    at[(size_t)k + 1] = at[(size_t)k] + (ends[j] - b) + 1;
+  }
+  oryx_ff::parallel_ranges(n, 1 << 16, [&](long long lo, long long hi, int) {
+    for (long long k = lo; k < hi; ++k) {
+      const long long j = idx[k];
+      const long long b = j ? ends[j - 1] + 1 : 0;
+      const long long l = ends[j] - b + 1;   // the line and its '\n'
+      memcpy(out + at[(size_t)k], buf + b, (size_t)l);
+    }
+  });
+  return at[(size_t)n];
+}
+
+}  // extern "C"

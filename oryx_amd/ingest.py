@@ -78,21 +78,38 @@ class IdDict:
 
 def parse_ratings(lines, users: IdDict, items: IdDict, default_ts: int,
                   strict: bool = False) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
-    """Parse rating lines (str list or newline-joined bytes) -> (u, i, strength, ts) arrays."""
+    """Parse rating lines (str list, newline-joined bytes or a :class:`TextLines` buffer)
+    -> (u, i, strength, ts) arrays."""
+    from .textlines import TextLines
+    if isinstance(lines, TextLines):
+        buf = lines.joined()
+        n_max = len(lines) + 1
+        if isinstance(buf, np.ndarray):
+            data = ctypes.cast(ctypes.c_void_p(buf.ctypes.data), ctypes.c_char_p)
+            n_bytes = buf.nbytes
+        else:
+            data, n_bytes = bytes(buf), len(buf)
+        return _parse_ratings_buf(data, n_bytes, n_max, users, items, default_ts, strict)
     if isinstance(lines, (bytes, bytearray)):
         data = bytes(lines)
         n_max = data.count(b"\n") + 1
     else:
         data = "\n".join(lines).encode("utf-8")
         n_max = len(lines) + 1
+    return _parse_ratings_buf(data, len(data), n_max, users, items, default_ts, strict)
+
+
+def _parse_ratings_buf(data, n_bytes: int, n_max: int, users: "IdDict", items: "IdDict",
+                       default_ts: int, strict: bool):
     u = np.empty(n_max, dtype=np.int64)
     i = np.empty(n_max, dtype=np.int64)
     s = np.empty(n_max, dtype=np.float64)
     t = np.empty(n_max, dtype=np.int64)
     vp = ctypes.c_void_p
     n = native.runtime().oryx_parse_ratings(
-        data, len(data), users.handle, items.handle, u.ctypes.data_as(vp), i.ctypes.data_as(vp),
-        s.ctypes.data_as(vp), t.ctypes.data_as(vp), n_max, int(default_ts), int(bool(strict)))
+        data, int(n_bytes), users.handle, items.handle, u.ctypes.data_as(vp),
+        i.ctypes.data_as(vp), s.ctypes.data_as(vp), t.ctypes.data_as(vp), n_max,
+        int(default_ts), int(bool(strict)))
     if n < 0:
         raise ValueError("Bad input line %d" % (-n - 1))
     return u[:n], i[:n], s[:n], t[:n]

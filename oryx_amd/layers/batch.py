@@ -41,6 +41,7 @@ from ..api import BatchLayerUpdate, Dataset
 from ..transport.producer import LogTopicProducer
 from ..utils import config as cfg
 from ..parallel import dist
+from ..textlines import TextLines, concat_lines
 from ..utils import faults, ioutils, lang, rng
 from .common import AbstractLayer, IntervalTimer, drain_dataset
 
@@ -53,9 +54,16 @@ _TS_RE = re.compile(r"-(\d+)\.")
 
 
 def _write_part(path_no_ext: str, records) -> str:
-    """Write one part file; keyless single-line messages as plain text (``.txt``)."""
+    """Write one part file; keyless single-line messages as plain text (``.txt``) -- a
+    :class:`TextLines` buffer is written as it is."""
     if isinstance(records, Dataset) and records.keyless:
         vals = records.values()
+        if isinstance(vals, TextLines):
+            path = path_no_ext + ".txt"
+            with open(path + ".w", "wb") as f:
+                f.write(memoryview(vals.joined()))
+            os.replace(path + ".w", path)
+            return path
         text = "\n".join(vals)
         if text.count("\n") == len(vals) - 1:
             path = path_no_ext + ".txt"
@@ -103,23 +111,23 @@ def read_past_data(data_dir: str, rank: int = 0, world: int = 1) -> Dataset:
     """All past records, or with ``world > 1`` this rank's share: part file j of the sorted
     listing belongs to rank ``j % world``."""
     pairs: List[Tuple[Optional[str], str]] = []
-    values: List[str] = []
+    texts = []
     paths = [p for p in sorted(ioutils.list_files(data_dir, "*/part-*"))
              if ".tmp" not in os.path.dirname(p) and not p.endswith(".w")]
     for j, path in enumerate(paths):
         if j % world != rank:
             continue
+        if path.endswith(".txt"):
+            # the file's bytes are the message buffer (no per-line strings)
+            with open(path, "rb") as f:
+                texts.append(TextLines.from_bytes(f.read()))
+            continue
         with open(path, "r", encoding="utf-8") as f:
-            if path.endswith(".txt"):
-                vals = f.read().split("\n")
-                if vals and vals[-1] == "":
-                    vals.pop()
-                values.extend(vals)
-                continue
             for line in f:
                 if line.strip():
                     k, m = json.loads(line)
                     pairs.append((k, m))
+    values = concat_lines(texts)
     if not pairs:
         return Dataset.from_values(values)
     return Dataset([(None, v) for v in values] + pairs)
@@ -130,7 +138,7 @@ def read_log_share(root: str, topic_name: str, starts: List[int], ends: List[int
     """Records of this rank's contiguous share of every partition's [start, end) range."""
     from ..transport import log as tlog
     out: List[Tuple[Optional[str], str]] = []
-    values: List[str] = []
+    texts = []
     topic = tlog.Topic(root, topic_name)
     try:
         for p, (lo, hi) in enumerate(zip(starts, ends)):
@@ -140,9 +148,9 @@ def read_log_share(root: str, topic_name: str, starts: List[int], ends: List[int
                 continue
             r = topic.reader(p, a)
             try:
-                vals, _ = r.read_text(b)
-                if vals is not None:
-                    values.extend(vals)
+                lines, _ = r.read_text_lines(b)
+                if lines is not None:
+                    texts.append(lines)
                     continue
                 while r.position < b:
                     recs = r.poll(min(65536, b - r.position), 100)
@@ -156,6 +164,7 @@ def read_log_share(root: str, topic_name: str, starts: List[int], ends: List[int
                 r.close()
     finally:
         topic.close()
+    values = concat_lines(texts)
     if not out:
         return Dataset.from_values(values)
     return Dataset([(None, v) for v in values] + out)

@@ -45,15 +45,16 @@ def drain_dataset(consumer: tlog.TopicConsumer,
                   end_offsets: Optional[List[int]] = None) -> Dataset:
     """Everything currently available as a :class:`Dataset`: partitions are read in bulk
     natively (messages only) unless a record has a key or a multi-line value."""
+    from ..textlines import concat_lines
     topic = consumer.topic
     ends = end_offsets or topic.end_offsets()
-    values: List[str] = []
+    texts = []
     pairs: List[Tuple[Optional[str], str]] = []
     for r in consumer.readers:
         target = ends[r.partition]
-        vals, _ = r.read_text(target)
-        if vals is not None:
-            values.extend(vals)
+        lines, _ = r.read_text_lines(target)
+        if lines is not None:
+            texts.append(lines)
             continue
         while r.position < target:
             recs = r.poll(min(65536, target - r.position), 50)
@@ -64,6 +65,8 @@ def drain_dataset(consumer: tlog.TopicConsumer,
                     r.seek(off)
                     break
                 pairs.append((k, v))
+    # keyless single-line messages stay one buffer (TextLines): no Python string per record
+    values = concat_lines(texts)
     if not pairs:
         return Dataset.from_values(values)
     return Dataset([(None, v) for v in values] + pairs)

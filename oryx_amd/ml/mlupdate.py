@@ -34,6 +34,7 @@ import time
 from typing import Any, List, Optional, Sequence, Tuple
 
 from ..api import BatchLayerUpdate, Dataset, TopicProducer
+from ..textlines import TextLines, concat_lines
 from .. import tracing
 from ..parallel import dist
 from ..utils import ioutils, lang, pmml as pmmlu, rng
@@ -109,6 +110,8 @@ class MLUpdate(BatchLayerUpdate):
         """Default: random split with probability ``test_fraction`` per datum."""
         gen = rng.get_random().generator
         mask = gen.random(len(new_data)) < self.test_fraction
+        if isinstance(new_data, TextLines):
+            return new_data.take(~mask), new_data.take(mask)
         train = [d for d, m in zip(new_data, mask) if not m]
         test = [d for d, m in zip(new_data, mask) if m]
         return train, test
@@ -409,11 +412,12 @@ class MLUpdate(BatchLayerUpdate):
         return {}
 
     def _split_train_test(self, new_msgs, past_msgs):
+        # TextLines buffers stay buffers (concat_lines / the apps' native splits)
         if self.test_fraction <= 0.0:
-            return (list(new_msgs) + list(past_msgs or [])), []
+            return concat_lines([new_msgs, past_msgs]), []
         if self.test_fraction >= 1.0:
-            return list(past_msgs or []), list(new_msgs)
+            return concat_lines([past_msgs]), new_msgs
         if not new_msgs:
             return list(past_msgs or []), []
-        train, test = self.split_new_data_to_train_test(list(new_msgs))
-        return train + list(past_msgs or []), test
+        train, test = self.split_new_data_to_train_test(new_msgs)
+        return concat_lines([train, past_msgs]), test

@@ -42,6 +42,7 @@ import numpy as np
 import torch
 
 from ... import ingest
+from ...textlines import TextLines, concat_lines
 from ...ml import hyperparams as hp
 from ...ml.mlupdate import MLUpdate
 from ...parallel import dist, shuffle
@@ -560,7 +561,7 @@ class ALSUpdate(MLUpdate):
                         for j, r in zip(mine.tolist(), rows))
         dist.barrier(ctx)
         # users owned by this rank (crc32 owner of the ID) with their known items
-        all_lines = list(new_data) + list(past_data or [])
+        all_lines = concat_lines([new_data, past_data])
         if self.no_known_items:
             owned = np.nonzero(shuffle.owner_of_strings(x_ids, W) == R)[0]
             xr = x_rows.take(owned).rows() if len(owned) else []
@@ -651,7 +652,7 @@ class ALSUpdate(MLUpdate):
         return x_ids, textfmt.format_rows(X), y_ids, textfmt.format_rows(Y)
 
     def _publish_local(self, pmml, new_data, past_data, model_parent_path, model_update_topic):
-        all_data = list(new_data) + list(past_data or [])
+        all_data = concat_lines([new_data, past_data])
         x_ids, x_text, y_ids, y_text = self._published_rows(pmml, model_parent_path)
         log.info("Sending item / Y data as model updates")
         if len(y_ids):
@@ -692,16 +693,19 @@ class ALSUpdate(MLUpdate):
                                                  int(ts.max()) if len(ts) else -big],
                                                 dtype=np.int64), self.dist_ctx, op="max")
             if mm[1] == -big:
-                return list(new_data), []
+                return new_data, []
             lo, hi = int(-mm[0]), int(mm[1])
         elif len(ts) == 0:
-            return list(new_data), []
+            return new_data, []
         else:
             lo, hi = int(ts.min()), int(ts.max())
         log.info("New data timestamp range: %d - %d", lo, hi)
         boundary = int(hi - self.get_test_fraction() * (hi - lo))
         log.info("Splitting at timestamp %d", boundary)
         # lines that fail to parse are dropped by the parser; keep alignment via per-line parse
+        if len(ts) == len(new_data) and isinstance(new_data, TextLines):
+            is_train = ts < boundary
+            return new_data.take(is_train), new_data.take(~is_train)
         train, test = [], []
         if len(ts) == len(new_data):
             for line, t in zip(new_data, ts.tolist()):

@@ -1,0 +1,194 @@
+"""Newline-delimited messages held as one byte buffer (the batch layer's bulk data form).
+
+The reference moves an interval's messages and its whole history through Spark as
+partitioned binary SequenceFiles (``[lambda]/batch/BatchUpdateFunction.java:103-130``,
+``SaveToHDFSFunction.java:59-76``): no per-record object until an app parses them.  Here the
+same role is played by :class:`TextLines`: the messages of a log drain, of a part file or of a
+train/test split stay in ONE UTF-8 buffer in which every line ends with ``b"\\n"``; the native
+parsers (``ingest.parse_ratings`` and friends) read that buffer directly, part files are that
+buffer written out, and selections (train/test masks, shares) are gathered natively.  It is a
+read-only ``Sequence[str]``, so any code that iterates or indexes it still works -- decoding
+then happens lazily, once.
+"""
+
+from __future__ import annotations
+
+import collections.abc
+import ctypes
+from typing import Iterable, List, Optional, Sequence, Union
+
+import numpy as np
+
+from . import native
+
+__all__ = ["TextLines", "concat_lines", "as_buffer"]
+
+_NL = 10
+
+
+def _addr(buf) -> int:
+    if isinstance(buf, np.ndarray):
+        return buf.ctypes.data
+    if isinstance(buf, bytearray):
+        return ctypes.addressof((ctypes.c_char * len(buf)).from_buffer(buf))
+    return ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p).value
+
+
+class TextLines(collections.abc.Sequence):
+    """``n`` messages in ``buf`` (bytes / bytearray / uint8 array), each followed by ``\\n``.
+
+    ``n`` may be given (the log's bulk read knows it); the line index (end offsets) is built
+    natively on first indexed access.
+    """
+
+    __slots__ = ("buf", "_n", "_ends", "_strs")
+
+    def __init__(self, buf, n: Optional[int] = None, ends: Optional[np.ndarray] = None):
+        if isinstance(buf, memoryview):
+            buf = bytes(buf)
+        self.buf = buf
+        self._ends = ends
+        self._strs: Optional[List[str]] = None
+        if n is None:
+            n = len(self.ends()) if len(buf) else 0
+        self._n = int(n)
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_strings(cls, strs: Iterable[str]) -> "TextLines":
+        strs = list(strs)
+        if not strs:
+            return cls(b"", 0)
+        data = ("\n".join(strs) + "\n").encode("utf-8")
+        return cls(data, len(strs))
+
+    @classmethod
+    def from_bytes(cls, data: bytes) -> "TextLines":
+        """Text (e.g. a part file); a missing final newline is added."""
+        if data and data[-1:] != b"\n":
+            data = bytes(data) + b"\n"
+        return cls(data)
+
+    # ------------------------------------------------------------------ sequence
+    def __len__(self) -> int:
+        return self._n
+
+    def nbytes(self) -> int:
+        return len(self.buf)
+
+    def ends(self) -> np.ndarray:
+        """Offset of every line's ``\\n`` (int64, native threaded scan)."""
+        if self._ends is None:
+            n_buf = len(self.buf)
+            if n_buf == 0:
+                self._ends = np.zeros(0, dtype=np.int64)
+            else:
+                cap = getattr(self, "_n", None) or max(1, n_buf // 8)
+                while True:
+                    out = np.empty(int(cap), dtype=np.int64)
+                    got = native.runtime().oryx_line_ends(_addr(self.buf), n_buf,
+                                                          out.ctypes.data, int(cap))
+                    if got >= 0:
+                        self._ends = out[:got]
+                        break
+                    cap = -got
+        return self._ends
+
+    def _decode_all(self) -> List[str]:
+        if self._strs is None:
+            text = bytes(self.buf).decode("utf-8") if not isinstance(self.buf, str) else self.buf
+            parts = text.split("\n")
+            if parts and parts[-1] == "":
+                parts.pop()
+            self._strs = parts
+        return self._strs
+
+    def __getitem__(self, j):
+        if isinstance(j, slice):
+            idx = np.arange(self._n)[j]
+            return self.take(idx)
+        if self._strs is not None:
+            return self._strs[j]
+        n = self._n
+        if j < 0:
+            j += n
+        if not 0 <= j < n:
+            raise IndexError(j)
+        if self._ends is None and j in (0, n - 1):
+            # first / last line without indexing the whole buffer
+            b = bytes(memoryview(self.buf)[:1 << 20]) if j == 0 else None
+            if j == 0 and b is not None and b"\n" in b:
+                return b[:b.index(b"\n")].decode("utf-8")
+            if j == n - 1:
+                mv = memoryview(self.buf)
+                tail = bytes(mv[max(0, len(mv) - (1 << 20)):len(mv) - 1])
+                if b"\n" in tail or len(tail) == len(mv) - 1:
+                    return tail[tail.rfind(b"\n") + 1:].decode("utf-8")
+        e = self.ends()
+        b = int(e[j - 1]) + 1 if j else 0
+        return bytes(memoryview(self.buf)[b:int(e[j])]).decode("utf-8")
+
+    def __iter__(self):
+        return iter(self._decode_all())
+
+    def __add__(self, other):
+        return concat_lines([self, other])
+
+    def __radd__(self, other):
+        return concat_lines([other, self])
+
+    def __eq__(self, other):
+        if isinstance(other, TextLines):
+            return self._n == other._n and bytes(self.buf) == bytes(other.buf)
+        if isinstance(other, (list, tuple)):
+            return list(self) == list(other)
+        return NotImplemented
+
+    def __repr__(self):
+        return "TextLines[%d lines, %d bytes]" % (self._n, len(self.buf))
+
+    # ------------------------------------------------------------------ bulk
+    def joined(self):
+        """The whole buffer: every message followed by ``\\n`` (what native parsers take)."""
+        return self.buf
+
+    def take(self, sel) -> "TextLines":
+        """Lines selected by a boolean mask or an index array, in that order (native gather)."""
+        sel = np.asarray(sel)
+        idx = np.flatnonzero(sel) if sel.dtype == bool else sel.astype(np.int64)
+        if len(idx) == self._n and (len(idx) == 0 or (idx[0] == 0 and
+                                                      np.all(np.diff(idx) == 1))):
+            return self
+        if len(idx) == 0:
+            return TextLines(b"", 0)
+        e = self.ends()
+        starts = np.r_[0, e[:-1] + 1]
+        size = int((e[idx] - starts[idx] + 1).sum())
+        out = np.empty(size, dtype=np.uint8)
+        idx = np.ascontiguousarray(idx, dtype=np.int64)
+        native.runtime().oryx_gather_lines(_addr(self.buf), e.ctypes.data, idx.ctypes.data,
+                                           len(idx), out.ctypes.data)
+        return TextLines(out, len(idx))
+
+
+def concat_lines(parts: Sequence[Union[TextLines, Sequence[str], None]]):
+    """Concatenation that stays a :class:`TextLines` when every non-empty part is one (else a
+    plain list of strings)."""
+    parts = [p for p in parts if p is not None and len(p)]
+    if not parts:
+        return TextLines(b"", 0)
+    if len(parts) == 1 and isinstance(parts[0], TextLines):
+        return parts[0]
+    if all(isinstance(p, TextLines) for p in parts):
+        bufs = [np.frombuffer(p.buf, dtype=np.uint8) if not isinstance(p.buf, np.ndarray)
+                else p.buf for p in parts]
+        return TextLines(np.concatenate(bufs), sum(len(p) for p in parts))
+    out: List[str] = []
+    for p in parts:
+        out.extend(p)
+    return out
+
+
+def as_buffer(lines) -> Optional[object]:
+    """The newline-terminated byte buffer of ``lines`` when it is a :class:`TextLines`."""
+    return lines.joined() if isinstance(lines, TextLines) else None

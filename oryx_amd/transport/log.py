@@ -341,6 +341,42 @@ class PartitionReader:
             out.append((off, ts, key, val))
         return out
 
+    def read_text_lines(self, end_offset: int):
+        """As :meth:`read_text` but the values stay one buffer: (:class:`TextLines` or None,
+        records read).  No per-record Python string is created."""
+        from ..textlines import TextLines
+        lib = _lib()
+        start = self.position
+        chunks: List[bytes] = []
+        total = 0
+        buf = getattr(_TLS, "text_buf", None)
+        if buf is None:
+            buf = _TLS.text_buf = ctypes.create_string_buffer(16 << 20)
+        cap = len(buf)
+        used = ctypes.c_longlong(0)
+        flags = ctypes.c_int(0)
+        while self.position < end_offset:
+            n = lib.oryx_reader_read_text(self._r, int(end_offset), buf, cap,
+                                          ctypes.byref(used), ctypes.byref(flags))
+            if n == -3:
+                raise LogCorruptionError(lib.oryx_log_last_error().decode())
+            if n < 0:
+                raise IOError(lib.oryx_log_last_error().decode())
+            if flags.value & 3:
+                self.seek(start)
+                return None, 0
+            if flags.value & 4:
+                cap = max(int(used.value), 2 * cap)
+                buf = ctypes.create_string_buffer(cap)
+                continue
+            if n == 0:
+                break
+            chunks.append(ctypes.string_at(buf, used.value))
+            total += n
+        if not chunks:
+            return TextLines(b"", 0), 0
+        return TextLines(chunks[0] if len(chunks) == 1 else b"".join(chunks), total), total
+
     def read_text(self, end_offset: int) -> Tuple[Optional[List[str]], int]:
         """Values of every record up to ``end_offset`` (exclusive) in one bulk native read.
 

@@ -1,0 +1,59 @@
+"""TextLines: the batch layer's one-buffer message form (drain -> part files -> parse)."""
+
+import pickle
+
+import numpy as np
+
+from oryx_amd import ingest
+from oryx_amd.api import Dataset
+from oryx_amd.layers.batch import read_past_data, save_interval_data
+from oryx_amd.textlines import TextLines, concat_lines
+from oryx_amd.transport import log as tlog
+
+
+def test_sequence_behaviour():
+    strs = ["u1,i1,1.0,5", "u2,ié,2.5,6", "", "u3,i3,,7"]
+    t = TextLines.from_strings(strs)
+    assert len(t) == 4 and list(t) == strs
+    assert t[0] == strs[0] and t[-1] == strs[-1] and t[1] == strs[1] and t[2] == ""
+    assert list(t[1:3]) == strs[1:3]
+    assert list(t.take(np.array([False, True, False, True]))) == [strs[1], strs[3]]
+    assert list(t.take(np.array([3, 0]))) == [strs[3], strs[0]]
+    both = concat_lines([t, TextLines.from_strings(["x"])])
+    assert isinstance(both, TextLines) and list(both) == strs + ["x"]
+    assert concat_lines([t, ["y"]]) == strs + ["y"]
+    assert list(pickle.loads(pickle.dumps(both))) == strs + ["x"]
+    assert list(TextLines.from_bytes(b"a\nb")) == ["a", "b"]
+
+
+def test_parse_ratings_from_buffer_equals_strings():
+    lines = ["u%d,i%d,%d.5,%d" % (j % 13, j % 7, j % 5, 1000 + j) for j in range(5000)]
+    t = concat_lines([TextLines.from_strings(lines[:2000]),
+                      TextLines.from_strings(lines[2000:])])
+    for src in (t, t.take(np.arange(len(t)) % 3 != 0)):
+        d1, d2, e1, e2 = ingest.IdDict(), ingest.IdDict(), ingest.IdDict(), ingest.IdDict()
+        a = ingest.parse_ratings(src, d1, d2, default_ts=0)
+        b = ingest.parse_ratings(list(src), e1, e2, default_ts=0)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+
+
+def test_drain_save_read_round_trip(tmp_path):
+    root = str(tmp_path / "log")
+    tlog.maybe_create_topic(root, "In", 3)
+    topic = tlog.Topic(root, "In")
+    msgs = ["u%d,i%d,1" % (j, j % 17) for j in range(3000)]
+    topic.append_batch([(None, m) for m in msgs])
+    from oryx_amd.layers.common import drain_dataset
+    cons = tlog.TopicConsumer(topic, start="earliest")
+    ds = drain_dataset(cons)
+    assert isinstance(ds.values(), TextLines)
+    assert sorted(ds.values()) == sorted(msgs)
+    data_dir = "file:" + str(tmp_path / "data") + "/"
+    save_interval_data(data_dir, 123, ds)
+    save_interval_data(data_dir, 124, Dataset.from_values(["u9,i9,2"]))
+    past = read_past_data(data_dir)
+    assert isinstance(past.values(), TextLines)
+    assert sorted(past.values()) == sorted(msgs + ["u9,i9,2"])
+    cons.close()
+    topic.close()
