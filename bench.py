@@ -81,6 +81,8 @@ def main(argv=None) -> int:
     ap.add_argument("--speed-events", type=int, default=10_000)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--gather-chunks", type=int, default=None,
+                    help="row ranges per half-step factor exchange (default: trainer's)")
     args = ap.parse_args(argv)
     for key, val in PRESETS[args.preset].items():
         if getattr(args, key) is None:
@@ -103,7 +105,8 @@ def main(argv=None) -> int:
     users, items, strength = _gen_ratings(args.users_per_gpu, args.items, args.ratings_per_gpu,
                                           ctx.rank, args.seed, dev)
     trainer = ALSTrainer(args.rank_k, lam=0.001, alpha=1.0, implicit=bool(args.implicit),
-                         ctx=ctx, seed=args.seed, precision=args.precision)
+                         ctx=ctx, seed=args.seed, precision=args.precision,
+                         gather_chunks=args.gather_chunks)
     trainer.prepare(users, items, strength, n_users, args.items)
     del users, items, strength
     trainer.init_factors()
@@ -250,6 +253,7 @@ def main(argv=None) -> int:
                                 "inverses, fused HIP fold-in, UP formatting) + UP block "
                                 "append to the update log; median of 12",
             "solve_failures": trainer.failures,
+            "gather_chunks": {"items": trainer.lay_i.C, "users": trainer.lay_u.C},
         }
         print(json.dumps(rec), flush=True)
     if ctx.is_distributed:

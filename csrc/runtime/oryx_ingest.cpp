@@ -71,6 +71,7 @@ class FlatIndex {
         if (k.size() <= 16) std::memcpy(sl.in, k.data(), k.size());
         else sl.ptr = k.data();
         ++used_;
+        last_ = j;
         *inserted = true;
         return next;
       }
@@ -81,6 +82,15 @@ class FlatIndex {
       }
       j = (j + 1) & m;
     }
+  }
+  // a long key inserted from a transient view is re-pointed at its stable copy
+  void repoint_last(const char* p) {
+    if (slots_[last_].len > 16) slots_[last_].ptr = p;
+  }
+  // empty, keeping the table's capacity (a reused dictionary allocates nothing)
+  void clear() {
+    for (Slot& sl : slots_) sl.code = -1;
+    used_ = 0;
   }
 
  private:
@@ -127,6 +137,7 @@ class FlatIndex {
   }
   std::vector<Slot> slots_;
   size_t used_ = 0;
+  size_t last_ = 0;
 };
 
 struct Dict {
@@ -137,12 +148,12 @@ struct Dict {
   std::deque<std::string> keys;
   std::mutex mu;
   int64_t encode(std::string_view s) {
-    const int32_t f = map.find(s);
-    if (f >= 0) return f;
-    const int32_t code = (int32_t)keys.size();
-    keys.emplace_back(s);
     bool ins;
-    map.find_or_add(std::string_view(keys.back()), code, &ins);
+    const int32_t code = map.find_or_add(s, (int32_t)keys.size(), &ins);
+    if (ins) {
+      keys.emplace_back(s);
+      map.repoint_last(keys.back().data());
+    }
     return code;
   }
 };
@@ -221,6 +232,15 @@ extern "C" {
 void* oryx_dict_new() { return new Dict(); }
 void oryx_dict_free(void* d) { delete static_cast<Dict*>(d); }
 long long oryx_dict_size(void* d) { return (long long)static_cast<Dict*>(d)->keys.size(); }
+
+// Empties a dictionary for reuse (the speed layer's per-micro-batch dictionaries): the hash
+// table keeps its capacity, so the next batch's IDs are inserted without allocating it again.
+void oryx_dict_clear(void* dh) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  d->map.clear();
+  d->keys.clear();
+}
 
 // Encodes n strings packed back to back (lengths in lens) -> codes.  Returns n.
 long long oryx_dict_encode(void* dh, const char* buf, long long buf_len, int n, long long* codes) {
@@ -338,9 +358,20 @@ struct RatingChunk {
           else ok = oryx_ff::parse_double(f[2].data(), f[2].data() + f[2].size(), sv);
         }
         if (ok && nf >= 4 && !f[3].empty()) {
-          double t;
-          ok = oryx_ff::parse_double(f[3].data(), f[3].data() + f[3].size(), t);
-          tv = (long long)t;
+          // epoch milliseconds are plain digits: integer fast path, the float parser for
+          // anything else ("1.7e12", signs, spaces)
+          const char* a = f[3].data();
+          const size_t m = f[3].size();
+          size_t d = 0;
+          long long iv = 0;
+          while (d < m && d < 18 && a[d] >= '0' && a[d] <= '9') iv = iv * 10 + (a[d++] - '0');
+          if (d == m) {
+            tv = iv;
+          } else {
+            double t;
+            ok = oryx_ff::parse_double(a, a + m, t);
+            tv = (long long)t;
+          }
         }
         if (ok) {
           if (gu) {
@@ -403,6 +434,11 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
     if (di != du && di->keys.empty()) di->map.reserve(est);
     ch[0].gu = du;
     ch[0].gi = di;
+    const size_t rows_est = std::min<size_t>((size_t)max_rows, (size_t)(len / 4) + 1);
+    ch[0].u.reserve(rows_est);
+    ch[0].i.reserve(rows_est);
+    ch[0].s.reserve(rows_est);
+    ch[0].ts.reserve(rows_est);
     ch[0].parse(buf, buf + len, default_ts, strict != 0);
     const RatingChunk& c = ch[0];
     if (c.bad_line >= 0) return -(c.bad_line + 1);
@@ -1634,6 +1670,32 @@ long long oryx_gather_lines(const char* buf, const long long* ends, const long l
     }
   });
   return at[(size_t)n];
+}
+
+}  // extern "C"
+
+extern "C" {
+
+// Concatenates n buffers (ptrs[k], lens[k] bytes) into out, the copy split into equal byte
+// ranges over the native threads (a drain's per-partition text buffers, hundreds of MB, into
+// the one buffer the parser reads).  Returns the bytes written.
+long long oryx_concat_buffers(const char* const* ptrs, const long long* lens, long long n,
+                              char* out) {
+  std::vector<long long> at((size_t)n + 1, 0);
+  for (long long k = 0; k < n; ++k) at[(size_t)k + 1] = at[(size_t)k] + lens[k];
+  const long long total = at[(size_t)n];
+  constexpr long long kPiece = 4ll << 20;
+  oryx_ff::parallel_ranges((total + kPiece - 1) / kPiece, 1, [&](long long lo, long long hi, int) {
+    const long long b = lo * kPiece, e = std::min(total, hi * kPiece);
+    // buffers overlapping [b, e)
+    long long k = (long long)(std::upper_bound(at.begin(), at.end(), b) - at.begin()) - 1;
+    for (; k < n && at[(size_t)k] < e; ++k) {
+      const long long s0 = std::max(b, at[(size_t)k]);
+      const long long s1 = std::min(e, at[(size_t)k + 1]);
+      if (s1 > s0) memcpy(out + s0, ptrs[k] + (s0 - at[(size_t)k]), (size_t)(s1 - s0));
+    }
+  });
+  return total;
 }
 
 }  // extern "C"

@@ -10,7 +10,7 @@
 //   <root>/<topic>/<p>/<base-offset>.log    segment files of framed records
 //   <root>/<topic>/.offsets/<group>         committed "partition offset" lines
 //
-// Record frame (little endian):  u32 magic | u32 crc32(payload) | u64 offset | i64 ts_ms |
+// Record frame (little endian):  u32 magic | u32 crc32c | u64 offset | i64 ts_ms |
 //                                u32 key_len (0xFFFFFFFF = null) | u32 value_len | key | value
 // Appends from any process are serialised with flock() on the partition directory's lock
 // file and written with one pwrite() (a block past 2 GB: consecutive ones); readers never
@@ -41,30 +41,47 @@
 
 namespace {
 
-constexpr uint32_t kMagic = 0x4F52594Cu;  // "ORYL"
+// "ORY2": frames checksummed with CRC-32C (the first format, "ORYL", used the IEEE CRC-32)
+constexpr uint32_t kMagic = 0x3259524Fu;
 constexpr size_t kHeader = 4 + 4 + 8 + 8 + 4 + 4;
 constexpr uint32_t kNullKey = 0xFFFFFFFFu;
 
-// CRC-32 (IEEE, zlib's polynomial), slicing-by-8: eight table lookups per 8 input bytes
-// (~1 byte/cycle instead of ~0.2 for the bytewise loop) -- every poll and bulk read checks
-// every record, and model loads read gigabytes of update messages.
+// CRC-32C (Castagnoli, the checksum of Kafka's v2 record batches): the SSE4.2 crc32
+// instruction does 8 bytes per instruction (~10 GB/s on one core, ~6x the IEEE table loop this
+// replaced) -- every poll and bulk read checks every record, model loads read gigabytes of
+// update messages and the speed layer appends ~15 MB of UP rows per micro-batch.  CPUs without
+// SSE4.2 take a slicing-by-8 table of the same polynomial.
 uint32_t crc_tab[8][256];
-std::once_flag crc_once;
+bool crc_hw = false;
 
 void init_crc() {
   for (uint32_t i = 0; i < 256; ++i) {
     uint32_t c = i;
-    for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? 0x82F63B78u ^ (c >> 1) : c >> 1;
     crc_tab[0][i] = c;
   }
   for (uint32_t i = 0; i < 256; ++i)
     for (int t = 1; t < 8; ++t)
       crc_tab[t][i] = (crc_tab[t - 1][i] >> 8) ^ crc_tab[0][crc_tab[t - 1][i] & 0xFF];
+  __builtin_cpu_init();
+  crc_hw = __builtin_cpu_supports("sse4.2");
 }
 
-uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc = 0) {
-  std::call_once(crc_once, init_crc);
-  crc = ~crc;
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(const uint8_t* p, size_t n, uint32_t crc) {
+  uint64_t c = crc;
+  while (n >= 8) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    c = __builtin_ia32_crc32di(c, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = (uint32_t)c;
+  while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+  return c32;
+}
+
+uint32_t crc32c_table(const uint8_t* p, size_t n, uint32_t crc) {
   while (n >= 8) {
     uint32_t lo, hi;
     memcpy(&lo, p, 4);
@@ -78,7 +95,17 @@ uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc = 0) {
     n -= 8;
   }
   while (n--) crc = crc_tab[0][(crc ^ *p++) & 0xFF] ^ (crc >> 8);
-  return ~crc;
+  return crc;
+}
+
+// tables and CPU check once, at library load (a call_once per record cost more than the
+// checksum of a short record)
+struct CrcInit {
+  CrcInit() { init_crc(); }
+} crc_init_at_load;
+
+inline uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc = 0) {
+  return ~(crc_hw ? crc32c_hw(p, n, ~crc) : crc32c_table(p, n, ~crc));
 }
 
 thread_local std::string g_err;
@@ -736,6 +763,26 @@ long long oryx_log_append_values_gap(void* h, int partition, const char* key, in
   return append_records(t, h, partition, recs, ts_ms, do_fsync, nullptr);
 }
 
+// Upper bound on the bytes oryx_reader_read_text delivers for the records from the reader's
+// position up to `end_offset`: the segment bytes from the position to the current end of the
+// log, less 31 per record (each frame has a 32-byte header; the text adds one '\n').  Lets
+// the caller allocate the output once.
+long long oryx_reader_text_bound(void* rh, long long end_offset) {
+  auto* r = static_cast<Reader*>(rh);
+  if (r->fd < 0) reader_seek(r, r->next_offset);
+  if (r->next_offset >= end_offset) return 0;
+  const std::string& dir = r->topic->parts[r->part].dir;
+  long long bytes = 0;
+  for (int64_t b : list_segments(dir)) {
+    if (b < r->seg_base) continue;
+    struct stat st;
+    if (stat(seg_name(dir, b).c_str(), &st) != 0) continue;
+    bytes += (long long)st.st_size - (b == r->seg_base ? (long long)r->pos : 0);
+  }
+  const long long bound = bytes - 31 * (end_offset - r->next_offset);
+  return bound > 0 ? bound : 0;
+}
+
 // Bulk text read for the batch layer's drains: every record from the reader's position up
 // to `end_offset` (exclusive) appended to `out` as `value '\n'`, reading the segment files in
 // 4 MB blocks (one pread per block instead of two per record).  Returns the number of
@@ -748,7 +795,9 @@ long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long 
   auto* r = static_cast<Reader*>(rh);
   const std::string& dir = r->topic->parts[r->part].dir;
   constexpr size_t kBlock = 4u << 20;
-  std::vector<uint8_t> buf(kBlock);
+  // per-thread block (a fresh 4 MB vector per call paid its page faults every time)
+  thread_local std::vector<uint8_t> buf;
+  if (buf.size() < kBlock) buf.resize(kBlock);
   long long used = 0, count = 0;
   *flags = 0;
   if (r->fd < 0) reader_seek(r, r->next_offset);

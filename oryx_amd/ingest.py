@@ -39,6 +39,12 @@ class IdDict:
     def __len__(self) -> int:
         return int(self._lib.oryx_dict_size(self._h))
 
+    def clear(self) -> "IdDict":
+        """Empty the dictionary, keeping its native table's capacity (reused per batch)."""
+        self._lib.oryx_dict_clear(self._h)
+        self._keys_cache = []
+        return self
+
     def encode(self, keys: Sequence[str]) -> np.ndarray:
         buf = b"\0".join(k.encode("utf-8") for k in keys) + b"\0"
         out = np.empty(len(keys), dtype=np.int64)

@@ -43,7 +43,7 @@ from ..utils import config as cfg
 from ..parallel import dist
 from ..textlines import TextLines, concat_lines
 from ..utils import faults, ioutils, lang, rng
-from .common import AbstractLayer, IntervalTimer, drain_dataset
+from .common import AbstractLayer, IntervalTimer, drain_dataset, read_text_parallel
 
 __all__ = ["BatchLayer", "save_interval_data", "read_past_data", "delete_old_data",
            "read_log_share", "save_interval_part"]
@@ -140,29 +140,28 @@ def read_log_share(root: str, topic_name: str, starts: List[int], ends: List[int
     out: List[Tuple[Optional[str], str]] = []
     texts = []
     topic = tlog.Topic(root, topic_name)
+    readers = []
     try:
         for p, (lo, hi) in enumerate(zip(starts, ends)):
             n = hi - lo
             a, b = lo + n * rank // world, lo + n * (rank + 1) // world
-            if b <= a:
+            if b > a:
+                readers.append((topic.reader(p, a), b))
+        for (r, b), lines in zip(readers, read_text_parallel(readers)):
+            if lines is not None:
+                texts.append(lines)
                 continue
-            r = topic.reader(p, a)
-            try:
-                lines, _ = r.read_text_lines(b)
-                if lines is not None:
-                    texts.append(lines)
-                    continue
-                while r.position < b:
-                    recs = r.poll(min(65536, b - r.position), 100)
-                    if not recs:
+            while r.position < b:
+                recs = r.poll(min(65536, b - r.position), 100)
+                if not recs:
+                    break
+                for off, _, k, v in recs:
+                    if off >= b:
                         break
-                    for off, _, k, v in recs:
-                        if off >= b:
-                            break
-                        out.append((k, v))
-            finally:
-                r.close()
+                    out.append((k, v))
     finally:
+        for r, _ in readers:
+            r.close()
         topic.close()
     values = concat_lines(texts)
     if not out:

@@ -41,6 +41,16 @@ class LayerContext:
         return self.dist.device
 
 
+def read_text_parallel(jobs):
+    """``PartitionReader.read_text_lines(end)`` of every (reader, end) job, partitions read
+    concurrently (the native read runs without the GIL); one result per job, in order."""
+    if len(jobs) <= 1:
+        return [r.read_text_lines(end)[0] for r, end in jobs]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
+        return list(ex.map(lambda job: job[0].read_text_lines(job[1])[0], jobs))
+
+
 def drain_dataset(consumer: tlog.TopicConsumer,
                   end_offsets: Optional[List[int]] = None) -> Dataset:
     """Everything currently available as a :class:`Dataset`: partitions are read in bulk
@@ -50,9 +60,10 @@ def drain_dataset(consumer: tlog.TopicConsumer,
     ends = end_offsets or topic.end_offsets()
     texts = []
     pairs: List[Tuple[Optional[str], str]] = []
-    for r in consumer.readers:
+    readers = list(consumer.readers)
+    bulk = read_text_parallel([(r, ends[r.partition]) for r in readers])
+    for r, lines in zip(readers, bulk):
         target = ends[r.partition]
-        lines, _ = r.read_text_lines(target)
         if lines is not None:
             texts.append(lines)
             continue

@@ -180,6 +180,7 @@ class ALSSpeedModelManager(SpeedModelManager):
             raise ValueError("bad min-model-load-fraction")
         self.model: Optional[ALSSpeedModel] = None
         self._stream = None
+        self._dicts = None
         # milliseconds per phase of the last build_updates (parse_aggregate, inverses, lookup
         # of the batch's IDs in the stores, foldin = kernel + validity flags to the host,
         # format_rows = GPU row text + copy, assemble = native UP message assembly)
@@ -247,7 +248,11 @@ class ALSSpeedModelManager(SpeedModelManager):
             return []
         import time
         t0 = time.perf_counter()
-        users, items = ingest.IdDict(), ingest.IdDict()
+        # per-batch dictionaries, reused (cleared) so their tables are not reallocated and
+        # re-faulted every micro-batch
+        if self._dicts is None:
+            self._dicts = (ingest.IdDict(), ingest.IdDict())
+        users, items = (d.clear() for d in self._dicts)
         u, i, s, ts = ingest.parse_ratings(new_data.values(), users, items, default_ts=0)
         u, i, s = aggregate_scores(u, i, s, ts, model.is_implicit())
         self.last_phase_ms = {"parse_aggregate": (time.perf_counter() - t0) * 1e3}

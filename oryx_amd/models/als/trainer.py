@@ -94,16 +94,22 @@ class RowLayout:
         c = torch.div(loc, self.cr, rounding_mode="floor")
         return (c * self.W + r) * self.cr + (loc - c * self.cr)
 
-    def gather(self, local: torch.Tensor, ctx: dist.DistContext, overlap_with=None):
+    def gather(self, local: torch.Tensor, ctx: dist.DistContext, overlap_with=None,
+               out: Optional[torch.Tensor] = None):
         """All-gather ``local`` ([local_rows, ...]) into the gathered layout; ``overlap_with``
-        (callable c -> None) runs before each range's exchange is started."""
+        (callable c -> None) runs before each range's exchange is started.  ``out``: the
+        previous gathered matrix, overwritten in place when its shape fits (the collectives
+        are ordered after every kernel already queued on the current stream, i.e. after the
+        last reads of the old rows), so the exchange allocates nothing per half-step."""
         if not ctx.is_distributed and self.C == 1:
             # one process, one range: the local shard IS the gathered matrix (no copy)
             if overlap_with is not None:
                 overlap_with(0)
             return local
-        out = torch.empty((self.rows,) + tuple(local.shape[1:]), dtype=local.dtype,
-                          device=local.device)
+        shape = (self.rows,) + tuple(local.shape[1:])
+        if out is None or tuple(out.shape) != shape or out.dtype != local.dtype or \
+                out.data_ptr() == local.data_ptr():
+            out = torch.empty(shape, dtype=local.dtype, device=local.device)
         handles = []
         for c in range(self.C):
             if overlap_with is not None:
@@ -367,7 +373,8 @@ class ALSTrainer:
             ev.record()
             self.events.append((label, ev))
 
-    def _half_step(self, parts, src_own_f32, src_full_bf16, dst_f32, dst_b_local, lay, name):
+    def _half_step(self, parts, src_own_f32, src_full_bf16, dst_f32, dst_b_local, lay, name,
+                   dst_full=None):
         ctx = self.ctx
         yty = None
         self._mark(name + ".start")
@@ -386,7 +393,7 @@ class ALSTrainer:
                 self._mark(name + ".solve")
         # range c's bf16 rows are exchanged while range c+1 is solved
         with tracing.range(name + ".solve+allgather"):
-            out = lay.gather(dst_b_local, ctx, overlap_with=solve)
+            out = lay.gather(dst_b_local, ctx, overlap_with=solve, out=dst_full)
         self._mark(name + ".exchange")
         return out
 
@@ -417,9 +424,9 @@ class ALSTrainer:
             watchdog.heartbeat("als.iteration")
             # items given users, then users given items (MLlib order)
             self.Yb = self._half_step(self.csr_i_parts, self.X, self.Xb, self.Y, self.Yb_local,
-                                      self.lay_i, "als.items")
+                                      self.lay_i, "als.items", self.Yb)
             self.Xb = self._half_step(self.csr_u_parts, self.Y, self.Yb, self.X, self.Xb_local,
-                                      self.lay_u, "als.users")
+                                      self.lay_u, "als.users", self.Xb)
 
     def train(self, iterations: int, checkpoint_dir: Optional[str] = None,
               checkpoint_interval: int = 0, fingerprint: str = "",

@@ -86,11 +86,14 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_dict_new", c_vp, [])
     _sig(lib, "oryx_dict_free", None, [c_vp])
     _sig(lib, "oryx_dict_size", c_ll, [c_vp])
+    _sig(lib, "oryx_dict_clear", None, [c_vp])
     _sig(lib, "oryx_dict_encode", c_ll, [c_vp, c_cp, c_ll, c_i, c_vp])
     _sig(lib, "oryx_dict_get", c_ll, [c_vp, c_cp, c_ll])
     _sig(lib, "oryx_dict_key", c_ll, [c_vp, c_ll, c_vp, c_ll])
     _sig(lib, "oryx_line_ends", c_ll, [c_vp, c_ll, c_vp, c_ll])
     _sig(lib, "oryx_gather_lines", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_concat_buffers", c_ll, [c_vp, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_reader_text_bound", c_ll, [c_vp, c_ll])
     _sig(lib, "oryx_parse_ratings", c_ll, [c_cp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                            c_ll, c_ll, c_i])
     _sig(lib, "oryx_format_float_rows", c_ll, [c_vp, c_ll, c_i, c_ll, c_vp, c_ll, c_vp])

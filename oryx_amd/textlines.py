@@ -181,8 +181,14 @@ def concat_lines(parts: Sequence[Union[TextLines, Sequence[str], None]]):
         return parts[0]
     if all(isinstance(p, TextLines) for p in parts):
         bufs = [np.frombuffer(p.buf, dtype=np.uint8) if not isinstance(p.buf, np.ndarray)
-                else p.buf for p in parts]
-        return TextLines(np.concatenate(bufs), sum(len(p) for p in parts))
+                else np.ascontiguousarray(p.buf) for p in parts]
+        lens = np.array([len(b) for b in bufs], dtype=np.int64)
+        out = np.empty(int(lens.sum()), dtype=np.uint8)
+        ptrs = np.array([b.ctypes.data for b in bufs], dtype=np.uint64)
+        # threaded native copy (hundreds of MB per drain)
+        native.runtime().oryx_concat_buffers(ptrs.ctypes.data, lens.ctypes.data, len(bufs),
+                                             out.ctypes.data)
+        return TextLines(out, sum(len(p) for p in parts))
     out: List[str] = []
     for p in parts:
         out.extend(p)

@@ -343,21 +343,24 @@ class PartitionReader:
 
     def read_text_lines(self, end_offset: int):
         """As :meth:`read_text` but the values stay one buffer: (:class:`TextLines` or None,
-        records read).  No per-record Python string is created."""
+        records read).  No per-record Python string is created: the records are read
+        natively straight into one array sized by the segment bytes left to read."""
+        import numpy as np
         from ..textlines import TextLines
         lib = _lib()
         start = self.position
-        chunks: List[bytes] = []
-        total = 0
-        buf = getattr(_TLS, "text_buf", None)
-        if buf is None:
-            buf = _TLS.text_buf = ctypes.create_string_buffer(16 << 20)
-        cap = len(buf)
+        if start >= end_offset:
+            return TextLines(b"", 0), 0
+        cap = max(int(lib.oryx_reader_text_bound(self._r, int(end_offset))), 1 << 16)
+        buf = np.empty(cap, dtype=np.uint8)
+        used_total = total = 0
         used = ctypes.c_longlong(0)
         flags = ctypes.c_int(0)
         while self.position < end_offset:
-            n = lib.oryx_reader_read_text(self._r, int(end_offset), buf, cap,
-                                          ctypes.byref(used), ctypes.byref(flags))
+            n = lib.oryx_reader_read_text(self._r, int(end_offset),
+                                          ctypes.c_void_p(buf.ctypes.data + used_total),
+                                          cap - used_total, ctypes.byref(used),
+                                          ctypes.byref(flags))
             if n == -3:
                 raise LogCorruptionError(lib.oryx_log_last_error().decode())
             if n < 0:
@@ -366,16 +369,17 @@ class PartitionReader:
                 self.seek(start)
                 return None, 0
             if flags.value & 4:
-                cap = max(int(used.value), 2 * cap)
-                buf = ctypes.create_string_buffer(cap)
+                # more was appended since the bound was taken: grow
+                cap = max(2 * cap, used_total + int(used.value))
+                grown = np.empty(cap, dtype=np.uint8)
+                grown[:used_total] = buf[:used_total]
+                buf = grown
                 continue
             if n == 0:
                 break
-            chunks.append(ctypes.string_at(buf, used.value))
+            used_total += int(used.value)
             total += n
-        if not chunks:
-            return TextLines(b"", 0), 0
-        return TextLines(chunks[0] if len(chunks) == 1 else b"".join(chunks), total), total
+        return TextLines(buf[:used_total], total), total
 
     def read_text(self, end_offset: int) -> Tuple[Optional[List[str]], int]:
         """Values of every record up to ``end_offset`` (exclusive) in one bulk native read.

@@ -18,6 +18,7 @@
 #   serving[=ARGS]      bench_serving.py [ARGS]
 #   prof=NAME:CMD       rocprofv3 --kernel-trace --stats of CMD (e.g. prof=als:bench.py,--steps,5)
 #   pmc=NAME:CTRS:CMD   one rocprofv3 --pmc pass (CTRS comma separated) of CMD
+#   env=K=V             export K=V for the following steps (env=K= unsets K)
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -26,6 +27,7 @@ PYTEST="python -u -m pytest -x -v --timeout 150 --timeout-method thread"
 
 fail() { echo "== FAILED: $1"; tail -30 "$2"; exit 1; }
 args() { echo "$1" | tr ',' ' '; }
+tag() { echo "$1" | tr -c 'a-zA-Z0-9\n' '_'; }
 
 for step in "$@"; do
   name=${step%%=*}
@@ -46,7 +48,7 @@ for step in "$@"; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $out 2>&1 || fail "$step" $out
       tail -2 $out ;;
     bench)
-      out=gpurun_out/bench${val:+_x}.json
+      out=gpurun_out/bench${val:+_$(tag "$val")}${ORYX_FORCE_COLLECTIVES:+_forced}.json
       timeout -k 10 600 python -u bench.py --steps 20 --warmup 5 $(args "$val") > $out 2> gpurun_out/bench.err || fail "$step" gpurun_out/bench.err
       tail -1 $out | cut -c1-3000 ;;
     halfstep)
@@ -83,6 +85,9 @@ for step in "$@"; do
       rm -rf gpurun_out/pmc_$pname
       timeout -s KILL 120 rocprofv3 --kernel-trace --stats --pmc $ctrs -d gpurun_out/pmc_$pname -o run --output-format csv -- python3 $cmd > gpurun_out/pmc_$pname.log 2>&1 || fail "$step" gpurun_out/pmc_$pname.log
       find gpurun_out/pmc_$pname -name "*counter_collection.csv" | head -1 | xargs -I{} head -3 {} | cut -c1-300 ;;
+    env)
+      kv=$val; k=${kv%%=*}; v=${kv#*=}
+      if [[ -n $v ]]; then export "$k=$v"; else unset "$k"; fi ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
