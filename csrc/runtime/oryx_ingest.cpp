@@ -140,14 +140,53 @@ class FlatIndex {
   size_t last_ = 0;
 };
 
+// A key that is a canonical decimal integer below kNumLimit ("0", "17", not "017" / "+1" /
+// "1.0"): such IDs (most real datasets') index a dense array instead of the hash table.  A
+// random probe into a table of 1e5-1e6 string slots costs a cache and TLB miss (~100-200 ns);
+// the array is 4 bytes per value and mostly cache resident.
+constexpr uint32_t kNumLimit = 1u << 24;
+
+inline bool numeric_key(std::string_view s, uint32_t* v) {
+  const size_t n = s.size();
+  if (n == 0 || n > 8 || (s[0] == '0' && n > 1)) return false;
+  uint32_t x = 0;
+  for (size_t j = 0; j < n; ++j) {
+    const unsigned d = (unsigned char)s[j] - '0';
+    if (d > 9) return false;
+    x = x * 10 + d;
+  }
+  if (x >= kNumLimit) return false;
+  *v = x;
+  return true;
+}
+
 struct Dict {
   // the index's long keys are views of the strings in `keys` (a deque: elements never move);
   // open addressing (FlatIndex): a micro-batch's fresh dictionary of 10k IDs costs no node
   // allocations, and lookups in a 1e6-ID dictionary one cache miss
   FlatIndex map;
   std::deque<std::string> keys;
+  // numeric keys: value -> code (-1 absent), and the values present (for clear())
+  std::vector<int32_t> num;
+  std::vector<uint32_t> num_present;
   std::mutex mu;
+  int64_t encode_num(uint32_t v) {
+    if (v >= num.size()) {
+      size_t sz = std::max<size_t>({(size_t)v + 1, num.size() * 2, 1024});
+      num.resize(std::min<size_t>(sz, kNumLimit), -1);
+    }
+    int32_t& c = num[v];
+    if (c >= 0) return c;
+    c = (int32_t)keys.size();
+    char b[12];
+    const auto r = std::to_chars(b, b + sizeof(b), v);
+    keys.emplace_back(b, (size_t)(r.ptr - b));
+    num_present.push_back(v);
+    return c;
+  }
   int64_t encode(std::string_view s) {
+    uint32_t v;
+    if (numeric_key(s, &v)) return encode_num(v);
     bool ins;
     const int32_t code = map.find_or_add(s, (int32_t)keys.size(), &ins);
     if (ins) {
@@ -155,6 +194,17 @@ struct Dict {
       map.repoint_last(keys.back().data());
     }
     return code;
+  }
+  int64_t find(std::string_view s) const {
+    uint32_t v;
+    if (numeric_key(s, &v)) return v < num.size() ? num[v] : -1;
+    return map.find(s);
+  }
+  void clear() {
+    map.clear();
+    for (uint32_t v : num_present) num[v] = -1;
+    num_present.clear();
+    keys.clear();
   }
 };
 
@@ -238,8 +288,7 @@ long long oryx_dict_size(void* d) { return (long long)static_cast<Dict*>(d)->key
 void oryx_dict_clear(void* dh) {
   Dict* d = static_cast<Dict*>(dh);
   std::lock_guard<std::mutex> g(d->mu);
-  d->map.clear();
-  d->keys.clear();
+  d->clear();
 }
 
 // Encodes n strings packed back to back (lengths in lens) -> codes.  Returns n.
@@ -260,7 +309,7 @@ long long oryx_dict_encode(void* dh, const char* buf, long long buf_len, int n, 
 long long oryx_dict_get(void* dh, const char* s, long long len) {
   Dict* d = static_cast<Dict*>(dh);
   std::lock_guard<std::mutex> g(d->mu);
-  return d->map.find(std::string_view(s, (size_t)len));
+  return d->find(std::string_view(s, (size_t)len));
 }
 
 // Copies key `code` into out (cap bytes); returns its length (or -1).
@@ -281,11 +330,20 @@ namespace {
 // order) from chunk-local maps of views; the caller merges the local dictionaries into the
 // global ones in chunk order, which reproduces the global first-appearance numbering.
 struct RatingChunk {
+  // per side (users / items): chunk-local codes of string keys, and the chunk's keys in
+  // first-appearance order (>= 0: a string key's local code; < 0: numeric key -(value + 1),
+  // which is also what the row stores -- its global code is read from the dictionary's
+  // dense array after the merge)
+  struct Side {
+    FlatIndex m;
+    std::vector<std::string_view> keys;
+    std::vector<int64_t> order;
+    std::vector<uint64_t> seen;      // bitmap of numeric values met in this chunk
+  };
   std::vector<int32_t> u, i;
   std::vector<double> s;
   std::vector<long long> ts;
-  FlatIndex umap, imap;
-  std::vector<std::string_view> ukeys, ikeys;
+  Side us, is;
   std::deque<std::string> owned;     // unescaped fields (quoted CSV / JSON lines)
   long long lines = 0, bad_line = -1;
   // single-chunk parse: codes straight from the global dictionaries (no chunk-local index
@@ -293,19 +351,32 @@ struct RatingChunk {
   Dict* gu = nullptr;
   Dict* gi = nullptr;
 
-  int32_t code(FlatIndex& m, std::vector<std::string_view>& keys, std::string_view k,
-               bool stable) {
+  int32_t code(Side& sd, std::string_view k, bool stable) {
+    uint32_t v;
+    if (numeric_key(k, &v)) {
+      const size_t w = v >> 6;
+      if (w >= sd.seen.size()) sd.seen.resize(std::max<size_t>(w + 1, sd.seen.size() * 2), 0);
+      const uint64_t bit = 1ull << (v & 63);
+      if (!(sd.seen[w] & bit)) {
+        sd.seen[w] |= bit;
+        sd.order.push_back(-(int64_t)v - 1);
+      }
+      return -(int32_t)v - 1;
+    }
     if (!stable) {
       // an unescaped token lives in a per-line buffer: index a stable copy, made only for a
       // key not seen before
-      const int32_t c = m.find(k);
+      const int32_t c = sd.m.find(k);
       if (c >= 0) return c;
       owned.emplace_back(k);
       k = owned.back();
     }
     bool inserted;
-    const int32_t c = m.find_or_add(k, (int32_t)keys.size(), &inserted);
-    if (inserted) keys.push_back(k);
+    const int32_t c = sd.m.find_or_add(k, (int32_t)sd.keys.size(), &inserted);
+    if (inserted) {
+      sd.keys.push_back(k);
+      sd.order.push_back(c);
+    }
     return c;
   }
 
@@ -378,8 +449,8 @@ struct RatingChunk {
             u.push_back((int32_t)gu->encode(f[0]));
             i.push_back((int32_t)gi->encode(f[1]));
           } else {
-            u.push_back(code(umap, ukeys, f[0], stable));
-            i.push_back(code(imap, ikeys, f[1], stable));
+            u.push_back(code(us, f[0], stable));
+            i.push_back(code(is, f[1], stable));
           }
           s.push_back(sv);
           ts.push_back(tv);
@@ -461,26 +532,37 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
     if (ch[(size_t)t].bad_line >= 0) return -(lines_before + ch[(size_t)t].bad_line + 1);
     lines_before += ch[(size_t)t].lines;
   }
-  // merge the chunk dictionaries in order, then write the rows at their offsets
+  // merge the chunk dictionaries in order (first appearances, numeric and string keys
+  // interleaved as met), then write the rows at their offsets
   std::vector<std::vector<int64_t>> umap((size_t)P), imap((size_t)P);
   std::vector<long long> off((size_t)P + 1, 0);
+  auto merge = [](Dict* d, const RatingChunk::Side& sd, std::vector<int64_t>& to_global) {
+    to_global.reserve(sd.keys.size());
+    for (int64_t e : sd.order) {
+      if (e < 0) d->encode_num((uint32_t)(-e - 1));
+      else to_global.push_back(d->encode(sd.keys[(size_t)e]));
+    }
+  };
   for (int t = 0; t < P; ++t) {
     RatingChunk& c = ch[(size_t)t];
-    umap[(size_t)t].reserve(c.ukeys.size());
-    for (auto k : c.ukeys) umap[(size_t)t].push_back(du->encode(k));
-    imap[(size_t)t].reserve(c.ikeys.size());
-    for (auto k : c.ikeys) imap[(size_t)t].push_back(di->encode(k));
+    merge(du, c.us, umap[(size_t)t]);
+    merge(di, c.is, imap[(size_t)t]);
     off[(size_t)t + 1] = off[(size_t)t] + (long long)c.u.size();
   }
   const long long total = off[(size_t)P] < max_rows ? off[(size_t)P] : max_rows;
+  const int32_t* unum = du->num.data();
+  const int32_t* inum = di->num.data();
   oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
     for (long long t = lo; t < hi; ++t) {
       const RatingChunk& c = ch[(size_t)t];
       const long long o = off[(size_t)t];
       const long long n = (long long)c.u.size();
+      const int64_t* um = umap[(size_t)t].data();
+      const int64_t* im = imap[(size_t)t].data();
       for (long long r = 0; r < n && o + r < total; ++r) {
-        out_u[o + r] = umap[(size_t)t][(size_t)c.u[(size_t)r]];
-        out_i[o + r] = imap[(size_t)t][(size_t)c.i[(size_t)r]];
+        const int32_t a = c.u[(size_t)r], b = c.i[(size_t)r];
+        out_u[o + r] = a < 0 ? unum[-(a + 1)] : um[a];
+        out_i[o + r] = b < 0 ? inum[-(b + 1)] : im[b];
         out_s[o + r] = c.s[(size_t)r];
         out_ts[o + r] = c.ts[(size_t)r];
       }

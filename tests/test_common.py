@@ -488,17 +488,22 @@ def test_parallel_ratings_parse_matches_sequential():
     n = 450_000
     u = g.integers(0, 30000, n)
     i = g.integers(0, 9000, n)
+    # ID spellings: strings, canonical integers (the dictionaries' dense numeric path),
+    # leading zeros and integers past the dense range (both hashed as strings)
+    ufmt = ["u%d", "%d", "0%d", "%d", "1677%04d"]
+    ifmt = ["i%d", "%d", "%d", "00%d"]
     lines = []
     for j in range(n):
         r = j % 97
+        uk, ik = ufmt[j % 5] % u[j], ifmt[j % 4] % i[j]
         if r == 0:
-            lines.append('["u%d","i%d",2.5,%d]' % (u[j], i[j], j))
+            lines.append('["%s","%s",2.5,%d]' % (uk, ik, j))
         elif r == 1:
-            lines.append('"u%d","i,%d",,%d' % (u[j], i[j], j))
+            lines.append('"%s","i,%s",,%d' % (uk, ik, j))
         elif r == 2:
-            lines.append("u%d,i%d" % (u[j], i[j]))
+            lines.append("%s,%s" % (uk, ik))
         else:
-            lines.append("u%d,i%d,%d.5,%d" % (u[j], i[j], j % 7, j))
+            lines.append("%s,%s,%d.5,%d" % (uk, ik, j % 7, j))
     blob = ("\n".join(lines)).encode()
     assert len(blob) >= 8 << 20
     big = ingest.IdDict(), ingest.IdDict()
@@ -510,6 +515,15 @@ def test_parallel_ratings_parse_matches_sequential():
     for k in range(4):
         np.testing.assert_array_equal(out_big[k], np.concatenate([p[k] for p in parts]))
     assert big[0].keys() == small[0].keys() and big[1].keys() == small[1].keys()
+    # codes number the keys in first-appearance order
+    ref_u, ref_i = {}, {}
+    for j in range(n):
+        ref_u.setdefault(ufmt[j % 5] % u[j], len(ref_u))
+        ik = ifmt[j % 4] % i[j]
+        ref_i.setdefault(("i," + ik) if j % 97 == 1 else ik, len(ref_i))
+    assert big[0].keys() == list(ref_u) and big[1].keys() == list(ref_i)
+    assert big[0].get("0") == ref_u.get("0", -1) and big[0].get("17") == ref_u.get("17", -1)
+    assert big[0].get("not-there") == -1 and big[0].get("99999999") == -1
     bad = list(lines)
     bad[400_000] = "only-one-field"
     with pytest.raises(ValueError, match="line 400000"):
