@@ -98,21 +98,41 @@ def aggregate_scores(u: np.ndarray, i: np.ndarray, s: np.ndarray, ts: np.ndarray
 
 
 def aggregate_scores_device(u: np.ndarray, i: np.ndarray, s: np.ndarray, ts: np.ndarray,
-                            implicit: bool, device) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
-    """:func:`aggregate_scores` on the device: two stable sorts (time, then (user, item)) and
-    segmented scans instead of a host lexsort -- same results."""
-    if len(u) == 0:
-        return u, i, s
+                            implicit: bool, device, to_host: bool = True):
+    """:func:`aggregate_scores` on the device -- same results.  Events are ordered by
+    (user, item) then time then arrival: with ONE stable radix sort of a composite
+    ``key << tbits | (ts - min ts)`` key when both fit in 63 bits (an interval's or a few
+    months' history), else two stable sorts (time, then key).  Segmented scans do the rest.
+    ``to_host=False`` leaves (user, item, value) on the device (int64, int64, fp64)."""
     dev = torch.device(device)
-    n_i = int(i.max()) + 1
-    key = torch.from_numpy(u.astype(np.int64) * n_i + i.astype(np.int64)).to(dev)
+    if len(u) == 0:
+        if to_host:
+            return u, i, s
+        e = torch.zeros(0, dtype=torch.int64, device=dev)
+        return e, e, torch.zeros(0, dtype=torch.float64, device=dev)
+    # dictionary codes travel as int32 (half the bytes of the host's int64)
+    ud = torch.from_numpy(np.ascontiguousarray(u, dtype=np.int32)).to(dev)
+    idv = torch.from_numpy(np.ascontiguousarray(i, dtype=np.int32)).to(dev)
     tt = torch.from_numpy(np.ascontiguousarray(ts, dtype=np.int64)).to(dev)
     vv = torch.from_numpy(np.ascontiguousarray(s, dtype=np.float64)).to(dev)
-    # arrival order breaks time ties: stable sort by time, then stable sort by key
-    o1 = torch.sort(tt, stable=True).indices
-    o2 = torch.sort(key[o1], stable=True).indices
-    order = o1[o2]
+    ext = torch.stack([ud.max().long(), idv.max().long(), tt.min(), tt.max()]).cpu().tolist()
+    n_u, n_i = int(ext[0]) + 1, int(ext[1]) + 1
+    key = ud.long() * n_i + idv.long()
+    del ud, idv
+    kbits = max(1, (n_u * n_i - 1).bit_length())
+    tbits = max(1, int(ext[3] - ext[2]).bit_length())
+    if kbits + tbits <= 63:
+        comp = (key << tbits) | (tt - ext[2])
+        order = torch.sort(comp, stable=True).indices
+        del comp
+    else:
+        # arrival order breaks time ties: stable sort by time, then stable sort by key
+        o1 = torch.sort(tt, stable=True).indices
+        o2 = torch.sort(key[o1], stable=True).indices
+        order = o1[o2]
+    del tt
     key_s, s_s = key[order], vv[order]
+    del key, vv, order
     n = key_s.numel()
     first = torch.ones(n, dtype=torch.bool, device=dev)
     first[1:] = key_s[1:] != key_s[:-1]
@@ -133,7 +153,10 @@ def aggregate_scores_device(u: np.ndarray, i: np.ndarray, s: np.ndarray, ts: np.
     keep = ~torch.isnan(out)
     gk = key_s[starts][keep]
     gu = torch.div(gk, n_i, rounding_mode="floor")
-    return (gu.cpu().numpy(), (gk - gu * n_i).cpu().numpy(), out[keep].cpu().numpy())
+    gi = gk - gu * n_i
+    if not to_host:
+        return gu, gi, out[keep]
+    return gu.cpu().numpy(), gi.cpu().numpy(), out[keep].cpu().numpy()
 
 
 _NO_TS = -(1 << 62)     # parse marker of a line without a timestamp
@@ -348,38 +371,65 @@ class ALSUpdate(MLUpdate):
         ph["parse"] = ph.get("parse", 0.0) + time.perf_counter() - tp
         tp = time.perf_counter()
         dev = self._ctx(context).device
+        ctx = self._ctx(context)
+        user_ids, item_ids = users.keys(), items.keys()
+        # every rank holds the same aggregated triples; each contributes a disjoint slice
+        part = slice(ctx.rank, None, ctx.world_size)
         if dev.type == "cuda":
-            u, i, s = aggregate_scores_device(u, i, s, ts, self.implicit, dev)
+            # aggregation, the used-ID masks and the dense remap stay on the device: the
+            # aggregated triples go straight into the trainer's CSR build
+            ud, idv, sd = aggregate_scores_device(u, i, s, ts, self.implicit, dev,
+                                                  to_host=False)
+            n_agg = int(ud.numel())
+            ph["aggregate"] = ph.get("aggregate", 0.0) + time.perf_counter() - tp
+            if n_agg == 0:
+                log.info("No ratings after aggregation")
+                return None
+            tp = time.perf_counter()
+            mu = torch.zeros(len(user_ids), dtype=torch.bool, device=dev)
+            mi = torch.zeros(len(item_ids), dtype=torch.bool, device=dev)
+            mu[ud] = True
+            mi[idv] = True
+            used_u = torch.nonzero(mu).flatten().cpu().numpy()
+            used_i = torch.nonzero(mi).flatten().cpu().numpy()
+            tr_u = (torch.cumsum(mu, 0) - 1)[ud][part]
+            tr_i = (torch.cumsum(mi, 0) - 1)[idv][part]
+            tr_s = sd[part].to(torch.float32)
+            host_triples = lambda: (ud.cpu().numpy(), idv.cpu().numpy(), sd.cpu().numpy())
         else:
             u, i, s = aggregate_scores(u, i, s, ts, self.implicit)
-        ph["aggregate"] = ph.get("aggregate", 0.0) + time.perf_counter() - tp
-        if len(u) == 0:
-            log.info("No ratings after aggregation")
-            return None
-        user_ids, item_ids = users.keys(), items.keys()
-        # only IDs that survived aggregation get factors (MLlib only emits rated rows)
-        used_u = np.unique(u)
-        used_i = np.unique(i)
-        remap_u = np.full(len(user_ids), -1, dtype=np.int64)
-        remap_u[used_u] = np.arange(len(used_u))
-        remap_i = np.full(len(item_ids), -1, dtype=np.int64)
-        remap_i[used_i] = np.arange(len(used_i))
-        ctx = self._ctx(context)
+            n_agg = len(u)
+            ph["aggregate"] = ph.get("aggregate", 0.0) + time.perf_counter() - tp
+            if n_agg == 0:
+                log.info("No ratings after aggregation")
+                return None
+            tp = time.perf_counter()
+            # only IDs that survived aggregation get factors (MLlib only emits rated rows)
+            used_u = np.unique(u)
+            used_i = np.unique(i)
+            remap_u = np.full(len(user_ids), -1, dtype=np.int64)
+            remap_u[used_u] = np.arange(len(used_u))
+            remap_i = np.full(len(item_ids), -1, dtype=np.int64)
+            remap_i[used_i] = np.arange(len(used_i))
+            tr_u = torch.from_numpy(remap_u[u][part])
+            tr_i = torch.from_numpy(remap_i[i][part])
+            tr_s = torch.from_numpy(s[part].astype(np.float32))
+            host_triples = lambda: (u, i, s)
         seed = rng.next_seed()
         trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx, seed=seed,
                              precision=self.precision)
         t0 = time.perf_counter()
-        # every rank holds the same aggregated triples; each contributes a disjoint slice
-        part = slice(ctx.rank, None, ctx.world_size)
-        trainer.prepare(torch.from_numpy(remap_u[u][part]), torch.from_numpy(remap_i[i][part]),
-                        torch.from_numpy(s[part].astype(np.float32)), len(used_u), len(used_i))
-        x_ids = [user_ids[j] for j in used_u]
-        y_ids = [item_ids[j] for j in used_i]
+        trainer.prepare(tr_u, tr_i, tr_s, len(used_u), len(used_i))
+        del tr_u, tr_i, tr_s
+        x_ids = [user_ids[j] for j in used_u.tolist()]
+        y_ids = [item_ids[j] for j in used_i.tolist()]
+        ph["ids_remap"] = ph.get("ids_remap", 0.0) + time.perf_counter() - tp - \
+            (trainer.timings.get("prepare_s") or 0)
         ckpt_dir, fingerprint = None, ""
         if self.checkpoint_interval > 0 and self.current_model_dir:
             # neither the world size nor the init seed: a checkpoint holds global factors, and
             # a group relaunched on fewer GPUs (parallel/elastic.py) resumes from it
-            fingerprint = _fingerprint(u, i, s, features, lam, alpha, self.implicit,
+            fingerprint = _fingerprint(*host_triples(), features, lam, alpha, self.implicit,
                                        self.iterations)
             ckpt_dir = os.path.join(self.current_model_dir, ".checkpoint",
                                     "als-" + fingerprint[:16])
@@ -400,7 +450,7 @@ class ALSUpdate(MLUpdate):
         x_rows = textfmt.format_rows(f.X) if ctx.is_main else None
         y_rows = textfmt.format_rows(f.Y) if ctx.is_main else None
         ph["format_rows"] = ph.get("format_rows", 0.0) + time.perf_counter() - tp
-        log.info("ALS %d ratings, %d users, %d items, rank %d: %.3fs", len(u), len(used_u),
+        log.info("ALS %d ratings, %d users, %d items, rank %d: %.3fs", n_agg, len(used_u),
                  len(used_i), features, time.perf_counter() - t0)
         if not ctx.is_main:
             return None
@@ -408,6 +458,7 @@ class ALSUpdate(MLUpdate):
         write_features(os.path.join(candidate_path, "X"), x_ids, x_rows)
         write_features(os.path.join(candidate_path, "Y"), y_ids, y_rows)
         ph["write_factors"] = ph.get("write_factors", 0.0) + time.perf_counter() - tp
+        tp = time.perf_counter()
         pmml = pmmlu.build_skeleton_pmml()
         pmml.add_extension("X", "X/")
         pmml.add_extension("Y", "Y/")
@@ -418,14 +469,15 @@ class ALSUpdate(MLUpdate):
             pmml.add_extension("alpha", alpha)
         pmml.add_extension_content("XIDs", x_ids)
         pmml.add_extension_content("YIDs", y_ids)
+        ph["pmml"] = ph.get("pmml", 0.0) + time.perf_counter() - tp
         self._cache[candidate_path] = {"x_ids": x_ids, "y_ids": y_ids, "X": X, "Y": Y,
                                        "x_rows": x_rows, "y_rows": y_rows}
         its = trainer.timings.get("iteration_ms", [])
         self._timings[candidate_path] = {
-            "ratings": int(len(u)), "users": len(used_u), "items": len(used_i),
+            "ratings": n_agg, "users": len(used_u), "items": len(used_i),
             "prepare_s": trainer.timings.get("prepare_s"), "iteration_ms": its,
             "resumed_from_iteration": getattr(trainer, "resumed_from", 0),
-            "ratings_per_s": (len(u) * 1e3 / (sum(its) / len(its))) if its else None}
+            "ratings_per_s": (n_agg * 1e3 / (sum(its) / len(its))) if its else None}
         return pmml
 
     # ---------------------------------------------------------------- sharded path

@@ -158,12 +158,14 @@ def test_device_aggregation_matches_host():
     i = g.integers(0, 40, n)
     s = g.integers(1, 5, n).astype(np.float64)
     s[g.random(n) < 0.1] = np.nan
-    ts = g.integers(0, 1000, n)         # many time ties: arrival order decides
-    for implicit in (True, False):
-        a = aggregate_scores(u, i, s, ts, implicit)
-        b = aggregate_scores_device(u, i, s, ts, implicit, "cpu")
-        for x, y in zip(a, b):
-            assert np.array_equal(x, y) or np.allclose(x, y, rtol=1e-12, equal_nan=True)
+    # many time ties (arrival order decides): one composite-key sort; a time range too wide
+    # to pack next to the (user, item) key: the two-sort path
+    for ts in (g.integers(0, 1000, n), g.integers(0, 1 << 60, n) // 977 * 977):
+        for implicit in (True, False):
+            a = aggregate_scores(u, i, s, ts, implicit)
+            b = aggregate_scores_device(u, i, s, ts, implicit, "cpu")
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y) or np.allclose(x, y, rtol=1e-12, equal_nan=True)
 
 
 @pytest.mark.gpu
