@@ -294,33 +294,40 @@ def format_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndarra
 
 
 def assemble_als_updates(users: IdDict, items: IdDict, u: np.ndarray, i: np.ndarray,
-                         xrows, yrows, vx: np.ndarray, vy: np.ndarray, with_known: bool):
+                         xrows, yrows, vx: np.ndarray, vy: np.ndarray, with_known: bool,
+                         lo: int = 0, hi: Optional[int] = None):
     """As :func:`format_als_updates` with the factor rows already formatted
     (:class:`~oryx_amd.ops.textfmt.RowText`, e.g. by the GPU formatter).  Returns a
-    :class:`~oryx_amd.api.MessageBlock` (one buffer; producers append it natively)."""
+    :class:`~oryx_amd.api.MessageBlock` (one buffer; producers append it natively).
+    ``lo`` / ``hi``: only the events [lo, hi) (a chunk of a pipelined publish)."""
     from .api import MessageBlock
-    n = len(u)
-    if n == 0:
+    hi = len(u) if hi is None else int(hi)
+    lo = int(lo)
+    n = hi - lo
+    if n <= 0:
         return MessageBlock(b"", np.zeros(0, dtype=np.int64))
-    u = np.ascontiguousarray(u, dtype=np.int64)
-    i = np.ascontiguousarray(i, dtype=np.int64)
-    vx = np.ascontiguousarray(vx, dtype=np.uint8)
-    vy = np.ascontiguousarray(vy, dtype=np.uint8)
-    xe = np.ascontiguousarray(xrows.ends, dtype=np.int64)
-    ye = np.ascontiguousarray(yrows.ends, dtype=np.int64)
+    u = np.ascontiguousarray(u[lo:hi], dtype=np.int64)
+    i = np.ascontiguousarray(i[lo:hi], dtype=np.int64)
+    vx = np.ascontiguousarray(vx[lo:hi], dtype=np.uint8)
+    vy = np.ascontiguousarray(vy[lo:hi], dtype=np.uint8)
+    xb = int(xrows.ends[lo - 1]) if lo else 0
+    yb = int(yrows.ends[lo - 1]) if lo else 0
+    xe = np.ascontiguousarray(xrows.ends[lo:hi] - xb, dtype=np.int64)
+    ye = np.ascontiguousarray(yrows.ends[lo:hi] - yb, dtype=np.int64)
     vp = ctypes.c_void_p
     lib = native.runtime()
-    cap = len(xrows.blob) + len(yrows.blob) + n * 256
+    cap = int(xe[-1]) + int(ye[-1]) + n * 256
     ends = np.empty(2 * n, dtype=np.int64)
     n_msgs = ctypes.c_longlong(0)
+    xptr = vp(_buf_ptr(xrows.blob).value + xb)
+    yptr = vp(_buf_ptr(yrows.blob).value + yb)
     while True:
         out = _host_buffer(cap)
         used = lib.oryx_assemble_als_updates(
             users.handle, items.handle, u.ctypes.data_as(vp), i.ctypes.data_as(vp),
-            _buf_ptr(xrows.blob), xe.ctypes.data_as(vp), _buf_ptr(yrows.blob),
-            ye.ctypes.data_as(vp), vx.ctypes.data_as(vp), vy.ctypes.data_as(vp), n,
-            int(bool(with_known)), out.ctypes.data_as(vp), cap, ends.ctypes.data_as(vp),
-            ctypes.byref(n_msgs))
+            xptr, xe.ctypes.data_as(vp), yptr, ye.ctypes.data_as(vp), vx.ctypes.data_as(vp),
+            vy.ctypes.data_as(vp), n, int(bool(with_known)), out.ctypes.data_as(vp), cap,
+            ends.ctypes.data_as(vp), ctypes.byref(n_msgs))
         if used >= 0:
             break
         cap = -used + 1

@@ -33,6 +33,57 @@ __all__ = ["SpeedLayer"]
 log = logging.getLogger(__name__)
 
 
+
+def publish_blocks(producer, blocks, stats: Optional[dict] = None) -> int:
+    """Append a stream of UP blocks (``MessageBlock`` or lists of messages) in order, each on
+    a writer thread while the next is produced (the native append and the native assembly
+    both run without the GIL, so the log write overlaps the rest of the interval's output).
+    Returns the number of messages sent; ``stats`` (a dict) receives ``write_ms`` (the
+    appends) and ``tail_ms`` (waiting for them after the last block was produced)."""
+    import queue
+    q: "queue.Queue" = queue.Queue(maxsize=2)
+    errors: list = []
+
+    write_s = [0.0]
+
+    def writer():
+        while True:
+            b = q.get()
+            if b is None:
+                return
+            if errors:
+                continue
+            t0 = time.perf_counter()
+            try:
+                if isinstance(b, MessageBlock):
+                    producer.send_block("UP", b)
+                else:
+                    producer.send_many(("UP", m) for m in b)
+            except BaseException as e:     # surfaced on the caller's thread
+                errors.append(e)
+            write_s[0] += time.perf_counter() - t0
+
+    t = threading.Thread(target=writer, name="oryx-up-writer", daemon=True)
+    t.start()
+    sent = 0
+    try:
+        for b in blocks:
+            if errors:
+                break
+            if len(b):
+                q.put(b)
+                sent += len(b)
+    finally:
+        t_end = time.perf_counter()
+        q.put(None)
+        t.join()
+    if stats is not None:
+        stats["write_ms"] = write_s[0] * 1e3
+        stats["tail_ms"] = (time.perf_counter() - t_end) * 1e3
+    if errors:
+        raise errors[0]
+    return sent
+
 class SpeedLayer(AbstractLayer):
     layer_name = "SpeedLayer"
     config_group = "speed"
@@ -93,13 +144,17 @@ class SpeedLayer(AbstractLayer):
         records = drain_dataset(self._input_consumer)
         sent = 0
         if len(records):
-            updates = self._manager.build_updates(records)
-            if isinstance(updates, MessageBlock):
-                self._producer.send_block("UP", updates)
-                sent = len(updates)
-            elif updates:
-                self._producer.send_many(("UP", u) for u in updates)
-                sent = len(updates) if hasattr(updates, "__len__") else 0
+            blocks = getattr(self._manager, "build_update_blocks", None)
+            if blocks is not None:
+                sent = publish_blocks(self._producer, blocks(records))
+            else:
+                updates = self._manager.build_updates(records)
+                if isinstance(updates, MessageBlock):
+                    self._producer.send_block("UP", updates)
+                    sent = len(updates)
+                elif updates:
+                    self._producer.send_many(("UP", u) for u in updates)
+                    sent = len(updates) if hasattr(updates, "__len__") else 0
             self._producer.flush()
         self.commit_input_offsets()
         self.intervals_run += 1

@@ -41,7 +41,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ... import ingest
+from ... import ingest, native
 from ...textlines import TextLines, concat_lines
 from ...ml import hyperparams as hp
 from ...ml.mlupdate import MLUpdate
@@ -70,6 +70,25 @@ def aggregate_scores(u: np.ndarray, i: np.ndarray, s: np.ndarray, ts: np.ndarray
     Implicit: sum of the values after the last NaN (delete) in time order; a trailing NaN drops
     the pair.  Explicit: the last value; NaN drops the pair.
     """
+    if len(u) == 0:
+        return u, i, s
+    # one native sort + group scan (csrc/runtime/oryx_ingest.cpp)
+    u = np.ascontiguousarray(u, dtype=np.int64)
+    i = np.ascontiguousarray(i, dtype=np.int64)
+    s = np.ascontiguousarray(s, dtype=np.float64)
+    ts = np.ascontiguousarray(ts, dtype=np.int64)
+    ou, oi = np.empty(len(u), np.int64), np.empty(len(u), np.int64)
+    os_ = np.empty(len(u), np.float64)
+    m = native.runtime().oryx_aggregate_scores(
+        u.ctypes.data, i.ctypes.data, s.ctypes.data, ts.ctypes.data, len(u),
+        int(bool(implicit)), ou.ctypes.data, oi.ctypes.data, os_.ctypes.data)
+    return ou[:m], oi[:m], os_[:m]
+
+
+def aggregate_scores_reference(u: np.ndarray, i: np.ndarray, s: np.ndarray, ts: np.ndarray,
+                               implicit: bool) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """numpy model of :func:`aggregate_scores` (tests compare the native and device paths
+    with it)."""
     if len(u) == 0:
         return u, i, s
     n_i = int(i.max()) + 1

@@ -243,9 +243,21 @@ class ALSSpeedModelManager(SpeedModelManager):
         return self._stream
 
     def build_updates(self, new_data: Dataset) -> List[str]:
+        """All UP messages of the interval (one :class:`~oryx_amd.api.MessageBlock` on the
+        GPU path)."""
+        blocks = list(self.build_update_blocks(new_data, chunks=1))
+        if not blocks:
+            return []
+        return blocks[0] if len(blocks) == 1 else [m for b in blocks for m in b]
+
+    def build_update_blocks(self, new_data: Dataset, chunks: int = 4):
+        """The interval's UP messages as a generator of blocks over consecutive event ranges
+        (the same messages in the same order as :meth:`build_updates`): a publisher appends
+        block j on another thread while block j + 1 is assembled
+        (:func:`oryx_amd.layers.speed.publish_blocks`)."""
         model = self.model
         if model is None or model.get_fraction_loaded() < self.min_model_load_fraction:
-            return []
+            return
         import time
         t0 = time.perf_counter()
         # per-batch dictionaries, reused (cleared) so their tables are not reallocated and
@@ -257,10 +269,16 @@ class ALSSpeedModelManager(SpeedModelManager):
         u, i, s = aggregate_scores(u, i, s, ts, model.is_implicit())
         self.last_phase_ms = {"parse_aggregate": (time.perf_counter() - t0) * 1e3}
         if len(u) == 0:
-            return []
+            return
         dev = model.device
         if dev.type == "cuda" and model.features <= 256:
-            return self._build_updates_fused(model, users, items, u, i, s)
+            yield from self._build_updates_fused(model, users, items, u, i, s, chunks)
+            return
+        out = self._build_updates_host(model, users, items, u, i, s)
+        if out:
+            yield out
+
+    def _build_updates_host(self, model, users, items, u, i, s) -> List[str]:
         try:
             xtx = model.get_xtx_solver()
             yty = model.get_yty_solver()
@@ -312,7 +330,7 @@ class ALSSpeedModelManager(SpeedModelManager):
                 out.append(self._to_update_json("Y", i_ids[j], y_rows[j], u_ids[j]))
         return out
 
-    def _build_updates_fused(self, model, users, items, u, i, s) -> List[str]:
+    def _build_updates_fused(self, model, users, items, u, i, s, chunks: int = 1):
         import time
         from ... import native
         ph = self.last_phase_ms
@@ -320,9 +338,9 @@ class ALSSpeedModelManager(SpeedModelManager):
         try:
             inv = model.solver_inverses()
         except mathx.SingularMatrixSolverException:
-            return []
+            return
         if inv is None:
-            return []
+            return
         ph["inverses"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
         xinv, yinv = inv
@@ -364,11 +382,16 @@ class ALSSpeedModelManager(SpeedModelManager):
             xrows = textfmt.format_rows(new_x)
             yrows = textfmt.format_rows(new_y)
         ph["format_rows"] = (time.perf_counter() - t0) * 1e3
-        t0 = time.perf_counter()
-        out = ingest.assemble_als_updates(users, items, u, i, xrows, yrows, valid[:n] > 0,
-                                          valid[n:] > 0, not self.no_known_items)
-        ph["assemble"] = (time.perf_counter() - t0) * 1e3
-        return out
+        ph["assemble"] = 0.0
+        vxh, vyh = valid[:n] > 0, valid[n:] > 0
+        chunks = max(1, min(int(chunks), n // 1024 or 1))
+        for c in range(chunks):
+            t0 = time.perf_counter()
+            blk = ingest.assemble_als_updates(users, items, u, i, xrows, yrows, vxh, vyh,
+                                              not self.no_known_items, lo=n * c // chunks,
+                                              hi=n * (c + 1) // chunks)
+            ph["assemble"] += (time.perf_counter() - t0) * 1e3
+            yield blk
 
     def _to_update_json(self, matrix: str, id_: str, vec_json: str, other: str) -> str:
         if self.no_known_items:

@@ -153,8 +153,9 @@ class ALSTrainer:
         self.events: Optional[list] = None
         # row ranges per half-step whose factor exchange overlaps the next range's solve
         self._explicit_chunks = bool(gather_chunks)
+        # (a forced world of one has nothing to exchange: ranges there only add launch tails)
         self.gather_chunks = int(gather_chunks) if gather_chunks else (
-            4 if self.ctx.is_distributed else 1)
+            4 if self.ctx.world_size > 1 else 1)
 
     # ------------------------------------------------------------------ data
     def prepare(self, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tensor,

@@ -160,12 +160,15 @@ def test_device_aggregation_matches_host():
     s[g.random(n) < 0.1] = np.nan
     # many time ties (arrival order decides): one composite-key sort; a time range too wide
     # to pack next to the (user, item) key: the two-sort path
+    from oryx_amd.models.als.batch import aggregate_scores_reference
     for ts in (g.integers(0, 1000, n), g.integers(0, 1 << 60, n) // 977 * 977):
         for implicit in (True, False):
-            a = aggregate_scores(u, i, s, ts, implicit)
-            b = aggregate_scores_device(u, i, s, ts, implicit, "cpu")
-            for x, y in zip(a, b):
-                assert np.array_equal(x, y) or np.allclose(x, y, rtol=1e-12, equal_nan=True)
+            ref = aggregate_scores_reference(u, i, s, ts, implicit)
+            for got in (aggregate_scores(u, i, s, ts, implicit),            # native
+                        aggregate_scores_device(u, i, s, ts, implicit, "cpu")):
+                for x, y in zip(ref, got):
+                    assert np.array_equal(x, y) or np.allclose(x, y, rtol=1e-12,
+                                                               equal_nan=True)
 
 
 @pytest.mark.gpu
