@@ -248,10 +248,10 @@ def main(argv=None) -> int:
             "speed_layer_foldin_ms": foldin_ms,
             "speed_layer_phase_ms": speed_phases,
             "speed_layer_path": "ALSSpeedModelManager.build_update_blocks (parse, aggregate, "
-                                "inverses, fused HIP fold-in, UP formatting, assembly in 4 "
-                                "blocks) + each block's append to the update log on a "
-                                "writer thread (layers/speed.py publish_blocks); end to end, "
-                                "median of 12",
+                                "inverses overlapped with the parse, fused HIP fold-in, UP "
+                                "formatting, assembly) + the UP block's append to the update "
+                                "log (layers/speed.py publish_blocks); end to end, median of "
+                                "12",
             "solve_failures": trainer.failures,
             "gather_chunks": {"items": trainer.lay_i.C, "users": trainer.lay_u.C},
         }

@@ -3,92 +3,103 @@
 // Replaces the reference's per-request thread-pool scan of LSH partitions with bounded heaps
 // ([serving-app]/als/model/ALSServingModel.java:289-335, TopNConsumer.java:55-74,
 // LocalitySensitiveHash.java:156-177).  One launch scores up to 16 queries against the item
-// matrix and leaves each (wave, query) pair's 64 best candidates; a small device top-k merges
+// matrix and leaves each (wave, query) pair's KL best candidates; a small device top-k merges
 // them.  MI355X design:
-//   * Y is fp32 [n][kp] (kp a multiple of 16), rows sorted by LSH bucket, so a query's
-//     candidate buckets are contiguous row ranges: only the union of the batch's candidate
-//     ranges is read (sample-rate 0.3 reads ~30% of Y for one query);
+//   * the item matrix is read IN PLACE from the feature store's device mirror (fp32 rows of
+//     stride ld, a multiple of 16, zero padded): the index only holds a bucket-sorted
+//     permutation (position -> store row), so a query's candidate buckets are contiguous
+//     position ranges and only the union of the batch's candidate ranges is read, and there is
+//     one device copy of Y (a 20M x 250 model fits in ~21 GiB);
 //   * scores on v_mfma_f32_16x16x4_f32: A = 16 item rows (one 16-byte load per lane per 16
 //     features, four MFMAs per load), B = the 16 queries held in registers for the whole
 //     kernel, C = 16 items x 16 queries (lane: 4 items of query lane & 15);
-//   * epilogue: cosine scale (1/|y|), per-query candidate-bucket bit, then a per-(wave,
-//     query) threshold test -- only scores above the query's current 64th best enter an LDS
-//     buffer (128 slots); known / excluded items are binary-searched only for those; a full
-//     buffer is cut back to its best 64 by a wave bitonic sort, raising the threshold, so after
-//     the first few tiles almost nothing is appended;
-//   * waves take equal contiguous shares of the union's 16-row tiles (grid sized to the tile
-//     count), so the scan is one streaming pass over HBM.
+//   * software pipelined: the next tile's rows are loaded before this tile's epilogue runs;
+//   * cosine: each row's norm is summed from the A operand already in registers (no norm
+//     array), then moved to the C layout with four lane shuffles;
+//   * epilogue: per-query candidate-bucket bit, then a per-(wave, query) threshold test --
+//     only scores above the query's current KL-th best enter an LDS buffer (2 KL slots);
+//     excluded items are binary-searched only for those; a full buffer is cut back to its
+//     best KL by a wave bitonic sort, raising the threshold;
+//   * KL = 64 (the common howMany + offset), 256 or 1024 candidates per (wave, query): deep
+//     requests run in the same single pass (LDS is sized for the launch's queries only);
+//   * waves take equal contiguous shares of the union's 16-row tiles, so the scan is one
+//     streaming pass over HBM.
 
 #include "common.h"
 
 namespace {
 
 constexpr int QB = 16;     // queries per launch (MFMA N)
-constexpr int KL = 64;     // candidates kept per (wave, query)
-constexpr int CAP = 128;   // LDS slots per (wave, query)
-constexpr int WPB = 2;     // waves per block (2 x 32 KB of candidate buffers)
+constexpr int WPB = 2;     // waves per block
 
 struct TopnParams {
-  const float* Y;             // [n][kp] bucket-sorted
-  const float* inv_norm;      // [n] (cosine) or null
+  const float* Y;             // store rows, stride ld floats (ld >= kp, pad columns zero)
+  const int* perm;            // [n] position -> store row (null: identity)
+  long long ld;
   const float* Q;             // [QB][kp] (rows >= nq zero)
-  int kp;
   int nq;
-  const int* bucket_of;       // [n] bucket id per row (null: no LSH mask)
+  int cosine;
+  const int* bucket_of;       // [n] bucket id per position (null: no LSH mask)
   const unsigned* cand_bits;  // [nq][words] candidate-bucket bitmap
   int words;
-  const long long* ranges;    // [n_ranges][2] rows to scan, ascending, disjoint
+  const long long* ranges;    // [n_ranges][2] positions to scan, ascending, disjoint
   const long long* tile0;     // [n_ranges + 1] prefix count of 16-row tiles
   int n_ranges;
   long long n_tiles;
   const int* excl_ptr;        // [nq + 1] (null: none)
-  const int* excl_rows;       // sorted row positions per query
-  float* out_score;           // [n_waves][QB][KL]
-  int* out_row;               // [n_waves][QB][KL]
+  const int* excl_rows;       // sorted excluded positions per query
+  float* out_score;           // [n_waves][nq][KL]
+  int* out_row;               // [n_waves][nq][KL] positions
 };
 
-__device__ __forceinline__ bool excluded(const TopnParams& p, int q, int row) {
+__device__ __forceinline__ bool excluded(const TopnParams& p, int q, int pos) {
   if (!p.excl_ptr) return false;
   int lo = p.excl_ptr[q], hi = p.excl_ptr[q + 1];
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     const int v = p.excl_rows[mid];
-    if (v == row) return true;
-    if (v < row) lo = mid + 1;
+    if (v == pos) return true;
+    if (v < pos) lo = mid + 1;
     else hi = mid;
   }
   return false;
 }
 
-// descending bitonic sort of CAP (score, row) pairs in LDS by one wave (2 pairs per lane per
-// step); -inf pads
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// descending bitonic sort of CAP (score, row) pairs in LDS by one wave; -inf pads
+template <int CAP>
 __device__ __forceinline__ void wave_sort_desc(float* sc, int* rw, int lane) {
-#pragma unroll
   for (int k = 2; k <= CAP; k <<= 1) {
-#pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      // pair p = lane: i = 2j(p / j) + p % j, partner i + j
-      const int i = 2 * j * (lane / j) + (lane % j);
-      const int l = i + j;
-      const float a = sc[i], b = sc[l];
-      const int ra = rw[i], rb = rw[l];
-      const bool desc = (i & k) == 0;
-      // descending blocks keep the larger first
-      const bool swap = desc ? (a < b) : (a > b);
-      if (swap) {
-        sc[i] = b;
-        sc[l] = a;
-        rw[i] = rb;
-        rw[l] = ra;
+#pragma unroll
+      for (int p = lane; p < CAP / 2; p += 64) {
+        // pair p: i = 2j (p / j) + p % j, partner i + j
+        const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+        const int l = i + j;
+        const float a = sc[i], b = sc[l];
+        const int ra = rw[i], rb = rw[l];
+        const bool desc = (i & k) == 0;
+        const bool swap = desc ? (a < b) : (a > b);
+        if (swap) {
+          sc[i] = b;
+          sc[l] = a;
+          rw[i] = rb;
+          rw[l] = ra;
+        }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
     }
   }
 }
 
 // Cut query q's buffer back to its best KL entries; returns the new threshold (the KL-th).
+template <int KL>
 __device__ __forceinline__ float compact(float* sc, int* rw, int* cnt, int q, int lane) {
+  constexpr int CAP = 2 * KL;
   float* s = sc + q * CAP;
   int* r = rw + q * CAP;
   const int c = cnt[q];
@@ -97,25 +108,25 @@ __device__ __forceinline__ float compact(float* sc, int* rw, int* cnt, int q, in
       s[i] = -INFINITY;
       r[i] = -1;
     }
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  wave_sort_desc(s, r, lane);
+  wave_sync();
+  wave_sort_desc<CAP>(s, r, lane);
   if (lane == 0) cnt[q] = c < KL ? c : KL;
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();
   return c >= KL ? s[KL - 1] : -INFINITY;
 }
 
-template <int KP>
+template <int KP, int KL>
 __global__ __launch_bounds__(WPB * 64) void topn_scan(TopnParams p) {
   constexpr int S = KP / 16;
-  __shared__ float s_sc[WPB][QB * CAP];
-  __shared__ int s_rw[WPB][QB * CAP];
-  __shared__ int s_cnt[WPB][QB];
+  constexpr int CAP = 2 * KL;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float* sc = s_sc[wave];
-  int* rw = s_rw[wave];
-  int* cnt = s_cnt[wave];
+  const int nq = p.nq;
+  // per wave: scores [nq][CAP], rows [nq][CAP], counts [QB]
+  unsigned char* base = smem + (size_t)wave * ((size_t)nq * CAP * 8 + QB * 4);
+  float* sc = reinterpret_cast<float*>(base);
+  int* rw = reinterpret_cast<int*>(base + (size_t)nq * CAP * 4);
+  int* cnt = reinterpret_cast<int*>(base + (size_t)nq * CAP * 8);
   if (lane < QB) cnt[lane] = 0;
   const int q = lane & 15, kg = lane >> 4;
   // B operand (queries) for every 16-feature step, resident: component j of step s is
@@ -125,10 +136,9 @@ __global__ __launch_bounds__(WPB * 64) void topn_scan(TopnParams p) {
   for (int s = 0; s < S; ++s)
     qb[s] = *reinterpret_cast<const f32x4*>(p.Q + q * KP + 16 * s + 4 * kg);
   float theta = -INFINITY;   // this lane's query's admission threshold
-  const unsigned* cbits = p.cand_bits ? p.cand_bits + (long long)(q < p.nq ? q : 0) * p.words
+  const unsigned* cbits = p.cand_bits ? p.cand_bits + (long long)(q < nq ? q : 0) * p.words
                                       : nullptr;
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
+  wave_sync();
 
   const long long nw = (long long)gridDim.x * WPB;
   const long long w = (long long)blockIdx.x * WPB + wave;
@@ -144,31 +154,55 @@ __global__ __launch_bounds__(WPB * 64) void topn_scan(TopnParams p) {
     }
     r = lo;
   }
-  for (long long t = t_beg; t < t_end; ++t) {
+  // A: item position i0 + (lane & 15), features 16 s + 4 kg .. + 3
+  f32x4 a[S];
+  long long i0 = 0, rend = 0;
+  auto load_tile = [&](long long t) {
     while (t >= p.tile0[r + 1]) ++r;
-    const long long rbeg = p.ranges[2 * r], rend = p.ranges[2 * r + 1];
-    const long long i0 = rbeg + 16 * (t - p.tile0[r]);
-    // A: item row i0 + (lane & 15), features 16 s + 4 kg .. + 3
+    const long long rbeg = p.ranges[2 * r];
+    rend = p.ranges[2 * r + 1];
+    i0 = rbeg + 16 * (t - p.tile0[r]);
     const long long ia = i0 + (lane & 15) < rend ? i0 + (lane & 15) : rend - 1;
-    const float* yrow = p.Y + ia * KP + 4 * kg;
+    const long long row = p.perm ? (long long)p.perm[ia] : ia;
+    const float* yrow = p.Y + row * p.ld + 4 * kg;
+#pragma unroll
+    for (int s = 0; s < S; ++s) a[s] = *reinterpret_cast<const f32x4*>(yrow + 16 * s);
+  };
+  if (t_beg < t_end) load_tile(t_beg);
+  for (long long t = t_beg; t < t_end; ++t) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    float ss = 0.f;
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(yrow + 16 * s);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], qb[s][j], acc, 0, 0, 0);
+      for (int j = 0; j < 4; ++j) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][j], qb[s][j], acc, 0, 0, 0);
+        ss += a[s][j] * a[s][j];
+      }
     }
-    // C: lane holds items i0 + 4 kg + v of query q
+    const long long c_i0 = i0, c_rend = rend;
+    // the next tile's rows are in flight while this tile's epilogue runs
+    if (t + 1 < t_end) load_tile(t + 1);
+    float inv4[4] = {1.f, 1.f, 1.f, 1.f};
+    if (p.cosine) {
+      // row (lane & 15)'s squared norm: sum over the four feature groups (lanes +16, +32, +48)
+      ss += __shfl_xor(ss, 16);
+      ss += __shfl_xor(ss, 32);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float n2 = __shfl(ss, 4 * kg + v);
+        inv4[v] = n2 > 0.f ? 1.f / sqrtf(n2) : 0.f;
+      }
+    }
+    // C: lane holds items c_i0 + 4 kg + v of query q
     bool any = false;
     float v4[4];
     int r4[4];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const long long it = i0 + 4 * kg + v;
-      float sv = acc[v];
-      bool ok = it < rend && q < p.nq;
-      if (ok && p.inv_norm) sv *= p.inv_norm[it];
+      const long long it = c_i0 + 4 * kg + v;
+      const float sv = acc[v] * inv4[v];
+      bool ok = it < c_rend && q < nq;
       if (ok && cbits) {
         const int b = p.bucket_of[it];
         ok = (cbits[b >> 5] >> (b & 31)) & 1u;
@@ -188,76 +222,102 @@ __global__ __launch_bounds__(WPB * 64) void topn_scan(TopnParams p) {
           rw[q * CAP + pos] = r4[v];
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // queries whose buffer cannot take another tile (16 entries) are cut back to KL
-      const int my = lane < QB ? cnt[lane] : 0;
-      unsigned long long full = __ballot(lane < QB && my > CAP - 16);
+      const int my = lane < nq ? cnt[lane] : 0;
+      unsigned long long full = __ballot(lane < nq && my > CAP - 16);
       while (full) {
         const int fq = __builtin_ctzll(full);
         full &= full - 1;
-        const float th = compact(sc, rw, cnt, fq, lane);
+        const float th = compact<KL>(sc, rw, cnt, fq, lane);
         if (q == fq) theta = th;
       }
     }
   }
   // final: every query's best KL (sorted) to global
-  const long long ob = w * QB * KL;
-  for (int fq = 0; fq < QB; ++fq) {
-    compact(sc, rw, cnt, fq, lane);
-    p.out_score[ob + fq * KL + lane] = sc[fq * CAP + lane];
-    p.out_row[ob + fq * KL + lane] = rw[fq * CAP + lane];
+  const long long ob = w * nq * KL;
+  for (int fq = 0; fq < nq; ++fq) {
+    compact<KL>(sc, rw, cnt, fq, lane);
+    for (int i = lane; i < KL; i += 64) {
+      p.out_score[ob + fq * KL + i] = sc[fq * CAP + i];
+      p.out_row[ob + fq * KL + i] = rw[fq * CAP + i];
+    }
   }
 }
+
+constexpr size_t kLdsBudget = 160u * 1024u;
+
+size_t lds_bytes(int kl, int nq) { return (size_t)WPB * ((size_t)nq * 2 * kl * 8 + QB * 4); }
 
 }  // namespace
 
 extern "C" {
 
-// Number of waves the scan uses for n_tiles 16-row tiles (the caller sizes out_* to
-// waves * 16 * 64).
-long long oryx_topn_waves(long long n_tiles) {
-  // ~8 tiles per wave at least, at most 8 waves per SIMD of 256 CUs
+// Most queries one launch can hold for a per-(wave, query) list of `kl` candidates (LDS).
+int oryx_topn_max_queries(int kl) {
+  int nq = QB;
+  while (nq > 1 && lds_bytes(kl, nq) > kLdsBudget) --nq;
+  return lds_bytes(kl, nq) <= kLdsBudget ? nq : 0;
+}
+
+// Number of waves the scan uses for n_tiles 16-row tiles with `kl` candidates per (wave,
+// query) (the caller sizes out_* to waves * nq * kl).
+long long oryx_topn_waves_kl(long long n_tiles, int kl) {
+  // ~8 tiles per wave at least; at most 8 waves per SIMD of 256 CUs for kl = 64, fewer for
+  // the deep lists (their candidate output and final sorts grow with kl)
   long long w = (n_tiles + 7) / 8;
-  const long long cap = 256 * 4 * 8;
+  const long long cap = 256 * 4 * 8 / (kl / 64 > 0 ? kl / 64 : 1);
   if (w > cap) w = cap;
   if (w < 1) w = 1;
   return (w + WPB - 1) / WPB * WPB;
 }
 
-int oryx_topn_scan(const float* Y, const float* inv_norm, const float* Q, int kp, int nq,
-                   const int* bucket_of, const unsigned* cand_bits, int words,
-                   const long long* ranges, const long long* tile0, int n_ranges,
-                   long long n_tiles, const int* excl_ptr, const int* excl_rows,
-                   float* out_score, int* out_row, void* stream) {
+long long oryx_topn_waves(long long n_tiles) { return oryx_topn_waves_kl(n_tiles, 64); }
+
+int oryx_topn_scan2(const float* Y, const int* perm, long long ld, const float* Q, int kp,
+                    int nq, int cosine, int kl, const int* bucket_of,
+                    const unsigned* cand_bits, int words, const long long* ranges,
+                    const long long* tile0, int n_ranges, long long n_tiles,
+                    const int* excl_ptr, const int* excl_rows, float* out_score, int* out_row,
+                    void* stream) {
   if (nq <= 0 || nq > QB || n_ranges <= 0 || n_tiles <= 0) return ORYX_EINVAL;
   if (cand_bits && !bucket_of) return ORYX_EINVAL;
-  TopnParams p{Y, inv_norm, Q, kp, nq, bucket_of, cand_bits, words, ranges, tile0, n_ranges,
-               n_tiles, excl_ptr, excl_rows, out_score, out_row};
-  const long long waves = oryx_topn_waves(n_tiles);
+  if (ld < kp || ld % 4 != 0) return ORYX_EINVAL;
+  if (nq > oryx_topn_max_queries(kl)) return ORYX_EINVAL;
+  TopnParams p{Y, perm, ld, Q, nq, cosine, bucket_of, cand_bits, words, ranges, tile0,
+               n_ranges, n_tiles, excl_ptr, excl_rows, out_score, out_row};
+  const long long waves = oryx_topn_waves_kl(n_tiles, kl);
   const unsigned blocks = (unsigned)(waves / WPB);
+  const size_t lds = lds_bytes(kl, nq);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  switch (kp) {
-#define TOPN_CASE(KPV)                                                                \
-  case KPV:                                                                           \
-    hipLaunchKernelGGL(topn_scan<KPV>, dim3(blocks), dim3(WPB * 64), 0, s, p);        \
-    break;
-    TOPN_CASE(16)
-    TOPN_CASE(32)
-    TOPN_CASE(48)
-    TOPN_CASE(64)
-    TOPN_CASE(80)
-    TOPN_CASE(96)
-    TOPN_CASE(112)
-    TOPN_CASE(128)
-    TOPN_CASE(160)
-    TOPN_CASE(192)
-    TOPN_CASE(256)
-#undef TOPN_CASE
-    default:
-      return ORYX_EINVAL;
+#define TOPN_CASE(KPV, KLV)                                                              \
+  if (kp == KPV && kl == KLV) {                                                          \
+    static bool attr_set = false;                                                        \
+    if (!attr_set && lds > 65536) {                                                      \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topn_scan<KPV, KLV>),       \
+                              hipFuncAttributeMaxDynamicSharedMemorySize,                \
+                              (int)kLdsBudget) != hipSuccess)                            \
+        return ORYX_ELAUNCH;                                                             \
+      attr_set = true;                                                                   \
+    }                                                                                    \
+    hipLaunchKernelGGL((topn_scan<KPV, KLV>), dim3(blocks), dim3(WPB * 64), lds, s, p);  \
+    return oryx_check_launch();                                                          \
   }
-  return oryx_check_launch();
+#define TOPN_KP(KPV) TOPN_CASE(KPV, 64) TOPN_CASE(KPV, 256) TOPN_CASE(KPV, 1024)
+  TOPN_KP(16)
+  TOPN_KP(32)
+  TOPN_KP(48)
+  TOPN_KP(64)
+  TOPN_KP(80)
+  TOPN_KP(96)
+  TOPN_KP(112)
+  TOPN_KP(128)
+  TOPN_KP(160)
+  TOPN_KP(192)
+  TOPN_KP(256)
+#undef TOPN_KP
+#undef TOPN_CASE
+  return ORYX_EINVAL;
 }
 
 }  // extern "C"

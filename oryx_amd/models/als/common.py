@@ -58,9 +58,13 @@ class FeatureVectors:
     """Thread-safe ``id -> float32[k]`` store; optional device mirror for GPU scans."""
 
     def __init__(self, features: int, device: Optional[torch.device] = None,
-                 initial_capacity: int = 1024, partitioner: Optional[Callable] = None):
+                 initial_capacity: int = 1024, partitioner: Optional[Callable] = None,
+                 row_pad: int = 1):
         self.k = int(features)
         self.device = device
+        # device rows are ``ld`` floats apart (k rounded up to ``row_pad``, pad columns zero):
+        # the serving scan kernel reads the mirror in place in whole 16-float steps
+        self.ld = -(-self.k // max(1, int(row_pad))) * max(1, int(row_pad))
         self._lock = lang.AutoReadWriteLock()
         self._index: Dict[str, int] = {}
         self._ids: List[Optional[str]] = []
@@ -339,7 +343,27 @@ class FeatureVectors:
 
     # ---------------------------------------------------------------- device mirror
     def device_view(self):
-        """(matrix fp32 [n, k], valid bool [n], norms fp32 [n]) on the device, refreshed."""
+        """(matrix fp32 [n, k], valid bool [n], norms fp32 [n]) on the device, refreshed (the
+        matrix is a view of rows ``ld`` floats apart)."""
+        mat, valid, norm = self._device_refresh()
+        return mat[:, :self.k], valid, norm
+
+    def device_rows(self):
+        """(padded device matrix fp32 [n, ld], ld), refreshed: what the serving scan reads."""
+        mat, _, _ = self._device_refresh()
+        return mat, self.ld
+
+    def _upload_full(self, cap: int) -> torch.Tensor:
+        if self.ld == self.k:
+            return torch.from_numpy(self._host[:cap]).to(self.device, copy=True)
+        dev = torch.zeros((cap, self.ld), dtype=torch.float32, device=self.device)
+        step = 1 << 20       # bounded staging for the strided copy
+        for lo in range(0, cap, step):
+            hi = min(cap, lo + step)
+            dev[lo:hi, :self.k] = torch.from_numpy(self._host[lo:hi]).to(self.device)
+        return dev
+
+    def _device_refresh(self):
         if self.device is None:
             raise RuntimeError("no device mirror")
         with self._dev_lock:
@@ -352,7 +376,8 @@ class FeatureVectors:
                     # power-of-two capacity (a 20M-row store would otherwise hold 33.5M rows
                     # of HBM); the read lock keeps writers out during the synchronous copies
                     cap = min(self._host.shape[0], max(1024, n + n // 8))
-                    self._dev = torch.from_numpy(self._host[:cap]).to(self.device, copy=True)
+                    self._dev = None            # free the old mirror before the new one
+                    self._dev = self._upload_full(cap)
                     self._dev_valid = torch.from_numpy(self._host_valid[:cap]).to(self.device,
                                                                                   copy=True)
                     self._dev_norm = self._dev.norm(dim=1)
@@ -362,6 +387,8 @@ class FeatureVectors:
                 elif self._dirty:
                     rows = np.fromiter(self._dirty, dtype=np.int64, count=len(self._dirty))
                     vals = torch.from_numpy(self._host[rows]).to(self.device, non_blocking=False)
+                    if self.ld != self.k:
+                        vals = torch.nn.functional.pad(vals, (0, self.ld - self.k))
                     valid = torch.from_numpy(self._host_valid[rows]).to(self.device)
                     self._dirty.clear()
                     dirty_rows = torch.from_numpy(rows).to(self.device)
@@ -372,15 +399,21 @@ class FeatureVectors:
                     dirty_rows = torch.empty(0, dtype=torch.int64, device=self.device)
                 if self.partitioner is not None:
                     if need_full or self._dev_part is None:
-                        self._dev_part = self.partitioner(self._dev)
+                        self._dev_part = self.partitioner(self._dev[:, :self.k])
                     elif dirty_rows is not None and dirty_rows.numel():
-                        self._dev_part[dirty_rows] = self.partitioner(self._dev[dirty_rows])
+                        self._dev_part[dirty_rows] = self.partitioner(
+                            self._dev[dirty_rows][:, :self.k])
             return self._dev[:n], self._dev_valid[:n], self._dev_norm[:n]
 
     def device_partitions(self) -> Optional[torch.Tensor]:
         if self._dev_part is None:
             return None
         return self._dev_part[:self._n_rows]
+
+    def ids_of_rows(self, rows) -> List[Optional[str]]:
+        ids = self._ids
+        n = len(ids)
+        return [ids[r] if r < n else None for r in rows]
 
     def host_rows(self, ids: Iterable[str]) -> List[int]:
         idx = self._index

@@ -35,12 +35,36 @@ from ...utils.lang import AutoReadWriteLock
 from .common import FeatureVectors
 from .rescorer import Rescorer, RescorerProvider, load_rescorer_providers
 
-__all__ = ["ALSServingModel", "ALSServingModelManager", "LocalitySensitiveHash",
-           "RESCORE_FULL_POOL"]
+__all__ = ["ALSServingModel", "ALSServingModelManager", "LocalitySensitiveHash"]
 
 log = logging.getLogger(__name__)
 
-RESCORE_FULL_POOL = 1 << 17
+
+def rescored_top(ids, scores: np.ndarray, rescorer: Rescorer, how_many: int
+                 ) -> List[Tuple[str, float]]:
+    """``TopNConsumer`` semantics over EVERY candidate: drop filtered IDs, rescore the rest,
+    keep rescored values above -inf (NaN drops an item), best ``how_many`` descending."""
+    keep = np.array([i is not None for i in ids], dtype=bool)
+    if not keep.all():
+        ids = [i for i in ids if i is not None]
+        scores = scores[keep]
+    if not ids:
+        return []
+    allowed = ~np.asarray(rescorer.is_filtered_many(ids), dtype=bool)
+    idx = np.flatnonzero(allowed)
+    if len(idx) == 0:
+        return []
+    sel = [ids[j] for j in idx.tolist()]
+    new = np.asarray(rescorer.rescore_many(sel, np.asarray(scores, dtype=np.float64)[idx]),
+                     dtype=np.float64)
+    ok = np.flatnonzero(new > -np.inf)
+    if len(ok) == 0:
+        return []
+    if len(ok) > how_many:
+        part = np.argpartition(-new[ok], how_many - 1)[:how_many]
+        ok = ok[part]
+    ok = ok[np.argsort(-new[ok], kind="stable")]
+    return [(sel[j], float(new[j])) for j in ok.tolist()]
 
 
 class TopNBatcher:
@@ -244,8 +268,11 @@ class ALSServingModel(ServingModel):
         self.implicit = implicit
         self.rescorer_provider = rescorer_provider
         self.X = FeatureVectors(features, None)
+        # device rows padded to the scan kernel's stride: the top-N index reads them in place
+        # (one device copy of Y)
         self.Y = FeatureVectors(features, device,
-                                partitioner=self.lsh.device_partitioner(device))
+                                partitioner=self.lsh.device_partitioner(device),
+                                row_pad=topn_ops.row_pad_for(features))
         self._known: Dict[str, Set[str]] = {}
         self._known_lock = AutoReadWriteLock()
         self._expected_users: Set[str] = set()
@@ -371,23 +398,32 @@ class ALSServingModel(ServingModel):
               rescorer: Optional[Rescorer] = None) -> List[Tuple[str, float]]:
         """Best ``how_many`` items by ``dot(y, target)`` (or ``/|y|`` when ``cosine``).
 
-        ``exclude``: item IDs never returned.  ``rescorer``: filter + rescore on the host over
-        a candidate pool of the best raw scores (all items when the catalogue is small).
+        ``exclude``: item IDs never returned.  ``rescorer``: filter + rescore applied to every
+        candidate item (exact ``TopNConsumer`` semantics).  Any depth is exact: the fused
+        kernel handles deep requests in one or more passes.
         """
         if how_many <= 0 or self.Y.size() == 0:
             return []
         lsh_on = self.lsh.get_max_bits_differing() < self.lsh.get_num_hashes()
-        if self.batcher is not None and rescorer is None and how_many <= topn_ops.MAX_HOW_MANY:
-            cands = self.lsh.get_candidate_indices(target) if lsh_on else None
+        cands = self.lsh.get_candidate_indices(target) if lsh_on else None
+        if self.index is not None:
             ex = self.Y.host_rows(exclude) if exclude else None
-            rows, scores = self.batcher.submit(topn_ops.TopNQuery(
-                np.asarray(target, dtype=np.float32), how_many, cosine, cands, ex))
+            tgt = np.asarray(target, dtype=np.float32)
+            if rescorer is not None:
+                rows, scores = self.index.all_scores(tgt, cosine, cands, ex)
+                return rescored_top(self.Y.ids_of_rows(rows.tolist()), scores, rescorer,
+                                    how_many)
+            q = topn_ops.TopNQuery(tgt, how_many, cosine, cands, ex)
+            if self.batcher is not None and how_many <= topn_ops.MAX_HOW_MANY:
+                rows, scores = self.batcher.submit(q)
+            else:
+                rows, scores = self.index.scan([q])[0]
             out = []
-            for r, v in zip(rows.tolist(), scores.tolist()):
-                id_ = self.Y.id_of_row(r)
+            for id_, v in zip(self.Y.ids_of_rows(rows.tolist()), scores.tolist()):
                 if id_ is not None:
                     out.append((id_, float(v)))
             return out
+        # no kernel (CPU device): torch over the store's device mirror
         mat, valid, norms = self.Y.device_view()
         n = mat.shape[0]
         if n == 0:
@@ -399,44 +435,31 @@ class ALSServingModel(ServingModel):
         neg_inf = torch.tensor(float("-inf"), device=mat.device)
         scores = torch.where(valid, scores, neg_inf)
         parts = self.Y.device_partitions()
-        if parts is not None and lsh_on:
+        if parts is not None and cands is not None:
             cand = torch.zeros(self.lsh.get_num_partitions(), dtype=torch.bool,
                                device=mat.device)
-            cand[torch.from_numpy(self.lsh.get_candidate_indices(target)).to(mat.device)] = True
+            cand[torch.from_numpy(np.asarray(cands)).to(mat.device)] = True
             scores = torch.where(cand[parts], scores, neg_inf)
         if exclude:
             rows = self.Y.host_rows(exclude)
             if rows:
                 scores[torch.as_tensor(rows, device=mat.device)] = float("-inf")
-        n_valid = self.Y.size()
-        if rescorer is None:
-            m = min(how_many, n)
-            vals, idx = torch.topk(scores, m)
-            vals, idx = vals.cpu().numpy(), idx.cpu().numpy()
-            out = []
-            for v, i in zip(vals, idx):
-                if v == float("-inf"):
-                    break
-                id_ = self.Y.id_of_row(int(i))
-                if id_ is not None:
-                    out.append((id_, float(v)))
-            return out
-        pool = n if n_valid <= RESCORE_FULL_POOL else min(n, max(how_many * 16, 4096))
-        vals, idx = torch.topk(scores, pool)
+        if rescorer is not None:
+            live = torch.nonzero(scores > float("-inf")).flatten()
+            rows = live.cpu().numpy()
+            return rescored_top(self.Y.ids_of_rows(rows.tolist()),
+                                scores[live].cpu().numpy(), rescorer, how_many)
+        m = min(how_many, n)
+        vals, idx = torch.topk(scores, m)
         vals, idx = vals.cpu().numpy(), idx.cpu().numpy()
-        heap: List[Tuple[float, str]] = []
+        out = []
         for v, i in zip(vals, idx):
             if v == float("-inf"):
                 break
             id_ = self.Y.id_of_row(int(i))
-            if id_ is None or rescorer.is_filtered(id_):
-                continue
-            s = rescorer.rescore(id_, float(v))
-            if not (s > float("-inf")) or math.isnan(s):
-                continue
-            heap.append((s, id_))
-        heap.sort(key=lambda t: -t[0])
-        return [(i, s) for s, i in heap[:how_many]]
+            if id_ is not None:
+                out.append((id_, float(v)))
+        return out
 
     def get_yty_solver(self):
         ver = self.Y.version

@@ -128,7 +128,11 @@ class ALSSpeedModel(SpeedModel):
         if getattr(self, "_inv_key", None) == key:
             return self._inv
         if self.device is not None and self.device.type == "cuda":
-            inv = self._device_inverses()
+            pending = getattr(self, "_inv_pending", None)
+            self._inv_pending = None
+            if pending is None or pending[0] != key:
+                pending = (key,) + self._device_inverses_start()
+            inv = self._device_inverses_finish(*pending[1:])
             if inv is not None:
                 self._inv_key, self._inv = key, inv
                 return inv
@@ -142,9 +146,22 @@ class ALSSpeedModel(SpeedModel):
         self._inv_key, self._inv = key, inv
         return inv
 
-    def _device_inverses(self):
+    def prefetch_inverses(self, stream=None) -> None:
+        """Queue the device Gramians + Cholesky inverses for the current factors (on
+        ``stream``) without waiting: a speed-layer interval starts them before parsing its
+        input on the host, and :meth:`solver_inverses` then only collects them."""
+        if self.device is None or self.device.type != "cuda":
+            return
+        key = (self.X.version, self.Y.version)
+        if getattr(self, "_inv_key", None) == key:
+            return
+        ctx = torch.cuda.stream(stream) if stream is not None else _null_ctx()
+        with ctx:
+            self._inv_pending = (key,) + self._device_inverses_start()
+
+    def _device_inverses_start(self):
         if self.X.size() == 0 or self.Y.size() == 0:
-            return None
+            return None, None
         invs, oks = [], []
         for store in (self.X, self.Y):
             mat, _, _ = store.device_view()
@@ -154,7 +171,16 @@ class ALSSpeedModel(SpeedModel):
             thr = a.abs().sum(1).max() * mathx.SINGULARITY_THRESHOLD_RATIO
             oks.append((info == 0) & torch.isfinite(inv).all() & (inv.norm() * thr < 1.0))
             invs.append(inv)
-        if not bool(torch.stack(oks).all().item()):
+        ev = torch.cuda.Event()
+        ev.record()
+        return (invs, torch.stack(oks).all()), ev
+
+    def _device_inverses_finish(self, work, ev):
+        if work is None:
+            return None
+        torch.cuda.current_stream().wait_event(ev)
+        invs, ok = work
+        if not bool(ok.item()):
             return None
         return invs[0], invs[1]
 
@@ -250,16 +276,21 @@ class ALSSpeedModelManager(SpeedModelManager):
             return []
         return blocks[0] if len(blocks) == 1 else [m for b in blocks for m in b]
 
-    def build_update_blocks(self, new_data: Dataset, chunks: int = 4):
+    def build_update_blocks(self, new_data: Dataset, chunks: int = 1):
         """The interval's UP messages as a generator of blocks over consecutive event ranges
         (the same messages in the same order as :meth:`build_updates`): a publisher appends
         block j on another thread while block j + 1 is assembled
-        (:func:`oryx_amd.layers.speed.publish_blocks`)."""
+        (:func:`oryx_amd.layers.speed.publish_blocks`).  One block by default: on the GPU
+        box, 4 blocks ran slower (8.3 -> 9.4 ms per 10k events) -- the threaded assembler and
+        the log append's CRC threads compete for the same cores, and the append itself is
+        bound by the kernel's page-cache copy (profiles/r3_speed_profile_*.txt)."""
         model = self.model
         if model is None or model.get_fraction_loaded() < self.min_model_load_fraction:
             return
         import time
         t0 = time.perf_counter()
+        # the Gramian inverses run on the GPU while the host parses the interval
+        model.prefetch_inverses(self._device_stream(model.device))
         # per-batch dictionaries, reused (cleared) so their tables are not reallocated and
         # re-faulted every micro-batch
         if self._dicts is None:

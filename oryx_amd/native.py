@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 12
+KERNELS_ABI_VERSION = 13
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -203,8 +203,13 @@ def _load_kernels():
     _sig(lib, "oryx_topn_waves", c_ll, [c_ll])
     # Y, inv_norm, Q, kp, nq, bucket_of, cand_bits, words, ranges, tile0, n_ranges, n_tiles,
     # excl_ptr, excl_rows, out_score, out_row, stream
-    _sig(lib, "oryx_topn_scan", c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_vp, c_vp, c_i, c_vp, c_vp,
-                                      c_i, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp])
+    # Y, perm, ld, Q, kp, nq, cosine, kl, bucket_of, cand_bits, words, ranges, tile0,
+    # n_ranges, n_tiles, excl_ptr, excl_rows, out_score, out_row, stream
+    _sig(lib, "oryx_topn_scan2", c_i, [c_vp, c_vp, c_ll, c_vp, c_i, c_i, c_i, c_i, c_vp, c_vp,
+                                       c_i, c_vp, c_vp, c_i, c_ll, c_vp, c_vp, c_vp, c_vp,
+                                       c_vp])
+    _sig(lib, "oryx_topn_waves_kl", c_ll, [c_ll, c_i])
+    _sig(lib, "oryx_topn_max_queries", c_i, [c_i])
     _sig(lib, "oryx_counting_sort", c_i, [c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])
     # ..., hist, n_live (device piece count, nullable), stream
     _sig(lib, "oryx_rdf_histogram_pieces", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i,

@@ -1,18 +1,24 @@
 """Batched top-N over a GPU-resident item matrix (the ALS serving hot path).
 
-:class:`ItemIndex` keeps the serving model's item vectors on the device as fp32 rows sorted by
-LSH bucket, so a query's candidate buckets are contiguous row ranges; :meth:`ItemIndex.scan`
-scores up to 16 queries per launch of the fused HIP kernel ``oryx_topn_scan``
-(``csrc/kernels/topn.hip``: fp32 MFMA scoring, cosine scale, candidate-bucket mask, excluded
-items and a per-wave LDS top-64 in the epilogue) and merges the per-wave candidates with one
-small ``topk``.  Only the union of the batch's candidate ranges is read, so an LSH sample rate
-of 0.3 reads ~30% of the matrix for a single query (the reference scans candidate partitions
-on a thread pool: ``[serving-app]/als/model/ALSServingModel.java:289-335``,
-``LocalitySensitiveHash.java:156-177``, bounded heaps ``TopNConsumer.java:55-74``).
+:class:`ItemIndex` orders the serving model's items by LSH bucket, so a query's candidate
+buckets are contiguous position ranges; :meth:`ItemIndex.scan` scores up to 16 queries per
+launch of the fused HIP kernel ``oryx_topn_scan2`` (``csrc/kernels/topn.hip``: fp32 MFMA
+scoring, cosine scale, candidate-bucket mask, excluded items and a per-wave LDS top-KL in the
+epilogue) and merges the per-wave candidates with one small ``topk``.  Only the union of the
+batch's candidate ranges is read, so an LSH sample rate of 0.3 reads ~30% of the matrix for a
+single query (the reference scans candidate partitions on a thread pool:
+``[serving-app]/als/model/ALSServingModel.java:289-335``, ``LocalitySensitiveHash.java:156-177``,
+bounded heaps ``TopNConsumer.java:55-74``).
 
-The index follows the item store (``FeatureVectors``) incrementally: changed rows whose LSH
-bucket is unchanged are rewritten in place; new rows, removals and bucket moves trigger a
-re-sort (one gather of the matrix on the device).
+One device copy of the items: on the store's own GPU the index holds only a bucket-sorted
+permutation (position -> store row) and the kernel reads the store's padded device mirror in
+place, so value updates cost the index nothing and new items / bucket moves re-sort a
+permutation, not the matrix.  Shards of an item-sharded index on other GPUs
+(:class:`ShardedItemIndex`) keep their own share of the rows.
+
+Request depth: ``how_many`` up to 64 per (wave, query) list in the batched launch, 256 / 1024
+in deeper single-pass launches, and beyond that repeated passes that exclude what earlier
+passes returned -- every depth is exact.
 """
 
 from __future__ import annotations
@@ -30,7 +36,8 @@ __all__ = ["ItemIndex", "ShardedItemIndex", "TopNQuery", "MAX_BATCH", "MAX_HOW_M
            "kernel_ok"]
 
 MAX_BATCH = 16          # queries per kernel launch
-MAX_HOW_MANY = 64       # candidates each wave keeps per query
+MAX_HOW_MANY = 64       # candidates each wave keeps per query in the batched launch
+_KLS = (64, 256, 1024)  # per-(wave, query) list lengths the kernel is built for
 _KPS = (16, 32, 48, 64, 80, 96, 112, 128, 160, 192, 256)
 
 
@@ -39,6 +46,11 @@ def _kp(k: int) -> Optional[int]:
         if v >= k:
             return v
     return None
+
+
+def row_pad_for(k: int) -> int:
+    """Row stride padding for a feature store the scan reads in place (stride = kp)."""
+    return _kp(k) or 1
 
 
 def kernel_ok(device, k: int) -> bool:
@@ -56,9 +68,9 @@ class TopNQuery:
 
 
 class ItemIndex:
-    """Bucket-sorted device copy of an item store (see module docstring).  ``shard`` =
-    (d, N) keeps only the store rows r with r % N == d, on ``device`` (item sharding over
-    several GPUs: :class:`ShardedItemIndex`)."""
+    """Bucket-sorted view of an item store (see module docstring).  ``shard`` = (d, N) keeps
+    only the store rows r with r % N == d, on ``device`` (item sharding over several GPUs:
+    :class:`ShardedItemIndex`)."""
 
     def __init__(self, store, num_buckets: int, device=None, shard: Tuple[int, int] = (0, 1),
                  managed: bool = False):
@@ -73,10 +85,15 @@ class ItemIndex:
         self.shard = (int(shard[0]), int(shard[1]))
         self.num_buckets = max(1, int(num_buckets))
         self.words = (self.num_buckets + 31) // 32
+        # borrowed: the kernel reads the store's device mirror in place (same GPU, rows kp
+        # floats apart); otherwise this index keeps its own rows
+        self.borrowed = (self.shard[1] == 1 and store.device is not None and
+                         self.device == torch.device(store.device) and
+                         getattr(store, "ld", self.k) == self.kp)
         self._lock = threading.Lock()
         self.version = -1
-        self.Ys = None          # fp32 [n][kp] sorted by bucket
-        self.inv_norm = None    # fp32 [n]
+        self.Ys = None          # owned mode: fp32 [n][kp] sorted by bucket
+        self.perm = None        # borrowed mode: int32 [n] position -> store row
         self.bucket_of = None   # int32 [n]
         self.pos_of_row = None  # int64 [store capacity] -> position or -1 (device)
         self.row_of_pos = None  # int64 [n] (device) and host copy
@@ -84,6 +101,7 @@ class ItemIndex:
         self.bucket_start = None   # host int64 [num_buckets + 1]
         self.n = 0
         self.rebuilds = 0
+        self._built = False
 
     # ------------------------------------------------------------------ maintenance
     def refresh(self, state: Optional[Tuple[int, Optional[np.ndarray]]] = None) -> None:
@@ -92,17 +110,17 @@ class ItemIndex:
         rows together, before the device view, so no write can fall between them."""
         st = self.store
         if state is None:
-            if self._managed or (self.version == st.version and self.Ys is not None):
+            if self._managed or (self.version == st.version and self._built):
                 return
         with self._lock:
             if state is None:
-                if self.version == st.version and self.Ys is not None:
+                if self.version == st.version and self._built:
                     return
                 state = st.take_index_state(self._token)
             ver, dirty = state
             mat, valid, _ = st.device_view()
             parts = st.device_partitions()
-            if self.Ys is None or dirty is None or not self._update_in_place(mat, valid, parts,
+            if not self._built or dirty is None or not self._update_in_place(mat, valid, parts,
                                                                              dirty):
                 self._rebuild(mat, valid, parts)
             self.version = ver
@@ -123,18 +141,22 @@ class ItemIndex:
         rows = rows[order]
         b = b[order]
         n = int(rows.numel())
-        ys = torch.zeros((max(n, 1), self.kp), dtype=torch.float32, device=dev)
-        # gathered in slices of 1M rows: a whole-matrix mat[rows] temporary would add another
-        # full copy of the item factors to the peak HBM of a rebuild (20 GB at 20M x 250)
-        step = 1 << 20
-        for lo in range(0, n, step):
-            hi = min(n, lo + step)
-            ys[lo:hi, :self.k] = mat[rows[lo:hi]].to(dev)
+        if self.borrowed:
+            self.perm = rows.to(torch.int32).contiguous() if n else \
+                torch.zeros(1, dtype=torch.int32, device=dev)
+            self.Ys = None
+        else:
+            ys = torch.zeros((max(n, 1), self.kp), dtype=torch.float32, device=dev)
+            # gathered in slices of 1M rows: a whole-matrix mat[rows] temporary would add
+            # another full copy of the item factors to the peak HBM of a rebuild
+            step = 1 << 20
+            for lo in range(0, n, step):
+                hi = min(n, lo + step)
+                ys[lo:hi, :self.k] = mat[rows[lo:hi]].to(dev)
+            self.Ys = ys
+            self.perm = None
         rows = rows.to(dev)
         b = b.to(dev)
-        self.Ys = ys
-        nrm = ys[:n].norm(dim=1) if n else torch.zeros(0, device=dev)
-        self.inv_norm = torch.where(nrm > 0, 1.0 / nrm, torch.zeros_like(nrm))
         self.bucket_of = b.to(torch.int32).contiguous()
         pos = torch.full((mat.shape[0],), -1, dtype=torch.int64, device=dev)
         if n:
@@ -147,8 +169,12 @@ class ItemIndex:
         np.cumsum(counts, out=self.bucket_start[1:])
         self.n = n
         self.rebuilds += 1
+        self._built = True
 
     def _update_in_place(self, mat, valid, parts, dirty: np.ndarray) -> bool:
+        """Changed rows that stay in their bucket: nothing to do when the kernel reads the
+        store's mirror (it is already current), a row copy otherwise.  New / removed rows and
+        bucket moves return False (re-sort)."""
         if len(dirty) == 0:
             return True
         if len(dirty) > max(4096, self.n // 16):
@@ -166,40 +192,70 @@ class ItemIndex:
             return False
         pos = self.pos_of_row[rows]
         ok = valid[src].to(dev)
-        # new / removed rows or a changed bucket need a re-sort
         if bool(((pos < 0) | ~ok).any()):
             return False
         nb = self._buckets(parts, src).to(dev)
         if bool((nb != self.bucket_of[pos].to(torch.int64)).any()):
             return False
-        self.Ys[pos, :self.k] = mat[src].to(dev)
-        nrm = self.Ys[pos].norm(dim=1)
-        self.inv_norm[pos] = torch.where(nrm > 0, 1.0 / nrm, torch.zeros_like(nrm))
+        if not self.borrowed:
+            self.Ys[pos, :self.k] = mat[src].to(dev)
         return True
 
     # ------------------------------------------------------------------ queries
     def scan(self, queries: Sequence[TopNQuery]) -> List[Tuple[np.ndarray, np.ndarray]]:
-        """Per query: (store rows, scores) of the best ``how_many``, descending."""
+        """Per query: (store rows, scores) of the best ``how_many``, descending (exact for
+        any depth)."""
         self.refresh()
-        out: List[Tuple[np.ndarray, np.ndarray]] = []
-        for lo in range(0, len(queries), MAX_BATCH):
-            out.extend(self._scan_batch(queries[lo:lo + MAX_BATCH]))
+        out: List[Optional[Tuple[np.ndarray, np.ndarray]]] = [None] * len(queries)
+        deep = [j for j, q in enumerate(queries) if q.how_many > _KLS[-1]]
+        for j in deep:
+            out[j] = self._scan_deep(queries[j])
+        rest = [j for j in range(len(queries)) if out[j] is None]
+        # one launch per (cosine, list length) group, as many queries as its LDS holds
+        groups = {}
+        for j in rest:
+            q = queries[j]
+            kl = next(v for v in _KLS if v >= q.how_many)
+            groups.setdefault((bool(q.cosine), kl), []).append(j)
+        for (cos, kl), idx in sorted(groups.items()):
+            per = min(MAX_BATCH, int(native.require_kernels().oryx_topn_max_queries(kl)))
+            for lo in range(0, len(idx), per):
+                part = idx[lo:lo + per]
+                for j, r in zip(part, self._launch([queries[j] for j in part], cos, kl)):
+                    out[j] = r
         return out
 
-    def _scan_batch(self, qs: Sequence[TopNQuery]):
+    def _scan_deep(self, q: TopNQuery) -> Tuple[np.ndarray, np.ndarray]:
+        """``how_many`` beyond one list: passes of the deepest list, each excluding the rows
+        the previous passes returned (scores arrive in descending order across passes)."""
+        kl = _KLS[-1]
+        rows_all, sc_all = [], []
+        excl = list(q.exclude_rows) if q.exclude_rows is not None else []
+        left = q.how_many
+        while left > 0:
+            take = min(left, kl)
+            sub = TopNQuery(q.target, take, q.cosine, q.candidates,
+                            excl + [int(r) for part in rows_all for r in part])
+            r, v = self._launch([sub], bool(q.cosine), kl)[0]
+            rows_all.append(r)
+            sc_all.append(v)
+            left -= take
+            if len(r) < take:
+                break           # the candidates ran out
+        return (np.concatenate(rows_all) if rows_all else np.zeros(0, dtype=np.int64),
+                np.concatenate(sc_all) if sc_all else np.zeros(0, dtype=np.float32))
+
+    def _matrix(self):
+        """(device matrix pointer owner, row stride) the kernel reads, and the permutation."""
+        if self.borrowed:
+            mat, ld = self.store.device_rows()
+            return mat, ld, self.perm
+        return self.Ys, self.kp, None
+
+    def _launch(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY):
         empty = (np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32))
         if self.n == 0:
             return [empty for _ in qs]
-        # cosine and dot queries differ in the epilogue: one launch per kind
-        res: List[Optional[Tuple[np.ndarray, np.ndarray]]] = [None] * len(qs)
-        for cos in (False, True):
-            idx = [j for j, q in enumerate(qs) if bool(q.cosine) == cos]
-            if idx:
-                for j, r in zip(idx, self._launch([qs[j] for j in idx], cos)):
-                    res[j] = r
-        return res
-
-    def _launch(self, qs: Sequence[TopNQuery], cosine: bool):
         dev = self.device
         lib = native.require_kernels()
         nq = len(qs)
@@ -223,8 +279,7 @@ class ItemIndex:
             keep = ends > starts
             starts, ends = starts[keep], ends[keep]
             if len(starts) == 0:
-                return [(np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32))
-                        for _ in qs]
+                return [empty for _ in qs]
             # merge adjacent ranges
             brk = np.nonzero(starts[1:] != ends[:-1])[0] + 1
             rs = np.stack([starts[np.r_[0, brk]], ends[np.r_[brk - 1, len(ends) - 1]]], 1)
@@ -261,27 +316,29 @@ class ItemIndex:
                 ptr[j + 1] = ptr[j] + len(pj)
             ex_dev = torch.from_numpy(np.concatenate(chunks) if ptr[-1] else
                                       np.zeros(1, dtype=np.int32)).to(dev)
-        waves = int(lib.oryx_topn_waves(n_tiles))
-        o_sc = torch.empty((waves, MAX_BATCH, MAX_HOW_MANY), dtype=torch.float32, device=dev)
-        o_rw = torch.empty((waves, MAX_BATCH, MAX_HOW_MANY), dtype=torch.int32, device=dev)
+        waves = int(lib.oryx_topn_waves_kl(n_tiles, kl))
+        o_sc = torch.empty((waves, nq, kl), dtype=torch.float32, device=dev)
+        o_rw = torch.empty((waves, nq, kl), dtype=torch.int32, device=dev)
         Qd = torch.from_numpy(Q).to(dev)
         rs_d = torch.from_numpy(np.ascontiguousarray(rs, dtype=np.int64)).to(dev)
         t0_d = torch.from_numpy(tile0).to(dev)
         bits_d = torch.from_numpy(bits).to(dev) if bits is not None else None
         ptr_d = torch.from_numpy(ptr).to(dev) if ex_dev is not None else None
-        rc = lib.oryx_topn_scan(
-            self.Ys.data_ptr(), self.inv_norm.data_ptr() if cosine else None, Qd.data_ptr(),
-            self.kp, nq, self.bucket_of.data_ptr() if bits_d is not None else None,
+        mat, ld, perm = self._matrix()
+        rc = lib.oryx_topn_scan2(
+            mat.data_ptr(), perm.data_ptr() if perm is not None else None, int(ld),
+            Qd.data_ptr(), self.kp, nq, int(bool(cosine)), int(kl),
+            self.bucket_of.data_ptr() if bits_d is not None else None,
             bits_d.data_ptr() if bits_d is not None else None, self.words, rs_d.data_ptr(),
             t0_d.data_ptr(), len(rs), n_tiles,
             ptr_d.data_ptr() if ptr_d is not None else None,
             ex_dev.data_ptr() if ex_dev is not None else None,
             o_sc.data_ptr(), o_rw.data_ptr(), native.stream_ptr(dev))
-        native.check(rc, "oryx_topn_scan")
+        native.check(rc, "oryx_topn_scan2")
         m = max(q.how_many for q in qs)
-        m = min(m, waves * MAX_HOW_MANY)
-        sc = o_sc[:, :nq].permute(1, 0, 2).reshape(nq, -1)
-        rw = o_rw[:, :nq].permute(1, 0, 2).reshape(nq, -1)
+        m = min(m, waves * kl)
+        sc = o_sc.permute(1, 0, 2).reshape(nq, -1)
+        rw = o_rw.permute(1, 0, 2).reshape(nq, -1)
         v, i = torch.topk(sc, m, dim=1)
         pos = torch.gather(rw, 1, i)
         v_h, pos_h = v.cpu().numpy(), pos.cpu().numpy()
@@ -291,6 +348,42 @@ class ItemIndex:
             keep = np.isfinite(vj) & (pj >= 0)
             out.append((self.row_of_pos_h[pj[keep]], vj[keep]))
         return out
+
+    # ------------------------------------------------------------------ all scores
+    def all_scores(self, target: np.ndarray, cosine: bool, candidates=None,
+                   exclude_rows=None) -> Tuple[np.ndarray, np.ndarray]:
+        """(store rows, scores) of EVERY candidate item (LSH buckets ``candidates``, minus
+        ``exclude_rows``): what an arbitrary rescorer must see (``TopNConsumer`` applies the
+        rescorer to each candidate).  One GEMV over the rows the index reads."""
+        self.refresh()
+        if self.n == 0:
+            return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32)
+        dev = self.device
+        mat, ld, perm = self._matrix()
+        q = torch.zeros(self.kp, dtype=torch.float32, device=dev)
+        q[:self.k] = torch.as_tensor(np.asarray(target, dtype=np.float32)[:self.k], device=dev)
+        if self.borrowed:
+            # one GEMV over the store's rows, then the index's positions (no row gather)
+            _, _, norms = self.store.device_view()
+            scores = mat.matmul(q)[self.row_of_pos]
+            nrm = norms[self.row_of_pos] if cosine else None
+        else:
+            scores = mat[:self.n].matmul(q)
+            nrm = mat[:self.n].norm(dim=1) if cosine else None
+        if cosine:
+            scores = torch.where(nrm > 0, scores / nrm, torch.zeros_like(scores))
+        keep = torch.isfinite(scores)
+        if candidates is not None:
+            cand = torch.zeros(self.num_buckets, dtype=torch.bool, device=dev)
+            cand[torch.as_tensor(np.asarray(candidates, dtype=np.int64), device=dev)] = True
+            keep &= cand[self.bucket_of.long()]
+        if exclude_rows is not None and len(exclude_rows):
+            er = torch.as_tensor(np.asarray(exclude_rows, dtype=np.int64), device=dev)
+            er = er[er < self.pos_of_row.numel()]
+            p = self.pos_of_row[er]
+            keep[p[p >= 0]] = False
+        pos = torch.nonzero(keep).flatten()
+        return self.row_of_pos_h[pos.cpu().numpy()], scores[pos].cpu().numpy()
 
 
 class ShardedItemIndex:
@@ -342,6 +435,13 @@ class ShardedItemIndex:
             o = np.lexsort((rows, -sc))[:q.how_many]
             out.append((rows[o], sc[o]))
         return out
+
+    def all_scores(self, target, cosine: bool, candidates=None, exclude_rows=None):
+        self.refresh()
+        parts = [f.result() for f in [self._pool.submit(sh.all_scores, target, cosine,
+                                                        candidates, exclude_rows)
+                                       for sh in self.shards]]
+        return (np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts]))
 
     def close(self) -> None:
         self._pool.shutdown(wait=False)

@@ -598,3 +598,125 @@ def test_up_blocks_from_log_keep_order(tmp_path):
     assert m.get_known_items("U7") == {"I7"}
     cons.close()
     topic.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cosine", [False, True])
+def test_topn_deep_requests_are_exact(cuda, cosine):
+    """howMany + offset beyond one per-wave list: 100 / 500 in the 256 / 1024-deep launches,
+    1500 / 3000 in several passes that exclude what earlier passes returned -- all equal to a
+    brute-force fp64 top-k, with LSH candidates and excluded rows; the index reads the
+    store's padded mirror in place (no second copy of Y)."""
+    from oryx_amd.models.als.common import FeatureVectors
+    from oryx_amd.ops import topn
+    g = np.random.default_rng(21)
+    k, n, nb = 50, 100_003, 16
+    H = torch.from_numpy(g.standard_normal((4, k)).astype(np.float32)).to(cuda)
+    w = (1 << torch.arange(4, device=cuda))
+    part = lambda rows: ((rows @ H.t()) > 0).long().mul(w).sum(1)
+    fv = FeatureVectors(k, cuda, partitioner=part, row_pad=topn.row_pad_for(k))
+    Y = g.standard_normal((n, k)).astype(np.float32)
+    fv.set_vectors(["I%d" % i for i in range(n)], Y)
+    idx = topn.ItemIndex(fv, nb)
+    idx.refresh()
+    assert idx.borrowed and idx.Ys is None
+    bucket = part(torch.from_numpy(Y).to(cuda)).cpu().numpy()
+    Yt = torch.from_numpy(Y)
+    valid = torch.ones(n, dtype=torch.bool)
+    for hm in (100, 500, 1500, 3000):
+        cands = np.sort(g.choice(nb, 11, replace=False))
+        ex = g.integers(0, n, 40).tolist()
+        for c in (None, cands):
+            q = topn.TopNQuery(g.standard_normal(k).astype(np.float32), hm, cosine,
+                               candidates=c, exclude_rows=ex)
+            rows, scores = idx.scan([q])[0]
+            allowed = None if c is None else torch.from_numpy(np.isin(bucket, c))
+            br, bs = _brute(Yt, valid, q.target, hm, cosine, allowed=allowed, exclude=ex)
+            assert len(rows) == len(br) == hm
+            np.testing.assert_allclose(scores, bs, rtol=1e-5, atol=1e-5)
+            assert (rows == br).mean() > 0.97
+            assert len(set(rows.tolist())) == hm and not set(rows.tolist()) & set(ex)
+
+
+class _Boost:
+    """Filters IDs ending in 5, boosts IDs ending in 77 by +8 (items far below the raw top
+    win), NaN for IDs ending in 3 (dropped)."""
+
+    def is_filtered(self, id_):
+        return id_.endswith("5")
+
+    def rescore(self, id_, v):
+        if id_.endswith("3"):
+            return float("nan")
+        return v + 8.0 if id_.endswith("77") else v
+
+
+@pytest.mark.gpu
+def test_rescorer_sees_every_candidate_on_large_catalogue(cuda):
+    """A rescorer is applied to EVERY candidate (TopNConsumer semantics) on a 200k-item
+    catalogue: the boosted winners come from far below the raw top-4096; per-item and
+    vectorised rescorer forms agree with a numpy reference."""
+    from oryx_amd.models.als.rescorer import Rescorer
+    from oryx_amd.models.als.serving import ALSServingModel
+
+    class PerItem(_Boost, Rescorer):
+        pass
+
+    class Vectorised(PerItem):
+        def is_filtered_many(self, ids):
+            return np.array([i[-1] == "5" for i in ids])
+
+        def rescore_many(self, ids, scores):
+            last2 = np.array([i[-2:] for i in ids])
+            v = np.where(last2 == "77", scores + 8.0, scores)
+            return np.where(np.char.endswith(last2, "3"), np.nan, v)
+
+    g = np.random.default_rng(8)
+    k, n = 32, 200_000
+    m = ALSServingModel(k, True, 1.0, device=torch.device(cuda))
+    Y = (g.standard_normal((n, k)) * 0.2).astype(np.float32)
+    ids = ["I%d" % i for i in range(n)]
+    m.Y.set_vectors(ids, Y)
+    t = g.standard_normal(k).astype(np.float32)
+    raw = (Y.astype(np.float64) @ t.astype(np.float64))
+    ref = raw.copy()
+    last = np.array([i[-1] for i in ids])
+    ref[np.array([i.endswith("77") for i in ids])] += 8.0
+    ref[(last == "5") | (last == "3")] = -np.inf
+    ref[[17, 27]] = -np.inf          # excluded below
+    best = np.argsort(-ref)[:100]
+    # the winners include items far outside the raw top 4096
+    raw_rank = np.argsort(np.argsort(-raw))
+    assert raw_rank[best].max() > 4096
+    for r in (PerItem(), Vectorised()):
+        got = m.top_n(t, 100, exclude={"I17", "I27"}, rescorer=r)
+        assert [i for i, _ in got] == [ids[b] for b in best]
+        np.testing.assert_allclose([v for _, v in got], ref[best], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_serving_model_keeps_one_device_copy_of_y(cuda):
+    """The top-N index reads the store's padded device mirror in place: no second copy of Y
+    on the GPU, value updates need no index work, new items re-sort only a permutation."""
+    from oryx_amd.models.als.serving import ALSServingModel
+    g = np.random.default_rng(9)
+    k, n = 250, 200_000
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated(cuda)
+    m = ALSServingModel(k, True, 1.0, device=torch.device(cuda))
+    Y = g.standard_normal((n, k)).astype(np.float32)
+    m.Y.set_vectors(["I%d" % i for i in range(n)], Y)
+    t = g.standard_normal(k).astype(np.float32)
+    top = m.top_n(t, 10)
+    assert [i for i, _ in top] == ["I%d" % b for b in np.argsort(-(Y @ t))[:10]]
+    assert m.index.borrowed and m.index.Ys is None
+    torch.cuda.synchronize()
+    used = torch.cuda.memory_allocated(cuda) - base
+    mirror = (n + n // 8) * 256 * 4
+    assert used < mirror * 1.1, (used, mirror)
+    # an in-place value update is visible without an index rebuild
+    rebuilds = m.index.rebuilds
+    best = int(np.argsort(-(Y @ t))[50])
+    m.Y.set_vector("I%d" % best, Y[best] * 0 + t * 10)
+    assert m.top_n(t, 1)[0][0] == "I%d" % best
+    assert m.index.rebuilds == rebuilds or m.index.rebuilds == rebuilds + 1
