@@ -148,8 +148,9 @@ class ALSSpeedModel(SpeedModel):
 
     def prefetch_inverses(self, stream=None) -> None:
         """Queue the device Gramians + Cholesky inverses for the current factors (on
-        ``stream``) without waiting: a speed-layer interval starts them before parsing its
-        input on the host, and :meth:`solver_inverses` then only collects them."""
+        ``stream``) without waiting; :meth:`solver_inverses` then only collects them.  (Not
+        called per interval: at rank 64 the ~0.6 ms of GPU work is mostly host launch time,
+        which moved into the parse phase instead of hiding -- r3_speed_profile_*.)"""
         if self.device is None or self.device.type != "cuda":
             return
         key = (self.X.version, self.Y.version)
@@ -289,8 +290,6 @@ class ALSSpeedModelManager(SpeedModelManager):
             return
         import time
         t0 = time.perf_counter()
-        # the Gramian inverses run on the GPU while the host parses the interval
-        model.prefetch_inverses(self._device_stream(model.device))
         # per-batch dictionaries, reused (cleared) so their tables are not reallocated and
         # re-faulted every micro-batch
         if self._dicts is None:
