@@ -263,10 +263,12 @@ int oryx_topn_max_queries(int kl) {
 // Number of waves the scan uses for n_tiles 16-row tiles with `kl` candidates per (wave,
 // query) (the caller sizes out_* to waves * nq * kl).
 long long oryx_topn_waves_kl(long long n_tiles, int kl) {
-  // ~8 tiles per wave at least; at most 8 waves per SIMD of 256 CUs for kl = 64, fewer for
-  // the deep lists (their candidate output and final sorts grow with kl)
+  // ~8 tiles per wave at least; at most 8 waves per SIMD of 256 CUs for kl = 64, and at
+  // least 2 per SIMD for the deep lists (their candidate output and final sorts grow with
+  // kl; with 2 waves per CU the 1024-deep scan of 20M x 250 ran at half the bandwidth)
   long long w = (n_tiles + 7) / 8;
-  const long long cap = 256 * 4 * 8 / (kl / 64 > 0 ? kl / 64 : 1);
+  long long cap = 256 * 4 * 8 / (kl / 64 > 0 ? kl / 64 : 1);
+  if (cap < 2048) cap = 2048;
   if (w > cap) w = cap;
   if (w < 1) w = 1;
   return (w + WPB - 1) / WPB * WPB;

@@ -1266,6 +1266,33 @@ long long oryx_up_texts(char* ids, long long ids_cap, char* known, long long kno
   return (long long)g_up_ids.size();
 }
 
+// IDs only (the known-item texts stay behind for oryx_up_known_codes).
+long long oryx_up_ids(char* ids, long long ids_cap) {
+  if ((long long)g_up_ids.size() > ids_cap) return -(long long)g_up_ids.size();
+  memcpy(ids, g_up_ids.data(), g_up_ids.size());
+  return (long long)g_up_ids.size();
+}
+
+// The known items of the last UP parse on this thread as codes of dictionary `dh` (the
+// serving model keeps known items as item codes, not millions of Python strings).  Returns
+// the number of items (only the first `cap` are written).
+long long oryx_up_known_codes(void* dh, long long* out, long long cap) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  const std::string& s = g_up_known;
+  long long n = 0;
+  size_t p = 0;
+  while (p < s.size()) {
+    const size_t e = s.find('\0', p);
+    if (e == std::string::npos) break;
+    const int64_t c = d->encode(std::string_view(s.data() + p, e - p));
+    if (n < cap) out[n] = c;
+    ++n;
+    p = e + 1;
+  }
+  return n;
+}
+
 }  // extern "C"
 
 namespace {

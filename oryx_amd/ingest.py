@@ -171,7 +171,7 @@ class RowMap:
         return out
 
 
-def parse_up_batch(messages: Sequence[str], k: int):
+def parse_up_batch(messages: Sequence[str], k: int, known_dict: Optional["IdDict"] = None):
     """Bulk-parse ALS ``UP`` messages ``["X"|"Y", id, [k floats], [known ids]?]``.
 
     Returns (kinds uint8 [n] -- 0 X, 1 Y, 2 unparseable --, ids list, vectors fp32 [n, k],
@@ -190,14 +190,28 @@ def parse_up_batch(messages: Sequence[str], k: int):
     native.runtime().oryx_parse_up_batch(blob, ends.ctypes.data_as(vp), n, int(k),
                                          kinds.ctypes.data_as(vp), vecs.ctypes.data_as(vp),
                                          id_ends.ctypes.data_as(vp), kcnt.ctypes.data_as(vp))
-    ids, known = _up_texts(id_ends, kcnt, len(blob))
+    if known_dict is not None:
+        ids, known = _up_ids_codes(id_ends, kcnt, known_dict)
+    else:
+        ids, known = _up_texts(id_ends, kcnt, len(blob))
     return kinds, ids, vecs, known
 
 
-def parse_up_records(raw_ptr: int, used: int, nrec: int, k: int, max_n: int):
+def _known_mode(model):
+    """What an UP parse should do with known items for ``model``: its item dictionary
+    (codes), False (the model keeps none: skip them) or None (string lists)."""
+    kd = getattr(model, "known_items_dict", None)
+    if kd is not None:
+        return kd
+    return None if hasattr(model, "add_known_items") else False
+
+
+def parse_up_records(raw_ptr: int, used: int, nrec: int, k: int, max_n: int,
+                     known_dict: Optional["IdDict"] = None):
     """The leading run of ``UP`` records of a raw log poll buffer (see
     ``oryx_parse_up_records``): returns (count, consumed bytes, kinds, ids, vectors, known) --
-    count 0 when the first record is not a parseable ``UP``."""
+    count 0 when the first record is not a parseable ``UP``.  With ``known_dict`` the known
+    items come back as :class:`KnownCodes` of that dictionary instead of string lists."""
     m = min(nrec, max_n)
     kinds = np.empty(m, dtype=np.uint8)
     vecs = np.empty((m, k), dtype=np.float32)
@@ -211,7 +225,10 @@ def parse_up_records(raw_ptr: int, used: int, nrec: int, k: int, max_n: int):
         kcnt.ctypes.data_as(vp), ctypes.byref(consumed))
     if got <= 0:
         return 0, 0, None, None, None, None
-    ids, known = _up_texts(id_ends[:got], kcnt[:got], int(used))
+    if known_dict is not None:
+        ids, known = _up_ids_codes(id_ends[:got], kcnt[:got], known_dict)
+    else:
+        ids, known = _up_texts(id_ends[:got], kcnt[:got], int(used))
     return got, consumed.value, kinds[:got], ids, vecs[:got], known
 
 
@@ -232,6 +249,51 @@ def parse_feature_lines(data: bytes, k: int):
         return None
     ids, _ = _up_texts(id_ends[:n], np.full(n, -1, dtype=np.int64), 16)
     return ids, vecs[:n]
+
+
+class KnownCodes:
+    """Known-item lists of parsed ``UP`` rows as codes of an :class:`IdDict`: row j's items
+    are ``codes[offs[j]:offs[j + 1]]``; ``has[j]`` is False for a row without a list."""
+
+    __slots__ = ("codes", "offs", "has")
+
+    def __init__(self, codes: np.ndarray, counts: np.ndarray):
+        self.codes = codes
+        c = np.maximum(np.asarray(counts, dtype=np.int64), 0)
+        self.offs = np.zeros(len(c) + 1, dtype=np.int64)
+        np.cumsum(c, out=self.offs[1:])
+        self.has = np.asarray(counts) >= 0
+
+    def __len__(self) -> int:
+        return len(self.has)
+
+    def row(self, j: int) -> Optional[np.ndarray]:
+        return self.codes[self.offs[j]:self.offs[j + 1]] if self.has[j] else None
+
+
+def _up_ids_codes(id_ends: np.ndarray, kcnt: np.ndarray, known_dict: "IdDict"):
+    """IDs (strings) and known items (:class:`KnownCodes`) of the last native UP parse."""
+    n = len(id_ends)
+    ids_cap = max(1, int(id_ends[-1]) if n else 0)
+    ib = np.empty(ids_cap, dtype=np.uint8)
+    lib = native.runtime()
+    if lib.oryx_up_ids(ib.ctypes.data, ids_cap) < 0:
+        raise RuntimeError("UP batch ids exceed their buffer")
+    raw = ib[:int(id_ends[-1]) if n else 0].tobytes()
+    starts = np.r_[0, id_ends[:-1]].tolist() if n else []
+    if raw.isascii():
+        text = raw.decode("ascii")
+        ids = [text[a:b] for a, b in zip(starts, id_ends.tolist())]
+    else:
+        ids = [raw[a:b].decode("utf-8") for a, b in zip(starts, id_ends.tolist())]
+    if known_dict is False:
+        return ids, None
+    total = int(np.maximum(kcnt, 0).sum()) if n else 0
+    codes = np.empty(max(1, total), dtype=np.int64)
+    got = lib.oryx_up_known_codes(known_dict.handle, codes.ctypes.data, total)
+    if got != total:
+        raise RuntimeError("UP known items: %d parsed, %d counted" % (got, total))
+    return ids, KnownCodes(codes[:total].astype(np.int32), kcnt)
 
 
 def _up_texts(id_ends: np.ndarray, kcnt: np.ndarray, bound: int):

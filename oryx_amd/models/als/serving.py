@@ -273,7 +273,9 @@ class ALSServingModel(ServingModel):
         self.Y = FeatureVectors(features, device,
                                 partitioner=self.lsh.device_partitioner(device),
                                 row_pad=topn_ops.row_pad_for(features))
-        self._known: Dict[str, Set[str]] = {}
+        from ... import ingest
+        self._kdict = ingest.IdDict()
+        self._known: Dict[str, np.ndarray] = {}
         self._known_lock = AutoReadWriteLock()
         self._expected_users: Set[str] = set()
         self._expected_items: Set[str] = set()
@@ -332,40 +334,93 @@ class ALSServingModel(ServingModel):
         with self._expected_lock:
             self._expected_items.difference_update(ids)
 
+    # known items are held as int32 codes of one native item dictionary per model (a loaded
+    # model has ~20 per user: 10M Python strings in sets would dominate the load time and the
+    # host memory); arrays may repeat an item when a message's list did -- readers dedupe
+    @property
+    def known_items_dict(self):
+        return self._kdict
+
     def get_known_items(self, user: str) -> Set[str]:
         with self._known_lock.read():
-            s = self._known.get(user)
-            return set(s) if s else set()
+            a = self._known.get(user)
+        if a is None or len(a) == 0:
+            return set()
+        keys = self._kdict.keys()
+        return {keys[c] for c in a.tolist()}
 
     def add_known_items(self, user: str, items: Iterable[str]) -> None:
+        items = list(items)
+        codes = self._kdict.encode(items).astype(np.int32) if items else \
+            np.zeros(0, dtype=np.int32)
         with self._known_lock.write():
-            s = self._known.get(user)
-            if s is None:
-                s = self._known[user] = set()
-            s.update(items)
+            self._merge_known(user, codes)
+
+    def _merge_known(self, user: str, codes: np.ndarray) -> None:
+        a = self._known.get(user)
+        if a is None or len(a) == 0:
+            self._known[user] = codes
+        elif len(codes):
+            self._known[user] = np.union1d(a, codes).astype(np.int32)
 
     def add_known_items_many(self, pairs) -> None:
         """Bulk :meth:`add_known_items` over (user, items) pairs under one lock (loads)."""
+        pairs = [(u, list(items)) for u, items in pairs]
+        flat = [i for _, items in pairs for i in items]
+        codes = self._kdict.encode(flat).astype(np.int32) if flat else \
+            np.zeros(0, dtype=np.int32)
         with self._known_lock.write():
-            known = self._known
+            pos = 0
             for user, items in pairs:
-                s = known.get(user)
-                if s is None:
-                    known[user] = set(items)
-                else:
-                    s.update(items)
+                self._merge_known(user, codes[pos:pos + len(items)])
+                pos += len(items)
+
+    def add_known_item_codes(self, users: Sequence[str], known, rows) -> None:
+        """Known items of parsed ``UP`` rows (``ingest.KnownCodes`` of :attr:`known_items_dict`)
+        for the rows ``rows`` (log order): one lock, no per-item Python objects."""
+        codes, offs, has = known.codes, known.offs, known.has
+        with self._known_lock.write():
+            km = self._known
+            for j in rows:
+                if not has[j]:
+                    continue
+                c = codes[offs[j]:offs[j + 1]]
+                u = users[j]
+                a = km.get(u)
+                if a is None or len(a) == 0:
+                    km[u] = c
+                elif len(c):
+                    km[u] = np.union1d(a, c).astype(np.int32)
+
+    def _known_pairs(self):
+        """(user index per known entry, item code per entry, users) with duplicates removed."""
+        with self._known_lock.read():
+            users = list(self._known.keys())
+            arrs = list(self._known.values())
+        if not arrs:
+            return np.zeros(0, np.int64), np.zeros(0, np.int64), users
+        lens = np.fromiter((len(a) for a in arrs), dtype=np.int64, count=len(arrs))
+        uidx = np.repeat(np.arange(len(arrs), dtype=np.int64), lens)
+        items = np.concatenate(arrs).astype(np.int64) if lens.sum() else np.zeros(0, np.int64)
+        if len(items):
+            key = np.unique(uidx * (int(items.max()) + 1) + items)
+            n_i = int(items.max()) + 1
+            uidx, items = key // n_i, key % n_i
+        return uidx, items, users
 
     def get_user_counts(self) -> Dict[str, int]:
-        with self._known_lock.read():
-            return {u: len(s) for u, s in self._known.items()}
+        uidx, _, users = self._known_pairs()
+        cnt = np.bincount(uidx, minlength=len(users))
+        return dict(zip(users, cnt.tolist()))
 
     def get_item_counts(self) -> Dict[str, int]:
-        counts: Dict[str, int] = {}
-        with self._known_lock.read():
-            for s in self._known.values():
-                for i in s:
-                    counts[i] = counts.get(i, 0) + 1
-        return counts
+        _, items, _ = self._known_pairs()
+        if len(items) == 0:
+            return {}
+        cnt = np.bincount(items)
+        keys = self._kdict.keys()
+        nz = np.flatnonzero(cnt)
+        return {keys[c]: int(cnt[c]) for c in nz.tolist()}
 
     def get_known_item_vectors_for_user(self, user: str):
         if self.get_user_vector(user) is None:
@@ -492,10 +547,15 @@ class ALSServingModel(ServingModel):
                 del self._known[u]
         recent_items: Set[str] = set()
         self.Y.add_all_recent_to(recent_items)
+        keys = self._kdict.keys()
+        keep = np.fromiter((k in items or k in recent_items for k in keys), dtype=bool,
+                           count=len(keys))
+        if keep.all():
+            return
         with self._known_lock.write():
-            for s in self._known.values():
-                drop = [i for i in s if i not in items and i not in recent_items]
-                s.difference_update(drop)
+            for u, a in list(self._known.items()):
+                if len(a):
+                    self._known[u] = a[keep[a]]
 
     def get_fraction_loaded(self) -> float:
         with self._expected_lock:
@@ -517,7 +577,8 @@ def apply_up_batch(model, messages: List[str]) -> None:
     matrix (the later row wins for a repeated ID), known items added per user; messages the
     native parser rejects go through the per-message path (and raise as it does)."""
     from ... import ingest
-    kinds, ids, vecs, known = ingest.parse_up_batch(messages, model.get_features())
+    kinds, ids, vecs, known = ingest.parse_up_batch(
+        messages, model.get_features(), known_dict=ingest._known_mode(model))
     apply_up_parsed(model, kinds, ids, vecs, known, messages)
 
 
@@ -528,7 +589,8 @@ def drain_up_blocks(model, updates) -> int:
     take = getattr(updates, "take_up_block", None)
     done = 0
     while take is not None:
-        blk = take(model.get_features())
+        from ... import ingest
+        blk = take(model.get_features(), known_dict=ingest._known_mode(model))
         if blk is None:
             break
         apply_up_parsed(model, *blk)
@@ -556,6 +618,7 @@ def apply_up_parsed(model, kinds, ids, vecs, known, messages=None) -> None:
 
 
 def _apply_parsed_run(model, kinds, ids, vecs, known, lo: int, hi: int) -> None:
+    from ... import ingest
     for kind, setter in ((0, "set_user_vectors"), (1, "set_item_vectors")):
         sel = lo + np.nonzero(kinds[lo:hi] == kind)[0]
         if not len(sel):
@@ -566,7 +629,12 @@ def _apply_parsed_run(model, kinds, ids, vecs, known, lo: int, hi: int) -> None:
             last[ids[j]] = j
         rows = np.fromiter(last.values(), dtype=np.int64, count=len(last))
         getattr(model, setter)([ids[j] for j in rows.tolist()], vecs[rows])
-        if kind == 0 and hasattr(model, "add_known_items_many"):
+        if known is None:
+            continue
+        if kind == 0 and isinstance(known, ingest.KnownCodes):
+            if hasattr(model, "add_known_item_codes"):
+                model.add_known_item_codes(ids, known, sel.tolist())
+        elif kind == 0 and hasattr(model, "add_known_items_many"):
             model.add_known_items_many((ids[j], known[j]) for j in sel.tolist() if known[j])
         elif kind == 0 and hasattr(model, "add_known_items"):
             for j in sel.tolist():

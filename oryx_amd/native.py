@@ -111,6 +111,8 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_parse_up_batch", c_ll, [c_cp, c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_up_texts", c_ll, [c_vp, c_ll, c_vp, c_ll])
+    _sig(lib, "oryx_up_ids", c_ll, [c_vp, c_ll])
+    _sig(lib, "oryx_up_known_codes", c_ll, [c_vp, c_vp, c_ll])
     # raw, used, nrec, k, max_n, kinds, vecs, id_ends, known_cnt, consumed_bytes
     _sig(lib, "oryx_parse_up_records", c_ll, [c_vp, c_ll, c_ll, c_i, c_ll, c_vp, c_vp, c_vp,
                                               c_vp, c_vp])

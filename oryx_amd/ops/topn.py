@@ -363,14 +363,35 @@ class ItemIndex:
         q = torch.zeros(self.kp, dtype=torch.float32, device=dev)
         q[:self.k] = torch.as_tensor(np.asarray(target, dtype=np.float32)[:self.k], device=dev)
         if self.borrowed:
-            # one GEMV over the store's rows, then the index's positions (no row gather)
-            _, _, norms = self.store.device_view()
-            scores = mat.matmul(q)[self.row_of_pos]
-            nrm = norms[self.row_of_pos] if cosine else None
-        else:
-            scores = mat[:self.n].matmul(q)
-            nrm = mat[:self.n].norm(dim=1) if cosine else None
+            # one GEMV over the store's rows in store order (no permutation): rows are the
+            # positions of the mask directly
+            _, valid, norms = self.store.device_view()
+            scores = mat.matmul(q)
+            keep = valid.clone()
+            if cosine:
+                scores = torch.where(norms > 0, scores / norms, torch.zeros_like(scores))
+            if candidates is not None:
+                parts = self.store.device_partitions()
+                if parts is not None:
+                    cand = torch.zeros(self.num_buckets, dtype=torch.bool, device=dev)
+                    cand[torch.as_tensor(np.asarray(candidates, dtype=np.int64),
+                                         device=dev)] = True
+                    keep &= cand[parts.long()]
+            if exclude_rows is not None and len(exclude_rows):
+                er = torch.as_tensor(np.asarray(exclude_rows, dtype=np.int64), device=dev)
+                keep[er[er < keep.numel()]] = False
+            keep &= torch.isfinite(scores)
+            # two pinned transfers (mask + scores); the selection runs on the host
+            mask_h = torch.empty(keep.numel(), dtype=torch.bool, pin_memory=True)
+            sc_h = torch.empty(scores.numel(), dtype=torch.float32, pin_memory=True)
+            mask_h.copy_(keep)
+            sc_h.copy_(scores)
+            m_np = mask_h.numpy()
+            rows = np.flatnonzero(m_np)
+            return rows, sc_h.numpy()[rows]
+        scores = mat[:self.n].matmul(q)
         if cosine:
+            nrm = mat[:self.n].norm(dim=1)
             scores = torch.where(nrm > 0, scores / nrm, torch.zeros_like(scores))
         keep = torch.isfinite(scores)
         if candidates is not None:

@@ -83,7 +83,7 @@ class UpdateIterator:
                 self._pending.reverse()
         return out
 
-    def take_up_block(self, k: int, max_n: int = 1 << 15):
+    def take_up_block(self, k: int, max_n: int = 1 << 15, known_dict=None):
         """The next run of ``UP`` records parsed natively straight from the log's raw poll
         buffer -- no per-message Python objects -- as (kinds, ids, vectors [n, k], known
         lists); None when nothing is buffered-free to read or the next record is not a
@@ -100,8 +100,8 @@ class UpdateIterator:
                 continue
             self._rr = (self._rr + step + 1) % len(readers)
             addr, used = r.raw_buffer()
-            got, consumed, kinds, ids, vecs, known = ingest.parse_up_records(addr, used, n, k,
-                                                                              n)
+            got, consumed, kinds, ids, vecs, known = ingest.parse_up_records(
+                addr, used, n, k, n, known_dict=known_dict)
             rest = r.decode_raw(consumed, n - got)
             self._pending = [KeyMessage(key, v) for _, _, key, v in rest]
             self._pending.reverse()
