@@ -1280,15 +1280,29 @@ long long oryx_up_known_codes(void* dh, long long* out, long long cap) {
   Dict* d = static_cast<Dict*>(dh);
   std::lock_guard<std::mutex> g(d->mu);
   const std::string& s = g_up_known;
-  long long n = 0;
-  size_t p = 0;
-  while (p < s.size()) {
+  // token spans, then lookups of the (mostly already known) items on the native threads --
+  // finds are read-only -- and the misses inserted in order on this thread, which numbers
+  // new items exactly as one sequential pass would
+  std::vector<std::pair<size_t, size_t>> tok;
+  tok.reserve(s.size() / 8 + 1);
+  for (size_t p = 0; p < s.size();) {
     const size_t e = s.find('\0', p);
     if (e == std::string::npos) break;
-    const int64_t c = d->encode(std::string_view(s.data() + p, e - p));
-    if (n < cap) out[n] = c;
-    ++n;
+    tok.emplace_back(p, e - p);
     p = e + 1;
+  }
+  const long long n = (long long)tok.size();
+  std::vector<long long> code((size_t)n);
+  oryx_ff::parallel_ranges(n, 1 << 15, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t)
+      code[(size_t)t] = d->find(std::string_view(s.data() + tok[(size_t)t].first,
+                                                 tok[(size_t)t].second));
+  });
+  for (long long t = 0; t < n; ++t) {
+    if (code[(size_t)t] < 0)
+      code[(size_t)t] = d->encode(std::string_view(s.data() + tok[(size_t)t].first,
+                                                   tok[(size_t)t].second));
+    if (t < cap) out[t] = code[(size_t)t];
   }
   return n;
 }

@@ -211,8 +211,16 @@ class FeatureVectors:
             rows = np.fromiter((index.get(i, -1) for i in ids), dtype=np.int64, count=len(ids))
             new_pos = np.nonzero(rows < 0)[0]
             if len(new_pos):
-                new_ids = [ids[j] for j in new_pos.tolist()]
-                if len(set(new_ids)) != len(new_ids):
+                new_ids = [ids[j] for j in new_pos.tolist()] if len(new_pos) < len(ids) \
+                    else (ids if isinstance(ids, list) else list(ids))
+                start = self._n_rows
+                before = len(index)
+                index.update(zip(new_ids, range(start, start + len(new_ids))))
+                dup = len(index) - before != len(new_ids)
+                if dup:
+                    for i in new_ids:
+                        index.pop(i, None)
+                if dup:
                     # duplicates within the batch: fall back to the one-by-one path
                     for id_, v in zip(ids, matrix):
                         row = index.get(id_)
@@ -229,10 +237,8 @@ class FeatureVectors:
                     self._idx_mark_all()
                     self.version += 1
                     return
-                start = self._n_rows
                 self._ensure_capacity(start + len(new_ids))
                 new_rows = np.arange(start, start + len(new_ids), dtype=np.int64)
-                index.update(zip(new_ids, new_rows.tolist()))
                 if self._journal is not None:
                     self._journal.append((True, new_ids, new_rows))
                 self._ids.extend(new_ids)

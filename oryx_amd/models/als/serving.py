@@ -585,16 +585,26 @@ def apply_up_batch(model, messages: List[str]) -> None:
 def drain_up_blocks(model, updates) -> int:
     """Apply the ``UP`` runs the update iterator can parse straight from the log
     (:meth:`~oryx_amd.serving.layer.UpdateIterator.take_up_block`) until a different message
-    or the end of what is available; returns rows applied."""
+    or the end of what is available; returns rows applied.  The next block is read and
+    parsed (native, without the GIL) on a helper thread while this one is applied to the
+    model; only that thread touches the iterator until the run ends."""
     take = getattr(updates, "take_up_block", None)
+    if take is None:
+        return 0
+    from concurrent.futures import ThreadPoolExecutor
+    from ... import ingest
+    k = model.get_features()
+    kd = ingest._known_mode(model)
     done = 0
-    while take is not None:
-        from ... import ingest
-        blk = take(model.get_features(), known_dict=ingest._known_mode(model))
-        if blk is None:
-            break
-        apply_up_parsed(model, *blk)
-        done += len(blk[0])
+    with ThreadPoolExecutor(max_workers=1, thread_name_prefix="oryx-up-parse") as ex:
+        fut = ex.submit(take, k, known_dict=kd)
+        while True:
+            blk = fut.result()
+            if blk is None:
+                break
+            fut = ex.submit(take, k, known_dict=kd)
+            apply_up_parsed(model, *blk)
+            done += len(blk[0])
     return done
 
 
