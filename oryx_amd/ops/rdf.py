@@ -814,7 +814,12 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
         is_split = split.feat >= 0
         rank = torch.cumsum(is_split.int(), 1) - is_split.int()
         child_base = torch.where(is_split, 2 * rank, torch.full_like(rank, -1))
-        if depth < max_depth:
+        # sparse level state: children are numbered densely per tree, so the next level
+        # needs 2 * (most splits in any tree) slots, not 2^(depth + 1) -- one small host read
+        # per level sizes every later histogram, split search and all-reduce to the live
+        # nodes (deep levels of a forest are mostly leaves)
+        live = int(is_split.sum(1).max()) if depth < max_depth else 0
+        if live > 0:
             _route(data, node_of, W, split, child_base, B, count_visits=False)
         vis = visits
         if ctx.is_distributed:
@@ -825,9 +830,9 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
               "cat": to_host(split.cat_left) if split.cat_left is not None else None,
               "event": torch.cuda.Event()}
         lv["event"].record()
-        if depth < max_depth:
-            # next level: 2W slots, rows grouped by (tree, node) with one counting sort
-            W2 = 2 * W
+        if live > 0:
+            # next level: 2 * live slots, rows grouped by (tree, node) with one counting sort
+            W2 = 2 * live
             finish = RowGroups.launch_from_nodes(node_of, W2, weight)
             perm, counts, visits = finish.device()
             W = W2
@@ -835,6 +840,8 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
         while pending:
             build(pending.pop(0))
         pending.append(lv)
+        if live == 0:
+            break
     while pending:
         build(pending.pop(0))
     watchdog.get().end_heartbeats()
