@@ -344,6 +344,10 @@ def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = 
     centers = c0
     _, d2 = assign(pts, centers, precision=precision)
     d2 = d2.clone()
+    # each point's nearest candidate so far, kept through the rounds: the candidate weights
+    # need no final assignment pass against all ~2k * steps candidates (that pass was as much
+    # distance work as all the rounds together)
+    best = torch.zeros(n, dtype=torch.int64, device=dev)
     l = 2.0 * k
     for _ in range(steps):
         phi = d2.double().sum()
@@ -357,11 +361,13 @@ def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = 
         new = _gather_rows(picked, ctx)
         if new.shape[0] == 0:
             continue
+        base = centers.shape[0]
         centers = torch.cat([centers, new])
-        _, dn = assign(pts, new, precision=precision)
+        idn, dn = assign(pts, new, precision=precision)
+        closer = dn < d2
+        best = torch.where(closer, idn.long() + base, best)
         d2 = torch.minimum(d2, dn)
-    idx, _ = assign(pts, centers, precision=precision)
-    w = torch.bincount(idx.long(), minlength=centers.shape[0]).double()
+    w = torch.bincount(best, minlength=centers.shape[0]).double()
     if ctx.is_distributed:
         dist.all_reduce_sum(w, ctx)
     chosen = _kmeanspp_weighted(centers.to(dev), w, k, gen).to(dev)
