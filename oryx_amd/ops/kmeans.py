@@ -349,6 +349,11 @@ def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = 
     # distance work as all the rounds together)
     best = torch.zeros(n, dtype=torch.int64, device=dev)
     l = 2.0 * k
+    # the per-point sampling uniforms come from a generator on the points' device, seeded
+    # from the host generator (drawing 12.5M fp64 uniforms on the host and copying them over
+    # took ~60 ms per round)
+    gd = torch.Generator(device=dev)
+    gd.manual_seed(int(torch.randint(0, 1 << 62, (1,), generator=gen)))
     for _ in range(steps):
         phi = d2.double().sum()
         if ctx.is_distributed:
@@ -356,7 +361,7 @@ def _init_parallel(pts, k, gen, ctx, steps: int = 5, precision: Optional[str] = 
         if float(phi) <= 0:
             break
         p = (l * d2.double() / phi).clamp_max(1.0)
-        r = torch.rand(n, generator=gen, dtype=torch.float64).to(dev)
+        r = torch.rand(n, generator=gd, dtype=torch.float64, device=dev)
         picked = x[(r < p)].float()
         new = _gather_rows(picked, ctx)
         if new.shape[0] == 0:
