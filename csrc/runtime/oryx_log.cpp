@@ -723,7 +723,7 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
       if (rolled) continue;
       if (count > 0 || std::chrono::steady_clock::now() >= deadline) break;
       std::this_thread::sleep_for(std::chrono::microseconds(sleep_us));
-      sleep_us = std::min(sleep_us * 2, 20000);
+      sleep_us = std::min(sleep_us * 2, 2000);   // <= 2 ms behind a new record
     } else if (count > 0) {
       break;  // deliver what we have
     }

@@ -98,3 +98,15 @@ def test_bench_forced_collectives_world_one():
     rec = _json_lines(out.stdout)[0]
     _check(rec, 1)
     assert rec["backend"] == "gloo"
+
+
+def test_bench_lambda_loop_cpu():
+    """bench_lambda.py: POST /ingest -> speed UP -> changed /recommend, end to end (tiny model,
+    CPU): every trial becomes visible."""
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench_lambda.py"), "--items", "3000",
+                        "--users", "500", "--features", "8", "--trials", "4", "--device", "cpu"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = json.loads(p.stdout.strip().splitlines()[-1])
+    assert rec["trials"] == 4 and rec["timeouts"] == 0 and rec["p50_ms"] > 0
