@@ -515,14 +515,20 @@ class ALSUpdate(MLUpdate):
     def _build_sharded(self, context, lines, features, lam, alpha, candidate_path):
         ctx = self._ctx(context)
         W = ctx.world_size
+        ph = self.phase_seconds
         t_parse = time.perf_counter()
         gu, gi, s, ts, utab, itab = self._parse_global(lines, ctx)
+        ph["parse"] = ph.get("parse", 0.0) + time.perf_counter() - t_parse
+        tp = time.perf_counter()
         # events of one user on one rank, for the time-ordered aggregation
         gu, gi, s, ts = shuffle.route(gu % W, ctx, gu, gi, s, ts)
+        ph["shuffle"] = ph.get("shuffle", 0.0) + time.perf_counter() - tp
+        tp = time.perf_counter()
         if ctx.device.type == "cuda":
             au, ai, av = aggregate_scores_device(gu, gi, s, ts, self.implicit, ctx.device)
         else:
             au, ai, av = aggregate_scores(gu, gi, s, ts, self.implicit)
+        ph["aggregate"] = ph.get("aggregate", 0.0) + time.perf_counter() - tp
         used_u = np.zeros(utab.total, dtype=np.int32)
         used_i = np.zeros(itab.total, dtype=np.int32)
         used_u[au] = 1
@@ -543,20 +549,29 @@ class ALSUpdate(MLUpdate):
         t0 = time.perf_counter()
         trainer.prepare(torch.from_numpy(dense_u[au]), torch.from_numpy(dense_i[ai]),
                         torch.from_numpy(av.astype(np.float32)), nu, ni)
+        ph["csr_prepare"] = ph.get("csr_prepare", 0.0) + time.perf_counter() - t0
+        tp = time.perf_counter()
         x_ids = shuffle.gather_strings(utab, ctx, keep=used_u)
         y_ids = shuffle.gather_strings(itab, ctx, keep=used_i)
+        ph["ids_gather"] = ph.get("ids_gather", 0.0) + time.perf_counter() - tp
         x_init = y_init = None
         if self.warm_start and self.current_model_dir:
             x_init, y_init = _warm_start_factors(self.current_model_dir, features, x_ids, y_ids)
+        tp = time.perf_counter()
         f = trainer.train(self.iterations, x_init=x_init, y_init=y_init)
         X = f.X.cpu().numpy()
         Y = f.Y.cpu().numpy()
+        ph["train"] = ph.get("train", 0.0) + time.perf_counter() - tp
+        tp = time.perf_counter()
         x_rows, y_rows = textfmt.format_rows(f.X), textfmt.format_rows(f.Y)
+        ph["format_rows"] = ph.get("format_rows", 0.0) + time.perf_counter() - tp
         log.info("ALS (sharded, %d ranks) %d ratings, %d users, %d items, rank %d: %.3fs", W,
                  n_ratings, nu, ni, features, time.perf_counter() - t0)
+        tp = time.perf_counter()
         if ctx.is_main:
             write_features(os.path.join(candidate_path, "X"), x_ids, x_rows)
             write_features(os.path.join(candidate_path, "Y"), y_ids, y_rows)
+        ph["write_factors"] = ph.get("write_factors", 0.0) + time.perf_counter() - tp
         pmml = pmmlu.build_skeleton_pmml()
         pmml.add_extension("X", "X/")
         pmml.add_extension("Y", "Y/")
@@ -627,28 +642,34 @@ class ALSUpdate(MLUpdate):
         x_ids, x_rows, y_ids, y_rows = self._published_rows(pmml, model_parent_path)
         mine = np.arange(R, len(y_ids), W)
         log.info("Rank %d sending %d item / Y rows as model updates", R, len(mine))
-        rows = y_rows.take(mine).rows() if len(mine) else []
-        topic.send_many(("UP", '["Y",%s,%s]' % (json.dumps(y_ids[j]), r))
-                        for j, r in zip(mine.tolist(), rows))
+        # rows assembled natively into one block per rank (no Python string per message)
+        if len(mine):
+            topic.send_block("UP", ingest.assemble_row_messages(
+                "Y", [y_ids[j] for j in mine.tolist()], y_rows.take(mine)))
         dist.barrier(ctx)
         # users owned by this rank (crc32 owner of the ID) with their known items
         all_lines = concat_lines([new_data, past_data])
         if self.no_known_items:
             owned = np.nonzero(shuffle.owner_of_strings(x_ids, W) == R)[0]
-            xr = x_rows.take(owned).rows() if len(owned) else []
-            topic.send_many(("UP", '["X",%s,%s]' % (json.dumps(x_ids[j]), r))
-                            for j, r in zip(owned.tolist(), xr))
+            if len(owned):
+                topic.send_block("UP", ingest.assemble_row_messages(
+                    "X", [x_ids[j] for j in owned.tolist()], x_rows.take(owned)))
         else:
             known = _known_items_sharded(all_lines, ctx)
             xmap = {k: j for j, k in enumerate(x_ids)}
             sel = [(xmap[uid], uid) for uid in known if uid in xmap]
             sel.sort()
             idx = np.array([j for j, _ in sel], dtype=np.int64)
-            xr = x_rows.take(idx).rows() if len(idx) else []
             log.info("Rank %d sending %d user / X rows as model updates", R, len(idx))
-            topic.send_many(("UP", '["X",%s,%s,%s]' % (json.dumps(uid), r,
-                                                        json.dumps(sorted(known[uid]))))
-                            for (_, uid), r in zip(sel, xr))
+            if len(idx):
+                texts = [json.dumps(sorted(known[uid]), separators=(",", ":"))
+                         for _, uid in sel]
+                blob = "".join(texts).encode("utf-8")
+                kt = textfmt.RowText(blob, np.cumsum(np.fromiter(
+                    (len(t.encode("utf-8")) for t in texts), dtype=np.int64, count=len(texts))))
+                topic.send_block("UP", ingest.assemble_row_messages(
+                    "X", [uid for _, uid in sel], x_rows.take(idx), kt,
+                    np.arange(len(idx), dtype=np.int64)))
         dist.barrier(ctx)
 
     def build_timings(self, candidate_path: str) -> dict:

@@ -110,3 +110,22 @@ def test_bench_lambda_loop_cpu():
     assert p.returncode == 0, p.stderr[-3000:]
     rec = json.loads(p.stdout.strip().splitlines()[-1])
     assert rec["trials"] == 4 and rec["timeouts"] == 0 and rec["p50_ms"] > 0
+
+
+def test_bench_batch_sharded_gloo_world_two():
+    """bench_batch.py --gpus 2 on CPU (gloo): the sharded generation (each rank reads its
+    share of the input partitions, route + aggregate + train + publish per rank) publishes
+    a MODEL and every UP row, with per-phase timings."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench_batch.py"), "--gpus", "2",
+                        "--device", "cpu", "--ratings", "60000", "--users", "2000", "--items",
+                        "800", "--features", "6", "--iterations", "2"],
+                       capture_output=True, text=True, timeout=400, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["config"]["sharded"] is True
+    ph = rec["phase_s"]
+    for key in ("parse", "shuffle", "aggregate", "train", "publish_up"):
+        assert key in ph, ph
+    # MODEL + one UP row per user and item that has ratings
+    assert rec["update_messages"] > 2000
