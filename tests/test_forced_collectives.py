@@ -3,8 +3,9 @@
 the collective-free single-process run.
 
 At world size one every all-reduce / all-gather / all-to-all is an identity, so the results
-must agree bit for bit; a difference means a collective path reorders, drops or re-lays-out
-data.  The ALS run with an explicit 3-range factor exchange checks the chunk-major gathered
+must agree bit for bit (k-means centers to fp32 rounding: its k-means++ draws use a device
+scan whose last bits vary run to run); a difference means a collective path reorders, drops
+or re-lays-out data.  The ALS run with an explicit 3-range factor exchange checks the chunk-major gathered
 layout and its remapped column ids; its padded shard changes the Gramian's fp32 summation
 order, so it is compared in the fp32 factor mode to a 1e-4 bound instead of bit for bit.  Runs in a child process, because the process
 group is process-global.
@@ -101,5 +102,7 @@ def test_forced_nccl_collectives_match_single_process(tmp_path):
     assert res["chunks3"] == 3
     assert res["als"] == [0.0, 0.0], res
     assert max(res["als3"]) <= 1e-4, res
-    assert res["km"] == [0.0, 0.0], res
+    # k-means++ draws over a device fp64 cumsum (a decoupled look-back scan: its last bits can
+    # differ run to run), so centers are compared to fp32 rounding, counts exactly
+    assert res["km"][0] <= 1e-5 and res["km"][1] == 0.0, res
     assert res["rdf"] is True, res
