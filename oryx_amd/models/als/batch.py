@@ -655,21 +655,15 @@ class ALSUpdate(MLUpdate):
                 topic.send_block("UP", ingest.assemble_row_messages(
                     "X", [x_ids[j] for j in owned.tolist()], x_rows.take(owned)))
         else:
-            known = _known_items_sharded(all_lines, ctx)
+            kusers, kt = _known_items_sharded(all_lines, ctx)
             xmap = {k: j for j, k in enumerate(x_ids)}
-            sel = [(xmap[uid], uid) for uid in known if uid in xmap]
-            sel.sort()
+            sel = sorted((xmap[uid], r) for r, uid in enumerate(kusers) if uid in xmap)
             idx = np.array([j for j, _ in sel], dtype=np.int64)
             log.info("Rank %d sending %d user / X rows as model updates", R, len(idx))
             if len(idx):
-                texts = [json.dumps(sorted(known[uid]), separators=(",", ":"))
-                         for _, uid in sel]
-                blob = "".join(texts).encode("utf-8")
-                kt = textfmt.RowText(blob, np.cumsum(np.fromiter(
-                    (len(t.encode("utf-8")) for t in texts), dtype=np.int64, count=len(texts))))
                 topic.send_block("UP", ingest.assemble_row_messages(
-                    "X", [uid for _, uid in sel], x_rows.take(idx), kt,
-                    np.arange(len(idx), dtype=np.int64)))
+                    "X", [x_ids[j] for j in idx.tolist()], x_rows.take(idx), kt,
+                    np.array([r for _, r in sel], dtype=np.int64)))
         dist.barrier(ctx)
 
     def build_timings(self, candidate_path: str) -> dict:
@@ -811,8 +805,11 @@ class ALSUpdate(MLUpdate):
         return train, test
 
 
-def _known_items_sharded(lines: Sequence[str], ctx) -> Dict[str, set]:
-    """Known items of the users this rank owns (crc32 owner), from every rank's lines."""
+def _known_items_sharded(lines: Sequence[str], ctx):
+    """Known items of the users this rank owns (crc32 owner), from every rank's lines:
+    (user IDs, :class:`~oryx_amd.ops.textfmt.RowText` of each user's JSON item array).  The
+    per-pair decision (last event in time order, not a delete) is vectorised and the arrays
+    are written natively (``ingest.known_items_text``) -- no Python set per user."""
     users, items = ingest.IdDict(), ingest.IdDict()
     u, i, s, ts = ingest.parse_ratings(lines, users, items, default_ts=0)
     uk, ik = users.keys(), items.keys()
@@ -827,9 +824,10 @@ def _known_items_sharded(lines: Sequence[str], ctx) -> Dict[str, set]:
     gu, gi, s, ts = shuffle.route(owner, ctx, gu, gi, s, ts)
     ustr = shuffle.gather_strings(utab, ctx)
     istr = shuffle.gather_strings(itab, ctx)
-    out: Dict[str, set] = {ustr[a]: set() for a in np.unique(gu).tolist()}
+    present = np.unique(gu)
+    user_list = [ustr[a] for a in present.tolist()]
     if len(gu) == 0:
-        return out
+        return user_list, textfmt.RowText(b"", np.zeros(0, dtype=np.int64))
     n_i = int(gi.max()) + 1
     key = gu * n_i + gi
     order = np.lexsort((np.arange(len(key)), ts, key))
@@ -837,9 +835,11 @@ def _known_items_sharded(lines: Sequence[str], ctx) -> Dict[str, set]:
     last = np.r_[key_s[1:] != key_s[:-1], True]
     keep = last & ~np.isnan(s_s)
     kk = key_s[keep]
-    for a, b in zip((kk // n_i).tolist(), (kk % n_i).tolist()):
-        out[ustr[a]].add(istr[b])
-    return out
+    uidx = np.searchsorted(present, kk // n_i)
+    names = ingest.IdDict()
+    names.encode(istr)                  # code j == global item j
+    kt = ingest.known_items_text(names, uidx, kk % n_i, len(present))
+    return user_list, kt
 
 
 def known_items_json(lines: Sequence[str], device=None) -> Dict[str, str]:
