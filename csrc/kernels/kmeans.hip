@@ -906,36 +906,51 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
       if (f == 2) list2[1 + base + (int)__popcll(m2 & ((1ull << lane) - 1ull))] = (int)(r0 + lane);
       n2 += __popcll(m2);
     }
+    // flag-1 points four at a time, one per 16-lane quarter of the wave (each lane sums a
+    // quarter of the dimensions in 4-wide runs, then four xor-shuffles within the quarter):
+    // a window's few flag-1 points no longer run one after another through the whole wave
     unsigned long long m = __ballot(f == 1);
+    const int qr = lane >> 4, ql = lane & 15;
     while (m) {
-      const int j = __builtin_ctzll(m);
-      m &= m - 1;
-      const long long r = r0 + j;
-      const float* xr = X + r * ldx;
-      float xv[8];
+      int js[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) xv[e] = lane + 64 * e < d ? xr[lane + 64 * e] : 0.f;
-      auto dist2 = [&](int c) {
-        const float* cr = C + (long long)c * d;
-        float sc = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float cv = lane + 64 * e < d ? cr[lane + 64 * e] : 0.f;
-          const float a = xv[e] - cv;
-          sc += a * a;
-        }
-        return sc;
-      };
-      const int i1 = assign[r], i2 = idx2[r];
-      const float s1 = wave_sum(dist2(i1)), s2 = wave_sum(dist2(i2));
-      const bool first = s1 < s2 || (s1 == s2 && i1 < i2);
-      const float bd = first ? s1 : s2;
-      const int bi = first ? i1 : i2;
-      if (lane == 0) {
-        assign[r] = bi;
-        mind[r] = bd;
+      for (int t = 0; t < 4; ++t) {
+        js[t] = m ? __builtin_ctzll(m) : -1;
+        if (m) m &= m - 1;
       }
-      ++n1;
+      const int j = js[qr];
+      float s1 = 0.f, s2 = 0.f;
+      int i1 = 0, i2 = 0;
+      const long long r = r0 + (j >= 0 ? j : 0);
+      if (j >= 0) {
+        i1 = assign[r];
+        i2 = idx2[r];
+        const float* xr = X + r * ldx;
+        const float* c1 = C + (long long)i1 * d;
+        const float* c2 = C + (long long)i2 * d;
+        for (int e = 4 * ql; e < d; e += 64) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            if (e + v < d) {
+              const float xv = xr[e + v];
+              const float a = xv - c1[e + v], b = xv - c2[e + v];
+              s1 += a * a;
+              s2 += b * b;
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) {
+        s1 += __shfl_xor(s1, off, 64);
+        s2 += __shfl_xor(s2, off, 64);
+      }
+      if (j >= 0 && ql == 0) {
+        const bool first = s1 < s2 || (s1 == s2 && i1 < i2);
+        assign[r] = first ? i1 : i2;
+        mind[r] = first ? s1 : s2;
+      }
+      n1 += (js[0] >= 0) + (js[1] >= 0) + (js[2] >= 0) + (js[3] >= 0);
     }
   }
   if (stats && lane == 0) {
