@@ -57,6 +57,12 @@ class IdDict:
         return int(self._lib.oryx_dict_get(self._h, b, len(b)))
 
     def keys(self) -> List[str]:
+        """Every key in code order (a copy)."""
+        return list(self.key_list())
+
+    def key_list(self) -> List[str]:
+        """Every key in code order: the dictionary's own cached list (read-only; no copy --
+        per-request lookups of a few codes in a 1M-key dictionary must not copy it)."""
         n = len(self)
         have = len(self._keys_cache)
         if have < n:
@@ -79,7 +85,7 @@ class IdDict:
                 starts = np.r_[0, ends[:-1]].tolist()
                 self._keys_cache.extend(raw[a:b].decode("utf-8")
                                         for a, b in zip(starts, ends.tolist()))
-        return self._keys_cache[:n]
+        return self._keys_cache if len(self._keys_cache) == n else self._keys_cache[:n]
 
 
 def parse_ratings(lines, users: IdDict, items: IdDict, default_ts: int,

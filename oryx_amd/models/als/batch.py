@@ -828,17 +828,16 @@ def _known_items_sharded(lines: Sequence[str], ctx):
     user_list = [ustr[a] for a in present.tolist()]
     if len(gu) == 0:
         return user_list, textfmt.RowText(b"", np.zeros(0, dtype=np.int64))
-    n_i = int(gi.max()) + 1
-    key = gu * n_i + gi
-    order = np.lexsort((np.arange(len(key)), ts, key))
-    key_s, s_s = key[order], s[order]
-    last = np.r_[key_s[1:] != key_s[:-1], True]
-    keep = last & ~np.isnan(s_s)
-    kk = key_s[keep]
-    uidx = np.searchsorted(present, kk // n_i)
+    # the last event of each pair in time order decides (a delete drops it): the explicit
+    # aggregation, sorted by (user, item) -- on the device when there is one
+    if ctx.device.type == "cuda":
+        ku, ki, _ = aggregate_scores_device(gu, gi, s, ts, False, ctx.device)
+    else:
+        ku, ki, _ = aggregate_scores(gu, gi, s, ts, False)
+    uidx = np.searchsorted(present, ku)
     names = ingest.IdDict()
     names.encode(istr)                  # code j == global item j
-    kt = ingest.known_items_text(names, uidx, kk % n_i, len(present))
+    kt = ingest.known_items_text(names, uidx, ki, len(present))
     return user_list, kt
 
 

@@ -346,7 +346,7 @@ class ALSServingModel(ServingModel):
             a = self._known.get(user)
         if a is None or len(a) == 0:
             return set()
-        keys = self._kdict.keys()
+        keys = self._kdict.key_list()
         return {keys[c] for c in a.tolist()}
 
     def add_known_items(self, user: str, items: Iterable[str]) -> None:
@@ -418,7 +418,7 @@ class ALSServingModel(ServingModel):
         if len(items) == 0:
             return {}
         cnt = np.bincount(items)
-        keys = self._kdict.keys()
+        keys = self._kdict.key_list()
         nz = np.flatnonzero(cnt)
         return {keys[c]: int(cnt[c]) for c in nz.tolist()}
 
@@ -547,7 +547,7 @@ class ALSServingModel(ServingModel):
                 del self._known[u]
         recent_items: Set[str] = set()
         self.Y.add_all_recent_to(recent_items)
-        keys = self._kdict.keys()
+        keys = self._kdict.key_list()
         keep = np.fromiter((k in items or k in recent_items for k in keys), dtype=bool,
                            count=len(keys))
         if keep.all():
