@@ -1190,6 +1190,34 @@ long long oryx_parse_up_records(const char* raw, long long used, long long nrec,
   return keep;
 }
 
+// As oryx_parse_up_records over a buffer of log frames (oryx_reader_poll_frames layout: per
+// frame u32 magic, u32 crc, u64 offset, i64 ts, u32 key length (0xFFFFFFFF: none), u32 value
+// length, key, value).
+long long oryx_parse_up_frames(const char* raw, long long used, long long nrec, int k,
+                               long long max_n, unsigned char* kinds, float* vecs,
+                               long long* id_ends, long long* known_cnt,
+                               long long* consumed_bytes) {
+  std::vector<long long> begin, end, after;
+  long long pos = 0;
+  for (long long r = 0; r < nrec && r < max_n; ++r) {
+    if (pos + 32 > used) break;
+    uint32_t kl, vl;
+    std::memcpy(&kl, raw + pos + 24, 4);
+    std::memcpy(&vl, raw + pos + 28, 4);
+    const long long kpos = pos + 32;
+    if (kl != 2 || raw[kpos] != 'U' || raw[kpos + 1] != 'P') break;
+    begin.push_back(kpos + 2);
+    end.push_back(kpos + 2 + vl);
+    pos = kpos + 2 + vl;
+    after.push_back(pos);
+  }
+  const long long n = (long long)begin.size();
+  const long long keep = n ? parse_up_spans(raw, begin.data(), end.data(), n, k, kinds, vecs,
+                                            id_ends, known_cnt, true) : 0;
+  *consumed_bytes = keep ? after[(size_t)keep - 1] : 0;
+  return keep;
+}
+
 // Factor part-file lines ([id,[k floats]] per line, the X/ Y/ text parts written by
 // write_features / the reference's saveFeaturesRDD) -> vecs [n][k] and the id texts (fetched
 // with oryx_up_texts, as after oryx_parse_up_batch).  Lines are split over the native threads.

@@ -763,6 +763,103 @@ long long oryx_log_append_values_gap(void* h, int partition, const char* key, in
   return append_records(t, h, partition, recs, ts_ms, do_fsync, nullptr);
 }
 
+// Bulk poll for consumers that parse records natively (the serving model load): complete
+// frames from the reader's position are read with ONE pread straight into `out`, in the
+// log's own frame layout (u32 magic | u32 crc | u64 offset | i64 ts | u32 key len
+// (0xFFFFFFFF = null) | u32 value len | key | value), and their CRCs are checked on the native
+// threads -- no per-record copy through the read-ahead block.  Never waits.  Returns the
+// number of frames (at most max_records; 0 when none is complete yet), -3 on a corrupt frame
+// that later data follows, or -(bytes needed) - 16 when the next frame alone exceeds out_cap.
+long long oryx_reader_poll_frames(void* rh, char* out, long long out_cap, int max_records,
+                                  long long* out_used) {
+  auto* r = static_cast<Reader*>(rh);
+  const std::string& dir = r->topic->parts[r->part].dir;
+  *out_used = 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (r->fd < 0) reader_seek(r, r->next_offset);
+    if (r->fd < 0) return 0;
+    r->blk_pos = -1;   // the poll read-ahead block is bypassed from here on
+    ssize_t got = pread(r->fd, out, (size_t)out_cap, r->pos);
+    if (got < 0) got = 0;
+    std::vector<size_t> at;
+    size_t p = 0;
+    while ((long long)at.size() < max_records && p + kHeader <= (size_t)got) {
+      const uint8_t* h = reinterpret_cast<const uint8_t*>(out) + p;
+      uint32_t magic, klen, vlen;
+      memcpy(&magic, h, 4); memcpy(&klen, h + 24, 4); memcpy(&vlen, h + 28, 4);
+      if (magic != kMagic) break;
+      const size_t plen = (klen == kNullKey ? 0 : klen) + (size_t)vlen;
+      if (p + kHeader + plen > (size_t)got) {
+        if (at.empty() && (long long)(kHeader + plen) > out_cap)
+          return -(long long)(kHeader + plen) - 16;
+        break;
+      }
+      at.push_back(p);
+      p += kHeader + plen;
+    }
+    const long long n = (long long)at.size();
+    if (n == 0) {
+      if (got > 0) return 0;          // a frame still being written
+      // end of this segment file: move to the next one when the writer has rolled
+      bool rolled = false;
+      for (int64_t b : list_segments(dir)) {
+        if (b > r->seg_base && b <= r->next_offset) {
+          close(r->fd);
+          r->seg_base = b;
+          r->pos = 0;
+          r->fd = open(seg_name(dir, b).c_str(), O_RDONLY);
+          rolled = true;
+          break;
+        }
+      }
+      if (!rolled) return 0;
+      continue;
+    }
+    std::vector<unsigned char> bad((size_t)n, 0);
+    oryx_ff::parallel_ranges(n, 512, [&](long long lo, long long hi, int) {
+      for (long long j = lo; j < hi; ++j) {
+        const uint8_t* f = reinterpret_cast<const uint8_t*>(out) + at[(size_t)j];
+        uint32_t crc, klen, vlen;
+        memcpy(&crc, f + 4, 4); memcpy(&klen, f + 24, 4); memcpy(&vlen, f + 28, 4);
+        const size_t plen = (klen == kNullKey ? 0 : klen) + (size_t)vlen;
+        if (crc32(f + kHeader, plen, crc32(f + 8, 16)) != crc) bad[(size_t)j] = 1;
+      }
+    });
+    long long good = n;
+    for (long long j = 0; j < n; ++j)
+      if (bad[(size_t)j]) { good = j; break; }
+    if (good < n) {
+      if (good == 0) {
+        // a bad frame followed by more data is corruption; at the tail it is a torn or
+        // in-progress write
+        const size_t p0 = at[0];
+        const uint8_t* f = reinterpret_cast<const uint8_t*>(out) + p0;
+        uint32_t klen, vlen;
+        memcpy(&klen, f + 24, 4); memcpy(&vlen, f + 28, 4);
+        const size_t flen = kHeader + (klen == kNullKey ? 0 : klen) + (size_t)vlen;
+        struct stat st;
+        if (fstat(r->fd, &st) == 0 && (long long)st.st_size >= r->pos + (long long)(flen + kHeader)) {
+          fail("corrupt record (crc mismatch) in " + dir + " at offset " +
+               std::to_string(r->next_offset));
+          return -3;
+        }
+        return 0;
+      }
+    }
+    const size_t last = at[(size_t)good - 1];
+    const uint8_t* f = reinterpret_cast<const uint8_t*>(out) + last;
+    uint64_t off;
+    uint32_t klen, vlen;
+    memcpy(&off, f + 8, 8); memcpy(&klen, f + 24, 4); memcpy(&vlen, f + 28, 4);
+    const size_t end = last + kHeader + (klen == kNullKey ? 0 : klen) + (size_t)vlen;
+    r->pos += (int64_t)end;
+    r->next_offset = (int64_t)off + 1;
+    *out_used = (long long)end;
+    return good;
+  }
+  return 0;
+}
+
 // Upper bound on the bytes oryx_reader_read_text delivers for the records from the reader's
 // position up to `end_offset`: the segment bytes from the position to the current end of the
 // log, less 31 per record (each frame has a 32-byte header; the text adds one '\n').  Lets

@@ -213,7 +213,7 @@ def _known_mode(model):
 
 
 def parse_up_records(raw_ptr: int, used: int, nrec: int, k: int, max_n: int,
-                     known_dict: Optional["IdDict"] = None):
+                     known_dict: Optional["IdDict"] = None, frames: bool = False):
     """The leading run of ``UP`` records of a raw log poll buffer (see
     ``oryx_parse_up_records``): returns (count, consumed bytes, kinds, ids, vectors, known) --
     count 0 when the first record is not a parseable ``UP``.  With ``known_dict`` the known
@@ -225,7 +225,9 @@ def parse_up_records(raw_ptr: int, used: int, nrec: int, k: int, max_n: int,
     kcnt = np.empty(m, dtype=np.int64)
     consumed = ctypes.c_longlong(0)
     vp = ctypes.c_void_p
-    got = native.runtime().oryx_parse_up_records(
+    fn = native.runtime().oryx_parse_up_frames if frames else \
+        native.runtime().oryx_parse_up_records
+    got = fn(
         ctypes.c_void_p(raw_ptr), int(used), int(nrec), int(k), int(max_n),
         kinds.ctypes.data_as(vp), vecs.ctypes.data_as(vp), id_ends.ctypes.data_as(vp),
         kcnt.ctypes.data_as(vp), ctypes.byref(consumed))

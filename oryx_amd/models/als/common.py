@@ -202,13 +202,18 @@ class FeatureVectors:
         self._idx_mark_all()
 
     def set_vectors(self, ids: Sequence[str], matrix: np.ndarray) -> None:
-        """Bulk insert/update (model loading): new IDs get one contiguous block of rows."""
+        """Bulk insert/update (model loading): new IDs get one contiguous block of rows; an ID
+        repeated within the batch ends with its last row."""
         matrix = np.asarray(matrix, dtype=np.float32)
         if matrix.ndim != 2 or matrix.shape[1] != self.k or len(ids) != matrix.shape[0]:
             raise ValueError("bad matrix shape %s for %d ids" % (matrix.shape, len(ids)))
         with self._lock.write():
             index = self._index
-            rows = np.fromiter((index.get(i, -1) for i in ids), dtype=np.int64, count=len(ids))
+            if index:
+                rows = np.fromiter((index.get(i, -1) for i in ids), dtype=np.int64,
+                                   count=len(ids))
+            else:
+                rows = np.full(len(ids), -1, dtype=np.int64)
             new_pos = np.nonzero(rows < 0)[0]
             if len(new_pos):
                 new_ids = [ids[j] for j in new_pos.tolist()] if len(new_pos) < len(ids) \

@@ -633,12 +633,11 @@ def _apply_parsed_run(model, kinds, ids, vecs, known, lo: int, hi: int) -> None:
         sel = lo + np.nonzero(kinds[lo:hi] == kind)[0]
         if not len(sel):
             continue
-        # last occurrence of each ID wins
-        last = {}
-        for j in sel.tolist():
-            last[ids[j]] = j
-        rows = np.fromiter(last.values(), dtype=np.int64, count=len(last))
-        getattr(model, setter)([ids[j] for j in rows.tolist()], vecs[rows])
+        # the bulk setters keep the last row of an ID repeated within the batch
+        if len(sel) == hi - lo:
+            getattr(model, setter)(ids[lo:hi], vecs[lo:hi])
+        else:
+            getattr(model, setter)([ids[j] for j in sel.tolist()], vecs[sel])
         if known is None:
             continue
         if kind == 0 and isinstance(known, ingest.KnownCodes):

@@ -93,6 +93,10 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_line_ends", c_ll, [c_vp, c_ll, c_vp, c_ll])
     _sig(lib, "oryx_gather_lines", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_concat_buffers", c_ll, [c_vp, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_reader_poll_frames", c_ll, [c_vp, c_vp, c_ll, ctypes.c_int,
+                                                ctypes.POINTER(c_ll)])
+    _sig(lib, "oryx_parse_up_frames", c_ll, [c_vp, c_ll, c_ll, ctypes.c_int, c_ll, c_vp, c_vp,
+                                             c_vp, c_vp, ctypes.POINTER(c_ll)])
     _sig(lib, "oryx_aggregate_scores", c_ll, [c_vp, c_vp, c_vp, c_vp, c_ll, ctypes.c_int,
                                               c_vp, c_vp, c_vp])
     _sig(lib, "oryx_reader_text_bound", c_ll, [c_vp, c_ll])

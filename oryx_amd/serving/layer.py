@@ -95,14 +95,14 @@ class UpdateIterator:
         readers = self.consumer.readers
         for step in range(len(readers)):
             r = readers[(self._rr + step) % len(readers)]
-            n = r.poll_raw(max_n, 0, min_buffer=64 << 20)
+            n = r.poll_frames(max_n)
             if not n:
                 continue
             self._rr = (self._rr + step + 1) % len(readers)
-            addr, used = r.raw_buffer()
+            addr, used = r.frame_buffer()
             got, consumed, kinds, ids, vecs, known = ingest.parse_up_records(
-                addr, used, n, k, n, known_dict=known_dict)
-            rest = r.decode_raw(consumed, n - got)
+                addr, used, n, k, n, known_dict=known_dict, frames=True)
+            rest = r.decode_frames(consumed, n - got)
             self._pending = [KeyMessage(key, v) for _, _, key, v in rest]
             self._pending.reverse()
             return (kinds, ids, vecs, known) if got else None

@@ -256,6 +256,7 @@ class Topic:
 
 
 _FRAME_HEADER = 32     # u32 magic, u32 crc, u64 offset, i64 ts, u32 key len, u32 value len
+_FRAME = struct.Struct("<IIqqII")
 
 
 class LogCorruptionError(IOError):
@@ -339,6 +340,50 @@ class PartitionReader:
             val = raw[pos:pos + vl].decode("utf-8")
             pos += vl
             out.append((off, ts, key, val))
+        return out
+
+    def poll_frames(self, max_records: int = 1 << 15, min_buffer: int = 64 << 20) -> int:
+        """Complete records from the position read in the log's frame layout into this
+        reader's frame buffer with one read (CRCs checked on the native threads); never
+        waits.  :meth:`frame_buffer` / :meth:`decode_frames` read them."""
+        import numpy as np
+        lib = _lib()
+        buf = getattr(self, "_frames", None)
+        if buf is None or len(buf) < min_buffer:
+            buf = self._frames = np.empty(int(min_buffer), dtype=np.uint8)
+        while True:
+            n = lib.oryx_reader_poll_frames(self._r, ctypes.c_void_p(buf.ctypes.data), len(buf),
+                                            int(max_records), ctypes.byref(self._used))
+            if n == -3:
+                raise LogCorruptionError(lib.oryx_log_last_error().decode())
+            if n < -3:
+                need = -n - 16
+                buf = self._frames = np.empty(max(2 * len(buf), need + 1024), dtype=np.uint8)
+                continue
+            if n < 0:
+                raise IOError(lib.oryx_log_last_error().decode())
+            return n
+
+    def frame_buffer(self) -> Tuple[int, int]:
+        """(address, bytes used) of the last :meth:`poll_frames`."""
+        return self._frames.ctypes.data, self._used.value
+
+    def decode_frames(self, start: int, count: int) -> List[Tuple[int, int, Optional[str], str]]:
+        """``count`` frames of the frame buffer from byte ``start`` as (offset, timestamp_ms,
+        key, value) tuples."""
+        out = []
+        raw = self._frames[start:self._used.value].tobytes() if count else b""
+        pos = 0
+        for _ in range(count):
+            _, _, off, ts, kl, vl = _FRAME.unpack_from(raw, pos)
+            pos += _FRAME_HEADER
+            if kl != 0xFFFFFFFF:
+                key = raw[pos:pos + kl].decode("utf-8")
+                pos += kl
+            else:
+                key = None
+            out.append((off, ts, key, raw[pos:pos + vl].decode("utf-8")))
+            pos += vl
         return out
 
     def read_text_lines(self, end_offset: int):

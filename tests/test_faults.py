@@ -155,6 +155,14 @@ def test_log_corruption_is_detected_not_waited_on(tmp_path):
     with pytest.raises(tlog.LogCorruptionError):
         c.poll(10, 200)
     c.close()
+    # the bulk frame poll (serving model loads) reports the same corruption after the good
+    # frames, and a torn tail (no later frame) as nothing to read yet
+    r = t.reader(0, 0)
+    assert r.poll_frames(10, 1 << 16) == 1
+    assert [v for _, _, _, v in r.decode_frames(0, 1)] == ["first"]
+    with pytest.raises(tlog.LogCorruptionError):
+        r.poll_frames(10, 1 << 16)
+    r.close()
     # a dropped record never reaches the log
     t2 = tlog.Topic(str(tmp_path), "T2", create_partitions=1)
     faults.arm("log.append", "drop")
