@@ -39,6 +39,11 @@ log = logging.getLogger(__name__)
 class UpdateIterator:
     """Blocking iterator of :class:`KeyMessage` over a topic, until closed."""
 
+    # records decoded into Python objects per poll: small, because a manager that can parse a
+    # run of UP rows natively (take_up_block) takes the rest of the run from the log itself
+    # (8192 decoded 2.7 KB rows cost ~0.4 s at the start of every model load)
+    POLL_RECORDS = 256
+
     def __init__(self, consumer: tlog.TopicConsumer, poll_ms: int = 100):
         self.consumer = consumer
         self.poll_ms = poll_ms
@@ -53,7 +58,7 @@ class UpdateIterator:
         while not self._pending:
             if self.closed:
                 raise StopIteration
-            recs = self.consumer.poll(8192, self.poll_ms)
+            recs = self.consumer.poll(self.POLL_RECORDS, self.poll_ms)
             self._pending = [KeyMessage(k, v) for _, _, _, k, v in recs]
             self._pending.reverse()
         return self._pending.pop()
@@ -72,13 +77,13 @@ class UpdateIterator:
                 out.append(self._pending.pop())
             return out
         if not self._pending and not self.closed:
-            recs = self.consumer.poll(8192, 0)
+            recs = self.consumer.poll(self.POLL_RECORDS, 0)
             self._pending = [KeyMessage(k, v) for _, _, _, k, v in recs]
             self._pending.reverse()
         while self._pending and len(out) < max_n and pred(self._pending[-1]):
             out.append(self._pending.pop())
             if not self._pending and len(out) < max_n and not self.closed:
-                recs = self.consumer.poll(8192, 0)
+                recs = self.consumer.poll(self.POLL_RECORDS, 0)
                 self._pending = [KeyMessage(k, v) for _, _, _, k, v in recs]
                 self._pending.reverse()
         return out
