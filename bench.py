@@ -248,7 +248,7 @@ def main(argv=None) -> int:
             "speed_layer_foldin_ms": foldin_ms,
             "speed_layer_phase_ms": speed_phases,
             "speed_layer_path": "ALSSpeedModelManager.build_update_blocks (parse, aggregate, "
-                                "inverses overlapped with the parse, fused HIP fold-in, UP "
+                                "inverses, fused HIP fold-in, UP "
                                 "formatting, assembly) + the UP block's append to the update "
                                 "log (layers/speed.py publish_blocks); end to end, median of "
                                 "12",

@@ -1188,6 +1188,76 @@ __global__ __launch_bounds__(256) void km_silhouette(
 
 }  // namespace
 
+
+// ---- weighted k-means++ over the k-means|| candidates (one draw + one D^2 update per center)
+//
+// km_pp_draw: ONE workgroup: p_i = w_i * d2_i (w alone for the first draw), an fp64 block
+// scan in a fixed order (deterministic, unlike a decoupled look-back scan), and the inverse
+// CDF lookup of uniform u[s]: the first i with cdf_i >= u[s] * total (torch.searchsorted's
+// left side), clamped to n - 1; a zero total takes fallback[s].  Writes chosen[s].
+// km_pp_update: d2_i = min(d2_i, max(|c_i|^2 - 2 c_i . c_j + |c_j|^2, 0)) for j = chosen[s]
+// (d2 initialised when `first`).  Two launches per center instead of a dozen torch ops.
+__global__ __launch_bounds__(1024) void km_pp_draw(const double* __restrict__ w,
+                                                   const double* __restrict__ d2, long long n,
+                                                   const double* __restrict__ u,
+                                                   const long long* __restrict__ fallback,
+                                                   int s, long long* __restrict__ chosen) {
+  __shared__ double part[1024];
+  __shared__ long long found;
+  const int tid = threadIdx.x;
+  const long long per = (n + 1023) / 1024;
+  const long long lo = tid * per, hi = lo + per < n ? lo + per : n;
+  double sum = 0.0;
+  for (long long i = lo; i < hi; ++i) sum += d2 ? w[i] * d2[i] : w[i];
+  part[tid] = sum;
+  if (tid == 0) found = -1;
+  __syncthreads();
+  // inclusive scan of the 1024 partial sums (Hillis-Steele, fixed order)
+  for (int off = 1; off < 1024; off <<= 1) {
+    const double v = tid >= off ? part[tid - off] : 0.0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  const double total = part[1023];
+  if (!(total > 0.0)) {
+    if (tid == 0) chosen[s] = fallback[s];
+    return;
+  }
+  const double target = u[s] * total;
+  const double before = tid ? part[tid - 1] : 0.0;
+  if (lo < hi && part[tid] >= target && (tid == 0 || before < target)) {
+    double c = before;
+    long long j = hi - 1;
+    for (long long i = lo; i < hi; ++i) {
+      c += d2 ? w[i] * d2[i] : w[i];
+      if (c >= target) { j = i; break; }
+    }
+    found = j;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    long long j = found >= 0 ? found : n - 1;
+    chosen[s] = j < n - 1 ? j : n - 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void km_pp_update(const double* __restrict__ c,
+                                                    const double* __restrict__ cn, long long n,
+                                                    int d, const long long* __restrict__ chosen,
+                                                    int s, int first, double* __restrict__ d2) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const long long j = chosen[s];
+  const double* a = c + i * d;
+  const double* b = c + j * d;
+  double dot = 0.0;
+  for (int e = 0; e < d; ++e) dot += a[e] * b[e];
+  double v = cn[i] - 2.0 * dot + cn[j];
+  v = v > 0.0 ? v : 0.0;
+  d2[i] = first ? v : (v < d2[i] ? v : d2[i]);
+}
+
 extern "C" {
 
 // X: bf16 [n][d_pad] (d_pad = 32 * dk), xnorm fp32 [n]; C: bf16 [k_pad][d_pad],
@@ -1510,4 +1580,22 @@ int oryx_kmeans_silhouette(const float* x, const float* xT, const int* cl, const
   return oryx_check_launch();
 }
 
+
+// Weighted k-means++ over n candidates c [n][d] (fp64, norms cn): k draws with uniforms u[k]
+// (fallback[k] for zero-mass draws) into chosen[k]; d2 [n] is workspace.
+int oryx_kmeans_pp(const double* c, const double* cn, const double* w, long long n, int d,
+                   int k, const double* u, const long long* fallback, long long* chosen,
+                   double* d2, void* stream) {
+  if (n <= 0 || k <= 0 || d <= 0) return ORYX_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned ub = (unsigned)((n + 255) / 256);
+  for (int s = 0; s < k; ++s) {
+    hipLaunchKernelGGL(km_pp_draw, dim3(1), dim3(1024), 0, st, w, s ? d2 : nullptr, n, u,
+                       fallback, s, chosen);
+    if (s + 1 < k)
+      hipLaunchKernelGGL(km_pp_update, dim3(ub), dim3(256), 0, st, c, cn, n, d, chosen, s,
+                         s == 0 ? 1 : 0, d2);
+  }
+  return oryx_check_launch();
+}
 }  // extern "C"

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 13
+KERNELS_ABI_VERSION = 14
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -233,6 +233,8 @@ def _load_kernels():
     _sig(lib, "oryx_rdf_best_split", c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_sorted_ws_bytes", c_ll, [c_ll, c_i])
+    _sig(lib, "oryx_kmeans_pp", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp])
     _sig(lib, "oryx_kmeans_accumulate_sorted", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i,
                                                      c_vp, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_accumulate", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_i, c_vp,

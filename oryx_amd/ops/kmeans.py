@@ -296,6 +296,18 @@ def _kmeanspp_weighted(cands: torch.Tensor, weights: torch.Tensor, k: int,
     fallback = torch.randint(0, n, (k,), generator=gen).to(dev)
     cn = (c * c).sum(1)
     chosen = torch.empty(k, dtype=torch.int64, device=dev)
+    if dev.type == "cuda" and native.kernels_available():
+        # two small kernels per center (kmeans.hip km_pp_draw / km_pp_update: a fixed-order
+        # fp64 scan, so the draws are deterministic)
+        c = c.contiguous()
+        d2 = torch.empty(n, dtype=torch.float64, device=dev)
+        lib = native.require_kernels()
+        native.check(lib.oryx_kmeans_pp(c.data_ptr(), cn.contiguous().data_ptr(),
+                                        w.contiguous().data_ptr(), n, c.shape[1], k,
+                                        u.data_ptr(), fallback.data_ptr(), chosen.data_ptr(),
+                                        d2.data_ptr(), native.stream_ptr(dev)),
+                     "oryx_kmeans_pp")
+        return c.index_select(0, chosen).float()
 
     def draw(p: torch.Tensor, s: int) -> torch.Tensor:
         cdf = torch.cumsum(p, 0)

@@ -663,3 +663,20 @@ def test_silhouette_kernel_matches_host(cuda):
     host = ev.silhouette_coefficient(clusters, pts, torch.device("cpu"))
     dev = ev.silhouette_coefficient(clusters, pts, cuda)
     assert dev == pytest.approx(host, rel=1e-5)
+
+
+@pytest.mark.gpu
+def test_kmeanspp_native_draws_match_torch_path(cuda):
+    """The k-means++ kernels (fixed-order fp64 scan + inverse-CDF draw, D^2 update) choose the
+    same candidates as the torch path on the CPU from the same host uniforms."""
+    g = torch.Generator().manual_seed(5)
+    cands = torch.randn(3000, 24, generator=g)
+    w = torch.randint(1, 50, (3000,), generator=g).double()
+    out = []
+    for dev in ("cpu", cuda):
+        gen = torch.Generator().manual_seed(11)
+        out.append(km._kmeanspp_weighted(cands.to(dev), w, 150, gen).cpu())
+    same = (out[0] == out[1]).all(1)
+    # one rounding-level flip would change every later draw; demand a long identical prefix
+    first_diff = int(torch.nonzero(~same)[0]) if not same.all() else len(same)
+    assert first_diff >= 100, first_diff
