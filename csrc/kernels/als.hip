@@ -1770,7 +1770,7 @@ int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const fl
   return oryx_check_launch();
 }
 
-int oryx_kernels_version() { return 14; }
+int oryx_kernels_version() { return 15; }
 
 int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 

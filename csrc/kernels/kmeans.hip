@@ -1378,11 +1378,15 @@ int oryx_kmeans_assign(const void* X, const float* xnorm, const void* C, long lo
 // then decides those exactly from the fp32 rows (Xf [n][ldx], Cf [k][d]), the flag-2 points
 // through km_rescore_full.  Only d_pad 64 / 128 / 256 (the 64-point-per-wave kernel) and
 // k_pad <= 65536.  idx2 / flags: [n] scratch; list2: [n + 1] int32 scratch.
+int oryx_kmeans_rescore_list(const float* Xf, int ldx, int d, const float* Cf, int k,
+                             const int* list2, long long max_rows, int* assign, float* mind,
+                             void* stream);
+
 int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, long long n,
                             int d_pad, int k_pad, const float* cnorm, const float* Xf, int ldx,
                             int d, const float* Cf, int k, float cmax, int* assign, float* mind,
                             int* idx2, unsigned char* flags, unsigned long long* stats,
-                            int* list2, void* stream) {
+                            int* list2, int defer_full, void* stream) {
   if (n <= 0) return ORYX_OK;
   if (n >= 0x7fffffffLL) return ORYX_EINVAL;                   // list2 holds int32 rows
   const int dk = d_pad / 32;
@@ -1432,10 +1436,23 @@ int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, lo
   if (hipMemsetAsync(list2, 0, sizeof(int), s) != hipSuccess) return ORYX_ELAUNCH;
   hipLaunchKernelGGL(km_rescore, dim3((unsigned)blocks), dim3(256), 0, s, Xf, ldx, d, Cf, k, n,
                      assign, idx2, flags, mind, stats, list2);
+  // defer_full: the caller takes the flag-2 list (list2) itself (a GEMM over the listed points
+  // with a certified top-1, the rest through oryx_kmeans_rescore_list)
+  if (defer_full) return oryx_check_launch();
+  return oryx_kmeans_rescore_list(Xf, ldx, d, Cf, k, list2, n, assign, mind, stream);
+}
+
+// Exact fp32 full rescan (km_rescore_full) of the rows in list2 ([0] = count, then rows);
+// max_rows bounds the count (sizes the grid).
+int oryx_kmeans_rescore_list(const float* Xf, int ldx, int d, const float* Cf, int k,
+                             const int* list2, long long max_rows, int* assign, float* mind,
+                             void* stream) {
+  if (max_rows <= 0) return ORYX_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   constexpr int RP = 32;
   const int dp = (d + 3) & ~3;
   const size_t smem = (size_t)RP * dp * 4 + 8 * RP * 4;
-  long long fblocks = (n + RP - 1) / RP;
+  long long fblocks = (max_rows + RP - 1) / RP;
   if (fblocks > 2048) fblocks = 2048;
   static bool full_attr = false;
   if (!full_attr && smem > 65536) {

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 14
+KERNELS_ABI_VERSION = 15
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -197,7 +197,9 @@ def _load_kernels():
     # stats, stream
     _sig(lib, "oryx_kmeans_assign_cert", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_i,
                                                c_i, c_vp, c_i, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                               c_vp, c_vp])
+                                               c_vp, c_i, c_vp])
+    _sig(lib, "oryx_kmeans_rescore_list", c_i, [c_vp, c_i, c_i, c_vp, c_i, c_vp, c_ll, c_vp,
+                                                c_vp, c_vp])
     # x, xT, cl, csize, s, d, partial, stream
     _sig(lib, "oryx_kmeans_silhouette", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_vp, c_vp])
     # X, Y, k, xrow, yrow, vals, xinv, yinv, implicit, n, new_x, new_y, vx, vy, stream

@@ -128,6 +128,55 @@ def _cert_ok(pts: "PointSet", k_pad: int) -> bool:
     return pts.d_pad in (64, 128, 256) and k_pad <= 65536
 
 
+def _rescore_flag2(x: "PointSet", dc, list2: torch.Tensor, out_a: torch.Tensor,
+                   out_d: torch.Tensor) -> None:
+    """The points the certified bf16 scan could not narrow to two candidates (list2: [0] =
+    count, then rows): an fp32 GEMM of their rows against every center gives distances
+    |x|^2 + |c|^2 - 2 x.c; a point whose GEMM best is ahead of its second best by more than
+    twice the GEMM's rounding bound takes it (it is then also the exact fp32 argmin), and only
+    the rest go through the exact per-dimension rescan (km_rescore_full) -- the rescan of all
+    of them cost ~3 ms per Lloyd step at K = 1000, d = 256."""
+    cnt = int(list2[0])
+    if cnt == 0:
+        return
+    dev = x.device
+    lib = native.require_kernels()
+    if torch.backends.cuda.matmul.allow_tf32:
+        # reduced-precision GEMMs void the rounding bound: every listed point is rescanned
+        native.check(lib.oryx_kmeans_rescore_list(
+            x.x.data_ptr(), x.x.stride(0), x.d, dc.cf.data_ptr(), dc.k, list2.data_ptr(), cnt,
+            out_a.data_ptr(), out_d.data_ptr(), native.stream_ptr(dev)),
+            "oryx_kmeans_rescore_list")
+        return
+    rows = list2[1:1 + cnt].long()
+    xf = x.x.index_select(0, rows)
+    cf = dc.cf[:dc.k]
+    xn = (xf * xf).sum(1)
+    cn = (cf * cf).sum(1)
+    d2 = torch.addmm(xn[:, None] + cn[None, :], xf, cf.t(), beta=1.0, alpha=-2.0)
+    top = torch.topk(d2, min(2, dc.k), dim=1, largest=False)
+    # rounding bound of the GEMM distance (and of the exact per-dimension sum), per point:
+    # (d + 2) unit roundoffs of |x|^2 + |c|^2 + 2 |x| |c|, with the largest center norm
+    cmax2 = cn.max()
+    bound = (x.d + 2) * 2.0 ** -23 * (xn + cmax2 + 2.0 * (xn * cmax2).sqrt())
+    if dc.k > 1:
+        ok = (top.values[:, 1] - top.values[:, 0]) > 4.0 * bound
+    else:
+        ok = torch.ones(cnt, dtype=torch.bool, device=dev)
+    sure = rows[ok]
+    out_a[sure] = top.indices[ok, 0].to(out_a.dtype)
+    out_d[sure] = top.values[ok, 0].clamp_min(0.0).to(out_d.dtype)
+    rest = rows[~ok]
+    if rest.numel():
+        lst = torch.empty(rest.numel() + 1, dtype=torch.int32, device=dev)
+        lst[0] = rest.numel()
+        lst[1:] = rest.to(torch.int32)
+        native.check(lib.oryx_kmeans_rescore_list(
+            x.x.data_ptr(), x.x.stride(0), x.d, dc.cf.data_ptr(), dc.k, lst.data_ptr(),
+            rest.numel(), out_a.data_ptr(), out_d.data_ptr(), native.stream_ptr(dev)),
+            "oryx_kmeans_rescore_list")
+
+
 def assign(x, centers: torch.Tensor, exact: bool = False, out=None,
            precision: Optional[str] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """(index [n], squared distance fp32 [n]) of the nearest center for each row.
@@ -162,9 +211,10 @@ def assign(x, centers: torch.Tensor, exact: bool = False, out=None,
                     x.xb.data_ptr(), x.xn.data_ptr(), dc.cb.data_ptr(), n, dc.d_pad, dc.k_pad,
                     dc.cnorm.data_ptr(), x.x.data_ptr(), x.x.stride(0), x.d, dc.cf.data_ptr(),
                     dc.k, dc.cmax, out_a.data_ptr(), out_d.data_ptr(), idx2.data_ptr(),
-                    flags.data_ptr(), st.data_ptr(), list2.data_ptr(),
+                    flags.data_ptr(), st.data_ptr(), list2.data_ptr(), 1,
                     native.stream_ptr(x.device))
                 native.check(rc, "oryx_kmeans_assign_cert")
+                _rescore_flag2(x, dc, list2, out_a, out_d)
                 return out_a, out_d
             else:
                 rc = lib.oryx_kmeans_assign(x.xb.data_ptr(), x.xn.data_ptr(),
