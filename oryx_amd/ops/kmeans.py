@@ -128,6 +128,13 @@ def _cert_ok(pts: "PointSet", k_pad: int) -> bool:
     return pts.d_pad in (64, 128, 256) and k_pad <= 65536
 
 
+# ORYX_KMEANS_GEMM_RESCORE=1: the flag-2 points go through _rescore_flag2 (fp32 GEMM with a
+# certified top-1) instead of the in-kernel full rescan.  Off by default: at K = 1000, d = 256
+# it measured 12.9 ms per Lloyd step against 11.8 (the host sync, row gather, GEMM and top-k
+# cost more than the rescan they replace; r3_bench_kmeans_fp32_gemm_rescore.json).
+_GEMM_RESCORE = os.environ.get("ORYX_KMEANS_GEMM_RESCORE", "0") == "1"
+
+
 def _rescore_flag2(x: "PointSet", dc, list2: torch.Tensor, out_a: torch.Tensor,
                    out_d: torch.Tensor) -> None:
     """The points the certified bf16 scan could not narrow to two candidates (list2: [0] =
@@ -211,10 +218,11 @@ def assign(x, centers: torch.Tensor, exact: bool = False, out=None,
                     x.xb.data_ptr(), x.xn.data_ptr(), dc.cb.data_ptr(), n, dc.d_pad, dc.k_pad,
                     dc.cnorm.data_ptr(), x.x.data_ptr(), x.x.stride(0), x.d, dc.cf.data_ptr(),
                     dc.k, dc.cmax, out_a.data_ptr(), out_d.data_ptr(), idx2.data_ptr(),
-                    flags.data_ptr(), st.data_ptr(), list2.data_ptr(), 1,
+                    flags.data_ptr(), st.data_ptr(), list2.data_ptr(), int(_GEMM_RESCORE),
                     native.stream_ptr(x.device))
                 native.check(rc, "oryx_kmeans_assign_cert")
-                _rescore_flag2(x, dc, list2, out_a, out_d)
+                if _GEMM_RESCORE:
+                    _rescore_flag2(x, dc, list2, out_a, out_d)
                 return out_a, out_d
             else:
                 rc = lib.oryx_kmeans_assign(x.xb.data_ptr(), x.xn.data_ptr(),
