@@ -1242,17 +1242,17 @@ __global__ __launch_bounds__(1024) void km_pp_draw(const double* __restrict__ w,
   }
 }
 
-__global__ __launch_bounds__(256) void km_pp_update(const double* __restrict__ c,
+// ct: the candidates dimension-major ([d][n]), so a wave's 64 candidates read one coalesced
+// 512-byte run per dimension (row-major reads put 64 rows' lines behind every load)
+__global__ __launch_bounds__(256) void km_pp_update(const double* __restrict__ ct,
                                                     const double* __restrict__ cn, long long n,
                                                     int d, const long long* __restrict__ chosen,
                                                     int s, int first, double* __restrict__ d2) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const long long j = chosen[s];
-  const double* a = c + i * d;
-  const double* b = c + j * d;
   double dot = 0.0;
-  for (int e = 0; e < d; ++e) dot += a[e] * b[e];
+  for (int e = 0; e < d; ++e) dot += ct[(long long)e * n + i] * ct[(long long)e * n + j];
   double v = cn[i] - 2.0 * dot + cn[j];
   v = v > 0.0 ? v : 0.0;
   d2[i] = first ? v : (v < d2[i] ? v : d2[i]);
@@ -1598,9 +1598,10 @@ int oryx_kmeans_silhouette(const float* x, const float* xT, const int* cl, const
 }
 
 
-// Weighted k-means++ over n candidates c [n][d] (fp64, norms cn): k draws with uniforms u[k]
+// Weighted k-means++ over n candidates ct [d][n] (fp64, dimension-major; norms cn): k draws
+// with uniforms u[k]
 // (fallback[k] for zero-mass draws) into chosen[k]; d2 [n] is workspace.
-int oryx_kmeans_pp(const double* c, const double* cn, const double* w, long long n, int d,
+int oryx_kmeans_pp(const double* ct, const double* cn, const double* w, long long n, int d,
                    int k, const double* u, const long long* fallback, long long* chosen,
                    double* d2, void* stream) {
   if (n <= 0 || k <= 0 || d <= 0) return ORYX_EINVAL;
@@ -1610,7 +1611,7 @@ int oryx_kmeans_pp(const double* c, const double* cn, const double* w, long long
     hipLaunchKernelGGL(km_pp_draw, dim3(1), dim3(1024), 0, st, w, s ? d2 : nullptr, n, u,
                        fallback, s, chosen);
     if (s + 1 < k)
-      hipLaunchKernelGGL(km_pp_update, dim3(ub), dim3(256), 0, st, c, cn, n, d, chosen, s,
+      hipLaunchKernelGGL(km_pp_update, dim3(ub), dim3(256), 0, st, ct, cn, n, d, chosen, s,
                          s == 0 ? 1 : 0, d2);
   }
   return oryx_check_launch();

@@ -358,9 +358,10 @@ def _kmeanspp_weighted(cands: torch.Tensor, weights: torch.Tensor, k: int,
         # two small kernels per center (kmeans.hip km_pp_draw / km_pp_update: a fixed-order
         # fp64 scan, so the draws are deterministic)
         c = c.contiguous()
+        ct = c.t().contiguous()
         d2 = torch.empty(n, dtype=torch.float64, device=dev)
         lib = native.require_kernels()
-        native.check(lib.oryx_kmeans_pp(c.data_ptr(), cn.contiguous().data_ptr(),
+        native.check(lib.oryx_kmeans_pp(ct.data_ptr(), cn.contiguous().data_ptr(),
                                         w.contiguous().data_ptr(), n, c.shape[1], k,
                                         u.data_ptr(), fallback.data_ptr(), chosen.data_ptr(),
                                         d2.data_ptr(), native.stream_ptr(dev)),
