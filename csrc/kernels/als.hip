@@ -1548,7 +1548,9 @@ __global__ __launch_bounds__(256) void pair_dots(const float* __restrict__ X,
 // als_solve_wave (register column Cholesky), 3 (default) / 4 = variant 2 with the
 // factorisation at raised issue priority (s_setprio 2 / 3: 2-6% faster half-steps than 2)
 static int g_als_variant = 5;
-// 64 < KP <= 128: 0 = als_solve_wide (default), 1 = als_solve_block (LDS Cholesky)
+// 64 < KP <= 128 and the fp32 factor mode: 0 (default) = als_solve_wide (fp32 mode at
+// KP <= 64: als_solve_wave), 1 = als_solve_block (LDS Cholesky, bf16 only), 2 (with variant 5)
+// = als_solve_batch_gl (als_batch.hip: LDS-DMA gather, batched block LDL^T)
 static int g_als_wide_variant = 0;
 
 extern "C" {
@@ -1562,7 +1564,7 @@ int oryx_als_set_variant(int v) {
 int oryx_als_get_variant() { return g_als_variant; }
 
 int oryx_als_set_wide_variant(int v) {
-  if (v < 0 || v > 1) return ORYX_EINVAL;
+  if (v < 0 || v > 2) return ORYX_EINVAL;
   g_als_wide_variant = v;
   return ORYX_OK;
 }
@@ -1628,6 +1630,14 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
       default:
         return ORYX_EINVAL;
     }
+  }
+  if (g_als_variant == 5 && g_als_wide_variant == 2 && (split || kp > 64)) {
+    // two rows per wave, LDS-DMA gather (als_batch.hip): 64 < KP <= 128 and the fp32 mode
+    const int cus = resident_panel_blocks / 2;
+    if (const int rc = oryx_als::batch_gl_launch(p, kp, split != 0, env_blocks ? env_blocks : cus,
+                                                 s))
+      return rc;
+    return ORYX_OK;
   }
   if (g_als_variant == 5 && !split && kp <= 64) {
     // four rows per wave, one wave per SIMD: one resident block per CU
@@ -1770,7 +1780,7 @@ int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const fl
   return oryx_check_launch();
 }
 
-int oryx_kernels_version() { return 15; }
+int oryx_kernels_version() { return 16; }
 
 int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 

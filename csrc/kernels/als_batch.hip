@@ -64,18 +64,257 @@ __host__ __device__ constexpr int tix(int pi, int qi) {
   return pi * M - pi * (pi - 1) / 2 + (qi - pi);
 }
 
+// scratch row stride in floats (ds_read_b128 rows conflict free)
+constexpr int BATCH_DS = 20;
+
 template <int KP, int NM, int D>
 struct BatchCfg {
   static constexpr int M = KP / 16;
   static constexpr int NT = M * (M + 1) / 2;
   static constexpr int IMG = ChunkImage<KP>::BYTES;
-  static constexpr int DS = 20;   // scratch row stride in floats (ds_read_b128 rows conflict free)
+  static constexpr int DS = BATCH_DS;
   static constexpr int SCR = NM * 16 * DS * 4;
   static constexpr int VEC = NM * 16 * 4;
   static constexpr int WAVE_BYTES = NM * IMG + NM * 256 + SCR + VEC;
   static constexpr int YTY_BYTES = NT * 64 * 16;
   static constexpr int BYTES = YTY_BYTES + 4 * WAVE_BYTES;
 };
+
+typedef __attribute__((address_space(3))) float lds_float;
+typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
+
+// Normal equations, batched block LDL^T + forward solve, back substitution of the NM rows one
+// wave holds (lane group g works on row g % NM).  acc: the upper 16x16 tiles of each row's
+// Gramian (YtY included), bpart / cnt: the gather's per-lane partials.  scr / vdis: the wave's
+// LDS scratch (NM*16 rows of DS floats, NM*16 floats).  Out: lane (m, r) holds x_m[16 pp + r]
+// in xs[pp].  hook(integral_constant<0>) runs after the first panel's LDL^T, hook(<1>) after the
+// first (M == 1) or second panel -- the next batch's metadata is fetched there, under the
+// solve.  phase(i) marks the per-phase cycle counters (analysis builds).
+template <int KP, int NM, typename Hook, typename Phase>
+__device__ __forceinline__ void batch_solve(const AlsParams& p, int lane,
+                                            f32x4 (&acc)[NM][(KP / 16) * (KP / 16 + 1) / 2],
+                                            float (&bpart)[NM][KP / 16], const float (&cnt)[NM],
+                                            const int (&slot)[NM], const bool (&valid)[NM],
+                                            lds_float* scr, lds_float* vdis, float (&xs)[KP / 16],
+                                            Hook&& hook, Phase&& phase) {
+  constexpr int M = KP / 16;
+  constexpr int DS = BATCH_DS;
+  const int g = lane >> 4, f = lane & 15;
+  const int mg = g & (NM - 1);
+  // ------------------------------------------------------------ normal equations
+  float cntw[NM];
+  static_for<NM>([&](auto Mc) {
+    constexpr int m = decltype(Mc)::value;
+    cntw[m] = wave_sum(cnt[m]);
+    reduce_bpart<M>(bpart[m]);   // lane (g, f): bpart[m][pi] = b_m[16 pi + f]
+    if (slot[m] >= 0) {
+      // split row: Gramian, b and count were summed by als_partial into ws[slot]
+      const float* src = p.ws + (int64_t)slot[m] * ws_stride(KP);
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+        for (int qi = pi; qi < M; ++qi)
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            acc[m][tix<M>(pi, qi)][v] += src[(16 * pi + 4 * g + v) * KP + 16 * qi + f];
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi) bpart[m][pi] = src[KP * KP + 16 * pi + f];
+      cntw[m] = src[KP * KP + KP];
+    }
+    // lambda n_u on the diagonal (1 on the zero-padded features, so they solve to 0)
+    int rel = f - 4 * g;
+    asm volatile("" : "+v"(rel));
+#pragma unroll
+    for (int pp = 0; pp < M; ++pp) {
+      const float dg = 16 * pp + f < p.k ? p.lambda * cntw[m] : 1.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[m][tix<M>(pp, pp)][v] += rel == v ? dg : 0.f;
+    }
+  });
+  // right-hand sides in group layout: lane (m, r) holds b_m[16 pi + r]
+  float rhs[M];
+#pragma unroll
+  for (int pi = 0; pi < M; ++pi) {
+    float r = bpart[0][pi];
+    static_for<NM - 1>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value + 1;
+      r = mg == m ? bpart[m][pi] : r;
+    });
+    rhs[pi] = r;
+  }
+
+  phase(2);
+  // ------------------------------------------------------------ block LDL^T + forward
+  float zp[M], disv[M];
+  int bad = 0;
+  static_for<M>([&](auto Pc) {
+    constexpr int pp = decltype(Pc)::value;
+    constexpr int td = tix<M>(pp, pp);
+    // diagonal tiles -> group layout: lane (m, r) gets column r of the tile, whose entries
+    // c <= r are the lower-triangle row r (the elimination below reads nothing else)
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+      *reinterpret_cast<lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g) = acc[m][td];
+    wave_sync();
+    float a[16], e[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[4 * q + u] = v[u];
+    }
+    wave_sync();
+    int fr = f;
+    asm volatile("" : "+v"(fr));
+#pragma unroll
+    for (int c = 0; c < 16; ++c) e[c] = c == fr ? 1.f : 0.f;
+    float dself = 1.f;
+    // [A | I] row operations on the lower triangle only: row r -= m_r row j uses the pivot
+    // row's entries a_j[c] (c > j), which by symmetry are a_c[j] -- column j of lane c,
+    // broadcast inside each 16-lane row; the identity half takes lane j's row as it is
+    static_for<16>([&](auto Jc) {
+      constexpr int j = decltype(Jc)::value;
+      float piv = rbc<j>(a[j]);
+      bad |= !(piv > 0.f);
+      piv = piv > 1e-30f ? piv : 1e-30f;
+      const float mr = a[j] * __builtin_amdgcn_rcpf(piv);
+      int rl = f - j;
+      asm volatile("" : "+v"(rl));
+      const float nml = rl > 0 ? -mr : 0.f;   // -L[r][j] (rows r <= j untouched)
+      dself = rl == 0 ? piv : dself;
+      // fused DPP FMAs (dpp_fmac.h); the next pivot column a[j+1] is the first of the group
+      dfa_range<j + 1, 15 - j>(a, a[j], nml);
+      dfb_range<j, 0, j>(nml, e);
+      e[j] = rl > 0 ? -mr : e[j];
+    });
+    phase(3);
+    if constexpr (pp == 0) hook(std::integral_constant<int, 0>{});
+    const float dis = __builtin_amdgcn_rsqf(dself);
+    disv[pp] = dis;
+    // forward: z_p = D^-1/2 Li r_p
+    float z0 = 0.f, z1 = 0.f;
+    dfc_range<0, 16>(z0, z1, rhs[pp], e);
+    const float z = (z0 + z1) * dis;
+    zp[pp] = z;
+    // Li rows and D^-1/2 to LDS; back as Li^T in accumulator layout (lane (g, f): Li[f][4g+v])
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q) =
+          f32x4{e[4 * q], e[4 * q + 1], e[4 * q + 2], e[4 * q + 3]};
+    vdis[mg * 16 + f] = dis;
+    wave_sync();
+    f32x4 Y[NM], d4[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      Y[m] = *reinterpret_cast<const lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g);
+      d4[m] = *reinterpret_cast<const lds_f32x4*>(vdis + m * 16 + 4 * g);
+    }
+    wave_sync();
+    // K_j = D^-1/2 Li U_pj in place of U_pj
+    static_for<M - 1 - pp>([&](auto Jc) {
+      constexpr int j = pp + 1 + decltype(Jc)::value;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        f32x4 K = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          K = __builtin_amdgcn_mfma_f32_16x16x4f32(Y[m][v], acc[m][tix<M>(pp, j)][v], K, 0, 0,
+                                                    0);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) K[v] *= d4[m][v];
+        acc[m][tix<M>(pp, j)] = K;
+      }
+    });
+    // trailing update U_ij -= K_i^T K_j (i <= j), before the rhs work so it overlaps it
+    static_for<M - 1 - pp>([&](auto Ic) {
+      constexpr int i = pp + 1 + decltype(Ic)::value;
+      static_for<M - i>([&](auto Jc) {
+        constexpr int j = i + decltype(Jc)::value;
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            acc[m][tix<M>(i, j)] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                -acc[m][tix<M>(pp, i)][v], acc[m][tix<M>(pp, j)][v], acc[m][tix<M>(i, j)], 0,
+                0, 0);
+      });
+    });
+    // r_i -= K_i^T z_p: column f of K_i to lane (m, f) through LDS, z broadcast by DPP
+    static_for<M - 1 - pp>([&](auto Ic) {
+      constexpr int i = pp + 1 + decltype(Ic)::value;
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+        *reinterpret_cast<lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g) = acc[m][tix<M>(pp, i)];
+      wave_sync();
+      float col[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) col[4 * q + u] = v[u];
+      }
+      wave_sync();
+      float o0 = 0.f, o1 = 0.f;
+      dfc_range<0, 16>(o0, o1, z, col);
+      rhs[i] -= o0 + o1;
+    });
+    // keep Li^T (accumulator layout) for the back substitution in the dead diagonal tile
+#pragma unroll
+    for (int m = 0; m < NM; ++m) acc[m][td] = Y[m];
+    if constexpr (pp == (M > 1 ? 1 : 0)) hook(std::integral_constant<int, 1>{});
+    phase(4);
+  });
+  {
+    const unsigned long long bm = __ballot(bad != 0);
+    if (lane == 0 && p.fail_count) {
+      int nbad = 0;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) nbad += (valid[m] && ((bm >> (16 * m)) & 0xFFFFull)) ? 1 : 0;
+      if (nbad) atomicAdd(p.fail_count, nbad);
+    }
+  }
+
+  // ------------------------------------------------------------ back substitution
+  // row form of an accumulator-layout tile T of every row: lane (m, r) gets T_m[r][0..15]
+  auto rows_of = [&](const f32x4* T, float (&out)[16]) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) scr[(m * 16 + 4 * g + v) * DS + f] = T[m][v];
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) out[4 * q + u] = v[u];
+    }
+    wave_sync();
+  };
+  static_for_desc<M>([&](auto Pc) {
+    constexpr int pp = decltype(Pc)::value;
+    float w = zp[pp];
+    static_for<M - 1 - pp>([&](auto Ic) {
+      constexpr int i = pp + 1 + decltype(Ic)::value;
+      f32x4 T[NM];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) T[m] = acc[m][tix<M>(pp, i)];
+      float row[16];
+      rows_of(T, row);   // lane (m, r): K_i[r][0..15]
+      float o0 = 0.f, o1 = 0.f;
+      dfc_range<0, 16>(o0, o1, xs[i], row);
+      w -= o0 + o1;
+    });
+    const float yv = w * disv[pp];
+    f32x4 T[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) T[m] = acc[m][tix<M>(pp, pp)];
+    float col[16];
+    rows_of(T, col);   // lane (m, a): Li^T[a][c] = Li[c][a]
+    float x0 = 0.f, x1 = 0.f;
+    dfc_range<0, 16>(x0, x1, yv, col);
+    xs[pp] = x0 + x1;
+  });
+}
 
 // D: chunks in flight per row (register ring depth); the wave keeps NM * D gathers in flight.
 // PROF: per-phase shader-clock cycles summed into prof[0..7] (analysis build,
@@ -96,8 +335,6 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
   constexpr int PPR = CI::PPR;
   constexpr int DS = C::DS;
   static_assert(NM == 4 || NM == 2, "lane group g owns row g % NM of the batch");
-  typedef __attribute__((address_space(3))) float lds_float;
-  typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
   __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
 
   const int lane = threadIdx.x & 63;
@@ -376,220 +613,13 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
 
     phase(1);
     stage1(bnext);
-    // ------------------------------------------------------------ normal equations
-    float cntw[NM];
-    static_for<NM>([&](auto Mc) {
-      constexpr int m = decltype(Mc)::value;
-      cntw[m] = wave_sum(cnt[m]);
-      reduce_bpart<M>(bpart[m]);   // lane (g, f): bpart[m][pi] = b_m[16 pi + f]
-      if (slot[m] >= 0) {
-        // split row: Gramian, b and count were summed by als_partial into ws[slot]
-        const float* src = p.ws + (int64_t)slot[m] * ws_stride(KP);
-#pragma unroll
-        for (int pi = 0; pi < M; ++pi)
-#pragma unroll
-          for (int qi = pi; qi < M; ++qi)
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-              acc[m][tix<M>(pi, qi)][v] += src[(16 * pi + 4 * g + v) * KP + 16 * qi + f];
-#pragma unroll
-        for (int pi = 0; pi < M; ++pi) bpart[m][pi] = src[KP * KP + 16 * pi + f];
-        cntw[m] = src[KP * KP + KP];
-      }
-      // lambda n_u on the diagonal (1 on the zero-padded features, so they solve to 0)
-      int rel = f - 4 * g;
-      asm volatile("" : "+v"(rel));
-#pragma unroll
-      for (int pp = 0; pp < M; ++pp) {
-        const float dg = 16 * pp + f < p.k ? p.lambda * cntw[m] : 1.f;
-#pragma unroll
-        for (int v = 0; v < 4; ++v) acc[m][tix<M>(pp, pp)][v] += rel == v ? dg : 0.f;
-      }
-    });
-    // right-hand sides in group layout: lane (m, r) holds b_m[16 pi + r]
-    float rhs[M];
-#pragma unroll
-    for (int pi = 0; pi < M; ++pi) {
-      float r = bpart[0][pi];
-      static_for<NM - 1>([&](auto Mc) {
-        constexpr int m = decltype(Mc)::value + 1;
-        r = mg == m ? bpart[m][pi] : r;
-      });
-      rhs[pi] = r;
-    }
-
-    phase(2);
-    // ------------------------------------------------------------ block LDL^T + forward
-    float zp[M], disv[M];
-    int bad = 0;
-    static_for<M>([&](auto Pc) {
-      constexpr int pp = decltype(Pc)::value;
-      constexpr int td = tix<M>(pp, pp);
-      // diagonal tiles -> group layout: lane (m, r) gets column r of the tile, whose entries
-      // c <= r are the lower-triangle row r (the elimination below reads nothing else)
-#pragma unroll
-      for (int m = 0; m < NM; ++m)
-        *reinterpret_cast<lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g) = acc[m][td];
-      wave_sync();
-      float a[16], e[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) a[4 * q + u] = v[u];
-      }
-      wave_sync();
-      int fr = f;
-      asm volatile("" : "+v"(fr));
-#pragma unroll
-      for (int c = 0; c < 16; ++c) e[c] = c == fr ? 1.f : 0.f;
-      float dself = 1.f;
-      // [A | I] row operations on the lower triangle only: row r -= m_r row j uses the pivot
-      // row's entries a_j[c] (c > j), which by symmetry are a_c[j] -- column j of lane c,
-      // broadcast inside each 16-lane row; the identity half takes lane j's row as it is
-      static_for<16>([&](auto Jc) {
-        constexpr int j = decltype(Jc)::value;
-        float piv = rbc<j>(a[j]);
-        bad |= !(piv > 0.f);
-        piv = piv > 1e-30f ? piv : 1e-30f;
-        const float mr = a[j] * __builtin_amdgcn_rcpf(piv);
-        int rl = f - j;
-        asm volatile("" : "+v"(rl));
-        const float nml = rl > 0 ? -mr : 0.f;   // -L[r][j] (rows r <= j untouched)
-        dself = rl == 0 ? piv : dself;
-        // fused DPP FMAs (dpp_fmac.h); the next pivot column a[j+1] is the first of the group
-        dfa_range<j + 1, 15 - j>(a, a[j], nml);
-        dfb_range<j, 0, j>(nml, e);
-        e[j] = rl > 0 ? -mr : e[j];
-      });
-      phase(3);
-      if constexpr (pp == 0) stage2();
-      const float dis = __builtin_amdgcn_rsqf(dself);
-      disv[pp] = dis;
-      // forward: z_p = D^-1/2 Li r_p
-      float z0 = 0.f, z1 = 0.f;
-      dfc_range<0, 16>(z0, z1, rhs[pp], e);
-      const float z = (z0 + z1) * dis;
-      zp[pp] = z;
-      // Li rows and D^-1/2 to LDS; back as Li^T in accumulator layout (lane (g, f): Li[f][4g+v])
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q) =
-            f32x4{e[4 * q], e[4 * q + 1], e[4 * q + 2], e[4 * q + 3]};
-      vdis[mg * 16 + f] = dis;
-      wave_sync();
-      f32x4 Y[NM], d4[NM];
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        Y[m] = *reinterpret_cast<const lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g);
-        d4[m] = *reinterpret_cast<const lds_f32x4*>(vdis + m * 16 + 4 * g);
-      }
-      wave_sync();
-      // K_j = D^-1/2 Li U_pj in place of U_pj
-      static_for<M - 1 - pp>([&](auto Jc) {
-        constexpr int j = pp + 1 + decltype(Jc)::value;
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-          f32x4 K = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int v = 0; v < 4; ++v)
-            K = __builtin_amdgcn_mfma_f32_16x16x4f32(Y[m][v], acc[m][tix<M>(pp, j)][v], K, 0, 0,
-                                                      0);
-#pragma unroll
-          for (int v = 0; v < 4; ++v) K[v] *= d4[m][v];
-          acc[m][tix<M>(pp, j)] = K;
-        }
-      });
-      // trailing update U_ij -= K_i^T K_j (i <= j), before the rhs work so it overlaps it
-      static_for<M - 1 - pp>([&](auto Ic) {
-        constexpr int i = pp + 1 + decltype(Ic)::value;
-        static_for<M - i>([&](auto Jc) {
-          constexpr int j = i + decltype(Jc)::value;
-#pragma unroll
-          for (int m = 0; m < NM; ++m)
-#pragma unroll
-            for (int v = 0; v < 4; ++v)
-              acc[m][tix<M>(i, j)] = __builtin_amdgcn_mfma_f32_16x16x4f32(
-                  -acc[m][tix<M>(pp, i)][v], acc[m][tix<M>(pp, j)][v], acc[m][tix<M>(i, j)], 0,
-                  0, 0);
-        });
-      });
-      // r_i -= K_i^T z_p: column f of K_i to lane (m, f) through LDS, z broadcast by DPP
-      static_for<M - 1 - pp>([&](auto Ic) {
-        constexpr int i = pp + 1 + decltype(Ic)::value;
-#pragma unroll
-        for (int m = 0; m < NM; ++m)
-          *reinterpret_cast<lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g) = acc[m][tix<M>(pp, i)];
-        wave_sync();
-        float col[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) col[4 * q + u] = v[u];
-        }
-        wave_sync();
-        float o0 = 0.f, o1 = 0.f;
-        dfc_range<0, 16>(o0, o1, z, col);
-        rhs[i] -= o0 + o1;
-      });
-      // keep Li^T (accumulator layout) for the back substitution in the dead diagonal tile
-#pragma unroll
-      for (int m = 0; m < NM; ++m) acc[m][td] = Y[m];
-      if constexpr (pp == (M > 1 ? 1 : 0)) stage3();
-      phase(4);
-    });
-    {
-      const unsigned long long bm = __ballot(bad != 0);
-      if (lane == 0 && p.fail_count) {
-        int nbad = 0;
-#pragma unroll
-        for (int m = 0; m < NM; ++m) nbad += (valid[m] && ((bm >> (16 * m)) & 0xFFFFull)) ? 1 : 0;
-        if (nbad) atomicAdd(p.fail_count, nbad);
-      }
-    }
-
-    // ------------------------------------------------------------ back substitution
     float xs[M];
-    // row form of an accumulator-layout tile T of every row: lane (m, r) gets T_m[r][0..15]
-    auto rows_of = [&](const f32x4* T, float (&out)[16]) {
-#pragma unroll
-      for (int m = 0; m < NM; ++m)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) scr[(m * 16 + 4 * g + v) * DS + f] = T[m][v];
-      wave_sync();
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 v = *reinterpret_cast<const lds_f32x4*>(scr + (mg * 16 + f) * DS + 4 * q);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) out[4 * q + u] = v[u];
-      }
-      wave_sync();
-    };
-    static_for_desc<M>([&](auto Pc) {
-      constexpr int pp = decltype(Pc)::value;
-      float w = zp[pp];
-      static_for<M - 1 - pp>([&](auto Ic) {
-        constexpr int i = pp + 1 + decltype(Ic)::value;
-        f32x4 T[NM];
-#pragma unroll
-        for (int m = 0; m < NM; ++m) T[m] = acc[m][tix<M>(pp, i)];
-        float row[16];
-        rows_of(T, row);   // lane (m, r): K_i[r][0..15]
-        float o0 = 0.f, o1 = 0.f;
-        dfc_range<0, 16>(o0, o1, xs[i], row);
-        w -= o0 + o1;
-      });
-      const float yv = w * disv[pp];
-      f32x4 T[NM];
-#pragma unroll
-      for (int m = 0; m < NM; ++m) T[m] = acc[m][tix<M>(pp, pp)];
-      float col[16];
-      rows_of(T, col);   // lane (m, a): Li^T[a][c] = Li[c][a]
-      float x0 = 0.f, x1 = 0.f;
-      dfc_range<0, 16>(x0, x1, yv, col);
-      xs[pp] = x0 + x1;
-    });
+    batch_solve<KP, NM>(p, lane, acc, bpart, cnt, slot, valid, scr, vdis, xs,
+                        [&](auto Hc) {
+                          if constexpr (decltype(Hc)::value == 0) stage2();
+                          else stage3();
+                        },
+                        phase);
 
     // lane (m, r) holds x_m[16 pp + r]
     int orow = rows[0];
@@ -612,6 +642,437 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
   if constexpr (PROF) {
     if (lane == 0)
       for (int i = 0; i < 7; ++i) atomicAdd(prof + i, ph[i]);
+  }
+}
+
+// ------------------------------------------------------------------ LDS-DMA batched kernel
+//
+// als_solve_batch_gl: the same two-rows-per-wave batched block-LDL^T solve for the kernels whose
+// Gramians do not leave room for a register gather ring: 64 < KP <= 128 (36 accumulator tiles
+// per row at KP = 128, 288 registers for the pair) and the fp32 factor mode (SPLIT: every
+// factor row is bf16 hi + lo, so a chunk is twice the bytes).  Y rows go straight from global
+// memory into the wave's LDS chunk image with global_load_lds_dwordx4 (no VGPR staging, no
+// ds_write pass); the chunk's 32 column ids and 32 values arrive the same way (one
+// global_load_lds_dword: lanes 0-31 ids, 32-63 values) one chunk ahead, so the column ids that
+// address the next gather are read from LDS, and the chunk loop holds no ordinary global load.
+//
+// Per wave: one image slot per row (SLOT bytes) and two metadata slots per row.  Round kk
+// consumes chunk kk of row 0 then of row 1; consuming (m, kk) ends by issuing the gather of
+// (m, kk + 1) into m's slot and the metadata of (m, kk + 2), so each row's gather lands while
+// the other row's chunk is on the MFMAs.  The DMA loads are issued from inline asm, outside the
+// compiler's waitcnt bookkeeping; the kernel waits for them itself: when (m, kk) starts, the
+// only VMEM operations issued after its gather are the other row's G, so vmcnt(G) retires it.
+// The next batch's metadata and first chunks are fetched under the current batch's solve
+// (hooks of batch_solve); the scratch of the solve does not alias the image slots.
+//
+// One wave per SIMD at KP > 64 (the pair's accumulators), two at KP <= 64 (fp32 factor mode).
+template <int KP, bool SPLIT, int NM_>
+struct GlCfg {
+  static constexpr int NM = NM_;
+  static constexpr int M = KP / 16;
+  static constexpr int NT = M * (M + 1) / 2;
+  static constexpr int IMG = ChunkImage<KP>::BYTES;
+  static constexpr int SLOT = IMG * (SPLIT ? 2 : 1);
+  static constexpr int NPL = ChunkImage<KP>::NPL;
+  static constexpr int G = NPL * (SPLIT ? 2 : 1) + 1;   // VMEM operations of one chunk issue
+  static constexpr int META = 256;                      // 32 column ids + 32 values
+  static constexpr int SCR = NM * 16 * BATCH_DS * 4;
+  static constexpr int WAVE_BYTES = NM * SLOT + NM * 2 * META + SCR + NM * 16 * 4;
+  // waves per SIMD: one for a pair of rows at KP > 64, two otherwise
+  static constexpr int WPE = (NM == 2 && KP > 64) ? 1 : 2;
+  static constexpr int BYTES = 4 * WAVE_BYTES;
+};
+
+// one LDS-DMA load: lane l's 16 (4) bytes from src land at LDS byte address lds + 16 l (4 l).
+// M0 carries the wave-uniform LDS base and is restored afterwards (the compiler reserves it).
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+__device__ __forceinline__ void glds4(const void* src, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+// wait until at most N vector-memory operations of this wave are outstanding
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// every LDS read issued so far has returned (before a DMA overwrites what they read)
+__device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// HOLD_HI: the hi fragments of a chunk stay in registers (the lo ones are re-read from the image
+// where they are used); otherwise both are re-read (KP > 64: registers)
+template <int KP, bool SPLIT, int NM_ = 2, bool PROF = false, bool HOLD_HI = (KP <= 64)>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    GlCfg<KP, SPLIT, NM_>::WPE, GlCfg<KP, SPLIT, NM_>::WPE))) void als_solve_batch_gl(AlsParams p,
+                                                                            unsigned long long* prof) {
+  using C = GlCfg<KP, SPLIT, NM_>;
+  using CI = ChunkImage<KP>;
+  constexpr int NM = C::NM;
+  constexpr int M = C::M;
+  constexpr int NT = C::NT;
+  constexpr int NPL = C::NPL;
+  constexpr int PPR = CI::PPR;
+  constexpr int G = C::G;
+  constexpr int YS = SPLIT ? 2 * KP : KP;   // factor row stride in bf16 elements
+  __shared__ __attribute__((aligned(16))) char smem[C::BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, f = lane & 15;
+  char* my = smem + wave * C::WAVE_BYTES;
+  const uint32_t my_lds = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)my);
+  auto slot_ptr = [&](int m) -> char* { return my + m * C::SLOT; };
+  auto slot_lds = [&](int m) -> uint32_t { return my_lds + m * C::SLOT; };
+  auto meta_ptr = [&](int m, int q) -> char* {
+    return my + NM * C::SLOT + (m * 2 + q) * C::META;
+  };
+  auto meta_lds = [&](int m, int q) -> uint32_t {
+    return my_lds + NM * C::SLOT + (m * 2 + q) * C::META;
+  };
+  lds_float* scr = (lds_float*)(my + NM * C::SLOT + NM * 2 * C::META);
+  lds_float* vdis = scr + NM * 16 * BATCH_DS;
+
+  // Lane-derived values are recomputed from an opaque lane id at each use in the chunk loop:
+  // hoisted out of it, they were spilled, and every scratch reload is a VMEM wait that the
+  // compiler counts as vmcnt(0) -- draining the LDS-DMA prefetch of the other row.
+  auto olane = [&]() -> int {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    return ln;
+  };
+  // per-lane image geometry: slot it*64 + lane of a chunk = rating srow(it), piece soff(it)
+  auto srow = [&](int it) -> int {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    return (it * 64 + ln) / PPR;
+  };
+  auto soff = [&](int it) -> int {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int sl = it * 64 + ln, r = sl / PPR, sc = sl % PPR;
+    return ((sc + CI::rot(r)) % PPR) * 8;
+  };
+  const int nb = (p.n_work + NM - 1) / NM;
+  const int total_waves = gridDim.x * 4;
+  // ph[7]: cycles waiting for LDS-DMA gathers, ph[8]: issuing them (both inside phase 1)
+  unsigned long long ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tp = PROF ? __builtin_amdgcn_s_memtime() : 0;
+  auto phase = [&](int ix) {
+    if constexpr (PROF) {
+      const unsigned long long tn = __builtin_amdgcn_s_memtime();
+      ph[ix] += tn - tp;
+      tp = tn;
+    }
+  };
+
+  // ---- next-batch metadata (wave-uniform; scalar loads) and its first chunks (LDS-DMA)
+  int rows_n[NM], slot_n[NM], len_n[NM];
+  int64_t b_n[NM], e_n[NM], beg_n[NM];
+  bool valid_n[NM];
+  auto stage1 = [&](int b) {
+    static_for<NM>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      const int w = b * NM + m;
+      valid_n[m] = w < p.n_work;
+      const int ww = valid_n[m] ? w : p.n_work - 1;   // tail: a real row, solved, not stored
+      rows_n[m] = p.row_ids ? sload(p.row_ids, ww) : ww;
+      slot_n[m] = (valid_n[m] && p.long_slot) ? sload(p.long_slot, ww) : -1;
+    });
+  };
+  // chunk ch's column ids (lanes 0-31) and values (lanes 32-63) of row m into meta slot q;
+  // offsets clamped into the row (a row without ratings reads element 0)
+  auto issue_meta = [&](int m, int64_t beg, int len, int ch, int q) {
+    const int64_t b0 = len > 0 ? beg : 0;
+    const int ln = olane();
+    int o = 32 * ch + (ln & 31);
+    o = o < len ? o : len - 1;
+    o = o < 0 ? 0 : o;
+    // ids and values are both 4-byte arrays: one uniform base each, the lane picks
+    const char* cb = reinterpret_cast<const char*>(p.col_idx + b0);
+    const char* vb = reinterpret_cast<const char*>(p.vals + b0);
+    const uint64_t d = (uint64_t)(vb - cb);
+    glds4(cb + ((uint64_t)((unsigned)o * 4u) + (ln < 32 ? 0ull : d)), meta_lds(m, q));
+  };
+  // chunk gather of row m into its image slot, column ids from meta slot q
+  const char* ybase = reinterpret_cast<const char*>(p.Y);
+  auto issue_y = [&](int m, int q) {
+    const __attribute__((address_space(3))) int* cid =
+        (const __attribute__((address_space(3))) int*)meta_ptr(m, q);
+    int c[NPL];
+#pragma unroll
+    for (int it = 0; it < NPL; ++it) c[it] = cid[srow(it)];
+#pragma unroll
+    for (int it = 0; it < NPL; ++it) {
+      const char* src = ybase + ((size_t)(unsigned)c[it] * (YS * 2) + (unsigned)(soff(it) * 2));
+      glds16(src, slot_lds(m) + it * 1024);
+      if constexpr (SPLIT) glds16(src + KP * 2, slot_lds(m) + C::IMG + it * 1024);
+    }
+  };
+  auto stage2 = [&]() {
+    static_for<NM>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      b_n[m] = sload(p.row_ptr, rows_n[m]);
+      e_n[m] = sload(p.row_ptr, rows_n[m] + 1);
+      beg_n[m] = b_n[m];
+      const int64_t en = (slot_n[m] >= 0 || !valid_n[m]) ? beg_n[m] : e_n[m];
+      len_n[m] = (int)(en - beg_n[m]);
+    });
+    static_for<NM>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      issue_meta(m, beg_n[m], len_n[m], 0, 0);
+      issue_meta(m, beg_n[m], len_n[m], 1, 1);
+    });
+  };
+  auto stage3 = [&]() {
+    vm_wait<0>();   // the metadata above (and anything older) has landed
+    static_for<NM>([&](auto Mc) { issue_y(decltype(Mc)::value, 0); });
+  };
+  if (blockIdx.x * 4 + wave < nb) {
+    stage1(blockIdx.x * 4 + wave);
+    stage2();
+    stage3();
+  }
+
+  const float alpha = p.alpha;
+  const bool implicit = p.implicit != 0;
+  for (int bi = blockIdx.x * 4 + wave; bi < nb; bi += total_waves) {
+    const int bnext = bi + total_waves < nb ? bi + total_waves : bi;
+    int rows[NM], slot[NM], len[NM];
+    bool valid[NM];
+    int nr = 0;
+    static_for<NM>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      rows[m] = rows_n[m];
+      slot[m] = slot_n[m];
+      valid[m] = valid_n[m];
+      len[m] = len_n[m];
+      const int nch = (len[m] + 31) / 32;
+      nr = nch > nr ? nch : nr;
+    });
+    int64_t beg[NM];
+    static_for<NM>([&](auto Mc) { beg[decltype(Mc)::value] = beg_n[decltype(Mc)::value]; });
+
+    phase(0);
+    // ------------------------------------------------------------ gather + MFMA Gramian
+    f32x4 acc[NM][NT];
+    float bpart[NM][M], cnt[NM];
+    // YtY in accumulator order: tile (pi, qi), lane (g, f) -> rows 16pi + 4g + v, column 16qi + f
+    // (one uniform base + a 32-bit lane offset per load: 64-bit per-load addresses hoisted out of
+    // the batch loop were spilled)
+    {
+      int lo = (4 * g * KP + f) * 4;
+      asm volatile("" : "+v"(lo));
+      const char* yb = reinterpret_cast<const char*>(p.YtY);
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+        for (int qi = pi; qi < M; ++qi)
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            acc[0][tix<M>(pi, qi)][v] = *reinterpret_cast<const float*>(
+                yb + (unsigned)(lo + ((16 * pi + v) * KP + 16 * qi) * 4));
+    }
+    static_for<NM>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value;
+      if constexpr (m > 0) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[m][t] = acc[0][t];
+      }
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi) bpart[m][pi] = 0.f;
+      cnt[m] = 0.f;
+    });
+
+    auto consume = [&](auto Mc, int kk) {
+      constexpr int m = decltype(Mc)::value;
+      const char* S = slot_ptr(m);
+      const int q = kk & 1;
+      // this lane's 8 ratings (8g .. 8g+7 of the chunk) -> Gramian / rhs weights
+      const int gl = olane() >> 4;
+      const f32x4 r0 = *(const lds_f32x4*)(meta_ptr(m, q) + 128 + 32 * gl);
+      const f32x4 r1 = *(const lds_f32x4*)(meta_ptr(m, q) + 128 + 32 * gl + 16);
+      // transposed-read byte offsets of this lane (operand pi, half h), made once per chunk from
+      // an opaque lane id: slot row 8g + 4h + q4, piece (2 pi + p4/2 - rot(row)) mod PPR
+      int tra[M][2];
+      {
+        const int ln = olane();
+        const int sb = (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)S;
+        const int q4 = (ln >> 2) & 3, p4 = ln & 3, gg = ln >> 4;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int row = 8 * gg + 4 * h + q4;
+          const int base = sb + row * KP * 2 + (p4 & 1) * 8;
+          const int c = (p4 >> 1) - CI::rot(row) + PPR;
+#pragma unroll
+          for (int pi = 0; pi < M; ++pi) tra[pi][h] = base + ((2 * pi + c) % PPR) * 16;
+        }
+      }
+      auto rd = [&](int off, int pi) -> bf16x8 {
+        typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4*)(uintptr_t)(uint32_t)(tra[pi][0] + off));
+        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+            (lds_bf16x4*)(uintptr_t)(uint32_t)(tra[pi][1] + off));
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      };
+      // each tile row re-reads its fragments at opaque (in-place redefined) addresses: merged
+      // with the previous row's reads of the same bytes, they would all be held in registers
+      auto fresh_addresses = [&]() {
+#pragma unroll
+        for (int pi = 0; pi < M; ++pi) asm volatile("" : "+v"(tra[pi][0]), "+v"(tra[pi][1]));
+      };
+      // Fragments are re-read from the image where they are used (KP > 64: holding them would
+      // spill the pair's accumulators; KP <= 64 holds the hi fragments).  LDS has the room: at
+      // KP = 128 fp32, 144 ds_read_b64_tr_b16 per chunk and row cost 288 LDS-array cycles per
+      // wave against 1728 cycles of MFMAs.
+      constexpr bool HOLD = HOLD_HI;
+      bf16x8 fbh[HOLD ? M : 1];
+      if constexpr (HOLD) {
+#pragma unroll
+        for (int pi = 0; pi < M; ++pi) fbh[pi] = rd(0, pi);
+      }
+      auto fbr = [&](int pi) -> bf16x8 {
+        if constexpr (HOLD) return fbh[pi];
+        else return rd(0, pi);
+      };
+      const int left = len[m] - 32 * kk - 8 * gl;
+      float wa[8], wb[8], cn = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // straight-line selects (a conditional expression here became a divergent branch)
+        const float r = j < 4 ? r0[j] : r1[j - 4];
+        const float lv = __builtin_amdgcn_fmed3f((float)(left - j), 0.f, 1.f);   // 1 iff j < left
+        const float c1 = alpha * fabsf(r);
+        const float pos = r > 0.f ? 1.f : 0.f;
+        const float a_ = implicit ? c1 : 1.f;
+        const float b_ = implicit ? pos * (1.f + c1) : r;
+        wa[j] = a_ * lv;
+        wb[j] = b_ * lv;
+        cn += (implicit ? pos : 1.f) * lv;
+      }
+      cnt[m] += (olane() & 15) == 0 ? cn : 0.f;
+      const f32x2 wap[4] = {f32x2{wa[0], wa[1]}, f32x2{wa[2], wa[3]}, f32x2{wa[4], wa[5]},
+                            f32x2{wa[6], wa[7]}};
+      const f32x2 wbp[4] = {f32x2{wb[0], wb[1]}, f32x2{wb[2], wb[3]}, f32x2{wb[4], wb[5]},
+                            f32x2{wb[6], wb[7]}};
+      typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+#pragma unroll
+      for (int qi = 0; qi < M; ++qi) {
+        // weighted operand of the larger feature index (see als_solve_batch): bf16(c y), and in
+        // the fp32 factor mode y = hi + lo and c y split into bf16 hi + lo
+        if constexpr (!(KP <= 64)) fresh_addresses();
+        const bf16x8 fq = fbr(qi);
+        const i32x4 raw = __builtin_bit_cast(i32x4, fq);
+        i32x4 rawl;
+        if constexpr (SPLIT) rawl = __builtin_bit_cast(i32x4, rd(C::IMG, qi));
+        i32x4 whi, wlo;
+        f32x2 bacc = f32x2{0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const unsigned u = (unsigned)raw[i];
+          f32x2 y = f32x2{__builtin_bit_cast(float, u << 16),
+                          __builtin_bit_cast(float, u & 0xffff0000u)};
+          if constexpr (SPLIT) {
+            const unsigned ul = (unsigned)rawl[i];
+            y += f32x2{__builtin_bit_cast(float, ul << 16),
+                       __builtin_bit_cast(float, ul & 0xffff0000u)};
+          }
+          const f32x2 cy = y * wap[i];
+          bacc = y * wbp[i] + bacc;
+          const bf16x2 h = __builtin_convertvector(cy, bf16x2);
+          whi[i] = __builtin_bit_cast(int, h);
+          if constexpr (SPLIT) {
+            const f32x2 hb = __builtin_convertvector(h, f32x2);
+            wlo[i] = __builtin_bit_cast(int, __builtin_convertvector(cy - hb, bf16x2));
+          }
+        }
+        const bf16x8 fa = __builtin_bit_cast(bf16x8, whi);
+        bpart[m][qi] += bacc[0] + bacc[1];
+#pragma unroll
+        for (int pi = 0; pi <= qi; ++pi) {
+          const bf16x8 fp = pi == qi ? fq : fbr(pi);
+          acc[m][tix<M>(pi, qi)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              fp, fa, acc[m][tix<M>(pi, qi)], 0, 0, 0);
+          if constexpr (SPLIT) {
+            const bf16x8 fal = __builtin_bit_cast(bf16x8, wlo);
+            acc[m][tix<M>(pi, qi)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                pi == qi ? __builtin_bit_cast(bf16x8, rawl) : rd(C::IMG, pi), fa,
+                acc[m][tix<M>(pi, qi)], 0, 0, 0);
+            acc[m][tix<M>(pi, qi)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fp, fal, acc[m][tix<M>(pi, qi)], 0, 0, 0);
+          }
+        }
+      }
+      if (kk + 1 < nr) {
+        // the slot's fragments and meta slot q's values have been read: overwrite them with
+        // chunk kk + 1 (ids from meta slot q ^ 1) and the metadata of chunk kk + 2
+        phase(1);
+        lds_drain();
+        issue_y(m, q ^ 1);
+        issue_meta(m, beg[m], len[m], kk + 2, q);
+        phase(8);
+      }
+    };
+    for (int kk = 0; kk < nr; ++kk) {
+      phase(1);
+      if (kk == 0 || NM == 1)
+        vm_wait<0>();
+      else
+        vm_wait<G>();
+      phase(7);
+      consume(std::integral_constant<int, 0>{}, kk);
+      if constexpr (NM == 2) {
+        phase(1);
+        if (kk + 1 < nr)
+          vm_wait<G>();
+        else
+          vm_wait<0>();
+        phase(7);
+        consume(std::integral_constant<int, 1>{}, kk);
+      }
+    }
+
+    phase(1);
+    stage1(bnext);
+    float xs[M];
+    batch_solve<KP, NM>(p, lane, acc, bpart, cnt, slot, valid, scr, vdis, xs,
+                        [&](auto Hc) {
+                          if constexpr (decltype(Hc)::value == 0) stage2();
+                          else stage3();
+                        },
+                        phase);
+
+    // lane (m, r) holds x_m[16 pp + r] (the other groups duplicate rows 0 .. NM-1)
+    const int orow = (NM == 2 && (g & 1)) ? rows[NM - 1] : rows[0];
+    const bool ok = (NM == 2 && (g & 1)) ? valid[NM - 1] : valid[0];
+    if (ok && g < NM) {
+#pragma unroll
+      for (int pp = 0; pp < M; ++pp) {
+        p.X[(int64_t)orow * KP + 16 * pp + f] = xs[pp];
+        if (p.Xb) store_xb<SPLIT, KP>(p.Xb, orow, 16 * pp + f, xs[pp]);
+      }
+    }
+    phase(5);
+    if constexpr (PROF) ph[6] += 1;
+  }
+  // no DMA into this workgroup's LDS may be in flight when the wave retires
+  vm_wait<0>();
+  if constexpr (PROF) {
+    if (lane == 0)
+      for (int i = 0; i < 9; ++i) atomicAdd(prof + i, ph[i]);
   }
 }
 
@@ -657,6 +1118,78 @@ int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s
     BATCH_CASE(48)
     BATCH_CASE(64)
 #undef BATCH_CASE
+    default:
+      return ORYX_EINVAL;
+  }
+  return oryx_check_launch();
+}
+
+// rows per wave of the rank-128 LDS-DMA kernel (ORYX_ALS_GL_NM: 2 = a pair at one wave per
+// SIMD, 1 = one row at two waves per SIMD); other KP always pair their rows
+static int gl_rows_per_wave() {
+  static const int v = [] {
+    const char* e = getenv("ORYX_ALS_GL_NM");
+    return e && atoi(e) == 1 ? 1 : 2;
+  }();
+  return v;
+}
+
+// ORYX_ALS_GL_HOLD=1: the rank-128 LDS-DMA kernel keeps the hi fragments in registers
+static bool gl_hold_hi() {
+  static const bool v = [] {
+    const char* e = getenv("ORYX_ALS_GL_HOLD");
+    return e && atoi(e) == 1;
+  }();
+  return v;
+}
+
+int batch_gl_launch(const AlsParams& p, int kp, bool split, int cus, hipStream_t s) {
+  // one resident generation: WPE blocks of 4 waves per CU, NM rows per wave
+  const int nm = kp == 128 ? gl_rows_per_wave() : 2;
+  const int nb = (p.n_work + nm - 1) / nm;
+  const int wpe = (nm == 2 && kp > 64) ? 1 : 2;
+  int blocks = (nb + 3) / 4;
+  if (blocks > cus * wpe) blocks = cus * wpe;
+  if (blocks < 1) blocks = 1;
+  if (kp == 128) {
+#define GL128(SP, NMV, PR)                                                                    \
+  do {                                                                                        \
+    if (gl_hold_hi())                                                                         \
+      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, PR, true>), dim3(blocks), dim3(256), \
+                         0, s, p, PR ? g_batch_prof : nullptr);                               \
+    else                                                                                      \
+      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, PR, false>), dim3(blocks),         \
+                         dim3(256), 0, s, p, PR ? g_batch_prof : nullptr);                    \
+  } while (0)
+    const bool pr = g_batch_prof != nullptr;
+    if (nm == 2) {
+      if (split) { if (pr) GL128(true, 2, true); else GL128(true, 2, false); }
+      else { if (pr) GL128(false, 2, true); else GL128(false, 2, false); }
+    } else {
+      if (split) { if (pr) GL128(true, 1, true); else GL128(true, 1, false); }
+      else { if (pr) GL128(false, 1, true); else GL128(false, 1, false); }
+    }
+#undef GL128
+    return oryx_check_launch();
+  }
+  switch (kp) {
+#define GL_CASE(KPV)                                                                          \
+  case KPV:                                                                                   \
+    if (split)                                                                                \
+      hipLaunchKernelGGL((als_solve_batch_gl<KPV, true>), dim3(blocks), dim3(256), 0, s, p,   \
+                         nullptr);                                                           \
+    else                                                                                      \
+      hipLaunchKernelGGL((als_solve_batch_gl<KPV, false>), dim3(blocks), dim3(256), 0, s, p,  \
+                         nullptr);                                                           \
+    break;
+    GL_CASE(16)
+    GL_CASE(32)
+    GL_CASE(48)
+    GL_CASE(64)
+    GL_CASE(80)
+    GL_CASE(96)
+    GL_CASE(112)
+#undef GL_CASE
     default:
       return ORYX_EINVAL;
   }

@@ -306,6 +306,19 @@ long long oryx_dict_encode(void* dh, const char* buf, long long buf_len, int n, 
   return n;
 }
 
+// Inserts every key of src (in src's code order) into dst; map_out[c] = dst code of src key c.
+// Merging per-segment dictionaries in segment order reproduces the codes a single parse of the
+// concatenated segments assigns (first appearance order).  Returns src's size.
+long long oryx_dict_merge(void* dst_h, void* src_h, long long* map_out) {
+  Dict* d = static_cast<Dict*>(dst_h);
+  Dict* s = static_cast<Dict*>(src_h);
+  if (d == s) return -1;
+  std::scoped_lock g(d->mu, s->mu);
+  long long c = 0;
+  for (const std::string& k : s->keys) map_out[c++] = d->encode(std::string_view(k));
+  return c;
+}
+
 long long oryx_dict_get(void* dh, const char* s, long long len) {
   Dict* d = static_cast<Dict*>(dh);
   std::lock_guard<std::mutex> g(d->mu);

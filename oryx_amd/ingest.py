@@ -52,6 +52,14 @@ class IdDict:
                                    out.ctypes.data_as(ctypes.c_void_p))
         return out
 
+    def merge_from(self, other: "IdDict") -> np.ndarray:
+        """Insert ``other``'s keys (in its code order); returns the codes they have here."""
+        out = np.empty(len(other), dtype=np.int64)
+        n = self._lib.oryx_dict_merge(self._h, other._h, out.ctypes.data_as(ctypes.c_void_p))
+        if n != len(out):
+            raise ValueError("dictionary merge failed")
+        return out
+
     def get(self, key: str) -> int:
         b = key.encode("utf-8")
         return int(self._lib.oryx_dict_get(self._h, b, len(b)))

@@ -118,9 +118,12 @@ def read_past_data(data_dir: str, rank: int = 0, world: int = 1) -> Dataset:
         if j % world != rank:
             continue
         if path.endswith(".txt"):
-            # the file's bytes are the message buffer (no per-line strings)
+            # the file's bytes are the message buffer (no per-line strings), keyed by the
+            # file's identity so apps can reuse their parse of it (models/als/history.py)
+            st = os.stat(path)
             with open(path, "rb") as f:
-                texts.append(TextLines.from_bytes(f.read()))
+                texts.append(TextLines.from_bytes(f.read()).with_key(
+                    ("part", os.path.abspath(path), st.st_size, st.st_mtime_ns)))
             continue
         with open(path, "r", encoding="utf-8") as f:
             for line in f:

@@ -51,6 +51,8 @@ from ...utils import config as cfg, ioutils, pmml as pmmlu, rng, text
 from . import evaluation
 from .trainer import ALSTrainer
 
+from .history import RatingsHistory
+
 __all__ = ["ALSUpdate", "aggregate_scores", "decay_rating", "parse_ratings"]
 
 log = logging.getLogger(__name__)
@@ -183,18 +185,21 @@ _NO_TS = -(1 << 62)     # parse marker of a line without a timestamp
 
 def parse_ratings(lines: Sequence[str], users: ingest.IdDict, items: ingest.IdDict,
                   decay_factor: float = 1.0, zero_threshold: float = 0.0,
-                  now_ms: Optional[int] = None, raw_out: Optional[list] = None):
+                  now_ms: Optional[int] = None, raw_out: Optional[list] = None,
+                  history: Optional[RatingsHistory] = None):
     """Parse + decay + zero-threshold.  ``raw_out`` (a list) receives the undecayed parse
     with lines lacking a timestamp at 0 -- what :func:`known_items_json_parsed` needs -- so
-    the publish step can skip a second parse of the same data."""
+    the publish step can skip a second parse of the same data.  ``history``: reuse the parse
+    of past part files seen in earlier generations (:mod:`.history`; same results)."""
     now = int(time.time() * 1000) if now_ms is None else now_ms
+    parse = history.parse_ratings if history is not None else ingest.parse_ratings
     if raw_out is not None:
-        u, i, s, ts0 = ingest.parse_ratings(lines, users, items, default_ts=_NO_TS)
+        u, i, s, ts0 = parse(lines, users, items, default_ts=_NO_TS)
         missing = ts0 == _NO_TS
         raw_out.extend([u, i, s, np.where(missing, 0, ts0)])
         ts = np.where(missing, now, ts0)
     else:
-        u, i, s, ts = ingest.parse_ratings(lines, users, items, default_ts=now)
+        u, i, s, ts = parse(lines, users, items, default_ts=now)
     if decay_factor < 1.0:
         days = np.maximum(0, now - ts) / 86400000.0
         s = np.where(ts >= now, s, s * np.power(decay_factor, days))
@@ -335,11 +340,24 @@ class ALSUpdate(MLUpdate):
         # the build's undecayed parse of the complete data set, reused by the publish step
         self._raw_parse: Optional[dict] = None
         self._timings: Dict[str, dict] = {}
+        # resident parse of past part files across generations (oryx.als.resident-history,
+        # default on; models/als/history.py)
+        rh = cfg.get_optional_bool(config, "oryx.als.resident-history")
+        self.resident_history = True if rh is None else bool(rh)
+        self.history: Optional[RatingsHistory] = None
         # cumulative seconds per phase of build / publish (bench_batch.py reads them)
         self.phase_seconds: Dict[str, float] = {}
 
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
+
+    def _history_for(self, device) -> Optional[RatingsHistory]:
+        if not self.resident_history:
+            return None
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        if self.history is None or self.history.device != dev:
+            self.history = RatingsHistory(dev)
+        return self.history
 
     def _raw_parse_slot(self, lines, users, items) -> Optional[list]:
         """A list for parse_ratings' raw output when the training lines are the complete data
@@ -386,7 +404,8 @@ class ALSUpdate(MLUpdate):
         users, items = ingest.IdDict(), ingest.IdDict()
         u, i, s, ts = parse_ratings(train_data, users, items, self.decay_factor,
                                     self.decay_zero_threshold, raw_out=self._raw_parse_slot(
-                                        train_data, users, items))
+                                        train_data, users, items),
+                                    history=self._history_for(self._ctx(context).device))
         ph["parse"] = ph.get("parse", 0.0) + time.perf_counter() - tp
         tp = time.perf_counter()
         dev = self._ctx(context).device
@@ -753,8 +772,9 @@ class ALSUpdate(MLUpdate):
         dev = self.dist_ctx.device if self.dist_ctx is not None else None
         if parsed is None:
             users, items = ingest.IdDict(), ingest.IdDict()
-            parsed = (users, items) + tuple(
-                ingest.parse_ratings(all_data, users, items, default_ts=0))
+            hist = self._history_for(dev) if dev is not None else self.history
+            parse = hist.parse_ratings if hist is not None else ingest.parse_ratings
+            parsed = (users, items) + tuple(parse(all_data, users, items, default_ts=0))
         users = parsed[0]
         known, present = known_items_spans(*parsed, device=dev)
         if known is None:

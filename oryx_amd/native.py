@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 15
+KERNELS_ABI_VERSION = 16
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -89,6 +89,7 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_dict_clear", None, [c_vp])
     _sig(lib, "oryx_dict_encode", c_ll, [c_vp, c_cp, c_ll, c_i, c_vp])
     _sig(lib, "oryx_dict_get", c_ll, [c_vp, c_cp, c_ll])
+    _sig(lib, "oryx_dict_merge", c_ll, [c_vp, c_vp, c_vp])
     _sig(lib, "oryx_dict_key", c_ll, [c_vp, c_ll, c_vp, c_ll])
     _sig(lib, "oryx_line_ends", c_ll, [c_vp, c_ll, c_vp, c_ll])
     _sig(lib, "oryx_gather_lines", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
@@ -176,7 +177,8 @@ def _load_kernels():
     _sig(lib, "oryx_als_get_variant", c_i, [])
     _sig(lib, "oryx_als_batch_profile", c_i, [c_vp])
     lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "5")))
-    # ORYX_ALS_WIDE_VARIANT: 64 < k <= 128 solve (0 = als_solve_wide, 1 = als_solve_block)
+    # ORYX_ALS_WIDE_VARIANT: 64 < k <= 128 and fp32-mode solve (2 = als_solve_batch_gl,
+    # 0 = als_solve_wide / als_solve_wave, 1 = als_solve_block)
     _sig(lib, "oryx_als_set_wide_variant", c_i, [c_i])
     lib.oryx_als_set_wide_variant(int(os.environ.get("ORYX_ALS_WIDE_VARIANT", "0")))
     # ..., n_long, ws, split (fp32 factors as bf16 hi|lo rows of 2*kp), stream

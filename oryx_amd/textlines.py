@@ -41,7 +41,7 @@ class TextLines(collections.abc.Sequence):
     natively on first indexed access.
     """
 
-    __slots__ = ("buf", "_n", "_ends", "_strs")
+    __slots__ = ("buf", "_n", "_ends", "_strs", "segments")
 
     def __init__(self, buf, n: Optional[int] = None, ends: Optional[np.ndarray] = None):
         if isinstance(buf, memoryview):
@@ -52,6 +52,19 @@ class TextLines(collections.abc.Sequence):
         if n is None:
             n = len(self.ends()) if len(buf) else 0
         self._n = int(n)
+        # provenance of consecutive byte ranges: [(key, n_lines, n_bytes)], key None for data
+        # without a stable identity; a keyed range is the content of e.g. one past part file
+        # (``layers.batch.read_past_data``), so a parse of it can be reused across generations
+        # (``models.als.history``).  None: one unkeyed range.
+        self.segments: Optional[List[tuple]] = None
+
+    def with_key(self, key) -> "TextLines":
+        """Mark the whole buffer as one keyed segment (returns self)."""
+        self.segments = [(key, self._n, len(self.buf))]
+        return self
+
+    def segment_list(self) -> List[tuple]:
+        return self.segments if self.segments is not None else [(None, self._n, len(self.buf))]
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -188,7 +201,10 @@ def concat_lines(parts: Sequence[Union[TextLines, Sequence[str], None]]):
         # threaded native copy (hundreds of MB per drain)
         native.runtime().oryx_concat_buffers(ptrs.ctypes.data, lens.ctypes.data, len(bufs),
                                              out.ctypes.data)
-        return TextLines(out, sum(len(p) for p in parts))
+        res = TextLines(out, sum(len(p) for p in parts))
+        if any(p.segments is not None for p in parts):
+            res.segments = [seg for p in parts for seg in p.segment_list()]
+        return res
     out: List[str] = []
     for p in parts:
         out.extend(p)

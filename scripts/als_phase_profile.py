@@ -14,8 +14,12 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-BATCH_PHASES = ["batch setup", "gather+mfma (4 rows)", "normal equations", "LDL^T 16x16 blocks",
-                "K + trailing MFMA + rhs", "back substitution + store"]
+BATCH_PHASES = ["batch setup", "gather+mfma (all rows of the batch)", "normal equations",
+                "LDL^T 16x16 blocks", "K + trailing MFMA + rhs", "back substitution + store"]
+# ORYX_PROF_K=128 [ORYX_PROF_PRECISION=fp32]: the rank-128 LDS-DMA batched kernel
+# (als_solve_batch_gl<128, split, PROF>) instead of the rank-64 register kernel
+K = int(os.environ.get("ORYX_PROF_K", "64"))
+PRECISION = os.environ.get("ORYX_PROF_PRECISION", "bf16")
 if os.environ.get("ORYX_ALS_VARIANT", "3") == "1":   # als_solve_wave (register Cholesky)
     PHASES = ["gather+mfma", "scatter/ws", "load A+YtY", "cholesky", "forward", "back+store"]
 else:                                               # als_solve_panel (default)
@@ -33,7 +37,7 @@ def main():
     dev = torch.device("cuda", 0)
     ctx = dist.DistContext(device=dev)
     users, items, strength = bench._gen_ratings(162_541, 59_047, 25_000_000, 0, 1234, dev)
-    tr = ALSTrainer(64, lam=0.001, alpha=1.0, implicit=True, ctx=ctx, seed=1)
+    tr = ALSTrainer(K, lam=0.001, alpha=1.0, implicit=True, ctx=ctx, seed=1, precision=PRECISION)
     tr.prepare(users, items, strength, 162_541, 59_047)
     tr.init_factors()
     lib = native.require_kernels()
@@ -45,11 +49,12 @@ def main():
                 ("items", tr.csr_i, tr.Xb, tr.X, tr.Y, tr.Yb_local),
                 ("users", tr.csr_u, tr.Yb, tr.Y, tr.X, tr.Xb_local)):
             yty = als_ops.gramian(src_f)
-            prof = torch.zeros(8, dtype=torch.int64, device=dev)
+            prof = torch.zeros(10, dtype=torch.int64, device=dev)
             lib.oryx_als_batch_profile(prof.data_ptr())
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            als_ops.solve_rows(csr, src_b, yty, dst, dstb, 64, 0.001, 1.0, True)
+            als_ops.solve_rows(csr, src_b, yty, dst, dstb, K, 0.001, 1.0, True,
+                               split=tr.split)
             torch.cuda.synchronize()
             ms = (time.perf_counter() - t0) * 1e3
             lib.oryx_als_batch_profile(None)
@@ -58,6 +63,10 @@ def main():
             out[name] = {"rows": int(csr.order.numel()), "batches": p[6], "nnz": csr.nnz,
                          "ms": ms, "cycles_per_batch": {k: p[i] / nb
                                                         for i, k in enumerate(BATCH_PHASES)}}
+            if K > 64:   # the LDS-DMA kernel also splits its gather phase
+                out[name]["gather_dma_wait_cycles_per_batch"] = p[7] / nb
+                out[name]["gather_dma_issue_cycles_per_batch"] = p[8] / nb
+        out["k"], out["precision"] = K, PRECISION
         print(json.dumps(out, indent=1))
         return
     for name, csr, src_b, src_f, dst in (("items", tr.csr_i, tr.Xb, tr.X, tr.Y),

@@ -1,0 +1,130 @@
+"""Resident parsed history (models/als/history.py): the cached per-part-file parse gives the
+same codes and columns as one parse of the concatenated text, reuses keyed segments across
+generations and drops aged-out ones."""
+
+import os
+
+import numpy as np
+import pytest
+
+from oryx_amd import ingest
+from oryx_amd.layers.batch import read_past_data
+from oryx_amd.models.als import batch as als_batch
+from oryx_amd.models.als.history import RatingsHistory
+from oryx_amd.textlines import TextLines, concat_lines
+
+
+def _lines(gen, n, users, items, with_ts=True, deletes=False):
+    out = []
+    for j in range(n):
+        u = "u%d" % gen.integers(users) if gen.random() < 0.5 else str(gen.integers(users))
+        i = "i%d" % gen.integers(items)
+        if deletes and gen.random() < 0.05:
+            v = ""
+        else:
+            v = "%.3f" % gen.uniform(-1, 5)
+        if with_ts and gen.random() < 0.8:
+            out.append("%s,%s,%s,%d" % (u, i, v, 1_600_000_000_000 + int(gen.integers(10**9))))
+        else:
+            out.append("%s,%s,%s" % (u, i, v))
+    return out
+
+
+def _write_parts(root, gen, n_parts, per_part):
+    paths = []
+    for p in range(n_parts):
+        d = os.path.join(root, "oryx-%d.data" % (1000 + p))
+        os.makedirs(d)
+        path = os.path.join(d, "part-00000.txt")
+        with open(path, "w") as f:
+            f.write("\n".join(_lines(gen, per_part, 300, 200, deletes=True)) + "\n")
+        paths.append(path)
+    return paths
+
+
+def _same(a, b):
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(np.asarray(x), np.asarray(y))
+
+
+def test_history_parse_matches_full_parse_cpu(tmp_path):
+    gen = np.random.default_rng(5)
+    _write_parts(str(tmp_path), gen, 4, 700)
+    past = read_past_data(str(tmp_path)).values()
+    assert isinstance(past, TextLines) and len(past.segments) == 4
+    new = TextLines.from_strings(_lines(gen, 500, 400, 250))
+    data = concat_lines([new, past])
+    assert [k is None for k, _, _ in data.segments] == [True, False, False, False, False]
+
+    h = RatingsHistory()
+    for default_ts in (0, 123, als_batch._NO_TS):
+        u1, i1 = ingest.IdDict(), ingest.IdDict()
+        ref = ingest.parse_ratings(data, u1, i1, default_ts=default_ts)
+        u2, i2 = ingest.IdDict(), ingest.IdDict()
+        got = h.parse_ratings(data, u2, i2, default_ts=default_ts)
+        _same(ref[:2], got[:2])
+        np.testing.assert_array_equal(np.isnan(ref[2]), np.isnan(got[2]))
+        np.testing.assert_array_equal(np.nan_to_num(ref[2]), np.nan_to_num(got[2]))
+        _same(ref[3:], got[3:])
+        assert u1.keys() == u2.keys() and i1.keys() == i2.keys()
+    # the four part files were parsed once, then reused; the unkeyed new data every time
+    assert h.stats["misses"] == 4 + 3 and h.stats["hits"] == 2 * 4
+    assert len(h) == 4
+
+
+def test_history_evicts_aged_out_parts_cpu(tmp_path):
+    gen = np.random.default_rng(6)
+    paths = _write_parts(str(tmp_path), gen, 3, 300)
+    h = RatingsHistory()
+    h.parse_ratings(read_past_data(str(tmp_path)).values(), ingest.IdDict(), ingest.IdDict(), 0)
+    assert len(h) == 3
+    os.remove(paths[0])
+    os.rmdir(os.path.dirname(paths[0]))
+    # an unkeyed parse (e.g. the evaluation's test data) evicts nothing
+    h.parse_ratings(TextLines.from_strings(_lines(gen, 10, 5, 5)), ingest.IdDict(),
+                    ingest.IdDict(), 0)
+    assert len(h) == 3
+    h.parse_ratings(read_past_data(str(tmp_path)).values(), ingest.IdDict(), ingest.IdDict(), 0)
+    assert len(h) == 2 and h.stats["misses"] == 3
+    # a rewritten part file (new size / mtime) is parsed again
+    with open(paths[1], "a") as f:
+        f.write("u1,i1,1.0\n")
+    h.parse_ratings(read_past_data(str(tmp_path)).values(), ingest.IdDict(), ingest.IdDict(), 0)
+    assert h.stats["misses"] == 4
+
+
+def test_als_parse_ratings_with_history_decay_cpu(tmp_path):
+    gen = np.random.default_rng(7)
+    _write_parts(str(tmp_path), gen, 2, 400)
+    data = concat_lines([TextLines.from_strings(_lines(gen, 200, 100, 100)),
+                         read_past_data(str(tmp_path)).values()])
+    h = RatingsHistory()
+    now = 1_600_000_000_000 + 2 * 10**9
+    for _ in range(2):
+        raw_a, raw_b = [], []
+        a = als_batch.parse_ratings(data, ingest.IdDict(), ingest.IdDict(), 0.9, 0.01,
+                                    now_ms=now, raw_out=raw_a)
+        b = als_batch.parse_ratings(data, ingest.IdDict(), ingest.IdDict(), 0.9, 0.01,
+                                    now_ms=now, raw_out=raw_b, history=h)
+        for x, y in zip(list(a) + raw_a, list(b) + raw_b):
+            np.testing.assert_array_equal(np.nan_to_num(np.asarray(x, dtype=np.float64)),
+                                          np.nan_to_num(np.asarray(y, dtype=np.float64)))
+    assert h.stats["hits"] == 2
+
+
+@pytest.mark.gpu
+def test_history_device_resident_matches(tmp_path):
+    import torch
+    gen = np.random.default_rng(8)
+    _write_parts(str(tmp_path), gen, 3, 2000)
+    data = concat_lines([TextLines.from_strings(_lines(gen, 500, 400, 250)),
+                         read_past_data(str(tmp_path)).values()])
+    h = RatingsHistory(torch.device("cuda", 0))
+    for _ in range(2):
+        u1, i1 = ingest.IdDict(), ingest.IdDict()
+        ref = ingest.parse_ratings(data, u1, i1, default_ts=7)
+        got = h.parse_ratings(data, ingest.IdDict(), ingest.IdDict(), default_ts=7)
+        _same(ref[:2], got[:2])
+        _same(ref[3:], got[3:])
+    assert h.stats["hits"] == 3
+    assert all(sg.u.is_cuda for sg in h._segs.values())
