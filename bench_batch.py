@@ -39,6 +39,11 @@ def main(argv=None) -> int:
     ap.add_argument("--dir", default=None, help="work dir (default: a fresh temp dir)")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--generations", type=int, default=1,
+                    help="generations to run (1 GPU): generation g > 1 appends --next-ratings "
+                         "new ratings and trains on them plus all earlier ones (the past part "
+                         "files -- the resident parsed history's steady state)")
+    ap.add_argument("--next-ratings", type=int, default=1_000_000)
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -81,20 +86,24 @@ def main(argv=None) -> int:
         layer._update = layer.load_update_instance()
         layer.build_input_consumer()
         rng = np.random.default_rng(7)
-        topic = tlog.Topic(work + "/log", "OryxInput")
-        t0 = time.perf_counter()
-        chunk = 1 << 20
         now = int(time.time() * 1000)
-        for lo in range(0, args.ratings, chunk):
-            n = min(chunk, args.ratings - lo)
-            u = (args.users * rng.random(n) ** 1.3).astype(np.int64)
-            it = (args.items * rng.random(n) ** 2.5).astype(np.int64)
-            s = rng.integers(1, 11, n) * 0.5
-            ts = now - rng.integers(0, 86_400_000, n)
-            lines = ["%d,%d,%.1f,%d" % row for row in zip(u.tolist(), it.tolist(), s.tolist(),
-                                                         ts.tolist())]
-            topic.append_batch([(None, l) for l in lines])
-        topic.close()
+
+        def append(n_total, now):
+            topic = tlog.Topic(work + "/log", "OryxInput")
+            chunk = 1 << 20
+            for lo in range(0, n_total, chunk):
+                n = min(chunk, n_total - lo)
+                u = (args.users * rng.random(n) ** 1.3).astype(np.int64)
+                it = (args.items * rng.random(n) ** 2.5).astype(np.int64)
+                s = rng.integers(1, 11, n) * 0.5
+                ts = now - rng.integers(0, 86_400_000, n)
+                lines = ["%d,%d,%.1f,%d" % row for row in zip(u.tolist(), it.tolist(),
+                                                             s.tolist(), ts.tolist())]
+                topic.append_batch([(None, l) for l in lines])
+            topic.close()
+
+        t0 = time.perf_counter()
+        append(args.ratings, now)
         t_ingest = time.perf_counter() - t0
         if torch.cuda.is_available():
             torch.cuda.synchronize()
@@ -102,6 +111,20 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         layer.run_interval(now)
         t_gen = time.perf_counter() - t0
+        later = []
+        for g in range(1, max(1, args.generations) if ctx.world_size == 1 else 1):
+            before = dict(layer._update.phase_seconds)
+            now += 60_000
+            append(args.next_ratings, now)
+            t0 = time.perf_counter()
+            layer.run_interval(now)
+            dt = time.perf_counter() - t0
+            after = layer._update.phase_seconds
+            hist = getattr(layer._update, "history", None)
+            later.append({"generation": g + 1, "generation_s": dt,
+                          "ratings": args.ratings + g * args.next_ratings,
+                          "phase_s": {k: after[k] - before.get(k, 0.0) for k in after},
+                          "history": dict(hist.stats) if hist is not None else None})
         layer.close()
     else:
         dist.barrier(ctx)
@@ -110,6 +133,8 @@ def main(argv=None) -> int:
         t_gen = time.perf_counter() - t0
     upd = layer._update
     phases = dict(getattr(upd, "phase_seconds", {}))
+    if not ctx.is_main:
+        later = []
     phases.update({"layer_" + k: v for k, v in layer.last_phases.items()})
     if ctx.is_main:
         # count what was published
@@ -121,6 +146,7 @@ def main(argv=None) -> int:
             "value": args.ratings / t_gen, "unit": "ratings/s", "higher_is_better": True,
             "n_gpus": ctx.world_size, "generation_s": t_gen, "log_append_s": t_ingest,
             "phase_s": phases, "update_messages": int(sum(ends)),
+            "later_generations": later,
             "config": {"ratings": args.ratings, "users": args.users, "items": args.items,
                        "features": args.features, "iterations": args.iterations,
                        "dtype": args.dtype, "partitions": args.partitions,

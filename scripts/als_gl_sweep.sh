@@ -1,4 +1,5 @@
 set -o pipefail
+export ORYX_ALS_WIDE_VARIANT=2
 cd $GRAFT_REPO_ROOT 2>/dev/null || cd /root/repo
 for cfg in "2 0" "2 1" "1 0" "1 1"; do
   set -- $cfg
