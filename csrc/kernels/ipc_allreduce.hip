@@ -1,0 +1,142 @@
+// ipc_allreduce.hip -- one-shot all-reduce of small fp32 payloads through peer mappings of the
+// ranks' exchange buffers (latency-optimal collectives for the k x k
+// Gramian and the K x (d + 1) centroid sums that replace MLlib's shuffles,
+// [mllib]/als/ALSUpdate.java:116-124, [mllib]/kmeans/KMeansUpdate.java:116-117).
+//
+// A ring all-reduce of a 64 KB Gramian over 8 GPUs is 14 dependent steps of ~8 KB each: it is
+// bound by per-step latency, not by xGMI bandwidth.  Here every rank stages its payload in its
+// own exchange buffer (uncached device memory, mapped into every other rank of the node with
+// hipIpcOpenMemHandle), raises a flag, waits for every peer's flag, and then each workgroup
+// sums its slice of all W payloads straight out of the peers' HBM over the point-to-point
+// xGMI links -- one dependent step.  Every rank sums in rank order 0..W-1, so all ranks get
+// bitwise the same result.
+//
+// Exchange buffer of one rank: [flags: 2 x 128 B][slot 0: cap floats][slot 1: cap floats].
+// Call `epoch` (1, 2, ...) uses slot epoch & 1 and sets flag[epoch & 1] = epoch.  A rank
+// rewrites a slot only two calls later, after it has seen every peer arrive at the call in
+// between -- which each peer does only after finishing its reads of the call before -- so two
+// slots suffice.  The flag wait is bounded (timeout_s, 120 s by default): a peer that never
+// arrives sets *err instead of hanging the GPU; the host checks it (parallel/ipc.py).
+#include <cstring>
+
+#include "common.h"
+
+namespace {
+
+constexpr int kMaxRanks = 16;
+constexpr long long kHeaderFloats = 64;   // 256 bytes of flags
+struct Peers {
+  float* p[kMaxRanks];
+};
+
+__device__ __forceinline__ unsigned* flag_of(float* buf, int slot) {
+  return reinterpret_cast<unsigned*>(buf) + slot * 32;
+}
+
+__global__ __launch_bounds__(256) void ipc_stage(const float* __restrict__ src,
+                                                 float* __restrict__ dst, long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256)
+    dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void ipc_signal_reduce(float* __restrict__ out, long long n,
+                                                         Peers peers, int W, int rank, int slot,
+                                                         unsigned epoch, long long slot_off,
+                                                         unsigned long long timeout_ticks,
+                                                         int* err) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // the staged payload (previous launch on this stream) is written back before the flag
+    __threadfence_system();
+    __hip_atomic_store(flag_of(peers.p[rank], slot), epoch, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x < W) {
+    // ranks may legitimately arrive seconds apart (host work before a collective); give up
+    // after timeout_ticks of the 100 MHz real-time clock
+    const unsigned* f = flag_of(peers.p[threadIdx.x], slot);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
+        atomicExch(err, 1 + (int)threadIdx.x);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  }
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    float acc = 0.f;
+    for (int r = 0; r < W; ++r)
+      acc += __hip_atomic_load(peers.p[r] + slot_off + i, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    out[i] = acc;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int oryx_ipc_alloc(long long bytes, void** out) {
+  void* p = nullptr;
+  if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached) != hipSuccess)
+    return ORYX_ELAUNCH;
+  if (hipMemset(p, 0, (size_t)bytes) != hipSuccess) return ORYX_ELAUNCH;
+  *out = p;
+  return ORYX_OK;
+}
+
+int oryx_ipc_free(void* p) { return hipFree(p) == hipSuccess ? ORYX_OK : ORYX_ELAUNCH; }
+
+int oryx_ipc_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+int oryx_ipc_handle(void* p, void* out) {
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, p) != hipSuccess) return ORYX_ELAUNCH;
+  std::memcpy(out, &h, sizeof(h));
+  return ORYX_OK;
+}
+
+int oryx_ipc_open(const void* handle, void** out) {
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle, sizeof(h));
+  void* p = nullptr;
+  if (hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+    return ORYX_ELAUNCH;
+  *out = p;
+  return ORYX_OK;
+}
+
+int oryx_ipc_close(void* p) {
+  return hipIpcCloseMemHandle(p) == hipSuccess ? ORYX_OK : ORYX_ELAUNCH;
+}
+
+// data: this rank's payload, reduced in place; peers: W exchange-buffer pointers (this rank's
+// own at [rank]); cap: slot capacity in floats.
+int oryx_ipc_allreduce_f32(float* data, long long n, void* const* peers, int W, int rank,
+                           unsigned epoch, long long cap, double timeout_s, int* err,
+                           void* stream) {
+  if (n <= 0) return ORYX_OK;
+  if (W < 1 || W > kMaxRanks || rank < 0 || rank >= W || n > cap || epoch == 0)
+    return ORYX_EINVAL;
+  Peers ps{};
+  for (int r = 0; r < W; ++r) ps.p[r] = static_cast<float*>(peers[r]);
+  const int slot = (int)(epoch & 1u);
+  const long long slot_off = kHeaderFloats + (long long)slot * cap;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  long long blocks = (n + 255) / 256;
+  if (blocks > 128) blocks = 128;
+  hipLaunchKernelGGL(ipc_stage, dim3((unsigned)blocks), dim3(256), 0, s, data,
+                     ps.p[rank] + slot_off, n);
+  const unsigned long long ticks =
+      (unsigned long long)((timeout_s > 0 ? timeout_s : 120.0) * 1e8);   // 100 MHz clock
+  hipLaunchKernelGGL(ipc_signal_reduce, dim3((unsigned)blocks), dim3(256), 0, s, data, n, ps, W,
+                     rank, slot, epoch, slot_off, ticks, err);
+  return oryx_check_launch();
+}
+
+long long oryx_ipc_header_floats() { return kHeaderFloats; }
+
+}  // extern "C"

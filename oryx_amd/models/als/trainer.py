@@ -458,6 +458,7 @@ class ALSTrainer:
                 with tracing.range("als.checkpoint"):
                     self.save_checkpoint(checkpoint_dir, done, fingerprint)
         watchdog.get().end_heartbeats()
+        dist.check_collectives(self.ctx)
         out = self.factors()
         if use_ckpt:
             dist.barrier(self.ctx)

@@ -193,6 +193,16 @@ def _load_kernels():
                                            c_vp, c_i, c_vp])
     _sig(lib, "oryx_gramian_f32", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])
+    # one-shot IPC all-reduce (ipc_allreduce.hip; parallel/ipc.py)
+    _sig(lib, "oryx_ipc_alloc", c_i, [c_ll, c_vp])
+    _sig(lib, "oryx_ipc_free", c_i, [c_vp])
+    _sig(lib, "oryx_ipc_handle_size", c_i, [])
+    _sig(lib, "oryx_ipc_handle", c_i, [c_vp, c_vp])
+    _sig(lib, "oryx_ipc_open", c_i, [c_vp, c_vp])
+    _sig(lib, "oryx_ipc_close", c_i, [c_vp])
+    _sig(lib, "oryx_ipc_allreduce_f32", c_i, [c_vp, c_ll, c_vp, c_i, c_i, ctypes.c_uint, c_ll,
+                                              ctypes.c_double, c_vp, c_vp])
+    _sig(lib, "oryx_ipc_header_floats", c_ll, [])
     _sig(lib, "oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
                                           c_vp])
     # X, xnorm, C, n, d_pad, k_pad, cnorm, Xf, ldx, d, Cf, k, cmax, assign, mind, idx2, flags,

@@ -545,6 +545,7 @@ def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
             dist.all_reduce_sum(cost, ctx)
             dist.all_reduce_sum(counts, ctx)
         watchdog.get().end_heartbeats()
+        dist.check_collectives(ctx)
         res = KMeansResult(centers, counts, float(cost), it)
         if best is None or res.cost < best.cost:
             best = res

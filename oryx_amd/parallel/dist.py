@@ -28,7 +28,7 @@ from . import watchdog
 __all__ = ["DistContext", "init_from_env", "get_context", "shard_range", "padded_shard_size",
            "all_gather_rows", "all_gather_rows_async", "all_reduce_sum", "broadcast_object",
            "barrier", "run_info", "split_groups", "broadcast_tensor", "all_gather_list",
-           "global_rank"]
+           "global_rank", "check_collectives"]
 
 
 @dataclass
@@ -46,6 +46,8 @@ class DistContext:
     # ORYX_FORCE_COLLECTIVES=1: a world of one still initialises the process group and runs
     # every collective (exercises the RCCL code paths on a single GPU)
     forced: bool = False
+    # one-shot peer-mapped all-reduce for small fp32 payloads (parallel/ipc.py), or None
+    ipc: Optional[object] = None
 
     @property
     def is_distributed(self) -> bool:
@@ -113,6 +115,8 @@ def init_from_env(device: Optional[str] = None, backend: Optional[str] = None,
         # destructors, a gloo / RCCL group can be destroyed while its worker threads are
         # still joinable (std::terminate, SIGABRT at exit)
         atexit.register(_destroy_groups)
+        from . import ipc
+        ctx.ipc = ipc.maybe_create(ctx)
     _context = ctx
     return ctx
 
@@ -212,10 +216,20 @@ def all_gather_rows_async(local: torch.Tensor, out: torch.Tensor, ctx: DistConte
 
 
 def all_reduce_sum(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:
+    """In-place sum over the group.  Small fp32 device tensors on a one-node world go through
+    the one-shot peer-mapped all-reduce (parallel/ipc.py); everything else through RCCL."""
     if ctx.is_distributed:
+        if ctx.ipc is not None and ctx.ipc.fits(t):
+            return ctx.ipc.all_reduce_(t)
         with watchdog.guard("all_reduce"):
             tdist.all_reduce(t, op=tdist.ReduceOp.SUM, group=ctx.group)
     return t
+
+
+def check_collectives(ctx: DistContext) -> None:
+    """Raise if a one-shot all-reduce timed out waiting for a peer (synchronises)."""
+    if ctx.ipc is not None and ctx.ipc.calls:
+        ctx.ipc.check()
 
 
 def global_rank(ctx: DistContext, rank: int) -> int:
