@@ -18,6 +18,11 @@ ratings are bit-identical with and without the cache.
 
 Segments whose key no longer appears among a generation's past data (aged out by
 ``max-age-data-hours``) are dropped.
+
+The new interval is parsed as an unkeyed segment; its parse is also remembered under a hash
+of its bytes (xxh3-128), and when the part file the layer saves from those same bytes is read
+back next generation (a keyed miss with the same hash) that parse is adopted -- so in steady
+state every interval goes through the text parser exactly once.
 """
 
 from __future__ import annotations
@@ -32,6 +37,11 @@ import torch
 
 from ... import ingest
 from ...textlines import TextLines
+
+try:
+    import xxhash
+except ImportError:   # pragma: no cover - no adoption of unkeyed parses without it
+    xxhash = None
 
 log = logging.getLogger(__name__)
 
@@ -55,7 +65,22 @@ class RatingsHistory:
     def __init__(self, device: Optional[torch.device] = None):
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self._segs: "OrderedDict[tuple, _Segment]" = OrderedDict()
-        self.stats = {"hits": 0, "misses": 0, "hit_bytes": 0, "parsed_bytes": 0}
+        # recent unkeyed parses (new intervals) by content hash, adopted when the same bytes
+        # come back as a part file
+        self._unkeyed: "OrderedDict[bytes, _Segment]" = OrderedDict()
+        self.stats = {"hits": 0, "misses": 0, "hit_bytes": 0, "parsed_bytes": 0,
+                      "adopted": 0}
+
+    UNKEYED_MIN_BYTES = 1 << 20
+    UNKEYED_KEEP = 4
+
+    @staticmethod
+    def _digest(buf, off: int, nbytes: int) -> Optional[bytes]:
+        if xxhash is None:
+            return None
+        view = memoryview(buf)[off:off + nbytes] if not isinstance(buf, np.ndarray) \
+            else buf[off:off + nbytes]
+        return xxhash.xxh3_128_digest(view) + nbytes.to_bytes(8, "little")
 
     def __len__(self) -> int:
         return len(self._segs)
@@ -88,7 +113,7 @@ class RatingsHistory:
         """Same results as ``ingest.parse_ratings(lines, users, items, default_ts)`` (codes in
         first-appearance order appended to ``users`` / ``items``), reusing the parse of every
         keyed segment seen before."""
-        if not isinstance(lines, TextLines) or lines.segments is None:
+        if not isinstance(lines, TextLines):
             return ingest.parse_ratings(lines, users, items, default_ts)
         buf = lines.joined()
         off = 0
@@ -103,9 +128,22 @@ class RatingsHistory:
                 self.stats["hit_bytes"] += nbytes
                 self._segs.move_to_end(key)
             else:
-                sg = self._parse_range(buf, off, nbytes, n_lines)
-                self.stats["misses"] += 1
-                self.stats["parsed_bytes"] += nbytes
+                dg = self._digest(buf, off, nbytes) \
+                    if nbytes >= self.UNKEYED_MIN_BYTES else None
+                sg = self._unkeyed.get(dg) if (dg is not None and key is not None) else None
+                if sg is not None:
+                    # this part file holds the bytes of an interval parsed as new data
+                    self.stats["adopted"] += 1
+                    self.stats["hit_bytes"] += nbytes
+                    del self._unkeyed[dg]
+                else:
+                    sg = self._parse_range(buf, off, nbytes, n_lines)
+                    self.stats["misses"] += 1
+                    self.stats["parsed_bytes"] += nbytes
+                    if key is None and dg is not None:
+                        self._unkeyed[dg] = sg
+                        while len(self._unkeyed) > self.UNKEYED_KEEP:
+                            self._unkeyed.popitem(last=False)
                 if key is not None:
                     self._segs[key] = sg
             if key is not None:

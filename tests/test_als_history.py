@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 from oryx_amd import ingest
+from oryx_amd.api import Dataset
 from oryx_amd.layers.batch import read_past_data
 from oryx_amd.models.als import batch as als_batch
 from oryx_amd.models.als.history import RatingsHistory
@@ -85,12 +86,12 @@ def test_history_evicts_aged_out_parts_cpu(tmp_path):
                     ingest.IdDict(), 0)
     assert len(h) == 3
     h.parse_ratings(read_past_data(str(tmp_path)).values(), ingest.IdDict(), ingest.IdDict(), 0)
-    assert len(h) == 2 and h.stats["misses"] == 3
+    assert len(h) == 2 and h.stats["misses"] == 3 + 1     # + the unkeyed parse
     # a rewritten part file (new size / mtime) is parsed again
     with open(paths[1], "a") as f:
         f.write("u1,i1,1.0\n")
     h.parse_ratings(read_past_data(str(tmp_path)).values(), ingest.IdDict(), ingest.IdDict(), 0)
-    assert h.stats["misses"] == 4
+    assert h.stats["misses"] == 5
 
 
 def test_als_parse_ratings_with_history_decay_cpu(tmp_path):
@@ -128,3 +129,25 @@ def test_history_device_resident_matches(tmp_path):
         _same(ref[3:], got[3:])
     assert h.stats["hits"] == 3
     assert all(sg.u.is_cuda for sg in h._segs.values())
+
+
+def test_history_adopts_new_interval_parse_cpu(tmp_path, monkeypatch):
+    """The new interval's parse is reused when its part file is read back."""
+    from oryx_amd.layers.batch import save_interval_data
+    monkeypatch.setattr(RatingsHistory, "UNKEYED_MIN_BYTES", 1)
+    gen = np.random.default_rng(9)
+    h = RatingsHistory()
+    new = TextLines.from_strings(_lines(gen, 800, 300, 200))
+    ref = ingest.parse_ratings(new, ingest.IdDict(), ingest.IdDict(), 0)
+    h.parse_ratings(concat_lines([new, read_past_data(str(tmp_path)).values()]),
+                    ingest.IdDict(), ingest.IdDict(), 0)
+    save_interval_data(str(tmp_path), 1234, Dataset.from_values(new))
+    new2 = TextLines.from_strings(_lines(gen, 100, 300, 200))
+    data = concat_lines([new2, read_past_data(str(tmp_path)).values()])
+    u1, i1 = ingest.IdDict(), ingest.IdDict()
+    want = ingest.parse_ratings(data, u1, i1, 0)
+    got = h.parse_ratings(data, ingest.IdDict(), ingest.IdDict(), 0)
+    assert h.stats["adopted"] == 1 and h.stats["misses"] == 2
+    _same(want[:2], got[:2])
+    _same(want[3:], got[3:])
+    assert len(ref[0]) == 800
