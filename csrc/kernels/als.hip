@@ -1563,6 +1563,8 @@ int oryx_als_set_variant(int v) {
 
 int oryx_als_get_variant() { return g_als_variant; }
 
+int oryx_als_get_wide_variant() { return g_als_wide_variant; }
+
 int oryx_als_set_wide_variant(int v) {
   if (v < 0 || v > 2) return ORYX_EINVAL;
   g_als_wide_variant = v;
@@ -1780,7 +1782,7 @@ int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const fl
   return oryx_check_launch();
 }
 
-int oryx_kernels_version() { return 16; }
+int oryx_kernels_version() { return 17; }
 
 int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 

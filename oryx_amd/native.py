@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 16
+KERNELS_ABI_VERSION = 17
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -180,6 +180,7 @@ def _load_kernels():
     # ORYX_ALS_WIDE_VARIANT: 64 < k <= 128 and fp32-mode solve (2 = als_solve_batch_gl,
     # 0 = als_solve_wide / als_solve_wave, 1 = als_solve_block)
     _sig(lib, "oryx_als_set_wide_variant", c_i, [c_i])
+    _sig(lib, "oryx_als_get_wide_variant", c_i, [])
     lib.oryx_als_set_wide_variant(int(os.environ.get("ORYX_ALS_WIDE_VARIANT", "0")))
     # ..., n_long, ws, split (fp32 factors as bf16 hi|lo rows of 2*kp), stream
     _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,

@@ -241,6 +241,19 @@ def solve_variant(v: int):
         lib.oryx_als_set_variant(old)
 
 
+@contextlib.contextmanager
+def solve_wide_variant(v: int):
+    """Temporarily select the KP > 64 / fp32-mode solve kernel (``ORYX_ALS_WIDE_VARIANT``:
+    0 = als_solve_wide / als_solve_wave, 1 = als_solve_block, 2 = als_solve_batch_gl)."""
+    lib = native.require_kernels()
+    old = lib.oryx_als_get_wide_variant()
+    native.check(lib.oryx_als_set_wide_variant(int(v)), "oryx_als_set_wide_variant")
+    try:
+        yield
+    finally:
+        lib.oryx_als_set_wide_variant(old)
+
+
 def _use_kernel(device: torch.device, kp: int) -> bool:
     return device.type == "cuda" and kp in _KERNEL_KPS
 

@@ -61,7 +61,8 @@ def _row_rel_err(x, ref, rows):
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", [10, 16, 32, 40, 64, 72, 100, 128])
 @pytest.mark.parametrize("implicit", [True, False])
-def test_kernel_vs_reference(cuda, k, implicit):
+@pytest.mark.parametrize("wide", [0, 2])
+def test_kernel_vs_reference(cuda, k, implicit, wide):
     """bf16 factor mode against an fp64 model of its declared operand arithmetic (bf16 y_i,
     bf16(c_i y_i), fp32 accumulation): per-row relative error within 1e-3, or within 4x of a
     torch fp32 solve of the same model."""
@@ -72,7 +73,10 @@ def test_kernel_vs_reference(cuda, k, implicit):
     xb = torch.zeros(700, kp, device=cuda, dtype=torch.bfloat16)
     fails = torch.zeros(1, dtype=torch.int32, device=cuda)
     lam = 0.05
-    als_ops.solve_rows(csr, yb, yty, x, xb, k, lam, 1.5, implicit, fail_count=fails)
+    if wide and k <= 64:
+        pytest.skip("the wide variant selects kernels for k > 64 only")
+    with als_ops.solve_variant(5), als_ops.solve_wide_variant(wide):
+        als_ops.solve_rows(csr, yb, yty, x, xb, k, lam, 1.5, implicit, fail_count=fails)
     torch.cuda.synchronize()
     rows = csr.order.long()
     ref64 = als_ops.solve_rows_reference(csr, yb.double(), yty, k, lam, 1.5, implicit,
@@ -94,10 +98,12 @@ def test_kernel_vs_reference(cuda, k, implicit):
 @pytest.mark.parametrize("k", [10, 48, 64, 100, 128])
 @pytest.mark.parametrize("implicit", [True, False])
 @pytest.mark.parametrize("split_rows", [False, True])
-def test_kernel_fp32_factors_vs_fp64(cuda, k, implicit, split_rows):
+@pytest.mark.parametrize("wide", [0, 2])
+def test_kernel_fp32_factors_vs_fp64(cuda, k, implicit, split_rows, wide):
     """fp32 factor mode (bf16 hi|lo operands, SPLIT kernels) on TRUE fp32 factors: per-row
     relative error vs an fp64 solve <= 5e-5 (the split carries ~2^-17 relative; a torch fp32
-    solve lands near 1e-6, the bf16 factor mode near 1e-2) and far below the bf16 mode's."""
+    solve lands near 1e-6, the bf16 factor mode near 1e-2) and far below the bf16 mode's.
+    wide=2: the LDS-DMA batched kernel (als_solve_batch_gl) instead of als_solve_wave/_wide."""
     csr, y, kp = _problem(700, 400, 30000, k, 100 + k, "cpu", neg=implicit)
     if split_rows:
         rows_, cols_ = csr.row_ptr, csr.cols      # rebuild with long rows cut into segments
@@ -113,7 +119,9 @@ def test_kernel_fp32_factors_vs_fp64(cuda, k, implicit, split_rows):
     x = torch.zeros(700, kp, device=cuda)
     xs = torch.zeros(700, 2 * kp, device=cuda, dtype=torch.bfloat16)
     fails = torch.zeros(1, dtype=torch.int32, device=cuda)
-    als_ops.solve_rows(csr, ys, yty, x, xs, k, 0.05, 1.5, implicit, fail_count=fails, split=True)
+    with als_ops.solve_variant(5), als_ops.solve_wide_variant(wide):
+        als_ops.solve_rows(csr, ys, yty, x, xs, k, 0.05, 1.5, implicit, fail_count=fails,
+                           split=True)
     torch.cuda.synchronize()
     rows = csr.order.long()
     ref64 = als_ops.solve_rows_reference(csr, y.double(), yty, k, 0.05, 1.5, implicit)
