@@ -237,6 +237,7 @@ def main(argv=None) -> int:
             },
             "world_size": info["world_size"],
             "backend": info["backend"],
+            "ipc_allreduce": info.get("ipc_allreduce", False),
             "rank_devices": [r.get("current_device", r["device"]) for r in info["ranks"]],
             "peak_hbm_gib_per_rank": float(peak.item()) / 2**30,
             "halfstep_ms": halfstep_ms,

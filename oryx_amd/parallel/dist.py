@@ -149,7 +149,8 @@ def run_info(ctx: DistContext) -> dict:
         backend = tdist.get_backend()
     else:
         allv, ws, backend = [me], 1, None
-    return {"world_size": ws, "backend": backend, "ranks": allv}
+    return {"world_size": ws, "backend": backend, "ranks": allv,
+            "ipc_allreduce": ctx.ipc is not None}
 
 
 def get_context() -> DistContext:
