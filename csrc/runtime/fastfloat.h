@@ -274,9 +274,11 @@ inline uint32_t parse_8digits(uint64_t x) {   // little-endian load of 8 ASCII d
   return (uint32_t)x;
 }
 
-// Parses [b, e) as a float; false when it is not a number (NaN / Infinity spellings are the
-// caller's).
-inline bool parse_float(const char* b, const char* e, float& out) {
+// Parses the number starting at b (not past e) as a float; *stop receives the first byte
+// after it.  PREFIX = false: the number must span all of [b, e).  False when there is no
+// number (NaN / Infinity spellings are the caller's).
+template <bool PREFIX>
+inline bool parse_float_impl(const char* b, const char* e, float& out, const char** stop) {
   static const double kP10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
                                   1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
                                   1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
@@ -342,7 +344,8 @@ inline bool parse_float(const char* b, const char* e, float& out) {
       if (x < 100000) x = x * 10 + (*p - '0');
     exp10 += eneg ? -x : x;
   }
-  if (p != e) return false;
+  if (!PREFIX && p != e) return false;
+  *stop = p;
   if (D == 0) {
     out = neg ? -0.0f : 0.0f;
     return true;
@@ -359,8 +362,19 @@ inline bool parse_float(const char* b, const char* e, float& out) {
       return true;
     }
   }
-  auto r = std::from_chars(b, e, out);
-  return r.ec == std::errc() && r.ptr == e;
+  auto r = std::from_chars(b, p, out);
+  return r.ec == std::errc() && r.ptr == p;
+}
+
+inline bool parse_float(const char* b, const char* e, float& out) {
+  const char* stop;
+  return parse_float_impl<false>(b, e, out, &stop);
+}
+
+// The number at the start of [b, e) (JSON array elements: the caller checks the delimiter
+// at *stop) -- one pass instead of a delimiter scan followed by parse_float.
+inline bool parse_float_prefix(const char* b, const char* e, float& out, const char** stop) {
+  return parse_float_impl<true>(b, e, out, stop);
 }
 
 // Parses [b, e) as a double: exact fast path for <= 19 significant digits, a mantissa that

@@ -1071,6 +1071,15 @@ int parse_one_up(const char* b, const char* e, int k, float* v, std::string& ids
     if (f && !c.eat(',')) { ok = false; break; }
     c.ws();
     const char* fb = c.p;
+    {
+      // one pass over a plain number followed by its delimiter
+      const char* stop;
+      if (oryx_ff::parse_float_prefix(fb, c.end, v[f], &stop) && stop > fb && stop < c.end &&
+          (*stop == ',' || *stop == ']' || *stop == ' ')) {
+        c.p = stop;
+        continue;
+      }
+    }
     while (c.p < c.end && *c.p != ',' && *c.p != ']' && *c.p != ' ') ++c.p;
     if (!oryx_ff::parse_float(fb, c.p, v[f])) {
       const std::string_view t(fb, (size_t)(c.p - fb));   // NaN / Infinity spellings
