@@ -1548,10 +1548,11 @@ __global__ __launch_bounds__(256) void pair_dots(const float* __restrict__ X,
 // als_solve_wave (register column Cholesky), 3 (default) / 4 = variant 2 with the
 // factorisation at raised issue priority (s_setprio 2 / 3: 2-6% faster half-steps than 2)
 static int g_als_variant = 5;
-// 64 < KP <= 128 and the fp32 factor mode: 0 (default) = als_solve_wide (fp32 mode at
-// KP <= 64: als_solve_wave), 1 = als_solve_block (LDS Cholesky, bf16 only), 2 (with variant 5)
-// = als_solve_batch_gl (als_batch.hip: LDS-DMA gather, batched block LDL^T)
-static int g_als_wide_variant = 0;
+// 64 < KP <= 128 and the fp32 factor mode: 2 (default, with variant 5) = als_solve_batch_gl
+// (als_batch.hip: LDS-DMA gather, batched block LDL^T; rank-128 fp32 12.3 ms per iteration vs
+// 13.9 for als_solve_wide); 0 = als_solve_wide (fp32 mode at KP <= 64: als_solve_wave),
+// 1 = als_solve_block (LDS Cholesky, bf16 only)
+static int g_als_wide_variant = 2;
 
 extern "C" {
 

@@ -1124,12 +1124,14 @@ int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s
   return oryx_check_launch();
 }
 
-// rows per wave of the rank-128 LDS-DMA kernel (ORYX_ALS_GL_NM: 2 = a pair at one wave per
-// SIMD, 1 = one row at two waves per SIMD); other KP always pair their rows
+// rows per wave of the rank-128 LDS-DMA kernel (ORYX_ALS_GL_NM: 1 (default) = one row at two
+// waves per SIMD, 2 = a pair at one wave per SIMD; rank-128 fp32, 25M ratings: 12.34 vs
+// 12.43 ms per iteration, bf16 8.38 vs 9.77 -- profiles/r3_als128_gl_sweep.txt); other KP
+// always pair their rows
 static int gl_rows_per_wave() {
   static const int v = [] {
     const char* e = getenv("ORYX_ALS_GL_NM");
-    return e && atoi(e) == 1 ? 1 : 2;
+    return e && atoi(e) == 2 ? 2 : 1;
   }();
   return v;
 }

@@ -181,7 +181,7 @@ def _load_kernels():
     # 0 = als_solve_wide / als_solve_wave, 1 = als_solve_block)
     _sig(lib, "oryx_als_set_wide_variant", c_i, [c_i])
     _sig(lib, "oryx_als_get_wide_variant", c_i, [])
-    lib.oryx_als_set_wide_variant(int(os.environ.get("ORYX_ALS_WIDE_VARIANT", "0")))
+    lib.oryx_als_set_wide_variant(int(os.environ.get("ORYX_ALS_WIDE_VARIANT", "2")))
     # ..., n_long, ws, split (fp32 factors as bf16 hi|lo rows of 2*kp), stream
     _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                       c_i, c_f, c_f, c_i, c_vp, c_vp, c_vp, c_i, c_i, c_vp,
