@@ -1578,7 +1578,7 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
                    const float* vals, const void* Y, const float* YtY, float* X, void* Xb,
                    int n_work, int k, int kp, float lambda, float alpha, int implicit,
                    int* fail_count, const int32_t* long_slot, const int64_t* segs, int n_seg,
-                   int n_long, float* ws, int split, void* stream) {
+                   int n_long, float* ws, int split, long long nnz, void* stream) {
   if (n_work <= 0) return ORYX_OK;
   if (n_seg > 0 && (!long_slot || !segs || !ws || n_long <= 0)) return ORYX_EINVAL;
   AlsParams p{row_ptr, row_ids, col_idx, vals, reinterpret_cast<const __bf16*>(Y), YtY, X,
@@ -1637,8 +1637,9 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
   if (g_als_variant == 5 && g_als_wide_variant == 2 && (split || kp > 64)) {
     // two rows per wave, LDS-DMA gather (als_batch.hip): 64 < KP <= 128 and the fp32 mode
     const int cus = resident_panel_blocks / 2;
+    const long long mean_len = n_work > 0 ? nnz / n_work : 0;
     if (const int rc = oryx_als::batch_gl_launch(p, kp, split != 0, env_blocks ? env_blocks : cus,
-                                                 s))
+                                                 mean_len, s))
       return rc;
     return ORYX_OK;
   }
@@ -1783,7 +1784,7 @@ int oryx_als_debug_gram(const int64_t* row_ptr, const int32_t* col_idx, const fl
   return oryx_check_launch();
 }
 
-int oryx_kernels_version() { return 17; }
+int oryx_kernels_version() { return 18; }
 
 int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 

@@ -703,6 +703,46 @@ __device__ __forceinline__ void glds4(const void* src, uint32_t lds) {
       : "v"(src), "s"(lds)
       : "memory");
 }
+// N LDS-DMA loads of 16 bytes per lane into consecutive 1 KB pieces from lds on: one asm
+// statement, M0 stepped by s_add (instead of saving / setting / restoring it per load)
+#ifndef ORYX_GL_ISSUE_BATCH
+#define ORYX_GL_ISSUE_BATCH 1
+#endif
+#ifndef ORYX_GL_COMPACT
+#define ORYX_GL_COMPACT 0
+#endif
+#define GL_L(i) "s_nop 0\n\tglobal_load_lds_dwordx4 %" #i ", off\n\t"
+#define GL_A "s_add_u32 m0, m0, 0x400\n\t"
+template <int N>
+__device__ __forceinline__ void glds16_run(const char* const (&src)[N], uint32_t lds) {
+  unsigned keep;
+  if constexpr (N == 8) {
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %9\n\t"
+                 GL_L(1) GL_A GL_L(2) GL_A GL_L(3) GL_A GL_L(4) GL_A GL_L(5) GL_A GL_L(6) GL_A
+                 GL_L(7) GL_A GL_L(8) "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src[0]), "v"(src[1]), "v"(src[2]), "v"(src[3]), "v"(src[4]), "v"(src[5]),
+                   "v"(src[6]), "v"(src[7]), "s"(lds)
+                 : "memory", "scc");
+  } else if constexpr (N == 16) {
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %17\n\t"
+                 GL_L(1) GL_A GL_L(2) GL_A GL_L(3) GL_A GL_L(4) GL_A GL_L(5) GL_A GL_L(6) GL_A
+                 GL_L(7) GL_A GL_L(8) GL_A GL_L(9) GL_A GL_L(10) GL_A GL_L(11) GL_A GL_L(12) GL_A
+                 GL_L(13) GL_A GL_L(14) GL_A GL_L(15) GL_A GL_L(16) "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src[0]), "v"(src[1]), "v"(src[2]), "v"(src[3]), "v"(src[4]), "v"(src[5]),
+                   "v"(src[6]), "v"(src[7]), "v"(src[8]), "v"(src[9]), "v"(src[10]),
+                   "v"(src[11]), "v"(src[12]), "v"(src[13]), "v"(src[14]), "v"(src[15]),
+                   "s"(lds)
+                 : "memory", "scc");
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) glds16(src[i], lds + i * 1024);
+  }
+}
+#undef GL_L
+#undef GL_A
+
 // wait until at most N vector-memory operations of this wave are outstanding
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -814,11 +854,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     int c[NPL];
 #pragma unroll
     for (int it = 0; it < NPL; ++it) c[it] = cid[srow(it)];
+    if constexpr (ORYX_GL_ISSUE_BATCH && C::IMG == NPL * 1024) {
+      // the hi pieces, then (fp32 mode) the lo pieces right behind them: one asm run
+      constexpr int NS = NPL * (SPLIT ? 2 : 1);
+      const char* src[NS];
 #pragma unroll
-    for (int it = 0; it < NPL; ++it) {
-      const char* src = ybase + ((size_t)(unsigned)c[it] * (YS * 2) + (unsigned)(soff(it) * 2));
-      glds16(src, slot_lds(m) + it * 1024);
-      if constexpr (SPLIT) glds16(src + KP * 2, slot_lds(m) + C::IMG + it * 1024);
+      for (int it = 0; it < NPL; ++it) {
+        src[it] = ybase + ((size_t)(unsigned)c[it] * (YS * 2) + (unsigned)(soff(it) * 2));
+        if constexpr (SPLIT) src[NPL + it] = src[it] + KP * 2;
+      }
+      glds16_run<NS>(src, slot_lds(m));
+    } else {
+#pragma unroll
+      for (int it = 0; it < NPL; ++it) {
+        const char* src =
+            ybase + ((size_t)(unsigned)c[it] * (YS * 2) + (unsigned)(soff(it) * 2));
+        glds16(src, slot_lds(m) + it * 1024);
+        if constexpr (SPLIT) glds16(src + KP * 2, slot_lds(m) + C::IMG + it * 1024);
+      }
     }
   };
   auto stage2 = [&]() {
@@ -906,7 +959,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
       const f32x4 r1 = *(const lds_f32x4*)(meta_ptr(m, q) + 128 + 32 * gl + 16);
       // transposed-read byte offsets of this lane (operand pi, half h), made once per chunk from
       // an opaque lane id: slot row 8g + 4h + q4, piece (2 pi + p4/2 - rot(row)) mod PPR
-      int tra[M][2];
+      // COMPACT (power-of-two pieces per row): two row bases and the rotation instead of the
+      // 2M-entry table, the piece offset recomputed per read (two VALU ops)
+      constexpr bool COMPACT = ORYX_GL_COMPACT && (PPR & (PPR - 1)) == 0 && !(KP <= 64);
+      int tra[COMPACT ? 1 : M][2];
+      int tb[2], tc[2];
       {
         const int ln = olane();
         const int sb = (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)S;
@@ -916,23 +973,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
           const int row = 8 * gg + 4 * h + q4;
           const int base = sb + row * KP * 2 + (p4 & 1) * 8;
           const int c = (p4 >> 1) - CI::rot(row) + PPR;
+          tb[h] = base;
+          tc[h] = c;
+          if constexpr (!COMPACT) {
 #pragma unroll
-          for (int pi = 0; pi < M; ++pi) tra[pi][h] = base + ((2 * pi + c) % PPR) * 16;
+            for (int pi = 0; pi < M; ++pi) tra[pi][h] = base + ((2 * pi + c) % PPR) * 16;
+          }
         }
       }
+      auto addr = [&](int pi, int h) -> int {
+        if constexpr (COMPACT) return tb[h] + (((2 * pi + tc[h]) & (PPR - 1)) << 4);
+        else return tra[pi][h];
+      };
       auto rd = [&](int off, int pi) -> bf16x8 {
         typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
         const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lds_bf16x4*)(uintptr_t)(uint32_t)(tra[pi][0] + off));
+            (lds_bf16x4*)(uintptr_t)(uint32_t)(addr(pi, 0) + off));
         const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
-            (lds_bf16x4*)(uintptr_t)(uint32_t)(tra[pi][1] + off));
+            (lds_bf16x4*)(uintptr_t)(uint32_t)(addr(pi, 1) + off));
         return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       };
       // each tile row re-reads its fragments at opaque (in-place redefined) addresses: merged
       // with the previous row's reads of the same bytes, they would all be held in registers
       auto fresh_addresses = [&]() {
+        if constexpr (COMPACT) {
+          asm volatile("" : "+v"(tb[0]), "+v"(tb[1]), "+v"(tc[0]), "+v"(tc[1]));
+        } else {
 #pragma unroll
-        for (int pi = 0; pi < M; ++pi) asm volatile("" : "+v"(tra[pi][0]), "+v"(tra[pi][1]));
+          for (int pi = 0; pi < M; ++pi) asm volatile("" : "+v"(tra[pi][0]), "+v"(tra[pi][1]));
+        }
       };
       // Fragments are re-read from the image where they are used (KP > 64: holding them would
       // spill the pair's accumulators; KP <= 64 holds the hi fragments).  LDS has the room: at
@@ -1124,16 +1193,18 @@ int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s
   return oryx_check_launch();
 }
 
-// rows per wave of the rank-128 LDS-DMA kernel (ORYX_ALS_GL_NM: 1 (default) = one row at two
-// waves per SIMD, 2 = a pair at one wave per SIMD; rank-128 fp32, 25M ratings: 12.34 vs
-// 12.43 ms per iteration, bf16 8.38 vs 9.77 -- profiles/r3_als128_gl_sweep.txt); other KP
-// always pair their rows
-static int gl_rows_per_wave() {
-  static const int v = [] {
+// rows per wave of the rank-128 LDS-DMA kernel: 1 = one row at two waves per SIMD, 2 = a pair
+// at one wave per SIMD.  Measured (profiles/r3_als128_gl_sweep.txt, rank-128 fp32, 25M
+// ratings): the items half-step (423 ratings per row on average) 5.19 ms with pairs vs 5.54
+// with single rows, the users half-step (154 per row) 7.08 vs 6.69 -- long rows amortise the
+// pair's one-wave-per-SIMD solve over more gather work.  ORYX_ALS_GL_NM=1/2 forces one.
+static int gl_rows_per_wave(long long mean_len) {
+  static const int forced = [] {
     const char* e = getenv("ORYX_ALS_GL_NM");
-    return e && atoi(e) == 2 ? 2 : 1;
+    return e ? atoi(e) : 0;
   }();
-  return v;
+  if (forced == 1 || forced == 2) return forced;
+  return mean_len >= 256 ? 2 : 1;
 }
 
 // ORYX_ALS_GL_HOLD=1: the rank-128 LDS-DMA kernel keeps the hi fragments in registers
@@ -1145,9 +1216,10 @@ static bool gl_hold_hi() {
   return v;
 }
 
-int batch_gl_launch(const AlsParams& p, int kp, bool split, int cus, hipStream_t s) {
+int batch_gl_launch(const AlsParams& p, int kp, bool split, int cus, long long mean_len,
+                    hipStream_t s) {
   // one resident generation: WPE blocks of 4 waves per CU, NM rows per wave
-  const int nm = kp == 128 ? gl_rows_per_wave() : 2;
+  const int nm = kp == 128 ? gl_rows_per_wave(mean_len) : 2;
   const int nb = (p.n_work + nm - 1) / nm;
   const int wpe = (nm == 2 && kp > 64) ? 1 : 2;
   int blocks = (nb + 3) / 4;

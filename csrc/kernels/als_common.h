@@ -31,7 +31,8 @@ struct AlsParams {
 // als_batch.hip: four rows per wave, block-LDL^T solve (KP <= 64, bf16 factors)
 int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s);
 // als_batch.hip: two rows per wave, LDS-DMA gather (64 < KP <= 128, and the fp32 factor mode)
-int batch_gl_launch(const AlsParams& p, int kp, bool split, int cus, hipStream_t s);
+int batch_gl_launch(const AlsParams& p, int kp, bool split, int cus, long long mean_len,
+                    hipStream_t s);
 // analysis: route KP=64 batch launches to the per-phase cycle counting build (nullptr: off)
 void batch_set_profile(unsigned long long* prof);
 
