@@ -1194,17 +1194,18 @@ int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s
 }
 
 // rows per wave of the rank-128 LDS-DMA kernel: 1 = one row at two waves per SIMD, 2 = a pair
-// at one wave per SIMD.  Measured (profiles/r3_als128_gl_sweep.txt, rank-128 fp32, 25M
-// ratings): the items half-step (423 ratings per row on average) 5.19 ms with pairs vs 5.54
-// with single rows, the users half-step (154 per row) 7.08 vs 6.69 -- long rows amortise the
-// pair's one-wave-per-SIMD solve over more gather work.  ORYX_ALS_GL_NM=1/2 forces one.
+// at one wave per SIMD.  Measured (rank-128 fp32; profiles/r3_als128_gl_sweep.txt and
+// r3_bench_als128_c3_fp32_gl*.json), pairs vs single rows per half-step at a mean row length
+// of 423: 5.19 vs 5.54 ms; 250: 28.3 vs 33.0; 154: 7.08 vs 6.69; 100: 46.1 vs 46.0 -- long
+// rows amortise the pair's one-wave-per-SIMD solve over more gather work.
+// ORYX_ALS_GL_NM=1/2 forces one.
 static int gl_rows_per_wave(long long mean_len) {
   static const int forced = [] {
     const char* e = getenv("ORYX_ALS_GL_NM");
     return e ? atoi(e) : 0;
   }();
   if (forced == 1 || forced == 2) return forced;
-  return mean_len >= 256 ? 2 : 1;
+  return mean_len >= 192 ? 2 : 1;
 }
 
 // ORYX_ALS_GL_HOLD=1: the rank-128 LDS-DMA kernel keeps the hi fragments in registers
