@@ -11,6 +11,8 @@
 #   smoke               __graft_entry__.smoke()
 #   bench[=ARGS]        bench.py --steps 20 --warmup 5 [ARGS, comma separated]
 #   halfstep[=V]        scripts/als_kernel_bench.py (per half-step ms) with ORYX_ALS_VARIANT=V
+#   hs[=ARGS]           scripts/als_kernel_bench.py ARGS (e.g. hs=--rank-k,128,--precision,fp32);
+#                       ORYX_KERNELS_SO / ORYX_ALS_* from the environment (A/B of builds)
 #   phases[=V]          scripts/als_phase_profile.py (per-phase cycles) with ORYX_ALS_VARIANT=V
 #   batch[=ARGS]        bench_batch.py --ratings 25000000 [ARGS]
 #   kmeans[=PREC]       bench_kmeans.py --precision PREC (fp32)
@@ -55,6 +57,10 @@ for step in "$@"; do
       out=gpurun_out/halfstep_v${val:-default}.json
       ORYX_ALS_VARIANT=${val:-${ORYX_ALS_VARIANT:-5}} timeout -k 10 400 python -u scripts/als_kernel_bench.py --reps 7 > $out 2> $out.err || fail "$step" $out.err
       cat $out ;;
+    hs)
+      out=gpurun_out/hs_$(tag "${val:-default}")${ORYX_KERNELS_SO:+_$(basename $ORYX_KERNELS_SO .so)}.json
+      timeout -k 10 300 python -u scripts/als_kernel_bench.py --reps 5 $(args "$val") > $out 2> $out.err || fail "$step" $out.err
+      cut -c1-400 $out ;;
     phases)
       out=gpurun_out/phases_v${val:-default}.json
       ORYX_ALS_VARIANT=${val:-${ORYX_ALS_VARIANT:-5}} timeout -k 10 400 python -u scripts/als_phase_profile.py > $out 2> $out.err || fail "$step" $out.err
