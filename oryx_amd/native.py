@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 17
+KERNELS_ABI_VERSION = 18
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -185,7 +185,7 @@ def _load_kernels():
     # ..., n_long, ws, split (fp32 factors as bf16 hi|lo rows of 2*kp), stream
     _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                       c_i, c_f, c_f, c_i, c_vp, c_vp, c_vp, c_i, c_i, c_vp,
-                                      c_i, c_vp])
+                                      c_i, c_ll, c_vp])
     _sig(lib, "oryx_als_ws_stride", c_i, [c_i])
     _sig(lib, "oryx_als_solve_profile64", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i,
                                                 c_i, c_f, c_f, c_i, c_vp, c_vp])

@@ -299,7 +299,7 @@ def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_ou
                                 csr.segs.data_ptr() if csr.n_seg else None,
                                 csr.n_seg, csr.n_long,
                                 ws.data_ptr() if ws is not None else None,
-                                int(bool(split)), native.stream_ptr(device))
+                                int(bool(split)), int(csr.nnz), native.stream_ptr(device))
         native.check(rc, "oryx_als_solve")
         return
     # exact reference path (CPU, or ranks beyond the kernel's range)
