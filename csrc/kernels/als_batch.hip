@@ -666,7 +666,7 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
 // (hooks of batch_solve); the scratch of the solve does not alias the image slots.
 //
 // One wave per SIMD at KP > 64 (the pair's accumulators), two at KP <= 64 (fp32 factor mode).
-template <int KP, bool SPLIT, int NM_>
+template <int KP, bool SPLIT, int NM_, int WPE_>
 struct GlCfg {
   static constexpr int NM = NM_;
   static constexpr int M = KP / 16;
@@ -678,8 +678,8 @@ struct GlCfg {
   static constexpr int META = 256;                      // 32 column ids + 32 values
   static constexpr int SCR = NM * 16 * BATCH_DS * 4;
   static constexpr int WAVE_BYTES = NM * SLOT + NM * 2 * META + SCR + NM * 16 * 4;
-  // waves per SIMD: one for a pair of rows at KP > 64, two otherwise
-  static constexpr int WPE = (NM == 2 && KP > 64) ? 1 : 2;
+  // waves per SIMD (1: 512 registers per wave)
+  static constexpr int WPE = WPE_;
   static constexpr int BYTES = 4 * WAVE_BYTES;
 };
 
@@ -753,11 +753,13 @@ __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)
 
 // HOLD_HI: the hi fragments of a chunk stay in registers (the lo ones are re-read from the image
 // where they are used); otherwise both are re-read (KP > 64: registers)
-template <int KP, bool SPLIT, int NM_ = 2, bool PROF = false, bool HOLD_HI = (KP <= 64)>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    GlCfg<KP, SPLIT, NM_>::WPE, GlCfg<KP, SPLIT, NM_>::WPE))) void als_solve_batch_gl(AlsParams p,
-                                                                            unsigned long long* prof) {
-  using C = GlCfg<KP, SPLIT, NM_>;
+// WPE_: waves per SIMD -- one for a pair of rows at KP > 64 (the pair's accumulators), and for
+// single rows of long average length (no spills at 512 registers); two otherwise
+template <int KP, bool SPLIT, int NM_ = 2, bool PROF = false, bool HOLD_HI = (KP <= 64),
+          int WPE_ = ((NM_ == 2 && KP > 64) ? 1 : 2)>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE_, WPE_))) void
+als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
+  using C = GlCfg<KP, SPLIT, NM_, WPE_>;
   using CI = ChunkImage<KP>;
   constexpr int NM = C::NM;
   constexpr int M = C::M;
@@ -1193,56 +1195,52 @@ int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s
   return oryx_check_launch();
 }
 
-// rows per wave of the rank-128 LDS-DMA kernel: 1 = one row at two waves per SIMD, 2 = a pair
-// at one wave per SIMD.  Measured (rank-128 fp32; profiles/r3_als128_gl_sweep.txt and
-// r3_bench_als128_c3_fp32_gl*.json), pairs vs single rows per half-step at a mean row length
-// of 423: 5.19 vs 5.54 ms; 250: 28.3 vs 33.0; 154: 7.08 vs 6.69; 100: 46.1 vs 46.0 -- long
-// rows amortise the pair's one-wave-per-SIMD solve over more gather work.
-// ORYX_ALS_GL_NM=1/2 forces one.
-static int gl_rows_per_wave(long long mean_len) {
-  static const int forced = [] {
+// Rank-128 configuration (rows per wave NM, waves per SIMD WPE) by the half-step's mean row
+// length.  Measured per half-step (rank-128 fp32, 25M ratings; profiles/r3_als128_gl_*):
+//   items (423 ratings per row): NM 1 / WPE 1 4.63 ms, NM 2 / WPE 1 5.17, NM 1 / WPE 2 5.54;
+//   users (154 per row):         NM 1 / WPE 2 6.46 ms, NM 1 / WPE 1 7.02, NM 2 / WPE 1 7.08.
+// Long rows want the spill-free 512-register wave (the gather dominates and a spill reload
+// waits for the whole DMA in flight); short rows want two waves per SIMD to overlap one row's
+// serial LDL^T with the other's gather.  ORYX_ALS_GL_NM / ORYX_ALS_GL_WPE force either.
+static void gl_config(long long mean_len, int& nm, int& wpe) {
+  static const int fnm = [] {
     const char* e = getenv("ORYX_ALS_GL_NM");
     return e ? atoi(e) : 0;
   }();
-  if (forced == 1 || forced == 2) return forced;
-  return mean_len >= 192 ? 2 : 1;
-}
-
-// ORYX_ALS_GL_HOLD=1: the rank-128 LDS-DMA kernel keeps the hi fragments in registers
-static bool gl_hold_hi() {
-  static const bool v = [] {
-    const char* e = getenv("ORYX_ALS_GL_HOLD");
-    return e && atoi(e) == 1;
+  static const int fwpe = [] {
+    const char* e = getenv("ORYX_ALS_GL_WPE");
+    return e ? atoi(e) : 0;
   }();
-  return v;
+  nm = fnm == 2 ? 2 : 1;
+  wpe = nm == 2 ? 1 : (mean_len >= 192 ? 1 : 2);
+  if (nm == 1 && (fwpe == 1 || fwpe == 2)) wpe = fwpe;
 }
 
 int batch_gl_launch(const AlsParams& p, int kp, bool split, int cus, long long mean_len,
                     hipStream_t s) {
   // one resident generation: WPE blocks of 4 waves per CU, NM rows per wave
-  const int nm = kp == 128 ? gl_rows_per_wave(mean_len) : 2;
+  int nm = 2, wpe = kp > 64 ? 1 : 2;
+  if (kp == 128) gl_config(mean_len, nm, wpe);
   const int nb = (p.n_work + nm - 1) / nm;
-  const int wpe = (nm == 2 && kp > 64) ? 1 : 2;
   int blocks = (nb + 3) / 4;
   if (blocks > cus * wpe) blocks = cus * wpe;
   if (blocks < 1) blocks = 1;
   if (kp == 128) {
-#define GL128(SP, NMV, PR)                                                                    \
+#define GL128(SP, NMV, WV)                                                                    \
   do {                                                                                        \
-    if (gl_hold_hi())                                                                         \
-      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, PR, true>), dim3(blocks), dim3(256), \
-                         0, s, p, PR ? g_batch_prof : nullptr);                               \
+    if (g_batch_prof)                                                                         \
+      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, true, false, WV>), dim3(blocks),   \
+                         dim3(256), 0, s, p, g_batch_prof);                                   \
     else                                                                                      \
-      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, PR, false>), dim3(blocks),         \
-                         dim3(256), 0, s, p, PR ? g_batch_prof : nullptr);                    \
+      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, false, false, WV>), dim3(blocks),  \
+                         dim3(256), 0, s, p, nullptr);                                        \
   } while (0)
-    const bool pr = g_batch_prof != nullptr;
     if (nm == 2) {
-      if (split) { if (pr) GL128(true, 2, true); else GL128(true, 2, false); }
-      else { if (pr) GL128(false, 2, true); else GL128(false, 2, false); }
+      if (split) GL128(true, 2, 1); else GL128(false, 2, 1);
+    } else if (wpe == 1) {
+      if (split) GL128(true, 1, 1); else GL128(false, 1, 1);
     } else {
-      if (split) { if (pr) GL128(true, 1, true); else GL128(true, 1, false); }
-      else { if (pr) GL128(false, 1, true); else GL128(false, 1, false); }
+      if (split) GL128(true, 1, 2); else GL128(false, 1, 2);
     }
 #undef GL128
     return oryx_check_launch();
