@@ -962,8 +962,12 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
       // transposed-read byte offsets of this lane (operand pi, half h), made once per chunk from
       // an opaque lane id: slot row 8g + 4h + q4, piece (2 pi + p4/2 - rot(row)) mod PPR
       // COMPACT (power-of-two pieces per row): two row bases and the rotation instead of the
-      // 2M-entry table, the piece offset recomputed per read (two VALU ops)
-      constexpr bool COMPACT = ORYX_GL_COMPACT && (PPR & (PPR - 1)) == 0 && !(KP <= 64);
+      // 2M-entry table, the piece offset recomputed per read (two VALU ops).  On by default
+      // at two waves per SIMD, where the 16 registers it frees cut the chunk loop's spills
+      // (rank-128 fp32 users half-step 6.38 vs 6.57 ms; profiles/r3_als128_gl_ab.txt); at
+      // 512 registers it only adds VALU work.
+      constexpr bool COMPACT = (ORYX_GL_COMPACT || C::WPE == 2) && (PPR & (PPR - 1)) == 0 &&
+                               !(KP <= 64);
       int tra[COMPACT ? 1 : M][2];
       int tb[2], tc[2];
       {
