@@ -498,7 +498,15 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
   std::unique_lock<std::mutex> gi(di->mu, std::defer_lock);
   if (di != du) gi.lock();
   // chunk boundaries at newlines
-  int P = len >= (8ll << 20) ? oryx_ff::native_threads() : 1;
+  // several chunks from 1 MB on, at least 256 KB each (measured on 8 host cores: 100k lines,
+  // 3 MB, 12.6 -> 8.6 ms; at 10k lines, 0.3 MB, thread start-up and the dictionary merge
+  // cost more than they save: 1.1 ms on one thread, 1.7 ms on four)
+  int P = 1;
+  if (len >= (1ll << 20)) {
+    const long long by_size = len / (256ll << 10);
+    P = (int)std::min<long long>(by_size, oryx_ff::native_threads());
+    if (P < 1) P = 1;
+  }
   std::vector<const char*> cut((size_t)P + 1);
   cut[0] = buf;
   cut[(size_t)P] = buf + len;
