@@ -1014,14 +1014,25 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
       // KP = 128 fp32, 144 ds_read_b64_tr_b16 per chunk and row cost 288 LDS-array cycles per
       // wave against 1728 cycles of MFMAs.
       constexpr bool HOLD = HOLD_HI;
-      bf16x8 fbh[HOLD ? M : 1];
+      // a single row at 512 registers also holds the fp32 mode's lo fragments (all reads up
+      // front, no re-reads, no per-tile-row LDS waits)
+      constexpr bool HOLD_LO = HOLD && SPLIT && NM == 1 && C::WPE == 1;
+      bf16x8 fbh[HOLD ? M : 1], fbl[HOLD_LO ? M : 1];
       if constexpr (HOLD) {
 #pragma unroll
         for (int pi = 0; pi < M; ++pi) fbh[pi] = rd(0, pi);
       }
+      if constexpr (HOLD_LO) {
+#pragma unroll
+        for (int pi = 0; pi < M; ++pi) fbl[pi] = rd(C::IMG, pi);
+      }
       auto fbr = [&](int pi) -> bf16x8 {
         if constexpr (HOLD) return fbh[pi];
         else return rd(0, pi);
+      };
+      auto flr = [&](int pi) -> bf16x8 {
+        if constexpr (HOLD_LO) return fbl[pi];
+        else return rd(C::IMG, pi);
       };
       const int left = len[m] - 32 * kk - 8 * gl;
       float wa[8], wb[8], cn = 0.f;
@@ -1052,7 +1063,7 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
         const bf16x8 fq = fbr(qi);
         const i32x4 raw = __builtin_bit_cast(i32x4, fq);
         i32x4 rawl;
-        if constexpr (SPLIT) rawl = __builtin_bit_cast(i32x4, rd(C::IMG, qi));
+        if constexpr (SPLIT) rawl = __builtin_bit_cast(i32x4, flr(qi));
         i32x4 whi, wlo;
         f32x2 bacc = f32x2{0.f, 0.f};
 #pragma unroll
@@ -1084,7 +1095,7 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
           if constexpr (SPLIT) {
             const bf16x8 fal = __builtin_bit_cast(bf16x8, wlo);
             acc[m][tix<M>(pi, qi)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                pi == qi ? __builtin_bit_cast(bf16x8, rawl) : rd(C::IMG, pi), fa,
+                pi == qi ? __builtin_bit_cast(bf16x8, rawl) : flr(pi), fa,
                 acc[m][tix<M>(pi, qi)], 0, 0, 0);
             acc[m][tix<M>(pi, qi)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
                 fp, fal, acc[m][tix<M>(pi, qi)], 0, 0, 0);
@@ -1220,6 +1231,14 @@ static void gl_config(long long mean_len, int& nm, int& wpe) {
   if (nm == 1 && (fwpe == 1 || fwpe == 2)) wpe = fwpe;
 }
 
+static bool gl_hold() {
+  static const bool v = [] {
+    const char* e = getenv("ORYX_ALS_GL_HOLD");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
 int batch_gl_launch(const AlsParams& p, int kp, bool split, int cus, long long mean_len,
                     hipStream_t s) {
   // one resident generation: WPE blocks of 4 waves per CU, NM rows per wave
@@ -1230,21 +1249,26 @@ int batch_gl_launch(const AlsParams& p, int kp, bool split, int cus, long long m
   if (blocks > cus * wpe) blocks = cus * wpe;
   if (blocks < 1) blocks = 1;
   if (kp == 128) {
-#define GL128(SP, NMV, WV)                                                                    \
+#define GL128(SP, NMV, WV, HV)                                                                \
   do {                                                                                        \
     if (g_batch_prof)                                                                         \
-      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, true, false, WV>), dim3(blocks),   \
+      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, true, HV, WV>), dim3(blocks),      \
                          dim3(256), 0, s, p, g_batch_prof);                                   \
     else                                                                                      \
-      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, false, false, WV>), dim3(blocks),  \
+      hipLaunchKernelGGL((als_solve_batch_gl<128, SP, NMV, false, HV, WV>), dim3(blocks),     \
                          dim3(256), 0, s, p, nullptr);                                        \
   } while (0)
     if (nm == 2) {
-      if (split) GL128(true, 2, 1); else GL128(false, 2, 1);
+      if (split) GL128(true, 2, 1, false); else GL128(false, 2, 1, false);
     } else if (wpe == 1) {
-      if (split) GL128(true, 1, 1); else GL128(false, 1, 1);
+      // one row per 512-register wave: fragments held in registers (ORYX_ALS_GL_HOLD=0: re-read)
+      if (gl_hold()) {
+        if (split) GL128(true, 1, 1, true); else GL128(false, 1, 1, true);
+      } else {
+        if (split) GL128(true, 1, 1, false); else GL128(false, 1, 1, false);
+      }
     } else {
-      if (split) GL128(true, 1, 2); else GL128(false, 1, 2);
+      if (split) GL128(true, 1, 2, false); else GL128(false, 1, 2, false);
     }
 #undef GL128
     return oryx_check_launch();
