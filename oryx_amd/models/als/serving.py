@@ -23,6 +23,7 @@ from __future__ import annotations
 import logging
 import math
 import threading
+import time
 from typing import Collection, Dict, Iterable, Iterator, List, Optional, Sequence, Set, Tuple
 
 import numpy as np
@@ -72,7 +73,10 @@ class TopNBatcher:
 
     Requests queue up while a launch runs; the worker takes everything queued (up to
     ``max_batch``), optionally waiting ``wait_s`` for more, and answers each request's event.
-    With ``max_batch <= 1`` requests run inline on the caller's thread.
+    A request that finds no launch running, nothing queued and the last launch uncontended (and
+    no ``wait_s``) runs inline on its own thread -- a lone client pays no hand-off to the
+    worker (20M x 250 at 1 worker: 6.97 -> 6.27 ms mean, p99 12.9 -> 6.5 ms).  With
+    ``max_batch <= 1`` requests always run inline.
     """
 
     def __init__(self, index: "topn_ops.ItemIndex", max_batch: int, wait_s: float):
@@ -84,34 +88,57 @@ class TopNBatcher:
         self._thread = None
         self._closed = False
         self._contended = False
+        self._busy = False        # a launch (inline or by the worker) is running
         self._last_scan_s = 0.0
         self.batches = 0
         self.requests = 0
+        self.inline = 0
 
     def submit(self, q: "topn_ops.TopNQuery"):
         if self.max_batch <= 1:
             return self.index.scan([q])[0]
         slot = [q, None, None, threading.Event()]
         with self._cv:
-            if self._thread is None:
-                self._thread = threading.Thread(target=self._run, name="OryxTopNBatcher",
-                                                daemon=True)
-                self._thread.start()
-            self._queue.append(slot)
-            self._cv.notify()
+            # (not after a contended launch: concurrent clients keep being batched)
+            inline = not self._busy and not self._queue and not self._contended and \
+                self.wait_s == 0 and not self._closed
+            if inline:
+                self._busy = True
+            else:
+                if self._thread is None:
+                    self._thread = threading.Thread(target=self._run, name="OryxTopNBatcher",
+                                                    daemon=True)
+                    self._thread.start()
+                self._queue.append(slot)
+                self._cv.notify()
+        if inline:
+            t0 = time.monotonic()
+            try:
+                return self.index.scan([q])[0]
+            finally:
+                self._last_scan_s = time.monotonic() - t0
+                with self._cv:
+                    self._busy = False
+                    self.batches += 1
+                    self.requests += 1
+                    self.inline += 1
+                    # requests that queued up meanwhile go to the worker (batched)
+                    self._contended = bool(self._queue)
+                    self._cv.notify_all()
         slot[3].wait()
         if slot[2] is not None:
             raise slot[2]
         return slot[1]
 
     def _run(self) -> None:
-        import time
         while True:
             with self._cv:
-                while not self._queue and not self._closed:
+                while (not self._queue or self._busy) and not self._closed:
                     self._cv.wait()
                 if self._closed and not self._queue:
                     return
+                while self._busy:          # closing: let an inline launch finish first
+                    self._cv.wait()
                 # wait for stragglers when asked to, or when requests queued up while the
                 # previous launch ran (concurrent clients): a tenth of that launch's time
                 wait = self.wait_s
@@ -126,6 +153,7 @@ class TopNBatcher:
                         self._cv.wait(left)
                 batch = self._queue[:self.max_batch]
                 del self._queue[:len(batch)]
+                self._busy = True
             t_scan = time.monotonic()
             try:
                 res = self.index.scan([b[0] for b in batch])
@@ -135,10 +163,12 @@ class TopNBatcher:
                 for b in batch:
                     b[2] = e
             self._last_scan_s = time.monotonic() - t_scan
-            self.batches += 1
-            self.requests += len(batch)
             with self._cv:
+                self.batches += 1
+                self.requests += len(batch)
                 self._contended = bool(self._queue) or len(batch) > 1
+                self._busy = False
+                self._cv.notify_all()
             for b in batch:
                 b[3].set()
 
