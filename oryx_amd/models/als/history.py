@@ -86,10 +86,13 @@ class RatingsHistory:
         return len(self._segs)
 
     def resident_bytes(self) -> int:
-        return sum(int(sg.u.numel()) * (4 + 4 + 8 + 8) for sg in self._segs.values())
+        segs = list(self._segs.values()) + list(self._unkeyed.values())
+        return sum(int(sg.u.numel()) * (4 + 4 + 8 + 8) for sg in segs)
 
     def clear(self) -> None:
+        """Drop every cached parse (keyed segments and remembered new intervals)."""
         self._segs.clear()
+        self._unkeyed.clear()
 
     # ------------------------------------------------------------------ parse
     def _parse_range(self, buf, off: int, nbytes: int, n_lines: int) -> _Segment:

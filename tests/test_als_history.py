@@ -151,3 +151,14 @@ def test_history_adopts_new_interval_parse_cpu(tmp_path, monkeypatch):
     _same(want[:2], got[:2])
     _same(want[3:], got[3:])
     assert len(ref[0]) == 800
+
+
+def test_history_clear_drops_everything_cpu(monkeypatch):
+    monkeypatch.setattr(RatingsHistory, "UNKEYED_MIN_BYTES", 1)
+    gen = np.random.default_rng(10)
+    h = RatingsHistory()
+    h.parse_ratings(TextLines.from_strings(_lines(gen, 300, 50, 50)), ingest.IdDict(),
+                    ingest.IdDict(), 0)
+    assert h.resident_bytes() > 0
+    h.clear()
+    assert len(h) == 0 and h.resident_bytes() == 0
