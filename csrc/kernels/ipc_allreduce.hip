@@ -16,7 +16,9 @@
 // rewrites a slot only two calls later, after it has seen every peer arrive at the call in
 // between -- which each peer does only after finishing its reads of the call before -- so two
 // slots suffice.  The flag wait is bounded (timeout_s, 120 s by default): a peer that never
-// arrives sets *err instead of hanging the GPU; the host checks it (parallel/ipc.py).
+// arrives sets *err instead of hanging the GPU, and the call's output (and that of every later
+// call until the host clears *err) is NaN rather than a sum over a stale slot; the host checks
+// and clears it (parallel/ipc.py).
 #include <cstring>
 
 #include "common.h"
@@ -65,6 +67,15 @@ __global__ __launch_bounds__(256) void ipc_signal_reduce(float* __restrict__ out
     }
   }
   __syncthreads();
+  // a peer that never arrived (this block's wait or any other block's) poisons the result
+  // with NaN instead of summing its stale slot: the caller's tensor is visibly wrong even
+  // before the host reads *err
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+         i += (long long)gridDim.x * 256)
+      out[i] = __builtin_nanf("");
+    return;
+  }
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256) {
     float acc = 0.f;

@@ -41,8 +41,12 @@
 
 namespace {
 
-// "ORY2": frames checksummed with CRC-32C (the first format, "ORYL", used the IEEE CRC-32)
+// "ORY2": frames checksummed with CRC-32C.  The first format, "ORYL", used the IEEE CRC-32
+// over the same bytes; its frames are still read (the checksum is picked by magic) and new
+// records are appended after them in the current format, so a log directory written by an
+// older build keeps every record and offset.
 constexpr uint32_t kMagic = 0x3259524Fu;
+constexpr uint32_t kMagicV1 = 0x4F52594Cu;
 constexpr size_t kHeader = 4 + 4 + 8 + 8 + 4 + 4;
 constexpr uint32_t kNullKey = 0xFFFFFFFFu;
 
@@ -52,17 +56,23 @@ constexpr uint32_t kNullKey = 0xFFFFFFFFu;
 // update messages and the speed layer appends ~15 MB of UP rows per micro-batch.  CPUs without
 // SSE4.2 take a slicing-by-8 table of the same polynomial.
 uint32_t crc_tab[8][256];
+uint32_t ieee_tab[8][256];   // legacy "ORYL" frames
 bool crc_hw = false;
 
-void init_crc() {
+void init_table(uint32_t tab[8][256], uint32_t poly) {
   for (uint32_t i = 0; i < 256; ++i) {
     uint32_t c = i;
-    for (int k = 0; k < 8; ++k) c = (c & 1) ? 0x82F63B78u ^ (c >> 1) : c >> 1;
-    crc_tab[0][i] = c;
+    for (int k = 0; k < 8; ++k) c = (c & 1) ? poly ^ (c >> 1) : c >> 1;
+    tab[0][i] = c;
   }
   for (uint32_t i = 0; i < 256; ++i)
     for (int t = 1; t < 8; ++t)
-      crc_tab[t][i] = (crc_tab[t - 1][i] >> 8) ^ crc_tab[0][crc_tab[t - 1][i] & 0xFF];
+      tab[t][i] = (tab[t - 1][i] >> 8) ^ tab[0][tab[t - 1][i] & 0xFF];
+}
+
+void init_crc() {
+  init_table(crc_tab, 0x82F63B78u);
+  init_table(ieee_tab, 0xEDB88320u);
   __builtin_cpu_init();
   crc_hw = __builtin_cpu_supports("sse4.2");
 }
@@ -81,7 +91,7 @@ __attribute__((target("sse4.2"))) uint32_t crc32c_hw(const uint8_t* p, size_t n,
   return c32;
 }
 
-uint32_t crc32c_table(const uint8_t* p, size_t n, uint32_t crc) {
+uint32_t crc_sliced(const uint32_t (*crc_tab)[256], const uint8_t* p, size_t n, uint32_t crc) {
   while (n >= 8) {
     uint32_t lo, hi;
     memcpy(&lo, p, 4);
@@ -105,7 +115,17 @@ struct CrcInit {
 } crc_init_at_load;
 
 inline uint32_t crc32(const uint8_t* p, size_t n, uint32_t crc = 0) {
-  return ~(crc_hw ? crc32c_hw(p, n, ~crc) : crc32c_table(p, n, ~crc));
+  return ~(crc_hw ? crc32c_hw(p, n, ~crc) : crc_sliced(crc_tab, p, n, ~crc));
+}
+
+inline bool known_magic(uint32_t m) { return m == kMagic || m == kMagicV1; }
+
+// Checksum of a complete frame at `f` with `plen` payload bytes: the 16 offset|ts bytes at
+// +8, then the payload, under the polynomial its magic names.
+inline uint32_t frame_crc(uint32_t magic, const uint8_t* f, size_t plen) {
+  if (magic == kMagicV1)
+    return ~crc_sliced(ieee_tab, f + kHeader, plen, crc_sliced(ieee_tab, f + 8, 16, ~0u));
+  return crc32(f + kHeader, plen, crc32(f + 8, 16));
 }
 
 thread_local std::string g_err;
@@ -251,16 +271,14 @@ int64_t scan_segment(const std::string& path, int64_t base, int64_t* end_pos,
       uint64_t off;
       memcpy(&magic, h, 4); memcpy(&crc, h + 4, 4); memcpy(&off, h + 8, 8);
       memcpy(&klen, h + 24, 4); memcpy(&vlen, h + 28, 4);
-      if (magic != kMagic) { bad = true; break; }
+      if (!known_magic(magic)) { bad = true; break; }
       size_t plen = (klen == kNullKey ? 0 : klen) + (size_t)vlen;
       if (at + kHeader + plen > (size_t)got) {
         if (kHeader + plen > buf.size()) buf.resize(kHeader + plen);
         straddle = true;
         break;
       }
-      uint32_t c = crc32(h + 8, 16);
-      c = crc32(h + kHeader, plen, c);
-      if (c != crc) { bad = true; break; }
+      if (frame_crc(magic, h, plen) != crc) { bad = true; break; }
       at += kHeader + plen;
       next = (int64_t)off + 1;
     }
@@ -278,6 +296,40 @@ int64_t scan_segment(const std::string& path, int64_t base, int64_t* end_pos,
   close(fd);
   *end_pos = pos;
   return next;
+}
+
+// Whether bytes [end_pos, size) of a segment can be the torn tail of an interrupted append:
+// shorter than a frame header, all zeros (a crashed write on a filesystem that had already
+// extended the file), or a single frame of a known format that runs to (or past) the end of
+// the file.  Anything else -- an unknown magic with data behind it, or a bad frame followed by
+// more bytes -- is not a torn write.
+bool torn_tail(const std::string& path, int64_t end_pos, int64_t size) {
+  const int64_t rem = size - end_pos;
+  if (rem < (int64_t)kHeader) return true;
+  int fd = open(path.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  std::vector<uint8_t> buf((size_t)std::min<int64_t>(rem, 1 << 20));
+  const ssize_t got = pread(fd, buf.data(), buf.size(), end_pos);
+  bool zeros = got == (ssize_t)buf.size();
+  for (ssize_t i = 0; zeros && i < got; ++i) zeros = buf[(size_t)i] == 0;
+  if (zeros && rem > (int64_t)buf.size()) {
+    // scan the rest of a large zero tail in blocks
+    for (int64_t at = end_pos + (int64_t)buf.size(); zeros && at < size;) {
+      const ssize_t g = pread(fd, buf.data(), buf.size(), at);
+      if (g <= 0) break;
+      for (ssize_t i = 0; zeros && i < g; ++i) zeros = buf[(size_t)i] == 0;
+      at += g;
+    }
+  }
+  close(fd);
+  if (zeros) return true;
+  if (got < (ssize_t)kHeader) return false;
+  uint32_t magic, klen, vlen;
+  memcpy(&magic, buf.data(), 4); memcpy(&klen, buf.data() + 24, 4);
+  memcpy(&vlen, buf.data() + 28, 4);
+  if (!known_magic(magic)) return false;
+  const int64_t flen = (int64_t)kHeader + (klen == kNullKey ? 0 : (int64_t)klen) + (int64_t)vlen;
+  return flen >= rem;
 }
 
 struct Reader {
@@ -334,7 +386,7 @@ void reader_seek(Reader* r, int64_t offset) {
     uint64_t off;
     memcpy(&magic, hdr, 4); memcpy(&off, hdr + 8, 8); memcpy(&klen, hdr + 24, 4);
     memcpy(&vlen, hdr + 28, 4);
-    if (magic != kMagic) break;
+    if (!known_magic(magic)) break;
     int64_t plen = (klen == kNullKey ? 0 : klen) + (int64_t)vlen;
     struct stat st;
     if (fstat(r->fd, &st) != 0 || st.st_size < r->pos + (int64_t)kHeader + plen) break;
@@ -452,9 +504,21 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
     if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN);
     return fail("open segment");
   }
-  // truncate any torn tail left by a crashed writer
+  // truncate a torn tail left by a crashed writer -- but only a tail that can be one: bytes
+  // past the last good frame that are not themselves followed by more data (a frame with an
+  // unknown magic or a bad checksum in the middle of a segment is corruption, and truncating
+  // there would silently drop every later record and re-issue committed offsets)
   struct stat st;
-  if (fstat(fd, &st) == 0 && st.st_size > end_pos) { if (ftruncate(fd, end_pos) != 0) {} }
+  if (fstat(fd, &st) == 0 && st.st_size > end_pos) {
+    if (!torn_tail(path, end_pos, (int64_t)st.st_size)) {
+      close(fd);
+      if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN);
+      errno = 0;
+      return fail("refusing to append: segment " + path + " holds unreadable data at byte " +
+                  std::to_string(end_pos) + " followed by more data (corrupt or unknown format)");
+    }
+    if (ftruncate(fd, end_pos) != 0) {}
+  }
   const size_t n = which.size();
   std::vector<size_t> at(n + 1);
   at[0] = 0;
@@ -662,15 +726,14 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
       int64_t ts;
       memcpy(&magic, h, 4); memcpy(&crc, h + 4, 4); memcpy(&off, h + 8, 8);
       memcpy(&ts, h + 16, 8); memcpy(&klen, h + 24, 4); memcpy(&vlen, h + 28, 4);
-      if (magic != kMagic) { r->blk_pos = -1; break; }
+      if (!known_magic(magic)) { r->blk_pos = -1; break; }
       size_t kl = klen == kNullKey ? 0 : klen;
       size_t plen = kl + vlen;
       // the whole frame, so header and payload are contiguous in the block
       const uint8_t* f = reader_bytes(r, r->pos, kHeader + plen);
       if (!f) break;
       const uint8_t* pl = f + kHeader;
-      uint32_t c = crc32(f + 8, 16);
-      if (crc32(pl, plen, c) != crc) {
+      if (frame_crc(magic, f, plen) != crc) {
         r->blk_pos = -1;
         // A torn or in-progress write can only be the tail of the segment; a bad frame with
         // a complete frame header written after it is corruption, reported instead of being
@@ -787,7 +850,7 @@ long long oryx_reader_poll_frames(void* rh, char* out, long long out_cap, int ma
       const uint8_t* h = reinterpret_cast<const uint8_t*>(out) + p;
       uint32_t magic, klen, vlen;
       memcpy(&magic, h, 4); memcpy(&klen, h + 24, 4); memcpy(&vlen, h + 28, 4);
-      if (magic != kMagic) break;
+      if (!known_magic(magic)) break;
       const size_t plen = (klen == kNullKey ? 0 : klen) + (size_t)vlen;
       if (p + kHeader + plen > (size_t)got) {
         if (at.empty() && (long long)(kHeader + plen) > out_cap)
@@ -819,10 +882,11 @@ long long oryx_reader_poll_frames(void* rh, char* out, long long out_cap, int ma
     oryx_ff::parallel_ranges(n, 512, [&](long long lo, long long hi, int) {
       for (long long j = lo; j < hi; ++j) {
         const uint8_t* f = reinterpret_cast<const uint8_t*>(out) + at[(size_t)j];
-        uint32_t crc, klen, vlen;
-        memcpy(&crc, f + 4, 4); memcpy(&klen, f + 24, 4); memcpy(&vlen, f + 28, 4);
+        uint32_t magic, crc, klen, vlen;
+        memcpy(&magic, f, 4); memcpy(&crc, f + 4, 4); memcpy(&klen, f + 24, 4);
+        memcpy(&vlen, f + 28, 4);
         const size_t plen = (klen == kNullKey ? 0 : klen) + (size_t)vlen;
-        if (crc32(f + kHeader, plen, crc32(f + 8, 16)) != crc) bad[(size_t)j] = 1;
+        if (frame_crc(magic, f, plen) != crc) bad[(size_t)j] = 1;
       }
     });
     long long good = n;
@@ -910,7 +974,7 @@ long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long 
       uint64_t off;
       memcpy(&magic, h, 4); memcpy(&crc, h + 4, 4); memcpy(&off, h + 8, 8);
       memcpy(&klen, h + 24, 4); memcpy(&vlen, h + 28, 4);
-      if (magic != kMagic) { got = 0; break; }
+      if (!known_magic(magic)) { got = 0; break; }
       size_t kl = klen == kNullKey ? 0 : klen;
       size_t plen = kl + vlen;
       if (at + kHeader + plen > (size_t)got) {
@@ -920,9 +984,7 @@ long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long 
         break;
       }
       // crc covers offset | ts | key | value (the 16 header bytes at +8 and the payload)
-      uint32_t c = crc32(h + 8, 16);
-      c = crc32(h + kHeader, plen, c);
-      if (c != crc) {
+      if (frame_crc(magic, h, plen) != crc) {
         *out_used = used;
         fail("corrupt record (crc mismatch) in " + dir + " at offset " +
              std::to_string(r->next_offset));

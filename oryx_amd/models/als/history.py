@@ -156,10 +156,11 @@ class RatingsHistory:
             mi = torch.from_numpy(items.merge_from(sg.items)).to(self.device)
             if sg.u.numel():
                 cols.append((mu[sg.u.long()], mi[sg.i.long()], sg.s, sg.ts))
-        if keyed:
-            # aged-out part files (no longer among the past data) leave the cache
-            for k in [k for k in self._segs if k not in keyed]:
-                del self._segs[k]
+        # aged-out part files (no longer among the past data) leave the cache -- also when
+        # none of this generation's input is keyed (every past file aged out, or past data
+        # without file identities): the cache must never pin segments nothing names
+        for k in [k for k in self._segs if k not in keyed]:
+            del self._segs[k]
         if not cols:
             e = np.zeros(0, dtype=np.int64)
             return e, e.copy(), np.zeros(0, dtype=np.float64), e.copy()

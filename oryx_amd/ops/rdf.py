@@ -642,6 +642,8 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
         if split.cat_left is not None:
             parts.append(split.cat_left.double().reshape(T, -1))
         host = torch.cat(parts, 1).cpu().numpy()
+        if ctx.is_distributed:
+            dist.check_collectives(ctx)      # see _train_device
         w = [p_.shape[1] for p_ in parts]
         cut = np.cumsum([0] + w)
         feat_h = host[:, cut[0]:cut[1]].astype(np.int64)
@@ -819,6 +821,11 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
         # per level sizes every later histogram, split search and all-reduce to the live
         # nodes (deep levels of a forest are mostly leaves)
         live = int(is_split.sum(1).max()) if depth < max_depth else 0
+        if ctx.is_distributed:
+            # the split search above consumed this level's all-reduced histograms: a one-shot
+            # all-reduce whose peer never arrived must fail the forest here, not grow trees
+            # from NaN statistics (the host already waited on the device for `live`)
+            dist.check_collectives(ctx)
         if live > 0:
             _route(data, node_of, W, split, child_base, B, count_visits=False)
         vis = visits

@@ -248,6 +248,12 @@ class ItemIndex:
     def _matrix(self):
         """(device matrix pointer owner, row stride) the kernel reads, and the permutation."""
         if self.borrowed:
+            # device_rows() applies every store write so far; writes that landed after this
+            # index's last refresh may have removed, reused or re-bucketed rows the
+            # permutation still names: bring the permutation up to the same version first
+            # (anything later still is filtered from the results in _launch)
+            if self.version != self.store.version:
+                self.refresh()
             mat, ld = self.store.device_rows()
             return mat, ld, self.perm
         return self.Ys, self.kp, None
@@ -342,11 +348,19 @@ class ItemIndex:
         v, i = torch.topk(sc, m, dim=1)
         pos = torch.gather(rw, 1, i)
         v_h, pos_h = v.cpu().numpy(), pos.cpu().numpy()
+        valid_h = self.store._host_valid if self.borrowed else None
         out = []
         for j, q in enumerate(qs):
             vj, pj = v_h[j, :q.how_many], pos_h[j, :q.how_many]
             keep = np.isfinite(vj) & (pj >= 0)
-            out.append((self.row_of_pos_h[pj[keep]], vj[keep]))
+            rows = self.row_of_pos_h[pj[keep]]
+            vj = vj[keep]
+            if valid_h is not None and len(rows):
+                # a row removed between the permutation and the launch is never returned
+                live = valid_h[np.minimum(rows, len(valid_h) - 1)] & (rows < len(valid_h))
+                if not live.all():
+                    rows, vj = rows[live], vj[live]
+            out.append((rows, vj))
         return out
 
     # ------------------------------------------------------------------ all scores

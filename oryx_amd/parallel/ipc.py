@@ -12,11 +12,13 @@ the gloo control group.
 
 Safety: the reducer runs a self-test against ``torch.distributed.all_reduce`` when it is
 created (all ranks agree on the verdict); a peer that never arrives makes the kernel stop
-waiting after 120 s and set an error flag (``check()``) instead of hanging the GPU.
-Tensors larger than the slot capacity, non-fp32 tensors and multi-node worlds use RCCL.
+waiting after 120 s, set an error flag and write NaN instead of the sum (``check()`` raises
+and clears the flag) instead of hanging the GPU.  Tensors larger than the slot capacity,
+non-fp32 tensors and multi-node worlds use RCCL.
 
-``ORYX_IPC_ALLREDUCE=1`` enables it for multi-rank CUDA (RCCL) worlds on one node and for a
-forced world of one (``ORYX_FORCE_COLLECTIVES=1``); it is off by default.
+It is on by default for multi-rank CUDA (RCCL) worlds on one node and for a forced world of
+one (``ORYX_FORCE_COLLECTIVES=1``) when the self-test passes; ``ORYX_IPC_ALLREDUCE=0`` turns
+it off.
 """
 
 from __future__ import annotations
@@ -108,10 +110,16 @@ class IpcAllReduce:
         return t
 
     def check(self) -> None:
-        """Raise if some call timed out waiting for a peer (synchronises the stream)."""
+        """Raise if some call timed out waiting for a peer (synchronises the stream).
+
+        The error flag is sticky on the device -- every call after a timeout returns NaN --
+        until this method reports it; it is cleared when raising, so a caller that recovers
+        (e.g. an elastic restart of the collective) starts from a clean flag."""
         e = int(self.err.item())
         if e:
-            raise RuntimeError("IPC all-reduce: rank %d never arrived" % (e - 1))
+            self.err.zero_()
+            raise RuntimeError("IPC all-reduce: rank %d never arrived (results since the "
+                               "timeout are NaN)" % (e - 1))
 
     def self_test(self) -> bool:
         """Sum rank-dependent probes both ways; True when every rank matched RCCL."""
@@ -144,8 +152,8 @@ def _single_node(ctx) -> bool:
 def maybe_create(ctx) -> Optional[IpcAllReduce]:
     """The node's reducer when enabled and its self-test passes (collective: every rank of
     ``ctx`` calls it); else None."""
-    mode = os.environ.get("ORYX_IPC_ALLREDUCE")
-    if mode != "1" or ctx.device.type != "cuda" or ctx.backend != "nccl":
+    mode = os.environ.get("ORYX_IPC_ALLREDUCE", "1")
+    if mode == "0" or ctx.device.type != "cuda" or ctx.backend != "nccl":
         return None
     if ctx.world_size > 16 or ctx.group is not None:
         return None

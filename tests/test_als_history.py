@@ -81,17 +81,18 @@ def test_history_evicts_aged_out_parts_cpu(tmp_path):
     assert len(h) == 3
     os.remove(paths[0])
     os.rmdir(os.path.dirname(paths[0]))
-    # an unkeyed parse (e.g. the evaluation's test data) evicts nothing
-    h.parse_ratings(TextLines.from_strings(_lines(gen, 10, 5, 5)), ingest.IdDict(),
-                    ingest.IdDict(), 0)
-    assert len(h) == 3
     h.parse_ratings(read_past_data(str(tmp_path)).values(), ingest.IdDict(), ingest.IdDict(), 0)
-    assert len(h) == 2 and h.stats["misses"] == 3 + 1     # + the unkeyed parse
+    assert len(h) == 2 and h.stats["misses"] == 3
     # a rewritten part file (new size / mtime) is parsed again
     with open(paths[1], "a") as f:
         f.write("u1,i1,1.0\n")
     h.parse_ratings(read_past_data(str(tmp_path)).values(), ingest.IdDict(), ingest.IdDict(), 0)
-    assert h.stats["misses"] == 5
+    assert h.stats["misses"] == 4 and len(h) == 2
+    # input with no keyed segment at all (every past file aged out) releases the cache too
+    # (segments nothing names must not stay resident on the device)
+    h.parse_ratings(TextLines.from_strings(_lines(gen, 10, 5, 5)), ingest.IdDict(),
+                    ingest.IdDict(), 0)
+    assert len(h) == 0 and h.resident_bytes() == 0
 
 
 def test_als_parse_ratings_with_history_decay_cpu(tmp_path):

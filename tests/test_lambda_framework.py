@@ -151,6 +151,62 @@ def test_torn_tail_is_truncated_not_spun_on(tmp_path):
     topic.close()
 
 
+def _legacy_frame(offset, value, key=None, ts=1234):
+    """One frame of the first log format ("ORYL", IEEE CRC-32 over offset|ts|key|value)."""
+    import struct
+    import zlib
+    k = b"" if key is None else key
+    body = struct.pack("<qq", offset, ts)
+    crc = zlib.crc32(k + value, zlib.crc32(body))
+    return (struct.pack("<II", 0x4F52594C, crc) + body
+            + struct.pack("<II", 0xFFFFFFFF if key is None else len(k), len(value)) + k + value)
+
+
+@pytest.mark.timeout(60)
+def test_legacy_format_segment_is_read_and_appended_to(tmp_path):
+    """A segment written by the first log format keeps its records: readers deliver them,
+    the end offset counts them and a new append continues after them."""
+    import os
+    root = str(tmp_path)
+    tlog.maybe_create_topic(root, "Old", 1)
+    seg = os.path.join(root, "Old", "0", "%020d.log" % 0)
+    with open(seg, "wb") as fh:
+        for i in range(3):
+            fh.write(_legacy_frame(i, b"old-%d" % i, key=b"k" if i == 1 else None))
+    topic = tlog.Topic(root, "Old")
+    assert topic.end_offset(0) == 3
+    assert topic.append(None, "new-3") == 3
+    recs = topic.reader(0, 0).poll(100, 100)
+    assert [r[3] for r in recs] == ["old-0", "old-1", "old-2", "new-3"]
+    assert recs[1][2] == "k"
+    # the bulk text read defers keyed records to poll(); from offset 2 on there are none
+    vals, n = topic.reader(0, 2).read_text(4)
+    assert n == 2 and vals == ["old-2", "new-3"]
+    topic.close()
+
+
+@pytest.mark.timeout(60)
+def test_unknown_frame_mid_segment_is_not_truncated(tmp_path):
+    """Bytes of an unknown format with more data behind them are corruption, not a torn
+    tail: an append fails loudly and leaves the segment as it was."""
+    import os
+    root = str(tmp_path)
+    tlog.maybe_create_topic(root, "Bad", 1)
+    topic = tlog.Topic(root, "Bad")
+    topic.append(None, "good-0")
+    topic.close()
+    seg = _segment_files(root, "Bad")[0]
+    junk = b"JUNK" + b"\x01" * 200
+    with open(seg, "ab") as fh:
+        fh.write(junk)
+    size = os.path.getsize(seg)
+    topic = tlog.Topic(root, "Bad")
+    with pytest.raises(Exception, match="refusing to append"):
+        topic.append(None, "after")
+    assert os.path.getsize(seg) == size
+    topic.close()
+
+
 @pytest.mark.timeout(60)
 def test_read_text_roll_then_poll_same_reader(tmp_path):
     """read_text rolling into the next segment drops the poll read-ahead block, so a later
