@@ -44,6 +44,9 @@ def main(argv=None) -> int:
                          "new ratings and trains on them plus all earlier ones (the past part "
                          "files -- the resident parsed history's steady state)")
     ap.add_argument("--next-ratings", type=int, default=1_000_000)
+    ap.add_argument("--test-fraction", type=float, default=0.0,
+                    help="oryx.ml.eval.test-fraction (the reference default is 0.1: the newest "
+                         "tenth of the interval's data is held out and AUC is evaluated)")
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -75,7 +78,7 @@ def main(argv=None) -> int:
         "oryx.als.iterations": args.iterations,
         "oryx.als.implicit": "true",
         "oryx.ml.eval.candidates": 1,
-        "oryx.ml.eval.test-fraction": 0.0,
+        "oryx.ml.eval.test-fraction": args.test_fraction,
         "oryx.gpu.device": args.device,
         "oryx.gpu.dtype": args.dtype,
     }, cfg.get_default())
@@ -111,6 +114,7 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         layer.run_interval(now)
         t_gen = time.perf_counter() - t0
+        sharded_path = layer._sharded()
         later = []
         for g in range(1, max(1, args.generations) if ctx.world_size == 1 else 1):
             before = dict(layer._update.phase_seconds)
@@ -131,11 +135,17 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         layer.run_follower()
         t_gen = time.perf_counter() - t0
+        sharded_path = layer._sharded()
     upd = layer._update
     phases = dict(getattr(upd, "phase_seconds", {}))
     if not ctx.is_main:
         later = []
     phases.update({"layer_" + k: v for k, v in layer.last_phases.items()})
+    # the layer's own phases plus the update's (whose sum is the layer's "update" phase)
+    lay = layer.last_phases
+    inner = sum(v for k, v in phases.items()
+                if not k.startswith("layer_") and k not in ("publish_y", "publish_x"))
+    attributed = inner + sum(v for k, v in lay.items() if k != "update")
     if ctx.is_main:
         # count what was published
         ut = tlog.Topic(work + "/log", "OryxUpdate")
@@ -146,11 +156,14 @@ def main(argv=None) -> int:
             "value": args.ratings / t_gen, "unit": "ratings/s", "higher_is_better": True,
             "n_gpus": ctx.world_size, "generation_s": t_gen, "log_append_s": t_ingest,
             "phase_s": phases, "update_messages": int(sum(ends)),
+            "attributed_s": attributed, "unattributed_s": t_gen - attributed,
             "later_generations": later,
             "config": {"ratings": args.ratings, "users": args.users, "items": args.items,
                        "features": args.features, "iterations": args.iterations,
                        "dtype": args.dtype, "partitions": args.partitions,
-                       "sharded": ctx.world_size > 1},
+                       "test_fraction": args.test_fraction,
+                       "sharded": bool(sharded_path),
+                       "forced_collectives": bool(ctx.forced)},
             "data": "synthetic power-law users x items, strengths 0.5..5, last-day timestamps",
         }
         print(json.dumps(rec), flush=True)

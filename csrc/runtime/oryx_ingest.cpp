@@ -325,6 +325,73 @@ long long oryx_dict_get(void* dh, const char* s, long long len) {
   return d->find(std::string_view(s, (size_t)len));
 }
 
+// ---- blob forms for the sharded batch layer's global dictionaries (parallel/shuffle.py):
+// keys travel between ranks as one byte blob plus end offsets, never as Python strings.
+
+// owner[c] = zlib crc32(key c) % world for keys [from, size) (the same owner function as
+// shuffle.owner_of_strings).  Returns the number of keys written.
+long long oryx_dict_owners(void* dh, long long from, int world, long long* owner) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  long long n = 0;
+  for (size_t c = (size_t)from; c < d->keys.size(); ++c, ++n) {
+    const std::string& k = d->keys[c];
+    const uLong h = crc32(0L, reinterpret_cast<const Bytef*>(k.data()), (uInt)k.size());
+    owner[n] = (long long)(h % (uLong)world);
+  }
+  return n;
+}
+
+// Inserts the n keys of blob (key j = blob[ends[j-1], ends[j])) in order; codes[j] = its
+// code.  Returns n.
+long long oryx_dict_encode_blob(void* dh, const char* blob, const long long* ends, long long n,
+                                long long* codes) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  long long at = 0;
+  for (long long j = 0; j < n; ++j) {
+    codes[j] = d->encode(std::string_view(blob + at, (size_t)(ends[j] - at)));
+    at = ends[j];
+  }
+  return n;
+}
+
+// As oryx_dict_encode_blob without inserting: codes[j] = -1 for keys not present.
+long long oryx_dict_find_blob(void* dh, const char* blob, const long long* ends, long long n,
+                              long long* codes) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  long long at = 0;
+  for (long long j = 0; j < n; ++j) {
+    codes[j] = d->find(std::string_view(blob + at, (size_t)(ends[j] - at)));
+    at = ends[j];
+  }
+  return n;
+}
+
+// The keys of codes[0..n) back to back in out; ends[j] = end offset of key j.  Returns bytes
+// used or -(bytes needed) when out is too small; an out-of-range code gives an empty key.
+long long oryx_dict_keys_blob_sel(void* dh, const long long* codes, long long n, char* out,
+                                  long long cap, long long* ends) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  const long long size = (long long)d->keys.size();
+  long long need = 0;
+  for (long long j = 0; j < n; ++j)
+    if (codes[j] >= 0 && codes[j] < size) need += (long long)d->keys[(size_t)codes[j]].size();
+  if (need > cap) return -need;
+  long long pos = 0;
+  for (long long j = 0; j < n; ++j) {
+    if (codes[j] >= 0 && codes[j] < size) {
+      const std::string& k = d->keys[(size_t)codes[j]];
+      memcpy(out + pos, k.data(), k.size());
+      pos += (long long)k.size();
+    }
+    ends[j] = pos;
+  }
+  return pos;
+}
+
 // Copies key `code` into out (cap bytes); returns its length (or -1).
 long long oryx_dict_key(void* dh, long long code, char* out, long long cap) {
   Dict* d = static_cast<Dict*>(dh);

@@ -364,9 +364,13 @@ const uint8_t* reader_bytes(Reader* r, int64_t pos, size_t n) {
   return r->blk.data();
 }
 
-// Position a reader at `offset` (clamped to [begin, end]).
+// Position a reader at `offset` (clamped to [begin, end]).  Frames before it are skipped in
+// 4 MB block reads (not two syscalls per frame: a consumer seeking to the end of a 3M-record
+// partition paid ~0.15 s), starting from the partition's cached end-of-log scan position
+// when that lies at or before the target (the common seek: to the end offset just read).
 void reader_seek(Reader* r, int64_t offset) {
-  const std::string& dir = r->topic->parts[r->part].dir;
+  Partition& P = r->topic->parts[r->part];
+  const std::string& dir = P.dir;
   std::vector<int64_t> segs = list_segments(dir);
   if (r->fd >= 0) { close(r->fd); r->fd = -1; }
   r->blk_pos = -1;
@@ -377,21 +381,44 @@ void reader_seek(Reader* r, int64_t offset) {
   r->seg_base = segs[idx];
   r->pos = 0;
   r->next_offset = segs[idx];
+  {
+    std::lock_guard<std::mutex> g(P.end_mu);
+    if (P.e_base == segs[idx] && P.e_next <= offset && P.e_next >= segs[idx]) {
+      r->pos = P.e_pos;
+      r->next_offset = P.e_next;
+    }
+  }
   r->fd = open(seg_name(dir, segs[idx]).c_str(), O_RDONLY);
-  // skip frames before offset
-  uint8_t hdr[kHeader];
-  while (r->fd >= 0 && r->next_offset < offset) {
-    if (pread(r->fd, hdr, kHeader, r->pos) != (ssize_t)kHeader) break;
-    uint32_t magic, klen, vlen;
-    uint64_t off;
-    memcpy(&magic, hdr, 4); memcpy(&off, hdr + 8, 8); memcpy(&klen, hdr + 24, 4);
-    memcpy(&vlen, hdr + 28, 4);
-    if (!known_magic(magic)) break;
-    int64_t plen = (klen == kNullKey ? 0 : klen) + (int64_t)vlen;
-    struct stat st;
-    if (fstat(r->fd, &st) != 0 || st.st_size < r->pos + (int64_t)kHeader + plen) break;
-    r->pos += kHeader + plen;
-    r->next_offset = (int64_t)off + 1;
+  if (r->fd < 0 || r->next_offset >= offset) return;
+  std::vector<uint8_t> buf(4u << 20);
+  while (r->next_offset < offset) {
+    const ssize_t got = pread(r->fd, buf.data(), buf.size(), r->pos);
+    if (got < (ssize_t)kHeader) break;
+    size_t at = 0;
+    bool straddle = false, stop = false;
+    while (at + kHeader <= (size_t)got && r->next_offset < offset) {
+      const uint8_t* h = buf.data() + at;
+      uint32_t magic, klen, vlen;
+      uint64_t off;
+      memcpy(&magic, h, 4); memcpy(&off, h + 8, 8); memcpy(&klen, h + 24, 4);
+      memcpy(&vlen, h + 28, 4);
+      if (!known_magic(magic)) { stop = true; break; }
+      const size_t plen = (klen == kNullKey ? 0 : klen) + (size_t)vlen;
+      if (at + kHeader + plen > (size_t)got) {
+        if (kHeader + plen > buf.size()) buf.resize(kHeader + plen);
+        straddle = true;
+        break;
+      }
+      at += kHeader + plen;
+      r->pos += (int64_t)(kHeader + plen);
+      r->next_offset = (int64_t)off + 1;
+    }
+    if (stop) break;
+    if (straddle) {
+      if ((size_t)got < buf.size() && at == 0) break;   // a frame still being written
+      continue;
+    }
+    if ((size_t)got < buf.size()) break;
   }
 }
 

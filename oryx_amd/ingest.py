@@ -64,6 +64,57 @@ class IdDict:
         b = key.encode("utf-8")
         return int(self._lib.oryx_dict_get(self._h, b, len(b)))
 
+    # ---- blob forms (keys as one uint8 buffer + int64 end offsets; no Python strings)
+    def owners(self, world: int, start: int = 0) -> np.ndarray:
+        """``zlib.crc32(key) % world`` of every key from code ``start`` on (int64)."""
+        out = np.empty(max(0, len(self) - start), dtype=np.int64)
+        if len(out):
+            self._lib.oryx_dict_owners(self._h, int(start), int(world), _ptr(out))
+        return out
+
+    def encode_blob(self, blob: np.ndarray, ends: np.ndarray) -> np.ndarray:
+        """Insert the keys of a blob in order; returns their codes."""
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        ends = np.ascontiguousarray(ends, dtype=np.int64)
+        out = np.empty(len(ends), dtype=np.int64)
+        if len(ends):
+            self._lib.oryx_dict_encode_blob(self._h, _ptr(blob), _ptr(ends), len(ends),
+                                            _ptr(out))
+        return out
+
+    def find_blob(self, blob: np.ndarray, ends: np.ndarray) -> np.ndarray:
+        """Codes of the keys of a blob (-1 when absent); inserts nothing."""
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        ends = np.ascontiguousarray(ends, dtype=np.int64)
+        out = np.empty(len(ends), dtype=np.int64)
+        if len(ends):
+            self._lib.oryx_dict_find_blob(self._h, _ptr(blob), _ptr(ends), len(ends),
+                                          _ptr(out))
+        return out
+
+    def keys_blob(self, codes: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """(blob, ends) of the keys of ``codes`` in that order (default: every key)."""
+        if codes is None:
+            codes = np.arange(len(self), dtype=np.int64)
+        codes = np.ascontiguousarray(codes, dtype=np.int64)
+        ends = np.empty(len(codes), dtype=np.int64)
+        if not len(codes):
+            return np.zeros(0, dtype=np.uint8), ends
+        cap = max(16 * len(codes), 1 << 12)
+        while True:
+            blob = np.empty(cap, dtype=np.uint8)
+            used = self._lib.oryx_dict_keys_blob_sel(self._h, _ptr(codes), len(codes),
+                                                     _ptr(blob), cap, _ptr(ends))
+            if used >= 0:
+                return blob[:used], ends
+            cap = -used
+
+    @classmethod
+    def from_blob(cls, blob: np.ndarray, ends: np.ndarray) -> "IdDict":
+        d = cls()
+        d.encode_blob(blob, ends)
+        return d
+
     def keys(self) -> List[str]:
         """Every key in code order (a copy)."""
         return list(self.key_list())
@@ -94,6 +145,29 @@ class IdDict:
                 self._keys_cache.extend(raw[a:b].decode("utf-8")
                                         for a, b in zip(starts, ends.tolist()))
         return self._keys_cache if len(self._keys_cache) == n else self._keys_cache[:n]
+
+
+def _ptr(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def blob_strings(blob: np.ndarray, ends: np.ndarray) -> List[str]:
+    """Python strings of a key blob (only where strings are really needed)."""
+    raw = bytes(memoryview(np.ascontiguousarray(blob, dtype=np.uint8)))
+    e = np.asarray(ends, dtype=np.int64).tolist()
+    s = [0] + e[:-1]
+    if raw.isascii():
+        text = raw.decode("ascii")
+        return [text[a:b] for a, b in zip(s, e)]
+    return [raw[a:b].decode("utf-8") for a, b in zip(s, e)]
+
+
+def strings_blob(keys: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
+    """(blob, ends) of Python strings."""
+    enc = [k.encode("utf-8") for k in keys]
+    ends = np.cumsum(np.fromiter((len(e) for e in enc), dtype=np.int64, count=len(enc)))
+    blob = np.frombuffer(b"".join(enc), dtype=np.uint8) if enc else np.zeros(0, np.uint8)
+    return blob, ends
 
 
 def parse_ratings(lines, users: IdDict, items: IdDict, default_ts: int,

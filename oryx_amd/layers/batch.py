@@ -328,16 +328,21 @@ class BatchLayer(AbstractLayer):
         if total <= 0:
             return 0
         ts = msg["ts"]
+        t0 = time.perf_counter()
         records = read_log_share(self.input_root, self.input_topic, msg["starts"], msg["ends"],
                                  dctx.rank, dctx.world_size)
+        ph = self.last_phases = {"drain": time.perf_counter() - t0}
         faults.point("batch.interval", timestamp=ts, records=len(records))
         log.info("Rank %d: update at %d with %d of %d new records", dctx.rank, ts,
                  len(records), total)
+        tp = time.perf_counter()
         past = read_past_data(self.data_dir, dctx.rank, dctx.world_size)
+        ph["read_past"] = time.perf_counter() - tp
         producer = None
         if self.update_topic and self.update_broker:
             producer = LogTopicProducer(self.update_broker, self.update_topic, self.config,
                                         async_=False, max_message=self.max_message)
+        tp = time.perf_counter()
         try:
             with rng.shared_seed_scope(msg["seed"]):
                 self._update.run_update(self._context, ts, records,
@@ -345,11 +350,14 @@ class BatchLayer(AbstractLayer):
         finally:
             if producer is not None:
                 producer.close()
+        ph["update"] = time.perf_counter() - tp
+        tp = time.perf_counter()
         save_interval_part(self.data_dir, ts, records, dctx.rank)
         dist.barrier(dctx)
         if dctx.is_main:
             _finish_interval_dir(self.data_dir, ts)
         dist.barrier(dctx)
+        ph["save_data"] = time.perf_counter() - tp
         return total
 
     def run_follower(self) -> int:

@@ -307,7 +307,10 @@ class MLUpdate(BatchLayerUpdate):
                 log.info("No update topic configured, not publishing models to a topic")
             return
         best_model_path = os.path.join(final_path, MODEL_FILE_NAME)
-        best_model = pmmlu.read(best_model_path)
+        # the PMML (with every ID of the model) is parsed only where it is needed: rank 0 sends
+        # it, the others only when the app publishes from it
+        best_model = pmmlu.read(best_model_path) if main or self.publish_needs_model() \
+            else None
         if main:
             if os.path.getsize(best_model_path) <= self.max_message_size:
                 model_update_topic.send("MODEL", pmmlu.to_string(best_model))
@@ -364,7 +367,11 @@ class MLUpdate(BatchLayerUpdate):
         params = combos[i % len(combos)]
         candidate_path = os.path.join(candidates_path, str(i))
         log.info("Building candidate %d with params %s", i, params)
+        t_split = time.perf_counter()
         train, test = self._split_train_test(new_msgs, past_msgs)
+        ph = getattr(self, "phase_seconds", None)
+        if isinstance(ph, dict):
+            ph["split"] = ph.get("split", 0.0) + time.perf_counter() - t_split
         ev = float("nan")
         n_train, n_test = self._global_count(len(train)), self._global_count(len(test))
         timing = {"candidate": i, "params": [str(p) for p in params], "train": n_train,
@@ -406,6 +413,12 @@ class MLUpdate(BatchLayerUpdate):
         tracing.record(dict(timing, event="candidate"))
         log.info("Model eval for params %s: %s (%s)", params, ev, candidate_path)
         return candidate_path, ev
+
+    def publish_needs_model(self) -> bool:
+        """Whether :meth:`publish_additional_model_data` on a non-zero rank of a sharded
+        generation reads the promoted model (the PMML); apps that publish from what each rank
+        built return False so those ranks skip parsing it."""
+        return True
 
     def build_timings(self, candidate_path: str) -> dict:
         """App-specific timing details of the last build (e.g. ALS iteration ms, ratings/s)."""

@@ -15,16 +15,13 @@ Equivalent of ``ALSUpdate`` (``[mllib]/als/ALSUpdate.java:78-498``) and its help
 * evaluation: AUC (implicit; per-user positives vs sampled negatives) or -RMSE, on device;
 * publishing: ``UP`` ``["Y",id,vec]`` rows first, then ``["X",id,vec,[known items]]``.
 
-Sharded (several ranks, :mod:`oryx_amd.layers.batch` sharded generations): each rank parses
-only its share of the lines; user / item strings get global codes from a distributed
-dictionary (:func:`oryx_amd.parallel.shuffle.unify_ids`, owner = crc32 % W -- the
-reference's parse-or-hash + reverse map, collision-free); events are routed to their user's
+Sharded (several ranks, :mod:`oryx_amd.layers.batch` sharded generations): see
+:mod:`.sharded` -- each rank parses its share (with its own resident history), IDs get
+global codes from native distributed dictionaries, events are routed once to their user's
 owner for the time-ordered aggregation (the reference's ``reduceByKey`` shuffle,
-``[mllib]/als/ALSUpdate.java:332-352``); the trainer re-partitions by item itself.  The test
-split boundary uses the global timestamp range; AUC / RMSE are per-rank partial sums
-all-reduced (``Evaluation.java:49-136``); each rank publishes its share of the Y rows, then of
-the X rows with the known items of the users it owns (``EnqueueFeatureVecsFn`` per
-partition).
+``[mllib]/als/ALSUpdate.java:332-352``), dense ids follow the trainer's row ownership so
+factors, ID strings and known items stay on their owner, and every rank writes and publishes
+its own rows.  The test split boundary uses the global timestamp range.
 """
 
 from __future__ import annotations
@@ -52,6 +49,7 @@ from . import evaluation
 from .trainer import ALSTrainer
 
 from .history import RatingsHistory
+from . import sharded
 
 __all__ = ["ALSUpdate", "aggregate_scores", "decay_rating", "parse_ratings"]
 
@@ -128,14 +126,20 @@ def aggregate_scores_device(u: np.ndarray, i: np.ndarray, s: np.ndarray, ts: np.
     dev = torch.device(device)
     if len(u) == 0:
         if to_host:
-            return u, i, s
+            return tuple(x.cpu().numpy() if isinstance(x, torch.Tensor) else x
+                         for x in (u, i, s))
         e = torch.zeros(0, dtype=torch.int64, device=dev)
         return e, e, torch.zeros(0, dtype=torch.float64, device=dev)
-    # dictionary codes travel as int32 (half the bytes of the host's int64)
-    ud = torch.from_numpy(np.ascontiguousarray(u, dtype=np.int32)).to(dev)
-    idv = torch.from_numpy(np.ascontiguousarray(i, dtype=np.int32)).to(dev)
-    tt = torch.from_numpy(np.ascontiguousarray(ts, dtype=np.int64)).to(dev)
-    vv = torch.from_numpy(np.ascontiguousarray(s, dtype=np.float64)).to(dev)
+    if isinstance(u, torch.Tensor):
+        # already on the device (the sharded path's routed events)
+        ud, idv = u.to(dev, torch.int32), i.to(dev, torch.int32)
+        tt, vv = ts.to(dev, torch.int64), s.to(dev, torch.float64)
+    else:
+        # dictionary codes travel as int32 (half the bytes of the host's int64)
+        ud = torch.from_numpy(np.ascontiguousarray(u, dtype=np.int32)).to(dev)
+        idv = torch.from_numpy(np.ascontiguousarray(i, dtype=np.int32)).to(dev)
+        tt = torch.from_numpy(np.ascontiguousarray(ts, dtype=np.int64)).to(dev)
+        vv = torch.from_numpy(np.ascontiguousarray(s, dtype=np.float64)).to(dev)
     ext = torch.stack([ud.max().long(), idv.max().long(), tt.min(), tt.max()]).cpu().tolist()
     n_u, n_i = int(ext[0]) + 1, int(ext[1]) + 1
     key = ud.long() * n_i + idv.long()
@@ -215,15 +219,16 @@ def _timestamps(lines: Sequence[str]) -> np.ndarray:
     return ts
 
 
-def write_features(path: str, ids: List[str], mat) -> None:
-    """``X/`` or ``Y/`` directory with one gzip part of ``[id,[floats]]`` JSON lines (the
-    reference's Spark text output with the gzip codec); ``mat`` is a float matrix or its
-    pre-formatted :class:`~oryx_amd.ops.textfmt.RowText`.  Lines are assembled and
-    compressed natively (multi-member gzip, one member per slice, threads)."""
+def write_features(path: str, ids, mat, part: int = 0) -> None:
+    """``X/`` or ``Y/`` directory with gzip part ``part`` of ``[id,[floats]]`` JSON lines (the
+    reference's Spark text output with the gzip codec); ``ids`` a list of strings or a key
+    (blob, ends) pair; ``mat`` is a float matrix or its pre-formatted
+    :class:`~oryx_amd.ops.textfmt.RowText`.  Lines are assembled and compressed natively
+    (multi-member gzip, one member per slice, threads)."""
     os.makedirs(path, exist_ok=True)
     rows = mat if isinstance(mat, textfmt.RowText) else textfmt.format_rows(mat)
-    block = ingest.assemble_row_messages("", list(ids), rows)
-    ingest.write_gzip(os.path.join(path, "part-00000.gz"), block.buf, level=1)
+    block = ingest.assemble_row_messages("", ids if isinstance(ids, tuple) else list(ids), rows)
+    ingest.write_gzip(os.path.join(path, "part-%05d.gz" % part), block.buf, level=1)
 
 
 def read_features(path: str) -> Tuple[List[str], np.ndarray]:
@@ -519,171 +524,38 @@ class ALSUpdate(MLUpdate):
         return pmml
 
     # ---------------------------------------------------------------- sharded path
-    def _parse_global(self, lines, ctx):
-        """This rank's lines -> (global user code, global item code, strength, ts) plus the
-        dictionaries' owner tables."""
-        users, items = ingest.IdDict(), ingest.IdDict()
-        u, i, s, ts = parse_ratings(lines, users, items, self.decay_factor,
-                                    self.decay_zero_threshold)
-        ucode, utab = shuffle.unify_ids(users.keys(), ctx)
-        icode, itab = shuffle.unify_ids(items.keys(), ctx)
-        gu = ucode[u] if len(u) else u
-        gi = icode[i] if len(i) else i
-        return gu, gi, s, ts, utab, itab
-
     def _build_sharded(self, context, lines, features, lam, alpha, candidate_path):
+        """Every rank builds from its share (:mod:`.sharded`)."""
         ctx = self._ctx(context)
-        W = ctx.world_size
-        ph = self.phase_seconds
-        t_parse = time.perf_counter()
-        gu, gi, s, ts, utab, itab = self._parse_global(lines, ctx)
-        ph["parse"] = ph.get("parse", 0.0) + time.perf_counter() - t_parse
-        tp = time.perf_counter()
-        # events of one user on one rank, for the time-ordered aggregation
-        gu, gi, s, ts = shuffle.route(gu % W, ctx, gu, gi, s, ts)
-        ph["shuffle"] = ph.get("shuffle", 0.0) + time.perf_counter() - tp
-        tp = time.perf_counter()
-        if ctx.device.type == "cuda":
-            au, ai, av = aggregate_scores_device(gu, gi, s, ts, self.implicit, ctx.device)
-        else:
-            au, ai, av = aggregate_scores(gu, gi, s, ts, self.implicit)
-        ph["aggregate"] = ph.get("aggregate", 0.0) + time.perf_counter() - tp
-        used_u = np.zeros(utab.total, dtype=np.int32)
-        used_i = np.zeros(itab.total, dtype=np.int32)
-        used_u[au] = 1
-        used_i[ai] = 1
-        used_u = shuffle.all_reduce_np(used_u, ctx) > 0
-        used_i = shuffle.all_reduce_np(used_i, ctx) > 0
-        nu, ni = int(used_u.sum()), int(used_i.sum())
-        n_ratings = int(sum(shuffle.all_gather_int(len(au), ctx)))
-        parse_s = time.perf_counter() - t_parse
-        if n_ratings == 0:
-            log.info("No ratings after aggregation")
-            return None
-        dense_u = np.cumsum(used_u) - 1
-        dense_i = np.cumsum(used_i) - 1
-        seed = rng.next_seed()
-        trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx, seed=seed,
-                             precision=self.precision)
-        t0 = time.perf_counter()
-        trainer.prepare(torch.from_numpy(dense_u[au]), torch.from_numpy(dense_i[ai]),
-                        torch.from_numpy(av.astype(np.float32)), nu, ni)
-        ph["csr_prepare"] = ph.get("csr_prepare", 0.0) + time.perf_counter() - t0
-        tp = time.perf_counter()
-        x_ids = shuffle.gather_strings(utab, ctx, keep=used_u)
-        y_ids = shuffle.gather_strings(itab, ctx, keep=used_i)
-        ph["ids_gather"] = ph.get("ids_gather", 0.0) + time.perf_counter() - tp
-        x_init = y_init = None
-        if self.warm_start and self.current_model_dir:
-            x_init, y_init = _warm_start_factors(self.current_model_dir, features, x_ids, y_ids)
-        tp = time.perf_counter()
-        f = trainer.train(self.iterations, x_init=x_init, y_init=y_init)
-        X = f.X.cpu().numpy()
-        Y = f.Y.cpu().numpy()
-        ph["train"] = ph.get("train", 0.0) + time.perf_counter() - tp
-        tp = time.perf_counter()
-        x_rows, y_rows = textfmt.format_rows(f.X), textfmt.format_rows(f.Y)
-        ph["format_rows"] = ph.get("format_rows", 0.0) + time.perf_counter() - tp
-        log.info("ALS (sharded, %d ranks) %d ratings, %d users, %d items, rank %d: %.3fs", W,
-                 n_ratings, nu, ni, features, time.perf_counter() - t0)
-        tp = time.perf_counter()
-        if ctx.is_main:
-            write_features(os.path.join(candidate_path, "X"), x_ids, x_rows)
-            write_features(os.path.join(candidate_path, "Y"), y_ids, y_rows)
-        ph["write_factors"] = ph.get("write_factors", 0.0) + time.perf_counter() - tp
-        pmml = pmmlu.build_skeleton_pmml()
-        pmml.add_extension("X", "X/")
-        pmml.add_extension("Y", "Y/")
-        pmml.add_extension("features", features)
-        pmml.add_extension("lambda", lam)
-        pmml.add_extension("implicit", self.implicit)
-        if self.implicit:
-            pmml.add_extension("alpha", alpha)
-        pmml.add_extension_content("XIDs", x_ids)
-        pmml.add_extension_content("YIDs", y_ids)
-        # every rank keeps what evaluation needs: factors, its dictionary share, dense maps
-        self._cache[candidate_path] = {
-            "x_ids": x_ids, "y_ids": y_ids, "X": X, "Y": Y, "utab": utab, "itab": itab,
-            "x_rows": x_rows, "y_rows": y_rows,
-            "dense_u": np.where(used_u, dense_u, -1), "dense_i": np.where(used_i, dense_i, -1)}
-        its = trainer.timings.get("iteration_ms", [])
-        self._timings[candidate_path] = {
-            "ratings": n_ratings, "users": nu, "items": ni, "ranks": W,
-            "parse_shuffle_aggregate_s": parse_s,
-            "prepare_s": trainer.timings.get("prepare_s"), "iteration_ms": its,
-            "ratings_per_s": (n_ratings * 1e3 / (sum(its) / len(its))) if its else None}
+        want_known = self.get_test_fraction() == 0.0 and not self.no_known_items
+        pmml, model = sharded.build(self, ctx, lines, features, lam, alpha, candidate_path,
+                                    want_known, history=self._history_for(ctx.device))
+        if model is not None:
+            self._cache[candidate_path] = {"sharded": model}
         return pmml
 
     def _evaluate_sharded(self, context, model_parent_path, test_data):
-        ctx = self._ctx(context)
-        f = self._cache[model_parent_path]
-        users, items = ingest.IdDict(), ingest.IdDict()
-        u, i, s, ts = parse_ratings(test_data, users, items, self.decay_factor,
-                                    self.decay_zero_threshold)
-        ucode = shuffle.lookup(users.keys(), f["utab"], ctx, mapping=f["dense_u"])
-        icode = shuffle.lookup(items.keys(), f["itab"], ctx, mapping=f["dense_i"])
-        # unknown test IDs keep a private negative code per string so aggregation still
-        # separates them (they are dropped afterwards)
-        gu = np.where(ucode[u] >= 0, ucode[u], -1 - u) if len(u) else u
-        gi = np.where(icode[i] >= 0, icode[i], -1 - i) if len(i) else i
-        W = ctx.world_size
-        owner = np.where(gu >= 0, gu % W, ctx.rank)
-        gu, gi, s, ts = shuffle.route(owner, ctx, gu, gi, s, ts)
-        # aggregate on compact codes (unknown IDs carry negative placeholders)
-        uu, uinv = np.unique(gu, return_inverse=True)
-        ii, iinv = np.unique(gi, return_inverse=True)
-        au, ai, av = aggregate_scores(uinv.astype(np.int64), iinv.astype(np.int64), s, ts,
-                                      self.implicit)
-        au, ai = (uu[au], ii[ai]) if len(au) else (au, ai)
-        device = ctx.device
-        X = torch.from_numpy(f["X"]).to(device)
-        Y = torch.from_numpy(f["Y"]).to(device)
-        mu = np.where(au >= 0, au, -1)
-        mi = np.where(ai >= 0, ai, -1)
-        if self.implicit:
-            known = (mu >= 0) & (mi >= 0)
-            items_all = np.unique(np.concatenate(shuffle.all_gather_var(
-                np.unique(mi[known]).astype(np.int64), ctx)))
-            tot, cnt = evaluation.auc_parts(X, Y, mu, mi, items_all, device=device)
-            tc = shuffle.all_reduce_np(np.array([tot, cnt], dtype=np.float64), ctx)
-            auc = float(tc[0] / tc[1]) if tc[1] > 0 else float("nan")
-            log.info("AUC: %s", auc)
-            return auc
-        se, n = evaluation.squared_error_parts(X, Y, mu, mi, av, device=device)
-        tc = shuffle.all_reduce_np(np.array([se, n], dtype=np.float64), ctx)
-        rmse = math.sqrt(tc[0] / tc[1]) if tc[1] > 0 else float("nan")
-        log.info("RMSE: %s", rmse)
-        return -rmse
+        return sharded.evaluate(self, self._ctx(context),
+                                self._cache[model_parent_path]["sharded"], test_data)
 
     def _publish_sharded(self, context, pmml, new_data, past_data, model_parent_path, topic):
         ctx = self._ctx(context)
-        W, R = ctx.world_size, ctx.rank
-        x_ids, x_rows, y_ids, y_rows = self._published_rows(pmml, model_parent_path)
-        mine = np.arange(R, len(y_ids), W)
-        log.info("Rank %d sending %d item / Y rows as model updates", R, len(mine))
-        # rows assembled natively into one block per rank (no Python string per message)
-        if len(mine):
-            topic.send_block("UP", ingest.assemble_row_messages(
-                "Y", [y_ids[j] for j in mine.tolist()], y_rows.take(mine)))
-        dist.barrier(ctx)
-        # users owned by this rank (crc32 owner of the ID) with their known items
-        all_lines = concat_lines([new_data, past_data])
-        if self.no_known_items:
-            owned = np.nonzero(shuffle.owner_of_strings(x_ids, W) == R)[0]
-            if len(owned):
-                topic.send_block("UP", ingest.assemble_row_messages(
-                    "X", [x_ids[j] for j in owned.tolist()], x_rows.take(owned)))
+        src = getattr(self, "promoted_from", None)
+        f = self._cache.get(src) if src else None
+        have = int(f is not None and "sharded" in f)
+        # every rank must take the same path: the winner of one candidate group (parallelism
+        # > 1) was built in memory only by that group's ranks
+        if int(shuffle.all_reduce_np(np.array([have], dtype=np.int64), ctx, op="min")[0]):
+            sharded.publish(self, ctx, f["sharded"], concat_lines([new_data, past_data]),
+                            topic)
         else:
-            kusers, kt = _known_items_sharded(all_lines, ctx)
-            xmap = {k: j for j, k in enumerate(x_ids)}
-            sel = sorted((xmap[uid], r) for r, uid in enumerate(kusers) if uid in xmap)
-            idx = np.array([j for j, _ in sel], dtype=np.int64)
-            log.info("Rank %d sending %d user / X rows as model updates", R, len(idx))
-            if len(idx):
-                topic.send_block("UP", ingest.assemble_row_messages(
-                    "X", [x_ids[j] for j in idx.tolist()], x_rows.take(idx), kt,
-                    np.array([r for _, r in sel], dtype=np.int64)))
-        dist.barrier(ctx)
+            sharded.publish_from_files(self, ctx, model_parent_path,
+                                       concat_lines([new_data, past_data]), topic)
+
+    def publish_needs_model(self) -> bool:
+        """The sharded publish works from each rank's build or the factor part files, never
+        from the PMML."""
+        return not self._sharded(self.dist_ctx) if self.dist_ctx is not None else True
 
     def build_timings(self, candidate_path: str) -> dict:
         return self._timings.pop(candidate_path, {})
@@ -823,42 +695,6 @@ class ALSUpdate(MLUpdate):
                     continue
                 (train if int(t[0]) < boundary else test).append(line)
         return train, test
-
-
-def _known_items_sharded(lines: Sequence[str], ctx):
-    """Known items of the users this rank owns (crc32 owner), from every rank's lines:
-    (user IDs, :class:`~oryx_amd.ops.textfmt.RowText` of each user's JSON item array).  The
-    per-pair decision (last event in time order, not a delete) is vectorised and the arrays
-    are written natively (``ingest.known_items_text``) -- no Python set per user."""
-    users, items = ingest.IdDict(), ingest.IdDict()
-    u, i, s, ts = ingest.parse_ratings(lines, users, items, default_ts=0)
-    uk, ik = users.keys(), items.keys()
-    W = ctx.world_size
-    # ship (user, item, strength, ts) rows to the user's owner as dictionary codes of a
-    # global table, then decide per pair by the last event
-    ucode, utab = shuffle.unify_ids(uk, ctx)
-    icode, itab = shuffle.unify_ids(ik, ctx)
-    gu = ucode[u] if len(u) else u
-    gi = icode[i] if len(i) else i
-    owner = shuffle.owner_of_strings(uk, W)[u] if len(u) else u
-    gu, gi, s, ts = shuffle.route(owner, ctx, gu, gi, s, ts)
-    ustr = shuffle.gather_strings(utab, ctx)
-    istr = shuffle.gather_strings(itab, ctx)
-    present = np.unique(gu)
-    user_list = [ustr[a] for a in present.tolist()]
-    if len(gu) == 0:
-        return user_list, textfmt.RowText(b"", np.zeros(0, dtype=np.int64))
-    # the last event of each pair in time order decides (a delete drops it): the explicit
-    # aggregation, sorted by (user, item) -- on the device when there is one
-    if ctx.device.type == "cuda":
-        ku, ki, _ = aggregate_scores_device(gu, gi, s, ts, False, ctx.device)
-    else:
-        ku, ki, _ = aggregate_scores(gu, gi, s, ts, False)
-    uidx = np.searchsorted(present, ku)
-    names = ingest.IdDict()
-    names.encode(istr)                  # code j == global item j
-    kt = ingest.known_items_text(names, uidx, ki, len(present))
-    return user_list, kt
 
 
 def known_items_json(lines: Sequence[str], device=None) -> Dict[str, str]:

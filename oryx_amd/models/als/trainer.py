@@ -276,6 +276,13 @@ class ALSTrainer:
             assert rows.shape[0] == hi - lo
             ok = ~torch.isnan(rows).any(1)
             dst[:hi - lo, :k] = torch.where(ok[:, None], rows, dst[:hi - lo, :k])
+        # rows without any rating are never solved (the CSRs' work lists skip them) and must
+        # not enter the other side's Gramian: they start, and stay, zero.  Only the sharded
+        # generation's dense ids have such rows (ids a padded owner shard does not use).
+        for csr, dst, n in ((self.csr_u, self.X, nu), (self.csr_i, self.Y, ni)):
+            empty = csr.row_ptr[1:n + 1] == csr.row_ptr[:n]
+            if n and bool(empty.any()):
+                dst[:n][empty] = 0.0
         self._publish_factors()
 
     def _publish_factors(self) -> None:

@@ -114,6 +114,10 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_csv_numeric_block", c_ll, [c_cp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp,
                                                c_ll])
     _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_dict_owners", c_ll, [c_vp, c_ll, c_i, c_vp])
+    _sig(lib, "oryx_dict_encode_blob", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_dict_find_blob", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_dict_keys_blob_sel", c_ll, [c_vp, c_vp, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_parse_up_batch", c_ll, [c_cp, c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_up_texts", c_ll, [c_vp, c_ll, c_vp, c_ll])
     _sig(lib, "oryx_up_ids", c_ll, [c_vp, c_ll])

@@ -250,3 +250,163 @@ def lookup(keys: Sequence[str], table: IdTable, ctx,
     if mapping is not None and len(codes):
         codes = np.where(codes >= 0, mapping[np.maximum(codes, 0)], -1)
     return codes
+
+
+# ---------------------------------------------------------------------- blob dictionaries
+# The sharded ALS batch layer's global dictionaries keep every key in native dictionaries
+# (ingest.IdDict) and move keys between ranks as byte blobs: no Python string per key on the
+# hot path (the string helpers above cost ~1 us per key per step).
+
+def _blob_reorder(blob: np.ndarray, ends: np.ndarray, order: np.ndarray
+                  ) -> Tuple[np.ndarray, np.ndarray]:
+    """Keys ``order`` of a (blob, ends) key list, as a new (blob, ends)."""
+    ends = np.asarray(ends, dtype=np.int64)
+    if len(order) == 0:
+        return np.zeros(0, dtype=np.uint8), np.zeros(0, dtype=np.int64)
+    starts = np.r_[0, ends[:-1]]
+    lens = ends - starts
+    lo = lens[order]
+    new_ends = np.cumsum(lo)
+    total = int(new_ends[-1])
+    # byte j of the output comes from starts[order[k]] + (j - new_start[k])
+    src = np.repeat(starts[order] - (new_ends - lo), lo) + np.arange(total, dtype=np.int64)
+    return np.ascontiguousarray(blob)[src], new_ends
+
+
+def route_blob(blob: np.ndarray, ends: np.ndarray, owner: np.ndarray, ctx: dist.DistContext
+               ) -> Tuple[np.ndarray, np.ndarray]:
+    """Send key j of a (blob, ends) list to rank ``owner[j]``; returns the received keys as
+    (blob, ends) in source-rank order, each source's keys in their original order."""
+    W = ctx.world_size
+    owner = np.asarray(owner, dtype=np.int64)
+    order = np.argsort(owner, kind="stable")
+    b, e = _blob_reorder(blob, ends, order)
+    lens = np.diff(np.r_[0, e])
+    cnt = np.bincount(owner, minlength=W)
+    kend = np.cumsum(cnt)
+    bend = np.r_[0, e][kend]
+    byte_counts = np.diff(np.r_[0, bend]).tolist()
+    dev = _dev(ctx)
+    got_lens = _exchange(torch.from_numpy(np.ascontiguousarray(lens)).to(dev), cnt.tolist(),
+                         ctx).cpu().numpy()
+    got_blob = _exchange(torch.from_numpy(np.ascontiguousarray(b)).to(dev), byte_counts,
+                         ctx).cpu().numpy()
+    return got_blob.astype(np.uint8, copy=False), np.cumsum(got_lens)
+
+
+class ShardedDict:
+    """A global string dictionary over the ranks of ``ctx``: key s is owned by rank
+    ``crc32(s) % W``; the owner numbers its keys in arrival order (source rank, then each
+    source's first-appearance order -- deterministic for deterministic inputs) in a native
+    :class:`~oryx_amd.ingest.IdDict` ``own``, and global code = ``offsets[owner]`` + the owner's
+    code, so global codes are dense in ``[0, total)`` and grouped by owner."""
+
+    def __init__(self, own, offsets: np.ndarray, ctx: dist.DistContext):
+        self.own = own
+        self.offsets = np.asarray(offsets, dtype=np.int64)
+        self.ctx = ctx
+
+    @property
+    def total(self) -> int:
+        return int(self.offsets[-1])
+
+    @property
+    def size(self) -> int:
+        """Keys this rank owns."""
+        return len(self.own)
+
+    @property
+    def lo(self) -> int:
+        return int(self.offsets[self.ctx.rank])
+
+    def owner_of(self, codes: np.ndarray) -> np.ndarray:
+        return np.searchsorted(self.offsets, np.asarray(codes), side="right") - 1
+
+    def owner_of_t(self, codes: torch.Tensor) -> torch.Tensor:
+        off = torch.as_tensor(self.offsets, device=codes.device)
+        return torch.searchsorted(off, codes, right=True) - 1
+
+    @classmethod
+    def build(cls, local, ctx: dist.DistContext) -> Tuple[np.ndarray, "ShardedDict"]:
+        """(global code of each key of the local dictionary ``local``, the dictionary)."""
+        from .. import ingest
+        if not ctx.is_distributed:
+            return np.arange(len(local), dtype=np.int64), cls(local, [0, len(local)], ctx)
+        blob, ends = local.keys_blob()
+        owner = local.owners(ctx.world_size)
+        rblob, rends = route_blob(blob, ends, owner, ctx)
+        own = ingest.IdDict()
+        local_codes = own.encode_blob(rblob, rends)
+        sizes = all_gather_int(len(own), ctx)
+        offsets = np.r_[0, np.cumsum(sizes)].astype(np.int64)
+        back = _reply(local_codes + offsets[ctx.rank], owner, ctx)
+        return back, cls(own, offsets, ctx)
+
+    def lookup(self, local) -> np.ndarray:
+        """Global codes of the keys of a local dictionary (-1 for keys nobody owns)."""
+        if not self.ctx.is_distributed:
+            blob, ends = local.keys_blob()
+            return self.own.find_blob(blob, ends)
+        blob, ends = local.keys_blob()
+        owner = local.owners(self.ctx.world_size)
+        rblob, rends = route_blob(blob, ends, owner, self.ctx)
+        c = self.own.find_blob(rblob, rends)
+        c = np.where(c >= 0, c + self.lo, -1)
+        return _reply(c, owner, self.ctx)
+
+    def all_keys_blob(self, keep: Optional[np.ndarray] = None,
+                      to_main: bool = False) -> Optional[Tuple[np.ndarray, np.ndarray]]:
+        """Every rank's keys in global code order as one (blob, ends) -- only the owned codes
+        with ``keep[code - lo]`` when given; on rank 0 only (None elsewhere) with
+        ``to_main``."""
+        codes = np.arange(self.size, dtype=np.int64)
+        if keep is not None:
+            codes = codes[np.asarray(keep, dtype=bool)[:self.size]]
+        blob, ends = self.own.keys_blob(codes)
+        if not self.ctx.is_distributed:
+            return blob, ends
+        lens = np.diff(np.r_[0, ends])
+        blobs = all_gather_var(blob, self.ctx)
+        lenss = all_gather_var(lens, self.ctx)
+        if to_main and not self.ctx.is_main:
+            return None
+        allb = np.concatenate(blobs) if blobs else np.zeros(0, np.uint8)
+        alll = np.concatenate(lenss) if lenss else np.zeros(0, np.int64)
+        return allb.astype(np.uint8, copy=False), np.cumsum(alll)
+
+
+def route_tensors(owner: torch.Tensor, ctx: dist.DistContext, *cols: torch.Tensor
+                  ) -> List[torch.Tensor]:
+    """:func:`route` for device tensors of one length (int64 / float64 / int32 / float32
+    columns packed into ONE all-to-all of 8-byte words): row j goes to rank ``owner[j]``."""
+    if not ctx.is_distributed:
+        return list(cols)
+    W = ctx.world_size
+    dev = _dev(ctx)
+    owner = owner.to(dev)
+    order = torch.argsort(owner, stable=True)
+    counts = torch.bincount(owner, minlength=W).cpu().tolist()
+    words = []
+    for c in cols:
+        c = c.to(dev)[order]
+        if c.dtype in (torch.float64, torch.int64):
+            words.append(c.contiguous().view(torch.int64))
+        elif c.dtype == torch.float32:
+            words.append(c.contiguous().view(torch.int32).to(torch.int64))
+        else:
+            words.append(c.to(torch.int64))
+    packed = torch.stack(words, 1) if words else torch.zeros((len(order), 0), dtype=torch.int64,
+                                                              device=dev)
+    recv = _exchange(packed, counts, ctx)
+    out = []
+    for j, c in enumerate(cols):
+        w = recv[:, j].contiguous()
+        if c.dtype == torch.float64:
+            out.append(w.view(torch.float64))
+        elif c.dtype == torch.int64:
+            out.append(w)
+        elif c.dtype == torch.float32:
+            out.append(w.to(torch.int32).view(torch.float32))
+        else:
+            out.append(w.to(c.dtype))
+    return out

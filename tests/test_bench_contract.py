@@ -125,7 +125,10 @@ def test_bench_batch_sharded_gloo_world_two():
     rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["config"]["sharded"] is True
     ph = rec["phase_s"]
-    for key in ("parse", "shuffle", "aggregate", "train", "publish_up"):
+    for key in ("parse", "dictionaries", "route", "aggregate", "train", "publish_up",
+                "layer_drain", "layer_update", "layer_save_data"):
         assert key in ph, ph
+    # every second of the generation is in some phase (within 10% + a little fixed cost)
+    assert rec["unattributed_s"] <= 0.1 * rec["generation_s"] + 0.5, rec
     # MODEL + one UP row per user and item that has ratings
     assert rec["update_messages"] > 2000
