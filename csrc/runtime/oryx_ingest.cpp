@@ -430,6 +430,11 @@ struct RatingChunk {
   // and merge; both dictionaries are locked by the caller)
   Dict* gu = nullptr;
   Dict* gi = nullptr;
+  // timestamps / strengths only (the train/test split): IDs are not encoded at all
+  bool no_ids = false;
+  // the raw text span [begin, end) of every parsed row's line (the time split copies lines)
+  bool want_spans = false;
+  std::vector<const char*> sp_b, sp_e;
 
   int32_t code(Side& sd, std::string_view k, bool stable) {
     uint32_t v;
@@ -525,7 +530,10 @@ struct RatingChunk {
           }
         }
         if (ok) {
-          if (gu) {
+          if (no_ids) {
+            u.push_back(0);
+            i.push_back(0);
+          } else if (gu) {
             u.push_back((int32_t)gu->encode(f[0]));
             i.push_back((int32_t)gi->encode(f[1]));
           } else {
@@ -534,6 +542,10 @@ struct RatingChunk {
           }
           s.push_back(sv);
           ts.push_back(tv);
+          if (want_spans) {
+            sp_b.push_back(p);
+            sp_e.push_back(le);
+          }
         } else if (strict && bad_line < 0) {
           bad_line = lines;
           return;
@@ -545,9 +557,155 @@ struct RatingChunk {
   }
 };
 
+// Chunks at line boundaries over the native threads, no dictionaries (see oryx_parse_ratings).
+long long parse_rows_no_ids(const char* buf, long long len, long long* out_u, long long* out_i,
+                            double* out_s, long long* out_ts, long long max_rows,
+                            long long default_ts, int strict) {
+  int P = 1;
+  if (len >= (1ll << 20))
+    P = (int)std::max<long long>(1, std::min<long long>(len / (256ll << 10),
+                                                       oryx_ff::native_threads()));
+  std::vector<const char*> cut((size_t)P + 1);
+  cut[0] = buf;
+  cut[(size_t)P] = buf + len;
+  for (int t = 1; t < P; ++t) {
+    const char* c = buf + len * t / P;
+    if (c < cut[(size_t)t - 1]) c = cut[(size_t)t - 1];
+    const char* nl = static_cast<const char*>(memchr(c, '\n', (size_t)(buf + len - c)));
+    cut[(size_t)t] = nl ? nl + 1 : buf + len;
+  }
+  std::vector<RatingChunk> ch((size_t)P);
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      ch[(size_t)t].no_ids = true;
+      ch[(size_t)t].parse(cut[(size_t)t], cut[(size_t)t + 1], default_ts, strict != 0);
+    }
+  });
+  long long lines_before = 0, o = 0;
+  for (int t = 0; t < P; ++t) {
+    if (ch[(size_t)t].bad_line >= 0) return -(lines_before + ch[(size_t)t].bad_line + 1);
+    lines_before += ch[(size_t)t].lines;
+  }
+  for (int t = 0; t < P; ++t) {
+    const RatingChunk& c = ch[(size_t)t];
+    for (size_t r = 0; r < c.s.size() && o < max_rows; ++r, ++o) {
+      if (out_u) out_u[o] = 0;
+      if (out_i) out_i[o] = 0;
+      out_s[o] = c.s[r];
+      out_ts[o] = c.ts[r];
+    }
+  }
+  return o;
+}
+
+// Line-aligned chunks of buf for P threads.
+std::vector<const char*> line_chunks(const char* buf, long long len, int P) {
+  std::vector<const char*> cut((size_t)P + 1);
+  cut[0] = buf;
+  cut[(size_t)P] = buf + len;
+  for (int t = 1; t < P; ++t) {
+    const char* c = buf + len * t / P;
+    if (c < cut[(size_t)t - 1]) c = cut[(size_t)t - 1];
+    const char* nl = static_cast<const char*>(memchr(c, '\n', (size_t)(buf + len - c)));
+    cut[(size_t)t] = nl ? nl + 1 : buf + len;
+  }
+  return cut;
+}
+
+int split_threads(long long len) {
+  if (len < (1ll << 20)) return 1;
+  return (int)std::max<long long>(1, std::min<long long>(len / (256ll << 10),
+                                                         oryx_ff::native_threads()));
+}
+
 }  // namespace
 
 extern "C" {
+
+// Timestamp range of the rating lines of buf (the rows oryx_parse_ratings accepts; lines
+// without a timestamp count as default_ts).  Returns the number of rows (0: no range).
+long long oryx_ts_range(const char* buf, long long len, long long default_ts,
+                        long long* out_min, long long* out_max) {
+  const int P = split_threads(len);
+  std::vector<const char*> cut = line_chunks(buf, len, P);
+  std::vector<long long> mn((size_t)P, std::numeric_limits<long long>::max()),
+      mx((size_t)P, std::numeric_limits<long long>::min()), cnt((size_t)P, 0);
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      RatingChunk c;
+      c.no_ids = true;
+      c.parse(cut[(size_t)t], cut[(size_t)t + 1], default_ts, false);
+      for (long long v : c.ts) {
+        mn[(size_t)t] = std::min(mn[(size_t)t], v);
+        mx[(size_t)t] = std::max(mx[(size_t)t], v);
+      }
+      cnt[(size_t)t] = (long long)c.ts.size();
+    }
+  });
+  long long n = 0, a = std::numeric_limits<long long>::max(), b = std::numeric_limits<long long>::min();
+  for (int t = 0; t < P; ++t) {
+    n += cnt[(size_t)t];
+    a = std::min(a, mn[(size_t)t]);
+    b = std::max(b, mx[(size_t)t]);
+  }
+  *out_min = a;
+  *out_max = b;
+  return n;
+}
+
+// The time split of MLUpdate.splitNewDataToTrainTest for ALS (ALSUpdate.java:237-254) in one
+// parallel pass: every parsable line of buf goes, in order and with its '\n', to out_lo when
+// its timestamp (default_ts when missing) is < boundary, else to out_hi (lines that do not
+// parse are dropped).  Both outputs need capacity len + 1.  Returns 0 (counts and byte sizes
+// in the out parameters).
+long long oryx_split_by_time(const char* buf, long long len, long long default_ts,
+                             long long boundary, char* out_lo, char* out_hi, long long* n_lo,
+                             long long* n_hi, long long* b_lo, long long* b_hi) {
+  const int P = split_threads(len);
+  std::vector<const char*> cut = line_chunks(buf, len, P);
+  std::vector<RatingChunk> ch((size_t)P);
+  std::vector<long long> blo((size_t)P, 0), bhi((size_t)P, 0), nlo((size_t)P, 0),
+      nhi((size_t)P, 0);
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      RatingChunk& c = ch[(size_t)t];
+      c.no_ids = true;
+      c.want_spans = true;
+      c.parse(cut[(size_t)t], cut[(size_t)t + 1], default_ts, false);
+      for (size_t r = 0; r < c.ts.size(); ++r) {
+        const long long l = (long long)(c.sp_e[r] - c.sp_b[r]) + 1;
+        if (c.ts[r] < boundary) { blo[(size_t)t] += l; ++nlo[(size_t)t]; }
+        else { bhi[(size_t)t] += l; ++nhi[(size_t)t]; }
+      }
+    }
+  });
+  std::vector<long long> olo((size_t)P + 1, 0), ohi((size_t)P + 1, 0);
+  for (int t = 0; t < P; ++t) {
+    olo[(size_t)t + 1] = olo[(size_t)t] + blo[(size_t)t];
+    ohi[(size_t)t + 1] = ohi[(size_t)t] + bhi[(size_t)t];
+  }
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      const RatingChunk& c = ch[(size_t)t];
+      char* wl = out_lo + olo[(size_t)t];
+      char* wh = out_hi + ohi[(size_t)t];
+      for (size_t r = 0; r < c.ts.size(); ++r) {
+        const size_t l = (size_t)(c.sp_e[r] - c.sp_b[r]);
+        char*& w = c.ts[r] < boundary ? wl : wh;
+        memcpy(w, c.sp_b[r], l);
+        w[l] = '\n';
+        w += l + 1;
+      }
+    }
+  });
+  long long a = 0, b = 0;
+  for (int t = 0; t < P; ++t) { a += nlo[(size_t)t]; b += nhi[(size_t)t]; }
+  *n_lo = a;
+  *n_hi = b;
+  *b_lo = olo[(size_t)P];
+  *b_hi = ohi[(size_t)P];
+  return 0;
+}
 
 // Parses newline-separated rating lines.  users/items: dictionaries; outputs per parsed row:
 // user code, item code, strength (NaN when the field is empty = delete; 1 when missing),
@@ -559,6 +717,11 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
                              long long* out_u, long long* out_i, double* out_s,
                              long long* out_ts, long long max_rows, long long default_ts,
                              int strict) {
+  if (!users || !items) {
+    // no dictionaries: every parsed row's strength and timestamp, IDs not encoded (codes 0)
+    return parse_rows_no_ids(buf, len, out_u, out_i, out_s, out_ts, max_rows, default_ts,
+                             strict);
+  }
   Dict* du = static_cast<Dict*>(users);
   Dict* di = static_cast<Dict*>(items);
   std::lock_guard<std::mutex> gu(du->mu);

@@ -193,6 +193,57 @@ def parse_ratings(lines, users: IdDict, items: IdDict, default_ts: int,
     return _parse_ratings_buf(data, len(data), n_max, users, items, default_ts, strict)
 
 
+def parse_timestamps(lines, default_ts: int = 0) -> np.ndarray:
+    """Timestamps of the rating lines :func:`parse_ratings` accepts (same rows), without
+    encoding any ID -- what a time-based train/test split needs."""
+    from .textlines import TextLines
+    if isinstance(lines, TextLines):
+        buf = lines.joined()
+        n_max = len(lines) + 1
+        if isinstance(buf, np.ndarray):
+            data = ctypes.cast(ctypes.c_void_p(buf.ctypes.data), ctypes.c_char_p)
+            n_bytes = buf.nbytes
+        else:
+            data, n_bytes = bytes(buf), len(buf)
+    else:
+        data = (bytes(lines) if isinstance(lines, (bytes, bytearray))
+                else "\n".join(lines).encode("utf-8"))
+        n_bytes = len(data)
+        n_max = data.count(b"\n") + 1
+    return _parse_ratings_buf(data, n_bytes, n_max, None, None, default_ts, False)[3]
+
+
+def _lines_ptr(lines):
+    buf = lines.joined()
+    if not isinstance(buf, np.ndarray):
+        buf = np.frombuffer(bytes(buf), dtype=np.uint8)
+    return buf, ctypes.c_void_p(buf.ctypes.data), int(buf.nbytes)
+
+
+def ts_range(lines, default_ts: int = 0) -> Optional[Tuple[int, int]]:
+    """(min, max) timestamp of a :class:`~oryx_amd.textlines.TextLines` buffer's rating
+    lines (native, threaded), or None without any parsable line."""
+    buf, ptr, n = _lines_ptr(lines)
+    lo, hi = ctypes.c_longlong(0), ctypes.c_longlong(0)
+    rows = native.runtime().oryx_ts_range(ptr, n, int(default_ts), ctypes.byref(lo),
+                                          ctypes.byref(hi))
+    return (int(lo.value), int(hi.value)) if rows > 0 else None
+
+
+def split_by_time(lines, boundary: int, default_ts: int = 0):
+    """(lines with timestamp < boundary, the rest) of a TextLines buffer, both TextLines in
+    the original order; unparsable lines are dropped (native, threaded, one pass)."""
+    from .textlines import TextLines
+    buf, ptr, n = _lines_ptr(lines)
+    lo = np.empty(n + 1, dtype=np.uint8)
+    hi = np.empty(n + 1, dtype=np.uint8)
+    c = [ctypes.c_longlong(0) for _ in range(4)]
+    native.runtime().oryx_split_by_time(ptr, n, int(default_ts), int(boundary), _ptr(lo),
+                                        _ptr(hi), *[ctypes.byref(x) for x in c])
+    return TextLines(lo[:c[2].value], int(c[0].value)), TextLines(hi[:c[3].value],
+                                                                  int(c[1].value))
+
+
 def _parse_ratings_buf(data, n_bytes: int, n_max: int, users: "IdDict", items: "IdDict",
                        default_ts: int, strict: bool):
     u = np.empty(n_max, dtype=np.int64)
@@ -201,7 +252,8 @@ def _parse_ratings_buf(data, n_bytes: int, n_max: int, users: "IdDict", items: "
     t = np.empty(n_max, dtype=np.int64)
     vp = ctypes.c_void_p
     n = native.runtime().oryx_parse_ratings(
-        data, int(n_bytes), users.handle, items.handle, u.ctypes.data_as(vp),
+        data, int(n_bytes), users.handle if users is not None else None,
+        items.handle if items is not None else None, u.ctypes.data_as(vp),
         i.ctypes.data_as(vp), s.ctypes.data_as(vp), t.ctypes.data_as(vp), n_max,
         int(default_ts), int(bool(strict)))
     if n < 0:

@@ -122,6 +122,10 @@ class MLUpdate(BatchLayerUpdate):
                    model_update_topic: Optional[TopicProducer]) -> None:
         if new_data is None:
             raise ValueError("new_data is required")
+        # candidate path -> (PMML document, its serialized text) of the models this process
+        # wrote this generation: the winner is published from memory, not re-read and
+        # re-serialized (a rank-64 model's PMML lists every user and item ID)
+        self._written = {}
         new_msgs = new_data.values()
         past_msgs = past_data.values() if past_data is not None else None
 
@@ -274,15 +278,17 @@ class MLUpdate(BatchLayerUpdate):
         best_model_path = os.path.join(final_path, MODEL_FILE_NAME)
         if not os.path.exists(best_model_path):
             return
+        t_p = time.perf_counter()
         needed = self.can_publish_additional_model_data()
         not_too_large = os.path.getsize(best_model_path) <= self.max_message_size
-        best_model = None
+        best_model = text = None
         if needed or not_too_large:
-            best_model = pmmlu.read(best_model_path)
+            best_model, text = self._promoted_model(best_model_path)
         if not_too_large:
-            model_update_topic.send("MODEL", pmmlu.to_string(best_model))
+            model_update_topic.send("MODEL", text)
         else:
             model_update_topic.send("MODEL-REF", ioutils.to_uri(best_model_path))
+        self._phase("model_publish", time.perf_counter() - t_p)
         if needed:
             self.publish_additional_model_data(context, best_model, new_msgs, past_msgs,
                                                final_path, model_update_topic)
@@ -309,13 +315,15 @@ class MLUpdate(BatchLayerUpdate):
         best_model_path = os.path.join(final_path, MODEL_FILE_NAME)
         # the PMML (with every ID of the model) is parsed only where it is needed: rank 0 sends
         # it, the others only when the app publishes from it
-        best_model = pmmlu.read(best_model_path) if main or self.publish_needs_model() \
-            else None
+        t_p = time.perf_counter()
+        best_model, text = self._promoted_model(best_model_path) \
+            if main or self.publish_needs_model() else (None, None)
         if main:
             if os.path.getsize(best_model_path) <= self.max_message_size:
-                model_update_topic.send("MODEL", pmmlu.to_string(best_model))
+                model_update_topic.send("MODEL", text)
             else:
                 model_update_topic.send("MODEL-REF", ioutils.to_uri(best_model_path))
+        self._phase("model_publish", time.perf_counter() - t_p)
         dist.barrier(dctx)
         if self.can_publish_additional_model_data():
             self.publish_additional_model_data(context, best_model, new_msgs, past_msgs,
@@ -369,9 +377,7 @@ class MLUpdate(BatchLayerUpdate):
         log.info("Building candidate %d with params %s", i, params)
         t_split = time.perf_counter()
         train, test = self._split_train_test(new_msgs, past_msgs)
-        ph = getattr(self, "phase_seconds", None)
-        if isinstance(ph, dict):
-            ph["split"] = ph.get("split", 0.0) + time.perf_counter() - t_split
+        self._phase("split", time.perf_counter() - t_split)
         ev = float("nan")
         n_train, n_test = self._global_count(len(train)), self._global_count(len(test))
         timing = {"candidate": i, "params": [str(p) for p in params], "train": n_train,
@@ -392,10 +398,14 @@ class MLUpdate(BatchLayerUpdate):
                     return None, ev
             else:
                 if writer:
+                    t_w = time.perf_counter()
                     os.makedirs(candidate_path, exist_ok=True)
                     model_path = os.path.join(candidate_path, MODEL_FILE_NAME)
                     log.info("Writing model to %s", model_path)
-                    pmmlu.write(model, model_path)
+                    text = pmmlu.to_string(model)
+                    ioutils.write_text(model_path, text)
+                    self._written[candidate_path] = (model, text)
+                    self._phase("pmml_write", time.perf_counter() - t_w)
                 if not n_test:
                     log.info("No test data available to evaluate model")
                 else:
@@ -413,6 +423,21 @@ class MLUpdate(BatchLayerUpdate):
         tracing.record(dict(timing, event="candidate"))
         log.info("Model eval for params %s: %s (%s)", params, ev, candidate_path)
         return candidate_path, ev
+
+    def _phase(self, name: str, seconds: float) -> None:
+        """Add to the app's ``phase_seconds`` (when it keeps one: bench_batch reads it)."""
+        ph = getattr(self, "phase_seconds", None)
+        if isinstance(ph, dict):
+            ph[name] = ph.get(name, 0.0) + seconds
+
+    def _promoted_model(self, path: str):
+        """(PMML document, serialized text) of the promoted model at ``path``: from memory
+        when this process wrote it, else read from the file."""
+        got = getattr(self, "_written", {}).get(getattr(self, "promoted_from", None))
+        if got is not None:
+            return got
+        text = ioutils.read_text(path)
+        return pmmlu.from_string(text), text
 
     def publish_needs_model(self) -> bool:
         """Whether :meth:`publish_additional_model_data` on a non-zero rank of a sharded

@@ -214,9 +214,7 @@ def parse_ratings(lines: Sequence[str], users: ingest.IdDict, items: ingest.IdDi
 
 
 def _timestamps(lines: Sequence[str]) -> np.ndarray:
-    d1, d2 = ingest.IdDict(), ingest.IdDict()
-    _, _, _, ts = ingest.parse_ratings(lines, d1, d2, default_ts=0)
-    return ts
+    return ingest.parse_timestamps(lines, default_ts=0)
 
 
 def write_features(path: str, ids, mat, part: int = 0) -> None:
@@ -484,8 +482,9 @@ class ALSUpdate(MLUpdate):
         f = trainer.train(self.iterations, checkpoint_dir=ckpt_dir,
                           checkpoint_interval=self.checkpoint_interval, fingerprint=fingerprint,
                           x_init=x_init, y_init=y_init)
-        X = f.X.cpu().numpy()
-        Y = f.Y.cpu().numpy()
+        X, Y = f.X, f.Y                 # stay on the device for the evaluation
+        if X.device.type == "cuda":
+            torch.cuda.synchronize(X.device)
         ph["train"] = ph.get("train", 0.0) + time.perf_counter() - tp
         tp = time.perf_counter()
         # the rows' JSON text, formatted where the factors live (GPU: textfmt.hip); reused by
@@ -574,25 +573,45 @@ class ALSUpdate(MLUpdate):
     def evaluate(self, context, model, model_parent_path, test_data, train_data):
         if self._sharded(context):
             return self._evaluate_sharded(context, model_parent_path, test_data)
+        tp = time.perf_counter()
+        try:
+            return self._evaluate_local(context, model, model_parent_path, test_data)
+        finally:
+            self.phase_seconds["eval"] = self.phase_seconds.get("eval", 0.0) + \
+                time.perf_counter() - tp
+
+    def _evaluate_local(self, context, model, model_parent_path, test_data):
         f = self._load(model_parent_path, model)
         users, items = ingest.IdDict(), ingest.IdDict()
         u, i, s, ts = parse_ratings(test_data, users, items, self.decay_factor,
                                     self.decay_zero_threshold)
-        u, i, s = aggregate_scores(u, i, s, ts, self.implicit)
-        xmap = {k: n for n, k in enumerate(f["x_ids"])}
-        ymap = {k: n for n, k in enumerate(f["y_ids"])}
-        ucodes = np.array([xmap.get(k, -1) for k in users.keys()], dtype=np.int64)
-        icodes = np.array([ymap.get(k, -1) for k in items.keys()], dtype=np.int64)
-        mu, mi = (ucodes[u] if len(u) else u), (icodes[i] if len(i) else i)
         device = self._ctx(context).device
-        X = torch.from_numpy(f["X"]).to(device)
-        Y = torch.from_numpy(f["Y"]).to(device)
+        # test IDs -> model rows through native dictionaries of the model's IDs
+        for key, ids in (("x_dict", f["x_ids"]), ("y_dict", f["y_ids"])):
+            if key not in f:
+                d = ingest.IdDict()
+                d.encode(list(ids))
+                f[key] = d
+        ucodes = f["x_dict"].find_blob(*users.keys_blob())
+        icodes = f["y_dict"].find_blob(*items.keys_blob())
+        if device.type == "cuda":
+            au, ai, av = aggregate_scores_device(u, i, s, ts, self.implicit, device,
+                                                 to_host=False)
+            mu = torch.from_numpy(ucodes).to(device)[au] if au.numel() else au
+            mi = torch.from_numpy(icodes).to(device)[ai] if ai.numel() else ai
+        else:
+            au, ai, av = aggregate_scores(u, i, s, ts, self.implicit)
+            mu = ucodes[au] if len(au) else au
+            mi = icodes[ai] if len(ai) else ai
+        X = f["X"] if isinstance(f["X"], torch.Tensor) else torch.from_numpy(f["X"])
+        Y = f["Y"] if isinstance(f["Y"], torch.Tensor) else torch.from_numpy(f["Y"])
+        X, Y = X.to(device), Y.to(device)
         if self.implicit:
             # AUC over test positives; items universe = distinct test items (known to the model)
             auc = evaluation.area_under_curve(X, Y, mu, mi, device=device)
             log.info("AUC: %s", auc)
             return auc
-        rmse = evaluation.rmse(X, Y, mu, mi, s, device=device)
+        rmse = evaluation.rmse(X, Y, mu, mi, av, device=device)
         log.info("RMSE: %s", rmse)
         return -rmse
 
@@ -662,8 +681,26 @@ class ALSUpdate(MLUpdate):
 
     # ---------------------------------------------------------------- split
     def split_new_data_to_train_test(self, new_data):
-        ts = _timestamps(new_data)
         sharded = self.dist_ctx is not None and self.dist_ctx.is_distributed
+        if isinstance(new_data, TextLines):
+            # one native pass for the range, one for the split (no per-line arrays)
+            rg = ingest.ts_range(new_data)
+            if sharded:
+                big = np.iinfo(np.int64).max
+                mm = shuffle.all_reduce_np(np.array([-(rg[0]) if rg else -big,
+                                                     rg[1] if rg else -big],
+                                                    dtype=np.int64), self.dist_ctx, op="max")
+                if mm[1] == -big:
+                    return new_data, []
+                rg = (int(-mm[0]), int(mm[1]))
+            if rg is None:
+                return new_data, []
+            lo, hi = rg
+            log.info("New data timestamp range: %d - %d", lo, hi)
+            boundary = int(hi - self.get_test_fraction() * (hi - lo))
+            log.info("Splitting at timestamp %d", boundary)
+            return ingest.split_by_time(new_data, boundary)
+        ts = _timestamps(new_data)
         if sharded:
             # the boundary comes from the global timestamp range of the new data
             big = np.iinfo(np.int64).max

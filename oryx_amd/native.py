@@ -115,6 +115,9 @@ def _register_runtime_extras(lib):
                                                c_ll])
     _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_owners", c_ll, [c_vp, c_ll, c_i, c_vp])
+    _sig(lib, "oryx_ts_range", c_ll, [c_vp, c_ll, c_ll, c_vp, c_vp])
+    _sig(lib, "oryx_split_by_time", c_ll, [c_vp, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,
+                                           c_vp, c_vp])
     _sig(lib, "oryx_dict_encode_blob", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_find_blob", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_keys_blob_sel", c_ll, [c_vp, c_vp, c_ll, c_vp, c_ll, c_vp])
