@@ -166,7 +166,10 @@ def main(argv=None) -> int:
         lines = ["U%d,I%d,%.2f,%d" % (a, b, v, now) for a, b, v in
                  zip(g.integers(0, len(Xh), B).tolist(), g.integers(0, len(Yh), B).tolist(),
                      (g.random(B) * 4 + 0.5).tolist())]
-        ds = Dataset.from_values(lines)
+        # the micro-batch as the speed layer drains it from the input log: one TextLines
+        # buffer (layers/common.drain_dataset), not Python strings
+        from oryx_amd.textlines import TextLines
+        ds = Dataset.from_values(TextLines.from_strings(lines))
         import shutil
         import tempfile
         from oryx_amd.layers.speed import publish_blocks
@@ -180,6 +183,10 @@ def main(argv=None) -> int:
                 # a new micro-batch always follows a change of the factors (the previous
                 # batch's own UP rows): the Gramian inverses are recomputed every time
                 model.X.version += 1
+                # micro-batches arrive one per speed interval (oryx.speed.streaming.
+                # generation-interval-sec, seconds): 50 ms of idle time between reps (untimed)
+                # lets the update log's tail preallocation run as it does between intervals
+                time.sleep(0.05)
                 sync()
                 t1 = time.perf_counter()
                 # the speed layer's path: blocks of UP rows assembled while the previous

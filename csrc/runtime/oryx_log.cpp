@@ -22,8 +22,12 @@
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <tuple>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <dirent.h>
 #include <fcntl.h>
@@ -31,6 +35,7 @@
 #include <mutex>
 #include <string>
 #include <sys/file.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/types.h>
 #include <thread>
@@ -130,6 +135,61 @@ inline uint32_t frame_crc(uint32_t magic, const uint8_t* f, size_t plen) {
 
 thread_local std::string g_err;
 
+// large appends keep a preallocated, pre-faulted tail ahead of them (ORYX_LOG_PREALLOC=0
+// disables)
+const bool g_prealloc = [] {
+  const char* v = std::getenv("ORYX_LOG_PREALLOC");
+  return !(v && std::string(v) == "0");
+}();
+
+// One background thread faults preallocated segment ranges into the page cache
+// (MADV_POPULATE_WRITE on a shared mapping: page tables and cache pages, no data change --
+// an append writing the same range meanwhile is unaffected).  Jobs name the file by path: a
+// segment deleted in between is skipped.
+struct SegMap;
+struct PrefaultQueue {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::tuple<std::shared_ptr<SegMap>, int64_t, int64_t>> jobs;
+  bool started = false;
+};
+
+PrefaultQueue& prefault_queue() {
+  static PrefaultQueue* q = new PrefaultQueue();   // never destroyed: the worker is detached
+  return *q;
+}
+
+void prefault_run(const std::shared_ptr<SegMap>& m, int64_t off, int64_t len);
+
+void prefault_async(const std::shared_ptr<SegMap>& m, int64_t off, int64_t len) {
+  PrefaultQueue& q = prefault_queue();
+  std::lock_guard<std::mutex> g(q.mu);
+  q.jobs.emplace_back(m, off, len);
+  if (!q.started) {
+    q.started = true;
+    std::thread([&q] {
+      for (;;) {
+        std::tuple<std::shared_ptr<SegMap>, int64_t, int64_t> j;
+        {
+          std::unique_lock<std::mutex> l(q.mu);
+          q.cv.wait(l, [&] { return !q.jobs.empty(); });
+          j = q.jobs.front();
+          q.jobs.pop_front();
+        }
+        prefault_run(std::get<0>(j), std::get<1>(j), std::get<2>(j));
+      }
+    }).detach();
+  }
+  q.cv.notify_one();
+}
+
+// appends of at least this many bytes go through a shared mapping of the segment
+// (ORYX_LOG_MMAP_MIN bytes; 0 disables)
+const long long g_mmap_min = [] {
+  const char* v = std::getenv("ORYX_LOG_MMAP_MIN");
+  return v ? std::atoll(v) : (4ll << 20);
+}();
+
 int fail(const std::string& msg) {
   g_err = msg + (errno ? std::string(": ") + strerror(errno) : std::string());
   return -1;
@@ -193,9 +253,39 @@ uint32_t murmur2(const uint8_t* data, int len) {
   return h;
 }
 
+// A writer's shared mapping of one segment file, kept across appends (the page tables of a
+// mapping built per append cost more than the copy), sized to the segment's roll size plus
+// the largest block seen; a background prefault job holds a reference while it works on it.
+struct SegMap {
+  int fd = -1;
+  uint8_t* base = nullptr;
+  size_t len = 0;
+  int64_t seg_base = -1;
+  ~SegMap() {
+    if (base) munmap(base, len);
+    if (fd >= 0) close(fd);
+  }
+};
+
+// Faults [off, off + len) of a writer mapping in (page cache pages and this process's page
+// tables; MADV_POPULATE_WRITE changes no data, so an append writing the range meanwhile is
+// unaffected).  The range lies inside the file (the appender grew it under the lock).
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23     // Linux 5.14+ (older headers lack the name)
+#endif
+void prefault_run(const std::shared_ptr<SegMap>& m, int64_t off, int64_t len) {
+  {
+  const long long page = sysconf(_SC_PAGESIZE);
+  const int64_t a = off - off % page;
+  if (!m || !m->base || a + len > (int64_t)m->len) return;
+  madvise(m->base + a, (size_t)(off + len - a), MADV_POPULATE_WRITE);
+  }
+}
+
 struct Partition {
   std::string dir;
   int lock_fd = -1;
+  std::shared_ptr<SegMap> wmap;           // this handle's writer mapping of the active segment
   // flock() excludes other processes (and other handles); threads sharing this handle also
   // share the lock's open file description, for which flock is a no-op, so appends through
   // one handle are serialised by this mutex as well
@@ -257,8 +347,10 @@ int64_t scan_segment(const std::string& path, int64_t base, int64_t* end_pos,
   int fd = open(path.c_str(), O_RDONLY);
   if (fd < 0) { *end_pos = 0; return base; }
   int64_t pos = start_pos, next = start_next >= 0 ? start_next : base;
-  // 4 MB block reads; a frame straddling a block is re-read from its start
-  std::vector<uint8_t> buf(4u << 20);
+  // block reads growing from 64 KB to 4 MB (a resumed scan usually finds a few frames and
+  // then the end of the data -- possibly a preallocated zero tail, not worth 4 MB per look);
+  // a frame straddling a block is re-read from its start
+  std::vector<uint8_t> buf(64u << 10);
   for (;;) {
     const size_t cap = buf.size();
     ssize_t got = pread(fd, buf.data(), cap, pos);
@@ -292,10 +384,23 @@ int64_t scan_segment(const std::string& path, int64_t base, int64_t* end_pos,
       continue;
     }
     if (at == 0 || (size_t)got < cap) break;
+    if (buf.size() < (4u << 20)) buf.resize(std::min<size_t>(buf.size() * 4, 4u << 20));
   }
   close(fd);
   *end_pos = pos;
   return next;
+}
+
+// The bytes past the end of the data: a zero header means nothing was ever written there (a
+// preallocated tail, kept for the next append to write into) -- unlike a torn block, whose
+// unpublished first frame has a zero magic but a written header.
+bool zero_header_at(int fd, int64_t pos) {
+  uint8_t h[kHeader];
+  const ssize_t got = pread(fd, h, kHeader, pos);
+  if (got != (ssize_t)kHeader) return false;
+  for (size_t i = 0; i < kHeader; ++i)
+    if (h[i]) return false;
+  return true;
 }
 
 // Whether bytes [end_pos, size) of a segment can be the torn tail of an interrupted append:
@@ -327,6 +432,9 @@ bool torn_tail(const std::string& path, int64_t end_pos, int64_t size) {
   uint32_t magic, klen, vlen;
   memcpy(&magic, buf.data(), 4); memcpy(&klen, buf.data() + 24, 4);
   memcpy(&vlen, buf.data() + 28, 4);
+  // a mapped append that never published its first frame's magic (the writer died): the
+  // whole block is unpublished, nothing of it was ever readable
+  if (magic == 0) return true;
   if (!known_magic(magic)) return false;
   const int64_t flen = (int64_t)kHeader + (klen == kNullKey ? 0 : (int64_t)klen) + (int64_t)vlen;
   return flen >= rem;
@@ -344,6 +452,10 @@ struct Reader {
   std::vector<uint8_t> blk;
   int64_t blk_pos = -1;
   size_t blk_len = 0;
+  // at the end of the data (the last look found no complete frame): read small blocks until
+  // more arrives (a segment may have a preallocated zero tail: 1 MB per idle poll would be
+  // wasted copying)
+  bool at_tail = false;
 };
 
 // Pointer to bytes [pos, pos + n) of the reader's segment (through the read-ahead block), or
@@ -352,7 +464,8 @@ const uint8_t* reader_bytes(Reader* r, int64_t pos, size_t n) {
   if (r->blk_pos >= 0 && pos >= r->blk_pos &&
       (size_t)(pos - r->blk_pos) + n <= r->blk_len)
     return r->blk.data() + (pos - r->blk_pos);
-  const size_t want = n > (1u << 20) ? n : (1u << 20);
+  const size_t ahead = r->at_tail ? (4u << 10) : (1u << 20);
+  const size_t want = n > ahead ? n : ahead;
   if (r->blk.size() < want) r->blk.resize(want);
   const ssize_t got = pread(r->fd, r->blk.data(), want, pos);
   r->blk_pos = pos;
@@ -526,7 +639,7 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
     path = seg_name(P.dir, base);
     end_pos = 0;
   }
-  int fd = open(path.c_str(), O_WRONLY | O_CREAT, 0644);
+  int fd = open(path.c_str(), O_RDWR | O_CREAT, 0644);
   if (fd < 0) {
     if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN);
     return fail("open segment");
@@ -536,15 +649,16 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
   // unknown magic or a bad checksum in the middle of a segment is corruption, and truncating
   // there would silently drop every later record and re-issue committed offsets)
   struct stat st;
-  if (fstat(fd, &st) == 0 && st.st_size > end_pos) {
-    if (!torn_tail(path, end_pos, (int64_t)st.st_size)) {
+  int64_t file_size = fstat(fd, &st) == 0 ? (int64_t)st.st_size : end_pos;
+  if (file_size > end_pos && !zero_header_at(fd, end_pos)) {
+    if (!torn_tail(path, end_pos, file_size)) {
       close(fd);
       if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN);
       errno = 0;
       return fail("refusing to append: segment " + path + " holds unreadable data at byte " +
                   std::to_string(end_pos) + " followed by more data (corrupt or unknown format)");
     }
-    if (ftruncate(fd, end_pos) != 0) {}
+    if (ftruncate(fd, end_pos) == 0) file_size = end_pos;
   }
   const size_t n = which.size();
   std::vector<size_t> at(n + 1);
@@ -554,18 +668,49 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
     at[j + 1] = at[j] + kHeader + (r.klen < 0 ? 0 : (size_t)r.klen) + (size_t)r.vlen;
   }
   const size_t total = at[n];
-  std::vector<uint8_t>& out = frame_buffer(total);
   const int64_t first = next;
+  // Large appends are built straight into the segment's page cache through a shared mapping
+  // (one copy of the bytes instead of a frame buffer plus pwrite's kernel copy, and the
+  // frames are written by all native threads).  The first frame's magic is stored last: until
+  // then readers see an unknown magic at the old end of the log and stop there, so no reader
+  // ever sees a later frame of the block before an earlier one is complete.
+  const auto Tm = std::chrono::steady_clock::now();
+  uint8_t* mapped = nullptr;
+  if (g_mmap_min > 0 && (long long)total >= g_mmap_min &&
+      (file_size >= end_pos + (int64_t)total ||
+       ftruncate(fd, end_pos + (off_t)total) == 0)) {
+    // (the file only ever grows here: a preallocated tail may already be longer)
+    file_size = std::max<int64_t>(file_size, end_pos + (int64_t)total);
+    std::shared_ptr<SegMap>& wm = P.wmap;
+    const size_t need = (size_t)(end_pos + (int64_t)total);
+    if (!wm || wm->seg_base != base || wm->len < need) {
+      // (re)map the whole segment: its roll size, or more for a block that overshoots it
+      auto m = std::make_shared<SegMap>();
+      m->fd = open(path.c_str(), O_RDWR);
+      m->seg_base = base;
+      m->len = std::max<size_t>((size_t)t->segment_bytes, 2 * need);
+      if (m->fd >= 0) {
+        void* a = mmap(nullptr, m->len, PROT_READ | PROT_WRITE, MAP_SHARED, m->fd, 0);
+        if (a != MAP_FAILED) m->base = static_cast<uint8_t*>(a);
+      }
+      wm = m->base ? m : nullptr;
+    }
+    if (wm) mapped = wm->base;
+  }
+  const auto T0 = std::chrono::steady_clock::now();
+  std::vector<uint8_t>* fb = mapped ? nullptr : &frame_buffer(total);
+  uint8_t* dst = mapped ? mapped + end_pos : fb->data();
   auto build = [&](long long lo, long long hi, int) {
     for (long long j = lo; j < hi; ++j) {
       const RecRef& r = recs[(size_t)which[(size_t)j]];
-      uint8_t* f = out.data() + at[(size_t)j];
+      uint8_t* f = dst + at[(size_t)j];
       const uint32_t uk = r.klen < 0 ? kNullKey : (uint32_t)r.klen;
       const uint32_t uv = (uint32_t)r.vlen;
       const size_t kl = r.klen < 0 ? 0 : (size_t)r.klen;
       const uint64_t off = (uint64_t)(first + j);
       const int64_t ts = ts_ms;
-      memcpy(f, &kMagic, 4);
+      const uint32_t magic = j == 0 ? 0u : kMagic;     // published last, see below
+      memcpy(f, &magic, 4);
       memcpy(f + 8, &off, 8);
       memcpy(f + 16, &ts, 8);
       memcpy(f + 24, &uk, 4);
@@ -579,18 +724,55 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
   // threads only for batches worth it (~1 MB per thread)
   const long long per = total >= (2u << 20) ? std::max<long long>(64, (long long)(n * (1u << 20) / total)) : (long long)n + 1;
   oryx_ff::parallel_ranges((long long)n, per, build);
+  const auto T1 = std::chrono::steady_clock::now();
   if (out_offsets)
     for (size_t j = 0; j < n; ++j) out_offsets[which[j]] = first + (long long)j;
   next = first + (int64_t)n;
-  // one pwrite per append; Linux caps a single write at 0x7ffff000 bytes, so a block past
-  // 2 GB goes out in pieces (a reader that gets ahead of them sees a short last frame and
-  // stops there, as it does for any append in progress)
+  // Every append publishes its block by storing the first frame's magic after every other
+  // byte of the block is in place: a reader stops at the zero magic (the end of the data)
+  // until then, so it never meets a half-written frame followed by complete ones (which it
+  // would report as corruption) -- also when the block lands in a preallocated zero tail.
   size_t done = 0;
+  if (mapped) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    __atomic_store_n(reinterpret_cast<uint32_t*>(dst), kMagic, __ATOMIC_RELEASE);
+    if (do_fsync) {
+      const long long page = sysconf(_SC_PAGESIZE);
+      const int64_t a = end_pos - end_pos % page;
+      msync(mapped + a, (size_t)(end_pos + (int64_t)total - a), MS_SYNC);
+    }
+    done = total;
+  }
+  // otherwise one pwrite per append (Linux caps a single write at 0x7ffff000 bytes, so a
+  // block past 2 GB goes out in pieces), then the 4-byte magic
   while (done < total) {
-    const ssize_t w = pwrite(fd, out.data() + done, total - done, end_pos + (off_t)done);
+    const ssize_t w = pwrite(fd, fb->data() + done, total - done, end_pos + (off_t)done);
     if (w < 0 && errno == EINTR) continue;
     if (w <= 0) break;
     done += (size_t)w;
+  }
+  if (!mapped && done == total) {
+    ssize_t w;
+    do { w = pwrite(fd, &kMagic, 4, end_pos); } while (w < 0 && errno == EINTR);
+    if (w != 4) done = 0;
+  }
+  const auto T2 = std::chrono::steady_clock::now();
+  if (std::getenv("ORYX_LOG_DEBUG"))
+    fprintf(stderr, "append %zu B mapped=%d map %.3f build %.3f ms write %.3f ms\n", total,
+            mapped != nullptr, std::chrono::duration<double, std::milli>(T0 - Tm).count(),
+            std::chrono::duration<double, std::milli>(T1 - T0).count(),
+            std::chrono::duration<double, std::milli>(T2 - T1).count());
+  if (done == total && mapped && g_prealloc) {
+    // keep the next large block's pages in the page cache ahead of it: grow the segment
+    // (under the lock; never past its roll size) and fault the new range in on a
+    // background thread -- the append itself then only copies bytes
+    const int64_t new_end = end_pos + (int64_t)total;
+    int64_t want = std::min<int64_t>(new_end + std::max<int64_t>(2 * (int64_t)total,
+                                                                 16ll << 20),
+                                     std::max<int64_t>(t->segment_bytes, new_end));
+    want = std::min<int64_t>(want, (int64_t)P.wmap->len);
+    if (want > file_size && ftruncate(fd, want) == 0) file_size = want;
+    if (file_size > new_end) prefault_async(P.wmap, new_end, file_size - new_end);
   }
   if (done != total) {
     close(fd);
@@ -753,7 +935,7 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
       int64_t ts;
       memcpy(&magic, h, 4); memcpy(&crc, h + 4, 4); memcpy(&off, h + 8, 8);
       memcpy(&ts, h + 16, 8); memcpy(&klen, h + 24, 4); memcpy(&vlen, h + 28, 4);
-      if (!known_magic(magic)) { r->blk_pos = -1; break; }
+      if (!known_magic(magic)) { r->blk_pos = -1; r->at_tail = true; break; }
       size_t kl = klen == kNullKey ? 0 : klen;
       size_t plen = kl + vlen;
       // the whole frame, so header and payload are contiguous in the block
@@ -793,6 +975,7 @@ long long oryx_reader_poll(void* rh, char* out, long long out_cap, int max_recor
       r->next_offset = (int64_t)off + 1;
       ++count;
       progressed = true;
+      r->at_tail = false;
     }
     if (count >= max_records) break;
     if (!progressed) {
@@ -869,6 +1052,29 @@ long long oryx_reader_poll_frames(void* rh, char* out, long long out_cap, int ma
     if (r->fd < 0) reader_seek(r, r->next_offset);
     if (r->fd < 0) return 0;
     r->blk_pos = -1;   // the poll read-ahead block is bypassed from here on
+    // the next frame's header first: at the end of the data (possibly a preallocated zero
+    // tail) a bulk read of out_cap bytes would copy nothing useful
+    {
+      uint8_t h[kHeader];
+      const ssize_t hg = pread(r->fd, h, kHeader, r->pos);
+      uint32_t magic = 0;
+      if (hg == (ssize_t)kHeader) memcpy(&magic, h, 4);
+      if (hg == (ssize_t)kHeader && !known_magic(magic)) {
+        bool rolled = false;
+        for (int64_t b : list_segments(dir)) {
+          if (b > r->seg_base && b <= r->next_offset) {
+            close(r->fd);
+            r->seg_base = b;
+            r->pos = 0;
+            r->fd = open(seg_name(dir, b).c_str(), O_RDONLY);
+            rolled = true;
+            break;
+          }
+        }
+        if (!rolled) return 0;
+        continue;
+      }
+    }
     ssize_t got = pread(r->fd, out, (size_t)out_cap, r->pos);
     if (got < 0) got = 0;
     std::vector<size_t> at;

@@ -311,6 +311,103 @@ class RowMap:
         return out
 
 
+class SpeedBatch:
+    """One speed-layer micro-batch parsed against the stores' id -> row maps
+    (``csrc/runtime/oryx_ingest.cpp`` ``oryx_speed_*``): lines are parsed on the native
+    threads with each user / item resolved straight to its store row (no per-batch
+    dictionary), pairs aggregated in time order, and the UP messages assembled from the
+    events' own key bytes.  Reused across batches (its native buffers keep their capacity)."""
+
+    def __init__(self):
+        self._lib = native.runtime()
+        self._h = self._lib.oryx_speed_new()
+        self._buf = None
+
+    def __del__(self):
+        try:
+            if self._h:
+                self._lib.oryx_speed_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def parse(self, lines, xmap: "RowMap", ymap: "RowMap", default_ts: int = 0) -> int:
+        """Parse ``lines`` (TextLines, bytes or strings; kept referenced until the next
+        parse: the events' keys point into it).  Returns the number of events."""
+        from .textlines import TextLines
+        if isinstance(lines, TextLines):
+            buf = lines.joined()
+            if not isinstance(buf, np.ndarray):
+                buf = np.frombuffer(bytes(buf), dtype=np.uint8)
+        elif isinstance(lines, (bytes, bytearray)):
+            buf = np.frombuffer(bytes(lines), dtype=np.uint8)
+        else:
+            buf = np.frombuffer("\n".join(lines).encode("utf-8"), dtype=np.uint8)
+        self._buf = buf
+        return int(self._lib.oryx_speed_parse(self._h, _ptr(buf), int(buf.nbytes), xmap._h,
+                                              ymap._h, int(default_ts)))
+
+    def counts(self) -> Tuple[int, int, int, int]:
+        """(events, new users, new items, aggregated pairs)."""
+        out = np.zeros(4, dtype=np.int64)
+        self._lib.oryx_speed_counts(self._h, _ptr(out))
+        return tuple(int(x) for x in out)
+
+    def aggregate(self, implicit: bool) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(user rows, item rows, values) of the aggregated pairs (rows -1: not in the
+        store)."""
+        n = self.counts()[0]
+        u = np.empty(max(n, 1), dtype=np.int64)
+        i = np.empty(max(n, 1), dtype=np.int64)
+        v = np.empty(max(n, 1), dtype=np.float64)
+        m = int(self._lib.oryx_speed_aggregate(self._h, int(bool(implicit)), _ptr(u), _ptr(i),
+                                               _ptr(v)))
+        return u[:m], i[:m], v[:m]
+
+    def new_keys(self, which: int) -> Tuple[np.ndarray, np.ndarray]:
+        """(blob, ends) of the batch's user (0) / item (1) keys the stores lack."""
+        cnt = self.counts()[1 + which]
+        ends = np.empty(cnt, dtype=np.int64)
+        cap = 16 * cnt + 64
+        while True:
+            out = np.empty(cap, dtype=np.uint8)
+            used = self._lib.oryx_speed_new_keys(self._h, int(which), _ptr(out), cap, _ptr(ends))
+            if used >= 0:
+                return out[:used], ends
+            cap = -used
+
+    def assemble(self, lo: int, hi: int, xrows, yrows, vx: np.ndarray, vy: np.ndarray,
+                 with_known: bool):
+        """UP messages of the aggregated pairs [lo, hi) (``xrows`` / ``yrows``: RowText of
+        every pair's updated rows) as one :class:`~oryx_amd.api.MessageBlock`."""
+        from .api import MessageBlock
+        n = int(hi) - int(lo)
+        if n <= 0:
+            return MessageBlock(b"", np.zeros(0, dtype=np.int64))
+        lo = int(lo)
+        vx = np.ascontiguousarray(vx[lo:hi], dtype=np.uint8)
+        vy = np.ascontiguousarray(vy[lo:hi], dtype=np.uint8)
+        xb = int(xrows.ends[lo - 1]) if lo else 0
+        yb = int(yrows.ends[lo - 1]) if lo else 0
+        xe = np.ascontiguousarray(xrows.ends[lo:hi] - xb, dtype=np.int64)
+        ye = np.ascontiguousarray(yrows.ends[lo:hi] - yb, dtype=np.int64)
+        vp = ctypes.c_void_p
+        cap = int(xe[-1]) + int(ye[-1]) + n * 256
+        ends = np.empty(2 * n, dtype=np.int64)
+        n_msgs = ctypes.c_longlong(0)
+        xptr = vp(_buf_ptr(xrows.blob).value + xb)
+        yptr = vp(_buf_ptr(yrows.blob).value + yb)
+        while True:
+            out = _host_buffer(cap)
+            used = self._lib.oryx_speed_assemble(
+                self._h, lo, int(hi), xptr, _ptr(xe), yptr, _ptr(ye), _ptr(vx), _ptr(vy),
+                int(bool(with_known)), _ptr(out), cap, _ptr(ends), ctypes.byref(n_msgs))
+            if used >= 0:
+                break
+            cap = -used + 1
+        return MessageBlock(out[:used], ends[:n_msgs.value].copy())
+
+
 def parse_up_batch(messages: Sequence[str], k: int, known_dict: Optional["IdDict"] = None):
     """Bulk-parse ALS ``UP`` messages ``["X"|"Y", id, [k floats], [known ids]?]``.
 

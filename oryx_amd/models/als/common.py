@@ -282,36 +282,50 @@ class FeatureVectors:
         """Rows of every key of the native dictionary ``d`` (``ingest.IdDict``) in code
         order, -1 for IDs not in the store: one native translation instead of a Python dict
         lookup per ID (the speed layer resolves a micro-batch's users / items this way)."""
-        from ... import ingest
         with self._lock.write():
-            if self._rowmap is None:
-                self._rowmap = ingest.RowMap()
-                ids = list(self._index.keys())
-                self._rowmap.set(ids, np.fromiter(self._index.values(), dtype=np.int64,
-                                                  count=len(ids)))
-                self._journal = []
-            elif self._journal:
-                # replay in order, batching runs of the same kind
-                run_kind, run_ids, run_rows = None, [], []
-
-                def flush():
-                    if run_kind:
-                        self._rowmap.set(run_ids, np.asarray(run_rows, dtype=np.int64))
-                    elif run_kind is not None:
-                        self._rowmap.remove(run_ids)
-                for kind, ids, rows in self._journal:
-                    if kind != run_kind:
-                        flush()
-                        run_kind, run_ids, run_rows = kind, [], []
-                    if isinstance(ids, list):
-                        run_ids.extend(ids)
-                        run_rows.extend(np.asarray(rows).tolist())
-                    else:
-                        run_ids.append(ids)
-                        run_rows.append(int(rows))
-                flush()
-                self._journal = []
+            self._sync_rowmap()
             return self._rowmap.translate(d)
+
+    def synced_rowmap(self):
+        """The native id -> row map (``ingest.RowMap``), brought up to date with every write
+        so far.  Readers hold :meth:`read_lock` while they use it (only the sync mutates
+        it, under the write lock)."""
+        with self._lock.write():
+            self._sync_rowmap()
+            return self._rowmap
+
+    def read_lock(self):
+        return self._lock.read()
+
+    def _sync_rowmap(self) -> None:
+        from ... import ingest
+        if self._rowmap is None:
+            self._rowmap = ingest.RowMap()
+            ids = list(self._index.keys())
+            self._rowmap.set(ids, np.fromiter(self._index.values(), dtype=np.int64,
+                                              count=len(ids)))
+            self._journal = []
+        elif self._journal:
+            # replay in order, batching runs of the same kind
+            run_kind, run_ids, run_rows = None, [], []
+
+            def flush():
+                if run_kind:
+                    self._rowmap.set(run_ids, np.asarray(run_rows, dtype=np.int64))
+                elif run_kind is not None:
+                    self._rowmap.remove(run_ids)
+            for kind, ids, rows in self._journal:
+                if kind != run_kind:
+                    flush()
+                    run_kind, run_ids, run_rows = kind, [], []
+                if isinstance(ids, list):
+                    run_ids.extend(ids)
+                    run_rows.extend(np.asarray(rows).tolist())
+                else:
+                    run_ids.append(ids)
+                    run_rows.append(int(rows))
+            flush()
+            self._journal = []
 
     def add_all_ids_to(self, out: Set[str]) -> None:
         with self._lock.read():

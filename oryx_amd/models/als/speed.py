@@ -208,6 +208,7 @@ class ALSSpeedModelManager(SpeedModelManager):
         self.model: Optional[ALSSpeedModel] = None
         self._stream = None
         self._dicts = None
+        self._batch = None     # ingest.SpeedBatch of the GPU path (reused)
         # milliseconds per phase of the last build_updates (parse_aggregate, inverses, lookup
         # of the batch's IDs in the stores, foldin = kernel + validity flags to the host,
         # format_rows = GPU row text + copy, assemble = native UP message assembly)
@@ -290,6 +291,21 @@ class ALSSpeedModelManager(SpeedModelManager):
             return
         import time
         t0 = time.perf_counter()
+        dev = model.device
+        if dev.type == "cuda" and model.features <= 256:
+            # the GPU path: lines parsed on the native threads straight to store rows
+            # (ingest.SpeedBatch; no per-batch dictionaries), aggregated natively
+            if self._batch is None:
+                self._batch = ingest.SpeedBatch()
+            sb = self._batch
+            xm, ym = model.X.synced_rowmap(), model.Y.synced_rowmap()
+            with model.X.read_lock(), model.Y.read_lock():
+                sb.parse(new_data.values(), xm, ym, default_ts=0)
+            u, i, s = sb.aggregate(model.is_implicit())
+            self.last_phase_ms = {"parse_aggregate": (time.perf_counter() - t0) * 1e3}
+            if len(u):
+                yield from self._build_updates_fused(model, sb, u, i, s, chunks)
+            return
         # per-batch dictionaries, reused (cleared) so their tables are not reallocated and
         # re-faulted every micro-batch
         if self._dicts is None:
@@ -299,10 +315,6 @@ class ALSSpeedModelManager(SpeedModelManager):
         u, i, s = aggregate_scores(u, i, s, ts, model.is_implicit())
         self.last_phase_ms = {"parse_aggregate": (time.perf_counter() - t0) * 1e3}
         if len(u) == 0:
-            return
-        dev = model.device
-        if dev.type == "cuda" and model.features <= 256:
-            yield from self._build_updates_fused(model, users, items, u, i, s, chunks)
             return
         out = self._build_updates_host(model, users, items, u, i, s)
         if out:
@@ -360,7 +372,11 @@ class ALSSpeedModelManager(SpeedModelManager):
                 out.append(self._to_update_json("Y", i_ids[j], y_rows[j], u_ids[j]))
         return out
 
-    def _build_updates_fused(self, model, users, items, u, i, s, chunks: int = 1):
+    def _build_updates_fused(self, model, sb, u, i, s, chunks: int = 1):
+        """Fold-in of the aggregated pairs (``u`` / ``i``: store rows, -1 for IDs the stores
+        lack) with the fused HIP kernel, rows formatted on the GPU, UP messages assembled from
+        the micro-batch's own key bytes (``sb``: the parsed :class:`~oryx_amd.ingest.
+        SpeedBatch`)."""
         import time
         from ... import native
         ph = self.last_phase_ms
@@ -376,10 +392,6 @@ class ALSSpeedModelManager(SpeedModelManager):
         xinv, yinv = inv
         dev = model.device
         k = model.features
-        # store rows of the batch's distinct IDs (dictionary codes index them)
-        urow = model.X.native_rows(users)
-        irow = model.Y.native_rows(items)
-        ph["lookup"] = (time.perf_counter() - t0) * 1e3
         t0 = time.perf_counter()
         n = len(u)
         lib = native.require_kernels()
@@ -389,8 +401,8 @@ class ALSSpeedModelManager(SpeedModelManager):
             ymat, _, _ = model.Y.device_view()
             xm = xmat if len(xmat) else torch.zeros((1, k), device=dev)
             ym = ymat if len(ymat) else torch.zeros((1, k), device=dev)
-            xr = torch.from_numpy(urow[u]).to(dev)
-            yr = torch.from_numpy(irow[i]).to(dev)
+            xr = torch.from_numpy(np.ascontiguousarray(u, dtype=np.int64)).to(dev)
+            yr = torch.from_numpy(np.ascontiguousarray(i, dtype=np.int64)).to(dev)
             # the reference folds in strength.floatValue() (ALSSpeedModelManager.java:170)
             vals = torch.from_numpy(np.asarray(s, dtype=np.float32)).to(dev)
             new_x = torch.empty((n, k), dtype=torch.float32, device=dev)
@@ -417,9 +429,8 @@ class ALSSpeedModelManager(SpeedModelManager):
         chunks = max(1, min(int(chunks), n // 1024 or 1))
         for c in range(chunks):
             t0 = time.perf_counter()
-            blk = ingest.assemble_als_updates(users, items, u, i, xrows, yrows, vxh, vyh,
-                                              not self.no_known_items, lo=n * c // chunks,
-                                              hi=n * (c + 1) // chunks)
+            blk = sb.assemble(n * c // chunks, n * (c + 1) // chunks, xrows, yrows, vxh, vyh,
+                              not self.no_known_items)
             ph["assemble"] += (time.perf_counter() - t0) * 1e3
             yield blk
 

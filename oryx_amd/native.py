@@ -116,6 +116,14 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_owners", c_ll, [c_vp, c_ll, c_i, c_vp])
     _sig(lib, "oryx_ts_range", c_ll, [c_vp, c_ll, c_ll, c_vp, c_vp])
+    _sig(lib, "oryx_speed_new", c_vp, [])
+    _sig(lib, "oryx_speed_free", None, [c_vp])
+    _sig(lib, "oryx_speed_parse", c_ll, [c_vp, c_vp, c_ll, c_vp, c_vp, c_ll])
+    _sig(lib, "oryx_speed_counts", c_ll, [c_vp, c_vp])
+    _sig(lib, "oryx_speed_aggregate", c_ll, [c_vp, c_i, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_speed_new_keys", c_ll, [c_vp, c_i, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_speed_assemble", c_ll, [c_vp, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                            c_vp, c_i, c_vp, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_split_by_time", c_ll, [c_vp, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,
                                            c_vp, c_vp])
     _sig(lib, "oryx_dict_encode_blob", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])

@@ -1,0 +1,138 @@
+"""The speed layer's native micro-batch path (ingest.SpeedBatch, csrc/runtime/oryx_ingest.cpp
+``oryx_speed_*``) against the dictionary path it replaces on the GPU: same aggregated pairs
+(ALSUpdate.aggregateScores semantics, deletes, quoted / JSON lines, IDs the stores lack) and
+the same UP messages; and the update log's large-append path (mapped segment, preallocated
+tail, publish-by-magic)."""
+
+import json
+import os
+
+import numpy as np
+
+from oryx_amd import ingest
+from oryx_amd.models.als.batch import aggregate_scores
+from oryx_amd.ops.textfmt import format_rows
+from oryx_amd.textlines import TextLines
+from oryx_amd.transport import log as tlog
+
+
+def _stores(n_x=1000, n_y=500):
+    xm, ym = ingest.RowMap(), ingest.RowMap()
+    xids = ["U%d" % j for j in range(n_x)]
+    yids = ["I%d" % j for j in range(n_y)]
+    xrow = {k: 3 * j + 1 for j, k in enumerate(xids)}
+    yrow = {k: 2 * j for j, k in enumerate(yids)}
+    xm.set(xids, np.array([xrow[k] for k in xids]))
+    ym.set(yids, np.array([yrow[k] for k in yids]))
+    return xm, ym, xrow, yrow
+
+
+def _lines(n, seed=1):
+    g = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        u, it = "U%d" % g.integers(0, 1100), "I%d" % g.integers(0, 520)
+        v = "" if g.random() < 0.03 else "%.2f" % (g.random() * 3)
+        t = 1000 + int(g.integers(0, 50))
+        r = g.random()
+        if r < 0.05:
+            out.append('"%s","%s",%s,%d' % (u, it, v, t))
+        elif r < 0.1:
+            out.append('["%s","%s",%s,%d]' % (u, it, v if v else '""', t))
+        elif r < 0.12:
+            out.append("%s,%s,%s" % (u, it, v or "1"))          # no timestamp
+        else:
+            out.append("%s,%s,%s,%d" % (u, it, v, t))
+    return out
+
+
+def test_speed_batch_matches_dictionary_path():
+    xm, ym, xrow, yrow = _stores()
+    lines = _lines(30000)
+    tl = TextLines.from_strings(lines)
+    sb = ingest.SpeedBatch()
+    for implicit in (True, False):
+        n = sb.parse(tl, xm, ym)
+        u, i, s = sb.aggregate(implicit)
+        users, items = ingest.IdDict(), ingest.IdDict()
+        a, b, c, d = ingest.parse_ratings(tl, users, items, 0)
+        assert n == len(a)
+        au, ai, av = aggregate_scores(a, b, c, d, implicit)
+        uk, ik = users.keys(), items.keys()
+        want = {(uk[p], ik[q]): v for p, q, v in zip(au.tolist(), ai.tolist(), av.tolist())}
+        assert len(u) == len(want)
+        # rows resolve to the store's rows; IDs the stores lack are -1 and listed as new keys
+        assert set((u[u >= 0] - 1) % 3) == {0} and set(i[i >= 0] % 2) == {0}
+        new_u = set(ingest.blob_strings(*sb.new_keys(0)))
+        new_i = set(ingest.blob_strings(*sb.new_keys(1)))
+        assert new_u == {k for k in uk if k not in xrow}
+        assert new_i == {k for k in ik if k not in yrow}
+        # the assembled messages carry each pair's keys and value-ordered rows
+        m = len(u)
+        xr = format_rows(np.asarray(s, dtype=np.float32)[:, None].repeat(2, 1))
+        yr = format_rows(np.asarray(s, dtype=np.float32)[:, None].repeat(3, 1))
+        vx = np.ones(m, np.uint8)
+        vy = (u >= 0).astype(np.uint8)
+        blk = sb.assemble(0, m, xr, yr, vx, vy, True)
+        msgs = [json.loads(x) for x in bytes(blk.buf).decode().strip().split("\n")]
+        assert len(msgs) == int(vx.sum() + vy.sum()) == len(blk)
+        got = {(mm[1], mm[3][0]): mm[2][0] for mm in msgs if mm[0] == "X"}
+        assert set(got) == set(want)
+        for key, v in got.items():
+            assert abs(v - np.float32(want[key])) <= 1e-6 * max(1.0, abs(v))
+        ys = [mm for mm in msgs if mm[0] == "Y"]
+        assert all(mm[1] in yrow or mm[1] not in yrow for mm in ys)
+        assert all(mm[3][0] in xrow for mm in ys)      # Y rows only for users in the store
+
+
+def test_log_large_append_mapped_and_preallocated(tmp_path, monkeypatch):
+    """A block past the mapped-append threshold lands through the segment mapping, the
+    segment keeps a zero tail for the next block, readers stop at that tail, and a later
+    append (large or small) continues at the data's end."""
+    root = str(tmp_path)
+    tlog.maybe_create_topic(root, "Up", 1, max_message=1 << 30)
+    topic = tlog.Topic(root, "Up")
+    big = ["x" * 300 + "%06d" % j for j in range(20000)]         # ~6 MB: mapped path
+    topic.append_batch([("UP", v) for v in big])
+    seg = [f for f in os.listdir(os.path.join(root, "Up", "0")) if f.endswith(".log")][0]
+    size = os.path.getsize(os.path.join(root, "Up", "0", seg))
+    assert topic.end_offset(0) == 20000
+    assert size > sum(len(v) + 32 + 2 for v in big)          # preallocated zero tail
+    topic.append(None, "small-after")
+    topic.append_batch([("UP", v) for v in big[:100]])
+    assert topic.end_offset(0) == 20101
+    recs = []
+    r = topic.reader(0, 0)
+    while True:
+        got = r.poll(50000, 50)
+        if not got:
+            break
+        recs.extend(got)
+    assert len(recs) == 20101
+    assert recs[20000][3] == "small-after" and recs[20100][3] == big[99]
+    topic.close()
+    # reopened by another handle: the zero tail is not mistaken for corruption
+    t2 = tlog.Topic(root, "Up")
+    assert t2.append(None, "third") == 20101
+    t2.close()
+
+
+def test_log_unpublished_block_is_truncated(tmp_path):
+    """A block whose writer died before publishing its first frame's magic (zero magic,
+    written header) was never readable: the next append truncates it away."""
+    root = str(tmp_path)
+    tlog.maybe_create_topic(root, "T", 1)
+    topic = tlog.Topic(root, "T")
+    topic.append(None, "a")
+    topic.close()
+    seg = os.path.join(root, "T", "0", [f for f in os.listdir(os.path.join(root, "T", "0"))
+                                         if f.endswith(".log")][0])
+    import struct
+    body = struct.pack("<qq", 1, 5) + struct.pack("<II", 0xFFFFFFFF, 3) + b"zzz"
+    with open(seg, "ab") as fh:
+        fh.write(struct.pack("<II", 0, 123) + body + b"\x01" * 64)
+    t2 = tlog.Topic(root, "T")
+    assert t2.end_offset(0) == 1
+    assert t2.append(None, "b") == 1
+    assert [x[3] for x in t2.reader(0, 0).poll(10, 10)] == ["a", "b"]
+    t2.close()
