@@ -27,6 +27,7 @@ OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_native")
 
 RUNTIME_SO = os.path.join(OUT, "liboryx_runtime.so")
 KERNELS_SO = os.path.join(OUT, "liboryx_kernels.so")
+TUNING_SO = os.path.join(OUT, "liboryx_kernels_tuning.so")
 
 ARCH = os.environ.get("ORYX_OFFLOAD_ARCH", "gfx950")
 
@@ -66,11 +67,18 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     return RUNTIME_SO
 
 
-def build_kernels(force: bool = False, verbose: bool = False) -> str:
+def build_kernels(force: bool = False, verbose: bool = False, tuning: bool = False) -> str:
+    """``liboryx_kernels.so``; ``tuning``: ``liboryx_kernels_tuning.so``, the same kernels plus
+    the superseded ones of ``csrc/kernels/tuning/`` (A/B runs: ``ORYX_KERNELS_SO`` points at
+    it and ``ORYX_ALS_VARIANT`` / ``ORYX_ALS_WIDE_VARIANT`` select them)."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    so = KERNELS_SO
+    if tuning:
+        srcs += sorted(glob.glob(os.path.join(CSRC, "kernels", "tuning", "*.hip")))
+        so = TUNING_SO
     os.makedirs(OUT, exist_ok=True)
-    if force or _stale(KERNELS_SO, srcs + hdrs):
+    if force or _stale(so, srcs + hdrs):
         hipcc = _hipcc()
         objdir = os.path.join(OUT, "obj")
         os.makedirs(objdir, exist_ok=True)
@@ -92,14 +100,14 @@ def build_kernels(force: bool = False, verbose: bool = False) -> str:
             out, _ = p.communicate()
             if p.returncode != 0:
                 raise RuntimeError("native build failed:\n$ %s\n%s" % (" ".join(cmd), out))
-        tmp = KERNELS_SO + ".tmp"
+        tmp = so + ".tmp"
         cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs
         if verbose:
             print(" ".join(cmd), flush=True)
         _run(cmd)
         _check_no_missing_stubs(tmp)
-        os.replace(tmp, KERNELS_SO)
-    return KERNELS_SO
+        os.replace(tmp, so)
+    return so
 
 
 def _check_no_missing_stubs(so: str) -> None:
@@ -122,4 +130,7 @@ def build(force: bool = False, verbose: bool = False) -> List[str]:
 
 
 if __name__ == "__main__":
-    print("\n".join(build(force="--force" in sys.argv, verbose=True)))
+    if "--tuning" in sys.argv:
+        print(build_kernels(force="--force" in sys.argv, verbose=True, tuning=True))
+    else:
+        print("\n".join(build(force="--force" in sys.argv, verbose=True)))

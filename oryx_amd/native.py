@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 18
+KERNELS_ABI_VERSION = 19
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -191,22 +191,33 @@ def _load_kernels():
     _sig(lib, "oryx_als_set_variant", c_i, [c_i])
     _sig(lib, "oryx_als_get_variant", c_i, [])
     _sig(lib, "oryx_als_batch_profile", c_i, [c_vp])
-    lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "5")))
+    rc_variant = lib.oryx_als_set_variant(int(os.environ.get("ORYX_ALS_VARIANT", "5")))
+    if rc_variant != 0:
+        raise RuntimeError("ORYX_ALS_VARIANT=%s needs the tuning build of the kernels "
+                           "(python -m oryx_amd._build --tuning; ORYX_KERNELS_SO=%s)"
+                           % (os.environ.get("ORYX_ALS_VARIANT"), _build.TUNING_SO))
     # ORYX_ALS_WIDE_VARIANT: 64 < k <= 128 and fp32-mode solve (2 = als_solve_batch_gl,
     # 0 = als_solve_wide / als_solve_wave, 1 = als_solve_block)
     _sig(lib, "oryx_als_set_wide_variant", c_i, [c_i])
     _sig(lib, "oryx_als_get_wide_variant", c_i, [])
-    lib.oryx_als_set_wide_variant(int(os.environ.get("ORYX_ALS_WIDE_VARIANT", "2")))
+    if lib.oryx_als_set_wide_variant(int(os.environ.get("ORYX_ALS_WIDE_VARIANT", "2"))) != 0:
+        raise RuntimeError("ORYX_ALS_WIDE_VARIANT=%s needs the tuning build of the kernels "
+                           "(python -m oryx_amd._build --tuning; ORYX_KERNELS_SO=%s)"
+                           % (os.environ.get("ORYX_ALS_WIDE_VARIANT"), _build.TUNING_SO))
     # ..., n_long, ws, split (fp32 factors as bf16 hi|lo rows of 2*kp), stream
     _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                       c_i, c_f, c_f, c_i, c_vp, c_vp, c_vp, c_i, c_i, c_vp,
                                       c_i, c_ll, c_vp])
     _sig(lib, "oryx_als_ws_stride", c_i, [c_i])
-    _sig(lib, "oryx_als_solve_profile64", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i,
-                                                c_i, c_f, c_f, c_i, c_vp, c_vp])
     _sig(lib, "oryx_gramian_ws_floats", c_i, [c_i])
-    _sig(lib, "oryx_als_debug_gram", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_f, c_i, c_ll, c_ll,
-                                           c_vp, c_i, c_vp])
+    _sig(lib, "oryx_als_tuning_available", c_i, [])
+    if lib.oryx_als_tuning_available():
+        # superseded kernels and their analysis entry points: the tuning build only
+        # (python -m oryx_amd._build --tuning; csrc/kernels/tuning/als_variants.hip)
+        _sig(lib, "oryx_als_solve_profile64", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                                    c_i, c_i, c_f, c_f, c_i, c_i, c_vp, c_vp])
+        _sig(lib, "oryx_als_debug_gram", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_f, c_i, c_ll,
+                                               c_ll, c_vp, c_i, c_vp])
     _sig(lib, "oryx_gramian_f32", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])
     # one-shot IPC all-reduce (ipc_allreduce.hip; parallel/ipc.py)

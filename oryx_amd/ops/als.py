@@ -229,6 +229,12 @@ def gramian(x: torch.Tensor) -> torch.Tensor:
     return x.t().matmul(x)
 
 
+def tuning_kernels_available() -> bool:
+    """Whether the loaded kernel library holds the superseded solve kernels (the tuning build,
+    ``csrc/kernels/tuning/``); the default build has only the als_batch.hip ones."""
+    return bool(native.require_kernels().oryx_als_tuning_available())
+
+
 @contextlib.contextmanager
 def solve_variant(v: int):
     """Temporarily select the KP <= 64 solve kernel (``ORYX_ALS_VARIANT`` values; A/B tests)."""

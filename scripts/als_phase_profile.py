@@ -80,6 +80,7 @@ def main():
                                           csr.cols.data_ptr(), csr.vals.data_ptr(),
                                           src_b.data_ptr(), yty.data_ptr(), dst.data_ptr(),
                                           int(csr.order.numel()), 64, 0.001, 1.0, 1,
+                                          int(os.environ.get("ORYX_ALS_VARIANT", "1")),
                                           prof.data_ptr(), native.stream_ptr(dev))
         native.check(rc, "profile")
         torch.cuda.synchronize()
