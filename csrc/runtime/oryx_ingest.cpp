@@ -1103,6 +1103,115 @@ long long oryx_csv_numeric_block(const char* buf, long long len, int F,
   return rows[(size_t)P];
 }
 
+// Numeric CSV rows straight to a float32 matrix (the k-means / RDF batch layers' parse of
+// millions of feature rows): every non-empty line of buf has exactly F comma-separated fields;
+// field f goes to column out_col[f] of out ([rows][P], out_col -1: skipped).  Numeric fields
+// (is_num[f]) are parsed exactly to double and rounded to float32 (as float(x) -> np.float32);
+// an empty numeric field is NaN.  Fields that are not numeric are recorded as spans
+// (span_off/span_len [rows][S], S = number of such fields, in field order; nullable when S =
+// 0).  Lines with quotes, backslash escapes or JSON arrays, or a field count other than F,
+// stop the parse: returns -(line + 1) of the first such line, else the number of rows (-2 when
+// more than max_rows).  Threads over line-aligned chunks.
+}  // extern "C"
+
+namespace {
+
+template <typename T>
+long long csv_to_matrix(const char* buf, long long len, int F, const unsigned char* is_num,
+                        const int* out_col, int P, T* out, long long* span_off, int* span_len,
+                        long long max_rows) {
+  int S = 0;
+  std::vector<int> span_idx((size_t)F, -1);
+  for (int f = 0; f < F; ++f)
+    if (!is_num[f]) span_idx[(size_t)f] = S++;
+  const int P_ = split_threads(len);
+  std::vector<const char*> cut = line_chunks(buf, len, P_);
+  std::vector<long long> rows((size_t)P_ + 1, 0), bad((size_t)P_, -1), lines((size_t)P_, 0);
+  oryx_ff::parallel_ranges(P_, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      long long r = 0, l = 0;
+      for (const char* p = cut[(size_t)t]; p < cut[(size_t)t + 1];) {
+        const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(cut[(size_t)t + 1] - p)));
+        const char* le = nl ? nl : cut[(size_t)t + 1];
+        if (le > p && !(le - p == 1 && *p == '\r')) ++r;
+        ++l;
+        p = nl ? nl + 1 : cut[(size_t)t + 1];
+      }
+      rows[(size_t)t + 1] = r;
+      lines[(size_t)t] = l;
+    }
+  });
+  for (int t = 0; t < P_; ++t) rows[(size_t)t + 1] += rows[(size_t)t];
+  if (rows[(size_t)P_] > max_rows) return -2;
+  oryx_ff::parallel_ranges(P_, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      long long row = rows[(size_t)t], line = 0;
+      for (const char* p = cut[(size_t)t]; p < cut[(size_t)t + 1];) {
+        const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(cut[(size_t)t + 1] - p)));
+        const char* le = nl ? nl : cut[(size_t)t + 1];
+        const char* lend = le;
+        if (lend > p && lend[-1] == '\r') --lend;
+        if (lend > p) {
+          T* o = out + row * P;
+          const char* q = p;
+          int f = 0;
+          bool ok = *p != '[' && !memchr(p, '\\', (size_t)(lend - p));
+          while (ok) {
+            const char* c = static_cast<const char*>(memchr(q, ',', (size_t)(lend - q)));
+            const char* fe = c ? c : lend;
+            if (f >= F || memchr(q, '"', (size_t)(fe - q))) { ok = false; break; }
+            if (is_num[f]) {
+              double v;
+              if (fe == q) v = std::numeric_limits<double>::quiet_NaN();
+              else if (!oryx_ff::parse_double(q, fe, v)) { ok = false; break; }
+              if (out_col[f] >= 0) o[out_col[f]] = (T)v;
+            } else {
+              const int si = span_idx[(size_t)f];
+              span_off[row * S + si] = q - buf;
+              span_len[row * S + si] = (int)(fe - q);
+              if (out_col[f] >= 0) o[out_col[f]] = std::numeric_limits<T>::quiet_NaN();
+            }
+            ++f;
+            if (!c) break;
+            q = c + 1;
+          }
+          if (!ok || f != F) {
+            bad[(size_t)t] = line;
+            return;
+          }
+          ++row;
+        }
+        ++line;
+        p = nl ? nl + 1 : cut[(size_t)t + 1];
+      }
+    }
+  });
+  long long before = 0;
+  for (int t = 0; t < P_; ++t) {
+    if (bad[(size_t)t] >= 0) return -(before + bad[(size_t)t] + 1);
+    before += lines[(size_t)t];
+  }
+  return rows[(size_t)P_];
+}
+
+}  // namespace
+
+extern "C" {
+
+long long oryx_csv_to_f32(const char* buf, long long len, int F, const unsigned char* is_num,
+                          const int* out_col, int P, float* out, long long* span_off,
+                          int* span_len, long long max_rows) {
+  return csv_to_matrix<float>(buf, len, F, is_num, out_col, P, out, span_off, span_len,
+                              max_rows);
+}
+
+long long oryx_csv_to_f64(const char* buf, long long len, int F, const unsigned char* is_num,
+                          const int* out_col, int P, double* out, long long* span_off,
+                          int* span_len, long long max_rows) {
+  return csv_to_matrix<double>(buf, len, F, is_num, out_col, P, out, span_off, span_len,
+                               max_rows);
+}
+
 // Formats rows of a float matrix as JSON arrays "[v0,v1,...]" with shortest round-trip
 // float32 text (fastfloat.h), back to back in out; row_ends[r] = end offset of row r.  Rows are
 // split over the native threads (each formats its range into its own buffer, then the parts

@@ -1,0 +1,296 @@
+"""Feature rows of the k-means and RDF batch layers: native parse straight to a device matrix,
+and the resident parsed history of past part files.
+
+The reference parses every record of every generation inside Spark tasks
+(``[mllib]/kmeans/KMeansUpdate.java:223-232`` ``parsedToVectorRDD``,
+``[mllib]/rdf/RDFUpdate.java:228-260`` ``parseToLabeledPointRDD`` after
+``getDistinctValues`` ``:207-225``).  Here one native, threaded pass
+(``csrc/runtime/oryx_ingest.cpp`` ``oryx_csv_to_f32`` / ``_f64``) turns a buffer of CSV lines
+into a float matrix -- numeric fields exactly parsed, empty numeric fields NaN -- and records
+the byte spans of categorical fields, which are then encoded column by column with one
+vectorised unique per column (codes in order of first appearance, as the reference's
+encodings).
+
+:class:`FeatureHistory` keeps each past part file's parse on the training device, keyed by
+the file's identity (``layers.batch.read_past_data`` marks each part file's byte range with
+``(path, size, mtime)``), with segment-local categorical codes; a generation merges the
+segments' distinct values in segment order -- the first-appearance order one parse of the
+concatenated text gives -- and remaps each segment's codes with one device gather.  The new
+interval's parse is remembered under a hash of its bytes and adopted when the same bytes come
+back as a part file, so in steady state every record is parsed once.
+
+Lines the native parser does not take (quoted fields, backslash escapes, JSON arrays, a field
+count other than the schema's) make the whole input go through the reference-compatible
+Python parser instead (``utils.text.parse_input_line``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import logging
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import native
+from ..textlines import TextLines
+from .schema import InputSchema
+
+try:
+    import xxhash
+except ImportError:   # pragma: no cover - no adoption of unkeyed parses without it
+    xxhash = None
+
+log = logging.getLogger(__name__)
+
+__all__ = ["FeatureBlock", "FeatureHistory", "parse_features"]
+
+
+@dataclass
+class FeatureBlock:
+    """Parsed feature rows: ``full`` [n, F] (numeric features as values, categorical ones as
+    codes into ``values[f]``), on ``full.device``."""
+    full: torch.Tensor
+    values: Dict[int, List[str]] = field(default_factory=dict)
+
+    def __len__(self) -> int:
+        return int(self.full.shape[0])
+
+    def predictors(self, schema: InputSchema) -> torch.Tensor:
+        idx = list(schema.predictor_feature_indices)
+        if idx and idx == list(range(idx[0], idx[0] + len(idx))):
+            return self.full[:, idx[0]:idx[0] + len(idx)]
+        return self.full[:, idx]
+
+    def target(self, schema: InputSchema) -> torch.Tensor:
+        if not schema.has_target():
+            return torch.full((len(self),), float("nan"), dtype=self.full.dtype,
+                              device=self.full.device)
+        return self.full[:, schema.get_target_feature_index()]
+
+
+@dataclass
+class _Seg:
+    full: torch.Tensor                 # categorical columns hold segment-local codes
+    values: Dict[int, List[str]]       # categorical feature -> segment-local distinct values
+    nbytes: int
+
+
+def _buf_view(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return buf
+    return np.frombuffer(bytes(buf), dtype=np.uint8)
+
+
+def _native_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: InputSchema,
+                  dtype: torch.dtype) -> Optional[Tuple[np.ndarray, Dict[int, np.ndarray],
+                                                       Dict[int, List[str]]]]:
+    """(matrix [rows, F] with categorical columns as local codes, -, local distinct values) of
+    bytes [off, off + nbytes) of ``buf``, or None when a line needs the general parser."""
+    F = schema.get_num_features()
+    is_num = np.array([0 if schema.is_categorical(f) else 1 for f in range(F)], dtype=np.uint8)
+    cats = [f for f in range(F) if schema.is_categorical(f)]
+    S = len(cats)
+    out_col = np.arange(F, dtype=np.int32)
+    np_dtype = np.float32 if dtype == torch.float32 else np.float64
+    full = np.empty((max(n_lines, 1), F), dtype=np_dtype)
+    span_off = np.empty((max(n_lines, 1), max(S, 1)), dtype=np.int64)
+    span_len = np.empty((max(n_lines, 1), max(S, 1)), dtype=np.int32)
+    lib = native.runtime()
+    fn = lib.oryx_csv_to_f32 if np_dtype == np.float32 else lib.oryx_csv_to_f64
+    base = buf.ctypes.data + off
+    vp = ctypes.c_void_p
+    got = fn(vp(base), int(nbytes), F, is_num.ctypes.data_as(vp), out_col.ctypes.data_as(vp), F,
+             full.ctypes.data_as(vp), span_off.ctypes.data_as(vp), span_len.ctypes.data_as(vp),
+             int(max(n_lines, 1)))
+    if got < 0:
+        return None
+    n = int(got)
+    full = full[:n]
+    values: Dict[int, List[str]] = {}
+    seg = buf[off:off + nbytes]
+    for si, f in enumerate(cats):
+        o = span_off[:n, si] - off
+        ln = span_len[:n, si]
+        L = int(ln.max()) if n else 0
+        if L > 0:
+            j = np.arange(L)
+            g = seg[np.minimum(o[:, None] + j, max(len(seg) - 1, 0))]
+            g[j >= ln[:, None]] = 0
+            vals = np.ascontiguousarray(g).view("S%d" % L).ravel()
+        else:
+            vals = np.zeros(n, dtype="S1")
+        uniq, first, inv = np.unique(vals, return_index=True, return_inverse=True)
+        # local codes in order of first appearance (the reference's encoding order)
+        order = np.argsort(first, kind="stable")
+        rank = np.empty(len(uniq), dtype=np.int64)
+        rank[order] = np.arange(len(uniq))
+        codes = rank[inv.reshape(-1)].astype(np_dtype)
+        names = [u.decode("utf-8") for u in uniq[order].tolist()]
+        if "" in names:
+            # an empty categorical value is missing (NaN), not a category
+            e = names.index("")
+            codes = np.where(codes == e, np.nan, np.where(codes > e, codes - 1, codes))
+            names = names[:e] + names[e + 1:]
+        full[:, f] = codes
+        values[f] = names
+    return full, {}, values
+
+
+def _python_block(lines: Sequence[str], schema: InputSchema, dtype: torch.dtype
+                  ) -> Tuple[np.ndarray, Dict[int, List[str]]]:
+    """The general parser (``parse_input_line``: quotes, escapes, JSON arrays)."""
+    from ..utils import text
+    F = schema.get_num_features()
+    rows = [text.parse_input_line(l) for l in lines]
+    rows = [r for r in rows if r is not None]
+    np_dtype = np.float32 if dtype == torch.float32 else np.float64
+    full = np.empty((len(rows), F), dtype=np_dtype)
+    values: Dict[int, List[str]] = {}
+    for f in range(F):
+        col = [r[f] if f < len(r) else "" for r in rows]
+        if schema.is_categorical(f):
+            seen: Dict[str, int] = {}
+            codes = []
+            for v in col:
+                if v == "":
+                    codes.append(np.nan)
+                    continue
+                codes.append(seen.setdefault(v, len(seen)))
+            full[:, f] = np.asarray(codes, dtype=np.float64)
+            values[f] = list(seen.keys())
+        elif schema.is_numeric(f):
+            full[:, f] = [float(v) if v != "" else np.nan for v in col]
+        else:
+            full[:, f] = np.nan
+    return full, values
+
+
+def _merge(segs: List[_Seg], schema: InputSchema, device) -> FeatureBlock:
+    F = schema.get_num_features()
+    cats = [f for f in range(F) if schema.is_categorical(f)]
+    if not segs:
+        return FeatureBlock(torch.zeros((0, F), device=device), {f: [] for f in cats})
+    full = torch.cat([sg.full for sg in segs]) if len(segs) > 1 else segs[0].full.clone()
+    values: Dict[int, List[str]] = {}
+    for f in cats:
+        index: Dict[str, int] = {}
+        pos = 0
+        for sg in segs:
+            local = sg.values.get(f, [])
+            remap = np.array([index.setdefault(v, len(index)) for v in local], dtype=np.float64)
+            n = int(sg.full.shape[0])
+            if len(local) and not np.array_equal(remap, np.arange(len(local))):
+                col = full[pos:pos + n, f]
+                ok = ~torch.isnan(col)
+                m = torch.from_numpy(remap).to(device, full.dtype)
+                col[ok] = m[col[ok].long()]
+            pos += n
+        values[f] = list(index.keys())
+    return FeatureBlock(full, values)
+
+
+def parse_features(lines, schema: InputSchema, device, dtype: torch.dtype = torch.float32,
+                   history: Optional["FeatureHistory"] = None) -> FeatureBlock:
+    """All records -> :class:`FeatureBlock` on ``device`` (see the module docstring)."""
+    if history is not None:
+        return history.parse(lines, schema, dtype)
+    return FeatureHistory(device, keep=False).parse(lines, schema, dtype)
+
+
+class FeatureHistory:
+    """Parse cache of keyed :class:`TextLines` segments of feature rows (module docstring).
+    ``keep=False``: a one-off parse (nothing is cached)."""
+
+    UNKEYED_MIN_BYTES = 1 << 20
+    UNKEYED_KEEP = 4
+
+    def __init__(self, device=None, keep: bool = True):
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.keep = keep
+        self._segs: "OrderedDict[tuple, _Seg]" = OrderedDict()
+        self._unkeyed: "OrderedDict[bytes, _Seg]" = OrderedDict()
+        self._schema_key = None
+        self.stats = {"hits": 0, "misses": 0, "hit_bytes": 0, "parsed_bytes": 0, "adopted": 0}
+
+    def __len__(self) -> int:
+        return len(self._segs)
+
+    def resident_bytes(self) -> int:
+        segs = list(self._segs.values()) + list(self._unkeyed.values())
+        return sum(int(sg.full.numel()) * sg.full.element_size() for sg in segs)
+
+    def clear(self) -> None:
+        self._segs.clear()
+        self._unkeyed.clear()
+
+    @staticmethod
+    def _digest(buf: np.ndarray, off: int, nbytes: int) -> Optional[bytes]:
+        if xxhash is None:
+            return None
+        return xxhash.xxh3_128_digest(buf[off:off + nbytes]) + nbytes.to_bytes(8, "little")
+
+    def _parse_range(self, buf: np.ndarray, off: int, nbytes: int, n_lines: int,
+                     schema: InputSchema, dtype) -> Optional[_Seg]:
+        got = _native_block(buf, off, nbytes, n_lines, schema, dtype)
+        if got is None:
+            return None
+        full, _, values = got
+        return _Seg(torch.from_numpy(full).to(self.device), values, nbytes)
+
+    def parse(self, lines, schema: InputSchema, dtype=torch.float32) -> FeatureBlock:
+        key_s = (tuple(schema.feature_names), tuple(schema.is_categorical(f) for f in
+                                                    range(schema.get_num_features())), dtype)
+        if self._schema_key != key_s:
+            self.clear()
+            self._schema_key = key_s
+        if not isinstance(lines, TextLines):
+            lines = TextLines.from_strings([l for l in lines]) if len(lines) else \
+                TextLines(b"", 0)
+        buf = _buf_view(lines.joined())
+        segs: List[_Seg] = []
+        keyed = set()
+        off = 0
+        for key, n_lines, nbytes in lines.segment_list():
+            if nbytes == 0:
+                continue
+            sg = self._segs.get(key) if (key is not None and self.keep) else None
+            if sg is not None and sg.nbytes == nbytes:
+                self.stats["hits"] += 1
+                self.stats["hit_bytes"] += nbytes
+                self._segs.move_to_end(key)
+            else:
+                dg = self._digest(buf, off, nbytes) \
+                    if (self.keep and nbytes >= self.UNKEYED_MIN_BYTES) else None
+                sg = self._unkeyed.get(dg) if (dg is not None and key is not None) else None
+                if sg is not None:
+                    self.stats["adopted"] += 1
+                    self.stats["hit_bytes"] += nbytes
+                    del self._unkeyed[dg]
+                else:
+                    sg = self._parse_range(buf, off, nbytes, n_lines, schema, dtype)
+                    if sg is None:
+                        # a line the native parser does not take: the general parser for all
+                        full, values = _python_block(list(lines), schema, dtype)
+                        blk = FeatureBlock(torch.from_numpy(full).to(self.device), {})
+                        blk.values = values
+                        return blk
+                    self.stats["misses"] += 1
+                    self.stats["parsed_bytes"] += nbytes
+                    if key is None and dg is not None:
+                        self._unkeyed[dg] = sg
+                        while len(self._unkeyed) > self.UNKEYED_KEEP:
+                            self._unkeyed.popitem(last=False)
+                if key is not None and self.keep:
+                    self._segs[key] = sg
+            if key is not None:
+                keyed.add(key)
+            segs.append(sg)
+            off += nbytes
+        if self.keep:
+            for k in [k for k in self._segs if k not in keyed]:
+                del self._segs[k]
+        return _merge(segs, schema, self.device)

@@ -10,16 +10,21 @@ Equivalent of ``KMeansUpdate`` (``[mllib]/kmeans/KMeansUpdate.java:68-232``):
   sizes -> PMML ``ClusteringModel`` (center-based, squared Euclidean) + DataDictionary;
 * ``evaluate``: train + test points scored with the configured strategy (higher is better).
 
-Divergence (deliberate): a cluster that ends up empty is re-seeded at the farthest point
-during Lloyd, so every published cluster has size >= 1 (MLlib can return an empty cluster,
-which the reference's ``fetchClusterCountsFromModel`` then fails on).
+Records are parsed natively straight to a device float32 matrix, and past part files' parses
+stay resident on the device across generations (:mod:`oryx_amd.models.features`).
+
+Divergence (deliberate, ``oryx.kmeans.reseed-empty-clusters``, default true): a cluster that
+ends up empty is re-seeded at the farthest point during Lloyd, so every published cluster has
+size >= 1.  MLlib keeps an empty cluster's old center (false here), and the reference's
+``fetchClusterCountsFromModel`` + ``pmmlClusteringModel`` then fail on the missing count
+(``KMeansUpdate.java:127-130``, ``:192-221``); with false this update publishes it with size 0.
 """
 
 from __future__ import annotations
 
 import logging
 import time
-from typing import List
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
@@ -28,11 +33,12 @@ from ...ml import hyperparams as hp
 from ...ml.mlupdate import MLUpdate
 from ...ops import kmeans as km_ops
 from ...parallel import dist
+from ...textlines import concat_lines
 from ...utils import rng
+from ..features import FeatureHistory, parse_features
 from ..schema import InputSchema
 from . import evaluation
-from .common import parse_feature_matrix, read_clusters, validate_pmml_vs_schema, \
-    clustering_model_pmml
+from .common import read_clusters, validate_pmml_vs_schema, clustering_model_pmml
 
 __all__ = ["KMeansUpdate"]
 
@@ -54,6 +60,12 @@ class KMeansUpdate(MLUpdate):
         self.input_schema = InputSchema(config)
         from ...utils import config as cfg
         self.precision = cfg.get_optional_string(config, "oryx.gpu.dtype") or "fp32"
+        rs = cfg.get_optional_bool(config, "oryx.kmeans.reseed-empty-clusters")
+        self.reseed_empty = True if rs is None else bool(rs)
+        rh = cfg.get_optional_bool(config, "oryx.kmeans.resident-history")
+        self.resident_history = True if rh is None else bool(rh)
+        self.history: Optional[FeatureHistory] = None
+        self.phase_seconds: Dict[str, float] = {}
         if self.max_iterations <= 0 or self.number_of_runs <= 0:
             raise ValueError("iterations and runs must be > 0")
         if self.initialization_strategy not in _INIT_STRATEGIES:
@@ -78,48 +90,72 @@ class KMeansUpdate(MLUpdate):
     def _sharded(self, ctx) -> bool:
         return ctx.is_distributed and self.dist_ctx is not None and self.dist_ctx.is_distributed
 
+    def _history_for(self, device) -> Optional[FeatureHistory]:
+        if not self.resident_history:
+            return None
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        if self.history is None or self.history.device != dev:
+            self.history = FeatureHistory(dev)
+        return self.history
+
+    def _points(self, lines, ctx) -> torch.Tensor:
+        """This rank's records -> predictor matrix, float32 on the device."""
+        tp = time.perf_counter()
+        blk = parse_features(lines, self.input_schema, ctx.device, torch.float32,
+                             history=self._history_for(ctx.device))
+        x = blk.predictors(self.input_schema).contiguous()
+        self.phase_seconds["parse"] = self.phase_seconds.get("parse", 0.0) + \
+            time.perf_counter() - tp
+        return x
+
     def build_model(self, context, train_data, hyper_parameters, candidate_path):
         k = int(hyper_parameters[0])
         if k <= 1:
             raise ValueError("k must be > 1")
         ctx = self._ctx(context)
-        x = parse_feature_matrix(list(train_data), self.input_schema)
+        x = self._points(train_data, ctx)
         sharded = self._sharded(ctx)
+        n = int(x.shape[0])
         if sharded:
             from ...parallel import shuffle
-            if sum(shuffle.all_gather_int(len(x), ctx)) == 0:
+            if sum(shuffle.all_gather_int(n, ctx)) == 0:
                 return None
-            if len(x) == 0:
-                x = np.zeros((0, self.input_schema.get_num_predictors()), dtype=np.float64)
-        elif len(x) == 0:
+        elif n == 0:
             return None
         t0 = time.perf_counter()
         # sharded: this rank's share of the records; otherwise every rank parsed everything
         # and takes a disjoint slice
-        rows = x if sharded else x[ctx.rank::ctx.world_size]
-        local = torch.from_numpy(rows.astype(np.float32)).to(ctx.device)
+        local = x if sharded else x[ctx.rank::ctx.world_size].contiguous()
         res = km_ops.kmeans_train(local, k, self.max_iterations, self.number_of_runs,
                                   self.initialization_strategy, seed=rng.next_seed(),
-                                  ctx=ctx, precision=self.precision)
+                                  ctx=ctx, precision=self.precision,
+                                  reseed_empty=self.reseed_empty)
         centers = res.centers.double().cpu().numpy()
         sizes = res.counts.cpu().numpy()
-        log.info("k-means k=%d on %d points x %d: cost %.6g, %d iterations, %.3fs", k, len(x),
+        self.phase_seconds["train"] = self.phase_seconds.get("train", 0.0) + \
+            time.perf_counter() - t0
+        log.info("k-means k=%d on %d points x %d: cost %.6g, %d iterations, %.3fs", k, n,
                  x.shape[1], res.cost, res.iterations, time.perf_counter() - t0)
         if not ctx.is_main and not sharded:
             return None
-        return clustering_model_pmml(self.input_schema, centers, sizes)
+        tp = time.perf_counter()
+        pmml = clustering_model_pmml(self.input_schema, centers, sizes)
+        self.phase_seconds["pmml"] = self.phase_seconds.get("pmml", 0.0) + \
+            time.perf_counter() - tp
+        return pmml
 
     def evaluate(self, context, model, model_parent_path, test_data, train_data):
         validate_pmml_vs_schema(model, self.input_schema)
-        x = parse_feature_matrix(list(train_data) + list(test_data), self.input_schema)
-        clusters = read_clusters(model)
         ctx = self._ctx(context)
+        x = self._points(concat_lines([train_data, test_data]), ctx)
+        tp = time.perf_counter()
+        clusters = read_clusters(model)
         if self._sharded(ctx):
-            if len(x) == 0:
-                x = np.zeros((0, len(clusters[0].center)), dtype=np.float64)
             ev = evaluation.evaluate_sharded(self.evaluation_strategy, clusters, x, ctx,
                                              device=ctx.device)
         else:
             ev = evaluation.evaluate(self.evaluation_strategy, clusters, x, device=ctx.device)
+        self.phase_seconds["eval"] = self.phase_seconds.get("eval", 0.0) + \
+            time.perf_counter() - tp
         log.info("k-means eval (%s): %s", self.evaluation_strategy, ev)
         return ev

@@ -80,19 +80,22 @@ def _assign(x: torch.Tensor, c: torch.Tensor) -> Tuple[torch.Tensor, torch.Tenso
     return idx, dist
 
 
+def _rows(data) -> int:
+    return int(data.shape[0]) if isinstance(data, torch.Tensor) else len(data)
+
+
+def _as_dev(data, dev) -> torch.Tensor:
+    """Points as a device tensor (a device matrix -- the batch layer's parse -- stays put)."""
+    if isinstance(data, torch.Tensor):
+        return data.to(dev)
+    return torch.as_tensor(np.asarray(data, dtype=np.float64)).to(dev)
+
+
 def fetch_cluster_metrics(clusters: Sequence[ClusterInfo], data, device=None
                           ) -> Dict[int, ClusterMetric]:
     """cluster id -> ClusterMetric over the points assigned to it (absent if none)."""
-    dev = _device(device)
-    x = torch.as_tensor(np.asarray(data, dtype=np.float64)).to(dev)
-    c = _centers(clusters, dev)
-    k = len(clusters)
-    idx, dist = _assign(x, c)
-    cnt = torch.bincount(idx, minlength=k)
-    s1 = torch.zeros(k, dtype=torch.float64, device=dev).index_add_(0, idx, dist)
-    s2 = torch.zeros(k, dtype=torch.float64, device=dev).index_add_(0, idx, dist * dist)
-    cnt, s1, s2 = cnt.cpu().tolist(), s1.cpu().tolist(), s2.cpu().tolist()
-    return {clusters[j].id: ClusterMetric(cnt[j], s1[j], s2[j]) for j in range(k) if cnt[j] > 0}
+    st = local_cluster_stats(clusters, data, device)
+    return _metrics_from_arrays(clusters, st[:, 0], st[:, 1], st[:, 2])
 
 
 def sum_squared_error(clusters, data, device=None) -> float:
@@ -136,7 +139,14 @@ def fetch_sample_data(data: np.ndarray, max_size: int = MAX_SAMPLE_SIZE) -> np.n
 def silhouette_coefficient(clusters, data, device=None, max_sample: int = MAX_SAMPLE_SIZE
                            ) -> float:
     dev = _device(device)
-    sample = fetch_sample_data(np.asarray(data, dtype=np.float64), max_sample)
+    if isinstance(data, torch.Tensor):
+        n = int(data.shape[0])
+        if n > max_sample:
+            keep = torch.from_numpy(rng.get_random().generator.random(n) < (max_sample / n))
+            data = data[keep.to(data.device)]
+        sample = data.double().cpu().numpy()
+    else:
+        sample = fetch_sample_data(np.asarray(data, dtype=np.float64), max_sample)
     s = len(sample)
     if s == 0:
         return 0.0
@@ -200,22 +210,33 @@ def _metrics_from_arrays(clusters, cnt, s1, s2) -> Dict[int, ClusterMetric]:
             for j in range(len(clusters)) if cnt[j] > 0}
 
 
-def local_cluster_stats(clusters, x: np.ndarray, device=None) -> np.ndarray:
-    """[K, 3] float64 (count, sum d, sum d^2) of this rank's points ``x``."""
+def local_cluster_stats(clusters, x, device=None) -> np.ndarray:
+    """[K, 3] float64 (count, sum d, sum d^2) of this rank's points ``x`` (numpy or a device
+    tensor)."""
     dev = _device(device)
     k = len(clusters)
     out = np.zeros((k, 3), dtype=np.float64)
-    if len(x) == 0:
+    if _rows(x) == 0:
         return out
     c = _centers(clusters, dev)
-    xt = torch.as_tensor(np.asarray(x, dtype=np.float64)).to(dev)
-    if dev.type == "cuda" and len(x) >= 65536:
+    if dev.type == "cuda" and _rows(x) >= 65536:
         from ...ops import kmeans as km_ops
-        idx, _ = km_ops.assign(xt.float(), c.float(), precision="fp32")
+        # nearest center on the MFMA assignment kernel (certified fp32), the distance to it
+        # in fp64, in slices (no fp64 copy of a multi-GB point matrix)
+        xf = x.to(dev, torch.float32) if isinstance(x, torch.Tensor) else \
+            torch.from_numpy(np.asarray(x, dtype=np.float32)).to(dev)
+        idx, _ = km_ops.assign(xf.contiguous(), c.float(), precision="fp32")
         idx = idx.long()
-        dist = (xt - c[idx]).pow(2).sum(1).sqrt()
+        dist = torch.empty(xf.shape[0], dtype=torch.float64, device=dev)
+        step = max(1, (1 << 26) // max(1, xf.shape[1]))
+        xs = x.to(dev) if isinstance(x, torch.Tensor) else None
+        for lo in range(0, xf.shape[0], step):
+            hi = min(xf.shape[0], lo + step)
+            src = xs[lo:hi] if xs is not None else \
+                torch.from_numpy(np.asarray(x[lo:hi], dtype=np.float64)).to(dev)
+            dist[lo:hi] = (src.double() - c[idx[lo:hi]]).pow(2).sum(1).sqrt()
     else:
-        idx, dist = _assign(xt, c)
+        idx, dist = _assign(_as_dev(x, dev).double(), c)
     out[:, 0] = torch.bincount(idx, minlength=k).double().cpu().numpy()
     out[:, 1] = torch.zeros(k, dtype=torch.float64, device=dev).index_add_(
         0, idx, dist).cpu().numpy()
@@ -253,12 +274,17 @@ def evaluate_sharded(strategy: str, clusters, x_local: np.ndarray, ctx, device=N
     """Like :func:`evaluate` over the union of every rank's ``x_local`` (collective)."""
     from ...parallel import shuffle, dist as dist_
     if strategy == "SILHOUETTE":
-        n_all = sum(shuffle.all_gather_int(len(x_local), ctx))
+        n_local = _rows(x_local)
+        n_all = sum(shuffle.all_gather_int(n_local, ctx))
         p = min(1.0, MAX_SAMPLE_SIZE / max(1, n_all))
-        keep = rng.get_random().generator.random(len(x_local)) < p
-        samp = np.asarray(x_local, dtype=np.float64)[keep]
-        d = np.asarray(x_local).shape[1] if np.asarray(x_local).ndim == 2 else \
-            len(clusters[0].center)
+        keep = rng.get_random().generator.random(n_local) < p
+        if isinstance(x_local, torch.Tensor):
+            samp = x_local[torch.from_numpy(keep).to(x_local.device)].double().cpu().numpy()
+            d = int(x_local.shape[1]) if x_local.dim() == 2 else len(clusters[0].center)
+        else:
+            samp = np.asarray(x_local, dtype=np.float64)[keep]
+            d = np.asarray(x_local).shape[1] if np.asarray(x_local).ndim == 2 else \
+                len(clusters[0].center)
         parts = shuffle.all_gather_var(samp.reshape(-1), ctx)
         sample = np.concatenate(parts).reshape(-1, d)
         val = silhouette_coefficient(clusters, sample, device, max_sample=len(sample) + 1) \

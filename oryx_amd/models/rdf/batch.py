@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import io
 import logging
+import math
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -30,6 +31,7 @@ from ...ops import rdf as rdf_ops
 from ...parallel import dist
 from ...utils import rng, text
 from ..classreg import CategoricalPrediction, NumericPrediction
+from ..features import FeatureBlock, FeatureHistory, parse_features
 from ..schema import CategoricalValueEncodings, InputSchema
 from . import pmml as rdf_pmml
 from .pmml import TreeSpecNode
@@ -259,6 +261,14 @@ def evaluate_forest(forest, encodings, schema: InputSchema, full: np.ndarray,
 
 
 class RDFUpdate(MLUpdate):
+    """Sharded like the ALS and k-means updates: each rank parses and trains on its share of
+    the records (native parse, resident history of past part files); categorical encodings
+    are merged over the ranks (first appearance, rank order), split thresholds come from a
+    sample gathered from every rank, the level histograms are all-reduced, and evaluation
+    sums per-rank partial counts."""
+
+    sharded_data = True
+
     def __init__(self, config):
         super().__init__(config)
         self.num_trees = config.get_int("oryx.rdf.num-trees")
@@ -272,6 +282,11 @@ class RDFUpdate(MLUpdate):
         self.input_schema = InputSchema(config)
         if not self.input_schema.has_target():
             raise ValueError("RDF needs a target feature")
+        from ...utils import config as cfg
+        rh = cfg.get_optional_bool(config, "oryx.rdf.resident-history")
+        self.resident_history = True if rh is None else bool(rh)
+        self.history: Optional[FeatureHistory] = None
+        self.phase_seconds: Dict[str, float] = {}
 
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
@@ -282,6 +297,72 @@ class RDFUpdate(MLUpdate):
         c = getattr(context, "dist", None)
         return c if c is not None else dist.get_context()
 
+    def _sharded(self, ctx) -> bool:
+        return ctx.is_distributed and self.dist_ctx is not None and self.dist_ctx.is_distributed
+
+    def _history_for(self, device) -> Optional[FeatureHistory]:
+        if not self.resident_history:
+            return None
+        dev = torch.device(device) if device is not None else torch.device("cpu")
+        if self.history is None or self.history.device != dev:
+            self.history = FeatureHistory(dev)
+        return self.history
+
+    def _phase(self, name: str, t0: float) -> None:
+        self.phase_seconds[name] = self.phase_seconds.get(name, 0.0) + time.perf_counter() - t0
+
+    def _parse(self, lines, ctx) -> FeatureBlock:
+        tp = time.perf_counter()
+        blk = parse_features(lines, self.input_schema, ctx.device, torch.float64,
+                             history=self._history_for(ctx.device))
+        self._phase("parse", tp)
+        return blk
+
+    def _global_encodings(self, blk: FeatureBlock, ctx) -> CategoricalValueEncodings:
+        """Encodings over every rank's records (first appearance, rank order); this rank's
+        categorical columns are recoded to them in place."""
+        schema = self.input_schema
+        cats = [f for f in range(schema.get_num_features()) if schema.is_categorical(f)]
+        if not cats:
+            return CategoricalValueEncodings({})
+        mine = {f: blk.values.get(f, []) for f in cats}
+        if self._sharded(ctx):
+            allv = [None] * ctx.world_size
+            torch.distributed.all_gather_object(allv, mine, group=ctx.control)
+        else:
+            allv = [mine]
+        values: Dict[int, List[str]] = {}
+        for f in cats:
+            index: Dict[str, int] = {}
+            for part in allv:
+                for v in part.get(f, []):
+                    index.setdefault(v, len(index))
+            values[f] = list(index.keys())
+            local = mine[f]
+            remap = np.array([index[v] for v in local], dtype=np.float64)
+            if len(local) and not np.array_equal(remap, np.arange(len(local))):
+                col = blk.full[:, f]
+                ok = ~torch.isnan(col)
+                col[ok] = torch.from_numpy(remap).to(col.device, col.dtype)[col[ok].long()]
+        return CategoricalValueEncodings(values)
+
+    def _threshold_sample(self, X: torch.Tensor, ns: int, seed: int, ctx) -> torch.Tensor:
+        """The rows split thresholds are computed from: this rank's rows on one rank; with
+        several, an equal-rate sample of every rank's rows gathered to all (identical bins
+        everywhere, as MLlib's sampled split finding)."""
+        if not self._sharded(ctx):
+            return X
+        from ...parallel import shuffle
+        n = int(X.shape[0])
+        total = sum(shuffle.all_gather_int(n, ctx))
+        rate = min(1.0, ns / max(1, total))
+        g = np.random.default_rng((seed * 31 + ctx.rank) & ((1 << 62) - 1))
+        pick = np.nonzero(g.random(n) < rate)[0] if rate < 1.0 else np.arange(n)
+        local = X[torch.from_numpy(pick).to(X.device)].double().cpu().numpy()
+        parts = shuffle.all_gather_var(local.reshape(-1), ctx)
+        P = int(X.shape[1])
+        return torch.from_numpy(np.concatenate(parts).reshape(-1, P))
+
     def build_model(self, context, train_data, hyper_parameters, candidate_path):
         max_split_candidates = int(hyper_parameters[0])
         max_depth = int(hyper_parameters[1])
@@ -291,64 +372,110 @@ class RDFUpdate(MLUpdate):
         if max_depth <= 0:
             raise ValueError("max-depth must be at least 1")
         schema = self.input_schema
-        rows = [text.parse_input_line(l) for l in train_data]
-        if not rows:
-            return None
-        encodings = CategoricalValueEncodings(distinct_values(rows, schema))
-        X, target, _ = parse_examples(rows, schema, encodings)
         ctx = self._ctx(context)
+        sharded = self._sharded(ctx)
+        blk = self._parse(train_data, ctx)
+        if sharded:
+            from ...parallel import shuffle
+            n_all = sum(shuffle.all_gather_int(len(blk), ctx))
+        else:
+            n_all = len(blk)
+        if n_all == 0:
+            return None
+        tp = time.perf_counter()
+        encodings = self._global_encodings(blk, ctx)
+        X = blk.predictors(schema)
+        target = blk.target(schema)
+        num_pred = [p for p in range(X.shape[1])
+                    if not schema.is_categorical(schema.predictor_to_feature_index(p))]
+        if len(blk) and (bool(torch.isnan(target).any()) or
+                         (num_pred and bool(torch.isnan(X[:, num_pred]).any()))):
+            raise ValueError("missing target or numeric feature value")
         P = schema.get_num_predictors()
         categorical = [schema.is_categorical(schema.predictor_to_feature_index(p))
                        for p in range(P)]
         arities = [encodings.get_value_count(schema.predictor_to_feature_index(p))
                    if categorical[p] else 0 for p in range(P)]
         seed = rng.next_seed()
-        t0 = time.perf_counter()
-        # every rank holds the same parsed rows; each trains on a disjoint slice and the level
-        # histograms are all-reduced
-        sl = slice(ctx.rank, None, ctx.world_size)
+        ns = max(10000, max_split_candidates * max_split_candidates)
+        src = self._threshold_sample(X, ns, seed, ctx)
+        # one process: every rank parsed everything and bins a disjoint slice
+        sl = slice(None) if sharded else slice(ctx.rank, None, ctx.world_size)
         data = rdf_ops.bin_features(X[sl], categorical, arities, max_split_candidates,
-                                    ctx.device, seed=seed, threshold_source=X)
+                                    ctx.device, seed=seed, threshold_source=src)
+        self._phase("bin", tp)
+        t0 = time.perf_counter()
         classification = schema.is_classification()
         C = encodings.get_value_count(schema.get_target_feature_index()) if classification \
             else 0
-        tgt = torch.from_numpy(target[sl])
+        tgt = target[sl]
         trained = rdf_ops.train_forest(data, tgt, C, self.num_trees, max_depth, impurity,
                                        seed=seed, ctx=ctx)
+        self._phase("train", t0)
         log.info("RDF %d trees depth %d on %d examples x %d predictors: %.3fs", self.num_trees,
-                 max_depth, len(rows), P, time.perf_counter() - t0)
-        if not ctx.is_main:
+                 max_depth, n_all, P, time.perf_counter() - t0)
+        if not ctx.is_main and not sharded:
             return None
+        tp = time.perf_counter()
         total = trained.predictor_counts.sum()
         if total <= 0:
             importances = np.zeros(P)
         else:
             importances = trained.predictor_counts / total
         roots = [_to_spec(r, data, schema, classification) for r in trained.roots]
-        return rdf_pmml.forest_to_pmml(roots, schema, encodings, importances, max_depth,
+        pmml = rdf_pmml.forest_to_pmml(roots, schema, encodings, importances, max_depth,
                                        max_split_candidates, impurity)
+        self._phase("pmml", tp)
+        return pmml
 
     def evaluate(self, context, model, model_parent_path, test_data, train_data):
         rdf_pmml.validate_pmml_vs_schema(model, self.input_schema)
         forest, encodings = rdf_pmml.read(model)
-        rows = [text.parse_input_line(l) for l in test_data]
-        try:
-            _, target, full = parse_examples(rows, self.input_schema, encodings)
-        except KeyError:
-            # a categorical value never seen in training: score example by example
-            rows = [r for r in rows if self._known(r, encodings)]
-            _, target, full = parse_examples(rows, self.input_schema, encodings)
-        ev = evaluate_forest(forest, encodings, self.input_schema, full, target,
-                             self._ctx(context).device)
-        if self.input_schema.is_classification():
+        ctx = self._ctx(context)
+        schema = self.input_schema
+        blk = parse_features(test_data, schema, ctx.device, torch.float64)
+        tp = time.perf_counter()
+        full = blk.full
+        keep = torch.ones(len(blk), dtype=torch.bool, device=full.device)
+        # categorical values -> the model's encodings; a value never seen in training drops
+        # its example (the reference scores only examples it can encode)
+        for f, vals in blk.values.items():
+            m = encodings.get_value_encoding_map(f)
+            remap = np.array([m.get(v, -1) for v in vals], dtype=np.float64)
+            col = full[:, f]
+            ok = ~torch.isnan(col)
+            mapped = torch.full_like(col, float("nan"))
+            if len(remap):
+                mapped[ok] = torch.from_numpy(remap).to(col.device, col.dtype)[col[ok].long()]
+            keep &= ~(mapped < 0)
+            if not schema.is_target(f):
+                keep &= ~torch.isnan(mapped)
+            full[:, f] = mapped
+        full = full[keep]
+        target = full[:, schema.get_target_feature_index()]
+        keep_t = ~torch.isnan(target)
+        full, target = full[keep_t], target[keep_t]
+        classification = schema.is_classification()
+        C = encodings.get_value_count(schema.get_target_feature_index()) if classification \
+            else 0
+        if len(full):
+            flat = rdf_ops.flatten_forest(forest, ctx.device, C)
+            vote = rdf_ops.forest_vote(flat, full.contiguous())
+            if classification:
+                num = float((vote.argmax(1) == target.long()).double().sum())
+            else:
+                num = float(((vote[:, 0] - target) ** 2).sum())
+        else:
+            num = 0.0
+        parts = np.array([num, float(len(full))], dtype=np.float64)
+        if self._sharded(ctx):
+            from ...parallel import shuffle
+            parts = shuffle.all_reduce_np(parts, ctx)
+        self._phase("eval", tp)
+        if classification:
+            ev = float(parts[0] / parts[1]) if parts[1] else 0.0
             log.info("Accuracy: %s", ev)
             return ev
+        ev = math.sqrt(parts[0] / parts[1]) if parts[1] else float("nan")
         log.info("RMSE: %s", ev)
         return -ev
-
-    def _known(self, row, encodings) -> bool:
-        s = self.input_schema
-        for i in range(s.get_num_features()):
-            if s.is_categorical(i) and row[i] not in encodings.get_value_encoding_map(i):
-                return False
-        return True

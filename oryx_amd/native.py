@@ -116,6 +116,10 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_owners", c_ll, [c_vp, c_ll, c_i, c_vp])
     _sig(lib, "oryx_ts_range", c_ll, [c_vp, c_ll, c_ll, c_vp, c_vp])
+    _sig(lib, "oryx_csv_to_f32", c_ll, [c_vp, c_ll, c_i, c_vp, c_vp, c_i, c_vp, c_vp, c_vp,
+                                        c_ll])
+    _sig(lib, "oryx_csv_to_f64", c_ll, [c_vp, c_ll, c_i, c_vp, c_vp, c_i, c_vp, c_vp, c_vp,
+                                        c_ll])
     _sig(lib, "oryx_speed_new", c_vp, [])
     _sig(lib, "oryx_speed_free", None, [c_vp])
     _sig(lib, "oryx_speed_parse", c_ll, [c_vp, c_vp, c_ll, c_vp, c_vp, c_ll])

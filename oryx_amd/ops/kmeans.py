@@ -503,8 +503,13 @@ def lloyd_step(pts: PointSet, centers: torch.Tensor, ctx, workspace=None,
 def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
                  init: str = "k-means||", seed: int = 0, epsilon: float = 1e-4,
                  ctx: Optional[dist.DistContext] = None,
-                 precision: Optional[str] = None) -> KMeansResult:
-    """Train k-means on this rank's rows ``x`` (the union over ranks is the data)."""
+                 precision: Optional[str] = None, reseed_empty: bool = True) -> KMeansResult:
+    """Train k-means on this rank's rows ``x`` (the union over ranks is the data).
+
+    ``reseed_empty``: a cluster left without points by a Lloyd step is moved to the point
+    farthest from its center (deliberate difference, the default); False keeps its old
+    center as MLlib's Lloyd loop does (``KMeans.runAlgorithm``: only clusters with points are
+    updated), so an empty cluster can survive into the model with size 0."""
     pts = _as_points(x)
     x = pts.x
     ctx = ctx or dist.DistContext(device=x.device)
@@ -527,7 +532,7 @@ def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
             watchdog.heartbeat("kmeans.iteration")
             new, counts, d2, n_empty = lloyd_step(pts, centers, ctx, ws, precision)
             moved = None
-            if n_empty:
+            if n_empty and reseed_empty:
                 # re-seed empty clusters at the points farthest from their centers
                 far = _farthest_points(x, d2, n_empty, ctx)
                 if far.shape[0] == n_empty:

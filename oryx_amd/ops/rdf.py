@@ -135,7 +135,7 @@ def bin_features(X, categorical: Sequence[bool], arities: Sequence[int], max_bin
     dtype = torch.uint8 if B <= 256 else torch.int16
     Xb = torch.empty((n, _row_stride(P, dtype)), dtype=dtype, device=device)[:, :P]
     for f in range(P):
-        col = X[:, f].to(device, torch.float64) if on_device else \
+        col = X[:, f].to(device, torch.float64).contiguous() if on_device else \
             torch.from_numpy(np.ascontiguousarray(X[:, f])).to(device)
         if categorical[f]:
             b = col.to(torch.int64)

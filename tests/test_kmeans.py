@@ -235,6 +235,20 @@ def test_kmeans_reseeds_empty_clusters():
     assert sorted(res.counts.tolist()) == [5, 5, 5]
 
 
+def test_kmeans_keep_empty_cluster_like_mllib():
+    """reseed_empty=False (oryx.kmeans.reseed-empty-clusters = false): an empty cluster keeps
+    its center (MLlib's Lloyd loop) and survives with size 0; the default moves it to the
+    farthest point, so every cluster ends non-empty."""
+    x = torch.tensor([[0.0, 0.0]] * 6 + [[10.0, 0.0]] * 6 + [[0.0, 30.0]])
+    # seed 0: the random init draws two centers from one of the dense points
+    kept = km.kmeans_train(x, 3, 10, runs=1, init="random", seed=0, reseed_empty=False)
+    reseeded = km.kmeans_train(x, 3, 10, runs=1, init="random", seed=0, reseed_empty=True)
+    assert sorted(kept.counts.tolist()) == [0, 6, 7]
+    empty = int((kept.counts == 0).nonzero()[0])
+    assert kept.centers[empty].tolist() in ([0.0, 0.0], [10.0, 0.0])   # not moved
+    assert sorted(reseeded.counts.tolist()) == [1, 6, 6]
+
+
 def _update_config(tmp_path, strategy="SILHOUETTE"):
     return _conf(**{"oryx__input-schema__num-features": 4,
                     "oryx__input-schema__categorical-features": "[]",
