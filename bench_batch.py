@@ -44,10 +44,29 @@ def main(argv=None) -> int:
                          "new ratings and trains on them plus all earlier ones (the past part "
                          "files -- the resident parsed history's steady state)")
     ap.add_argument("--next-ratings", type=int, default=1_000_000)
-    ap.add_argument("--test-fraction", type=float, default=0.0,
+    ap.add_argument("--test-fraction", type=float, default=None,
                     help="oryx.ml.eval.test-fraction (the reference default is 0.1: the newest "
-                         "tenth of the interval's data is held out and AUC is evaluated)")
+                         "tenth of the interval's data is held out and evaluated); default 0.0 "
+                         "for ALS, 0.1 for k-means and RDF")
+    ap.add_argument("--app", default="als", choices=["als", "kmeans", "rdf"],
+                    help="als (default), kmeans (BASELINE config #4's per-GPU share: "
+                         "--points 12.5M x --dims 256, k 1000) or rdf (config #5's per-GPU "
+                         "share: --points 6.25M x --dims 100 predictors)")
+    ap.add_argument("--points", type=int, default=None)
+    ap.add_argument("--dims", type=int, default=None)
+    ap.add_argument("--k", type=int, default=1000, help="k-means clusters")
+    ap.add_argument("--trees", type=int, default=20, help="RDF trees")
+    ap.add_argument("--depth", type=int, default=8, help="RDF max depth")
+    ap.add_argument("--chunk", type=int, default=1 << 20, help="generated rows per append")
     args = ap.parse_args(argv)
+    if args.test_fraction is None:
+        args.test_fraction = 0.0 if args.app == "als" else 0.1
+    if args.app == "kmeans":
+        args.points = args.points or 12_500_000
+        args.dims = args.dims or 256
+    elif args.app == "rdf":
+        args.points = args.points or 6_250_000
+        args.dims = args.dims or 100
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oryx_amd.parallel import launch
@@ -66,22 +85,46 @@ def main(argv=None) -> int:
     if work is None:
         work = dist.broadcast_object(tempfile.mkdtemp(prefix="oryx_bench_batch_")
                                      if ctx.is_main else None, ctx)
-    conf = cfg.overlay_on({
-        "oryx.batch.update-class": "com.cloudera.oryx.app.batch.mllib.als.ALSUpdate",
+    base = {
         "oryx.input-topic.broker": "log:" + work + "/log",
         "oryx.update-topic.broker": "log:" + work + "/log",
         "oryx.input-topic.partitions": args.partitions,
+        "oryx.input-topic.message.max-size": 1 << 30,
         "oryx.update-topic.message.max-size": 1 << 30,
         "oryx.batch.storage.data-dir": work + "/data",
         "oryx.batch.storage.model-dir": work + "/model",
-        "oryx.als.hyperparams.features": args.features,
-        "oryx.als.iterations": args.iterations,
-        "oryx.als.implicit": "true",
         "oryx.ml.eval.candidates": 1,
         "oryx.ml.eval.test-fraction": args.test_fraction,
         "oryx.gpu.device": args.device,
         "oryx.gpu.dtype": args.dtype,
-    }, cfg.get_default())
+    }
+    if args.app == "als":
+        base.update({
+            "oryx.batch.update-class": "com.cloudera.oryx.app.batch.mllib.als.ALSUpdate",
+            "oryx.als.hyperparams.features": args.features,
+            "oryx.als.iterations": args.iterations,
+            "oryx.als.implicit": "true"})
+    elif args.app == "kmeans":
+        base.update({
+            "oryx.batch.update-class": "com.cloudera.oryx.app.batch.mllib.kmeans.KMeansUpdate",
+            "oryx.input-schema.num-features": args.dims,
+            "oryx.input-schema.categorical-features": "[]",
+            "oryx.kmeans.hyperparams.k": args.k,
+            "oryx.kmeans.iterations": args.iterations,
+            "oryx.kmeans.runs": 1,
+            "oryx.kmeans.evaluation-strategy": "SILHOUETTE",
+            "oryx.gpu.dtype": "fp32"})
+    else:
+        base.update({
+            "oryx.batch.update-class": "com.cloudera.oryx.app.batch.mllib.rdf.RDFUpdate",
+            "oryx.input-schema.num-features": args.dims + 1,
+            "oryx.input-schema.target-feature": '"%d"' % args.dims,
+            "oryx.input-schema.categorical-features": '["%d"]' % args.dims,
+            "oryx.rdf.num-trees": args.trees,
+            "oryx.rdf.hyperparams.max-depth": args.depth,
+            "oryx.rdf.hyperparams.max-split-candidates": 32,
+            "oryx.rdf.hyperparams.impurity": "gini"})
+    conf = cfg.overlay_on(base, cfg.get_default())
     layer = BatchLayer(conf)
     t_ingest = 0.0
     if ctx.is_main:
@@ -91,7 +134,42 @@ def main(argv=None) -> int:
         rng = np.random.default_rng(7)
         now = int(time.time() * 1000)
 
+        def append_features(n_total, now):
+            """k-means / RDF input generated on the device and formatted there as CSV lines
+            (values on a 0.01 grid): chunks appended round-robin over the partitions."""
+            from oryx_amd.ops import textfmt
+            from oryx_amd.api import MessageBlock
+            dev = ctx.device
+            g = torch.Generator(device=dev)
+            g.manual_seed(7)
+            topic = tlog.Topic(work + "/log", "OryxInput")
+            if args.app == "kmeans":
+                centers = torch.randn(args.k, args.dims, generator=g, device=dev) * 10
+            for j, lo in enumerate(range(0, n_total, args.chunk)):
+                m = min(args.chunk, n_total - lo)
+                if args.app == "kmeans":
+                    c = torch.randint(0, args.k, (m,), generator=g, device=dev)
+                    x = centers[c] + torch.randn(m, args.dims, generator=g, device=dev)
+                else:
+                    f = torch.randn(m, args.dims, generator=g, device=dev)
+                    y = ((f[:, 0] + f[:, 1] * f[:, 2] + 0.3 * f[:, 3]) > 0).float()
+                    x = torch.cat([f, y[:, None]], 1)
+                x = torch.round(x * 100) / 100
+                if dev.type == "cuda":
+                    rows = textfmt.format_csv(x)
+                    blk = MessageBlock(rows.blob, rows.ends - 1)
+                    topic.append_block(blk, partition=j % args.partitions,
+                                       timestamp_ms=now)
+                else:
+                    xs = x.cpu().numpy()
+                    lines = [",".join("%g" % v for v in row) for row in xs]
+                    topic.append_values(lines, partition=j % args.partitions,
+                                        timestamp_ms=now)
+            topic.close()
+
         def append(n_total, now):
+            if args.app != "als":
+                return append_features(n_total, now)
             topic = tlog.Topic(work + "/log", "OryxInput")
             chunk = 1 << 20
             for lo in range(0, n_total, chunk):
@@ -106,7 +184,8 @@ def main(argv=None) -> int:
             topic.close()
 
         t0 = time.perf_counter()
-        append(args.ratings, now)
+        n_records = args.ratings if args.app == "als" else args.points
+        append(n_records, now)
         t_ingest = time.perf_counter() - t0
         if torch.cuda.is_available():
             torch.cuda.synchronize()
@@ -151,20 +230,38 @@ def main(argv=None) -> int:
         ut = tlog.Topic(work + "/log", "OryxUpdate")
         ends = ut.end_offsets()
         ut.close()
+        n_records = args.ratings if args.app == "als" else args.points
+        metric = {"als": "ALS batch generation ratings/sec (input log -> published MODEL + UP "
+                         "rows)",
+                  "kmeans": "k-means batch generation points/sec (input log -> parse -> "
+                            "k-means -> evaluation -> published MODEL)",
+                  "rdf": "RDF batch generation examples/sec (input log -> parse -> forest -> "
+                         "evaluation -> published MODEL)"}[args.app]
+        unit = {"als": "ratings/s", "kmeans": "points/s", "rdf": "examples/s"}[args.app]
         rec = {
-            "metric": "ALS batch generation ratings/sec (input log -> published MODEL + UP rows)",
-            "value": args.ratings / t_gen, "unit": "ratings/s", "higher_is_better": True,
+            "metric": metric, "app": args.app,
+            "value": n_records / t_gen, "unit": unit, "higher_is_better": True,
             "n_gpus": ctx.world_size, "generation_s": t_gen, "log_append_s": t_ingest,
             "phase_s": phases, "update_messages": int(sum(ends)),
             "attributed_s": attributed, "unattributed_s": t_gen - attributed,
             "later_generations": later,
-            "config": {"ratings": args.ratings, "users": args.users, "items": args.items,
-                       "features": args.features, "iterations": args.iterations,
-                       "dtype": args.dtype, "partitions": args.partitions,
+            "config": ({"ratings": args.ratings, "users": args.users, "items": args.items,
+                        "features": args.features} if args.app == "als" else
+                       {"points": args.points, "dims": args.dims,
+                        "k": args.k if args.app == "kmeans" else None,
+                        "trees": args.trees if args.app == "rdf" else None,
+                        "depth": args.depth if args.app == "rdf" else None}) | {
+                       "iterations": args.iterations,
+                       "dtype": args.dtype if args.app == "als" else "fp32",
+                       "partitions": args.partitions,
                        "test_fraction": args.test_fraction,
                        "sharded": bool(sharded_path),
                        "forced_collectives": bool(ctx.forced)},
-            "data": "synthetic power-law users x items, strengths 0.5..5, last-day timestamps",
+            "data": ("synthetic power-law users x items, strengths 0.5..5, last-day timestamps"
+                     if args.app == "als" else
+                     "synthetic Gaussian blobs around k random centers, values on a 0.01 grid"
+                     if args.app == "kmeans" else
+                     "synthetic Gaussian predictors, binary target from a fixed rule"),
         }
         print(json.dumps(rec), flush=True)
         if args.dir is None:

@@ -206,6 +206,8 @@ __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 
 constexpr int WPB = 4;   // waves (rows) per block
 
+// CSV: the row as "v0,v1,...\n" (the batch layers' input lines) instead of "[v0,v1,...]"
+template <bool CSV = false>
 __global__ __launch_bounds__(WPB * 64) void fmt_row_len(const float* __restrict__ M,
                                                         long long n, int k, long long ld,
                                                         int* __restrict__ row_len) {
@@ -216,9 +218,10 @@ __global__ __launch_bounds__(WPB * 64) void fmt_row_len(const float* __restrict_
   int len = 0;
   for (int f = lane; f < k; f += 64) len += float_json(M[r * ld + f], buf);
   len = wave_sum_i(len);
-  if (lane == 0) row_len[r] = len + (k > 0 ? k - 1 : 0) + 2;
+  if (lane == 0) row_len[r] = len + (k > 0 ? k - 1 : 0) + (CSV ? 1 : 2);
 }
 
+template <bool CSV = false>
 __global__ __launch_bounds__(WPB * 64) void fmt_row_text(const float* __restrict__ M,
                                                          long long n, int k, long long ld,
                                                          const long long* __restrict__ row_end,
@@ -229,8 +232,8 @@ __global__ __launch_bounds__(WPB * 64) void fmt_row_text(const float* __restrict
   if (r >= n) return;
   const long long start = row_end[r] - row_len[r];
   char* o = out + start;
-  if (lane == 0) o[0] = '[';
-  long long base = 1;   // bytes of the row before this chunk of 64 features
+  if (!CSV && lane == 0) o[0] = '[';
+  long long base = CSV ? 0 : 1;   // bytes of the row before this chunk of 64 features
   char buf[20];
   for (int f0 = 0; f0 < k; f0 += 64) {
     const int f = f0 + lane;
@@ -245,7 +248,7 @@ __global__ __launch_bounds__(WPB * 64) void fmt_row_text(const float* __restrict
     }
     base += __shfl(incl, 63, 64);
   }
-  if (lane == 0) o[row_len[r] - 1] = ']';
+  if (lane == 0) o[row_len[r] - 1] = CSV ? '\n' : ']';
 }
 
 }  // namespace
@@ -258,7 +261,7 @@ int oryx_format_rows_len(const float* M, long long n, int k, long long ld, int* 
   if (n <= 0) return ORYX_OK;
   if (k < 0 || ld < k) return ORYX_EINVAL;
   const unsigned blocks = (unsigned)((n + WPB - 1) / WPB);
-  hipLaunchKernelGGL(fmt_row_len, dim3(blocks), dim3(WPB * 64), 0,
+  hipLaunchKernelGGL(fmt_row_len<false>, dim3(blocks), dim3(WPB * 64), 0,
                      reinterpret_cast<hipStream_t>(stream), M, n, k, ld, row_len);
   return oryx_check_launch();
 }
@@ -271,7 +274,30 @@ int oryx_format_rows_text(const float* M, long long n, int k, long long ld,
   if (n <= 0) return ORYX_OK;
   if (k < 0 || ld < k) return ORYX_EINVAL;
   const unsigned blocks = (unsigned)((n + WPB - 1) / WPB);
-  hipLaunchKernelGGL(fmt_row_text, dim3(blocks), dim3(WPB * 64), 0,
+  hipLaunchKernelGGL(fmt_row_text<false>, dim3(blocks), dim3(WPB * 64), 0,
+                     reinterpret_cast<hipStream_t>(stream), M, n, k, ld, row_end, row_len, out);
+  return oryx_check_launch();
+}
+
+// As the two calls above with each row as a CSV line "v0,v1,...\n" (row_len includes the
+// newline).
+int oryx_format_csv_len(const float* M, long long n, int k, long long ld, int* row_len,
+                        void* stream) {
+  if (n <= 0) return ORYX_OK;
+  if (k < 0 || ld < k) return ORYX_EINVAL;
+  const unsigned blocks = (unsigned)((n + WPB - 1) / WPB);
+  hipLaunchKernelGGL(fmt_row_len<true>, dim3(blocks), dim3(WPB * 64), 0,
+                     reinterpret_cast<hipStream_t>(stream), M, n, k, ld, row_len);
+  return oryx_check_launch();
+}
+
+int oryx_format_csv_text(const float* M, long long n, int k, long long ld,
+                         const long long* row_end, const int* row_len, char* out,
+                         void* stream) {
+  if (n <= 0) return ORYX_OK;
+  if (k < 0 || ld < k) return ORYX_EINVAL;
+  const unsigned blocks = (unsigned)((n + WPB - 1) / WPB);
+  hipLaunchKernelGGL(fmt_row_text<true>, dim3(blocks), dim3(WPB * 64), 0,
                      reinterpret_cast<hipStream_t>(stream), M, n, k, ld, row_end, row_len, out);
   return oryx_check_launch();
 }

@@ -308,14 +308,14 @@ class RDFUpdate(MLUpdate):
             self.history = FeatureHistory(dev)
         return self.history
 
-    def _phase(self, name: str, t0: float) -> None:
+    def _tick(self, name: str, t0: float) -> None:
         self.phase_seconds[name] = self.phase_seconds.get(name, 0.0) + time.perf_counter() - t0
 
     def _parse(self, lines, ctx) -> FeatureBlock:
         tp = time.perf_counter()
         blk = parse_features(lines, self.input_schema, ctx.device, torch.float64,
                              history=self._history_for(ctx.device))
-        self._phase("parse", tp)
+        self._tick("parse", tp)
         return blk
 
     def _global_encodings(self, blk: FeatureBlock, ctx) -> CategoricalValueEncodings:
@@ -403,7 +403,7 @@ class RDFUpdate(MLUpdate):
         sl = slice(None) if sharded else slice(ctx.rank, None, ctx.world_size)
         data = rdf_ops.bin_features(X[sl], categorical, arities, max_split_candidates,
                                     ctx.device, seed=seed, threshold_source=src)
-        self._phase("bin", tp)
+        self._tick("bin", tp)
         t0 = time.perf_counter()
         classification = schema.is_classification()
         C = encodings.get_value_count(schema.get_target_feature_index()) if classification \
@@ -411,7 +411,7 @@ class RDFUpdate(MLUpdate):
         tgt = target[sl]
         trained = rdf_ops.train_forest(data, tgt, C, self.num_trees, max_depth, impurity,
                                        seed=seed, ctx=ctx)
-        self._phase("train", t0)
+        self._tick("train", t0)
         log.info("RDF %d trees depth %d on %d examples x %d predictors: %.3fs", self.num_trees,
                  max_depth, n_all, P, time.perf_counter() - t0)
         if not ctx.is_main and not sharded:
@@ -425,7 +425,7 @@ class RDFUpdate(MLUpdate):
         roots = [_to_spec(r, data, schema, classification) for r in trained.roots]
         pmml = rdf_pmml.forest_to_pmml(roots, schema, encodings, importances, max_depth,
                                        max_split_candidates, impurity)
-        self._phase("pmml", tp)
+        self._tick("pmml", tp)
         return pmml
 
     def evaluate(self, context, model, model_parent_path, test_data, train_data):
@@ -471,7 +471,7 @@ class RDFUpdate(MLUpdate):
         if self._sharded(ctx):
             from ...parallel import shuffle
             parts = shuffle.all_reduce_np(parts, ctx)
-        self._phase("eval", tp)
+        self._tick("eval", tp)
         if classification:
             ev = float(parts[0] / parts[1]) if parts[1] else 0.0
             log.info("Accuracy: %s", ev)

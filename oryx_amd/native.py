@@ -251,6 +251,8 @@ def _load_kernels():
     # M, n, k, ld, row_len, stream / M, n, k, ld, row_end, row_len, out, stream
     _sig(lib, "oryx_format_rows_len", c_i, [c_vp, c_ll, c_i, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_format_rows_text", c_i, [c_vp, c_ll, c_i, c_ll, c_vp, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_format_csv_len", c_i, [c_vp, c_ll, c_i, c_ll, c_vp, c_vp])
+    _sig(lib, "oryx_format_csv_text", c_i, [c_vp, c_ll, c_i, c_ll, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_topn_waves", c_ll, [c_ll])
     # Y, inv_norm, Q, kp, nq, bucket_of, cand_bits, words, ranges, tile0, n_ranges, n_tiles,
     # excl_ptr, excl_rows, out_score, out_row, stream

@@ -91,3 +91,32 @@ def _format_device(mat: torch.Tensor) -> RowText:
     host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
     host.copy_(out)
     return RowText(host.numpy(), ends.cpu().numpy())
+
+
+def format_csv(mat: torch.Tensor, pinned: bool = True) -> RowText:
+    """CSV lines ``v0,v1,...\n`` of every row of a device float32 matrix (shortest round-trip
+    float32 text, as :func:`format_rows`), formatted on the GPU; ``ends[r]`` is the end of row
+    r's newline.  For generating batch-layer input (bench_batch.py)."""
+    m = mat.detach()
+    if m.dtype != torch.float32:
+        m = m.float()
+    if m.stride(1) != 1:
+        m = m.contiguous()
+    n, k = m.shape
+    if n == 0:
+        return RowText(b"", np.zeros(0, dtype=np.int64))
+    lib = native.require_kernels()
+    dev = m.device
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    stream = native.stream_ptr(dev)
+    native.check(lib.oryx_format_csv_len(m.data_ptr(), n, k, m.stride(0), lens.data_ptr(),
+                                         stream), "oryx_format_csv_len")
+    ends = torch.cumsum(lens, 0, dtype=torch.int64)
+    total = int(ends[-1])
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    native.check(lib.oryx_format_csv_text(m.data_ptr(), n, k, m.stride(0), ends.data_ptr(),
+                                          lens.data_ptr(), out.data_ptr(), stream),
+                 "oryx_format_csv_text")
+    host = torch.empty(total, dtype=torch.uint8, pin_memory=pinned)
+    host.copy_(out)
+    return RowText(host.numpy(), ends.cpu().numpy())

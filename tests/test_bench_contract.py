@@ -132,3 +132,20 @@ def test_bench_batch_sharded_gloo_world_two():
     assert rec["unattributed_s"] <= 0.1 * rec["generation_s"] + 0.5, rec
     # MODEL + one UP row per user and item that has ratings
     assert rec["update_messages"] > 2000
+
+
+def test_bench_batch_kmeans_and_rdf_cpu():
+    """bench_batch.py --app kmeans / rdf (CPU, small): a generation from the input log to a
+    published MODEL with parse / train / eval phases, every second attributed."""
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    for app, extra in (("kmeans", ["--k", "6", "--iterations", "4"]),
+                       ("rdf", ["--trees", "3", "--depth", "3"])):
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "bench_batch.py"), "--app", app,
+                            "--device", "cpu", "--points", "6000", "--dims", "8"] + extra,
+                           capture_output=True, text=True, timeout=400, env=env)
+        assert p.returncode == 0, p.stderr[-3000:]
+        rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+        assert rec["app"] == app and rec["update_messages"] >= 1
+        for key in ("parse", "train", "eval", "pmml_write", "layer_update"):
+            assert key in rec["phase_s"], rec["phase_s"]
+        assert rec["unattributed_s"] <= 0.1 * rec["generation_s"] + 0.5, rec
