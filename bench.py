@@ -64,6 +64,93 @@ PRESETS = {
 }
 
 
+def emulate(args) -> int:
+    """--emulate-world W --emulate-rank r: rank r's per-rank workload of a W-GPU weak-scaling
+    run on one GPU (see the argument's help).  Prints one JSON line (not the headline
+    metric: the collectives are not executed, their payloads are reported)."""
+    from oryx_amd.parallel import dist
+    from oryx_amd.models.als.trainer import ALSTrainer
+    W, R = int(args.emulate_world), int(args.emulate_rank)
+    if not 0 <= R < W:
+        raise SystemExit("--emulate-rank must be in [0, --emulate-world)")
+    dev = dist._pick_device(0, args.device)
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    ctx = dist.DistContext(rank=R, world_size=W, device=dev, emulated=True)
+    t0 = time.perf_counter()
+    bu, bi = [[], [], []], [[], [], []]
+    nnz_world = 0
+    for q in range(W):
+        u, i, s = _gen_ratings(args.users_per_gpu, args.items, args.ratings_per_gpu, q,
+                               args.seed, dev)
+        nnz_world += int(u.numel())
+        mu, mi = (u % W) == R, (i % W) == R
+        for dst, m in ((bu, mu), (bi, mi)):
+            dst[0].append(u[m])
+            dst[1].append(i[m])
+            dst[2].append(s[m])
+        del u, i, s
+    by_user = [torch.cat(c) for c in bu]
+    by_item = [torch.cat(c) for c in bi]
+    gen_s = time.perf_counter() - t0
+    trainer = ALSTrainer(args.rank_k, lam=0.001, alpha=1.0, implicit=bool(args.implicit),
+                         ctx=ctx, seed=args.seed, precision=args.precision,
+                         gather_chunks=args.gather_chunks)
+    trainer.prepare_routed(by_user, by_item, args.users_per_gpu * W, args.items)
+    nnz_u, nnz_i = int(by_user[0].numel()), int(by_item[0].numel())
+    del by_user, by_item
+    trainer.init_factors()
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        trainer.iterate(1)
+    sync()
+    t0 = time.perf_counter()
+    trainer.iterate(args.steps)
+    sync()
+    ms = (time.perf_counter() - t0) * 1e3 / max(1, args.steps)
+    halfstep_ms = trainer.phase_breakdown(3)
+    elem = 4 if trainer.split else 2
+    kp = trainer.kp
+    # what one iteration's collectives would move on this rank (ring algorithms: an
+    # all-gather sends this rank's shard and receives W - 1 others; an all-reduce of B bytes
+    # sends and receives 2 (W - 1) / W B)
+    gram = kp * kp * 4
+    ag = {"items": trainer.lay_i.local_rows * kp * elem,
+          "users": trainer.lay_u.local_rows * kp * elem}
+    coll = {"allreduce_gramian_bytes": 2 * gram,
+            "allgather_send_bytes": ag["items"] + ag["users"],
+            "allgather_recv_bytes": (W - 1) * (ag["items"] + ag["users"]),
+            "allreduce_wire_bytes": int(2 * 2 * (W - 1) / W * gram)}
+    # xGMI: 7 links x ~153 GB/s per GPU; a ring all-gather is bound by one link per peer
+    # step, so the received bytes over ~64 GB/s of effective ring bandwidth (RCCL's
+    # multi-channel rings reach roughly that per GPU pair) bounds the exposed exchange
+    coll["allgather_ring_est_ms"] = coll["allgather_recv_bytes"] / 64e9 * 1e3
+    rec = {
+        "metric": "ALS per-rank iteration time, emulated %d-GPU weak scaling (rank %d)" % (W, R),
+        "emulated": True, "world": W, "rank": R, "preset": args.preset,
+        "ms_per_step": ms, "steps": args.steps, "warmup": args.warmup,
+        "halfstep_ms": halfstep_ms,
+        "ratings_world": nnz_world, "ratings_user_csr": nnz_u, "ratings_item_csr": nnz_i,
+        "rows": {"users": trainer.u_hi - trainer.u_lo, "items": trainer.i_hi - trainer.i_lo,
+                 "gather_chunks_items": trainer.lay_i.C, "gather_chunks_users": trainer.lay_u.C},
+        "collectives_per_iteration": coll,
+        "per_gpu_ratings_per_s": nnz_world / W * 1e3 / ms,
+        "config": {"rank_k": args.rank_k, "precision": args.precision,
+                   "ratings_per_gpu": args.ratings_per_gpu, "users_per_gpu": args.users_per_gpu,
+                   "items": args.items},
+        "generate_s": gen_s, "prepare_s": trainer.timings.get("prepare_s"),
+        "solve_failures": trainer.failures,
+        "peak_hbm_gib": (torch.cuda.max_memory_allocated(dev) / 2 ** 30
+                         if dev.type == "cuda" else None),
+    }
+    print(json.dumps(rec), flush=True)
+    return 0
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__)
@@ -83,12 +170,21 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="auto")
     ap.add_argument("--gather-chunks", type=int, default=None,
                     help="row ranges per half-step factor exchange (default: trainer's)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="one GPU plays rank --emulate-rank of a W-rank weak-scaling run: it "
+                         "builds that rank's exact post-all-to-all CSRs (from every rank's "
+                         "generated ratings) and full-size gathered factor buffers, runs the "
+                         "half-steps with collectives that move nothing, and reports their "
+                         "times plus the bytes each collective would move")
+    ap.add_argument("--emulate-rank", type=int, default=0)
     args = ap.parse_args(argv)
     for key, val in PRESETS[args.preset].items():
         if getattr(args, key) is None:
             setattr(args, key, val)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    if args.emulate_world > 1:
+        return emulate(args)
     from oryx_amd.parallel import launch
     rc = launch.relaunch_if_needed(os.path.abspath(__file__), argv, args.gpus)
     if rc is not None:

@@ -101,7 +101,7 @@ class RowLayout:
         previous gathered matrix, overwritten in place when its shape fits (the collectives
         are ordered after every kernel already queued on the current stream, i.e. after the
         last reads of the old rows), so the exchange allocates nothing per half-step."""
-        if not ctx.is_distributed and self.C == 1:
+        if ctx.world_size == 1 and self.C == 1:
             # one process, one range: the local shard IS the gathered matrix (no copy)
             if overlap_with is not None:
                 overlap_with(0)
@@ -110,6 +110,13 @@ class RowLayout:
         if out is None or tuple(out.shape) != shape or out.dtype != local.dtype or \
                 out.data_ptr() == local.data_ptr():
             out = torch.empty(shape, dtype=local.dtype, device=local.device)
+            if ctx.emulated:
+                # the other ranks' rows of an emulated world: copies of this rank's (sane
+                # values for the solves that read them; an emulated exchange moves nothing)
+                for c in range(self.C):
+                    blk = local[c * self.cr:(c + 1) * self.cr]
+                    out[c * self.W * self.cr:(c + 1) * self.W * self.cr].copy_(
+                        blk.repeat((self.W,) + (1,) * (blk.dim() - 1)))
         handles = []
         for c in range(self.C):
             if overlap_with is not None:
@@ -184,6 +191,35 @@ class ALSTrainer:
         gu, gi = self._position(users, self.su), self._position(items, self.si)
         by_user = self._route(gu, gi, ratings, users % W)
         by_item = self._route(gu, gi, ratings, items % W)
+        self._build_csrs(by_user, by_item)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        self.timings["prepare_s"] = time.perf_counter() - t0
+
+    def prepare_routed(self, by_user, by_item, n_users: int, n_items: int) -> None:
+        """As :meth:`prepare` from triples already at their owners: ``by_user`` = (user,
+        item, rating) of the users this rank owns (id % W == rank), ``by_item`` = those of
+        the items it owns -- what the two all-to-alls deliver (bench.py --emulate-world builds
+        one rank's share of a larger world this way)."""
+        ctx = self.ctx
+        dev = self.device
+        self.n_users, self.n_items = int(n_users), int(n_items)
+        W, R = ctx.world_size, ctx.rank
+        self.su = dist.padded_shard_size(self.n_users, W)
+        self.si = dist.padded_shard_size(self.n_items, W)
+        self.u_lo, self.u_hi = R * self.su, R * self.su + self._owned(self.n_users)
+        self.i_lo, self.i_hi = R * self.si, R * self.si + self._owned(self.n_items)
+        conv = lambda t: (self._position(t[0].to(dev, torch.int64), self.su),
+                          self._position(t[1].to(dev, torch.int64), self.si),
+                          t[2].to(dev, torch.float32))
+        t0 = time.perf_counter()
+        self._build_csrs(conv(by_user), conv(by_item))
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        self.timings["prepare_s"] = time.perf_counter() - t0
+
+    def _build_csrs(self, by_user, by_item) -> None:
+        W = self.ctx.world_size
         self.lay_u = RowLayout(self.n_users, W, self._chunks_for(self.n_users))
         self.lay_i = RowLayout(self.n_items, W, self._chunks_for(self.n_items))
         # column ids index the gathered (chunk-major) copy of the opposite factors
@@ -196,9 +232,6 @@ class ALSTrainer:
         self.csr_u_parts = self._row_parts(self.csr_u, self.lay_u)
         self.csr_i_parts = self._row_parts(self.csr_i, self.lay_i)
         self.local_nnz = self.csr_u.nnz
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        self.timings["prepare_s"] = time.perf_counter() - t0
 
     # a factor matrix is exchanged in ranges only when the exchange is worth hiding and each
     # range still fills the GPU (small ranges leave CUs idle in every launch's tail)

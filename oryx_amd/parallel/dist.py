@@ -48,10 +48,14 @@ class DistContext:
     forced: bool = False
     # one-shot peer-mapped all-reduce for small fp32 payloads (parallel/ipc.py), or None
     ipc: Optional[object] = None
+    # one process playing rank `rank` of a `world_size` world (bench.py --emulate-world): the
+    # layouts are the real world's, collectives move nothing (an all-gather writes only this
+    # rank's slot, an all-reduce is the identity)
+    emulated: bool = False
 
     @property
     def is_distributed(self) -> bool:
-        return self.world_size > 1 or self.forced
+        return (self.world_size > 1 or self.forced) and not self.emulated
 
     @property
     def is_main(self) -> bool:
@@ -206,6 +210,10 @@ def all_gather_rows_async(local: torch.Tensor, out: torch.Tensor, ctx: DistConte
     queued on the current stream (the producer of ``local``), so compute launched afterwards
     overlaps it; ``wait()`` makes the current stream wait for it.
     """
+    if ctx.emulated:
+        n = local.shape[0]
+        out[ctx.rank * n:(ctx.rank + 1) * n].copy_(local)
+        return None
     if not ctx.is_distributed:
         out.copy_(local)
         return None

@@ -149,3 +149,24 @@ def test_bench_batch_kmeans_and_rdf_cpu():
         for key in ("parse", "train", "eval", "pmml_write", "layer_update"):
             assert key in rec["phase_s"], rec["phase_s"]
         assert rec["unattributed_s"] <= 0.1 * rec["generation_s"] + 0.5, rec
+
+
+def test_bench_emulate_world_cpu():
+    """bench.py --emulate-world: one process builds rank r's share of a W-rank run (its user
+    CSR holds the users id % W == r of every rank, its item CSR the items id % W == r) and
+    reports per-iteration time and collective payloads."""
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--emulate-world", "4",
+                        "--emulate-rank", "2", "--device", "cpu", "--rank-k", "8",
+                        "--ratings-per-gpu", "8000", "--users-per-gpu", "1000", "--items",
+                        "300", "--steps", "1", "--warmup", "1", "--precision", "fp32"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["emulated"] and rec["world"] == 4 and rec["rank"] == 2
+    assert rec["rows"]["users"] == 1000 and rec["rows"]["items"] == 75
+    # about a quarter of the world's ratings on each side
+    assert 0.15 < rec["ratings_user_csr"] / rec["ratings_world"] < 0.35
+    assert rec["collectives_per_iteration"]["allgather_recv_bytes"] == \
+        3 * rec["collectives_per_iteration"]["allgather_send_bytes"]
+    assert rec["solve_failures"] == 0
