@@ -39,13 +39,14 @@ PUBLISHED = {
 CLIENT = r"""
 import http.client, json, random, sys, time
 port, users, n, seed = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+query = sys.argv[5] if len(sys.argv) > 5 else ""
 rnd = random.Random(seed)
 conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
 lat = []
 errors = 0
 t0 = time.perf_counter()
 for _ in range(n):
-    path = "/recommend/U%d" % rnd.randrange(users)
+    path = "/recommend/U%d%s" % (rnd.randrange(users), query)
     t = time.perf_counter()
     conn.request("GET", path, headers={"Accept": "application/json"})
     r = conn.getresponse()
@@ -69,11 +70,19 @@ def make_data(items: int, users: int, features: int, seed: int):
     return Y, X, item_ids, user_ids, counts, known
 
 
-def build_model(data, features: int, sample_rate: float, max_batch: int = 16):
+def build_model(data, features: int, sample_rate: float, max_batch: int = 16,
+                rescorer: bool = False):
     import torch
     from oryx_amd.models.als.serving import ALSServingModel
+    provider = None
+    if rescorer:
+        # the example provider (models/als/rescorer.py): drops every item whose numeric ID is
+        # a multiple of 10 and scales the other scores (device form: a cached row mask)
+        from oryx_amd.models.als.rescorer import ItemFilterRescorerProvider
+        os.environ["ORYX_EXAMPLE_RESCORER_EXCLUDE_MOD"] = "10"
+        provider = ItemFilterRescorerProvider()
     Y, X, item_ids, user_ids, counts, known = data
-    model = ALSServingModel(features, True, sample_rate, max_batch=max_batch)
+    model = ALSServingModel(features, True, sample_rate, provider, max_batch=max_batch)
     chunk = 1 << 21
     for lo in range(0, len(item_ids), chunk):
         model.Y.set_vectors(item_ids[lo:lo + chunk], Y[lo:lo + chunk])
@@ -92,7 +101,7 @@ def build_model(data, features: int, sample_rate: float, max_batch: int = 16):
 
 
 def serve_and_measure(model, users: int, workers: int, requests: int, warmup: int,
-                      seed: int):
+                      seed: int, query: str = ""):
     from oryx_amd.api import AbstractServingModelManager
     from oryx_amd.serving.layer import ServingLayer
     from oryx_amd.utils import config as cfg
@@ -117,7 +126,7 @@ def serve_and_measure(model, users: int, workers: int, requests: int, warmup: in
 
     def run(n):
         procs = [subprocess.Popen([sys.executable, "-c", CLIENT, str(port), str(users),
-                                   str(n), str(seed * 100 + w)],
+                                   str(n), str(seed * 100 + w), query],
                                   stdout=subprocess.PIPE, text=True)
                  for w in range(workers)]
         outs = [json.loads(p.communicate()[0]) for p in procs]
@@ -273,6 +282,9 @@ def main(argv=None) -> int:
     ap.add_argument("--max-batch", type=int, default=16)
     ap.add_argument("--time-to-ready", action="store_true",
                     help="measure the model load through the update topic instead")
+    ap.add_argument("--rescorer", action="store_true",
+                    help="requests carry rescorerParams for the example ItemFilterRescorer "
+                         "provider (every candidate filtered / rescored, on the device)")
     args = ap.parse_args(argv)
     if args.time_to_ready:
         print(json.dumps(time_to_ready(args.items, args.users, args.features, args.seed)),
@@ -290,16 +302,18 @@ def main(argv=None) -> int:
         data = make_data(items, args.users, features, args.seed)
         for rate in rates:
             t0 = time.perf_counter()
-            model = build_model(data, features, rate, args.max_batch)
+            model = build_model(data, features, rate, args.max_batch, args.rescorer)
             build_s = time.perf_counter() - t0
             for w in workers:
                 if model.batcher is not None:
                     model.batcher.batches = model.batcher.requests = 0
-                qps, lat, total, errors = serve_and_measure(model, args.users, w,
-                                                            args.requests, args.warmup,
-                                                            args.seed)
-                print(json.dumps(record(model, args, qps, lat, total, errors, build_s, w, rate,
-                                        items, features)), flush=True)
+                qps, lat, total, errors = serve_and_measure(
+                    model, args.users, w, args.requests, args.warmup, args.seed,
+                    "?rescorerParams=factor:1.5" if args.rescorer else "")
+                rec = record(model, args, qps, lat, total, errors, build_s, w, rate, items,
+                             features)
+                rec["rescorer"] = bool(args.rescorer)
+                print(json.dumps(rec), flush=True)
             if model.batcher is not None:
                 model.batcher.close()
             del model

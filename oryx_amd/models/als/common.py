@@ -435,6 +435,29 @@ class FeatureVectors:
             return None
         return self._dev_part[:self._n_rows]
 
+    def id_array(self) -> np.ndarray:
+        """Every row's ID (None for free rows) as a numpy object array, cached per store
+        version: candidate IDs are then one fancy index (``id_array()[rows]``), not a Python
+        list built per request."""
+        c = getattr(self, "_id_arr", None)
+        if c is not None and c[0] == self.version:
+            return c[1]
+        with self._lock.read():
+            arr = np.empty(len(self._ids), dtype=object)
+            arr[:] = self._ids
+            ver = self.version
+        self._id_arr = (ver, arr)
+        return arr
+
+    def row_mask(self, ids, device=None):
+        """Bool tensor over the store's rows: True at the rows of ``ids`` (on ``device``)."""
+        import torch
+        rows = self.host_rows(ids)
+        m = torch.zeros(max(self._n_rows, 1), dtype=torch.bool)
+        if rows:
+            m[torch.as_tensor(rows, dtype=torch.int64)] = True
+        return m.to(device) if device is not None else m
+
     def ids_of_rows(self, rows) -> List[Optional[str]]:
         ids = self._ids
         n = len(ids)

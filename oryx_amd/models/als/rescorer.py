@@ -25,7 +25,8 @@ import numpy as np
 from ...utils import lang
 
 __all__ = ["Rescorer", "RescorerProvider", "AbstractRescorerProvider", "MultiRescorer",
-           "MultiRescorerProvider", "load_rescorer_providers"]
+           "MultiRescorerProvider", "load_rescorer_providers", "ItemFilterRescorer",
+           "ItemFilterRescorerProvider"]
 
 
 class Rescorer(abc.ABC):
@@ -45,6 +46,16 @@ class Rescorer(abc.ABC):
         """``rescore`` of every (ID, score) pair (float64 array; NaN drops the item)."""
         return np.fromiter((float(self.rescore(i, float(v))) for i, v in zip(ids, scores)),
                            dtype=np.float64, count=len(ids))
+
+    # -- device form (an extension: rescoring without leaving the GPU)
+    def rescore_device(self, rows, scores, store):
+        """Optional: the filtered + rescored scores of candidate items on the device --
+        ``rows`` (int64 store rows) and ``scores`` (fp32 raw scores) are device tensors of
+        the candidates, ``store`` the item :class:`~oryx_amd.models.als.common.FeatureVectors`
+        (``store.row_mask(ids)`` / ``store.id_array()`` map IDs to rows).  Return a float
+        tensor like ``scores`` where NaN or -inf drops the item, or None when this rescorer
+        has no device form (the host forms then run over every candidate)."""
+        return None
 
 
 class RescorerProvider(abc.ABC):
@@ -124,6 +135,116 @@ class MultiRescorer(Rescorer):
             nan = np.isnan(v)
             v = np.where(nan, np.nan, np.asarray(r.rescore_many(ids, v), dtype=np.float64))
         return v
+
+    def rescore_device(self, rows, scores, store):
+        import torch
+        v = scores
+        for r in self.rescorers:
+            nv = r.rescore_device(rows, v, store)
+            if nv is None:
+                return None
+            v = torch.where(torch.isnan(v), v, nv)
+        return v
+
+
+class ItemFilterRescorer(Rescorer):
+    """Drops a set of item IDs and multiplies every other score by ``factor`` -- the
+    per-item and array forms and a device form (a cached row mask) give the same results."""
+
+    def __init__(self, excluded: Sequence[str], factor: float = 1.0):
+        self.excluded = frozenset(excluded)
+        self.factor = float(factor)
+        self._mask = None          # (store id, store version, device mask)
+
+    def rescore(self, id_, value):
+        return float("nan") if id_ in self.excluded else value * self.factor
+
+    def is_filtered(self, id_):
+        return id_ in self.excluded
+
+    def is_filtered_many(self, ids):
+        ex = self.excluded
+        return np.fromiter((i in ex for i in ids), dtype=bool, count=len(ids))
+
+    def rescore_many(self, ids, scores):
+        v = np.asarray(scores, dtype=np.float64) * self.factor
+        v[self.is_filtered_many(ids)] = np.nan
+        return v
+
+    def rescore_device(self, rows, scores, store):
+        import torch
+        key = (id(store), store.version)
+        if self._mask is None or self._mask[0] != key[0] or self._mask[1] != key[1]:
+            self._mask = key + (store.row_mask(self.excluded, rows.device),)
+        m = self._mask[2]
+        hit = m[rows.clamp(max=m.numel() - 1)] & (rows < m.numel())
+        out = scores * self.factor
+        return torch.where(hit, torch.full_like(out, float("nan")), out)
+
+
+class ItemFilterRescorerProvider(AbstractRescorerProvider):
+    """An example provider (``oryx.als.rescorer-provider-class``): ``rescorerParams`` values
+    ``exclude:<id>`` drop items and ``factor:<x>`` scales scores, for /recommend and
+    /similarity; ``ORYX_EXAMPLE_RESCORER_EXCLUDE_MOD`` (bench_serving.py) additionally drops
+    every item whose numeric ID suffix is divisible by the given modulus."""
+
+    @staticmethod
+    def _parse(args) -> Optional[Rescorer]:
+        import os
+        excl, factor = [], 1.0
+        for a in args or []:
+            if a.startswith("exclude:"):
+                excl.append(a[len("exclude:"):])
+            elif a.startswith("factor:"):
+                factor = float(a[len("factor:"):])
+        mod = os.environ.get("ORYX_EXAMPLE_RESCORER_EXCLUDE_MOD")
+        if mod:
+            return _ModExcludeRescorer(int(mod), factor, excl)
+        if not excl and factor == 1.0:
+            return None
+        return ItemFilterRescorer(excl, factor)
+
+    def get_recommend_rescorer(self, user_ids, args):
+        return self._parse(args)
+
+    def get_most_similar_items_rescorer(self, args):
+        return self._parse(args)
+
+
+class _ModExcludeRescorer(ItemFilterRescorer):
+    """Drops items whose trailing digits are divisible by ``mod`` (plus explicit IDs)."""
+
+    def __init__(self, mod: int, factor: float, excl: Sequence[str]):
+        super().__init__(excl, factor)
+        self.mod = mod
+
+    def _dropped(self, id_) -> bool:
+        if id_ in self.excluded:
+            return True
+        digits = id_[len(id_.rstrip("0123456789")):]
+        return bool(digits) and int(digits) % self.mod == 0
+
+    def rescore(self, id_, value):
+        return float("nan") if self._dropped(id_) else value * self.factor
+
+    def is_filtered(self, id_):
+        return self._dropped(id_)
+
+    def is_filtered_many(self, ids):
+        return np.fromiter((self._dropped(i) for i in ids), dtype=bool, count=len(ids))
+
+    def rescore_device(self, rows, scores, store):
+        import torch
+        key = (id(store), store.version)
+        if self._mask is None or self._mask[0] != key[0] or self._mask[1] != key[1]:
+            ids = store.id_array()
+            drop = np.fromiter((i is not None and self._dropped(i) for i in ids), dtype=bool,
+                               count=len(ids))
+            self._mask = key + (torch.from_numpy(drop).to(rows.device),)
+        m = self._mask[2]
+        hit = m[rows.clamp(max=max(m.numel() - 1, 0))] & (rows < m.numel())
+        out = scores * self.factor
+        return torch.where(hit, torch.full_like(out, float("nan")), out)
 
 
 def _build(rescorers):

@@ -45,17 +45,22 @@ def rescored_top(ids, scores: np.ndarray, rescorer: Rescorer, how_many: int
                  ) -> List[Tuple[str, float]]:
     """``TopNConsumer`` semantics over EVERY candidate: drop filtered IDs, rescore the rest,
     keep rescored values above -inf (NaN drops an item), best ``how_many`` descending."""
-    keep = np.array([i is not None for i in ids], dtype=bool)
-    if not keep.all():
-        ids = [i for i in ids if i is not None]
-        scores = scores[keep]
-    if not ids:
+    if isinstance(ids, np.ndarray):
+        keep = ids != None                                  # noqa: E711 (element-wise)
+        if not keep.all():
+            ids, scores = ids[keep], scores[keep]
+    else:
+        keep = np.array([i is not None for i in ids], dtype=bool)
+        if not keep.all():
+            ids = [i for i in ids if i is not None]
+            scores = scores[keep]
+    if not len(ids):
         return []
     allowed = ~np.asarray(rescorer.is_filtered_many(ids), dtype=bool)
     idx = np.flatnonzero(allowed)
     if len(idx) == 0:
         return []
-    sel = [ids[j] for j in idx.tolist()]
+    sel = ids[idx] if isinstance(ids, np.ndarray) else [ids[j] for j in idx.tolist()]
     new = np.asarray(rescorer.rescore_many(sel, np.asarray(scores, dtype=np.float64)[idx]),
                      dtype=np.float64)
     ok = np.flatnonzero(new > -np.inf)
@@ -478,6 +483,27 @@ class ALSServingModel(ServingModel):
         return self.Y.size()
 
     # ---------------------------------------------------------------- top-N on the GPU
+    def _rescored_top_n(self, tgt, cosine, cands, ex, rescorer, how_many):
+        """Every candidate through the rescorer: on the device when it has a device form
+        (``Rescorer.rescore_device``: scores stay on the GPU, top-N by a device top-k), else
+        the host array forms over the candidates' IDs (one fancy index of the store's cached
+        ID array, no per-request Python list)."""
+        rows, scores = self.index.all_scores_device(tgt, cosine, cands, ex)
+        if rows.numel() == 0:
+            return []
+        new = rescorer.rescore_device(rows, scores, self.Y)
+        if new is not None:
+            ok = torch.nonzero(new > float("-inf")).flatten()      # NaN compares false
+            if ok.numel() == 0:
+                return []
+            v, j = torch.topk(new[ok].double(), min(how_many, ok.numel()))
+            r = rows[ok[j]].cpu().numpy()
+            ids = self.Y.id_array()[r]
+            return [(i, float(x)) for i, x in zip(ids.tolist(), v.cpu().tolist())
+                    if i is not None]
+        rh, sh = rows.cpu().numpy(), scores.cpu().numpy()
+        return rescored_top(self.Y.id_array()[rh], sh, rescorer, how_many)
+
     def top_n(self, target: np.ndarray, how_many: int, cosine: bool = False,
               exclude: Optional[Collection[str]] = None,
               rescorer: Optional[Rescorer] = None) -> List[Tuple[str, float]]:
@@ -495,9 +521,7 @@ class ALSServingModel(ServingModel):
             ex = self.Y.host_rows(exclude) if exclude else None
             tgt = np.asarray(target, dtype=np.float32)
             if rescorer is not None:
-                rows, scores = self.index.all_scores(tgt, cosine, cands, ex)
-                return rescored_top(self.Y.ids_of_rows(rows.tolist()), scores, rescorer,
-                                    how_many)
+                return self._rescored_top_n(tgt, cosine, cands, ex, rescorer, how_many)
             q = topn_ops.TopNQuery(tgt, how_many, cosine, cands, ex)
             if self.batcher is not None and how_many <= topn_ops.MAX_HOW_MANY:
                 rows, scores = self.batcher.submit(q)

@@ -364,15 +364,17 @@ class ItemIndex:
         return out
 
     # ------------------------------------------------------------------ all scores
-    def all_scores(self, target: np.ndarray, cosine: bool, candidates=None,
-                   exclude_rows=None) -> Tuple[np.ndarray, np.ndarray]:
-        """(store rows, scores) of EVERY candidate item (LSH buckets ``candidates``, minus
-        ``exclude_rows``): what an arbitrary rescorer must see (``TopNConsumer`` applies the
-        rescorer to each candidate).  One GEMV over the rows the index reads."""
+    def all_scores_device(self, target: np.ndarray, cosine: bool, candidates=None,
+                          exclude_rows=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(store rows int64, scores fp32) of EVERY candidate item (LSH buckets
+        ``candidates``, minus ``exclude_rows``) as device tensors: what an arbitrary rescorer
+        must see (``TopNConsumer`` applies the rescorer to each candidate).  One GEMV over the
+        rows the index reads."""
         self.refresh()
-        if self.n == 0:
-            return np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32)
         dev = self.device
+        if self.n == 0:
+            e = torch.zeros(0, dtype=torch.int64, device=dev)
+            return e, torch.zeros(0, dtype=torch.float32, device=dev)
         mat, ld, perm = self._matrix()
         q = torch.zeros(self.kp, dtype=torch.float32, device=dev)
         q[:self.k] = torch.as_tensor(np.asarray(target, dtype=np.float32)[:self.k], device=dev)
@@ -395,14 +397,8 @@ class ItemIndex:
                 er = torch.as_tensor(np.asarray(exclude_rows, dtype=np.int64), device=dev)
                 keep[er[er < keep.numel()]] = False
             keep &= torch.isfinite(scores)
-            # two pinned transfers (mask + scores); the selection runs on the host
-            mask_h = torch.empty(keep.numel(), dtype=torch.bool, pin_memory=True)
-            sc_h = torch.empty(scores.numel(), dtype=torch.float32, pin_memory=True)
-            mask_h.copy_(keep)
-            sc_h.copy_(scores)
-            m_np = mask_h.numpy()
-            rows = np.flatnonzero(m_np)
-            return rows, sc_h.numpy()[rows]
+            rows = torch.nonzero(keep).flatten()
+            return rows, scores[rows]
         scores = mat[:self.n].matmul(q)
         if cosine:
             nrm = mat[:self.n].norm(dim=1)
@@ -418,7 +414,20 @@ class ItemIndex:
             p = self.pos_of_row[er]
             keep[p[p >= 0]] = False
         pos = torch.nonzero(keep).flatten()
-        return self.row_of_pos_h[pos.cpu().numpy()], scores[pos].cpu().numpy()
+        return self.row_of_pos[pos], scores[pos]
+
+    def all_scores(self, target: np.ndarray, cosine: bool, candidates=None,
+                   exclude_rows=None) -> Tuple[np.ndarray, np.ndarray]:
+        """:meth:`all_scores_device` on the host: (store rows, scores) numpy arrays."""
+        rows, sc = self.all_scores_device(target, cosine, candidates, exclude_rows)
+        if rows.device.type == "cuda" and rows.numel():
+            # pinned staging: one DMA each
+            rh = torch.empty(rows.numel(), dtype=torch.int64, pin_memory=True)
+            sh = torch.empty(sc.numel(), dtype=torch.float32, pin_memory=True)
+            rh.copy_(rows)
+            sh.copy_(sc)
+            return rh.numpy(), sh.numpy()
+        return rows.cpu().numpy(), sc.cpu().numpy()
 
 
 class ShardedItemIndex:
@@ -470,6 +479,11 @@ class ShardedItemIndex:
             o = np.lexsort((rows, -sc))[:q.how_many]
             out.append((rows[o], sc[o]))
         return out
+
+    def all_scores_device(self, target, cosine: bool, candidates=None, exclude_rows=None):
+        r, s = self.all_scores(target, cosine, candidates, exclude_rows)
+        dev = self.shards[0].device
+        return torch.from_numpy(r).to(dev), torch.from_numpy(s).to(dev)
 
     def all_scores(self, target, cosine: bool, candidates=None, exclude_rows=None):
         self.refresh()

@@ -7,4 +7,5 @@ timeout -k 10 300 python scripts/bench_log_append.py > gpurun_out/r4_log_append.
 timeout -k 10 300 python bench_batch.py --ratings 25000000 --test-fraction 0.1 > gpurun_out/r4_bb_single_tf.json 2> gpurun_out/r4_bb_single_tf.err || exit 1
 timeout -k 10 300 python bench_batch.py --ratings 25000000 > gpurun_out/r4_bb_single.json 2> gpurun_out/r4_bb_single.err || exit 1
 timeout -k 10 400 python bench_batch.py --app rdf --points 6250000 > gpurun_out/r4_bb_rdf.json 2> gpurun_out/r4_bb_rdf.err || exit 1
+timeout -k 10 300 python bench.py --emulate-world 8 --emulate-rank 0 --steps 10 --warmup 3 > gpurun_out/r4_emul_c2_w8.json 2> gpurun_out/r4_emul_c2_w8.err || exit 1
 echo done

@@ -282,3 +282,31 @@ def test_speed_device_inverses_match_host_rrqr(cuda):
     bad.Y.set_vectors(["I%d" % j for j in range(len(Yb))], Yb)
     with pytest.raises(mathx.SingularMatrixSolverException):
         bad.solver_inverses()
+
+
+def test_item_filter_rescorer_forms_agree_cpu():
+    """ItemFilterRescorer: per-item, array and device forms give the same filter / scores;
+    the store's cached ID array and row mask line up with its rows."""
+    import torch
+    from oryx_amd.models.als.common import FeatureVectors
+    from oryx_amd.models.als.rescorer import ItemFilterRescorer, ItemFilterRescorerProvider
+    store = FeatureVectors(2)
+    ids = ["I%d" % j for j in range(20)]
+    store.set_vectors(ids, np.ones((20, 2), dtype=np.float32))
+    store.remove_vector("I4")
+    arr = store.id_array()
+    assert arr[4] is None and list(arr[:4]) == ids[:4]
+    r = ItemFilterRescorer(["I3", "I7", "I4"], 2.0)
+    rows = torch.arange(20)
+    scores = torch.linspace(0, 1, 20)
+    live = np.array([i is not None for i in arr])     # row 4 is free (its ID removed)
+    dev = r.rescore_device(rows, scores, store).double().numpy()[live]
+    lids = [i for i in arr if i is not None]
+    host = r.rescore_many(lids, scores.double().numpy()[live])
+    per = np.array([r.rescore(i, float(v)) for i, v in zip(lids, scores.numpy()[live])])
+    np.testing.assert_allclose(dev, host, rtol=1e-6, equal_nan=True)
+    np.testing.assert_allclose(host, per, rtol=1e-12, equal_nan=True)
+    assert [lids[j] for j in np.flatnonzero(np.isnan(host))] == ["I3", "I7"]
+    p = ItemFilterRescorerProvider()
+    assert p.get_recommend_rescorer(["U1"], []) is None
+    assert p.get_recommend_rescorer(["U1"], ["exclude:I2", "factor:3"]).is_filtered("I2")

@@ -688,10 +688,32 @@ def test_rescorer_sees_every_candidate_on_large_catalogue(cuda):
     # the winners include items far outside the raw top 4096
     raw_rank = np.argsort(np.argsort(-raw))
     assert raw_rank[best].max() > 4096
-    for r in (PerItem(), Vectorised()):
+    class Device(Vectorised):
+        # the device form (here computed from the array forms, returned as a device tensor)
+        def rescore_device(self, rows, scores, store):
+            idl = store.id_array()[rows.cpu().numpy()]
+            v = self.rescore_many(idl, scores.double().cpu().numpy())
+            v[self.is_filtered_many(idl)] = np.nan
+            return torch.from_numpy(v).to(rows.device)
+
+    for r in (PerItem(), Vectorised(), Device()):
         got = m.top_n(t, 100, exclude={"I17", "I27"}, rescorer=r)
         assert [i for i, _ in got] == [ids[b] for b in best]
         np.testing.assert_allclose([v for _, v in got], ref[best], rtol=1e-5, atol=1e-5)
+    # the example provider's device-capable filter: same answer as its host forms
+    from oryx_amd.models.als.rescorer import ItemFilterRescorer
+
+    class HostOnly(ItemFilterRescorer):
+        def rescore_device(self, rows, scores, store):
+            return None
+
+    excl = ["I%d" % int(b) for b in np.argsort(-raw)[:50:3]]
+    dev_r, host_r = ItemFilterRescorer(excl, 2.0), HostOnly(excl, 2.0)
+    a = m.top_n(t, 40, rescorer=dev_r)
+    b = m.top_n(t, 40, rescorer=host_r)
+    assert [i for i, _ in a] == [i for i, _ in b]
+    assert not set(excl) & {i for i, _ in a}
+    np.testing.assert_allclose([v for _, v in a], [v for _, v in b], rtol=1e-6)
 
 
 @pytest.mark.gpu
