@@ -17,10 +17,17 @@
 
 #pragma once
 
+#include <unistd.h>
+
+#include <atomic>
 #include <charconv>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -444,8 +451,74 @@ inline int native_threads() {
   return n;
 }
 
+// Persistent worker threads for parallel_ranges (native_threads() - 1 of them, started on
+// first use): a speed-layer micro-batch runs several parallel loops of ~0.1 ms each, where
+// creating and joining fresh threads per loop cost about as much as the work.  Tasks are
+// queued; a caller waiting for its own tasks runs queued ones meanwhile, so nested and
+// concurrent calls (the speed layer's writer thread beside the main thread) cannot deadlock.
+// A forked child (pid differs) starts a pool of its own.
+struct ThreadPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::function<void()>> q;
+  std::atomic<int> queued{0};
+
+  explicit ThreadPool(int workers) {
+    for (int w = 0; w < workers; ++w)
+      std::thread([this] {
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> l(mu);
+            cv.wait(l, [&] { return !q.empty(); });
+            f = std::move(q.front());
+            q.pop_front();
+            queued.fetch_sub(1, std::memory_order_relaxed);
+          }
+          f();
+        }
+      }).detach();
+  }
+
+  void push(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      q.push_back(std::move(f));
+      queued.fetch_add(1, std::memory_order_relaxed);
+    }
+    cv.notify_one();
+  }
+
+  bool run_one() {
+    if (queued.load(std::memory_order_relaxed) == 0) return false;
+    std::function<void()> f;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      if (q.empty()) return false;
+      f = std::move(q.front());
+      q.pop_front();
+      queued.fetch_sub(1, std::memory_order_relaxed);
+    }
+    f();
+    return true;
+  }
+};
+
+inline ThreadPool& thread_pool() {
+  static std::mutex mu;
+  static ThreadPool* pool = nullptr;   // never destroyed: its workers are detached
+  static long pid = 0;
+  std::lock_guard<std::mutex> g(mu);
+  if (!pool || pid != (long)getpid()) {
+    pool = new ThreadPool(native_threads() - 1);
+    pid = (long)getpid();
+  }
+  return *pool;
+}
+
 // Runs fn(lo, hi, part) over `parts` contiguous ranges of [0, n) (part 0 on the caller's
-// thread); parts = min(threads, n / min_per_part), at least 1.  Returns parts.
+// thread, the rest on the pool); parts = min(threads, n / min_per_part), at least 1.
+// Returns parts.
 template <class Fn>
 int parallel_ranges(long long n, long long min_per_part, Fn&& fn) {
   long long parts = min_per_part > 0 ? n / min_per_part : n;
@@ -456,12 +529,16 @@ int parallel_ranges(long long n, long long min_per_part, Fn&& fn) {
     fn(0LL, n, 0);
     return 1;
   }
-  std::vector<std::thread> th;
-  th.reserve((size_t)P - 1);
+  ThreadPool& pool = thread_pool();
+  std::atomic<int> left(P - 1);
   for (int t = 1; t < P; ++t)
-    th.emplace_back([&, t] { fn(n * t / P, n * (t + 1) / P, t); });
+    pool.push([&, t] {
+      fn(n * t / P, n * (t + 1) / P, t);
+      left.fetch_sub(1, std::memory_order_acq_rel);
+    });
   fn(0LL, n / P, 0);
-  for (auto& x : th) x.join();
+  while (left.load(std::memory_order_acquire) > 0)
+    if (!pool.run_one()) std::this_thread::yield();
   return P;
 }
 

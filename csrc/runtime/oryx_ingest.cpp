@@ -2302,9 +2302,42 @@ long long oryx_aggregate_scores(const long long* u, const long long* i, const do
 
 namespace {
 
+// JSON-quoted length of a key, and the quoted key written at dst (returns the end): keys
+// that need no escaping (the usual case) are '"' + bytes + '"' without a temporary string.
+bool plain_json(const char* s, size_t n) {
+  for (size_t k = 0; k < n; ++k) {
+    const unsigned char c = (unsigned char)s[k];
+    if (c < 0x20 || c >= 0x80 || c == '"' || c == '\\') return false;
+  }
+  return true;
+}
+
+size_t quoted_len(std::string_view k) {
+  if (plain_json(k.data(), k.size())) return k.size() + 2;
+  std::string q;
+  json_quote(k.data(), k.size(), q);
+  return q.size();
+}
+
+// (ql: the key's quoted_len; a key that needs escapes always quotes longer than size + 2)
+char* put_quoted(std::string_view k, size_t ql, char* o) {
+  if (ql == k.size() + 2) {
+    *o++ = '"';
+    memcpy(o, k.data(), k.size());
+    o += k.size();
+    *o++ = '"';
+    return o;
+  }
+  std::string q;
+  json_quote(k.data(), k.size(), q);
+  memcpy(o, q.data(), q.size());
+  return o + q.size();
+}
+
 struct SpeedBatch {
   // per event: store row (>= 0) or -(new key index) - 1; strength; timestamp; key views
   std::vector<int64_t> u, i;
+  std::vector<uint32_t> uql, iql;       // the keys' JSON-quoted lengths (quoted_len)
   std::vector<double> s;
   std::vector<long long> ts;
   std::vector<std::string_view> uk, ik;
@@ -2320,6 +2353,7 @@ struct SpeedBatch {
 
   void clear() {
     u.clear(); i.clear(); s.clear(); ts.clear(); uk.clear(); ik.clear(); owned.clear();
+    uql.clear(); iql.clear();
     nu_idx.clear(); ni_idx.clear(); nu_keys.clear(); ni_keys.clear();
     au.clear(); ai.clear(); rep.clear(); av.clear();
   }
@@ -2346,6 +2380,7 @@ int bit_width(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 
 struct SpeedChunk {
   std::vector<int64_t> u, i;
+  std::vector<uint32_t> uql, iql;
   std::vector<double> s;
   std::vector<long long> ts;
   std::vector<std::string_view> uk, ik;
@@ -2409,6 +2444,8 @@ long long oryx_speed_parse(void* h, const char* buf, long long len, void* xm, vo
             c.ts.push_back(tv);
             c.uk.push_back(a);
             c.ik.push_back(bk);
+            c.uql.push_back((uint32_t)quoted_len(a));
+            c.iql.push_back((uint32_t)quoted_len(bk));
           }
         }
         p = nl ? nl + 1 : end;
@@ -2418,8 +2455,10 @@ long long oryx_speed_parse(void* h, const char* buf, long long len, void* xm, vo
   size_t n = 0;
   for (auto& c : ch) n += c.u.size();
   b->u.reserve(n); b->i.reserve(n); b->s.reserve(n); b->ts.reserve(n);
-  b->uk.reserve(n); b->ik.reserve(n);
+  b->uk.reserve(n); b->ik.reserve(n); b->uql.reserve(n); b->iql.reserve(n);
   for (auto& c : ch) {
+    b->uql.insert(b->uql.end(), c.uql.begin(), c.uql.end());
+    b->iql.insert(b->iql.end(), c.iql.begin(), c.iql.end());
     for (size_t r = 0; r < c.u.size(); ++r) {
       int64_t ur = c.u[r], ir = c.i[r];
       bool ins;
@@ -2543,6 +2582,111 @@ long long oryx_speed_aggregate(void* h, int implicit, long long* out_u, long lon
     out_s[k] = b->av[k];
   }
   return (long long)m;
+}
+
+long long oryx_log_append_fill(void* h, int partition, const char* key, int key_len,
+                               const long long* lens, int n,
+                               void (*fill)(void* ctx, long long j, char* dst), void* ctx,
+                               long long ts_ms, int do_fsync);
+
+}  // extern "C"
+
+namespace {
+
+// What oryx_speed_append's fill callback needs: message m is side sides[m] (0 X, 1 Y) of
+// aggregated pair pair[m] (indexed from lo).
+struct SpeedFill {
+  const SpeedBatch* b;
+  long long lo;
+  const char* xtext;
+  const long long* xends;
+  const char* ytext;
+  const long long* yends;
+  int with_known;
+  std::vector<int32_t> pair;
+  std::vector<uint8_t> side;
+};
+
+void speed_fill(void* ctx, long long m, char* o) {
+  const SpeedFill& F = *static_cast<const SpeedFill*>(ctx);
+  const long long e = F.pair[(size_t)m];
+  const int64_t r = F.b->rep[(size_t)(F.lo + e)];
+  const std::string_view uk = F.b->uk[(size_t)r], ik = F.b->ik[(size_t)r];
+  const bool y = F.side[(size_t)m] != 0;
+  const long long* ends = y ? F.yends : F.xends;
+  const long long s0 = e ? ends[e - 1] : 0;
+  memcpy(o, y ? "[\"Y\"," : "[\"X\",", 5);
+  const size_t uq = F.b->uql[(size_t)r], iq = F.b->iql[(size_t)r];
+  o = put_quoted(y ? ik : uk, y ? iq : uq, o + 5);
+  *o++ = ',';
+  memcpy(o, (y ? F.ytext : F.xtext) + s0, (size_t)(ends[e] - s0));
+  o += ends[e] - s0;
+  if (F.with_known) {
+    *o++ = ',';
+    *o++ = '[';
+    o = put_quoted(y ? uk : ik, y ? uq : iq, o);
+    *o++ = ']';
+  }
+  *o = ']';
+}
+
+}  // namespace
+
+extern "C" {
+
+// The aggregated pairs [lo, hi)'s UP messages (the layout of oryx_speed_assemble, without the
+// separators) appended to the log `topic` as records with key "UP", formatted by the log's
+// writer threads straight into the segment (oryx_log_append_fill): the row text crosses
+// memory once between the GPU's copy and the page cache.  Valid until the batch's next
+// parse.  Returns the last offset written, -1 on error, -2 when a message exceeds the topic's
+// maximum size (nothing written); *n_msgs receives the number of messages.
+long long oryx_speed_append(void* h, void* topic, int partition, long long lo, long long hi,
+                            const char* xtext, const long long* xends, const char* ytext,
+                            const long long* yends, const unsigned char* vx,
+                            const unsigned char* vy, int with_known, long long ts_ms,
+                            int do_fsync, long long* n_msgs) {
+  const auto T0 = std::chrono::steady_clock::now();
+  const SpeedBatch* b = static_cast<const SpeedBatch*>(h);
+  const long long n = hi - lo;
+  SpeedFill F{b, lo, xtext, xends, ytext, yends, with_known, {}, {}};
+  std::vector<long long> cnt((size_t)n + 1, 0);
+  for (long long e = 0; e < n; ++e) cnt[(size_t)e + 1] = cnt[(size_t)e] + (vx[e] ? 1 : 0) + (vy[e] ? 1 : 0);
+  const long long m = cnt[(size_t)n];
+  *n_msgs = m;
+  if (m == 0) return -1;
+  F.pair.resize((size_t)m);
+  F.side.resize((size_t)m);
+  std::vector<long long> lens((size_t)m);
+  const auto T1 = std::chrono::steady_clock::now();
+  oryx_ff::parallel_ranges(n, 32768, [&](long long a, long long z, int) {
+    for (long long e = a; e < z; ++e) {
+      const int64_t r = b->rep[(size_t)(lo + e)];
+      const long long lu = b->uql[(size_t)r], li = b->iql[(size_t)r];
+      long long j = cnt[(size_t)e];
+      if (vx[e]) {
+        const long long xs = e ? xends[e - 1] : 0;
+        F.pair[(size_t)j] = (int32_t)e;
+        F.side[(size_t)j] = 0;
+        lens[(size_t)j++] = 5 + lu + 1 + (xends[e] - xs) + (with_known ? 3 + li : 0) + 1;
+      }
+      if (vy[e]) {
+        const long long ys = e ? yends[e - 1] : 0;
+        F.pair[(size_t)j] = (int32_t)e;
+        F.side[(size_t)j] = 1;
+        lens[(size_t)j++] = 5 + li + 1 + (yends[e] - ys) + (with_known ? 3 + lu : 0) + 1;
+      }
+    }
+  });
+  if (std::getenv("ORYX_LOG_DEBUG"))
+    fprintf(stderr, "speed_append sizes %.3f ms (setup %.3f)\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count(),
+            std::chrono::duration<double, std::milli>(T1 - T0).count());
+  const long long res = oryx_log_append_fill(topic, partition, "UP", 2, lens.data(), (int)m,
+                                             speed_fill, &F, ts_ms, do_fsync);
+  if (std::getenv("ORYX_LOG_DEBUG"))
+    fprintf(stderr, "speed_append total %.3f ms\n",
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count());
+  return res;
 }
 
 // The aggregated pairs [lo, hi)'s UP messages (same layout as oryx_assemble_als_updates:

@@ -274,6 +274,12 @@ struct SegMap {
 #define MADV_POPULATE_WRITE 23     // Linux 5.14+ (older headers lack the name)
 #endif
 void prefault_run(const std::shared_ptr<SegMap>& m, int64_t off, int64_t len) {
+  if (len < 0) {
+    // a retired writer mapping (its segment is full): cut the file's unused preallocated
+    // tail at `off`, the end of its data; the mapping itself goes with the last reference
+    if (m && m->fd >= 0) (void)!ftruncate(m->fd, off);
+    return;
+  }
   {
   const long long page = sysconf(_SC_PAGESIZE);
   const int64_t a = off - off % page;
@@ -614,12 +620,52 @@ std::vector<uint8_t>& frame_buffer(size_t need) {
   return out;
 }
 
+// The segment just filled (its data reached the roll size): the next append starts a new
+// segment at offset `next`.  Create and size it now and fault its first pages in on the
+// background thread, so that append (a speed layer's next micro-batch) finds its pages ready
+// instead of paying a fresh mapping's page faults; the full segment's mapping retires on
+// the background thread, which also cuts its unused zero tail.  Readers treat the new,
+// all-zero segment as the end of the data (a zero magic), as they do a preallocated tail.
+// Called under the partition's locks.
+void pre_roll(Topic* t, Partition& P, int64_t next, size_t total) {
+  const std::string path = seg_name(P.dir, next);
+  const int fd = open(path.c_str(), O_RDWR | O_CREAT, 0644);
+  if (fd < 0) return;
+  struct stat st;
+  const int64_t want = std::min<int64_t>(std::max<int64_t>(2 * (int64_t)total, 16ll << 20),
+                                         t->segment_bytes);
+  if (fstat(fd, &st) != 0 || st.st_size != 0 || ftruncate(fd, want) != 0) {
+    close(fd);
+    return;
+  }
+  auto m = std::make_shared<SegMap>();
+  m->fd = fd;
+  m->seg_base = next;
+  m->len = (size_t)t->segment_bytes + 4 * total;
+  void* a = mmap(nullptr, m->len, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  if (a == MAP_FAILED) return;           // (m closes fd)
+  m->base = static_cast<uint8_t*>(a);
+  std::shared_ptr<SegMap> old = std::move(P.wmap);
+  P.wmap = m;
+  if (old) prefault_async(old, P.c_pos, -1);
+  prefault_async(m, 0, want);
+  P.c_base = next;
+  P.c_pos = 0;
+  P.c_next = next;
+}
+
 // Appends `recs` (already validated) to partition `part` under its locks; records get
 // consecutive offsets.  Frames are built straight from the records' memory, their CRCs over
 // several threads for large batches.  Returns the last offset written, or -1.
+// A producer that writes record j's value bytes straight into its frame (`vlen` bytes at
+// dst) instead of the log copying them from the caller's memory.
+typedef void (*FillFn)(void* ctx, long long j, char* dst);
+
 long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
                            const std::vector<int>& which, long long ts_ms, int do_fsync,
-                           long long* out_offsets) {
+                           long long* out_offsets, FillFn fill = nullptr,
+                           void* fill_ctx = nullptr) {
+  const auto Ts = std::chrono::steady_clock::now();
   Partition& P = t->parts[part];
   std::lock_guard<std::mutex> in_process(*P.mu);
   if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_EX);
@@ -688,7 +734,8 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
       auto m = std::make_shared<SegMap>();
       m->fd = open(path.c_str(), O_RDWR);
       m->seg_base = base;
-      m->len = std::max<size_t>((size_t)t->segment_bytes, 2 * need);
+      // (room for the block that overshoots the roll size too)
+      m->len = std::max<size_t>((size_t)t->segment_bytes + 2 * total, 2 * need);
       if (m->fd >= 0) {
         void* a = mmap(nullptr, m->len, PROT_READ | PROT_WRITE, MAP_SHARED, m->fd, 0);
         if (a != MAP_FAILED) m->base = static_cast<uint8_t*>(a);
@@ -716,7 +763,10 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
       memcpy(f + 24, &uk, 4);
       memcpy(f + 28, &uv, 4);
       if (kl) memcpy(f + kHeader, r.key, kl);
-      memcpy(f + kHeader + kl, r.val, (size_t)r.vlen);
+      if (fill)
+        fill(fill_ctx, (long long)which[(size_t)j], reinterpret_cast<char*>(f + kHeader + kl));
+      else
+        memcpy(f + kHeader + kl, r.val, (size_t)r.vlen);
       const uint32_t crc = crc32(f + kHeader, kl + (size_t)r.vlen, crc32(f + 8, 16));
       memcpy(f + 4, &crc, 4);
     }
@@ -758,8 +808,9 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
   }
   const auto T2 = std::chrono::steady_clock::now();
   if (std::getenv("ORYX_LOG_DEBUG"))
-    fprintf(stderr, "append %zu B mapped=%d map %.3f build %.3f ms write %.3f ms\n", total,
-            mapped != nullptr, std::chrono::duration<double, std::milli>(T0 - Tm).count(),
+    fprintf(stderr, "append %zu B mapped=%d open %.3f map %.3f build %.3f ms write %.3f ms\n",
+            total, mapped != nullptr, std::chrono::duration<double, std::milli>(Tm - Ts).count(),
+            std::chrono::duration<double, std::milli>(T0 - Tm).count(),
             std::chrono::duration<double, std::milli>(T1 - T0).count(),
             std::chrono::duration<double, std::milli>(T2 - T1).count());
   if (done == total && mapped && g_prealloc) {
@@ -767,9 +818,12 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
     // (under the lock; never past its roll size) and fault the new range in on a
     // background thread -- the append itself then only copies bytes
     const int64_t new_end = end_pos + (int64_t)total;
+    // (up to a block past the roll size: the block that crosses it lands there too, and the
+    // unused rest is cut when the segment retires, see pre_roll)
     int64_t want = std::min<int64_t>(new_end + std::max<int64_t>(2 * (int64_t)total,
                                                                  16ll << 20),
-                                     std::max<int64_t>(t->segment_bytes, new_end));
+                                     std::max<int64_t>(t->segment_bytes + (int64_t)total,
+                                                       new_end));
     want = std::min<int64_t>(want, (int64_t)P.wmap->len);
     if (want > file_size && ftruncate(fd, want) == 0) file_size = want;
     if (file_size > new_end) prefault_async(P.wmap, new_end, file_size - new_end);
@@ -784,13 +838,18 @@ long long append_partition(Topic* t, int part, const std::vector<RecRef>& recs,
   P.c_base = base;
   P.c_pos = end_pos + (int64_t)total;
   P.c_next = next;
+  if (mapped && g_prealloc && P.c_pos >= t->segment_bytes) pre_roll(t, P, next, total);
   if (P.lock_fd >= 0) flock(P.lock_fd, LOCK_UN);
+  if (std::getenv("ORYX_LOG_DEBUG"))
+    fprintf(stderr, "append tail %.3f ms\n", std::chrono::duration<double, std::milli>(
+        std::chrono::steady_clock::now() - T2).count());
   return next - 1;
 }
 
 // Validates the records, routes them to partitions (-1: by key / round robin) and appends.
 long long append_records(Topic* t, void* h, int partition, const std::vector<RecRef>& recs,
-                         long long ts_ms, int do_fsync, long long* out_offsets) {
+                         long long ts_ms, int do_fsync, long long* out_offsets,
+                         FillFn fill = nullptr, void* fill_ctx = nullptr) {
   errno = 0;
   if (ts_ms < 0) ts_ms = now_ms();
   const size_t n = recs.size();
@@ -809,7 +868,8 @@ long long append_records(Topic* t, void* h, int partition, const std::vector<Rec
   long long last = -1;
   for (int part = 0; part < t->partitions; ++part) {
     if (idx[part].empty()) continue;
-    const long long l = append_partition(t, part, recs, idx[part], ts_ms, do_fsync, out_offsets);
+    const long long l = append_partition(t, part, recs, idx[part], ts_ms, do_fsync, out_offsets,
+                                         fill, fill_ctx);
     if (l < 0) return -1;
     last = l;
   }
@@ -1034,6 +1094,23 @@ long long oryx_log_append_values_gap(void* h, int partition, const char* key, in
     v += lens[i] + gap;
   }
   return append_records(t, h, partition, recs, ts_ms, do_fsync, nullptr);
+}
+
+// Records sharing one key whose values a producer writes itself: record j has lens[j] value
+// bytes, which fill(ctx, j, dst) stores at dst -- straight into the segment's mapped page
+// cache on the large-append path, so a producer that formats its messages there (the speed
+// layer's UP assembly, oryx_speed_append) costs one pass over the bytes, CRCs included (each
+// frame's CRC is computed by the thread that just wrote it).  fill runs on several native
+// threads at once for large appends.  Same results as oryx_log_append_values.
+long long oryx_log_append_fill(void* h, int partition, const char* key, int key_len,
+                               const long long* lens, int n, FillFn fill, void* ctx,
+                               long long ts_ms, int do_fsync) {
+  auto* t = static_cast<Topic*>(h);
+  std::vector<RecRef> recs((size_t)n);
+  for (int i = 0; i < n; ++i)
+    recs[(size_t)i] = RecRef{key_len < 0 ? nullptr : key, key_len < 0 ? -1 : key_len, nullptr,
+                             (int64_t)lens[i]};
+  return append_records(t, h, partition, recs, ts_ms, do_fsync, nullptr, fill, ctx);
 }
 
 // Bulk poll for consumers that parse records natively (the serving model load): complete

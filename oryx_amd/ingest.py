@@ -322,6 +322,7 @@ class SpeedBatch:
         self._lib = native.runtime()
         self._h = self._lib.oryx_speed_new()
         self._buf = None
+        self._gen = 0        # bumped by every parse (deferred blocks check it)
 
     def __del__(self):
         try:
@@ -344,6 +345,7 @@ class SpeedBatch:
         else:
             buf = np.frombuffer("\n".join(lines).encode("utf-8"), dtype=np.uint8)
         self._buf = buf
+        self._gen += 1
         return int(self._lib.oryx_speed_parse(self._h, _ptr(buf), int(buf.nbytes), xmap._h,
                                               ymap._h, int(default_ts)))
 
@@ -385,18 +387,10 @@ class SpeedBatch:
         if n <= 0:
             return MessageBlock(b"", np.zeros(0, dtype=np.int64))
         lo = int(lo)
-        vx = np.ascontiguousarray(vx[lo:hi], dtype=np.uint8)
-        vy = np.ascontiguousarray(vy[lo:hi], dtype=np.uint8)
-        xb = int(xrows.ends[lo - 1]) if lo else 0
-        yb = int(yrows.ends[lo - 1]) if lo else 0
-        xe = np.ascontiguousarray(xrows.ends[lo:hi] - xb, dtype=np.int64)
-        ye = np.ascontiguousarray(yrows.ends[lo:hi] - yb, dtype=np.int64)
-        vp = ctypes.c_void_p
+        vx, vy, xe, ye, xptr, yptr = _row_args(xrows, yrows, vx, vy, lo, int(hi))
         cap = int(xe[-1]) + int(ye[-1]) + n * 256
         ends = np.empty(2 * n, dtype=np.int64)
         n_msgs = ctypes.c_longlong(0)
-        xptr = vp(_buf_ptr(xrows.blob).value + xb)
-        yptr = vp(_buf_ptr(yrows.blob).value + yb)
         while True:
             out = _host_buffer(cap)
             used = self._lib.oryx_speed_assemble(
@@ -406,6 +400,85 @@ class SpeedBatch:
                 break
             cap = -used + 1
         return MessageBlock(out[:used], ends[:n_msgs.value].copy())
+
+
+    def deferred(self, lo: int, hi: int, xrows, yrows, vx: np.ndarray, vy: np.ndarray,
+                 with_known: bool) -> "DeferredUpBlock":
+        """The same messages as :meth:`assemble`, not yet formatted: a block that the native
+        log formats straight into its segment when appended (:meth:`DeferredUpBlock.
+        append_to`), or into a buffer on first access otherwise.  Valid until the next
+        :meth:`parse`."""
+        return DeferredUpBlock(self, int(lo), int(hi), xrows, yrows, vx, vy, with_known)
+
+
+def _row_args(xrows, yrows, vx, vy, lo, hi):
+    vx = np.ascontiguousarray(vx[lo:hi], dtype=np.uint8)
+    vy = np.ascontiguousarray(vy[lo:hi], dtype=np.uint8)
+    xb = int(xrows.ends[lo - 1]) if lo else 0
+    yb = int(yrows.ends[lo - 1]) if lo else 0
+    xe = np.ascontiguousarray(xrows.ends[lo:hi] - xb, dtype=np.int64)
+    ye = np.ascontiguousarray(yrows.ends[lo:hi] - yb, dtype=np.int64)
+    xptr = ctypes.c_void_p(_buf_ptr(xrows.blob).value + xb)
+    yptr = ctypes.c_void_p(_buf_ptr(yrows.blob).value + yb)
+    return vx, vy, xe, ye, xptr, yptr
+
+
+from .api import MessageBlock as _MessageBlock  # noqa: E402
+
+
+class DeferredUpBlock(_MessageBlock):
+    """A speed-layer micro-batch's UP messages (``SpeedBatch.deferred``) held as the parsed
+    batch plus the GPU-formatted row text: appended to a native log topic it is formatted by
+    the log's writer threads straight into the segment, CRCs included
+    (``oryx_speed_append`` -> ``oryx_log_append_fill``), so the row bytes are copied once
+    after the GPU's; any other use materialises the ordinary :class:`MessageBlock` buffer."""
+
+    __slots__ = ("_sb", "_gen", "_lo", "_hi", "_rows", "_with_known", "_n", "_block")
+
+    def __init__(self, sb: SpeedBatch, lo: int, hi: int, xrows, yrows, vx, vy,
+                 with_known: bool):
+        self._sb, self._gen, self._lo, self._hi = sb, sb._gen, lo, hi
+        self._rows = (xrows, yrows, vx, vy)
+        self._with_known = bool(with_known)
+        self._n = int(np.count_nonzero(vx[lo:hi])) + int(np.count_nonzero(vy[lo:hi])) \
+            if hi > lo else 0
+        self._block = None
+        self._cache = None
+
+    def _check(self):
+        if self._sb._gen != self._gen:
+            raise RuntimeError("deferred UP block used after its speed batch was re-parsed")
+
+    def materialize(self) -> _MessageBlock:
+        if self._block is None:
+            self._check()
+            xrows, yrows, vx, vy = self._rows
+            self._block = self._sb.assemble(self._lo, self._hi, xrows, yrows, vx, vy,
+                                            self._with_known)
+        return self._block
+
+    buf = property(lambda self: self.materialize().buf)
+    ends = property(lambda self: self.materialize().ends)
+    sep = property(lambda self: 1)
+
+    def __len__(self) -> int:
+        return self._n
+
+    def append_to(self, handle, partition: int = -1, timestamp_ms: int = -1,
+                  fsync: bool = False) -> int:
+        """Append as key-``UP`` records to the native topic ``handle``; the native result
+        (last offset, -1 error, -2 a message over the topic's maximum, nothing written)."""
+        if self._n == 0:
+            return -1
+        self._check()
+        sb = self._sb
+        xrows, yrows, vx, vy = self._rows
+        vx, vy, xe, ye, xptr, yptr = _row_args(xrows, yrows, vx, vy, self._lo, self._hi)
+        n_msgs = ctypes.c_longlong(0)
+        return int(sb._lib.oryx_speed_append(
+            sb._h, handle, int(partition), self._lo, self._hi, xptr, _ptr(xe), yptr, _ptr(ye),
+            _ptr(vx), _ptr(vy), int(self._with_known), int(timestamp_ms), int(bool(fsync)),
+            ctypes.byref(n_msgs)))
 
 
 def parse_up_batch(messages: Sequence[str], k: int, known_dict: Optional["IdDict"] = None):

@@ -273,7 +273,8 @@ class ALSSpeedModelManager(SpeedModelManager):
     def build_updates(self, new_data: Dataset) -> List[str]:
         """All UP messages of the interval (one :class:`~oryx_amd.api.MessageBlock` on the
         GPU path)."""
-        blocks = list(self.build_update_blocks(new_data, chunks=1))
+        blocks = [b.materialize() if hasattr(b, "materialize") else b
+                  for b in self.build_update_blocks(new_data, chunks=1)]
         if not blocks:
             return []
         return blocks[0] if len(blocks) == 1 else [m for b in blocks for m in b]
@@ -429,7 +430,10 @@ class ALSSpeedModelManager(SpeedModelManager):
         chunks = max(1, min(int(chunks), n // 1024 or 1))
         for c in range(chunks):
             t0 = time.perf_counter()
-            blk = sb.assemble(n * c // chunks, n * (c + 1) // chunks, xrows, yrows, vxh, vyh,
+            # formatted by the log's writer threads straight into the update-log segment
+            # when published to a native topic (ingest.DeferredUpBlock), so the assembly
+            # time shows in the append
+            blk = sb.deferred(n * c // chunks, n * (c + 1) // chunks, xrows, yrows, vxh, vyh,
                               not self.no_known_items)
             ph["assemble"] += (time.perf_counter() - t0) * 1e3
             yield blk

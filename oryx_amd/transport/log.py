@@ -202,6 +202,14 @@ class Topic:
             return -1
         if faults.armed():
             return self.append_values(list(block), partition, timestamp_ms, fsync, key=key)
+        if key == "UP" and hasattr(block, "append_to"):
+            # formats itself straight into the segment (ingest.DeferredUpBlock)
+            res = block.append_to(self._h, int(partition), int(timestamp_ms), fsync)
+            if res == -2:
+                raise MessageTooLargeError(_lib().oryx_log_last_error().decode())
+            if res < 0:
+                raise IOError(_lib().oryx_log_last_error().decode())
+            return res
         lens = np.ascontiguousarray(block.lengths(), dtype=np.int64)
         buf = block.buf
         if isinstance(buf, np.ndarray):

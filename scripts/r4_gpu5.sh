@@ -8,4 +8,5 @@ timeout -k 10 300 python bench_batch.py --ratings 25000000 --test-fraction 0.1 >
 timeout -k 10 300 python bench_batch.py --ratings 25000000 > gpurun_out/r4_bb_single.json 2> gpurun_out/r4_bb_single.err || exit 1
 timeout -k 10 400 python bench_batch.py --app rdf --points 6250000 > gpurun_out/r4_bb_rdf.json 2> gpurun_out/r4_bb_rdf.err || exit 1
 timeout -k 10 300 python bench.py --emulate-world 8 --emulate-rank 0 --steps 10 --warmup 3 > gpurun_out/r4_emul_c2_w8.json 2> gpurun_out/r4_emul_c2_w8.err || exit 1
+timeout -k 10 400 python -u bench_serving.py --items 20000000 --features 250 --sample-rate 1.0 --workers 1,4 --requests 200 --warmup 20 --rescorer > gpurun_out/r4_serving_rescorer.jsonl 2> gpurun_out/r4_serving_rescorer.err || exit 1
 echo done

@@ -136,3 +136,58 @@ def test_log_unpublished_block_is_truncated(tmp_path):
     assert t2.append(None, "b") == 1
     assert [x[3] for x in t2.reader(0, 0).poll(10, 10)] == ["a", "b"]
     t2.close()
+
+
+def _read_all(topic):
+    recs, r = [], topic.reader(0, 0)
+    while True:
+        got = r.poll(100000, 50)
+        if not got:
+            return recs
+        recs.extend(got)
+
+
+def test_deferred_block_formats_into_the_log(tmp_path):
+    """A deferred UP block appended to a native topic (formatted by the log's writer
+    threads in the segment, CRCs included) leaves exactly the records of the assembled
+    block -- on the pwrite path and on the mapped large-append path, keys needing JSON
+    escapes included; used after the batch's next parse it refuses."""
+    import pytest
+    xm, ym, _, _ = _stores()
+    lines = _lines(20000) + ['["U\\"q","Iü",1.5,1001]', '["U1","I\\\\x",2,1002]']
+    tl = TextLines.from_strings(lines)
+    sb = ingest.SpeedBatch()
+    sb.parse(tl, xm, ym)
+    u, i, s = sb.aggregate(True)
+    m = len(u)
+    g = np.random.default_rng(3)
+    xr = format_rows(g.normal(size=(m, 24)).astype(np.float32))
+    yr = format_rows(g.normal(size=(m, 24)).astype(np.float32))
+    vx = (g.random(m) < 0.9).astype(np.uint8)
+    vy = (g.random(m) < 0.8).astype(np.uint8)
+    for rep in range(2):
+        # the full block (> 4 MB) takes the mapped append, the half one pwrite
+        root = str(tmp_path / ("t%d" % rep))
+        tlog.maybe_create_topic(root, "A", 1, max_message=1 << 24)
+        tlog.maybe_create_topic(root, "B", 1, max_message=1 << 24)
+        a, b = tlog.Topic(root, "A"), tlog.Topic(root, "B")
+        for lo, hi, with_known in ((0, m, True), (17, m // 2, False)):
+            a.append_block(sb.assemble(lo, hi, xr, yr, vx, vy, with_known), key="UP")
+            blk = sb.deferred(lo, hi, xr, yr, vx, vy, with_known)
+            assert len(blk) == int(vx[lo:hi].sum() + vy[lo:hi].sum())
+            b.append_block(blk, key="UP")
+        sizes = [os.path.getsize(os.path.join(root, "B", "0", f))
+                 for f in os.listdir(os.path.join(root, "B", "0")) if f.endswith(".log")]
+        assert max(sizes) > 4 << 20
+        ra, rb = _read_all(a), _read_all(b)
+        assert len(ra) == len(rb) > m
+        assert [(x[2], x[3]) for x in ra] == [(x[2], x[3]) for x in rb]
+        assert any('"U\\"q"' in x[3] for x in rb) and any("\\u00fc" in x[3] for x in rb)
+        a.close()
+        b.close()
+    blk = sb.deferred(0, m, xr, yr, vx, vy, True)
+    assert list(blk)[:3] == list(sb.assemble(0, m, xr, yr, vx, vy, True))[:3]
+    stale = sb.deferred(0, m, xr, yr, vx, vy, True)
+    sb.parse(tl, xm, ym)
+    with pytest.raises(RuntimeError):
+        stale.materialize()
