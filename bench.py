@@ -219,6 +219,9 @@ def main(argv=None) -> int:
     sync()
     dist.barrier(ctx)
     sync()
+    if os.environ.get("ORYX_BENCH_TIMED_MARK"):
+        # (scripts/speed_under_load.py: another process waits for the timed loop to start)
+        open(os.environ["ORYX_BENCH_TIMED_MARK"], "w").close()
     t0 = time.perf_counter()
     trainer.iterate(args.steps)
     sync()

@@ -194,6 +194,9 @@ def main(argv=None) -> int:
         layer.run_interval(now)
         t_gen = time.perf_counter() - t0
         sharded_path = layer._sharded()
+        # the first generation's phases (phase_seconds accumulates over generations)
+        first_phases = dict(getattr(layer._update, "phase_seconds", {}))
+        first_lay = dict(layer.last_phases)
         later = []
         for g in range(1, max(1, args.generations) if ctx.world_size == 1 else 1):
             before = dict(layer._update.phase_seconds)
@@ -207,6 +210,7 @@ def main(argv=None) -> int:
             later.append({"generation": g + 1, "generation_s": dt,
                           "ratings": args.ratings + g * args.next_ratings,
                           "phase_s": {k: after[k] - before.get(k, 0.0) for k in after},
+                          "layer_phase_s": dict(layer.last_phases),
                           "history": dict(hist.stats) if hist is not None else None})
         layer.close()
     else:
@@ -215,13 +219,14 @@ def main(argv=None) -> int:
         layer.run_follower()
         t_gen = time.perf_counter() - t0
         sharded_path = layer._sharded()
-    upd = layer._update
-    phases = dict(getattr(upd, "phase_seconds", {}))
+        first_phases = dict(getattr(layer._update, "phase_seconds", {}))
+        first_lay = dict(layer.last_phases)
+    phases = first_phases
     if not ctx.is_main:
         later = []
-    phases.update({"layer_" + k: v for k, v in layer.last_phases.items()})
+    phases.update({"layer_" + k: v for k, v in first_lay.items()})
     # the layer's own phases plus the update's (whose sum is the layer's "update" phase)
-    lay = layer.last_phases
+    lay = first_lay
     inner = sum(v for k, v in phases.items()
                 if not k.startswith("layer_") and k not in ("publish_y", "publish_x"))
     attributed = inner + sum(v for k, v in lay.items() if k != "update")

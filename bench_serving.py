@@ -61,7 +61,15 @@ print(json.dumps({"n": n, "wall": time.perf_counter() - t0, "lat": lat, "errors"
 def make_data(items: int, users: int, features: int, seed: int):
     """Item / user factor matrices, ids and Poisson(20) known items (LoadTestALSModelFactory)."""
     rng = np.random.default_rng(seed)
-    Y = rng.standard_normal((items, features), dtype=np.float32)
+    # generated in chunks with a progress line each (20M x 250 takes minutes: a silent run
+    # that long looks hung to a supervisor)
+    Y = np.empty((items, features), dtype=np.float32)
+    step = 1 << 21
+    for lo in range(0, items, step):
+        Y[lo:lo + step] = rng.standard_normal((min(step, items - lo), features),
+                                              dtype=np.float32)
+        print("make_data: %d / %d item rows" % (min(items, lo + step), items), file=sys.stderr,
+              flush=True)
     X = rng.standard_normal((users, features), dtype=np.float32)
     item_ids = ["I%d" % i for i in range(items)]
     user_ids = ["U%d" % i for i in range(users)]
@@ -88,10 +96,14 @@ def build_model(data, features: int, sample_rate: float, max_batch: int = 16,
         model.Y.set_vectors(item_ids[lo:lo + chunk], Y[lo:lo + chunk])
     for lo in range(0, len(user_ids), chunk):
         model.X.set_vectors(user_ids[lo:lo + chunk], X[lo:lo + chunk])
+    print("build_model: factors loaded", file=sys.stderr, flush=True)
     pos = 0
     for u, c in enumerate(counts.tolist()):
         model.add_known_items(user_ids[u], [item_ids[i] for i in known[pos:pos + c].tolist()])
         pos += c
+        if u % 100000 == 0:
+            print("build_model: known items %d / %d users" % (u, len(counts)), file=sys.stderr,
+                  flush=True)
     model.Y.device_view()          # push the matrix to HBM before timing
     if model.index is not None:
         model.index.refresh()      # and build the bucket-sorted scan index

@@ -28,7 +28,7 @@ from typing import Iterable, Iterator, List, Optional, Set
 import numpy as np
 import torch
 
-from ... import ingest
+from ... import ingest, native
 from ...api import Dataset, KeyMessage, SpeedModel, SpeedModelManager
 from ...ops import als as als_ops, textfmt
 from ...utils import mathx, pmml as pmmlu, text
@@ -163,6 +163,23 @@ class ALSSpeedModel(SpeedModel):
     def _device_inverses_start(self):
         if self.X.size() == 0 or self.Y.size() == 0:
             return None, None
+        if self.features <= 128 and native.kernels_available():
+            # both Gramians (fp32 MFMA) and both certified inverses in one more launch
+            # (csrc/kernels/spdinv.hip)
+            grams = [als_ops.gramian(store.device_view()[0]).contiguous()
+                     for store in (self.X, self.Y)]
+            k = self.features
+            invs = [torch.empty((k, k), dtype=torch.float64, device=self.device)
+                    for _ in range(2)]
+            ok = torch.empty(2, dtype=torch.int32, device=self.device)
+            rc = native.kernels().oryx_spd_inverse_pair(
+                grams[0].data_ptr(), grams[1].data_ptr(), k, invs[0].data_ptr(),
+                invs[1].data_ptr(), float(mathx.SINGULARITY_THRESHOLD_RATIO), ok.data_ptr(),
+                native.stream_ptr(self.device))
+            native.check(rc, "oryx_spd_inverse_pair")
+            ev = torch.cuda.Event()
+            ev.record()
+            return (invs, ok, grams), ev
         invs, oks = [], []
         for store in (self.X, self.Y):
             mat, _, _ = store.device_view()
@@ -180,8 +197,8 @@ class ALSSpeedModel(SpeedModel):
         if work is None:
             return None
         torch.cuda.current_stream().wait_event(ev)
-        invs, ok = work
-        if not bool(ok.item()):
+        invs, ok = work[0], work[1]
+        if not bool(ok.cpu().min() if ok.dtype == torch.int32 else ok.item()):
             return None
         return invs[0], invs[1]
 
@@ -406,10 +423,10 @@ class ALSSpeedModelManager(SpeedModelManager):
             yr = torch.from_numpy(np.ascontiguousarray(i, dtype=np.int64)).to(dev)
             # the reference folds in strength.floatValue() (ALSSpeedModelManager.java:170)
             vals = torch.from_numpy(np.asarray(s, dtype=np.float32)).to(dev)
-            new_x = torch.empty((n, k), dtype=torch.float32, device=dev)
-            new_y = torch.empty((n, k), dtype=torch.float32, device=dev)
-            vx = torch.empty(n, dtype=torch.uint8, device=dev)
-            vy = torch.empty(n, dtype=torch.uint8, device=dev)
+            # both sides' rows in one matrix (formatted in one pass), flags likewise
+            new = torch.empty((2 * n, k), dtype=torch.float32, device=dev)
+            flags = torch.empty(2 * n, dtype=torch.uint8, device=dev)
+            new_x, new_y, vx, vy = new[:n], new[n:], flags[:n], flags[n:]
             rc = lib.oryx_als_foldin(xm.contiguous().data_ptr(), ym.contiguous().data_ptr(), k,
                                      xr.data_ptr(), yr.data_ptr(), vals.data_ptr(),
                                      xinv.contiguous().data_ptr(), yinv.contiguous().data_ptr(),
@@ -417,13 +434,15 @@ class ALSSpeedModelManager(SpeedModelManager):
                                      new_y.data_ptr(), vx.data_ptr(), vy.data_ptr(),
                                      native.stream_ptr(dev))
             native.check(rc, "oryx_als_foldin")
-            valid = torch.cat([vx, vy]).cpu().numpy()
             ph["foldin"] = (time.perf_counter() - t0) * 1e3
             t0 = time.perf_counter()
             # the updated rows become JSON text on the device (csrc/kernels/textfmt.hip);
-            # only the text crosses to the host
-            xrows = textfmt.format_rows(new_x)
-            yrows = textfmt.format_rows(new_y)
+            # only the text crosses to the host, after the row ends and the validity flags
+            # (two host round trips for the whole fold-in)
+            rows, valid = textfmt.format_rows_and(new, flags)
+        xend = int(rows.ends[n - 1])
+        xrows = textfmt.RowText(rows.blob[:xend], rows.ends[:n])
+        yrows = textfmt.RowText(rows.blob[xend:], rows.ends[n:] - xend)
         ph["format_rows"] = (time.perf_counter() - t0) * 1e3
         ph["assemble"] = 0.0
         vxh, vyh = valid[:n] > 0, valid[n:] > 0

@@ -93,6 +93,43 @@ def _format_device(mat: torch.Tensor) -> RowText:
     return RowText(host.numpy(), ends.cpu().numpy())
 
 
+_TEXT_WS = {}
+
+
+def format_rows_and(mat: torch.Tensor, extra: torch.Tensor):
+    """:func:`format_rows` of a device fp32 matrix with two host round trips in all: the
+    text goes to a cached device buffer sized by the longest possible row (a float is at
+    most 18 characters), and the row ends come back together with ``extra`` (a small device
+    tensor, e.g. validity flags, returned as an int64 numpy array) before the one copy of the
+    text.  Returns (RowText, extra on the host)."""
+    m = mat.detach()
+    if m.dtype != torch.float32 or m.dim() != 2 or m.stride(1) != 1 or m.device.type != "cuda":
+        raise ValueError("need a row-contiguous 2-D float32 device matrix")
+    n, k = m.shape
+    if n == 0:
+        return RowText(b"", np.zeros(0, dtype=np.int64)), extra.cpu().numpy().astype(np.int64)
+    lib = native.require_kernels()
+    dev = m.device
+    stream = native.stream_ptr(dev)
+    lens = torch.empty(n, dtype=torch.int32, device=dev)
+    native.check(lib.oryx_format_rows_len(m.data_ptr(), n, k, m.stride(0), lens.data_ptr(),
+                                          stream), "oryx_format_rows_len")
+    ends = torch.cumsum(lens, 0, dtype=torch.int64)
+    bound = n * (19 * k + 2)
+    ws = _TEXT_WS.get(dev)
+    if ws is None or ws.numel() < bound:
+        ws = torch.empty(bound, dtype=torch.uint8, device=dev)
+        _TEXT_WS[dev] = ws
+    native.check(lib.oryx_format_rows_text(m.data_ptr(), n, k, m.stride(0), ends.data_ptr(),
+                                           lens.data_ptr(), ws.data_ptr(), stream),
+                 "oryx_format_rows_text")
+    small = torch.cat([ends, extra.reshape(-1).to(torch.int64)]).cpu().numpy()
+    total = int(small[n - 1])
+    host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    host.copy_(ws[:total])
+    return RowText(host.numpy(), small[:n]), small[n:]
+
+
 def format_csv(mat: torch.Tensor, pinned: bool = True) -> RowText:
     """CSV lines ``v0,v1,...\n`` of every row of a device float32 matrix (shortest round-trip
     float32 text, as :func:`format_rows`), formatted on the GPU; ``ends[r]`` is the end of row

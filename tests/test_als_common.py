@@ -310,3 +310,44 @@ def test_item_filter_rescorer_forms_agree_cpu():
     p = ItemFilterRescorerProvider()
     assert p.get_recommend_rescorer(["U1"], []) is None
     assert p.get_recommend_rescorer(["U1"], ["exclude:I2", "factor:3"]).is_filtered("I2")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [50, 64, 128])
+def test_spd_inverse_pair_kernel(cuda, k):
+    """oryx_spd_inverse_pair (csrc/kernels/spdinv.hip): fp64 Gauss-Jordan inverses of two
+    fp32 Gramians against torch.linalg.inv of the same matrices in fp64 (fp32-reference
+    style: the same op in plain PyTorch); an indefinite matrix and a near-singular one are
+    not certified (ok = 0)."""
+    from oryx_amd import native
+    g = torch.Generator().manual_seed(k)
+    A = torch.randn(4 * k, k, generator=g)
+    B = torch.randn(3 * k, k, generator=g)
+    lib = native.require_kernels()
+
+    def run(G0, G1):
+        G0 = G0.to(cuda, torch.float32).contiguous()
+        G1 = G1.to(cuda, torch.float32).contiguous()
+        I0 = torch.empty((k, k), dtype=torch.float64, device=cuda)
+        I1 = torch.empty_like(I0)
+        ok = torch.zeros(2, dtype=torch.int32, device=cuda)
+        rc = lib.oryx_spd_inverse_pair(G0.data_ptr(), G1.data_ptr(), k, I0.data_ptr(),
+                                       I1.data_ptr(), float(mathx.SINGULARITY_THRESHOLD_RATIO),
+                                       ok.data_ptr(), native.stream_ptr(torch.device(cuda)))
+        assert rc == 0
+        torch.cuda.synchronize()
+        return I0.cpu(), I1.cpu(), ok.cpu().tolist()
+
+    G0, G1 = A.T @ A, B.T @ B
+    I0, I1, ok = run(G0, G1)
+    assert ok == [1, 1]
+    for inv, G in ((I0, G0), (I1, G1)):
+        ref = torch.linalg.inv(G.double())
+        torch.testing.assert_close(inv, ref, rtol=1e-9, atol=1e-12)
+    indefinite = G0.clone()
+    indefinite[3, 3] = -1.0
+    near = B.T @ B
+    near[:, 1] = near[:, 0]
+    near[1, :] = near[0, :]                 # rank deficient
+    _, _, ok = run(indefinite, near)
+    assert ok == [0, 0]
