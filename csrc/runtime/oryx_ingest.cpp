@@ -981,6 +981,27 @@ void oryx_rowmap_remove(void* h, const char* blob, const long long* ends, long l
 }
 
 // out[c] = row of dictionary key c (-1 when absent) for every code of the dictionary.
+// The numeric suffix (trailing decimal digits, at most 18) of every live key, written at its
+// row of out [n_rows] (rows without a key or without digits: -1).  For rescorers that select
+// items by ID pattern: one pass over the map instead of a Python loop over every ID.
+long long oryx_rowmap_key_suffixes(void* h, long long* out, long long n_rows) {
+  const RowMap* m = static_cast<const RowMap*>(h);
+  for (long long r = 0; r < n_rows; ++r) out[r] = -1;
+  long long hit = 0;
+  for (const auto& sl : m->slots) {
+    if (sl.state != 0 || sl.row < 0 || sl.row >= n_rows) continue;
+    const char* k = m->key_of(sl);
+    size_t e = sl.len, b = e;
+    while (b > 0 && e - b < 18 && (unsigned)(k[b - 1] - '0') < 10u) --b;
+    if (b == e) continue;
+    long long v = 0;
+    for (size_t q = b; q < e; ++q) v = v * 10 + (k[q] - '0');
+    out[sl.row] = v;
+    ++hit;
+  }
+  return hit;
+}
+
 long long oryx_rowmap_translate(void* h, void* dh, long long* out) {
   const RowMap* m = static_cast<RowMap*>(h);
   Dict* d = static_cast<Dict*>(dh);

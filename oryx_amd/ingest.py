@@ -302,6 +302,15 @@ class RowMap:
         self._lib.oryx_rowmap_remove(self._h, blob, ends.ctypes.data_as(ctypes.c_void_p),
                                      len(ids))
 
+    def key_suffixes(self, n_rows: int) -> np.ndarray:
+        """int64 [n_rows]: the trailing decimal digits of the key at each row (-1: no key
+        there, or no digits), in one native pass over the map."""
+        out = np.empty(max(int(n_rows), 0), dtype=np.int64)
+        if len(out):
+            self._lib.oryx_rowmap_key_suffixes(self._h, out.ctypes.data_as(ctypes.c_void_p),
+                                               len(out))
+        return out
+
     def translate(self, d: "IdDict") -> np.ndarray:
         """Row of every key of ``d`` in code order (-1: not in the map)."""
         out = np.empty(len(d), dtype=np.int64)

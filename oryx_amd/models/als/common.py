@@ -83,6 +83,9 @@ class FeatureVectors:
         self.partitioner = partitioner        # rows -> partition ids (device LSH)
         self._dev_part = None
         self.version = 0
+        # bumped only when the ID <-> row assignment changes (IDs added or removed), not by
+        # value updates: caches keyed by ID (id_array, rescorer row masks) survive the latter
+        self.id_version = 0
         # rows changed since the last take_index_dirty() (serving ItemIndex); None = all
         # rows changed since each index consumer's last take_index_state (token -> rows; None:
         # everything may have changed).  One set per consumer: two indexes over one store
@@ -144,6 +147,7 @@ class FeatureVectors:
                 self._index[id_] = row
                 self._ids[row] = id_
                 self._recent.add(id_)
+                self.id_version += 1
                 if self._journal is not None:
                     self._journal.append((True, id_, row))
             self._host[row] = v
@@ -234,6 +238,7 @@ class FeatureVectors:
                             index[id_] = row
                             self._ids[row] = id_
                             self._recent.add(id_)
+                            self.id_version += 1
                             if self._journal is not None:
                                 self._journal.append((True, id_, row))
                         self._host[row] = v
@@ -248,6 +253,7 @@ class FeatureVectors:
                     self._journal.append((True, new_ids, new_rows))
                 self._ids.extend(new_ids)
                 self._recent.update(new_ids)
+                self.id_version += 1
                 self._n_rows = start + len(new_ids)
                 rows[new_pos] = new_rows
             self._host[rows] = matrix
@@ -273,6 +279,7 @@ class FeatureVectors:
             self._host[row] = 0.0
             self._host_valid[row] = False
             self._ids[row] = None
+            self.id_version += 1
             self._free.append(row)
             self._dirty.add(row)
             self._idx_mark((row,))
@@ -440,14 +447,21 @@ class FeatureVectors:
         version: candidate IDs are then one fancy index (``id_array()[rows]``), not a Python
         list built per request."""
         c = getattr(self, "_id_arr", None)
-        if c is not None and c[0] == self.version:
+        if c is not None and c[0] == self.id_version:
             return c[1]
         with self._lock.read():
             arr = np.empty(len(self._ids), dtype=object)
             arr[:] = self._ids
-            ver = self.version
+            ver = self.id_version
         self._id_arr = (ver, arr)
         return arr
+
+    def key_suffixes(self) -> np.ndarray:
+        """int64 per row: the numeric suffix of the row's ID (-1: free row or no digits),
+        from the native id -> row mirror (``ingest.RowMap.key_suffixes``)."""
+        rm = self.synced_rowmap()
+        with self._lock.read():
+            return rm.key_suffixes(self._n_rows)
 
     def row_mask(self, ids, device=None):
         """Bool tensor over the store's rows: True at the rows of ``ids`` (on ``device``)."""

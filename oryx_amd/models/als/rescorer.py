@@ -17,7 +17,9 @@ vectorised versions (numpy over the arrays) makes rescored requests as fast as p
 from __future__ import annotations
 
 import abc
+import collections
 import math
+import threading
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -173,7 +175,7 @@ class ItemFilterRescorer(Rescorer):
 
     def rescore_device(self, rows, scores, store):
         import torch
-        key = (id(store), store.version)
+        key = (id(store), store.id_version)
         if self._mask is None or self._mask[0] != key[0] or self._mask[1] != key[1]:
             self._mask = key + (store.row_mask(self.excluded, rows.device),)
         m = self._mask[2]
@@ -188,8 +190,28 @@ class ItemFilterRescorerProvider(AbstractRescorerProvider):
     /similarity; ``ORYX_EXAMPLE_RESCORER_EXCLUDE_MOD`` (bench_serving.py) additionally drops
     every item whose numeric ID suffix is divisible by the given modulus."""
 
+    def __init__(self):
+        # rescorers by request arguments, reused across requests so that their device row
+        # masks are built once per store ID layout, not per request
+        self._cache: "collections.OrderedDict" = collections.OrderedDict()
+        self._cache_lock = threading.Lock()
+
+    def _parse(self, args) -> Optional[Rescorer]:
+        import os
+        key = (tuple(args or ()), os.environ.get("ORYX_EXAMPLE_RESCORER_EXCLUDE_MOD"))
+        with self._cache_lock:
+            if key in self._cache:
+                self._cache.move_to_end(key)
+                return self._cache[key]
+        r = self._build(args)
+        with self._cache_lock:
+            self._cache[key] = r
+            while len(self._cache) > 64:
+                self._cache.popitem(last=False)
+        return r
+
     @staticmethod
-    def _parse(args) -> Optional[Rescorer]:
+    def _build(args) -> Optional[Rescorer]:
         import os
         excl, factor = [], 1.0
         for a in args or []:
@@ -221,7 +243,7 @@ class _ModExcludeRescorer(ItemFilterRescorer):
     def _dropped(self, id_) -> bool:
         if id_ in self.excluded:
             return True
-        digits = id_[len(id_.rstrip("0123456789")):]
+        digits = id_[len(id_.rstrip("0123456789")):][-18:]    # as RowMap.key_suffixes
         return bool(digits) and int(digits) % self.mod == 0
 
     def rescore(self, id_, value):
@@ -235,11 +257,13 @@ class _ModExcludeRescorer(ItemFilterRescorer):
 
     def rescore_device(self, rows, scores, store):
         import torch
-        key = (id(store), store.version)
+        key = (id(store), store.id_version)
         if self._mask is None or self._mask[0] != key[0] or self._mask[1] != key[1]:
-            ids = store.id_array()
-            drop = np.fromiter((i is not None and self._dropped(i) for i in ids), dtype=bool,
-                               count=len(ids))
+            # every row's numeric ID suffix in one native pass over the store's id map
+            suf = store.key_suffixes()
+            drop = (suf >= 0) & (suf % self.mod == 0)
+            if self.excluded:
+                drop[store.host_rows(self.excluded)] = True
             self._mask = key + (torch.from_numpy(drop).to(rows.device),)
         m = self._mask[2]
         hit = m[rows.clamp(max=max(m.numel() - 1, 0))] & (rows < m.numel())

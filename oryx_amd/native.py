@@ -128,6 +128,7 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_speed_new_keys", c_ll, [c_vp, c_i, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_speed_assemble", c_ll, [c_vp, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_vp, c_i, c_vp, c_ll, c_vp, c_vp])
+    _sig(lib, "oryx_rowmap_key_suffixes", c_ll, [c_vp, c_vp, c_ll])
     _sig(lib, "oryx_speed_append", c_ll, [c_vp, c_vp, c_i, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,
                                           c_vp, c_vp, c_i, c_ll, c_i, c_vp])
     _sig(lib, "oryx_split_by_time", c_ll, [c_vp, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,

@@ -310,6 +310,40 @@ def test_item_filter_rescorer_forms_agree_cpu():
     p = ItemFilterRescorerProvider()
     assert p.get_recommend_rescorer(["U1"], []) is None
     assert p.get_recommend_rescorer(["U1"], ["exclude:I2", "factor:3"]).is_filtered("I2")
+    # the provider reuses one rescorer per argument list (its device mask survives requests)
+    assert p.get_recommend_rescorer(["U2"], ["exclude:I2", "factor:3"]) is \
+        p.get_recommend_rescorer(["U1"], ["exclude:I2", "factor:3"])
+
+
+def test_mod_exclude_rescorer_native_suffixes_cpu(monkeypatch):
+    """The benchmark's example rescorer (drop IDs whose numeric suffix is divisible by N):
+    its device mask comes from the store's native ID map (key_suffixes) and agrees with the
+    per-item form, also after rows are removed and reused; value updates keep the mask."""
+    import torch
+    from oryx_amd.models.als.common import FeatureVectors
+    from oryx_amd.models.als.rescorer import ItemFilterRescorerProvider
+    monkeypatch.setenv("ORYX_EXAMPLE_RESCORER_EXCLUDE_MOD", "7")
+    store = FeatureVectors(2)
+    ids = ["I%d" % j for j in range(50)] + ["x", "item-0042", "a12b"]
+    store.set_vectors(ids, np.ones((len(ids), 2), dtype=np.float32))
+    store.remove_vector("I14")
+    store.set_vector("Z21", np.ones(2, dtype=np.float32))        # reuses row 14
+    suf = store.key_suffixes()
+    arr = store.id_array()
+    for row, i in enumerate(arr):
+        want = -1 if i is None or not i[-1].isdigit() else \
+            int(i[len(i.rstrip("0123456789")):])
+        assert suf[row] == want, (row, i)
+    r = ItemFilterRescorerProvider().get_recommend_rescorer(["U1"], ["factor:2", "exclude:I3"])
+    rows = torch.arange(len(arr))
+    scores = torch.ones(len(arr))
+    dev = r.rescore_device(rows, scores, store).numpy()
+    per = np.array([r.rescore(i, 1.0) if i is not None else np.nan for i in arr])
+    np.testing.assert_allclose(dev, per, equal_nan=True)
+    assert np.isnan(dev[arr.tolist().index("Z21")]) and np.isnan(dev[3])
+    v_ids = store.id_version
+    store.set_vector("I1", np.zeros(2, dtype=np.float32))
+    assert store.id_version == v_ids and r._mask[1] == v_ids
 
 
 @pytest.mark.gpu
