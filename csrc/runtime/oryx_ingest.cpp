@@ -625,6 +625,47 @@ std::vector<const char*> line_chunks(const char* buf, long long len, int P) {
   return cut;
 }
 
+// Calls fn(begin, end) for every non-empty line of [p, end) (end excludes the '\n' and a
+// trailing '\r'), as RatingChunk::parse delimits them.
+template <class Fn>
+void for_each_line(const char* p, const char* end, Fn&& fn) {
+  while (p < end) {
+    const char* nl = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
+    const char* le = nl ? nl : end;
+    const char* lend = le;
+    if (lend > p && lend[-1] == '\r') --lend;
+    if (lend > p) fn(p, lend);
+    p = nl ? nl + 1 : end;
+  }
+}
+
+// The timestamp of one rating line as parse_ratings reads it (default_ts when absent); false
+// for a line parse_ratings would drop.
+struct LineScratch {
+  std::vector<std::string> toks;
+  std::string field;
+};
+
+inline bool line_ts(const char* b, const char* e, long long default_ts, long long* ts,
+                    LineScratch& sc) {
+  std::vector<std::string>& toks = sc.toks;
+  std::string& field = sc.field;
+  std::string_view f[4];
+  bool stable;
+  double sv;
+  *ts = default_ts;
+  return parse_rating_fields(b, e, toks, field, f, &stable, &sv, ts);
+}
+
+template <class Fn>
+void for_each_line_ts(const char* p, const char* end, long long default_ts, Fn&& fn) {
+  LineScratch sc;
+  for_each_line(p, end, [&](const char* b, const char* e) {
+    long long v;
+    if (line_ts(b, e, default_ts, &v, sc)) fn(b, e, v);
+  });
+}
+
 int split_threads(long long len) {
   if (len < (1ll << 20)) return 1;
   return (int)std::max<long long>(1, std::min<long long>(len / (256ll << 10),
@@ -645,14 +686,16 @@ long long oryx_ts_range(const char* buf, long long len, long long default_ts,
       mx((size_t)P, std::numeric_limits<long long>::min()), cnt((size_t)P, 0);
   oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
     for (long long t = lo; t < hi; ++t) {
-      RatingChunk c;
-      c.no_ids = true;
-      c.parse(cut[(size_t)t], cut[(size_t)t + 1], default_ts, false);
-      for (long long v : c.ts) {
-        mn[(size_t)t] = std::min(mn[(size_t)t], v);
-        mx[(size_t)t] = std::max(mx[(size_t)t], v);
-      }
-      cnt[(size_t)t] = (long long)c.ts.size();
+      long long a = std::numeric_limits<long long>::max(), b = std::numeric_limits<long long>::min(), c = 0;
+      for_each_line_ts(cut[(size_t)t], cut[(size_t)t + 1], default_ts,
+                       [&](const char*, const char*, long long v) {
+                         a = std::min(a, v);
+                         b = std::max(b, v);
+                         ++c;
+                       });
+      mn[(size_t)t] = a;
+      mx[(size_t)t] = b;
+      cnt[(size_t)t] = c;
     }
   });
   long long n = 0, a = std::numeric_limits<long long>::max(), b = std::numeric_limits<long long>::min();
@@ -674,43 +717,64 @@ long long oryx_ts_range(const char* buf, long long len, long long default_ts,
 long long oryx_split_by_time(const char* buf, long long len, long long default_ts,
                              long long boundary, char* out_lo, char* out_hi, long long* n_lo,
                              long long* n_hi, long long* b_lo, long long* b_hi) {
+  const auto T0 = std::chrono::steady_clock::now();
   const int P = split_threads(len);
   std::vector<const char*> cut = line_chunks(buf, len, P);
-  std::vector<RatingChunk> ch((size_t)P);
+  // pass 1: each parsable line's side (1 byte per line) and the bytes per side per chunk
+  // (raw arrays sized for the most lines a chunk can hold: a vector's push_back per line
+  // cost 3x the parse -- its end pointer cannot stay in a register across byte stores)
+  std::vector<std::unique_ptr<uint8_t[]>> side((size_t)P);
   std::vector<long long> blo((size_t)P, 0), bhi((size_t)P, 0), nlo((size_t)P, 0),
       nhi((size_t)P, 0);
   oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
     for (long long t = lo; t < hi; ++t) {
-      RatingChunk& c = ch[(size_t)t];
-      c.no_ids = true;
-      c.want_spans = true;
-      c.parse(cut[(size_t)t], cut[(size_t)t + 1], default_ts, false);
-      for (size_t r = 0; r < c.ts.size(); ++r) {
-        const long long l = (long long)(c.sp_e[r] - c.sp_b[r]) + 1;
-        if (c.ts[r] < boundary) { blo[(size_t)t] += l; ++nlo[(size_t)t]; }
-        else { bhi[(size_t)t] += l; ++nhi[(size_t)t]; }
-      }
+      side[(size_t)t].reset(new uint8_t[(size_t)((cut[(size_t)t + 1] - cut[(size_t)t]) / 2 + 2)]);
+      uint8_t* sd = side[(size_t)t].get();
+      size_t r = 0;
+      long long bl = 0, bh = 0, cl = 0, chh = 0;
+      LineScratch sc;
+      for_each_line(cut[(size_t)t], cut[(size_t)t + 1], [&](const char* b, const char* e) {
+        long long v;
+        const bool ok = line_ts(b, e, default_ts, &v, sc);
+        const long long l = (long long)(e - b) + 1;
+        const bool low = v < boundary;
+        bl += ok && low ? l : 0;
+        cl += ok && low;
+        bh += ok && !low ? l : 0;
+        chh += ok && !low;
+        sd[r++] = ok ? (uint8_t)!low : (uint8_t)2;
+      });
+      blo[(size_t)t] = bl; bhi[(size_t)t] = bh; nlo[(size_t)t] = cl; nhi[(size_t)t] = chh;
     }
   });
+  const auto T1 = std::chrono::steady_clock::now();
   std::vector<long long> olo((size_t)P + 1, 0), ohi((size_t)P + 1, 0);
   for (int t = 0; t < P; ++t) {
     olo[(size_t)t + 1] = olo[(size_t)t] + blo[(size_t)t];
     ohi[(size_t)t + 1] = ohi[(size_t)t] + bhi[(size_t)t];
   }
+  // pass 2: copy runs of consecutive same-side lines
   oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
     for (long long t = lo; t < hi; ++t) {
-      const RatingChunk& c = ch[(size_t)t];
+      const uint8_t* sd = side[(size_t)t].get();
       char* wl = out_lo + olo[(size_t)t];
       char* wh = out_hi + ohi[(size_t)t];
-      for (size_t r = 0; r < c.ts.size(); ++r) {
-        const size_t l = (size_t)(c.sp_e[r] - c.sp_b[r]);
-        char*& w = c.ts[r] < boundary ? wl : wh;
-        memcpy(w, c.sp_b[r], l);
+      size_t r = 0;
+      for_each_line(cut[(size_t)t], cut[(size_t)t + 1], [&](const char* b, const char* e) {
+        const uint8_t k = sd[r++];
+        if (k == 2) return;
+        char*& w = k == 0 ? wl : wh;
+        const size_t l = (size_t)(e - b);
+        memcpy(w, b, l);
         w[l] = '\n';
         w += l + 1;
-      }
+      });
     }
   });
+  if (std::getenv("ORYX_LOG_DEBUG"))
+    fprintf(stderr, "split P=%d pass1 %.3f ms pass2 %.3f ms\n", P,
+            std::chrono::duration<double, std::milli>(T1 - T0).count(),
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T1).count());
   long long a = 0, b = 0;
   for (int t = 0; t < P; ++t) { a += nlo[(size_t)t]; b += nhi[(size_t)t]; }
   *n_lo = a;
