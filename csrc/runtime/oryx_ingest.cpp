@@ -498,6 +498,13 @@ struct RatingChunk {
   // the raw text span [begin, end) of every parsed row's line (the time split copies lines)
   bool want_spans = false;
   std::vector<const char*> sp_b, sp_e;
+  // direct output (oryx_parse_ratings' multi-chunk path): rows go straight to these arrays
+  // (room for every line of the chunk) instead of the vectors above -- no intermediate copy
+  long long* d_u = nullptr;
+  long long* d_i = nullptr;
+  double* d_s = nullptr;
+  long long* d_ts = nullptr;
+  long long d_n = 0;
 
   int32_t code(Side& sd, std::string_view k, bool stable) {
     uint32_t v;
@@ -542,7 +549,13 @@ struct RatingChunk {
         double sv;
         long long tv = default_ts;
         const bool ok = parse_rating_fields(p, lend, toks, field, f, &stable, &sv, &tv);
-        if (ok) {
+        if (ok && d_u) {
+          d_u[d_n] = code(us, f[0], stable);
+          d_i[d_n] = code(is, f[1], stable);
+          d_s[d_n] = sv;
+          d_ts[d_n] = tv;
+          ++d_n;
+        } else if (ok) {
           if (no_ids) {
             u.push_back(0);
             i.push_back(0);
@@ -569,6 +582,73 @@ struct RatingChunk {
     }
   }
 };
+
+// oryx_parse_ratings' multi-chunk parse writing rows in place: chunk t parses into the
+// outputs from index lines_at[t] (its first line), the chunk dictionaries are merged in
+// order, then the rows' chunk-local codes become global ones -- in parallel when no line was
+// dropped (rows then sit exactly where they belong), else in chunk order, moving each chunk's
+// rows down to close the gaps (destinations never pass the rows still to be read).
+long long parse_direct(Dict* du, Dict* di, std::vector<RatingChunk>& ch,
+                       const std::vector<const char*>& cut, const std::vector<long long>& lines_at,
+                       long long* out_u, long long* out_i, double* out_s, long long* out_ts,
+                       long long default_ts, int strict) {
+  const int P = (int)ch.size();
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      RatingChunk& c = ch[(size_t)t];
+      const long long o = lines_at[(size_t)t];
+      c.d_u = out_u + o;
+      c.d_i = out_i + o;
+      c.d_s = out_s + o;
+      c.d_ts = out_ts + o;
+      c.parse(cut[(size_t)t], cut[(size_t)t + 1], default_ts, strict != 0);
+    }
+  });
+  long long lines_before = 0;
+  for (int t = 0; t < P; ++t) {
+    if (ch[(size_t)t].bad_line >= 0) return -(lines_before + ch[(size_t)t].bad_line + 1);
+    lines_before += ch[(size_t)t].lines;
+  }
+  std::vector<std::vector<int64_t>> umap((size_t)P), imap((size_t)P);
+  std::vector<long long> off((size_t)P + 1, 0);
+  bool dense = true;
+  auto merge = [](Dict* d, const RatingChunk::Side& sd, std::vector<int64_t>& to_global) {
+    to_global.reserve(sd.keys.size());
+    for (int64_t e : sd.order) {
+      if (e < 0) d->encode_num((uint32_t)(-e - 1));
+      else to_global.push_back(d->encode(sd.keys[(size_t)e]));
+    }
+  };
+  for (int t = 0; t < P; ++t) {
+    RatingChunk& c = ch[(size_t)t];
+    merge(du, c.us, umap[(size_t)t]);
+    merge(di, c.is, imap[(size_t)t]);
+    off[(size_t)t + 1] = off[(size_t)t] + c.d_n;
+    dense = dense && off[(size_t)t] == lines_at[(size_t)t];
+  }
+  const int32_t* unum = du->num.data();
+  const int32_t* inum = di->num.data();
+  auto remap = [&](long long t) {
+    const RatingChunk& c = ch[(size_t)t];
+    const long long src = lines_at[(size_t)t], dst = off[(size_t)t];
+    const int64_t* um = umap[(size_t)t].data();
+    const int64_t* im = imap[(size_t)t].data();
+    for (long long r = 0; r < c.d_n; ++r) {
+      const long long a = out_u[src + r], b = out_i[src + r];
+      out_u[dst + r] = a < 0 ? unum[-(a + 1)] : um[a];
+      out_i[dst + r] = b < 0 ? inum[-(b + 1)] : im[b];
+      out_s[dst + r] = out_s[src + r];
+      out_ts[dst + r] = out_ts[src + r];
+    }
+  };
+  if (dense)
+    oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+      for (long long t = lo; t < hi; ++t) remap(t);
+    });
+  else
+    for (int t = 0; t < P; ++t) remap(t);
+  return off[(size_t)P];
+}
 
 // Chunks at line boundaries over the native threads, no dictionaries (see oryx_parse_ratings).
 long long parse_rows_no_ids(const char* buf, long long len, long long* out_u, long long* out_i,
@@ -850,6 +930,20 @@ long long oryx_parse_ratings(const char* buf, long long len, void* users, void* 
     }
     return n;
   }
+  // lines per chunk (an upper bound on its rows): when the output holds them all, every
+  // chunk parses straight into the output at its first line's index
+  std::vector<long long> lines_at((size_t)P + 1, 0);
+  oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
+    for (long long t = lo; t < hi; ++t) {
+      const char* b = cut[(size_t)t];
+      const char* e = cut[(size_t)t + 1];
+      lines_at[(size_t)t + 1] = (long long)std::count(b, e, '\n') + (e > b && e[-1] != '\n');
+    }
+  });
+  for (int t = 0; t < P; ++t) lines_at[(size_t)t + 1] += lines_at[(size_t)t];
+  if (lines_at[(size_t)P] <= max_rows)
+    return parse_direct(du, di, ch, cut, lines_at, out_u, out_i, out_s, out_ts, default_ts,
+                        strict);
   oryx_ff::parallel_ranges(P, 1, [&](long long lo, long long hi, int) {
     for (long long t = lo; t < hi; ++t)
       ch[(size_t)t].parse(cut[(size_t)t], cut[(size_t)t + 1], default_ts, strict != 0);

@@ -57,3 +57,45 @@ def test_drain_save_read_round_trip(tmp_path):
     assert sorted(past.values()) == sorted(msgs + ["u9,i9,2"])
     cons.close()
     topic.close()
+
+
+def test_multichunk_parse_matches_single_chunk_with_dropped_lines():
+    """A buffer large enough for the threaded in-place parse (rows written at their line's
+    index, codes remapped, gaps from dropped / empty lines closed) gives the rows, codes and
+    dictionaries of the sequential single-chunk parse; strict mode reports the first bad
+    line's number."""
+    g = np.random.default_rng(4)
+    lines = []
+    for j in range(120000):
+        r = g.random()
+        u = ("u%d" % g.integers(0, 5000)) if r < 0.5 else str(g.integers(0, 5000))
+        it = str(g.integers(0, 3000)) if r < 0.7 else "i%d" % g.integers(0, 3000)
+        if r < 0.01:
+            lines.append("")                       # empty line: no row
+        elif r < 0.02:
+            lines.append("justone")                # unparsable: dropped
+        elif r < 0.03:
+            lines.append('"%s","%s",1.5,%d' % (u, it, j))
+        else:
+            lines.append("%s,%s,%.1f,%d" % (u, it, g.random() * 4, j))
+    big = TextLines.from_strings(lines)
+    assert len(memoryview(big.joined())) > (2 << 20)
+    d1, d2 = ingest.IdDict(), ingest.IdDict()
+    a = ingest.parse_ratings(big, d1, d2, default_ts=0)
+    e1, e2 = ingest.IdDict(), ingest.IdDict()
+    rows = [ingest.parse_ratings([ln], e1, e2, default_ts=0) for ln in lines if ln]
+    want = [np.concatenate([r[k] for r in rows]) for k in range(4)]
+    for x, y in zip(a, want):
+        np.testing.assert_array_equal(x, y)
+    assert d1.keys() == e1.keys() and d2.keys() == e2.keys()
+    clean = TextLines.from_strings([ln for ln in lines if ln and ln != "justone"])
+    c1, c2 = ingest.IdDict(), ingest.IdDict()
+    b = ingest.parse_ratings(clean, c1, c2, default_ts=0)
+    for x, y in zip(b, want):
+        np.testing.assert_array_equal(x, y)
+    bad_at = [j for j, ln in enumerate(lines) if ln == "justone"][0]
+    try:
+        ingest.parse_ratings(big, ingest.IdDict(), ingest.IdDict(), default_ts=0, strict=True)
+        raise AssertionError("strict parse accepted a bad line")
+    except ValueError as e:
+        assert "line %d" % bad_at in str(e)
