@@ -34,6 +34,8 @@ constexpr int WPB = 2;     // waves per block
 
 struct TopnParams {
   const float* Y;             // store rows, stride ld floats (ld >= kp, pad columns zero)
+  const __bf16* Yb;           // bf16 scan: the rows' bf16 mirror, stride ldb (>= kp, pad 0)
+  long long ldb;
   const int* perm;            // [n] position -> store row (null: identity)
   long long ld;
   const float* Q;             // [QB][kp] (rows >= nq zero)
@@ -115,9 +117,14 @@ __device__ __forceinline__ float compact(float* sc, int* rw, int* cnt, int q, in
   return c >= KL ? s[KL - 1] : -INFINITY;
 }
 
-template <int KP, int KL>
+// BF: scores from the bf16 mirror (queries rounded to bf16 too) on
+// v_mfma_f32_16x16x32_bf16 -- half the bytes of the fp32 scan; the caller re-ranks the
+// candidates exactly in fp32 and certifies the cut (ops/topn.py ItemIndex._launch_bf16).
+// KP % 32 == 0 there, no cosine.
+template <int KP, int KL, bool BF>
 __global__ __launch_bounds__(WPB * 64) void topn_scan(TopnParams p) {
   constexpr int S = KP / 16;
+  constexpr int SB = BF ? KP / 32 : 1;
   constexpr int CAP = 2 * KL;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -131,10 +138,19 @@ __global__ __launch_bounds__(WPB * 64) void topn_scan(TopnParams p) {
   const int q = lane & 15, kg = lane >> 4;
   // B operand (queries) for every 16-feature step, resident: component j of step s is
   // Q[q][16 s + 4 kg + j]
-  f32x4 qb[S];
+  f32x4 qb[BF ? 1 : S];
+  bf16x8 qb8[SB];
+  if constexpr (BF) {
+    // lane (q, kg) holds Q[q][32 s + 8 kg .. + 7] for every 32-feature step
 #pragma unroll
-  for (int s = 0; s < S; ++s)
-    qb[s] = *reinterpret_cast<const f32x4*>(p.Q + q * KP + 16 * s + 4 * kg);
+    for (int s = 0; s < SB; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) qb8[s][j] = (__bf16)p.Q[q * KP + 32 * s + 8 * kg + j];
+  } else {
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      qb[s] = *reinterpret_cast<const f32x4*>(p.Q + q * KP + 16 * s + 4 * kg);
+  }
   float theta = -INFINITY;   // this lane's query's admission threshold
   const unsigned* cbits = p.cand_bits ? p.cand_bits + (long long)(q < nq ? q : 0) * p.words
                                       : nullptr;
@@ -155,7 +171,8 @@ __global__ __launch_bounds__(WPB * 64) void topn_scan(TopnParams p) {
     r = lo;
   }
   // A: item position i0 + (lane & 15), features 16 s + 4 kg .. + 3
-  f32x4 a[S];
+  f32x4 a[BF ? 1 : S];
+  bf16x8 a8[SB];
   long long i0 = 0, rend = 0;
   auto load_tile = [&](long long t) {
     while (t >= p.tile0[r + 1]) ++r;
@@ -164,27 +181,39 @@ __global__ __launch_bounds__(WPB * 64) void topn_scan(TopnParams p) {
     i0 = rbeg + 16 * (t - p.tile0[r]);
     const long long ia = i0 + (lane & 15) < rend ? i0 + (lane & 15) : rend - 1;
     const long long row = p.perm ? (long long)p.perm[ia] : ia;
-    const float* yrow = p.Y + row * p.ld + 4 * kg;
+    if constexpr (BF) {
+      const __bf16* yrow = p.Yb + row * p.ldb + 8 * kg;
 #pragma unroll
-    for (int s = 0; s < S; ++s) a[s] = *reinterpret_cast<const f32x4*>(yrow + 16 * s);
+      for (int s = 0; s < SB; ++s) a8[s] = *reinterpret_cast<const bf16x8*>(yrow + 32 * s);
+    } else {
+      const float* yrow = p.Y + row * p.ld + 4 * kg;
+#pragma unroll
+      for (int s = 0; s < S; ++s) a[s] = *reinterpret_cast<const f32x4*>(yrow + 16 * s);
+    }
   };
   if (t_beg < t_end) load_tile(t_beg);
   for (long long t = t_beg; t < t_end; ++t) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     float ss = 0.f;
+    if constexpr (BF) {
 #pragma unroll
-    for (int s = 0; s < S; ++s) {
+      for (int s = 0; s < SB; ++s)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8[s], qb8[s], acc, 0, 0, 0);
+    } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][j], qb[s][j], acc, 0, 0, 0);
-        ss += a[s][j] * a[s][j];
+      for (int s = 0; s < S; ++s) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s][j], qb[s][j], acc, 0, 0, 0);
+          ss += a[s][j] * a[s][j];
+        }
       }
     }
     const long long c_i0 = i0, c_rend = rend;
     // the next tile's rows are in flight while this tile's epilogue runs
     if (t + 1 < t_end) load_tile(t + 1);
     float inv4[4] = {1.f, 1.f, 1.f, 1.f};
-    if (p.cosine) {
+    if (!BF && p.cosine) {
       // row (lane & 15)'s squared norm: sum over the four feature groups (lanes +16, +32, +48)
       ss += __shfl_xor(ss, 16);
       ss += __shfl_xor(ss, 32);
@@ -276,36 +305,51 @@ long long oryx_topn_waves_kl(long long n_tiles, int kl) {
 
 long long oryx_topn_waves(long long n_tiles) { return oryx_topn_waves_kl(n_tiles, 64); }
 
-int oryx_topn_scan2(const float* Y, const int* perm, long long ld, const float* Q, int kp,
-                    int nq, int cosine, int kl, const int* bucket_of,
-                    const unsigned* cand_bits, int words, const long long* ranges,
-                    const long long* tile0, int n_ranges, long long n_tiles,
-                    const int* excl_ptr, const int* excl_rows, float* out_score, int* out_row,
-                    void* stream) {
+// Y fp32 rows (stride ld) or, with Yb non-null, the bf16 mirror (stride ldb; kp % 32 == 0,
+// cosine 0, kl 64): the bf16 scan.
+int oryx_topn_scan3(const float* Y, const __bf16* Yb, long long ldb, const int* perm,
+                    long long ld, const float* Q, int kp, int nq, int cosine, int kl,
+                    const int* bucket_of, const unsigned* cand_bits, int words,
+                    const long long* ranges, const long long* tile0, int n_ranges,
+                    long long n_tiles, const int* excl_ptr, const int* excl_rows,
+                    float* out_score, int* out_row, void* stream) {
   if (nq <= 0 || nq > QB || n_ranges <= 0 || n_tiles <= 0) return ORYX_EINVAL;
   if (cand_bits && !bucket_of) return ORYX_EINVAL;
-  if (ld < kp || ld % 4 != 0) return ORYX_EINVAL;
+  const bool bf = Yb != nullptr;
+  if (bf ? (ldb < kp || ldb % 8 != 0 || kp % 32 != 0 || cosine || kl != 64)
+         : (ld < kp || ld % 4 != 0))
+    return ORYX_EINVAL;
   if (nq > oryx_topn_max_queries(kl)) return ORYX_EINVAL;
-  TopnParams p{Y, perm, ld, Q, nq, cosine, bucket_of, cand_bits, words, ranges, tile0,
-               n_ranges, n_tiles, excl_ptr, excl_rows, out_score, out_row};
+  TopnParams p{Y, Yb, ldb, perm, ld, Q, nq, cosine, bucket_of, cand_bits, words, ranges,
+               tile0, n_ranges, n_tiles, excl_ptr, excl_rows, out_score, out_row};
   const long long waves = oryx_topn_waves_kl(n_tiles, kl);
   const unsigned blocks = (unsigned)(waves / WPB);
   const size_t lds = lds_bytes(kl, nq);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-#define TOPN_CASE(KPV, KLV)                                                              \
-  if (kp == KPV && kl == KLV) {                                                          \
+#define TOPN_CASE3(KPV, KLV, BFV)                                                        \
+  if (kp == KPV && kl == KLV && bf == BFV) {                                             \
     static bool attr_set = false;                                                        \
     if (!attr_set && lds > 65536) {                                                      \
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topn_scan<KPV, KLV>),       \
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&topn_scan<KPV, KLV, BFV>),  \
                               hipFuncAttributeMaxDynamicSharedMemorySize,                \
                               (int)kLdsBudget) != hipSuccess)                            \
         return ORYX_ELAUNCH;                                                             \
       attr_set = true;                                                                   \
     }                                                                                    \
-    hipLaunchKernelGGL((topn_scan<KPV, KLV>), dim3(blocks), dim3(WPB * 64), lds, s, p);  \
+    hipLaunchKernelGGL((topn_scan<KPV, KLV, BFV>), dim3(blocks), dim3(WPB * 64), lds, s, \
+                       p);                                                               \
     return oryx_check_launch();                                                          \
   }
+#define TOPN_CASE(KPV, KLV) TOPN_CASE3(KPV, KLV, false)
 #define TOPN_KP(KPV) TOPN_CASE(KPV, 64) TOPN_CASE(KPV, 256) TOPN_CASE(KPV, 1024)
+#define TOPN_BF(KPV) TOPN_CASE3(KPV, 64, true)
+  TOPN_BF(32)
+  TOPN_BF(64)
+  TOPN_BF(96)
+  TOPN_BF(128)
+  TOPN_BF(160)
+  TOPN_BF(192)
+  TOPN_BF(256)
   TOPN_KP(16)
   TOPN_KP(32)
   TOPN_KP(48)
@@ -317,9 +361,22 @@ int oryx_topn_scan2(const float* Y, const int* perm, long long ld, const float* 
   TOPN_KP(160)
   TOPN_KP(192)
   TOPN_KP(256)
+#undef TOPN_BF
 #undef TOPN_KP
 #undef TOPN_CASE
+#undef TOPN_CASE3
   return ORYX_EINVAL;
+}
+
+int oryx_topn_scan2(const float* Y, const int* perm, long long ld, const float* Q, int kp,
+                    int nq, int cosine, int kl, const int* bucket_of,
+                    const unsigned* cand_bits, int words, const long long* ranges,
+                    const long long* tile0, int n_ranges, long long n_tiles,
+                    const int* excl_ptr, const int* excl_rows, float* out_score, int* out_row,
+                    void* stream) {
+  return oryx_topn_scan3(Y, nullptr, 0, perm, ld, Q, kp, nq, cosine, kl, bucket_of, cand_bits,
+                         words, ranges, tile0, n_ranges, n_tiles, excl_ptr, excl_rows,
+                         out_score, out_row, stream);
 }
 
 }  // extern "C"

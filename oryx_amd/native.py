@@ -266,6 +266,9 @@ def _load_kernels():
     _sig(lib, "oryx_topn_scan2", c_i, [c_vp, c_vp, c_ll, c_vp, c_i, c_i, c_i, c_i, c_vp, c_vp,
                                        c_i, c_vp, c_vp, c_i, c_ll, c_vp, c_vp, c_vp, c_vp,
                                        c_vp])
+    _sig(lib, "oryx_topn_scan3", c_i, [c_vp, c_vp, c_ll, c_vp, c_ll, c_vp, c_i, c_i, c_i, c_i,
+                                       c_vp, c_vp, c_i, c_vp, c_vp, c_i, c_ll, c_vp, c_vp,
+                                       c_vp, c_vp, c_vp])
     _sig(lib, "oryx_topn_waves_kl", c_ll, [c_ll, c_i])
     _sig(lib, "oryx_topn_max_queries", c_i, [c_i])
     _sig(lib, "oryx_counting_sort", c_i, [c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])

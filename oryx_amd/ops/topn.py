@@ -37,6 +37,14 @@ __all__ = ["ItemIndex", "ShardedItemIndex", "TopNQuery", "MAX_BATCH", "MAX_HOW_M
 
 MAX_BATCH = 16          # queries per kernel launch
 MAX_HOW_MANY = 64       # candidates each wave keeps per query in the batched launch
+BF16_POOL = 64          # candidates the bf16 scan re-ranks exactly per query
+BF16_MAX_HOW_MANY = 32  # deeper requests scan in fp32
+
+
+def _bf16_default() -> bool:
+    """The bf16 scan is on unless ORYX_TOPN_BF16=0 (it is exact: certified or rescanned)."""
+    import os
+    return os.environ.get("ORYX_TOPN_BF16", "1") != "0"
 _KLS = (64, 256, 1024)  # per-(wave, query) list lengths the kernel is built for
 _KPS = (16, 32, 48, 64, 80, 96, 112, 128, 160, 192, 256)
 
@@ -73,7 +81,7 @@ class ItemIndex:
     :class:`ShardedItemIndex`)."""
 
     def __init__(self, store, num_buckets: int, device=None, shard: Tuple[int, int] = (0, 1),
-                 managed: bool = False):
+                 managed: bool = False, bf16: Optional[bool] = None):
         self.store = store
         # managed: a ShardedItemIndex takes the store's changes once and hands every shard
         # its share; the shard never consumes the store's dirty set itself
@@ -102,6 +110,17 @@ class ItemIndex:
         self.n = 0
         self.rebuilds = 0
         self._built = False
+        # bf16 scan with exact fp32 re-rank of a certified candidate pool (_launch_bf16):
+        # dot-product queries of <= BF16_MAX_HOW_MANY on the store's own GPU
+        self.bf16 = (bf16 if bf16 is not None else _bf16_default()) and self.borrowed and \
+            self.kp is not None
+        self.kpb = -(-self.kp // 32) * 32 if self.kp else None
+        self._yb = None            # bf16 [rows, kpb] mirror of the store's rows (store order)
+        self._yb_key = None        # (store version, rows) the mirror was converted at
+        self._yb_token = store.register_index_consumer() if self.bf16 else None
+        self._max_norm = 0.0       # >= every mirrored row's L2 norm
+        self.bf16_certified = 0
+        self.bf16_fallbacks = 0
 
     # ------------------------------------------------------------------ maintenance
     def refresh(self, state: Optional[Tuple[int, Optional[np.ndarray]]] = None) -> None:
@@ -259,13 +278,136 @@ class ItemIndex:
         return self.Ys, self.kp, None
 
     def _launch(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY):
-        empty = (np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32))
-        if self.n == 0:
-            return [empty for _ in qs]
+        if (self.bf16 and not cosine and kl == MAX_HOW_MANY and self.n > 0 and
+                all(q.how_many <= BF16_MAX_HOW_MANY for q in qs)):
+            out, failed = self._launch_bf16(qs)
+            if failed:
+                redo = self._launch_fp32([qs[j] for j in failed], cosine, kl)
+                for j, r in zip(failed, redo):
+                    out[j] = r
+            return out
+        return self._launch_fp32(qs, cosine, kl)
+
+    # ------------------------------------------------------------------ bf16 scan
+    def _bf16_rows(self) -> torch.Tensor:
+        """The bf16 mirror of the store's device rows, brought up to date: the rows written
+        since the last call are converted (all of them after a reallocation), and the norm
+        bound follows them.  The changed rows are taken before the device rows are read, so
+        a write landing in between is converted again next time, never missed."""
+        st = self.store
+        ver, dirty = st.take_index_state(self._yb_token)
+        mat, _ = st.device_rows()
+        rows = mat.shape[0]
+        yb = self._yb
+        k = self.k
+        _, _, norms = st.device_view()
+        if yb is None or yb.shape[0] != rows or dirty is None or len(dirty) > rows // 8:
+            if yb is None or yb.shape[0] != rows:
+                yb = torch.zeros((rows, self.kpb), dtype=torch.bfloat16, device=mat.device)
+            step = 1 << 20
+            for lo in range(0, rows, step):
+                hi = min(rows, lo + step)
+                yb[lo:hi, :k] = mat[lo:hi, :k].to(torch.bfloat16)
+            self._max_norm = float(norms[:rows].max()) if rows else 0.0
+        elif len(dirty):
+            d = torch.from_numpy(np.asarray(dirty, dtype=np.int64)).to(mat.device)
+            d = d[d < rows]
+            if d.numel():
+                yb[d, :k] = mat[d, :k].to(torch.bfloat16)
+                self._max_norm = max(self._max_norm, float(norms[d].max()))
+        self._yb = yb
+        self._yb_key = (ver, rows)
+        return yb
+
+    def _launch_bf16(self, qs: Sequence[TopNQuery]):
+        """Dot-product queries through the bf16 scan: the kernel keeps each query's best
+        BF16_POOL candidates by bf16 score (items and query rounded to bf16, fp32
+        accumulation); those are re-scored exactly in fp32 and the query's top how_many
+        taken from them.  The pool is certified to hold the exact answer when every item
+        outside it scores below the pool's how_many-th exact score: an item's bf16 score is
+        within E = (2u + u^2 + 2k 2^-24) |x| max|y| of its fp32 score (u = 2^-8, the bf16
+        rounding of both operands; Cauchy-Schwarz), so outside items score at most
+        (pool's last bf16 score) + E.  Uncertified queries are returned in ``failed`` (the
+        caller rescans them in fp32).  Returns (results, failed indices)."""
         dev = self.device
         lib = native.require_kernels()
         nq = len(qs)
-        Q = np.zeros((MAX_BATCH, self.kp), dtype=np.float32)
+        kl = MAX_HOW_MANY
+        prep = self._prep(qs, self.kpb)
+        if prep is None:
+            empty = (np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32))
+            return [empty for _ in qs], []
+        Q, rs, tile0, n_tiles, bits, ptr, ex_dev = prep
+        mat, ld, perm = self._matrix()
+        yb = self._bf16_rows()          # covers every row the permutation names
+        waves = int(lib.oryx_topn_waves_kl(n_tiles, kl))
+        o_sc = torch.empty((waves, nq, kl), dtype=torch.float32, device=dev)
+        o_rw = torch.empty((waves, nq, kl), dtype=torch.int32, device=dev)
+        Qd = torch.from_numpy(Q).to(dev)
+        rs_d = torch.from_numpy(np.ascontiguousarray(rs, dtype=np.int64)).to(dev)
+        t0_d = torch.from_numpy(tile0).to(dev)
+        bits_d = torch.from_numpy(bits).to(dev) if bits is not None else None
+        ptr_d = torch.from_numpy(ptr).to(dev) if ex_dev is not None else None
+        rc = lib.oryx_topn_scan3(
+            mat.data_ptr(), yb.data_ptr(), self.kpb,
+            perm.data_ptr() if perm is not None else None, int(ld), Qd.data_ptr(), self.kpb,
+            nq, 0, kl, self.bucket_of.data_ptr() if bits_d is not None else None,
+            bits_d.data_ptr() if bits_d is not None else None, self.words, rs_d.data_ptr(),
+            t0_d.data_ptr(), len(rs), n_tiles,
+            ptr_d.data_ptr() if ptr_d is not None else None,
+            ex_dev.data_ptr() if ex_dev is not None else None,
+            o_sc.data_ptr(), o_rw.data_ptr(), native.stream_ptr(dev))
+        native.check(rc, "oryx_topn_scan3")
+        pool = min(BF16_POOL, waves * kl)
+        sc = o_sc.permute(1, 0, 2).reshape(nq, -1)
+        rw = o_rw.permute(1, 0, 2).reshape(nq, -1)
+        v, i = torch.topk(sc, pool, dim=1)                 # bf16 scores, descending
+        pos = torch.gather(rw, 1, i)
+        ok = torch.isfinite(v) & (pos >= 0)
+        rows = self.perm[pos.clamp(min=0).long()].long()
+        exact = (mat[rows][..., :self.k] * Qd[:nq, None, :self.k]).sum(-1)
+        exact = torch.where(ok, exact, torch.full_like(exact, -float("inf")))
+        kmax = max(q.how_many for q in qs)
+        ev, ei = torch.topk(exact, kmax, dim=1)
+        epos = torch.gather(pos, 1, ei)
+        small = torch.cat([ev, epos.float(), v[:, -1:], ok.sum(1, keepdim=True).float()], 1)
+        h = small.cpu().numpy()
+        ev_h, epos_h = h[:, :kmax], h[:, kmax:2 * kmax].astype(np.int64)
+        last_h, nvalid_h = h[:, 2 * kmax], h[:, 2 * kmax + 1].astype(np.int64)
+        u = 2.0 ** -8
+        c = 2 * u + u * u + 2 * self.k * 2.0 ** -24
+        out: List[Optional[Tuple[np.ndarray, np.ndarray]]] = [None] * nq
+        failed = []
+        for j, q in enumerate(qs):
+            x = np.asarray(q.target, dtype=np.float64)[:self.k]
+            bound = c * float(np.sqrt(x @ x)) * self._max_norm
+            tau = ev_h[j, q.how_many - 1]
+            if nvalid_h[j] < pool or (np.isfinite(tau) and last_h[j] + bound < tau):
+                self.bf16_certified += 1
+                out[j] = self._finish_one(ev_h[j, :q.how_many], epos_h[j, :q.how_many])
+            else:
+                self.bf16_fallbacks += 1
+                failed.append(j)
+        return out, failed
+
+    def _finish_one(self, vj: np.ndarray, pj: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        keep = np.isfinite(vj) & (pj >= 0)
+        rows = self.row_of_pos_h[pj[keep]]
+        vj = np.asarray(vj[keep], dtype=np.float32)
+        valid_h = self.store._host_valid if self.borrowed else None
+        if valid_h is not None and len(rows):
+            live = valid_h[np.minimum(rows, len(valid_h) - 1)] & (rows < len(valid_h))
+            if not live.all():
+                rows, vj = rows[live], vj[live]
+        return rows, vj
+
+    def _prep(self, qs: Sequence[TopNQuery], kp: int):
+        """Host-side launch inputs shared by the scans: queries [MAX_BATCH, kp], candidate
+        ranges and tiles, bucket bitmaps, excluded positions; None when nothing is
+        scanned."""
+        dev = self.device
+        nq = len(qs)
+        Q = np.zeros((MAX_BATCH, kp), dtype=np.float32)
         for j, q in enumerate(qs):
             Q[j, :self.k] = np.asarray(q.target, dtype=np.float32)[:self.k]
         # candidate ranges: union over the batch; per-query bucket bitmaps when pruning
@@ -285,7 +427,7 @@ class ItemIndex:
             keep = ends > starts
             starts, ends = starts[keep], ends[keep]
             if len(starts) == 0:
-                return [empty for _ in qs]
+                return None
             # merge adjacent ranges
             brk = np.nonzero(starts[1:] != ends[:-1])[0] + 1
             rs = np.stack([starts[np.r_[0, brk]], ends[np.r_[brk - 1, len(ends) - 1]]], 1)
@@ -322,6 +464,19 @@ class ItemIndex:
                 ptr[j + 1] = ptr[j] + len(pj)
             ex_dev = torch.from_numpy(np.concatenate(chunks) if ptr[-1] else
                                       np.zeros(1, dtype=np.int32)).to(dev)
+        return Q, rs, tile0, n_tiles, bits, ptr, ex_dev
+
+    def _launch_fp32(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY):
+        empty = (np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32))
+        if self.n == 0:
+            return [empty for _ in qs]
+        dev = self.device
+        lib = native.require_kernels()
+        nq = len(qs)
+        prep = self._prep(qs, self.kp)
+        if prep is None:
+            return [empty for _ in qs]
+        Q, rs, tile0, n_tiles, bits, ptr, ex_dev = prep
         waves = int(lib.oryx_topn_waves_kl(n_tiles, kl))
         o_sc = torch.empty((waves, nq, kl), dtype=torch.float32, device=dev)
         o_rw = torch.empty((waves, nq, kl), dtype=torch.int32, device=dev)
@@ -348,20 +503,9 @@ class ItemIndex:
         v, i = torch.topk(sc, m, dim=1)
         pos = torch.gather(rw, 1, i)
         v_h, pos_h = v.cpu().numpy(), pos.cpu().numpy()
-        valid_h = self.store._host_valid if self.borrowed else None
-        out = []
-        for j, q in enumerate(qs):
-            vj, pj = v_h[j, :q.how_many], pos_h[j, :q.how_many]
-            keep = np.isfinite(vj) & (pj >= 0)
-            rows = self.row_of_pos_h[pj[keep]]
-            vj = vj[keep]
-            if valid_h is not None and len(rows):
-                # a row removed between the permutation and the launch is never returned
-                live = valid_h[np.minimum(rows, len(valid_h) - 1)] & (rows < len(valid_h))
-                if not live.all():
-                    rows, vj = rows[live], vj[live]
-            out.append((rows, vj))
-        return out
+        # (a row removed between the permutation and the launch is never returned)
+        return [self._finish_one(v_h[j, :q.how_many], pos_h[j, :q.how_many])
+                for j, q in enumerate(qs)]
 
     # ------------------------------------------------------------------ all scores
     def all_scores_device(self, target: np.ndarray, cosine: bool, candidates=None,

@@ -350,14 +350,15 @@ def _brute(Y, valid, q, how_many, cosine=False, allowed=None, exclude=()):
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,n", [(10, 5000), (50, 100_003), (250, 40_000)])
 @pytest.mark.parametrize("cosine", [False, True])
-def test_topn_kernel_matches_bruteforce(cuda, k, n, cosine):
+@pytest.mark.parametrize("bf16", [True, False])
+def test_topn_kernel_matches_bruteforce(cuda, k, n, cosine, bf16):
     from oryx_amd.models.als.common import FeatureVectors
     from oryx_amd.ops import topn
     g = np.random.default_rng(k + n)
-    fv = FeatureVectors(k, cuda)
+    fv = FeatureVectors(k, cuda, row_pad=topn.row_pad_for(k))
     Y = g.standard_normal((n, k)).astype(np.float32)
     fv.set_vectors(["I%d" % i for i in range(n)], Y)
-    idx = topn.ItemIndex(fv, 1)
+    idx = topn.ItemIndex(fv, 1, bf16=bf16)
     qs = [topn.TopNQuery(g.standard_normal(k).astype(np.float32), hm, cosine,
                          exclude_rows=g.integers(0, n, 30).tolist())
           for hm in (1, 10, 64, 7, 33)]
@@ -371,6 +372,57 @@ def test_topn_kernel_matches_bruteforce(cuda, k, n, cosine):
         assert np.allclose(scores, bs, rtol=1e-5, atol=1e-5)
         assert (rows == br).mean() > 0.9
         assert not set(rows.tolist()) & set(q.exclude_rows)
+    if bf16 and not cosine:
+        assert idx.bf16_certified > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [50, 250])
+def test_topn_bf16_scan_exact_and_certified(cuda, k):
+    """The bf16 scan + exact fp32 re-rank returns exactly torch.topk of the fp32 scores
+    (same rows, scores to fp32 summation order), with exclusions; items built to tie within
+    the bf16 error bound defeat the certificate and are rescanned in fp32 -- still exact; a
+    value update reaches the bf16 mirror before the next query."""
+    from oryx_amd.models.als.common import FeatureVectors
+    from oryx_amd.ops import topn
+    g = np.random.default_rng(k)
+    n = 50_000
+    fv = FeatureVectors(k, cuda, row_pad=topn.row_pad_for(k))
+    Y = g.standard_normal((n, k)).astype(np.float32)
+    fv.set_vectors(["I%d" % i for i in range(n)], Y)
+    idx = topn.ItemIndex(fv, 1, bf16=True)
+    assert idx.bf16
+
+    def check(qs):
+        res = idx.scan(qs)
+        Yd = torch.from_numpy(Y).to(cuda)
+        for q, (rows, scores) in zip(qs, res):
+            s = Yd @ torch.from_numpy(q.target).to(cuda)
+            if q.exclude_rows:
+                s[torch.as_tensor(q.exclude_rows, device=cuda)] = -float("inf")
+            v, i = torch.topk(s, q.how_many)
+            assert rows.tolist() == i.cpu().tolist()
+            np.testing.assert_allclose(scores, v.cpu().numpy(), rtol=2e-6, atol=2e-5)
+
+    qs = [topn.TopNQuery(g.standard_normal(k).astype(np.float32), hm,
+                         exclude_rows=g.integers(0, n, 20).tolist() if hm > 5 else None)
+          for hm in (1, 5, 10, 10, 32, 20, 3)]
+    c0 = idx.bf16_certified
+    check(qs)
+    assert idx.bf16_certified - c0 == len(qs) and idx.bf16_fallbacks == 0
+    # a value update: the new best item must be found through the mirror
+    t = qs[2].target
+    Y[123] = (t / np.linalg.norm(t) * 40).astype(np.float32)
+    fv.set_vector("I123", Y[123])
+    check([topn.TopNQuery(t, 10)])
+    # near-ties: 200 items along the query, scores within ~1e-4 (far inside the bf16 bound)
+    base = (t / np.linalg.norm(t) * 30).astype(np.float32)
+    ties = np.arange(1000, 1200)
+    Y[ties] = base[None, :] * (1 + 1e-4 * g.standard_normal((200, 1))).astype(np.float32)
+    fv.set_vectors(["I%d" % r for r in ties], Y[ties])
+    f0 = idx.bf16_fallbacks
+    check([topn.TopNQuery(t, 10)])
+    assert idx.bf16_fallbacks == f0 + 1
 
 
 @pytest.mark.gpu
