@@ -132,6 +132,9 @@ def serve_and_measure(model, users: int, workers: int, requests: int, warmup: in
         "oryx.serving.no-init-topics": "true",
         "oryx.serving.application-resources": '"com.cloudera.oryx.app.serving,'
                                               'com.cloudera.oryx.app.serving.als"',
+        # ORYX_BENCH_PYTHON_HTTP=1: the Python http.server front end (A/B)
+        "oryx.serving.api.native-http":
+            "false" if os.environ.get("ORYX_BENCH_PYTHON_HTTP") == "1" else "true",
     }, cfg.get_default())
     layer = ServingLayer(conf, manager=_Manager(conf), host="127.0.0.1").start()
     port = layer.actual_port
@@ -325,6 +328,8 @@ def main(argv=None) -> int:
                 rec = record(model, args, qps, lat, total, errors, build_s, w, rate, items,
                              features)
                 rec["rescorer"] = bool(args.rescorer)
+                rec["front_end"] = "python http.server" if \
+                    os.environ.get("ORYX_BENCH_PYTHON_HTTP") == "1" else "native (oryx_http.cpp)"
                 print(json.dumps(rec), flush=True)
             if model.batcher is not None:
                 model.batcher.close()

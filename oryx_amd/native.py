@@ -129,6 +129,13 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_speed_assemble", c_ll, [c_vp, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_vp, c_i, c_vp, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_rowmap_key_suffixes", c_ll, [c_vp, c_vp, c_ll])
+    _sig(lib, "oryx_http_start", c_vp, [c_cp, c_i, c_i, c_ll])
+    _sig(lib, "oryx_http_port", c_i, [c_vp])
+    _sig(lib, "oryx_http_served", c_ll, [c_vp])
+    _sig(lib, "oryx_http_next", c_ll, [c_vp, c_vp, c_ll, c_i])
+    _sig(lib, "oryx_http_respond", c_i, [c_vp, ctypes.c_ulonglong, c_cp, c_ll, c_i])
+    _sig(lib, "oryx_http_stop", None, [c_vp])
+    _sig(lib, "oryx_http_free", None, [c_vp])
     _sig(lib, "oryx_speed_append", c_ll, [c_vp, c_vp, c_i, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,
                                           c_vp, c_vp, c_i, c_ll, c_i, c_vp])
     _sig(lib, "oryx_split_by_time", c_ll, [c_vp, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,

@@ -278,15 +278,19 @@ class ItemIndex:
         return self.Ys, self.kp, None
 
     def _launch(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY):
-        if (self.bf16 and not cosine and kl == MAX_HOW_MANY and self.n > 0 and
-                all(q.how_many <= BF16_MAX_HOW_MANY for q in qs)):
-            out, failed = self._launch_bf16(qs)
-            if failed:
-                redo = self._launch_fp32([qs[j] for j in failed], cosine, kl)
-                for j, r in zip(failed, redo):
-                    out[j] = r
-            return out
-        return self._launch_fp32(qs, cosine, kl)
+        shallow = [j for j, q in enumerate(qs) if q.how_many <= BF16_MAX_HOW_MANY] \
+            if self.bf16 and not cosine and kl == MAX_HOW_MANY and self.n > 0 else []
+        if not shallow:
+            return self._launch_fp32(qs, cosine, kl)
+        out: List[Optional[Tuple[np.ndarray, np.ndarray]]] = [None] * len(qs)
+        res, failed = self._launch_bf16([qs[j] for j in shallow])
+        for j, r in zip(shallow, res):
+            out[j] = r
+        rest = [shallow[f] for f in failed] + [j for j in range(len(qs)) if j not in shallow]
+        if rest:
+            for j, r in zip(rest, self._launch_fp32([qs[j] for j in rest], cosine, kl)):
+                out[j] = r
+        return out
 
     # ------------------------------------------------------------------ bf16 scan
     def _bf16_rows(self) -> torch.Tensor:

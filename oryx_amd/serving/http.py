@@ -20,6 +20,7 @@ Replaces the reference's embedded Tomcat + Jersey stack (``[lserving]/ServingLay
 from __future__ import annotations
 
 import email.parser
+import email.utils
 import gzip
 import hashlib
 import http.server
@@ -32,6 +33,7 @@ import re
 import secrets
 import socketserver
 import ssl
+import struct
 import threading
 import time
 import urllib.parse
@@ -528,6 +530,150 @@ class _Handler(http.server.BaseHTTPRequestHandler):
     do_PUT = _handle
     do_DELETE = _handle
     do_HEAD = _handle
+
+
+def _respond_bytes(srv, req_headers: Dict[str, str], method: str, target: str, path: str,
+                   resp: "Response", t0: float) -> bytes:
+    """A response's bytes as one buffer (compression as negotiated), shared by the servers."""
+    payload = resp.body
+    headers_out = dict(resp.headers)
+    if payload and resp.content_type in _COMPRESSIBLE and len(payload) > 64:
+        ae = (req_headers.get("accept-encoding") or "").lower()
+        if "gzip" in ae:
+            payload = gzip.compress(payload, 5)
+            headers_out["Content-Encoding"] = "gzip"
+        elif "deflate" in ae:
+            payload = zlib.compress(payload, 5)
+            headers_out["Content-Encoding"] = "deflate"
+    lines = ["HTTP/1.1 %d %s" % (resp.status, HTTP_STATUS.get(resp.status, "")),
+             "Server: Oryx", "Date: " + email.utils.formatdate(usegmt=True)]
+    if resp.content_type:
+        lines.append("Content-Type: " + resp.content_type + "; charset=UTF-8")
+    for k, v in headers_out.items():
+        lines.append("%s: %s" % (k, v))
+    lines.append("Content-Length: %d" % len(payload))
+    head = ("\r\n".join(lines) + "\r\n\r\n").encode("latin-1")
+    if srv.metrics is not None:
+        srv.metrics.observe_request(path, resp.status, time.perf_counter() - t0)
+    return head + payload if method != "HEAD" and payload else head
+
+
+class NativeHTTPServer:
+    """The serving front end on the native HTTP loop (``csrc/runtime/oryx_http.cpp``: epoll
+    accept / parse / keep-alive / pipelining on a native thread): ``threads`` Python handler
+    threads take complete requests from its queue (blocking without the GIL) and hand back
+    response bytes, so Python runs only routing and the endpoint per request.  Same routes,
+    auth, compression and metrics as :class:`OryxHTTPServer` (which keeps the TLS path)."""
+
+    def __init__(self, host: str, port: int, router: "Router", app_context: dict,
+                 auth: Optional[DigestAuth] = None, metrics=None, threads: int = 16,
+                 max_body: int = 64 << 20):
+        from .. import native
+        self.router = router
+        self.app_context = app_context
+        self.auth = auth
+        self.metrics = metrics
+        self._lib = native.runtime()
+        self._h = self._lib.oryx_http_start(host.encode() if host else b"", int(port), 1024,
+                                            int(max_body))
+        if not self._h:
+            raise OSError("cannot listen on %s:%d" % (host, port))
+        self.server_address = (host, int(self._lib.oryx_http_port(self._h)))
+        self._threads: List[threading.Thread] = []
+        self._n_threads = max(1, int(threads))
+        self._stopping = False
+
+    @property
+    def port(self) -> int:
+        return self.server_address[1]
+
+    def start_background(self) -> threading.Thread:
+        for j in range(self._n_threads):
+            t = threading.Thread(target=self._work, name="oryx-http-%d" % j, daemon=True)
+            t.start()
+            self._threads.append(t)
+        return self._threads[0]
+
+    def _work(self) -> None:
+        import ctypes
+        lib, h = self._lib, self._h
+        cap = 1 << 16
+        buf = ctypes.create_string_buffer(cap)
+        while not self._stopping:
+            n = lib.oryx_http_next(h, buf, cap, 200)
+            if n == 0:
+                continue
+            if n == -1:
+                return
+            if n < 0:
+                cap = -n
+                buf = ctypes.create_string_buffer(cap)
+                continue
+            raw = buf.raw[:n]
+            rid, ml, tl, hl, bl = struct.unpack_from("<QIIIQ", raw, 0)
+            o = 28
+            method = raw[o:o + ml].decode("latin-1")
+            o += ml
+            target = raw[o:o + tl].decode("latin-1")
+            o += tl
+            hraw = raw[o:o + hl].decode("latin-1")
+            o += hl
+            body = raw[o:o + bl]
+            try:
+                out, close = self._handle(method, target, hraw, body)
+            except Exception:                       # never leave a request unanswered
+                log.exception("request failed")
+                out = (b"HTTP/1.1 500 Internal Server Error\r\nContent-Length: 0\r\n"
+                       b"Connection: close\r\n\r\n")
+                close = True
+            lib.oryx_http_respond(h, rid, out, len(out), int(close))
+
+    def _handle(self, method: str, target: str, hraw: str, body: bytes):
+        t0 = time.perf_counter()
+        headers: Dict[str, str] = {}
+        for line in hraw.split("\r\n"):
+            k, sep, v = line.partition(":")
+            if sep:
+                key = k.strip().lower()
+                v = v.strip()
+                headers[key] = headers[key] + ", " + v if key in headers else v
+        parsed = urllib.parse.urlsplit(target)
+        query = urllib.parse.parse_qs(parsed.query, keep_blank_values=True)
+        req = Request(method, parsed.path, query, headers, body, self.app_context)
+        verdict = "ok" if self.auth is None else self.auth.verify(
+            method, target, headers.get("authorization"))
+        if verdict != "ok":
+            resp = Response(401, b"401 Unauthorized\n", TEXT,
+                            {"WWW-Authenticate": self.auth.challenge(stale=verdict == "stale")})
+        else:
+            resp = self.router.dispatch(req)
+        close = "close" in (headers.get("connection") or "").lower()
+        return _respond_bytes(self, headers, method, target, parsed.path, resp, t0), close
+
+    def shutdown(self) -> None:
+        self._stopping = True
+        self._lib.oryx_http_stop(self._h)
+        for t in self._threads:
+            t.join(timeout=5)
+
+    def server_close(self) -> None:
+        if self._h:
+            if not self._stopping:
+                self.shutdown()
+            if not any(t.is_alive() for t in self._threads):
+                self._lib.oryx_http_free(self._h)
+            self._h = None
+
+
+def make_server(host: str, port: int, router: "Router", app_context: dict,
+                ssl_context: Optional[ssl.SSLContext] = None,
+                auth: Optional[DigestAuth] = None, metrics=None, native: bool = True,
+                threads: int = 16):
+    """The native front end (:class:`NativeHTTPServer`) unless TLS is configured or
+    ``native`` is off; the Python :class:`OryxHTTPServer` otherwise."""
+    if native and ssl_context is None:
+        return NativeHTTPServer(host, port, router, app_context, auth, metrics, threads)
+    return OryxHTTPServer(host, port, router, app_context, ssl_context, auth, metrics)
 
 
 class OryxHTTPServer(socketserver.ThreadingMixIn, http.server.HTTPServer):

@@ -153,6 +153,8 @@ class ServingLayer:
         self.keystore_password = cfg.get_optional_string(config,
                                                          "oryx.serving.api.keystore-password")
         self.context_path = config.get_string("oryx.serving.api.context-path")
+        self.native_http = config.get_bool("oryx.serving.api.native-http")
+        self.handler_threads = config.get_int("oryx.serving.api.handler-threads")
         self.update_topic = config.get_string("oryx.update-topic.message.topic")
         self.update_broker = config.get_string("oryx.update-topic.broker")
         self.input_topic = config.get_string("oryx.input-topic.message.topic")
@@ -160,7 +162,7 @@ class ServingLayer:
         self.max_message = config.get_int("oryx.update-topic.message.max-size")
         self._manager = manager
         self._input_producer = input_producer
-        self._server: Optional[http.OryxHTTPServer] = None
+        self._server = None       # http.NativeHTTPServer or http.OryxHTTPServer
         self._consumer_thread: Optional[threading.Thread] = None
         self._updates: Optional[UpdateIterator] = None
         self._consumer: Optional[tlog.TopicConsumer] = None
@@ -195,8 +197,11 @@ class ServingLayer:
         if self.user_name and self.password:
             auth = http.DigestAuth(self.user_name, self.password)
         port = self.secure_port if ssl_ctx is not None else self.port
-        self._server = http.OryxHTTPServer(self.host, port, router, self.context, ssl_ctx, auth,
-                                           self.metrics)
+        # the native front end (csrc/runtime/oryx_http.cpp) unless TLS is on or
+        # oryx.serving.api.native-http is false
+        self._server = http.make_server(self.host, port, router, self.context, ssl_ctx, auth,
+                                        self.metrics, native=self.native_http,
+                                        threads=self.handler_threads)
         self._server.start_background()
         log.info("Serving layer listening on %s:%d%s", self.host, self._server.port,
                  " (HTTPS)" if ssl_ctx else "")

@@ -787,6 +787,8 @@ def test_serving_model_keeps_one_device_copy_of_y(cuda):
     torch.cuda.synchronize()
     used = torch.cuda.memory_allocated(cuda) - base
     mirror = (n + n // 8) * 256 * 4
+    if m.index.bf16:
+        mirror += (n + n // 8) * 256 * 2        # the bf16 scan's half-size mirror
     assert used < mirror * 1.1, (used, mirror)
     # an in-place value update is visible without an index rebuild
     rebuilds = m.index.rebuilds
