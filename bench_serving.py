@@ -135,6 +135,7 @@ def serve_and_measure(model, users: int, workers: int, requests: int, warmup: in
         # ORYX_BENCH_PYTHON_HTTP=1: the Python http.server front end (A/B)
         "oryx.serving.api.native-http":
             "false" if os.environ.get("ORYX_BENCH_PYTHON_HTTP") == "1" else "true",
+        "oryx.serving.api.handler-threads": int(os.environ.get("ORYX_BENCH_HTTP_THREADS", "16")),
     }, cfg.get_default())
     layer = ServingLayer(conf, manager=_Manager(conf), host="127.0.0.1").start()
     port = layer.actual_port
@@ -329,7 +330,9 @@ def main(argv=None) -> int:
                              features)
                 rec["rescorer"] = bool(args.rescorer)
                 rec["front_end"] = "python http.server" if \
-                    os.environ.get("ORYX_BENCH_PYTHON_HTTP") == "1" else "native (oryx_http.cpp)"
+                    os.environ.get("ORYX_BENCH_PYTHON_HTTP") == "1" else \
+                    "native (oryx_http.cpp), %s handler threads" % \
+                    os.environ.get("ORYX_BENCH_HTTP_THREADS", "16")
                 print(json.dumps(rec), flush=True)
             if model.batcher is not None:
                 model.batcher.close()

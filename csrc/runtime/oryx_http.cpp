@@ -70,12 +70,12 @@ struct Server {
   int lfd = -1, efd = -1, wfd = -1;   // listener, epoll, eventfd (responses ready / stop)
   int port = 0;
   long long max_body = 64ll << 20;
-  std::thread loop;
   std::atomic<bool> stop{false};
-  // requests ready for the handlers
+  // requests ready for the handlers; `leader`: a handler thread is polling the sockets
   std::mutex qmu;
   std::condition_variable qcv;
   std::deque<Req> ready;
+  bool leader = false;
   // connection state: taken by the loop per event and by a handler thread that writes its
   // response straight to the socket (oryx_http_respond: no hop through the loop thread)
   std::mutex cmu;
@@ -197,11 +197,9 @@ void submit(Server* S, Conn* c) {
   r.id = S->next_id++;
   const uint64_t seq = c->next_seq++;
   S->inflight[r.id] = {c->cid, seq};
-  {
-    std::lock_guard<std::mutex> g(S->qmu);
-    S->ready.push_back(std::move(r));
-  }
-  S->qcv.notify_one();
+  // (no wake-up here: the polling thread takes a request itself when its poll returns)
+  std::lock_guard<std::mutex> g(S->qmu);
+  S->ready.push_back(std::move(r));
 }
 
 // Parses whatever complete requests c->in holds.
@@ -335,11 +333,13 @@ void parse_input(Server* S, Conn* c) {
   }
 }
 
-void run_loop(Server* S) {
-  std::vector<epoll_event> evs(256);
-  char buf[64 * 1024];
-  while (!S->stop.load()) {
-    const int n = epoll_wait(S->efd, evs.data(), (int)evs.size(), 200);
+// One round of the event loop, run by the handler thread that currently leads (see
+// oryx_http_next): waits up to wait_ms for socket events and handles them all.
+void poll_once(Server* S, int wait_ms) {
+  epoll_event evs[256];
+  static thread_local char buf[64 * 1024];
+  {
+    const int n = epoll_wait(S->efd, evs, 256, wait_ms);
     for (int k = 0; k < n; ++k) {
       const int fd = evs[k].data.fd;
       std::lock_guard<std::mutex> g(S->cmu);
@@ -404,7 +404,8 @@ void run_loop(Server* S) {
 
 extern "C" {
 
-// Binds host:port (port 0: any free port), starts the loop.  Returns a handle or null.
+// Binds host:port (port 0: any free port).  The sockets are polled by the threads calling
+// oryx_http_next.  Returns a handle or null.
 void* oryx_http_start(const char* host, int port, int backlog, long long max_body) {
   auto* S = new Server();
   if (max_body > 0) S->max_body = max_body;
@@ -442,7 +443,6 @@ void* oryx_http_start(const char* host, int port, int backlog, long long max_bod
   epoll_ctl(S->efd, EPOLL_CTL_ADD, S->lfd, &ev);
   ev.data.fd = S->wfd;
   epoll_ctl(S->efd, EPOLL_CTL_ADD, S->wfd, &ev);
-  S->loop = std::thread(run_loop, S);
   return S;
 }
 
@@ -455,13 +455,34 @@ long long oryx_http_served(void* h) { return static_cast<Server*>(h)->served.loa
 //   method target headers ("Name: value\r\n" lines) body
 // Waits up to timeout_ms.  Returns the packed size, 0 on timeout, -1 once the server is
 // stopping, or -(size needed) when out is too small (the request stays queued).
+//
+// Leader / followers: there is no loop thread.  A caller finding no request ready becomes
+// the poller if no other thread is (the others wait); when its poll returns it hands the
+// poller role on (waking one waiting thread) and takes the first request itself -- so at low
+// concurrency a request goes from the socket to its handler on the same thread, with no
+// thread wake-up in between.
 long long oryx_http_next(void* h, char* out, long long cap, int timeout_ms) {
   auto* S = static_cast<Server*>(h);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
   std::unique_lock<std::mutex> l(S->qmu);
-  if (!S->qcv.wait_for(l, std::chrono::milliseconds(timeout_ms),
-                       [&] { return !S->ready.empty() || S->stop.load(); }))
-    return 0;
-  if (S->ready.empty()) return -1;
+  for (;;) {
+    if (S->stop.load()) return -1;
+    if (!S->ready.empty()) break;
+    const auto now = std::chrono::steady_clock::now();
+    if (now >= deadline) return 0;
+    if (!S->leader) {
+      S->leader = true;
+      l.unlock();
+      const long long left =
+          std::chrono::duration_cast<std::chrono::milliseconds>(deadline - now).count();
+      poll_once(S, (int)std::max<long long>(1, std::min<long long>(left, 50)));
+      l.lock();
+      S->leader = false;
+      S->qcv.notify_one();     // the next poller (or a taker of further ready requests)
+      continue;
+    }
+    S->qcv.wait_until(l, deadline);
+  }
   const Req& r = S->ready.front();
   const long long need = 28 + (long long)(r.method.size() + r.target.size() + r.headers.size() +
                                           r.body.size());
@@ -479,6 +500,7 @@ long long oryx_http_next(void* h, char* out, long long cap, int timeout_ms) {
   memcpy(o, r.headers.data(), hl); o += hl;
   memcpy(o, r.body.data(), bl);
   S->ready.pop_front();
+  if (!S->ready.empty()) S->qcv.notify_one();
   return need;
 }
 
@@ -510,10 +532,13 @@ int oryx_http_respond(void* h, unsigned long long id, const char* data, long lon
 void oryx_http_stop(void* h) {
   auto* S = static_cast<Server*>(h);
   if (!S || S->stop.exchange(true)) return;
-  S->qcv.notify_all();
   const uint64_t one = 1;
-  (void)!write(S->wfd, &one, sizeof(one));
-  if (S->loop.joinable()) S->loop.join();
+  (void)!write(S->wfd, &one, sizeof(one));     // ends a poll in progress
+  {
+    std::unique_lock<std::mutex> l(S->qmu);
+    S->qcv.notify_all();
+    S->qcv.wait_for(l, std::chrono::seconds(5), [&] { return !S->leader; });
+  }
   std::lock_guard<std::mutex> g(S->cmu);
   for (auto& kv : S->conns) close(kv.first);
   S->conns.clear();
