@@ -41,6 +41,29 @@ BF16_POOL = 64          # candidates the bf16 scan re-ranks exactly per query
 BF16_MAX_HOW_MANY = 32  # deeper requests scan in fp32
 
 
+def _upload(arrays, device) -> List[torch.Tensor]:
+    """Host arrays to the device in ONE copy: packed back to back (16-byte aligned) into a
+    pinned staging buffer, then viewed per array on the device."""
+    offs, total = [], 0
+    for a in arrays:
+        offs.append(total)
+        total += -(-a.nbytes // 16) * 16
+    host = torch.empty(max(total, 16), dtype=torch.uint8, pin_memory=True)
+    hb = host.numpy()
+    for a, o in zip(arrays, offs):
+        hb[o:o + a.nbytes] = np.ascontiguousarray(a).reshape(-1).view(np.uint8)
+    dev = host.to(device, non_blocking=True)
+    out = []
+    for a, o in zip(arrays, offs):
+        t = dev[o:o + a.nbytes].view(_TORCH_DTYPE[a.dtype.str])
+        out.append(t.view(a.shape))
+    return out
+
+
+_TORCH_DTYPE = {np.dtype(np.float32).str: torch.float32, np.dtype(np.int64).str: torch.int64,
+                np.dtype(np.int32).str: torch.int32, np.dtype(np.uint32).str: torch.int32}
+
+
 def _bf16_default() -> bool:
     """The bf16 scan is on unless ORYX_TOPN_BF16=0 (it is exact: certified or rescanned)."""
     import os
@@ -181,6 +204,7 @@ class ItemIndex:
         if n:
             pos[rows] = torch.arange(n, device=dev)
         self.pos_of_row = pos
+        self.pos_of_row_h = pos.cpu().numpy()
         self.row_of_pos = rows
         self.row_of_pos_h = rows.cpu().numpy()
         counts = torch.bincount(b, minlength=self.num_buckets).cpu().numpy()
@@ -299,6 +323,9 @@ class ItemIndex:
         bound follows them.  The changed rows are taken before the device rows are read, so
         a write landing in between is converted again next time, never missed."""
         st = self.store
+        if self._yb is not None and self._yb_key is not None and \
+                self._yb_key[0] == st.version and self._yb_key[1] == self._yb.shape[0]:
+            return self._yb            # nothing written since the last conversion
         ver, dirty = st.take_index_state(self._yb_token)
         mat, _ = st.device_rows()
         rows = mat.shape[0]
@@ -341,25 +368,20 @@ class ItemIndex:
         if prep is None:
             empty = (np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32))
             return [empty for _ in qs], []
-        Q, rs, tile0, n_tiles, bits, ptr, ex_dev = prep
+        Qd, rs_d, t0_d, bits_d, ptr_d, ex_d, n_ranges, n_tiles = prep
         mat, ld, perm = self._matrix()
         yb = self._bf16_rows()          # covers every row the permutation names
         waves = int(lib.oryx_topn_waves_kl(n_tiles, kl))
         o_sc = torch.empty((waves, nq, kl), dtype=torch.float32, device=dev)
         o_rw = torch.empty((waves, nq, kl), dtype=torch.int32, device=dev)
-        Qd = torch.from_numpy(Q).to(dev)
-        rs_d = torch.from_numpy(np.ascontiguousarray(rs, dtype=np.int64)).to(dev)
-        t0_d = torch.from_numpy(tile0).to(dev)
-        bits_d = torch.from_numpy(bits).to(dev) if bits is not None else None
-        ptr_d = torch.from_numpy(ptr).to(dev) if ex_dev is not None else None
         rc = lib.oryx_topn_scan3(
             mat.data_ptr(), yb.data_ptr(), self.kpb,
             perm.data_ptr() if perm is not None else None, int(ld), Qd.data_ptr(), self.kpb,
             nq, 0, kl, self.bucket_of.data_ptr() if bits_d is not None else None,
             bits_d.data_ptr() if bits_d is not None else None, self.words, rs_d.data_ptr(),
-            t0_d.data_ptr(), len(rs), n_tiles,
+            t0_d.data_ptr(), n_ranges, n_tiles,
             ptr_d.data_ptr() if ptr_d is not None else None,
-            ex_dev.data_ptr() if ex_dev is not None else None,
+            ex_d.data_ptr() if ex_d is not None else None,
             o_sc.data_ptr(), o_rw.data_ptr(), native.stream_ptr(dev))
         native.check(rc, "oryx_topn_scan3")
         pool = min(BF16_POOL, waves * kl)
@@ -367,28 +389,31 @@ class ItemIndex:
         rw = o_rw.permute(1, 0, 2).reshape(nq, -1)
         v, i = torch.topk(sc, pool, dim=1)                 # bf16 scores, descending
         pos = torch.gather(rw, 1, i)
-        ok = torch.isfinite(v) & (pos >= 0)
-        rows = self.perm[pos.clamp(min=0).long()].long()
-        exact = (mat[rows][..., :self.k] * Qd[:nq, None, :self.k]).sum(-1)
-        exact = torch.where(ok, exact, torch.full_like(exact, -float("inf")))
-        kmax = max(q.how_many for q in qs)
-        ev, ei = torch.topk(exact, kmax, dim=1)
-        epos = torch.gather(pos, 1, ei)
-        small = torch.cat([ev, epos.float(), v[:, -1:], ok.sum(1, keepdim=True).float()], 1)
-        h = small.cpu().numpy()
-        ev_h, epos_h = h[:, :kmax], h[:, kmax:2 * kmax].astype(np.int64)
-        last_h, nvalid_h = h[:, 2 * kmax], h[:, 2 * kmax + 1].astype(np.int64)
+        # exact fp32 scores of the pool: gather its rows, one batched dot with the queries
+        # (invalid slots -- position -1 -- score row 0 and are dropped on the host)
+        rows = torch.index_select(self.perm, 0, pos.clamp(min=0).flatten())
+        fp = torch.index_select(mat, 0, rows).view(nq, pool, ld)
+        # (ld <= kpb; both operands' columns past k are zero)
+        exact = torch.bmm(fp, Qd[:nq, :ld].unsqueeze(2)).squeeze(2)
+        h = torch.cat([v.view(torch.int32), pos, exact.view(torch.int32)], 1).cpu().numpy()
+        v_h = h[:, :pool].view(np.float32)
+        pos_h = h[:, pool:2 * pool]
+        ex_h = h[:, 2 * pool:].view(np.float32).copy()
+        okm = np.isfinite(v_h) & (pos_h >= 0)
+        ex_h[~okm] = -np.inf
         u = 2.0 ** -8
         c = 2 * u + u * u + 2 * self.k * 2.0 ** -24
         out: List[Optional[Tuple[np.ndarray, np.ndarray]]] = [None] * nq
         failed = []
         for j, q in enumerate(qs):
+            hm = q.how_many
+            order = np.argsort(-ex_h[j], kind="stable")[:hm]
+            tau = ex_h[j, order[-1]] if len(order) == hm else -np.inf
             x = np.asarray(q.target, dtype=np.float64)[:self.k]
             bound = c * float(np.sqrt(x @ x)) * self._max_norm
-            tau = ev_h[j, q.how_many - 1]
-            if nvalid_h[j] < pool or (np.isfinite(tau) and last_h[j] + bound < tau):
+            if int(okm[j].sum()) < pool or (np.isfinite(tau) and v_h[j, -1] + bound < tau):
                 self.bf16_certified += 1
-                out[j] = self._finish_one(ev_h[j, :q.how_many], epos_h[j, :q.how_many])
+                out[j] = self._finish_one(ex_h[j, order], pos_h[j, order])
             else:
                 self.bf16_fallbacks += 1
                 failed.append(j)
@@ -406,10 +431,11 @@ class ItemIndex:
         return rows, vj
 
     def _prep(self, qs: Sequence[TopNQuery], kp: int):
-        """Host-side launch inputs shared by the scans: queries [MAX_BATCH, kp], candidate
-        ranges and tiles, bucket bitmaps, excluded positions; None when nothing is
-        scanned."""
-        dev = self.device
+        """Launch inputs shared by the scans, built on the host and sent in ONE host-to-device
+        copy: queries [MAX_BATCH, kp], candidate ranges and their tile prefix, per-query
+        bucket bitmaps, excluded positions.  Returns (Q, ranges, tile0, bits or None, ptr or
+        None, excluded or None, n_ranges, n_tiles) device tensors / counts, or None when
+        nothing is scanned."""
         nq = len(qs)
         Q = np.zeros((MAX_BATCH, kp), dtype=np.float32)
         for j, q in enumerate(qs):
@@ -437,38 +463,37 @@ class ItemIndex:
             rs = np.stack([starts[np.r_[0, brk]], ends[np.r_[brk - 1, len(ends) - 1]]], 1)
         else:
             rs = np.array([[0, self.n]], dtype=np.int64)
+        rs = np.ascontiguousarray(rs, dtype=np.int64)
         tiles = (rs[:, 1] - rs[:, 0] + 15) // 16
         tile0 = np.zeros(len(rs) + 1, dtype=np.int64)
         np.cumsum(tiles, out=tile0[1:])
         n_tiles = int(tile0[-1])
-        # excluded store rows -> sorted positions per query
-        ptr = np.zeros(nq + 1, dtype=np.int32)
-        ex_parts = []
-        any_ex = False
-        for j, q in enumerate(qs):
-            er = q.exclude_rows
-            if er is not None and len(er):
-                any_ex = True
-                ex_parts.append(np.asarray(er, dtype=np.int64))
-            else:
-                ex_parts.append(np.zeros(0, dtype=np.int64))
-        ex_dev = None
-        if any_ex:
-            flat = torch.from_numpy(np.concatenate(ex_parts)).to(dev)
-            p = self.pos_of_row[flat.clamp(0, self.pos_of_row.numel() - 1)]
-            p = torch.where(flat < self.pos_of_row.numel(), p, torch.full_like(p, -1))
-            p_h = p.cpu().numpy()
-            lo = 0
+        # excluded store rows -> sorted positions per query (the host position map)
+        ptr = ex = None
+        if any(q.exclude_rows is not None and len(q.exclude_rows) for q in qs):
+            pmap = self.pos_of_row_h
+            ptr = np.zeros(nq + 1, dtype=np.int32)
             chunks = []
-            for j, e in enumerate(ex_parts):
-                pj = np.sort(p_h[lo:lo + len(e)])
-                pj = pj[pj >= 0].astype(np.int32)
-                lo += len(e)
+            for j, q in enumerate(qs):
+                er = q.exclude_rows
+                if er is not None and len(er):
+                    e = np.asarray(er, dtype=np.int64)
+                    e = e[(e >= 0) & (e < len(pmap))]
+                    pj = np.sort(pmap[e])
+                    pj = pj[pj >= 0].astype(np.int32)
+                else:
+                    pj = np.zeros(0, dtype=np.int32)
                 chunks.append(pj)
                 ptr[j + 1] = ptr[j] + len(pj)
-            ex_dev = torch.from_numpy(np.concatenate(chunks) if ptr[-1] else
-                                      np.zeros(1, dtype=np.int32)).to(dev)
-        return Q, rs, tile0, n_tiles, bits, ptr, ex_dev
+            ex = np.concatenate(chunks) if ptr[-1] else np.zeros(1, dtype=np.int32)
+        parts = [Q, rs, tile0] + [a for a in (bits, ptr, ex) if a is not None]
+        dev_parts = _upload(parts, self.device)
+        Qd, rs_d, t0_d = dev_parts[:3]
+        rest = iter(dev_parts[3:])
+        bits_d = next(rest) if bits is not None else None
+        ptr_d = next(rest) if ptr is not None else None
+        ex_d = next(rest) if ex is not None else None
+        return Qd, rs_d, t0_d, bits_d, ptr_d, ex_d, len(rs), n_tiles
 
     def _launch_fp32(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY):
         empty = (np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32))
@@ -480,24 +505,19 @@ class ItemIndex:
         prep = self._prep(qs, self.kp)
         if prep is None:
             return [empty for _ in qs]
-        Q, rs, tile0, n_tiles, bits, ptr, ex_dev = prep
+        Qd, rs_d, t0_d, bits_d, ptr_d, ex_d, n_ranges, n_tiles = prep
         waves = int(lib.oryx_topn_waves_kl(n_tiles, kl))
         o_sc = torch.empty((waves, nq, kl), dtype=torch.float32, device=dev)
         o_rw = torch.empty((waves, nq, kl), dtype=torch.int32, device=dev)
-        Qd = torch.from_numpy(Q).to(dev)
-        rs_d = torch.from_numpy(np.ascontiguousarray(rs, dtype=np.int64)).to(dev)
-        t0_d = torch.from_numpy(tile0).to(dev)
-        bits_d = torch.from_numpy(bits).to(dev) if bits is not None else None
-        ptr_d = torch.from_numpy(ptr).to(dev) if ex_dev is not None else None
         mat, ld, perm = self._matrix()
         rc = lib.oryx_topn_scan2(
             mat.data_ptr(), perm.data_ptr() if perm is not None else None, int(ld),
             Qd.data_ptr(), self.kp, nq, int(bool(cosine)), int(kl),
             self.bucket_of.data_ptr() if bits_d is not None else None,
             bits_d.data_ptr() if bits_d is not None else None, self.words, rs_d.data_ptr(),
-            t0_d.data_ptr(), len(rs), n_tiles,
+            t0_d.data_ptr(), n_ranges, n_tiles,
             ptr_d.data_ptr() if ptr_d is not None else None,
-            ex_dev.data_ptr() if ex_dev is not None else None,
+            ex_d.data_ptr() if ex_d is not None else None,
             o_sc.data_ptr(), o_rw.data_ptr(), native.stream_ptr(dev))
         native.check(rc, "oryx_topn_scan2")
         m = max(q.how_many for q in qs)
@@ -506,7 +526,8 @@ class ItemIndex:
         rw = o_rw.permute(1, 0, 2).reshape(nq, -1)
         v, i = torch.topk(sc, m, dim=1)
         pos = torch.gather(rw, 1, i)
-        v_h, pos_h = v.cpu().numpy(), pos.cpu().numpy()
+        h = torch.cat([v.view(torch.int32), pos], 1).cpu().numpy()     # one copy back
+        v_h, pos_h = h[:, :m].view(np.float32), h[:, m:]
         # (a row removed between the permutation and the launch is never returned)
         return [self._finish_one(v_h[j, :q.how_many], pos_h[j, :q.how_many])
                 for j, q in enumerate(qs)]
