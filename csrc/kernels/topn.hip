@@ -295,7 +295,13 @@ long long oryx_topn_waves_kl(long long n_tiles, int kl) {
   // ~8 tiles per wave at least; at most 8 waves per SIMD of 256 CUs for kl = 64, and at
   // least 2 per SIMD for the deep lists (their candidate output and final sorts grow with
   // kl; with 2 waves per CU the 1024-deep scan of 20M x 250 ran at half the bandwidth)
-  long long w = (n_tiles + 7) / 8;
+  // ORYX_TOPN_TILES_PER_WAVE overrides the 8 tiles per wave (tuning sweeps)
+  static const long long tpw = [] {
+    const char* e = getenv("ORYX_TOPN_TILES_PER_WAVE");
+    const long long v = e ? atoll(e) : 8;
+    return v > 0 ? v : 8;
+  }();
+  long long w = (n_tiles + tpw - 1) / tpw;
   long long cap = 256 * 4 * 8 / (kl / 64 > 0 ? kl / 64 : 1);
   if (cap < 2048) cap = 2048;
   if (w > cap) w = cap;
