@@ -31,6 +31,43 @@ import time
 import torch
 
 
+def _speed_latency(centers, counts, true_c, events: int, dev) -> dict:
+    """The k-means speed layer on the trained model: ``events`` new points (CSV lines from
+    the same mixture) per micro-batch, build + append of the cluster updates."""
+    import shutil
+    import tempfile
+    import numpy as np
+    from oryx_amd.api import Dataset
+    from oryx_amd.layers.speed import measure_intervals
+    from oryx_amd.models.kmeans.common import ClusterInfo
+    from oryx_amd.models.kmeans.speed import KMeansSpeedModel, KMeansSpeedModelManager
+    from oryx_amd.textlines import TextLines
+    from oryx_amd.transport.producer import LogTopicProducer
+    from oryx_amd.utils import config as cfg
+    k, d = centers.shape
+    conf = cfg.overlay_on({
+        "oryx.input-schema.feature-names": "[%s]" % ",".join('"f%d"' % j for j in range(d)),
+        "oryx.input-schema.categorical-features": "[]"}, cfg.get_default())
+    mgr = KMeansSpeedModelManager(conf)
+    c_h = centers.double().cpu().numpy()
+    n_h = counts.cpu().numpy()
+    mgr.model = KMeansSpeedModel([ClusterInfo(j, c_h[j], max(1, int(n_h[j])))
+                                  for j in range(k)], dev)
+    g = np.random.default_rng(11)
+    tc = true_c.cpu().numpy()
+    pts = tc[g.integers(0, k, events)] + g.standard_normal((events, d))
+    lines = [",".join("%.6f" % v for v in row) for row in pts]
+    ds = Dataset.from_values(TextLines.from_strings(lines))
+    logdir = tempfile.mkdtemp(prefix="oryx_bench_kmeans_speed_")
+    producer = LogTopicProducer("log:" + logdir, "OryxUpdate", async_=False,
+                                max_message=1 << 30)
+    try:
+        return measure_intervals(mgr, ds, producer, reps=12, warmup=2)
+    finally:
+        producer.close()
+        shutil.rmtree(logdir, ignore_errors=True)
+
+
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser(description=__doc__)
@@ -44,6 +81,9 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="auto")
     ap.add_argument("--precision", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--init", choices=["k-means||", "sample"], default="k-means||")
+    ap.add_argument("--speed-events", type=int, default=10_000,
+                    help="speed-layer micro-batch size timed against the trained centers "
+                         "(0: skip)")
     args = ap.parse_args(argv)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -117,6 +157,9 @@ def main(argv=None) -> int:
     st = km.CERT_STATS.get(dev)
     rescored = None if st is None else [v / args.steps for v in st.tolist()]
     info = dist.run_info(ctx)
+    speed = None
+    if ctx.is_main and args.speed_events > 0:
+        speed = _speed_latency(centers, counts, true_c, args.speed_events, dev)
     if ctx.is_main:
         print(json.dumps({
             "world_size": info["world_size"], "backend": info["backend"],
@@ -137,6 +180,14 @@ def main(argv=None) -> int:
             "tflops": 2.0 * n * W * k * d / (ms * 1e-3) / 1e12,
             "counted_points": total_counts, "empty_clusters_seen": empties,
             "init_ms": init_ms, "rescored_points_per_step": rescored,
+            "speed_layer_update_ms": speed["median_ms"] if speed else None,
+            "speed_layer_update_p90_ms": speed["p90_ms"] if speed else None,
+            "speed_layer_reps": speed["reps"] if speed else None,
+            "speed_layer_events": args.speed_events,
+            "speed_layer_messages": speed["messages"] if speed else None,
+            "speed_layer_path": "KMeansSpeedModelManager.build_updates against the trained "
+                                "centers + the UP messages' append to an update log, end to "
+                                "end (layers/speed.measure_intervals)",
         }), flush=True)
     if ctx.is_distributed:
         torch.distributed.destroy_process_group()

@@ -2931,3 +2931,121 @@ long long oryx_speed_assemble(void* h, long long lo, long long hi, const char* x
 }
 
 }  // extern "C"
+
+// ---- k-means speed-layer updates: [clusterID,[center...],count] lines with every double
+// written as Python's repr (json.dumps) writes it -- the shortest digits that round-trip,
+// fixed notation for decimal exponents -4..15, else d.ddde+XX -- so the native messages are
+// byte-identical to text.join_json's ([speed-app]/kmeans/KMeansSpeedModelManager.java:
+// 110-124 builds them per touched cluster).
+
+namespace {
+
+// Python repr of a finite double (json.dumps: NaN / Infinity for the others) at o; returns
+// the end.
+char* write_double_repr(double v, char* o) {
+  if (std::isnan(v)) { memcpy(o, "NaN", 3); return o + 3; }
+  if (std::isinf(v)) {
+    if (v < 0) *o++ = '-';
+    memcpy(o, "Infinity", 8);
+    return o + 8;
+  }
+  if (v == 0.0) {
+    if (std::signbit(v)) *o++ = '-';
+    memcpy(o, "0.0", 3);
+    return o + 3;
+  }
+  char buf[40];
+  // shortest round-trip digits in scientific form: [-]d[.ddd]e(+|-)XX
+  auto r = std::to_chars(buf, buf + sizeof(buf), v, std::chars_format::scientific);
+  const char* p = buf;
+  if (*p == '-') { *o++ = '-'; ++p; }
+  const char* e = static_cast<const char*>(memchr(p, 'e', (size_t)(r.ptr - p)));
+  char digits[24];
+  int nd = 0;
+  for (const char* q = p; q < e; ++q)
+    if (*q != '.') digits[nd++] = *q;
+  int exp10 = 0;
+  {
+    const char* q = e + 1;
+    const bool neg = *q == '-';
+    if (*q == '+' || *q == '-') ++q;
+    std::from_chars(q, r.ptr, exp10);
+    if (neg) exp10 = -exp10;
+  }
+  if (exp10 >= -4 && exp10 < 16) {
+    if (exp10 >= 0) {
+      for (int j = 0; j <= exp10; ++j) *o++ = j < nd ? digits[j] : '0';
+      *o++ = '.';
+      if (nd > exp10 + 1) {
+        for (int j = exp10 + 1; j < nd; ++j) *o++ = digits[j];
+      } else {
+        *o++ = '0';
+      }
+    } else {
+      *o++ = '0';
+      *o++ = '.';
+      for (int j = 0; j < -exp10 - 1; ++j) *o++ = '0';
+      for (int j = 0; j < nd; ++j) *o++ = digits[j];
+    }
+    return o;
+  }
+  *o++ = digits[0];
+  if (nd > 1) {
+    *o++ = '.';
+    for (int j = 1; j < nd; ++j) *o++ = digits[j];
+  }
+  *o++ = 'e';
+  *o++ = exp10 < 0 ? '-' : '+';
+  const int ax = exp10 < 0 ? -exp10 : exp10;
+  if (ax < 10) *o++ = '0';
+  char eb[8];
+  const int el = snprintf(eb, sizeof(eb), "%d", ax);
+  memcpy(o, eb, (size_t)el);
+  return o + el;
+}
+
+}  // namespace
+
+extern "C" {
+
+// n lines "[id,[c_0,...,c_{d-1}],count]" ('\n' after each) for the rows of centers [n][d];
+// ends[j] = end of line j (before its '\n').  Returns bytes, or -(bytes needed).
+long long oryx_format_cluster_updates(const long long* ids, const double* centers,
+                                      const long long* counts, long long n, int d, char* out,
+                                      long long cap, long long* ends) {
+  // a double takes at most 24 characters, an int64 20
+  const long long per = 2 + 21 + 2 + (long long)d * 25 + 2 + 21 + 2;
+  if (n * per > cap) return -(n * per);
+  std::vector<long long> len((size_t)n + 1, 0);
+  std::vector<std::string> lines((size_t)n);
+  oryx_ff::parallel_ranges(n, 64, [&](long long lo, long long hi, int) {
+    for (long long j = lo; j < hi; ++j) {
+      std::string& s = lines[(size_t)j];
+      s.resize((size_t)per);
+      char* o = &s[0];
+      *o++ = '[';
+      o += snprintf(o, 24, "%lld", ids[j]);
+      *o++ = ',';
+      *o++ = '[';
+      for (int f = 0; f < d; ++f) {
+        if (f) *o++ = ',';
+        o = write_double_repr(centers[j * d + f], o);
+      }
+      *o++ = ']';
+      *o++ = ',';
+      o += snprintf(o, 24, "%lld", counts[j]);
+      *o++ = ']';
+      s.resize((size_t)(o - &s[0]));
+    }
+  });
+  long long pos = 0;
+  for (long long j = 0; j < n; ++j) {
+    memcpy(out + pos, lines[(size_t)j].data(), lines[(size_t)j].size());
+    pos += (long long)lines[(size_t)j].size();
+    ends[j] = pos;
+    out[pos++] = '\n';
+  }
+  return pos;
+}
+
+}  // extern "C"

@@ -490,6 +490,29 @@ class DeferredUpBlock(_MessageBlock):
             ctypes.byref(n_msgs)))
 
 
+def format_cluster_updates(ids, centers, counts):
+    """k-means speed-layer update messages ``[id,[center...],count]`` (one per row of
+    ``centers`` [n, d] float64) as a :class:`~oryx_amd.api.MessageBlock`, byte-identical to
+    ``text.join_json([id, [float(v) ...], count])`` (native, threaded)."""
+    from .api import MessageBlock
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    centers = np.ascontiguousarray(centers, dtype=np.float64)
+    counts = np.ascontiguousarray(counts, dtype=np.int64)
+    n = len(ids)
+    if n == 0:
+        return MessageBlock(b"", np.zeros(0, dtype=np.int64))
+    d = centers.shape[1]
+    ends = np.empty(n, dtype=np.int64)
+    cap = n * (52 + 25 * d)
+    while True:
+        out = np.empty(cap, dtype=np.uint8)
+        used = native.runtime().oryx_format_cluster_updates(
+            _ptr(ids), _ptr(centers), _ptr(counts), n, d, _ptr(out), cap, _ptr(ends))
+        if used >= 0:
+            return MessageBlock(out[:used], ends)
+        cap = -used
+
+
 def parse_up_batch(messages: Sequence[str], k: int, known_dict: Optional["IdDict"] = None):
     """Bulk-parse ALS ``UP`` messages ``["X"|"Y", id, [k floats], [known ids]?]``.
 

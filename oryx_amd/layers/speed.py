@@ -28,7 +28,7 @@ from ..utils import config as cfg
 from ..utils import lang
 from .common import AbstractLayer, IntervalTimer, drain_dataset
 
-__all__ = ["SpeedLayer"]
+__all__ = ["SpeedLayer", "measure_intervals", "publish_blocks"]
 
 log = logging.getLogger(__name__)
 
@@ -83,6 +83,44 @@ def publish_blocks(producer, blocks, stats: Optional[dict] = None) -> int:
     if errors:
         raise errors[0]
     return sent
+
+def measure_intervals(manager, dataset: Dataset, producer, reps: int = 12, warmup: int = 2,
+                      gap_s: float = 0.05) -> dict:
+    """The speed layer's per-interval latency for one micro-batch, as :meth:`SpeedLayer.
+    run_interval` spends it: the manager's update build plus the append of every update to
+    ``producer`` (the update log), timed end to end over ``reps`` repetitions after
+    ``warmup`` (``gap_s`` idle between, as between intervals).  Returns median / p90 ms, the
+    per-rep times and the messages per interval (the benchmarks' speed-layer records)."""
+    import numpy as np
+    times = []
+    sent = 0
+    dev = getattr(manager, "device", None)
+    for rep in range(warmup + reps):
+        time.sleep(gap_s)
+        try:
+            import torch
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+        except ImportError:     # pragma: no cover
+            pass
+        t0 = time.perf_counter()
+        blocks = getattr(manager, "build_update_blocks", None)
+        if blocks is not None:
+            sent = publish_blocks(producer, blocks(dataset))
+        else:
+            updates = manager.build_updates(dataset)
+            if isinstance(updates, MessageBlock):
+                producer.send_block("UP", updates)
+            elif updates:
+                producer.send_many(("UP", u) for u in updates)
+            sent = len(updates) if updates is not None else 0
+        producer.flush()
+        if rep >= warmup:
+            times.append((time.perf_counter() - t0) * 1e3)
+    del dev
+    return {"median_ms": float(np.median(times)), "p90_ms": float(np.percentile(times, 90)),
+            "reps": reps, "times_ms": times, "messages": int(sent)}
+
 
 class SpeedLayer(AbstractLayer):
     layer_name = "SpeedLayer"

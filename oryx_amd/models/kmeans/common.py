@@ -251,6 +251,44 @@ class ClusterSet:
                 self._dev_version = self._version
             return self._dev_centers
 
+    def device_state(self) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """(centers fp64 [k, d], centers feature-major fp64 [d, k], counts int64 [k]) on the
+        device, rebuilt when the clusters changed."""
+        with self._lock:
+            st = getattr(self, "_dev_state", None)
+            if st is None or st[0] != self._version:
+                c = self._device_centers()
+                cnt = torch.tensor([ci.count for ci in self.clusters], dtype=torch.int64,
+                                   device=self.device)
+                st = (self._version, c, c.t().contiguous(), cnt)
+                self._dev_state = st
+            return st[1], st[2], st[3]
+
+    def set_many(self, positions: Sequence[int], centers: np.ndarray,
+                 counts: Sequence[int]) -> None:
+        """Replace the centers and counts of the clusters at ``positions`` (one version bump)."""
+        with self._lock:
+            for j, pos in enumerate(positions):
+                old = self.clusters[pos]
+                info = ClusterInfo(old.id, centers[j], int(counts[j]))
+                self.clusters[pos] = info
+            self._version += 1
+
+    def nearest_batch_device(self, x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(positions int64 [n], distances fp64 [n]) of device points ``x`` fp64 [n, d] by the
+        exact fp64 kernel (``oryx_kmeans_nearest_f64``, csrc/kernels/kmeans_speed.hip)."""
+        from ... import native
+        _, ct, _ = self.device_state()
+        x = x.to(torch.float64).contiguous()
+        n, d = x.shape
+        idx = torch.empty(n, dtype=torch.int64, device=x.device)
+        dist = torch.empty(n, dtype=torch.float64, device=x.device)
+        rc = native.require_kernels().oryx_kmeans_nearest_f64(
+            x.data_ptr(), n, d, ct.data_ptr(), int(ct.shape[1]), idx.data_ptr(),
+            dist.data_ptr(), native.stream_ptr(x.device))
+        native.check(rc, "oryx_kmeans_nearest_f64")
+        return idx, dist
+
     def nearest_batch(self, x: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
         """(positions int64 [n], Euclidean distances float64 [n]) for points ``x``.
 

@@ -20,8 +20,10 @@ from typing import List, Optional
 import numpy as np
 import torch
 
+from ... import ingest, native
 from ...api import Dataset, SpeedModel, SpeedModelManager
 from ...utils import pmml as pmmlu, text
+from ..features import parse_features
 from ..schema import InputSchema
 from .common import ClusterSet, parse_feature_matrix, read_clusters, validate_pmml_vs_schema
 
@@ -79,6 +81,10 @@ class KMeansSpeedModelManager(SpeedModelManager):
         model = self.model
         if model is None:
             return []
+        cs = model.clusters
+        if (cs.device is not None and cs.device.type == "cuda" and native.kernels_available()
+                and 0 < self.input_schema.get_num_predictors() <= 1024):
+            return self._build_updates_device(new_data)
         x = parse_feature_matrix(new_data.values(), self.input_schema)
         if len(x) == 0:
             return []
@@ -94,6 +100,44 @@ class KMeansSpeedModelManager(SpeedModelManager):
             model.set_cluster(pos, info)
             out.append(text.join_json([info.id, [float(v) for v in info.center], info.count]))
         return out
+
+    def _build_updates_device(self, new_data: Dataset):
+        """The GPU path: the micro-batch parsed natively straight to a device fp64 matrix
+        (models/features.parse_features), nearest clusters by the exact fp64 kernel,
+        per-cluster sums / counts by index_add / bincount, the running means of the touched
+        clusters (ClusterInfo.update's formula, vectorised), and the messages formatted
+        natively (ingest.format_cluster_updates: the same bytes as text.join_json) in one
+        MessageBlock."""
+        from ...textlines import TextLines
+        cs = self.model.clusters
+        lines = new_data.values()
+        if not isinstance(lines, TextLines):
+            lines = TextLines.from_strings([str(v) for v in lines])
+        if len(lines) == 0:
+            return []
+        block = parse_features(lines, self.input_schema, cs.device, torch.float64)
+        x = block.predictors(self.input_schema)
+        if x.shape[0] == 0:
+            return []
+        idx, _ = cs.nearest_batch_device(x)
+        centers, _, counts = cs.device_state()
+        k, d = centers.shape
+        sums = torch.zeros((k, d), dtype=torch.float64, device=x.device)
+        sums.index_add_(0, idx, x.to(torch.float64))
+        n_new = torch.bincount(idx, minlength=k)
+        touched = torch.nonzero(n_new).flatten()
+        nt = n_new[touched]
+        total = nt + counts[touched]
+        c = centers[touched]
+        mean = sums[touched] / nt[:, None].to(torch.float64)
+        frac = nt.to(torch.float64) / total.to(torch.float64)
+        new_c = c + frac[:, None] * (mean - c)
+        pos_h = touched.cpu().numpy()
+        new_h = new_c.cpu().numpy()
+        tot_h = total.cpu().numpy()
+        cs.set_many(pos_h.tolist(), new_h, tot_h.tolist())
+        ids = np.array([cs.clusters[p].id for p in pos_h.tolist()], dtype=np.int64)
+        return ingest.format_cluster_updates(ids, new_h, tot_h)
 
     def close(self) -> None:
         pass

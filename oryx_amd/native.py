@@ -129,6 +129,8 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_speed_assemble", c_ll, [c_vp, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_vp, c_i, c_vp, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_rowmap_key_suffixes", c_ll, [c_vp, c_vp, c_ll])
+    _sig(lib, "oryx_format_cluster_updates", c_ll, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_ll,
+                                                    c_vp])
     _sig(lib, "oryx_http_start", c_vp, [c_cp, c_i, c_i, c_ll])
     _sig(lib, "oryx_http_port", c_i, [c_vp])
     _sig(lib, "oryx_http_served", c_ll, [c_vp])
@@ -233,6 +235,7 @@ def _load_kernels():
         _sig(lib, "oryx_als_debug_gram", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_f, c_i, c_ll,
                                                c_ll, c_vp, c_i, c_vp])
     _sig(lib, "oryx_gramian_f32", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_kmeans_nearest_f64", c_i, [c_vp, c_ll, c_i, c_vp, c_i, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_spd_inverse_pair", c_i, [c_vp, c_vp, c_i, c_vp, c_vp, ctypes.c_double,
                                              c_vp, c_vp])
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])

@@ -309,6 +309,49 @@ def test_speed_manager_running_mean():
     assert got[2] == [2, [-1.5, 0.0], 4]
 
 
+@pytest.mark.gpu
+def test_speed_manager_device_path_matches_host(cuda):
+    """The GPU speed path (native parse to a device fp64 matrix, exact fp64 nearest-center
+    kernel, index_add sums, vectorised running means, native message formatting) gives the
+    golden running-mean example exactly, and on 20k random points over 300 clusters x 64
+    dims the same touched clusters, counts and centers (to summation order) as the host
+    path; the model's clusters end up updated alike."""
+    import json
+    from oryx_amd.models.kmeans.speed import KMeansSpeedModel
+    conf = _conf(**{"oryx__input-schema__feature-names": '["x","y"]',
+                    "oryx__input-schema__categorical-features": "[]"})
+    mgr = KMeansSpeedModelManager(conf)
+    mgr.consume(iter([KeyMessage("MODEL", pm.to_string(dummy_pmml()))]))
+    assert mgr.model.clusters.device.type == "cuda"
+    ups = mgr.build_updates(Dataset([(None, "1,1"), (None, "3,-1"), (None, "-3,0")]))
+    got = [json.loads(u) for u in ups]
+    assert got[0] == [0, [1.0, 0.5], 2] and got[2] == [2, [-1.5, 0.0], 4]
+    assert got[1][0] == 1 and got[1][2] == 3
+    assert got[1][1] == pytest.approx([2 + 1 / 3, -1.0])
+    g = np.random.default_rng(3)
+    k, d, n = 300, 64, 20000
+    names = "[%s]" % ",".join('"f%d"' % j for j in range(d))
+    conf = _conf(**{"oryx__input-schema__feature-names": names,
+                    "oryx__input-schema__categorical-features": "[]"})
+    centers = g.standard_normal((k, d)) * 3
+    pts = centers[g.integers(0, k, n)] + g.standard_normal((n, d))
+    lines = [",".join(repr(float(v)) for v in row) for row in pts]
+    outs = []
+    for device in (torch.device(cuda), None):
+        m = KMeansSpeedModelManager(conf)
+        m.model = KMeansSpeedModel([ClusterInfo(10 + j, centers[j], 1 + j % 7)
+                                    for j in range(k)], device)
+        if device is None:
+            m.model.clusters.device = None
+        outs.append([json.loads(u) for u in m.build_updates(Dataset([(None, l)
+                                                                       for l in lines]))])
+    dev, host = outs
+    assert [u[0] for u in dev] == [u[0] for u in host]
+    assert [u[2] for u in dev] == [u[2] for u in host]
+    np.testing.assert_allclose(np.array([u[1] for u in dev]), np.array([u[1] for u in host]),
+                               rtol=1e-12, atol=1e-12)
+
+
 # ---------------------------------------------------------------- serving
 
 def _test_model():
