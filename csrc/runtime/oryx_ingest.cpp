@@ -3049,3 +3049,56 @@ long long oryx_format_cluster_updates(const long long* ids, const double* center
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// RDF speed-layer updates for n touched leaves ([speed-app]/rdf/RDFSpeedModelManager.java:
+// 112-151): classification (nc > 0) '[tree,ID,{"c":count,...}]' over the classes with a
+// nonzero count (counts [n][nc]), regression (nc == 0) '[tree,ID,mean,count]' (means [n],
+// counts [n]); ID = leaf_ids' pre-quoted JSON text of leaf j (idx[j] into the blob).  Lines
+// '\n'-separated, ends[j] before the '\n'.  Returns bytes, or -(bytes needed).
+long long oryx_format_leaf_updates(long long n, const long long* trees, const char* id_blob,
+                                   const long long* id_ends, const long long* idx,
+                                   const long long* counts, int nc, const double* means,
+                                   char* out, long long cap, long long* ends) {
+  long long need = 0;
+  for (long long j = 0; j < n; ++j) {
+    const long long k = idx[j];
+    const long long il = id_ends[k] - (k ? id_ends[k - 1] : 0);
+    need += 2 * 21 + il + 8 + (nc > 0 ? (long long)nc * 46 : 24 + 21) + 1;
+  }
+  if (need > cap) return -need;
+  char* o = out;
+  for (long long j = 0; j < n; ++j) {
+    const long long k = idx[j];
+    const long long ib = k ? id_ends[k - 1] : 0;
+    *o++ = '[';
+    o += snprintf(o, 24, "%lld", trees[j]);
+    *o++ = ',';
+    memcpy(o, id_blob + ib, (size_t)(id_ends[k] - ib));
+    o += id_ends[k] - ib;
+    *o++ = ',';
+    if (nc > 0) {
+      *o++ = '{';
+      bool first = true;
+      for (int c = 0; c < nc; ++c) {
+        const long long v = counts[j * nc + c];
+        if (!v) continue;
+        if (!first) *o++ = ',';
+        first = false;
+        o += snprintf(o, 48, "\"%d\":%lld", c, v);
+      }
+      *o++ = '}';
+    } else {
+      o = write_double_repr(means[j], o);
+      *o++ = ',';
+      o += snprintf(o, 24, "%lld", counts[j]);
+    }
+    *o++ = ']';
+    ends[j] = o - out;
+    *o++ = '\n';
+  }
+  return o - out;
+}
+
+}  // extern "C"

@@ -490,6 +490,35 @@ class DeferredUpBlock(_MessageBlock):
             ctypes.byref(n_msgs)))
 
 
+def format_leaf_updates(trees, id_blob, id_ends, idx, counts, nc: int, means=None):
+    """RDF speed-layer update messages as a :class:`~oryx_amd.api.MessageBlock` (native):
+    classification (``nc`` > 0, ``counts`` [n, nc]) ``[tree,ID,{"c":count,...}]`` over the
+    nonzero classes, regression (``nc`` == 0, ``means`` / ``counts`` [n])
+    ``[tree,ID,mean,count]``; ``ID`` = entry ``idx[j]`` of the pre-quoted JSON ID blob."""
+    from .api import MessageBlock
+    trees = np.ascontiguousarray(trees, dtype=np.int64)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    counts = np.ascontiguousarray(counts, dtype=np.int64)
+    id_ends = np.ascontiguousarray(id_ends, dtype=np.int64)
+    n = len(trees)
+    if n == 0:
+        return MessageBlock(b"", np.zeros(0, dtype=np.int64))
+    mp = None
+    if means is not None:
+        means = np.ascontiguousarray(means, dtype=np.float64)
+        mp = _ptr(means)
+    ends = np.empty(n, dtype=np.int64)
+    cap = 1 << 16
+    while True:
+        out = np.empty(cap, dtype=np.uint8)
+        used = native.runtime().oryx_format_leaf_updates(
+            n, _ptr(trees), _buf_ptr(id_blob), _ptr(id_ends), _ptr(idx), _ptr(counts), int(nc),
+            mp, _ptr(out), cap, _ptr(ends))
+        if used >= 0:
+            return MessageBlock(out[:used], ends)
+        cap = -used
+
+
 def format_cluster_updates(ids, centers, counts):
     """k-means speed-layer update messages ``[id,[center...],count]`` (one per row of
     ``centers`` [n, d] float64) as a :class:`~oryx_amd.api.MessageBlock`, byte-identical to

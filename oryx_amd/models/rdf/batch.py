@@ -57,10 +57,19 @@ def parse_csv_block(lines: Sequence[str], schema: InputSchema,
     lines (no JSON arrays, no quoting): one C-level CSV parse (pandas) with numeric columns
     read straight to float64.  Returns ``(X, target, full)`` or None when the block does not
     qualify (the caller then takes the general path)."""
-    if not lines:
+    if not len(lines):
         return None
-    blob = "\n".join(lines)
+    from ...textlines import TextLines
     F = schema.get_num_features()
+    if isinstance(lines, TextLines):
+        # the buffer as drained: parsed in place (no per-line strings)
+        buf = lines.joined()
+        data = buf.tobytes() if isinstance(buf, np.ndarray) else bytes(buf)
+        full = _native_csv_block(data, len(lines), schema, encodings, F)
+        if full is not None:
+            return _split_full(full, schema)
+        lines = list(lines)
+    blob = "\n".join(lines)
     # the native parser rejects quotes, backslashes and JSON-array lines itself
     full = _native_csv_block(blob, len(lines), schema, encodings, F)
     if full is not None:
@@ -115,14 +124,14 @@ def _split_full(full: np.ndarray, schema: InputSchema):
     return X, target, full
 
 
-def _native_csv_block(blob: str, n: int, schema: InputSchema,
+def _native_csv_block(blob, n: int, schema: InputSchema,
                       encodings: CategoricalValueEncodings, F: int) -> Optional[np.ndarray]:
     """The block through the native threaded CSV parser (``oryx_csv_numeric_block``: exact
     fast-path doubles, categorical fields as spans mapped here); None when a line does not
     qualify or a value is unknown (the pandas / general path then decides)."""
     from ... import native
     import ctypes
-    data = blob.encode("utf-8")
+    data = blob if isinstance(blob, bytes) else blob.encode("utf-8")
     is_num = np.array([1 if schema.is_numeric(fi) else 0 for fi in range(F)], dtype=np.uint8)
     full = np.empty((n, F), dtype=np.float64)
     # spans are written for every non-numeric field (numeric entries stay unused)

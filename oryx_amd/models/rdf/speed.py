@@ -18,6 +18,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 import torch
 
+from ... import ingest
 from ...api import Dataset, SpeedModel, SpeedModelManager
 from ...ops import rdf as rdf_ops
 from ...utils import pmml as pmmlu, text
@@ -51,6 +52,12 @@ class RDFSpeedModel(SpeedModel):
     def flat(self, device, num_classes):
         if self._flat is None:
             self._flat = rdf_ops.flatten_forest(self.forest, device, num_classes)
+            # per flat node: its tree and its ID as JSON text (the update messages' fields)
+            roots = self._flat.roots.cpu().numpy().astype(np.int64)
+            n = len(self._flat.nodes)
+            self.tree_of = np.searchsorted(roots, np.arange(n), side="right") - 1
+            self.id_blob, self.id_ends = ingest.strings_blob(
+                [json.dumps(nd.get_id()) for nd in self._flat.nodes])
         return self._flat
 
     def get_fraction_loaded(self) -> float:
@@ -87,8 +94,8 @@ class RDFSpeedModelManager(SpeedModelManager):
         if model is None:
             return []
         schema = self.input_schema
-        values = list(new_data.values())
-        if not values:
+        values = new_data.values()
+        if not len(values):
             return []
         parsed = parse_csv_block(values, schema, model.encodings)
         if parsed is None:
@@ -98,6 +105,8 @@ class RDFSpeedModelManager(SpeedModelManager):
         C = model.encodings.get_value_count(schema.get_target_feature_index()) \
             if schema.is_classification() else 0
         flat = model.flat(self.device, C)
+        if self.device.type == "cuda":
+            return self._updates_device(model, flat, full, target, C)
         leaves = rdf_ops.forest_leaves(flat, torch.from_numpy(full).to(self.device)).cpu() \
             .numpy()                                             # [n, T]
         has_target = ~np.isnan(target)
@@ -134,6 +143,41 @@ class RDFSpeedModelManager(SpeedModelManager):
                 out.append(json.dumps([trees[j], flat.nodes[leaf].get_id(), means[j],
                                        int(counts[j])], separators=(",", ":")))
         return out
+
+    def _updates_device(self, model, flat, full, target, C: int):
+        """Leaves by the traversal kernel, per-(leaf, class) counts (or per-leaf sums) by one
+        bincount on the device, the touched leaves' messages formatted natively
+        (``ingest.format_leaf_updates``): one MessageBlock."""
+        dev = self.device
+        X = torch.from_numpy(np.ascontiguousarray(full)).to(dev)
+        leaves = rdf_ops.forest_leaves(flat, X)                      # [n, T] int64
+        tv = torch.from_numpy(np.ascontiguousarray(target)).to(dev)
+        ok = ~torch.isnan(tv)
+        leaves, tv = leaves[ok], tv[ok]
+        if leaves.numel() == 0:
+            return []
+        n_nodes = len(flat.nodes)
+        T = leaves.shape[1]
+        if C > 0:
+            cls = tv.to(torch.int64).clamp(0, C - 1)
+            key = (leaves * C + cls[:, None]).reshape(-1)
+            cnt = torch.bincount(key, minlength=n_nodes * C).view(n_nodes, C)
+            touched = torch.nonzero(cnt.sum(1)).flatten()
+            t_h = touched.cpu().numpy()
+            c_h = cnt[touched].cpu().numpy()
+            return ingest.format_leaf_updates(model.tree_of[t_h], model.id_blob,
+                                              model.id_ends, t_h, c_h, C)
+        flat_leaf = leaves.reshape(-1)
+        vals = tv[:, None].expand(-1, T).reshape(-1)
+        cnt = torch.bincount(flat_leaf, minlength=n_nodes)
+        sums = torch.zeros(n_nodes, dtype=torch.float64, device=dev).index_add_(0, flat_leaf,
+                                                                                vals)
+        touched = torch.nonzero(cnt).flatten()
+        t_h = touched.cpu().numpy()
+        n_h = cnt[touched].cpu().numpy()
+        m_h = (sums[touched] / cnt[touched].to(torch.float64)).cpu().numpy()
+        return ingest.format_leaf_updates(model.tree_of[t_h], model.id_blob, model.id_ends,
+                                          t_h, n_h, 0, m_h)
 
     def close(self) -> None:
         pass

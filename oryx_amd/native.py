@@ -129,6 +129,8 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_speed_assemble", c_ll, [c_vp, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_vp, c_i, c_vp, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_rowmap_key_suffixes", c_ll, [c_vp, c_vp, c_ll])
+    _sig(lib, "oryx_format_leaf_updates", c_ll, [c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_i,
+                                                 c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_format_cluster_updates", c_ll, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_ll,
                                                     c_vp])
     _sig(lib, "oryx_http_start", c_vp, [c_cp, c_i, c_i, c_ll])

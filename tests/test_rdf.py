@@ -374,6 +374,36 @@ def test_speed_manager_leaf_updates():
     serving.consume(iter([KeyMessage(k, m)] + [KeyMessage("UP", json.dumps(u)) for u in ups]))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("classification", [True, False])
+def test_speed_manager_device_path_matches_host(cuda, classification):
+    """The GPU speed path (leaf kernel, one device bincount, native message formatting)
+    emits the same updates in the same order as the host path, from a TextLines buffer."""
+    from oryx_amd.textlines import TextLines
+    conf = _rdf_conf(classification, trees=3)
+    upd = RDFUpdate(conf)
+    MockTopicProducer.clear()
+    upd.run_update(None, 1, Dataset([(None, l) for l in _lines(800, classification)]), None,
+                   "/tmp/rdfm_dev", MockTopicProducer())
+    (k, m), = MockTopicProducer.get_key_messages()
+    lines = _lines(300, classification, 9)
+    outs = []
+    for device in (torch.device(cuda), torch.device("cpu")):
+        mgr = RDFSpeedModelManager(conf)
+        mgr.device = device
+        mgr.consume(iter([KeyMessage(k, m)]))
+        outs.append([json.loads(u) for u in mgr.build_updates(
+            Dataset.from_values(TextLines.from_strings(lines)))])
+    dev, host = outs
+    assert len(dev) == len(host) > 0
+    for a, b in zip(dev, host):
+        assert a[:2] == b[:2]
+        if classification:
+            assert a[2] == b[2]
+        else:
+            assert a[3] == b[3] and a[2] == pytest.approx(b[2], rel=1e-12)
+
+
 # ---------------------------------------------------------------- GPU kernels
 
 @pytest.mark.gpu
