@@ -220,6 +220,8 @@ def time_to_ready(items: int, users: int, features: int, seed: int) -> dict:
             hi = min(items, lo + chunk)
             topic.append_block(ingest.assemble_row_messages(
                 "Y", item_ids[lo:hi], ingest.format_float_rows_blob(Y[lo:hi])), key="UP")
+            print("time_to_ready: log %d / %d item rows" % (hi, items), file=sys.stderr,
+                  flush=True)
         pos = np.r_[0, np.cumsum(counts)]
         names = ingest.IdDict()
         names.encode(["I%d" % i for i in range(items)])
@@ -258,6 +260,9 @@ def time_to_ready(items: int, users: int, features: int, seed: int) -> dict:
                     break
                 if time.perf_counter() - t0 > 3000:
                     raise TimeoutError("model not loaded")
+                if int((time.perf_counter() - t0) * 50) % 500 == 0:
+                    print("time_to_ready: loading, %.0f s" % (time.perf_counter() - t0),
+                          file=sys.stderr, flush=True)
                 time.sleep(0.02)
             ready_s = time.perf_counter() - t0
             # first query also pushes the matrix to HBM and builds the scan index
