@@ -125,38 +125,94 @@ def main(argv=None) -> int:
                 r.read()
                 return r.status
 
-            lat = []
-            timeouts = 0
+            # the update log, read from its end before each trial: the speed layer's UP
+            # for the trial's user tells a published update (then: is it in the serving
+            # model yet?) from a micro-batch that produced none for the user (a no-op
+            # fold-in: the implicit target moved nothing, e.g. Xu.Yi already >= 1)
+            upd_topic = tlog.Topic(root, "OryxUpdate")
+            in_topic = tlog.Topic(root, "OryxInput")
+            lat, up_lat, vis_lat = [], [], []
+            timeouts = noops = unchanged_lists = 0
             for trial in range(args.trials + 3):
                 u = "U%d" % int(g.integers(args.users))
                 i = "I%d" % int(g.integers(args.items))
                 st, before = get("/recommend/%s?howMany=10" % u)
                 assert st == 200, st
+                reader = upd_topic.reader(0, upd_topic.end_offset(0))
+                in_end = in_topic.end_offset(0)
                 t_send = time.perf_counter()
                 assert post("/ingest", ("%s,%s,5\n" % (u, i)).encode()) in (200, 204)
-                seen = None
+                seen = t_up = t_vis = None
+                up_vec = None
+                runs_at_input = None
                 while time.perf_counter() - t_send < 10.0:
-                    st, now = get("/recommend/%s?howMany=10" % u)
-                    if now != before:
-                        seen = time.perf_counter()
+                    if runs_at_input is None and in_topic.end_offset(0) > in_end:
+                        runs_at_input = speed.intervals_run   # the rating is in the input log
+                    if up_vec is None:
+                        for _, _, key, msg in reader.poll(4096, 0):
+                            if key == "UP" and msg.startswith('["X","%s",' % u):
+                                up_vec = np.asarray(json.loads(msg)[2], dtype=np.float32)
+                                t_up = time.perf_counter()
+                    if up_vec is not None and t_vis is None:
+                        cur = serving.manager.get_model().get_user_vector(u)
+                        if cur is not None and np.array_equal(np.asarray(cur, np.float32),
+                                                              up_vec):
+                            t_vis = time.perf_counter()
+                    if seen is None:
+                        st, now = get("/recommend/%s?howMany=10" % u)
+                        if now != before:
+                            seen = time.perf_counter()
+                    if seen is not None and t_vis is not None:
                         break
-                if seen is None:
-                    timeouts += 1
-                elif trial >= 3:
+                    # two intervals past the one that drained the rating and still no UP
+                    # for the user: the fold-in was a no-op
+                    if up_vec is None and runs_at_input is not None and \
+                            speed.intervals_run >= runs_at_input + 2:
+                        for _, _, key, msg in reader.poll(4096, 0):
+                            if key == "UP" and msg.startswith('["X","%s",' % u):
+                                up_vec = np.asarray(json.loads(msg)[2], dtype=np.float32)
+                                t_up = time.perf_counter()
+                        if up_vec is None:
+                            break
+                    time.sleep(0.0005)
+                reader.close()
+                if up_vec is None:
+                    noops += runs_at_input is not None
+                    timeouts += runs_at_input is None
+                    continue
+                if trial < 3:
+                    continue
+                up_lat.append((t_up - t_send) * 1e3)
+                if t_vis is not None:
+                    vis_lat.append((t_vis - t_send) * 1e3)
+                else:
+                    timeouts += 1                 # published but never applied: lost
+                if seen is not None:
                     lat.append((seen - t_send) * 1e3)
+                else:
+                    unchanged_lists += 1          # applied, but the top 10 did not change
+            upd_topic.close()
+            in_topic.close()
             conn.close()
         finally:
             stop.set()
             speed.close()
             serving.close()
+        vis_a = np.asarray(vis_lat)
+        up_a = np.asarray(up_lat)
         lat_a = np.asarray(lat)
+        pct = lambda a, q: float(np.percentile(a, q)) if len(a) else None
         print(json.dumps({
-            "metric": "ingest -> visible latency (POST /ingest -> speed UP -> /recommend "
-                      "changes)",
-            "p50_ms": float(np.percentile(lat_a, 50)) if len(lat) else None,
-            "p90_ms": float(np.percentile(lat_a, 90)) if len(lat) else None,
-            "max_ms": float(lat_a.max()) if len(lat) else None,
-            "trials": len(lat), "timeouts": timeouts, "interval_ms": args.interval_ms,
+            "metric": "ingest -> visible latency (POST /ingest -> speed UP -> the serving "
+                      "model holds the user's new vector)",
+            "p50_ms": pct(vis_a, 50), "p90_ms": pct(vis_a, 90),
+            "max_ms": float(vis_a.max()) if len(vis_a) else None,
+            "ingest_to_up_in_log_p50_ms": pct(up_a, 50), "ingest_to_up_in_log_p90_ms":
+                pct(up_a, 90),
+            "recommend_changed_p50_ms": pct(lat_a, 50), "recommend_changed_p90_ms":
+                pct(lat_a, 90),
+            "trials": len(vis_lat), "noop_foldins": noops, "lost_or_timeouts": timeouts,
+            "applied_but_top10_unchanged": unchanged_lists, "interval_ms": args.interval_ms,
             "items": args.items, "users": args.users, "features": k,
             "model_load_s": load_s,
             "path": "HTTP POST /ingest -> input log (async producer) -> speed layer micro-batch "
