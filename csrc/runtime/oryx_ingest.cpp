@@ -1199,6 +1199,61 @@ long long oryx_rowmap_translate(void* h, void* dh, long long* out) {
 // straight into its rows).  Returns the row count, or -(line + 1) of the first line that is
 // not plain CSV with F fields (a quote, a backslash or a leading '[' included) or has an
 // unparseable numeric field (the caller then takes the general path).
+}  // extern "C"
+
+namespace {
+
+// A plain decimal field at p ("[-+]digits[.digits][e[-+]digits]", at most 19 significant
+// digits, a value exactly representable by the one-rounding product D * 10^e) ending at ','
+// or lend: the value and the field's end; nullptr when the field needs the general parser
+// (oryx_ff::parse_double) -- more digits, exponents beyond 10^22, other characters.  Found
+// in the same pass that parses it: no per-field memchr.
+inline const char* fast_decimal_field(const char* p, const char* lend, double& out) {
+  static const double kP10[] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  const char* q = p;
+  bool neg = false;
+  if (q < lend && (*q == '-' || *q == '+')) neg = *q++ == '-';
+  uint64_t D = 0;
+  int nd = 0, frac = 0;
+  while (q < lend && (unsigned)(*q - '0') < 10u) {
+    D = D * 10 + (uint64_t)(*q++ - '0');
+    ++nd;
+  }
+  if (q < lend && *q == '.') {
+    ++q;
+    while (q < lend && (unsigned)(*q - '0') < 10u) {
+      D = D * 10 + (uint64_t)(*q++ - '0');
+      ++nd;
+      ++frac;
+    }
+  }
+  if (nd == 0 || nd > 19) return nullptr;
+  int e10 = -frac;
+  if (q < lend && (*q == 'e' || *q == 'E')) {
+    ++q;
+    bool eneg = false;
+    if (q < lend && (*q == '-' || *q == '+')) eneg = *q++ == '-';
+    int x = 0, ne = 0;
+    while (q < lend && (unsigned)(*q - '0') < 10u && ne < 4) {
+      x = x * 10 + (*q++ - '0');
+      ++ne;
+    }
+    if (!ne) return nullptr;
+    e10 += eneg ? -x : x;
+  }
+  if (q < lend && *q != ',') return nullptr;
+  if (D > (1ull << 53) || e10 < -22 || e10 > 22) return nullptr;
+  const double v = e10 < 0 ? (double)D / kP10[-e10] : (double)D * kP10[e10];
+  out = neg ? -v : v;
+  return q;
+}
+
+}  // namespace
+
+extern "C" {
+
 long long oryx_csv_numeric_block(const char* buf, long long len, int F,
                                  const unsigned char* is_num, double* out, long long* span_off,
                                  int* span_len, long long max_rows) {
@@ -1246,11 +1301,21 @@ long long oryx_csv_numeric_block(const char* buf, long long len, int F,
           const char* q = p;
           int f = 0;
           // JSON-array lines and backslash escapes belong to the general parser
-          bool ok = *p != '[' && !memchr(p, '\\', (size_t)(lend - p));
+          bool ok = *p != '[' && !memchr(p, '\\', (size_t)(lend - p)) &&
+                    !memchr(p, '"', (size_t)(lend - p));
           while (ok) {
+            if (f < F && is_num[f]) {
+              const char* fe = fast_decimal_field(q, lend, o[f]);
+              if (fe) {
+                ++f;
+                if (fe >= lend) break;
+                q = fe + 1;
+                continue;
+              }
+            }
             const char* c = static_cast<const char*>(memchr(q, ',', (size_t)(lend - q)));
             const char* fe = c ? c : lend;
-            if (f >= F || memchr(q, '"', (size_t)(fe - q))) { ok = false; break; }
+            if (f >= F) { ok = false; break; }
             if (is_num[f]) {
               if (fe == q) o[f] = std::numeric_limits<double>::quiet_NaN();
               else if (!oryx_ff::parse_double(q, fe, o[f])) ok = false;
@@ -1334,11 +1399,23 @@ long long csv_to_matrix(const char* buf, long long len, int F, const unsigned ch
           T* o = out + row * P;
           const char* q = p;
           int f = 0;
-          bool ok = *p != '[' && !memchr(p, '\\', (size_t)(lend - p));
+          bool ok = *p != '[' && !memchr(p, '\\', (size_t)(lend - p)) &&
+                    !memchr(p, '"', (size_t)(lend - p));
           while (ok) {
+            if (f < F && is_num[f]) {
+              double v;
+              const char* fe = fast_decimal_field(q, lend, v);
+              if (fe) {
+                if (out_col[f] >= 0) o[out_col[f]] = (T)v;
+                ++f;
+                if (fe >= lend) break;
+                q = fe + 1;
+                continue;
+              }
+            }
             const char* c = static_cast<const char*>(memchr(q, ',', (size_t)(lend - q)));
             const char* fe = c ? c : lend;
-            if (f >= F || memchr(q, '"', (size_t)(fe - q))) { ok = false; break; }
+            if (f >= F) { ok = false; break; }
             if (is_num[f]) {
               double v;
               if (fe == q) v = std::numeric_limits<double>::quiet_NaN();
