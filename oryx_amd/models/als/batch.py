@@ -363,16 +363,39 @@ class ALSUpdate(MLUpdate):
         return self.history
 
     def _raw_parse_slot(self, lines, users, items) -> Optional[list]:
-        """A list for parse_ratings' raw output when the training lines are the complete data
-        set (test fraction 0: MLUpdate trains on new + past data, exactly what the publish
-        step joins known items from); None otherwise."""
-        if self.get_test_fraction() != 0.0 or not lines:
+        """A list for parse_ratings' raw output of the training lines, kept for the publish
+        step's known items: with test fraction 0 MLUpdate trains on new + past data, exactly
+        what that step joins known items from; with a test split the training lines lack only
+        the held-out test lines, which the publish step then parses alone and appends
+        (``_known_items_parse``)."""
+        if not lines:
             self._raw_parse = None
             return None
         out: list = []
         self._raw_parse = {"n": len(lines), "first": lines[0], "last": lines[-1],
                            "users": users, "items": items, "arrays": out}
         return out
+
+    def _known_items_parse(self, all_data):
+        """(users, items, u, i, s, ts) of every event of the generation for the known items:
+        the build's memoised parse when it covered the whole data set; with a test split, the
+        memoised parse of the training lines plus a parse of just the held-out test lines
+        into the same dictionaries (instead of re-parsing all of the new data); None when
+        neither applies."""
+        parsed = self._raw_parse_for(all_data)
+        if parsed is not None:
+            return parsed
+        m = self._raw_parse
+        test = getattr(self, "_split_test", None)
+        if m is None or len(m["arrays"]) != 4 or test is None or not len(test) or \
+                m["n"] + len(test) != len(all_data):
+            return None
+        users, items = m["users"], m["items"]
+        tu, ti, tsv, tts = ingest.parse_ratings(test, users, items, default_ts=_NO_TS)
+        tts = np.where(tts == _NO_TS, 0, tts)
+        u, i, sv, ts = m["arrays"]
+        return (users, items, np.concatenate([u, tu]), np.concatenate([i, ti]),
+                np.concatenate([sv, tsv]), np.concatenate([ts, tts]))
 
     def _raw_parse_for(self, lines):
         """(users, items, u, i, s, ts) of the memoised parse when it is of ``lines``."""
@@ -635,6 +658,7 @@ class ALSUpdate(MLUpdate):
             # the generation is done: drop the candidates' factors and the parse memo
             self._cache.clear()
             self._raw_parse = None
+            self._split_test = None
 
     def _published_rows(self, pmml, model_parent_path):
         """(x_ids, X rows text, y_ids, Y rows text) of the promoted model: from the build's
@@ -659,7 +683,7 @@ class ALSUpdate(MLUpdate):
         if self.no_known_items:
             model_update_topic.send_block("UP", ingest.assemble_row_messages("X", x_ids, x_text))
             return
-        parsed = self._raw_parse_for(all_data)
+        parsed = self._known_items_parse(all_data)
         dev = self.dist_ctx.device if self.dist_ctx is not None else None
         if parsed is None:
             users, items = ingest.IdDict(), ingest.IdDict()
@@ -699,7 +723,9 @@ class ALSUpdate(MLUpdate):
             log.info("New data timestamp range: %d - %d", lo, hi)
             boundary = int(hi - self.get_test_fraction() * (hi - lo))
             log.info("Splitting at timestamp %d", boundary)
-            return ingest.split_by_time(new_data, boundary)
+            train, test = ingest.split_by_time(new_data, boundary)
+            self._split_test = test           # the publish step's known items add these
+            return train, test
         ts = _timestamps(new_data)
         if sharded:
             # the boundary comes from the global timestamp range of the new data

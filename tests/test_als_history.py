@@ -163,3 +163,37 @@ def test_history_clear_drops_everything_cpu(monkeypatch):
     assert h.resident_bytes() > 0
     h.clear()
     assert len(h) == 0 and h.resident_bytes() == 0
+
+
+def test_known_items_with_test_split_cover_all_data_cpu(tmp_path):
+    """With a held-out test split, the published X rows' known items still cover every event
+    of the generation (train + test + past): the build's parse of the training lines plus a
+    parse of only the test lines, not a re-parse of all the data."""
+    import json
+    from oryx_amd.transport.producer import MockTopicProducer
+    from oryx_amd.utils import config as cfg
+    gen = np.random.default_rng(8)
+    _write_parts(str(tmp_path / "past"), gen, 2, 400)
+    past = read_past_data(str(tmp_path / "past"))
+    new = Dataset.from_values(TextLines.from_strings(
+        ["u%d,i%d,%.2f,%d" % (gen.integers(80), gen.integers(60), gen.uniform(0.5, 4),
+                               1_700_000_000_000 + j * 1000) for j in range(3000)]))
+    conf = cfg.overlay_on({
+        "oryx.batch.update-class": '"com.cloudera.oryx.app.batch.mllib.als.ALSUpdate"',
+        "oryx.ml.eval.test-fraction": 0.3,
+        "oryx.ml.eval.candidates": 1,
+        "oryx.als.hyperparams.features": 4,
+        "oryx.als.iterations": 2,
+        "oryx.gpu.device": '"cpu"',
+    }, cfg.get_default())
+    upd = als_batch.ALSUpdate(conf)
+    MockTopicProducer.clear()
+    upd.run_update(None, 1_700_000_999_999, new, past, str(tmp_path / "model"),
+                   MockTopicProducer())
+    assert upd._raw_parse is None and getattr(upd, "_split_test", None) is None
+    xs = [json.loads(m) for k, m in MockTopicProducer.get_key_messages()
+          if k == "UP" and m.startswith('["X"')]
+    assert xs
+    want = als_batch.known_items(list(new.values()) + list(past.values()))
+    for x in xs:
+        assert set(x[3]) == want[x[1]], x[1]
