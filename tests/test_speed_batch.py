@@ -191,3 +191,28 @@ def test_deferred_block_formats_into_the_log(tmp_path):
     sb.parse(tl, xm, ym)
     with pytest.raises(RuntimeError):
         stale.materialize()
+
+
+def test_leaf_update_formatter_matches_json():
+    """ingest.format_leaf_updates (the RDF speed layer's native formatter) writes the bytes of
+    the reference-format messages json.dumps would: classification '[tree,ID,{"c":n,...}]'
+    over the nonzero classes, regression '[tree,ID,mean,count]' with Python float repr."""
+    g = np.random.default_rng(2)
+    ids = ["r", "r-+", 'r-"q', "rü+-", "r--+-+-+"]
+    blob, ends = ingest.strings_blob([json.dumps(i) for i in ids])
+    n = 40
+    idx = g.integers(0, len(ids), n)
+    trees = g.integers(0, 50, n)
+    counts = g.integers(0, 4, (n, 3)) * (g.random((n, 3)) < 0.7)
+    counts[:, 0] += 1
+    blk = ingest.format_leaf_updates(trees, blob, ends, idx, counts, 3)
+    want = ['[%d,%s,{%s}]' % (t, json.dumps(ids[k]), ",".join('"%d":%d' % (c, v) for c, v in
+                                                          enumerate(row) if v))
+            for t, k, row in zip(trees.tolist(), idx.tolist(), counts.tolist())]
+    assert list(blk) == want
+    means = g.standard_normal(n) * 10.0 ** g.integers(-8, 8, n)
+    cnt = g.integers(1, 1000, n)
+    blk = ingest.format_leaf_updates(trees, blob, ends, idx, cnt, 0, means)
+    want = [json.dumps([t, ids[k], m, c], separators=(",", ":"))
+            for t, k, m, c in zip(trees.tolist(), idx.tolist(), means.tolist(), cnt.tolist())]
+    assert list(blk) == want
