@@ -445,12 +445,15 @@ class ItemIndex:
         bits = None
         if use_lsh:
             allb = np.zeros(self.num_buckets, dtype=bool)
-            bits = np.zeros((nq, self.words), dtype=np.uint32)
+            mask = np.zeros((nq, self.words * 32), dtype=bool)
             for j, q in enumerate(qs):
-                c = np.arange(self.num_buckets) if q.candidates is None else \
-                    np.asarray(q.candidates, dtype=np.int64)
-                allb[c] = True
-                np.bitwise_or.at(bits[j], c >> 5, (np.uint32(1) << (c & 31).astype(np.uint32)))
+                if q.candidates is None:
+                    mask[j, :self.num_buckets] = True
+                else:
+                    mask[j, np.asarray(q.candidates, dtype=np.int64)] = True
+            allb |= mask[:, :self.num_buckets].any(0)
+            # per-query bucket bitmaps (bit b of word b // 32), one packbits for the batch
+            bits = np.packbits(mask, axis=1, bitorder="little").view(np.uint32)
             sel = np.nonzero(allb)[0]
             starts = self.bucket_start[sel]
             ends = self.bucket_start[sel + 1]
