@@ -100,12 +100,15 @@ class CSR:
 
 # Rows longer than the split threshold are cut into segments (one wave each, partial normal
 # equations added with fp32 atomics) so one popular row does not set the kernel's tail.  The
-# threshold adapts to the data: max(SPLIT_MIN, SPLIT_MEAN_FACTOR x mean row length), segments
-# half of it -- at 1 GPU (items: mean 423 ratings) that is 4096/2048, which measured 13 %
-# faster than 2048/1024 (fewer atomics); with 8 GPUs' item shards (mean ~3.4k) typical rows
-# stay whole.  ORYX_ALS_SPLIT="thr,seg" fixes both (tuning runs).
+# threshold adapts to the data: max(SPLIT_MIN, min(SPLIT_MEAN_FACTOR x mean row length,
+# nnz / SPLIT_WORK_UNITS)), segments half of it -- at 1 GPU (items: mean 423 ratings) that is
+# 4096/2048, which measured 13 % faster than 2048/1024 (fewer atomics); an 8-GPU rank's item
+# shard (c2: 7.4k items, mean 3.5k ratings) gets 6250/3125: 1.755 ms per iteration against
+# 1.864 with the mean-only rule (4x mean = 13.9k: the longest whole rows set the tail), 1.85 at
+# 4096 and 1.82 at 8192 (r4_emul_c2_w8_split_*.json).  ORYX_ALS_SPLIT="thr,seg" fixes both.
 SPLIT_MIN = 4096
 SPLIT_MEAN_FACTOR = 4
+SPLIT_WORK_UNITS = 4096
 _SPLIT_ENV = os.environ.get("ORYX_ALS_SPLIT")
 
 
@@ -114,7 +117,7 @@ def split_params(nnz: int, n_nonempty: int) -> Tuple[int, int]:
         thr, seg = (int(v) for v in _SPLIT_ENV.split(","))
         return thr, seg
     mean = nnz / max(1, n_nonempty)
-    thr = max(SPLIT_MIN, int(SPLIT_MEAN_FACTOR * mean))
+    thr = max(SPLIT_MIN, int(min(SPLIT_MEAN_FACTOR * mean, nnz / SPLIT_WORK_UNITS)))
     return thr, max(256, thr // 2)
 
 

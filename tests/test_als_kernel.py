@@ -248,10 +248,13 @@ def test_gramian_kernel(cuda, n, kp):
 
 def test_split_params_adapt_to_mean_row_length():
     # 1 GPU item CSR of the bench (mean 423 ratings/row) -> 4096/2048; an 8-GPU item shard
-    # (mean ~3.4k) raises the threshold so typical rows stay on one wave
+    # (mean ~3.4k) raises the threshold, bounded by the work per split unit (nnz / 4096)
     assert als_ops.split_params(25_000_000, 59_047) == (4096, 2048)
-    thr, seg = als_ops.split_params(25_000_000, 7_381)
-    assert thr == 4 * int(25_000_000 / 7_381) and seg == thr // 2
+    thr, seg = als_ops.split_params(25_600_000, 7_381)
+    assert thr == 6250 and seg == 3125
+    # few short rows: the mean bound applies
+    thr, seg = als_ops.split_params(100_000_000, 500_000)
+    assert thr == 4096 and seg == 2048
 
 
 def test_reference_solve_fp64_cpu():
