@@ -970,7 +970,7 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
 // walks tiles of the list until the device-side count is exhausted.
 template <int RP>
 __global__ __launch_bounds__(256) void km_rescore_full(const float* __restrict__ X, int ldx,
-                                                       int d, const float* __restrict__ C,
+                                                       int d, const float* __restrict__ CT2,
                                                        int k, const int* __restrict__ list2,
                                                        int* __restrict__ assign,
                                                        float* __restrict__ mind) {
@@ -998,30 +998,22 @@ __global__ __launch_bounds__(256) void km_rescore_full(const float* __restrict__
     for (int c0 = wave * 64; c0 < k; c0 += 256) {
       const int c = c0 + lane;
       const bool live = c < k;
-      const float* cr = C + (long long)(live ? c : 0) * d;
+      // the centers in feature-pair-major order (CT2 [dp / 2][k] of (dim 2j, dim 2j + 1)
+      // pairs): consecutive lanes -- consecutive centers -- read consecutive 8-byte pairs, one
+      // coalesced 512-byte line set per load instruction instead of 64 scattered row reads
+      const f32x2* ct = reinterpret_cast<const f32x2*>(CT2) + (live ? c : 0);
+      auto load_slice = [&](int e0, f32x2* cv) {
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+          const int e = e0 + 2 * q;
+          cv[q] = e < dp ? ct[(long long)(e >> 1) * k] : f32x2{0.f, 0.f};
+        }
+      };
       // even / odd dimensions in the two halves of packed fp32 pairs (v_pk_add_f32 /
       // v_pk_fma_f32: two lanes' worth of work per instruction), summed at the end
       f32x2 acc[RP];
 #pragma unroll
       for (int p = 0; p < RP; ++p) acc[p] = f32x2{0.f, 0.f};
-      // center slices: 16 dwordx4 loads per 64 dimensions when rows are 16-byte aligned
-      // (d % 4 == 0)
-      auto load_slice = [&](int e0, f32x2* cv) {
-        if ((d & 3) == 0) {
-          const f32x4* c4 = reinterpret_cast<const f32x4*>(cr + e0);
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const f32x4 v = e0 + 4 * q < d ? c4[q] : f32x4{0.f, 0.f, 0.f, 0.f};
-            cv[2 * q] = f32x2{v[0], v[1]};
-            cv[2 * q + 1] = f32x2{v[2], v[3]};
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < 32; ++q)
-            cv[q] = f32x2{e0 + 2 * q < d ? cr[e0 + 2 * q] : 0.f,
-                          e0 + 2 * q + 1 < d ? cr[e0 + 2 * q + 1] : 0.f};
-        }
-      };
       for (int e0 = 0; e0 < dp; e0 += 64) {
         f32x2 cv[32];
         load_slice(e0, cv);
@@ -1378,15 +1370,16 @@ int oryx_kmeans_assign(const void* X, const float* xnorm, const void* C, long lo
 // then decides those exactly from the fp32 rows (Xf [n][ldx], Cf [k][d]), the flag-2 points
 // through km_rescore_full.  Only d_pad 64 / 128 / 256 (the 64-point-per-wave kernel) and
 // k_pad <= 65536.  idx2 / flags: [n] scratch; list2: [n + 1] int32 scratch.
-int oryx_kmeans_rescore_list(const float* Xf, int ldx, int d, const float* Cf, int k,
+int oryx_kmeans_rescore_list(const float* Xf, int ldx, int d, const float* CT2, int k,
                              const int* list2, long long max_rows, int* assign, float* mind,
                              void* stream);
 
 int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, long long n,
                             int d_pad, int k_pad, const float* cnorm, const float* Xf, int ldx,
-                            int d, const float* Cf, int k, float cmax, int* assign, float* mind,
-                            int* idx2, unsigned char* flags, unsigned long long* stats,
-                            int* list2, int defer_full, void* stream) {
+                            int d, const float* Cf, const float* CT2, int k, float cmax,
+                            int* assign, float* mind, int* idx2, unsigned char* flags,
+                            unsigned long long* stats, int* list2, int defer_full,
+                            void* stream) {
   if (n <= 0) return ORYX_OK;
   if (n >= 0x7fffffffLL) return ORYX_EINVAL;                   // list2 holds int32 rows
   const int dk = d_pad / 32;
@@ -1439,12 +1432,12 @@ int oryx_kmeans_assign_cert(const void* X, const float* xnorm, const void* C, lo
   // defer_full: the caller takes the flag-2 list (list2) itself (a GEMM over the listed points
   // with a certified top-1, the rest through oryx_kmeans_rescore_list)
   if (defer_full) return oryx_check_launch();
-  return oryx_kmeans_rescore_list(Xf, ldx, d, Cf, k, list2, n, assign, mind, stream);
+  return oryx_kmeans_rescore_list(Xf, ldx, d, CT2, k, list2, n, assign, mind, stream);
 }
 
 // Exact fp32 full rescan (km_rescore_full) of the rows in list2 ([0] = count, then rows);
 // max_rows bounds the count (sizes the grid).
-int oryx_kmeans_rescore_list(const float* Xf, int ldx, int d, const float* Cf, int k,
+int oryx_kmeans_rescore_list(const float* Xf, int ldx, int d, const float* CT2, int k,
                              const int* list2, long long max_rows, int* assign, float* mind,
                              void* stream) {
   if (max_rows <= 0) return ORYX_OK;
@@ -1460,7 +1453,7 @@ int oryx_kmeans_rescore_list(const float* Xf, int ldx, int d, const float* Cf, i
     full_attr = true;
   }
   hipLaunchKernelGGL((km_rescore_full<RP>), dim3((unsigned)fblocks), dim3(256), smem, s, Xf,
-                     ldx, d, Cf, k, list2, assign, mind);
+                     ldx, d, CT2, k, list2, assign, mind);
   return oryx_check_launch();
 }
 

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 20
+KERNELS_ABI_VERSION = 21
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -253,11 +253,11 @@ def _load_kernels():
     _sig(lib, "oryx_ipc_header_floats", c_ll, [])
     _sig(lib, "oryx_kmeans_assign", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp,
                                           c_vp])
-    # X, xnorm, C, n, d_pad, k_pad, cnorm, Xf, ldx, d, Cf, k, cmax, assign, mind, idx2, flags,
-    # stats, stream
+    # X, xnorm, C, n, d_pad, k_pad, cnorm, Xf, ldx, d, Cf, CT2, k, cmax, assign, mind, idx2,
+    # flags, stats, list2, defer_full, stream
     _sig(lib, "oryx_kmeans_assign_cert", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_i,
-                                               c_i, c_vp, c_i, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                               c_vp, c_i, c_vp])
+                                               c_i, c_vp, c_vp, c_i, c_f, c_vp, c_vp, c_vp, c_vp,
+                                               c_vp, c_vp, c_i, c_vp])
     _sig(lib, "oryx_kmeans_rescore_list", c_i, [c_vp, c_i, c_i, c_vp, c_i, c_vp, c_ll, c_vp,
                                                 c_vp, c_vp])
     # x, xT, cl, csize, s, d, partial, stream

@@ -67,6 +67,18 @@ class DeviceCenters:
         self.cnorm = cn
         self.cf = centers.to(torch.float32).contiguous()
         self._cmax = None
+        self._ct2 = None
+
+    @property
+    def ct2(self) -> torch.Tensor:
+        """The fp32 centers in feature-pair-major order for the exact full rescan kernel:
+        [dp / 2][k][2] with dp = d rounded up to 4 (pad dimensions zero)."""
+        if self._ct2 is None:
+            dp = (self.d + 3) // 4 * 4
+            c = torch.zeros((self.k, dp), dtype=torch.float32, device=self.cf.device)
+            c[:, :self.d] = self.cf
+            self._ct2 = c.view(self.k, dp // 2, 2).permute(1, 0, 2).contiguous()
+        return self._ct2
 
     @property
     def cmax(self) -> float:
@@ -151,7 +163,7 @@ def _rescore_flag2(x: "PointSet", dc, list2: torch.Tensor, out_a: torch.Tensor,
     if torch.backends.cuda.matmul.allow_tf32:
         # reduced-precision GEMMs void the rounding bound: every listed point is rescanned
         native.check(lib.oryx_kmeans_rescore_list(
-            x.x.data_ptr(), x.x.stride(0), x.d, dc.cf.data_ptr(), dc.k, list2.data_ptr(), cnt,
+            x.x.data_ptr(), x.x.stride(0), x.d, dc.ct2.data_ptr(), dc.k, list2.data_ptr(), cnt,
             out_a.data_ptr(), out_d.data_ptr(), native.stream_ptr(dev)),
             "oryx_kmeans_rescore_list")
         return
@@ -179,7 +191,7 @@ def _rescore_flag2(x: "PointSet", dc, list2: torch.Tensor, out_a: torch.Tensor,
         lst[0] = rest.numel()
         lst[1:] = rest.to(torch.int32)
         native.check(lib.oryx_kmeans_rescore_list(
-            x.x.data_ptr(), x.x.stride(0), x.d, dc.cf.data_ptr(), dc.k, lst.data_ptr(),
+            x.x.data_ptr(), x.x.stride(0), x.d, dc.ct2.data_ptr(), dc.k, lst.data_ptr(),
             rest.numel(), out_a.data_ptr(), out_d.data_ptr(), native.stream_ptr(dev)),
             "oryx_kmeans_rescore_list")
 
@@ -217,7 +229,8 @@ def assign(x, centers: torch.Tensor, exact: bool = False, out=None,
                 rc = lib.oryx_kmeans_assign_cert(
                     x.xb.data_ptr(), x.xn.data_ptr(), dc.cb.data_ptr(), n, dc.d_pad, dc.k_pad,
                     dc.cnorm.data_ptr(), x.x.data_ptr(), x.x.stride(0), x.d, dc.cf.data_ptr(),
-                    dc.k, dc.cmax, out_a.data_ptr(), out_d.data_ptr(), idx2.data_ptr(),
+                    dc.ct2.data_ptr(), dc.k, dc.cmax, out_a.data_ptr(), out_d.data_ptr(),
+                    idx2.data_ptr(),
                     flags.data_ptr(), st.data_ptr(), list2.data_ptr(), int(_GEMM_RESCORE),
                     native.stream_ptr(x.device))
                 native.check(rc, "oryx_kmeans_assign_cert")
