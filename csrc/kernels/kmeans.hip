@@ -891,6 +891,10 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
                                                   int* __restrict__ list2) {
   const int lane = threadIdx.x & 63;
   const long long nw = (long long)gridDim.x * 4;
+  // float4 loads of rows and centers when every row starts on 16 bytes
+  const bool vec = (d & 3) == 0 && (ldx & 3) == 0 &&
+                   ((reinterpret_cast<unsigned long long>(X) |
+                     reinterpret_cast<unsigned long long>(C)) & 15) == 0;
   // per-wave tallies, one atomic per wave at the end (a per-point atomic on one address
   // serialised ~10^6 updates in L2)
   unsigned long long n1 = 0, n2 = 0;
@@ -928,14 +932,43 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
         const float* xr = X + r * ldx;
         const float* c1 = C + (long long)i1 * d;
         const float* c2 = C + (long long)i2 * d;
-        for (int e = 4 * ql; e < d; e += 64) {
+        if (vec) {
+          // same per-lane order as the scalar loop below, with the row and both center slices
+          // of a 256-dimension chunk loaded as float4s before any arithmetic (12 loads in
+          // flight instead of one round trip per 4-dimension run)
+          for (int e0 = 4 * ql; e0 < d; e0 += 256) {
+            f32x4 xv[4], av[4], bv[4];
 #pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            if (e + v < d) {
-              const float xv = xr[e + v];
-              const float a = xv - c1[e + v], b = xv - c2[e + v];
-              s1 += a * a;
-              s2 += b * b;
+            for (int it = 0; it < 4; ++it) {
+              const int e = e0 + 64 * it;
+              if (e < d) {
+                xv[it] = *reinterpret_cast<const f32x4*>(xr + e);
+                av[it] = *reinterpret_cast<const f32x4*>(c1 + e);
+                bv[it] = *reinterpret_cast<const f32x4*>(c2 + e);
+              }
+            }
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+              if (e0 + 64 * it < d) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                  const float a = xv[it][v] - av[it][v], b = xv[it][v] - bv[it][v];
+                  s1 += a * a;
+                  s2 += b * b;
+                }
+              }
+            }
+          }
+        } else {
+          for (int e = 4 * ql; e < d; e += 64) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              if (e + v < d) {
+                const float xv = xr[e + v];
+                const float a = xv - c1[e + v], b = xv - c2[e + v];
+                s1 += a * a;
+                s2 += b * b;
+              }
             }
           }
         }
@@ -960,31 +993,36 @@ __global__ __launch_bounds__(256) void km_rescore(const float* __restrict__ X, i
 }
 
 // Exact fp32 argmin over every center for the flag-2 points of km_rescore (list2: [0] =
-// count, then rows).  Per point the old path streamed all K center rows through one wave
-// (1 MB of L2 reads per point at K = 1000, d = 256); here a workgroup takes RP points at a
-// time with their rows staged in LDS (read as broadcasts), each lane owns one center of a
-// 64-center chunk and keeps that center's 64-dimension slice in registers, accumulating
-// (x - c)^2 in dimension order for all RP points -- K x d x 4 bytes of center traffic per RP
-// points and two VALU ops per (point, center, dimension).  (min, lowest index) per point is
-// reduced over lanes, then over the 4 waves through LDS.  Persistent grid: every workgroup
-// walks tiles of the list until the device-side count is exhausted.
-template <int RP>
-__global__ __launch_bounds__(256) void km_rescore_full(const float* __restrict__ X, int ldx,
+// count, then rows).  A workgroup takes RP points at a time with their rows staged in LDS
+// (read as broadcasts); each lane owns CPL centers (c0 + lane + 64 j: coalesced loads) and
+// walks the dimensions in SL-wide slices held in registers, so one LDS read of 4 dimensions
+// of a point feeds 4 CPL packed-fp32 ops -- register blocking over points x centers keeps the
+// LDS data path (one 8-cycle broadcast per read) under the VALU rate, and consecutive FMAs go
+// to independent accumulators.  Each (point, center) sum runs over the dimensions in
+// increasing order in two halves (even / odd dimensions, the halves of the packed pairs)
+// that are added at the end.  (min, lowest index) per point is reduced over lanes, then over
+// the 4 waves through LDS.  Persistent grid: every workgroup walks tiles of the list until
+// the device-side count is exhausted.
+template <int RP, int CPL, int SL>
+__global__ __launch_bounds__(256, 2) void km_rescore_full(const float* __restrict__ X, int ldx,
                                                        int d, const float* __restrict__ CT2,
                                                        int k, const int* __restrict__ list2,
                                                        int* __restrict__ assign,
                                                        float* __restrict__ mind) {
-  extern __shared__ __attribute__((aligned(16))) float xs[];     // [RP][dp] + reduction
+  extern __shared__ __attribute__((aligned(16))) float xs[];     // [RP][dq] + reduction
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int dp = (d + 3) & ~3;
-  float* red_d = xs + RP * dp;                                   // [4][RP]
+  // LDS rows padded to whole SL-dimension slices with zeros, as are the centers (CT2): the
+  // padding adds (0 - 0)^2 = +0 to the sums, and the slice loop has no bounds test
+  const int dq = (d + SL - 1) / SL * SL;
+  float* red_d = xs + RP * dq;                                   // [4][RP]
   int* red_i = reinterpret_cast<int*>(red_d + 4 * RP);          // [4][RP]
   const int cnt = list2[0];
+  const f32x2* ct2 = reinterpret_cast<const f32x2*>(CT2);
   for (int t0 = blockIdx.x * RP; t0 < cnt; t0 += gridDim.x * RP) {
     const int np = cnt - t0 < RP ? cnt - t0 : RP;
     __syncthreads();                                             // previous tile done
-    for (int i = tid; i < RP * dp; i += 256) {
-      const int p = i / dp, e = i - p * dp;
+    for (int i = tid; i < RP * dq; i += 256) {
+      const int p = i / dq, e = i - p * dq;
       xs[i] = (p < np && e < d) ? X[(long long)list2[1 + t0 + p] * ldx + e] : 0.f;
     }
     __syncthreads();
@@ -995,53 +1033,53 @@ __global__ __launch_bounds__(256) void km_rescore_full(const float* __restrict__
       best[p] = INFINITY;
       bidx[p] = 0x7fffffff;
     }
-    for (int c0 = wave * 64; c0 < k; c0 += 256) {
-      const int c = c0 + lane;
-      const bool live = c < k;
-      // the centers in feature-pair-major order (CT2 [dp / 2][k] of (dim 2j, dim 2j + 1)
-      // pairs): consecutive lanes -- consecutive centers -- read consecutive 8-byte pairs, one
-      // coalesced 512-byte line set per load instruction instead of 64 scattered row reads
-      const f32x2* ct = reinterpret_cast<const f32x2*>(CT2) + (live ? c : 0);
-      auto load_slice = [&](int e0, f32x2* cv) {
+    for (int c0 = wave * 64 * CPL; c0 < k; c0 += 256 * CPL) {
+      // CT2 [k / 64][dq / 2][64] (64-center tiles of dimension pairs, zero padded): lane
+      // `lane` of tile c0 / 64 + j reads its pairs 512 bytes apart
+      const f32x2* cb[CPL];
 #pragma unroll
-        for (int q = 0; q < 32; ++q) {
-          const int e = e0 + 2 * q;
-          cv[q] = e < dp ? ct[(long long)(e >> 1) * k] : f32x2{0.f, 0.f};
-        }
-      };
-      // even / odd dimensions in the two halves of packed fp32 pairs (v_pk_add_f32 /
-      // v_pk_fma_f32: two lanes' worth of work per instruction), summed at the end
-      f32x2 acc[RP];
+      for (int j = 0; j < CPL; ++j) {
+        const int tile = c0 / 64 + j;
+        cb[j] = ct2 + ((long long)(tile * 64 < k ? tile : 0) * (dq / 2)) * 64 + lane;
+      }
+      f32x2 acc[RP][CPL];
 #pragma unroll
-      for (int p = 0; p < RP; ++p) acc[p] = f32x2{0.f, 0.f};
-      for (int e0 = 0; e0 < dp; e0 += 64) {
-        f32x2 cv[32];
-        load_slice(e0, cv);
-        const int q4n = (dp - e0) >= 64 ? 16 : (dp - e0) >> 2;
+      for (int p = 0; p < RP; ++p)
 #pragma unroll
-        for (int p = 0; p < RP; ++p) {
-          const f32x4* xp = reinterpret_cast<const f32x4*>(xs + p * dp + e0);
-          f32x2 a = acc[p];
+        for (int j = 0; j < CPL; ++j) acc[p][j] = f32x2{0.f, 0.f};
+      for (int e0 = 0; e0 < dq; e0 += SL) {
+        f32x2 cv[CPL][SL / 2];
 #pragma unroll
-          for (int q4 = 0; q4 < 16; ++q4) {
-            if (q4 < q4n) {
-              const f32x4 xv = xp[q4];
-              f32x2 t = f32x2{xv[0], xv[1]} - cv[2 * q4];
-              a = __builtin_elementwise_fma(t, t, a);
-              t = f32x2{xv[2], xv[3]} - cv[2 * q4 + 1];
-              a = __builtin_elementwise_fma(t, t, a);
+        for (int q = 0; q < SL / 2; ++q)
+#pragma unroll
+          for (int j = 0; j < CPL; ++j) cv[j][q] = cb[j][((e0 >> 1) + q) * 64];
+#pragma unroll
+        for (int q4 = 0; q4 < SL / 4; ++q4) {
+#pragma unroll
+          for (int p = 0; p < RP; ++p) {
+            const f32x4 xv = *reinterpret_cast<const f32x4*>(xs + p * dq + e0 + 4 * q4);
+            const f32x2 xa = f32x2{xv[0], xv[1]}, xb = f32x2{xv[2], xv[3]};
+#pragma unroll
+            for (int j = 0; j < CPL; ++j) {
+              f32x2 t = xa - cv[j][2 * q4];
+              acc[p][j] = __builtin_elementwise_fma(t, t, acc[p][j]);
+              t = xb - cv[j][2 * q4 + 1];
+              acc[p][j] = __builtin_elementwise_fma(t, t, acc[p][j]);
             }
           }
-          acc[p] = a;
         }
       }
-      if (live) {
 #pragma unroll
-        for (int p = 0; p < RP; ++p) {
-          const float v = acc[p][0] + acc[p][1];
-          if (v < best[p]) {                                     // c grows: ties keep the lower
-            best[p] = v;
-            bidx[p] = c;
+      for (int j = 0; j < CPL; ++j) {
+        const int c = c0 + 64 * j + lane;
+        if (c < k) {
+#pragma unroll
+          for (int p = 0; p < RP; ++p) {
+            const float v = acc[p][j][0] + acc[p][j][1];
+            if (v < best[p]) {                       // a lane's centers grow with j: ties keep
+              best[p] = v;                           // the lower index
+              bidx[p] = c;
+            }
           }
         }
       }
@@ -1442,18 +1480,35 @@ int oryx_kmeans_rescore_list(const float* Xf, int ldx, int d, const float* CT2, 
                              void* stream) {
   if (max_rows <= 0) return ORYX_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  constexpr int RP = 32;
-  const int dp = (d + 3) & ~3;
-  const size_t smem = (size_t)RP * dp * 4 + 8 * RP * 4;
-  long long fblocks = (max_rows + RP - 1) / RP;
-  if (fblocks > 2048) fblocks = 2048;
-  static bool full_attr = false;
-  if (!full_attr && smem > 65536) {
-    if (!oryx_set_max_lds(&km_rescore_full<RP>, (int)smem)) return ORYX_ELAUNCH;
-    full_attr = true;
+  // (points per tile, centers per lane, dimension slice): ORYX_KM_FULL_VARIANT picks one of
+  // the instantiations for A/B runs; CT2 is padded to 16 dimensions, so SL <= 16
+  static const int variant =
+      getenv("ORYX_KM_FULL_VARIANT") ? atoi(getenv("ORYX_KM_FULL_VARIANT")) : 0;
+  constexpr int SL = 16;
+  const int dq = (d + SL - 1) / SL * SL;              // CT2 holds dq / 2 pair rows
+#define FULL_LAUNCH(RP, CPL)                                                                  \
+  {                                                                                           \
+    const size_t smem = (size_t)RP * dq * 4 + 8 * RP * 4;                                     \
+    long long fblocks = (max_rows + RP - 1) / RP;                                             \
+    if (fblocks > 4096) fblocks = 4096;                                                       \
+    static bool full_attr = false;                                                            \
+    if (!full_attr && smem > 65536) {                                                         \
+      if (!oryx_set_max_lds(&km_rescore_full<RP, CPL, SL>, (int)smem)) return ORYX_ELAUNCH;   \
+      full_attr = true;                                                                       \
+    }                                                                                         \
+    hipLaunchKernelGGL((km_rescore_full<RP, CPL, SL>), dim3((unsigned)fblocks), dim3(256),    \
+                       smem, s, Xf, ldx, d, CT2, k, list2, assign, mind);                     \
   }
-  hipLaunchKernelGGL((km_rescore_full<RP>), dim3((unsigned)fblocks), dim3(256), smem, s, Xf,
-                     ldx, d, CT2, k, list2, assign, mind);
+  switch (variant) {
+    case 1: FULL_LAUNCH(16, 2) break;
+    case 2: FULL_LAUNCH(4, 4) break;
+    case 3: FULL_LAUNCH(8, 4) break;
+    case 4: FULL_LAUNCH(4, 2) break;
+    default: FULL_LAUNCH(8, 2) break;   // K = 1000, d = 256: 0.55 ms per 37k points
+                                        // (8, 4): 0.68, (4, 4): 0.69, (16, 2): 1.24
+
+  }
+#undef FULL_LAUNCH
   return oryx_check_launch();
 }
 

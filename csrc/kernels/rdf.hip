@@ -152,15 +152,21 @@ __global__ __launch_bounds__(256) void rdf_route(const BinT* __restrict__ Xb, lo
 // Route without visit counting (the grouped path takes node visits from the per-level
 // counting sort): one thread per row walks ALL trees, so the row's bytes come from HBM once
 // per level and the other trees' reads of it hit L1/L2, instead of every tree streaming the
-// whole bin matrix (grid y = tree in rdf_route).
-template <typename BinT>
+// whole bin matrix (grid y = tree in rdf_route).  KEYS: also writes the next level's
+// counting-sort keys (see rdf_sort_keys: width = the next level's node slots; bootstrap
+// weight 0 -> the visits-only key range; rows in leaves -> 2 T width), which saves the
+// separate pass that re-reads node_of and the weights.
+template <typename BinT, bool KEYS>
 __global__ __launch_bounds__(256) void rdf_route_rows(const BinT* __restrict__ Xb, long long n,
                                                       int P, int T, int* __restrict__ node_of,
                                                       int nodes,
                                                       const int* __restrict__ split_feat,
                                                       const int* __restrict__ split_bin,
                                                       const unsigned char* __restrict__ cat_left,
-                                                      int B, const int* __restrict__ child_base) {
+                                                      int B, const int* __restrict__ child_base,
+                                                      const unsigned char* __restrict__ weight,
+                                                      int width, int* __restrict__ keys) {
+  const int dead = 2 * T * width;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256) {
     const BinT* xr = Xb + i * P;
@@ -168,9 +174,15 @@ __global__ __launch_bounds__(256) void rdf_route_rows(const BinT* __restrict__ X
     // memory round trips per 8 trees instead of three per tree
     for (int t0 = 0; t0 < T; t0 += 8) {
       int node[8], f[8], sb[8], cb[8], b[8];
+      unsigned int w[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
         node[u] = t0 + u < T ? node_of[(long long)(t0 + u) * n + i] : -1;
+      if (KEYS) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          w[u] = (weight && node[u] >= 0) ? weight[(long long)(t0 + u) * n + i] : 1u;
+      }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const long long tn = (long long)(t0 + u) * nodes + node[u];
@@ -182,16 +194,23 @@ __global__ __launch_bounds__(256) void rdf_route_rows(const BinT* __restrict__ X
       for (int u = 0; u < 8; ++u) b[u] = f[u] >= 0 ? (int)xr[f[u]] : 0;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        if (node[u] < 0) continue;
-        int* slot = node_of + (long long)(t0 + u) * n + i;
+        if (t0 + u >= T) break;
+        const long long k = (long long)(t0 + u) * n + i;
+        if (node[u] < 0) {
+          if (KEYS) keys[k] = dead;
+          continue;
+        }
         if (f[u] < 0) {
-          *slot = -1;
+          node_of[k] = -1;
+          if (KEYS) keys[k] = dead;
           continue;
         }
         const long long tn = (long long)(t0 + u) * nodes + node[u];
         const bool right =
             (cat_left && sb[u] < 0) ? cat_left[tn * B + b[u]] == 0 : b[u] > sb[u];
-        *slot = cb[u] + (right ? 1 : 0);
+        const int nn = cb[u] + (right ? 1 : 0);
+        node_of[k] = nn;
+        if (KEYS) keys[k] = (t0 + u) * width + nn + (w[u] == 0 ? T * width : 0);
       }
     }
   }
@@ -448,6 +467,59 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
     const float v = CLS ? (float)reinterpret_cast<const unsigned int*>(lh)[k] : lh[k];
     if (v != 0.f) atomicAdd(gh + k, v);
   }
+}
+
+// Node label totals only (the last level: every node there becomes a leaf, so the split search
+// needs its weighted label statistics and nothing per feature).  Rows in their natural order
+// (node_of, the bootstrap weights and the labels are all read coalesced -- through the
+// counting-sort permutation they would be one scattered cache line per row): grid x = row
+// blocks, y = tree; the tree's width x S totals are privatised in LDS (integer counts for
+// classification: bootstrap weights are small integers) and flushed with one global atomic
+// per non-zero entry into hist [T][width][S].  visits [T][width] (+=) counts every row at
+// the node, bootstrap weight 0 included (the PMML recordCount input the counting sort gives
+// the other levels).
+template <bool CLS>
+__global__ __launch_bounds__(256) void rdf_node_totals(const int* __restrict__ node_of,
+                                                       const unsigned char* __restrict__ weight,
+                                                       const int* __restrict__ label,
+                                                       const float* __restrict__ y, int S,
+                                                       long long n, int width,
+                                                       long long rows_per_block,
+                                                       float* __restrict__ hist,
+                                                       unsigned long long* __restrict__ visits) {
+  extern __shared__ float lh[];                      // [width][S], then [width] visit counts
+  const int t = blockIdx.y;
+  const int len = width * S;
+  unsigned int* lv = reinterpret_cast<unsigned int*>(lh + len);
+  for (int i = threadIdx.x; i < len + width; i += 256) lh[i] = 0.f;   // 0.f, 0u: same bits
+  __syncthreads();
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  const int* nd = node_of + (long long)t * n;
+  const unsigned char* wt = weight ? weight + (long long)t * n : nullptr;
+  for (long long i = r0 + threadIdx.x; i < r1; i += 256) {
+    const int node = nd[i];
+    if (node < 0) continue;
+    atomicAdd(lv + node, 1u);
+    const unsigned int w = wt ? wt[i] : 1u;
+    if (w == 0) continue;
+    if (CLS) {
+      atomicAdd(reinterpret_cast<unsigned int*>(lh) + node * S + label[i], w);
+    } else {
+      const float yi = y[i], wf = (float)w;
+      atomicAdd(lh + node * S, wf);
+      atomicAdd(lh + node * S + 1, wf * yi);
+      atomicAdd(lh + node * S + 2, wf * yi * yi);
+    }
+  }
+  __syncthreads();
+  float* gh = hist + (long long)t * len;
+  for (int i = threadIdx.x; i < len; i += 256) {
+    const float v = CLS ? (float)reinterpret_cast<const unsigned int*>(lh)[i] : lh[i];
+    if (v != 0.f) atomicAdd(gh + i, v);
+  }
+  for (int i = threadIdx.x; i < width; i += 256)
+    if (lv[i]) atomicAdd(visits + (long long)t * width + i, (unsigned long long)lv[i]);
 }
 
 // Flattened forest scoring: per (example, tree) walk from the tree's root to a leaf.
@@ -850,13 +922,14 @@ int oryx_rdf_route(const void* Xb, int bin_bytes, long long n, int P, int T, int
     long long blocks = (n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
     if (bin_bytes == 1)
-      hipLaunchKernelGGL((rdf_route_rows<unsigned char>), dim3((unsigned)blocks), dim3(256), 0, s,
-                         reinterpret_cast<const unsigned char*>(Xb), n, P, T, node_of, nodes,
-                         split_feat, split_bin, cat_left, B, child_base);
+      hipLaunchKernelGGL((rdf_route_rows<unsigned char, false>), dim3((unsigned)blocks),
+                         dim3(256), 0, s, reinterpret_cast<const unsigned char*>(Xb), n, P, T,
+                         node_of, nodes, split_feat, split_bin, cat_left, B, child_base,
+                         nullptr, 0, nullptr);
     else if (bin_bytes == 2)
-      hipLaunchKernelGGL((rdf_route_rows<short>), dim3((unsigned)blocks), dim3(256), 0, s,
+      hipLaunchKernelGGL((rdf_route_rows<short, false>), dim3((unsigned)blocks), dim3(256), 0, s,
                          reinterpret_cast<const short*>(Xb), n, P, T, node_of, nodes, split_feat,
-                         split_bin, cat_left, B, child_base);
+                         split_bin, cat_left, B, child_base, nullptr, 0, nullptr);
     else
       return ORYX_EINVAL;
     return oryx_check_launch();
@@ -881,6 +954,30 @@ int oryx_rdf_route(const void* Xb, int bin_bytes, long long n, int P, int T, int
     return ORYX_EINVAL;
   }
 #undef ROUTE_LAUNCH
+  return oryx_check_launch();
+}
+
+// Route every open row one level down AND write the next level's counting-sort keys
+// (keys [T][n] int32, next-level width `width`; weight [T][n] nullable) in one pass.
+int oryx_rdf_route_keys(const void* Xb, int bin_bytes, long long n, int P, int T, int* node_of,
+                        int nodes, const int* split_feat, const int* split_bin,
+                        const unsigned char* cat_left, int B, const int* child_base,
+                        const unsigned char* weight, int width, int* keys, void* stream) {
+  if (n <= 0 || T <= 0) return ORYX_OK;
+  if (!keys || width <= 0 || 2LL * T * width >= (1LL << 31)) return ORYX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  long long blocks = (n + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (bin_bytes == 1)
+    hipLaunchKernelGGL((rdf_route_rows<unsigned char, true>), dim3((unsigned)blocks), dim3(256),
+                       0, s, reinterpret_cast<const unsigned char*>(Xb), n, P, T, node_of, nodes,
+                       split_feat, split_bin, cat_left, B, child_base, weight, width, keys);
+  else if (bin_bytes == 2)
+    hipLaunchKernelGGL((rdf_route_rows<short, true>), dim3((unsigned)blocks), dim3(256), 0, s,
+                       reinterpret_cast<const short*>(Xb), n, P, T, node_of, nodes, split_feat,
+                       split_bin, cat_left, B, child_base, weight, width, keys);
+  else
+    return ORYX_EINVAL;
   return oryx_check_launch();
 }
 
@@ -941,6 +1038,31 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
     }
   }
 #undef PIECE_LAUNCH
+  return oryx_check_launch();
+}
+
+// Last-level node totals: hist [T][width][S] and visits [T][width] (+=) from node_of [T][n]
+// (-1: in a leaf).
+int oryx_rdf_node_totals(const int* node_of, const unsigned char* weight, const int* label,
+                         const float* y, int S, int cls, int T, long long n, int width,
+                         float* hist, unsigned long long* visits, void* stream) {
+  if (n <= 0 || T <= 0 || width <= 0) return ORYX_OK;
+  if (S <= 0 || !visits || (cls && !label) || (!cls && (!y || S != 3))) return ORYX_EINVAL;
+  const size_t smem = (size_t)width * (S + 1) * 4;
+  if (smem > 64 * 1024) return ORYX_EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  // ~2048 workgroups in all: enough to fill the chip, few flushes
+  long long per_tree = 2048 / T;
+  if (per_tree < 1) per_tree = 1;
+  long long rpb = (n + per_tree - 1) / per_tree;
+  if (rpb < 4096) rpb = 4096;
+  const dim3 grid((unsigned)((n + rpb - 1) / rpb), (unsigned)T);
+  if (cls)
+    hipLaunchKernelGGL(rdf_node_totals<true>, grid, dim3(256), smem, s, node_of, weight, label,
+                       y, S, n, width, rpb, hist, visits);
+  else
+    hipLaunchKernelGGL(rdf_node_totals<false>, grid, dim3(256), smem, s, node_of, weight, label,
+                       y, S, n, width, rpb, hist, visits);
   return oryx_check_launch();
 }
 

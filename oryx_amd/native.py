@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 21
+KERNELS_ABI_VERSION = 22
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -288,6 +288,13 @@ def _load_kernels():
     _sig(lib, "oryx_rdf_histogram_pieces", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i,
                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                                  c_vp, c_i, c_i, c_vp, c_vp, c_vp])
+    # Xb, bin_bytes, n, P, T, node_of, nodes, feat, bin, cat_left, B, child_base, weight,
+    # width, keys, stream
+    _sig(lib, "oryx_rdf_route_keys", c_i, [c_vp, c_i, c_ll, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp,
+                                           c_i, c_vp, c_vp, c_i, c_vp, c_vp])
+    # node_of, weight, label, y, S, cls, T, n, width, hist, visits, stream
+    _sig(lib, "oryx_rdf_node_totals", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_ll, c_i,
+                                            c_vp, c_vp, c_vp])
     # X, n, F, T, roots, feat, thr, cat_off, cat_bits, cat_len, left, right, leaf_value, C,
     # weights, vote, stream
     _sig(lib, "oryx_rdf_forest_vote", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp, c_vp, c_vp,

@@ -71,13 +71,17 @@ class DeviceCenters:
 
     @property
     def ct2(self) -> torch.Tensor:
-        """The fp32 centers in feature-pair-major order for the exact full rescan kernel:
-        [dp / 2][k][2] with dp = d rounded up to 4 (pad dimensions zero)."""
+        """The fp32 centers for the exact full rescan kernel, in 64-center tiles of
+        dimension pairs: [ceil(k / 64)][dq / 2][64][2] with dq = d rounded up to 16 (the
+        kernel's dimension slice) -- a lane's successive pair loads are 512 bytes apart (one
+        base address, immediate offsets) and a wave's load covers 512 consecutive bytes.  Pad
+        dimensions and pad centers are zero."""
         if self._ct2 is None:
-            dp = (self.d + 3) // 4 * 4
-            c = torch.zeros((self.k, dp), dtype=torch.float32, device=self.cf.device)
-            c[:, :self.d] = self.cf
-            self._ct2 = c.view(self.k, dp // 2, 2).permute(1, 0, 2).contiguous()
+            dq = (self.d + 15) // 16 * 16
+            kc = (self.k + 63) // 64
+            c = torch.zeros((kc * 64, dq), dtype=torch.float32, device=self.cf.device)
+            c[:self.k, :self.d] = self.cf
+            self._ct2 = c.view(kc, 64, dq // 2, 2).permute(0, 2, 1, 3).contiguous()
         return self._ct2
 
     @property

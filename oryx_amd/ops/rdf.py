@@ -347,7 +347,8 @@ class RowGroups:
 
     @staticmethod
     def launch_from_nodes(node_of: torch.Tensor, width: int,
-                          weight: Optional[torch.Tensor] = None):
+                          weight: Optional[torch.Tensor] = None,
+                          keys: Optional[torch.Tensor] = None):
         """Queue the level's counting sort on the device and return ``finish()`` (which waits
         for the counts and builds the RowGroups), or None when the key space is too wide; the
         host can do other work between the two."""
@@ -361,12 +362,13 @@ class RowGroups:
             return None
         dev = node_of.device
         lib = native.require_kernels()
-        keys = torch.empty(T * n, dtype=torch.int32, device=dev)
-        w = weight.contiguous() if weight is not None else None
-        rc = lib.oryx_rdf_sort_keys(node_of.contiguous().data_ptr(),
-                                    w.data_ptr() if w is not None else None, T, n, width,
-                                    keys.data_ptr(), native.stream_ptr(dev))
-        native.check(rc, "oryx_rdf_sort_keys")
+        if keys is None:       # (given: written by the fused route, rdf_route_rows<KEYS>)
+            keys = torch.empty(T * n, dtype=torch.int32, device=dev)
+            w = weight.contiguous() if weight is not None else None
+            rc = lib.oryx_rdf_sort_keys(node_of.contiguous().data_ptr(),
+                                        w.data_ptr() if w is not None else None, T, n, width,
+                                        keys.data_ptr(), native.stream_ptr(dev))
+            native.check(rc, "oryx_rdf_sort_keys")
         perm = torch.empty(T * n, dtype=torch.int32, device=dev)
         counts = torch.empty(k, dtype=torch.int64, device=dev)
         ws = torch.empty(int(lib.oryx_kmeans_sorted_ws_bytes(T * n, k)), dtype=torch.uint8,
@@ -681,6 +683,11 @@ _DEVICE_LOOP = os.environ.get("ORYX_RDF_DEVICE_LOOP", "1") != "0"
 _ROW_ORDER = os.environ.get("ORYX_RDF_ROW_ORDER", "1") != "0"
 
 
+def _totals_ok(width: int, S: int) -> bool:
+    """The last level's node totals fit rdf_node_totals' LDS (width x (S + 1) words)."""
+    return width * (S + 1) * 4 <= 64 * 1024
+
+
 def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classification: bool,
                   kind: str, weight, T: int, Fs: int, max_depth: int, seed: int,
                   ctx: dist.DistContext) -> TrainedForest:
@@ -763,12 +770,28 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
     for depth in range(max_depth + 1):
         faults.point("rdf.level", depth=depth, rank=ctx.rank)
         watchdog.heartbeat("rdf.level")
-        feats = sample_feats(W)
+        last = depth == max_depth and _totals_ok(W, S)
+        feats = sample_feats(W) if not last else None
         chunk = max(1, _HIST_BUDGET // max(1, T * Fs * B * S))
         parts = []
-        for lo in range(0, W, chunk):
+        if last:
+            # last level: every node becomes a leaf, so only its label totals (and visits) are
+            # needed -- one coalesced pass over node_of / weights / labels, no bin-matrix
+            # reads and no counting sort before it
+            tot = torch.zeros((T, W, 1, 1, S), dtype=torch.float32, device=dev)
+            visits = torch.zeros((T, W), dtype=torch.int64, device=dev)
+            native.check(lib.oryx_rdf_node_totals(
+                node_of.data_ptr(), weight.data_ptr() if weight is not None else None,
+                label.data_ptr() if classification else None,
+                None if classification else y.data_ptr(), S, int(classification), T, n, W,
+                tot.data_ptr(), visits.data_ptr(), stream), "oryx_rdf_node_totals")
+            if ctx.is_distributed:
+                dist.all_reduce_sum(tot, ctx)
+            parts.append(_choose_splits_kernel(
+                tot, torch.zeros((T, W, 1), dtype=torch.int32, device=dev), data, kind,
+                force_leaf=True))
+        for lo in range(0, W if not last else 0, chunk):
             hi = min(W, lo + chunk)
-            hist = torch.zeros((T, hi - lo, Fs, B, S), dtype=torch.float32, device=dev)
             max_pieces = (T * n + _PIECE - 1) // _PIECE + T * (hi - lo)
             ptree = torch.empty(max_pieces, dtype=torch.int32, device=dev)
             pnode = torch.empty(max_pieces, dtype=torch.int32, device=dev)
@@ -791,6 +814,7 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
                 ptree, pnode = ptree[order].contiguous(), pnode[order].contiguous()
                 pbeg, pend = pbeg[order].contiguous(), pend[order].contiguous()
             fe = feats[:, lo:hi].contiguous()
+            hist = torch.zeros((T, hi - lo, Fs, B, S), dtype=torch.float32, device=dev)
             native.check(lib.oryx_rdf_histogram_pieces(
                 data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0),
                 label.data_ptr() if classification else None,
@@ -826,8 +850,28 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
             # all-reduce whose peer never arrived must fail the forest here, not grow trees
             # from NaN statistics (the host already waited on the device for `live`)
             dist.check_collectives(ctx)
+        keys = None
+        # the next level is the last one and takes its totals straight from node_of
+        next_last = depth + 1 == max_depth and live > 0 and _totals_ok(2 * live, S)
         if live > 0:
-            _route(data, node_of, W, split, child_base, B, count_visits=False)
+            W2 = 2 * live
+            if next_last:
+                _route(data, node_of, W, split, child_base, B, count_visits=False)
+            elif 2 * T * W2 + 1 <= _SORT_MAX_KEYS and T * n < (1 << 31):
+                # route + the next level's counting-sort keys in one pass
+                keys = torch.empty(T * n, dtype=torch.int32, device=dev)
+                cl = split.cat_left.contiguous() if split.cat_left is not None else None
+                sf = split.feat.int().contiguous()
+                sb = split.bin.int().contiguous()
+                cb = child_base.int().contiguous()
+                native.check(lib.oryx_rdf_route_keys(
+                    data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0), T,
+                    node_of.data_ptr(), W, sf.data_ptr(), sb.data_ptr(),
+                    cl.data_ptr() if cl is not None else None, B, cb.data_ptr(),
+                    weight.data_ptr() if weight is not None else None, W2, keys.data_ptr(),
+                    stream), "oryx_rdf_route_keys")
+            else:
+                _route(data, node_of, W, split, child_base, B, count_visits=False)
         vis = visits
         if ctx.is_distributed:
             vis = vis.clone()
@@ -839,9 +883,11 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
         lv["event"].record()
         if live > 0:
             # next level: 2 * live slots, rows grouped by (tree, node) with one counting sort
-            W2 = 2 * live
-            finish = RowGroups.launch_from_nodes(node_of, W2, weight)
-            perm, counts, visits = finish.device()
+            if next_last:
+                perm = counts = visits = None
+            else:
+                finish = RowGroups.launch_from_nodes(node_of, W2, weight, keys=keys)
+                perm, counts, visits = finish.device()
             W = W2
         # the previous level's nodes are built while this level's work runs
         while pending:
