@@ -22,6 +22,8 @@
 //
 // rdf_forest_leaf: scoring -- walks flattened trees (K14) for a batch of examples.
 
+#include <cmath>
+
 #include "common.h"
 
 namespace {
@@ -212,6 +214,137 @@ __global__ __launch_bounds__(256) void rdf_route_rows(const BinT* __restrict__ X
         node_of[k] = nn;
         if (KEYS) keys[k] = (t0 + u) * width + nn + (w[u] == 0 ? T * width : 0);
       }
+    }
+  }
+}
+
+// LDS variant of rdf_route_rows for byte bins without categorical splits.  Per (row, tree) the
+// global kernel gathers three split-table entries and one bin byte, each a scattered access
+// (a wave touches up to 64 lines per load), so the texture-address path bounds it.  Here a
+// workgroup first packs the level's split tables into LDS (one word per node: feature in
+// bits 0-7, 255 = leaf; split bin in bits 8-15; child base in bits 16-31), then walks tiles
+// of 256 consecutive rows: the tile's row bytes are copied into LDS with coalesced dword
+// loads (pitch `pitch` dwords, odd, so the 64 lanes' byte reads hit distinct banks) and each
+// thread routes its row through all trees with LDS lookups only.  node_of / weight / keys
+// stay coalesced global accesses.  Requires P % 4 == 0 (every row starts on a dword),
+// features < 255, B <= 256 and child bases < 65536 (the launcher checks).
+template <bool KEYS>
+__global__ __launch_bounds__(256) void rdf_route_lds(const unsigned char* __restrict__ Xb,
+                                                     long long n, int P, int ndw, int pitch,
+                                                     int T, int* __restrict__ node_of, int nodes,
+                                                     const int* __restrict__ split_feat,
+                                                     const int* __restrict__ split_bin,
+                                                     const int* __restrict__ child_base,
+                                                     const unsigned char* __restrict__ weight,
+                                                     int width, int* __restrict__ keys) {
+  extern __shared__ unsigned int rsm[];
+  const int tid = threadIdx.x;
+  const int tn_all = T * nodes;
+  unsigned int* tab = rsm;                                  // [T * nodes]
+  unsigned int* rows = rsm + tn_all;                        // [256][pitch]
+  const unsigned char* rowb = reinterpret_cast<const unsigned char*>(rows);
+  for (int j = tid; j < tn_all; j += 256) {
+    const int f = split_feat[j];
+    tab[j] = f < 0 ? 0xFFu
+                   : ((unsigned)f | (((unsigned)split_bin[j] & 0xFFu) << 8) |
+                      ((unsigned)child_base[j] << 16));
+  }
+  const int dead = 2 * T * width;
+  const unsigned int* Xw = reinterpret_cast<const unsigned int*>(Xb);
+  const int rw = P >> 2;                                    // row pitch in dwords
+  constexpr int TG = 32;                                    // trees whose loads go out together
+  for (long long r0 = (long long)blockIdx.x * 256; r0 < n; r0 += (long long)gridDim.x * 256) {
+    const int nr = n - r0 < 256 ? (int)(n - r0) : 256;
+    const long long i = r0 + tid;
+    const bool mine = tid < nr;
+    // this tile's node ids and bootstrap weights for the first TG trees are loaded before the
+    // row staging, so their round trip overlaps it (one memory wait per tile, not one per tree
+    // group and operand)
+    int node[TG];
+    unsigned int w[TG];
+#pragma unroll
+    for (int u = 0; u < TG; ++u) {
+      node[u] = (mine && u < T) ? node_of[(long long)u * n + i] : -1;
+      if (KEYS) w[u] = (mine && u < T && weight) ? weight[(long long)u * n + i] : 1u;
+    }
+    __syncthreads();                                        // table ready / previous tile done
+    // 32 lanes per row, 8 rows per pass: consecutive rows are consecutive in memory
+    for (int r = tid >> 5; r < nr; r += 8) {
+      const int c = tid & 31;
+      const unsigned int* src = Xw + (r0 + r) * rw;
+      for (int cc = c; cc < ndw; cc += 32) rows[r * pitch + cc] = src[cc];
+    }
+    __syncthreads();
+    if (!mine) continue;
+    const unsigned char* xr = rowb + tid * pitch * 4;
+    for (int t0 = 0; t0 < T; t0 += TG) {
+      if (t0 > 0) {
+#pragma unroll
+        for (int u = 0; u < TG; ++u) {
+          node[u] = t0 + u < T ? node_of[(long long)(t0 + u) * n + i] : -1;
+          if (KEYS) w[u] = (t0 + u < T && weight) ? weight[(long long)(t0 + u) * n + i] : 1u;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < TG; ++u) {
+        if (t0 + u >= T) break;
+        const long long k = (long long)(t0 + u) * n + i;
+        if (node[u] < 0) {
+          if (KEYS) keys[k] = dead;
+          continue;
+        }
+        const unsigned int e = tab[(t0 + u) * nodes + node[u]];
+        const unsigned int f = e & 0xFFu;
+        if (f == 0xFFu) {
+          node_of[k] = -1;
+          if (KEYS) keys[k] = dead;
+          continue;
+        }
+        const unsigned int b = xr[f];
+        const int nn = (int)(e >> 16) + (b > ((e >> 8) & 0xFFu) ? 1 : 0);
+        node_of[k] = nn;
+        if (KEYS) keys[k] = (t0 + u) * width + nn + (w[u] == 0 ? T * width : 0);
+      }
+    }
+  }
+}
+
+// Poisson(1) bootstrap counts of every (tree, row), [T][n] uint8, in one pass: a counter-
+// based hash (splitmix64 of seed and the flat index) gives one 24-bit uniform per entry and
+// the inverse CDF (P(X <= k), k < 23, in constant memory) turns it into a count -- the
+// distribution torch.poisson / rand + bucketize give, without the 4-byte uniforms and 8-byte
+// bucket indices they write and re-read.  Four entries per thread, one dword store.
+__constant__ float kPoissonCdf[23];
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ unsigned int poisson1(unsigned long long seed, unsigned long long k) {
+  const float u = (float)(splitmix64(seed ^ (k * 0xD1B54A32D192ED03ull)) >> 40) *
+                  (1.0f / 16777216.0f);
+  unsigned int c = 0;
+  while (c < 23 && kPoissonCdf[c] <= u) ++c;
+  return c;
+}
+
+__global__ __launch_bounds__(256) void rdf_poisson_weights(unsigned long long seed,
+                                                           long long total,
+                                                           unsigned char* __restrict__ out) {
+  const long long nq = (total + 3) / 4;
+  for (long long q = (long long)blockIdx.x * 256 + threadIdx.x; q < nq;
+       q += (long long)gridDim.x * 256) {
+    const long long k0 = q * 4;
+    if (k0 + 4 <= total) {
+      unsigned int v = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v |= poisson1(seed, (unsigned long long)(k0 + j)) << (8 * j);
+      reinterpret_cast<unsigned int*>(out)[q] = v;
+    } else {
+      for (long long k = k0; k < total; ++k) out[k] = (unsigned char)poisson1(seed, k);
     }
   }
 }
@@ -912,12 +1045,43 @@ int oryx_rdf_histogram(const void* Xb, int bin_bytes, long long n, int P, const 
   return oryx_check_launch();
 }
 
-int oryx_rdf_route(const void* Xb, int bin_bytes, long long n, int P, int T, int* node_of,
-                   int nodes, const int* split_feat, const int* split_bin,
+// rdf_route_lds when it applies (byte bins, no categorical split tables, dword-aligned rows,
+// the packed table fields fit, LDS fits); returns false to fall back to rdf_route_rows.
+static bool route_lds_launch(const void* Xb, int bin_bytes, long long n, int P, int p_used,
+                             int T, int* node_of, int nodes, const int* split_feat,
+                             const int* split_bin, const unsigned char* cat_left,
+                             const int* child_base, const unsigned char* weight, int width,
+                             int* keys, hipStream_t s) {
+  static const bool off = getenv("ORYX_RDF_ROUTE_LDS") && atoi(getenv("ORYX_RDF_ROUTE_LDS")) == 0;
+  if (off || bin_bytes != 1 || cat_left || P % 4 != 0 || p_used <= 0 || p_used > 255 ||
+      p_used > P || 2LL * nodes >= 65536)
+    return false;
+  const int ndw = (p_used + 3) / 4;
+  const int pitch = ndw | 1;
+  const size_t smem = ((size_t)T * nodes + 256 * (size_t)pitch) * 4;
+  if (smem > 64 * 1024) return false;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (keys)
+    hipLaunchKernelGGL(rdf_route_lds<true>, dim3((unsigned)blocks), dim3(256), smem, s,
+                       reinterpret_cast<const unsigned char*>(Xb), n, P, ndw, pitch, T, node_of,
+                       nodes, split_feat, split_bin, child_base, weight, width, keys);
+  else
+    hipLaunchKernelGGL(rdf_route_lds<false>, dim3((unsigned)blocks), dim3(256), smem, s,
+                       reinterpret_cast<const unsigned char*>(Xb), n, P, ndw, pitch, T, node_of,
+                       nodes, split_feat, split_bin, child_base, nullptr, 0, nullptr);
+  return true;
+}
+
+int oryx_rdf_route(const void* Xb, int bin_bytes, long long n, int P, int p_used, int T,
+                   int* node_of, int nodes, const int* split_feat, const int* split_bin,
                    const unsigned char* cat_left, int B, const int* child_base,
                    unsigned long long* visits, void* stream) {
   if (n <= 0 || T <= 0) return ORYX_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!visits && route_lds_launch(Xb, bin_bytes, n, P, p_used, T, node_of, nodes, split_feat,
+                                  split_bin, cat_left, child_base, nullptr, 1, nullptr, s))
+    return oryx_check_launch();
   if (!visits) {
     long long blocks = (n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
@@ -959,13 +1123,16 @@ int oryx_rdf_route(const void* Xb, int bin_bytes, long long n, int P, int T, int
 
 // Route every open row one level down AND write the next level's counting-sort keys
 // (keys [T][n] int32, next-level width `width`; weight [T][n] nullable) in one pass.
-int oryx_rdf_route_keys(const void* Xb, int bin_bytes, long long n, int P, int T, int* node_of,
-                        int nodes, const int* split_feat, const int* split_bin,
+int oryx_rdf_route_keys(const void* Xb, int bin_bytes, long long n, int P, int p_used, int T,
+                        int* node_of, int nodes, const int* split_feat, const int* split_bin,
                         const unsigned char* cat_left, int B, const int* child_base,
                         const unsigned char* weight, int width, int* keys, void* stream) {
   if (n <= 0 || T <= 0) return ORYX_OK;
   if (!keys || width <= 0 || 2LL * T * width >= (1LL << 31)) return ORYX_EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (route_lds_launch(Xb, bin_bytes, n, P, p_used, T, node_of, nodes, split_feat, split_bin,
+                       cat_left, child_base, weight, width, keys, s))
+    return oryx_check_launch();
   long long blocks = (n + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (bin_bytes == 1)
@@ -981,7 +1148,7 @@ int oryx_rdf_route_keys(const void* Xb, int bin_bytes, long long n, int P, int T
   return oryx_check_launch();
 }
 
-int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
+int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P, int p_used,
                               const int* label, const float* y, int S, int cls,
                               const unsigned char* weight, const int* perm,
                               const int* piece_tree, const int* piece_node,
@@ -998,9 +1165,11 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
   static const bool staged_ok =
       !(getenv("ORYX_RDF_HIST") && atoi(getenv("ORYX_RDF_HIST")) == 0);
   if (staged_ok && bin_bytes == 1 && n * (long long)P < (1LL << 34) && n * (long long)P >= 4) {
-    // dwords covering any row alignment; a row pitch that is a multiple of 4 bytes (the
-    // padded pitch of ops/rdf.py) starts every row on a dword, so the pitch itself suffices
-    const int ndw = P % 4 == 0 ? P / 4 : (P + 3) / 4 + 1;
+    // dwords covering the row's used bytes (p_used <= P: the padding of a padded pitch is
+    // never read) at any row alignment; a row pitch that is a multiple of 4 bytes (the padded
+    // pitch of ops/rdf.py) starts every row on a dword
+    const int pu = p_used > 0 && p_used < P ? p_used : P;
+    const int ndw = P % 4 == 0 ? (pu + 3) / 4 : (pu + 3) / 4 + 1;
     const int rsw = ndw | 1;
     const long long smem_st = per_node_bytes + ((Fs + 3) & ~3) * 4LL + 256LL * rsw * 4;
     if (smem_st <= 64 * 1024) {
@@ -1063,6 +1232,32 @@ int oryx_rdf_node_totals(const int* node_of, const unsigned char* weight, const 
   else
     hipLaunchKernelGGL(rdf_node_totals<false>, grid, dim3(256), smem, s, node_of, weight, label,
                        y, S, n, width, rpb, hist, visits);
+  return oryx_check_launch();
+}
+
+// Poisson(1) bootstrap weights [total] uint8 (total = T * n; out 4-byte aligned).
+int oryx_rdf_poisson_weights(unsigned long long seed, long long total, unsigned char* out,
+                             void* stream) {
+  if (total <= 0) return ORYX_OK;
+  if (reinterpret_cast<unsigned long long>(out) & 3) return ORYX_EINVAL;
+  static bool table = false;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!table) {
+    float cdf[23];
+    double p = std::exp(-1.0), acc = 0.0;
+    for (int k = 0; k < 23; ++k) {
+      acc += p;
+      cdf[k] = (float)acc;
+      p /= (double)(k + 1);
+    }
+    if (hipMemcpyToSymbol(HIP_SYMBOL(kPoissonCdf), cdf, sizeof(cdf)) != hipSuccess)
+      return ORYX_ELAUNCH;
+    table = true;
+  }
+  long long blocks = ((total + 3) / 4 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(rdf_poisson_weights, dim3((unsigned)blocks), dim3(256), 0, s, seed, total,
+                     out);
   return oryx_check_launch();
 }
 

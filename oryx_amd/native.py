@@ -285,13 +285,15 @@ def _load_kernels():
     _sig(lib, "oryx_topn_max_queries", c_i, [c_i])
     _sig(lib, "oryx_counting_sort", c_i, [c_vp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp])
     # ..., hist, n_live (device piece count, nullable), stream
-    _sig(lib, "oryx_rdf_histogram_pieces", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i,
+    _sig(lib, "oryx_rdf_histogram_pieces", c_i, [c_vp, c_i, c_ll, c_i, c_i, c_vp, c_vp, c_i, c_i,
                                                  c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                                  c_vp, c_i, c_i, c_vp, c_vp, c_vp])
-    # Xb, bin_bytes, n, P, T, node_of, nodes, feat, bin, cat_left, B, child_base, weight,
-    # width, keys, stream
-    _sig(lib, "oryx_rdf_route_keys", c_i, [c_vp, c_i, c_ll, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp,
-                                           c_i, c_vp, c_vp, c_i, c_vp, c_vp])
+    # seed, total, out, stream
+    _sig(lib, "oryx_rdf_poisson_weights", c_i, [ctypes.c_ulonglong, c_ll, c_vp, c_vp])
+    # Xb, bin_bytes, n, P, p_used, T, node_of, nodes, feat, bin, cat_left, B, child_base,
+    # weight, width, keys, stream
+    _sig(lib, "oryx_rdf_route_keys", c_i, [c_vp, c_i, c_ll, c_i, c_i, c_i, c_vp, c_i, c_vp, c_vp,
+                                           c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_vp])
     # node_of, weight, label, y, S, cls, T, n, width, hist, visits, stream
     _sig(lib, "oryx_rdf_node_totals", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_i, c_ll, c_i,
                                             c_vp, c_vp, c_vp])
@@ -317,11 +319,11 @@ def _load_kernels():
     # hist, stream
     _sig(lib, "oryx_rdf_histogram", c_i, [c_vp, c_i, c_ll, c_i, c_vp, c_vp, c_i, c_i, c_vp, c_i,
                                           c_vp, c_i, c_i, c_vp, c_i, c_i, c_vp, c_vp])
-    # Xb, bin_bytes, n, P, T, node_of, nodes, split_feat, split_bin, cat_left, B, child_base,
-    # visits, stream
+    # Xb, bin_bytes, n, P (row pitch), p_used (bytes of a row in use), T, node_of, nodes,
+    # split_feat, split_bin, cat_left, B, child_base, visits, stream
     _sig(lib, "oryx_rdf_sort_keys", c_i, [c_vp, c_vp, c_i, c_ll, c_i, c_vp, c_vp])
-    _sig(lib, "oryx_rdf_route", c_i, [c_vp, c_i, c_ll, c_i, c_i, c_vp, c_i, c_vp, c_vp, c_vp,
-                                      c_i, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_rdf_route", c_i, [c_vp, c_i, c_ll, c_i, c_i, c_i, c_vp, c_i, c_vp, c_vp,
+                                      c_vp, c_i, c_vp, c_vp, c_vp])
     # X, n, F, T, roots, feat, thr, cat_off, cat_bits, cat_len, left, right, leaf, stream
     _sig(lib, "oryx_rdf_forest_leaf", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp, c_vp, c_vp,
                                             c_vp, c_vp, c_vp, c_vp, c_vp])

@@ -423,7 +423,7 @@ def _histogram_groups(data: BinnedData, label, y, S, cls, weight, groups: RowGro
     lib = native.require_kernels()
     fe = feats.contiguous()
     rc = lib.oryx_rdf_histogram_pieces(
-        data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0),
+        data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0), P,
         label.data_ptr() if cls else None,
         None if cls else y.data_ptr(), S, int(cls),
         weight.data_ptr() if weight is not None else None,
@@ -450,7 +450,8 @@ def _route(data: BinnedData, node_of, nodes, split: LevelSplits, child_base, B,
         sf = split.feat.int().contiguous()
         sb = split.bin.int().contiguous()
         cb = child_base.int().contiguous()
-        rc = lib.oryx_rdf_route(data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0), T,
+        rc = lib.oryx_rdf_route(data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0),
+                                data.Xb.shape[1], T,
                                 node_of.data_ptr(), nodes, sf.data_ptr(), sb.data_ptr(),
                                 cl.data_ptr() if cl is not None else None, B, cb.data_ptr(),
                                 visits.data_ptr() if visits is not None else None,
@@ -537,7 +538,14 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
             dist.all_reduce_sum(s, ctx)
         y_shift = float(s[0] / s[1].clamp_min(1.0))
         y = (yd - y_shift).to(torch.float32).contiguous()
-    if T > 1:
+    if T > 1 and dev.type == "cuda":
+        # one fused pass (rdf_poisson_weights: hashed uniforms through the Poisson(1) inverse
+        # CDF, uint8 out) instead of rand + bucketize + cast over T x n
+        weight = torch.empty((T, n), dtype=torch.uint8, device=dev)
+        native.check(native.require_kernels().oryx_rdf_poisson_weights(
+            (seed * 31 + ctx.rank + 7) & ((1 << 64) - 1), T * n, weight.data_ptr(),
+            native.stream_ptr(dev)), "oryx_rdf_poisson_weights")
+    elif T > 1:
         gd = torch.Generator(device=dev)
         gd.manual_seed((seed * 31 + ctx.rank + 7) & ((1 << 62) - 1))
         # Poisson(1) bootstrap counts by inverse CDF of one uniform per (tree, row): same
@@ -740,24 +748,29 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
         cat_h = lv["cat"].numpy() if lv["cat"] is not None else None
         np.add.at(predictor_counts, lv["feat"].numpy()[lv["feat"].numpy() >= 0],
                   lv["vis"].numpy()[lv["feat"].numpy() >= 0])
+        # label statistics stay numpy row views (not containers the cyclic GC tracks: as
+        # Python lists, ~10^4 more tracked objects per forest made the collector's passes
+        # over the live trees cost more than the build itself)
+        tot_l = tot_h
         new_level: List[List[Optional[TrainedNode]]] = []
+        TN = TrainedNode
         for t in range(T):
             row: List[Optional[TrainedNode]] = []
-            ft, bt, vt, st = feat_l[t], bin_l[t], vis_l[t], tot_h[t]
-            for slot, node in enumerate(level_nodes[t]):
-                node.count = vt[slot]
-                node.stats = st[slot]
-                f = ft[slot]
+            app = row.append
+            for slot, (node, f, b, c, st) in enumerate(zip(level_nodes[t], feat_l[t], bin_l[t],
+                                                          vis_l[t], tot_l[t])):
+                node.count = c
+                node.stats = st
                 if f >= 0:
                     node.feature = f
-                    node.bin = bt[slot]
-                    if node.bin < 0:
+                    node.bin = b
+                    if b < 0:
                         node.cat_left = np.nonzero(cat_h[t, slot])[0]
                     nid = node.id
-                    node.left = left = TrainedNode(nid + "-")
-                    node.right = right = TrainedNode(nid + "+")
-                    row.append(left)
-                    row.append(right)
+                    node.left = left = TN(nid + "-")
+                    node.right = right = TN(nid + "+")
+                    app(left)
+                    app(right)
             new_level.append(row)
         level_nodes = new_level
 
@@ -816,7 +829,7 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
             fe = feats[:, lo:hi].contiguous()
             hist = torch.zeros((T, hi - lo, Fs, B, S), dtype=torch.float32, device=dev)
             native.check(lib.oryx_rdf_histogram_pieces(
-                data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0),
+                data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0), P,
                 label.data_ptr() if classification else None,
                 None if classification else y.data_ptr(), S, int(classification),
                 weight.data_ptr() if weight is not None else None,
@@ -865,7 +878,7 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
                 sb = split.bin.int().contiguous()
                 cb = child_base.int().contiguous()
                 native.check(lib.oryx_rdf_route_keys(
-                    data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0), T,
+                    data.Xb.data_ptr(), data.bin_bytes, n, data.Xb.stride(0), P, T,
                     node_of.data_ptr(), W, sf.data_ptr(), sb.data_ptr(),
                     cl.data_ptr() if cl is not None else None, B, cb.data_ptr(),
                     weight.data_ptr() if weight is not None else None, W2, keys.data_ptr(),

@@ -642,3 +642,23 @@ def test_device_level_loop_matches_host_loop(cuda, classification, monkeypatch):
     monkeypatch.setattr(rdf_ops, "_DEVICE_LOOP", True)
     f = rdf_ops.train_forest(data, tgt, 2 if classification else 0, 6, 5, kind, seed=4)
     assert all(r.feature >= 0 and r.count == 30000 for r in f.roots)
+
+
+@pytest.mark.gpu
+def test_device_poisson_bootstrap_weights(cuda):
+    """rdf_poisson_weights: Poisson(1) counts (mean 1, variance 1, P(0) = 1/e), deterministic
+    per seed, different across seeds, any length (tail handling)."""
+    from oryx_amd import native
+    lib = native.require_kernels()
+    out = {}
+    for seed, total in ((5, 4_000_003), (5, 4_000_003), (6, 4_000_003)):
+        w = torch.empty(total, dtype=torch.uint8, device=cuda)
+        native.check(lib.oryx_rdf_poisson_weights(seed, total, w.data_ptr(),
+                                                  native.stream_ptr(cuda)), "poisson")
+        out.setdefault(seed, []).append(w.cpu())
+    a = out[5][0].double()
+    assert abs(a.mean().item() - 1.0) < 3e-3 and abs(a.var().item() - 1.0) < 5e-3
+    assert abs((a == 0).double().mean().item() - np.exp(-1.0)) < 2e-3
+    assert abs((a == 2).double().mean().item() - np.exp(-1.0) / 2) < 2e-3
+    assert torch.equal(out[5][0], out[5][1])
+    assert not torch.equal(out[5][0], out[6][0])
