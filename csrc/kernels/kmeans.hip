@@ -229,10 +229,18 @@ __device__ __forceinline__ float km_packi(float x, unsigned idx, unsigned mask) 
   return __uint_as_float((__float_as_uint(x) & ~mask) | idx);
 }
 
+// v_max_f32 without the operand canonicalisation fmaxf gets (the packed values are finite
+// numbers, never signalling NaNs): one instruction instead of three
+__device__ __forceinline__ float km_max2(float a, float b) {
+  float m;
+  asm("v_max_f32 %0, %1, %2" : "=v"(m) : "v"(a), "v"(b));
+  return m;
+}
+
 __device__ __forceinline__ void km_insert3(float p, float& b1, float& b2, float& b3) {
   b3 = __builtin_amdgcn_fmed3f(b2, b3, p);
   b2 = __builtin_amdgcn_fmed3f(b1, b2, p);
-  b1 = fmaxf(b1, p);
+  b1 = km_max2(b1, p);
 }
 
 // Most groups hold nothing above the lane's third best once the scan is under way: a group
@@ -243,7 +251,7 @@ __device__ __forceinline__ void km_epilogue_top3(const f32x4& ac, int ctg, int g
   float p[4];
 #pragma unroll
   for (int v = 0; v < 4; ++v) p[v] = km_packi(ac[v], base + v, mask);
-  const float m = fmaxf(km_max3(p[0], p[1], p[2]), p[3]);
+  const float m = km_max3(km_max3(p[0], p[1], p[2]), p[3], p[3]);
   if (__builtin_expect(__any(m > b3), 0)) {
 #pragma unroll
     for (int v = 0; v < 4; ++v) km_insert3(p[v], b1, b2, b3);
