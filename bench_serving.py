@@ -193,6 +193,8 @@ def time_to_ready(items: int, users: int, features: int, seed: int) -> dict:
     import tempfile
     import torch
     from oryx_amd import ingest
+    from oryx_amd.models.als import serving as als_serving
+    from oryx_amd.serving import layer as serving_layer
     from oryx_amd.serving.layer import ServingLayer
     from oryx_amd.transport import log as tlog
     from oryx_amd.utils import config as cfg, pmml as pmmlu
@@ -278,6 +280,8 @@ def time_to_ready(items: int, users: int, features: int, seed: int) -> dict:
                 "update_log_gb": log_bytes / 1e9, "log_build_s": gen_s, "ready_s": ready_s,
                 "rows_per_s": (items + users) / ready_s,
                 "first_query_s": first_query_s, "model_hbm_gib": hbm,
+                "drain": dict(als_serving.DRAIN_STATS),
+                "take": dict(serving_layer.TAKE_STATS, **ingest.PARSE_STATS),
                 "data": "synthetic Gaussian factors, Poisson(20) known items per user"}
     finally:
         shutil.rmtree(work, ignore_errors=True)

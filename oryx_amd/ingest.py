@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import json
+import time
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -577,6 +578,9 @@ def _known_mode(model):
     return None if hasattr(model, "add_known_items") else False
 
 
+PARSE_STATS = {"native_s": 0.0}
+
+
 def parse_up_records(raw_ptr: int, used: int, nrec: int, k: int, max_n: int,
                      known_dict: Optional["IdDict"] = None, frames: bool = False):
     """The leading run of ``UP`` records of a raw log poll buffer (see
@@ -592,10 +596,12 @@ def parse_up_records(raw_ptr: int, used: int, nrec: int, k: int, max_n: int,
     vp = ctypes.c_void_p
     fn = native.runtime().oryx_parse_up_frames if frames else \
         native.runtime().oryx_parse_up_records
+    t0 = time.perf_counter()
     got = fn(
         ctypes.c_void_p(raw_ptr), int(used), int(nrec), int(k), int(max_n),
         kinds.ctypes.data_as(vp), vecs.ctypes.data_as(vp), id_ends.ctypes.data_as(vp),
         kcnt.ctypes.data_as(vp), ctypes.byref(consumed))
+    PARSE_STATS["native_s"] += time.perf_counter() - t0
     if got <= 0:
         return 0, 0, None, None, None, None
     if known_dict is not None:

@@ -585,12 +585,15 @@ class ALSServingModel(ServingModel):
         with self._expected_lock:
             self._expected_users = set(users)
             self.X.remove_all_ids_from(self._expected_users)
+            # the expected rows arrive as UP messages next: room for all of them at once
+            self.X.reserve_extra(len(self._expected_users))
 
     def retain_recent_and_item_ids(self, items: Collection[str]) -> None:
         self.Y.retain_recent_and_ids(items)
         with self._expected_lock:
             self._expected_items = set(items)
             self.Y.remove_all_ids_from(self._expected_items)
+            self.Y.reserve_extra(len(self._expected_items))
 
     def retain_recent_and_known_items(self, users: Collection[str], items: Collection[str]
                                       ) -> None:
@@ -653,13 +656,25 @@ def drain_up_blocks(model, updates) -> int:
     with ThreadPoolExecutor(max_workers=1, thread_name_prefix="oryx-up-parse") as ex:
         fut = ex.submit(take, k, known_dict=kd)
         while True:
+            t0 = time.perf_counter()
             blk = fut.result()
+            t1 = time.perf_counter()
             if blk is None:
+                DRAIN_STATS["wait_s"] += t1 - t0
                 break
             fut = ex.submit(take, k, known_dict=kd)
             apply_up_parsed(model, *blk)
             done += len(blk[0])
+            DRAIN_STATS["wait_s"] += t1 - t0
+            DRAIN_STATS["apply_s"] += time.perf_counter() - t1
+            DRAIN_STATS["rows"] += len(blk[0])
+            DRAIN_STATS["blocks"] += 1
     return done
+
+
+# where a bulk model load spends its time (the bench's time-to-ready record reads these):
+# waiting for the parse thread's next block vs applying blocks on this thread
+DRAIN_STATS = {"wait_s": 0.0, "apply_s": 0.0, "rows": 0, "blocks": 0}
 
 
 def apply_up_parsed(model, kinds, ids, vecs, known, messages=None) -> None:
@@ -688,10 +703,13 @@ def _apply_parsed_run(model, kinds, ids, vecs, known, lo: int, hi: int) -> None:
         if not len(sel):
             continue
         # the bulk setters keep the last row of an ID repeated within the batch
+        t0 = time.perf_counter()
         if len(sel) == hi - lo:
             getattr(model, setter)(ids[lo:hi], vecs[lo:hi])
         else:
             getattr(model, setter)([ids[j] for j in sel.tolist()], vecs[sel])
+        DRAIN_STATS["set_" + setter[4:8] + "_s"] = \
+            DRAIN_STATS.get("set_" + setter[4:8] + "_s", 0.0) + time.perf_counter() - t0
         if known is None:
             continue
         if kind == 0 and isinstance(known, ingest.KnownCodes):

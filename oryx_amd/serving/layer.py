@@ -100,14 +100,20 @@ class UpdateIterator:
         readers = self.consumer.readers
         for step in range(len(readers)):
             r = readers[(self._rr + step) % len(readers)]
+            t0 = time.perf_counter()
             n = r.poll_frames(max_n)
             if not n:
                 continue
+            t1 = time.perf_counter()
             self._rr = (self._rr + step + 1) % len(readers)
             addr, used = r.frame_buffer()
             got, consumed, kinds, ids, vecs, known = ingest.parse_up_records(
                 addr, used, n, k, n, known_dict=known_dict, frames=True)
+            t2 = time.perf_counter()
             rest = r.decode_frames(consumed, n - got)
+            TAKE_STATS["poll_s"] += t1 - t0
+            TAKE_STATS["parse_s"] += t2 - t1
+            TAKE_STATS["rest_s"] += time.perf_counter() - t2
             self._pending = [KeyMessage(key, v) for _, _, key, v in rest]
             self._pending.reverse()
             return (kinds, ids, vecs, known) if got else None
@@ -115,6 +121,10 @@ class UpdateIterator:
 
     def close(self) -> None:
         self.closed = True
+
+
+# where the bulk UP reads of take_up_block spend their time (bench records read these)
+TAKE_STATS = {"poll_s": 0.0, "parse_s": 0.0, "rest_s": 0.0}
 
 
 def resource_modules(config) -> List[str]:
