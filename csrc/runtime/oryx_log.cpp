@@ -1152,8 +1152,33 @@ long long oryx_reader_poll_frames(void* rh, char* out, long long out_cap, int ma
         continue;
       }
     }
-    ssize_t got = pread(r->fd, out, (size_t)out_cap, r->pos);
-    if (got < 0) got = 0;
+    // the bulk read in 8 MB chunks on the native threads: one pread is a single-threaded
+    // page-cache copy (~5 GB/s), which bounded a 57 GB model load
+    ssize_t got = 0;
+    {
+      constexpr long long kChunk = 8LL << 20;
+      const long long nch = (out_cap + kChunk - 1) / kChunk;
+      std::vector<long long> cgot((size_t)nch, 0);
+      const int fd = r->fd;
+      const long long base = r->pos;
+      oryx_ff::parallel_ranges(nch, 1, [&](long long lo, long long hi, int) {
+        for (long long c = lo; c < hi; ++c) {
+          const long long off = c * kChunk;
+          const long long len = std::min(kChunk, out_cap - off);
+          long long done = 0;
+          while (done < len) {
+            const ssize_t g = pread(fd, out + off + done, (size_t)(len - done), base + off + done);
+            if (g <= 0) break;
+            done += g;
+          }
+          cgot[(size_t)c] = done;
+        }
+      });
+      for (long long c = 0; c < nch; ++c) {
+        got += (ssize_t)cgot[(size_t)c];
+        if (cgot[(size_t)c] < std::min(kChunk, out_cap - c * kChunk)) break;   // end of data
+      }
+    }
     std::vector<size_t> at;
     size_t p = 0;
     while ((long long)at.size() < max_records && p + kHeader <= (size_t)got) {
