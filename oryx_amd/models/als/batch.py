@@ -32,6 +32,7 @@ import json
 import logging
 import math
 import os
+import struct
 import time
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -268,12 +269,35 @@ def read_features(path: str) -> Tuple[List[str], np.ndarray]:
     return ids, mats[0] if len(mats) == 1 else np.concatenate(mats)
 
 
+def _i64(c: int) -> int:
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+_FP_MULS = [_i64(c) for c in (0x9E3779B97F4A7C15, 0xC2B2AE3D27D4EB4F, 0x165667B19E3779F9,
+                              0x27D4EB2F165667C5, 0xFF51AFD7ED558CCD)]
+
+
 def _fingerprint(u, i, s, *params) -> str:
     """Identity of one training run: the aggregated ratings plus every setting that shapes
-    the factors (a checkpoint is only resumed by the same run)."""
+    the factors (a checkpoint is only resumed by the same run).  The triples are mixed
+    where they live (the device after a GPU aggregation: no 0.5 s host copy and hash of 25M
+    triples): every (user, item, score bits, position) goes through a multiply-xorshift
+    mix, and two wrapping 64-bit sums of the mixes (one position-weighted) plus the count
+    and the settings are hashed."""
+    t = [a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
+         for a in (u, i, s)]
+    dev = t[0].device
+    n = t[0].numel()
+    c1, c2, c3, c4, c5 = _FP_MULS
+    k = torch.arange(n, device=dev, dtype=torch.int64)
+    x = t[0].to(torch.int64) * c1 + t[1].to(dev, torch.int64) * c2 + \
+        t[2].to(dev, torch.float64).view(torch.int64) * c3 + k * c4
+    x = x ^ (x >> 29)
+    x = x * c5
+    x = x ^ (x >> 32)
+    a, b = int(x.sum()), int((x * (k | 1)).sum())
     h = hashlib.blake2b(digest_size=20)
-    for a in (u, i, s):
-        h.update(np.ascontiguousarray(a).tobytes())
+    h.update(struct.pack("<qqq", n, a, b))
     h.update(repr(params).encode())
     return h.hexdigest()
 
@@ -459,7 +483,7 @@ class ALSUpdate(MLUpdate):
             tr_u = (torch.cumsum(mu, 0) - 1)[ud][part]
             tr_i = (torch.cumsum(mi, 0) - 1)[idv][part]
             tr_s = sd[part].to(torch.float32)
-            host_triples = lambda: (ud.cpu().numpy(), idv.cpu().numpy(), sd.cpu().numpy())
+            triples = lambda: (ud, idv, sd)        # fingerprinted on the device
         else:
             u, i, s = aggregate_scores(u, i, s, ts, self.implicit)
             n_agg = len(u)
@@ -478,7 +502,7 @@ class ALSUpdate(MLUpdate):
             tr_u = torch.from_numpy(remap_u[u][part])
             tr_i = torch.from_numpy(remap_i[i][part])
             tr_s = torch.from_numpy(s[part].astype(np.float32))
-            host_triples = lambda: (u, i, s)
+            triples = lambda: (u, i, s)
         seed = rng.next_seed()
         trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx, seed=seed,
                              precision=self.precision)
@@ -493,7 +517,7 @@ class ALSUpdate(MLUpdate):
         if self.checkpoint_interval > 0 and self.current_model_dir:
             # neither the world size nor the init seed: a checkpoint holds global factors, and
             # a group relaunched on fewer GPUs (parallel/elastic.py) resumes from it
-            fingerprint = _fingerprint(*host_triples(), features, lam, alpha, self.implicit,
+            fingerprint = _fingerprint(*triples(), features, lam, alpha, self.implicit,
                                        self.iterations)
             ckpt_dir = os.path.join(self.current_model_dir, ".checkpoint",
                                     "als-" + fingerprint[:16])
