@@ -23,6 +23,7 @@ passes returned -- every depth is exact.
 
 from __future__ import annotations
 
+import os
 import threading
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
@@ -64,9 +65,12 @@ _TORCH_DTYPE = {np.dtype(np.float32).str: torch.float32, np.dtype(np.int64).str:
                 np.dtype(np.int32).str: torch.int32, np.dtype(np.uint32).str: torch.int32}
 
 
+# fp32 scan bytes (rows x padded rank x 4) from which the bf16 scan is used
+BF16_MIN_BYTES = int(os.environ.get("ORYX_TOPN_BF16_MIN_BYTES", str(1 << 30)))
+
+
 def _bf16_default() -> bool:
     """The bf16 scan is on unless ORYX_TOPN_BF16=0 (it is exact: certified or rescanned)."""
-    import os
     return os.environ.get("ORYX_TOPN_BF16", "1") != "0"
 _KLS = (64, 256, 1024)  # per-(wave, query) list lengths the kernel is built for
 _KPS = (16, 32, 48, 64, 80, 96, 112, 128, 160, 192, 256)
@@ -302,8 +306,11 @@ class ItemIndex:
         return self.Ys, self.kp, None
 
     def _launch(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY):
+        # the bf16 scan halves the bytes a scan reads; below BF16_MIN_BYTES of fp32 rows the
+        # scan is launch-bound anyway and the exact re-rank's extra ops cost more than it saves
+        big = self.n * (self.kp or 0) * 4 >= BF16_MIN_BYTES
         shallow = [j for j, q in enumerate(qs) if q.how_many <= BF16_MAX_HOW_MANY] \
-            if self.bf16 and not cosine and kl == MAX_HOW_MANY and self.n > 0 else []
+            if self.bf16 and big and not cosine and kl == MAX_HOW_MANY and self.n > 0 else []
         if not shallow:
             return self._launch_fp32(qs, cosine, kl)
         out: List[Optional[Tuple[np.ndarray, np.ndarray]]] = [None] * len(qs)

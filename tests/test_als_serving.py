@@ -351,9 +351,10 @@ def _brute(Y, valid, q, how_many, cosine=False, allowed=None, exclude=()):
 @pytest.mark.parametrize("k,n", [(10, 5000), (50, 100_003), (250, 40_000)])
 @pytest.mark.parametrize("cosine", [False, True])
 @pytest.mark.parametrize("bf16", [True, False])
-def test_topn_kernel_matches_bruteforce(cuda, k, n, cosine, bf16):
+def test_topn_kernel_matches_bruteforce(cuda, k, n, cosine, bf16, monkeypatch):
     from oryx_amd.models.als.common import FeatureVectors
     from oryx_amd.ops import topn
+    monkeypatch.setattr(topn, "BF16_MIN_BYTES", 0)     # the bf16 scan at test sizes too
     g = np.random.default_rng(k + n)
     fv = FeatureVectors(k, cuda, row_pad=topn.row_pad_for(k))
     Y = g.standard_normal((n, k)).astype(np.float32)
@@ -378,13 +379,14 @@ def test_topn_kernel_matches_bruteforce(cuda, k, n, cosine, bf16):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", [50, 250])
-def test_topn_bf16_scan_exact_and_certified(cuda, k):
+def test_topn_bf16_scan_exact_and_certified(cuda, k, monkeypatch):
     """The bf16 scan + exact fp32 re-rank returns exactly torch.topk of the fp32 scores
     (same rows, scores to fp32 summation order), with exclusions; items built to tie within
     the bf16 error bound defeat the certificate and are rescanned in fp32 -- still exact; a
     value update reaches the bf16 mirror before the next query."""
     from oryx_amd.models.als.common import FeatureVectors
     from oryx_amd.ops import topn
+    monkeypatch.setattr(topn, "BF16_MIN_BYTES", 0)
     g = np.random.default_rng(k)
     n = 50_000
     fv = FeatureVectors(k, cuda, row_pad=topn.row_pad_for(k))
