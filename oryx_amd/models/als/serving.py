@@ -136,46 +136,71 @@ class TopNBatcher:
         return slot[1]
 
     def _run(self) -> None:
+        """The worker: takes the queued requests as one batch and launches it; while that
+        batch's kernel and copy back run, the next batch is taken and launched, and only then
+        is the first one finished (ItemIndex.scan_async) -- the host work of one batch
+        overlaps the device work of the other."""
+        pending = None            # (batch, finish, t_launch, error) of the batch in flight
         while True:
+            batch = None
             with self._cv:
-                while (not self._queue or self._busy) and not self._closed:
-                    self._cv.wait()
-                if self._closed and not self._queue:
-                    return
-                while self._busy:          # closing: let an inline launch finish first
-                    self._cv.wait()
-                # wait for stragglers when asked to, or when requests queued up while the
-                # previous launch ran (concurrent clients): a tenth of that launch's time
-                wait = self.wait_s
-                if self._contended and self._last_scan_s > 0:
-                    wait = max(wait, min(0.1 * self._last_scan_s, 0.005))
-                if wait > 0 and len(self._queue) < self.max_batch:
-                    deadline = time.monotonic() + wait
-                    while len(self._queue) < self.max_batch:
-                        left = deadline - time.monotonic()
-                        if left <= 0:
-                            break
-                        self._cv.wait(left)
-                batch = self._queue[:self.max_batch]
-                del self._queue[:len(batch)]
-                self._busy = True
-            t_scan = time.monotonic()
+                if pending is None:
+                    while (not self._queue or self._busy) and not self._closed:
+                        self._cv.wait()
+                    if self._closed and not self._queue:
+                        return
+                    while self._busy:          # closing: let an inline launch finish first
+                        self._cv.wait()
+                    # wait for stragglers when asked to, or when requests queued up while the
+                    # previous launch ran (concurrent clients): a tenth of that launch's time
+                    wait = self.wait_s
+                    if self._contended and self._last_scan_s > 0:
+                        wait = max(wait, min(0.1 * self._last_scan_s, 0.005))
+                    if wait > 0 and len(self._queue) < self.max_batch:
+                        deadline = time.monotonic() + wait
+                        while len(self._queue) < self.max_batch:
+                            left = deadline - time.monotonic()
+                            if left <= 0:
+                                break
+                            self._cv.wait(left)
+                if self._queue:
+                    batch = self._queue[:self.max_batch]
+                    del self._queue[:len(batch)]
+                    self._busy = True
+            launched = None
+            if batch is not None:
+                t_scan = time.monotonic()
+                try:
+                    launched = (batch, self.index.scan_async([b[0] for b in batch]), t_scan,
+                                None)
+                except Exception as e:   # answered to every waiting request
+                    launched = (batch, None, t_scan, e)
+            if pending is not None:
+                self._finish(pending, more=launched is not None)
+            pending = launched
+
+    def _finish(self, pending, more: bool) -> None:
+        batch, fin, t_scan, err = pending
+        if err is None:
             try:
-                res = self.index.scan([b[0] for b in batch])
+                res = fin()
                 for b, r in zip(batch, res):
                     b[1] = r
-            except Exception as e:   # answered to every waiting request
-                for b in batch:
-                    b[2] = e
-            self._last_scan_s = time.monotonic() - t_scan
-            with self._cv:
-                self.batches += 1
-                self.requests += len(batch)
-                self._contended = bool(self._queue) or len(batch) > 1
-                self._busy = False
-                self._cv.notify_all()
+            except Exception as e:
+                err = e
+        if err is not None:
             for b in batch:
-                b[3].set()
+                b[2] = err
+        with self._cv:
+            self._last_scan_s = time.monotonic() - t_scan
+            self.batches += 1
+            self.requests += len(batch)
+            self._contended = bool(self._queue) or len(batch) > 1 or more
+            if not more:
+                self._busy = False
+            self._cv.notify_all()
+        for b in batch:
+            b[3].set()
 
     def close(self) -> None:
         with self._cv:

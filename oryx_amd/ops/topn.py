@@ -272,6 +272,24 @@ class ItemIndex:
                     out[j] = r
         return out
 
+    def scan_async(self, queries: Sequence[TopNQuery]):
+        """Launch :meth:`scan` and return ``finish()`` -> its results.  A batch that is one
+        fp32 launch (the common micro-batch) only queues its work here: the kernel, the
+        merge and the copy back into pinned memory run while the caller prepares the next
+        batch, and ``finish()`` waits for them; anything else completes inside this call."""
+        self.refresh()
+        if queries and self.n > 0 and len(queries) <= MAX_BATCH:
+            cos = bool(queries[0].cosine)
+            kl = next((v for v in _KLS if v >= max(q.how_many for q in queries)), None)
+            if kl is not None and all(bool(q.cosine) == cos for q in queries) and \
+                    len(queries) <= int(native.require_kernels().oryx_topn_max_queries(kl)) \
+                    and not self._bf16_queries(queries, cos, kl):
+                # the scan groups by list length: one group only when every query maps to kl
+                if all(next(v for v in _KLS if v >= q.how_many) == kl for q in queries):
+                    return self._launch_fp32(queries, cos, kl, asynchronous=True)
+        out = self.scan(queries)
+        return lambda: out
+
     def _scan_deep(self, q: TopNQuery) -> Tuple[np.ndarray, np.ndarray]:
         """``how_many`` beyond one list: passes of the deepest list, each excluding the rows
         the previous passes returned (scores arrive in descending order across passes)."""
@@ -305,12 +323,17 @@ class ItemIndex:
             return mat, ld, self.perm
         return self.Ys, self.kp, None
 
-    def _launch(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY):
-        # the bf16 scan halves the bytes a scan reads; below BF16_MIN_BYTES of fp32 rows the
-        # scan is launch-bound anyway and the exact re-rank's extra ops cost more than it saves
+    def _bf16_queries(self, qs: Sequence[TopNQuery], cosine: bool, kl: int) -> List[int]:
+        """Positions of the queries the bf16 scan takes.  It halves the bytes a scan reads;
+        below BF16_MIN_BYTES of fp32 rows the scan is launch-bound anyway and the exact
+        re-rank's extra ops cost more than it saves."""
         big = self.n * (self.kp or 0) * 4 >= BF16_MIN_BYTES
-        shallow = [j for j, q in enumerate(qs) if q.how_many <= BF16_MAX_HOW_MANY] \
-            if self.bf16 and big and not cosine and kl == MAX_HOW_MANY and self.n > 0 else []
+        if not (self.bf16 and big and not cosine and kl == MAX_HOW_MANY and self.n > 0):
+            return []
+        return [j for j, q in enumerate(qs) if q.how_many <= BF16_MAX_HOW_MANY]
+
+    def _launch(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY):
+        shallow = self._bf16_queries(qs, cosine, kl)
         if not shallow:
             return self._launch_fp32(qs, cosine, kl)
         out: List[Optional[Tuple[np.ndarray, np.ndarray]]] = [None] * len(qs)
@@ -426,9 +449,10 @@ class ItemIndex:
                 failed.append(j)
         return out, failed
 
-    def _finish_one(self, vj: np.ndarray, pj: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    def _finish_one(self, vj: np.ndarray, pj: np.ndarray,
+                    row_of_pos: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
         keep = np.isfinite(vj) & (pj >= 0)
-        rows = self.row_of_pos_h[pj[keep]]
+        rows = (self.row_of_pos_h if row_of_pos is None else row_of_pos)[pj[keep]]
         vj = np.asarray(vj[keep], dtype=np.float32)
         valid_h = self.store._host_valid if self.borrowed else None
         if valid_h is not None and len(rows):
@@ -505,16 +529,19 @@ class ItemIndex:
         ex_d = next(rest) if ex is not None else None
         return Qd, rs_d, t0_d, bits_d, ptr_d, ex_d, len(rs), n_tiles
 
-    def _launch_fp32(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY):
+    def _launch_fp32(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY,
+                     asynchronous: bool = False):
         empty = (np.zeros(0, dtype=np.int64), np.zeros(0, dtype=np.float32))
-        if self.n == 0:
-            return [empty for _ in qs]
+        if self.n == 0 or not qs:
+            out = [empty for _ in qs]
+            return (lambda: out) if asynchronous else out
         dev = self.device
         lib = native.require_kernels()
         nq = len(qs)
         prep = self._prep(qs, self.kp)
         if prep is None:
-            return [empty for _ in qs]
+            out = [empty for _ in qs]
+            return (lambda: out) if asynchronous else out
         Qd, rs_d, t0_d, bits_d, ptr_d, ex_d, n_ranges, n_tiles = prep
         waves = int(lib.oryx_topn_waves_kl(n_tiles, kl))
         o_sc = torch.empty((waves, nq, kl), dtype=torch.float32, device=dev)
@@ -536,11 +563,25 @@ class ItemIndex:
         rw = o_rw.permute(1, 0, 2).reshape(nq, -1)
         v, i = torch.topk(sc, m, dim=1)
         pos = torch.gather(rw, 1, i)
-        h = torch.cat([v.view(torch.int32), pos], 1).cpu().numpy()     # one copy back
-        v_h, pos_h = h[:, :m].view(np.float32), h[:, m:]
-        # (a row removed between the permutation and the launch is never returned)
-        return [self._finish_one(v_h[j, :q.how_many], pos_h[j, :q.how_many])
-                for j, q in enumerate(qs)]
+        hd = torch.cat([v.view(torch.int32), pos], 1)
+        rop = self.row_of_pos_h          # the permutation these positions refer to
+
+        def finish(h):
+            v_h, pos_h = h[:, :m].view(np.float32), h[:, m:]
+            # (a row removed between the permutation and the launch is never returned)
+            return [self._finish_one(v_h[j, :q.how_many], pos_h[j, :q.how_many], rop)
+                    for j, q in enumerate(qs)]
+        if not asynchronous:
+            return finish(hd.cpu().numpy())                               # one copy back
+        host = torch.empty(hd.shape, dtype=torch.int32, pin_memory=True)
+        host.copy_(hd, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+
+        def wait_and_finish():
+            ev.synchronize()
+            return finish(host.numpy())
+        return wait_and_finish
 
     # ------------------------------------------------------------------ all scores
     def all_scores_device(self, target: np.ndarray, cosine: bool, candidates=None,
@@ -645,6 +686,10 @@ class ShardedItemIndex:
             for f in [self._pool.submit(sh.refresh, state) for sh in self.shards]:
                 f.result()
             self.version = state[0]
+
+    def scan_async(self, queries: Sequence[TopNQuery]):
+        out = self.scan(queries)
+        return lambda: out
 
     def scan(self, queries: Sequence[TopNQuery]) -> List[Tuple[np.ndarray, np.ndarray]]:
         self.refresh()
