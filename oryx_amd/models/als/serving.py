@@ -171,8 +171,14 @@ class TopNBatcher:
             if batch is not None:
                 t_scan = time.monotonic()
                 try:
-                    launched = (batch, self.index.scan_async([b[0] for b in batch]), t_scan,
-                                None)
+                    qs = [b[0] for b in batch]
+                    start = getattr(self.index, "scan_async", None)
+                    if start is not None:
+                        fin = start(qs)
+                    else:                      # an index without asynchronous launches
+                        res = self.index.scan(qs)
+                        fin = lambda: res     # noqa: E731
+                    launched = (batch, fin, t_scan, None)
                 except Exception as e:   # answered to every waiting request
                     launched = (batch, None, t_scan, e)
             if pending is not None:
