@@ -351,4 +351,10 @@ def main(argv=None) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    rc = main()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    # no interpreter finalisation: a daemon thread (HTTP handlers, the top-N batcher) that
+    # returns from a GIL-free native call while the interpreter shuts down is ended with a
+    # forced unwind, which aborts the process after the records are already written
+    os._exit(rc)

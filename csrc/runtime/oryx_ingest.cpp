@@ -3178,4 +3178,111 @@ long long oryx_format_leaf_updates(long long n, const long long* trees, const ch
   return o - out;
 }
 
+// Top-N launch inputs of one batch (ops/topn.py ItemIndex._prep) packed into `out` (the
+// pinned staging buffer of the single host-to-device copy), sections 16-byte aligned in this
+// order: Q [max_batch][kp] fp32 (targets, zero padded), ranges [nr][2] i64 (the union of the
+// queries' LSH buckets as merged store-position ranges; the whole store without LSH), tile0
+// [nr + 1] i64 (16-row tile prefix), then with LSH per-query bucket bitmaps [nq][words] u32
+// (bit b of word b / 32), then with exclusions ptr [nq + 1] i32 and the sorted excluded
+// positions ex [max(1, total)] i32.  cand_ptr == nullptr: no LSH; cand_all[j] = 1: query j
+// scans every bucket.  ex_ptr == nullptr: no exclusions.  info: n_ranges, n_tiles, and the
+// byte offsets of ranges, tile0, bits, ptr, ex (-1 when absent), then the bytes used.
+// Returns 0, 1 when no range is left to scan, -1 when `out` is too small.
+long long oryx_topn_prep(int nq, int k, int kp, int max_batch, const float* targets,
+                         const long long* cand_ptr, const long long* cand,
+                         const unsigned char* cand_all, int num_buckets, int words,
+                         const long long* bucket_start, long long n_rows, const long long* ex_ptr,
+                         const long long* ex_rows, const long long* pos_of_row, long long n_pos,
+                         unsigned char* out, long long out_cap, long long* info) {
+  auto al = [](long long v) { return (v + 15) & ~15LL; };
+  std::vector<std::pair<long long, long long>> rs;
+  std::vector<uint32_t> bits;
+  if (cand_ptr) {
+    bits.assign((size_t)nq * (size_t)words, 0u);
+    std::vector<unsigned char> any((size_t)num_buckets, 0);
+    for (int j = 0; j < nq; ++j) {
+      uint32_t* bj = bits.data() + (size_t)j * words;
+      if (cand_all && cand_all[j]) {
+        for (int b = 0; b < num_buckets; ++b) bj[b >> 5] |= 1u << (b & 31);
+        std::fill(any.begin(), any.end(), (unsigned char)1);
+        continue;
+      }
+      for (long long q = cand_ptr[j]; q < cand_ptr[j + 1]; ++q) {
+        const long long b = cand[q];
+        if (b < 0 || b >= num_buckets) continue;
+        bj[b >> 5] |= 1u << (b & 31);
+        any[(size_t)b] = 1;
+      }
+    }
+    for (int b = 0; b < num_buckets; ++b) {
+      if (!any[(size_t)b]) continue;
+      const long long s0 = bucket_start[b], e0 = bucket_start[b + 1];
+      if (e0 <= s0) continue;
+      if (!rs.empty() && rs.back().second == s0) rs.back().second = e0;
+      else rs.emplace_back(s0, e0);
+    }
+    if (rs.empty()) return 1;
+  } else {
+    rs.emplace_back(0, n_rows);
+  }
+  const long long nr = (long long)rs.size();
+  // excluded rows -> sorted positions per query
+  std::vector<int32_t> ptr, ex;
+  if (ex_ptr) {
+    ptr.assign((size_t)nq + 1, 0);
+    std::vector<int32_t> pj;
+    for (int j = 0; j < nq; ++j) {
+      pj.clear();
+      for (long long q = ex_ptr[j]; q < ex_ptr[j + 1]; ++q) {
+        const long long r = ex_rows[q];
+        if (r < 0 || r >= n_pos) continue;
+        const long long p = pos_of_row[r];
+        if (p >= 0) pj.push_back((int32_t)p);
+      }
+      std::sort(pj.begin(), pj.end());
+      ex.insert(ex.end(), pj.begin(), pj.end());
+      ptr[(size_t)j + 1] = (int32_t)ex.size();
+    }
+    if (ex.empty()) ex.push_back(0);
+  }
+  const long long o_q = 0;
+  const long long o_rs = al(o_q + (long long)max_batch * kp * 4);
+  const long long o_t0 = al(o_rs + nr * 16);
+  long long o = al(o_t0 + (nr + 1) * 8);
+  const long long o_bits = cand_ptr ? o : -1;
+  if (cand_ptr) o = al(o + (long long)bits.size() * 4);
+  const long long o_ptr = ex_ptr ? o : -1;
+  if (ex_ptr) o = al(o + (long long)ptr.size() * 4);
+  const long long o_ex = ex_ptr ? o : -1;
+  if (ex_ptr) o = al(o + (long long)ex.size() * 4);
+  if (o > out_cap) return -1;
+  float* Q = reinterpret_cast<float*>(out + o_q);
+  std::memset(Q, 0, (size_t)max_batch * kp * 4);
+  for (int j = 0; j < nq; ++j)
+    std::memcpy(Q + (size_t)j * kp, targets + (size_t)j * k, (size_t)k * 4);
+  long long* R = reinterpret_cast<long long*>(out + o_rs);
+  long long* T0 = reinterpret_cast<long long*>(out + o_t0);
+  T0[0] = 0;
+  for (long long r = 0; r < nr; ++r) {
+    R[2 * r] = rs[(size_t)r].first;
+    R[2 * r + 1] = rs[(size_t)r].second;
+    T0[r + 1] = T0[r] + (rs[(size_t)r].second - rs[(size_t)r].first + 15) / 16;
+  }
+  if (cand_ptr) std::memcpy(out + o_bits, bits.data(), bits.size() * 4);
+  if (ex_ptr) {
+    std::memcpy(out + o_ptr, ptr.data(), ptr.size() * 4);
+    std::memcpy(out + o_ex, ex.data(), ex.size() * 4);
+  }
+  info[0] = nr;
+  info[1] = T0[nr];
+  info[2] = o_rs;
+  info[3] = o_t0;
+  info[4] = o_bits;
+  info[5] = o_ptr;
+  info[6] = o_ex;
+  info[7] = o;
+  info[8] = (long long)ex.size();
+  return 0;
+}
+
 }  // extern "C"

@@ -23,6 +23,8 @@ passes returned -- every depth is exact.
 
 from __future__ import annotations
 
+import ctypes
+import itertools
 import os
 import threading
 from dataclasses import dataclass
@@ -38,6 +40,7 @@ __all__ = ["ItemIndex", "ShardedItemIndex", "TopNQuery", "MAX_BATCH", "MAX_HOW_M
 
 MAX_BATCH = 16          # queries per kernel launch
 MAX_HOW_MANY = 64       # candidates each wave keeps per query in the batched launch
+_EMPTY_I64 = np.zeros(0, dtype=np.int64)
 BF16_POOL = 64          # candidates the bf16 scan re-ranks exactly per query
 BF16_MAX_HOW_MANY = 32  # deeper requests scan in fp32
 
@@ -462,72 +465,62 @@ class ItemIndex:
         return rows, vj
 
     def _prep(self, qs: Sequence[TopNQuery], kp: int):
-        """Launch inputs shared by the scans, built on the host and sent in ONE host-to-device
-        copy: queries [MAX_BATCH, kp], candidate ranges and their tile prefix, per-query
-        bucket bitmaps, excluded positions.  Returns (Q, ranges, tile0, bits or None, ptr or
-        None, excluded or None, n_ranges, n_tiles) device tensors / counts, or None when
-        nothing is scanned."""
-        nq = len(qs)
-        Q = np.zeros((MAX_BATCH, kp), dtype=np.float32)
+        """Launch inputs shared by the scans, packed by one native call
+        (``oryx_topn_prep``) straight into a pinned staging buffer and sent in ONE
+        host-to-device copy: queries [MAX_BATCH, kp], candidate ranges and their tile prefix,
+        per-query bucket bitmaps, excluded positions.  Returns (Q, ranges, tile0, bits or
+        None, ptr or None, excluded or None, n_ranges, n_tiles) device tensors / counts, or
+        None when nothing is scanned."""
+        nq, k = len(qs), self.k
+        targets = np.empty((nq, k), dtype=np.float32)
         for j, q in enumerate(qs):
-            Q[j, :self.k] = np.asarray(q.target, dtype=np.float32)[:self.k]
-        # candidate ranges: union over the batch; per-query bucket bitmaps when pruning
-        use_lsh = any(q.candidates is not None for q in qs)
-        bits = None
-        if use_lsh:
-            allb = np.zeros(self.num_buckets, dtype=bool)
-            mask = np.zeros((nq, self.words * 32), dtype=bool)
-            for j, q in enumerate(qs):
-                if q.candidates is None:
-                    mask[j, :self.num_buckets] = True
-                else:
-                    mask[j, np.asarray(q.candidates, dtype=np.int64)] = True
-            allb |= mask[:, :self.num_buckets].any(0)
-            # per-query bucket bitmaps (bit b of word b // 32), one packbits for the batch
-            bits = np.packbits(mask, axis=1, bitorder="little").view(np.uint32)
-            sel = np.nonzero(allb)[0]
-            starts = self.bucket_start[sel]
-            ends = self.bucket_start[sel + 1]
-            keep = ends > starts
-            starts, ends = starts[keep], ends[keep]
-            if len(starts) == 0:
-                return None
-            # merge adjacent ranges
-            brk = np.nonzero(starts[1:] != ends[:-1])[0] + 1
-            rs = np.stack([starts[np.r_[0, brk]], ends[np.r_[brk - 1, len(ends) - 1]]], 1)
-        else:
-            rs = np.array([[0, self.n]], dtype=np.int64)
-        rs = np.ascontiguousarray(rs, dtype=np.int64)
-        tiles = (rs[:, 1] - rs[:, 0] + 15) // 16
-        tile0 = np.zeros(len(rs) + 1, dtype=np.int64)
-        np.cumsum(tiles, out=tile0[1:])
-        n_tiles = int(tile0[-1])
-        # excluded store rows -> sorted positions per query (the host position map)
-        ptr = ex = None
+            targets[j] = np.asarray(q.target, dtype=np.float32)[:k]
+        vp = ctypes.c_void_p
+        cand_ptr = cand = cand_all = None
+        if any(q.candidates is not None for q in qs):
+            cl = [np.asarray(q.candidates, dtype=np.int64) if q.candidates is not None else
+                  _EMPTY_I64 for q in qs]
+            cand_ptr = np.zeros(nq + 1, dtype=np.int64)
+            np.cumsum([len(c) for c in cl], out=cand_ptr[1:])
+            cand = np.concatenate(cl) if cand_ptr[-1] else np.zeros(1, dtype=np.int64)
+            cand_all = np.fromiter((q.candidates is None for q in qs), dtype=np.uint8, count=nq)
+        ex_ptr = ex_rows = None
         if any(q.exclude_rows is not None and len(q.exclude_rows) for q in qs):
-            pmap = self.pos_of_row_h
-            ptr = np.zeros(nq + 1, dtype=np.int32)
-            chunks = []
-            for j, q in enumerate(qs):
-                er = q.exclude_rows
-                if er is not None and len(er):
-                    e = np.asarray(er, dtype=np.int64)
-                    e = e[(e >= 0) & (e < len(pmap))]
-                    pj = np.sort(pmap[e])
-                    pj = pj[pj >= 0].astype(np.int32)
-                else:
-                    pj = np.zeros(0, dtype=np.int32)
-                chunks.append(pj)
-                ptr[j + 1] = ptr[j] + len(pj)
-            ex = np.concatenate(chunks) if ptr[-1] else np.zeros(1, dtype=np.int32)
-        parts = [Q, rs, tile0] + [a for a in (bits, ptr, ex) if a is not None]
-        dev_parts = _upload(parts, self.device)
-        Qd, rs_d, t0_d = dev_parts[:3]
-        rest = iter(dev_parts[3:])
-        bits_d = next(rest) if bits is not None else None
-        ptr_d = next(rest) if ptr is not None else None
-        ex_d = next(rest) if ex is not None else None
-        return Qd, rs_d, t0_d, bits_d, ptr_d, ex_d, len(rs), n_tiles
+            el = [q.exclude_rows if q.exclude_rows is not None else () for q in qs]
+            ex_ptr = np.zeros(nq + 1, dtype=np.int64)
+            np.cumsum([len(e) for e in el], out=ex_ptr[1:])
+            ex_rows = np.fromiter(itertools.chain.from_iterable(el), dtype=np.int64,
+                                  count=int(ex_ptr[-1]))
+        nb = self.num_buckets if cand_ptr is not None else 1
+        cap = MAX_BATCH * kp * 4 + nb * 16 + (nb + 1) * 8 + nq * self.words * 4 + \
+            (nq + 1) * 4 + (len(ex_rows) + 1 if ex_rows is not None else 0) * 4 + 6 * 16
+        host = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
+        info = np.empty(9, dtype=np.int64)
+        pos = self.pos_of_row_h
+        rc = native.runtime().oryx_topn_prep(
+            nq, k, kp, MAX_BATCH, targets.ctypes.data_as(vp),
+            cand_ptr.ctypes.data_as(vp) if cand_ptr is not None else None,
+            cand.ctypes.data_as(vp) if cand is not None else None,
+            cand_all.ctypes.data_as(vp) if cand_all is not None else None,
+            self.num_buckets, self.words, self.bucket_start.ctypes.data_as(vp), int(self.n),
+            ex_ptr.ctypes.data_as(vp) if ex_ptr is not None else None,
+            ex_rows.ctypes.data_as(vp) if ex_rows is not None else None,
+            pos.ctypes.data_as(vp), len(pos), ctypes.c_void_p(host.data_ptr()), cap,
+            info.ctypes.data_as(vp))
+        if rc == 1:
+            return None
+        if rc != 0:
+            raise RuntimeError("oryx_topn_prep: staging buffer too small")
+        nr, n_tiles, o_rs, o_t0, o_bits, o_ptr, o_ex, used, n_ex = (int(v) for v in info)
+        dev = host[:used].to(self.device, non_blocking=True)
+        Qd = dev[:MAX_BATCH * kp * 4].view(torch.float32).view(MAX_BATCH, kp)
+        rs_d = dev[o_rs:o_rs + nr * 16].view(torch.int64).view(nr, 2)
+        t0_d = dev[o_t0:o_t0 + (nr + 1) * 8].view(torch.int64)
+        bits_d = dev[o_bits:o_bits + nq * self.words * 4].view(torch.int32).view(
+            nq, self.words) if o_bits >= 0 else None
+        ptr_d = dev[o_ptr:o_ptr + (nq + 1) * 4].view(torch.int32) if o_ptr >= 0 else None
+        ex_d = dev[o_ex:o_ex + n_ex * 4].view(torch.int32) if o_ex >= 0 else None
+        return Qd, rs_d, t0_d, bits_d, ptr_d, ex_d, nr, n_tiles
 
     def _launch_fp32(self, qs: Sequence[TopNQuery], cosine: bool, kl: int = MAX_HOW_MANY,
                      asynchronous: bool = False):
