@@ -878,15 +878,25 @@ __global__ __launch_bounds__(64) void rdf_best_split(
   long long best_idx = 0x7FFFFFFFFFFFFFFFLL;
   const bool leaf_node = force_leaf || wn < 2.0 || parent <= 1e-12 || B < 2;
   unsigned short* ord = s_ord + lane * B;
+  // without categorical predictors a feature's split positions are spread over LPF lanes
+  // (Fs = 10: 6 lanes each instead of 10 busy lanes of 64); a lane first sums the bins
+  // before its chunk in bin order, so every left-hand total -- and so every gain -- is the
+  // same fp64 number the one-lane walk computes
+  const int LPF = (!is_cat && Fs <= 32) ? 64 / Fs : 1;
+  const int CH = (B - 1 + LPF - 1) / LPF;
   if (!leaf_node) {
-    for (int jj = lane; jj < Fs; jj += 64) {
+    for (int u = lane; u < Fs * LPF; u += 64) {
+      const int jj = u / LPF, k0 = (u - jj * LPF) * CH;
+      const int k1 = LPF == 1 ? B - 1 : (k0 + CH < B - 1 ? k0 + CH : B - 1);
       const int f = fj[jj];
       const float* hf = h + (long long)jj * B * S;
       const bool cat = is_cat && is_cat[f];
       if (cat) rdf_cat_order(hf, B, S, kind, maj, ord);
       double left[RDF_MAX_S], right[RDF_MAX_S];
       for (int s = 0; s < S; ++s) left[s] = 0.0;
-      for (int k = 0; k + 1 < B; ++k) {
+      for (int b = 0; b < k0; ++b)
+        for (int s = 0; s < S; ++s) left[s] += (double)hf[(long long)b * S + s];
+      for (int k = k0; k < k1; ++k) {
         const int b = cat ? ord[k] : k;
         for (int s = 0; s < S; ++s) {
           left[s] += (double)hf[(long long)b * S + s];
