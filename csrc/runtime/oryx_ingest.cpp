@@ -3285,4 +3285,59 @@ long long oryx_topn_prep(int nq, int k, int kp, int max_batch, const float* targ
   return 0;
 }
 
+// 128-bit content digest of a byte range (the identity under which parsed text is cached:
+// ALS / feature histories adopt a parse when the same bytes come back as a part file; not
+// cryptographic).  4 MB chunks over the native threads, each with a hardware CRC-32C and a
+// position-weighted 64-bit sum of its 8-byte words; the per-chunk values are then mixed in
+// chunk order with the length.  ~20 GB/s per thread, where a single-threaded xxh3 pass over a
+// 29 GB interval took seconds.
+__attribute__((target("sse4.2"))) static void digest_chunk(const unsigned char* p, size_t n,
+                                                           uint32_t* crc_out,
+                                                           uint64_t* sum_out) {
+  uint64_t c = 0xFFFFFFFFu, sum = 0, i = 1;
+  size_t k = 0;
+  for (; k + 8 <= n; k += 8, i += 2) {
+    uint64_t v;
+    std::memcpy(&v, p + k, 8);
+    c = __builtin_ia32_crc32di(c, v);
+    sum += v * i;
+  }
+  uint32_t c32 = (uint32_t)c;
+  uint64_t tail = 0;
+  for (size_t j = 0; k + j < n; ++j) {
+    c32 = __builtin_ia32_crc32qi(c32, p[k + j]);
+    tail |= (uint64_t)p[k + j] << (8 * j);
+  }
+  sum += tail * i;
+  *crc_out = ~c32;
+  *sum_out = sum;
+}
+
+static inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void oryx_digest128(const unsigned char* p, long long n, unsigned long long* out) {
+  constexpr long long kChunk = 4LL << 20;
+  const long long nch = n > 0 ? (n + kChunk - 1) / kChunk : 0;
+  std::vector<uint32_t> crc((size_t)nch);
+  std::vector<uint64_t> sum((size_t)nch);
+  oryx_ff::parallel_ranges(nch, 1, [&](long long lo, long long hi, int) {
+    for (long long c = lo; c < hi; ++c) {
+      const long long o = c * kChunk;
+      digest_chunk(p + o, (size_t)std::min(kChunk, n - o), &crc[(size_t)c], &sum[(size_t)c]);
+    }
+  });
+  uint64_t h1 = mix64((uint64_t)n), h2 = mix64((uint64_t)n ^ 0x5851F42D4C957F2Dull);
+  for (long long c = 0; c < nch; ++c) {
+    h1 = mix64(h1 ^ ((uint64_t)crc[(size_t)c] << 32 | (uint64_t)c));
+    h2 = mix64(h2 + sum[(size_t)c]);
+  }
+  out[0] = h1;
+  out[1] = h2;
+}
+
 }  // extern "C"

@@ -578,6 +578,19 @@ def _known_mode(model):
     return None if hasattr(model, "add_known_items") else False
 
 
+def content_digest(buf, off: int, nbytes: int) -> bytes:
+    """24-byte identity of ``buf[off:off + nbytes]`` (numpy uint8 array or bytes): the
+    parallel native digest (``oryx_digest128``) plus the length."""
+    out = np.empty(2, dtype=np.uint64)
+    if isinstance(buf, np.ndarray):
+        base = buf.ctypes.data
+    else:
+        base = ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p).value
+    native.runtime().oryx_digest128(ctypes.c_void_p(base + int(off)), int(nbytes),
+                                    out.ctypes.data_as(ctypes.c_void_p))
+    return out.tobytes() + int(nbytes).to_bytes(8, "little")
+
+
 PARSE_STATS = {"native_s": 0.0}
 
 

@@ -38,11 +38,6 @@ import torch
 from ... import ingest
 from ...textlines import TextLines
 
-try:
-    import xxhash
-except ImportError:   # pragma: no cover - no adoption of unkeyed parses without it
-    xxhash = None
-
 log = logging.getLogger(__name__)
 
 __all__ = ["RatingsHistory"]
@@ -76,11 +71,7 @@ class RatingsHistory:
 
     @staticmethod
     def _digest(buf, off: int, nbytes: int) -> Optional[bytes]:
-        if xxhash is None:
-            return None
-        view = memoryview(buf)[off:off + nbytes] if not isinstance(buf, np.ndarray) \
-            else buf[off:off + nbytes]
-        return xxhash.xxh3_128_digest(view) + nbytes.to_bytes(8, "little")
+        return ingest.content_digest(buf, off, nbytes)
 
     def __len__(self) -> int:
         return len(self._segs)

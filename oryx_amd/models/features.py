@@ -35,14 +35,9 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from .. import native
+from .. import ingest, native
 from ..textlines import TextLines
 from .schema import InputSchema
-
-try:
-    import xxhash
-except ImportError:   # pragma: no cover - no adoption of unkeyed parses without it
-    xxhash = None
 
 log = logging.getLogger(__name__)
 
@@ -229,9 +224,7 @@ class FeatureHistory:
 
     @staticmethod
     def _digest(buf: np.ndarray, off: int, nbytes: int) -> Optional[bytes]:
-        if xxhash is None:
-            return None
-        return xxhash.xxh3_128_digest(buf[off:off + nbytes]) + nbytes.to_bytes(8, "little")
+        return ingest.content_digest(buf, off, nbytes)
 
     def _parse_range(self, buf: np.ndarray, off: int, nbytes: int, n_lines: int,
                      schema: InputSchema, dtype) -> Optional[_Seg]:

@@ -137,6 +137,7 @@ def _register_runtime_extras(lib):
     # bucket_start, n_rows, ex_ptr, ex_rows, pos_of_row, n_pos, out, out_cap, info
     _sig(lib, "oryx_topn_prep", c_ll, [c_i, c_i, c_i, c_i, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                        c_vp, c_ll, c_vp, c_vp, c_vp, c_ll, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_digest128", None, [c_vp, c_ll, c_vp])
     _sig(lib, "oryx_http_start", c_vp, [c_cp, c_i, c_i, c_ll])
     _sig(lib, "oryx_http_port", c_i, [c_vp])
     _sig(lib, "oryx_http_served", c_ll, [c_vp])
