@@ -114,6 +114,9 @@ class KMeansUpdate(MLUpdate):
             raise ValueError("k must be > 1")
         ctx = self._ctx(context)
         x = self._points(train_data, ctx)
+        # the evaluation of this candidate scores train + test points: it takes these parsed
+        # rows instead of re-joining and re-reading the training text
+        self._train_points = (train_data, x)
         sharded = self._sharded(ctx)
         n = int(x.shape[0])
         if sharded:
@@ -147,7 +150,16 @@ class KMeansUpdate(MLUpdate):
     def evaluate(self, context, model, model_parent_path, test_data, train_data):
         validate_pmml_vs_schema(model, self.input_schema)
         ctx = self._ctx(context)
-        x = self._points(concat_lines([train_data, test_data]), ctx)
+        cached = getattr(self, "_train_points", None)
+        self._train_points = None
+        if cached is not None and cached[0] is train_data:
+            # rows in the order of concat_lines([train, test]): the training rows, then the
+            # test rows (the evaluation sums over points, so a rank's row order is immaterial)
+            x = cached[1]
+            if test_data is not None and len(test_data):
+                x = torch.cat([x, self._points(test_data, ctx)])
+        else:
+            x = self._points(concat_lines([train_data, test_data]), ctx)
         tp = time.perf_counter()
         clusters = read_clusters(model)
         if self._sharded(ctx):

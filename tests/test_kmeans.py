@@ -737,3 +737,19 @@ def test_kmeanspp_native_draws_match_torch_path(cuda):
     # one rounding-level flip would change every later draw; demand a long identical prefix
     first_diff = int(torch.nonzero(~same)[0]) if not same.all() else len(same)
     assert first_diff >= 100, first_diff
+
+
+@pytest.mark.parametrize("strategy", ["SSE", "DAVIES_BOULDIN"])
+def test_kmeans_evaluate_reuses_parsed_training_points(tmp_path, strategy):
+    """evaluate() scores train + test points: taking the rows build_model parsed plus a parse
+    of the test lines gives the same value as parsing the joined text again."""
+    from oryx_amd.textlines import TextLines
+    pts, _ = _blobs(n_per=60)
+    lines = [",".join(repr(float(v)) for v in p) for p in pts]
+    train, test = TextLines.from_strings(lines[:150]), TextLines.from_strings(lines[150:])
+    upd = KMeansUpdate(_update_config(tmp_path, strategy))
+    model = upd.build_model(None, train, [4], None)
+    cached = upd.evaluate(None, model, None, test, train)
+    upd._train_points = None                  # forces the joined parse
+    fresh = upd.evaluate(None, model, None, test, train)
+    assert cached == pytest.approx(fresh, rel=1e-9, abs=1e-12)
