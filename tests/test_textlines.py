@@ -99,3 +99,21 @@ def test_multichunk_parse_matches_single_chunk_with_dropped_lines():
         raise AssertionError("strict parse accepted a bad line")
     except ValueError as e:
         assert "line %d" % bad_at in str(e)
+
+
+def test_content_digest_identity():
+    """ingest.content_digest (the parse caches' identity of a byte range): deterministic,
+    equal for the same bytes given as numpy or bytes and at any offset, different after a
+    one-bit change or a length change, across the 4 MB chunk boundary."""
+    import numpy as np
+    from oryx_amd import ingest
+    rng = np.random.default_rng(0)
+    b = rng.integers(0, 255, (9 << 20) + 13, dtype=np.uint8)
+    d = ingest.content_digest(b, 0, len(b))
+    assert d == ingest.content_digest(b, 0, len(b)) and len(d) == 24
+    assert ingest.content_digest(b.tobytes(), 0, len(b)) == d
+    assert ingest.content_digest(b, 7, 1000) == ingest.content_digest(b[7:1007].copy(), 0, 1000)
+    c = b.copy()
+    c[(4 << 20) + 1] ^= 1
+    assert ingest.content_digest(c, 0, len(c)) != d
+    assert ingest.content_digest(b, 0, len(b) - 1) != d
