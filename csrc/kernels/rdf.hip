@@ -466,7 +466,7 @@ __global__ __launch_bounds__(256) void rdf_histogram_pieces(
 // RSW dwords of LDS (odd, so the 64 lanes' byte reads fall on distinct banks); a row that
 // starts off a dword boundary (P % 4 != 0) is copied from the aligned dword below it and read
 // at byte offset (i * P) & 3.
-template <bool CLS>
+template <bool CLS, bool SPARSE, int HS>
 __global__ __launch_bounds__(256) void rdf_histogram_staged(
     const unsigned char* __restrict__ Xb, long long n, int P, const int* __restrict__ label,
     const float* __restrict__ y, int S, const unsigned char* __restrict__ weight,
@@ -493,7 +493,26 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
   for (int i = tid; i < per_node; i += 256) lh[i] = 0.f;   // 0.f and 0u share the bits
   const int* fj = feats + ((long long)t * nodes + node) * Fs;
   for (int j = tid; j < Fs; j += 256) fjs[j] = fj[j];
+  // SPARSE (dword-aligned rows, Fs <= 32): only the distinct dwords holding the node's
+  // features are staged -- at most Fs of the row's P / 4 -- so the staging slices are that
+  // much smaller (more workgroups per CU) and each feature byte is read at s_fo[j]
+  __shared__ int s_dw[32], s_fo[32], s_nd;
   __syncthreads();
+  if (SPARSE) {
+    if (tid == 0) {
+      int nd = 0;
+      for (int j = 0; j < Fs; ++j) {
+        const int d = fjs[j] >> 2;
+        int q = 0;
+        while (q < nd && s_dw[q] != d) ++q;
+        if (q == nd) s_dw[nd++] = d;
+        s_fo[j] = q * 4 + (fjs[j] & 3);
+      }
+      s_nd = nd;
+    }
+    __syncthreads();
+  }
+  const int ndw = SPARSE ? s_nd : NDW;
   const long long p0 = piece_lo[pc], p1 = piece_hi[pc];
   const long long toff = (long long)t * n;
   const unsigned int* Xw = reinterpret_cast<const unsigned int*>(Xb);
@@ -536,24 +555,29 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
     const unsigned int wb = i >= 0 ? (unsigned int)((i * P) >> 2) : 0u;   // first word of row
     // row word bases of the 64 rows, shuffled with every lane active (a bpermute reads 0
     // from a lane that is switched off)
-    unsigned int wbr[32];
+    // in two halves of HS steps: HS loads in flight per lane instead of 32 keeps the kernel
+    // under the VGPR count of 3 waves per SIMD (ORYX_RDF_STAGE_STEPS=32: one pass)
+    for (int h0 = 0; h0 < 32; h0 += HS) {
+      unsigned int wbr[HS];
 #pragma unroll
-    for (int it = 0; it < 32; ++it) wbr[it] = (unsigned int)__shfl((int)wb, 2 * it + half, 64);
-    for (int wp = 0; wp * 32 < NDW; ++wp) {
-      const int w = wp * 32 + wl;
-      if (w < NDW) {
-        // rows past the batch end load row 0 into their (unused) slots: no per-step predicate.
-        // Only words wi <= nfull can hold bytes of a row, so the index is clamped to the last
-        // full word and the partial one comes from tailw.
-        unsigned int v[32];
+      for (int it = 0; it < HS; ++it)
+        wbr[it] = (unsigned int)__shfl((int)wb, 2 * (h0 + it) + half, 64);
+      for (int wp = 0; wp * 32 < ndw; ++wp) {
+        const int w = wp * 32 + wl;
+        if (w < ndw) {
+          // rows past the batch end load row 0 into their (unused) slots: no per-step
+          // predicate.  Only words wi <= nfull can hold bytes of a row, so the index is
+          // clamped to the last full word and the partial one comes from tailw.
+          unsigned int v[HS];
 #pragma unroll
-        for (int it = 0; it < 32; ++it) {
-          const unsigned int wi = wbr[it] + (unsigned int)w;
-          v[it] = Xw[wi < nfull ? wi : nfull - 1];
-          if (wi == nfull) v[it] = tailw;
+          for (int it = 0; it < HS; ++it) {
+            const unsigned int wi = wbr[it] + (unsigned int)(SPARSE ? s_dw[w] : w);
+            v[it] = Xw[wi < nfull ? wi : nfull - 1];
+            if (wi == nfull) v[it] = tailw;
+          }
+#pragma unroll
+          for (int it = 0; it < HS; ++it) rows[(2 * (h0 + it) + half) * RSW + w] = v[it];
         }
-#pragma unroll
-        for (int it = 0; it < 32; ++it) rows[(2 * it + half) * RSW + w] = v[it];
       }
     }
     // this wave's LDS writes before its reads (LDS executes one wave's accesses in order;
@@ -570,13 +594,14 @@ __global__ __launch_bounds__(256) void rdf_histogram_staged(
     }
     const unsigned int wcnt = (unsigned int)v0;
     if (v0 != 0.f) {
-      const unsigned char* xr = rowb + lane * RSW * 4 + (int)((icur * P) & 3);
+      const unsigned char* xr = rowb + lane * RSW * 4 + (SPARSE ? 0 : (int)((icur * P) & 3));
       // features in groups of 8: the 8 byte reads are issued before the 8 atomics (the
       // feature indices come from LDS, copied there once per workgroup)
       for (int j0 = 0; j0 < Fs; j0 += 8) {
         int b[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) b[u] = j0 + u < Fs ? xr[fjs[j0 + u]] : 0;
+        for (int u = 0; u < 8; ++u)
+          b[u] = j0 + u < Fs ? xr[SPARSE ? s_fo[j0 + u] : fjs[j0 + u]] : 0;
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           if (j0 + u >= Fs) break;
@@ -1180,19 +1205,38 @@ int oryx_rdf_histogram_pieces(const void* Xb, int bin_bytes, long long n, int P,
     // pitch of ops/rdf.py) starts every row on a dword
     const int pu = p_used > 0 && p_used < P ? p_used : P;
     const int ndw = P % 4 == 0 ? (pu + 3) / 4 : (pu + 3) / 4 + 1;
-    const int rsw = ndw | 1;
+    // sparse staging (only the node's feature dwords) when rows are dword-aligned and the
+    // subset is small: ORYX_RDF_STAGE_SPARSE=0 stages whole rows
+    static const bool sparse_ok =
+        !(getenv("ORYX_RDF_STAGE_SPARSE") && atoi(getenv("ORYX_RDF_STAGE_SPARSE")) == 0);
+    const bool sparse = sparse_ok && P % 4 == 0 && Fs <= 32 && Fs < ndw;
+    static const int steps =
+        getenv("ORYX_RDF_STAGE_STEPS") ? atoi(getenv("ORYX_RDF_STAGE_STEPS")) : 16;
+    const int rsw = (sparse ? Fs : ndw) | 1;
     const long long smem_st = per_node_bytes + ((Fs + 3) & ~3) * 4LL + 256LL * rsw * 4;
     if (smem_st <= 64 * 1024) {
-      if (cls)
-        hipLaunchKernelGGL((rdf_histogram_staged<true>), dim3((unsigned)n_pieces), dim3(256),
-                           smem_st, s, reinterpret_cast<const unsigned char*>(Xb), n, P, label,
-                           y, S, weight, perm, piece_tree, piece_node, piece_lo, piece_hi,
-                           nodes, feats, Fs, B, hist, ndw, rsw, n_live);
-      else
-        hipLaunchKernelGGL((rdf_histogram_staged<false>), dim3((unsigned)n_pieces), dim3(256),
-                           smem_st, s, reinterpret_cast<const unsigned char*>(Xb), n, P, label,
-                           y, S, weight, perm, piece_tree, piece_node, piece_lo, piece_hi,
-                           nodes, feats, Fs, B, hist, ndw, rsw, n_live);
+#define STAGED_LAUNCH(C, SP)                                                                  \
+  if (steps == 32)                                                                            \
+    hipLaunchKernelGGL((rdf_histogram_staged<C, SP, 32>), dim3((unsigned)n_pieces), dim3(256), \
+                       smem_st, s, reinterpret_cast<const unsigned char*>(Xb), n, P, label, y, \
+                       S, weight, perm, piece_tree, piece_node, piece_lo, piece_hi, nodes,    \
+                       feats, Fs, B, hist, ndw, rsw, n_live);                                 \
+  else if (steps == 8)                                                                        \
+    hipLaunchKernelGGL((rdf_histogram_staged<C, SP, 8>), dim3((unsigned)n_pieces), dim3(256),  \
+                       smem_st, s, reinterpret_cast<const unsigned char*>(Xb), n, P, label, y, \
+                       S, weight, perm, piece_tree, piece_node, piece_lo, piece_hi, nodes,    \
+                       feats, Fs, B, hist, ndw, rsw, n_live);                                 \
+  else                                                                                        \
+  hipLaunchKernelGGL((rdf_histogram_staged<C, SP, 16>), dim3((unsigned)n_pieces), dim3(256),   \
+                     smem_st, s, reinterpret_cast<const unsigned char*>(Xb), n, P, label, y,  \
+                     S, weight, perm, piece_tree, piece_node, piece_lo, piece_hi, nodes,      \
+                     feats, Fs, B, hist, ndw, rsw, n_live)
+      if (cls) {
+        if (sparse) STAGED_LAUNCH(true, true); else STAGED_LAUNCH(true, false);
+      } else {
+        if (sparse) STAGED_LAUNCH(false, true); else STAGED_LAUNCH(false, false);
+      }
+#undef STAGED_LAUNCH
       return oryx_check_launch();
     }
   }
