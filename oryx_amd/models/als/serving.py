@@ -73,6 +73,11 @@ def rescored_top(ids, scores: np.ndarray, rescorer: Rescorer, how_many: int
     return [(sel[j], float(new[j])) for j in ok.tolist()]
 
 
+def _done(result):
+    """A finisher that returns ``result`` (bound here, per batch, not late in a loop)."""
+    return lambda: result
+
+
 class TopNBatcher:
     """Micro-batches concurrent top-N requests into shared kernel launches.
 
@@ -176,8 +181,9 @@ class TopNBatcher:
                     if start is not None:
                         fin = start(qs)
                     else:                      # an index without asynchronous launches
-                        res = self.index.scan(qs)
-                        fin = lambda: res     # noqa: E731
+                        # bind this batch's result now: the next loop iteration rebinds
+                        # the local before this batch is finished
+                        fin = _done(self.index.scan(qs))
                     launched = (batch, fin, t_scan, None)
                 except Exception as e:   # answered to every waiting request
                     launched = (batch, None, t_scan, e)

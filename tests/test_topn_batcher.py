@@ -58,6 +58,33 @@ def test_concurrent_clients_are_batched_cpu():
     b.close()
 
 
+def test_pipelined_batches_keep_their_own_results_cpu():
+    """An index without scan_async: batch B is launched before batch A is finished, so A's
+    finisher must return A's results (regression: a late-bound closure handed A B's)."""
+    idx = _FakeIndex(delay=0.002)
+    b = TopNBatcher(idx, max_batch=3, wait_s=0.0)
+    out = {}
+    errs = []
+
+    def client(c):
+        try:
+            for k in range(40):
+                q = (c, k)
+                out[q] = b.submit(q)
+        except Exception as e:   # noqa: BLE001
+            errs.append(e)
+
+    ts = [threading.Thread(target=client, args=(c,)) for c in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=60)
+    assert not errs and len(out) == 320
+    bad = [q for q, v in out.items() if v != ("r", q)]
+    assert not bad, bad[:5]
+    b.close()
+
+
 def test_wait_window_disables_inline_cpu():
     idx = _FakeIndex()
     b = TopNBatcher(idx, max_batch=8, wait_s=0.001)
