@@ -1,16 +1,26 @@
-// oryx_http.cpp -- the serving layer's native HTTP/1.1 front end.
+// oryx_http.cpp -- the serving layer's native HTTP/1.1 (and HTTPS) front end.
 //
 // The reference serves its REST endpoints from embedded Tomcat ([lserving]/ServingLayer.java:
-// 194-245: a connector with its own acceptor and poller threads in front of the servlet
-// worker pool).  Here an epoll loop on one native thread accepts connections and parses
-// requests (request line, headers, Content-Length or chunked bodies, keep-alive and
-// pipelining); complete requests wait in a queue that the Python handler threads take from
-// (oryx_http_next blocks without the GIL), and their responses come back as ready bytes
-// (oryx_http_respond) that the loop writes in request order per connection.  So the Python
-// side does only routing and the endpoint's own work per request: no per-connection thread,
-// no header parsing in Python, no socket calls.
+// 194-245: one NIO connector, HTTP or HTTPS, with its own acceptor and poller threads in front
+// of the servlet worker pool).  Here the sockets are polled by the handler threads themselves
+// (leader / followers, see oryx_http_next): the poller accepts connections and parses requests
+// (request line, headers, Content-Length or chunked bodies, keep-alive and pipelining);
+// complete requests wait in a queue that the Python handler threads take from (oryx_http_next
+// blocks without the GIL), and their responses come back as ready bytes (oryx_http_respond)
+// that are written in request order per connection.  So the Python side does only routing and
+// the endpoint's own work per request: no per-connection thread, no header parsing in Python,
+// no socket calls.
 //
-// TLS is not handled here (the Python server keeps that path).
+// HTTPS (oryx_http_tls): the same loop with an OpenSSL session per connection in non-blocking
+// mode -- the handshake runs inside the first reads and writes, a read that needs a write (or
+// the reverse) waits for the matching epoll event.  Every SSL call on a connection is made
+// under the connection-table lock, so a session is never used by two threads at once.
+//
+// Limits: headers <= 64 KB (431); bodies <= max_body (413), checked before they are buffered:
+// a Content-Length above it, a chunk size that does not parse or that would take the body past
+// it (written without the addition, so huge sizes cannot wrap) all end the connection.
+// Chunked bodies are parsed incrementally (the state lives on the connection), so a body sent
+// in many small pieces costs linear time.
 
 #include <arpa/inet.h>
 #include <errno.h>
@@ -18,6 +28,8 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -47,14 +59,23 @@ struct Req {
   std::string method, target, headers, body;
 };
 
+// chunked-body parse state
+enum ChunkState { kSize, kData, kDataEnd, kTrailers };
+
 struct Conn {
   int fd = -1;
   uint64_t cid = 0;
+  SSL* ssl = nullptr;              // HTTPS session (null: plain HTTP)
+  bool ssl_rd_wants_out = false;   // the last SSL_read needs the socket writable
+  bool ssl_wr_wants_in = false;    // the last SSL_write needs the socket readable
   std::string in;                  // unparsed input
   size_t scan = 0;                 // header-end search resumes here
   // a request whose headers are parsed and whose body is still arriving
   bool in_body = false, chunked = false, close_after = false;
   long long body_len = 0;
+  ChunkState cstate = kSize;
+  long long chunk_left = 0;        // bytes of the current chunk still to come
+  size_t trailer_bytes = 0;
   Req cur;
   // responses by request sequence; next_out = the next one to write
   uint64_t next_seq = 0, next_out = 0;
@@ -70,14 +91,15 @@ struct Server {
   int lfd = -1, efd = -1, wfd = -1;   // listener, epoll, eventfd (responses ready / stop)
   int port = 0;
   long long max_body = 64ll << 20;
+  SSL_CTX* tls = nullptr;
   std::atomic<bool> stop{false};
   // requests ready for the handlers; `leader`: a handler thread is polling the sockets
   std::mutex qmu;
   std::condition_variable qcv;
   std::deque<Req> ready;
   bool leader = false;
-  // connection state: taken by the loop per event and by a handler thread that writes its
-  // response straight to the socket (oryx_http_respond: no hop through the loop thread)
+  // connection state: taken by the poller per event and by a handler thread that writes its
+  // response straight to the socket (oryx_http_respond: no hop through the poller)
   std::mutex cmu;
   std::unordered_map<int, std::unique_ptr<Conn>> conns;
   std::unordered_map<uint64_t, std::pair<uint64_t, uint64_t>> inflight;  // id -> (cid, seq)
@@ -113,6 +135,52 @@ const char* status_text(int code) {
   }
 }
 
+// ---- transport: plain socket or TLS session.  Return > 0 bytes, 0 at EOF, -1 when the call
+// would block (the connection's ssl_*_wants_* flags say on what), -2 on an error.
+ssize_t conn_recv(Conn* c, char* buf, size_t n) {
+  if (!c->ssl) {
+    for (;;) {
+      const ssize_t r = recv(c->fd, buf, n, 0);
+      if (r >= 0) return r;
+      if (errno == EINTR) continue;
+      return (errno == EAGAIN || errno == EWOULDBLOCK) ? -1 : -2;
+    }
+  }
+  c->ssl_rd_wants_out = false;
+  ERR_clear_error();
+  const int r = SSL_read(c->ssl, buf, (int)std::min<size_t>(n, 1 << 30));
+  if (r > 0) return r;
+  switch (SSL_get_error(c->ssl, r)) {
+    case SSL_ERROR_WANT_READ: return -1;
+    case SSL_ERROR_WANT_WRITE: c->ssl_rd_wants_out = true; return -1;
+    case SSL_ERROR_ZERO_RETURN: return 0;
+    case SSL_ERROR_SYSCALL:
+      if (errno == EINTR || errno == EAGAIN) return -1;
+      return 0;
+    default: return -2;
+  }
+}
+
+ssize_t conn_send(Conn* c, const char* p, size_t n) {
+  if (!c->ssl) {
+    for (;;) {
+      const ssize_t w = send(c->fd, p, n, MSG_NOSIGNAL);
+      if (w >= 0) return w;
+      if (errno == EINTR) continue;
+      return (errno == EAGAIN || errno == EWOULDBLOCK) ? -1 : -2;
+    }
+  }
+  c->ssl_wr_wants_in = false;
+  ERR_clear_error();
+  const int w = SSL_write(c->ssl, p, (int)std::min<size_t>(n, 1 << 30));
+  if (w > 0) return w;
+  switch (SSL_get_error(c->ssl, w)) {
+    case SSL_ERROR_WANT_WRITE: return -1;
+    case SSL_ERROR_WANT_READ: c->ssl_wr_wants_in = true; return -1;
+    default: return -2;
+  }
+}
+
 // An error response produced by the loop itself (malformed request): written after the
 // connection's earlier responses, then the connection closes.
 void loop_error(Server* S, Conn* c, int code) {
@@ -122,14 +190,21 @@ void loop_error(Server* S, Conn* c, int code) {
                   std::to_string(body.size()) + "\r\nConnection: close\r\n\r\n" + body;
   c->done[c->next_seq++] = {r, true};
   c->read_shut = true;
+  c->in.clear();
   (void)S;
 }
 
 void close_conn(Server* S, int fd) {
   auto it = S->conns.find(fd);
   if (it == S->conns.end()) return;
-  S->fd_of_cid.erase(it->second->cid);
+  Conn* c = it->second.get();
+  S->fd_of_cid.erase(c->cid);
   epoll_ctl(S->efd, EPOLL_CTL_DEL, fd, nullptr);
+  if (c->ssl) {
+    SSL_shutdown(c->ssl);          // best effort close_notify (non-blocking socket)
+    SSL_free(c->ssl);
+    c->ssl = nullptr;
+  }
   close(fd);
   S->conns.erase(it);
 }
@@ -169,21 +244,20 @@ bool flush_conn(Server* S, Conn* c) {
         ++c->next_out;
       }
     }
-    const ssize_t w = send(c->fd, c->out.data() + c->out_off, c->out.size() - c->out_off,
-                           MSG_NOSIGNAL);
+    const ssize_t w = conn_send(c, c->out.data() + c->out_off, c->out.size() - c->out_off);
     if (w > 0) {
       c->out_off += (size_t)w;
       continue;
     }
-    if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) {
-      want_write(S, c, true);
+    if (w == -1) {
+      // blocked: on writability (or, TLS, on readability: the poller retries on EPOLLIN)
+      want_write(S, c, !c->ssl_wr_wants_in || c->ssl_rd_wants_out);
       return true;
     }
-    if (w < 0 && errno == EINTR) continue;
     close_conn(S, c->fd);
     return false;
   }
-  want_write(S, c, false);
+  want_write(S, c, c->ssl_rd_wants_out);
   if (c->read_shut && c->next_out == c->next_seq) {
     close_conn(S, c->fd);
     return false;
@@ -202,6 +276,95 @@ void submit(Server* S, Conn* c) {
   S->ready.push_back(std::move(r));
 }
 
+// Parses a chunk-size line "HEX[;ext]": true and the size when it is 1-15 hex digits.
+bool parse_chunk_size(const char* s, size_t n, long long& out) {
+  size_t k = 0;
+  long long v = 0;
+  while (k < n && isxdigit((unsigned char)s[k])) {
+    if (k == 15) return false;     // > 2^60: no body is that large (and no overflow below)
+    const char ch = s[k];
+    const int d = ch <= '9' ? ch - '0' : (tolower((unsigned char)ch) - 'a' + 10);
+    v = v * 16 + d;
+    ++k;
+  }
+  if (k == 0) return false;
+  while (k < n && (s[k] == ' ' || s[k] == '\t')) ++k;
+  if (k < n && s[k] != ';') return false;
+  out = v;
+  return true;
+}
+
+// Consumes what c->in holds of a chunked body, from its front: chunk sizes, data (appended
+// to the request body), the CRLF after each chunk, trailers.  Returns 1 when the body is
+// complete, 0 when more input is needed, or an HTTP error status.
+int parse_chunked(Server* S, Conn* c) {
+  size_t p = 0;
+  int rc = 0;
+  for (;;) {
+    if (c->cstate == kSize) {
+      const size_t le = c->in.find("\r\n", p);
+      if (le == std::string::npos) {
+        if (c->in.size() - p > 1024) rc = 400;     // a size line is short
+        break;
+      }
+      long long sz = 0;
+      if (!parse_chunk_size(c->in.data() + p, le - p, sz)) {
+        rc = 400;
+        break;
+      }
+      // sz > max_body - body: the remaining allowance, never a sum that could wrap
+      if (sz > S->max_body - (long long)c->cur.body.size()) {
+        rc = 413;
+        break;
+      }
+      p = le + 2;
+      if (sz == 0) {
+        c->cstate = kTrailers;
+        c->trailer_bytes = 0;
+      } else {
+        c->cstate = kData;
+        c->chunk_left = sz;
+      }
+    } else if (c->cstate == kData) {
+      const size_t avail = c->in.size() - p;
+      if (avail == 0) break;
+      const size_t take = (size_t)std::min<long long>(c->chunk_left, (long long)avail);
+      c->cur.body.append(c->in, p, take);
+      p += take;
+      c->chunk_left -= (long long)take;
+      if (c->chunk_left == 0) c->cstate = kDataEnd;
+    } else if (c->cstate == kDataEnd) {
+      if (c->in.size() - p < 2) break;
+      if (c->in[p] != '\r' || c->in[p + 1] != '\n') {
+        rc = 400;
+        break;
+      }
+      p += 2;
+      c->cstate = kSize;
+    } else {   // trailers: header lines up to an empty line
+      const size_t nl = c->in.find("\r\n", p);
+      if (nl == std::string::npos) {
+        if (c->trailer_bytes + (c->in.size() - p) > kMaxHeader) rc = 431;
+        break;
+      }
+      c->trailer_bytes += nl + 2 - p;
+      if (c->trailer_bytes > kMaxHeader) {
+        rc = 431;
+        break;
+      }
+      const bool end = nl == p;
+      p = nl + 2;
+      if (end) {
+        c->cstate = kSize;
+        rc = 1;
+        break;
+      }
+    }
+  }
+  c->in.erase(0, p);
+  return rc;
+}
+
 // Parses whatever complete requests c->in holds.
 void parse_input(Server* S, Conn* c) {
   for (;;) {
@@ -212,6 +375,10 @@ void parse_input(Server* S, Conn* c) {
       if (e == std::string::npos) {
         c->scan = c->in.size();
         if (c->in.size() > kMaxHeader) loop_error(S, c, 431);
+        return;
+      }
+      if (e > kMaxHeader) {
+        loop_error(S, c, 431);
         return;
       }
       c->scan = 0;
@@ -249,8 +416,9 @@ void parse_input(Server* S, Conn* c) {
           if (ieq(name, nn, "content-length")) {
             const std::string v = lower_trim(h + colon + 1, q - colon - 1);
             char* endp = nullptr;
+            errno = 0;
             c->body_len = strtoll(v.c_str(), &endp, 10);
-            if (v.empty() || *endp || c->body_len < 0) {
+            if (v.empty() || *endp || c->body_len < 0 || errno == ERANGE) {
               loop_error(S, c, 400);
               return;
             }
@@ -278,45 +446,22 @@ void parse_input(Server* S, Conn* c) {
       c->close_after = !keep;
       c->in.erase(0, e + 4);
       c->in_body = true;
+      c->cstate = kSize;
       // a client that waits for "100 Continue" before its body gets it at once (when no
       // earlier response on the connection is still due, which it would have to follow)
       if (expect_continue && (c->chunked || (long long)c->in.size() < c->body_len) &&
           c->next_out == c->next_seq && c->out.empty()) {
         static const char k100[] = "HTTP/1.1 100 Continue\r\n\r\n";
-        (void)!send(c->fd, k100, sizeof(k100) - 1, MSG_NOSIGNAL);
+        (void)conn_send(c, k100, sizeof(k100) - 1);
       }
     }
     // body
     if (c->chunked) {
-      // chunks: hex size [;ext] CRLF data CRLF ... 0 CRLF [trailers] CRLF
-      size_t p = 0;
-      std::string body;
-      for (;;) {
-        const size_t le = c->in.find("\r\n", p);
-        if (le == std::string::npos) return;           // need more
-        const long long sz = strtoll(c->in.substr(p, le - p).c_str(), nullptr, 16);
-        if (sz < 0 || (long long)body.size() + sz > S->max_body) {
-          loop_error(S, c, 413);
-          return;
-        }
-        if (sz == 0) {
-          // trailers end at an empty line
-          const size_t te = c->in.find("\r\n", le + 2);
-          if (te == std::string::npos) return;
-          size_t end = le + 2;
-          while (true) {
-            const size_t nl = c->in.find("\r\n", end);
-            if (nl == std::string::npos) return;
-            if (nl == end) { end += 2; break; }
-            end = nl + 2;
-          }
-          c->cur.body = std::move(body);
-          c->in.erase(0, end);
-          break;
-        }
-        if (c->in.size() < le + 2 + (size_t)sz + 2) return;
-        body.append(c->in, le + 2, (size_t)sz);
-        p = le + 2 + (size_t)sz + 2;
+      const int rc = parse_chunked(S, c);
+      if (rc == 0) return;                       // need more
+      if (rc != 1) {
+        loop_error(S, c, rc);
+        return;
       }
     } else {
       if ((long long)c->in.size() < c->body_len) return;
@@ -328,6 +473,7 @@ void parse_input(Server* S, Conn* c) {
     submit(S, c);
     if (close_after) {
       c->read_shut = true;     // no further requests on this connection
+      c->in.clear();
       return;
     }
   }
@@ -352,6 +498,15 @@ void poll_once(Server* S, int wait_ms) {
           auto c = std::make_unique<Conn>();
           c->fd = cfd;
           c->cid = S->next_cid++;
+          if (S->tls) {
+            c->ssl = SSL_new(S->tls);
+            if (!c->ssl || SSL_set_fd(c->ssl, cfd) != 1) {
+              if (c->ssl) SSL_free(c->ssl);
+              close(cfd);
+              continue;
+            }
+            SSL_set_accept_state(c->ssl);   // the handshake runs inside the first read
+          }
           S->fd_of_cid[c->cid] = cfd;
           epoll_event ev{};
           ev.events = EPOLLIN | EPOLLRDHUP;
@@ -369,23 +524,29 @@ void poll_once(Server* S, int wait_ms) {
       auto it = S->conns.find(fd);
       if (it == S->conns.end()) continue;
       Conn* c = it->second.get();
-      if (evs[k].events & EPOLLOUT) {
+      const uint32_t e = evs[k].events;
+      // a TLS write blocked on readability retries on any event; so does a TLS read blocked
+      // on writability (both below)
+      if ((e & EPOLLOUT) || (c->ssl && c->ssl_wr_wants_in)) {
         if (!flush_conn(S, c)) continue;
       }
-      if (evs[k].events & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) {
+      if ((e & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) ||
+          (c->ssl && c->ssl_rd_wants_out && (e & EPOLLOUT))) {
         bool eof = false;
         for (;;) {
-          const ssize_t r = recv(fd, buf, sizeof(buf), 0);
+          const ssize_t r = conn_recv(c, buf, sizeof(buf));
           if (r > 0) {
-            if (!c->read_shut) c->in.append(buf, (size_t)r);
+            if (!c->read_shut) {
+              c->in.append(buf, (size_t)r);
+              // parse as the bytes arrive: complete requests and chunk data leave c->in, so
+              // what it holds stays bounded by one header block or one Content-Length body
+              parse_input(S, c);
+            }
             continue;
           }
-          if (r == 0) eof = true;
-          else if (errno == EINTR) continue;
-          else if (errno != EAGAIN && errno != EWOULDBLOCK) eof = true;
+          if (r == 0 || r == -2) eof = true;
           break;
         }
-        parse_input(S, c);
         if (eof) {
           // the client closed: answer what it already sent only if it can still read
           if (c->next_out == c->next_seq) {
@@ -399,6 +560,16 @@ void poll_once(Server* S, int wait_ms) {
     }
   }
 }
+
+int tls_password_cb(char* buf, int size, int, void* u) {
+  const char* pw = static_cast<const char*>(u);
+  if (!pw) return 0;
+  const int n = (int)std::min<size_t>(strlen(pw), (size_t)size);
+  memcpy(buf, pw, (size_t)n);
+  return n;
+}
+
+thread_local std::string tls_err;
 
 }  // namespace
 
@@ -445,6 +616,46 @@ void* oryx_http_start(const char* host, int port, int backlog, long long max_bod
   epoll_ctl(S->efd, EPOLL_CTL_ADD, S->wfd, &ev);
   return S;
 }
+
+// Serves HTTPS on the server's socket: PEM certificate chain `cert`, private key `key` (null
+// or empty: the key is in `cert`), `password` for an encrypted key (may be null).  TLS 1.2 is
+// the minimum (the reference's connector allows TLSv1.2 and 1.1; 1.1 is deprecated).  Call
+// before the first oryx_http_next.  Returns 0, or -1 (oryx_http_tls_error says why).
+int oryx_http_tls(void* h, const char* cert, const char* key, const char* password) {
+  auto* S = static_cast<Server*>(h);
+  tls_err.clear();
+  SSL_CTX* ctx = SSL_CTX_new(TLS_server_method());
+  if (!ctx) {
+    tls_err = "SSL_CTX_new failed";
+    return -1;
+  }
+  SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+  SSL_CTX_set_mode(ctx, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER |
+                            SSL_MODE_RELEASE_BUFFERS);
+  SSL_CTX_set_options(ctx, SSL_OP_NO_RENEGOTIATION);
+  std::string pw = password ? password : "";
+  SSL_CTX_set_default_passwd_cb(ctx, tls_password_cb);
+  SSL_CTX_set_default_passwd_cb_userdata(ctx, password ? (void*)pw.c_str() : nullptr);
+  const char* kf = key && *key ? key : cert;
+  auto fail = [&](const char* what) {
+    char eb[256];
+    ERR_error_string_n(ERR_get_error(), eb, sizeof(eb));
+    tls_err = std::string(what) + ": " + eb;
+    SSL_CTX_free(ctx);
+    return -1;
+  };
+  if (SSL_CTX_use_certificate_chain_file(ctx, cert) != 1) return fail("certificate");
+  if (SSL_CTX_use_PrivateKey_file(ctx, kf, SSL_FILETYPE_PEM) != 1) return fail("private key");
+  if (SSL_CTX_check_private_key(ctx) != 1) return fail("key does not match certificate");
+  // the password is only needed while loading
+  SSL_CTX_set_default_passwd_cb_userdata(ctx, nullptr);
+  std::lock_guard<std::mutex> g(S->cmu);
+  if (S->tls) SSL_CTX_free(S->tls);
+  S->tls = ctx;
+  return 0;
+}
+
+const char* oryx_http_tls_error() { return tls_err.c_str(); }
 
 int oryx_http_port(void* h) { return static_cast<Server*>(h)->port; }
 
@@ -523,7 +734,7 @@ int oryx_http_respond(void* h, unsigned long long id, const char* data, long lon
   Conn* c = ct->second.get();
   c->done[seq] = {std::move(bytes), close_after != 0};
   // written from this thread when it is the connection's next response (the socket is
-  // non-blocking: what does not fit now is written by the loop on EPOLLOUT)
+  // non-blocking: what does not fit now is written by the poller on EPOLLOUT)
   flush_conn(S, c);
   return 0;
 }
@@ -540,7 +751,10 @@ void oryx_http_stop(void* h) {
     S->qcv.wait_for(l, std::chrono::seconds(5), [&] { return !S->leader; });
   }
   std::lock_guard<std::mutex> g(S->cmu);
-  for (auto& kv : S->conns) close(kv.first);
+  for (auto& kv : S->conns) {
+    if (kv.second->ssl) SSL_free(kv.second->ssl);
+    close(kv.first);
+  }
   S->conns.clear();
   close(S->lfd);
   close(S->efd);
@@ -548,6 +762,10 @@ void oryx_http_stop(void* h) {
 }
 
 // Frees a stopped server (no handler thread may still use it).
-void oryx_http_free(void* h) { delete static_cast<Server*>(h); }
+void oryx_http_free(void* h) {
+  auto* S = static_cast<Server*>(h);
+  if (S && S->tls) SSL_CTX_free(S->tls);
+  delete S;
+}
 
 }  // extern "C"

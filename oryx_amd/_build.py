@@ -59,7 +59,7 @@ def build_runtime(force: bool = False, verbose: bool = False) -> str:
     if force or _stale(RUNTIME_SO, srcs + hdrs):
         tmp = RUNTIME_SO + ".tmp"
         cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-Wall", "-pthread",
-               "-o", tmp] + srcs + ["-lz"]
+               "-o", tmp] + srcs + ["-lz", "-lssl", "-lcrypto"]
         if verbose:
             print(" ".join(cmd), flush=True)
         _run(cmd)

@@ -145,6 +145,8 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_http_respond", c_i, [c_vp, ctypes.c_ulonglong, c_cp, c_ll, c_i])
     _sig(lib, "oryx_http_stop", None, [c_vp])
     _sig(lib, "oryx_http_free", None, [c_vp])
+    _sig(lib, "oryx_http_tls", c_i, [c_vp, c_cp, c_cp, c_cp])
+    _sig(lib, "oryx_http_tls_error", c_cp, [])
     _sig(lib, "oryx_speed_append", c_ll, [c_vp, c_vp, c_i, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,
                                           c_vp, c_vp, c_i, c_ll, c_i, c_vp])
     _sig(lib, "oryx_split_by_time", c_ll, [c_vp, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,

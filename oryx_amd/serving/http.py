@@ -567,7 +567,8 @@ class NativeHTTPServer:
 
     def __init__(self, host: str, port: int, router: "Router", app_context: dict,
                  auth: Optional[DigestAuth] = None, metrics=None, threads: int = 16,
-                 max_body: int = 64 << 20):
+                 max_body: int = 64 << 20, tls: Optional[Tuple[str, Optional[str],
+                                                               Optional[str]]] = None):
         from .. import native
         self.router = router
         self.app_context = app_context
@@ -578,6 +579,18 @@ class NativeHTTPServer:
                                             int(max_body))
         if not self._h:
             raise OSError("cannot listen on %s:%d" % (host, port))
+        if tls is not None:
+            # HTTPS on the same loop: PEM certificate chain, key (None: in the certificate
+            # file), key password (ServingLayer.java:194-245 keystore)
+            cert, key, password = tls
+            enc = (lambda v: v.encode() if v else None)
+            if self._lib.oryx_http_tls(self._h, enc(cert), enc(key), enc(password)) != 0:
+                err = (self._lib.oryx_http_tls_error() or b"").decode(errors="replace")
+                self._lib.oryx_http_stop(self._h)
+                self._lib.oryx_http_free(self._h)
+                self._h = None
+                raise ssl.SSLError("TLS setup failed: %s" % err)
+        self.tls = tls is not None
         self.server_address = (host, int(self._lib.oryx_http_port(self._h)))
         self._threads: List[threading.Thread] = []
         self._n_threads = max(1, int(threads))
@@ -609,7 +622,10 @@ class NativeHTTPServer:
                 cap = -n
                 buf = ctypes.create_string_buffer(cap)
                 continue
-            raw = buf.raw[:n]
+            raw = ctypes.string_at(buf, n)
+            if cap > (1 << 20):             # one large body: do not keep a huge buffer
+                cap = 1 << 16
+                buf = ctypes.create_string_buffer(cap)
             rid, ml, tl, hl, bl = struct.unpack_from("<QIIIQ", raw, 0)
             o = 28
             method = raw[o:o + ml].decode("latin-1")
@@ -668,11 +684,14 @@ class NativeHTTPServer:
 def make_server(host: str, port: int, router: "Router", app_context: dict,
                 ssl_context: Optional[ssl.SSLContext] = None,
                 auth: Optional[DigestAuth] = None, metrics=None, native: bool = True,
-                threads: int = 16):
-    """The native front end (:class:`NativeHTTPServer`) unless TLS is configured or
-    ``native`` is off; the Python :class:`OryxHTTPServer` otherwise."""
-    if native and ssl_context is None:
-        return NativeHTTPServer(host, port, router, app_context, auth, metrics, threads)
+                threads: int = 16,
+                tls_files: Optional[Tuple[str, Optional[str], Optional[str]]] = None):
+    """The native front end (:class:`NativeHTTPServer`, HTTP or -- with ``tls_files`` =
+    (certificate chain, key, password) -- HTTPS); the Python :class:`OryxHTTPServer` when
+    ``native`` is off or TLS comes only as an ``ssl_context``."""
+    if native and (ssl_context is None or tls_files is not None):
+        return NativeHTTPServer(host, port, router, app_context, auth, metrics, threads,
+                                tls=tls_files)
     return OryxHTTPServer(host, port, router, app_context, ssl_context, auth, metrics)
 
 

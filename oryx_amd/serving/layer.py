@@ -207,11 +207,16 @@ class ServingLayer:
         if self.user_name and self.password:
             auth = http.DigestAuth(self.user_name, self.password)
         port = self.secure_port if ssl_ctx is not None else self.port
-        # the native front end (csrc/runtime/oryx_http.cpp) unless TLS is on or
-        # oryx.serving.api.native-http is false
+        tls_files = None
+        if ssl_ctx is not None:
+            tls_files = (ioutils.to_local_path(self.keystore_file),
+                         ioutils.to_local_path(self.key_file) if self.key_file else None,
+                         self.keystore_password)
+        # the native front end (csrc/runtime/oryx_http.cpp: HTTP, or HTTPS through OpenSSL)
+        # unless oryx.serving.api.native-http is false
         self._server = http.make_server(self.host, port, router, self.context, ssl_ctx, auth,
                                         self.metrics, native=self.native_http,
-                                        threads=self.handler_threads)
+                                        threads=self.handler_threads, tls_files=tls_files)
         self._server.start_background()
         log.info("Serving layer listening on %s:%d%s", self.host, self._server.port,
                  " (HTTPS)" if ssl_ctx else "")

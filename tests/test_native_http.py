@@ -147,3 +147,138 @@ def test_expect_continue_malformed_and_concurrency():
     finally:
         srv.shutdown()
         srv.server_close()
+
+
+def _raw(srv, data, n=1, timeout=10.0):
+    s = socket.create_connection(("127.0.0.1", srv.port), timeout=timeout)
+    try:
+        s.sendall(data)
+        return _recv_responses(s, n, timeout)
+    finally:
+        s.close()
+
+
+def test_chunked_limits_and_incremental_parse():
+    """Chunk sizes are validated before anything is buffered: a size past max_body, a size that
+    would wrap a signed sum (1-byte chunk then 7fff...f), a non-hex size -- all answered with an
+    error and the connection closed; a body of many tiny chunks is parsed incrementally."""
+    def echo(req):
+        return ohttp.Response(200, req.raw_body, ohttp.TEXT)
+
+    srv = ohttp.NativeHTTPServer("127.0.0.1", 0,
+                                 ohttp.Router([ohttp.Route("POST", "/echo", echo,
+                                                           produces=(ohttp.TEXT,))], "/"),
+                                 {}, threads=2, max_body=1 << 20)
+    srv.start_background()
+    head = b"POST /echo HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n"
+    try:
+        # larger than max_body
+        (st, _, _), = _raw(srv, head + b"200000\r\n")
+        assert st == 413
+        # overflow attempt: the second size alone exceeds what is left
+        (st, _, _), = _raw(srv, head + b"1\r\na\r\n7fffffffffffffff\r\n")
+        assert st in (400, 413)           # 16 hex digits: rejected as malformed
+        (st, _, _), = _raw(srv, head + b"1\r\na\r\nfffffffffffffff\r\n")
+        assert st == 413
+        # 16+ hex digits / junk sizes
+        (st, _, _), = _raw(srv, head + b"10000000000000000\r\n")
+        assert st == 400
+        (st, _, _), = _raw(srv, head + b"zz\r\n")
+        assert st == 400
+        # 20k one-byte chunks sent in small pieces, then a normal request on the same socket
+        body = b"".join(b"1\r\n%c\r\n" % (65 + j % 26) for j in range(20000)) + b"0\r\n\r\n"
+        s = socket.create_connection(("127.0.0.1", srv.port), timeout=30)
+        try:
+            s.sendall(head)
+            t0 = time.perf_counter()
+            for o in range(0, len(body), 97):
+                s.sendall(body[o:o + 97])
+            s.sendall(b"POST /echo HTTP/1.1\r\nHost: x\r\nContent-Length: 2\r\n\r\nok")
+            out = _recv_responses(s, 2, 30)
+            dt = time.perf_counter() - t0
+        finally:
+            s.close()
+        want = bytes(65 + j % 26 for j in range(20000))
+        assert [o[0] for o in out] == [200, 200] and out[0][2] == want and out[1][2] == b"ok"
+        assert dt < 10.0
+        # Content-Length above max_body
+        (st, _, _), = _raw(srv, b"POST /echo HTTP/1.1\r\nContent-Length: 2000000\r\n\r\n")
+        assert st == 413
+    finally:
+        srv.shutdown()
+        srv.server_close()
+
+
+def test_native_https(tmp_path):
+    """HTTPS on the native loop (OpenSSL, non-blocking handshake): keep-alive requests,
+    a chunked body, pipelining, and a plain-HTTP client refused."""
+    import shutil
+    import ssl
+    import subprocess
+    if not shutil.which("openssl"):
+        pytest.skip("no openssl binary to make a test certificate")
+    cert, key = str(tmp_path / "c.pem"), str(tmp_path / "k.pem")
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", key,
+                    "-out", cert, "-days", "2", "-subj", "/CN=127.0.0.1"], check=True,
+                   capture_output=True, timeout=60)
+
+    def echo(req):
+        return ohttp.Response(200, req.raw_body, ohttp.TEXT)
+
+    def hello(req):
+        return "hello %s" % ",".join(req.query.get("x", []))
+
+    routes = [ohttp.Route("POST", "/echo", echo, produces=(ohttp.TEXT,)),
+              ohttp.Route("GET", "/hello", hello, produces=(ohttp.TEXT,))]
+    srv = ohttp.NativeHTTPServer("127.0.0.1", 0, ohttp.Router(routes, "/"), {}, threads=4,
+                                 tls=(cert, key, None))
+    srv.start_background()
+    try:
+        ctx = ssl.create_default_context(cafile=cert)
+        ctx.check_hostname = False
+        c = http.client.HTTPSConnection("127.0.0.1", srv.port, timeout=10, context=ctx)
+        for j in range(20):
+            c.request("GET", "/hello?x=%d" % j)
+            r = c.getresponse()
+            assert r.status == 200 and r.read() == b"hello %d" % j
+        big = bytes(range(256)) * 2000
+        c.request("POST", "/echo", body=iter([big[:1000], big[1000:]]),
+                  headers={"Transfer-Encoding": "chunked"}, encode_chunked=True)
+        r = c.getresponse()
+        assert r.status == 200 and r.read() == big
+        c.close()
+        # pipelined over one TLS connection
+        raw = socket.create_connection(("127.0.0.1", srv.port), timeout=10)
+        s = ctx.wrap_socket(raw, server_hostname="127.0.0.1")
+        s.sendall(b"".join(b"GET /hello?x=%d HTTP/1.1\r\nHost: x\r\n\r\n" % j
+                           for j in range(10)))
+        out = _recv_responses(s, 10)
+        s.close()
+        assert [o[2] for o in out] == [b"hello %d" % j for j in range(10)]
+        # concurrent TLS clients
+        errs = []
+
+        def client(cid):
+            try:
+                cc = http.client.HTTPSConnection("127.0.0.1", srv.port, timeout=20, context=ctx)
+                for j in range(10):
+                    cc.request("GET", "/hello?x=%d-%d" % (cid, j))
+                    rr = cc.getresponse()
+                    assert rr.read() == b"hello %d-%d" % (cid, j)
+                cc.close()
+            except Exception as e:   # noqa: BLE001
+                errs.append(e)
+        ts = [threading.Thread(target=client, args=(i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(30)
+        assert not errs, errs[:2]
+        # plain HTTP against the TLS port gets no HTTP answer
+        with pytest.raises(Exception):
+            pc = http.client.HTTPConnection("127.0.0.1", srv.port, timeout=5)
+            pc.request("GET", "/hello")
+            pc.getresponse().read()
+    finally:
+        srv.shutdown()
+        srv.server_close()

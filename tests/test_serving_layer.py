@@ -165,6 +165,9 @@ def test_https_and_digest_auth(tmp_path):
                   "oryx.serving.api.user-name": "oryx",
                   "oryx.serving.api.password": "pass"})
     try:
+        from oryx_amd.serving.http import NativeHTTPServer
+        # HTTPS stays on the native front end (OpenSSL in oryx_http.cpp)
+        assert isinstance(lay._server, NativeHTTPServer) and lay._server.tls
         url = "https://127.0.0.1:%d/recommend/U0" % lay.actual_port
         ctx = ssl.create_default_context(cafile=cert)
         ctx.check_hostname = False
