@@ -83,6 +83,336 @@ struct BatchCfg {
 typedef __attribute__((address_space(3))) float lds_float;
 typedef __attribute__((address_space(3))) f32x4 lds_f32x4;
 
+// ---- replica layout of the solve (NM < 4 rows per wave): lane group g works on batch row
+// g % NM as replica q = g / NM of R = 4 / NM.  The group-layout work (LDL^T of the diagonal
+// tiles, forward / rhs / back substitution) splits a 16-column panel over the replicas --
+// replica q owns columns R k + q, k < 16 / R -- instead of repeating it R times.
+// v_permlane32_swap / v_permlane16_swap of a value with itself: (lo, hi) = the lower / upper
+// half's value (32) or the even / odd row's value of each row pair (16), on every lane.  Inline
+// asm: hipcc treats the two results of the swap builtins as interchangeable when both operands
+// hold the same value, and picks the wrong one.  The nops cover a VALU write of the operands
+// before the swap and a DPP read of its results right after it (neither is visible to the
+// compiler's hazard recognizer through the asm).
+__device__ __forceinline__ void swap32(float v, float& lo, float& hi) {
+  float a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  lo = a;
+  hi = b;
+}
+__device__ __forceinline__ void swap16(float v, float& ev, float& od) {
+  float a = v, b = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  ev = a;
+  od = b;
+}
+// The value replica QJ holds for the same (row, tile row r), on every lane:
+template <int R, int QJ>
+__device__ __forceinline__ float from_rep(float v) {
+  if constexpr (R == 1) {
+    return v;
+  } else if constexpr (R == 2) {   // replicas = wave halves
+    float lo, hi;
+    swap32(v, lo, hi);
+    return QJ == 0 ? lo : hi;
+  } else {                         // replicas = 16-lane rows: pair rows, then halves
+    float ev, od, lo, hi;
+    swap16(v, ev, od);
+    swap32((QJ & 1) ? od : ev, lo, hi);
+    return (QJ >> 1) ? hi : lo;
+  }
+}
+// sum over the replicas (every replica gets it)
+template <int R>
+__device__ __forceinline__ float rep_sum(float v) {
+  if constexpr (R == 1) {
+    return v;
+  } else if constexpr (R == 2) {
+    float lo, hi;
+    swap32(v, lo, hi);
+    return lo + hi;
+  } else {
+    float ev, od, lo, hi;
+    swap16(v, ev, od);
+    swap32(ev + od, lo, hi);
+    return lo + hi;
+  }
+}
+// DPP row_ror:N (lane i of each 16-lane row reads lane (i - N) mod 16)
+template <int N>
+__device__ __forceinline__ float ror(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x120 + N, 0xF, 0xF, false));
+}
+// a copy in which lane i of replica q holds lane (i + q) mod 16's value, so that a DPP
+// broadcast of lane R k reads column R k + q of the replica
+template <int R>
+__device__ __forceinline__ float rep_rot(float v, int q) {
+  if constexpr (R == 1) {
+    return v;
+  } else if constexpr (R == 2) {
+    const float t = ror<15>(v);
+    return q ? t : v;
+  } else {
+    const float t1 = ror<15>(v), t2 = ror<14>(v), t3 = ror<13>(v);
+    float r = q == 1 ? t1 : v;
+    r = q == 2 ? t2 : r;
+    return q == 3 ? t3 : r;
+  }
+}
+
+#ifndef ORYX_ALS_SOLVE_LEGACY
+#define ORYX_ALS_SOLVE_LEGACY 0
+#endif
+#if !ORYX_ALS_SOLVE_LEGACY
+// Normal equations, batched block LDL^T + forward solve, back substitution of the NM rows one
+// wave holds (lane group g works on row g % NM as replica g / NM, see from_rep).  acc: the
+// upper 16x16 tiles of each row's Gramian (YtY included), bpart / cnt: the gather's per-lane
+// partials.  scr / vdis: the wave's LDS scratch (NM*16 rows of DS floats, NM*16 floats).  Out:
+// lane (m, r) holds x_m[16 pp + r] in xs[pp] (every replica).  hook(integral_constant<0>) runs
+// after the first panel's LDL^T, hook(<1>) after the first (M == 1) or second panel -- the
+// next batch's metadata is fetched there, under the solve.  phase(i) marks the per-phase cycle
+// counters (analysis builds).
+//
+// Per panel p, the diagonal tile's LDL^T runs as row operations on [A | I] in row form: lane
+// (row r, replica q) holds A[r][R k + q] and Li[r][R k + q]; step j subtracts m_r = A[r][j] /
+// A[j][j] times pivot row j (a DPP broadcast of lane j inside each 16-lane row) from the rows
+// below it.  The A half only needs the columns right of j and the Li half the ones up to j,
+// so a step costs about 16 / R + 1 fused DPP FMAs; m_r comes from replica j % R by one or two
+// lane-swap instructions.  Row form reads the pivot row's entries right of the diagonal, so
+// the tile is made symmetric in LDS first (the upper entries of a Gramian tile built from
+// bf16(c y) operands are not exactly the lower ones: the lower triangle is the matrix).
+template <int KP, int NM, typename Hook, typename Phase>
+__device__ __forceinline__ void batch_solve(const AlsParams& p, int lane,
+                                            f32x4 (&acc)[NM][(KP / 16) * (KP / 16 + 1) / 2],
+                                            float (&bpart)[NM][KP / 16], const float (&cnt)[NM],
+                                            const int (&slot)[NM], const bool (&valid)[NM],
+                                            lds_float* scr, lds_float* vdis, float (&xs)[KP / 16],
+                                            Hook&& hook, Phase&& phase) {
+  constexpr int M = KP / 16;
+  constexpr int DS = BATCH_DS;
+  constexpr int R = 4 / NM;
+  constexpr int NC = 16 / R;
+  const int g = lane >> 4, f = lane & 15;
+  const int mg = g & (NM - 1);
+  int q = g / NM;
+  asm volatile("" : "+v"(q));
+  // this lane's scratch row and its first column (R k + q: immediate offsets R k)
+  lds_float* srow = scr + (mg * 16 + f) * DS + q;
+  // ------------------------------------------------------------ normal equations
+  float cntw[NM];
+  static_for<NM>([&](auto Mc) {
+    constexpr int m = decltype(Mc)::value;
+    cntw[m] = wave_sum(cnt[m]);
+    reduce_bpart<M>(bpart[m]);   // lane (g, f): bpart[m][pi] = b_m[16 pi + f]
+    if (slot[m] >= 0) {
+      // split row: Gramian, b and count were summed by als_partial into ws[slot]
+      const float* src = p.ws + (int64_t)slot[m] * ws_stride(KP);
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi)
+#pragma unroll
+        for (int qi = pi; qi < M; ++qi)
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            acc[m][tix<M>(pi, qi)][v] += src[(16 * pi + 4 * g + v) * KP + 16 * qi + f];
+#pragma unroll
+      for (int pi = 0; pi < M; ++pi) bpart[m][pi] = src[KP * KP + 16 * pi + f];
+      cntw[m] = src[KP * KP + KP];
+    }
+    // lambda n_u on the diagonal (1 on the zero-padded features, so they solve to 0)
+    int rel = f - 4 * g;
+    asm volatile("" : "+v"(rel));
+#pragma unroll
+    for (int pp = 0; pp < M; ++pp) {
+      const float dg = 16 * pp + f < p.k ? p.lambda * cntw[m] : 1.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[m][tix<M>(pp, pp)][v] += rel == v ? dg : 0.f;
+    }
+  });
+  // right-hand sides in group layout: lane (m, r) holds b_m[16 pi + r]
+  float rhs[M];
+#pragma unroll
+  for (int pi = 0; pi < M; ++pi) {
+    float r = bpart[0][pi];
+    static_for<NM - 1>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value + 1;
+      r = mg == m ? bpart[m][pi] : r;
+    });
+    rhs[pi] = r;
+  }
+
+  phase(2);
+  // ------------------------------------------------------------ block LDL^T + forward
+  float zp[M], disv[M];
+  int bad = 0;
+  static_for<M>([&](auto Pc) {
+    constexpr int pp = decltype(Pc)::value;
+    constexpr int td = tix<M>(pp, pp);
+    // diagonal tiles -> symmetric rows in LDS: scratch row (m, b) position a = T(a, b) for
+    // a <= b (the accumulator column), then T(a, b) also to row a position b for a < b
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+      *reinterpret_cast<lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g) = acc[m][td];
+    {
+      int rel = f - 4 * g;
+      asm volatile("" : "+v"(rel));
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          if (rel > v) scr[(m * 16 + 4 * g + v) * DS + f] = acc[m][td][v];
+    }
+    wave_sync();
+    float a[NC], e[NC];
+#pragma unroll
+    for (int k = 0; k < NC; ++k) a[k] = srow[R * k];
+    wave_sync();
+    {
+      int fq = f - q;
+      asm volatile("" : "+v"(fq));
+#pragma unroll
+      for (int k = 0; k < NC; ++k) e[k] = R * k == fq ? 1.f : 0.f;
+    }
+    static_for<16>([&](auto Jc) {
+      constexpr int j = decltype(Jc)::value;
+      const float val = from_rep<R, j % R>(a[j / R]);   // A[r][j], every replica
+      float piv = rbc<j>(val);
+      piv = piv > 1e-30f ? piv : 1e-30f;
+      int rl = f - j;
+      asm volatile("" : "+v"(rl));
+      const float nml = rl > 0 ? -(val * __builtin_amdgcn_rcpf(piv)) : 0.f;
+      // A half: columns right of j; Li half: columns up to j (Li[r][j] = -m_r comes out of
+      // the pivot row's Li[j][j] = 1)
+      dfb_n<j, (j + 1) / R, NC - (j + 1) / R>(nml, a);
+      dfb_n<j, 0, j / R + 1>(nml, e);
+    });
+    phase(3);
+    if constexpr (pp == 0) hook(std::integral_constant<int, 0>{});
+    // the pivots: A[r][r] is left in place (rows are not touched from their own step on)
+#pragma unroll
+    for (int k = 0; k < NC; ++k) srow[R * k] = a[k];
+    wave_sync();
+    float dself = scr[(mg * 16 + f) * DS + f];
+    wave_sync();
+    bad |= !(dself > 0.f);
+    dself = dself > 1e-30f ? dself : 1e-30f;
+    const float dis = __builtin_amdgcn_rsqf(dself);
+    disv[pp] = dis;
+    // forward: z_p = D^-1/2 Li r_p
+    float z0 = 0.f, z1 = 0.f;
+    dfc_s<R, 0, NC>(z0, z1, rep_rot<R>(rhs[pp], q), e);
+    const float z = rep_sum<R>(z0 + z1) * dis;
+    zp[pp] = z;
+    const float zq = rep_rot<R>(z, q);
+    // Li rows and D^-1/2 to LDS; back as Li^T in accumulator layout (lane (g, f): Li[f][4g+v])
+#pragma unroll
+    for (int k = 0; k < NC; ++k) srow[R * k] = e[k];
+    vdis[mg * 16 + f] = dis;
+    wave_sync();
+    f32x4 Y[NM], d4[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      Y[m] = *reinterpret_cast<const lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g);
+      d4[m] = *reinterpret_cast<const lds_f32x4*>(vdis + m * 16 + 4 * g);
+    }
+    wave_sync();
+    // K_j = D^-1/2 Li U_pj in place of U_pj
+    static_for<M - 1 - pp>([&](auto Jc) {
+      constexpr int j = pp + 1 + decltype(Jc)::value;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        f32x4 K = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          K = __builtin_amdgcn_mfma_f32_16x16x4f32(Y[m][v], acc[m][tix<M>(pp, j)][v], K, 0, 0,
+                                                    0);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) K[v] *= d4[m][v];
+        acc[m][tix<M>(pp, j)] = K;
+      }
+    });
+    // trailing update U_ij -= K_i^T K_j (i <= j), before the rhs work so it overlaps it
+    static_for<M - 1 - pp>([&](auto Ic) {
+      constexpr int i = pp + 1 + decltype(Ic)::value;
+      static_for<M - i>([&](auto Jc) {
+        constexpr int j = i + decltype(Jc)::value;
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+            acc[m][tix<M>(i, j)] = __builtin_amdgcn_mfma_f32_16x16x4f32(
+                -acc[m][tix<M>(pp, i)][v], acc[m][tix<M>(pp, j)][v], acc[m][tix<M>(i, j)], 0,
+                0, 0);
+      });
+    });
+    // r_i -= K_i^T z_p: column r of K_i to lane (m, r) through LDS (the replica's columns),
+    // z broadcast by DPP
+    static_for<M - 1 - pp>([&](auto Ic) {
+      constexpr int i = pp + 1 + decltype(Ic)::value;
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+        *reinterpret_cast<lds_f32x4*>(scr + (m * 16 + f) * DS + 4 * g) = acc[m][tix<M>(pp, i)];
+      wave_sync();
+      float col[NC];
+#pragma unroll
+      for (int k = 0; k < NC; ++k) col[k] = srow[R * k];
+      wave_sync();
+      float o0 = 0.f, o1 = 0.f;
+      dfc_s<R, 0, NC>(o0, o1, zq, col);
+      rhs[i] -= rep_sum<R>(o0 + o1);
+    });
+    // keep Li^T (accumulator layout) for the back substitution in the dead diagonal tile
+#pragma unroll
+    for (int m = 0; m < NM; ++m) acc[m][td] = Y[m];
+    if constexpr (pp == (M > 1 ? 1 : 0)) hook(std::integral_constant<int, 1>{});
+    phase(4);
+  });
+  {
+    const unsigned long long bm = __ballot(bad != 0);
+    if (lane == 0 && p.fail_count) {
+      int nbad = 0;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) nbad += (valid[m] && ((bm >> (16 * m)) & 0xFFFFull)) ? 1 : 0;
+      if (nbad) atomicAdd(p.fail_count, nbad);
+    }
+  }
+
+  // ------------------------------------------------------------ back substitution
+  // row form of an accumulator-layout tile T of every row: lane (m, r, q) gets T_m[r][R k + q]
+  auto rows_of = [&](const f32x4* T, float (&out)[NC]) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) scr[(m * 16 + 4 * g + v) * DS + f] = T[m][v];
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < NC; ++k) out[k] = srow[R * k];
+    wave_sync();
+  };
+  static_for_desc<M>([&](auto Pc) {
+    constexpr int pp = decltype(Pc)::value;
+    float w0 = 0.f, w1 = 0.f;
+    static_for<M - 1 - pp>([&](auto Ic) {
+      constexpr int i = pp + 1 + decltype(Ic)::value;
+      f32x4 T[NM];
+#pragma unroll
+      for (int m = 0; m < NM; ++m) T[m] = acc[m][tix<M>(pp, i)];
+      float row[NC];
+      rows_of(T, row);   // K_i[r][R k + q]
+      dfc_s<R, 0, NC>(w0, w1, rep_rot<R>(xs[i], q), row);
+    });
+    const float yv = (zp[pp] - rep_sum<R>(w0 + w1)) * disv[pp];
+    f32x4 T[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) T[m] = acc[m][tix<M>(pp, pp)];
+    float col[NC];
+    rows_of(T, col);   // Li^T[a][c] = Li[c][a], c = R k + q
+    float x0 = 0.f, x1 = 0.f;
+    dfc_s<R, 0, NC>(x0, x1, rep_rot<R>(yv, q), col);
+    xs[pp] = rep_sum<R>(x0 + x1);
+  });
+}
+
+#else   // the pre-r5 solve (each replica repeats the group-layout work), for A/B builds
 // Normal equations, batched block LDL^T + forward solve, back substitution of the NM rows one
 // wave holds (lane group g works on row g % NM).  acc: the upper 16x16 tiles of each row's
 // Gramian (YtY included), bpart / cnt: the gather's per-lane partials.  scr / vdis: the wave's
@@ -315,6 +645,8 @@ __device__ __forceinline__ void batch_solve(const AlsParams& p, int lane,
     xs[pp] = x0 + x1;
   });
 }
+
+#endif  // ORYX_ALS_SOLVE_LEGACY
 
 // D: chunks in flight per row (register ring depth); the wave keeps NM * D gathers in flight.
 // PROF: per-phase shader-clock cycles summed into prof[0..7] (analysis build,
@@ -677,7 +1009,14 @@ struct GlCfg {
   static constexpr int G = NPL * (SPLIT ? 2 : 1) + 1;   // VMEM operations of one chunk issue
   static constexpr int META = 256;                      // 32 column ids + 32 values
   static constexpr int SCR = NM * 16 * BATCH_DS * 4;
-  static constexpr int WAVE_BYTES = NM * SLOT + NM * 2 * META + SCR + NM * 16 * 4;
+  // four rows per wave: the solve's scratch lives in image slots 2-3 (their next chunks are
+  // issued after the solve), so two such waves per SIMD fit the CU's LDS
+  // (when it fits there: KP >= 64)
+  static constexpr bool ALIAS = NM == 4 && 2 * SLOT >= SCR + NM * 16 * 4;
+  static constexpr int WAVE_BYTES =
+      NM * SLOT + NM * 2 * META + (ALIAS ? 0 : SCR + NM * 16 * 4);
+  // image slots whose next chunks are prefetched under the solve
+  static constexpr int PRE = ALIAS ? 2 : NM;
   // waves per SIMD (1: 512 registers per wave)
   static constexpr int WPE = WPE_;
   static constexpr int BYTES = 4 * WAVE_BYTES;
@@ -784,7 +1123,8 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
   auto meta_lds = [&](int m, int q) -> uint32_t {
     return my_lds + NM * C::SLOT + (m * 2 + q) * C::META;
   };
-  lds_float* scr = (lds_float*)(my + NM * C::SLOT + NM * 2 * C::META);
+  lds_float* scr =
+      (lds_float*)(C::ALIAS ? my + 2 * C::SLOT : my + NM * C::SLOT + NM * 2 * C::META);
   lds_float* vdis = scr + NM * 16 * BATCH_DS;
 
   // Lane-derived values are recomputed from an opaque lane id at each use in the chunk loop:
@@ -891,14 +1231,15 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
       issue_meta(m, beg_n[m], len_n[m], 1, 1);
     });
   };
-  auto stage3 = [&]() {
+  // the first chunks of rows 0 .. N-1 (under the solve: the slots its scratch does not use)
+  auto stage3 = [&](auto Nc) {
     vm_wait<0>();   // the metadata above (and anything older) has landed
-    static_for<NM>([&](auto Mc) { issue_y(decltype(Mc)::value, 0); });
+    static_for<decltype(Nc)::value>([&](auto Mc) { issue_y(decltype(Mc)::value, 0); });
   };
   if (blockIdx.x * 4 + wave < nb) {
     stage1(blockIdx.x * 4 + wave);
     stage2();
-    stage3();
+    stage3(std::integral_constant<int, NM>{});
   }
 
   const float alpha = p.alpha;
@@ -1112,23 +1453,25 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
         phase(8);
       }
     };
+    // Round kk consumes chunk kk of rows 0 .. NM-1.  Waiting for (m, kk)'s gather: the VMEM
+    // operations issued after it are (m+1 .. NM-1, kk) from the previous round and, unless
+    // this is the last round, (0 .. m-1, kk+1) from this one -- G each (round 0: everything of
+    // the first chunks has been waited for at m = 0).
     for (int kk = 0; kk < nr; ++kk) {
-      phase(1);
-      if (kk == 0 || NM == 1)
-        vm_wait<0>();
-      else
-        vm_wait<G>();
-      phase(7);
-      consume(std::integral_constant<int, 0>{}, kk);
-      if constexpr (NM == 2) {
+      static_for<NM>([&](auto Mc) {
+        constexpr int m = decltype(Mc)::value;
         phase(1);
-        if (kk + 1 < nr)
-          vm_wait<G>();
-        else
-          vm_wait<0>();
+        if (kk == 0) {
+          if (m == 0 || nr == 1) vm_wait<0>();
+          else vm_wait<m * G>();
+        } else if (kk + 1 < nr) {
+          vm_wait<(NM - 1) * G>();
+        } else {
+          vm_wait<(NM - 1 - m) * G>();
+        }
         phase(7);
-        consume(std::integral_constant<int, 1>{}, kk);
-      }
+        consume(Mc, kk);
+      });
     }
 
     phase(1);
@@ -1137,13 +1480,23 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
     batch_solve<KP, NM>(p, lane, acc, bpart, cnt, slot, valid, scr, vdis, xs,
                         [&](auto Hc) {
                           if constexpr (decltype(Hc)::value == 0) stage2();
-                          else stage3();
+                          else stage3(std::integral_constant<int, C::PRE>{});
                         },
                         phase);
+    if constexpr (C::ALIAS) {
+      // the scratch slots are free again: the next batch's first chunks of rows PRE ..
+      lds_drain();
+      static_for<NM - C::PRE>([&](auto Mc) { issue_y(C::PRE + decltype(Mc)::value, 0); });
+    }
 
-    // lane (m, r) holds x_m[16 pp + r] (the other groups duplicate rows 0 .. NM-1)
-    const int orow = (NM == 2 && (g & 1)) ? rows[NM - 1] : rows[0];
-    const bool ok = (NM == 2 && (g & 1)) ? valid[NM - 1] : valid[0];
+    // lane (m, r) holds x_m[16 pp + r] (NM < 4: the other groups duplicate rows 0 .. NM-1)
+    int orow = rows[0];
+    bool ok = valid[0];
+    static_for<NM - 1>([&](auto Mc) {
+      constexpr int m = decltype(Mc)::value + 1;
+      orow = (g & (NM - 1)) == m ? rows[m] : orow;
+      ok = (g & (NM - 1)) == m ? valid[m] : ok;
+    });
     if (ok && g < NM) {
 #pragma unroll
       for (int pp = 0; pp < M; ++pp) {
@@ -1210,8 +1563,8 @@ int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s
   return oryx_check_launch();
 }
 
-// Rank-128 configuration (rows per wave NM, waves per SIMD WPE) by the half-step's mean row
-// length.  Measured per half-step (rank-128 fp32, 25M ratings; profiles/r3_als128_gl_*):
+// Rank-128 configuration (rows per wave NM, waves per SIMD WPE).  Measured per half-step
+// before the replica-split solve (rank-128 fp32, 25M ratings; profiles/r3_als128_gl_*):
 //   items (423 ratings per row): NM 1 / WPE 1 4.63 ms, NM 2 / WPE 1 5.17, NM 1 / WPE 2 5.54;
 //   users (154 per row):         NM 1 / WPE 2 6.46 ms, NM 1 / WPE 1 7.02, NM 2 / WPE 1 7.08.
 // Long rows want the spill-free 512-register wave (the gather dominates and a spill reload
@@ -1227,7 +1580,11 @@ static void gl_config(long long mean_len, int& nm, int& wpe) {
     return e ? atoi(e) : 0;
   }();
   nm = fnm == 2 ? 2 : 1;
-  wpe = nm == 2 ? 1 : (mean_len >= 192 ? 1 : 2);
+  // r5: with the replica-split solve (a panel's group-layout work on four lane groups instead
+  // of repeated by each) the one-wave configuration wins at every row length: users 6.11 ms
+  // (two waves: 8.0, where the 256-register wave spills), items 4.18 ms
+  (void)mean_len;
+  wpe = 1;
   if (nm == 1 && (fwpe == 1 || fwpe == 2)) wpe = fwpe;
 }
 
