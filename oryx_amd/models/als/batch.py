@@ -530,8 +530,13 @@ class ALSUpdate(MLUpdate):
                           checkpoint_interval=self.checkpoint_interval, fingerprint=fingerprint,
                           x_init=x_init, y_init=y_init)
         X, Y = f.X, f.Y                 # stay on the device for the evaluation
-        if X.device.type == "cuda":
-            torch.cuda.synchronize(X.device)
+        if self.get_test_fraction() <= 0.0:
+            X = Y = None                # no evaluation: only the row text is kept
+        elif X._base is not None or Y._base is not None:
+            # compact copies: a view would keep the trainer's padded buffers alive
+            X, Y = X.clone(), Y.clone()
+        if f.X.device.type == "cuda":
+            torch.cuda.synchronize(f.X.device)
         ph["train"] = ph.get("train", 0.0) + time.perf_counter() - tp
         tp = time.perf_counter()
         # the rows' JSON text, formatted where the factors live (GPU: textfmt.hip); reused by
@@ -607,8 +612,8 @@ class ALSUpdate(MLUpdate):
         return self._timings.pop(candidate_path, {})
 
     # ---------------------------------------------------------------- evaluate
-    def _load(self, model_parent_path: str, pmml) -> dict:
-        cached = self._cache.get(model_parent_path)
+    def _load(self, model_parent_path: str, pmml, from_files: bool = False) -> dict:
+        cached = None if from_files else self._cache.get(model_parent_path)
         if cached is not None:
             return cached
         x_ids, X = read_features(os.path.join(model_parent_path,
@@ -650,8 +655,16 @@ class ALSUpdate(MLUpdate):
             au, ai, av = aggregate_scores(u, i, s, ts, self.implicit)
             mu = ucodes[au] if len(au) else au
             mi = icodes[ai] if len(ai) else ai
+        if f.get("X") is None or f.get("Y") is None:       # released or never kept
+            f = dict(f)
+            f.update({k: v for k, v in self._load(model_parent_path, model,
+                                                           from_files=True).items()
+                      if k in ("X", "Y")})
         X = f["X"] if isinstance(f["X"], torch.Tensor) else torch.from_numpy(f["X"])
         Y = f["Y"] if isinstance(f["Y"], torch.Tensor) else torch.from_numpy(f["Y"])
+        cached = self._cache.get(model_parent_path)
+        if cached is not None:
+            self._release_factors(cached)
         X, Y = X.to(device), Y.to(device)
         if self.implicit:
             # AUC over test positives; items universe = distinct test items (known to the model)
@@ -661,6 +674,11 @@ class ALSUpdate(MLUpdate):
         rmse = evaluation.rmse(X, Y, mu, mi, av, device=device)
         log.info("RMSE: %s", rmse)
         return -rmse
+
+    def _release_factors(self, f: dict) -> None:
+        """A candidate's factor matrices are not needed once it is evaluated (publish uses the
+        row text): free them instead of pinning device memory while later candidates train."""
+        f["X"] = f["Y"] = None
 
     # ---------------------------------------------------------------- publish
     def can_publish_additional_model_data(self) -> bool:

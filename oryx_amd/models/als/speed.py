@@ -178,7 +178,7 @@ class ALSSpeedModel(SpeedModel):
                 native.stream_ptr(self.device))
             native.check(rc, "oryx_spd_inverse_pair")
             ev = torch.cuda.Event()
-            ev.record()
+            ev.record(torch.cuda.current_stream(self.device))   # the launching stream
             return (invs, ok, grams), ev
         invs, oks = [], []
         for store in (self.X, self.Y):
@@ -190,13 +190,13 @@ class ALSSpeedModel(SpeedModel):
             oks.append((info == 0) & torch.isfinite(inv).all() & (inv.norm() * thr < 1.0))
             invs.append(inv)
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(torch.cuda.current_stream(self.device))
         return (invs, torch.stack(oks).all()), ev
 
     def _device_inverses_finish(self, work, ev):
         if work is None:
             return None
-        torch.cuda.current_stream().wait_event(ev)
+        torch.cuda.current_stream(self.device).wait_event(ev)
         invs, ok = work[0], work[1]
         if not bool(ok.cpu().min() if ok.dtype == torch.int32 else ok.item()):
             return None

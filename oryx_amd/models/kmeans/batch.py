@@ -99,9 +99,11 @@ class KMeansUpdate(MLUpdate):
         return self.history
 
     def _points(self, lines, ctx) -> torch.Tensor:
-        """This rank's records -> predictor matrix, float32 on the device."""
+        """This rank's records -> predictor matrix, float64 on the device: the evaluation
+        metrics score the parsed values in double precision as the reference does
+        (KMeansUpdate.java:139-178); training takes a float32 copy."""
         tp = time.perf_counter()
-        blk = parse_features(lines, self.input_schema, ctx.device, torch.float32,
+        blk = parse_features(lines, self.input_schema, ctx.device, torch.float64,
                              history=self._history_for(ctx.device))
         x = blk.predictors(self.input_schema).contiguous()
         self.phase_seconds["parse"] = self.phase_seconds.get("parse", 0.0) + \
@@ -113,18 +115,28 @@ class KMeansUpdate(MLUpdate):
         if k <= 1:
             raise ValueError("k must be > 1")
         ctx = self._ctx(context)
-        x = self._points(train_data, ctx)
+        x64 = self._points(train_data, ctx)
         # the evaluation of this candidate scores train + test points: it takes these parsed
         # rows instead of re-joining and re-reading the training text
-        self._train_points = (train_data, x)
+        self._train_points = (train_data, x64)
         sharded = self._sharded(ctx)
-        n = int(x.shape[0])
+        n = int(x64.shape[0])
         if sharded:
             from ...parallel import shuffle
             if sum(shuffle.all_gather_int(n, ctx)) == 0:
                 return None
         elif n == 0:
             return None
+        # train in float32 on points shifted by the (global) mean: k-means is translation
+        # invariant, and the fp32 distance expansion |x|^2 - 2 x.c + |c|^2 loses everything to
+        # cancellation when features carry a large common offset; the shift comes back on the
+        # centers in float64
+        s = torch.stack([x64.sum(0), torch.full((x64.shape[1],), float(n), dtype=torch.float64,
+                                                 device=x64.device)])
+        if sharded:
+            dist.all_reduce_sum(s, ctx)
+        shift = s[0] / s[1].clamp_min(1.0)
+        x = (x64 - shift).float()
         t0 = time.perf_counter()
         # sharded: this rank's share of the records; otherwise every rank parsed everything
         # and takes a disjoint slice
@@ -133,7 +145,7 @@ class KMeansUpdate(MLUpdate):
                                   self.initialization_strategy, seed=rng.next_seed(),
                                   ctx=ctx, precision=self.precision,
                                   reseed_empty=self.reseed_empty)
-        centers = res.centers.double().cpu().numpy()
+        centers = (res.centers.double() + shift).cpu().numpy()
         sizes = res.counts.cpu().numpy()
         self.phase_seconds["train"] = self.phase_seconds.get("train", 0.0) + \
             time.perf_counter() - t0

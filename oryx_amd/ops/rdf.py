@@ -893,7 +893,7 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
               "tot": to_host(split.totals), "vis": to_host(vis),
               "cat": to_host(split.cat_left) if split.cat_left is not None else None,
               "event": torch.cuda.Event()}
-        lv["event"].record()
+        lv["event"].record(torch.cuda.current_stream(dev))
         if live > 0:
             # next level: 2 * live slots, rows grouped by (tree, node) with one counting sort
             if next_last:

@@ -569,7 +569,7 @@ class ItemIndex:
         host = torch.empty(hd.shape, dtype=torch.int32, pin_memory=True)
         host.copy_(hd, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record()
+        ev.record(torch.cuda.current_stream(dev))   # the launching stream, not the current device's
 
         def wait_and_finish():
             ev.synchronize()

@@ -753,3 +753,22 @@ def test_kmeans_evaluate_reuses_parsed_training_points(tmp_path, strategy):
     upd._train_points = None                  # forces the joined parse
     fresh = upd.evaluate(None, model, None, test, train)
     assert cached == pytest.approx(fresh, rel=1e-9, abs=1e-12)
+
+
+def test_kmeans_update_evaluation_is_double_precision(tmp_path):
+    """Evaluation scores the parsed points in float64 (KMeansUpdate.java:139-178): features
+    with a large offset and a small spread (1e6 + O(0.01): float32 spacing there is 0.0625)
+    give the fp64 SSE of the text values, not of float32-rounded points."""
+    rs = np.random.default_rng(3)
+    pts = 1e6 + rs.normal(0, 0.02, (400, 4)) + np.repeat(np.arange(4)[:, None] * 4.0, 100, 0)
+    lines = ["%.6f,%.6f,%.6f,%.6f" % tuple(p) for p in pts]
+    upd = KMeansUpdate(_update_config(tmp_path, "SSE"))
+    pmml = upd.build_model(None, lines, [4], str(tmp_path / "cand"))
+    ev = upd.evaluate(None, pmml, str(tmp_path), [], lines)
+    cen = np.stack([c.center for c in read_clusters(pmml)])
+    x = np.array([[float(t) for t in l.split(",")] for l in lines])
+    d2 = ((x[:, None, :] - cen[None, :, :]) ** 2).sum(2).min(1)
+    assert ev == pytest.approx(-d2.sum(), rel=1e-9)
+    x32 = x.astype(np.float32).astype(np.float64)
+    d32 = ((x32[:, None, :] - cen[None, :, :]) ** 2).sum(2).min(1)
+    assert abs(-d32.sum() - ev) > 1e-6 * abs(ev)      # float32 points would differ
