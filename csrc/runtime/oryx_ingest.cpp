@@ -3340,4 +3340,19 @@ void oryx_digest128(const unsigned char* p, long long n, unsigned long long* out
   out[1] = h2;
 }
 
+// A 64-bit hash of every key of a blob (key i = bytes [ends[i-1], ends[i])), mixed with
+// `seed`: FNV-1a over the bytes, then the splitmix64 finalizer.  The ALS trainer keys its
+// random factor initialisation by it, so a row starts from the same vector at any world size.
+void oryx_blob_hash64(const unsigned char* blob, const long long* ends, long long n,
+                      unsigned long long seed, unsigned long long* out) {
+  oryx_ff::parallel_ranges(n, 1 << 14, [&](long long lo, long long hi, int) {
+    for (long long i = lo; i < hi; ++i) {
+      const long long b = i ? ends[i - 1] : 0;
+      uint64_t h = 0xCBF29CE484222325ull ^ seed;
+      for (long long j = b; j < ends[i]; ++j) h = (h ^ blob[j]) * 0x100000001B3ull;
+      out[i] = mix64(h ^ (uint64_t)(ends[i] - b));
+    }
+  });
+}
+
 }  // extern "C"

@@ -163,6 +163,18 @@ def blob_strings(blob: np.ndarray, ends: np.ndarray) -> List[str]:
     return [raw[a:b].decode("utf-8") for a, b in zip(s, e)]
 
 
+def blob_hash64(blob: np.ndarray, ends: np.ndarray, seed: int = 0) -> np.ndarray:
+    """uint64 hash of every key of a (blob, ends) pair (native FNV-1a + splitmix64)."""
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    ends = np.ascontiguousarray(ends, dtype=np.int64)
+    out = np.empty(len(ends), dtype=np.uint64)
+    if len(ends):
+        from . import native
+        native.runtime().oryx_blob_hash64(_ptr(blob), _ptr(ends), len(ends),
+                                          int(seed) & ((1 << 64) - 1), _ptr(out))
+    return out
+
+
 def strings_blob(keys: Sequence[str]) -> Tuple[np.ndarray, np.ndarray]:
     """(blob, ends) of Python strings."""
     enc = [k.encode("utf-8") for k in keys]

@@ -47,7 +47,7 @@ from ...parallel import dist, shuffle
 from ...ops import textfmt
 from ...utils import config as cfg, ioutils, pmml as pmmlu, rng, text
 from . import evaluation
-from .trainer import ALSTrainer
+from .trainer import ALS_INIT_SEED, ALSTrainer
 
 from .history import RatingsHistory
 from . import sharded
@@ -505,7 +505,7 @@ class ALSUpdate(MLUpdate):
             triples = lambda: (u, i, s)
         seed = rng.next_seed()
         trainer = ALSTrainer(features, lam, alpha, self.implicit, ctx=ctx, seed=seed,
-                             precision=self.precision)
+                             precision=self.precision, init_seed=ALS_INIT_SEED)
         t0 = time.perf_counter()
         trainer.prepare(tr_u, tr_i, tr_s, len(used_u), len(used_i))
         del tr_u, tr_i, tr_s
@@ -526,9 +526,13 @@ class ALSUpdate(MLUpdate):
             x_init, y_init = _warm_start_factors(self.current_model_dir, features, x_ids, y_ids)
         ph["csr_prepare"] = ph.get("csr_prepare", 0.0) + (trainer.timings.get("prepare_s") or 0)
         tp = time.perf_counter()
+        # random rows keyed by ID hash (this rank's rows: every world_size-th)
+        W_, R_ = max(1, ctx.world_size), ctx.rank
+        xh = ingest.blob_hash64(*ingest.strings_blob(x_ids[R_::W_]))
+        yh = ingest.blob_hash64(*ingest.strings_blob(y_ids[R_::W_]))
         f = trainer.train(self.iterations, checkpoint_dir=ckpt_dir,
                           checkpoint_interval=self.checkpoint_interval, fingerprint=fingerprint,
-                          x_init=x_init, y_init=y_init)
+                          x_init=x_init, y_init=y_init, x_keys=xh, y_keys=yh)
         X, Y = f.X, f.Y                 # stay on the device for the evaluation
         if self.get_test_fraction() <= 0.0:
             X = Y = None                # no evaluation: only the row text is kept

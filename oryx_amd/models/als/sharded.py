@@ -156,7 +156,7 @@ def build(upd, ctx: dist.DistContext, lines, features: int, lam: float, alpha: f
     the others, :class:`ShardedModel`) or (None, None) without ratings."""
     from ...utils import pmml as pmmlu, rng
     from .batch import aggregate_scores_device, write_features
-    from .trainer import ALSTrainer
+    from .trainer import ALS_INIT_SEED, ALSTrainer
     W, R, dev = ctx.world_size, ctx.rank, ctx.device
     ph = upd.phase_seconds
     now = int(time.time() * 1000)
@@ -201,7 +201,7 @@ def build(upd, ctx: dist.DistContext, lines, features: int, lam: float, alpha: f
     counts_i = [int(x) for x in (base[1:] - base[:-1]).cpu().tolist()]
     n_users, n_items = W * max(counts_u), W * max(counts_i)
     trainer = ALSTrainer(features, lam, alpha, upd.implicit, ctx=ctx, seed=rng.next_seed(),
-                         precision=upd.precision)
+                         precision=upd.precision, init_seed=ALS_INIT_SEED)
     du = user_j[au] * W + R
     di = item_dense[ai]
     ph["ids_remap"] = ph.get("ids_remap", 0.0) + time.perf_counter() - tp
@@ -219,7 +219,9 @@ def build(upd, ctx: dist.DistContext, lines, features: int, lam: float, alpha: f
         x_init, y_init = _warm_start_sharded(upd.current_model_dir, features, x_keys, y_keys,
                                              n_users, n_items, W, R)
     tp = time.perf_counter()
-    trainer.train(upd.iterations, x_init=x_init, y_init=y_init)
+    # random rows keyed by ID: the same start as a one-rank generation of the same data
+    trainer.train(upd.iterations, x_init=x_init, y_init=y_init,
+                  x_keys=ingest.blob_hash64(*x_keys), y_keys=ingest.blob_hash64(*y_keys))
     _sync(dev)
     ph["train"] = ph.get("train", 0.0) + time.perf_counter() - tp
     tp = time.perf_counter()

@@ -46,6 +46,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
+import numpy as np
 import torch
 
 from ...ops import als as als_ops
@@ -131,6 +132,55 @@ class RowLayout:
         return out
 
 
+# the batch layer's keyed init seed: fixed, as MLlib's ALS default seed is (a per-class
+# constant), so a generation's factors do not depend on RNG call order or the world size
+ALS_INIT_SEED = 0x0A15_5EED
+
+
+def _u64_to_i64(c: int) -> int:
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+_GOLD = _u64_to_i64(0x9E3779B97F4A7C15)
+_MIX1 = _u64_to_i64(0xBF58476D1CE4E5B9)
+_MIX2 = _u64_to_i64(0x94D049BB133111EB)
+
+
+def _lsr(z: torch.Tensor, s: int) -> torch.Tensor:
+    return (z >> s) & ((1 << (64 - s)) - 1)
+
+
+def _mix64(z: torch.Tensor) -> torch.Tensor:
+    """splitmix64 finalizer on int64 tensors (two's-complement wrapping arithmetic)."""
+    z = z + _GOLD
+    z = (z ^ _lsr(z, 30)) * _MIX1
+    z = (z ^ _lsr(z, 27)) * _MIX2
+    return z ^ _lsr(z, 31)
+
+
+def keyed_unit_gaussian(keys: np.ndarray, k: int, kp: int, seed: int, device) -> torch.Tensor:
+    """Unit-norm Gaussian rows [n, kp] (features past k zero) where row j depends only on
+    (seed, keys[j]) -- a 64-bit hash of the row's ID -- and not on which rank holds the row or
+    in which order: the same ID starts from the same vector at any world size (MLlib's ALS
+    seeds its random init with a fixed default, ALSUpdate.java:116-124).  Box-Muller on two
+    splitmix64 streams per (key, feature), computed on ``device``."""
+    n = len(keys)
+    out = torch.zeros((n, kp), dtype=torch.float32, device=device)
+    if n == 0:
+        return out
+    h = torch.from_numpy(np.ascontiguousarray(keys, dtype=np.uint64).view(np.int64)).to(device)
+    sd = _u64_to_i64((int(seed) * 0x2545F4914F6CDD1D) & ((1 << 64) - 1))
+    f = torch.arange(k, dtype=torch.int64, device=device) * _GOLD
+    z1 = _mix64(_mix64(h[:, None] ^ sd) ^ f)
+    z2 = _mix64(z1 ^ _MIX2)
+    u1 = (_lsr(z1, 11).double() + 0.5) * 2.0 ** -53
+    u2 = _lsr(z2, 11).double() * 2.0 ** -53
+    g = torch.sqrt(-2.0 * torch.log(u1)) * torch.cos(2.0 * np.pi * u2)
+    g = g / g.norm(dim=1, keepdim=True).clamp_min(1e-12)
+    out[:, :k] = g.to(torch.float32)
+    return out
+
+
 def _unit_gaussian(n: int, k: int, kp: int, gen: torch.Generator, device) -> torch.Tensor:
     v = torch.randn((n, k), generator=gen, dtype=torch.float32, device="cpu")
     v = v / v.norm(dim=1, keepdim=True).clamp_min(1e-12)
@@ -142,7 +192,8 @@ def _unit_gaussian(n: int, k: int, kp: int, gen: torch.Generator, device) -> tor
 class ALSTrainer:
     def __init__(self, features: int, lam: float, alpha: float, implicit: bool,
                  ctx: Optional[dist.DistContext] = None, seed: int = 0,
-                 gather_chunks: Optional[int] = None, precision: str = "bf16"):
+                 gather_chunks: Optional[int] = None, precision: str = "bf16",
+                 init_seed: Optional[int] = None):
         if precision not in ("bf16", "fp32"):
             raise ValueError("precision must be bf16 or fp32, not %r" % (precision,))
         self.precision = precision
@@ -155,6 +206,8 @@ class ALSTrainer:
         self.ctx = ctx or dist.get_context()
         self.device = self.ctx.device
         self.seed = int(seed)
+        # keyed random init (init_factors with ID hashes): a fixed seed, as MLlib's default
+        self.init_seed = int(init_seed) if init_seed is not None else self.seed
         self.timings: Dict[str, float] = {}
         self.fail_count = None
         self.events: Optional[list] = None
@@ -289,9 +342,14 @@ class ALSTrainer:
 
     # ------------------------------------------------------------------ factors
     def init_factors(self, x_init: Optional[torch.Tensor] = None,
-                     y_init: Optional[torch.Tensor] = None) -> None:
+                     y_init: Optional[torch.Tensor] = None,
+                     x_keys: Optional[np.ndarray] = None,
+                     y_keys: Optional[np.ndarray] = None) -> None:
         """Random unit-norm Gaussian rows (MLlib's init), or warm-start from given factors
-        (full [n, k] matrices; rows containing NaN are initialised at random)."""
+        (full [n, k] matrices; rows containing NaN are initialised at random).  With
+        ``x_keys`` / ``y_keys`` (uint64 ID hashes of this rank's local rows, in local row
+        order) the random rows are keyed by ID (:func:`keyed_unit_gaussian`, seed
+        ``init_seed``): independent of the world size and of row placement."""
         ctx, dev, k, kp = self.ctx, self.device, self.k, self.kp
         gen = torch.Generator(device="cpu")
         gen.manual_seed((self.seed * 1000003 + ctx.rank) & ((1 << 62) - 1))
@@ -299,8 +357,15 @@ class ALSTrainer:
         # local shards padded to whole gather ranges (rows past the shard stay zero)
         self.X = torch.zeros((self.lay_u.local_rows, kp), dtype=torch.float32, device=dev)
         self.Y = torch.zeros((self.lay_i.local_rows, kp), dtype=torch.float32, device=dev)
-        self.X[:nu] = _unit_gaussian(nu, k, kp, gen, dev)
-        self.Y[:ni] = _unit_gaussian(ni, k, kp, gen, dev)
+        for keys, dst, n in ((x_keys, self.X, nu), (y_keys, self.Y, ni)):
+            if keys is not None:
+                keys = np.asarray(keys, dtype=np.uint64)
+                m = min(n, len(keys))
+                dst[:m] = keyed_unit_gaussian(keys[:m], k, kp, self.init_seed, dev)
+                if m < n:
+                    dst[m:n] = _unit_gaussian(n - m, k, kp, gen, dev)
+            else:
+                dst[:n] = _unit_gaussian(n, k, kp, gen, dev)
         for init, dst, lo, hi in ((x_init, self.X, self.u_lo, self.u_hi),
                                   (y_init, self.Y, self.i_lo, self.i_hi)):
             if init is None:
@@ -472,7 +537,9 @@ class ALSTrainer:
     def train(self, iterations: int, checkpoint_dir: Optional[str] = None,
               checkpoint_interval: int = 0, fingerprint: str = "",
               x_init: Optional[torch.Tensor] = None,
-              y_init: Optional[torch.Tensor] = None) -> ALSFactors:
+              y_init: Optional[torch.Tensor] = None,
+              x_keys: Optional[np.ndarray] = None,
+              y_keys: Optional[np.ndarray] = None) -> ALSFactors:
         """Initialise (or resume from ``checkpoint_dir``) and run ``iterations`` iterations,
         checkpointing every ``checkpoint_interval``; a completed run removes its checkpoint."""
         done = 0
@@ -481,7 +548,7 @@ class ALSTrainer:
             done = self.load_checkpoint(checkpoint_dir, fingerprint)
         self.resumed_from = done
         if done == 0:
-            self.init_factors(x_init, y_init)
+            self.init_factors(x_init, y_init, x_keys, y_keys)
         done = min(done, iterations)
         while done < iterations:
             step = iterations - done

@@ -138,6 +138,7 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_topn_prep", c_ll, [c_i, c_i, c_i, c_i, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                        c_vp, c_ll, c_vp, c_vp, c_vp, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_digest128", None, [c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_blob_hash64", None, [c_vp, c_vp, c_ll, ctypes.c_ulonglong, c_vp])
     _sig(lib, "oryx_http_start", c_vp, [c_cp, c_i, c_i, c_ll])
     _sig(lib, "oryx_http_port", c_i, [c_vp])
     _sig(lib, "oryx_http_served", c_ll, [c_vp])
