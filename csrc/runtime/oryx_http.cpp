@@ -692,7 +692,9 @@ long long oryx_http_next(void* h, char* out, long long cap, int timeout_ms) {
       S->qcv.notify_one();     // the next poller (or a taker of further ready requests)
       continue;
     }
-    S->qcv.wait_until(l, deadline);
+    // timed waits on the system clock (pthread_cond_timedwait): the steady-clock form maps to
+    // pthread_cond_clockwait, which ThreadSanitizer's runtime does not intercept
+    S->qcv.wait_until(l, std::chrono::system_clock::now() + (deadline - now));
   }
   const Req& r = S->ready.front();
   const long long need = 28 + (long long)(r.method.size() + r.target.size() + r.headers.size() +
@@ -748,7 +750,8 @@ void oryx_http_stop(void* h) {
   {
     std::unique_lock<std::mutex> l(S->qmu);
     S->qcv.notify_all();
-    S->qcv.wait_for(l, std::chrono::seconds(5), [&] { return !S->leader; });
+    S->qcv.wait_until(l, std::chrono::system_clock::now() + std::chrono::seconds(5),
+                      [&] { return !S->leader; });
   }
   std::lock_guard<std::mutex> g(S->cmu);
   for (auto& kv : S->conns) {

@@ -1,0 +1,505 @@
+// runtime_stress2.cpp -- the round-4 native concurrency code under sanitizer builds
+// (SURVEY.md section 5.2), alongside runtime_stress.cpp:
+//
+//   1. oryx_log_append_fill: writer threads on two topic handles whose fill callbacks format
+//      the values straight into the mapped segment (the speed layer's hot path; fill runs on
+//      the native pool for large appends), small segments so that appends roll; at the same
+//      time a frame reader (oryx_reader_poll_frames) and a text reader (oryx_reader_read_text)
+//      tail the partition across the rolls and check every record's content and order;
+//   2. the native HTTP front end (oryx_http.cpp) with four handler threads (leader /
+//      followers) and concurrent clients: keep-alive request loops, pipelined bursts, chunked
+//      bodies sent in small pieces, 413 (oversized Content-Length and chunk size) and 431
+//      (header flood), 400 (bad chunk size), and clients that close abruptly mid-request or
+//      before reading their responses;
+//   3. oryx_topn_prep from several threads at once on shared inputs (LSH bitmaps, exclusions);
+//   4. the persistent ThreadPool (parallel_ranges) entered from several threads at once
+//      (oryx_blob_hash64 and oryx_digest128 split their work over it).
+//
+// Exit status 0 = no check failed.
+
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+extern "C" {
+void* oryx_log_open(const char*, const char*, int, long long, long long);
+void oryx_log_close(void*);
+const char* oryx_log_last_error();
+typedef void (*FillFn)(void* ctx, long long j, char* dst);
+long long oryx_log_append_fill(void* h, int partition, const char* key, int key_len,
+                               const long long* lens, int n, FillFn fill, void* ctx,
+                               long long ts_ms, int do_fsync);
+void* oryx_reader_open(void*, int, long long);
+void oryx_reader_close(void*);
+long long oryx_reader_poll_frames(void* rh, char* out, long long out_cap, int max_records,
+                                  long long* out_used);
+long long oryx_reader_read_text(void* rh, long long end_offset, char* out, long long out_cap,
+                                long long* out_used, int* flags);
+void* oryx_http_start(const char* host, int port, int backlog, long long max_body);
+int oryx_http_port(void* h);
+long long oryx_http_next(void* h, char* out, long long cap, int timeout_ms);
+int oryx_http_respond(void* h, unsigned long long id, const char* data, long long len,
+                      int close_after);
+void oryx_http_stop(void* h);
+void oryx_http_free(void* h);
+long long oryx_topn_prep(int nq, int k, int kp, int max_batch, const float* targets,
+                         const long long* cand_ptr, const long long* cand,
+                         const unsigned char* cand_all, int num_buckets, int words,
+                         const long long* bucket_start, long long n_rows, const long long* ex_ptr,
+                         const long long* ex_rows, const long long* pos_of_row, long long n_pos,
+                         unsigned char* out, long long out_cap, long long* info);
+void oryx_blob_hash64(const unsigned char* blob, const long long* ends, long long n,
+                      unsigned long long seed, unsigned long long* out);
+void oryx_digest128(const unsigned char* p, long long n, unsigned long long* out);
+}
+
+static std::atomic<int> g_errors{0};
+
+#define CHECK(c)                                                       \
+  do {                                                                 \
+    if (!(c)) {                                                        \
+      fprintf(stderr, "check failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      ++g_errors;                                                      \
+    }                                                                  \
+  } while (0)
+
+// ---------------------------------------------------------------- 1. append_fill + readers
+
+struct FillCtx {
+  int writer, batch;
+};
+
+static std::string value_of(int w, int b, long long j) {
+  char buf[64];
+  const int n = snprintf(buf, sizeof(buf), "[\"X\",\"w%d-b%d-%lld\",%lld]", w, b, j, j * 7);
+  std::string s(buf, (size_t)n);
+  s.append((size_t)(j % 37), 'z');
+  return s;
+}
+
+static void fill_fn(void* ctx, long long j, char* dst) {
+  const auto* c = static_cast<const FillCtx*>(ctx);
+  const std::string v = value_of(c->writer, c->batch, j);
+  memcpy(dst, v.data(), v.size());
+}
+
+static void test_append_fill(const char* root) {
+  const int writers = 2, batches = 6, n = 3000;
+  const long long total = (long long)writers * batches * n;
+  void* t1 = oryx_log_open(root, "Fill", 1, 1 << 20, 256 << 10);   // 256 KB segments: rolls
+  void* t2 = oryx_log_open(root, "Fill", 1, 1 << 20, 256 << 10);
+  CHECK(t1 && t2);
+  if (!t1 || !t2) return;
+  std::atomic<bool> done{false};
+  std::vector<std::thread> th;
+  for (int w = 0; w < writers; ++w) {
+    th.emplace_back([&, w] {
+      for (int b = 0; b < batches; ++b) {
+        std::vector<long long> lens((size_t)n);
+        for (long long j = 0; j < n; ++j) lens[(size_t)j] = (long long)value_of(w, b, j).size();
+        FillCtx c{w, b};
+        CHECK(oryx_log_append_fill(w ? t2 : t1, 0, "UP", 2, lens.data(), n, fill_fn, &c, -1,
+                                   0) >= 0);
+      }
+    });
+  }
+  // frame reader: every frame's value parses back to its (writer, batch, j) and, per writer,
+  // the batches arrive whole and in order
+  th.emplace_back([&] {
+    void* r = oryx_reader_open(t1, 0, 0);
+    std::vector<char> out(1 << 20);
+    long long got = 0, last_off = -1;
+    auto t_end = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+    while (got < total && std::chrono::steady_clock::now() < t_end) {
+      long long used = 0;
+      const long long n_fr = oryx_reader_poll_frames(r, out.data(), (long long)out.size(), 4096,
+                                                     &used);
+      CHECK(n_fr >= 0);
+      if (n_fr <= 0) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        continue;
+      }
+      long long pos = 0;
+      for (long long i = 0; i < n_fr; ++i) {
+        uint32_t kl, vl;
+        long long off;
+        memcpy(&off, out.data() + pos + 8, 8);
+        memcpy(&kl, out.data() + pos + 24, 4);
+        memcpy(&vl, out.data() + pos + 28, 4);
+        CHECK(off == last_off + 1);
+        last_off = off;
+        CHECK(kl == 2 && memcmp(out.data() + pos + 32, "UP", 2) == 0);
+        const char* v = out.data() + pos + 32 + kl;
+        int w = -1, b = -1;
+        long long j = -1;
+        CHECK(sscanf(v, "[\"X\",\"w%d-b%d-%lld\"", &w, &b, &j) == 3);
+        if (w >= 0 && b >= 0 && j >= 0) CHECK(value_of(w, b, j) == std::string(v, vl));
+        pos += 32 + kl + vl;
+      }
+      got += n_fr;
+    }
+    CHECK(got == total);
+    oryx_reader_close(r);
+  });
+  // text reader: the same records as text lines, up to whatever end offset it sees
+  th.emplace_back([&] {
+    void* r = oryx_reader_open(t2, 0, 0);
+    std::vector<char> out(1 << 20);
+    long long got = 0;
+    auto t_end = std::chrono::steady_clock::now() + std::chrono::seconds(120);
+    while (got < total && std::chrono::steady_clock::now() < t_end) {
+      long long used = 0;
+      int flags = 0;
+      const long long n_rec = oryx_reader_read_text(r, got + 2000, out.data(),
+                                                    (long long)out.size(), &used, &flags);
+      CHECK(n_rec >= 0);
+      if (n_rec <= 0) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        continue;
+      }
+      long long lines = 0;
+      for (long long p = 0; p < used; ++p) lines += out[(size_t)p] == '\n';
+      CHECK(lines == n_rec);
+      got += n_rec;
+    }
+    CHECK(got == total);
+    oryx_reader_close(r);
+  });
+  for (auto& x : th) x.join();
+  done = true;
+  oryx_log_close(t1);
+  oryx_log_close(t2);
+}
+
+// ---------------------------------------------------------------- 2. HTTP front end
+
+static int connect_to(int port) {
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)port);
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  if (connect(fd, (sockaddr*)&a, sizeof(a)) != 0) {
+    close(fd);
+    return -1;
+  }
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+  timeval tv{10, 0};
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  return fd;
+}
+
+static bool send_all(int fd, const std::string& s) {
+  size_t o = 0;
+  while (o < s.size()) {
+    const ssize_t w = send(fd, s.data() + o, s.size() - o, MSG_NOSIGNAL);
+    if (w <= 0) return false;
+    o += (size_t)w;
+  }
+  return true;
+}
+
+// n responses: status codes and bodies
+static bool read_responses(int fd, int n, std::vector<int>& st, std::vector<std::string>& bodies) {
+  std::string buf;
+  char tmp[65536];
+  while ((int)st.size() < n) {
+    size_t he;
+    while ((he = buf.find("\r\n\r\n")) == std::string::npos) {
+      const ssize_t r = recv(fd, tmp, sizeof(tmp), 0);
+      if (r <= 0) return false;
+      buf.append(tmp, (size_t)r);
+    }
+    const int code = atoi(buf.c_str() + 9);
+    size_t cl = 0;
+    const size_t p = buf.find("Content-Length: ");
+    if (p != std::string::npos && p < he) cl = (size_t)atoll(buf.c_str() + p + 16);
+    while (buf.size() < he + 4 + cl) {
+      const ssize_t r = recv(fd, tmp, sizeof(tmp), 0);
+      if (r <= 0) return false;
+      buf.append(tmp, (size_t)r);
+    }
+    st.push_back(code);
+    bodies.push_back(buf.substr(he + 4, cl));
+    buf.erase(0, he + 4 + cl);
+  }
+  return true;
+}
+
+static void test_http() {
+  void* S = oryx_http_start("127.0.0.1", 0, 256, 1 << 20);
+  CHECK(S != nullptr);
+  if (!S) return;
+  const int port = oryx_http_port(S);
+  std::atomic<bool> stop{false};
+  std::vector<std::thread> handlers;
+  for (int h = 0; h < 4; ++h) {
+    handlers.emplace_back([&] {
+      std::vector<char> buf(1 << 16);
+      while (!stop) {
+        long long n = oryx_http_next(S, buf.data(), (long long)buf.size(), 50);
+        if (n == -1) return;
+        if (n == 0) continue;
+        if (n < 0) {
+          buf.resize((size_t)-n);
+          continue;
+        }
+        uint64_t id;
+        uint32_t ml, tl, hl;
+        uint64_t bl;
+        memcpy(&id, buf.data(), 8);
+        memcpy(&ml, buf.data() + 8, 4);
+        memcpy(&tl, buf.data() + 12, 4);
+        memcpy(&hl, buf.data() + 16, 4);
+        memcpy(&bl, buf.data() + 20, 8);
+        const std::string target(buf.data() + 28 + ml, tl);
+        const std::string body(buf.data() + 28 + ml + tl + hl, bl);
+        const std::string payload = target + "|" + std::to_string(bl) + "|" +
+                                    (body.size() > 64 ? body.substr(0, 64) : body);
+        const std::string resp = "HTTP/1.1 200 OK\r\nContent-Length: " +
+                                 std::to_string(payload.size()) + "\r\n\r\n" + payload;
+        oryx_http_respond(S, id, resp.data(), (long long)resp.size(), 0);
+      }
+    });
+  }
+  std::vector<std::thread> clients;
+  // keep-alive loops with pipelined bursts
+  for (int c = 0; c < 6; ++c) {
+    clients.emplace_back([&, c] {
+      const int fd = connect_to(port);
+      CHECK(fd >= 0);
+      if (fd < 0) return;
+      for (int rep = 0; rep < 20; ++rep) {
+        std::string burst;
+        for (int j = 0; j < 5; ++j)
+          burst += "GET /c" + std::to_string(c) + "/" + std::to_string(rep * 5 + j) +
+                   " HTTP/1.1\r\nHost: x\r\n\r\n";
+        CHECK(send_all(fd, burst));
+        std::vector<int> st;
+        std::vector<std::string> b;
+        CHECK(read_responses(fd, 5, st, b));
+        for (int j = 0; j < (int)b.size(); ++j)
+          CHECK(b[(size_t)j].rfind("/c" + std::to_string(c) + "/" +
+                                   std::to_string(rep * 5 + j) + "|", 0) == 0);
+      }
+      close(fd);
+    });
+  }
+  // chunked bodies in small pieces
+  for (int c = 0; c < 3; ++c) {
+    clients.emplace_back([&, c] {
+      const int fd = connect_to(port);
+      CHECK(fd >= 0);
+      if (fd < 0) return;
+      for (int rep = 0; rep < 4; ++rep) {
+        std::string req = "POST /chunk HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n";
+        std::string want;
+        for (int k = 0; k < 300; ++k) {
+          const std::string piece(1 + (k + c) % 13, (char)('a' + k % 26));
+          char hx[16];
+          snprintf(hx, sizeof(hx), "%zx\r\n", piece.size());
+          req += hx + piece + "\r\n";
+          want += piece;
+        }
+        req += "0\r\n\r\n";
+        for (size_t o = 0; o < req.size(); o += 41) CHECK(send_all(fd, req.substr(o, 41)));
+        std::vector<int> st;
+        std::vector<std::string> b;
+        CHECK(read_responses(fd, 1, st, b));
+        if (!b.empty())
+          CHECK(b[0] == "/chunk|" + std::to_string(want.size()) + "|" + want.substr(0, 64));
+      }
+      close(fd);
+    });
+  }
+  // errors: 413 (Content-Length, chunk size), 431 (header flood), 400 (bad chunk size)
+  clients.emplace_back([&] {
+    const char* reqs[] = {
+        "POST /x HTTP/1.1\r\nContent-Length: 99999999\r\n\r\n",
+        "POST /x HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n1\r\na\r\nfffffffffffffff\r\n",
+        "POST /x HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n"};
+    const int want[] = {413, 413, 400};
+    for (int k = 0; k < 3; ++k) {
+      const int fd = connect_to(port);
+      CHECK(fd >= 0);
+      if (fd < 0) continue;
+      CHECK(send_all(fd, reqs[k]));
+      std::vector<int> st;
+      std::vector<std::string> b;
+      CHECK(read_responses(fd, 1, st, b));
+      if (!st.empty()) CHECK(st[0] == want[k]);
+      close(fd);
+    }
+    const int fd = connect_to(port);
+    if (fd >= 0) {
+      std::string flood = "GET /x HTTP/1.1\r\n";
+      while (flood.size() < 70000) flood += "X-Pad: aaaaaaaaaaaaaaaaaaaaaaaaaaaaaaaa\r\n";
+      send_all(fd, flood);
+      std::vector<int> st;
+      std::vector<std::string> b;
+      CHECK(read_responses(fd, 1, st, b));
+      if (!st.empty()) CHECK(st[0] == 431);
+      close(fd);
+    }
+  });
+  // abrupt closes: mid-headers, mid-body, and after sending without reading the answers
+  for (int c = 0; c < 4; ++c) {
+    clients.emplace_back([&, c] {
+      for (int rep = 0; rep < 25; ++rep) {
+        const int fd = connect_to(port);
+        if (fd < 0) continue;
+        if (c == 0) send_all(fd, "GET /half HTTP/1.1\r\nHo");
+        if (c == 1) send_all(fd, "POST /b HTTP/1.1\r\nContent-Length: 100\r\n\r\nabc");
+        if (c == 2)
+          send_all(fd, "GET /a HTTP/1.1\r\n\r\nGET /b HTTP/1.1\r\n\r\nGET /c HTTP/1.1\r\n\r\n");
+        if (c == 3) {
+          linger lg{1, 0};   // RST on close
+          setsockopt(fd, SOL_SOCKET, SO_LINGER, &lg, sizeof(lg));
+          send_all(fd, "GET /rst HTTP/1.1\r\n\r\n");
+        }
+        close(fd);
+      }
+    });
+  }
+  for (auto& x : clients) x.join();
+  // the server still answers after all that
+  {
+    const int fd = connect_to(port);
+    CHECK(fd >= 0);
+    if (fd >= 0) {
+      CHECK(send_all(fd, "GET /final HTTP/1.1\r\n\r\n"));
+      std::vector<int> st;
+      std::vector<std::string> b;
+      CHECK(read_responses(fd, 1, st, b));
+      if (!b.empty()) CHECK(b[0].rfind("/final|", 0) == 0);
+      close(fd);
+    }
+  }
+  stop = true;
+  oryx_http_stop(S);
+  for (auto& x : handlers) x.join();
+  oryx_http_free(S);
+}
+
+// ---------------------------------------------------------------- 3. top-N prep
+
+static void test_topn_prep() {
+  const int nq = 8, k = 50, kp = 64, nb = 70, words = (nb + 31) / 32;
+  const long long n_rows = 5000;
+  std::vector<float> targets((size_t)nq * k);
+  for (size_t i = 0; i < targets.size(); ++i) targets[i] = (float)(i % 17) * 0.25f;
+  std::vector<long long> bstart(nb + 1);
+  for (int b = 0; b <= nb; ++b) bstart[(size_t)b] = n_rows * b / nb;
+  std::vector<long long> cand_ptr(nq + 1, 0), cand;
+  std::vector<unsigned char> cand_all(nq, 0);
+  for (int j = 0; j < nq; ++j) {
+    for (int b = j; b < nb; b += 3 + j) cand.push_back(b);
+    cand.push_back(-5);          // ignored
+    cand.push_back(nb + 9);      // ignored
+    cand_ptr[(size_t)j + 1] = (long long)cand.size();
+  }
+  cand_all[5] = 1;
+  std::vector<long long> ex_ptr(nq + 1, 0), ex_rows, pos_of_row((size_t)n_rows);
+  for (long long r = 0; r < n_rows; ++r) pos_of_row[(size_t)r] = (r * 7919) % n_rows;
+  for (int j = 0; j < nq; ++j) {
+    for (int e = 0; e < 40; ++e) ex_rows.push_back((j * 131 + e * 977) % (n_rows + 50) - 10);
+    ex_ptr[(size_t)j + 1] = (long long)ex_rows.size();
+  }
+  auto run = [&](std::vector<unsigned char>& out, std::vector<long long>& info) {
+    out.assign(1 << 20, 0);
+    info.assign(9, 0);
+    return oryx_topn_prep(nq, k, kp, 16, targets.data(), cand_ptr.data(), cand.data(),
+                          cand_all.data(), nb, words, bstart.data(), n_rows, ex_ptr.data(),
+                          ex_rows.data(), pos_of_row.data(), n_rows, out.data(),
+                          (long long)out.size(), info.data());
+  };
+  std::vector<unsigned char> ref;
+  std::vector<long long> ref_info;
+  CHECK(run(ref, ref_info) == 0);
+  {
+    std::vector<unsigned char> small(64);
+    std::vector<long long> info(9);
+    CHECK(oryx_topn_prep(nq, k, kp, 16, targets.data(), cand_ptr.data(), cand.data(),
+                         cand_all.data(), nb, words, bstart.data(), n_rows, ex_ptr.data(),
+                         ex_rows.data(), pos_of_row.data(), n_rows, small.data(),
+                         (long long)small.size(), info.data()) == -1);
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < 6; ++t) {
+    th.emplace_back([&] {
+      for (int rep = 0; rep < 50; ++rep) {
+        std::vector<unsigned char> out;
+        std::vector<long long> info;
+        CHECK(run(out, info) == 0);
+        CHECK(info == ref_info);
+        CHECK(memcmp(out.data(), ref.data(), (size_t)ref_info[7]) == 0);
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
+// ---------------------------------------------------------------- 4. thread pool
+
+static void test_pool() {
+  std::string blob;
+  std::vector<long long> ends;
+  for (int i = 0; i < 200000; ++i) {
+    blob += "user-" + std::to_string(i * 31);
+    ends.push_back((long long)blob.size());
+  }
+  std::vector<unsigned long long> ref(ends.size());
+  oryx_blob_hash64((const unsigned char*)blob.data(), ends.data(), (long long)ends.size(), 9,
+                   ref.data());
+  std::vector<unsigned char> big(64 << 20);
+  for (size_t i = 0; i < big.size(); ++i) big[i] = (unsigned char)(i * 2654435761u >> 13);
+  unsigned long long dref[2];
+  oryx_digest128(big.data(), (long long)big.size(), dref);
+  std::vector<std::thread> th;
+  for (int t = 0; t < 6; ++t) {
+    th.emplace_back([&, t] {
+      for (int rep = 0; rep < 8; ++rep) {
+        if ((t + rep) & 1) {
+          std::vector<unsigned long long> h(ends.size());
+          oryx_blob_hash64((const unsigned char*)blob.data(), ends.data(),
+                           (long long)ends.size(), 9, h.data());
+          CHECK(h == ref);
+        } else {
+          unsigned long long d[2];
+          oryx_digest128(big.data(), (long long)big.size(), d);
+          CHECK(d[0] == dref[0] && d[1] == dref[1]);
+        }
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    fprintf(stderr, "usage: runtime_stress2 <dir>\n");
+    return 2;
+  }
+  test_append_fill(argv[1]);
+  printf("append_fill + frame / text readers: errors %d\n", g_errors.load());
+  test_http();
+  printf("http: errors %d\n", g_errors.load());
+  test_topn_prep();
+  printf("topn_prep: errors %d\n", g_errors.load());
+  test_pool();
+  printf("thread pool: errors %d\n", g_errors.load());
+  return g_errors.load() == 0 ? 0 : 1;
+}

@@ -1,16 +1,30 @@
 #!/bin/bash
-# Builds the native host runtime (log, offsets, ingest) with the stress driver under
-# AddressSanitizer + UndefinedBehaviorSanitizer and under ThreadSanitizer, and runs both
-# (host code only: GPU sanitizers are not available on the MI355X pool).
+# Builds the native host runtime (log, offsets, ingest, HTTP front end) with the two stress
+# drivers under AddressSanitizer + UndefinedBehaviorSanitizer and under ThreadSanitizer, and
+# runs them (host code only: GPU sanitizers are not available on the MI355X pool).
+#   runtime_stress.cpp:  producers / partition readers / offsets / ingest parser
+#   runtime_stress2.cpp: append_fill writers + frame and text readers across segment rolls,
+#                        the HTTP server under concurrent, pipelined, chunked and abusive
+#                        clients, oryx_topn_prep from several threads, the native thread pool
 set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${1:-/tmp/oryx_sanitize}
 mkdir -p "$OUT"
-SRCS="csrc/runtime/oryx_log.cpp csrc/runtime/oryx_ingest.cpp csrc/runtime/tests/runtime_stress.cpp"
-g++ -std=c++17 -O1 -g -fno-omit-frame-pointer -pthread -fsanitize=address,undefined \
-    -fno-sanitize-recover=undefined -o "$OUT/stress_asan" $SRCS -lz
-g++ -std=c++17 -O1 -g -pthread -fsanitize=thread -o "$OUT/stress_tsan" $SRCS -lz
-rm -rf "$OUT/log_asan" "$OUT/log_tsan"
-ASAN_OPTIONS=detect_leaks=1:halt_on_error=1 "$OUT/stress_asan" "$OUT/log_asan"
-TSAN_OPTIONS=halt_on_error=1 "$OUT/stress_tsan" "$OUT/log_tsan"
+RT="csrc/runtime/oryx_log.cpp csrc/runtime/oryx_ingest.cpp csrc/runtime/oryx_http.cpp"
+LIBS="-lz -lssl -lcrypto"
+ASAN="-std=c++17 -O1 -g -fno-omit-frame-pointer -pthread -fsanitize=address,undefined -fno-sanitize-recover=undefined"
+TSAN="-std=c++17 -O1 -g -pthread -fsanitize=thread"
+for prog in runtime_stress runtime_stress2; do
+  g++ $ASAN -o "$OUT/${prog}_asan" $RT csrc/runtime/tests/$prog.cpp $LIBS &
+  g++ $TSAN -o "$OUT/${prog}_tsan" $RT csrc/runtime/tests/$prog.cpp $LIBS &
+done
+wait
+for prog in runtime_stress runtime_stress2; do
+  rm -rf "$OUT/${prog}_log_asan" "$OUT/${prog}_log_tsan"
+  mkdir -p "$OUT/${prog}_log_asan" "$OUT/${prog}_log_tsan"
+  echo "== $prog (ASan + UBSan)"
+  ASAN_OPTIONS=detect_leaks=1:halt_on_error=1 "$OUT/${prog}_asan" "$OUT/${prog}_log_asan"
+  echo "== $prog (TSan)"
+  TSAN_OPTIONS=halt_on_error=1:second_deadlock_stack=1 "$OUT/${prog}_tsan" "$OUT/${prog}_log_tsan"
+done
 echo "sanitizers clean"
