@@ -3185,14 +3185,18 @@ long long oryx_format_leaf_updates(long long n, const long long* trees, const ch
 // [nr + 1] i64 (16-row tile prefix), then with LSH per-query bucket bitmaps [nq][words] u32
 // (bit b of word b / 32), then with exclusions ptr [nq + 1] i32 and the sorted excluded
 // positions ex [max(1, total)] i32.  cand_ptr == nullptr: no LSH; cand_all[j] = 1: query j
-// scans every bucket.  ex_ptr == nullptr: no exclusions.  info: n_ranges, n_tiles, and the
-// byte offsets of ranges, tile0, bits, ptr, ex (-1 when absent), then the bytes used.
-// Returns 0, 1 when no range is left to scan, -1 when `out` is too small.
+// scans every bucket.  ex_ptr == nullptr: no exclusions.  [delta_lo, delta_hi): the index's
+// unsorted delta segment of positions (rows added or moved since its last sort), scanned by
+// every query after the bucket ranges (the kernel's bucket mask still filters its rows).
+// info: n_ranges, n_tiles, and the byte offsets of ranges, tile0, bits, ptr, ex (-1 when
+// absent), then the bytes used.  Returns 0, 1 when no range is left to scan, -1 when `out` is
+// too small.
 long long oryx_topn_prep(int nq, int k, int kp, int max_batch, const float* targets,
                          const long long* cand_ptr, const long long* cand,
                          const unsigned char* cand_all, int num_buckets, int words,
                          const long long* bucket_start, long long n_rows, const long long* ex_ptr,
                          const long long* ex_rows, const long long* pos_of_row, long long n_pos,
+                         long long delta_lo, long long delta_hi,
                          unsigned char* out, long long out_cap, long long* info) {
   auto al = [](long long v) { return (v + 15) & ~15LL; };
   std::vector<std::pair<long long, long long>> rs;
@@ -3221,10 +3225,14 @@ long long oryx_topn_prep(int nq, int k, int kp, int max_batch, const float* targ
       if (!rs.empty() && rs.back().second == s0) rs.back().second = e0;
       else rs.emplace_back(s0, e0);
     }
-    if (rs.empty()) return 1;
-  } else {
+  } else if (n_rows > 0) {
     rs.emplace_back(0, n_rows);
   }
+  if (delta_hi > delta_lo) {
+    if (!rs.empty() && rs.back().second == delta_lo) rs.back().second = delta_hi;
+    else rs.emplace_back(delta_lo, delta_hi);
+  }
+  if (rs.empty()) return 1;
   const long long nr = (long long)rs.size();
   // excluded rows -> sorted positions per query
   std::vector<int32_t> ptr, ex;

@@ -59,6 +59,7 @@ long long oryx_topn_prep(int nq, int k, int kp, int max_batch, const float* targ
                          const unsigned char* cand_all, int num_buckets, int words,
                          const long long* bucket_start, long long n_rows, const long long* ex_ptr,
                          const long long* ex_rows, const long long* pos_of_row, long long n_pos,
+                         long long delta_lo, long long delta_hi,
                          unsigned char* out, long long out_cap, long long* info);
 void oryx_blob_hash64(const unsigned char* blob, const long long* ends, long long n,
                       unsigned long long seed, unsigned long long* out);
@@ -423,8 +424,8 @@ static void test_topn_prep() {
     info.assign(9, 0);
     return oryx_topn_prep(nq, k, kp, 16, targets.data(), cand_ptr.data(), cand.data(),
                           cand_all.data(), nb, words, bstart.data(), n_rows, ex_ptr.data(),
-                          ex_rows.data(), pos_of_row.data(), n_rows, out.data(),
-                          (long long)out.size(), info.data());
+                          ex_rows.data(), pos_of_row.data(), n_rows, n_rows - 300, n_rows,
+                          out.data(), (long long)out.size(), info.data());
   };
   std::vector<unsigned char> ref;
   std::vector<long long> ref_info;
@@ -434,7 +435,7 @@ static void test_topn_prep() {
     std::vector<long long> info(9);
     CHECK(oryx_topn_prep(nq, k, kp, 16, targets.data(), cand_ptr.data(), cand.data(),
                          cand_all.data(), nb, words, bstart.data(), n_rows, ex_ptr.data(),
-                         ex_rows.data(), pos_of_row.data(), n_rows, small.data(),
+                         ex_rows.data(), pos_of_row.data(), n_rows, 0, 0, small.data(),
                          (long long)small.size(), info.data()) == -1);
   }
   std::vector<std::thread> th;

@@ -134,9 +134,11 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_format_cluster_updates", c_ll, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_ll,
                                                     c_vp])
     # nq, k, kp, max_batch, targets, cand_ptr, cand, cand_all, num_buckets, words,
-    # bucket_start, n_rows, ex_ptr, ex_rows, pos_of_row, n_pos, out, out_cap, info
+    # bucket_start, n_rows, ex_ptr, ex_rows, pos_of_row, n_pos, delta_lo, delta_hi, out,
+    # out_cap, info
     _sig(lib, "oryx_topn_prep", c_ll, [c_i, c_i, c_i, c_i, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
-                                       c_vp, c_ll, c_vp, c_vp, c_vp, c_ll, c_vp, c_ll, c_vp])
+                                       c_vp, c_ll, c_vp, c_vp, c_vp, c_ll, c_ll, c_ll, c_vp,
+                                       c_ll, c_vp])
     _sig(lib, "oryx_digest128", None, [c_vp, c_ll, c_vp])
     _sig(lib, "oryx_blob_hash64", None, [c_vp, c_vp, c_ll, ctypes.c_ulonglong, c_vp])
     _sig(lib, "oryx_http_start", c_vp, [c_cp, c_i, c_i, c_ll])

@@ -122,7 +122,10 @@ class ItemIndex:
         self.device = torch.device(device) if device is not None else store.device
         self.shard = (int(shard[0]), int(shard[1]))
         self.num_buckets = max(1, int(num_buckets))
-        self.words = (self.num_buckets + 31) // 32
+        # bucket id num_buckets marks a dead position (a row that moved or left since the
+        # last sort): no query's bucket mask ever holds it
+        self.dead_bucket = self.num_buckets
+        self.words = (self.num_buckets + 1 + 31) // 32
         # borrowed: the kernel reads the store's device mirror in place (same GPU, rows kp
         # floats apart); otherwise this index keeps its own rows
         self.borrowed = (self.shard[1] == 1 and store.device is not None and
@@ -137,8 +140,16 @@ class ItemIndex:
         self.row_of_pos = None  # int64 [n] (device) and host copy
         self.row_of_pos_h = None
         self.bucket_start = None   # host int64 [num_buckets + 1]
+        # positions [0, n_main) are sorted by bucket; [n_main, n) is the delta segment: rows
+        # added or re-bucketed since that sort, appended as they come and scanned by every
+        # query (the kernel's bucket mask filters them); n_dead positions are dead
         self.n = 0
+        self.n_main = 0
+        self.n_dead = 0
+        self.cap = 0
         self.rebuilds = 0
+        self.incremental = 0       # refreshes absorbed without a re-sort
+        self.delta_added = 0       # rows appended to the delta segment, ever
         self._built = False
         # bf16 scan with exact fp32 re-rank of a certified candidate pool (_launch_bf16):
         # dot-product queries of <= BF16_MAX_HOW_MANY on the store's own GPU
@@ -180,6 +191,8 @@ class ItemIndex:
         return parts[rows].to(torch.int64)
 
     def _rebuild(self, mat, valid, parts) -> None:
+        """Re-sort every live row by bucket; room for a delta segment of max(64K, n / 16)
+        positions behind the sorted ones."""
         dev = self.device
         rows = torch.nonzero(valid, as_tuple=False).flatten()
         d, nsh = self.shard
@@ -190,12 +203,14 @@ class ItemIndex:
         rows = rows[order]
         b = b[order]
         n = int(rows.numel())
+        cap = n + max(1 << 16, n // 16)
         if self.borrowed:
-            self.perm = rows.to(torch.int32).contiguous() if n else \
-                torch.zeros(1, dtype=torch.int32, device=dev)
+            perm = torch.zeros(cap, dtype=torch.int32, device=dev)
+            perm[:n] = rows.to(torch.int32)
+            self.perm = perm
             self.Ys = None
         else:
-            ys = torch.zeros((max(n, 1), self.kp), dtype=torch.float32, device=dev)
+            ys = torch.zeros((cap, self.kp), dtype=torch.float32, device=dev)
             # gathered in slices of 1M rows: a whole-matrix mat[rows] temporary would add
             # another full copy of the item factors to the peak HBM of a rebuild
             step = 1 << 20
@@ -206,28 +221,50 @@ class ItemIndex:
             self.perm = None
         rows = rows.to(dev)
         b = b.to(dev)
-        self.bucket_of = b.to(torch.int32).contiguous()
+        bucket_of = torch.full((cap,), self.dead_bucket, dtype=torch.int32, device=dev)
+        bucket_of[:n] = b.to(torch.int32)
+        self.bucket_of = bucket_of
         pos = torch.full((mat.shape[0],), -1, dtype=torch.int64, device=dev)
         if n:
             pos[rows] = torch.arange(n, device=dev)
         self.pos_of_row = pos
         self.pos_of_row_h = pos.cpu().numpy()
-        self.row_of_pos = rows
-        self.row_of_pos_h = rows.cpu().numpy()
+        rop = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+        rop[:n] = rows
+        self.row_of_pos = rop
+        self.row_of_pos_h = rop.cpu().numpy()
         counts = torch.bincount(b, minlength=self.num_buckets).cpu().numpy()
         self.bucket_start = np.zeros(self.num_buckets + 1, dtype=np.int64)
-        np.cumsum(counts, out=self.bucket_start[1:])
-        self.n = n
+        np.cumsum(counts[:self.num_buckets], out=self.bucket_start[1:])
+        self.n = self.n_main = n
+        self.n_dead = 0
+        self.cap = cap
         self.rebuilds += 1
         self._built = True
 
+    def _grow_row_maps(self, rows: int) -> None:
+        """The store grew: extend the row -> position maps (device and host) to ``rows``."""
+        old = self.pos_of_row.numel()
+        if rows <= old:
+            return
+        rows = max(rows, old + old // 2)
+        pos = torch.full((rows,), -1, dtype=torch.int64, device=self.device)
+        pos[:old] = self.pos_of_row
+        self.pos_of_row = pos
+        ph = np.full(rows, -1, dtype=np.int64)
+        ph[:old] = self.pos_of_row_h
+        self.pos_of_row_h = ph
+
     def _update_in_place(self, mat, valid, parts, dirty: np.ndarray) -> bool:
-        """Changed rows that stay in their bucket: nothing to do when the kernel reads the
-        store's mirror (it is already current), a row copy otherwise.  New / removed rows and
-        bucket moves return False (re-sort)."""
+        """Absorb the changed rows without a re-sort (ALSServingModel.setItemVector moves one
+        item between LSH partitions, ALSServingModel.java:161-183): a row that stays in its
+        bucket needs nothing when the kernel reads the store's mirror (a row copy otherwise);
+        a row that left its bucket, or left the store, kills its position (bucket -> dead);
+        a new or moved row is appended to the delta segment.  Returns False when a re-sort is
+        due instead: many changes at once, the delta segment full, or many dead positions."""
         if len(dirty) == 0:
             return True
-        if len(dirty) > max(4096, self.n // 16):
+        if len(dirty) > max(4096, self.n_main // 16):
             return False
         dev = self.device
         d, nsh = self.shard
@@ -236,19 +273,48 @@ class ItemIndex:
             dirty = dirty[dirty % nsh == d]
             if len(dirty) == 0:
                 return True
+        self._grow_row_maps(int(mat.shape[0]))
         src = torch.from_numpy(dirty).to(mat.device)
         rows = src.to(dev)
-        if int(rows.max()) >= self.pos_of_row.numel():
-            return False
         pos = self.pos_of_row[rows]
         ok = valid[src].to(dev)
-        if bool(((pos < 0) | ~ok).any()):
-            return False
         nb = self._buckets(parts, src).to(dev)
-        if bool((nb != self.bucket_of[pos].to(torch.int64)).any()):
+        cur = torch.where(pos >= 0, self.bucket_of[pos.clamp(min=0)].to(torch.int64),
+                          torch.full_like(pos, -1))
+        stay = (pos >= 0) & ok & (nb == cur)
+        kill = (pos >= 0) & ~stay
+        add = ok & ~stay
+        n_kill, n_add = (int(v) for v in torch.stack([kill.sum(), add.sum()]).tolist())
+        if self.n + n_add > self.cap or \
+                self.n_dead + n_kill > max(1 << 14, self.n_main // 8):
             return False
-        if not self.borrowed:
-            self.Ys[pos, :self.k] = mat[src].to(dev)
+        if not self.borrowed and bool(stay.any()):
+            self.Ys[pos[stay], :self.k] = mat[src[stay.to(src.device)]].to(dev)
+        if n_kill:
+            kp_ = pos[kill]
+            self.bucket_of[kp_] = self.dead_bucket
+            self.row_of_pos[kp_] = -1
+            self.pos_of_row[rows[kill]] = -1
+            kh = kp_.cpu().numpy()
+            self.row_of_pos_h[kh] = -1
+            self.pos_of_row_h[rows[kill].cpu().numpy()] = -1
+            self.n_dead += n_kill
+        if n_add:
+            q = torch.arange(self.n, self.n + n_add, dtype=torch.int64, device=dev)
+            ra = rows[add]
+            if self.borrowed:
+                self.perm[q] = ra.to(torch.int32)
+            else:
+                self.Ys[q, :self.k] = mat[src[add.to(src.device)]].to(dev)
+            self.bucket_of[q] = nb[add].to(torch.int32)
+            self.row_of_pos[q] = ra
+            self.pos_of_row[ra] = q
+            rh = ra.cpu().numpy()
+            self.row_of_pos_h[self.n:self.n + n_add] = rh
+            self.pos_of_row_h[rh] = np.arange(self.n, self.n + n_add, dtype=np.int64)
+            self.n += n_add
+            self.delta_added += n_add
+        self.incremental += 1
         return True
 
     # ------------------------------------------------------------------ queries
@@ -457,6 +523,9 @@ class ItemIndex:
         keep = np.isfinite(vj) & (pj >= 0)
         rows = (self.row_of_pos_h if row_of_pos is None else row_of_pos)[pj[keep]]
         vj = np.asarray(vj[keep], dtype=np.float32)
+        if len(rows) and bool((rows < 0).any()):       # killed after the launch
+            live = rows >= 0
+            rows, vj = rows[live], vj[live]
         valid_h = self.store._host_valid if self.borrowed else None
         if valid_h is not None and len(rows):
             live = valid_h[np.minimum(rows, len(valid_h) - 1)] & (rows < len(valid_h))
@@ -491,8 +560,13 @@ class ItemIndex:
             np.cumsum([len(e) for e in el], out=ex_ptr[1:])
             ex_rows = np.fromiter(itertools.chain.from_iterable(el), dtype=np.int64,
                                   count=int(ex_ptr[-1]))
+        if cand_ptr is None and self.n_dead:
+            # dead positions are masked by bucket: every query scans every (live) bucket
+            cand_ptr = np.zeros(nq + 1, dtype=np.int64)
+            cand = np.zeros(1, dtype=np.int64)
+            cand_all = np.ones(nq, dtype=np.uint8)
         nb = self.num_buckets if cand_ptr is not None else 1
-        cap = MAX_BATCH * kp * 4 + nb * 16 + (nb + 1) * 8 + nq * self.words * 4 + \
+        cap = MAX_BATCH * kp * 4 + (nb + 1) * 16 + (nb + 2) * 8 + nq * self.words * 4 + \
             (nq + 1) * 4 + (len(ex_rows) + 1 if ex_rows is not None else 0) * 4 + 6 * 16
         host = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
         info = np.empty(9, dtype=np.int64)
@@ -502,11 +576,12 @@ class ItemIndex:
             cand_ptr.ctypes.data_as(vp) if cand_ptr is not None else None,
             cand.ctypes.data_as(vp) if cand is not None else None,
             cand_all.ctypes.data_as(vp) if cand_all is not None else None,
-            self.num_buckets, self.words, self.bucket_start.ctypes.data_as(vp), int(self.n),
+            self.num_buckets, self.words, self.bucket_start.ctypes.data_as(vp),
+            int(self.n_main),
             ex_ptr.ctypes.data_as(vp) if ex_ptr is not None else None,
             ex_rows.ctypes.data_as(vp) if ex_rows is not None else None,
-            pos.ctypes.data_as(vp), len(pos), ctypes.c_void_p(host.data_ptr()), cap,
-            info.ctypes.data_as(vp))
+            pos.ctypes.data_as(vp), len(pos), int(self.n_main), int(self.n),
+            ctypes.c_void_p(host.data_ptr()), cap, info.ctypes.data_as(vp))
         if rc == 1:
             return None
         if rc != 0:
@@ -616,11 +691,11 @@ class ItemIndex:
         if cosine:
             nrm = mat[:self.n].norm(dim=1)
             scores = torch.where(nrm > 0, scores / nrm, torch.zeros_like(scores))
-        keep = torch.isfinite(scores)
+        keep = torch.isfinite(scores) & (self.bucket_of[:self.n] != self.dead_bucket)
         if candidates is not None:
-            cand = torch.zeros(self.num_buckets, dtype=torch.bool, device=dev)
+            cand = torch.zeros(self.num_buckets + 1, dtype=torch.bool, device=dev)
             cand[torch.as_tensor(np.asarray(candidates, dtype=np.int64), device=dev)] = True
-            keep &= cand[self.bucket_of.long()]
+            keep &= cand[self.bucket_of[:self.n].long()]
         if exclude_rows is not None and len(exclude_rows):
             er = torch.as_tensor(np.asarray(exclude_rows, dtype=np.int64), device=dev)
             er = er[er < self.pos_of_row.numel()]

@@ -798,3 +798,65 @@ def test_serving_model_keeps_one_device_copy_of_y(cuda):
     m.Y.set_vector("I%d" % best, Y[best] * 0 + t * 10)
     assert m.top_n(t, 1)[0][0] == "I%d" % best
     assert m.index.rebuilds == rebuilds or m.index.rebuilds == rebuilds + 1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sharded", [False, True])
+def test_index_absorbs_moves_new_items_and_removals_incrementally(cuda, sharded):
+    """Speed-layer style updates -- items re-bucketed by their new vectors, brand-new items,
+    removed items -- are absorbed without re-sorting (ALSServingModel.java:161-183 moves one
+    item between LSH partitions): moved / new rows go to the delta segment, old positions die
+    in the dead bucket, and every scan stays exact against brute force (LSH candidates, full
+    scans and exclusions).  sharded: the owned-rows mode (ShardedItemIndex over 2 shards)."""
+    from oryx_amd.models.als.common import FeatureVectors
+    from oryx_amd.ops import topn
+    g = np.random.default_rng(21)
+    k, n, nb = 32, 40_000, 32
+    H = torch.from_numpy(g.standard_normal((5, k)).astype(np.float32)).to(cuda)
+    w = (1 << torch.arange(5, device=cuda))
+    part = lambda rows: ((rows @ H.t()) > 0).long().mul(w).sum(1)
+    fv = FeatureVectors(k, cuda, partitioner=part)
+    ids = ["I%d" % i for i in range(n)]
+    Y = {i: g.standard_normal(k).astype(np.float32) for i in ids}
+    fv.set_vectors(ids, np.stack([Y[i] for i in ids]))
+    idx = topn.ShardedItemIndex(fv, nb, [cuda, cuda]) if sharded else topn.ItemIndex(fv, nb)
+    shards = idx.shards if sharded else [idx]
+    idx.refresh()
+    base_rebuilds = [s.rebuilds for s in shards]
+    next_id = n
+    for step in range(8):
+        # 300 moved (fresh random vectors: most change bucket), 200 new, 100 removed
+        moved = g.choice(sorted(Y), 300, replace=False)
+        for i in moved:
+            Y[i] = g.standard_normal(k).astype(np.float32)
+        fv.set_vectors(list(moved), np.stack([Y[i] for i in moved]))
+        new = ["I%d" % (next_id + j) for j in range(200)]
+        next_id += 200
+        for i in new:
+            Y[i] = g.standard_normal(k).astype(np.float32)
+        fv.set_vectors(new, np.stack([Y[i] for i in new]))
+        for i in g.choice(sorted(set(Y) - set(moved) - set(new)), 100, replace=False):
+            fv.remove_vector(i)
+            del Y[i]
+        # brute force over the store rows
+        mat, valid, _ = fv.device_view()
+        mat, valid = mat.cpu(), valid.cpu().clone()
+        bucket = part(mat.to(cuda)).cpu()
+        qs = []
+        for j in range(12):
+            c = np.sort(g.choice(nb, 10, replace=False)) if j % 3 else None
+            ex = g.choice(int(valid.numel()), 5).tolist() if j % 4 == 0 else None
+            qs.append(topn.TopNQuery(g.standard_normal(k).astype(np.float32), 10,
+                                     candidates=c, exclude_rows=ex))
+        res = idx.scan(qs)
+        for q, (rows, scores) in zip(qs, res):
+            allowed = None if q.candidates is None else \
+                torch.from_numpy(np.isin(bucket.numpy(), q.candidates))
+            br, bs = _brute(mat, valid, q.target, 10, allowed=allowed,
+                            exclude=q.exclude_rows or ())
+            assert np.allclose(scores, bs, rtol=1e-5, atol=1e-5), (step, scores, bs)
+            assert len(set(rows.tolist())) == len(rows)          # no duplicates
+            assert bool(valid[torch.as_tensor(rows, dtype=torch.long)].all())
+    # every step absorbed in place: no re-sort, rows in the delta segment, dead positions
+    assert [s.rebuilds for s in shards] == base_rebuilds
+    assert all(s.incremental >= 8 and s.delta_added > 0 and s.n_dead > 0 for s in shards)

@@ -12,7 +12,7 @@ from oryx_amd import native
 MAX_BATCH = 16
 
 
-def _reference(targets, kp, cands, excl, nb, bucket_start, n, pos):
+def _reference(targets, kp, cands, excl, nb, bucket_start, n, pos, nd=0):
     nq, k = targets.shape
     words = (nb + 31) // 32
     Q = np.zeros((MAX_BATCH, kp), np.float32)
@@ -30,12 +30,21 @@ def _reference(targets, kp, cands, excl, nb, bucket_start, n, pos):
         st, en = bucket_start[sel], bucket_start[sel + 1]
         keep = en > st
         st, en = st[keep], en[keep]
-        if not len(st):
-            return None
-        brk = np.nonzero(st[1:] != en[:-1])[0] + 1
-        rs = np.stack([st[np.r_[0, brk]], en[np.r_[brk - 1, len(en) - 1]]], 1)
+        if len(st):
+            brk = np.nonzero(st[1:] != en[:-1])[0] + 1
+            rs = np.stack([st[np.r_[0, brk]], en[np.r_[brk - 1, len(en) - 1]]], 1)
+        else:
+            rs = np.zeros((0, 2), np.int64)
     else:
-        rs = np.array([[0, n]], np.int64)
+        rs = np.array([[0, n]], np.int64) if n > 0 else np.zeros((0, 2), np.int64)
+    if nd:                          # the delta segment [n, n + nd), scanned by every query
+        if len(rs) and rs[-1, 1] == n:
+            rs = rs.copy()
+            rs[-1, 1] = n + nd
+        else:
+            rs = np.concatenate([rs, np.array([[n, n + nd]], np.int64)])
+    if not len(rs):
+        return None
     tiles = (rs[:, 1] - rs[:, 0] + 15) // 16
     t0 = np.zeros(len(rs) + 1, np.int64)
     np.cumsum(tiles, out=t0[1:])
@@ -68,9 +77,10 @@ def test_topn_prep_matches_numpy_packing():
         bucket_start = np.zeros(nb + 1, np.int64)
         np.cumsum(counts, out=bucket_start[1:])
         n = int(bucket_start[-1])
-        nrows = n + int(rng.integers(0, 50))
+        nd = int(rng.integers(0, 40)) if rng.random() < 0.5 else 0
+        nrows = n + nd + int(rng.integers(0, 50))
         pos = np.full(nrows, -1, np.int64)
-        pos[rng.permutation(nrows)[:n]] = np.arange(n)
+        pos[rng.permutation(nrows)[:n + nd]] = np.arange(n + nd)
         nq = int(rng.integers(1, 9))
         lsh = rng.random() < 0.7
         cands = [np.unique(rng.integers(0, nb, int(rng.integers(0, min(nb, 20) + 1))))
@@ -80,7 +90,7 @@ def test_topn_prep_matches_numpy_packing():
         excl = [rng.integers(-2, nrows + 3, int(rng.integers(0, 30))).tolist()
                 if rng.random() < 0.6 else None for _ in range(nq)]
         targets = rng.standard_normal((nq, k)).astype(np.float32)
-        ref = _reference(targets, kp, cands, excl, nb, bucket_start, n, pos)
+        ref = _reference(targets, kp, cands, excl, nb, bucket_start, n, pos, nd)
         cp = ca = c = None
         if any(x is not None for x in cands):
             cl = [x if x is not None else np.zeros(0, np.int64) for x in cands]
@@ -103,8 +113,8 @@ def test_topn_prep_matches_numpy_packing():
                                 (nb + 31) // 32, bucket_start.ctypes.data_as(vp), n,
                                 ep.ctypes.data_as(vp) if ep is not None else None,
                                 er.ctypes.data_as(vp) if er is not None else None,
-                                pos.ctypes.data_as(vp), len(pos), out.ctypes.data_as(vp),
-                                len(out), info.ctypes.data_as(vp))
+                                pos.ctypes.data_as(vp), len(pos), n, n + nd,
+                                out.ctypes.data_as(vp), len(out), info.ctypes.data_as(vp))
         if ref is None:
             assert rc == 1
             continue
