@@ -36,6 +36,12 @@ import torch
 from oryx_amd.parallel import dist
 
 out_dir = sys.argv[1]
+import traceback
+def _excepthook(t, v, tb):
+    with open(os.path.join(out_dir, "error_%s.txt" % os.environ.get("RANK", "0")), "w") as fh:
+        fh.write("".join(traceback.format_exception(t, v, tb)))
+    sys.__excepthook__(t, v, tb)
+sys.excepthook = _excepthook
 DEV = os.environ.get("ORYX_MR_DEVICE", "cuda:0")
 SMALL = DEV == "cpu"
 ctx = dist.init_from_env(device=DEV, backend="gloo")
@@ -215,7 +221,9 @@ def _run_worlds(tmp_path, device):
                "--nproc-per-node=%d" % world, "--master-addr=127.0.0.1",
                "--master-port=%d" % _port(), str(script), str(d)]
         r = subprocess.run(cmd, env=env, timeout=400, capture_output=True, text=True)
-        assert r.returncode == 0, (world, r.stdout[-2000:], r.stderr[-4000:])
+        errs = "".join(open(os.path.join(d, f)).read() for f in sorted(os.listdir(d))
+                       if f.startswith("error_"))
+        assert r.returncode == 0, (world, errs or r.stderr[-4000:])
         outs[world] = d
     res2 = json.loads((outs[2] / "res0.json").read_text())
     assert res2["world"] == 2
