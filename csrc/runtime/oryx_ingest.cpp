@@ -1508,15 +1508,18 @@ long long oryx_format_float_rows(const float* mat, long long n, int k, long long
 
 // All keys from `from` on, back to back in out; ends[j] = end offset of key from + j.
 // Returns bytes used, or -(bytes needed) when out is too small.
-long long oryx_dict_keys_blob(void* dh, long long from, char* out, long long cap,
+// Keys from .. to - 1 (clamped to the size) back to back into out, their end offsets into
+// ends (to - from entries at most: a dictionary growing concurrently never writes past it).
+long long oryx_dict_keys_blob(void* dh, long long from, long long to, char* out, long long cap,
                               long long* ends) {
   auto* d = static_cast<Dict*>(dh);
   std::lock_guard<std::mutex> g(d->mu);
+  const size_t end = std::min((size_t)std::max(to, 0LL), d->keys.size());
   long long need = 0;
-  for (size_t c = (size_t)from; c < d->keys.size(); ++c) need += (long long)d->keys[c].size();
+  for (size_t c = (size_t)from; c < end; ++c) need += (long long)d->keys[c].size();
   if (need > cap) return -need;
   long long pos = 0;
-  for (size_t c = (size_t)from; c < d->keys.size(); ++c) {
+  for (size_t c = (size_t)from; c < end; ++c) {
     memcpy(out + pos, d->keys[c].data(), d->keys[c].size());
     pos += (long long)d->keys[c].size();
     ends[c - from] = pos;

@@ -7,6 +7,7 @@ sites it replaces).
 from __future__ import annotations
 
 import ctypes
+import threading
 import json
 import time
 from typing import List, Optional, Sequence, Tuple
@@ -26,6 +27,8 @@ class IdDict:
         self._lib = native.runtime()
         self._h = self._lib.oryx_dict_new()
         self._keys_cache: List[str] = []
+        # key_list is called from many serving threads at once: one of them extends the cache
+        self._keys_lock = threading.Lock()
 
     def __del__(self):
         try:
@@ -43,7 +46,8 @@ class IdDict:
     def clear(self) -> "IdDict":
         """Empty the dictionary, keeping its native table's capacity (reused per batch)."""
         self._lib.oryx_dict_clear(self._h)
-        self._keys_cache = []
+        with self._keys_lock:
+            self._keys_cache = []
         return self
 
     def encode(self, keys: Sequence[str]) -> np.ndarray:
@@ -124,28 +128,35 @@ class IdDict:
         """Every key in code order: the dictionary's own cached list (read-only; no copy --
         per-request lookups of a few codes in a 1M-key dictionary must not copy it)."""
         n = len(self)
-        have = len(self._keys_cache)
-        if have < n:
-            # one native call: the new keys back to back plus their end offsets
-            ends = np.empty(n - have, dtype=np.int64)
-            cap = 1 << 16
-            while True:
-                buf = ctypes.create_string_buffer(cap)
-                used = self._lib.oryx_dict_keys_blob(self._h, have, buf, cap,
-                                                     ends.ctypes.data_as(ctypes.c_void_p))
-                if used >= 0:
-                    break
-                cap = -used + 1
-            raw = ctypes.string_at(buf, used)
-            if used == (ends[-1] if len(ends) else 0) and raw.isascii():
-                text = raw.decode("ascii")
-                starts = np.r_[0, ends[:-1]].tolist()
-                self._keys_cache.extend(text[a:b] for a, b in zip(starts, ends.tolist()))
-            else:
-                starts = np.r_[0, ends[:-1]].tolist()
-                self._keys_cache.extend(raw[a:b].decode("utf-8")
-                                        for a, b in zip(starts, ends.tolist()))
-        return self._keys_cache if len(self._keys_cache) == n else self._keys_cache[:n]
+        cache = self._keys_cache
+        if len(cache) >= n:
+            return cache if len(cache) == n else cache[:n]
+        with self._keys_lock:
+            cache = self._keys_cache
+            have = len(cache)
+            if have < n:
+                new = self._fetch_keys(have, n)
+                # (a fully built list: one atomic extend, readers see old or whole new keys)
+                cache.extend(new)
+        return cache if len(cache) == n else cache[:n]
+
+    def _fetch_keys(self, have: int, n: int) -> List[str]:
+        """Keys ``have`` .. ``n - 1`` in code order (one native call)."""
+        ends = np.empty(n - have, dtype=np.int64)
+        cap = 1 << 16
+        while True:
+            buf = ctypes.create_string_buffer(cap)
+            used = self._lib.oryx_dict_keys_blob(self._h, have, n, buf, cap,
+                                                 ends.ctypes.data_as(ctypes.c_void_p))
+            if used >= 0:
+                break
+            cap = -used + 1
+        raw = ctypes.string_at(buf, used)
+        starts = np.r_[0, ends[:-1]].tolist()
+        if used == (ends[-1] if len(ends) else 0) and raw.isascii():
+            text = raw.decode("ascii")
+            return [text[a:b] for a, b in zip(starts, ends.tolist())]
+        return [raw[a:b].decode("utf-8") for a, b in zip(starts, ends.tolist())]
 
 
 def _ptr(a: np.ndarray) -> ctypes.c_void_p:

@@ -113,7 +113,7 @@ def _register_runtime_extras(lib):
     # buf, len, F, is_num, out, span_off, span_len, max_rows
     _sig(lib, "oryx_csv_numeric_block", c_ll, [c_cp, c_ll, c_i, c_vp, c_vp, c_vp, c_vp,
                                                c_ll])
-    _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_dict_keys_blob", c_ll, [c_vp, c_ll, c_ll, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_owners", c_ll, [c_vp, c_ll, c_i, c_vp])
     _sig(lib, "oryx_ts_range", c_ll, [c_vp, c_ll, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_csv_to_f32", c_ll, [c_vp, c_ll, c_i, c_vp, c_vp, c_i, c_vp, c_vp, c_vp,
