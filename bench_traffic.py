@@ -27,6 +27,7 @@ incremental refreshes during the mix (per speed interval), its delta-segment and
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import shutil
@@ -119,6 +120,66 @@ def write_model_log(root, data, features):
             "X", user_ids[lo:hi], ingest.format_float_rows_blob(X[lo:hi]), kt,
             np.arange(hi - lo)), key="UP")
     topic.close()
+
+
+SPEED_CHILD = r"""
+import json, os, sys, threading, time
+sys.path.insert(0, sys.argv[1])
+from oryx_amd.layers.speed import SpeedLayer
+from oryx_amd.utils import config as cfg
+conf = cfg.deserialize(open(sys.argv[2]).read())
+users, interval_ms = int(sys.argv[3]), float(sys.argv[4])
+speed = SpeedLayer(conf).start(start_timer=False)
+t0 = time.time()
+while True:
+    sm = speed.manager.model
+    if sm is not None and sm.get_fraction_loaded() >= 1.0 and sm.X.size() == users:
+        break
+    time.sleep(0.05)
+print(json.dumps({"loaded_s": time.time() - t0}), flush=True)
+assert sys.stdin.readline().strip() == "go"
+stop = threading.Event()
+durs = []
+def run():
+    while not stop.is_set():
+        t = time.perf_counter()
+        speed.run_interval()
+        dt = time.perf_counter() - t
+        durs.append(dt * 1e3)
+        if interval_ms / 1e3 > dt:
+            stop.wait(interval_ms / 1e3 - dt)
+th = threading.Thread(target=run, daemon=True)
+th.start()
+sys.stdin.readline()
+stop.set()
+th.join(120)
+print(json.dumps({"intervals": speed.intervals_run, "up_rows": speed.updates_sent,
+                  "interval_ms": durs}), flush=True)
+speed.close()
+os._exit(0)
+"""
+
+
+class _GcPauses:
+    """Times the serving interpreter's cyclic-GC passes (a gen-2 pass over a big heap stops
+    every handler thread)."""
+
+    def __init__(self):
+        self.t = None
+        self.ms = {0: [], 1: [], 2: []}
+        gc.callbacks.append(self._cb)
+
+    def _cb(self, phase, info):
+        if phase == "start":
+            self.t = time.perf_counter()
+        elif self.t is not None:
+            self.ms[info["generation"]].append((time.perf_counter() - self.t) * 1e3)
+
+    def take(self):
+        out = {"gen%d" % g: {"n": len(v), "max_ms": max(v) if v else 0.0,
+                             "total_ms": sum(v)} for g, v in self.ms.items()}
+        self.ms = {0: [], 1: [], 2: []}
+        return out
 
 
 def _stats(v):
@@ -229,7 +290,6 @@ def main(argv=None) -> int:
     args = ap.parse_args(argv)
     import bench_serving
     import torch
-    from oryx_amd.layers.speed import SpeedLayer
     from oryx_amd.serving.layer import ServingLayer
     from oryx_amd.utils import config as cfg
 
@@ -262,15 +322,20 @@ def main(argv=None) -> int:
         }, cfg.get_default())
         t0 = time.perf_counter()
         serving = ServingLayer(conf, host="127.0.0.1").start()
-        speed = None if args.no_speed else SpeedLayer(conf).start(start_timer=False)
-        stop = threading.Event()
+        # the speed layer in its own process, as deployed (oryx-run.sh speed): it shares the
+        # GPU with the serving layer, not its interpreter
+        speed = None
+        if not args.no_speed:
+            conf_path = os.path.join(work, "speed.conf")
+            with open(conf_path, "w") as fh:
+                fh.write(cfg.serialize(conf))
+            speed = subprocess.Popen([sys.executable, "-c", SPEED_CHILD, ROOT, conf_path,
+                                      str(args.users), str(args.speed_interval_ms)],
+                                     stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
         try:
             while True:
-                sm = speed.manager.model if speed is not None else None
                 vm = serving.manager.get_model()
-                sp_ok = speed is None or (sm is not None and sm.get_fraction_loaded() >= 1.0
-                                          and sm.X.size() == args.users)
-                if sp_ok and vm is not None and vm.get_fraction_loaded() >= 1.0 and \
+                if vm is not None and vm.get_fraction_loaded() >= 1.0 and \
                         vm.get_num_users() == args.users and vm.get_num_items() == args.items:
                     break
                 if time.perf_counter() - t0 > 3000:
@@ -280,6 +345,8 @@ def main(argv=None) -> int:
                           file=sys.stderr, flush=True)
                 time.sleep(0.02)
             rec["load_s"] = time.perf_counter() - t0
+            if speed is not None:
+                rec["speed_load_s"] = json.loads(speed.stdout.readline())["loaded_s"]
             vm = serving.manager.get_model()
             vm.top_n(np.zeros(args.features, np.float32), 10)   # device mirror + index
             port = serving.actual_port
@@ -290,43 +357,36 @@ def main(argv=None) -> int:
                           {"recommend": 1.0}, args.seed + 17)
             # ---- idle baseline: /recommend only, nothing written
             print("bench_traffic: idle phase", file=sys.stderr, flush=True)
+            gcp = _GcPauses()
             s0 = _server_side(serving)
             smp = _Sampler().start() if args.sample else None
             rec["idle"] = run_phase(port, args, {"recommend": 1.0}, args.seed)
             if smp is not None:
                 rec["idle_stack_samples"] = smp.stop()
             rec["idle_server"] = _server_delta(s0, _server_side(serving))
+            rec["idle_gc"] = gcp.take()
             if speed is None:
                 return 0 if print(json.dumps(rec), flush=True) is None else 0
             # ---- the mix with the speed layer live
             c0 = _index_counters(vm)
-            runs0, sent0 = speed.intervals_run, speed.updates_sent
-            slow = []
-
-            def micro_batches():
-                while not stop.is_set():
-                    t = time.perf_counter()
-                    speed.run_interval()
-                    dt = time.perf_counter() - t
-                    slow.append(dt * 1e3)
-                    left = args.speed_interval_ms / 1e3 - dt
-                    if left > 0:
-                        stop.wait(left)
-            runner = threading.Thread(target=micro_batches, name="speed-batches", daemon=True)
-            runner.start()
+            speed.stdin.write("go\n")
+            speed.stdin.flush()
             print("bench_traffic: mix phase", file=sys.stderr, flush=True)
             s0 = _server_side(serving)
             rec["mix_phase"] = run_phase(port, args, mix, args.seed + 1)
             rec["mix_server"] = _server_delta(s0, _server_side(serving))
-            stop.set()
-            runner.join(timeout=60)
+            rec["mix_gc"] = gcp.take()
+            speed.stdin.write("stop\n")
+            speed.stdin.flush()
+            sp = json.loads(speed.stdout.readline())
             # let the last UP rows reach the serving model, then count what the index did
             time.sleep(1.0)
             vm.top_n(np.zeros(args.features, np.float32), 10)
             c1 = _index_counters(vm)
-            runs = speed.intervals_run - runs0
-            rec["speed"] = {"intervals": runs, "up_rows": speed.updates_sent - sent0,
-                            "interval_ms": _stats(slow)}
+            runs = sp["intervals"]
+            rec["speed"] = {"intervals": runs, "up_rows": sp["up_rows"],
+                            "interval_ms": _stats(sp["interval_ms"]),
+                            "process": "separate (as deployed)"}
             rec["index"] = {k: c1.get(k, 0) - c0.get(k, 0) for k in ("rebuilds", "incremental",
                                                                     "delta_added")}
             rec["index"].update(delta_rows_now=c1.get("delta_rows"), dead_now=c1.get("dead"))
@@ -335,9 +395,9 @@ def main(argv=None) -> int:
             mix99 = rec["mix_phase"].get("recommend", {}).get("p99_ms")
             rec["recommend_p99_mix_over_idle"] = (mix99 / idle99) if idle99 and mix99 else None
         finally:
-            stop.set()
-            if speed is not None:
-                speed.close()
+            if speed is not None and speed.poll() is None:
+                speed.kill()
+                speed.wait(30)
             serving.close()
         if torch.cuda.is_available():
             rec["device"] = torch.cuda.get_device_name(0)

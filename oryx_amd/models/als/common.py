@@ -83,9 +83,13 @@ class FeatureVectors:
         self.ld = -(-self.k // max(1, int(row_pad))) * max(1, int(row_pad))
         self._lock = lang.AutoReadWriteLock()
         self._index: Dict[str, int] = {}
-        self._ids: List[Optional[str]] = []
+        # row -> ID (None: free row) and row -> "added since the last retain" flags, as
+        # numpy arrays rather than a list and a set of strings: neither is a cyclic-GC
+        # container, so a 20M-row store adds nothing to a gen-2 collection's walk (the list
+        # and set of 20M item IDs cost the serving process ~1 s of stopped handlers per pass)
+        self._ids = np.empty(0, dtype=object)
+        self._recent_rows = np.zeros(0, dtype=bool)
         self._free: List[int] = []
-        self._recent: Set[str] = set()
         cap = max(16, int(initial_capacity))
         self._host = np.zeros((cap, self.k), dtype=np.float32)
         self._host_valid = np.zeros(cap, dtype=bool)
@@ -133,7 +137,7 @@ class FeatureVectors:
         return self._index.get(id_)
 
     def id_of_row(self, row: int) -> Optional[str]:
-        return self._ids[row] if row < len(self._ids) else None
+        return self._ids[row] if 0 <= row < self._n_rows else None
 
     def _alloc_row(self) -> int:
         if self._free:
@@ -149,8 +153,20 @@ class FeatureVectors:
             self._dirty_all = True
             self._idx_mark_all()
         self._n_rows += 1
-        self._ids.append(None)
+        self._ids_fit(self._n_rows)
         return row
+
+    def _ids_fit(self, rows: int) -> None:
+        """Grow the row -> ID and recent-flag arrays to hold ``rows`` rows."""
+        cap = len(self._ids)
+        if rows <= cap:
+            return
+        cap = max(rows, 2 * cap, 1024)
+        ids = np.empty(cap, dtype=object)
+        ids[:len(self._ids)] = self._ids
+        rec = np.zeros(cap, dtype=bool)
+        rec[:len(self._recent_rows)] = self._recent_rows
+        self._ids, self._recent_rows = ids, rec
 
     def set_vector(self, id_: str, vector) -> None:
         v = np.asarray(vector, dtype=np.float32)
@@ -162,7 +178,7 @@ class FeatureVectors:
                 row = self._alloc_row()
                 self._index[id_] = row
                 self._ids[row] = id_
-                self._recent.add(id_)
+                self._recent_rows[row] = True
                 self.id_version += 1
                 if self._journal is not None:
                     self._journal.append((True, id_, row))
@@ -272,7 +288,7 @@ class FeatureVectors:
                             row = self._alloc_row()
                             index[id_] = row
                             self._ids[row] = id_
-                            self._recent.add(id_)
+                            self._recent_rows[row] = True
                             self.id_version += 1
                             if self._journal is not None:
                                 self._journal.append((True, id_, row))
@@ -286,8 +302,10 @@ class FeatureVectors:
                 new_rows = np.arange(start, start + len(new_ids), dtype=np.int64)
                 if self._journal is not None:
                     self._journal.append((True, new_ids, new_rows))
-                self._ids.extend(new_ids)
-                self._recent.update(new_ids)
+                end = start + len(new_ids)
+                self._ids_fit(end)
+                self._ids[start:end] = new_ids
+                self._recent_rows[start:end] = True
                 self.id_version += 1
                 self._n_rows = start + len(new_ids)
                 rows[new_pos] = new_rows
@@ -321,13 +339,13 @@ class FeatureVectors:
 
     def _remove_locked(self, id_: str) -> None:
         row = self._index.pop(id_, None)
-        self._recent.discard(id_)
         if row is not None and self._journal is not None:
             self._journal.append((False, id_, row))
         if row is not None:
             self._host[row] = 0.0
             self._host_valid[row] = False
             self._ids[row] = None
+            self._recent_rows[row] = False
             self.id_version += 1
             self._free.append(row)
             self._dirty.add(row)
@@ -393,7 +411,8 @@ class FeatureVectors:
 
     def add_all_recent_to(self, out: Set[str]) -> None:
         with self._lock.read():
-            out.update(self._recent)
+            n = self._n_rows
+            out.update(self._ids[:n][self._recent_rows[:n]].tolist())
 
     def all_ids(self) -> List[str]:
         with self._lock.read():
@@ -402,9 +421,10 @@ class FeatureVectors:
     def retain_recent_and_ids(self, new_model_ids: Collection[str]) -> None:
         keep = new_model_ids if isinstance(new_model_ids, (set, frozenset)) else set(new_model_ids)
         with self._lock.write():
-            for id_ in [i for i in self._index if i not in keep and i not in self._recent]:
+            rec = self._recent_rows
+            for id_ in [i for i, r in self._index.items() if i not in keep and not rec[r]]:
                 self._remove_locked(id_)
-            self._recent.clear()
+            self._recent_rows[:] = False
 
     def for_each(self, fn: Callable[[str, np.ndarray], None]) -> None:
         with self._lock.read():
@@ -492,18 +512,12 @@ class FeatureVectors:
         return self._dev_part[:self._n_rows]
 
     def id_array(self) -> np.ndarray:
-        """Every row's ID (None for free rows) as a numpy object array, cached per store
-        version: candidate IDs are then one fancy index (``id_array()[rows]``), not a Python
-        list built per request."""
-        c = getattr(self, "_id_arr", None)
-        if c is not None and c[0] == self.id_version:
-            return c[1]
+        """Every row's ID (None for free rows) as a numpy object array -- a view of the
+        store's own row -> ID array, no copy: candidate IDs are then one fancy index
+        (``id_array()[rows]``), not a Python list built per request.  Use it at once (a row
+        freed and reused later shows its new ID)."""
         with self._lock.read():
-            arr = np.empty(len(self._ids), dtype=object)
-            arr[:] = self._ids
-            ver = self.id_version
-        self._id_arr = (ver, arr)
-        return arr
+            return self._ids[:self._n_rows]
 
     def key_suffixes(self) -> np.ndarray:
         """int64 per row: the numeric suffix of the row's ID (-1: free row or no digits),
@@ -523,8 +537,8 @@ class FeatureVectors:
 
     def ids_of_rows(self, rows) -> List[Optional[str]]:
         ids = self._ids
-        n = len(ids)
-        return [ids[r] if r < n else None for r in rows]
+        n = self._n_rows
+        return [ids[r] if 0 <= r < n else None for r in rows]
 
     def host_rows(self, ids: Iterable[str]) -> List[int]:
         idx = self._index

@@ -400,11 +400,17 @@ class ALSServingModel(ServingModel):
         self.X.set_vectors(ids, mat)
         with self._expected_lock:
             self._expected_users.difference_update(ids)
+            if not self._expected_users:
+                # a drained set keeps its 20M-slot table (walked by every gen-2 GC pass)
+                self._expected_users = set()
 
     def set_item_vectors(self, ids: Sequence[str], mat: np.ndarray) -> None:
         self.Y.set_vectors(ids, mat)
         with self._expected_lock:
             self._expected_items.difference_update(ids)
+            if not self._expected_items:
+                # a drained set keeps its 20M-slot table (walked by every gen-2 GC pass)
+                self._expected_items = set()
 
     # known items are held as int32 codes of one native item dictionary per model (a loaded
     # model has ~20 per user: 10M Python strings in sets would dominate the load time and the
@@ -852,6 +858,9 @@ class ALSServingModelManager(AbstractServingModelManager):
                 self.model.retain_recent_and_known_items(xids, yids)
                 self.model.retain_recent_and_user_ids(xids)
                 self.model.retain_recent_and_item_ids(yids)
+                # the loop frame outlives this message: drop the ID sets (20M strings in
+                # a set stay in every gen-2 GC walk until the next model otherwise)
+                del xids, yids, pmml
                 log.info("Model updated: %s", self.model)
             else:
                 raise ValueError("Bad message: %r" % (km,))

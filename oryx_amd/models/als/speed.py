@@ -276,6 +276,9 @@ class ALSSpeedModelManager(SpeedModelManager):
                 yids = set(pmml.get_extension_content("YIDs") or [])
                 self.model.retain_recent_and_user_ids(xids)
                 self.model.retain_recent_and_item_ids(yids)
+                # the loop frame outlives this message: drop the ID sets (20M strings in
+                # a set stay in every gen-2 GC walk until the next model otherwise)
+                del xids, yids, pmml
                 log.info("Model updated: %s", self.model)
             else:
                 raise ValueError("Bad message: %r" % (km,))

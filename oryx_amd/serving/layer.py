@@ -15,6 +15,7 @@ Equivalent of ``ServingLayer`` + ``ModelManagerListener`` (``[lserving]/ServingL
 
 from __future__ import annotations
 
+import gc
 import logging
 import os
 import ssl
@@ -217,6 +218,10 @@ class ServingLayer:
         self._server = http.make_server(self.host, port, router, self.context, ssl_ctx, auth,
                                         self.metrics, native=self.native_http,
                                         threads=self.handler_threads, tls_files=tls_files)
+        # everything built so far (modules, torch, the router) lives as long as the process:
+        # out of the cyclic GC's generations, so a gen-2 pass under traffic walks only what
+        # requests and updates allocate (handlers stop for the whole pass)
+        gc.freeze()
         self._server.start_background()
         log.info("Serving layer listening on %s:%d%s", self.host, self._server.port,
                  " (HTTPS)" if ssl_ctx else "")

@@ -37,5 +37,9 @@ def test_key_list_concurrent_growth_cpu():
     assert not errs, errs[:3]
     keys = d.key_list()
     assert len(keys) == 150_000 and keys[-1] == "k149999"
-    assert keys is d.key_list()            # cached: the same list object, no copy
-    assert len(d._keys_cache) == len(d)    # no duplicated segments
+    again = d.key_list()
+    assert again.base is keys.base             # cached: views of one array, no copy
+    assert d._keys_cache[1] == len(d)          # no duplicated segments
+    assert list(d._keys_cache[0][:len(d)]) == ["k%d" % i for i in range(150_000)]
+    import gc
+    assert not gc.is_tracked(d._keys_cache[0])  # invisible to the cyclic GC
