@@ -64,6 +64,36 @@ PRESETS = {
 }
 
 
+# effective one-direction bandwidth of one xGMI link (7 links x ~153 GB/s per GPU, both
+# directions): what one peer-to-peer stream of stores sustains, an assumption of the estimate
+XGMI_LINK_GBPS = 64.0
+
+
+def exchange_schedule(trainer, halfstep_ms: dict, W: int, elem: int) -> dict:
+    """Exposed factor-exchange time per iteration estimated from the per-link schedule of the
+    range-by-range exchange (range c moves while range c + 1 is solved; the last range's
+    transfer is exposed, and so is any range whose transfer outlasts the next solve):
+
+    * peer push (parallel/ipc.py IpcAllGather): a range goes to the W - 1 peers over W - 1
+      different links at once, so it takes range_bytes / link bandwidth;
+    * ring all-gather: every byte of the W - 1 other ranks' ranges crosses this rank's one
+      inbound ring link, (W - 1) range_bytes / link bandwidth."""
+    bw = XGMI_LINK_GBPS * 1e9
+    out = {"link_gbps_assumed": XGMI_LINK_GBPS}
+    for half, lay in (("items", trainer.lay_i), ("users", trainer.lay_u)):
+        rb = lay.cr * trainer.kp * elem
+        solve_c = halfstep_ms.get("%s_solve_ms" % half, 0.0) / max(1, lay.C)
+        for how, t in (("push", rb / bw * 1e3), ("ring", (W - 1) * rb / bw * 1e3)):
+            exposed = t + sum(max(0.0, t - solve_c) for _ in range(lay.C - 1))
+            out["%s_%s_ms" % (half, how)] = exposed
+        out["%s_range_bytes" % half] = rb
+        out["%s_ranges" % half] = lay.C
+        out["%s_solve_per_range_ms" % half] = solve_c
+    out["push_ms_per_iteration"] = out["items_push_ms"] + out["users_push_ms"]
+    out["ring_ms_per_iteration"] = out["items_ring_ms"] + out["users_ring_ms"]
+    return out
+
+
 def emulate(args) -> int:
     """--emulate-world W --emulate-rank r: rank r's per-rank workload of a W-GPU weak-scaling
     run on one GPU (see the argument's help).  Prints one JSON line (not the headline
@@ -129,6 +159,7 @@ def emulate(args) -> int:
     # step, so the received bytes over ~64 GB/s of effective ring bandwidth (RCCL's
     # multi-channel rings reach roughly that per GPU pair) bounds the exposed exchange
     coll["allgather_ring_est_ms"] = coll["allgather_recv_bytes"] / 64e9 * 1e3
+    coll["exposed_exchange_est"] = exchange_schedule(trainer, halfstep_ms, W, elem)
     rec = {
         "metric": "ALS per-rank iteration time, emulated %d-GPU weak scaling (rank %d)" % (W, R),
         "emulated": True, "world": W, "rank": R, "preset": args.preset,
@@ -344,6 +375,7 @@ def main(argv=None) -> int:
             "world_size": info["world_size"],
             "backend": info["backend"],
             "ipc_allreduce": info.get("ipc_allreduce", False),
+            "allgather": info.get("allgather"),
             "rank_devices": [r.get("current_device", r["device"]) for r in info["ranks"]],
             "peak_hbm_gib_per_rank": float(peak.item()) / 2**30,
             "halfstep_ms": halfstep_ms,

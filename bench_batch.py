@@ -196,10 +196,12 @@ def main(argv=None) -> int:
         sharded_path = layer._sharded()
         # the first generation's phases (phase_seconds accumulates over generations)
         first_phases = dict(getattr(layer._update, "phase_seconds", {}))
+        first_train = dict(getattr(layer._update, "train_phases", {}) or {})
         first_lay = dict(layer.last_phases)
         later = []
         for g in range(1, max(1, args.generations) if ctx.world_size == 1 else 1):
             before = dict(layer._update.phase_seconds)
+            before_t = dict(getattr(layer._update, "train_phases", {}) or {})
             now += 60_000
             append(args.next_ratings, now)
             t0 = time.perf_counter()
@@ -211,6 +213,9 @@ def main(argv=None) -> int:
                           "ratings": args.ratings + g * args.next_ratings,
                           "phase_s": {k: after[k] - before.get(k, 0.0) for k in after},
                           "layer_phase_s": dict(layer.last_phases),
+                          "train_phase_s": {k: v - before_t.get(k, 0.0) for k, v in
+                                            (getattr(layer._update, "train_phases", {})
+                                             or {}).items()},
                           "history": dict(hist.stats) if hist is not None else None})
         layer.close()
     else:
@@ -220,6 +225,7 @@ def main(argv=None) -> int:
         t_gen = time.perf_counter() - t0
         sharded_path = layer._sharded()
         first_phases = dict(getattr(layer._update, "phase_seconds", {}))
+        first_train = dict(getattr(layer._update, "train_phases", {}) or {})
         first_lay = dict(layer.last_phases)
     phases = first_phases
     if not ctx.is_main:
@@ -247,7 +253,9 @@ def main(argv=None) -> int:
             "metric": metric, "app": args.app,
             "value": n_records / t_gen, "unit": unit, "higher_is_better": True,
             "n_gpus": ctx.world_size, "generation_s": t_gen, "log_append_s": t_ingest,
-            "phase_s": phases, "update_messages": int(sum(ends)),
+            "phase_s": phases,
+            "train_phase_s": first_train,
+            "update_messages": int(sum(ends)),
             "attributed_s": attributed, "unattributed_s": t_gen - attributed,
             "later_generations": later,
             "config": ({"ratings": args.ratings, "users": args.users, "items": args.items,

@@ -40,8 +40,15 @@ CLIENT = r"""
 import http.client, json, random, sys, time
 port, users, n, seed = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
 query = sys.argv[5] if len(sys.argv) > 5 else ""
+cafile = sys.argv[6] if len(sys.argv) > 6 else ""
 rnd = random.Random(seed)
-conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
+if cafile:
+    import ssl
+    # one keep-alive TLS connection per client (as the reference's load test): one handshake
+    conn = http.client.HTTPSConnection("127.0.0.1", port, timeout=60,
+                                       context=ssl.create_default_context(cafile=cafile))
+else:
+    conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
 lat = []
 errors = 0
 t0 = time.perf_counter()
@@ -112,8 +119,18 @@ def build_model(data, features: int, sample_rate: float, max_batch: int = 16,
     return model
 
 
+def _self_signed(dirname: str):
+    """(cert, key) PEM files of a throwaway self-signed certificate for 127.0.0.1."""
+    cert, key = os.path.join(dirname, "cert.pem"), os.path.join(dirname, "key.pem")
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-keyout", key,
+                    "-out", cert, "-days", "2", "-subj", "/CN=127.0.0.1",
+                    "-addext", "subjectAltName=IP:127.0.0.1"], check=True,
+                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    return cert, key
+
+
 def serve_and_measure(model, users: int, workers: int, requests: int, warmup: int,
-                      seed: int, query: str = ""):
+                      seed: int, query: str = "", tls: bool = False):
     from oryx_amd.api import AbstractServingModelManager
     from oryx_amd.serving.layer import ServingLayer
     from oryx_amd.utils import config as cfg
@@ -137,12 +154,21 @@ def serve_and_measure(model, users: int, workers: int, requests: int, warmup: in
             "false" if os.environ.get("ORYX_BENCH_PYTHON_HTTP") == "1" else "true",
         "oryx.serving.api.handler-threads": int(os.environ.get("ORYX_BENCH_HTTP_THREADS", "16")),
     }, cfg.get_default())
+    cafile = ""
+    if tls:
+        # HTTPS on the native front end (OpenSSL inside csrc/runtime/oryx_http.cpp)
+        import tempfile
+        cert, key = _self_signed(tempfile.mkdtemp(prefix="oryx_bench_tls_"))
+        conf = cfg.overlay_on({"oryx.serving.api.secure-port": 0,
+                               "oryx.serving.api.keystore-file": '"%s"' % cert,
+                               "oryx.serving.api.key-file": '"%s"' % key}, conf)
+        cafile = cert
     layer = ServingLayer(conf, manager=_Manager(conf), host="127.0.0.1").start()
     port = layer.actual_port
 
     def run(n):
         procs = [subprocess.Popen([sys.executable, "-c", CLIENT, str(port), str(users),
-                                   str(n), str(seed * 100 + w), query],
+                                   str(n), str(seed * 100 + w), query, cafile],
                                   stdout=subprocess.PIPE, text=True)
                  for w in range(workers)]
         outs = [json.loads(p.communicate()[0]) for p in procs]
@@ -310,6 +336,9 @@ def main(argv=None) -> int:
     ap.add_argument("--rescorer", action="store_true",
                     help="requests carry rescorerParams for the example ItemFilterRescorer "
                          "provider (every candidate filtered / rescored, on the device)")
+    ap.add_argument("--tls", choices=("off", "on", "both"), default="off",
+                    help="HTTPS on the native front end (self-signed certificate); both: an "
+                         "HTTP and an HTTPS run per worker count, with their req/s ratio")
     args = ap.parse_args(argv)
     if args.time_to_ready:
         print(json.dumps(time_to_ready(args.items, args.users, args.features, args.seed)),
@@ -329,20 +358,28 @@ def main(argv=None) -> int:
             t0 = time.perf_counter()
             model = build_model(data, features, rate, args.max_batch, args.rescorer)
             build_s = time.perf_counter() - t0
+            modes = {"off": (False,), "on": (True,), "both": (False, True)}[args.tls]
             for w in workers:
-                if model.batcher is not None:
-                    model.batcher.batches = model.batcher.requests = 0
-                qps, lat, total, errors = serve_and_measure(
-                    model, args.users, w, args.requests, args.warmup, args.seed,
-                    "?rescorerParams=factor:1.5" if args.rescorer else "")
-                rec = record(model, args, qps, lat, total, errors, build_s, w, rate, items,
-                             features)
-                rec["rescorer"] = bool(args.rescorer)
-                rec["front_end"] = "python http.server" if \
-                    os.environ.get("ORYX_BENCH_PYTHON_HTTP") == "1" else \
-                    "native (oryx_http.cpp), %s handler threads" % \
-                    os.environ.get("ORYX_BENCH_HTTP_THREADS", "16")
-                print(json.dumps(rec), flush=True)
+                http_qps = None
+                for tls in modes:
+                    if model.batcher is not None:
+                        model.batcher.batches = model.batcher.requests = 0
+                    qps, lat, total, errors = serve_and_measure(
+                        model, args.users, w, args.requests, args.warmup, args.seed,
+                        "?rescorerParams=factor:1.5" if args.rescorer else "", tls=tls)
+                    rec = record(model, args, qps, lat, total, errors, build_s, w, rate,
+                                 items, features)
+                    rec["rescorer"] = bool(args.rescorer)
+                    rec["front_end"] = "python http.server" if \
+                        os.environ.get("ORYX_BENCH_PYTHON_HTTP") == "1" else \
+                        "native (oryx_http.cpp), %s handler threads" % \
+                        os.environ.get("ORYX_BENCH_HTTP_THREADS", "16")
+                    rec["tls"] = tls
+                    if tls and http_qps:
+                        rec["https_over_http_qps"] = qps / http_qps
+                    if not tls:
+                        http_qps = qps
+                    print(json.dumps(rec), flush=True)
             if model.batcher is not None:
                 model.batcher.close()
             del model

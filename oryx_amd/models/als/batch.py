@@ -374,6 +374,8 @@ class ALSUpdate(MLUpdate):
         self.history: Optional[RatingsHistory] = None
         # cumulative seconds per phase of build / publish (bench_batch.py reads them)
         self.phase_seconds: Dict[str, float] = {}
+        # the "train" phase broken down (ALSTrainer.train's laps; accumulates like the above)
+        self.train_phases: Dict[str, float] = {}
 
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
@@ -528,8 +530,9 @@ class ALSUpdate(MLUpdate):
         tp = time.perf_counter()
         # random rows keyed by ID hash (this rank's rows: every world_size-th)
         W_, R_ = max(1, ctx.world_size), ctx.rank
-        xh = ingest.blob_hash64(*ingest.strings_blob(x_ids[R_::W_]))
-        yh = ingest.blob_hash64(*ingest.strings_blob(y_ids[R_::W_]))
+        # (key bytes straight from the native dictionaries: no Python strings re-encoded)
+        xh = ingest.blob_hash64(*users.keys_blob(np.ascontiguousarray(used_u[R_::W_])))
+        yh = ingest.blob_hash64(*items.keys_blob(np.ascontiguousarray(used_i[R_::W_])))
         f = trainer.train(self.iterations, checkpoint_dir=ckpt_dir,
                           checkpoint_interval=self.checkpoint_interval, fingerprint=fingerprint,
                           x_init=x_init, y_init=y_init, x_keys=xh, y_keys=yh)
@@ -542,6 +545,13 @@ class ALSUpdate(MLUpdate):
         if f.X.device.type == "cuda":
             torch.cuda.synchronize(f.X.device)
         ph["train"] = ph.get("train", 0.0) + time.perf_counter() - tp
+        for key in ("init_ms", "checkpoint_ms", "factors_ms"):
+            if key in trainer.timings:
+                self.train_phases[key[:-3]] = self.train_phases.get(key[:-3], 0.0) + \
+                    trainer.timings[key] / 1e3
+        its_ms = trainer.timings.get("iteration_ms", [])
+        self.train_phases["iterations"] = self.train_phases.get("iterations", 0.0) + \
+            sum(its_ms) / 1e3
         tp = time.perf_counter()
         # the rows' JSON text, formatted where the factors live (GPU: textfmt.hip); reused by
         # the X/ Y/ files and the UP messages

@@ -224,6 +224,13 @@ def build(upd, ctx: dist.DistContext, lines, features: int, lam: float, alpha: f
                   x_keys=ingest.blob_hash64(*x_keys), y_keys=ingest.blob_hash64(*y_keys))
     _sync(dev)
     ph["train"] = ph.get("train", 0.0) + time.perf_counter() - tp
+    tph = getattr(upd, "train_phases", None)
+    if tph is not None:
+        for key in ("init_ms", "checkpoint_ms", "factors_ms"):
+            if key in trainer.timings:
+                tph[key[:-3]] = tph.get(key[:-3], 0.0) + trainer.timings[key] / 1e3
+        tph["iterations"] = tph.get("iterations", 0.0) + \
+            sum(trainer.timings.get("iteration_ms", [])) / 1e3
     tp = time.perf_counter()
     k = features
     X_local = trainer.X[:trainer.su, :k]

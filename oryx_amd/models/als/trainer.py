@@ -96,12 +96,31 @@ class RowLayout:
         return (c * self.W + r) * self.cr + (loc - c * self.cr)
 
     def gather(self, local: torch.Tensor, ctx: dist.DistContext, overlap_with=None,
-               out: Optional[torch.Tensor] = None):
+               out: Optional[torch.Tensor] = None, name: Optional[str] = None):
         """All-gather ``local`` ([local_rows, ...]) into the gathered layout; ``overlap_with``
         (callable c -> None) runs before each range's exchange is started.  ``out``: the
         previous gathered matrix, overwritten in place when its shape fits (the collectives
         are ordered after every kernel already queued on the current stream, i.e. after the
-        last reads of the old rows), so the exchange allocates nothing per half-step."""
+        last reads of the old rows), so the exchange allocates nothing per half-step.
+
+        ``name`` ("X" / "Y"): with the node's peer-push all-gather (``ctx.ipc_gather``) the
+        gathered matrix is that gatherer's peer-mapped buffer of this name, and each range's
+        rows are written straight into every rank's copy as soon as they are solved."""
+        ag = getattr(ctx, "ipc_gather", None)
+        if ag is not None and name is not None and ctx.is_distributed:
+            shape = (self.rows,) + tuple(local.shape[1:])
+            full = ag.buffer(name, shape, local.dtype)
+            # from here on the peers may overwrite this rank's copy: every kernel that read
+            # its previous contents is already queued ahead on this stream
+            ag.begin(name)
+            for c in range(self.C):
+                if overlap_with is not None:
+                    overlap_with(c)
+                ag.push(name, local[c * self.cr:(c + 1) * self.cr],
+                        (c * self.W + ctx.rank) * self.cr, self.C, c)
+            with watchdog.guard("all_gather_rows"):
+                ag.end(name, self.C)
+            return full
         if ctx.world_size == 1 and self.C == 1:
             # one process, one range: the local shard IS the gathered matrix (no copy)
             if overlap_with is not None:
@@ -290,13 +309,20 @@ class ALSTrainer:
     # range still fills the GPU (small ranges leave CUs idle in every launch's tail)
     OVERLAP_MIN_BYTES = 16 << 20
     OVERLAP_MIN_ROWS = 8192
+    OVERLAP_MIN_ROWS_W = 2048
 
     def _chunks_for(self, n_total: int) -> int:
         c = self.gather_chunks
         if c <= 1 or self._explicit_chunks:
             return max(1, c)
         shard = dist.padded_shard_size(n_total, self.ctx.world_size)
-        if n_total * self.kp * (4 if self.split else 2) < self.OVERLAP_MIN_BYTES or shard // c < self.OVERLAP_MIN_ROWS:
+        if self.ctx.world_size > 1:
+            # a real (or emulated) exchange: always in ranges, so all but the last range's
+            # transfer hides behind the next range's solve; ranges of at least
+            # OVERLAP_MIN_ROWS_W rows still fill the GPU's launches
+            return max(1, min(c, shard // self.OVERLAP_MIN_ROWS_W))
+        if n_total * self.kp * (4 if self.split else 2) < self.OVERLAP_MIN_BYTES or \
+                shard // c < self.OVERLAP_MIN_ROWS:
             return 1
         return c
 
@@ -387,8 +413,8 @@ class ALSTrainer:
         ctx = self.ctx
         self.Xb_local = self._operand(self.X)
         self.Yb_local = self._operand(self.Y)
-        self.Xb = self.lay_u.gather(self.Xb_local, ctx)
-        self.Yb = self.lay_i.gather(self.Yb_local, ctx)
+        self.Xb = self.lay_u.gather(self.Xb_local, ctx, name="X")
+        self.Yb = self.lay_i.gather(self.Yb_local, ctx, name="Y")
         self.fail_count = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.iterations_done = 0
 
@@ -480,7 +506,7 @@ class ALSTrainer:
             self.events.append((label, ev))
 
     def _half_step(self, parts, src_own_f32, src_full_bf16, dst_f32, dst_b_local, lay, name,
-                   dst_full=None):
+                   dst_full=None, mat=None):
         ctx = self.ctx
         yty = None
         self._mark(name + ".start")
@@ -499,7 +525,7 @@ class ALSTrainer:
                 self._mark(name + ".solve")
         # range c's bf16 rows are exchanged while range c+1 is solved
         with tracing.range(name + ".solve+allgather"):
-            out = lay.gather(dst_b_local, ctx, overlap_with=solve, out=dst_full)
+            out = lay.gather(dst_b_local, ctx, overlap_with=solve, out=dst_full, name=mat)
         self._mark(name + ".exchange")
         return out
 
@@ -530,9 +556,9 @@ class ALSTrainer:
             watchdog.heartbeat("als.iteration")
             # items given users, then users given items (MLlib order)
             self.Yb = self._half_step(self.csr_i_parts, self.X, self.Xb, self.Y, self.Yb_local,
-                                      self.lay_i, "als.items", self.Yb)
+                                      self.lay_i, "als.items", self.Yb, "Y")
             self.Xb = self._half_step(self.csr_u_parts, self.Y, self.Yb, self.X, self.Xb_local,
-                                      self.lay_u, "als.users", self.Xb)
+                                      self.lay_u, "als.users", self.Xb, "X")
 
     def train(self, iterations: int, checkpoint_dir: Optional[str] = None,
               checkpoint_interval: int = 0, fingerprint: str = "",
@@ -543,12 +569,14 @@ class ALSTrainer:
         """Initialise (or resume from ``checkpoint_dir``) and run ``iterations`` iterations,
         checkpointing every ``checkpoint_interval``; a completed run removes its checkpoint."""
         done = 0
+        t0 = time.perf_counter()
         use_ckpt = bool(checkpoint_dir) and checkpoint_interval > 0
         if use_ckpt:
             done = self.load_checkpoint(checkpoint_dir, fingerprint)
         self.resumed_from = done
         if done == 0:
             self.init_factors(x_init, y_init, x_keys, y_keys)
+        self._lap("init_ms", t0)
         done = min(done, iterations)
         while done < iterations:
             step = iterations - done
@@ -562,16 +590,28 @@ class ALSTrainer:
                 [(time.perf_counter() - t_it) * 1e3 / step] * step)
             done += step
             if use_ckpt and done < iterations and done % checkpoint_interval == 0:
+                t_ck = time.perf_counter()
                 with tracing.range("als.checkpoint"):
                     self.save_checkpoint(checkpoint_dir, done, fingerprint)
+                self._lap("checkpoint_ms", t_ck)
         watchdog.get().end_heartbeats()
         dist.check_collectives(self.ctx)
+        t_f = time.perf_counter()
         out = self.factors()
+        self._lap("factors_ms", t_f)
         if use_ckpt:
+            t_ck = time.perf_counter()
             dist.barrier(self.ctx)
             if self.ctx.is_main:
                 shutil.rmtree(checkpoint_dir, ignore_errors=True)
+            self._lap("checkpoint_ms", t_ck)
         return out
+
+    def _lap(self, name: str, t0: float) -> None:
+        """Adds the milliseconds since ``t0`` (device work included) to ``timings[name]``."""
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        self.timings[name] = self.timings.get(name, 0.0) + (time.perf_counter() - t0) * 1e3
 
     def factors(self, gather: bool = True) -> ALSFactors:
         """Full fp32 factors (all-gathered from the owned shards)."""

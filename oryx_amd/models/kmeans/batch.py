@@ -66,6 +66,8 @@ class KMeansUpdate(MLUpdate):
         self.resident_history = True if rh is None else bool(rh)
         self.history: Optional[FeatureHistory] = None
         self.phase_seconds: Dict[str, float] = {}
+        # the "train" phase broken down (kmeans_train's timings; accumulates like the above)
+        self.train_phases: Dict[str, float] = {}
         if self.max_iterations <= 0 or self.number_of_runs <= 0:
             raise ValueError("iterations and runs must be > 0")
         if self.initialization_strategy not in _INIT_STRATEGIES:
@@ -131,20 +133,24 @@ class KMeansUpdate(MLUpdate):
         # invariant, and the fp32 distance expansion |x|^2 - 2 x.c + |c|^2 loses everything to
         # cancellation when features carry a large common offset; the shift comes back on the
         # centers in float64
+        t0 = time.perf_counter()
         s = torch.stack([x64.sum(0), torch.full((x64.shape[1],), float(n), dtype=torch.float64,
                                                  device=x64.device)])
         if sharded:
             dist.all_reduce_sum(s, ctx)
         shift = s[0] / s[1].clamp_min(1.0)
         x = (x64 - shift).float()
-        t0 = time.perf_counter()
+        tm = self.train_phases
+        if x.device.type == "cuda":
+            torch.cuda.synchronize(x.device)
+        tm["shift"] = tm.get("shift", 0.0) + time.perf_counter() - t0
         # sharded: this rank's share of the records; otherwise every rank parsed everything
         # and takes a disjoint slice
         local = x if sharded else x[ctx.rank::ctx.world_size].contiguous()
         res = km_ops.kmeans_train(local, k, self.max_iterations, self.number_of_runs,
                                   self.initialization_strategy, seed=rng.next_seed(),
                                   ctx=ctx, precision=self.precision,
-                                  reseed_empty=self.reseed_empty)
+                                  reseed_empty=self.reseed_empty, timings=tm)
         centers = (res.centers.double() + shift).cpu().numpy()
         sizes = res.counts.cpu().numpy()
         self.phase_seconds["train"] = self.phase_seconds.get("train", 0.0) + \

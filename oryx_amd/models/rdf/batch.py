@@ -296,6 +296,8 @@ class RDFUpdate(MLUpdate):
         self.resident_history = True if rh is None else bool(rh)
         self.history: Optional[FeatureHistory] = None
         self.phase_seconds: Dict[str, float] = {}
+        # the "train" phase broken down (train_forest's timings; accumulates like the above)
+        self.train_phases: Dict[str, float] = {}
 
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
@@ -419,7 +421,7 @@ class RDFUpdate(MLUpdate):
             else 0
         tgt = target[sl]
         trained = rdf_ops.train_forest(data, tgt, C, self.num_trees, max_depth, impurity,
-                                       seed=seed, ctx=ctx)
+                                       seed=seed, ctx=ctx, timings=self.train_phases)
         self._tick("train", t0)
         log.info("RDF %d trees depth %d on %d examples x %d predictors: %.3fs", self.num_trees,
                  max_depth, n_all, P, time.perf_counter() - t0)

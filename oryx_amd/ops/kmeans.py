@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import math
 import os
+import time
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -520,13 +521,30 @@ def lloyd_step(pts: PointSet, centers: torch.Tensor, ctx, workspace=None,
 def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
                  init: str = "k-means||", seed: int = 0, epsilon: float = 1e-4,
                  ctx: Optional[dist.DistContext] = None,
-                 precision: Optional[str] = None, reseed_empty: bool = True) -> KMeansResult:
+                 precision: Optional[str] = None, reseed_empty: bool = True,
+                 timings: Optional[dict] = None) -> KMeansResult:
     """Train k-means on this rank's rows ``x`` (the union over ranks is the data).
+
+    ``timings``: when given, seconds per phase are added to it (``points`` -- the point set
+    and its bf16 copy, ``init``, ``lloyd`` with ``lloyd_steps``, ``reseed``, ``final``), each
+    closed by a device synchronize, so a generation can attribute its ``train`` time.
 
     ``reseed_empty``: a cluster left without points by a Lloyd step is moved to the point
     farthest from its center (deliberate difference, the default); False keeps its old
     center as MLlib's Lloyd loop does (``KMeans.runAlgorithm``: only clusters with points are
     updated), so an empty cluster can survive into the model with size 0."""
+    dev0 = x.x.device if isinstance(x, PointSet) else x.device
+    mark = [time.perf_counter()]
+
+    def lap(name):
+        if timings is None:
+            return
+        if dev0.type == "cuda":
+            torch.cuda.synchronize(dev0)
+        t = time.perf_counter()
+        timings[name] = timings.get(name, 0.0) + t - mark[0]
+        mark[0] = t
+
     pts = _as_points(x)
     x = pts.x
     ctx = ctx or dist.DistContext(device=x.device)
@@ -535,6 +553,7 @@ def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
     if pts.xb is not None:
         ws = (torch.empty(pts.n, dtype=torch.int32, device=pts.device),
               torch.empty(pts.n, dtype=torch.float32, device=pts.device))
+    lap("points")
     for run in range(max(1, runs)):
         gen = torch.Generator()
         gen.manual_seed((seed * 7919 + run * 104729 + ctx.rank) & ((1 << 62) - 1))
@@ -542,6 +561,7 @@ def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
             centers = _init_random(x, k, gen, ctx)
         else:
             centers = _init_parallel(pts, k, gen, ctx)
+        lap("init")
         kk = centers.shape[0]
         it = 0
         for it in range(1, max_iterations + 1):
@@ -550,14 +570,19 @@ def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
             new, counts, d2, n_empty = lloyd_step(pts, centers, ctx, ws, precision)
             moved = None
             if n_empty and reseed_empty:
+                lap("lloyd")
                 # re-seed empty clusters at the points farthest from their centers
                 far = _farthest_points(x, d2, n_empty, ctx)
                 if far.shape[0] == n_empty:
                     new[counts == 0] = far
                     moved = float("inf")
+                lap("reseed")
             if moved is None:
                 moved = (new - centers).pow(2).sum(1).max().item() if kk else 0.0
             centers = new
+            if timings is not None:
+                timings["lloyd_steps"] = timings.get("lloyd_steps", 0) + 1
+            lap("lloyd")
             if moved <= epsilon * epsilon:
                 break
         idx, d2 = assign(pts, centers, exact=True)
@@ -569,6 +594,7 @@ def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
         watchdog.get().end_heartbeats()
         dist.check_collectives(ctx)
         res = KMeansResult(centers, counts, float(cost), it)
+        lap("final")
         if best is None or res.cost < best.cost:
             best = res
     return best

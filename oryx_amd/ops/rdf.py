@@ -28,6 +28,7 @@ On CPU the same algorithm runs with ``index_add`` (tests / the ``local[*]`` plum
 from __future__ import annotations
 
 import math
+import time
 import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
@@ -511,8 +512,22 @@ def _feature_subset_size(P: int, num_trees: int, classification: bool) -> int:
 def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_trees: int,
                  max_depth: int, impurity: str, seed: int = 0,
                  ctx: Optional[dist.DistContext] = None,
-                 feature_subset: Optional[int] = None) -> TrainedForest:
-    """``target``: int class encodings (``num_classes`` > 0) or float values (regression)."""
+                 feature_subset: Optional[int] = None,
+                 timings: Optional[dict] = None) -> TrainedForest:
+    """``target``: int class encodings (``num_classes`` > 0) or float values (regression).
+    ``timings``: seconds per phase are added to it (``prep`` -- targets and bootstrap
+    weights, ``levels`` -- the level loop with the overlapped host node builds, ``tail`` --
+    the last level's node build), each closed by a device synchronize."""
+    t_mark = [time.perf_counter()]
+
+    def lap(name):
+        if timings is None:
+            return
+        if data.Xb.device.type == "cuda":
+            torch.cuda.synchronize(data.Xb.device)
+        t = time.perf_counter()
+        timings[name] = timings.get(name, 0.0) + t - t_mark[0]
+        t_mark[0] = t
     classification = num_classes > 0
     kind = impurity if classification else "variance"
     if classification and kind not in ("gini", "entropy"):
@@ -559,8 +574,10 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     Fs = feature_subset or _feature_subset_size(P, T, classification)
     if dev.type == "cuda" and _GROUPED and _DEVICE_LOOP and T * (1 << max_depth) <= 8191 and \
             n * T < (1 << 31) and _split_kernel_ok(data, S):
+        lap("prep")
         return _train_device(data, label, y, y_shift, S, classification, kind, weight, T, Fs,
-                             max_depth, seed, ctx)
+                             max_depth, seed, ctx, lap)
+    lap("prep")
     node_of = torch.zeros((T, n), dtype=torch.int32, device=dev)
     roots = [TrainedNode("r") for _ in range(T)]
     level_nodes: List[List[Optional[TrainedNode]]] = [[r] for r in roots]
@@ -683,6 +700,7 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
     if pending is not None:
         build_level(*pending)
     watchdog.get().end_heartbeats()
+    lap("levels")
     return TrainedForest(roots, predictor_counts, classification)
 
 
@@ -698,7 +716,7 @@ def _totals_ok(width: int, S: int) -> bool:
 
 def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classification: bool,
                   kind: str, weight, T: int, Fs: int, max_depth: int, seed: int,
-                  ctx: dist.DistContext) -> TrainedForest:
+                  ctx: dist.DistContext, lap=None) -> TrainedForest:
     """The level loop with no host round trip inside it (GPU, forests whose widest level fits
     the counting sort's key space).  Level d has 2^d node slots per tree (slots past a tree's
     real nodes stay empty: no rows, so no pieces, and they come out as leaves); per level the
@@ -908,8 +926,12 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
         pending.append(lv)
         if live == 0:
             break
+    if lap is not None:
+        lap("levels")
     while pending:
         build(pending.pop(0))
+    if lap is not None:
+        lap("tail")
     watchdog.get().end_heartbeats()
     return TrainedForest(roots, predictor_counts, classification)
 

@@ -48,6 +48,8 @@ class DistContext:
     forced: bool = False
     # one-shot peer-mapped all-reduce for small fp32 payloads (parallel/ipc.py), or None
     ipc: Optional[object] = None
+    # peer-push all-gather of the replicated factor matrices (parallel/ipc.py), or None
+    ipc_gather: Optional[object] = None
     # one process playing rank `rank` of a `world_size` world (bench.py --emulate-world): the
     # layouts are the real world's, collectives move nothing (an all-gather writes only this
     # rank's slot, an all-reduce is the identity)
@@ -121,6 +123,7 @@ def init_from_env(device: Optional[str] = None, backend: Optional[str] = None,
         atexit.register(_destroy_groups)
         from . import ipc
         ctx.ipc = ipc.maybe_create(ctx)
+        ctx.ipc_gather = ipc.maybe_create_gather(ctx)
     _context = ctx
     return ctx
 
@@ -154,7 +157,18 @@ def run_info(ctx: DistContext) -> dict:
     else:
         allv, ws, backend = [me], 1, None
     return {"world_size": ws, "backend": backend, "ranks": allv,
-            "ipc_allreduce": ctx.ipc is not None}
+            "ipc_allreduce": ctx.ipc is not None, "allgather": allgather_kind(ctx)}
+
+
+def allgather_kind(ctx: DistContext) -> str:
+    """Which exchange the replicated factor matrices go through."""
+    if ctx.emulated:
+        return "emulated (nothing moved)"
+    if not ctx.is_distributed:
+        return "none (one rank)"
+    if ctx.ipc_gather is not None:
+        return "ipc-push (peer-mapped, per-range epoch flags)"
+    return "rccl" if ctx.backend == "nccl" else str(ctx.backend)
 
 
 def get_context() -> DistContext:
@@ -236,9 +250,12 @@ def all_reduce_sum(t: torch.Tensor, ctx: DistContext) -> torch.Tensor:
 
 
 def check_collectives(ctx: DistContext) -> None:
-    """Raise if a one-shot all-reduce timed out waiting for a peer (synchronises)."""
+    """Raise if a one-shot all-reduce or a peer-push all-gather timed out waiting for a peer
+    (synchronises)."""
     if ctx.ipc is not None and ctx.ipc.calls:
         ctx.ipc.check()
+    if ctx.ipc_gather is not None and ctx.ipc_gather.pushes:
+        ctx.ipc_gather.check()
 
 
 def global_rank(ctx: DistContext, rank: int) -> int:

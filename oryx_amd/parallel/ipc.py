@@ -35,7 +35,7 @@ from .. import native
 
 log = logging.getLogger(__name__)
 
-__all__ = ["IpcAllReduce", "maybe_create"]
+__all__ = ["IpcAllReduce", "IpcAllGather", "maybe_create", "maybe_create_gather"]
 
 
 class IpcAllReduce:
@@ -142,6 +142,217 @@ class IpcAllReduce:
         if self.W > 1 or self.ctx.forced:
             tdist.all_reduce(flag, group=self.ctx.group)
         return int(flag.item()) == 0
+
+
+class IpcAllGather:
+    """Peer-push all-gather of replicated row matrices (kernel: ``ipc_allgather.hip``).
+
+    :meth:`buffer` hands out a matrix that every rank holds a peer mapping of (collective:
+    every rank calls it with the same name and shape; the mapping is made once and kept while
+    the shape stays).  An exchange is :meth:`begin` (this rank may be overwritten from now on),
+    one :meth:`push` per row range (its solved rows into every rank's copy, on a side stream,
+    after the kernels already queued on the current stream) and :meth:`end` (the current
+    stream waits for the side stream and for every peer's rows).  Waits are bounded; a timeout
+    sets the error flag that :meth:`check` raises on."""
+
+    GROUPS = 32            # workgroups per pushed range
+
+    def __init__(self, ctx, timeout_s: float = 120.0):
+        self.ctx = ctx
+        self.lib = native.require_kernels()
+        self.W, self.rank = ctx.world_size, ctx.rank
+        self.timeout_s = float(timeout_s)
+        lim = (ctypes.c_int * 4)()
+        self.lib.oryx_ipc_gather_limits(lim)
+        self.max_ranks, self.max_mats, self.max_chunks, self.max_groups = list(lim)
+        if self.W > self.max_ranks:
+            raise RuntimeError("IPC all-gather: %d ranks > %d" % (self.W, self.max_ranks))
+        self.group = ctx.control if ctx.control is not None else ctx.group
+        self._hs = int(self.lib.oryx_ipc_handle_size())
+        # flag buffers: own (uncached, zeroed) and every peer's mapping of theirs
+        own = ctypes.c_void_p()
+        native.check(self.lib.oryx_ipc_alloc(int(self.lib.oryx_ipc_gather_flag_bytes()),
+                                             ctypes.byref(own)), "oryx_ipc_alloc")
+        self._flags_own = own.value
+        self._opened: List[int] = []
+        h = (ctypes.c_char * self._hs)()
+        native.check(self.lib.oryx_ipc_handle(ctypes.c_void_p(self._flags_own), h),
+                     "oryx_ipc_handle")
+        ptrs = self._exchange(bytes(h), 0, self._flags_own)
+        self._flags = (ctypes.c_void_p * self.W)(*ptrs)
+        self.err = torch.zeros(1, dtype=torch.int32, device=ctx.device)
+        self.side = torch.cuda.Stream(device=ctx.device)
+        self._mats = {}        # name -> dict(t, m, epoch, dst, opened)
+        self.pushes = 0
+
+    def _exchange(self, handle: bytes, offset: int, own_ptr: int) -> List[int]:
+        """All ranks' (handle, offset) -> one pointer per rank (own one as is, peers' opened)."""
+        allh: List[Optional[tuple]] = [None] * self.W
+        if self.W > 1:
+            tdist.all_gather_object(allh, (handle, int(offset)), group=self.group)
+        else:
+            allh = [(handle, int(offset))]
+        out = []
+        for r, (hb, off) in enumerate(allh):
+            if r == self.rank:
+                out.append(own_ptr)
+                continue
+            p = ctypes.c_void_p()
+            native.check(self.lib.oryx_ipc_open(hb, ctypes.byref(p)), "oryx_ipc_open")
+            self._opened.append(p.value)
+            out.append(p.value + off)
+        return out
+
+    def buffer(self, name: str, shape, dtype) -> torch.Tensor:
+        """The replicated matrix ``name`` (collective on first use or a new shape)."""
+        shape = tuple(int(x) for x in shape)
+        e = self._mats.get(name)
+        if e is not None and tuple(e["t"].shape) == shape and e["t"].dtype == dtype:
+            return e["t"]
+        if e is None and len(self._mats) >= self.max_mats:
+            raise RuntimeError("IPC all-gather: more than %d matrices" % self.max_mats)
+        m = e["m"] if e is not None else len(self._mats)
+        if e is not None:
+            # every peer unmaps the old copy before any rank frees it
+            for p in e["opened"]:
+                self.lib.oryx_ipc_close(ctypes.c_void_p(p))
+                self._opened.remove(p)
+            if self.W > 1:
+                tdist.barrier(group=self.group)
+        t = torch.empty(shape, dtype=dtype, device=self.ctx.device)
+        h = (ctypes.c_char * self._hs)()
+        off = ctypes.c_longlong()
+        native.check(self.lib.oryx_ipc_handle_range(ctypes.c_void_p(t.data_ptr()), h,
+                                                    ctypes.byref(off)), "oryx_ipc_handle_range")
+        before = list(self._opened)
+        ptrs = self._exchange(bytes(h), off.value, t.data_ptr())
+        opened = [p for p in self._opened if p not in before]
+        self._mats[name] = {"t": t, "m": m, "epoch": e["epoch"] if e is not None else 0,
+                            "dst": (ctypes.c_void_p * self.W)(*ptrs), "opened": opened}
+        return t
+
+    def owns(self, t: torch.Tensor) -> Optional[str]:
+        for name, e in self._mats.items():
+            if e["t"].data_ptr() == t.data_ptr() and e["t"].shape == t.shape:
+                return name
+        return None
+
+    def begin(self, name: str) -> None:
+        e = self._mats[name]
+        e["epoch"] += 1
+        native.check(self.lib.oryx_ipc_gather_ready(
+            ctypes.c_void_p(self._flags_own), e["m"], e["epoch"] & 0xFFFFFFFF,
+            ctypes.c_void_p(native.stream_ptr(self.ctx.device))), "oryx_ipc_gather_ready")
+        e["side_ready"] = False
+
+    def push(self, name: str, src: torch.Tensor, row0: int, chunks: int, c: int) -> None:
+        """Push ``src`` (contiguous rows) into row ``row0`` of every rank's copy, as range
+        ``c`` of ``chunks`` of this exchange."""
+        e = self._mats[name]
+        t = e["t"]
+        row_bytes = t.stride(0) * t.element_size()
+        cur = torch.cuda.current_stream(self.ctx.device)
+        self.side.wait_stream(cur)
+        src = src.contiguous()
+        with torch.cuda.stream(self.side):
+            native.check(self.lib.oryx_ipc_gather_push(
+                ctypes.c_void_p(src.data_ptr()), src.numel() * src.element_size(), e["dst"],
+                int(row0) * row_bytes, self._flags, self.W, self.rank, e["m"], int(chunks),
+                int(c), self.GROUPS, e["epoch"] & 0xFFFFFFFF, self.timeout_s,
+                ctypes.c_void_p(self.err.data_ptr()),
+                ctypes.c_void_p(native.stream_ptr(self.ctx.device))),
+                "oryx_ipc_gather_push")
+        # the source rows must outlive the side stream's read of them
+        src.record_stream(self.side)
+        self.pushes += 1
+
+    def end(self, name: str, chunks: int) -> None:
+        e = self._mats[name]
+        cur = torch.cuda.current_stream(self.ctx.device)
+        cur.wait_stream(self.side)
+        native.check(self.lib.oryx_ipc_gather_wait(
+            ctypes.c_void_p(self._flags_own), self.W, e["m"], int(chunks), self.GROUPS,
+            e["epoch"] & 0xFFFFFFFF, self.timeout_s, ctypes.c_void_p(self.err.data_ptr()),
+            ctypes.c_void_p(native.stream_ptr(self.ctx.device))), "oryx_ipc_gather_wait")
+
+    def check(self) -> None:
+        e = int(self.err.item())
+        if e:
+            self.err.zero_()
+            raise RuntimeError("IPC all-gather: rank %d never arrived" % (e - 1))
+
+    def self_test(self) -> bool:
+        """Gather rank-dependent rows both ways (peer push and torch.distributed); True when
+        every rank matched bitwise."""
+        ok = True
+        name = "__selftest__"
+        try:
+            W, rows, cols = self.W, 1000, 64
+            C = 3
+            cr = -(-rows // C)
+            out = self.buffer(name, (C * W * cr, cols), torch.bfloat16)
+            base = torch.arange(C * cr * cols, device=self.ctx.device, dtype=torch.float32)
+            local = ((base % 251) * (self.rank + 1) + self.rank).to(torch.bfloat16) \
+                .reshape(C * cr, cols)
+            self.begin(name)
+            for c in range(C):
+                self.push(name, local[c * cr:(c + 1) * cr], (c * W + self.rank) * cr, C, c)
+            self.end(name, C)
+            torch.cuda.synchronize(self.ctx.device)
+            self.check()
+            ref = torch.empty_like(out)
+            for c in range(C):
+                blk = local[c * cr:(c + 1) * cr].contiguous()
+                parts = list(ref[c * W * cr:(c + 1) * W * cr].chunk(W, 0))
+                if W > 1:
+                    tdist.all_gather(parts, blk, group=self.ctx.group)
+                else:
+                    parts[0].copy_(blk)
+            ok = bool(torch.equal(out.view(torch.int16), ref.view(torch.int16)))
+        except Exception as e:   # noqa: BLE001 -- any failure disables the path
+            log.warning("IPC all-gather self-test failed on rank %d: %s", self.rank, e)
+            ok = False
+        flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=self.ctx.device)
+        if self.W > 1:
+            tdist.all_reduce(flag, group=self.ctx.group)
+        return int(flag.item()) == 0
+
+    def close(self) -> None:
+        for p in self._opened:
+            self.lib.oryx_ipc_close(ctypes.c_void_p(p))
+        self._opened = []
+        self._mats = {}
+        if self._flags_own:
+            self.lib.oryx_ipc_free(ctypes.c_void_p(self._flags_own))
+            self._flags_own = None
+
+
+def maybe_create_gather(ctx) -> Optional[IpcAllGather]:
+    """The node's peer-push all-gather when enabled and its self-test passes (collective);
+    else None.  ``ORYX_IPC_ALLGATHER``: 1 (default) on for one-node RCCL worlds, 0 off,
+    ``any`` also under gloo (ranks sharing one GPU in tests)."""
+    mode = os.environ.get("ORYX_IPC_ALLGATHER", "1")
+    if mode == "0" or ctx.device.type != "cuda" or ctx.world_size < 2 or \
+            (ctx.backend != "nccl" and mode != "any"):
+        return None
+    if ctx.world_size > 16 or ctx.group is not None or not _single_node(ctx):
+        return None
+    try:
+        ag = IpcAllGather(ctx)
+    except Exception as e:   # noqa: BLE001
+        log.warning("IPC all-gather unavailable on rank %d: %s", ctx.rank, e)
+        ag = None
+    flag = torch.tensor([0 if ag is not None else 1], dtype=torch.int32, device=ctx.device)
+    tdist.all_reduce(flag, group=ctx.group)
+    if int(flag.item()) != 0:
+        if ag is not None:
+            ag.close()
+        return None
+    if not ag.self_test():
+        ag.close()
+        return None
+    log.info("IPC peer-push all-gather enabled (%d ranks)", ctx.world_size)
+    return ag
 
 
 def _single_node(ctx) -> bool:

@@ -46,7 +46,7 @@ DEV = os.environ.get("ORYX_MR_DEVICE", "cuda:0")
 SMALL = DEV == "cpu"
 ctx = dist.init_from_env(device=DEV, backend="gloo")
 W, R = ctx.world_size, ctx.rank
-res = {"world": W, "ipc": ctx.ipc is not None}
+res = {"world": W, "ipc": ctx.ipc is not None, "allgather": dist.allgather_kind(ctx)}
 
 # ------------------------------------------------------------------ ALS trainer
 from oryx_amd import ingest
@@ -137,6 +137,7 @@ if ctx.is_main:
     layer.close()
 else:
     res["joined"] = layer.run_follower()
+res["pushes"] = ctx.ipc_gather.pushes if ctx.ipc_gather is not None else 0
 with open(os.path.join(out_dir, "res%d.json" % R), "w") as fh:
     json.dump(res, fh)
 '''
@@ -210,15 +211,20 @@ def _run_worlds(tmp_path, device):
     script = tmp_path / "worker.py"
     script.write_text(WORKER.replace("ROOT", repr(ROOT)))
     outs = {}
-    for world in (1, 2):
-        d = tmp_path / ("w%d" % world)
+    # "push": world 2 with the factor exchange through the peer-push all-gather
+    # (ipc_allgather.hip) instead of gloo's staged all-gather
+    runs = (1, 2) if device == "cpu" else (1, 2, "push")
+    for world in runs:
+        d = tmp_path / ("w%s" % world)
         d.mkdir()
         env = dict(os.environ, OMP_NUM_THREADS="2", ORYX_IPC_ALLREDUCE="any",
+                   ORYX_IPC_ALLGATHER="any" if world == "push" else "0",
                    ORYX_MR_DEVICE=device,
                    HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY",
                                                              "0"))
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-               "--nproc-per-node=%d" % world, "--master-addr=127.0.0.1",
+               "--nproc-per-node=%d" % (2 if world == "push" else world),
+               "--master-addr=127.0.0.1",
                "--master-port=%d" % _port(), str(script), str(d)]
         r = subprocess.run(cmd, env=env, timeout=400, capture_output=True, text=True)
         errs = "".join(open(os.path.join(d, f)).read() for f in sorted(os.listdir(d))
@@ -259,6 +265,21 @@ def _run_worlds(tmp_path, device):
     assert worst < 5e-2, worst
     a1, a2 = _auc(X1, Y1, test, 300), _auc(X2, Y2, test, 300)
     assert a1 > 0.7 and abs(a1 - a2) < 1e-3, (a1, a2)
+    if "push" not in outs:
+        return
+    # ---- peer-push all-gather: bitwise the gloo-staged exchange's results
+    rp = json.loads((outs["push"] / "res0.json").read_text())
+    assert rp["allgather"].startswith("ipc-push") and rp["pushes"] > 0, rp
+    assert not res2["allgather"].startswith("ipc-push"), res2
+    for k, prec, _ in cases:
+        a = torch.load(outs[2] / ("trainer_%d_%s.pt" % (k, prec)))
+        b = torch.load(outs["push"] / ("trainer_%d_%s.pt" % (k, prec)))
+        for m in ("X", "Y"):
+            assert torch.equal(a[m], b[m]), (k, prec, m)
+    Xp, Yp, Kp, _ = _read_model(outs["push"] / "gen")
+    assert Kp == K2 and set(Xp) == set(X2)
+    assert all(np.array_equal(X2[i], Xp[i]) for i in X2)
+    assert all(np.array_equal(Y2[i], Yp[i]) for i in Y2)
 
 
 @pytest.mark.gpu
