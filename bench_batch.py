@@ -25,6 +25,23 @@ import sys
 import tempfile
 import time
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _cprofile_top(prof, n: int = 30):
+    """The n functions with the most cumulative and the most own time."""
+    import pstats
+    st = pstats.Stats(prof)
+    rows = []
+    for (fn, line, name), (cc, nc, tt, ct, _) in st.stats.items():
+        rows.append((ct, tt, nc, "%s:%d(%s)" % (os.path.relpath(fn, ROOT)
+                                                  if fn.startswith(ROOT) else fn, line, name)))
+    def fmt(rs):
+        return [{"cum_s": round(r[0], 4), "own_s": round(r[1], 4), "calls": r[2], "fn": r[3]}
+                for r in rs]
+    return {"by_cumulative": fmt(sorted(rows, reverse=True)[:n]),
+            "by_own": fmt(sorted(rows, key=lambda r: -r[1])[:n])}
+
 
 def main(argv=None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
@@ -44,6 +61,12 @@ def main(argv=None) -> int:
                          "new ratings and trains on them plus all earlier ones (the past part "
                          "files -- the resident parsed history's steady state)")
     ap.add_argument("--next-ratings", type=int, default=1_000_000)
+    ap.add_argument("--no-warm-up", action="store_true",
+                    help="skip the batch layer's start-up warm-up (first-call costs then land "
+                         "in the first generation)")
+    ap.add_argument("--cprofile", action="store_true",
+                    help="profile the first generation's host side (cProfile): the top "
+                         "functions by cumulative time go into the record")
     ap.add_argument("--test-fraction", type=float, default=None,
                     help="oryx.ml.eval.test-fraction (the reference default is 0.1: the newest "
                          "tenth of the interval's data is held out and evaluated); default 0.0 "
@@ -131,6 +154,10 @@ def main(argv=None) -> int:
         layer._context = layer.layer_context()
         layer._update = layer.load_update_instance()
         layer.build_input_consumer()
+        # what BatchLayer.start does before its first interval (outside the timed generation,
+        # reported as startup_warm_up_s)
+        if not args.no_warm_up:
+            layer.warm_up()
         rng = np.random.default_rng(7)
         now = int(time.time() * 1000)
 
@@ -190,9 +217,17 @@ def main(argv=None) -> int:
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         dist.barrier(ctx)
+        prof = None
+        if args.cprofile:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         layer.run_interval(now)
         t_gen = time.perf_counter() - t0
+        if prof is not None:
+            prof.disable()
+            cprof_top = _cprofile_top(prof)
         sharded_path = layer._sharded()
         # the first generation's phases (phase_seconds accumulates over generations)
         first_phases = dict(getattr(layer._update, "phase_seconds", {}))
@@ -255,6 +290,8 @@ def main(argv=None) -> int:
             "n_gpus": ctx.world_size, "generation_s": t_gen, "log_append_s": t_ingest,
             "phase_s": phases,
             "train_phase_s": first_train,
+            "startup_warm_up_s": layer.warm_up_s,
+            "cprofile_top": cprof_top if args.cprofile and ctx.is_main else None,
             "update_messages": int(sum(ends)),
             "attributed_s": attributed, "unattributed_s": t_gen - attributed,
             "later_generations": later,

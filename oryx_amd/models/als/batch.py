@@ -380,6 +380,35 @@ class ALSUpdate(MLUpdate):
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
 
+    def warm_up(self, context) -> None:
+        """Start-up warm-up (``BatchLayer.warm_up``): a tiny build on this rank's device with
+        every configured rank and the configured precision -- the device aggregation, the
+        trainer's solve / Gramian kernels, the keyed init and the row formatter load their
+        code objects here, not inside the first generation.  Local (no collectives)."""
+        ctx = self._ctx(context)
+        dev = ctx.device
+        if dev.type != "cuda":
+            return
+        local = dist.DistContext(device=dev)
+        feats = sorted({int(round(float(v))) for v in
+                        self.hyper_param_values[0].get_trial_values(max(1, self.candidates))})
+        rs = np.random.default_rng(1)
+        nu, ni, nnz = 512, 256, 8192
+        u = rs.integers(0, nu, nnz)
+        i = rs.integers(0, ni, nnz)
+        ts = rs.integers(0, 1000, nnz)
+        ud, idv, sd = aggregate_scores_device(u, i, np.ones(nnz), ts, self.implicit, dev,
+                                              to_host=False)
+        keys_u = np.arange(nu, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        keys_i = np.arange(ni, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)
+        for k in feats:
+            tr = ALSTrainer(k, 0.1, 1.0, self.implicit, ctx=local, seed=1,
+                            precision=self.precision, init_seed=ALS_INIT_SEED)
+            tr.prepare(ud, idv, sd.to(torch.float32), nu, ni)
+            f = tr.train(2, x_keys=keys_u, y_keys=keys_i)
+            textfmt.format_rows(f.X)
+        torch.cuda.synchronize(dev)
+
     def _history_for(self, device) -> Optional[RatingsHistory]:
         if not self.resident_history:
             return None

@@ -430,29 +430,77 @@ class ALSTrainer:
                 "n_users": self.n_users, "n_items": self.n_items, "k": self.k,
                 "fingerprint": str(fingerprint)}
 
-    def save_checkpoint(self, directory: str, iteration: int, fingerprint: str = "") -> None:
+    def save_checkpoint(self, directory: str, iteration: int, fingerprint: str = "",
+                        background: bool = False) -> None:
         """Write the factors after ``iteration`` (collective: every rank calls it; rank 0
-        writes one safetensors file and then ``latest.json``, both atomically)."""
-        from safetensors.torch import save_file
+        writes one safetensors file and then ``latest.json``, both atomically).
+
+        ``background``: rank 0 copies the factors to pinned host memory on a side stream and
+        a thread writes the files while the iterations go on (the copy overlaps compute, the
+        write overlaps everything); the next checkpoint or the end of the run waits for it
+        (:meth:`_finish_checkpoint`).  A crash before the write lands leaves the previous
+        checkpoint in place, which is all a checkpoint promises."""
         ctx = self.ctx
+        self._finish_checkpoint()
         f = self.factors()
         if ctx.is_main:
-            it_dir = os.path.join(directory, "it%d" % iteration)
-            os.makedirs(it_dir, exist_ok=True)
-            path = os.path.join(it_dir, "factors.safetensors")
-            save_file({"X": f.X.detach().cpu().contiguous(),
-                       "Y": f.Y.detach().cpu().contiguous()}, path + ".tmp",
-                      metadata={k: str(v) for k, v in
-                                self._layout(fingerprint, iteration).items()})
-            os.replace(path + ".tmp", path)
-            meta = os.path.join(directory, "latest.json")
-            with open(meta + ".tmp", "w") as fh:
-                json.dump(self._layout(fingerprint, iteration), fh)
-            os.replace(meta + ".tmp", meta)
-            for name in os.listdir(directory):
-                if name.startswith("it") and name != "it%d" % iteration:
-                    shutil.rmtree(os.path.join(directory, name), ignore_errors=True)
-        dist.barrier(ctx)
+            meta = self._layout(fingerprint, iteration)
+            if background and f.X.is_cuda:
+                import threading
+                side = getattr(self, "_ckpt_stream", None)
+                if side is None:
+                    side = self._ckpt_stream = torch.cuda.Stream(device=f.X.device)
+                hx = torch.empty(f.X.shape, dtype=f.X.dtype, pin_memory=True)
+                hy = torch.empty(f.Y.shape, dtype=f.Y.dtype, pin_memory=True)
+                side.wait_stream(torch.cuda.current_stream(f.X.device))
+                with torch.cuda.stream(side):
+                    hx.copy_(f.X, non_blocking=True)
+                    hy.copy_(f.Y, non_blocking=True)
+                    done = torch.cuda.Event()
+                    done.record(side)
+                f.X.record_stream(side)
+                f.Y.record_stream(side)
+                self._ckpt_cancel = threading.Event()
+                cancel = self._ckpt_cancel
+
+                def write():
+                    done.synchronize()
+                    if not cancel.is_set():
+                        self._write_checkpoint(directory, iteration, meta, hx, hy)
+                self._ckpt_thread = threading.Thread(target=write, name="als-checkpoint",
+                                                     daemon=True)
+                self._ckpt_thread.start()
+            else:
+                self._write_checkpoint(directory, iteration, meta, f.X.detach().cpu(),
+                                       f.Y.detach().cpu())
+        if not background:
+            dist.barrier(ctx)
+
+    def _write_checkpoint(self, directory: str, iteration: int, meta: dict, X, Y) -> None:
+        from safetensors.torch import save_file
+        it_dir = os.path.join(directory, "it%d" % iteration)
+        os.makedirs(it_dir, exist_ok=True)
+        path = os.path.join(it_dir, "factors.safetensors")
+        save_file({"X": X.contiguous(), "Y": Y.contiguous()}, path + ".tmp",
+                  metadata={k: str(v) for k, v in meta.items()})
+        os.replace(path + ".tmp", path)
+        mpath = os.path.join(directory, "latest.json")
+        with open(mpath + ".tmp", "w") as fh:
+            json.dump(meta, fh)
+        os.replace(mpath + ".tmp", mpath)
+        for name in os.listdir(directory):
+            if name.startswith("it") and name != "it%d" % iteration:
+                shutil.rmtree(os.path.join(directory, name), ignore_errors=True)
+
+    def _finish_checkpoint(self, cancel: bool = False) -> None:
+        """Wait for a background checkpoint write (``cancel``: drop it if not yet begun)."""
+        th = getattr(self, "_ckpt_thread", None)
+        if th is None:
+            return
+        if cancel:
+            self._ckpt_cancel.set()
+        th.join()
+        self._ckpt_thread = None
 
     def load_checkpoint(self, directory: str, fingerprint: str = "") -> int:
         """Restore the latest complete checkpoint if it matches this run (any world size);
@@ -578,6 +626,31 @@ class ALSTrainer:
             self.init_factors(x_init, y_init, x_keys, y_keys)
         self._lap("init_ms", t0)
         done = min(done, iterations)
+        try:
+            self._iterate_with_checkpoints(done, iterations, use_ckpt, checkpoint_dir,
+                                           checkpoint_interval, fingerprint)
+        except BaseException:
+            # a failed run keeps its newest checkpoint: let a write under way land first
+            self._finish_checkpoint()
+            raise
+        watchdog.get().end_heartbeats()
+        dist.check_collectives(self.ctx)
+        t_f = time.perf_counter()
+        out = self.factors()
+        self._lap("factors_ms", t_f)
+        if use_ckpt:
+            t_ck = time.perf_counter()
+            # the run is complete: a checkpoint write not yet started is dropped, one under
+            # way is finished, and the directory goes
+            self._finish_checkpoint(cancel=True)
+            dist.barrier(self.ctx)
+            if self.ctx.is_main:
+                shutil.rmtree(checkpoint_dir, ignore_errors=True)
+            self._lap("checkpoint_ms", t_ck)
+        return out
+
+    def _iterate_with_checkpoints(self, done, iterations, use_ckpt, checkpoint_dir,
+                                  checkpoint_interval, fingerprint) -> None:
         while done < iterations:
             step = iterations - done
             if use_ckpt:
@@ -592,20 +665,8 @@ class ALSTrainer:
             if use_ckpt and done < iterations and done % checkpoint_interval == 0:
                 t_ck = time.perf_counter()
                 with tracing.range("als.checkpoint"):
-                    self.save_checkpoint(checkpoint_dir, done, fingerprint)
+                    self.save_checkpoint(checkpoint_dir, done, fingerprint, background=True)
                 self._lap("checkpoint_ms", t_ck)
-        watchdog.get().end_heartbeats()
-        dist.check_collectives(self.ctx)
-        t_f = time.perf_counter()
-        out = self.factors()
-        self._lap("factors_ms", t_f)
-        if use_ckpt:
-            t_ck = time.perf_counter()
-            dist.barrier(self.ctx)
-            if self.ctx.is_main:
-                shutil.rmtree(checkpoint_dir, ignore_errors=True)
-            self._lap("checkpoint_ms", t_ck)
-        return out
 
     def _lap(self, name: str, t0: float) -> None:
         """Adds the milliseconds since ``t0`` (device work included) to ``timings[name]``."""

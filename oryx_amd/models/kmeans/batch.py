@@ -83,6 +83,27 @@ class KMeansUpdate(MLUpdate):
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
 
+    def warm_up(self, context) -> None:
+        """Start-up warm-up (``BatchLayer.warm_up``): k-means on a few thousand random points
+        of the schema's dimension with every configured k, on this rank's device (the assign
+        / accumulate / k-means|| kernels of those shapes load here).  Local."""
+        ctx = self._ctx(context)
+        dev = ctx.device
+        if dev.type != "cuda":
+            return
+        d = self.input_schema.get_num_predictors()
+        ks = sorted({int(round(float(v))) for v in
+                     self.hyper_param_values[0].get_trial_values(max(1, self.candidates))})
+        local = dist.DistContext(device=dev)
+        g = torch.Generator(device=dev).manual_seed(1)
+        for k in ks:
+            if k <= 1:
+                continue
+            x = torch.randn((max(4096, 4 * k), d), device=dev, generator=g)
+            km_ops.kmeans_train(x, k, 2, 1, self.initialization_strategy, seed=1, ctx=local,
+                                precision=self.precision, reseed_empty=self.reseed_empty)
+        torch.cuda.synchronize(dev)
+
     def _ctx(self, context) -> dist.DistContext:
         if isinstance(context, dist.DistContext):
             return context

@@ -302,6 +302,34 @@ class RDFUpdate(MLUpdate):
     def get_hyper_parameter_values(self):
         return self.hyper_param_values
 
+    def warm_up(self, context) -> None:
+        """Start-up warm-up (``BatchLayer.warm_up``): a forest of the configured size over a
+        few thousand random numeric rows of the schema's width, on this rank's device (the
+        binning, histogram, split, route and sort kernels load here).  Local."""
+        ctx = self._ctx(context)
+        dev = ctx.device
+        if dev.type != "cuda":
+            return
+        schema = self.input_schema
+        P = schema.get_num_predictors()
+        bins = max(2, int(round(float(self.hyper_param_values[0].get_trial_values(1)[0]))))
+        depth = max(1, int(round(float(self.hyper_param_values[1].get_trial_values(1)[0]))))
+        imp = str(self.hyper_param_values[2].get_trial_values(1)[0])
+        rs = np.random.default_rng(1)
+        X = rs.normal(0, 1, (8192, P))
+        data = rdf_ops.bin_features(X, [False] * P, [0] * P, bins, dev, seed=1,
+                                    threshold_source=X)
+        local = dist.DistContext(device=dev)
+        if schema.is_classification():
+            y = torch.from_numpy((X[:, 0] > 0).astype(np.int64))
+            rdf_ops.train_forest(data, y, 2, self.num_trees, depth,
+                                 imp if imp in ("gini", "entropy") else "gini", seed=1,
+                                 ctx=local)
+        else:
+            rdf_ops.train_forest(data, torch.from_numpy(X[:, 0].copy()), 0, self.num_trees,
+                                 depth, "variance", seed=1, ctx=local)
+        torch.cuda.synchronize(dev)
+
     def _ctx(self, context) -> dist.DistContext:
         if isinstance(context, dist.DistContext):
             return context

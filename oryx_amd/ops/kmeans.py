@@ -518,6 +518,26 @@ def lloyd_step(pts: PointSet, centers: torch.Tensor, ctx, workspace=None,
     return new, counts, d2, int((~nonempty).sum())
 
 
+def _final_assign(pts: "PointSet", centers: torch.Tensor, ws, precision: Optional[str]):
+    """Assignment of every point to the final centers (the model's cluster sizes) and the
+    exact fp32 squared distance to its center (the run's cost).  Certified fp32 argmin on
+    the MFMA kernel, then the distance to the assigned center computed directly per row (one
+    read of the points) -- instead of the exact full scan of every point against every
+    center, ~4x longer at 12.5M x 256 points, K = 1000."""
+    precision = precision or DEFAULT_PRECISION
+    if pts.xb is None or precision != "fp32" or pts.x.device.type != "cuda":
+        return assign(pts, centers, exact=True)
+    idx, _ = assign(pts, centers, out=ws, precision="fp32")
+    x, c = pts.x, centers.float()
+    d2 = torch.empty(pts.n, dtype=torch.float32, device=x.device)
+    step = max(1, (1 << 28) // max(1, x.shape[1] * 4))      # ~256 MB of differences
+    for lo in range(0, pts.n, step):
+        hi = min(pts.n, lo + step)
+        diff = x[lo:hi] - c.index_select(0, idx[lo:hi].long())
+        d2[lo:hi] = diff.mul_(diff).sum(1)
+    return idx.long(), d2
+
+
 def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
                  init: str = "k-means||", seed: int = 0, epsilon: float = 1e-4,
                  ctx: Optional[dist.DistContext] = None,
@@ -585,7 +605,7 @@ def kmeans_train(x, k: int, max_iterations: int, runs: int = 1,
             lap("lloyd")
             if moved <= epsilon * epsilon:
                 break
-        idx, d2 = assign(pts, centers, exact=True)
+        idx, d2 = _final_assign(pts, centers, ws, precision)
         cost = d2.double().sum()
         counts = torch.bincount(idx, minlength=kk).to(torch.int64)
         if ctx.is_distributed:
