@@ -217,6 +217,21 @@ def main(argv=None) -> int:
         if torch.cuda.is_available():
             torch.cuda.synchronize()
         dist.barrier(ctx)
+        # cyclic-GC passes inside the generation (a gen-2 pass stops the interpreter for as
+        # long as its walk over every tracked object takes)
+        import gc
+        gc_ms = {"n": 0, "total_ms": 0.0, "max_ms": 0.0}
+        gc_t = [None]
+
+        def _gc_cb(phase, info):
+            if phase == "start":
+                gc_t[0] = time.perf_counter()
+            elif gc_t[0] is not None:
+                dt = (time.perf_counter() - gc_t[0]) * 1e3
+                gc_ms["n"] += 1
+                gc_ms["total_ms"] += dt
+                gc_ms["max_ms"] = max(gc_ms["max_ms"], dt)
+        gc.callbacks.append(_gc_cb)
         prof = None
         if args.cprofile:
             import cProfile
@@ -225,6 +240,7 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         layer.run_interval(now)
         t_gen = time.perf_counter() - t0
+        gc.callbacks.remove(_gc_cb)
         if prof is not None:
             prof.disable()
             cprof_top = _cprofile_top(prof)
@@ -291,6 +307,7 @@ def main(argv=None) -> int:
             "phase_s": phases,
             "train_phase_s": first_train,
             "startup_warm_up_s": layer.warm_up_s,
+            "gc_in_generation": gc_ms if ctx.is_main else None,
             "cprofile_top": cprof_top if args.cprofile and ctx.is_main else None,
             "update_messages": int(sum(ends)),
             "attributed_s": attributed, "unattributed_s": t_gen - attributed,

@@ -269,6 +269,7 @@ class BatchLayer(AbstractLayer):
             self._run_sharded_main(ts, t_start)
             return
         records = drain_dataset(self._input_consumer)
+        n_records = len(records)
         ph = self.last_phases = {"drain": time.perf_counter() - t_start}
         faults.point("batch.interval", timestamp=ts, records=len(records))
         dctx = self._context.dist if self._context is not None else None
@@ -300,9 +301,13 @@ class BatchLayer(AbstractLayer):
             tp = time.perf_counter()
             save_interval_data(self.data_dir, ts, records)
             ph["save_data"] = time.perf_counter() - tp
+            tp = time.perf_counter()
+            del new_data, past
+            records = None
+            ph["release"] = time.perf_counter() - tp
         self.commit_input_offsets()
         rec = {"event": "batch_interval", "layer_id": self.id, "timestamp": ts,
-               "records": len(records), "seconds": time.perf_counter() - t_start}
+               "records": n_records, "seconds": time.perf_counter() - t_start}
         tracing.record(rec)
         if self.timings_file:
             with open(self.timings_file, "a") as f:

@@ -420,6 +420,11 @@ class MLUpdate(BatchLayerUpdate):
                     with open(os.path.join(candidate_path, TIMINGS_FILE_NAME), "w") as f:
                         json.dump(dict(timing, eval=ev if ev == ev else None), f)
         timing["eval"] = ev if ev == ev else None
+        # the candidate's train / test buffers (the whole interval's text for the apps that
+        # parse on the device) are freed here, as a phase of their own
+        t_r = time.perf_counter()
+        del train, test
+        self._phase("release", time.perf_counter() - t_r)
         tracing.record(dict(timing, event="candidate"))
         log.info("Model eval for params %s: %s (%s)", params, ev, candidate_path)
         return candidate_path, ev

@@ -450,21 +450,20 @@ class ALSTrainer:
                 side = getattr(self, "_ckpt_stream", None)
                 if side is None:
                     side = self._ckpt_stream = torch.cuda.Stream(device=f.X.device)
-                hx = torch.empty(f.X.shape, dtype=f.X.dtype, pin_memory=True)
-                hy = torch.empty(f.Y.shape, dtype=f.Y.dtype, pin_memory=True)
-                side.wait_stream(torch.cuda.current_stream(f.X.device))
-                with torch.cuda.stream(side):
-                    hx.copy_(f.X, non_blocking=True)
-                    hy.copy_(f.Y, non_blocking=True)
-                    done = torch.cuda.Event()
-                    done.record(side)
-                f.X.record_stream(side)
-                f.Y.record_stream(side)
+                # device copies the iterations cannot touch (at world 1 the factors are views
+                # of the live matrices), taken in stream order
+                X, Y = f.X.clone(), f.Y.clone()
+                ready = torch.cuda.Event()
+                ready.record(torch.cuda.current_stream(f.X.device))
                 self._ckpt_cancel = threading.Event()
                 cancel = self._ckpt_cancel
 
                 def write():
-                    done.synchronize()
+                    # the device -> host copies run on the side stream (the copy engine,
+                    # beside the iterations) and block only this thread
+                    with torch.cuda.stream(side):
+                        side.wait_event(ready)
+                        hx, hy = X.cpu(), Y.cpu()
                     if not cancel.is_set():
                         self._write_checkpoint(directory, iteration, meta, hx, hy)
                 self._ckpt_thread = threading.Thread(target=write, name="als-checkpoint",
@@ -658,7 +657,7 @@ class ALSTrainer:
             t_it = time.perf_counter()
             self.iterate(step)
             if self.device.type == "cuda":
-                torch.cuda.synchronize(self.device)
+                torch.cuda.current_stream(self.device).synchronize()
             self.timings.setdefault("iteration_ms", []).extend(
                 [(time.perf_counter() - t_it) * 1e3 / step] * step)
             done += step
@@ -671,7 +670,8 @@ class ALSTrainer:
     def _lap(self, name: str, t0: float) -> None:
         """Adds the milliseconds since ``t0`` (device work included) to ``timings[name]``."""
         if self.device.type == "cuda":
-            torch.cuda.synchronize(self.device)
+            # this stream only (a background checkpoint copy runs on its own)
+            torch.cuda.current_stream(self.device).synchronize()
         self.timings[name] = self.timings.get(name, 0.0) + (time.perf_counter() - t0) * 1e3
 
     def factors(self, gather: bool = True) -> ALSFactors:
