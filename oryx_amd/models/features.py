@@ -108,7 +108,7 @@ def _native_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     values: Dict[int, List[str]] = {}
     seg = buf[off:off + nbytes]
     for si, f in enumerate(cats):
-        o = span_off[:n, si] - off
+        o = span_off[:n, si]          # (relative to the parsed range: the native call saw base)
         ln = span_len[:n, si]
         L = int(ln.max()) if n else 0
         if L > 0:
