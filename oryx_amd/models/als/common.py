@@ -99,7 +99,16 @@ class FeatureVectors:
         self._dev = None                      # fp32 [cap, k]
         self._dev_valid = None                # bool [cap]
         self._dev_norm = None                 # fp32 [cap]
-        self._dev_lock = threading.Lock()
+        self._dev_lock = threading.RLock()
+        # VtV kept current by rank-one corrections (gramian()): the Gramian of the state at the
+        # last full computation, plus the old (removed / overwritten) and new row values since
+        self._gram: Optional[torch.Tensor] = None
+        self._gram_sub: List[np.ndarray] = []
+        self._gram_add: List[np.ndarray] = []
+        self._gram_pending = 0
+        self._gram_corrected = 0
+        self._gram_lock = threading.Lock()
+        self.gram_stats = {"full": 0, "incremental": 0}
         self.partitioner = partitioner        # rows -> partition ids (device LSH)
         self._dev_part = None
         self.version = 0
@@ -174,6 +183,7 @@ class FeatureVectors:
             raise ValueError("vector length %s != features %d" % (v.shape, self.k))
         with self._lock.write():
             row = self._index.get(id_)
+            old = None
             if row is None:
                 row = self._alloc_row()
                 self._index[id_] = row
@@ -182,6 +192,10 @@ class FeatureVectors:
                 self.id_version += 1
                 if self._journal is not None:
                     self._journal.append((True, id_, row))
+            elif self._gram is not None and self._host_valid[row]:
+                old = self._host[row][None].copy()
+            if self._gram is not None:
+                self._gram_note(old, v[None])
             self._host[row] = v
             self._host_valid[row] = True
             self._dirty.add(row)
@@ -282,6 +296,7 @@ class FeatureVectors:
                         index.pop(i, None)
                 if dup:
                     # duplicates within the batch: fall back to the one-by-one path
+                    self._gram_drop()
                     for id_, v in zip(ids, matrix):
                         row = index.get(id_)
                         if row is None:
@@ -312,10 +327,18 @@ class FeatureVectors:
                 if len(new_pos) == len(ids):
                     # every ID new (the bulk load): one contiguous block, slice copies
                     end = start + len(ids)
+                    if self._gram is not None:
+                        self._gram_note(None, matrix)
                     self._host[start:end] = matrix
                     self._host_valid[start:end] = True
                     self._mark_written(rows)
                     return
+            if self._gram is not None:
+                if len(np.unique(rows)) != len(rows):
+                    self._gram_drop()          # a repeated row: only its last value stays
+                else:
+                    was = self._host_valid[rows]
+                    self._gram_note(self._host[rows[was]] if was.any() else None, matrix)
             self._host[rows] = matrix
             self._host_valid[rows] = True
             self._mark_written(rows)
@@ -342,6 +365,8 @@ class FeatureVectors:
         if row is not None and self._journal is not None:
             self._journal.append((False, id_, row))
         if row is not None:
+            if self._gram is not None and self._host_valid[row]:
+                self._gram_note(self._host[row][None].copy(), None)
             self._host[row] = 0.0
             self._host_valid[row] = False
             self._ids[row] = None
@@ -436,11 +461,76 @@ class FeatureVectors:
         if self.size() == 0:
             return None
         if self.device is not None and self.device.type == "cuda":
-            mat, _, _ = self.device_view()
-            return mat.t().matmul(mat).double().cpu().numpy()
+            return self.gramian().cpu().numpy()
         with self._lock.read():
             m = self._host[:self._n_rows][self._host_valid[:self._n_rows]]
             return mathx.transpose_times_self(m)
+
+    # ---------------------------------------------------------------- incremental Gramian
+    # corrections kept per row change; past this many pending rows (or once the corrections
+    # since the last full computation add up to the store's size) the next call recomputes
+    GRAM_MAX_PENDING = 1 << 16
+
+    def _gram_note(self, old: Optional[np.ndarray], new: Optional[np.ndarray]) -> None:
+        """Record a change for gramian() (write lock held; called only while _gram is set)."""
+        n = 0
+        if old is not None and len(old):
+            self._gram_sub.append(np.array(old, dtype=np.float32))
+            n = len(old)
+        if new is not None and len(new):
+            self._gram_add.append(np.array(new, dtype=np.float32))
+            n = max(n, len(new))
+        self._gram_pending += n
+        if self._gram_pending > max(self.GRAM_MAX_PENDING, self._n_rows // 8):
+            self._gram_drop()
+
+    def _gram_drop(self) -> None:
+        self._gram = None
+        self._gram_sub, self._gram_add = [], []
+        self._gram_pending = 0
+
+    def gramian(self) -> Optional[torch.Tensor]:
+        """VtV (float64 [k, k], on the device mirror's device) of the current vectors.
+
+        The first call (and one after a bulk load) multiplies the whole device mirror; after
+        that each call only applies the rank-one corrections of the rows written or removed
+        since (new rows' v v^T added, old values' subtracted, in float64): a speed layer whose
+        model takes a few hundred UP rows per micro-batch no longer re-reads a 20M x 250
+        matrix per interval.  The full product comes back once the corrections since it add up
+        to the store's size (drift stays at float64 rounding of that many updates)."""
+        if self.device is None or self.size() == 0:
+            return None
+        from ...ops import als as als_ops
+        with self._gram_lock:
+            with self._dev_lock, self._lock.write():
+                g = self._gram
+                full = g is None or self._gram_corrected > max(self._n_rows, 1)
+                if full:
+                    self._gram_drop()
+                    # writers wait for the mirror refresh and the product's launch; rows they
+                    # write after it are corrections
+                    mat = self.device_view()[0]
+                    g = als_ops.gramian(mat).double() if mat.is_cuda else \
+                        mat.t().double().matmul(mat.double())
+                    if g.is_cuda:
+                        # the mirror's rows are read before a later refresh rewrites them
+                        torch.cuda.current_stream(g.device).synchronize()
+                    self._gram = g
+                    self._gram_corrected = 0
+                    self.gram_stats["full"] += 1
+                    return g.clone()
+                sub, add = self._gram_sub, self._gram_add
+                self._gram_sub, self._gram_add = [], []
+                self._gram_corrected += self._gram_pending
+                self._gram_pending = 0
+            # (the lock-free part: only this method touches _gram's values)
+            dev = g.device
+            for mats, sign in ((add, 1.0), (sub, -1.0)):
+                if mats:
+                    m = torch.from_numpy(np.concatenate(mats)).to(dev, torch.float64)
+                    g.addmm_(m.t(), m, alpha=sign)
+            self.gram_stats["incremental"] += 1
+            return g.clone()
 
     # ---------------------------------------------------------------- device mirror
     def device_view(self):

@@ -166,8 +166,8 @@ class ALSSpeedModel(SpeedModel):
         if self.features <= 128 and native.kernels_available():
             # both Gramians (fp32 MFMA) and both certified inverses in one more launch
             # (csrc/kernels/spdinv.hip)
-            grams = [als_ops.gramian(store.device_view()[0]).contiguous()
-                     for store in (self.X, self.Y)]
+            # (kept current by rank-one corrections: FeatureVectors.gramian)
+            grams = [store.gramian().float().contiguous() for store in (self.X, self.Y)]
             k = self.features
             invs = [torch.empty((k, k), dtype=torch.float64, device=self.device)
                     for _ in range(2)]
@@ -182,8 +182,7 @@ class ALSSpeedModel(SpeedModel):
             return (invs, ok, grams), ev
         invs, oks = [], []
         for store in (self.X, self.Y):
-            mat, _, _ = store.device_view()
-            a = als_ops.gramian(mat).double()
+            a = store.gramian()
             chol, info = torch.linalg.cholesky_ex(a)
             inv = torch.cholesky_inverse(chol)
             thr = a.abs().sum(1).max() * mathx.SINGULARITY_THRESHOLD_RATIO

@@ -385,3 +385,39 @@ def test_spd_inverse_pair_kernel(cuda, k):
     near[1, :] = near[0, :]                 # rank deficient
     _, _, ok = run(indefinite, near)
     assert ok == [0, 0]
+
+
+def test_incremental_gramian_tracks_writes_and_removals_cpu():
+    """FeatureVectors.gramian: one full product, then rank-one corrections per written /
+    removed row (speed layer micro-batches), equal to VtV of the current rows."""
+    import torch
+    from oryx_amd.models.als.common import FeatureVectors
+    rs = np.random.default_rng(4)
+    k = 12
+    fv = FeatureVectors(k, device=torch.device("cpu"))
+
+    def ref():
+        n = fv._n_rows
+        m = fv._host[:n][fv._host_valid[:n]].astype(np.float64)
+        return m.T @ m
+
+    ids = ["i%d" % j for j in range(3000)]
+    fv.set_vectors(ids, rs.normal(0, 1, (3000, k)).astype(np.float32))
+    g = fv.gramian().numpy()
+    assert np.allclose(g, ref(), rtol=1e-5, atol=1e-3)
+    assert fv.gram_stats == {"full": 1, "incremental": 0}
+    for rnd in range(6):
+        for j in rs.integers(0, 3000, 40):                  # overwrite existing rows
+            fv.set_vector("i%d" % j, rs.normal(0, 1, k).astype(np.float32))
+        for j in range(5):                                  # new rows
+            fv.set_vector("n%d_%d" % (rnd, j), rs.normal(0, 1, k).astype(np.float32))
+        sel = ["i%d" % j for j in rs.choice(3000, 30, replace=False)]
+        fv.set_vectors(sel, rs.normal(0, 1, (30, k)).astype(np.float32))   # bulk, existing
+        fv.remove_vector("i%d" % rs.integers(0, 3000))
+        g = fv.gramian().numpy()
+        assert np.allclose(g, ref(), rtol=1e-6, atol=1e-6), rnd
+    assert fv.gram_stats["full"] == 1 and fv.gram_stats["incremental"] == 6
+    # a batch repeating an ID drops the corrections: the next call recomputes in full
+    fv.set_vectors(["i1", "i1"], rs.normal(0, 1, (2, k)).astype(np.float32))
+    assert np.allclose(fv.gramian().numpy(), ref(), rtol=1e-5, atol=1e-3)
+    assert fv.gram_stats["full"] == 2
