@@ -630,8 +630,9 @@ int oryx_http_tls(void* h, const char* cert, const char* key, const char* passwo
     return -1;
   }
   SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
-  SSL_CTX_set_mode(ctx, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER |
-                            SSL_MODE_RELEASE_BUFFERS);
+  // (no SSL_MODE_RELEASE_BUFFERS: a keep-alive connection would free and re-allocate its
+  // record buffers around every request)
+  SSL_CTX_set_mode(ctx, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
   SSL_CTX_set_options(ctx, SSL_OP_NO_RENEGOTIATION);
   std::string pw = password ? password : "";
   SSL_CTX_set_default_passwd_cb(ctx, tls_password_cb);
