@@ -241,3 +241,35 @@ def test_auc_drift_bf16_vs_fp32(cuda):
     assert auc["cpu_fp32"] > 0.8, auc                    # the planted structure is learned
     assert abs(auc["gpu_fp32"] - auc["cpu_fp32"]) < 2e-3, auc
     assert abs(auc["gpu_bf16"] - auc["cpu_fp32"]) < 1e-2, auc
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,precision,chunks", [(64, "bf16", 1), (128, "fp32", 1),
+                                                (32, "bf16", 3)])
+def test_graph_replay_matches_eager_gpu(cuda, k, precision, chunks):
+    """One process, ORYX_ALS_GRAPH=1: iterations after the first are one captured HIP graph
+    replayed (ALSTrainer._replay) -- bitwise the eager launches' factors, over several replays and
+    after re-publishing the factors (which drops the captured graph)."""
+    u, i, r = _data(seed=9, n_u=4000, n_i=1500, nnz=90000)
+    out = []
+    for graphs in (False, True):
+        tr = ALSTrainer(k, lam=0.05, alpha=1.0, implicit=True,
+                        ctx=dist.DistContext(device=cuda), seed=2, precision=precision,
+                        gather_chunks=chunks)
+        tr._GRAPHS = graphs
+        tr.prepare(u, i, r, 4000, 1500)
+        gi = torch.Generator().manual_seed(3)
+        tr.init_factors(torch.randn(4000, k, generator=gi) * 0.3,
+                        torch.randn(1500, k, generator=gi) * 0.3)
+        tr.iterate(4)
+        assert (tr._graph is not None) == graphs
+        f1 = tr.factors()
+        tr.init_factors(f1.X.cpu(), f1.Y.cpu())     # new buffers: the graph is dropped
+        assert tr._graph is None
+        tr.iterate(3)
+        torch.cuda.synchronize()
+        out.append((f1, tr.factors(), tr.failures))
+    (a1, a2, fa), (b1, b2, fb) = out
+    assert fa == fb == 0
+    for x, y in ((a1, b1), (a2, b2)):
+        assert torch.equal(x.X, y.X) and torch.equal(x.Y, y.Y)
