@@ -67,7 +67,7 @@ __host__ __device__ constexpr int tix(int pi, int qi) {
 // scratch row stride in floats (ds_read_b128 rows conflict free)
 constexpr int BATCH_DS = 20;
 
-template <int KP, int NM, int D>
+template <int KP, int NM, int D, bool YG = false>
 struct BatchCfg {
   static constexpr int M = KP / 16;
   static constexpr int NT = M * (M + 1) / 2;
@@ -76,7 +76,9 @@ struct BatchCfg {
   static constexpr int SCR = NM * 16 * DS * 4;
   static constexpr int VEC = NM * 16 * 4;
   static constexpr int WAVE_BYTES = NM * IMG + NM * 256 + SCR + VEC;
-  static constexpr int YTY_BYTES = NT * 64 * 16;
+  // YG: YtY read from global memory into the accumulators instead of staged in LDS (frees
+  // the block's LDS for a third block per CU)
+  static constexpr int YTY_BYTES = YG ? 0 : NT * 64 * 16;
   static constexpr int BYTES = YTY_BYTES + 4 * WAVE_BYTES;
 };
 
@@ -656,10 +658,16 @@ __device__ __forceinline__ void batch_solve(const AlsParams& p, int lane,
 // work is duplicated, but the SIMD interleaves the two waves' VALU streams -- one wave alone
 // issues a VALU instruction every 4 cycles, two fill the SIMD-32's 2-cycle slots -- and one
 // wave's gather overlaps the other's MFMA-heavy solve).
-template <int KP, int NM, int D, bool PROF = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4 / NM, 4 / NM))) void
+// BPC: resident blocks of 4 waves per CU (waves per SIMD).  Past 4 / NM the YtY tiles come
+// from global memory (YG) so that BPC blocks' LDS fits the CU's 160 KB: at NM = 2, rank 64,
+// three blocks of 45.5 KB instead of two of 55.8 KB -- a third wave per SIMD to hide the
+// solve's latency-bound LDL^T chain behind the other waves' work.
+template <int KP, int NM, int D, bool PROF = false, int BPC = 4 / NM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void
 als_solve_batch(AlsParams p, unsigned long long* prof) {
-  using C = BatchCfg<KP, NM, D>;
+  constexpr bool YG = BPC > 4 / NM;
+  using C = BatchCfg<KP, NM, D, YG>;
+  static_assert(C::BYTES * BPC <= 160 * 1024, "BPC blocks do not fit the CU's LDS");
   using CI = ChunkImage<KP>;
   constexpr int M = C::M;
   constexpr int NT = C::NT;
@@ -680,7 +688,7 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
   lds_float* vdis = scr + NM * 16 * DS;
 
   // YtY in accumulator order: tile t, lane l -> rows 16pi + 4(l>>4) + v, column 16qi + (l&15)
-  {
+  if constexpr (!YG) {
     float* ya = reinterpret_cast<float*>(smem);
     for (int i = threadIdx.x; i < NT * 64; i += 256) {
       const int t = i >> 6, ln = i & 63;
@@ -818,8 +826,26 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
     float bpart[NM][M], cnt[NM];
     static_for<NM>([&](auto Mc) {
       constexpr int m = decltype(Mc)::value;
+      if constexpr (YG) {
+        if constexpr (m == 0) {
+          // (rows 16 pi + 4 g + v, columns 16 qi + f of YtY; L2-resident, 4 KB per row)
+          static_for<M>([&](auto Pc) {
+            constexpr int pi = decltype(Pc)::value;
+            static_for<M - pi>([&](auto Qc) {
+              constexpr int qi = pi + decltype(Qc)::value;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[m][t] = ytya[t * 64 + lane];
+              for (int v = 0; v < 4; ++v)
+                acc[0][tix<M>(pi, qi)][v] = p.YtY[(16 * pi + 4 * g + v) * KP + 16 * qi + f];
+            });
+          });
+        } else {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) acc[m][t] = acc[0][t];
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[m][t] = ytya[t * 64 + lane];
+      }
 #pragma unroll
       for (int pi = 0; pi < M; ++pi) bpart[m][pi] = 0.f;
       cnt[m] = 0.f;
@@ -1523,6 +1549,9 @@ namespace oryx_als {
 #define ORYX_ALS_BATCH_DEPTH 1
 #endif
 // rows per wave: 2 (two waves per SIMD, default) or 4 (one wave per SIMD)
+#ifndef ORYX_ALS_BATCH_BPC_DEFAULT
+#define ORYX_ALS_BATCH_BPC_DEFAULT 2
+#endif
 #ifndef ORYX_ALS_BATCH_NM
 #define ORYX_ALS_BATCH_NM 2
 #endif
@@ -1531,26 +1560,45 @@ static unsigned long long* g_batch_prof = nullptr;
 
 void batch_set_profile(unsigned long long* prof) { g_batch_prof = prof; }
 
+// blocks of 4 waves per CU for the rank <= 64 solve: ORYX_ALS_BATCH_BPC (NM = 2: 2 or 3)
+static int batch_bpc() {
+  static const int v = [] {
+    const char* e = getenv("ORYX_ALS_BATCH_BPC");
+    return e ? atoi(e) : ORYX_ALS_BATCH_BPC_DEFAULT;
+  }();
+  return v;
+}
+
 int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s) {
   constexpr int NM = ORYX_ALS_BATCH_NM;
   constexpr int D = ORYX_ALS_BATCH_DEPTH;
-  // one resident generation: 4 / NM blocks of 4 waves per CU (max_blocks = CUs unless
+  constexpr int BPC0 = 4 / NM;
+  const bool three = NM == 2 && batch_bpc() == 3;
+  // one resident generation: BPC blocks of 4 waves per CU (max_blocks = CUs unless
   // overridden by ORYX_ALS_MAX_BLOCKS)
   const int nb = (p.n_work + NM - 1) / NM;
   int blocks = (nb + 3) / 4;
-  const int cap = max_blocks * (4 / NM);
+  const int cap = max_blocks * (three ? 3 : BPC0);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   if (g_batch_prof && kp == 64) {
-    hipLaunchKernelGGL((als_solve_batch<64, NM, D, true>), dim3(blocks), dim3(256), 0, s, p,
-                       g_batch_prof);
+    if (three)
+      hipLaunchKernelGGL((als_solve_batch<64, NM, D, true, 3>), dim3(blocks), dim3(256), 0, s,
+                         p, g_batch_prof);
+    else
+      hipLaunchKernelGGL((als_solve_batch<64, NM, D, true>), dim3(blocks), dim3(256), 0, s, p,
+                         g_batch_prof);
     return oryx_check_launch();
   }
   switch (kp) {
 #define BATCH_CASE(KPV)                                                                       \
   case KPV:                                                                                   \
-    hipLaunchKernelGGL((als_solve_batch<KPV, NM, D>), dim3(blocks), dim3(256), 0, s, p,      \
-                       nullptr);                                                             \
+    if (three)                                                                                \
+      hipLaunchKernelGGL((als_solve_batch<KPV, NM, D, false, 3>), dim3(blocks), dim3(256), 0, \
+                         s, p, nullptr);                                                     \
+    else                                                                                      \
+      hipLaunchKernelGGL((als_solve_batch<KPV, NM, D>), dim3(blocks), dim3(256), 0, s, p,    \
+                         nullptr);                                                           \
     break;
     BATCH_CASE(16)
     BATCH_CASE(32)
