@@ -1,0 +1,158 @@
+// csv.hip -- numeric CSV lines to a feature matrix on the GPU (the k-means / RDF batch layers'
+// parse of millions of feature rows; SURVEY.md section 2: KMeansUpdate / RDFUpdate parse every
+// record into vectors, [mllib]/kmeans/KMeansUpdate.java:223-232).
+//
+// The host parser (csrc/runtime/oryx_ingest.cpp csv_to_matrix) writes a [rows][F] float64
+// matrix to host memory that is then copied to the device and freed: at 12.5M x 256 that is a
+// 25.6 GB host array (page faults, then a 25.6 GB copy, then a 25.6 GB free).  Here the text
+// itself goes to the device (smaller than its parse) and one thread per line parses it there,
+// with the host parser's exact fast path: up to 19 significant digits, a decimal exponent
+// within +-22, mantissa <= 2^53 -> one correctly rounded double operation (Clinger's fast
+// path), then cast to the output type like the host's (T)v.  An empty field is NaN.  Any
+// other form (quotes, escapes, JSON arrays, more digits, other exponents, a field count other
+// than F, an empty line) sets *bad and the caller parses the block on the host instead, so
+// results are bitwise the host parser's whenever this kernel accepts the input.
+//
+// Bytes are read as aligned 16-byte words (the device buffer is padded by 16 bytes), one word
+// per 16 characters of the thread's line.
+#include "common.h"
+
+namespace {
+
+__constant__ double kP10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+struct ByteReader {
+  const uint4* base;
+  long long word = -1;
+  uint4 w;
+  __device__ __forceinline__ int at(long long pos) {
+    const long long wi = pos >> 4;
+    if (wi != word) {
+      w = base[wi];
+      word = wi;
+    }
+    const int k = (int)(pos & 15);
+    const unsigned u = k < 4 ? w.x : k < 8 ? w.y : k < 12 ? w.z : w.w;
+    return (int)((u >> (8 * (k & 3))) & 0xFFu);
+  }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void csv_lines_kernel(const uint4* __restrict__ buf,
+                                                        const long long* __restrict__ starts,
+                                                        const long long* __restrict__ ends,
+                                                        long long n, int F,
+                                                        const int* __restrict__ out_col, int P,
+                                                        T* __restrict__ out, int* bad) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    ByteReader rd{buf};
+    long long p = starts[i];
+    long long le = ends[i];
+    if (le > p && rd.at(le - 1) == '\r') --le;
+    bool ok = le > p;
+    T* o = out + i * P;
+    int f = 0;
+    while (ok) {
+      // one field starting at p
+      int c = p < le ? rd.at(p) : ',';
+      if (c == ',') {   // empty field: NaN
+        if (f >= F) { ok = false; break; }
+        if (out_col[f] >= 0) o[out_col[f]] = (T)__builtin_nan("");
+      } else {
+        bool neg = false;
+        if (c == '-' || c == '+') {
+          neg = c == '-';
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+        }
+        unsigned long long D = 0;
+        int nd = 0, frac = 0;
+        while ((unsigned)(c - '0') < 10u) {
+          D = D * 10 + (unsigned long long)(c - '0');
+          ++nd;
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+        }
+        if (c == '.') {
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+          while ((unsigned)(c - '0') < 10u) {
+            D = D * 10 + (unsigned long long)(c - '0');
+            ++nd;
+            ++frac;
+            ++p;
+            c = p < le ? rd.at(p) : ',';
+          }
+        }
+        if (nd == 0 || nd > 19) { ok = false; break; }
+        int e10 = -frac;
+        if (c == 'e' || c == 'E') {
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+          bool eneg = false;
+          if (c == '-' || c == '+') {
+            eneg = c == '-';
+            ++p;
+            c = p < le ? rd.at(p) : ',';
+          }
+          int x = 0, ne = 0;
+          while ((unsigned)(c - '0') < 10u && ne < 4) {
+            x = x * 10 + (c - '0');
+            ++ne;
+            ++p;
+            c = p < le ? rd.at(p) : ',';
+          }
+          if (!ne) { ok = false; break; }
+          e10 += eneg ? -x : x;
+        }
+        if (c != ',' || f >= F || D > (1ull << 53) || e10 < -22 || e10 > 22) {
+          ok = false;
+          break;
+        }
+        const double v = e10 < 0 ? (double)D / kP10[-e10] : (double)D * kP10[e10];
+        if (out_col[f] >= 0) o[out_col[f]] = (T)(neg ? -v : v);
+      }
+      ++f;
+      if (p >= le) break;   // the line ended with this field
+      ++p;                  // past the comma
+      if (p >= le) {        // a trailing comma: one more (empty) field
+        if (f >= F) { ok = false; break; }
+        if (out_col[f] >= 0) o[out_col[f]] = (T)__builtin_nan("");
+        ++f;
+        break;
+      }
+    }
+    if (!ok || f != F) atomicOr(bad, 1);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// buf: the lines' bytes on the device, padded to a multiple of 16 plus 16; starts / ends: each
+// line's first byte and its '\n' (device int64, n lines); out: [n][P] (f64 when is_f64, else
+// f32); *bad (zeroed by the caller) is set when any line is not in the fast-path form.
+int oryx_csv_lines_to_matrix(const void* buf, const long long* starts, const long long* ends,
+                             long long n, int F, const int* out_col, int P, void* out,
+                             int is_f64, int* bad, void* stream) {
+  if (n <= 0) return ORYX_OK;
+  if (F <= 0 || P <= 0 || (reinterpret_cast<uintptr_t>(buf) & 15)) return ORYX_EINVAL;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 256LL * 64) blocks = 256LL * 64;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (is_f64)
+    hipLaunchKernelGGL(csv_lines_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
+                       static_cast<const uint4*>(buf), starts, ends, n, F, out_col, P,
+                       static_cast<double*>(out), bad);
+  else
+    hipLaunchKernelGGL(csv_lines_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
+                       static_cast<const uint4*>(buf), starts, ends, n, F, out_col, P,
+                       static_cast<float*>(out), bad);
+  return oryx_check_launch();
+}
+
+}  // extern "C"

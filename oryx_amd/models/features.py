@@ -135,6 +135,56 @@ def _native_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     return full, {}, values
 
 
+def _device_ok(schema: InputSchema, device) -> bool:
+    """The device parser applies: a GPU, every feature numeric (categorical fields need the
+    host's byte spans), the kernels built, not switched off (ORYX_GPU_CSV=0)."""
+    import os
+    if device.type != "cuda" or os.environ.get("ORYX_GPU_CSV", "1") == "0":
+        return False
+    if any(schema.is_categorical(f) for f in range(schema.get_num_features())):
+        return False
+    return native.kernels_available()
+
+
+def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: InputSchema,
+                  dtype: torch.dtype, device) -> Optional[torch.Tensor]:
+    """Bytes [off, off + nbytes) of ``buf`` parsed on the device (``csv.hip``): the text goes
+    to the GPU (smaller than its parse) and one thread per line parses it with the host
+    parser's exact fast path; the [rows, F] matrix never exists on the host.  None when some
+    line is not in that form (the caller then parses on the host: same results)."""
+    F = schema.get_num_features()
+    lib = native.runtime()
+    base = buf.ctypes.data + off
+    cap = max(1, n_lines or nbytes // 8)
+    while True:
+        ends = np.empty(cap, dtype=np.int64)
+        got = lib.oryx_line_ends(ctypes.c_void_p(base), int(nbytes), ends.ctypes.data, cap)
+        if got >= 0:
+            ends = ends[:got]
+            break
+        cap = -got
+    n = len(ends)
+    if n == 0:
+        return torch.zeros((0, F), dtype=dtype, device=device)
+    starts = np.empty(n, dtype=np.int64)
+    starts[0] = 0
+    starts[1:] = ends[:-1] + 1
+    text = torch.empty(((nbytes + 31) // 16) * 16, dtype=torch.uint8, device=device)
+    text[:nbytes].copy_(torch.from_numpy(buf[off:off + nbytes]))
+    d_starts = torch.from_numpy(starts).to(device)
+    d_ends = torch.from_numpy(ends).to(device)
+    out_col = torch.arange(F, dtype=torch.int32, device=device)
+    out = torch.empty((n, F), dtype=dtype, device=device)
+    bad = torch.zeros(1, dtype=torch.int32, device=device)
+    native.check(native.require_kernels().oryx_csv_lines_to_matrix(
+        text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, out_col.data_ptr(), F,
+        out.data_ptr(), int(dtype == torch.float64), bad.data_ptr(),
+        native.stream_ptr(device)), "oryx_csv_lines_to_matrix")
+    if int(bad.item()):
+        return None
+    return out
+
+
 def _python_block(lines: Sequence[str], schema: InputSchema, dtype: torch.dtype
                   ) -> Tuple[np.ndarray, Dict[int, List[str]]]:
     """The general parser (``parse_input_line``: quotes, escapes, JSON arrays)."""
@@ -228,6 +278,12 @@ class FeatureHistory:
 
     def _parse_range(self, buf: np.ndarray, off: int, nbytes: int, n_lines: int,
                      schema: InputSchema, dtype) -> Optional[_Seg]:
+        if _device_ok(schema, self.device):
+            full = _device_block(buf, off, nbytes, n_lines, schema, dtype, self.device)
+            if full is not None:
+                self.stats["device_parsed_bytes"] = \
+                    self.stats.get("device_parsed_bytes", 0) + nbytes
+                return _Seg(full, {}, nbytes)
         got = _native_block(buf, off, nbytes, n_lines, schema, dtype)
         if got is None:
             return None

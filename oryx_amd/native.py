@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 23
+KERNELS_ABI_VERSION = 24
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -261,6 +261,9 @@ def _load_kernels():
     _sig(lib, "oryx_ipc_allreduce_f32", c_i, [c_vp, c_ll, c_vp, c_i, c_i, ctypes.c_uint, c_ll,
                                               ctypes.c_double, c_vp, c_vp])
     _sig(lib, "oryx_ipc_header_floats", c_ll, [])
+    # numeric CSV lines -> feature matrix on the device (csv.hip; models/features.py)
+    _sig(lib, "oryx_csv_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_i, c_vp,
+                                                c_i, c_vp, c_vp])
     # peer-push all-gather (ipc_allgather.hip; parallel/ipc.py IpcAllGather)
     _sig(lib, "oryx_ipc_gather_flag_bytes", c_ll, [])
     _sig(lib, "oryx_ipc_gather_limits", c_i, [c_vp])

@@ -2,9 +2,12 @@
 several segments (the new interval followed by past part files, as a later generation sees it)
 parses to the same rows and categorical encodings as one parse of the concatenated text, with
 and without the resident history.  Regression: categorical fields of every segment after the
-first were read at the wrong byte offsets (values such as "," became categories)."""
+first were read at the wrong byte offsets (values such as "," became categories).  On a GPU the
+all-numeric parse runs on the device (csrc/kernels/csv.hip) and matches the host parser
+bitwise."""
 
 import numpy as np
+import pytest
 import torch
 
 from oryx_amd.models.features import FeatureHistory, parse_features
@@ -55,3 +58,61 @@ def test_multi_segment_parse_matches_one_parse_cpu():
             assert sorted(got.values[4]) == ["no", "yes"]
             assert torch.equal(torch.nan_to_num(got.full, -7.0),
                                torch.nan_to_num(one.full, -7.0))
+
+
+def _numeric_schema(n):
+    conf = cfg.overlay_on({"oryx.input-schema.num-features": n}, cfg.get_default())
+    return InputSchema(conf)
+
+
+def _numeric_lines(rs, n, F):
+    out = []
+    for j in range(n):
+        vals = []
+        for f in range(F):
+            kind = rs.integers(0, 9)
+            x = rs.normal(0, 50)
+            if kind == 0:
+                vals.append("")                              # empty: NaN
+            elif kind == 1:
+                vals.append("%de%d" % (rs.integers(-999, 999), rs.integers(-20, 20)))
+            elif kind == 2:
+                vals.append("+%.6f" % abs(x))
+            elif kind == 3:
+                vals.append("%d" % int(x))
+            elif kind == 4:
+                vals.append("%.17g" % x)                     # 17 significant digits
+            else:
+                vals.append("%.2f" % x)
+        out.append(",".join(vals) + ("\r" if j % 7 == 0 else ""))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_device_csv_parse_matches_host_bitwise(cuda, dtype, monkeypatch):
+    """csv.hip on the device == the host parser, bitwise (NaN where empty), for numeric rows
+    with signs, exponents, 17-digit values, empty fields, trailing commas and CR line ends;
+    lines outside the fast path fall back to the host parse (same results)."""
+    from oryx_amd import native
+    from oryx_amd.models import features as feats
+    native.require_kernels()
+    rs = np.random.default_rng(11)
+    F = 37
+    schema = _numeric_schema(F)
+    lines = _numeric_lines(rs, 5000, F)
+    lines[17] = lines[17][:lines[17].rfind(",")] + ","           # trailing comma: empty last
+    variants = {"plain": lines,
+                "fallback": lines[:100] + ["1.5E+30," + ",".join(["1"] * (F - 1))] + lines[100:]}
+    for name, ls in variants.items():
+        tl = TextLines.from_strings(ls)
+        monkeypatch.setenv("ORYX_GPU_CSV", "0")
+        host = parse_features(tl, schema, torch.device(cuda), dtype=dtype)
+        monkeypatch.setenv("ORYX_GPU_CSV", "1")
+        hist = FeatureHistory(torch.device(cuda), keep=False)
+        dev = hist.parse(tl, schema, dtype)
+        assert dev.full.dtype == dtype and dev.full.shape == host.full.shape
+        a = host.full.cpu().numpy().view(np.int64 if dtype == torch.float64 else np.int32)
+        b = dev.full.cpu().numpy().view(np.int64 if dtype == torch.float64 else np.int32)
+        assert np.array_equal(a, b), name
+        assert (hist.stats.get("device_parsed_bytes", 0) > 0) == (name == "plain"), name
