@@ -61,7 +61,11 @@ def test_multi_segment_parse_matches_one_parse_cpu():
 
 
 def _numeric_schema(n):
-    conf = cfg.overlay_on({"oryx.input-schema.num-features": n}, cfg.get_default())
+    names = ["f%d" % i for i in range(n)]
+    conf = cfg.overlay_on({
+        "oryx.input-schema.feature-names": "[%s]" % ",".join('"%s"' % x for x in names),
+        "oryx.input-schema.numeric-features": "[%s]" % ",".join('"%s"' % x for x in names),
+    }, cfg.get_default())
     return InputSchema(conf)
 
 
