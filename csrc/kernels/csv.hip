@@ -8,10 +8,11 @@
 // itself goes to the device (smaller than its parse) and one thread per line parses it there,
 // with the host parser's exact fast path: up to 19 significant digits, a decimal exponent
 // within +-22, mantissa <= 2^53 -> one correctly rounded double operation (Clinger's fast
-// path), then cast to the output type like the host's (T)v.  An empty field is NaN.  Any
-// other form (quotes, escapes, JSON arrays, more digits, other exponents, a field count other
-// than F, an empty line) sets *bad and the caller parses the block on the host instead, so
-// results are bitwise the host parser's whenever this kernel accepts the input.
+// path), then cast to the output type like the host's (T)v.  An empty field is NaN.  A line in
+// any other form (17-digit mantissas past 2^53, other exponents, quotes, escapes, JSON arrays,
+// a field count other than F, an empty line) is flagged in bad[line] and counted in *n_bad;
+// the caller parses just those lines on the host and writes their rows in, so the matrix is
+// bitwise the host parser's.
 //
 // Bytes are read as aligned 16-byte words (the device buffer is padded by 16 bytes), one word
 // per 16 characters of the thread's line.
@@ -45,7 +46,9 @@ __global__ __launch_bounds__(256) void csv_lines_kernel(const uint4* __restrict_
                                                         const long long* __restrict__ ends,
                                                         long long n, int F,
                                                         const int* __restrict__ out_col, int P,
-                                                        T* __restrict__ out, int* bad) {
+                                                        T* __restrict__ out,
+                                                        unsigned char* __restrict__ bad,
+                                                        int* n_bad) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
        i += (long long)gridDim.x * 256) {
     ByteReader rd{buf};
@@ -125,7 +128,9 @@ __global__ __launch_bounds__(256) void csv_lines_kernel(const uint4* __restrict_
         break;
       }
     }
-    if (!ok || f != F) atomicOr(bad, 1);
+    const bool b = !ok || f != F;
+    bad[i] = b ? 1 : 0;
+    if (b) atomicAdd(n_bad, 1);
   }
 }
 
@@ -135,10 +140,11 @@ extern "C" {
 
 // buf: the lines' bytes on the device, padded to a multiple of 16 plus 16; starts / ends: each
 // line's first byte and its '\n' (device int64, n lines); out: [n][P] (f64 when is_f64, else
-// f32); *bad (zeroed by the caller) is set when any line is not in the fast-path form.
+// f32); bad[n]: 1 for each line not in the fast-path form, *n_bad (zeroed by the caller)
+// their count.
 int oryx_csv_lines_to_matrix(const void* buf, const long long* starts, const long long* ends,
                              long long n, int F, const int* out_col, int P, void* out,
-                             int is_f64, int* bad, void* stream) {
+                             int is_f64, unsigned char* bad, int* n_bad, void* stream) {
   if (n <= 0) return ORYX_OK;
   if (F <= 0 || P <= 0 || (reinterpret_cast<uintptr_t>(buf) & 15)) return ORYX_EINVAL;
   long long blocks = (n + 255) / 256;
@@ -147,11 +153,11 @@ int oryx_csv_lines_to_matrix(const void* buf, const long long* starts, const lon
   if (is_f64)
     hipLaunchKernelGGL(csv_lines_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
                        static_cast<const uint4*>(buf), starts, ends, n, F, out_col, P,
-                       static_cast<double*>(out), bad);
+                       static_cast<double*>(out), bad, n_bad);
   else
     hipLaunchKernelGGL(csv_lines_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
                        static_cast<const uint4*>(buf), starts, ends, n, F, out_col, P,
-                       static_cast<float*>(out), bad);
+                       static_cast<float*>(out), bad, n_bad);
   return oryx_check_launch();
 }
 

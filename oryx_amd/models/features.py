@@ -150,8 +150,9 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
                   dtype: torch.dtype, device) -> Optional[torch.Tensor]:
     """Bytes [off, off + nbytes) of ``buf`` parsed on the device (``csv.hip``): the text goes
     to the GPU (smaller than its parse) and one thread per line parses it with the host
-    parser's exact fast path; the [rows, F] matrix never exists on the host.  None when some
-    line is not in that form (the caller then parses on the host: same results)."""
+    parser's exact fast path; the [rows, F] matrix never exists on the host.  Lines outside
+    that form are parsed on the host and their rows written in (bitwise the host parser's).
+    None when such a line needs the general parser (the caller then takes that path)."""
     F = schema.get_num_features()
     lib = native.runtime()
     base = buf.ctypes.data + off
@@ -175,13 +176,22 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     d_ends = torch.from_numpy(ends).to(device)
     out_col = torch.arange(F, dtype=torch.int32, device=device)
     out = torch.empty((n, F), dtype=dtype, device=device)
-    bad = torch.zeros(1, dtype=torch.int32, device=device)
+    bad = torch.empty(n, dtype=torch.uint8, device=device)
+    n_bad = torch.zeros(1, dtype=torch.int32, device=device)
     native.check(native.require_kernels().oryx_csv_lines_to_matrix(
         text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, out_col.data_ptr(), F,
-        out.data_ptr(), int(dtype == torch.float64), bad.data_ptr(),
+        out.data_ptr(), int(dtype == torch.float64), bad.data_ptr(), n_bad.data_ptr(),
         native.stream_ptr(device)), "oryx_csv_lines_to_matrix")
-    if int(bad.item()):
-        return None
+    if int(n_bad.item()):
+        idx = torch.nonzero(bad).flatten().cpu().numpy()
+        if (ends[idx] == starts[idx]).any():
+            return None                 # an empty line: the host parser skips it (row count)
+        sub = TextLines(buf[off:off + nbytes], n, ends).take(idx)
+        got = _native_block(np.ascontiguousarray(sub.joined()), 0, sub.nbytes(), len(idx),
+                            schema, dtype)
+        if got is None or got[0].shape[0] != len(idx):
+            return None
+        out[torch.from_numpy(idx).to(device)] = torch.from_numpy(got[0]).to(device)
     return out
 
 
