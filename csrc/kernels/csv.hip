@@ -14,6 +14,10 @@
 // the caller parses just those lines on the host and writes their rows in, so the matrix is
 // bitwise the host parser's.
 //
+// Non-numeric (categorical) fields are not parsed here: their byte spans go to span_off /
+// span_len ([rows][S], offsets into the buffer, in field order) and the host encodes them
+// (np.unique over the spans' bytes, as for its own parse), writing the codes into the matrix.
+//
 // Bytes are read as aligned 16-byte words (the device buffer is padded by 16 bytes), one word
 // per 16 characters of the thread's line.
 #include "common.h"
@@ -45,8 +49,11 @@ __global__ __launch_bounds__(256) void csv_lines_kernel(const uint4* __restrict_
                                                         const long long* __restrict__ starts,
                                                         const long long* __restrict__ ends,
                                                         long long n, int F,
+                                                        const unsigned char* __restrict__ is_num,
                                                         const int* __restrict__ out_col, int P,
                                                         T* __restrict__ out,
+                                                        long long* __restrict__ span_off,
+                                                        int* __restrict__ span_len, int S,
                                                         unsigned char* __restrict__ bad,
                                                         int* n_bad) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
@@ -55,13 +62,25 @@ __global__ __launch_bounds__(256) void csv_lines_kernel(const uint4* __restrict_
     long long p = starts[i];
     long long le = ends[i];
     if (le > p && rd.at(le - 1) == '\r') --le;
-    bool ok = le > p;
+    // (a JSON array line starts with '[': the host parser takes it, so it is flagged here)
+    bool ok = le > p && rd.at(p) != '[';
     T* o = out + i * P;
-    int f = 0;
+    int f = 0, si = 0;
     while (ok) {
       // one field starting at p
       int c = p < le ? rd.at(p) : ',';
-      if (c == ',') {   // empty field: NaN
+      if (f < F && !is_num[f]) {   // categorical: its span, NaN in the matrix for now
+        const long long q0 = p;
+        while (p < le && c != ',' && c != '"' && c != '\\') {
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+        }
+        if (c == '"' || c == '\\' || si >= S) { ok = false; break; }
+        span_off[i * S + si] = q0;
+        span_len[i * S + si] = (int)(p - q0);
+        ++si;
+        if (out_col[f] >= 0) o[out_col[f]] = (T)__builtin_nan("");
+      } else if (c == ',') {   // empty field: NaN
         if (f >= F) { ok = false; break; }
         if (out_col[f] >= 0) o[out_col[f]] = (T)__builtin_nan("");
       } else {
@@ -123,6 +142,12 @@ __global__ __launch_bounds__(256) void csv_lines_kernel(const uint4* __restrict_
       ++p;                  // past the comma
       if (p >= le) {        // a trailing comma: one more (empty) field
         if (f >= F) { ok = false; break; }
+        if (!is_num[f]) {
+          if (si >= S) { ok = false; break; }
+          span_off[i * S + si] = p;
+          span_len[i * S + si] = 0;
+          ++si;
+        }
         if (out_col[f] >= 0) o[out_col[f]] = (T)__builtin_nan("");
         ++f;
         break;
@@ -139,12 +164,15 @@ __global__ __launch_bounds__(256) void csv_lines_kernel(const uint4* __restrict_
 extern "C" {
 
 // buf: the lines' bytes on the device, padded to a multiple of 16 plus 16; starts / ends: each
-// line's first byte and its '\n' (device int64, n lines); out: [n][P] (f64 when is_f64, else
-// f32); bad[n]: 1 for each line not in the fast-path form, *n_bad (zeroed by the caller)
-// their count.
+// line's first byte and its '\n' (device int64, n lines); is_num[F]: numeric fields (the others
+// are categorical: spans in span_off / span_len [n][S], S of them); out: [n][P] (f64 when
+// is_f64, else f32); bad[n]: 1 for each line not in the fast-path form, *n_bad (zeroed by the
+// caller) their count.
 int oryx_csv_lines_to_matrix(const void* buf, const long long* starts, const long long* ends,
-                             long long n, int F, const int* out_col, int P, void* out,
-                             int is_f64, unsigned char* bad, int* n_bad, void* stream) {
+                             long long n, int F, const unsigned char* is_num,
+                             const int* out_col, int P, void* out, int is_f64,
+                             long long* span_off, int* span_len, int S, unsigned char* bad,
+                             int* n_bad, void* stream) {
   if (n <= 0) return ORYX_OK;
   if (F <= 0 || P <= 0 || (reinterpret_cast<uintptr_t>(buf) & 15)) return ORYX_EINVAL;
   long long blocks = (n + 255) / 256;
@@ -152,12 +180,12 @@ int oryx_csv_lines_to_matrix(const void* buf, const long long* starts, const lon
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (is_f64)
     hipLaunchKernelGGL(csv_lines_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
-                       static_cast<const uint4*>(buf), starts, ends, n, F, out_col, P,
-                       static_cast<double*>(out), bad, n_bad);
+                       static_cast<const uint4*>(buf), starts, ends, n, F, is_num, out_col, P,
+                       static_cast<double*>(out), span_off, span_len, S, bad, n_bad);
   else
     hipLaunchKernelGGL(csv_lines_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
-                       static_cast<const uint4*>(buf), starts, ends, n, F, out_col, P,
-                       static_cast<float*>(out), bad, n_bad);
+                       static_cast<const uint4*>(buf), starts, ends, n, F, is_num, out_col, P,
+                       static_cast<float*>(out), span_off, span_len, S, bad, n_bad);
   return oryx_check_launch();
 }
 

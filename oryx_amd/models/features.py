@@ -105,11 +105,23 @@ def _native_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
         return None
     n = int(got)
     full = full[:n]
+    values, codes = _encode_spans(buf[off:off + nbytes], span_off[:n], span_len[:n], cats,
+                                  np_dtype)
+    for f in cats:
+        full[:, f] = codes[f]
+    return full, {}, values
+
+
+def _encode_spans(seg: np.ndarray, span_off: np.ndarray, span_len: np.ndarray, cats,
+                  np_dtype) -> Tuple[Dict[int, List[str]], Dict[int, np.ndarray]]:
+    """Categorical codes of each span column (spans relative to ``seg``), in order of first
+    appearance (empty = NaN): (distinct values, codes) per categorical feature."""
+    n = span_off.shape[0]
     values: Dict[int, List[str]] = {}
-    seg = buf[off:off + nbytes]
+    out_codes: Dict[int, np.ndarray] = {}
     for si, f in enumerate(cats):
-        o = span_off[:n, si]          # (relative to the parsed range: the native call saw base)
-        ln = span_len[:n, si]
+        o = span_off[:, si]
+        ln = span_len[:, si]
         L = int(ln.max()) if n else 0
         if L > 0:
             j = np.arange(L)
@@ -130,30 +142,31 @@ def _native_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
             e = names.index("")
             codes = np.where(codes == e, np.nan, np.where(codes > e, codes - 1, codes))
             names = names[:e] + names[e + 1:]
-        full[:, f] = codes
+        out_codes[f] = codes
         values[f] = names
-    return full, {}, values
+    return values, out_codes
 
 
 def _device_ok(schema: InputSchema, device) -> bool:
-    """The device parser applies: a GPU, every feature numeric (categorical fields need the
-    host's byte spans), the kernels built, not switched off (ORYX_GPU_CSV=0)."""
+    """The device parser applies: a GPU, the kernels built, not switched off (ORYX_GPU_CSV=0)."""
     import os
     if device.type != "cuda" or os.environ.get("ORYX_GPU_CSV", "1") == "0":
-        return False
-    if any(schema.is_categorical(f) for f in range(schema.get_num_features())):
         return False
     return native.kernels_available()
 
 
 def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: InputSchema,
-                  dtype: torch.dtype, device) -> Optional[torch.Tensor]:
+                  dtype: torch.dtype, device
+                  ) -> Optional[Tuple[torch.Tensor, Dict[int, List[str]]]]:
     """Bytes [off, off + nbytes) of ``buf`` parsed on the device (``csv.hip``): the text goes
     to the GPU (smaller than its parse) and one thread per line parses it with the host
     parser's exact fast path; the [rows, F] matrix never exists on the host.  Lines outside
     that form are parsed on the host and their rows written in (bitwise the host parser's).
-    None when such a line needs the general parser (the caller then takes that path)."""
+    Categorical fields come back as byte spans and are encoded on the host.  Returns (matrix,
+    categorical values), or None when the caller should parse on the host instead."""
     F = schema.get_num_features()
+    cats = [f for f in range(F) if schema.is_categorical(f)]
+    S = len(cats)
     lib = native.runtime()
     base = buf.ctypes.data + off
     cap = max(1, n_lines or nbytes // 8)
@@ -166,7 +179,7 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
         cap = -got
     n = len(ends)
     if n == 0:
-        return torch.zeros((0, F), dtype=dtype, device=device)
+        return torch.zeros((0, F), dtype=dtype, device=device), {f: [] for f in cats}
     starts = np.empty(n, dtype=np.int64)
     starts[0] = 0
     starts[1:] = ends[:-1] + 1
@@ -175,14 +188,22 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     d_starts = torch.from_numpy(starts).to(device)
     d_ends = torch.from_numpy(ends).to(device)
     out_col = torch.arange(F, dtype=torch.int32, device=device)
+    is_num = torch.tensor([0 if f in cats else 1 for f in range(F)], dtype=torch.uint8,
+                          device=device)
     out = torch.empty((n, F), dtype=dtype, device=device)
+    sp_off = torch.empty((n, max(S, 1)), dtype=torch.int64, device=device)
+    sp_len = torch.empty((n, max(S, 1)), dtype=torch.int32, device=device)
     bad = torch.empty(n, dtype=torch.uint8, device=device)
     n_bad = torch.zeros(1, dtype=torch.int32, device=device)
     native.check(native.require_kernels().oryx_csv_lines_to_matrix(
-        text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, out_col.data_ptr(), F,
-        out.data_ptr(), int(dtype == torch.float64), bad.data_ptr(), n_bad.data_ptr(),
-        native.stream_ptr(device)), "oryx_csv_lines_to_matrix")
+        text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, is_num.data_ptr(),
+        out_col.data_ptr(), F, out.data_ptr(), int(dtype == torch.float64), sp_off.data_ptr(),
+        sp_len.data_ptr(), S, bad.data_ptr(), n_bad.data_ptr(), native.stream_ptr(device)),
+        "oryx_csv_lines_to_matrix")
+    values: Dict[int, List[str]] = {}
     if int(n_bad.item()):
+        if S:
+            return None     # (the host subset's local categories would need a re-encode)
         idx = torch.nonzero(bad).flatten().cpu().numpy()
         if (ends[idx] == starts[idx]).any():
             return None                 # an empty line: the host parser skips it (row count)
@@ -192,7 +213,13 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
         if got is None or got[0].shape[0] != len(idx):
             return None
         out[torch.from_numpy(idx).to(device)] = torch.from_numpy(got[0]).to(device)
-    return out
+    if S:
+        np_dtype = np.float32 if dtype == torch.float32 else np.float64
+        values, codes = _encode_spans(buf[off:off + nbytes], sp_off.cpu().numpy(),
+                                      sp_len.cpu().numpy(), cats, np_dtype)
+        for f in cats:
+            out[:, f] = torch.from_numpy(codes[f]).to(device)
+    return out, values
 
 
 def _python_block(lines: Sequence[str], schema: InputSchema, dtype: torch.dtype
@@ -289,11 +316,11 @@ class FeatureHistory:
     def _parse_range(self, buf: np.ndarray, off: int, nbytes: int, n_lines: int,
                      schema: InputSchema, dtype) -> Optional[_Seg]:
         if _device_ok(schema, self.device):
-            full = _device_block(buf, off, nbytes, n_lines, schema, dtype, self.device)
-            if full is not None:
+            got = _device_block(buf, off, nbytes, n_lines, schema, dtype, self.device)
+            if got is not None:
                 self.stats["device_parsed_bytes"] = \
                     self.stats.get("device_parsed_bytes", 0) + nbytes
-                return _Seg(full, {}, nbytes)
+                return _Seg(got[0], got[1], nbytes)
         got = _native_block(buf, off, nbytes, n_lines, schema, dtype)
         if got is None:
             return None

@@ -262,8 +262,8 @@ def _load_kernels():
                                               ctypes.c_double, c_vp, c_vp])
     _sig(lib, "oryx_ipc_header_floats", c_ll, [])
     # numeric CSV lines -> feature matrix on the device (csv.hip; models/features.py)
-    _sig(lib, "oryx_csv_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_i, c_vp,
-                                                c_i, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_csv_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp, c_i,
+                                                c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_vp, c_vp])
     # peer-push all-gather (ipc_allgather.hip; parallel/ipc.py IpcAllGather)
     _sig(lib, "oryx_ipc_gather_flag_bytes", c_ll, [])
     _sig(lib, "oryx_ipc_gather_limits", c_i, [c_vp])

@@ -126,3 +126,33 @@ def test_device_csv_parse_matches_host_bitwise(cuda, dtype, monkeypatch):
         b = dev.full.cpu().numpy().view(np.int64 if dtype == torch.float64 else np.int32)
         assert np.array_equal(a, b), name
         assert hist.stats.get("device_parsed_bytes", 0) > 0, name
+
+
+@pytest.mark.gpu
+def test_device_csv_parse_with_categoricals_matches_host(cuda, monkeypatch):
+    """Categorical fields through the device parser: spans on the device, codes on the host
+    -- the same matrix (bitwise) and the same distinct values in first-appearance order as the
+    host parser, over several segments and through the resident history."""
+    from oryx_amd import native
+    native.require_kernels()
+    rs = np.random.default_rng(5)
+    schema = _schema()
+    parts = []
+    for i, colors in enumerate((["red", "green"], ["blue", "", "violet"], ["red", "cyan"])):
+        tl = TextLines.from_strings(_lines(rs, 700 + 300 * i, colors))
+        if i:
+            tl.with_key(("part", i))
+        parts.append(tl)
+    multi = concat_lines(parts)
+    for dtype in (torch.float32, torch.float64):
+        monkeypatch.setenv("ORYX_GPU_CSV", "0")
+        host = parse_features(multi, schema, torch.device(cuda), dtype=dtype)
+        monkeypatch.setenv("ORYX_GPU_CSV", "1")
+        hist = FeatureHistory(torch.device(cuda))
+        for _ in range(2):
+            dev = parse_features(multi, schema, torch.device(cuda), dtype=dtype, history=hist)
+            assert dev.values == host.values
+            a = torch.nan_to_num(host.full, -7.0).cpu().numpy()
+            b = torch.nan_to_num(dev.full, -7.0).cpu().numpy()
+            assert np.array_equal(a, b)
+        assert hist.stats.get("device_parsed_bytes", 0) > 0
