@@ -286,7 +286,8 @@ def main(argv=None) -> int:
     lay = first_lay
     inner = sum(v for k, v in phases.items()
                 if not k.startswith("layer_") and k not in ("publish_y", "publish_x"))
-    attributed = inner + sum(v for k, v in lay.items() if k != "update")
+    # (save_data_total runs beside the update: only its exposed part, save_data, counts)
+    attributed = inner + sum(v for k, v in lay.items() if k not in ("update", "save_data_total"))
     if ctx.is_main:
         # count what was published
         ut = tlog.Topic(work + "/log", "OryxUpdate")
