@@ -220,6 +220,10 @@ def _run_worlds(tmp_path, device):
         env = dict(os.environ, OMP_NUM_THREADS="2", ORYX_IPC_ALLREDUCE="any",
                    ORYX_IPC_ALLGATHER="any" if world == "push" else "0",
                    ORYX_MR_DEVICE=device,
+                   # each launch waits for its kernel: a device fault is reported at the
+                   # launch that caused it (an intermittent illegal access in the RDF part at
+                   # world 2 surfaced only at a later sync: profiles/r5_multirank_rdf_fault.log)
+                   AMD_SERIALIZE_KERNEL="3",
                    HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY",
                                                              "0"))
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
