@@ -137,6 +137,60 @@ const char* status_text(int code) {
 
 // ---- transport: plain socket or TLS session.  Return > 0 bytes, 0 at EOF, -1 when the call
 // would block (the connection's ssl_*_wants_* flags say on what), -2 on an error.
+// The connection BIO of a TLS socket: OpenSSL's socket BIO writes with plain send(), which
+// raises SIGPIPE in whichever thread writes to a connection the client already closed (a
+// handler thread answering a vanished client); this one sends with MSG_NOSIGNAL and reads
+// with recv(), keeping the socket BIO's retry semantics (EAGAIN / EINTR -> retry).
+int nosig_write(BIO* b, const char* p, int n) {
+  const int fd = (int)BIO_get_fd(b, nullptr);
+  const ssize_t w = send(fd, p, (size_t)n, MSG_NOSIGNAL);
+  BIO_clear_retry_flags(b);
+  if (w < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR))
+    BIO_set_retry_write(b);
+  return (int)w;
+}
+
+int nosig_read(BIO* b, char* p, int n) {
+  const int fd = (int)BIO_get_fd(b, nullptr);
+  const ssize_t r = recv(fd, p, (size_t)n, 0);
+  BIO_clear_retry_flags(b);
+  if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR))
+    BIO_set_retry_read(b);
+  return (int)r;
+}
+
+long nosig_ctrl(BIO* b, int cmd, long num, void* ptr) {
+  switch (cmd) {
+    case BIO_C_SET_FD:
+      BIO_set_data(b, reinterpret_cast<void*>((intptr_t) * static_cast<int*>(ptr)));
+      BIO_set_init(b, 1);
+      return 1;
+    case BIO_C_GET_FD: {
+      const int fd = BIO_get_init(b) ? (int)reinterpret_cast<intptr_t>(BIO_get_data(b)) : -1;
+      if (ptr) *static_cast<int*>(ptr) = fd;
+      return fd;
+    }
+    case BIO_CTRL_FLUSH:
+      return 1;
+    default:
+      (void)num;
+      return 0;
+  }
+}
+
+BIO_METHOD* nosig_method() {
+  static BIO_METHOD* m = [] {
+    BIO_METHOD* x = BIO_meth_new(BIO_get_new_index() | BIO_TYPE_SOURCE_SINK |
+                                     BIO_TYPE_DESCRIPTOR,
+                                 "oryx socket (MSG_NOSIGNAL)");
+    BIO_meth_set_write(x, nosig_write);
+    BIO_meth_set_read(x, nosig_read);
+    BIO_meth_set_ctrl(x, nosig_ctrl);
+    return x;
+  }();
+  return m;
+}
+
 ssize_t conn_recv(Conn* c, char* buf, size_t n) {
   if (!c->ssl) {
     for (;;) {
@@ -500,11 +554,15 @@ void poll_once(Server* S, int wait_ms) {
           c->cid = S->next_cid++;
           if (S->tls) {
             c->ssl = SSL_new(S->tls);
-            if (!c->ssl || SSL_set_fd(c->ssl, cfd) != 1) {
+            BIO* bio = c->ssl ? BIO_new(nosig_method()) : nullptr;
+            if (!bio) {
               if (c->ssl) SSL_free(c->ssl);
               close(cfd);
               continue;
             }
+            int fd_arg = cfd;
+            BIO_ctrl(bio, BIO_C_SET_FD, 0, &fd_arg);
+            SSL_set_bio(c->ssl, bio, bio);   // (the SSL owns the BIO; the fd stays ours)
             SSL_set_accept_state(c->ssl);   // the handshake runs inside the first read
           }
           S->fd_of_cid[c->cid] = cfd;

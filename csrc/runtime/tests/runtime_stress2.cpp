@@ -13,7 +13,11 @@
 //      before reading their responses;
 //   3. oryx_topn_prep from several threads at once on shared inputs (LSH bitmaps, exclusions);
 //   4. the persistent ThreadPool (parallel_ranges) entered from several threads at once
-//      (oryx_blob_hash64 and oryx_digest128 split their work over it).
+//      (oryx_blob_hash64 and oryx_digest128 split their work over it);
+//   5. the HTTP front end with TLS (oryx_http_tls: OpenSSL in non-blocking mode inside the
+//      same leader / follower loop) under concurrent TLS clients: keep-alive pipelined
+//      requests, handshakes abandoned halfway, plain HTTP sent to the TLS port, and clients
+//      that close right after sending.  Needs a certificate: runtime_stress2 <dir> <cert> <key>.
 //
 // Exit status 0 = no check failed.
 
@@ -22,6 +26,9 @@
 #include <netinet/tcp.h>
 #include <sys/socket.h>
 #include <unistd.h>
+
+#include <openssl/err.h>
+#include <openssl/ssl.h>
 
 #include <atomic>
 #include <chrono>
@@ -53,6 +60,7 @@ long long oryx_http_next(void* h, char* out, long long cap, int timeout_ms);
 int oryx_http_respond(void* h, unsigned long long id, const char* data, long long len,
                       int close_after);
 void oryx_http_stop(void* h);
+int oryx_http_tls(void* h, const char* cert, const char* key, const char* password);
 void oryx_http_free(void* h);
 long long oryx_topn_prep(int nq, int k, int kp, int max_batch, const float* targets,
                          const long long* cand_ptr, const long long* cand,
@@ -489,6 +497,151 @@ static void test_pool() {
   for (auto& x : th) x.join();
 }
 
+// ---------------------------------------------------------------- 5. HTTPS
+
+static void serve(void* S, std::atomic<bool>& stop, std::vector<std::thread>& handlers) {
+  for (int h = 0; h < 4; ++h) {
+    handlers.emplace_back([S, &stop] {
+      std::vector<char> buf(1 << 16);
+      while (!stop) {
+        long long n = oryx_http_next(S, buf.data(), (long long)buf.size(), 50);
+        if (n == -1) return;
+        if (n == 0) continue;
+        if (n < 0) {
+          buf.resize((size_t)-n);
+          continue;
+        }
+        uint64_t id;
+        uint32_t ml, tl;
+        memcpy(&id, buf.data(), 8);
+        memcpy(&ml, buf.data() + 8, 4);
+        memcpy(&tl, buf.data() + 12, 4);
+        const std::string target(buf.data() + 28 + ml, tl);
+        const std::string resp = "HTTP/1.1 200 OK\r\nContent-Length: " +
+                                 std::to_string(target.size()) + "\r\n\r\n" + target;
+        oryx_http_respond(S, id, resp.data(), (long long)resp.size(), 0);
+      }
+    });
+  }
+}
+
+static bool ssl_write_all(SSL* ssl, const std::string& s) {
+  size_t o = 0;
+  while (o < s.size()) {
+    const int w = SSL_write(ssl, s.data() + o, (int)(s.size() - o));
+    if (w <= 0) return false;
+    o += (size_t)w;
+  }
+  return true;
+}
+
+static bool ssl_read_responses(SSL* ssl, int n, std::vector<std::string>& bodies) {
+  std::string buf;
+  char tmp[16384];
+  while ((int)bodies.size() < n) {
+    size_t he;
+    while ((he = buf.find("\r\n\r\n")) == std::string::npos) {
+      const int r = SSL_read(ssl, tmp, sizeof(tmp));
+      if (r <= 0) return false;
+      buf.append(tmp, (size_t)r);
+    }
+    size_t cl = 0;
+    const size_t p = buf.find("Content-Length: ");
+    if (p != std::string::npos && p < he) cl = (size_t)atoll(buf.c_str() + p + 16);
+    while (buf.size() < he + 4 + cl) {
+      const int r = SSL_read(ssl, tmp, sizeof(tmp));
+      if (r <= 0) return false;
+      buf.append(tmp, (size_t)r);
+    }
+    bodies.push_back(buf.substr(he + 4, cl));
+    buf.erase(0, he + 4 + cl);
+  }
+  return true;
+}
+
+static void test_https(const char* cert, const char* key) {
+  void* S = oryx_http_start("127.0.0.1", 0, 256, 1 << 20);
+  CHECK(S != nullptr);
+  if (!S) return;
+  CHECK(oryx_http_tls(S, cert, key, nullptr) == 0);
+  const int port = oryx_http_port(S);
+  std::atomic<bool> stop{false};
+  std::vector<std::thread> handlers;
+  serve(S, stop, handlers);
+  SSL_CTX* cctx = SSL_CTX_new(TLS_client_method());
+  SSL_CTX_set_verify(cctx, SSL_VERIFY_NONE, nullptr);
+  std::vector<std::thread> clients;
+  // keep-alive TLS connections with pipelined bursts
+  for (int c = 0; c < 6; ++c) {
+    clients.emplace_back([&, c] {
+      const int fd = connect_to(port);
+      CHECK(fd >= 0);
+      if (fd < 0) return;
+      SSL* ssl = SSL_new(cctx);
+      SSL_set_fd(ssl, fd);
+      CHECK(SSL_connect(ssl) == 1);
+      for (int rep = 0; rep < 15; ++rep) {
+        std::string burst;
+        for (int j = 0; j < 4; ++j)
+          burst += "GET /t" + std::to_string(c) + "/" + std::to_string(rep * 4 + j) +
+                   " HTTP/1.1\r\nHost: x\r\n\r\n";
+        CHECK(ssl_write_all(ssl, burst));
+        std::vector<std::string> b;
+        CHECK(ssl_read_responses(ssl, 4, b));
+        for (int j = 0; j < (int)b.size(); ++j)
+          CHECK(b[(size_t)j] == "/t" + std::to_string(c) + "/" + std::to_string(rep * 4 + j));
+      }
+      SSL_shutdown(ssl);
+      SSL_free(ssl);
+      close(fd);
+    });
+  }
+  // abandoned handshakes, plain HTTP to the TLS port, closes right after a request
+  for (int c = 0; c < 3; ++c) {
+    clients.emplace_back([&, c] {
+      for (int rep = 0; rep < 15; ++rep) {
+        const int fd = connect_to(port);
+        if (fd < 0) continue;
+        if (c == 0) {
+          send_all(fd, std::string("\x16\x03\x01\x02\x00\x01\x00\x01\xfc\x03\x03", 11));
+        } else if (c == 1) {
+          send_all(fd, "GET /plain HTTP/1.1\r\nHost: x\r\n\r\n");
+          char tmp[256];
+          (void)recv(fd, tmp, sizeof(tmp), 0);
+        } else {
+          SSL* ssl = SSL_new(cctx);
+          SSL_set_fd(ssl, fd);
+          if (SSL_connect(ssl) == 1) ssl_write_all(ssl, "GET /gone HTTP/1.1\r\n\r\n");
+          SSL_free(ssl);
+        }
+        close(fd);
+      }
+    });
+  }
+  for (auto& x : clients) x.join();
+  // the server still answers over TLS after all that
+  {
+    const int fd = connect_to(port);
+    CHECK(fd >= 0);
+    if (fd >= 0) {
+      SSL* ssl = SSL_new(cctx);
+      SSL_set_fd(ssl, fd);
+      CHECK(SSL_connect(ssl) == 1);
+      CHECK(ssl_write_all(ssl, "GET /final HTTP/1.1\r\n\r\n"));
+      std::vector<std::string> b;
+      CHECK(ssl_read_responses(ssl, 1, b));
+      if (!b.empty()) CHECK(b[0] == "/final");
+      SSL_free(ssl);
+      close(fd);
+    }
+  }
+  SSL_CTX_free(cctx);
+  stop = true;
+  oryx_http_stop(S);
+  for (auto& x : handlers) x.join();
+  oryx_http_free(S);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: runtime_stress2 <dir>\n");
@@ -502,5 +655,9 @@ int main(int argc, char** argv) {
   printf("topn_prep: errors %d\n", g_errors.load());
   test_pool();
   printf("thread pool: errors %d\n", g_errors.load());
+  if (argc >= 4) {
+    test_https(argv[2], argv[3]);
+    printf("https: errors %d\n", g_errors.load());
+  }
   return g_errors.load() == 0 ? 0 : 1;
 }
