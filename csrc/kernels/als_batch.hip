@@ -1581,10 +1581,11 @@ int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s
   const int cap = max_blocks * (three ? 3 : BPC0);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
+  constexpr int BPC3 = NM == 2 ? 3 : BPC0;   // (the third block exists only for NM = 2)
   if (g_batch_prof && kp == 64) {
     if (three)
-      hipLaunchKernelGGL((als_solve_batch<64, NM, D, true, 3>), dim3(blocks), dim3(256), 0, s,
-                         p, g_batch_prof);
+      hipLaunchKernelGGL((als_solve_batch<64, NM, D, true, BPC3>), dim3(blocks), dim3(256), 0,
+                         s, p, g_batch_prof);
     else
       hipLaunchKernelGGL((als_solve_batch<64, NM, D, true>), dim3(blocks), dim3(256), 0, s, p,
                          g_batch_prof);
@@ -1594,8 +1595,8 @@ int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s
 #define BATCH_CASE(KPV)                                                                       \
   case KPV:                                                                                   \
     if (three)                                                                                \
-      hipLaunchKernelGGL((als_solve_batch<KPV, NM, D, false, 3>), dim3(blocks), dim3(256), 0, \
-                         s, p, nullptr);                                                     \
+      hipLaunchKernelGGL((als_solve_batch<KPV, NM, D, false, BPC3>), dim3(blocks), dim3(256), \
+                         0, s, p, nullptr);                                                  \
     else                                                                                      \
       hipLaunchKernelGGL((als_solve_batch<KPV, NM, D>), dim3(blocks), dim3(256), 0, s, p,    \
                          nullptr);                                                           \
