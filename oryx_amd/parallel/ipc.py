@@ -283,7 +283,9 @@ class IpcAllGather:
 
     def self_test(self) -> bool:
         """Gather rank-dependent rows both ways (peer push and torch.distributed); True when
-        every rank matched bitwise."""
+        every rank matched bitwise.  Three exchanges into the same buffer, each compared after
+        it: the comparison reads pull the previous contents into this GPU's L2 caches, so a
+        wait that failed to drop them would show as a mismatch here (not as stale factors)."""
         ok = True
         name = "__selftest__"
         try:
@@ -292,23 +294,25 @@ class IpcAllGather:
             cr = -(-rows // C)
             out = self.buffer(name, (C * W * cr, cols), torch.bfloat16)
             base = torch.arange(C * cr * cols, device=self.ctx.device, dtype=torch.float32)
-            local = ((base % 251) * (self.rank + 1) + self.rank).to(torch.bfloat16) \
-                .reshape(C * cr, cols)
-            self.begin(name)
-            for c in range(C):
-                self.push(name, local[c * cr:(c + 1) * cr], (c * W + self.rank) * cr, C, c)
-            self.end(name, C)
-            torch.cuda.synchronize(self.ctx.device)
-            self.check()
             ref = torch.empty_like(out)
-            for c in range(C):
-                blk = local[c * cr:(c + 1) * cr].contiguous()
-                parts = list(ref[c * W * cr:(c + 1) * W * cr].chunk(W, 0))
-                if W > 1:
-                    tdist.all_gather(parts, blk, group=self.ctx.group)
-                else:
-                    parts[0].copy_(blk)
-            ok = bool(torch.equal(out.view(torch.int16), ref.view(torch.int16)))
+            for rnd in range(3):
+                local = ((base % 251) * (self.rank + 1 + 7 * rnd) + self.rank - rnd) \
+                    .to(torch.bfloat16).reshape(C * cr, cols)
+                self.begin(name)
+                for c in range(C):
+                    self.push(name, local[c * cr:(c + 1) * cr], (c * W + self.rank) * cr, C,
+                              c)
+                self.end(name, C)
+                torch.cuda.synchronize(self.ctx.device)
+                self.check()
+                for c in range(C):
+                    blk = local[c * cr:(c + 1) * cr].contiguous()
+                    parts = list(ref[c * W * cr:(c + 1) * W * cr].chunk(W, 0))
+                    if W > 1:
+                        tdist.all_gather(parts, blk, group=self.ctx.group)
+                    else:
+                        parts[0].copy_(blk)
+                ok = ok and bool(torch.equal(out.view(torch.int16), ref.view(torch.int16)))
         except Exception as e:   # noqa: BLE001 -- any failure disables the path
             log.warning("IPC all-gather self-test failed on rank %d: %s", self.rank, e)
             ok = False
