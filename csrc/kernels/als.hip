@@ -40,9 +40,14 @@ namespace {
 // 256-byte run per atomic instruction).  Runs before the solve kernel, which then takes long
 // rows' normal equations from the workspace: a row with 1e5 ratings is spread over ~100
 // waves instead of serialising on one (the tail of the popular-item half-step).
-template <int KP, bool SPLIT = false>
+// STORE: each segment's record goes to its own slot of seg_ws with plain stores instead (no
+// atomics; als_partial_reduce then sums each row's segments), which lets the segments be
+// short -- more waves in flight for the latency-bound gather -- without the atomic traffic
+// growing with their number.
+template <int KP, bool SPLIT = false, bool STORE = false>
 __global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* __restrict__ segs,
-                                                  int n_seg, float* __restrict__ ws) {
+                                                  int n_seg, float* __restrict__ ws,
+                                                  float* __restrict__ seg_ws) {
   constexpr int M = KP / 16;
   constexpr int NT = M * (M + 1) / 2;
   constexpr int GB = ChunkImage<KP>::BYTES * (SPLIT ? 2 : 1);
@@ -65,7 +70,7 @@ __global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* _
     wave_accumulate<KP, false, SPLIT>(p, beg, end, G, Wab, acc, bpart, cnt_acc);
     reduce_bpart<M>(bpart);
     const float cnt = wave_sum(cnt_acc);
-    float* dst = ws + slot * ws_stride(KP);
+    float* dst = STORE ? seg_ws + (int64_t)sgi * ws_stride(KP) : ws + slot * ws_stride(KP);
     int t = 0;
 #pragma unroll
     for (int pi = 0; pi < M; ++pi) {
@@ -78,18 +83,56 @@ __global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* _
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int i = pi * 16 + gg * 4 + v, j = qi * 16 + ff;
-          atomicAdd(dst + i * KP + j, acc[t][v]);
-          if (pi != qi) atomicAdd(dst + j * KP + i, acc[t][v]);
+          if constexpr (STORE) {
+            dst[i * KP + j] = acc[t][v];
+            if (pi != qi) dst[j * KP + i] = acc[t][v];
+          } else {
+            atomicAdd(dst + i * KP + j, acc[t][v]);
+            if (pi != qi) atomicAdd(dst + j * KP + i, acc[t][v]);
+          }
         }
     }
     // after the reduction lane (g, fl) holds b[pi*16 + fl] for every pi: lane l adds
     // features l and l + 64
-    if (lane < KP) atomicAdd(dst + KP * KP + lane, pick_bpart<M>(bpart, g));
-    if (lane + 64 < KP) atomicAdd(dst + KP * KP + 64 + lane, pick_bpart<M>(bpart, g + 4));
-    if (lane == 0) atomicAdd(dst + KP * KP + KP, cnt);
+    if constexpr (STORE) {
+      if (lane < KP) dst[KP * KP + lane] = pick_bpart<M>(bpart, g);
+      if (lane + 64 < KP) dst[KP * KP + 64 + lane] = pick_bpart<M>(bpart, g + 4);
+      if (lane == 0) dst[KP * KP + KP] = cnt;
+    } else {
+      if (lane < KP) atomicAdd(dst + KP * KP + lane, pick_bpart<M>(bpart, g));
+      if (lane + 64 < KP) atomicAdd(dst + KP * KP + 64 + lane, pick_bpart<M>(bpart, g + 4));
+      if (lane == 0) atomicAdd(dst + KP * KP + KP, cnt);
+    }
   }
 }
 
+
+// Sum of each long row's segment records (STORE mode of als_partial): block (slot, chunk)
+// adds up floats [256 chunk, 256 chunk + 256) of the slot's records, in segment order (the
+// segments of a slot are contiguous in segs, slot-major).
+__global__ __launch_bounds__(256) void als_partial_reduce(const int64_t* __restrict__ segs,
+                                                         int n_seg, const float* __restrict__ seg_ws,
+                                                         float* __restrict__ ws, int stride) {
+  __shared__ int s_lo, s_hi;
+  const int slot = blockIdx.x;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = n_seg;                     // first segment with slot >= this one
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (segs[4 * (int64_t)mid + 1] < slot) lo = mid + 1; else hi = mid;
+    }
+    int e = lo;
+    while (e < n_seg && segs[4 * (int64_t)e + 1] == slot) ++e;
+    s_lo = lo;
+    s_hi = e;
+  }
+  __syncthreads();
+  const int f = blockIdx.y * 256 + threadIdx.x;
+  if (f >= stride) return;
+  float acc = 0.f;
+  for (int sg = s_lo; sg < s_hi; ++sg) acc += seg_ws[(int64_t)sg * stride + f];
+  ws[(int64_t)slot * stride + f] = acc;
+}
 
 // ------------------------------------------------------------------ helpers
 
@@ -186,20 +229,38 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
   const int max_blocks = env_blocks ? env_blocks : 256 * 16;
   const bool deep = g_als_variant >= 2 && g_als_variant <= 4;
   const int panel_blocks = env_blocks ? env_blocks : (deep ? resident_panel_blocks : 256 * 16);
+  // long rows: segment records stored, then reduced per row (ws: n_long reduced records
+  // followed by n_seg segment records); ORYX_ALS_PARTIAL_ATOMIC=1: the older atomic adds
+  static const bool atomic_partial = [] {
+    const char* e = getenv("ORYX_ALS_PARTIAL_ATOMIC");
+    return e && atoi(e) == 1;
+  }();
   if (n_seg > 0) {
-    if (hipMemsetAsync(ws, 0, sizeof(float) * (size_t)n_long * ws_stride(kp), s) != hipSuccess)
+    const int stride = ws_stride(kp);
+    float* seg_ws = ws + (size_t)n_long * stride;
+    if (atomic_partial &&
+        hipMemsetAsync(ws, 0, sizeof(float) * (size_t)n_long * stride, s) != hipSuccess)
       return ORYX_ELAUNCH;
     int blocks = (n_seg + 3) / 4;
     if (blocks > max_blocks) blocks = max_blocks;
     switch (kp) {
 #define PART_CASE(KPV)                                                                    \
   case KPV:                                                                               \
-    if (split)                                                                            \
-      hipLaunchKernelGGL((als_partial<KPV, true>), dim3(blocks), dim3(256), 0, s, p, segs,  \
-                         n_seg, ws);                                                      \
-    else                                                                                  \
-      hipLaunchKernelGGL((als_partial<KPV, false>), dim3(blocks), dim3(256), 0, s, p, segs, \
-                         n_seg, ws);                                                      \
+    if (atomic_partial) {                                                                 \
+      if (split)                                                                          \
+        hipLaunchKernelGGL((als_partial<KPV, true>), dim3(blocks), dim3(256), 0, s, p,     \
+                           segs, n_seg, ws, nullptr);                                     \
+      else                                                                                \
+        hipLaunchKernelGGL((als_partial<KPV, false>), dim3(blocks), dim3(256), 0, s, p,    \
+                           segs, n_seg, ws, nullptr);                                     \
+    } else {                                                                              \
+      if (split)                                                                          \
+        hipLaunchKernelGGL((als_partial<KPV, true, true>), dim3(blocks), dim3(256), 0, s,  \
+                           p, segs, n_seg, ws, seg_ws);                                   \
+      else                                                                                \
+        hipLaunchKernelGGL((als_partial<KPV, false, true>), dim3(blocks), dim3(256), 0, s, \
+                           p, segs, n_seg, ws, seg_ws);                                   \
+    }                                                                                     \
     break;
       PART_CASE(16)
       PART_CASE(32)
@@ -213,6 +274,9 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
       default:
         return ORYX_EINVAL;
     }
+    if (!atomic_partial)
+      hipLaunchKernelGGL(als_partial_reduce, dim3((unsigned)n_long, (unsigned)((stride + 255) / 256)),
+                         dim3(256), 0, s, segs, n_seg, seg_ws, ws, stride);
   }
   if (g_als_variant == 5 && g_als_wide_variant == 2 && (split || kp > 64)) {
     // two rows per wave, LDS-DMA gather (als_batch.hip): 64 < KP <= 128 and the fp32 mode

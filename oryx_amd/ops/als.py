@@ -89,10 +89,12 @@ class CSR:
                    order.to(torch.int32).contiguous(), long_slot, segs, n_long)
 
     def workspace(self, kp: int) -> Optional[torch.Tensor]:
-        """fp32 scratch for the split rows' partial normal equations (kernel zeroes it)."""
+        """fp32 scratch for the split rows' partial normal equations: one reduced record per
+        long row, then one record per segment (``als_partial`` stores each segment's record,
+        ``als_partial_reduce`` sums them per row)."""
         if self.n_seg == 0:
             return None
-        need = self.n_long * ws_stride(kp)
+        need = (self.n_long + self.n_seg) * ws_stride(kp)
         if self._ws is None or self._ws.numel() < need or self._ws.device != self.row_ptr.device:
             self._ws = torch.empty(need, dtype=torch.float32, device=self.row_ptr.device)
         return self._ws
