@@ -110,9 +110,12 @@ __global__ __launch_bounds__(256) void als_partial(AlsParams p, const int64_t* _
 // Sum of each long row's segment records (STORE mode of als_partial): block (slot, chunk)
 // adds up floats [256 chunk, 256 chunk + 256) of the slot's records, in segment order (the
 // segments of a slot are contiguous in segs, slot-major).
+// flags (nullable): flags[slot] += 1 once a block's part of the record is written (the
+// batched solve, running concurrently, waits for all of a record's blocks).
 __global__ __launch_bounds__(256) void als_partial_reduce(const int64_t* __restrict__ segs,
                                                          int n_seg, const float* __restrict__ seg_ws,
-                                                         float* __restrict__ ws, int stride) {
+                                                         float* __restrict__ ws, int stride,
+                                                         unsigned* __restrict__ flags) {
   __shared__ int s_lo, s_hi;
   const int slot = blockIdx.x;
   if (threadIdx.x == 0) {
@@ -128,10 +131,16 @@ __global__ __launch_bounds__(256) void als_partial_reduce(const int64_t* __restr
   }
   __syncthreads();
   const int f = blockIdx.y * 256 + threadIdx.x;
-  if (f >= stride) return;
-  float acc = 0.f;
-  for (int sg = s_lo; sg < s_hi; ++sg) acc += seg_ws[(int64_t)sg * stride + f];
-  ws[(int64_t)slot * stride + f] = acc;
+  if (f < stride) {
+    float acc = 0.f;
+    for (int sg = s_lo; sg < s_hi; ++sg) acc += seg_ws[(int64_t)sg * stride + f];
+    ws[(int64_t)slot * stride + f] = acc;
+  }
+  if (flags) {
+    __threadfence();   // this block's writes, agent scope, before the count goes up
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(flags + slot, 1u);
+  }
 }
 
 // ------------------------------------------------------------------ helpers
@@ -197,11 +206,15 @@ int oryx_als_set_wide_variant(int v) {
 
 // long_slot [n_work] (nullable) marks split rows; segs [n_seg][4] = (row, slot, beg, end);
 // ws: workspace of n_long * ws_stride(kp) floats (zeroed here).
+// epoch (1, 2, ... per workspace; 0: no overlap): the long rows' partial sums run on a side
+// stream concurrently with the batched solve, which waits per long row on the flags after
+// the workspace's records (zeroed when the workspace was allocated).
 int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t* col_idx,
                    const float* vals, const void* Y, const float* YtY, float* X, void* Xb,
                    int n_work, int k, int kp, float lambda, float alpha, int implicit,
                    int* fail_count, const int32_t* long_slot, const int64_t* segs, int n_seg,
-                   int n_long, float* ws, int split, long long nnz, void* stream) {
+                   int n_long, float* ws, int split, long long nnz, unsigned epoch,
+                   void* stream) {
   if (n_work <= 0) return ORYX_OK;
   if (n_seg > 0 && (!long_slot || !segs || !ws || n_long <= 0)) return ORYX_EINVAL;
   AlsParams p{row_ptr, row_ids, col_idx, vals, reinterpret_cast<const __bf16*>(Y), YtY, X,
@@ -235,9 +248,37 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
     const char* e = getenv("ORYX_ALS_PARTIAL_ATOMIC");
     return e && atoi(e) == 1;
   }();
+  // the overlap needs the batched kernels (they wait per long row) and the stored records
+  const bool batched = g_als_variant == 5 && (g_als_wide_variant == 2 || (!split && kp <= 64));
+  const bool overlap = n_seg > 0 && epoch > 0 && batched && !atomic_partial;
+  hipStream_t ps = s;   // the stream of the long rows' partial sums
+  hipEvent_t done = nullptr;
+  if (overlap) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return ORYX_ELAUNCH;
+    static hipStream_t side[16] = {};
+    static hipEvent_t ev_in[16] = {}, ev_done[16] = {};
+    if (!side[dev]) {
+      if (hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&ev_in[dev], hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&ev_done[dev], hipEventDisableTiming) != hipSuccess)
+        return ORYX_ELAUNCH;
+    }
+    // the side stream starts after everything already queued on s (the factors it reads)
+    if (hipEventRecord(ev_in[dev], s) != hipSuccess ||
+        hipStreamWaitEvent(side[dev], ev_in[dev], 0) != hipSuccess)
+      return ORYX_ELAUNCH;
+    ps = side[dev];
+    done = ev_done[dev];
+  }
   if (n_seg > 0) {
+    // ws: n_long reduced records | n_seg segment records | n_long uint32 flags
     const int stride = ws_stride(kp);
     float* seg_ws = ws + (size_t)n_long * stride;
+    // (counted at every epoch, overlapped or not, so that they keep pace with the epochs)
+    unsigned* flags = epoch > 0 && !atomic_partial
+                          ? reinterpret_cast<unsigned*>(ws + (size_t)(n_long + n_seg) * stride)
+                          : nullptr;
     if (atomic_partial &&
         hipMemsetAsync(ws, 0, sizeof(float) * (size_t)n_long * stride, s) != hipSuccess)
       return ORYX_ELAUNCH;
@@ -255,11 +296,11 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
                            segs, n_seg, ws, nullptr);                                     \
     } else {                                                                              \
       if (split)                                                                          \
-        hipLaunchKernelGGL((als_partial<KPV, true, true>), dim3(blocks), dim3(256), 0, s,  \
+        hipLaunchKernelGGL((als_partial<KPV, true, true>), dim3(blocks), dim3(256), 0, ps, \
                            p, segs, n_seg, ws, seg_ws);                                   \
       else                                                                                \
-        hipLaunchKernelGGL((als_partial<KPV, false, true>), dim3(blocks), dim3(256), 0, s, \
-                           p, segs, n_seg, ws, seg_ws);                                   \
+        hipLaunchKernelGGL((als_partial<KPV, false, true>), dim3(blocks), dim3(256), 0,    \
+                           ps, p, segs, n_seg, ws, seg_ws);                               \
     }                                                                                     \
     break;
       PART_CASE(16)
@@ -274,25 +315,37 @@ int oryx_als_solve(const int64_t* row_ptr, const int32_t* row_ids, const int32_t
       default:
         return ORYX_EINVAL;
     }
-    if (!atomic_partial)
-      hipLaunchKernelGGL(als_partial_reduce, dim3((unsigned)n_long, (unsigned)((stride + 255) / 256)),
-                         dim3(256), 0, s, segs, n_seg, seg_ws, ws, stride);
+    if (!atomic_partial) {
+      const unsigned chunks = (unsigned)((stride + 255) / 256);
+      hipLaunchKernelGGL(als_partial_reduce, dim3((unsigned)n_long, chunks), dim3(256), 0, ps,
+                         segs, n_seg, seg_ws, ws, stride, flags);
+      if (overlap) {
+        // the batched solve takes the long rows (first in row_ids) last and waits for each
+        // row's record: every one of its `chunks` reduce blocks of this epoch counted
+        p.rot = n_long < n_work ? n_long : 0;
+        p.part_flags = flags;
+        p.part_want = epoch * chunks;
+        if (hipEventRecord(done, ps) != hipSuccess) return ORYX_ELAUNCH;
+      }
+    }
   }
+  if (oryx_check_launch() != ORYX_OK) return ORYX_ELAUNCH;
+  int rc = -1;
   if (g_als_variant == 5 && g_als_wide_variant == 2 && (split || kp > 64)) {
     // two rows per wave, LDS-DMA gather (als_batch.hip): 64 < KP <= 128 and the fp32 mode
     const int cus = resident_panel_blocks / 2;
     const long long mean_len = n_work > 0 ? nnz / n_work : 0;
-    if (const int rc = oryx_als::batch_gl_launch(p, kp, split != 0, env_blocks ? env_blocks : cus,
-                                                 mean_len, s))
-      return rc;
-    return ORYX_OK;
-  }
-  if (g_als_variant == 5 && !split && kp <= 64) {
-    // four rows per wave, one wave per SIMD: one resident block per CU
+    rc = oryx_als::batch_gl_launch(p, kp, split != 0, env_blocks ? env_blocks : cus, mean_len,
+                                   s);
+  } else if (g_als_variant == 5 && !split && kp <= 64) {
+    // two rows per wave, two waves per SIMD (als_batch.hip)
     const int cus = resident_panel_blocks / 2;
-    if (const int rc = oryx_als::batch_solve_launch(p, kp, env_blocks ? env_blocks : cus, s))
-      return rc;
-    return ORYX_OK;
+    rc = oryx_als::batch_solve_launch(p, kp, env_blocks ? env_blocks : cus, s);
+  }
+  if (rc >= 0) {
+    // later work on s (the next half-step rewrites the workspace) follows the side stream
+    if (done && hipStreamWaitEvent(s, done, 0) != hipSuccess) return ORYX_ELAUNCH;
+    return rc;
   }
   // a superseded kernel selected for an A/B run: only in the tuning build
   if (!oryx_als_solve_variant) return ORYX_EINVAL;
@@ -321,7 +374,7 @@ int oryx_als_batch_profile(unsigned long long* prof) {
 // 1 when the superseded kernels (tuning/als_variants.hip) are linked into this library
 int oryx_als_tuning_available() { return oryx_als_solve_variant ? 1 : 0; }
 
-int oryx_kernels_version() { return 24; }
+int oryx_kernels_version() { return 25; }
 
 int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 

@@ -208,6 +208,7 @@ __device__ __forceinline__ void batch_solve(const AlsParams& p, int lane,
     reduce_bpart<M>(bpart[m]);   // lane (g, f): bpart[m][pi] = b_m[16 pi + f]
     if (slot[m] >= 0) {
       // split row: Gramian, b and count were summed by als_partial into ws[slot]
+      wait_long_row(p, slot[m]);
       const float* src = p.ws + (int64_t)slot[m] * ws_stride(KP);
 #pragma unroll
       for (int pi = 0; pi < M; ++pi)
@@ -441,6 +442,7 @@ __device__ __forceinline__ void batch_solve(const AlsParams& p, int lane,
     reduce_bpart<M>(bpart[m]);   // lane (g, f): bpart[m][pi] = b_m[16 pi + f]
     if (slot[m] >= 0) {
       // split row: Gramian, b and count were summed by als_partial into ws[slot]
+      wait_long_row(p, slot[m]);
       const float* src = p.ws + (int64_t)slot[m] * ws_stride(KP);
 #pragma unroll
       for (int pi = 0; pi < M; ++pi)
@@ -747,7 +749,9 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
       constexpr int m = decltype(Mc)::value;
       const int w = b * NM + m;
       valid_n[m] = w < p.n_work;
-      const int ww = valid_n[m] ? w : p.n_work - 1;   // tail: a real row, solved, not stored
+      int ww = valid_n[m] ? w : p.n_work - 1;   // tail: a real row, solved, not stored
+      ww += p.rot;                                  // (rotated: the long rows come last)
+      ww -= ww >= p.n_work ? p.n_work : 0;
       rows_n[m] = p.row_ids ? sload(p.row_ids, ww) : ww;
       slot_n[m] = (valid_n[m] && p.long_slot) ? sload(p.long_slot, ww) : -1;
     });
@@ -1195,7 +1199,9 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
       constexpr int m = decltype(Mc)::value;
       const int w = b * NM + m;
       valid_n[m] = w < p.n_work;
-      const int ww = valid_n[m] ? w : p.n_work - 1;   // tail: a real row, solved, not stored
+      int ww = valid_n[m] ? w : p.n_work - 1;   // tail: a real row, solved, not stored
+      ww += p.rot;                                  // (rotated: the long rows come last)
+      ww -= ww >= p.n_work ? p.n_work : 0;
       rows_n[m] = p.row_ids ? sload(p.row_ids, ww) : ww;
       slot_n[m] = (valid_n[m] && p.long_slot) ? sload(p.long_slot, ww) : -1;
     });

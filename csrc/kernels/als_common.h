@@ -26,7 +26,34 @@ struct AlsParams {
   // ws[slot] (summed beforehand by als_partial over fixed-size segments of the row)
   const int32_t* long_slot;  // [n_work] (nullable)
   const float* ws;           // [n_long][ws_stride(KP)]
+  // the long rows' records are reduced on a concurrent stream while the batched solve runs:
+  // it takes its work items rotated by rot (the long rows, first in row_ids, come last) and
+  // waits until part_flags[slot] reaches part_want before reading ws[slot] (nullable: the
+  // records were complete before the launch)
+  int rot = 0;
+  const unsigned* part_flags = nullptr;
+  unsigned part_want = 0;
 };
+
+// Wait (lane 0 of the wave, bounded) until a long row's reduced record is complete, then
+// acquire at agent scope: the record was written on other CUs / XCDs.  A timeout (2 s) marks
+// the solve failed (fail_count += 2^20) instead of hanging the GPU.
+__device__ __forceinline__ void wait_long_row(const AlsParams& p, int slot) {
+  if (!p.part_flags) return;
+  if ((threadIdx.x & 63) == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(p.part_flags + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           p.part_want) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+        if (p.fail_count) atomicAdd(p.fail_count, 1 << 20);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // als_batch.hip: four rows per wave, block-LDL^T solve (KP <= 64, bf16 factors)
 int batch_solve_launch(const AlsParams& p, int kp, int max_blocks, hipStream_t s);

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 24
+KERNELS_ABI_VERSION = 25
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -232,10 +232,11 @@ def _load_kernels():
         raise RuntimeError("ORYX_ALS_WIDE_VARIANT=%s needs the tuning build of the kernels "
                            "(python -m oryx_amd._build --tuning; ORYX_KERNELS_SO=%s)"
                            % (os.environ.get("ORYX_ALS_WIDE_VARIANT"), _build.TUNING_SO))
-    # ..., n_long, ws, split (fp32 factors as bf16 hi|lo rows of 2*kp), stream
+    # ..., n_long, ws, split (fp32 factors as bf16 hi|lo rows of 2*kp), nnz, epoch (long
+    # rows' partial sums beside the solve; 0 = before it), stream
     _sig(lib, "oryx_als_solve", c_i, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i, c_i,
                                       c_i, c_f, c_f, c_i, c_vp, c_vp, c_vp, c_i, c_i, c_vp,
-                                      c_i, c_ll, c_vp])
+                                      c_i, c_ll, ctypes.c_uint, c_vp])
     _sig(lib, "oryx_als_ws_stride", c_i, [c_i])
     _sig(lib, "oryx_gramian_ws_floats", c_i, [c_i])
     _sig(lib, "oryx_als_tuning_available", c_i, [])

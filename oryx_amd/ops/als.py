@@ -57,6 +57,7 @@ class CSR:
     segs: Optional[torch.Tensor] = None
     n_long: int = 0
     _ws: Optional[torch.Tensor] = None
+    _ws_epoch: int = 0
 
     @property
     def nnz(self) -> int:
@@ -91,13 +92,22 @@ class CSR:
     def workspace(self, kp: int) -> Optional[torch.Tensor]:
         """fp32 scratch for the split rows' partial normal equations: one reduced record per
         long row, then one record per segment (``als_partial`` stores each segment's record,
-        ``als_partial_reduce`` sums them per row)."""
+        ``als_partial_reduce`` sums them per row), then one uint32 completion counter per
+        long row (zeroed here; the solves count epochs on it, :meth:`next_epoch`)."""
         if self.n_seg == 0:
             return None
-        need = (self.n_long + self.n_seg) * ws_stride(kp)
+        need = (self.n_long + self.n_seg) * ws_stride(kp) + self.n_long
         if self._ws is None or self._ws.numel() < need or self._ws.device != self.row_ptr.device:
-            self._ws = torch.empty(need, dtype=torch.float32, device=self.row_ptr.device)
+            self._ws = torch.zeros(need, dtype=torch.float32, device=self.row_ptr.device)
+            self._ws_epoch = 0
         return self._ws
+
+    def next_epoch(self) -> int:
+        """The epoch of the next solve on this workspace (1, 2, ...; its counters never
+        reset: a long row's counter reaches epoch x blocks once that solve's record is
+        complete)."""
+        self._ws_epoch += 1
+        return self._ws_epoch
 
 
 # Rows longer than the split threshold are cut into segments (one wave each, partial normal
@@ -269,6 +279,11 @@ def _use_kernel(device: torch.device, kp: int) -> bool:
     return device.type == "cuda" and kp in _KERNEL_KPS
 
 
+# the long rows' partial sums run on a side stream beside the batched solve (which waits per
+# long row); ORYX_ALS_PARTIAL_OVERLAP=0 runs them before it on the same stream
+_PARTIAL_OVERLAP = os.environ.get("ORYX_ALS_PARTIAL_OVERLAP", "1") != "0"
+
+
 def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_out: torch.Tensor,
                xb_out: Optional[torch.Tensor], k: int, lam: float, alpha: float,
                implicit: bool, y_f32: Optional[torch.Tensor] = None,
@@ -310,7 +325,9 @@ def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_ou
                                 csr.segs.data_ptr() if csr.n_seg else None,
                                 csr.n_seg, csr.n_long,
                                 ws.data_ptr() if ws is not None else None,
-                                int(bool(split)), int(csr.nnz), native.stream_ptr(device))
+                                int(bool(split)), int(csr.nnz),
+                                csr.next_epoch() if (ws is not None and _PARTIAL_OVERLAP) else 0,
+                                native.stream_ptr(device))
         native.check(rc, "oryx_als_solve")
         return
     # exact reference path (CPU, or ranks beyond the kernel's range)
