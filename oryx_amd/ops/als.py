@@ -279,9 +279,12 @@ def _use_kernel(device: torch.device, kp: int) -> bool:
     return device.type == "cuda" and kp in _KERNEL_KPS
 
 
-# the long rows' partial sums run on a side stream beside the batched solve (which waits per
-# long row); ORYX_ALS_PARTIAL_OVERLAP=0 runs them before it on the same stream
-_PARTIAL_OVERLAP = os.environ.get("ORYX_ALS_PARTIAL_OVERLAP", "1") != "0"
+# ORYX_ALS_PARTIAL_OVERLAP=1: the long rows' partial sums run on a side stream beside the
+# batched solve (which takes the split rows last and waits per row).  Off by default: the
+# resident solve grid holds every CU, so the partial sums only start as solve blocks retire
+# and the waiting rows end up on the critical path -- rank 64 items 1.03 ms against 0.61
+# serial, rank 128 fp32 5.54 against 4.04 (profiles/r5_partial_overlap_ab.txt)
+_PARTIAL_OVERLAP = os.environ.get("ORYX_ALS_PARTIAL_OVERLAP", "0") == "1"
 
 
 def solve_rows(csr: CSR, y_bf16: torch.Tensor, yty: Optional[torch.Tensor], x_out: torch.Tensor,
