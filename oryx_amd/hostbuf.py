@@ -1,0 +1,59 @@
+"""Large host byte buffers whose memory is returned off the caller's thread
+(``csrc/runtime/oryx_hostbuf.cpp``).
+
+The batch layer's text -- a generation's drain, its train / test selections, concatenations
+of new and past data -- lives in uint8 arrays of up to tens of GB.  Dropping the last reference
+to a numpy-allocated one unmaps it right there, with the GIL held (~65 ms per GB with 4 KB
+pages); the reference's Spark executors leave that to the JVM's background collector
+(``[lambda]/batch/BatchUpdateFunction.java:103-130``).  :func:`empty` returns an array over a
+native mapping instead; when the array and every view of it are gone, a finalizer queues the
+unmap on the runtime's reaper thread and returns.
+
+``ORYX_HOSTBUF=0`` turns this off (plain ``np.empty``); ``ORYX_HOSTBUF_MIN_MB`` (default 64)
+is the smallest buffer that takes the native path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import weakref
+
+import numpy as np
+
+from . import native
+
+__all__ = ["empty", "stats", "quiesce"]
+
+_MIN = int(float(os.environ.get("ORYX_HOSTBUF_MIN_MB", "64")) * (1 << 20))
+_ON = os.environ.get("ORYX_HOSTBUF", "1") != "0"
+
+
+def empty(n: int) -> np.ndarray:
+    """An uninitialised (in fact zero-filled) uint8 array of ``n`` bytes."""
+    n = int(n)
+    if not _ON or n < _MIN:
+        return np.empty(n, dtype=np.uint8)
+    lib = native.runtime()
+    p = lib.oryx_hostbuf_alloc(n)
+    if not p:
+        return np.empty(n, dtype=np.uint8)
+    raw = (ctypes.c_uint8 * n).from_address(p)
+    # the array's base chain (memoryview -> ctypes array) keeps ``raw`` alive as long as any
+    # view of the buffer exists; the finalizer runs once the last one is gone
+    fin = weakref.finalize(raw, lib.oryx_hostbuf_free, p, n)
+    fin.atexit = False
+    return np.frombuffer(raw, dtype=np.uint8)
+
+
+def stats() -> dict:
+    """Bytes queued for unmapping and bytes unmapped by the reaper so far."""
+    out = (ctypes.c_longlong * 2)()
+    native.runtime().oryx_hostbuf_stats(out)
+    return {"pending_bytes": int(out[0]), "freed_bytes": int(out[1])}
+
+
+def quiesce(timeout_s: float = -1.0) -> int:
+    """Waits for queued unmaps (tests, memory-tight phases); returns the bytes still pending."""
+    ms = -1 if timeout_s < 0 else int(timeout_s * 1e3)
+    return int(native.runtime().oryx_hostbuf_quiesce(ms))

@@ -14,7 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import native
+from . import hostbuf, native
 
 __all__ = ["IdDict", "parse_ratings", "format_float_rows", "format_als_updates",
            "parse_up_batch"]
@@ -905,7 +905,7 @@ def read_gzip(raw: bytes):
     if size < 0:
         import gzip
         return gzip.decompress(raw)
-    out = np.empty(max(1, size), dtype=np.uint8)
+    out = hostbuf.empty(max(1, size))
     got = lib.oryx_gzip_indexed_inflate(raw, len(raw), out.ctypes.data_as(ctypes.c_void_p),
                                         size)
     if got != size:

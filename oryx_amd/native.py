@@ -92,6 +92,10 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_dict_merge", c_ll, [c_vp, c_vp, c_vp])
     _sig(lib, "oryx_dict_key", c_ll, [c_vp, c_ll, c_vp, c_ll])
     _sig(lib, "oryx_line_ends", c_ll, [c_vp, c_ll, c_vp, c_ll])
+    _sig(lib, "oryx_hostbuf_alloc", c_vp, [c_ll])
+    _sig(lib, "oryx_hostbuf_free", None, [c_vp, c_ll])
+    _sig(lib, "oryx_hostbuf_stats", None, [c_vp])
+    _sig(lib, "oryx_hostbuf_quiesce", c_ll, [c_ll])
     _sig(lib, "oryx_gather_lines", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_concat_buffers", c_ll, [c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_reader_poll_frames", c_ll, [c_vp, c_vp, c_ll, ctypes.c_int,

@@ -19,7 +19,7 @@ from typing import Iterable, List, Optional, Sequence, Union
 
 import numpy as np
 
-from . import native
+from . import hostbuf, native
 
 __all__ = ["TextLines", "concat_lines", "as_buffer"]
 
@@ -177,7 +177,7 @@ class TextLines(collections.abc.Sequence):
         e = self.ends()
         starts = np.r_[0, e[:-1] + 1]
         size = int((e[idx] - starts[idx] + 1).sum())
-        out = np.empty(size, dtype=np.uint8)
+        out = hostbuf.empty(size)
         idx = np.ascontiguousarray(idx, dtype=np.int64)
         native.runtime().oryx_gather_lines(_addr(self.buf), e.ctypes.data, idx.ctypes.data,
                                            len(idx), out.ctypes.data)
@@ -196,7 +196,7 @@ def concat_lines(parts: Sequence[Union[TextLines, Sequence[str], None]]):
         bufs = [np.frombuffer(p.buf, dtype=np.uint8) if not isinstance(p.buf, np.ndarray)
                 else np.ascontiguousarray(p.buf) for p in parts]
         lens = np.array([len(b) for b in bufs], dtype=np.int64)
-        out = np.empty(int(lens.sum()), dtype=np.uint8)
+        out = hostbuf.empty(int(lens.sum()))
         ptrs = np.array([b.ctypes.data for b in bufs], dtype=np.uint64)
         # threaded native copy (hundreds of MB per drain)
         native.runtime().oryx_concat_buffers(ptrs.ctypes.data, lens.ctypes.data, len(bufs),

@@ -27,7 +27,7 @@ from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from .. import native
+from .. import hostbuf, native
 from ..utils import faults
 
 __all__ = ["Topic", "PartitionReader", "TopicConsumer", "Record", "get_offsets", "set_offsets",
@@ -405,7 +405,7 @@ class PartitionReader:
         if start >= end_offset:
             return TextLines(b"", 0), 0
         cap = max(int(lib.oryx_reader_text_bound(self._r, int(end_offset))), 1 << 16)
-        buf = np.empty(cap, dtype=np.uint8)
+        buf = hostbuf.empty(cap)
         used_total = total = 0
         used = ctypes.c_longlong(0)
         flags = ctypes.c_int(0)
@@ -424,7 +424,7 @@ class PartitionReader:
             if flags.value & 4:
                 # more was appended since the bound was taken: grow
                 cap = max(2 * cap, used_total + int(used.value))
-                grown = np.empty(cap, dtype=np.uint8)
+                grown = hostbuf.empty(cap)
                 grown[:used_total] = buf[:used_total]
                 buf = grown
                 continue
