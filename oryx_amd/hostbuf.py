@@ -23,7 +23,7 @@ import numpy as np
 
 from . import native
 
-__all__ = ["empty", "stats", "quiesce"]
+__all__ = ["empty", "read_text_file", "stats", "quiesce"]
 
 _MIN = int(float(os.environ.get("ORYX_HOSTBUF_MIN_MB", "64")) * (1 << 20))
 _ON = os.environ.get("ORYX_HOSTBUF", "1") != "0"
@@ -44,6 +44,23 @@ def empty(n: int) -> np.ndarray:
     fin = weakref.finalize(raw, lib.oryx_hostbuf_free, p, n)
     fin.atexit = False
     return np.frombuffer(raw, dtype=np.uint8)
+
+
+def read_text_file(path: str) -> np.ndarray:
+    """The bytes of a text file as a uint8 array ending with a newline (one is appended when
+    the file lacks it), read by concurrent native preads into an :func:`empty` buffer."""
+    size = os.path.getsize(path)
+    out = empty(size + 1)
+    got = int(native.runtime().oryx_read_file_parallel(os.fsencode(path), out.ctypes.data,
+                                                       size, min(16, os.cpu_count() or 1)))
+    if got < 0:
+        raise OSError(-got, os.strerror(-got), path)
+    if got == 0:
+        return out[:0]
+    if out[got - 1] != 10:
+        out[got] = 10
+        got += 1
+    return out[:got]
 
 
 def stats() -> dict:

@@ -37,7 +37,7 @@ import threading
 import time
 from typing import List, Optional, Tuple
 
-from .. import tracing
+from .. import hostbuf, tracing
 from ..api import BatchLayerUpdate, Dataset
 from ..transport.producer import LogTopicProducer
 from ..utils import config as cfg
@@ -122,9 +122,8 @@ def read_past_data(data_dir: str, rank: int = 0, world: int = 1) -> Dataset:
             # the file's bytes are the message buffer (no per-line strings), keyed by the
             # file's identity so apps can reuse their parse of it (models/als/history.py)
             st = os.stat(path)
-            with open(path, "rb") as f:
-                texts.append(TextLines.from_bytes(f.read()).with_key(
-                    ("part", os.path.abspath(path), st.st_size, st.st_mtime_ns)))
+            texts.append(TextLines(hostbuf.read_text_file(path)).with_key(
+                ("part", os.path.abspath(path), st.st_size, st.st_mtime_ns)))
             continue
         with open(path, "r", encoding="utf-8") as f:
             for line in f:

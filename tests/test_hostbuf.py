@@ -50,3 +50,19 @@ def test_text_selection_and_concat_on_native_buffers_cpu(monkeypatch):
     del sel, both
     gc.collect()
     assert hostbuf.quiesce(10) == 0
+
+
+def test_read_text_file_parallel_pieces_and_final_newline_cpu(tmp_path, monkeypatch):
+    monkeypatch.setattr(hostbuf, "_MIN", 1 << 20)
+    rs = np.random.default_rng(0)
+    body = rs.integers(48, 58, size=(70 << 20) + 12345, dtype=np.uint8)   # > 2 pieces
+    body[::97] = 10
+    for tail in (b"", b"x", b"\n"):
+        p = tmp_path / "part-00000.txt"
+        data = body.tobytes() + tail
+        p.write_bytes(data)
+        got = hostbuf.read_text_file(str(p))
+        want = data if data.endswith(b"\n") else data + b"\n"
+        assert got.tobytes() == want
+    p.write_bytes(b"")
+    assert len(hostbuf.read_text_file(str(p))) == 0
