@@ -46,7 +46,13 @@ struct Reaper {
       auto job = q.front();
       q.pop_front();
       lk.unlock();
-      munmap(job.first, job.second);
+      // in 64 MB pieces: munmap holds the process's mmap lock for writing while it frees a
+      // range, and a whole 17 GB buffer at once stalled every page fault of the layer's own
+      // thread for ~1 s (measured: a k-means model publish went from 0.02 to 1.09 s)
+      constexpr size_t kPiece = 64u << 20;
+      char* base = static_cast<char*>(job.first);
+      for (size_t off = 0; off < job.second; off += kPiece)
+        munmap(base + off, job.second - off < kPiece ? job.second - off : kPiece);
       lk.lock();
       pending -= (long long)job.second;
       freed += (long long)job.second;

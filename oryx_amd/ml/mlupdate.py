@@ -33,8 +33,10 @@ import os
 import time
 from typing import Any, List, Optional, Sequence, Tuple
 
+import numpy as np
+
 from ..api import BatchLayerUpdate, Dataset, TopicProducer
-from ..textlines import TextLines, concat_lines
+from ..textlines import LineSelection, TextLines, concat_lines
 from .. import tracing
 from ..parallel import dist
 from ..utils import ioutils, lang, pmml as pmmlu, rng
@@ -110,6 +112,11 @@ class MLUpdate(BatchLayerUpdate):
         """Default: random split with probability ``test_fraction`` per datum."""
         gen = rng.get_random().generator
         mask = gen.random(len(new_data)) < self.test_fraction
+        if isinstance(new_data, TextLines) and not isinstance(new_data, LineSelection):
+            # lazy selections: no text is copied unless a consumer asks for the bytes (the
+            # feature apps' parser selects parsed rows instead, models/features.py)
+            return (LineSelection(new_data, np.flatnonzero(~mask)),
+                    LineSelection(new_data, np.flatnonzero(mask)))
         if isinstance(new_data, TextLines):
             return new_data.take(~mask), new_data.take(mask)
         train = [d for d, m in zip(new_data, mask) if not m]

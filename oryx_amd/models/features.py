@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import weakref
 from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -36,7 +37,7 @@ import numpy as np
 import torch
 
 from .. import ingest, native
-from ..textlines import TextLines
+from ..textlines import LineConcat, LineSelection, TextLines, _Lazy
 from .schema import InputSchema
 
 log = logging.getLogger(__name__)
@@ -72,6 +73,7 @@ class _Seg:
     full: torch.Tensor                 # categorical columns hold segment-local codes
     values: Dict[int, List[str]]       # categorical feature -> segment-local distinct values
     nbytes: int
+    owned: bool = False                # ``full`` is this parse's own (not a cached tensor)
 
 
 def _buf_view(buf) -> np.ndarray:
@@ -256,7 +258,10 @@ def _merge(segs: List[_Seg], schema: InputSchema, device) -> FeatureBlock:
     cats = [f for f in range(F) if schema.is_categorical(f)]
     if not segs:
         return FeatureBlock(torch.zeros((0, F), device=device), {f: [] for f in cats})
-    full = torch.cat([sg.full for sg in segs]) if len(segs) > 1 else segs[0].full.clone()
+    if len(segs) > 1:
+        full = torch.cat([sg.full for sg in segs])
+    else:
+        full = segs[0].full if segs[0].owned else segs[0].full.clone()
     values: Dict[int, List[str]] = {}
     for f in cats:
         index: Dict[str, int] = {}
@@ -273,6 +278,37 @@ def _merge(segs: List[_Seg], schema: InputSchema, device) -> FeatureBlock:
             pos += n
         values[f] = list(index.keys())
     return FeatureBlock(full, values)
+
+
+def _select_rows(parent: _Seg, index: np.ndarray, cats: List[int], device) -> _Seg:
+    """Rows ``index`` of a parsed block, categorical codes renumbered in their order of first
+    appearance among those rows (what a parse of just those lines assigns)."""
+    full = parent.full.index_select(0, torch.from_numpy(index).to(device))
+    values: Dict[int, List[str]] = {}
+    for f in cats:
+        pv = parent.values.get(f, [])
+        col = full[:, f]
+        ok = ~torch.isnan(col)
+        c = col[ok].long()
+        if not pv or c.numel() == 0:
+            values[f] = []
+            continue
+        n = c.numel()
+        first = torch.full((len(pv),), n, dtype=torch.int64, device=device)
+        first.scatter_reduce_(0, c, torch.arange(n, device=device), reduce="amin")
+        present = torch.nonzero(first < n).flatten()
+        order = present[torch.argsort(first[present])]
+        remap = torch.full((len(pv),), -1, dtype=torch.int64, device=device)
+        remap[order] = torch.arange(order.numel(), device=device)
+        col[ok] = remap[c].to(full.dtype)
+        values[f] = [pv[i] for i in order.tolist()]
+    return _Seg(full, values, 0, owned=True)
+
+
+# parse of the parent of LineSelections (the interval a train / test split selects from),
+# shared by the train parse and the evaluation's test parse of one generation:
+# (id(parent), schema key, device) -> (weak reference to the parent, its parse)
+_SELECTION_PARENTS: "Dict[tuple, Tuple[weakref.ref, _Seg]]" = {}
 
 
 def parse_features(lines, schema: InputSchema, device, dtype: torch.dtype = torch.float32,
@@ -336,9 +372,63 @@ class FeatureHistory:
         if not isinstance(lines, TextLines):
             lines = TextLines.from_strings([l for l in lines]) if len(lines) else \
                 TextLines(b"", 0)
+        parts = lines.parts if isinstance(lines, LineConcat) else [lines]
+        segs: List[_Seg] = []
+        keyed: set = set()
+        for part in parts:
+            sg = self._selection(part, schema, dtype, key_s, keyed) \
+                if isinstance(part, LineSelection) else None
+            if sg is not None:
+                segs.append(sg)
+                continue
+            if isinstance(part, _Lazy):
+                part = part.materialize()
+            got = self._text_segs(part, schema, dtype, keyed)
+            if got is None:
+                # a line the native parser does not take: the general parser for all
+                full, values = _python_block(list(lines), schema, dtype)
+                blk = FeatureBlock(torch.from_numpy(full).to(self.device), {})
+                blk.values = values
+                return blk
+            segs.extend(got)
+        if self.keep:
+            for k in [k for k in self._segs if k not in keyed]:
+                del self._segs[k]
+        return _merge(segs, schema, self.device)
+
+    def _selection(self, part: LineSelection, schema: InputSchema, dtype, key_s,
+                   keyed: set) -> Optional[_Seg]:
+        """A train / test selection: its rows of the parent's parse (parsed once per parent
+        and shared through ``_SELECTION_PARENTS``), or None to parse its own text."""
+        parent = part.parent
+        if isinstance(parent, _Lazy) or not len(part):
+            return None
+        mk = (id(parent), key_s, str(self.device))
+        hit = _SELECTION_PARENTS.get(mk)
+        psg = hit[1] if hit is not None and hit[0]() is parent else None
+        if psg is None:
+            got = self._text_segs(parent, schema, dtype, keyed)
+            if not got:
+                return None
+            blk = _merge(got, schema, self.device)
+            if int(blk.full.shape[0]) != len(parent):
+                return None       # (an empty line the parser skips: rows and lines differ)
+            psg = _Seg(blk.full, blk.values, parent.nbytes())
+            for k in [k for k, v in _SELECTION_PARENTS.items() if v[0]() is None]:
+                del _SELECTION_PARENTS[k]
+            ref = weakref.ref(parent, lambda _r, mk=mk: _SELECTION_PARENTS.pop(mk, None))
+            _SELECTION_PARENTS[mk] = (ref, psg)
+        else:
+            self.stats["selection_hits"] = self.stats.get("selection_hits", 0) + 1
+        cats = [f for f in range(schema.get_num_features()) if schema.is_categorical(f)]
+        return _select_rows(psg, part.index, cats, self.device)
+
+    def _text_segs(self, lines: TextLines, schema: InputSchema, dtype,
+                   keyed: set) -> Optional[List[_Seg]]:
+        """The parse of each byte segment of ``lines`` (cached ones reused, keyed ones added to
+        ``keyed``), or None when a line needs the general parser."""
         buf = _buf_view(lines.joined())
         segs: List[_Seg] = []
-        keyed = set()
         off = 0
         for key, n_lines, nbytes in lines.segment_list():
             if nbytes == 0:
@@ -359,11 +449,7 @@ class FeatureHistory:
                 else:
                     sg = self._parse_range(buf, off, nbytes, n_lines, schema, dtype)
                     if sg is None:
-                        # a line the native parser does not take: the general parser for all
-                        full, values = _python_block(list(lines), schema, dtype)
-                        blk = FeatureBlock(torch.from_numpy(full).to(self.device), {})
-                        blk.values = values
-                        return blk
+                        return None
                     self.stats["misses"] += 1
                     self.stats["parsed_bytes"] += nbytes
                     if key is None and dg is not None:
@@ -376,7 +462,4 @@ class FeatureHistory:
                 keyed.add(key)
             segs.append(sg)
             off += nbytes
-        if self.keep:
-            for k in [k for k in self._segs if k not in keyed]:
-                del self._segs[k]
-        return _merge(segs, schema, self.device)
+        return segs

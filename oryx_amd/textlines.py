@@ -21,7 +21,7 @@ import numpy as np
 
 from . import hostbuf, native
 
-__all__ = ["TextLines", "concat_lines", "as_buffer"]
+__all__ = ["TextLines", "LineSelection", "LineConcat", "concat_lines", "as_buffer"]
 
 _NL = 10
 
@@ -41,7 +41,7 @@ class TextLines(collections.abc.Sequence):
     natively on first indexed access.
     """
 
-    __slots__ = ("buf", "_n", "_ends", "_strs", "segments")
+    __slots__ = ("buf", "_n", "_ends", "_strs", "segments", "__weakref__")
 
     def __init__(self, buf, n: Optional[int] = None, ends: Optional[np.ndarray] = None):
         if isinstance(buf, memoryview):
@@ -184,14 +184,106 @@ class TextLines(collections.abc.Sequence):
         return TextLines(out, len(idx))
 
 
+class _Lazy(TextLines):
+    """A :class:`TextLines` whose bytes are built only when something reads them: every
+    accessor goes through :meth:`materialize`.  Parsers that understand the subclasses
+    (``models.features.FeatureHistory``) work from their parts instead."""
+
+    __slots__ = ("_mat",)
+
+    def materialize(self) -> TextLines:
+        if self._mat is None:
+            self._mat = self._build()
+        return self._mat
+
+    def _build(self) -> TextLines:
+        raise NotImplementedError
+
+    buf = property(lambda self: self.materialize().buf)
+
+    def ends(self) -> np.ndarray:
+        return self.materialize().ends()
+
+    def nbytes(self) -> int:
+        return self.materialize().nbytes()
+
+    def segment_list(self) -> List[tuple]:
+        return self.materialize().segment_list()
+
+    def with_key(self, key) -> "TextLines":
+        return self.materialize().with_key(key)
+
+    def __getitem__(self, j):
+        return self.materialize()[j]
+
+    def __iter__(self):
+        return iter(self.materialize())
+
+    def _decode_all(self) -> List[str]:
+        return self.materialize()._decode_all()
+
+    def take(self, sel) -> "TextLines":
+        return self.materialize().take(sel)
+
+    def __repr__(self):
+        return "%s[%d lines]" % (type(self).__name__, self._n)
+
+
+class LineSelection(_Lazy):
+    """Lines ``index`` (increasing) of ``parent``, gathered into a buffer of their own only if
+    one is asked for.  The random train / test split of the feature apps
+    (``MLUpdate.split_new_data_to_train_test``) returns these: their parser parses the parent
+    once and selects rows on the device, so the split copies no text and the parse of the
+    whole interval is the one a later generation adopts for its part file."""
+
+    __slots__ = ("parent", "index")
+
+    def __init__(self, parent: TextLines, index: np.ndarray):
+        self.parent = parent
+        self.index = np.ascontiguousarray(index, dtype=np.int64)
+        self._n = len(self.index)
+        self._ends = None
+        self._strs = None
+        self.segments = None
+        self._mat = None
+
+    def _build(self) -> TextLines:
+        return self.parent.take(self.index)
+
+
+class LineConcat(_Lazy):
+    """``parts`` one after another (the train selection followed by past part files),
+    concatenated only if a buffer is asked for."""
+
+    __slots__ = ("parts",)
+
+    def __init__(self, parts: Sequence[TextLines]):
+        flat: List[TextLines] = []
+        for p in parts:
+            flat.extend(p.parts if isinstance(p, LineConcat) else [p])
+        self.parts = flat
+        self._n = sum(len(p) for p in flat)
+        self._ends = None
+        self._strs = None
+        self.segments = None
+        self._mat = None
+
+    def _build(self) -> TextLines:
+        return concat_lines([p.materialize() if isinstance(p, _Lazy) else p
+                             for p in self.parts])
+
+
 def concat_lines(parts: Sequence[Union[TextLines, Sequence[str], None]]):
     """Concatenation that stays a :class:`TextLines` when every non-empty part is one (else a
-    plain list of strings)."""
+    plain list of strings); a :class:`LineConcat` when a part is a lazy selection."""
     parts = [p for p in parts if p is not None and len(p)]
     if not parts:
         return TextLines(b"", 0)
     if len(parts) == 1 and isinstance(parts[0], TextLines):
         return parts[0]
+    if all(isinstance(p, TextLines) for p in parts) and \
+            any(isinstance(p, _Lazy) for p in parts):
+        return LineConcat(parts)
     if all(isinstance(p, TextLines) for p in parts):
         bufs = [np.frombuffer(p.buf, dtype=np.uint8) if not isinstance(p.buf, np.ndarray)
                 else np.ascontiguousarray(p.buf) for p in parts]

@@ -156,3 +156,60 @@ def test_device_csv_parse_with_categoricals_matches_host(cuda, monkeypatch):
             b = torch.nan_to_num(dev.full, -7.0).cpu().numpy()
             assert np.array_equal(a, b)
         assert hist.stats.get("device_parsed_bytes", 0) > 0
+
+
+def test_lazy_split_selection_parse_matches_materialized_cpu(monkeypatch):
+    _lazy_split_case(torch.device("cpu"), monkeypatch)
+
+
+@pytest.mark.gpu
+def test_lazy_split_selection_parse_matches_materialized_gpu(cuda, monkeypatch):
+    from oryx_amd import native
+    native.require_kernels()
+    monkeypatch.setenv("ORYX_GPU_CSV", "1")
+    _lazy_split_case(torch.device(cuda), monkeypatch)
+
+
+def _lazy_split_case(dev, monkeypatch):
+    """A train / test split as LineSelections of the interval (MLUpdate's default split):
+    the parser parses the interval once and selects rows, renumbering categorical codes in
+    the selection's own first-appearance order -- the same block as a parse of the selected
+    text -- and the interval's parse is adopted when its bytes come back as a part file."""
+    from oryx_amd.textlines import LineConcat, LineSelection
+    monkeypatch.setattr(FeatureHistory, "UNKEYED_MIN_BYTES", 1)
+    rs = np.random.default_rng(7)
+    schema = _schema()
+    new = TextLines.from_strings(_lines(rs, 900, ["red", "green", "blue", "cyan", ""]))
+    past = TextLines.from_strings(_lines(rs, 400, ["violet", "red"])).with_key(("part", 0))
+    mask = rs.random(len(new)) < 0.2
+    mask[0] = True                      # the first line's colour appears first only in test
+    train = LineSelection(new, np.flatnonzero(~mask))
+    test = LineSelection(new, np.flatnonzero(mask))
+    both = concat_lines([train, past])
+    assert isinstance(both, LineConcat) and len(both) == len(train) + len(past)
+    hist = FeatureHistory(dev)
+    got_train = parse_features(both, schema, dev, history=hist)
+    got_test = parse_features(test, schema, dev)          # a one-off parser: shared parent
+    want_train = parse_features(concat_lines([new.take(~mask), past]), schema, dev)
+    want_test = parse_features(new.take(mask), schema, dev)
+    for got, want in ((got_train, want_train), (got_test, want_test)):
+        assert got.values == want.values
+        assert torch.equal(torch.nan_to_num(got.full, -7.0), torch.nan_to_num(want.full, -7.0))
+    # the whole interval's parse is what the next generation's part file adopts
+    part = TextLines(np.frombuffer(bytes(new.joined()), dtype=np.uint8).copy(), len(new)) \
+        .with_key(("part", 1))
+    parse_features(concat_lines([part, past]), schema, dev, history=hist)
+    assert hist.stats["adopted"] == 1
+    assert bytes(train.joined()) == bytes(new.take(~mask).joined())   # bytes on demand
+
+
+def test_default_split_returns_lazy_selections_cpu():
+    from oryx_amd.ml.mlupdate import MLUpdate
+    from oryx_amd.textlines import LineSelection
+    import types
+    upd = types.SimpleNamespace(test_fraction=0.25)
+    tl = TextLines.from_strings(["%d" % i for i in range(1000)])
+    train, test = MLUpdate.split_new_data_to_train_test(upd, tl)
+    assert isinstance(train, LineSelection) and isinstance(test, LineSelection)
+    assert len(train) + len(test) == 1000
+    assert sorted(int(x) for x in list(train) + list(test)) == list(range(1000))
