@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import threading
 import weakref
 from collections import OrderedDict
 from dataclasses import dataclass, field
@@ -157,6 +158,48 @@ def _device_ok(schema: InputSchema, device) -> bool:
     return native.kernels_available()
 
 
+_STAGE_BYTES = 64 << 20
+_STAGES = 3
+
+
+def h2d(buf: np.ndarray, off: int, nbytes: int, dst: torch.Tensor,
+        staged: Optional[bool] = None) -> None:
+    """``buf[off:off + nbytes]`` (pageable host memory) into ``dst[:nbytes]`` on the GPU.
+
+    Staged (default, ``ORYX_H2D_STAGED=0`` for a plain ``copy_``): 64 MB pieces are copied
+    into pinned staging buffers by the native threads (``oryx_concat_buffers``) and DMA'd
+    asynchronously from there, the next piece's copy overlapping the current DMA; a pageable
+    ``copy_`` is staged by the HIP runtime one piece at a time on one thread."""
+    import os
+    if staged is None:
+        staged = os.environ.get("ORYX_H2D_STAGED", "1") != "0"
+    src = buf[off:off + nbytes]
+    if not staged or nbytes < 2 * _STAGE_BYTES or dst.device.type != "cuda":
+        dst[:nbytes].copy_(torch.from_numpy(src))
+        return
+    lib = native.runtime()
+    stream = torch.cuda.current_stream(dst.device)
+    stages = [torch.empty(_STAGE_BYTES, dtype=torch.uint8, pin_memory=True)
+              for _ in range(_STAGES)]
+    events: List[Optional[torch.cuda.Event]] = [None] * _STAGES
+    ptrs = np.zeros(1, dtype=np.uint64)
+    lens = np.zeros(1, dtype=np.int64)
+    base = src.ctypes.data
+    for i, lo in enumerate(range(0, nbytes, _STAGE_BYTES)):
+        n = min(_STAGE_BYTES, nbytes - lo)
+        j = i % _STAGES
+        if events[j] is not None:
+            events[j].synchronize()          # the DMA out of this staging buffer is done
+        ptrs[0] = base + lo
+        lens[0] = n
+        lib.oryx_concat_buffers(ptrs.ctypes.data, lens.ctypes.data, 1, stages[j].data_ptr())
+        dst[lo:lo + n].copy_(stages[j][:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        events[j] = ev
+    # (the caching pinned allocator holds each staging block until its last copy completes)
+
+
 def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: InputSchema,
                   dtype: torch.dtype, device
                   ) -> Optional[Tuple[torch.Tensor, Dict[int, List[str]]]]:
@@ -186,7 +229,7 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     starts[0] = 0
     starts[1:] = ends[:-1] + 1
     text = torch.empty(((nbytes + 31) // 16) * 16, dtype=torch.uint8, device=device)
-    text[:nbytes].copy_(torch.from_numpy(buf[off:off + nbytes]))
+    h2d(buf, off, nbytes, text)
     d_starts = torch.from_numpy(starts).to(device)
     d_ends = torch.from_numpy(ends).to(device)
     out_col = torch.arange(F, dtype=torch.int32, device=device)
@@ -303,6 +346,30 @@ def _select_rows(parent: _Seg, index: np.ndarray, cats: List[int], device) -> _S
         col[ok] = remap[c].to(full.dtype)
         values[f] = [pv[i] for i in order.tolist()]
     return _Seg(full, values, 0, owned=True)
+
+
+class _Digest(threading.Thread):
+    """``ingest.content_digest`` of a byte range on a thread of its own (the native hash runs
+    without the GIL, beside the parse of the same bytes)."""
+
+    def __init__(self, buf: np.ndarray, off: int, nbytes: int):
+        super().__init__(daemon=True)
+        self._args = (buf, off, nbytes)
+        self._out: Optional[bytes] = None
+        self._err: Optional[BaseException] = None
+        self.start()
+
+    def run(self) -> None:
+        try:
+            self._out = ingest.content_digest(*self._args)
+        except BaseException as e:   # re-raised in result()
+            self._err = e
+
+    def result(self) -> bytes:
+        self.join()
+        if self._err is not None:
+            raise self._err
+        return self._out
 
 
 # parse of the parent of LineSelections (the interval a train / test split selects from),
@@ -439,8 +506,12 @@ class FeatureHistory:
                 self.stats["hit_bytes"] += nbytes
                 self._segs.move_to_end(key)
             else:
-                dg = self._digest(buf, off, nbytes) \
-                    if (self.keep and nbytes >= self.UNKEYED_MIN_BYTES) else None
+                dg, pending = None, None
+                if self.keep and nbytes >= self.UNKEYED_MIN_BYTES:
+                    if key is not None:     # (the adoption lookup needs it first)
+                        dg = self._digest(buf, off, nbytes)
+                    else:                   # (only stored: hashed beside the parse)
+                        pending = _Digest(buf, off, nbytes)
                 sg = self._unkeyed.get(dg) if (dg is not None and key is not None) else None
                 if sg is not None:
                     self.stats["adopted"] += 1
@@ -448,6 +519,8 @@ class FeatureHistory:
                     del self._unkeyed[dg]
                 else:
                     sg = self._parse_range(buf, off, nbytes, n_lines, schema, dtype)
+                    if pending is not None:
+                        dg = pending.result()
                     if sg is None:
                         return None
                     self.stats["misses"] += 1

@@ -213,3 +213,17 @@ def test_default_split_returns_lazy_selections_cpu():
     assert isinstance(train, LineSelection) and isinstance(test, LineSelection)
     assert len(train) + len(test) == 1000
     assert sorted(int(x) for x in list(train) + list(test)) == list(range(1000))
+
+
+@pytest.mark.gpu
+def test_staged_h2d_copy_bitwise(cuda):
+    """The pinned, natively staged host -> device copy of the parser's text (several 64 MB
+    pieces and a partial last one, from an offset) equals the source bytes."""
+    from oryx_amd.models.features import h2d
+    rs = np.random.default_rng(2)
+    n = (200 << 20) + 12345
+    buf = rs.integers(0, 256, size=n + 77, dtype=np.uint8)
+    dst = torch.empty(n + 32, dtype=torch.uint8, device=cuda)
+    h2d(buf, 77, n, dst, staged=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dst[:n].cpu(), torch.from_numpy(buf[77:77 + n]))
