@@ -5,10 +5,13 @@ Usage: python scripts/h2d_probe.py [GB]
 """
 
 import json
+import os
 import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from oryx_amd import hostbuf, native
 from oryx_amd.models.features import h2d
