@@ -3367,3 +3367,60 @@ void oryx_blob_hash64(const unsigned char* blob, const long long* ends, long lon
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// Categorical codes of n byte spans (span j = base[off[j * stride], + len[j * stride])), in
+// order of first appearance, an empty span -1 (missing): the feature apps' encoding of a
+// categorical column (RDFUpdate.getDistinctValues, [mllib]/rdf/RDFUpdate.java:207-225, then
+// the value -> index maps).  Each thread encodes a contiguous range of rows with a local
+// table; the tables are merged in range order, so the numbering is the sequential one.
+// first_row[k] = the row where distinct value k first appears.  Returns the number of
+// distinct values.
+long long oryx_encode_spans(const char* base, const long long* off, const int* len, long long n,
+                            long long stride, long long* codes, long long* first_row) {
+  if (n <= 0) return 0;
+  const int T = oryx_ff::native_threads();
+  std::vector<std::unordered_map<std::string_view, long long>> local((size_t)T);
+  std::vector<std::vector<long long>> lfirst((size_t)T);
+  const int P = oryx_ff::parallel_ranges(n, 1 << 15, [&](long long lo, long long hi, int t) {
+    auto& m = local[(size_t)t];
+    auto& fr = lfirst[(size_t)t];
+    for (long long j = lo; j < hi; ++j) {
+      const int l = len[j * stride];
+      if (l <= 0) {
+        codes[j] = -1;
+        continue;
+      }
+      const std::string_view k(base + off[j * stride], (size_t)l);
+      auto it = m.try_emplace(k, (long long)fr.size());
+      if (it.second) fr.push_back(j);
+      codes[j] = it.first->second;
+    }
+  });
+  // merge in range order: global ids in order of first appearance
+  std::unordered_map<std::string_view, long long> global;
+  std::vector<std::vector<long long>> remap((size_t)P);
+  long long G = 0;
+  for (int t = 0; t < P; ++t) {
+    remap[(size_t)t].resize(lfirst[(size_t)t].size());
+    for (size_t k = 0; k < lfirst[(size_t)t].size(); ++k) {
+      const long long j = lfirst[(size_t)t][k];
+      const std::string_view key(base + off[j * stride], (size_t)len[j * stride]);
+      auto it = global.try_emplace(key, G);
+      if (it.second) first_row[G++] = j;
+      remap[(size_t)t][k] = it.first->second;
+    }
+  }
+  if (P > 1 || G != (long long)lfirst[0].size()) {
+    // (the same n and piece size: the same P ranges as the encoding pass)
+    oryx_ff::parallel_ranges(n, 1 << 15, [&](long long lo, long long hi, int t) {
+      const auto& rm = remap[(size_t)t];
+      for (long long j = lo; j < hi; ++j)
+        if (codes[j] >= 0) codes[j] = rm[(size_t)codes[j]];
+    });
+  }
+  return G;
+}
+
+}  // extern "C"

@@ -122,6 +122,27 @@ def _encode_spans(seg: np.ndarray, span_off: np.ndarray, span_len: np.ndarray, c
     n = span_off.shape[0]
     values: Dict[int, List[str]] = {}
     out_codes: Dict[int, np.ndarray] = {}
+    if n and cats:
+        # native: per-thread tables merged in row order (oryx_encode_spans)
+        so = np.ascontiguousarray(span_off, dtype=np.int64)
+        sl = np.ascontiguousarray(span_len, dtype=np.int32)
+        S = so.shape[1]
+        seg = np.ascontiguousarray(seg)
+        lib = native.runtime()
+        codes = np.empty(n, dtype=np.int64)
+        first = np.empty(n, dtype=np.int64)
+        for si, f in enumerate(cats):
+            k = int(lib.oryx_encode_spans(seg.ctypes.data, so[:, si:].ctypes.data,
+                                          sl[:, si:].ctypes.data, n, S, codes.ctypes.data,
+                                          first.ctypes.data))
+            rows = first[:k]
+            o, ln = so[rows, si], sl[rows, si]
+            values[f] = [bytes(seg[a:a + b]).decode("utf-8") for a, b in zip(o.tolist(),
+                                                                            ln.tolist())]
+            c = codes.astype(np_dtype)
+            c[codes < 0] = np.nan
+            out_codes[f] = c
+        return values, out_codes
     for si, f in enumerate(cats):
         o = span_off[:, si]
         ln = span_len[:, si]
@@ -166,13 +187,14 @@ def h2d(buf: np.ndarray, off: int, nbytes: int, dst: torch.Tensor,
         staged: Optional[bool] = None) -> None:
     """``buf[off:off + nbytes]`` (pageable host memory) into ``dst[:nbytes]`` on the GPU.
 
-    Staged (default, ``ORYX_H2D_STAGED=0`` for a plain ``copy_``): 64 MB pieces are copied
-    into pinned staging buffers by the native threads (``oryx_concat_buffers``) and DMA'd
-    asynchronously from there, the next piece's copy overlapping the current DMA; a pageable
-    ``copy_`` is staged by the HIP runtime one piece at a time on one thread."""
+    Plain ``copy_`` by default: the HIP runtime moves pageable memory at 56 GB/s on the
+    MI355X box (profiles/r5_h2d_v2.json).  ``staged`` / ``ORYX_H2D_STAGED=1``: 64 MB pieces
+    copied into pinned staging buffers by the native threads (``oryx_concat_buffers``) and
+    DMA'd from there, the next piece's copy overlapping the current DMA -- measured at the same
+    56 GB/s, so it stays off."""
     import os
     if staged is None:
-        staged = os.environ.get("ORYX_H2D_STAGED", "1") != "0"
+        staged = os.environ.get("ORYX_H2D_STAGED", "0") == "1"
     src = buf[off:off + nbytes]
     if not staged or nbytes < 2 * _STAGE_BYTES or dst.device.type != "cuda":
         dst[:nbytes].copy_(torch.from_numpy(src))

@@ -227,3 +227,30 @@ def test_staged_h2d_copy_bitwise(cuda):
     h2d(buf, 77, n, dst, staged=True)
     torch.cuda.synchronize()
     assert torch.equal(dst[:n].cpu(), torch.from_numpy(buf[77:77 + n]))
+
+
+def test_native_span_encoding_first_appearance_order_cpu():
+    """oryx_encode_spans (per-thread tables merged in row order) numbers values in their
+    order of first appearance over all rows, empty spans missing -- as one sequential pass."""
+    from oryx_amd.models.features import _encode_spans
+    rs = np.random.default_rng(4)
+    n = 300_000                                   # several thread ranges
+    words = ["v%d" % i for i in range(5000)]
+    pick = np.minimum(rs.zipf(1.3, size=n) - 1, len(words) - 1)
+    vals = [words[i] if rs.random() > 0.05 else "" for i in pick]
+    text = ",".join(vals).encode()
+    offs, lens, at = [], [], 0
+    for v in vals:
+        offs.append(at)
+        lens.append(len(v))
+        at += len(v) + 1
+    seg = np.frombuffer(text, dtype=np.uint8)
+    so = np.array(offs, dtype=np.int64)[:, None]
+    sl = np.array(lens, dtype=np.int32)[:, None]
+    values, codes = _encode_spans(seg, so, sl, [0], np.float64)
+    want_vals, want_codes = {}, []
+    for v in vals:
+        want_codes.append(np.nan if v == "" else want_vals.setdefault(v, len(want_vals)))
+    assert values[0] == list(want_vals)
+    assert np.array_equal(np.nan_to_num(codes[0], nan=-1.0),
+                          np.nan_to_num(np.array(want_codes, dtype=np.float64), nan=-1.0))
