@@ -249,6 +249,8 @@ def main(argv=None) -> int:
         first_phases = dict(getattr(layer._update, "phase_seconds", {}))
         first_train = dict(getattr(layer._update, "train_phases", {}) or {})
         first_lay = dict(layer.last_phases)
+        h1 = getattr(layer._update, "history", None)
+        first_hist = json.loads(json.dumps(h1.stats)) if h1 is not None else None
         later = []
         for g in range(1, max(1, args.generations) if ctx.world_size == 1 else 1):
             before = dict(layer._update.phase_seconds)
@@ -278,6 +280,7 @@ def main(argv=None) -> int:
         first_phases = dict(getattr(layer._update, "phase_seconds", {}))
         first_train = dict(getattr(layer._update, "train_phases", {}) or {})
         first_lay = dict(layer.last_phases)
+        first_hist = None
     phases = first_phases
     if not ctx.is_main:
         later = []
@@ -312,6 +315,7 @@ def main(argv=None) -> int:
             "cprofile_top": cprof_top if args.cprofile and ctx.is_main else None,
             "update_messages": int(sum(ends)),
             "attributed_s": attributed, "unattributed_s": t_gen - attributed,
+            "history_first": first_hist,
             "later_generations": later,
             "config": ({"ratings": args.ratings, "users": args.users, "items": args.items,
                         "features": args.features} if args.app == "als" else

@@ -223,7 +223,7 @@ def h2d(buf: np.ndarray, off: int, nbytes: int, dst: torch.Tensor,
 
 
 def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: InputSchema,
-                  dtype: torch.dtype, device
+                  dtype: torch.dtype, device, laps: Optional[Dict[str, float]] = None
                   ) -> Optional[Tuple[torch.Tensor, Dict[int, List[str]]]]:
     """Bytes [off, off + nbytes) of ``buf`` parsed on the device (``csv.hip``): the text goes
     to the GPU (smaller than its parse) and one thread per line parses it with the host
@@ -231,6 +231,15 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     that form are parsed on the host and their rows written in (bitwise the host parser's).
     Categorical fields come back as byte spans and are encoded on the host.  Returns (matrix,
     categorical values), or None when the caller should parse on the host instead."""
+    import time
+    t_last = [time.perf_counter()]
+
+    def lap(name):
+        if laps is not None:
+            t = time.perf_counter()
+            laps[name] = laps.get(name, 0.0) + t - t_last[0]
+            t_last[0] = t
+
     F = schema.get_num_features()
     cats = [f for f in range(F) if schema.is_categorical(f)]
     S = len(cats)
@@ -250,10 +259,12 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     starts = np.empty(n, dtype=np.int64)
     starts[0] = 0
     starts[1:] = ends[:-1] + 1
+    lap("line_scan")
     text = torch.empty(((nbytes + 31) // 16) * 16, dtype=torch.uint8, device=device)
     h2d(buf, off, nbytes, text)
     d_starts = torch.from_numpy(starts).to(device)
     d_ends = torch.from_numpy(ends).to(device)
+    lap("h2d")
     out_col = torch.arange(F, dtype=torch.int32, device=device)
     is_num = torch.tensor([0 if f in cats else 1 for f in range(F)], dtype=torch.uint8,
                           device=device)
@@ -268,7 +279,9 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
         sp_len.data_ptr(), S, bad.data_ptr(), n_bad.data_ptr(), native.stream_ptr(device)),
         "oryx_csv_lines_to_matrix")
     values: Dict[int, List[str]] = {}
-    if int(n_bad.item()):
+    bad_lines = int(n_bad.item())
+    lap("kernel")
+    if bad_lines:
         if S:
             return None     # (the host subset's local categories would need a re-encode)
         idx = torch.nonzero(bad).flatten().cpu().numpy()
@@ -280,12 +293,14 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
         if got is None or got[0].shape[0] != len(idx):
             return None
         out[torch.from_numpy(idx).to(device)] = torch.from_numpy(got[0]).to(device)
+        lap("host_lines")
     if S:
         np_dtype = np.float32 if dtype == torch.float32 else np.float64
         values, codes = _encode_spans(buf[off:off + nbytes], sp_off.cpu().numpy(),
                                       sp_len.cpu().numpy(), cats, np_dtype)
         for f in cats:
             out[:, f] = torch.from_numpy(codes[f]).to(device)
+        lap("categorical")
     return out, values
 
 
@@ -441,7 +456,8 @@ class FeatureHistory:
     def _parse_range(self, buf: np.ndarray, off: int, nbytes: int, n_lines: int,
                      schema: InputSchema, dtype) -> Optional[_Seg]:
         if _device_ok(schema, self.device):
-            got = _device_block(buf, off, nbytes, n_lines, schema, dtype, self.device)
+            got = _device_block(buf, off, nbytes, n_lines, schema, dtype, self.device,
+                                self.stats.setdefault("device_parse_s", {}))
             if got is not None:
                 self.stats["device_parsed_bytes"] = \
                     self.stats.get("device_parsed_bytes", 0) + nbytes
