@@ -64,8 +64,12 @@ __host__ __device__ constexpr int tix(int pi, int qi) {
   return pi * M - pi * (pi - 1) / 2 + (qi - pi);
 }
 
-// scratch row stride in floats (ds_read_b128 rows conflict free)
-constexpr int BATCH_DS = 20;
+// scratch row stride in floats (20: ds_read_b128 rows conflict free; ORYX_ALS_BATCH_DS=16 packs
+// the rows, A/B only)
+#ifndef ORYX_ALS_BATCH_DS
+#define ORYX_ALS_BATCH_DS 20
+#endif
+constexpr int BATCH_DS = ORYX_ALS_BATCH_DS;
 
 template <int KP, int NM, int D, bool YG = false>
 struct BatchCfg {
@@ -667,7 +671,8 @@ __device__ __forceinline__ void batch_solve(const AlsParams& p, int lane,
 template <int KP, int NM, int D, bool PROF = false, int BPC = 4 / NM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BPC, BPC))) void
 als_solve_batch(AlsParams p, unsigned long long* prof) {
-  constexpr bool YG = BPC > 4 / NM;
+  // YtY from global memory only when BPC blocks with it staged in LDS do not fit
+  constexpr bool YG = BPC > 4 / NM && BatchCfg<KP, NM, D, false>::BYTES * BPC > 160 * 1024;
   using C = BatchCfg<KP, NM, D, YG>;
   static_assert(C::BYTES * BPC <= 160 * 1024, "BPC blocks do not fit the CU's LDS");
   using CI = ChunkImage<KP>;

@@ -1219,23 +1219,28 @@ __global__ __launch_bounds__(256, 2) void km_rescore_full(const float* __restric
 // point i, a_i = mean distance to the other points of its cluster, b_i = smallest mean
 // distance to another cluster, s_i = (b - a) / max(a, b) (0 for singleton clusters).  The
 // sample is sorted by cluster, so the columns of one cluster are contiguous: a thread owns row
-// i and streams every column once, accumulating Euclidean distances (fp32 differences squared,
-// sqrt, fp64 sums) into a running per-cluster sum that is finalised into a / b whenever the
-// column's cluster changes -- no [s, s] distance matrix and no [s, k] per-cluster GEMM.  Column
-// tiles (32 columns x 64 dimensions) come through LDS as broadcast reads; the row's own
-// coordinates come from the transposed copy xT [d][s] (coalesced across the block's rows).
-// Output: per-block partial sums of s_i (fp64).
+// i and streams the columns of its block's column range once, accumulating Euclidean
+// distances (fp32 differences squared, sqrt, fp64 sums) into a running per-cluster sum that is
+// finalised whenever the column's cluster changes -- no [s, s] distance matrix and no [s, k]
+// per-cluster GEMM.  The columns are split into ranges at cluster boundaries (blockIdx.y), so
+// a 100k sample runs as thousands of blocks instead of 391, each range giving per row the sum
+// over its own cluster (when the range holds it) and the smallest mean over the others;
+// km_silhouette_fin combines the ranges.  Column tiles (32 columns x 64 dimensions) come
+// through LDS as broadcast reads; the row's own coordinates come from the transposed copy
+// xT [d][s] (coalesced across the block's rows); differences and squares are packed pairs
+// (v_pk_add_f32 / v_pk_fma_f32).
 constexpr int SIL_TC = 32, SIL_DC = 64;
-__global__ __launch_bounds__(256) void km_silhouette(
+__global__ __launch_bounds__(256) void km_silhouette_part(
     const float* __restrict__ x, const float* __restrict__ xT, const int* __restrict__ cl,
-    const int* __restrict__ csize, int s, int d, double* __restrict__ partial) {
+    const int* __restrict__ csize, int s, int d, const int* __restrict__ bounds,
+    double* __restrict__ a_part, double* __restrict__ b_part) {
   __shared__ float tile[SIL_DC][SIL_TC];
   __shared__ int tcl[SIL_TC];
-  __shared__ double red[256];
   const int tid = threadIdx.x;
   const int i = blockIdx.x * 256 + tid;
   const bool live = i < s;
   const int own = live ? cl[i] : -1;
+  const int c0 = bounds[blockIdx.y], c1 = bounds[blockIdx.y + 1];
   double a = 0.0, b = INFINITY;
   int cur = -1;
   double cur_sum = 0.0;
@@ -1248,32 +1253,32 @@ __global__ __launch_bounds__(256) void km_silhouette(
       b = m < b ? m : b;
     }
   };
-  for (int j0 = 0; j0 < s; j0 += SIL_TC) {
-    float acc[SIL_TC];
+  for (int j0 = c0; j0 < c1; j0 += SIL_TC) {
+    f32x2 acc[SIL_TC / 2];
 #pragma unroll
-    for (int c = 0; c < SIL_TC; ++c) acc[c] = 0.f;
+    for (int c = 0; c < SIL_TC / 2; ++c) acc[c] = f32x2{0.f, 0.f};
     __syncthreads();
-    if (tid < SIL_TC) tcl[tid] = j0 + tid < s ? cl[j0 + tid] : -1;
+    if (tid < SIL_TC) tcl[tid] = j0 + tid < c1 ? cl[j0 + tid] : -1;
     for (int d0 = 0; d0 < d; d0 += SIL_DC) {
       __syncthreads();
       for (int e = tid; e < SIL_TC * SIL_DC; e += 256) {
         const int c = e / SIL_DC, dd = e % SIL_DC;
         const int j = j0 + c, dim = d0 + dd;
-        tile[dd][c] = (j < s && dim < d) ? x[(long long)j * d + dim] : 0.f;
+        tile[dd][c] = (j < c1 && dim < d) ? x[(long long)j * d + dim] : 0.f;
       }
       __syncthreads();
       const int dn = d - d0 < SIL_DC ? d - d0 : SIL_DC;
       for (int dd = 0; dd < dn; ++dd) {
         const float xi = live ? xT[(long long)(d0 + dd) * s + i] : 0.f;
+        const f32x2 xi2 = f32x2{xi, xi};
         const f32x4* tr = reinterpret_cast<const f32x4*>(&tile[dd][0]);
 #pragma unroll
         for (int q = 0; q < SIL_TC / 4; ++q) {
           const f32x4 v = tr[q];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float df = xi - v[e];
-            acc[4 * q + e] += df * df;
-          }
+          const f32x2 d01 = xi2 - f32x2{v[0], v[1]};
+          const f32x2 d23 = xi2 - f32x2{v[2], v[3]};
+          acc[2 * q] = d01 * d01 + acc[2 * q];
+          acc[2 * q + 1] = d23 * d23 + acc[2 * q + 1];
         }
       }
     }
@@ -1287,14 +1292,34 @@ __global__ __launch_bounds__(256) void km_silhouette(
           cur = cc;
           cur_sum = 0.0;
         }
-        cur_sum += (double)sqrtf(acc[c]);
+        cur_sum += (double)sqrtf(acc[c >> 1][c & 1]);
       }
     }
   }
-  double sil = 0.0;
   if (live) {
     finish(cur, cur_sum);
-    const int n_own = csize[own];
+    a_part[(long long)blockIdx.y * s + i] = a;
+    b_part[(long long)blockIdx.y * s + i] = b;
+  }
+}
+
+// The column ranges' per-row results -> s_i, per-block partial sums (fp64).
+__global__ __launch_bounds__(256) void km_silhouette_fin(
+    const int* __restrict__ cl, const int* __restrict__ csize, int s, int nsplit,
+    const double* __restrict__ a_part, const double* __restrict__ b_part,
+    double* __restrict__ partial) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  const int i = blockIdx.x * 256 + tid;
+  double sil = 0.0;
+  if (i < s) {
+    double a = 0.0, b = INFINITY;
+    for (int r = 0; r < nsplit; ++r) {
+      a += a_part[(long long)r * s + i];
+      const double br = b_part[(long long)r * s + i];
+      b = br < b ? br : b;
+    }
+    const int n_own = csize[cl[i]];
     if (n_own > 1) {
       a /= (double)(n_own - 1);
       sil = a < b ? 1.0 - a / b : (a > b ? b / a - 1.0 : 0.0);
@@ -1741,14 +1766,22 @@ int oryx_kmeans_accumulate_sorted(const float* X, const int* assign, const float
 }
 
 // x [s][d] and xT [d][s] fp32 of the sample sorted by cluster id cl [s] (every id in
-// [0, k), csize[k] = points per cluster); partial [ceil(s / 256)] receives per-block sums of
-// the points' silhouettes.
+// [0, k), csize[k] = points per cluster); bounds [nsplit + 1]: column ranges (increasing, 0
+// to s, each boundary the first column of a cluster); work: 2 * nsplit * s doubles; partial
+// [ceil(s / 256)] receives per-block sums of the points' silhouettes.
 int oryx_kmeans_silhouette(const float* x, const float* xT, const int* cl, const int* csize,
-                           int s, int d, double* partial, void* stream) {
+                           int s, int d, const int* bounds, int nsplit, double* work,
+                           double* partial, void* stream) {
   if (s <= 0) return ORYX_OK;
-  if (d <= 0) return ORYX_EINVAL;
-  hipLaunchKernelGGL(km_silhouette, dim3((unsigned)((s + 255) / 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), x, xT, cl, csize, s, d, partial);
+  if (d <= 0 || nsplit <= 0 || nsplit > 65535) return ORYX_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const unsigned rb = (unsigned)((s + 255) / 256);
+  double* a_part = work;
+  double* b_part = work + (long long)nsplit * s;
+  hipLaunchKernelGGL(km_silhouette_part, dim3(rb, (unsigned)nsplit), dim3(256), 0, st, x, xT,
+                     cl, csize, s, d, bounds, a_part, b_part);
+  hipLaunchKernelGGL(km_silhouette_fin, dim3(rb), dim3(256), 0, st, cl, csize, s, nsplit,
+                     a_part, b_part, partial);
   return oryx_check_launch();
 }
 

@@ -197,9 +197,19 @@ def _silhouette_kernel(x: torch.Tensor, idx: torch.Tensor, k: int) -> float:
     xt = xs.t().contiguous()
     cl = idx[order].to(torch.int32).contiguous()
     size = torch.bincount(idx.long(), minlength=k).to(torch.int32)
-    partial = torch.empty((s + 255) // 256, dtype=torch.float64, device=x.device)
+    # column ranges at cluster boundaries, enough of them for >= ~2048 blocks
+    row_blocks = (s + 255) // 256
+    want = max(1, min(64, -(-2048 // row_blocks)))
+    starts = np.concatenate([[0], np.cumsum(size.cpu().numpy().astype(np.int64))])
+    cuts = np.unique(starts[np.searchsorted(starts, np.arange(1, want) * s / want)])
+    bounds = np.unique(np.concatenate([[0], cuts[(cuts > 0) & (cuts < s)], [s]]))
+    nsplit = len(bounds) - 1
+    d_bounds = torch.from_numpy(bounds.astype(np.int32)).to(x.device)
+    work = torch.empty(2 * nsplit * s, dtype=torch.float64, device=x.device)
+    partial = torch.empty(row_blocks, dtype=torch.float64, device=x.device)
     rc = lib.oryx_kmeans_silhouette(xs.data_ptr(), xt.data_ptr(), cl.data_ptr(),
-                                    size.data_ptr(), s, d, partial.data_ptr(),
+                                    size.data_ptr(), s, d, d_bounds.data_ptr(), nsplit,
+                                    work.data_ptr(), partial.data_ptr(),
                                     native.stream_ptr(x.device))
     native.check(rc, "oryx_kmeans_silhouette")
     return float(partial.sum()) / s

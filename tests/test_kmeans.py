@@ -720,6 +720,15 @@ def test_silhouette_kernel_matches_host(cuda):
     host = ev.silhouette_coefficient(clusters, pts, torch.device("cpu"))
     dev = ev.silhouette_coefficient(clusters, pts, cuda)
     assert dev == pytest.approx(host, rel=1e-5)
+    # many column ranges (300 clusters of skewed sizes, 20k points: 64 ranges at cluster
+    # boundaries) and a dimension that is not a multiple of the 64-wide tiles
+    cs = [g.normal(0, 6, 37) for _ in range(300)]
+    sizes = np.minimum(g.zipf(1.6, 300), 800)
+    pts = np.concatenate([g.normal(c, 1.0, (int(m), 37)) for c, m in zip(cs, sizes)])
+    clusters = [ClusterInfo(i, c.tolist(), 1) for i, c in enumerate(cs)]
+    host = ev.silhouette_coefficient(clusters, pts, torch.device("cpu"))
+    dev = ev.silhouette_coefficient(clusters, pts, cuda)
+    assert dev == pytest.approx(host, rel=1e-5)
 
 
 @pytest.mark.gpu
