@@ -51,17 +51,59 @@ def read_text_parallel(jobs):
         return list(ex.map(lambda job: job[0].read_text_lines(job[1])[0], jobs))
 
 
+def _read_text_one_buffer(jobs):
+    """Every (reader, end) job's text read concurrently into ONE buffer (each partition into
+    its slice, sized by the reader's bound), gaps closed afterwards: the drain's text without
+    per-partition buffers and a concatenating copy.  None when a partition needs the
+    per-record path (keys, multi-line values) or grew past its bound."""
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    from .. import hostbuf
+    from ..textlines import TextLines
+    bounds = [r.text_bound(end) for r, end in jobs]
+    total = sum(bounds)
+    if total == 0:
+        return TextLines(b"", 0)
+    buf = hostbuf.empty(total)
+    offs = np.concatenate([[0], np.cumsum(bounds)]).astype(np.int64)
+    base = buf.ctypes.data
+    with ThreadPoolExecutor(max_workers=min(len(jobs), 16)) as ex:
+        got = list(ex.map(lambda k: jobs[k][0].read_text_into(
+            jobs[k][1], base + int(offs[k]), bounds[k]), range(len(jobs))))
+    if any(g is None for g in got):
+        # (readers that did read keep their new position: rewind them for the fallback)
+        return None
+    at = 0
+    n = 0
+    for k, (used, recs) in enumerate(got):
+        if used and at != offs[k]:
+            ctypes.memmove(base + at, base + int(offs[k]), used)
+        at += used
+        n += recs
+    return TextLines(buf[:at], n)
+
+
 def drain_dataset(consumer: tlog.TopicConsumer,
                   end_offsets: Optional[List[int]] = None) -> Dataset:
     """Everything currently available as a :class:`Dataset`: partitions are read in bulk
-    natively (messages only) unless a record has a key or a multi-line value."""
+    natively (messages only, into one buffer) unless a record has a key or a multi-line
+    value."""
     from ..textlines import concat_lines
     topic = consumer.topic
     ends = end_offsets or topic.end_offsets()
     texts = []
     pairs: List[Tuple[Optional[str], str]] = []
     readers = list(consumer.readers)
-    bulk = read_text_parallel([(r, ends[r.partition]) for r in readers])
+    jobs = [(r, ends[r.partition]) for r in readers]
+    starts = [r.position for r in readers]
+    one = _read_text_one_buffer(jobs) if len(jobs) > 1 else None
+    if one is not None:
+        return Dataset.from_values(one)
+    for r, p in zip(readers, starts):
+        if r.position != p:
+            r.seek(p)
+    bulk = read_text_parallel(jobs)
     for r, lines in zip(readers, bulk):
         target = ends[r.partition]
         if lines is not None:

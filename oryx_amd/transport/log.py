@@ -434,6 +434,39 @@ class PartitionReader:
             total += n
         return TextLines(buf[:used_total], total), total
 
+    def text_bound(self, end_offset: int) -> int:
+        """Upper bound of the bytes :meth:`read_text_into` writes up to ``end_offset``."""
+        if self.position >= end_offset:
+            return 0
+        return int(_lib().oryx_reader_text_bound(self._r, int(end_offset)))
+
+    def read_text_into(self, end_offset: int, addr: int, cap: int):
+        """As :meth:`read_text_lines`, into ``cap`` bytes at ``addr`` (a slice of the caller's
+        buffer): (bytes written, records read), or None -- position unchanged -- when a record
+        has a key or a multi-line value, or the text does not fit."""
+        lib = _lib()
+        start = self.position
+        used_total = total = 0
+        used = ctypes.c_longlong(0)
+        flags = ctypes.c_int(0)
+        while self.position < end_offset:
+            n = lib.oryx_reader_read_text(self._r, int(end_offset),
+                                          ctypes.c_void_p(addr + used_total),
+                                          cap - used_total, ctypes.byref(used),
+                                          ctypes.byref(flags))
+            if n == -3:
+                raise LogCorruptionError(lib.oryx_log_last_error().decode())
+            if n < 0:
+                raise IOError(lib.oryx_log_last_error().decode())
+            if flags.value & 7:
+                self.seek(start)
+                return None
+            if n == 0:
+                break
+            used_total += int(used.value)
+            total += n
+        return used_total, total
+
     def read_text(self, end_offset: int) -> Tuple[Optional[List[str]], int]:
         """Values of every record up to ``end_offset`` (exclusive) in one bulk native read.
 

@@ -59,6 +59,37 @@ def test_drain_save_read_round_trip(tmp_path):
     topic.close()
 
 
+def test_one_buffer_drain_with_gaps_and_key_fallback(tmp_path, monkeypatch):
+    """The drain reads every partition into its slice of one buffer: records appended after
+    the end offsets were taken leave gaps (bounds count them) that are closed, in partition
+    order; a keyed record sends the drain to the per-record path with readers rewound."""
+    from oryx_amd import hostbuf
+    from oryx_amd.layers.common import drain_dataset
+    monkeypatch.setattr(hostbuf, "_MIN", 1 << 10)
+    root = str(tmp_path / "log")
+    tlog.maybe_create_topic(root, "In", 4)
+    topic = tlog.Topic(root, "In")
+    msgs = ["u%d,i%d,%d" % (j, j % 17, j % 5) for j in range(5000)]
+    topic.append_batch([(None, m) for m in msgs])
+    ends = topic.end_offsets()
+    late = ["late%d,x,1" % j for j in range(700)]
+    topic.append_batch([(None, m) for m in late])          # past the end offsets
+    cons = tlog.TopicConsumer(topic, start="earliest")
+    ds = drain_dataset(cons, ends)
+    vals = ds.values()
+    assert isinstance(vals, TextLines) and len(vals) == len(msgs)
+    assert sorted(vals) == sorted(msgs)
+    assert [r.position for r in cons.readers] == [ends[r.partition] for r in cons.readers]
+    rest = drain_dataset(cons)
+    assert sorted(rest.values()) == sorted(late)
+    # a keyed record: per-record path for that partition, all records still there once
+    topic.append_batch([(None, "a,b,1"), ("k", "c,d,2"), (None, "e,f,3")])
+    got = drain_dataset(cons)
+    assert sorted(v for v in got.values()) == ["a,b,1", "c,d,2", "e,f,3"]
+    cons.close()
+    topic.close()
+
+
 def test_multichunk_parse_matches_single_chunk_with_dropped_lines():
     """A buffer large enough for the threaded in-place parse (rows written at their line's
     index, codes remapped, gaps from dropped / empty lines closed) gives the rows, codes and
