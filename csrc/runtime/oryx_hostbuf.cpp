@@ -128,6 +128,38 @@ long long oryx_hostbuf_quiesce(long long timeout_ms) {
   return r.pending;
 }
 
+// Faults in [p, p + n) from `threads` threads (MADV_POPULATE_WRITE per slice where the kernel
+// has it, else one store per 4 KB page): a buffer that several writers fill at once would
+// otherwise take every first-touch fault inside their copies.
+void oryx_hostbuf_prefault(void* p, long long n, int threads) {
+  if (!p || n <= 0) return;
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  constexpr long long kAlign = 2ll << 20;
+  long long per = (n + threads - 1) / threads;
+  per = (per + kAlign - 1) / kAlign * kAlign;
+  auto work = [p, n, per](int t) {
+    const long long lo = (long long)t * per;
+    if (lo >= n) return;
+    const long long len = lo + per < n ? per : n - lo;
+    char* b = static_cast<char*>(p) + lo;
+#ifdef MADV_POPULATE_WRITE
+    if (madvise(b, (size_t)len, MADV_POPULATE_WRITE) == 0) return;
+#endif
+    for (long long o = 0; o < len; o += 4096) reinterpret_cast<volatile char*>(b)[o] = 0;
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) {
+    try {
+      pool.emplace_back(work, t);
+    } catch (...) {
+      work(t);
+    }
+  }
+  work(0);
+  for (auto& th : pool) th.join();
+}
+
 // Reads bytes [0, n) of the file at path into out with up to `threads` concurrent preads of
 // 32 MB pieces (a past interval's part file, tens of GB at config #4's shape: one read() call
 // into a fresh Python bytes object ran at ~4 GB/s, single-threaded copy plus page faults).

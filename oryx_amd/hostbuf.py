@@ -46,6 +46,13 @@ def empty(n: int) -> np.ndarray:
     return np.frombuffer(raw, dtype=np.uint8)
 
 
+def prefault(buf: np.ndarray, threads: int = 16) -> None:
+    """Faults ``buf``'s pages in from ``threads`` native threads (before concurrent writers)."""
+    if len(buf):
+        native.runtime().oryx_hostbuf_prefault(buf.ctypes.data, len(buf),
+                                               min(threads, os.cpu_count() or 1))
+
+
 def read_text_file(path: str) -> np.ndarray:
     """The bytes of a text file as a uint8 array ending with a newline (one is appended when
     the file lacks it), read by concurrent native preads into an :func:`empty` buffer."""

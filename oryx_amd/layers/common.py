@@ -10,6 +10,7 @@ generation interval.  Spark Streaming's micro-batch scheduler becomes :class:`In
 from __future__ import annotations
 
 import logging
+import os
 import threading
 import time
 import uuid
@@ -66,6 +67,8 @@ def _read_text_one_buffer(jobs):
     if total == 0:
         return TextLines(b"", 0)
     buf = hostbuf.empty(total)
+    if os.environ.get("ORYX_DRAIN_PREFAULT", "0") == "1":
+        hostbuf.prefault(buf)
     offs = np.concatenate([[0], np.cumsum(bounds)]).astype(np.int64)
     base = buf.ctypes.data
     with ThreadPoolExecutor(max_workers=min(len(jobs), 16)) as ex:
@@ -97,7 +100,8 @@ def drain_dataset(consumer: tlog.TopicConsumer,
     readers = list(consumer.readers)
     jobs = [(r, ends[r.partition]) for r in readers]
     starts = [r.position for r in readers]
-    one = _read_text_one_buffer(jobs) if len(jobs) > 1 else None
+    one = _read_text_one_buffer(jobs) \
+        if len(jobs) > 1 and os.environ.get("ORYX_DRAIN_ONE_BUFFER", "1") != "0" else None
     if one is not None:
         return Dataset.from_values(one)
     for r, p in zip(readers, starts):
