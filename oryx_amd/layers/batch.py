@@ -37,6 +37,8 @@ import threading
 import time
 from typing import List, Optional, Tuple
 
+import numpy as np
+
 from .. import hostbuf, tracing
 from ..api import BatchLayerUpdate, Dataset
 from ..transport.producer import LogTopicProducer
@@ -61,8 +63,12 @@ def _write_part(path_no_ext: str, records) -> str:
         vals = records.values()
         if isinstance(vals, TextLines):
             path = path_no_ext + ".txt"
-            with open(path + ".w", "wb") as f:
-                f.write(memoryview(vals.joined()))
+            buf = vals.joined()
+            if isinstance(buf, np.ndarray) and len(buf) >= (64 << 20):
+                hostbuf.write_file(path + ".w", buf)      # concurrent native pwrites
+            else:
+                with open(path + ".w", "wb") as f:
+                    f.write(memoryview(buf))
             os.replace(path + ".w", path)
             return path
         text = "\n".join(vals)
