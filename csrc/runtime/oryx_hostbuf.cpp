@@ -128,57 +128,6 @@ long long oryx_hostbuf_quiesce(long long timeout_ms) {
   return r.pending;
 }
 
-// Writes buf[0, n) as the whole content of the file at path (created or truncated; sized
-// first, then filled by up to `threads` concurrent pwrites of 32 MB pieces): a generation's
-// part file, tens of GB at config #4's shape, where one write() call copied into the page
-// cache on one thread at ~9 GB/s.  Returns 0 or -errno.
-long long oryx_write_file_parallel(const char* path, const char* buf, long long n,
-                                   int threads) {
-  const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
-  if (fd < 0) return -(long long)errno;
-  if (n > 0 && ftruncate(fd, (off_t)n) != 0) {
-    const int e = errno;
-    close(fd);
-    return -(long long)e;
-  }
-  constexpr long long kPiece = 32ll << 20;
-  const long long pieces = (n + kPiece - 1) / kPiece;
-  if (threads < 1) threads = 1;
-  if (threads > 64) threads = 64;
-  if ((long long)threads > pieces) threads = (int)(pieces > 0 ? pieces : 1);
-  std::atomic<long long> next{0};
-  std::atomic<int> err{0};
-  auto work = [&] {
-    for (;;) {
-      const long long k = next.fetch_add(1);
-      if (k >= pieces || err.load()) return;
-      long long off = k * kPiece;
-      const long long end = off + kPiece < n ? off + kPiece : n;
-      while (off < end) {
-        const ssize_t put = pwrite(fd, buf + off, (size_t)(end - off), (off_t)off);
-        if (put < 0) {
-          if (errno == EINTR) continue;
-          err.store(errno);
-          return;
-        }
-        off += put;
-      }
-    }
-  };
-  std::vector<std::thread> pool;
-  for (int t = 1; t < threads; ++t) {
-    try {
-      pool.emplace_back(work);
-    } catch (...) {
-      break;
-    }
-  }
-  work();
-  for (auto& t : pool) t.join();
-  if (close(fd) != 0 && !err.load()) err.store(errno);
-  return err.load() ? -(long long)err.load() : 0;
-}
-
 // Faults in [p, p + n) from `threads` threads (MADV_POPULATE_WRITE per slice where the kernel
 // has it, else one store per 4 KB page): a buffer that several writers fill at once would
 // otherwise take every first-touch fault inside their copies.

@@ -70,16 +70,6 @@ def read_text_file(path: str) -> np.ndarray:
     return out[:got]
 
 
-def write_file(path: str, buf) -> None:
-    """``buf`` (uint8 array) as the whole content of ``path``, written by concurrent native
-    pwrites."""
-    buf = np.ascontiguousarray(buf, dtype=np.uint8)
-    rc = int(native.runtime().oryx_write_file_parallel(os.fsencode(path), buf.ctypes.data,
-                                                       len(buf), min(16, os.cpu_count() or 1)))
-    if rc < 0:
-        raise OSError(-rc, os.strerror(-rc), path)
-
-
 def stats() -> dict:
     """Bytes queued for unmapping and bytes unmapped by the reaper so far."""
     out = (ctypes.c_longlong * 2)()

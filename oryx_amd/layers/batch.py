@@ -37,8 +37,6 @@ import threading
 import time
 from typing import List, Optional, Tuple
 
-import numpy as np
-
 from .. import hostbuf, tracing
 from ..api import BatchLayerUpdate, Dataset
 from ..transport.producer import LogTopicProducer
@@ -63,12 +61,8 @@ def _write_part(path_no_ext: str, records) -> str:
         vals = records.values()
         if isinstance(vals, TextLines):
             path = path_no_ext + ".txt"
-            buf = vals.joined()
-            if isinstance(buf, np.ndarray) and len(buf) >= (64 << 20):
-                hostbuf.write_file(path + ".w", buf)      # concurrent native pwrites
-            else:
-                with open(path + ".w", "wb") as f:
-                    f.write(memoryview(buf))
+            with open(path + ".w", "wb") as f:
+                f.write(memoryview(vals.joined()))
             os.replace(path + ".w", path)
             return path
         text = "\n".join(vals)

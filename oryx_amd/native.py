@@ -98,7 +98,6 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_hostbuf_quiesce", c_ll, [c_ll])
     _sig(lib, "oryx_read_file_parallel", c_ll, [c_cp, c_vp, c_ll, c_i])
     _sig(lib, "oryx_hostbuf_prefault", None, [c_vp, c_ll, c_i])
-    _sig(lib, "oryx_write_file_parallel", c_ll, [c_cp, c_vp, c_ll, c_i])
     _sig(lib, "oryx_encode_spans", c_ll, [c_vp, c_vp, c_vp, c_ll, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_gather_lines", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_concat_buffers", c_ll, [c_vp, c_vp, c_ll, c_vp])

@@ -66,14 +66,3 @@ def test_read_text_file_parallel_pieces_and_final_newline_cpu(tmp_path, monkeypa
         assert got.tobytes() == want
     p.write_bytes(b"")
     assert len(hostbuf.read_text_file(str(p))) == 0
-
-
-def test_write_file_parallel_pieces_cpu(tmp_path):
-    rs = np.random.default_rng(1)
-    data = rs.integers(0, 256, size=(70 << 20) + 999, dtype=np.uint8)
-    p = tmp_path / "part.w"
-    p.write_bytes(b"x" * (100 << 20))                  # longer old content: truncated
-    hostbuf.write_file(str(p), data)
-    assert p.read_bytes() == data.tobytes()
-    hostbuf.write_file(str(p), data[:0])
-    assert p.read_bytes() == b""
