@@ -66,6 +66,7 @@ def test_one_buffer_drain_with_gaps_and_key_fallback(tmp_path, monkeypatch):
     from oryx_amd import hostbuf
     from oryx_amd.layers.common import drain_dataset
     monkeypatch.setattr(hostbuf, "_MIN", 1 << 10)
+    monkeypatch.setenv("ORYX_DRAIN_ONE_BUFFER", "1")
     root = str(tmp_path / "log")
     tlog.maybe_create_topic(root, "In", 4)
     topic = tlog.Topic(root, "In")
