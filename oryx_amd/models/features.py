@@ -243,28 +243,23 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     F = schema.get_num_features()
     cats = [f for f in range(F) if schema.is_categorical(f)]
     S = len(cats)
-    lib = native.runtime()
-    base = buf.ctypes.data + off
-    cap = max(1, n_lines or nbytes // 8)
-    while True:
-        ends = np.empty(cap, dtype=np.int64)
-        got = lib.oryx_line_ends(ctypes.c_void_p(base), int(nbytes), ends.ctypes.data, cap)
-        if got >= 0:
-            ends = ends[:got]
-            break
-        cap = -got
-    n = len(ends)
-    if n == 0:
+    if nbytes == 0:
         return torch.zeros((0, F), dtype=dtype, device=device), {f: [] for f in cats}
-    starts = np.empty(n, dtype=np.int64)
-    starts[0] = 0
-    starts[1:] = ends[:-1] + 1
-    lap("line_scan")
     text = torch.empty(((nbytes + 31) // 16) * 16, dtype=torch.uint8, device=device)
     h2d(buf, off, nbytes, text)
-    d_starts = torch.from_numpy(starts).to(device)
-    d_ends = torch.from_numpy(ends).to(device)
     lap("h2d")
+    # line ends found on the device (the text is there anyway): 1 GB pieces of
+    # nonzero(text == '\n') instead of a host scan of the whole buffer
+    piece = 1 << 30
+    d_ends = torch.cat([torch.nonzero(text[lo:min(nbytes, lo + piece)] == 10).flatten() + lo
+                        for lo in range(0, nbytes, piece)])
+    n = int(d_ends.numel())
+    if n == 0:
+        return torch.zeros((0, F), dtype=dtype, device=device), {f: [] for f in cats}
+    d_starts = torch.empty_like(d_ends)
+    d_starts[0] = 0
+    d_starts[1:] = d_ends[:-1] + 1
+    lap("line_scan")
     out_col = torch.arange(F, dtype=torch.int32, device=device)
     is_num = torch.tensor([0 if f in cats else 1 for f in range(F)], dtype=torch.uint8,
                           device=device)
@@ -285,6 +280,8 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
         if S:
             return None     # (the host subset's local categories would need a re-encode)
         idx = torch.nonzero(bad).flatten().cpu().numpy()
+        ends = d_ends.cpu().numpy()
+        starts = d_starts.cpu().numpy()
         if (ends[idx] == starts[idx]).any():
             return None                 # an empty line: the host parser skips it (row count)
         sub = TextLines(buf[off:off + nbytes], n, ends).take(idx)
