@@ -18,6 +18,7 @@ from __future__ import annotations
 import ctypes
 import os
 import weakref
+from typing import Optional
 
 import numpy as np
 
@@ -29,10 +30,11 @@ _MIN = int(float(os.environ.get("ORYX_HOSTBUF_MIN_MB", "64")) * (1 << 20))
 _ON = os.environ.get("ORYX_HOSTBUF", "1") != "0"
 
 
-def empty(n: int) -> np.ndarray:
-    """An uninitialised (in fact zero-filled) uint8 array of ``n`` bytes."""
+def empty(n: int, min_bytes: Optional[int] = None) -> np.ndarray:
+    """An uninitialised (in fact zero-filled) uint8 array of ``n`` bytes (native from
+    ``min_bytes``, default ``ORYX_HOSTBUF_MIN_MB``)."""
     n = int(n)
-    if not _ON or n < _MIN:
+    if not _ON or n < (_MIN if min_bytes is None else min(_MIN, int(min_bytes))):
         return np.empty(n, dtype=np.uint8)
     lib = native.runtime()
     p = lib.oryx_hostbuf_alloc(n)

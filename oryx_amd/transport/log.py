@@ -262,6 +262,19 @@ class Topic:
     def reader(self, partition: int, offset: int) -> "PartitionReader":
         return PartitionReader(self, partition, offset)
 
+    def segment_bases(self, partition: int) -> List[int]:
+        """First offsets of the partition's segment files, ascending."""
+        pdir = os.path.join(self.root, self.name, str(partition))
+        out = []
+        try:
+            names = os.listdir(pdir)
+        except OSError:
+            return out
+        for f in names:
+            if f.endswith(".log") and f[:-4].isdigit():
+                out.append(int(f[:-4]))
+        return sorted(out)
+
 
 _FRAME_HEADER = 32     # u32 magic, u32 crc, u64 offset, i64 ts, u32 key len, u32 value len
 _FRAME = struct.Struct("<IIqqII")
@@ -405,7 +418,9 @@ class PartitionReader:
         if start >= end_offset:
             return TextLines(b"", 0), 0
         cap = max(int(lib.oryx_reader_text_bound(self._r, int(end_offset))), 1 << 16)
-        buf = hostbuf.empty(cap)
+        # (from 8 MB: a drain reads a partition as one buffer per 64 MB segment, freed in bulk
+        # after the concatenation -- on the reaper thread, not the layer's)
+        buf = hostbuf.empty(cap, min_bytes=8 << 20)
         used_total = total = 0
         used = ctypes.c_longlong(0)
         flags = ctypes.c_int(0)
@@ -424,7 +439,7 @@ class PartitionReader:
             if flags.value & 4:
                 # more was appended since the bound was taken: grow
                 cap = max(2 * cap, used_total + int(used.value))
-                grown = hostbuf.empty(cap)
+                grown = hostbuf.empty(cap, min_bytes=8 << 20)
                 grown[:used_total] = buf[:used_total]
                 buf = grown
                 continue

@@ -91,6 +91,34 @@ def test_one_buffer_drain_with_gaps_and_key_fallback(tmp_path, monkeypatch):
     topic.close()
 
 
+def test_drain_reads_segments_in_parallel_in_order(tmp_path):
+    """Partitions of many small segment files: the drain reads the segment ranges on worker
+    threads and keeps every partition's records in log order."""
+    from oryx_amd.layers.common import drain_dataset
+    root = str(tmp_path / "log")
+    tlog.maybe_create_topic(root, "In", 3, segment_bytes=1 << 12)
+    topic = tlog.Topic(root, "In", segment_bytes=1 << 12)
+    msgs = ["m%05d,%s" % (j, "x" * (j % 37)) for j in range(6000)]
+    for lo in range(0, len(msgs), 100):        # (a segment rolls between appends)
+        topic.append_batch([(None, m) for m in msgs[lo:lo + 100]])
+    assert len(topic.segment_bases(0)) > 10
+    cons = tlog.TopicConsumer(topic, start="earliest")
+    # per partition, the order the per-record path gives
+    ends = topic.end_offsets()
+    want = {}
+    for r in cons.readers:
+        rr = topic.reader(r.partition, r.position)
+        want[r.partition] = []
+        while rr.position < ends[r.partition]:
+            want[r.partition] += [v for _, _, _, v in rr.poll(100000, 50)]
+        rr.close()
+    vals = list(drain_dataset(cons, ends).values())
+    assert vals == [m for p in range(3) for m in want[p]]
+    assert [r.position for r in cons.readers] == ends
+    cons.close()
+    topic.close()
+
+
 def test_multichunk_parse_matches_single_chunk_with_dropped_lines():
     """A buffer large enough for the threaded in-place parse (rows written at their line's
     index, codes remapped, gaps from dropped / empty lines closed) gives the rows, codes and
