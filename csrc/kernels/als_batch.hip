@@ -755,8 +755,10 @@ als_solve_batch(AlsParams p, unsigned long long* prof) {
       const int w = b * NM + m;
       valid_n[m] = w < p.n_work;
       int ww = valid_n[m] ? w : p.n_work - 1;   // tail: a real row, solved, not stored
-      ww += p.rot;                                  // (rotated: the long rows come last)
-      ww -= ww >= p.n_work ? p.n_work : 0;
+      if (!ORYX_ALS_NO_PART_WAIT) {
+        ww += p.rot;                                // (rotated: the long rows come last)
+        ww -= ww >= p.n_work ? p.n_work : 0;
+      }
       rows_n[m] = p.row_ids ? sload(p.row_ids, ww) : ww;
       slot_n[m] = (valid_n[m] && p.long_slot) ? sload(p.long_slot, ww) : -1;
     });
@@ -1205,8 +1207,10 @@ als_solve_batch_gl(AlsParams p, unsigned long long* prof) {
       const int w = b * NM + m;
       valid_n[m] = w < p.n_work;
       int ww = valid_n[m] ? w : p.n_work - 1;   // tail: a real row, solved, not stored
-      ww += p.rot;                                  // (rotated: the long rows come last)
-      ww -= ww >= p.n_work ? p.n_work : 0;
+      if (!ORYX_ALS_NO_PART_WAIT) {
+        ww += p.rot;                                // (rotated: the long rows come last)
+        ww -= ww >= p.n_work ? p.n_work : 0;
+      }
       rows_n[m] = p.row_ids ? sload(p.row_ids, ww) : ww;
       slot_n[m] = (valid_n[m] && p.long_slot) ? sload(p.long_slot, ww) : -1;
     });

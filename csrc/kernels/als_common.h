@@ -38,8 +38,11 @@ struct AlsParams {
 // Wait (lane 0 of the wave, bounded) until a long row's reduced record is complete, then
 // acquire at agent scope: the record was written on other CUs / XCDs.  A timeout (2 s) marks
 // the solve failed (fail_count += 2^20) instead of hanging the GPU.
+#ifndef ORYX_ALS_NO_PART_WAIT
+#define ORYX_ALS_NO_PART_WAIT 0
+#endif
 __device__ __forceinline__ void wait_long_row(const AlsParams& p, int slot) {
-  if (!p.part_flags) return;
+  if (ORYX_ALS_NO_PART_WAIT || !p.part_flags) return;
   if ((threadIdx.x & 63) == 0) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(p.part_flags + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
