@@ -15,6 +15,7 @@
 // Mappings ask for transparent huge pages (MADV_HUGEPAGE: first-touch faults and the unmap
 // walk 512x fewer page-table entries where the kernel grants them).
 #include <errno.h>
+#include <pthread.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <unistd.h>
@@ -65,10 +66,21 @@ struct Reaper {
   }
 };
 
+// Never destroyed: the detached thread may still be waiting on it at exit.  A forked child
+// gets a fresh one (no reaper thread exists there, and the parent's lock may have been held
+// at the fork): the parent's queued mappings are left to the child's exit.
+std::atomic<Reaper*> g_reaper{nullptr};
+
+void reaper_after_fork_child() { g_reaper.store(new Reaper()); }
+
 Reaper& reaper() {
-  // never destroyed: the detached thread may still be waiting on it at exit
-  static Reaper* r = new Reaper();
-  return *r;
+  static const bool once = [] {
+    g_reaper.store(new Reaper());
+    pthread_atfork(nullptr, nullptr, reaper_after_fork_child);
+    return true;
+  }();
+  (void)once;
+  return *g_reaper.load();
 }
 
 }  // namespace

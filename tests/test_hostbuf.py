@@ -66,3 +66,27 @@ def test_read_text_file_parallel_pieces_and_final_newline_cpu(tmp_path, monkeypa
         assert got.tobytes() == want
     p.write_bytes(b"")
     assert len(hostbuf.read_text_file(str(p))) == 0
+
+
+def test_reaper_in_a_forked_child_cpu(monkeypatch):
+    """A forked child gets a reaper of its own (the parent's thread does not exist there)."""
+    import os
+    monkeypatch.setattr(hostbuf, "_MIN", 1 << 20)
+    a = hostbuf.empty(4 << 20)
+    a[:] = 1
+    del a
+    gc.collect()
+    assert hostbuf.quiesce(10) == 0
+    pid = os.fork()
+    if pid == 0:
+        ok = False
+        try:
+            b = hostbuf.empty(4 << 20)
+            b[:] = 2
+            del b
+            gc.collect()
+            ok = hostbuf.quiesce(10) == 0 and hostbuf.stats()["freed_bytes"] == 4 << 20
+        finally:
+            os._exit(0 if ok else 3)
+    _, st = os.waitpid(pid, 0)
+    assert os.WEXITSTATUS(st) == 0
