@@ -218,6 +218,17 @@ def _timestamps(lines: Sequence[str]) -> np.ndarray:
     return ingest.parse_timestamps(lines, default_ts=0)
 
 
+def _blob_keys(blob_ends) -> List[str]:
+    """The keys of a (blob, ends) pair as strings."""
+    blob, ends = blob_ends
+    b = bytes(blob)
+    out, at = [], 0
+    for e in np.asarray(ends).tolist():
+        out.append(b[at:e].decode("utf-8"))
+        at = e
+    return out
+
+
 def write_features(path: str, ids, mat, part: int = 0) -> None:
     """``X/`` or ``Y/`` directory with gzip part ``part`` of ``[id,[floats]]`` JSON lines (the
     reference's Spark text output with the gzip codec); ``ids`` a list of strings or a key
@@ -592,8 +603,12 @@ class ALSUpdate(MLUpdate):
         if not ctx.is_main:
             return None
         tp = time.perf_counter()
-        write_features(os.path.join(candidate_path, "X"), x_ids, x_rows)
-        write_features(os.path.join(candidate_path, "Y"), y_ids, y_rows)
+        # the IDs' bytes straight from the native dictionaries (the X/ Y/ files and the UP
+        # messages take them as (blob, ends): no Python string is encoded again)
+        x_blob = users.keys_blob(np.ascontiguousarray(used_u, dtype=np.int64))
+        y_blob = items.keys_blob(np.ascontiguousarray(used_i, dtype=np.int64))
+        write_features(os.path.join(candidate_path, "X"), x_blob, x_rows)
+        write_features(os.path.join(candidate_path, "Y"), y_blob, y_rows)
         ph["write_factors"] = ph.get("write_factors", 0.0) + time.perf_counter() - tp
         tp = time.perf_counter()
         pmml = pmmlu.build_skeleton_pmml()
@@ -608,7 +623,9 @@ class ALSUpdate(MLUpdate):
         pmml.add_extension_content("YIDs", y_ids)
         ph["pmml"] = ph.get("pmml", 0.0) + time.perf_counter() - tp
         self._cache[candidate_path] = {"x_ids": x_ids, "y_ids": y_ids, "X": X, "Y": Y,
-                                       "x_rows": x_rows, "y_rows": y_rows}
+                                       "x_rows": x_rows, "y_rows": y_rows,
+                                       "x_blob": x_blob, "y_blob": y_blob,
+                                       "x_codes": np.asarray(used_u), "users": users}
         its = trainer.timings.get("iteration_ms", [])
         self._timings[candidate_path] = {
             "ratings": n_agg, "users": len(used_u), "items": len(used_i),
@@ -747,11 +764,13 @@ class ALSUpdate(MLUpdate):
 
     def _published_rows(self, pmml, model_parent_path):
         """(x_ids, X rows text, y_ids, Y rows text) of the promoted model: from the build's
-        cache when the winner was built in this process, else read back from its files."""
+        cache when the winner was built in this process (IDs as native (blob, ends) pairs),
+        else read back from its files."""
         src = getattr(self, "promoted_from", None)
         f = self._cache.get(src) if src else None
         if f is not None and f.get("x_rows") is not None:
-            return f["x_ids"], f["x_rows"], f["y_ids"], f["y_rows"]
+            return (f.get("x_blob") or f["x_ids"]), f["x_rows"], \
+                (f.get("y_blob") or f["y_ids"]), f["y_rows"]
         x_ids, X = read_features(os.path.join(model_parent_path, pmml.get_extension_value("X")))
         y_ids, Y = read_features(os.path.join(model_parent_path, pmml.get_extension_value("Y")))
         return x_ids, textfmt.format_rows(X), y_ids, textfmt.format_rows(Y)
@@ -759,11 +778,15 @@ class ALSUpdate(MLUpdate):
     def _publish_local(self, pmml, new_data, past_data, model_parent_path, model_update_topic):
         all_data = concat_lines([new_data, past_data])
         x_ids, x_text, y_ids, y_text = self._published_rows(pmml, model_parent_path)
+
+        def count(ids):
+            return len(ids[1]) if isinstance(ids, tuple) else len(ids)
+
         log.info("Sending item / Y data as model updates")
-        if len(y_ids):
+        if count(y_ids):
             model_update_topic.send_block("UP", ingest.assemble_row_messages("Y", y_ids, y_text))
         log.info("Sending user / X data as model updates")
-        if not len(x_ids):
+        if not count(x_ids):
             return
         if self.no_known_items:
             model_update_topic.send_block("UP", ingest.assemble_row_messages("X", x_ids, x_text))
@@ -781,7 +804,13 @@ class ALSUpdate(MLUpdate):
             return
         # join: users without any event are not sent
         n_u = len(present)
-        code = users.encode(list(x_ids))
+        src = getattr(self, "promoted_from", None)
+        f = self._cache.get(src) if src else None
+        if f is not None and f.get("users") is users and f.get("x_codes") is not None:
+            code = np.asarray(f["x_codes"], dtype=np.int64)    # (x row j = user code used_u[j])
+        else:
+            code = users.encode(list(x_ids) if not isinstance(x_ids, tuple)
+                                else _blob_keys(x_ids))
         ok = code < n_u
         ok[ok] = present[code[ok]]
         kidx = np.where(ok, code, -1)
