@@ -245,17 +245,16 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     S = len(cats)
     if nbytes == 0:
         return torch.zeros((0, F), dtype=dtype, device=device), {f: [] for f in cats}
+    # the line ends are found by the native threads while the text goes up to the device
+    scan = _LineEnds(buf, off, nbytes, n_lines)
     text = torch.empty(((nbytes + 31) // 16) * 16, dtype=torch.uint8, device=device)
     h2d(buf, off, nbytes, text)
     lap("h2d")
-    # line ends found on the device (the text is there anyway): 1 GB pieces of
-    # nonzero(text == '\n') instead of a host scan of the whole buffer
-    piece = 1 << 30
-    d_ends = torch.cat([torch.nonzero(text[lo:min(nbytes, lo + piece)] == 10).flatten() + lo
-                        for lo in range(0, nbytes, piece)])
-    n = int(d_ends.numel())
+    ends = scan.result()
+    n = len(ends)
     if n == 0:
         return torch.zeros((0, F), dtype=dtype, device=device), {f: [] for f in cats}
+    d_ends = torch.from_numpy(ends).to(device)
     d_starts = torch.empty_like(d_ends)
     d_starts[0] = 0
     d_starts[1:] = d_ends[:-1] + 1
@@ -280,8 +279,9 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
         if S:
             return None     # (the host subset's local categories would need a re-encode)
         idx = torch.nonzero(bad).flatten().cpu().numpy()
-        ends = d_ends.cpu().numpy()
-        starts = d_starts.cpu().numpy()
+        starts = np.empty(n, dtype=np.int64)
+        starts[0] = 0
+        starts[1:] = ends[:-1] + 1
         if (ends[idx] == starts[idx]).any():
             return None                 # an empty line: the host parser skips it (row count)
         sub = TextLines(buf[off:off + nbytes], n, ends).take(idx)
@@ -400,6 +400,40 @@ class _Digest(threading.Thread):
             self._err = e
 
     def result(self) -> bytes:
+        self.join()
+        if self._err is not None:
+            raise self._err
+        return self._out
+
+
+class _LineEnds(threading.Thread):
+    """The ``'\n'`` offsets of ``buf[off:off + nbytes]`` (native threaded scan) on a thread of
+    its own, beside the text's upload to the device."""
+
+    def __init__(self, buf: np.ndarray, off: int, nbytes: int, n_lines: int):
+        super().__init__(daemon=True)
+        self._args = (buf, off, nbytes, n_lines)
+        self._out: Optional[np.ndarray] = None
+        self._err: Optional[BaseException] = None
+        self.start()
+
+    def run(self) -> None:
+        try:
+            buf, off, nbytes, n_lines = self._args
+            lib = native.runtime()
+            cap = max(1, n_lines or nbytes // 8)
+            while True:
+                ends = np.empty(cap, dtype=np.int64)
+                got = lib.oryx_line_ends(ctypes.c_void_p(buf.ctypes.data + off), int(nbytes),
+                                         ends.ctypes.data, cap)
+                if got >= 0:
+                    self._out = ends[:got]
+                    return
+                cap = -got
+        except BaseException as e:   # re-raised in result()
+            self._err = e
+
+    def result(self) -> np.ndarray:
         self.join()
         if self._err is not None:
             raise self._err
