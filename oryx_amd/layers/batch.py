@@ -37,6 +37,8 @@ import threading
 import time
 from typing import List, Optional, Tuple
 
+import numpy as np
+
 from .. import hostbuf, tracing
 from ..api import BatchLayerUpdate, Dataset
 from ..transport.producer import LogTopicProducer
@@ -81,13 +83,43 @@ def _write_part(path_no_ext: str, records) -> str:
     return path_no_ext
 
 
-def save_interval_data(data_dir: str, timestamp: int, records) -> Optional[str]:
+def _write_text_parts(tmp: str, buf) -> bool:
+    """A large keyless text buffer as part-00000.txt, part-00001.txt, ... cut at
+    :func:`~oryx_amd.textlines.part_edges`, written concurrently (one write() per file: the
+    files scale on the box's filesystem, one big file does not -- 22.5 GB took 2.2 s and was
+    the k-means generation's critical path).  False when one file is all there is."""
+    from concurrent.futures import ThreadPoolExecutor
+    from ..textlines import part_edges
+    if not isinstance(buf, np.ndarray):
+        buf = np.frombuffer(buf, dtype=np.uint8)
+    edges = part_edges(buf)
+    if len(edges) <= 2:
+        return False
+
+    def write(j):
+        path = os.path.join(tmp, "part-%05d.txt" % j)
+        with open(path + ".w", "wb") as f:
+            f.write(memoryview(buf[edges[j]:edges[j + 1]]))
+        os.replace(path + ".w", path)
+
+    with ThreadPoolExecutor(max_workers=len(edges) - 1) as ex:
+        list(ex.map(write, range(len(edges) - 1)))
+    return True
+
+
+def save_interval_data(data_dir: str, timestamp: int, records,
+                       split: bool = False) -> Optional[str]:
+    """The interval's records as ``oryx-<ts>.data/part-*``; ``split``: a large keyless text
+    interval as several part files (:func:`_write_text_parts`)."""
     if not records or not len(records):
         return None
     d = os.path.join(ioutils.to_local_path(data_dir), "oryx-%d.data" % timestamp)
     tmp = d + ".tmp"
     os.makedirs(tmp, exist_ok=True)
-    _write_part(os.path.join(tmp, "part-00000"), records)
+    vals = records.values() if split and isinstance(records, Dataset) and records.keyless \
+        else None
+    if not (isinstance(vals, TextLines) and _write_text_parts(tmp, vals.joined())):
+        _write_part(os.path.join(tmp, "part-00000"), records)
     os.replace(tmp, d)
     return d
 
@@ -311,7 +343,10 @@ class BatchLayer(AbstractLayer):
             ph["read_past"] = time.perf_counter() - tp
             # the interval's data goes to the data dir while the update runs (disk writes
             # beside GPU / parse work); the interval ends only once it is there
-            saver = _Background(save_interval_data, self.data_dir, ts, records)
+            # (apps whose parsers adopt part files by byte range take a large interval as
+            # several files, written concurrently)
+            saver = _Background(save_interval_data, self.data_dir, ts, records,
+                                bool(getattr(self._update, "split_interval_files", False)))
             producer = None
             if self.update_topic and self.update_broker:
                 producer = LogTopicProducer(self.update_broker, self.update_topic, self.config,

@@ -75,6 +75,7 @@ class _Seg:
     values: Dict[int, List[str]]       # categorical feature -> segment-local distinct values
     nbytes: int
     owned: bool = False                # ``full`` is this parse's own (not a cached tensor)
+    ends: Optional[np.ndarray] = None  # the segment's '\n' offsets (when the parse had them)
 
 
 def _buf_view(buf) -> np.ndarray:
@@ -244,7 +245,8 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     cats = [f for f in range(F) if schema.is_categorical(f)]
     S = len(cats)
     if nbytes == 0:
-        return torch.zeros((0, F), dtype=dtype, device=device), {f: [] for f in cats}
+        return torch.zeros((0, F), dtype=dtype, device=device), {f: [] for f in cats}, \
+            np.zeros(0, dtype=np.int64)
     # the line ends are found by the native threads while the text goes up to the device
     scan = _LineEnds(buf, off, nbytes, n_lines)
     text = torch.empty(((nbytes + 31) // 16) * 16, dtype=torch.uint8, device=device)
@@ -253,7 +255,7 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     ends = scan.result()
     n = len(ends)
     if n == 0:
-        return torch.zeros((0, F), dtype=dtype, device=device), {f: [] for f in cats}
+        return torch.zeros((0, F), dtype=dtype, device=device), {f: [] for f in cats}, ends
     d_ends = torch.from_numpy(ends).to(device)
     d_starts = torch.empty_like(d_ends)
     d_starts[0] = 0
@@ -298,7 +300,7 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
         for f in cats:
             out[:, f] = torch.from_numpy(codes[f]).to(device)
         lap("categorical")
-    return out, values
+    return out, values, ends
 
 
 def _python_block(lines: Sequence[str], schema: InputSchema, dtype: torch.dtype
@@ -384,22 +386,30 @@ def _select_rows(parent: _Seg, index: np.ndarray, cats: List[int], device) -> _S
 
 class _Digest(threading.Thread):
     """``ingest.content_digest`` of a byte range on a thread of its own (the native hash runs
-    without the GIL, beside the parse of the same bytes)."""
+    without the GIL, beside the parse of the same bytes), and of the part files the batch
+    layer saves it as (``textlines.part_edges``): ``result()`` -> (digest, [(edge0, edge1,
+    digest)] or [])."""
 
     def __init__(self, buf: np.ndarray, off: int, nbytes: int):
         super().__init__(daemon=True)
         self._args = (buf, off, nbytes)
-        self._out: Optional[bytes] = None
+        self._out = None
         self._err: Optional[BaseException] = None
         self.start()
 
     def run(self) -> None:
         try:
-            self._out = ingest.content_digest(*self._args)
+            from ..textlines import part_edges
+            buf, off, nbytes = self._args
+            whole = ingest.content_digest(buf, off, nbytes)
+            edges = part_edges(buf[off:off + nbytes])
+            chunks = [(a, b, ingest.content_digest(buf, off + a, b - a))
+                      for a, b in zip(edges[:-1], edges[1:])] if len(edges) > 2 else []
+            self._out = (whole, chunks)
         except BaseException as e:   # re-raised in result()
             self._err = e
 
-    def result(self) -> bytes:
+    def result(self):
         self.join()
         if self._err is not None:
             raise self._err
@@ -466,6 +476,9 @@ class FeatureHistory:
         self.keep = keep
         self._segs: "OrderedDict[tuple, _Seg]" = OrderedDict()
         self._unkeyed: "OrderedDict[bytes, _Seg]" = OrderedDict()
+        # part-file digest -> (digest of the unkeyed parse it is a byte range of, first row,
+        # end row): a large interval is saved as several part files (layers/batch.py)
+        self._unkeyed_chunks: Dict[bytes, Tuple[bytes, int, int]] = {}
         self._schema_key = None
         self.stats = {"hits": 0, "misses": 0, "hit_bytes": 0, "parsed_bytes": 0, "adopted": 0}
 
@@ -479,6 +492,7 @@ class FeatureHistory:
     def clear(self) -> None:
         self._segs.clear()
         self._unkeyed.clear()
+        self._unkeyed_chunks.clear()
 
     @staticmethod
     def _digest(buf: np.ndarray, off: int, nbytes: int) -> Optional[bytes]:
@@ -492,7 +506,7 @@ class FeatureHistory:
             if got is not None:
                 self.stats["device_parsed_bytes"] = \
                     self.stats.get("device_parsed_bytes", 0) + nbytes
-                return _Seg(got[0], got[1], nbytes)
+                return _Seg(got[0], got[1], nbytes, ends=got[2])
         got = _native_block(buf, off, nbytes, n_lines, schema, dtype)
         if got is None:
             return None
@@ -531,6 +545,38 @@ class FeatureHistory:
             for k in [k for k in self._segs if k not in keyed]:
                 del self._segs[k]
         return _merge(segs, schema, self.device)
+
+    def _add_chunks(self, dg: bytes, sg: _Seg, chunks, buf: np.ndarray, off: int,
+                    nbytes: int) -> None:
+        """Remember the part files an unkeyed parse will come back as (row ranges by the
+        segment's line ends)."""
+        if not chunks:
+            return
+        ends = sg.ends
+        if ends is None:
+            ends = TextLines(buf[off:off + nbytes]).ends()
+        if len(ends) != int(sg.full.shape[0]):
+            return                     # (lines the parser dropped: rows and lines differ)
+        for a, b, cdg in chunks:
+            lo = int(np.searchsorted(ends, a, side="left"))
+            hi = int(np.searchsorted(ends, b, side="left"))
+            self._unkeyed_chunks[cdg] = (dg, lo, hi)
+
+    def _drop_chunks(self, dg: bytes) -> None:
+        for k in [k for k, v in self._unkeyed_chunks.items() if v[0] == dg]:
+            del self._unkeyed_chunks[k]
+
+    def _adopt_chunk(self, cdg: bytes, schema: InputSchema) -> _Seg:
+        """A part file that is a byte range of a remembered unkeyed parse: its rows (codes
+        renumbered as a parse of the file alone numbers them); the parse is released once its
+        last part file is adopted."""
+        dg, lo, hi = self._unkeyed_chunks.pop(cdg)
+        parent = self._unkeyed[dg]
+        cats = [f for f in range(schema.get_num_features()) if schema.is_categorical(f)]
+        sg = _select_rows(parent, np.arange(lo, hi, dtype=np.int64), cats, self.device)
+        if not any(v[0] == dg for v in self._unkeyed_chunks.values()):
+            del self._unkeyed[dg]
+        return sg
 
     def _selection(self, part: LineSelection, schema: InputSchema, dtype, key_s,
                    keyed: set) -> Optional[_Seg]:
@@ -586,18 +632,28 @@ class FeatureHistory:
                     self.stats["adopted"] += 1
                     self.stats["hit_bytes"] += nbytes
                     del self._unkeyed[dg]
+                    self._drop_chunks(dg)
+                elif dg is not None and key is not None and dg in self._unkeyed_chunks:
+                    sg = self._adopt_chunk(dg, schema)
+                    sg.nbytes = nbytes        # (cached under the part file's key from now on)
+                    sg.owned = False
+                    self.stats["adopted"] += 1
+                    self.stats["hit_bytes"] += nbytes
                 else:
                     sg = self._parse_range(buf, off, nbytes, n_lines, schema, dtype)
+                    chunks = []
                     if pending is not None:
-                        dg = pending.result()
+                        dg, chunks = pending.result()
                     if sg is None:
                         return None
                     self.stats["misses"] += 1
                     self.stats["parsed_bytes"] += nbytes
                     if key is None and dg is not None:
                         self._unkeyed[dg] = sg
+                        self._add_chunks(dg, sg, chunks, buf, off, nbytes)
                         while len(self._unkeyed) > self.UNKEYED_KEEP:
-                            self._unkeyed.popitem(last=False)
+                            old, _ = self._unkeyed.popitem(last=False)
+                            self._drop_chunks(old)
                 if key is not None and self.keep:
                     self._segs[key] = sg
             if key is not None:

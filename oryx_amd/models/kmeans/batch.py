@@ -49,6 +49,9 @@ _INIT_STRATEGIES = ("k-means||", "random")
 
 class KMeansUpdate(MLUpdate):
     sharded_data = True
+    # the interval is saved as several part files when large; FeatureHistory adopts each
+    # from the interval's parse (models/features.py)
+    split_interval_files = True
 
     def __init__(self, config):
         super().__init__(config)

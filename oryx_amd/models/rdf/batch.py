@@ -276,6 +276,10 @@ class RDFUpdate(MLUpdate):
     sample gathered from every rank, the level histograms are all-reduced, and evaluation
     sums per-rank partial counts."""
 
+    # the interval is saved as several part files when large; FeatureHistory adopts each
+    # from the interval's parse (models/features.py)
+    split_interval_files = True
+
     sharded_data = True
 
     def __init__(self, config):

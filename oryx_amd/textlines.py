@@ -21,7 +21,8 @@ import numpy as np
 
 from . import hostbuf, native
 
-__all__ = ["TextLines", "LineSelection", "LineConcat", "concat_lines", "as_buffer"]
+__all__ = ["TextLines", "LineSelection", "LineConcat", "concat_lines", "as_buffer",
+           "part_edges"]
 
 _NL = 10
 
@@ -306,3 +307,38 @@ def concat_lines(parts: Sequence[Union[TextLines, Sequence[str], None]]):
 def as_buffer(lines) -> Optional[object]:
     """The newline-terminated byte buffer of ``lines`` when it is a :class:`TextLines`."""
     return lines.joined() if isinstance(lines, TextLines) else None
+
+
+# A large interval is saved as several part files written concurrently (one write() per file
+# scales with the files on the box's filesystem; one file does not: scripts/write_probe.py).
+PART_FILE_BYTES = 1 << 30
+MAX_PART_FILES = 16
+SPLIT_MIN_BYTES = 4 << 30
+
+
+def part_edges(buf, nbytes: Optional[int] = None) -> List[int]:
+    """Byte offsets [0, ..., nbytes] splitting a newline-terminated buffer into the part files
+    it is saved as (from SPLIT_MIN_BYTES): ceil(nbytes / PART_FILE_BYTES) pieces (at most
+    MAX_PART_FILES), each cut
+    just after the first newline at or past its even share.  The batch layer's save and the
+    feature parsers' adoption of part files (models/features.py) both use this, so a saved
+    interval's files are byte ranges the parser of that interval can name."""
+    b = np.frombuffer(buf, dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+    n = len(b) if nbytes is None else int(nbytes)
+    parts = 1 if n < SPLIT_MIN_BYTES else min(MAX_PART_FILES, max(1, -(-n // PART_FILE_BYTES)))
+    edges = [0]
+    for j in range(1, parts):
+        p = max(edges[-1], n * j // parts)
+        q = -1
+        step = 1 << 20
+        while p < n and q < 0:
+            w = b[p:min(n, p + step)]
+            hit = np.flatnonzero(w == 10)
+            if len(hit):
+                q = p + int(hit[0]) + 1
+            p += step
+        if q <= edges[-1] or q >= n:
+            continue
+        edges.append(q)
+    edges.append(n)
+    return edges

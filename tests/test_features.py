@@ -254,3 +254,40 @@ def test_native_span_encoding_first_appearance_order_cpu():
     assert values[0] == list(want_vals)
     assert np.array_equal(np.nan_to_num(codes[0], nan=-1.0),
                           np.nan_to_num(np.array(want_codes, dtype=np.float64), nan=-1.0))
+
+
+def test_interval_saved_as_several_part_files_is_adopted_cpu(monkeypatch, tmp_path):
+    """A large interval is saved as several part files (textlines.part_edges; the batch
+    layer writes them concurrently); the next generation adopts each of them from the
+    interval's parse -- no re-parse -- with the rows and categorical encodings a parse of the
+    files gives."""
+    from oryx_amd import textlines
+    from oryx_amd.api import Dataset
+    from oryx_amd.layers.batch import read_past_data, save_interval_data
+    from oryx_amd.textlines import LineSelection
+    monkeypatch.setattr(FeatureHistory, "UNKEYED_MIN_BYTES", 1)
+    monkeypatch.setattr(textlines, "PART_FILE_BYTES", 4000)
+    monkeypatch.setattr(textlines, "SPLIT_MIN_BYTES", 4000)
+    rs = np.random.default_rng(9)
+    schema = _schema()
+    new = TextLines.from_strings(_lines(rs, 1500, ["red", "green", "blue", "", "cyan"]))
+    dev = torch.device("cpu")
+    hist = FeatureHistory(dev)
+    mask = rs.random(len(new)) < 0.1
+    parse_features(LineSelection(new, np.flatnonzero(~mask)), schema, dev, history=hist)
+    data_dir = "file:" + str(tmp_path / "data") + "/"
+    save_interval_data(data_dir, 77, Dataset.from_values(new), split=True)
+    past = read_past_data(data_dir).values()
+    assert len(past.segment_list()) > 4            # several part files
+    assert sorted(past) == sorted(new)
+    before = hist.stats["parsed_bytes"]
+    got = parse_features(past, schema, dev, history=hist)
+    assert hist.stats["parsed_bytes"] == before    # every part file adopted
+    assert hist.stats["adopted"] == len(past.segment_list())
+    want = parse_features(TextLines(np.frombuffer(bytes(past.joined()), dtype=np.uint8).copy()),
+                          schema, dev)
+    assert got.values == want.values
+    assert torch.equal(torch.nan_to_num(got.full, -7.0), torch.nan_to_num(want.full, -7.0))
+    # and once cached under their keys, the part files are hits
+    parse_features(past, schema, dev, history=hist)
+    assert hist.stats["hits"] == len(past.segment_list())
