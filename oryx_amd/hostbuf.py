@@ -55,13 +55,14 @@ def prefault(buf: np.ndarray, threads: int = 16) -> None:
                                                min(threads, os.cpu_count() or 1))
 
 
-def read_text_file(path: str) -> np.ndarray:
+def read_text_file(path: str, threads: int = 16) -> np.ndarray:
     """The bytes of a text file as a uint8 array ending with a newline (one is appended when
-    the file lacks it), read by concurrent native preads into an :func:`empty` buffer."""
+    the file lacks it), read by ``threads`` concurrent native preads into an :func:`empty`
+    buffer."""
     size = os.path.getsize(path)
     out = empty(size + 1)
-    got = int(native.runtime().oryx_read_file_parallel(os.fsencode(path), out.ctypes.data,
-                                                       size, min(16, os.cpu_count() or 1)))
+    got = int(native.runtime().oryx_read_file_parallel(
+        os.fsencode(path), out.ctypes.data, size, max(1, min(threads, os.cpu_count() or 1))))
     if got < 0:
         raise OSError(-got, os.strerror(-got), path)
     if got == 0:

@@ -44,7 +44,7 @@ from ..api import BatchLayerUpdate, Dataset
 from ..transport.producer import LogTopicProducer
 from ..utils import config as cfg
 from ..parallel import dist
-from ..textlines import TextLines, concat_lines
+from ..textlines import LineConcat, TextLines, concat_lines
 from ..utils import faults, ioutils, lang, rng
 from .common import AbstractLayer, IntervalTimer, drain_dataset, read_text_parallel
 
@@ -143,26 +143,39 @@ def _finish_interval_dir(data_dir: str, timestamp: int) -> None:
 def read_past_data(data_dir: str, rank: int = 0, world: int = 1) -> Dataset:
     """All past records, or with ``world > 1`` this rank's share: part file j of the sorted
     listing belongs to rank ``j % world``."""
+    from concurrent.futures import ThreadPoolExecutor
     pairs: List[Tuple[Optional[str], str]] = []
     texts = []
     paths = [p for p in sorted(ioutils.list_files(data_dir, "*/part-*"))
              if ".tmp" not in os.path.dirname(p) and not p.endswith(".w")]
-    for j, path in enumerate(paths):
-        if j % world != rank:
-            continue
-        if path.endswith(".txt"):
-            # the file's bytes are the message buffer (no per-line strings), keyed by the
-            # file's identity so apps can reuse their parse of it (models/als/history.py)
-            st = os.stat(path)
-            texts.append(TextLines(hostbuf.read_text_file(path)).with_key(
-                ("part", os.path.abspath(path), st.st_size, st.st_mtime_ns)))
+    mine = [p for j, p in enumerate(paths) if j % world == rank]
+    txt = [p for p in mine if p.endswith(".txt")]
+    # the .txt files' bytes are the message buffers (no per-line strings), keyed by the
+    # file's identity so apps can reuse their parse of it (models/als/history.py,
+    # models/features.py); several files are read at once, 16 preads in flight in all
+    per = max(1, 16 // max(1, len(txt)))
+
+    def load(path):
+        st = os.stat(path)
+        return TextLines(hostbuf.read_text_file(path, per)).with_key(
+            ("part", os.path.abspath(path), st.st_size, st.st_mtime_ns))
+
+    loaded = {}
+    if txt:
+        with ThreadPoolExecutor(max_workers=min(16, len(txt))) as ex:
+            loaded = dict(zip(txt, ex.map(load, txt)))
+    for path in mine:
+        if path in loaded:
+            texts.append(loaded[path])
             continue
         with open(path, "r", encoding="utf-8") as f:
             for line in f:
                 if line.strip():
                     k, m = json.loads(line)
                     pairs.append((k, m))
-    values = concat_lines(texts)
+    # several part files stay a lazy concatenation: the feature parsers take them part by part
+    # (cached / adopted parses), others get the joined buffer when they ask for its bytes
+    values = LineConcat(texts) if len(texts) > 1 and not pairs else concat_lines(texts)
     if not pairs:
         return Dataset.from_values(values)
     return Dataset([(None, v) for v in values] + pairs)

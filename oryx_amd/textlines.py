@@ -201,6 +201,10 @@ class _Lazy(TextLines):
         raise NotImplementedError
 
     buf = property(lambda self: self.materialize().buf)
+    segments = property(lambda self: self.segment_list_or_none())
+
+    def segment_list_or_none(self) -> Optional[List[tuple]]:
+        return self.materialize().segments
 
     def ends(self) -> np.ndarray:
         return self.materialize().ends()
@@ -245,7 +249,6 @@ class LineSelection(_Lazy):
         self._n = len(self.index)
         self._ends = None
         self._strs = None
-        self.segments = None
         self._mat = None
 
     def _build(self) -> TextLines:
@@ -266,8 +269,19 @@ class LineConcat(_Lazy):
         self._n = sum(len(p) for p in flat)
         self._ends = None
         self._strs = None
-        self.segments = None
         self._mat = None
+
+    def segment_list_or_none(self) -> Optional[List[tuple]]:
+        # (from the parts, without joining them, when none of them is lazy)
+        if any(isinstance(p, _Lazy) for p in self.parts):
+            return self.materialize().segments
+        if all(p.segments is None for p in self.parts):
+            return None
+        return [seg for p in self.parts for seg in p.segment_list()]
+
+    def segment_list(self) -> List[tuple]:
+        segs = self.segment_list_or_none()
+        return segs if segs is not None else self.materialize().segment_list()
 
     def _build(self) -> TextLines:
         return concat_lines([p.materialize() if isinstance(p, _Lazy) else p
@@ -313,7 +327,7 @@ def as_buffer(lines) -> Optional[object]:
 # scales with the files on the box's filesystem; one file does not: scripts/write_probe.py).
 PART_FILE_BYTES = 1 << 30
 MAX_PART_FILES = 16
-SPLIT_MIN_BYTES = 4 << 30
+SPLIT_MIN_BYTES = 8 << 30
 
 
 def part_edges(buf, nbytes: Optional[int] = None) -> List[int]:
