@@ -836,14 +836,20 @@ constexpr int RDF_MAX_S = 32;   // label statistics per bin the split kernel kee
 
 // label centroid of bin b (regression: mean; classification: share of class maj); +inf when
 // the bin is empty
+// (a NaN centroid -- from a NaN in the histogram -- ranks as an empty bin: rdf_cat_order's
+// counting ranks must stay a permutation of [0, B), or ord[] keeps stale entries that later
+// index the histogram and cat_left out of bounds)
 __device__ __forceinline__ double rdf_centroid(const float* hf, int b, int S, int kind, int maj) {
+  double v;
   if (kind == 2) {
     const double cnt = (double)hf[(long long)b * S];
-    return cnt > 0.0 ? (double)hf[(long long)b * S + 1] / cnt : INFINITY;
+    v = cnt > 0.0 ? (double)hf[(long long)b * S + 1] / cnt : INFINITY;
+  } else {
+    double c2 = 0.0;
+    for (int s = 0; s < S; ++s) c2 += (double)hf[(long long)b * S + s];
+    v = c2 > 0.0 ? (double)hf[(long long)b * S + maj] / c2 : INFINITY;
   }
-  double c2 = 0.0;
-  for (int s = 0; s < S; ++s) c2 += (double)hf[(long long)b * S + s];
-  return c2 > 0.0 ? (double)hf[(long long)b * S + maj] / c2 : INFINITY;
+  return v == v ? v : INFINITY;
 }
 
 // ord[r] = the bin of rank r in centroid order (ties by bin index, empty bins last)
