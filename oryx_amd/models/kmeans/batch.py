@@ -38,7 +38,7 @@ from ...utils import rng
 from ..features import FeatureHistory, parse_features
 from ..schema import InputSchema
 from . import evaluation
-from .common import read_clusters, validate_pmml_vs_schema, clustering_model_pmml
+from .common import ClusterInfo, read_clusters, validate_pmml_vs_schema, clustering_model_pmml
 
 __all__ = ["KMeansUpdate"]
 
@@ -185,6 +185,14 @@ class KMeansUpdate(MLUpdate):
             return None
         tp = time.perf_counter()
         pmml = clustering_model_pmml(self.input_schema, centers, sizes)
+        # the evaluation of this candidate takes the clusters as built instead of parsing them
+        # back out of the PMML (its real arrays are shortest round-trip decimals: the same
+        # doubles)
+        try:
+            self._built_clusters = (pmml, [ClusterInfo(i, centers[i].tolist(), int(sizes[i]))
+                                           for i in range(len(centers))])
+        except ValueError:               # (e.g. an empty cluster: the PMML path decides)
+            self._built_clusters = None
         self.phase_seconds["pmml"] = self.phase_seconds.get("pmml", 0.0) + \
             time.perf_counter() - tp
         return pmml
@@ -203,7 +211,9 @@ class KMeansUpdate(MLUpdate):
         else:
             x = self._points(concat_lines([train_data, test_data]), ctx)
         tp = time.perf_counter()
-        clusters = read_clusters(model)
+        built = getattr(self, "_built_clusters", None)
+        self._built_clusters = None
+        clusters = built[1] if built is not None and built[0] is model else read_clusters(model)
         if self._sharded(ctx):
             ev = evaluation.evaluate_sharded(self.evaluation_strategy, clusters, x, ctx,
                                              device=ctx.device)
