@@ -18,6 +18,8 @@ import os
 import xml.etree.ElementTree as ET
 from typing import Iterable, List, Optional
 
+import numpy as np
+
 from . import text as _text
 from . import ioutils
 
@@ -198,8 +200,19 @@ def read_pmml_from_update_key_message(key: str, message: str) -> PMMLDoc:
 def to_array(values, as_int: bool = False) -> ET.Element:
     vals = list(values)
     arr = ET.Element(q("Array"), {"type": "int" if as_int else "real", "n": str(len(vals))})
-    arr.text = _text.join_pmml_delimited_numbers(
-        [int(v) for v in vals] if as_int else [float(v) for v in vals])
+    if as_int:
+        arr.text = _text.join_pmml_delimited_numbers([int(v) for v in vals])
+        return arr
+    a = np.asarray(vals, dtype=np.float64)
+    # Double.toString is Python's shortest repr wherever Java writes plain decimals (0 and
+    # 1e-3 <= |x| < 1e7); only the other values need the Java formatting one by one
+    plain = (a == 0) | ((np.abs(a) >= 1e-3) & (np.abs(a) < 1e7))
+    fl = a.tolist()
+    if bool(plain.all()):
+        arr.text = " ".join(map(repr, fl))
+    else:
+        arr.text = " ".join(repr(x) if p else _text.java_double_str(x)
+                            for x, p in zip(fl, plain.tolist()))
     return arr
 
 

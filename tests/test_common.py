@@ -529,3 +529,16 @@ def test_parallel_ratings_parse_matches_sequential():
     with pytest.raises(ValueError, match="line 400000"):
         ingest.parse_ratings(("\n".join(bad)).encode(), ingest.IdDict(), ingest.IdDict(),
                              default_ts=0, strict=True)
+
+
+def test_pmml_real_array_fast_path_matches_java_formatting():
+    """to_array's vectorised path (repr where Java writes plain decimals) gives exactly the
+    Double.toString text element by element, thresholds and specials included."""
+    import numpy as np
+    from oryx_amd.utils import pmml as pm, text
+    rs = np.random.default_rng(1)
+    vals = [0.0, -0.0, 1.0, 1e-3, 9.99e-4, 5e-4, 1e7, 9999999.5, 1.5e-10, -2.5e8,
+            float("nan"), float("inf"), 0.1, -3.14159, 123456.789]
+    vals += list(rs.normal(0, 3, 500)) + list(rs.normal(0, 1e-3, 500))
+    for vs in (vals, [v for v in vals if v == 0 or 1e-3 <= abs(v) < 1e7]):
+        assert pm.to_array(vs).text == " ".join(text.java_double_str(v) for v in vs)
