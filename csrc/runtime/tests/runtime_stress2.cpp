@@ -72,6 +72,13 @@ long long oryx_topn_prep(int nq, int k, int kp, int max_batch, const float* targ
 void oryx_blob_hash64(const unsigned char* blob, const long long* ends, long long n,
                       unsigned long long seed, unsigned long long* out);
 void oryx_digest128(const unsigned char* p, long long n, unsigned long long* out);
+void* oryx_hostbuf_alloc(long long n);
+void oryx_hostbuf_free(void* p, long long n);
+void oryx_hostbuf_stats(long long* out);
+long long oryx_hostbuf_quiesce(long long timeout_ms);
+long long oryx_read_file_parallel(const char* path, char* out, long long n, int threads);
+long long oryx_encode_spans(const char* base, const long long* off, const int* len, long long n,
+                            long long stride, long long* codes, long long* first_row);
 }
 
 static std::atomic<int> g_errors{0};
@@ -642,6 +649,84 @@ static void test_https(const char* cert, const char* key) {
   oryx_http_free(S);
 }
 
+// ---------------------------------------------------------------- 6. host buffers, spans
+
+// writers allocating / filling / freeing host buffers on several threads while the reaper
+// unmaps them; the parallel file read of a file written here; the threaded categorical span
+// encoding against a sequential first-appearance numbering
+static void test_hostbuf(const char* dir) {
+  std::vector<std::thread> ts;
+  for (int w = 0; w < 6; ++w)
+    ts.emplace_back([w] {
+      for (int k = 0; k < 40; ++k) {
+        const long long n = (1ll << 20) * (1 + (w + k) % 5) + 4096 * k;
+        char* p = static_cast<char*>(oryx_hostbuf_alloc(n));
+        CHECK(p != nullptr);
+        if (!p) return;
+        CHECK(p[n - 1] == 0);
+        memset(p, 'a' + w, (size_t)n);
+        CHECK(p[n / 2] == 'a' + w);
+        oryx_hostbuf_free(p, n);
+      }
+    });
+  for (auto& t : ts) t.join();
+  CHECK(oryx_hostbuf_quiesce(10000) == 0);
+  long long st[2];
+  oryx_hostbuf_stats(st);
+  CHECK(st[0] == 0 && st[1] > 0);
+
+  const std::string path = std::string(dir) + "/hostbuf_read.txt";
+  std::string data;
+  for (int j = 0; j < 3000000; ++j) data += (char)('0' + j % 10), data += (j % 7 ? ',' : '\n');
+  FILE* f = fopen(path.c_str(), "wb");
+  CHECK(f != nullptr);
+  if (f) {
+    fwrite(data.data(), 1, data.size(), f);
+    fclose(f);
+    std::vector<char> got(data.size());
+    CHECK(oryx_read_file_parallel(path.c_str(), got.data(), (long long)got.size(), 8) ==
+          (long long)data.size());
+    CHECK(memcmp(got.data(), data.data(), data.size()) == 0);
+  }
+
+  const long long n = 400000;
+  std::string text;
+  std::vector<long long> off(n);
+  std::vector<int> len(n);
+  unsigned long long z = 12345;
+  for (long long j = 0; j < n; ++j) {
+    z = z * 6364136223846793005ull + 1442695040888963407ull;
+    const int v = (int)((z >> 33) % 3000);
+    const std::string key = (z >> 20) % 19 == 0 ? std::string() : "v" + std::to_string(v * v % 997);
+    off[j] = (long long)text.size();
+    len[j] = (int)key.size();
+    text += key;
+    text += ',';
+  }
+  std::vector<long long> codes(n), first(n);
+  const long long k = oryx_encode_spans(text.data(), off.data(), len.data(), n, 1, codes.data(),
+                                        first.data());
+  std::vector<std::string> seen;
+  bool ok = true;
+  for (long long j = 0; j < n && ok; ++j) {
+    if (len[j] == 0) {
+      ok = codes[j] == -1;
+      continue;
+    }
+    const std::string key = text.substr((size_t)off[j], (size_t)len[j]);
+    long long c = -1;
+    for (size_t q = 0; q < seen.size(); ++q)
+      if (seen[q] == key) c = (long long)q;
+    if (c < 0) {
+      c = (long long)seen.size();
+      seen.push_back(key);
+      ok = first[c] == j;
+    }
+    ok = ok && codes[j] == c;
+  }
+  CHECK(ok && k == (long long)seen.size());
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: runtime_stress2 <dir>\n");
@@ -655,6 +740,8 @@ int main(int argc, char** argv) {
   printf("topn_prep: errors %d\n", g_errors.load());
   test_pool();
   printf("thread pool: errors %d\n", g_errors.load());
+  test_hostbuf(argv[1]);
+  printf("host buffers / parallel read / span encoding: errors %d\n", g_errors.load());
   if (argc >= 4) {
     test_https(argv[2], argv[3]);
     printf("https: errors %d\n", g_errors.load());

@@ -11,7 +11,7 @@ set -euo pipefail
 cd "$(dirname "$0")/.."
 OUT=${1:-/tmp/oryx_sanitize}
 mkdir -p "$OUT"
-RT="csrc/runtime/oryx_log.cpp csrc/runtime/oryx_ingest.cpp csrc/runtime/oryx_http.cpp"
+RT="csrc/runtime/oryx_log.cpp csrc/runtime/oryx_ingest.cpp csrc/runtime/oryx_http.cpp csrc/runtime/oryx_hostbuf.cpp"
 LIBS="-lz -lssl -lcrypto"
 ASAN="-std=c++17 -O1 -g -fno-omit-frame-pointer -pthread -fsanitize=address,undefined -fno-sanitize-recover=undefined"
 TSAN="-std=c++17 -O1 -g -pthread -fsanitize=thread"
