@@ -137,10 +137,18 @@ long long oryx_hostbuf_quiesce(long long timeout_ms) {
   Reaper& r = reaper();
   std::unique_lock<std::mutex> lk(r.mu);
   auto done = [&] { return r.pending == 0; };
-  if (timeout_ms < 0)
+  if (timeout_ms < 0) {
     r.idle.wait(lk, done);
-  else
-    r.idle.wait_for(lk, std::chrono::milliseconds(timeout_ms), done);
+    return r.pending;
+  }
+  // (a bounded wait by polling: condition_variable::wait_for goes through
+  // pthread_cond_clockwait, which ThreadSanitizer does not see release the mutex)
+  const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (!done() && std::chrono::steady_clock::now() < until) {
+    lk.unlock();
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    lk.lock();
+  }
   return r.pending;
 }
 
