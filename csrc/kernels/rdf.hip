@@ -884,7 +884,7 @@ __global__ __launch_bounds__(64) void rdf_best_split(
     const unsigned char* __restrict__ is_cat, int T, int W, int Fs, int B, int S, int kind,
     int force_leaf, int* __restrict__ out_feat, int* __restrict__ out_bin,
     double* __restrict__ out_tot, float* __restrict__ out_gain,
-    unsigned char* __restrict__ cat_left) {
+    unsigned char* __restrict__ cat_left, int* __restrict__ err) {
   extern __shared__ unsigned short s_ord[];   // [64][B] categorical orders (when used)
   const int lane = threadIdx.x;
   const long long node = blockIdx.x;          // t * W + slot
@@ -900,6 +900,13 @@ __global__ __launch_bounds__(64) void rdf_best_split(
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     tot[s] = v;
   }
+  // every statistic of the node must be finite (label counts, weights and label sums: an
+  // all-reduced histogram holding NaN / inf means corrupted input -- a peer's stale or
+  // poisoned slot -- and must fail the forest, not quietly drop bins from the search)
+  bool finite = true;
+  for (long long i = lane; i < (long long)Fs * B * S; i += 64) finite = finite && isfinite(h[i]);
+  const bool bad = __any(!finite);
+  if (bad && lane == 0 && err) atomicOr(err, 1);
   double wn;
   const double parent = rdf_impurity(tot, S, kind, &wn);
   int maj = 0;
@@ -907,7 +914,7 @@ __global__ __launch_bounds__(64) void rdf_best_split(
     for (int s = 1; s < S; ++s) if (tot[s] > tot[maj]) maj = s;
   double best = -INFINITY;
   long long best_idx = 0x7FFFFFFFFFFFFFFFLL;
-  const bool leaf_node = force_leaf || wn < 2.0 || parent <= 1e-12 || B < 2;
+  const bool leaf_node = bad || force_leaf || wn < 2.0 || parent <= 1e-12 || B < 2;
   unsigned short* ord = s_ord + lane * B;
   // without categorical predictors a feature's split positions are spread over LPF lanes
   // (Fs = 10: 6 lanes each instead of 10 busy lanes of 64); a lane first sums the bins
@@ -917,7 +924,14 @@ __global__ __launch_bounds__(64) void rdf_best_split(
   const int CH = (B - 1 + LPF - 1) / LPF;
   if (!leaf_node) {
     for (int u = lane; u < Fs * LPF; u += 64) {
-      const int jj = u / LPF, k0 = (u - jj * LPF) * CH;
+      // the chunk start is clamped to the last split position: the trailing lanes of a
+      // feature can start past it ((LPF - 1) * CH > B - 1, e.g. B = 32, Fs = 6: LPF = 10,
+      // CH = 4, k0 up to 36), and their prefix walk over bins [0, k0) then read the next
+      // feature's bins -- for the last feature of the last node, past the end of hist.  That
+      // read ran off the histogram's allocation whenever the caching allocator had placed it
+      // at the end of a segment: the intermittent illegal access of the world-2 RDF test.
+      const int jj = u / LPF;
+      const int k0 = min((u - jj * LPF) * CH, B - 1);
       const int k1 = LPF == 1 ? B - 1 : (k0 + CH < B - 1 ? k0 + CH : B - 1);
       const int f = fj[jj];
       const float* hf = h + (long long)jj * B * S;
@@ -1014,18 +1028,19 @@ int oryx_rdf_expand_pieces(const long long* counts, int T, int W, int lo, int hi
   return oryx_check_launch();
 }
 
-// hist [T][W][Fs][B][S] fp32 -> best split per (tree, node); see rdf_best_split.
+// hist [T][W][Fs][B][S] fp32 -> best split per (tree, node); see rdf_best_split.  err
+// (nullable): set to 1 when some node's histogram holds a non-finite value.
 int oryx_rdf_best_split(const float* hist, const int* feats, const unsigned char* is_cat, int T,
                         int W, int Fs, int B, int S, int kind, int force_leaf, int* out_feat,
                         int* out_bin, double* out_tot, float* out_gain,
-                        unsigned char* cat_left, void* stream) {
+                        unsigned char* cat_left, int* err, void* stream) {
   if (T <= 0 || W <= 0) return ORYX_OK;
   if (S < 1 || S > RDF_MAX_S || B < 1 || kind < 0 || kind > 2) return ORYX_EINVAL;
   const size_t smem = is_cat ? (size_t)64 * B * sizeof(unsigned short) : 0;
   if (smem > 64 * 1024) return ORYX_EINVAL;
   hipLaunchKernelGGL(rdf_best_split, dim3((unsigned)(T * W)), dim3(64), smem,
                      reinterpret_cast<hipStream_t>(stream), hist, feats, is_cat, T, W, Fs, B, S,
-                     kind, force_leaf, out_feat, out_bin, out_tot, out_gain, cat_left);
+                     kind, force_leaf, out_feat, out_bin, out_tot, out_gain, cat_left, err);
   return oryx_check_launch();
 }
 

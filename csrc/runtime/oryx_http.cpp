@@ -30,6 +30,7 @@
 #include <netinet/tcp.h>
 #include <openssl/err.h>
 #include <openssl/ssl.h>
+#include <openssl/x509.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -49,6 +50,8 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
+
+#include "oryx_keystore.h"
 
 namespace {
 
@@ -675,10 +678,12 @@ void* oryx_http_start(const char* host, int port, int backlog, long long max_bod
   return S;
 }
 
-// Serves HTTPS on the server's socket: PEM certificate chain `cert`, private key `key` (null
-// or empty: the key is in `cert`), `password` for an encrypted key (may be null).  TLS 1.2 is
-// the minimum (the reference's connector allows TLSv1.2 and 1.1; 1.1 is deprecated).  Call
-// before the first oryx_http_next.  Returns 0, or -1 (oryx_http_tls_error says why).
+// Serves HTTPS on the server's socket.  `cert` is a Java keystore -- JKS or PKCS#12, as the
+// reference's keystore-file (oryx_keystore.cpp), `password` its keystore-password -- or a PEM
+// certificate chain with private key `key` (null or empty: the key is in `cert`) and
+// `password` for an encrypted key (may be null).  TLS 1.2 is the minimum (the reference's
+// connector allows TLSv1.2 and 1.1; 1.1 is deprecated).  Call before the first
+// oryx_http_next.  Returns 0, or -1 (oryx_http_tls_error says why).
 int oryx_http_tls(void* h, const char* cert, const char* key, const char* password) {
   auto* S = static_cast<Server*>(h);
   tls_err.clear();
@@ -703,8 +708,29 @@ int oryx_http_tls(void* h, const char* cert, const char* key, const char* passwo
     SSL_CTX_free(ctx);
     return -1;
   };
-  if (SSL_CTX_use_certificate_chain_file(ctx, cert) != 1) return fail("certificate");
-  if (SSL_CTX_use_PrivateKey_file(ctx, kf, SSL_FILETYPE_PEM) != 1) return fail("private key");
+  EVP_PKEY* ks_key = nullptr;
+  X509* ks_cert = nullptr;
+  STACK_OF(X509)* ks_chain = nullptr;
+  std::string ks_why;
+  const int ks = oryx::keystore_load(cert, password, nullptr, &ks_key, &ks_cert, &ks_chain,
+                                     &ks_why);
+  if (ks == oryx::kKeystoreOk) {
+    // certificate, chain and key straight from the keystore (no PEM files)
+    int ok = SSL_CTX_use_certificate(ctx, ks_cert) == 1 && SSL_CTX_use_PrivateKey(ctx, ks_key) == 1;
+    for (int i = 0; ok && i < sk_X509_num(ks_chain); ++i)
+      ok = SSL_CTX_add1_chain_cert(ctx, sk_X509_value(ks_chain, i)) == 1;
+    EVP_PKEY_free(ks_key);
+    X509_free(ks_cert);
+    sk_X509_pop_free(ks_chain, X509_free);
+    if (!ok) return fail("keystore");
+  } else if (ks != oryx::kKeystoreNotKeystore) {
+    tls_err = ks_why;
+    SSL_CTX_free(ctx);
+    return -1;
+  } else {
+    if (SSL_CTX_use_certificate_chain_file(ctx, cert) != 1) return fail("certificate");
+    if (SSL_CTX_use_PrivateKey_file(ctx, kf, SSL_FILETYPE_PEM) != 1) return fail("private key");
+  }
   if (SSL_CTX_check_private_key(ctx) != 1) return fail("key does not match certificate");
   // the password is only needed while loading
   SSL_CTX_set_default_passwd_cb_userdata(ctx, nullptr);

@@ -33,6 +33,7 @@ import json
 import logging
 import os
 import re
+import shutil
 import threading
 import time
 from typing import List, Optional, Tuple
@@ -108,9 +109,12 @@ def _write_text_parts(tmp: str, buf) -> bool:
 
 
 def save_interval_data(data_dir: str, timestamp: int, records,
-                       split: bool = False) -> Optional[str]:
+                       split: bool = False, publish: bool = True) -> Optional[str]:
     """The interval's records as ``oryx-<ts>.data/part-*``; ``split``: a large keyless text
-    interval as several part files (:func:`_write_text_parts`)."""
+    interval as several part files (:func:`_write_text_parts`).  ``publish=False`` leaves them
+    in ``oryx-<ts>.data.tmp`` (past-data readers skip it) for :func:`_finish_interval_dir` or
+    :func:`_discard_interval_dir` to settle once the interval's update has succeeded or
+    failed."""
     if not records or not len(records):
         return None
     d = os.path.join(ioutils.to_local_path(data_dir), "oryx-%d.data" % timestamp)
@@ -120,6 +124,8 @@ def save_interval_data(data_dir: str, timestamp: int, records,
         else None
     if not (isinstance(vals, TextLines) and _write_text_parts(tmp, vals.joined())):
         _write_part(os.path.join(tmp, "part-00000"), records)
+    if not publish:
+        return tmp
     os.replace(tmp, d)
     return d
 
@@ -138,6 +144,15 @@ def _finish_interval_dir(data_dir: str, timestamp: int) -> None:
     tmp = os.path.join(root, "oryx-%d.data.tmp" % timestamp)
     if os.path.isdir(tmp):
         os.replace(tmp, os.path.join(root, "oryx-%d.data" % timestamp))
+
+
+def _discard_interval_dir(data_dir: str, timestamp: int) -> None:
+    """Drop an interval's unpublished data (its update failed: the offsets stay uncommitted,
+    so the next interval re-reads these records and saves them then -- saving them now too
+    would put them in the past data twice)."""
+    tmp = os.path.join(ioutils.to_local_path(data_dir), "oryx-%d.data.tmp" % timestamp)
+    if os.path.isdir(tmp):
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def read_past_data(data_dir: str, rank: int = 0, world: int = 1) -> Dataset:
@@ -338,6 +353,9 @@ class BatchLayer(AbstractLayer):
         if self._sharded():
             self._run_sharded_main(ts, t_start)
             return
+        # where this interval starts: a failed update rewinds here, so the next interval
+        # re-reads (and only then saves) the same records
+        starts = [(r, r.position) for r in self._input_consumer.readers]
         records = drain_dataset(self._input_consumer)
         n_records = len(records)
         ph = self.last_phases = {"drain": time.perf_counter() - t_start}
@@ -354,12 +372,16 @@ class BatchLayer(AbstractLayer):
             tp = time.perf_counter()
             past = read_past_data(self.data_dir)
             ph["read_past"] = time.perf_counter() - tp
-            # the interval's data goes to the data dir while the update runs (disk writes
-            # beside GPU / parse work); the interval ends only once it is there
-            # (apps whose parsers adopt part files by byte range take a large interval as
-            # several files, written concurrently)
+            # the interval's data is written while the update runs (disk writes beside GPU /
+            # parse work) into oryx-<ts>.data.tmp, and published -- renamed into the past
+            # data -- only after the update has succeeded, as the reference saves only after
+            # a successful update (BatchLayer.java:103-124); apps whose parsers adopt part
+            # files by byte range take a large interval as several files, written
+            # concurrently
             saver = _Background(save_interval_data, self.data_dir, ts, records,
-                                bool(getattr(self._update, "split_interval_files", False)))
+                                bool(getattr(self._update, "split_interval_files", False)),
+                                False)
+            ok = False
             producer = None
             if self.update_topic and self.update_broker:
                 producer = LogTopicProducer(self.update_broker, self.update_topic, self.config,
@@ -370,12 +392,19 @@ class BatchLayer(AbstractLayer):
                     self._update.run_update(self._context, ts, new_data,
                                             past if len(past) else None, self.model_dir,
                                             producer)
+                ok = True
             finally:
                 if producer is not None:
                     producer.close()
                 ph["update"] = time.perf_counter() - tp
                 tp = time.perf_counter()
                 saver.wait()
+                if ok and saver.error is None:
+                    _finish_interval_dir(self.data_dir, ts)
+                else:
+                    _discard_interval_dir(self.data_dir, ts)
+                    for r, pos in starts:
+                        r.seek(pos)
                 # (the part of the save not hidden behind the update)
                 ph["save_data"] = time.perf_counter() - tp
                 ph["save_data_total"] = saver.seconds

@@ -157,6 +157,10 @@ def _register_runtime_extras(lib):
     _sig(lib, "oryx_http_free", None, [c_vp])
     _sig(lib, "oryx_http_tls", c_i, [c_vp, c_cp, c_cp, c_cp])
     _sig(lib, "oryx_http_tls_error", c_cp, [])
+    # path, password, alias, cert_pem*, cert_len*, key_pem*, key_len*
+    _sig(lib, "oryx_keystore_to_pem", c_i, [c_cp, c_cp, c_cp, c_vp, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_keystore_free", None, [c_vp])
+    _sig(lib, "oryx_keystore_error", c_cp, [])
     _sig(lib, "oryx_speed_append", c_ll, [c_vp, c_vp, c_i, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,
                                           c_vp, c_vp, c_i, c_ll, c_i, c_vp])
     _sig(lib, "oryx_split_by_time", c_ll, [c_vp, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,
@@ -337,9 +341,9 @@ def _load_kernels():
     _sig(lib, "oryx_rdf_expand_pieces", c_i, [c_vp, c_i, c_i, c_i, c_i, c_ll, c_i, c_vp, c_vp,
                                               c_vp, c_vp, c_vp, c_vp])
     # hist, feats, is_cat, T, W, Fs, B, S, kind, force_leaf, feat, bin, tot, gain, cat_left,
-    # stream
+    # err, stream
     _sig(lib, "oryx_rdf_best_split", c_i, [c_vp, c_vp, c_vp, c_i, c_i, c_i, c_i, c_i, c_i, c_i,
-                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
+                                           c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_sorted_ws_bytes", c_ll, [c_ll, c_i])
     _sig(lib, "oryx_kmeans_pp", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp, c_vp,
                                       c_vp])

@@ -240,15 +240,28 @@ def _choose_splits(hist: torch.Tensor, feats: torch.Tensor, data: BinnedData, ki
 _KIND = {"gini": 0, "entropy": 1, "variance": 2}
 
 
+def _check_split_err(err: torch.Tensor, depth: int, ctx) -> None:
+    """Raise when the split search met a non-finite histogram entry (synchronises).  Bootstrap
+    counts, label counts and label sums are finite by construction, so a NaN / inf there means
+    the level's (all-reduced) statistics are corrupt; trees grown from them would be silently
+    wrong."""
+    if int(err.item()):
+        err.zero_()
+        raise RuntimeError("RDF level %d: non-finite split statistics on rank %d%s"
+                           % (depth, ctx.rank, " (after the all-reduce)" if ctx.is_distributed
+                              else ""))
+
+
 def _split_kernel_ok(data: BinnedData, S: int) -> bool:
     return S <= 32 and (not any(data.categorical) or 64 * data.B * 2 <= 64 * 1024)
 
 
 def _choose_splits_kernel(hist: torch.Tensor, feats: torch.Tensor, data: BinnedData, kind: str,
-                          force_leaf: bool) -> LevelSplits:
+                          force_leaf: bool, err: Optional[torch.Tensor] = None) -> LevelSplits:
     """:func:`_choose_splits` as one HIP kernel (``rdf_best_split``: a wave per node, a lane
     per candidate feature, fp64 prefix sums and gains) instead of ~25 tensor ops over
-    [T, N, Fs, B, S] temporaries."""
+    [T, N, Fs, B, S] temporaries.  ``err`` (int32 [1], optional) is set to 1 when a node's
+    histogram holds a non-finite value (see :func:`_check_split_err`)."""
     T, N, Fs, B, S = hist.shape
     dev = hist.device
     lib = native.require_kernels()
@@ -265,6 +278,7 @@ def _choose_splits_kernel(hist: torch.Tensor, feats: torch.Tensor, data: BinnedD
                                  _KIND[kind], int(bool(force_leaf)), feat.data_ptr(),
                                  sbin.data_ptr(), tot.data_ptr(), gain.data_ptr(),
                                  cl.data_ptr() if cl is not None else None,
+                                 err.data_ptr() if err is not None else None,
                                  native.stream_ptr(dev))
     native.check(rc, "oryx_rdf_best_split")
     return LevelSplits(feat.long(), sbin.long(), cl, tot, gain)
@@ -631,6 +645,7 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
         # histogram in node chunks that fit the budget
         chunk = max(1, _HIST_BUDGET // max(1, T * Fs * B * S))
         splits = []
+        nonfinite = torch.zeros((), dtype=torch.bool, device=dev)
         for lo in range(0, nodes, chunk):
             hi = min(nodes, lo + chunk)
             if groups is not None:
@@ -641,6 +656,8 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
                                   hi - lo, feats[:, lo:hi], B)
             if ctx.is_distributed:
                 dist.all_reduce_sum(hist, ctx)
+                # see _check_split_err: read with the level's one host transfer below
+                nonfinite = nonfinite | ~torch.isfinite(hist).all()
             splits.append(_choose_splits(hist, feats[:, lo:hi], data, kind,
                                          force_leaf=depth == max_depth))
         split = LevelSplits(
@@ -671,6 +688,7 @@ def train_forest(data: BinnedData, target: torch.Tensor, num_classes: int, num_t
         host = torch.cat(parts, 1).cpu().numpy()
         if ctx.is_distributed:
             dist.check_collectives(ctx)      # see _train_device
+            _check_split_err(nonfinite.int().reshape(1), depth, ctx)
         w = [p_.shape[1] for p_ in parts]
         cut = np.cumsum([0] + w)
         feat_h = host[:, cut[0]:cut[1]].astype(np.int64)
@@ -743,6 +761,7 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
     perm = None
     pending = []
     any_cat = any(data.categorical)
+    split_err = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def sample_feats(width: int) -> torch.Tensor:
         if Fs < P:
@@ -820,7 +839,7 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
                 dist.all_reduce_sum(tot, ctx)
             parts.append(_choose_splits_kernel(
                 tot, torch.zeros((T, W, 1), dtype=torch.int32, device=dev), data, kind,
-                force_leaf=True))
+                force_leaf=True, err=split_err))
         for lo in range(0, W if not last else 0, chunk):
             hi = min(W, lo + chunk)
             max_pieces = (T * n + _PIECE - 1) // _PIECE + T * (hi - lo)
@@ -858,7 +877,7 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
             if ctx.is_distributed:
                 dist.all_reduce_sum(hist, ctx)
             parts.append(_choose_splits_kernel(hist, fe, data, kind,
-                                               force_leaf=depth == max_depth))
+                                               force_leaf=depth == max_depth, err=split_err))
             del hist
         if len(parts) == 1:
             split = parts[0]
@@ -876,6 +895,7 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
         # per level sizes every later histogram, split search and all-reduce to the live
         # nodes (deep levels of a forest are mostly leaves)
         live = int(is_split.sum(1).max()) if depth < max_depth else 0
+        _check_split_err(split_err, depth, ctx)
         if ctx.is_distributed:
             # the split search above consumed this level's all-reduced histograms: a one-shot
             # all-reduce whose peer never arrived must fail the forest here, not grow trees

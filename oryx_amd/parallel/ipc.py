@@ -13,7 +13,9 @@ the gloo control group.
 Safety: the reducer runs a self-test against ``torch.distributed.all_reduce`` when it is
 created (all ranks agree on the verdict); a peer that never arrives makes the kernel stop
 waiting after 120 s, set an error flag and write NaN instead of the sum (``check()`` raises
-and clears the flag) instead of hanging the GPU.  Tensors larger than the slot capacity,
+and clears the flag) instead of hanging the GPU.  Every staged payload carries its call's
+epoch, element count and per-workgroup checksums, which the reducers verify: ranks whose
+collective sequences diverged, or a slot read stale, raise at ``check()`` too.  Tensors larger than the slot capacity,
 non-fp32 tensors and multi-node worlds use RCCL.
 
 It is on by default for multi-rank CUDA (RCCL) worlds on one node and for a forced world of
@@ -118,8 +120,14 @@ class IpcAllReduce:
         e = int(self.err.item())
         if e:
             self.err.zero_()
-            raise RuntimeError("IPC all-reduce: rank %d never arrived (results since the "
-                               "timeout are NaN)" % (e - 1))
+            if e > 2000:
+                why = "rank %d's staged payload failed its checksum" % (e - 2001)
+            elif e > 1000:
+                why = ("rank %d's slot holds another call's payload (epoch / size mismatch: "
+                       "the ranks disagree on their sequence of collectives)" % (e - 1001))
+            else:
+                why = "rank %d never arrived" % (e - 1)
+            raise RuntimeError("IPC all-reduce: %s (results since then are NaN)" % why)
 
     def self_test(self) -> bool:
         """Sum rank-dependent probes both ways; True when every rank matched RCCL."""
@@ -213,7 +221,9 @@ class IpcAllGather:
             raise RuntimeError("IPC all-gather: more than %d matrices" % self.max_mats)
         m = e["m"] if e is not None else len(self._mats)
         if e is not None:
-            # every peer unmaps the old copy before any rank frees it
+            # this rank's last pushes through the old mappings have finished before they are
+            # closed, and every peer unmaps the old copy before any rank frees it
+            self.side.synchronize()
             for p in e["opened"]:
                 self.lib.oryx_ipc_close(ctypes.c_void_p(p))
                 self._opened.remove(p)
@@ -322,6 +332,8 @@ class IpcAllGather:
         return int(flag.item()) == 0
 
     def close(self) -> None:
+        # no push of this rank may still be writing through a mapping that is closed here
+        self.side.synchronize()
         for p in self._opened:
             self.lib.oryx_ipc_close(ctypes.c_void_p(p))
         self._opened = []

@@ -15,14 +15,17 @@ Equivalent of ``ServingLayer`` + ``ModelManagerListener`` (``[lserving]/ServingL
 
 from __future__ import annotations
 
+import ctypes
 import gc
 import logging
 import os
 import ssl
+import tempfile
 import threading
 import time
-from typing import Iterator, List, Optional
+from typing import Iterator, List, Optional, Tuple
 
+from .. import native
 from ..api import KeyMessage, ServingModelManager
 from ..metrics import Registry
 from ..transport import log as tlog
@@ -149,6 +152,31 @@ def resource_modules(config) -> List[str]:
     return out
 
 
+def keystore_pem(path: str, password: Optional[str], alias: Optional[str] = None
+                 ) -> Optional[Tuple[bytes, bytes]]:
+    """(certificate chain PEM, private key PEM) of a JKS or PKCS#12 keystore, or None when
+    ``path`` is not a keystore (PEM).  Raises ``ValueError`` for a wrong password or a file it
+    cannot read (native parser: ``csrc/runtime/oryx_keystore.cpp``)."""
+    lib = native.runtime()
+    cert_p, key_p = ctypes.c_void_p(), ctypes.c_void_p()
+    cert_n, key_n = ctypes.c_longlong(), ctypes.c_longlong()
+    enc = (lambda v: v.encode() if v is not None else None)
+    rc = lib.oryx_keystore_to_pem(enc(path), enc(password), enc(alias), ctypes.byref(cert_p),
+                                  ctypes.byref(cert_n), ctypes.byref(key_p),
+                                  ctypes.byref(key_n))
+    if rc == 1:
+        return None
+    if rc != 0:
+        raise ValueError("keystore %s: %s" % (path, (lib.oryx_keystore_error() or b"")
+                                              .decode(errors="replace")))
+    try:
+        return (ctypes.string_at(cert_p.value, cert_n.value),
+                ctypes.string_at(key_p.value, key_n.value))
+    finally:
+        lib.oryx_keystore_free(cert_p)
+        lib.oryx_keystore_free(key_p)
+
+
 class ServingLayer:
     def __init__(self, config, manager: Optional[ServingModelManager] = None,
                  input_producer=None, host: str = "0.0.0.0"):
@@ -229,6 +257,9 @@ class ServingLayer:
         return self
 
     def _ssl_context(self) -> Optional[ssl.SSLContext]:
+        """HTTPS when ``keystore-file`` is set: a Java keystore (JKS or PKCS#12, unlocked by
+        ``keystore-password``, as the reference's Tomcat connector takes it:
+        ``ServingLayer.java:214-217``) or a PEM certificate chain (+ ``key-file``)."""
         cert = self.keystore_file
         if not cert:
             return None
@@ -236,7 +267,20 @@ class ServingLayer:
         key = ioutils.to_local_path(self.key_file) if self.key_file else None
         ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
         ctx.minimum_version = ssl.TLSVersion.TLSv1_2
-        ctx.load_cert_chain(cert, key, password=self.keystore_password)
+        pem = keystore_pem(cert, self.keystore_password)
+        if pem is None:
+            ctx.load_cert_chain(cert, key, password=self.keystore_password)
+            return ctx
+        # ssl loads only files: the keystore's PEM form goes through a private temporary
+        # directory that exists only while it is loaded (the native front end reads the
+        # keystore itself, oryx_keystore.cpp)
+        with tempfile.TemporaryDirectory(prefix="oryx-tls-") as d:
+            cp, kp = os.path.join(d, "cert.pem"), os.path.join(d, "key.pem")
+            for path, text in ((cp, pem[0]), (kp, pem[1])):
+                fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
+                with os.fdopen(fd, "wb") as fh:
+                    fh.write(text)
+            ctx.load_cert_chain(cp, kp)
         return ctx
 
     def _start_update_consumer(self) -> None:

@@ -292,6 +292,62 @@ def test_batch_layer_new_and_past_data(tmp_path):
         sorted(produced)
 
 
+class FlakyBatchUpdate(BatchLayerUpdate):
+    """Fails its first update, then records like MockBatchUpdate."""
+    calls = 0
+    intervals = []
+
+    def __init__(self, config=None):
+        pass
+
+    def run_update(self, context, timestamp, new_data, past_data, model_dir, topic):
+        FlakyBatchUpdate.calls += 1
+        if FlakyBatchUpdate.calls == 1:
+            raise RuntimeError("injected update failure")
+        FlakyBatchUpdate.intervals.append(
+            (timestamp, new_data.values(), past_data.values() if past_data else []))
+
+
+def test_failed_update_saves_no_data_and_retry_does_not_duplicate(tmp_path):
+    """The interval's data is published into the past data only after its update succeeded
+    (BatchLayer.java:103-124: update, then SaveToHDFSFunction, then UpdateOffsetsFn).  A
+    failed update leaves no data dir behind and rewinds the consumer, so the next interval
+    sees the same records once as new data and the past data holds them once."""
+    import os
+    from oryx_amd.layers.batch import read_past_data
+    FlakyBatchUpdate.calls = 0
+    FlakyBatchUpdate.intervals = []
+    config = _config(tmp_path, **{"oryx.batch.update-class":
+                                  "tests.test_lambda_framework.FlakyBatchUpdate"})
+    root = str(tmp_path / "log")
+    data_dir = config.get_string("oryx.batch.storage.data-dir")
+    local = str(tmp_path / "data")
+    tlog.maybe_create_topic(root, "OryxInput", 2)
+    tlog.maybe_create_topic(root, "OryxUpdate", 1)
+    batch = BatchLayer(config)
+    batch.run_interval()
+    prod = LogTopicProducer("localhost:9092", "OryxInput", config, async_=False)
+    first = ["a%d" % j for j in range(40)]
+    for j, m in enumerate(first):
+        prod.send(str(j), m)
+    with pytest.raises(RuntimeError, match="injected"):
+        batch.run_interval(1000)
+    assert not os.path.isdir(local) or not [d for d in os.listdir(local)
+                                            if d.startswith("oryx-")]
+    batch.run_interval(2000)                  # the retry: same records as new data
+    second = ["b%d" % j for j in range(10)]
+    for j, m in enumerate(second):
+        prod.send(str(j), m)
+    batch.run_interval(3000)
+    prod.close()
+    batch.close()
+    assert [sorted(new) for _, new, _ in FlakyBatchUpdate.intervals] == \
+        [sorted(first), sorted(second)]
+    assert sorted(FlakyBatchUpdate.intervals[1][2]) == sorted(first)
+    assert sorted(read_past_data(data_dir).values()) == sorted(first + second)
+    assert sorted(os.listdir(local)) == ["oryx-2000.data", "oryx-3000.data"]
+
+
 # ---------------------------------------------------------------- SpeedLayerIT
 
 class MockSpeedModelManager(SpeedModelManager):

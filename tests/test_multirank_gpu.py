@@ -14,7 +14,8 @@ here each app's distributed path runs with the GPU kernels and collectives that 
 * k-means: Lloyd steps from the same centers over halves of the points (assign kernel,
   segment sums, the all-reduce) vs all points: centers within fp32 rounding;
 * RDF: one tree, every feature, over halves of the rows (histogram kernels, all-reduced
-  split statistics): the identical tree.
+  split statistics): the identical tree, with numeric predictors and with a categorical one.
+  Kernels run unserialised (launches overlap the IPC all-reduce as in production).
 """
 
 import json
@@ -90,20 +91,48 @@ if R == 0:
 from oryx_amd.ops import rdf as rdf_ops
 Xf = rs.normal(0, 1, (24000, 6))
 yc = ((Xf[:, 0] + 0.5 * Xf[:, 1] ** 2 - Xf[:, 2] * Xf[:, 3]) > 0.3).astype(np.int64)
-data = rdf_ops.bin_features(Xf[R::W], [False] * 6, [0] * 6, 32, torch.device(DEV),
-                            seed=2, threshold_source=Xf)
-forest = rdf_ops.train_forest(data, torch.from_numpy(yc[R::W]), 2, 1, 6, "gini", seed=4,
-                              ctx=ctx, feature_subset=6)
 def walk(n):
     d = {"id": n.id, "count": int(n.count)}
     if n.feature >= 0 and n.left is not None:
         d.update(f=int(n.feature), b=int(n.bin), l=walk(n.left), r=walk(n.right))
+        if n.cat_left is not None:
+            d["cl"] = [int(v) for v in np.asarray(n.cat_left).ravel().tolist()]
     else:
         d["stats"] = [float(v) for v in np.asarray(n.stats, dtype=np.float64).ravel().tolist()]
     return d
-if R == 0:
-    with open(os.path.join(out_dir, "rdf.json"), "w") as fh:
-        json.dump(walk(forest.roots[0]), fh)
+# all-numeric (6 predictors, 32 bins: the split search's lane chunking at Fs = 6), then with a
+# categorical predictor of arity 7 that the label depends on (RDFUpdateIT's categorical
+# feature): the centroid-ordered categorical splits run over all-reduced histograms too
+cat = rs.integers(0, 7, 24000)
+yk = ((Xf[:, 0] + 1.2 * np.isin(cat, [1, 4, 5]) - 0.8 * (cat == 6) + 0.3 * Xf[:, 1]) > 0.4) \
+    .astype(np.int64)
+Xk = np.concatenate([Xf[:, :4], cat[:, None].astype(np.float64)], 1)
+for name, X_, y_, iscat, ar in (("rdf", Xf, yc, [False] * 6, [0] * 6),
+                                ("rdf_cat", Xk, yk, [False] * 4 + [True], [0] * 4 + [7])):
+    data = rdf_ops.bin_features(X_[R::W], iscat, ar, 32, torch.device(DEV), seed=2,
+                                threshold_source=X_)
+    forest = rdf_ops.train_forest(data, torch.from_numpy(y_[R::W]), 2, 1, 6, "gini", seed=4,
+                                  ctx=ctx, feature_subset=X_.shape[1])
+    dist.check_collectives(ctx)
+    if R == 0:
+        with open(os.path.join(out_dir, name + ".json"), "w") as fh:
+            json.dump(walk(forest.roots[0]), fh)
+
+# ------------------------------------------------------------------ IPC slot headers
+# ranks whose collective sequences diverge (here: different sizes at one call) must be told,
+# not handed a sum over another call's payload; the next matching call is clean again
+if ctx.ipc is not None:
+    t = torch.ones(100 + 20 * R, device=DEV)
+    ctx.ipc.all_reduce_(t)
+    try:
+        ctx.ipc.check()
+        res["mismatch"] = "undetected"
+    except RuntimeError as e:
+        res["mismatch"] = str(e)
+    t = torch.ones(1000, device=DEV) * (R + 1)
+    ctx.ipc.all_reduce_(t)
+    ctx.ipc.check()
+    res["after_mismatch"] = float(t.sum())
 
 # ------------------------------------------------------------------ ALS batch generation
 from oryx_amd.layers.batch import BatchLayer
@@ -220,10 +249,6 @@ def _run_worlds(tmp_path, device):
         env = dict(os.environ, OMP_NUM_THREADS="2", ORYX_IPC_ALLREDUCE="any",
                    ORYX_IPC_ALLGATHER="any" if world == "push" else "0",
                    ORYX_MR_DEVICE=device,
-                   # each launch waits for its kernel: a device fault is reported at the
-                   # launch that caused it (an intermittent illegal access in the RDF part at
-                   # world 2 surfaced only at a later sync: profiles/r5_multirank_rdf_fault.log)
-                   AMD_SERIALIZE_KERNEL="3",
                    HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY",
                                                              "0"))
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
@@ -240,6 +265,10 @@ def _run_worlds(tmp_path, device):
     assert json.loads((outs[2] / "res1.json").read_text())["joined"] == 1
     if device != "cpu":
         assert res2["ipc"], res2          # the small sums went through the IPC all-reduce
+        for rr in (0, 1):
+            rj = json.loads((outs[2] / ("res%d.json" % rr)).read_text())
+            assert "size mismatch" in rj["mismatch"], rj
+            assert rj["after_mismatch"] == 3000.0, rj
     import torch
     # ---- ALS trainer (kernel tolerance: bf16 replicated factors can flip a rounding)
     cases = ((16, "fp32", 1e-4),) if device == "cpu" else ((64, "bf16", 2e-2), (96, "fp32", 1e-3))
@@ -254,9 +283,12 @@ def _run_worlds(tmp_path, device):
     a, b = torch.load(outs[1] / "kmeans.pt"), torch.load(outs[2] / "kmeans.pt")
     assert torch.equal(a["n"], b["n"])
     assert float((a["c"] - b["c"]).abs().max()) < 1e-4
-    # ---- RDF: the identical tree
-    assert json.loads((outs[1] / "rdf.json").read_text()) == \
-        json.loads((outs[2] / "rdf.json").read_text())
+    # ---- RDF: the identical tree (numeric predictors; with a categorical one, which the
+    # tree must use)
+    for name in ("rdf", "rdf_cat"):
+        t1 = json.loads((outs[1] / (name + ".json")).read_text())
+        assert t1 == json.loads((outs[2] / (name + ".json")).read_text()), name
+    assert '"cl"' in (outs[1] / "rdf_cat.json").read_text()
     # ---- ALS generation: one-rank single path vs two-rank sharded path
     X1, Y1, K1, pm1 = _read_model(outs[1] / "gen")
     X2, Y2, K2, pm2 = _read_model(outs[2] / "gen")

@@ -616,6 +616,36 @@ def test_split_kernel_matches_tensor_search(cuda, cls, kind, with_cat):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Fs,B", [(6, 32), (1, 32), (5, 17), (7, 100)])
+def test_split_kernel_lane_chunks_past_the_last_bin(cuda, Fs, B):
+    """Shapes whose per-feature lane chunks start past the last split position ((64 // Fs - 1)
+    * ceil((B - 1) / (64 // Fs)) > B - 1: B = 32, Fs = 6 is the world-2 RDF test's level) --
+    the chunk start is clamped, so no lane reads bins of the next feature (or past the end of
+    the histogram), and the search still matches the tensor search.  A non-finite histogram
+    entry sets the error flag and turns its node into a leaf."""
+    T, N, S, P = 2, 3, 2, 8
+    hist, feats = _random_level(T, N, Fs, B, S, P, True, seed=B + Fs)
+    data = rdf_ops.BinnedData(torch.zeros((1, P), dtype=torch.uint8, device=cuda), [B] * P,
+                              [None] * P, [False] * P, B)
+    ref = rdf_ops._choose_splits(hist.double().to(cuda), feats.to(cuda), data, "gini", False)
+    err = torch.zeros(1, dtype=torch.int32, device=cuda)
+    got = rdf_ops._choose_splits_kernel(hist.to(cuda), feats.to(cuda), data, "gini", False,
+                                        err=err)
+    assert int(err.item()) == 0
+    assert torch.equal(got.feat.cpu(), ref.feat.cpu())
+    assert torch.equal(got.bin.cpu(), ref.bin.cpu())
+    bad = hist.clone()
+    bad[1, 2, Fs - 1, B - 1, 1] = float("nan")
+    got = rdf_ops._choose_splits_kernel(bad.to(cuda), feats.to(cuda), data, "gini", False,
+                                        err=err)
+    assert int(err.item()) == 1
+    assert int(got.feat[1, 2]) == -1
+    with pytest.raises(RuntimeError, match="non-finite"):
+        rdf_ops._check_split_err(err, 3, type("C", (), {"rank": 0, "is_distributed": False}))
+    assert int(err.item()) == 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("classification", [True, False])
 def test_device_level_loop_matches_host_loop(cuda, classification, monkeypatch):
     """The sync-free level loop (device pieces, split kernel, pipelined host tree build)
