@@ -376,6 +376,7 @@ def main(argv=None) -> int:
             "backend": info["backend"],
             "ipc_allreduce": info.get("ipc_allreduce", False),
             "allgather": info.get("allgather"),
+            "allgather_selftest": info.get("allgather_selftest"),
             "rank_devices": [r.get("current_device", r["device"]) for r in info["ranks"]],
             "peak_hbm_gib_per_rank": float(peak.item()) / 2**30,
             "halfstep_ms": halfstep_ms,

@@ -237,10 +237,15 @@ def main(argv=None) -> int:
             import cProfile
             prof = cProfile.Profile()
             prof.enable()
+        if torch.cuda.is_available():
+            torch.cuda.reset_peak_memory_stats()
         t0 = time.perf_counter()
         layer.run_interval(now)
         t_gen = time.perf_counter() - t0
         gc.callbacks.remove(_gc_cb)
+        # the first generation's peak device memory (the caching allocator's view)
+        peak_hbm = torch.cuda.max_memory_allocated() / 2**30 if torch.cuda.is_available() \
+            else None
         if prof is not None:
             prof.disable()
             cprof_top = _cprofile_top(prof)
@@ -276,6 +281,7 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         layer.run_follower()
         t_gen = time.perf_counter() - t0
+        peak_hbm = None
         sharded_path = layer._sharded()
         first_phases = dict(getattr(layer._update, "phase_seconds", {}))
         first_train = dict(getattr(layer._update, "train_phases", {}) or {})
@@ -311,6 +317,7 @@ def main(argv=None) -> int:
             "phase_s": phases,
             "train_phase_s": first_train,
             "startup_warm_up_s": layer.warm_up_s,
+            "peak_hbm_gib_first_generation": peak_hbm,
             "gc_in_generation": gc_ms if ctx.is_main else None,
             "cprofile_top": cprof_top if args.cprofile and ctx.is_main else None,
             "update_messages": int(sum(ends)),

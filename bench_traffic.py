@@ -53,12 +53,14 @@ rnd = random.Random(seed)
 conn = http.client.HTTPConnection("127.0.0.1", port, timeout=60)
 lat = {n: [] for n in names}
 err = {n: 0 for n in names}
+slow = []      # (wall-clock start, ms, endpoint) of requests over 25 ms
 t_end = time.perf_counter() + dur
 while time.perf_counter() < t_end:
     ep = rnd.choices(names, weights)[0]
     u = "U%d" % rnd.randrange(users)
     i = "I%d" % rnd.randrange(items)
     t = time.perf_counter()
+    tw = time.time()
     try:
         if ep == "pref":
             conn.request("POST", "/pref/%s/%s" % (u, i), body=str(rnd.randint(1, 5)).encode(),
@@ -77,11 +79,13 @@ while time.perf_counter() < t_end:
     el = (time.perf_counter() - t) * 1e3
     lat[ep].append(el)
     err[ep] += 0 if ok else 1
+    if el > 25.0:
+        slow.append((tw, el, ep))
     if gap_ms > 0:
         want = rnd.expovariate(1.0 / gap_ms)
         if el < want:
             time.sleep((want - el) / 1e3)
-print(json.dumps({"lat": lat, "err": err}))
+print(json.dumps({"lat": lat, "err": err, "slow": slow}))
 """
 
 
@@ -136,20 +140,25 @@ while True:
     if sm is not None and sm.get_fraction_loaded() >= 1.0 and sm.X.size() == users:
         break
     time.sleep(0.05)
-# what the first micro-batch would otherwise do under the mix: the model's device mirror and
-# its Gramians (kept current incrementally from here on)
+# the manager warms a completely loaded model on its consumer thread (row maps, device
+# mirrors, Gramians: ALSSpeedModel.warm); wait for it like a deployment's first interval would
 t1 = time.time()
-sm.solver_inverses()
-print(json.dumps({"loaded_s": t1 - t0, "warm_s": time.time() - t1}), flush=True)
+mgr = speed.manager
+while mgr.warm_s is None:
+    time.sleep(0.05)
+print(json.dumps({"loaded_s": t1 - t0, "warm_s": time.time() - t1,
+                  "manager_warm_s": mgr.warm_s}), flush=True)
 assert sys.stdin.readline().strip() == "go"
 stop = threading.Event()
 durs = []
+phases = []
 def run():
     while not stop.is_set():
         t = time.perf_counter()
         speed.run_interval()
         dt = time.perf_counter() - t
         durs.append(dt * 1e3)
+        phases.append(dict(getattr(mgr, "last_phase_ms", {}) or {}))
         if interval_ms / 1e3 > dt:
             stop.wait(interval_ms / 1e3 - dt)
 th = threading.Thread(target=run, daemon=True)
@@ -158,7 +167,7 @@ sys.stdin.readline()
 stop.set()
 th.join(120)
 print(json.dumps({"intervals": speed.intervals_run, "up_rows": speed.updates_sent,
-                  "interval_ms": durs}), flush=True)
+                  "interval_ms": durs, "interval_phase_ms": phases}), flush=True)
 speed.close()
 os._exit(0)
 """
@@ -260,6 +269,7 @@ class _Sampler:
 
 def run_phase(port, args, mix, seed):
     gap = args.workers * args.interval_ms
+    t_start = time.time()
     procs = [subprocess.Popen([sys.executable, "-c", CLIENT, str(port), str(args.users),
                                str(args.items), str(args.duration_s), str(gap),
                                str(seed * 1000 + w), json.dumps(mix)],
@@ -268,7 +278,54 @@ def run_phase(port, args, mix, seed):
     outs = [json.loads(p.communicate()[0]) for p in procs]
     lat = {ep: sum((o["lat"][ep] for o in outs), []) for ep in mix}
     err = {ep: sum(o["err"][ep] for o in outs) for ep in mix}
-    return {ep: dict(_stats(lat[ep]), errors=err[ep]) for ep in mix}
+    res = {ep: dict(_stats(lat[ep]), errors=err[ep]) for ep in mix}
+    slow = sorted((tuple(x) for o in outs for x in o.get("slow", [])), key=lambda x: -x[1])
+    res["_slow"] = slow[:40]
+    res["_t_start"] = t_start
+    return res
+
+
+class _StallWatch:
+    """A thread that sleeps 1 ms at a time in the serving process and records every wake-up
+    that came more than 15 ms late (wall-clock time, ms): a pause of the whole interpreter --
+    a GIL held by a long native call, a GC pass -- shows up here, and the record lines it up
+    with the slow requests and the UP applications."""
+
+    def __init__(self):
+        self.stalls = []
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True, name="stall-watch")
+
+    def _run(self):
+        last = time.perf_counter()
+        while not self._stop.is_set():
+            time.sleep(0.001)
+            now = time.perf_counter()
+            if now - last > 0.015:
+                self.stalls.append((time.time() - (now - last), (now - last) * 1e3))
+            last = now
+
+    def start(self):
+        self._t.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        self._t.join()
+        return self.stalls
+
+
+def _attribute_slow(slow, stalls, applies, t_start):
+    """Per slow request (start, ms, endpoint): when it started (seconds into the phase), and
+    the serving-process stalls and UP applications whose time overlaps it."""
+    out = []
+    for t0, ms, ep in slow:
+        t1 = t0 + ms / 1e3
+        st = [round(d, 1) for (s0, d) in stalls if s0 < t1 and s0 + d / 1e3 > t0]
+        ap = [(round(d, 1), n) for (s0, d, n) in applies if s0 < t1 and s0 + d / 1e3 > t0]
+        out.append({"ms": round(ms, 1), "endpoint": ep, "at_s": round(t0 - t_start, 3),
+                    "stalls_ms": st, "up_apply": ap})
+    return out
 
 
 def main(argv=None) -> int:
@@ -352,6 +409,7 @@ def main(argv=None) -> int:
             if speed is not None:
                 ld = json.loads(speed.stdout.readline())
                 rec["speed_load_s"], rec["speed_warm_s"] = ld["loaded_s"], ld["warm_s"]
+                rec["speed_manager_warm_s"] = ld.get("manager_warm_s")
             vm = serving.manager.get_model()
             vm.top_n(np.zeros(args.features, np.float32), 10)   # device mirror + index
             port = serving.actual_port
@@ -366,6 +424,8 @@ def main(argv=None) -> int:
             s0 = _server_side(serving)
             smp = _Sampler().start() if args.sample else None
             rec["idle"] = run_phase(port, args, {"recommend": 1.0}, args.seed)
+            rec["idle"].pop("_slow", None)
+            rec["idle"].pop("_t_start", None)
             if smp is not None:
                 rec["idle_stack_samples"] = smp.stop()
             rec["idle_server"] = _server_delta(s0, _server_side(serving))
@@ -378,7 +438,19 @@ def main(argv=None) -> int:
             speed.stdin.flush()
             print("bench_traffic: mix phase", file=sys.stderr, flush=True)
             s0 = _server_side(serving)
+            sw = _StallWatch().start()
             rec["mix_phase"] = run_phase(port, args, mix, args.seed + 1)
+            stalls = sw.stop()
+            slow = rec["mix_phase"].pop("_slow", [])
+            t_mix = rec["mix_phase"].pop("_t_start")
+            mgr = serving.manager
+            # (UP applications of the mix phase only: the model load's are long and earlier)
+            applies = [a for a in getattr(mgr, "apply_log", []) if a[0] >= t_mix]
+            rec["mix_attribution"] = {
+                "stalls": [(round(t - t_mix, 3), round(d, 1))
+                           for t, d in sorted(stalls, key=lambda x: -x[1])[:20]],
+                "up_apply_ms": _stats([d for _, d, _ in applies]) if applies else None,
+                "slow_requests": _attribute_slow(slow, stalls, applies, t_mix)}
             rec["mix_server"] = _server_delta(s0, _server_side(serving))
             rec["mix_gc"] = gcp.take()
             speed.stdin.write("stop\n")
@@ -391,7 +463,11 @@ def main(argv=None) -> int:
             runs = sp["intervals"]
             rec["speed"] = {"intervals": runs, "up_rows": sp["up_rows"],
                             "interval_ms": _stats(sp["interval_ms"]),
-                            "process": "separate (as deployed)"}
+                            "process": "separate (as deployed)",
+                            # every interval: its duration and the manager's phases
+                            "per_interval": [dict(ms=d, phases=p) for d, p in
+                                             zip(sp["interval_ms"],
+                                                 sp.get("interval_phase_ms", []))]}
             rec["index"] = {k: c1.get(k, 0) - c0.get(k, 0) for k in ("rebuilds", "incremental",
                                                                     "delta_added")}
             rec["index"].update(delta_rows_now=c1.get("delta_rows"), dead_now=c1.get("dead"))

@@ -16,10 +16,27 @@
 //     still reading.
 //   * DONE: after a workgroup's rows are written, every thread fences at system scope and
 //     thread 0 stores done[m][src][c][g] = e into each destination's flag buffer.
-//   * WAIT: before the matrix is read, a kernel of 32 workgroups (every XCD gets some:
-//     workgroups are dispatched round-robin over the 8 XCDs) waits for every done flag of the
-//     epoch and then fences at system scope, which invalidates each XCD's L2 of lines the peers
-//     overwrote underneath it.
+//   * WAIT: before the matrix is read, a kernel of 32 workgroups waits for every done flag of
+//     the epoch and then fences at system scope.
+//
+// Why the readers cannot see stale rows (the receive copy is ordinary coarse-grained device
+// memory, which the solve kernels read through L2): in the gfx942 / gfx950 memory model (LLVM
+// AMDGPUUsage, "Memory Model GFX942"), device-local memory is mapped MTYPE RW with the PTE C-bit
+// set when the agent has several L2s, and the C-bit makes a write to a local line that does not
+// come through this XCD's L2 probe and invalidate the line there (the document names writes
+// from CUs of other L2s and from the CPU; a peer GPU's xGMI write enters this HBM through the
+// same data fabric as the CPU's -- that it is probed the same way is our reading, which the
+// self-test below checks).  So the L2s cannot hold a line older than a completed peer write;
+// what can be stale is a CU's vector L1, which every kernel start
+// invalidates (the dispatch's acquire), and the solve kernels start after the wait kernel has
+// seen the DONE flags (which each pusher raises after a system-scope release of its writes).
+// The system-scope fence at the end of the wait covers what the model leaves to software for
+// memory that is not local (peer-mapped flag words, uncached).  This is the hardware's
+// contract as documented, not something a one-GPU test can show, so the start-up self-test
+// (IpcAllGather.self_test) checks it where it matters: every XCD reads the whole destination
+// before each push round (ipc_xcd_probe: its L2 and L1 then hold the old lines) and compares it
+// with the reference after; any stale line fails the self-test and the exchange falls back to
+// RCCL.
 // Every wait is bounded (timeout_s, the 100 MHz real-time clock): a peer that never arrives
 // sets *err (1 + its rank) and the waiter gives up instead of hanging the GPU; the host checks
 // *err after the exchange (parallel/ipc.py) and falls back to RCCL.
@@ -112,9 +129,46 @@ __global__ __launch_bounds__(256) void ipc_wait_gathered(const unsigned* own_fla
   __threadfence_system();
 }
 
+// Coherence probe of the self-test: every workgroup reads the WHOLE buffer (16-byte units) and
+// counts units that differ from ref (out[0] +=), and records the XCD it ran on (out[1] |= 1 <<
+// XCC_ID): with enough workgroups every XCD's L2 (and its CUs' L1s) reads every line.  The
+// loads are plain loads on purpose -- the ones the solve kernels use.
+__global__ __launch_bounds__(256) void ipc_xcd_probe(const uint4* __restrict__ buf,
+                                                     const uint4* __restrict__ ref, long long n16,
+                                                     int* out) {
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) s_bad = 0;
+  __syncthreads();
+  int bad = 0;
+  for (long long i = threadIdx.x; i < n16; i += 256) {
+    const uint4 a = buf[i], b = ref[i];
+    bad += (a.x != b.x) | (a.y != b.y) | (a.z != b.z) | (a.w != b.w);
+  }
+  if (bad) atomicAdd(&s_bad, bad);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (s_bad) atomicAdd(out, s_bad);
+    atomicOr(out + 1, 1 << (xcc & 15));
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// out[0] += units of buf (n16 16-byte units) that differ from ref; out[1] |= the XCDs that read
+int oryx_ipc_xcd_probe(const void* buf, const void* ref, long long n16, int* out,
+                       void* stream) {
+  if (n16 <= 0) return ORYX_OK;
+  if ((reinterpret_cast<uintptr_t>(buf) & 15) || (reinterpret_cast<uintptr_t>(ref) & 15))
+    return ORYX_EINVAL;
+  hipLaunchKernelGGL(ipc_xcd_probe, dim3(64), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), static_cast<const uint4*>(buf),
+                     static_cast<const uint4*>(ref), n16, out);
+  return oryx_check_launch();
+}
 
 long long oryx_ipc_gather_flag_bytes() { return kFlagWords * 4; }
 

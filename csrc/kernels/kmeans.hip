@@ -1334,6 +1334,192 @@ __global__ __launch_bounds__(256) void km_silhouette_fin(
   if (tid == 0) partial[blockIdx.x] = red[0];
 }
 
+// MFMA silhouette (K10 on the matrix cores; SilhouetteCoefficient.java:52-77, :107-137): the
+// same per-point quantities as km_silhouette_part (the sum of distances to the point's own
+// cluster, the smallest mean distance to another one, per column range), with the pairwise
+// distances from d^2(i, j) = |x_i|^2 + |x_j|^2 - 2 x_i.x_j and the dot products on
+// v_mfma_f32_16x16x4_f32 (exact fp32 products and sums: the fmaf chain, bitwise) -- half the
+// arithmetic of the difference-square form, at the matrix-core rate.  The caller centres the
+// sample (distances unchanged, norms small: less cancellation) and pads rows to 4 KS floats.
+//
+// Workgroup: 4 waves x RS subtiles of 16 rows; a wave keeps its rows' whole coordinates in
+// registers (rf[r][kk], KS VGPRs per subtile: KS <= 64, d <= 256; RS = 3 at KS = 64 keeps them
+// in the 256 architectural VGPRs without spills) and streams 16-column tiles
+// of its column range through LDS (double-buffered, one barrier per tile).  The k index of the
+// 16x16x4 MFMA is the lane group g: step kk uses dimension g KS + kk, so each lane reads its
+// column's (and row's) dimensions contiguously (ds_read_b128).  Tile output, lane l: row i =
+// l % 16 of the subtile, columns 4 g .. 4 g + 3 of the tile (D' = columns x rows).  Epilogue per
+// tile: sqrt of the clamped d^2 (the point itself: 0), a lane-group reduction per distinct
+// column cluster of the tile (usually one: the sample is sorted by cluster), and a running fp64
+// per-cluster sum finalised when the column cluster changes.
+template <int KS, int RS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void
+km_silhouette_mfma(const float* __restrict__ x, const float* __restrict__ xn,
+                   const int* __restrict__ cl, const int* __restrict__ csize, int s,
+                   const int* __restrict__ bounds, double* __restrict__ a_part,
+                   double* __restrict__ b_part) {
+  constexpr int DP = 4 * KS;        // padded row length (floats)
+  constexpr int LS = DP + 4;        // LDS row stride: column rows 4 banks apart
+  constexpr int PF = KS / 16;       // float4 staging loads per thread per tile
+  __shared__ __attribute__((aligned(16))) float ct[2][16 * LS];
+  __shared__ float cn[2][16];
+  __shared__ int ccl[2][16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int row0 = blockIdx.x * (64 * RS) + wave * (16 * RS);
+  float rf[RS][KS];
+  float ni[RS];
+  int own[RS];
+  double a[RS], b[RS], cur_sum[RS];
+#pragma unroll
+  for (int r = 0; r < RS; ++r) {
+    const int i = row0 + 16 * r + li;
+    const f32x4* src = reinterpret_cast<const f32x4*>(x + (long long)i * DP + g * KS);
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) {
+      const f32x4 v = src[q];
+      rf[r][4 * q] = v[0];
+      rf[r][4 * q + 1] = v[1];
+      rf[r][4 * q + 2] = v[2];
+      rf[r][4 * q + 3] = v[3];
+    }
+    ni[r] = xn[i];
+    own[r] = i < s ? cl[i] : -1;
+    a[r] = 0.0;
+    b[r] = INFINITY;
+    cur_sum[r] = 0.0;
+  }
+  int cur = -1;
+  auto finish = [&](int c) {
+    if (c < 0) return;
+    const double inv = 1.0 / (double)csize[c];
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+      if (c == own[r]) {
+        a[r] = cur_sum[r];
+      } else {
+        const double m = cur_sum[r] * inv;
+        b[r] = m < b[r] ? m : b[r];
+      }
+      cur_sum[r] = 0.0;
+    }
+  };
+  const int c0 = bounds[blockIdx.y], c1 = bounds[blockIdx.y + 1];
+  const int nt = (c1 - c0 + 15) / 16;
+  // staging: thread (column sc = tid / 16, part sp = tid % 16) moves PF float4s of the column
+  const int sc = tid >> 4, sp = tid & 15;
+  f32x4 pf[PF];
+  auto fetch = [&](int t) {
+    const int j = c0 + 16 * t + sc;
+    const int jj = j < s ? j : s - 1;     // columns past the range: loaded, never counted
+    const f32x4* src = reinterpret_cast<const f32x4*>(x + (long long)jj * DP + sp * (DP / 16));
+#pragma unroll
+    for (int q = 0; q < PF; ++q) pf[q] = src[q];
+  };
+  auto stage = [&](int t, int buf) {
+    f32x4* dst = reinterpret_cast<f32x4*>(&ct[buf][sc * LS + sp * (DP / 16)]);
+#pragma unroll
+    for (int q = 0; q < PF; ++q) dst[q] = pf[q];
+    if (tid < 16) {
+      const int j = c0 + 16 * t + tid;
+      const bool in = j < c1;
+      cn[buf][tid] = in ? xn[j] : 0.f;
+      ccl[buf][tid] = in ? cl[j] : -1;
+    }
+  };
+  if (nt > 0) {
+    fetch(0);
+    stage(0, 0);
+  }
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nt) fetch(t + 1);
+    f32x4 acc[RS];
+#pragma unroll
+    for (int r = 0; r < RS; ++r) acc[r] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4* cb = reinterpret_cast<const f32x4*>(&ct[buf][li * LS + g * KS]);
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) {
+      const f32x4 cv = cb[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int r = 0; r < RS; ++r)
+          acc[r] = __builtin_amdgcn_mfma_f32_16x16x4f32(cv[e], rf[r][4 * q + e], acc[r], 0, 0,
+                                                        0);
+    }
+    // distances of this lane's (row, column) pairs
+    const int jt = c0 + 16 * t;
+    float v[RS][4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float nj = cn[buf][4 * g + e];
+      const int j = jt + 4 * g + e;
+#pragma unroll
+      for (int r = 0; r < RS; ++r) {
+        const float d2 = fmaf(-2.f, acc[r][e], ni[r] + nj);
+        const float dv = sqrtf(d2 > 0.f ? d2 : 0.f);
+        v[r][e] = j == row0 + 16 * r + li ? 0.f : dv;
+      }
+    }
+    const int cfirst = ccl[buf][0], clast = ccl[buf][15];
+    if (cfirst == clast && cfirst >= 0) {
+      // the whole tile in one cluster (the common case)
+      if (cfirst != cur) {
+        finish(cur);
+        cur = cfirst;
+      }
+#pragma unroll
+      for (int r = 0; r < RS; ++r) {
+        float p = (v[r][0] + v[r][1]) + (v[r][2] + v[r][3]);
+        p += __shfl_xor(p, 16, 64);
+        p += __shfl_xor(p, 32, 64);
+        cur_sum[r] += (double)p;
+      }
+    } else {
+      // a cluster boundary inside the tile: each run of equal column clusters in order
+      int pos = 0;
+      while (pos < 16) {
+        const int cc = ccl[buf][pos];
+        if (cc < 0) break;                 // past the range's end
+        int end = pos + 1;
+        while (end < 16 && ccl[buf][end] == cc) ++end;
+        if (cc != cur) {
+          finish(cur);
+          cur = cc;
+        }
+#pragma unroll
+        for (int r = 0; r < RS; ++r) {
+          float p = 0.f;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = 4 * g + e;
+            p += (m >= pos && m < end) ? v[r][e] : 0.f;
+          }
+          p += __shfl_xor(p, 16, 64);
+          p += __shfl_xor(p, 32, 64);
+          cur_sum[r] += (double)p;
+        }
+        pos = end;
+      }
+    }
+    if (t + 1 < nt) stage(t + 1, buf ^ 1);
+    __syncthreads();
+  }
+  finish(cur);
+  if (g == 0) {
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+      const int i = row0 + 16 * r + li;
+      if (i < s) {
+        a_part[(long long)blockIdx.y * s + i] = a[r];
+        b_part[(long long)blockIdx.y * s + i] = b[r];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 
@@ -1780,6 +1966,51 @@ int oryx_kmeans_silhouette(const float* x, const float* xT, const int* cl, const
   double* b_part = work + (long long)nsplit * s;
   hipLaunchKernelGGL(km_silhouette_part, dim3(rb, (unsigned)nsplit), dim3(256), 0, st, x, xT,
                      cl, csize, s, d, bounds, a_part, b_part);
+  hipLaunchKernelGGL(km_silhouette_fin, dim3(rb), dim3(256), 0, st, cl, csize, s, nsplit,
+                     a_part, b_part, partial);
+  return oryx_check_launch();
+}
+
+
+// Rows per workgroup of the MFMA form (the padding unit of its input).
+static int sil_rs64() {
+  // 16-row subtiles per wave at ks = 64: 3 (192 VGPRs of coordinates, a few spills) or 2
+  // (ORYX_KM_SIL_RS=2: no spills, twice the column traffic per row)
+  static const int rs = getenv("ORYX_KM_SIL_RS") && atoi(getenv("ORYX_KM_SIL_RS")) == 2 ? 2 : 3;
+  return rs;
+}
+
+int oryx_kmeans_silhouette_mfma_rows(int ks) { return ks == 64 ? 64 * sil_rs64() : 256; }
+
+// The MFMA form (km_silhouette_mfma): xp [rows padded to oryx_kmeans_silhouette_mfma_rows][4 ks]
+// fp32 of the CENTRED sample sorted by cluster (padding rows and dimensions past d zero), xn
+// [same rows] squared norms; ks in {16, 32, 64} (d <= 4 ks); the rest as
+// oryx_kmeans_silhouette.
+int oryx_kmeans_silhouette_mfma(const float* xp, const float* xn, const int* cl,
+                                const int* csize, int s, int ks, const int* bounds, int nsplit,
+                                double* work, double* partial, void* stream) {
+  if (s <= 0) return ORYX_OK;
+  if (nsplit <= 0 || nsplit > 65535 || (ks != 16 && ks != 32 && ks != 64) ||
+      (reinterpret_cast<unsigned long long>(xp) & 15))
+    return ORYX_EINVAL;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  double* a_part = work;
+  double* b_part = work + (long long)nsplit * s;
+  const unsigned rows = (unsigned)oryx_kmeans_silhouette_mfma_rows(ks);
+  const dim3 grid((unsigned)((s + rows - 1) / rows), (unsigned)nsplit);
+  if (ks == 16)
+    hipLaunchKernelGGL((km_silhouette_mfma<16, 4>), grid, dim3(256), 0, st, xp, xn, cl, csize,
+                       s, bounds, a_part, b_part);
+  else if (ks == 32)
+    hipLaunchKernelGGL((km_silhouette_mfma<32, 4>), grid, dim3(256), 0, st, xp, xn, cl, csize,
+                       s, bounds, a_part, b_part);
+  else if (sil_rs64() == 2)
+    hipLaunchKernelGGL((km_silhouette_mfma<64, 2>), grid, dim3(256), 0, st, xp, xn, cl, csize,
+                       s, bounds, a_part, b_part);
+  else
+    hipLaunchKernelGGL((km_silhouette_mfma<64, 3>), grid, dim3(256), 0, st, xp, xn, cl, csize,
+                       s, bounds, a_part, b_part);
+  const unsigned rb = (unsigned)((s + 255) / 256);
   hipLaunchKernelGGL(km_silhouette_fin, dim3(rb), dim3(256), 0, st, cl, csize, s, nsplit,
                      a_part, b_part, partial);
   return oryx_check_launch();

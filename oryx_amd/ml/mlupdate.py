@@ -127,6 +127,19 @@ class MLUpdate(BatchLayerUpdate):
     def run_update(self, context, timestamp: int, new_data: Dataset,
                    past_data: Optional[Dataset], model_dir: str,
                    model_update_topic: Optional[TopicProducer]) -> None:
+        try:
+            self._run_update(context, timestamp, new_data, past_data, model_dir,
+                             model_update_topic)
+        finally:
+            # files an app writes in the background (ALS factor parts) are complete before
+            # the generation ends, whatever path it took
+            join = getattr(self, "join_files", None)
+            if join is not None:
+                join()
+
+    def _run_update(self, context, timestamp: int, new_data: Dataset,
+                    past_data: Optional[Dataset], model_dir: str,
+                    model_update_topic: Optional[TopicProducer]) -> None:
         if new_data is None:
             raise ValueError("new_data is required")
         # candidate path -> (PMML document, its serialized text) of the models this process

@@ -236,9 +236,61 @@ def write_features(path: str, ids, mat, part: int = 0) -> None:
     :class:`~oryx_amd.ops.textfmt.RowText`.  Lines are assembled and compressed natively
     (multi-member gzip, one member per slice, threads)."""
     os.makedirs(path, exist_ok=True)
+    _write_features_to(os.path.join(path, "part-%05d.gz" % part), ids, mat)
+
+
+def _write_features_to(target: str, ids, mat) -> None:
     rows = mat if isinstance(mat, textfmt.RowText) else textfmt.format_rows(mat)
     block = ingest.assemble_row_messages("", ids if isinstance(ids, tuple) else list(ids), rows)
-    ingest.write_gzip(os.path.join(path, "part-%05d.gz" % part), block.buf, level=1)
+    ingest.write_gzip(target, block.buf, level=1)
+
+
+class _FactorFilesWriter:
+    """The ``X/`` and ``Y/`` part files written on a background thread while the generation
+    goes on (publishing the MODEL and the UP rows, which read nothing from them).  The part
+    files are created -- and held open -- before the thread starts and written through their
+    descriptors (``/proc/self/fd``), so promoting the candidate directory (a rename) under the
+    writer moves them along; :meth:`join` waits and re-raises.  Reference: the model's X/ Y/
+    are saved before the updates are published (``ALSUpdate.java:194-230``); here the bytes
+    land in the same files, overlapped with the publish."""
+
+    def __init__(self, jobs):
+        import threading
+        self._fds = []
+        targets = []
+        for path, ids, rows in jobs:
+            os.makedirs(path, exist_ok=True)
+            fd = os.open(os.path.join(path, "part-00000.gz"),
+                         os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+            self._fds.append(fd)
+            targets.append(("/proc/self/fd/%d" % fd, ids, rows))
+        self.error: Optional[BaseException] = None
+        self.seconds = 0.0
+
+        def run():
+            t0 = time.perf_counter()
+            try:
+                for target, ids, rows in targets:
+                    _write_features_to(target, ids, rows)
+            except BaseException as e:   # noqa: BLE001 -- re-raised by join
+                self.error = e
+            finally:
+                self.seconds = time.perf_counter() - t0
+        self._t = threading.Thread(target=run, name="oryx-als-factor-files", daemon=True)
+        self._t.start()
+
+    def join(self) -> None:
+        self._t.join()
+        for fd in self._fds:
+            os.close(fd)
+        self._fds = []
+        if self.error is not None:
+            err, self.error = self.error, None
+            raise err
+
+
+_BACKGROUND_FACTOR_FILES = os.environ.get("ORYX_ALS_BACKGROUND_FILES", "1") != "0" and \
+    os.path.isdir("/proc/self/fd")
 
 
 def read_features(path: str) -> Tuple[List[str], np.ndarray]:
@@ -378,6 +430,7 @@ class ALSUpdate(MLUpdate):
         # the build's undecayed parse of the complete data set, reused by the publish step
         self._raw_parse: Optional[dict] = None
         self._timings: Dict[str, dict] = {}
+        self._writers: List[_FactorFilesWriter] = []     # factor files written in background
         # resident parse of past part files across generations (oryx.als.resident-history,
         # default on; models/als/history.py)
         rh = cfg.get_optional_bool(config, "oryx.als.resident-history")
@@ -607,8 +660,14 @@ class ALSUpdate(MLUpdate):
         # messages take them as (blob, ends): no Python string is encoded again)
         x_blob = users.keys_blob(np.ascontiguousarray(used_u, dtype=np.int64))
         y_blob = items.keys_blob(np.ascontiguousarray(used_i, dtype=np.int64))
-        write_features(os.path.join(candidate_path, "X"), x_blob, x_rows)
-        write_features(os.path.join(candidate_path, "Y"), y_blob, y_rows)
+        jobs = [(os.path.join(candidate_path, "X"), x_blob, x_rows),
+                (os.path.join(candidate_path, "Y"), y_blob, y_rows)]
+        if _BACKGROUND_FACTOR_FILES:
+            # written beside the rest of the generation (joined at its end: join_files)
+            self._writers.append(_FactorFilesWriter(jobs))
+        else:
+            for path, ids, rows in jobs:
+                write_features(path, ids, rows)
         ph["write_factors"] = ph.get("write_factors", 0.0) + time.perf_counter() - tp
         tp = time.perf_counter()
         pmml = pmmlu.build_skeleton_pmml()
@@ -761,6 +820,26 @@ class ALSUpdate(MLUpdate):
             self._cache.clear()
             self._raw_parse = None
             self._split_test = None
+        self.join_files()
+
+    def join_files(self) -> None:
+        """Wait for the factor part files written in the background (every candidate's);
+        re-raises a writer's error.  The generation ends only once its files are complete."""
+        tp = time.perf_counter()
+        writers, self._writers = self._writers, []
+        err = None
+        for w in writers:
+            try:
+                w.join()
+            except BaseException as e:   # noqa: BLE001 -- after every writer has finished
+                err = err or e
+            self.phase_seconds["write_factors_total"] = \
+                self.phase_seconds.get("write_factors_total", 0.0) + w.seconds
+        if writers:
+            self.phase_seconds["write_factors_wait"] = \
+                self.phase_seconds.get("write_factors_wait", 0.0) + time.perf_counter() - tp
+        if err is not None:
+            raise err
 
     def _published_rows(self, pmml, model_parent_path):
         """(x_ids, X rows text, y_ids, Y rows text) of the promoted model: from the build's

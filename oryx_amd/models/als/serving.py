@@ -20,6 +20,7 @@ Equivalent of ``ALSServingModel`` / ``ALSServingModelManager`` / ``LocalitySensi
 
 from __future__ import annotations
 
+import collections
 import logging
 import math
 import threading
@@ -801,6 +802,9 @@ class ALSServingModelManager(AbstractServingModelManager):
             avail = torch.cuda.device_count()
             self.scan_devices = [torch.device("cuda", j % avail) for j in range(ng)]
         self.model: Optional[ALSServingModel] = None
+        # the last UP applications: (wall-clock start, ms, rows) -- what a latency record
+        # correlates its slow requests with (bench_traffic.py)
+        self.apply_log = collections.deque(maxlen=1024)
 
     def consume(self, updates: Iterator[KeyMessage], context=None) -> None:
         countdown = 10000
@@ -816,10 +820,13 @@ class ALSServingModelManager(AbstractServingModelManager):
                     # a run of UP rows already fetched: one native parse, bulk row updates
                     # the decoded UP rows already fetched, then the rest of the run parsed
                     # natively from the log buffer
+                    t_wall, t0 = time.time(), time.perf_counter()
                     batch = [message] + [m.message for m in take(lambda m: m.key == "UP",
                                                                  poll=False)]
                     apply_up_batch(self.model, batch)
-                    countdown -= len(batch) + drain_up_blocks(self.model, updates)
+                    n_up = len(batch) + drain_up_blocks(self.model, updates)
+                    self.apply_log.append((t_wall, (time.perf_counter() - t0) * 1e3, n_up))
+                    countdown -= n_up
                     if countdown <= 0:
                         log.info("%s", self.model)
                         countdown = 10000

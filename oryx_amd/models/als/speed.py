@@ -201,6 +201,25 @@ class ALSSpeedModel(SpeedModel):
             return None
         return invs[0], invs[1]
 
+    def warm(self) -> float:
+        """Build what the first micro-batch would otherwise build under traffic: both stores'
+        native id -> row maps (a 20M-ID store takes seconds), their device mirrors, the
+        Gramians and their inverses.  Called by the manager's consumer once the model is
+        completely loaded (and again after each new MODEL has loaded); later writes are kept
+        current incrementally (row-map journal, dirty rows, rank-one Gramian corrections).
+        Returns the seconds taken."""
+        import time
+        t0 = time.perf_counter()
+        self.X.synced_rowmap()
+        self.Y.synced_rowmap()
+        if self.device is not None and self.device.type == "cuda" and \
+                self.X.size() and self.Y.size():
+            try:
+                self.solver_inverses()
+            except mathx.SingularMatrixSolverException:
+                pass           # the interval reports it, as it would have
+        return time.perf_counter() - t0
+
     def get_fraction_loaded(self) -> float:
         with self._lock:
             expected = len(self._expected_users) + len(self._expected_items)
@@ -225,6 +244,8 @@ class ALSSpeedModelManager(SpeedModelManager):
         self._stream = None
         self._dicts = None
         self._batch = None     # ingest.SpeedBatch of the GPU path (reused)
+        self._warmed = None    # the model last warmed (ALSSpeedModel.warm) once loaded
+        self.warm_s: Optional[float] = None
         # milliseconds per phase of the last build_updates (parse_aggregate, inverses, lookup
         # of the batch's IDs in the stores, foldin = kernel + validity flags to the host,
         # format_rows = GPU row text + copy, assemble = native UP message assembly)
@@ -249,6 +270,7 @@ class ALSSpeedModelManager(SpeedModelManager):
                     if countdown <= 0:
                         log.info("%s", self.model)
                         countdown = 10000
+                    self._maybe_warm()
                     continue
                 update = text.read_json(message)
                 id_ = str(update[1])
@@ -263,6 +285,7 @@ class ALSSpeedModelManager(SpeedModelManager):
                 if countdown <= 0:
                     log.info("%s", self.model)
                     countdown = 10000
+                self._maybe_warm()
             elif key in ("MODEL", "MODEL-REF"):
                 log.info("Loading new model")
                 pmml = pmmlu.read_pmml_from_update_key_message(key, message)
@@ -275,12 +298,25 @@ class ALSSpeedModelManager(SpeedModelManager):
                 yids = set(pmml.get_extension_content("YIDs") or [])
                 self.model.retain_recent_and_user_ids(xids)
                 self.model.retain_recent_and_item_ids(yids)
+                self._warmed = None        # warm again once this model has loaded
                 # the loop frame outlives this message: drop the ID sets (20M strings in
                 # a set stay in every gen-2 GC walk until the next model otherwise)
                 del xids, yids, pmml
                 log.info("Model updated: %s", self.model)
             else:
                 raise ValueError("Bad message: %r" % (km,))
+
+    def _maybe_warm(self) -> None:
+        """Warm the model on this (consumer) thread once it has completely loaded: the first
+        micro-batch after a load otherwise built the 20M-entry row maps and the device
+        mirrors itself -- a 5 s interval under traffic at 20M x 250
+        (profiles/r5_traffic_20m_250_*_v4.json)."""
+        m = self.model
+        if m is None or self._warmed is m or m.get_fraction_loaded() < 1.0:
+            return
+        self._warmed = m
+        self.warm_s = m.warm()
+        log.info("Speed model warmed in %.2fs", self.warm_s)
 
     def _device_stream(self, device):
         if device.type != "cuda":

@@ -21,6 +21,7 @@ probability everywhere) and gathered, and rank 0's value is broadcast.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -186,19 +187,41 @@ def silhouette_coefficient(clusters, data, device=None, max_sample: int = MAX_SA
     return float(total) / s
 
 
+_SIL_MFMA = os.environ.get("ORYX_KM_SIL_MFMA", "1") != "0"
+
+
 def _silhouette_kernel(x: torch.Tensor, idx: torch.Tensor, k: int) -> float:
-    """Mean silhouette on the GPU (``km_silhouette``: sample sorted by cluster, one pass of
-    streamed distances per point with running per-cluster sums)."""
+    """Mean silhouette on the GPU: the sample sorted by cluster, one pass over the columns
+    per row block with running per-cluster sums.  Dimensions <= 256: the distances come from
+    fp32 MFMA dot products of the centred sample (``km_silhouette_mfma``); wider samples (or
+    ``ORYX_KM_SIL_MFMA=0``) stream packed fp32 differences on the VALU
+    (``km_silhouette_part``)."""
     from ... import native
     lib = native.require_kernels()
     s, d = x.shape
     order = torch.argsort(idx, stable=True)
-    xs = x[order].to(torch.float32).contiguous()
-    xt = xs.t().contiguous()
     cl = idx[order].to(torch.int32).contiguous()
     size = torch.bincount(idx.long(), minlength=k).to(torch.int32)
+    mfma = _SIL_MFMA and d <= 256
+    if mfma:
+        ks = 16 if d <= 64 else (32 if d <= 128 else 64)
+        rows = int(lib.oryx_kmeans_silhouette_mfma_rows(ks))
+        sp = -(-s // rows) * rows
+        # centred in fp64 (distances unchanged; small norms: less cancellation in
+        # |a|^2 + |b|^2 - 2 a.b), rows and dimensions zero-padded to the kernel's tiles
+        xc = x[order].to(torch.float64)
+        xc = xc - xc.mean(0, keepdim=True)
+        xp = torch.zeros((sp, 4 * ks), dtype=torch.float32, device=x.device)
+        xp[:s, :d] = xc.to(torch.float32)
+        xn = torch.zeros(sp, dtype=torch.float32, device=x.device)
+        xn[:s] = xp[:s].to(torch.float64).pow(2).sum(1).to(torch.float32)
+        del xc
+        row_blocks = sp // rows
+    else:
+        xs = x[order].to(torch.float32).contiguous()
+        xt = xs.t().contiguous()
+        row_blocks = (s + 255) // 256
     # column ranges at cluster boundaries, enough of them for >= ~2048 blocks
-    row_blocks = (s + 255) // 256
     want = max(1, min(64, -(-2048 // row_blocks)))
     starts = np.concatenate([[0], np.cumsum(size.cpu().numpy().astype(np.int64))])
     cuts = np.unique(starts[np.searchsorted(starts, np.arange(1, want) * s / want)])
@@ -206,12 +229,19 @@ def _silhouette_kernel(x: torch.Tensor, idx: torch.Tensor, k: int) -> float:
     nsplit = len(bounds) - 1
     d_bounds = torch.from_numpy(bounds.astype(np.int32)).to(x.device)
     work = torch.empty(2 * nsplit * s, dtype=torch.float64, device=x.device)
-    partial = torch.empty(row_blocks, dtype=torch.float64, device=x.device)
-    rc = lib.oryx_kmeans_silhouette(xs.data_ptr(), xt.data_ptr(), cl.data_ptr(),
-                                    size.data_ptr(), s, d, d_bounds.data_ptr(), nsplit,
-                                    work.data_ptr(), partial.data_ptr(),
-                                    native.stream_ptr(x.device))
-    native.check(rc, "oryx_kmeans_silhouette")
+    partial = torch.empty((s + 255) // 256, dtype=torch.float64, device=x.device)
+    if mfma:
+        rc = lib.oryx_kmeans_silhouette_mfma(xp.data_ptr(), xn.data_ptr(), cl.data_ptr(),
+                                             size.data_ptr(), s, ks, d_bounds.data_ptr(),
+                                             nsplit, work.data_ptr(), partial.data_ptr(),
+                                             native.stream_ptr(x.device))
+        native.check(rc, "oryx_kmeans_silhouette_mfma")
+    else:
+        rc = lib.oryx_kmeans_silhouette(xs.data_ptr(), xt.data_ptr(), cl.data_ptr(),
+                                        size.data_ptr(), s, d, d_bounds.data_ptr(), nsplit,
+                                        work.data_ptr(), partial.data_ptr(),
+                                        native.stream_ptr(x.device))
+        native.check(rc, "oryx_kmeans_silhouette")
     return float(partial.sum()) / s
 
 

@@ -277,6 +277,7 @@ def _load_kernels():
     _sig(lib, "oryx_csv_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp, c_i,
                                                 c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_vp, c_vp])
     # peer-push all-gather (ipc_allgather.hip; parallel/ipc.py IpcAllGather)
+    _sig(lib, "oryx_ipc_xcd_probe", c_i, [c_vp, c_vp, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_ipc_gather_flag_bytes", c_ll, [])
     _sig(lib, "oryx_ipc_gather_limits", c_i, [c_vp])
     _sig(lib, "oryx_ipc_handle_range", c_i, [c_vp, c_vp, c_vp])
@@ -296,6 +297,10 @@ def _load_kernels():
     _sig(lib, "oryx_kmeans_rescore_list", c_i, [c_vp, c_i, c_i, c_vp, c_i, c_vp, c_ll, c_vp,
                                                 c_vp, c_vp])
     # x, xT, cl, csize, s, d, partial, stream
+    _sig(lib, "oryx_kmeans_silhouette_mfma_rows", c_i, [c_i])
+    # xp, xn, cl, csize, s, ks, bounds, nsplit, work, partial, stream
+    _sig(lib, "oryx_kmeans_silhouette_mfma", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_vp, c_i,
+                                                   c_vp, c_vp, c_vp])
     _sig(lib, "oryx_kmeans_silhouette", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_i, c_vp, c_i, c_vp,
                                               c_vp, c_vp])
     # X, Y, k, xrow, yrow, vals, xinv, yinv, implicit, n, new_x, new_y, vx, vy, stream

@@ -156,8 +156,12 @@ def run_info(ctx: DistContext) -> dict:
         backend = tdist.get_backend()
     else:
         allv, ws, backend = [me], 1, None
-    return {"world_size": ws, "backend": backend, "ranks": allv,
-            "ipc_allreduce": ctx.ipc is not None, "allgather": allgather_kind(ctx)}
+    out = {"world_size": ws, "backend": backend, "ranks": allv,
+           "ipc_allreduce": ctx.ipc is not None, "allgather": allgather_kind(ctx)}
+    ag = ctx.ipc_gather
+    if ag is not None:
+        out["allgather_selftest"] = dict(getattr(ag, "self_test_info", {}))
+    return out
 
 
 def allgather_kind(ctx: DistContext) -> str:

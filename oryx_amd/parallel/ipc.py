@@ -192,6 +192,7 @@ class IpcAllGather:
         self.side = torch.cuda.Stream(device=ctx.device)
         self._mats = {}        # name -> dict(t, m, epoch, dst, opened)
         self.pushes = 0
+        self.self_test_info: dict = {}
 
     def _exchange(self, handle: bytes, offset: int, own_ptr: int) -> List[int]:
         """All ranks' (handle, offset) -> one pointer per rank (own one as is, peers' opened)."""
@@ -291,13 +292,23 @@ class IpcAllGather:
             self.err.zero_()
             raise RuntimeError("IPC all-gather: rank %d never arrived" % (e - 1))
 
+    def _probe(self, buf: torch.Tensor, ref: torch.Tensor, out: torch.Tensor) -> None:
+        native.check(self.lib.oryx_ipc_xcd_probe(
+            ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(ref.data_ptr()),
+            buf.numel() * buf.element_size() // 16, ctypes.c_void_p(out.data_ptr()),
+            ctypes.c_void_p(native.stream_ptr(self.ctx.device))), "oryx_ipc_xcd_probe")
+
     def self_test(self) -> bool:
         """Gather rank-dependent rows both ways (peer push and torch.distributed); True when
-        every rank matched bitwise.  Three exchanges into the same buffer, each compared after
-        it: the comparison reads pull the previous contents into this GPU's L2 caches, so a
-        wait that failed to drop them would show as a mismatch here (not as stale factors)."""
+        every rank matched bitwise.  Three exchanges into the same buffer.  Before each push
+        round every XCD reads the whole destination (``ipc_xcd_probe``: the old rows then sit in
+        every XCD's L2 and in CUs' L1s), and after the exchange every XCD reads it again and
+        compares it with the reference: a stale line anywhere fails the test (see the
+        coherence note in ``ipc_allgather.hip``).  The verdict is kept in
+        :attr:`self_test_info` (reported by ``bench.py``)."""
         ok = True
         name = "__selftest__"
+        info = {"rounds": 0, "stale_units": 0, "pre_mismatch_units": 0, "xcd_mask": 0}
         try:
             W, rows, cols = self.W, 1000, 64
             C = 3
@@ -305,16 +316,19 @@ class IpcAllGather:
             out = self.buffer(name, (C * W * cr, cols), torch.bfloat16)
             base = torch.arange(C * cr * cols, device=self.ctx.device, dtype=torch.float32)
             ref = torch.empty_like(out)
+            probe = torch.zeros(4, dtype=torch.int32, device=self.ctx.device)
             for rnd in range(3):
                 local = ((base % 251) * (self.rank + 1 + 7 * rnd) + self.rank - rnd) \
                     .to(torch.bfloat16).reshape(C * cr, cols)
+                if rnd > 0:
+                    # the previous round's rows, read through every XCD before the peers
+                    # overwrite them (probe[2]: the copy must still hold them)
+                    self._probe(out, ref, probe[2:4])
                 self.begin(name)
                 for c in range(C):
                     self.push(name, local[c * cr:(c + 1) * cr], (c * W + self.rank) * cr, C,
                               c)
                 self.end(name, C)
-                torch.cuda.synchronize(self.ctx.device)
-                self.check()
                 for c in range(C):
                     blk = local[c * cr:(c + 1) * cr].contiguous()
                     parts = list(ref[c * W * cr:(c + 1) * W * cr].chunk(W, 0))
@@ -322,14 +336,26 @@ class IpcAllGather:
                         tdist.all_gather(parts, blk, group=self.ctx.group)
                     else:
                         parts[0].copy_(blk)
+                self._probe(out, ref, probe[0:2])
+                torch.cuda.synchronize(self.ctx.device)
+                self.check()
                 ok = ok and bool(torch.equal(out.view(torch.int16), ref.view(torch.int16)))
+                info["rounds"] += 1
+            p = probe.cpu().tolist()
+            info.update(stale_units=p[0], pre_mismatch_units=p[2], xcd_mask=p[1] | p[3])
+            ok = ok and p[0] == 0 and p[2] == 0
         except Exception as e:   # noqa: BLE001 -- any failure disables the path
             log.warning("IPC all-gather self-test failed on rank %d: %s", self.rank, e)
+            info["error"] = str(e)
             ok = False
+        info["xcds_read"] = bin(int(info["xcd_mask"])).count("1")
         flag = torch.tensor([0 if ok else 1], dtype=torch.int32, device=self.ctx.device)
         if self.W > 1:
             tdist.all_reduce(flag, group=self.ctx.group)
-        return int(flag.item()) == 0
+        info["ok"] = int(flag.item()) == 0
+        info["ok_here"] = ok
+        self.self_test_info = info
+        return info["ok"]
 
     def close(self) -> None:
         # no push of this rank may still be writing through a mapping that is closed here

@@ -18,6 +18,8 @@
 #   kmeans[=PREC]       bench_kmeans.py --precision PREC (fp32)
 #   rdf                 bench_rdf.py
 #   serving[=ARGS]      bench_serving.py [ARGS]
+#   sil                 scripts/silhouette_probe.py (MFMA vs VALU silhouette, 100k x 256, k = 1000)
+#   traffic[=RATE]      bench_traffic.py 20M items x 250, LSH sample rate RATE (0.3), speed layer live
 #   prof=NAME:CMD       rocprofv3 --kernel-trace --stats of CMD (e.g. prof=als:bench.py,--steps,5)
 #   pmc=NAME:CTRS:CMD   one rocprofv3 --pmc pass (CTRS comma separated) of CMD
 #   env=K=V             export K=V for the following steps (env=K= unsets K)
@@ -81,6 +83,14 @@ for step in "$@"; do
       out=gpurun_out/bench_serving.jsonl
       timeout -k 10 1100 python -u bench_serving.py $(args "$val") > $out 2> $out.err || fail "$step" $out.err
       cut -c1-400 $out ;;
+    sil)
+      out=gpurun_out/silhouette${val:+_$(tag "$val")}.json
+      timeout -k 10 300 python -u scripts/silhouette_probe.py > $out 2> $out.err || fail "$step" $out.err
+      cat $out ;;
+    traffic)
+      out=gpurun_out/traffic_20m_250_lsh$(tag "${val:-0.3}").json
+      timeout -k 10 600 python -u bench_traffic.py --items 20000000 --users 500000 --features 250 --sample-rate ${val:-0.3} > $out 2> $out.err || fail "$step" $out.err
+      tail -1 $out | cut -c1-1500 ;;
     prof)
       pname=${val%%:*}; cmd=$(args "${val#*:}")
       rm -rf gpurun_out/prof_$pname

@@ -1,5 +1,5 @@
 """Per-half-step roofline table of the ALS solve kernels from the rocprofv3 passes of
-scripts/r5_roofline.sh (rank 64 bf16 c2, rank 128 fp32; 25M ratings, 162,541 users, 59,047
+scripts/archive/r5_roofline.sh (rank 64 bf16 c2, rank 128 fp32; 25M ratings, 162,541 users, 59,047
 items).  Writes profiles/r5_als_roofline.json and profiles/r5_als_roofline.md.
 
 Half-steps: the solve kernel's dispatches alternate items, users (MLlib order) from the first

@@ -157,6 +157,12 @@ def test_batch_layer_als_end_to_end(tmp_path):
                                           speed.manager.model.get_fraction_loaded() < 1.0):
             time.sleep(0.1)
         assert speed.manager.model is not None
+        # the consumer warmed the completely loaded model (row maps built off the interval)
+        while time.time() < deadline and speed.manager.warm_s is None:
+            time.sleep(0.05)
+        assert speed.manager.warm_s is not None
+        assert speed.manager.model.X._rowmap is not None
+        assert speed.manager.model.Y._rowmap is not None
         known_u = sorted(xids)[0]
         known_i = sorted(yids)[0]
         prod.send("x", "%s,%s,2,%d" % (known_u, known_i, int(time.time() * 1000)))

@@ -167,6 +167,7 @@ if ctx.is_main:
 else:
     res["joined"] = layer.run_follower()
 res["pushes"] = ctx.ipc_gather.pushes if ctx.ipc_gather is not None else 0
+res["selftest"] = ctx.ipc_gather.self_test_info if ctx.ipc_gather is not None else None
 with open(os.path.join(out_dir, "res%d.json" % R), "w") as fh:
     json.dump(res, fh)
 '''
@@ -306,6 +307,11 @@ def _run_worlds(tmp_path, device):
     # ---- peer-push all-gather: bitwise the gloo-staged exchange's results
     rp = json.loads((outs["push"] / "res0.json").read_text())
     assert rp["allgather"].startswith("ipc-push") and rp["pushes"] > 0, rp
+    # the start-up self-test read the destination through every XCD before and after each
+    # push round and found no stale line
+    st = rp["selftest"]
+    assert st["ok"] and st["rounds"] == 3 and st["stale_units"] == 0, st
+    assert st["xcds_read"] == 8, st
     assert not res2["allgather"].startswith("ipc-push"), res2
     for k, prec, _ in cases:
         a = torch.load(outs[2] / ("trainer_%d_%s.pt" % (k, prec)))
