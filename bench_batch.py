@@ -294,7 +294,8 @@ def main(argv=None) -> int:
     # the layer's own phases plus the update's (whose sum is the layer's "update" phase)
     lay = first_lay
     inner = sum(v for k, v in phases.items()
-                if not k.startswith("layer_") and k not in ("publish_y", "publish_x"))
+                if not k.startswith(("layer_", "pub_")) and
+                k not in ("publish_y", "publish_x", "write_factors_total"))
     # (save_data_total runs beside the update: only its exposed part, save_data, counts)
     attributed = inner + sum(v for k, v in lay.items() if k not in ("update", "save_data_total"))
     if ctx.is_main:

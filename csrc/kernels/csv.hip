@@ -159,6 +159,149 @@ __global__ __launch_bounds__(256) void csv_lines_kernel(const uint4* __restrict_
   }
 }
 
+// ALS rating lines "user,item[,strength[,timestamp]]" (ALSUpdate.parsedToRatingRDD,
+// [mllib]/als/ALSUpdate.java:260-290) on the GPU: one thread per line, the host parser's plain
+// CSV fast path (csrc/runtime/oryx_ingest.cpp parse_rating_fields) for lines whose user and
+// item IDs are canonical decimal keys below 2^24 (the dense-array keys of the host
+// dictionaries, numeric_key) -- out_u / out_i get the key VALUES (the caller numbers them in
+// first-appearance order, as the host dictionaries do).  Strength: 1 without the field, NaN
+// when it is empty, else the fast-path double (bitwise the host's); timestamp: default_ts
+// without the field or when it is empty, else up to 18 plain digits.  Fields past the fourth
+// are ignored, as on the host.  Any other line (an empty one, quotes, escapes, a JSON array,
+// a non-canonical key, another number form) is flagged in bad[] / *n_bad: the caller then
+// parses the whole range on the host.
+__device__ __forceinline__ bool rating_key(ByteReader& rd, long long& p, long long le, int& c,
+                                           int* v) {
+  // canonical decimal: 1..8 digits, no leading zero unless the key is "0", below 2^24
+  const long long q0 = p;
+  unsigned x = 0;
+  while ((unsigned)(c - '0') < 10u) {
+    x = x * 10 + (unsigned)(c - '0');
+    ++p;
+    c = p < le ? rd.at(p) : ',';
+    if (p - q0 > 8) return false;
+  }
+  const long long nd = p - q0;
+  if (nd == 0 || c != ',' || x >= (1u << 24)) return false;
+  if (nd > 1 && rd.at(q0) == '0') return false;
+  *v = (int)x;
+  return true;
+}
+
+__global__ __launch_bounds__(256) void rating_lines_kernel(
+    const uint4* __restrict__ buf, const long long* __restrict__ starts,
+    const long long* __restrict__ ends, long long n, long long default_ts,
+    int* __restrict__ out_u, int* __restrict__ out_i, double* __restrict__ out_s,
+    long long* __restrict__ out_ts, unsigned char* __restrict__ bad, int* n_bad) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (long long)gridDim.x * 256) {
+    ByteReader rd{buf};
+    long long p = starts[i];
+    long long le = ends[i];
+    if (le > p && rd.at(le - 1) == '\r') --le;
+    bool ok = le > p && rd.at(p) != '[';
+    // the host's fast path needs a line without quotes or backslashes anywhere
+    for (long long q = p; ok && q < le; ++q) {
+      const int ch = rd.at(q);
+      ok = ch != '"' && ch != '\\';
+    }
+    int uv = 0, iv = 0;
+    double sv = 1.0;
+    long long tv = default_ts;
+    int c = ok ? rd.at(p) : 0;
+    ok = ok && rating_key(rd, p, le, c, &uv);
+    if (ok) {
+      if (p >= le) {
+        ok = false;                          // no item field
+      } else {
+        ++p;
+        c = p < le ? rd.at(p) : ',';
+        ok = rating_key(rd, p, le, c, &iv);
+      }
+    }
+    if (ok && p < le) {
+      // strength: the third field
+      ++p;
+      c = p < le ? rd.at(p) : ',';
+      if (c == ',') {
+        sv = __builtin_nan("");
+      } else {
+        bool neg = false;
+        if (c == '-' || c == '+') {
+          neg = c == '-';
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+        }
+        unsigned long long D = 0;
+        int nd = 0, frac = 0;
+        while ((unsigned)(c - '0') < 10u) {
+          D = D * 10 + (unsigned long long)(c - '0');
+          ++nd;
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+        }
+        if (c == '.') {
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+          while ((unsigned)(c - '0') < 10u) {
+            D = D * 10 + (unsigned long long)(c - '0');
+            ++nd;
+            ++frac;
+            ++p;
+            c = p < le ? rd.at(p) : ',';
+          }
+        }
+        int e10 = -frac;
+        if (nd > 0 && (c == 'e' || c == 'E')) {
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+          bool eneg = false;
+          if (c == '-' || c == '+') {
+            eneg = c == '-';
+            ++p;
+            c = p < le ? rd.at(p) : ',';
+          }
+          int x = 0, ne = 0;
+          while ((unsigned)(c - '0') < 10u && ne < 4) {
+            x = x * 10 + (c - '0');
+            ++ne;
+            ++p;
+            c = p < le ? rd.at(p) : ',';
+          }
+          if (!ne) nd = 0;
+          e10 += eneg ? -x : x;
+        }
+        ok = nd > 0 && nd <= 19 && c == ',' && D <= (1ull << 53) && e10 >= -22 && e10 <= 22;
+        if (ok) {
+          const double v = e10 < 0 ? (double)D / kP10[-e10] : (double)D * kP10[e10];
+          sv = neg ? -v : v;
+        }
+      }
+      if (ok && p < le) {
+        // timestamp: the fourth field (up to the next comma; later fields are ignored)
+        ++p;
+        c = p < le ? rd.at(p) : ',';
+        long long t = 0;
+        int nd = 0;
+        while ((unsigned)(c - '0') < 10u && nd < 18) {
+          t = t * 10 + (c - '0');
+          ++nd;
+          ++p;
+          c = p < le ? rd.at(p) : ',';
+        }
+        if (c != ',') ok = false;            // another number form: the host parses it
+        else if (nd > 0) tv = t;
+      }
+    }
+    out_u[i] = uv;
+    out_i[i] = iv;
+    out_s[i] = sv;
+    out_ts[i] = tv;
+    bad[i] = ok ? 0 : 1;
+    if (!ok) atomicAdd(n_bad, 1);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -186,6 +329,21 @@ int oryx_csv_lines_to_matrix(const void* buf, const long long* starts, const lon
     hipLaunchKernelGGL(csv_lines_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
                        static_cast<const uint4*>(buf), starts, ends, n, F, is_num, out_col, P,
                        static_cast<float*>(out), span_off, span_len, S, bad, n_bad);
+  return oryx_check_launch();
+}
+
+// Rating lines (see rating_lines_kernel): buf padded as for oryx_csv_lines_to_matrix; per line
+// the user / item key values, strength, timestamp; bad[n] / *n_bad (zeroed by the caller).
+int oryx_rating_lines(const void* buf, const long long* starts, const long long* ends,
+                      long long n, long long default_ts, int* out_u, int* out_i, double* out_s,
+                      long long* out_ts, unsigned char* bad, int* n_bad, void* stream) {
+  if (n <= 0) return ORYX_OK;
+  if (reinterpret_cast<uintptr_t>(buf) & 15) return ORYX_EINVAL;
+  long long blocks = (n + 255) / 256;
+  if (blocks > 256LL * 64) blocks = 256LL * 64;
+  hipLaunchKernelGGL(rating_lines_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), static_cast<const uint4*>(buf),
+                     starts, ends, n, default_ts, out_u, out_i, out_s, out_ts, bad, n_bad);
   return oryx_check_launch();
 }
 

@@ -1343,8 +1343,9 @@ __global__ __launch_bounds__(256) void km_silhouette_fin(
 // sample (distances unchanged, norms small: less cancellation) and pads rows to 4 KS floats.
 //
 // Workgroup: 4 waves x RS subtiles of 16 rows; a wave keeps its rows' whole coordinates in
-// registers (rf[r][kk], KS VGPRs per subtile: KS <= 64, d <= 256; RS = 3 at KS = 64 keeps them
-// in the 256 architectural VGPRs without spills) and streams 16-column tiles
+// registers (rf[r][kk], KS VGPRs per subtile: KS <= 64, d <= 256; at KS = 64, RS = 2 fits two
+// waves per SIMD, 214 VGPRs, so one wave's epilogue hides under the other's MFMAs) and streams
+// 16-column tiles
 // of its column range through LDS (double-buffered, one barrier per tile).  The k index of the
 // 16x16x4 MFMA is the lane group g: step kk uses dimension g KS + kk, so each lane reads its
 // column's (and row's) dimensions contiguously (ds_read_b128).  Tile output, lane l: row i =
@@ -1352,8 +1353,8 @@ __global__ __launch_bounds__(256) void km_silhouette_fin(
 // tile: sqrt of the clamped d^2 (the point itself: 0), a lane-group reduction per distinct
 // column cluster of the tile (usually one: the sample is sorted by cluster), and a running fp64
 // per-cluster sum finalised when the column cluster changes.
-template <int KS, int RS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void
+template <int KS, int RS, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void
 km_silhouette_mfma(const float* __restrict__ x, const float* __restrict__ xn,
                    const int* __restrict__ cl, const int* __restrict__ csize, int s,
                    const int* __restrict__ bounds, double* __restrict__ a_part,
@@ -1974,13 +1975,17 @@ int oryx_kmeans_silhouette(const float* x, const float* xT, const int* cl, const
 
 // Rows per workgroup of the MFMA form (the padding unit of its input).
 static int sil_rs64() {
-  // 16-row subtiles per wave at ks = 64: 3 (192 VGPRs of coordinates, a few spills) or 2
-  // (ORYX_KM_SIL_RS=2: no spills, twice the column traffic per row)
-  static const int rs = getenv("ORYX_KM_SIL_RS") && atoi(getenv("ORYX_KM_SIL_RS")) == 2 ? 2 : 3;
-  return rs;
+  // 16-row subtiles per wave at ks = 64: 22 (the default: two subtiles, two waves per SIMD --
+  // one wave's epilogue and tile staging run under the other's MFMAs; 51.4 ms at 100k x 256,
+  // profiles/r6_silhouette_mfma_rs22_v1.json), 3 (ORYX_KM_SIL_RS=3: 192 VGPRs of coordinates,
+  // one wave per SIMD, 59.7 ms) or 2 (one wave per SIMD, 61.6 ms)
+  static const int rs = getenv("ORYX_KM_SIL_RS") ? atoi(getenv("ORYX_KM_SIL_RS")) : 22;
+  return rs == 2 || rs == 3 ? rs : 22;
 }
 
-int oryx_kmeans_silhouette_mfma_rows(int ks) { return ks == 64 ? 64 * sil_rs64() : 256; }
+int oryx_kmeans_silhouette_mfma_rows(int ks) {
+  return ks == 64 ? 64 * (sil_rs64() == 22 ? 2 : sil_rs64()) : 256;
+}
 
 // The MFMA form (km_silhouette_mfma): xp [rows padded to oryx_kmeans_silhouette_mfma_rows][4 ks]
 // fp32 of the CENTRED sample sorted by cluster (padding rows and dimensions past d zero), xn
@@ -2007,6 +2012,9 @@ int oryx_kmeans_silhouette_mfma(const float* xp, const float* xn, const int* cl,
   else if (sil_rs64() == 2)
     hipLaunchKernelGGL((km_silhouette_mfma<64, 2>), grid, dim3(256), 0, st, xp, xn, cl, csize,
                        s, bounds, a_part, b_part);
+  else if (sil_rs64() == 22)
+    hipLaunchKernelGGL((km_silhouette_mfma<64, 2, 2>), grid, dim3(256), 0, st, xp, xn, cl,
+                       csize, s, bounds, a_part, b_part);
   else
     hipLaunchKernelGGL((km_silhouette_mfma<64, 3>), grid, dim3(256), 0, st, xp, xn, cl, csize,
                        s, bounds, a_part, b_part);

@@ -306,6 +306,22 @@ long long oryx_dict_encode(void* dh, const char* buf, long long buf_len, int n, 
   return n;
 }
 
+// Encodes n canonical decimal keys given by value (each < 2^24: the dense-array keys of
+// numeric_key) in order -> codes: what encoding their decimal strings would do, without the
+// strings (the device rating parse numbers a segment's keys in first-appearance order and
+// hands them over here).  Returns n, or -1 for a value out of range.
+long long oryx_dict_encode_nums(void* dh, const int32_t* vals, long long n, long long* codes) {
+  Dict* d = static_cast<Dict*>(dh);
+  std::lock_guard<std::mutex> g(d->mu);
+  for (long long j = 0; j < n; ++j)
+    if (vals[j] < 0 || (uint32_t)vals[j] >= kNumLimit) return -1;
+  for (long long j = 0; j < n; ++j) {
+    const int64_t c = d->encode_num((uint32_t)vals[j]);
+    if (codes) codes[j] = c;
+  }
+  return n;
+}
+
 // Inserts every key of src (in src's code order) into dst; map_out[c] = dst code of src key c.
 // Merging per-segment dictionaries in segment order reproduces the codes a single parse of the
 // concatenated segments assigns (first appearance order).  Returns src's size.

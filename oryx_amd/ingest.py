@@ -60,6 +60,18 @@ class IdDict:
                                    out.ctypes.data_as(ctypes.c_void_p))
         return out
 
+    def encode_nums(self, values) -> np.ndarray:
+        """Encode canonical decimal keys given as int values (< 2^24) in order: the same codes
+        as encoding ``[str(v) for v in values]``, without building the strings."""
+        vals = np.ascontiguousarray(values, dtype=np.int32)
+        out = np.empty(len(vals), dtype=np.int64)
+        vp = ctypes.c_void_p
+        rc = self._lib.oryx_dict_encode_nums(self._h, vals.ctypes.data_as(vp), len(vals),
+                                             out.ctypes.data_as(vp))
+        if rc < 0:
+            raise ValueError("numeric key out of range")
+        return out
+
     def merge_from(self, other: "IdDict") -> np.ndarray:
         """Insert ``other``'s keys (in its code order); returns the codes they have here."""
         out = np.empty(len(other), dtype=np.int64)

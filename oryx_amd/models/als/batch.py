@@ -191,12 +191,26 @@ _NO_TS = -(1 << 62)     # parse marker of a line without a timestamp
 def parse_ratings(lines: Sequence[str], users: ingest.IdDict, items: ingest.IdDict,
                   decay_factor: float = 1.0, zero_threshold: float = 0.0,
                   now_ms: Optional[int] = None, raw_out: Optional[list] = None,
-                  history: Optional[RatingsHistory] = None):
+                  history: Optional[RatingsHistory] = None, device_out: bool = False):
     """Parse + decay + zero-threshold.  ``raw_out`` (a list) receives the undecayed parse
     with lines lacking a timestamp at 0 -- what :func:`known_items_json_parsed` needs -- so
     the publish step can skip a second parse of the same data.  ``history``: reuse the parse
-    of past part files seen in earlier generations (:mod:`.history`; same results)."""
+    of past part files seen in earlier generations (:mod:`.history`; same results).
+    ``device_out`` (with a GPU history, no time decay): the columns stay device tensors."""
     now = int(time.time() * 1000) if now_ms is None else now_ms
+    if device_out and history is not None and history.device.type == "cuda" and \
+            decay_factor >= 1.0:
+        # (decay keeps the host path: np.power is the reference's arithmetic)
+        u, i, s, ts0 = history.parse_ratings(lines, users, items, default_ts=_NO_TS,
+                                             device_out=True)
+        missing = ts0 == _NO_TS
+        if raw_out is not None:
+            raw_out.extend([u, i, s, torch.where(missing, torch.zeros_like(ts0), ts0)])
+        ts = torch.where(missing, torch.full_like(ts0, now), ts0)
+        if zero_threshold > 0.0:
+            keep = s > zero_threshold
+            u, i, s, ts = u[keep], i[keep], s[keep], ts[keep]
+        return u, i, s, ts
     parse = history.parse_ratings if history is not None else ingest.parse_ratings
     if raw_out is not None:
         u, i, s, ts0 = parse(lines, users, items, default_ts=_NO_TS)
@@ -243,6 +257,28 @@ def _write_features_to(target: str, ids, mat) -> None:
     rows = mat if isinstance(mat, textfmt.RowText) else textfmt.format_rows(mat)
     block = ingest.assemble_row_messages("", ids if isinstance(ids, tuple) else list(ids), rows)
     ingest.write_gzip(target, block.buf, level=1)
+
+
+class _Sender:
+    """One ``send_block`` on a helper thread (the native append releases the GIL)."""
+
+    def __init__(self, topic, block):
+        import threading
+        self.error: Optional[BaseException] = None
+
+        def run():
+            try:
+                topic.send_block("UP", block)
+            except BaseException as e:   # noqa: BLE001 -- re-raised by join
+                self.error = e
+        self._t = threading.Thread(target=run, name="oryx-als-send-y", daemon=True)
+        self._t.start()
+
+    def join(self, raise_error: bool = True) -> None:
+        self._t.join()
+        if raise_error and self.error is not None:
+            err, self.error = self.error, None
+            raise err
 
 
 class _FactorFilesWriter:
@@ -513,6 +549,12 @@ class ALSUpdate(MLUpdate):
         tu, ti, tsv, tts = ingest.parse_ratings(test, users, items, default_ts=_NO_TS)
         tts = np.where(tts == _NO_TS, 0, tts)
         u, i, sv, ts = m["arrays"]
+        if isinstance(u, torch.Tensor):
+            # the training parse stayed on the device (parse_ratings device_out)
+            dv = u.device
+            up = lambda a, like: torch.from_numpy(np.ascontiguousarray(a)).to(dv, like.dtype)
+            return (users, items, torch.cat([u, up(tu, u)]), torch.cat([i, up(ti, i)]),
+                    torch.cat([sv, up(tsv, sv)]), torch.cat([ts, up(tts, ts)]))
         return (users, items, np.concatenate([u, tu]), np.concatenate([i, ti]),
                 np.concatenate([sv, tsv]), np.concatenate([ts, tts]))
 
@@ -550,7 +592,8 @@ class ALSUpdate(MLUpdate):
         u, i, s, ts = parse_ratings(train_data, users, items, self.decay_factor,
                                     self.decay_zero_threshold, raw_out=self._raw_parse_slot(
                                         train_data, users, items),
-                                    history=self._history_for(self._ctx(context).device))
+                                    history=self._history_for(self._ctx(context).device),
+                                    device_out=self._ctx(context).device.type == "cuda")
         ph["parse"] = ph.get("parse", 0.0) + time.perf_counter() - tp
         tp = time.perf_counter()
         dev = self._ctx(context).device
@@ -861,15 +904,44 @@ class ALSUpdate(MLUpdate):
         def count(ids):
             return len(ids[1]) if isinstance(ids, tuple) else len(ids)
 
+        ph = self.phase_seconds
+
+        def lap(name, t0):
+            ph["pub_" + name] = ph.get("pub_" + name, 0.0) + time.perf_counter() - t0
+            return time.perf_counter()
+
+        tp = time.perf_counter()
         log.info("Sending item / Y data as model updates")
+        y_send = None
         if count(y_ids):
-            model_update_topic.send_block("UP", ingest.assemble_row_messages("Y", y_ids, y_text))
+            y_block = ingest.assemble_row_messages("Y", y_ids, y_text)
+            tp = lap("assemble_y", tp)
+            if self.no_known_items or not count(x_ids):
+                model_update_topic.send_block("UP", y_block)
+                tp = lap("send_y", tp)
+            else:
+                # the Y block goes to the log on a helper thread while the known items are
+                # computed (device sorts, native text); it is appended before the X block
+                y_send = _Sender(model_update_topic, y_block)
         log.info("Sending user / X data as model updates")
         if not count(x_ids):
             return
         if self.no_known_items:
             model_update_topic.send_block("UP", ingest.assemble_row_messages("X", x_ids, x_text))
+            lap("send_x", tp)
             return
+        try:
+            self._publish_x_known(all_data, users_x=(x_ids, x_text), topic=model_update_topic,
+                                  y_send=y_send, lap=lap)
+        finally:
+            if y_send is not None:
+                y_send.join(raise_error=False)
+
+    def _publish_x_known(self, all_data, users_x, topic, y_send, lap):
+        """The X rows with each user's known items (see :meth:`_publish_local`)."""
+        x_ids, x_text = users_x
+        model_update_topic = topic
+        tp = time.perf_counter()
         parsed = self._known_items_parse(all_data)
         dev = self.dist_ctx.device if self.dist_ctx is not None else None
         if parsed is None:
@@ -879,7 +951,10 @@ class ALSUpdate(MLUpdate):
             parsed = (users, items) + tuple(parse(all_data, users, items, default_ts=0))
         users = parsed[0]
         known, present = known_items_spans(*parsed, device=dev)
+        tp = lap("known_items", tp)
         if known is None:
+            if y_send is not None:
+                y_send.join()
             return
         # join: users without any event are not sent
         n_u = len(present)
@@ -893,8 +968,13 @@ class ALSUpdate(MLUpdate):
         ok = code < n_u
         ok[ok] = present[code[ok]]
         kidx = np.where(ok, code, -1)
-        model_update_topic.send_block("UP", ingest.assemble_row_messages("X", x_ids, x_text,
-                                                                         known, kidx))
+        x_block = ingest.assemble_row_messages("X", x_ids, x_text, known, kidx)
+        tp = lap("assemble_x", tp)
+        if y_send is not None:
+            y_send.join()                 # Y rows first, as the reference publishes them
+            tp = lap("wait_y", tp)
+        model_update_topic.send_block("UP", x_block)
+        lap("send_x", tp)
 
     # ---------------------------------------------------------------- split
     def split_new_data_to_train_test(self, new_data):
@@ -982,12 +1062,24 @@ def known_items_spans(users, items, u, i, s, ts, device=None):
     ik = items.keys()
     n_i, n_u = len(ik), len(users)
     dev = torch.device(device) if device is not None else torch.device("cpu")
-    key = torch.from_numpy(u * n_i + i).to(dev)
-    tt = torch.from_numpy(ts).to(dev)
+    if isinstance(u, torch.Tensor):
+        # (the build's parse, still on the device)
+        dev = u.device
+        key = u.long() * n_i + i.long()
+        tt = ts
+        nan_all = torch.isnan(s)
+        present = np.zeros(n_u, dtype=bool)
+        present[torch.unique(u).cpu().numpy()] = True
+    else:
+        key = torch.from_numpy(u * n_i + i).to(dev)
+        tt = torch.from_numpy(ts).to(dev)
+        nan_all = torch.from_numpy(np.isnan(s)).to(dev)
+        present = np.zeros(n_u, dtype=bool)
+        present[u] = True
     o1 = torch.sort(tt, stable=True).indices
     order = o1[torch.sort(key[o1], stable=True).indices]
     key_s = key[order]
-    nan_s = torch.from_numpy(np.isnan(s)).to(dev)[order]
+    nan_s = nan_all[order]
     last = torch.ones_like(key_s, dtype=torch.bool)
     last[:-1] = key_s[1:] != key_s[:-1]
     kk = key_s[last & ~nan_s]
@@ -1000,8 +1092,6 @@ def known_items_spans(users, items, u, i, s, ts, device=None):
     o2 = torch.sort(uu * n_i + rk, stable=True).indices
     uu = uu[o2].cpu().numpy()
     ii = ii[o2].cpu().numpy()
-    present = np.zeros(n_u, dtype=bool)
-    present[u] = True
     return ingest.known_items_text(items, uu, ii, n_u), present
 
 

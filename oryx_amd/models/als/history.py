@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import os
 from collections import OrderedDict
 from typing import Optional, Tuple
 
@@ -43,6 +44,23 @@ log = logging.getLogger(__name__)
 __all__ = ["RatingsHistory"]
 
 _NO_TS = -(1 << 62)    # parse marker of a line without a timestamp (same as models/als/batch)
+
+
+_DEVICE_PARSE = os.environ.get("ORYX_ALS_DEVICE_PARSE", "1") != "0"
+
+
+def _first_appearance_codes(v: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(int32 code per element, distinct values in code order) with codes numbered in order
+    of first appearance -- the numbering a dictionary fed the elements in order gives."""
+    n = int(v.numel())
+    uniq, inv = torch.unique(v, sorted=True, return_inverse=True)
+    first = torch.full((uniq.numel(),), n, dtype=torch.int64, device=v.device)
+    first.scatter_reduce_(0, inv.long(), torch.arange(n, dtype=torch.int64, device=v.device),
+                          reduce="amin", include_self=True)
+    order = torch.argsort(first)
+    rank = torch.empty_like(order)
+    rank[order] = torch.arange(order.numel(), dtype=order.dtype, device=v.device)
+    return rank[inv].to(torch.int32), uniq[order]
 
 
 class _Segment:
@@ -86,7 +104,17 @@ class RatingsHistory:
         self._unkeyed.clear()
 
     # ------------------------------------------------------------------ parse
+    DEVICE_PARSE_MIN_BYTES = 4 << 20
+
     def _parse_range(self, buf, off: int, nbytes: int, n_lines: int) -> _Segment:
+        if self.device.type == "cuda" and nbytes >= self.DEVICE_PARSE_MIN_BYTES and \
+                _DEVICE_PARSE:
+            sg = self._parse_range_device(buf, off, nbytes)
+            if sg is not None:
+                self.stats["device_parsed_bytes"] = \
+                    self.stats.get("device_parsed_bytes", 0) + nbytes
+                return sg
+            self.stats["device_fallbacks"] = self.stats.get("device_fallbacks", 0) + 1
         users, items = ingest.IdDict(), ingest.IdDict()
         if isinstance(buf, np.ndarray):
             view = buf[off:off + nbytes]
@@ -102,13 +130,63 @@ class RatingsHistory:
                         torch.from_numpy(np.ascontiguousarray(s)).to(dev),
                         torch.from_numpy(np.ascontiguousarray(ts)).to(dev), nbytes)
 
+    def _parse_range_device(self, buf, off: int, nbytes: int) -> Optional[_Segment]:
+        """The range parsed on the GPU (``oryx_rating_lines``, csv.hip): the text goes to the
+        device (smaller than its parse), one thread per line; the segment's user / item keys
+        are numbered in first-appearance order there (unique values, their first line, sorted)
+        and only the distinct keys come back to fill the segment's dictionaries.  Codes,
+        strengths and timestamps are bitwise the host parser's; None (the caller parses on the
+        host) when any line is not in the plain form with canonical decimal IDs below 2^24."""
+        from ... import native
+        if not native.kernels_available():
+            return None
+        lib = native.require_kernels()
+        dev = self.device
+        view = np.frombuffer(buf, dtype=np.uint8, count=nbytes, offset=off) \
+            if not isinstance(buf, np.ndarray) else buf[off:off + nbytes]
+        pad = ((nbytes + 15) // 16) * 16 + 16
+        text = torch.empty(pad, dtype=torch.uint8, device=dev)
+        text[:nbytes].copy_(torch.from_numpy(view))
+        text[nbytes:].zero_()
+        ends = torch.nonzero(text[:nbytes] == 10).flatten()
+        if view[nbytes - 1] != 10:
+            ends = torch.cat([ends, torch.full((1,), nbytes, dtype=torch.int64, device=dev)])
+        n = int(ends.numel())
+        starts = torch.empty_like(ends)
+        starts[:1] = 0
+        starts[1:] = ends[:-1] + 1
+        uv = torch.empty(n, dtype=torch.int32, device=dev)
+        iv = torch.empty(n, dtype=torch.int32, device=dev)
+        sv = torch.empty(n, dtype=torch.float64, device=dev)
+        tv = torch.empty(n, dtype=torch.int64, device=dev)
+        bad = torch.empty(n, dtype=torch.uint8, device=dev)
+        n_bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        native.check(lib.oryx_rating_lines(
+            text.data_ptr(), starts.data_ptr(), ends.data_ptr(), n, _NO_TS, uv.data_ptr(),
+            iv.data_ptr(), sv.data_ptr(), tv.data_ptr(), bad.data_ptr(), n_bad.data_ptr(),
+            native.stream_ptr(dev)), "oryx_rating_lines")
+        del text, starts, ends, bad
+        if int(n_bad.item()):
+            return None
+        users, items = ingest.IdDict(), ingest.IdDict()
+        cu, ku = _first_appearance_codes(uv)
+        ci, ki = _first_appearance_codes(iv)
+        users.encode_nums(ku.cpu().numpy())
+        items.encode_nums(ki.cpu().numpy())
+        return _Segment(users, items, cu, ci, sv, tv, nbytes)
+
     def parse_ratings(self, lines, users: ingest.IdDict, items: ingest.IdDict,
-                      default_ts: int) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+                      default_ts: int, device_out: bool = False):
         """Same results as ``ingest.parse_ratings(lines, users, items, default_ts)`` (codes in
         first-appearance order appended to ``users`` / ``items``), reusing the parse of every
-        keyed segment seen before."""
+        keyed segment seen before.  ``device_out``: the columns stay tensors on the history's
+        device (user / item int64, strength fp64, timestamp int64) instead of host arrays."""
         if not isinstance(lines, TextLines):
-            return ingest.parse_ratings(lines, users, items, default_ts)
+            out = ingest.parse_ratings(lines, users, items, default_ts)
+            if device_out and self.device.type == "cuda":
+                return tuple(torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+                             for a in out)
+            return out
         buf = lines.joined()
         off = 0
         keyed = set()
@@ -154,10 +232,15 @@ class RatingsHistory:
             del self._segs[k]
         if not cols:
             e = np.zeros(0, dtype=np.int64)
-            return e, e.copy(), np.zeros(0, dtype=np.float64), e.copy()
+            out = e, e.copy(), np.zeros(0, dtype=np.float64), e.copy()
+            if device_out and self.device.type == "cuda":
+                return tuple(torch.from_numpy(a).to(self.device) for a in out)
+            return out
         u = torch.cat([c[0] for c in cols])
         i = torch.cat([c[1] for c in cols])
         s = torch.cat([c[2] for c in cols])
         ts = torch.cat([c[3] for c in cols])
         ts = torch.where(ts == _NO_TS, torch.full_like(ts, int(default_ts)), ts)
+        if device_out and self.device.type == "cuda":
+            return u, i, s, ts
         return u.cpu().numpy(), i.cpu().numpy(), s.cpu().numpy(), ts.cpu().numpy()

@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 26
+KERNELS_ABI_VERSION = 27
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -165,6 +165,7 @@ def _register_runtime_extras(lib):
                                           c_vp, c_vp, c_i, c_ll, c_i, c_vp])
     _sig(lib, "oryx_split_by_time", c_ll, [c_vp, c_ll, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,
                                            c_vp, c_vp])
+    _sig(lib, "oryx_dict_encode_nums", c_ll, [c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_encode_blob", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_find_blob", c_ll, [c_vp, c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_dict_keys_blob_sel", c_ll, [c_vp, c_vp, c_ll, c_vp, c_ll, c_vp])
@@ -274,6 +275,9 @@ def _load_kernels():
                                               ctypes.c_double, c_vp, c_vp])
     _sig(lib, "oryx_ipc_header_floats", c_ll, [])
     # numeric CSV lines -> feature matrix on the device (csv.hip; models/features.py)
+    # buf, starts, ends, n, default_ts, out_u, out_i, out_s, out_ts, bad, n_bad, stream
+    _sig(lib, "oryx_rating_lines", c_i, [c_vp, c_vp, c_vp, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp, c_vp, c_vp])
     _sig(lib, "oryx_csv_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp, c_i,
                                                 c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_vp, c_vp])
     # peer-push all-gather (ipc_allgather.hip; parallel/ipc.py IpcAllGather)

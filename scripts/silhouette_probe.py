@@ -23,7 +23,7 @@ def main():
     x = torch.randn((s, d), device="cuda", dtype=torch.float64, generator=g)
     w = torch.from_numpy(np.random.default_rng(1).zipf(1.5, k).clip(1, 5000).astype(np.float64))
     idx = torch.multinomial(w, s, replacement=True).to("cuda")
-    out = {"s": s, "d": d, "k": k, "rs64": os.environ.get("ORYX_KM_SIL_RS", "3")}
+    out = {"s": s, "d": d, "k": k, "rs64": os.environ.get("ORYX_KM_SIL_RS", "22 (default)")}
     # the MFMA kernel (default) and the VALU kernel it replaced, same sample
     for name, mfma in (("mfma", True), ("valu", False)):
         ev._SIL_MFMA = mfma

@@ -132,6 +132,83 @@ def test_history_device_resident_matches(tmp_path):
     assert all(sg.u.is_cuda for sg in h._segs.values())
 
 
+def _numeric_lines(gen, n, users, items, odd=False):
+    """Numeric-ID rating lines in every form the device parser takes (plain, missing / empty
+    fields, exponents, signs, CRLF, extra fields); ``odd``: also a line it must hand back."""
+    out = []
+    for j in range(n):
+        u, i = int(gen.integers(users)), int(gen.integers(items))
+        r = gen.random()
+        if r < 0.55:
+            out.append("%d,%d,%.1f,%d" % (u, i, gen.uniform(0, 5), 1_600_000_000_000 + j))
+        elif r < 0.62:
+            out.append("%d,%d" % (u, i))
+        elif r < 0.68:
+            out.append("%d,%d," % (u, i))
+        elif r < 0.73:
+            out.append("%d,%d,,%d" % (u, i, 1_600_000_000_000 + j))
+        elif r < 0.78:
+            out.append("%d,%d,%.3e,%d" % (u, i, gen.uniform(-3, 3), j))
+        elif r < 0.83:
+            out.append("%d,%d,+%.2f" % (u, i, gen.uniform(0, 2)))
+        elif r < 0.88:
+            out.append("%d,%d,%.4f,%d\r" % (u, i, gen.uniform(0, 9), j))
+        elif r < 0.93:
+            out.append("%d,%d,2.5,%d,extra,fields" % (u, i, j))
+        else:
+            out.append("%d,%d,-%.2f," % (u, i, gen.uniform(0, 1)))
+    if odd:
+        out.insert(len(out) // 2, "007,%d,1.0" % int(gen.integers(items)))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("odd", [False, True])
+def test_history_device_parse_matches_host_parse(tmp_path, monkeypatch, odd):
+    """The GPU rating parse (oryx_rating_lines + first-appearance numbering on the device)
+    gives the host parser's dictionaries, codes, strengths (NaN where empty) and timestamps
+    bitwise; a range with a line it does not take (a non-canonical key) is parsed on the host
+    instead.  Also through ``parse_ratings(device_out=True)``, the build's path."""
+    import torch
+    from oryx_amd.models.als import history as hist_mod
+    monkeypatch.setattr(RatingsHistory, "DEVICE_PARSE_MIN_BYTES", 0)
+    gen = np.random.default_rng(9)
+    root = str(tmp_path)
+    for p in range(3):
+        d = os.path.join(root, "oryx-%d.data" % (1000 + p))
+        os.makedirs(d)
+        with open(os.path.join(d, "part-00000.txt"), "w", newline="") as f:
+            f.write("\n".join(_numeric_lines(gen, 3000, 900, 400, odd=odd and p == 1)) + "\n")
+    data = concat_lines([TextLines.from_strings(_numeric_lines(gen, 1500, 1000, 450)),
+                         read_past_data(root).values()])
+    h = RatingsHistory(torch.device("cuda", 0))
+    for default_ts in (0, 77):
+        u1, i1 = ingest.IdDict(), ingest.IdDict()
+        ref = ingest.parse_ratings(data, u1, i1, default_ts=default_ts)
+        u2, i2 = ingest.IdDict(), ingest.IdDict()
+        got = h.parse_ratings(data, u2, i2, default_ts=default_ts)
+        _same(ref[:2], got[:2])
+        np.testing.assert_array_equal(np.isnan(ref[2]), np.isnan(got[2]))
+        np.testing.assert_array_equal(np.nan_to_num(ref[2]), np.nan_to_num(got[2]))
+        _same(ref[3:], got[3:])
+        assert u1.keys() == u2.keys() and i1.keys() == i2.keys()
+    assert h.stats.get("device_parsed_bytes", 0) > 0
+    assert h.stats.get("device_fallbacks", 0) == (1 if odd else 0)
+    # the build's path: columns stay on the device
+    u3, i3 = ingest.IdDict(), ingest.IdDict()
+    raw = []
+    dv = als_batch.parse_ratings(data, u3, i3, raw_out=raw, now_ms=5, history=h,
+                                 device_out=True)
+    assert all(isinstance(x, torch.Tensor) and x.is_cuda for x in dv)
+    u4, i4 = ingest.IdDict(), ingest.IdDict()
+    raw_h = []
+    hv = als_batch.parse_ratings(data, u4, i4, raw_out=raw_h, now_ms=5)
+    for x, y in zip(list(dv) + raw, list(hv) + raw_h):
+        np.testing.assert_array_equal(np.nan_to_num(x.cpu().numpy().astype(np.float64)),
+                                      np.nan_to_num(np.asarray(y, dtype=np.float64)))
+    assert hist_mod._DEVICE_PARSE
+
+
 def test_history_adopts_new_interval_parse_cpu(tmp_path, monkeypatch):
     """The new interval's parse is reused when its part file is read back."""
     from oryx_amd.layers.batch import save_interval_data
