@@ -189,8 +189,10 @@ int jks_recover_key(const unsigned char* der, size_t n, const std::vector<unsign
   }
   unsigned char got[20];
   sha1_parts(pw, plain->data(), plain->size(), nullptr, 0, got);
+  // (check points into epki's octet string: compared before epki is freed)
+  const bool match = memcmp(got, check, 20) == 0;
   X509_SIG_free(epki);
-  if (memcmp(got, check, 20) != 0) {
+  if (!match) {
     *err = "JKS private key: wrong password";
     return kKeystoreBadPassword;
   }

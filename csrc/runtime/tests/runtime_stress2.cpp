@@ -62,6 +62,11 @@ int oryx_http_respond(void* h, unsigned long long id, const char* data, long lon
 void oryx_http_stop(void* h);
 int oryx_http_tls(void* h, const char* cert, const char* key, const char* password);
 void oryx_http_free(void* h);
+int oryx_keystore_to_pem(const char* path, const char* password, const char* alias,
+                         char** cert_pem, long long* cert_len, char** key_pem,
+                         long long* key_len);
+void oryx_keystore_free(char* p);
+const char* oryx_keystore_error();
 long long oryx_topn_prep(int nq, int k, int kp, int max_batch, const float* targets,
                          const long long* cand_ptr, const long long* cand,
                          const unsigned char* cand_all, int num_buckets, int words,
@@ -727,6 +732,68 @@ static void test_hostbuf(const char* dir) {
   CHECK(ok && k == (long long)seen.size());
 }
 
+// The keystore readers (oryx_keystore.cpp) from several threads at once on the same files, and
+// on every truncation and a byte-flipped copy of each file: valid stores decode, damaged ones
+// fail cleanly (no crash, no leak, no read past the buffer).
+static void test_keystores(const char* dir, const char* const* stores, int n_stores) {
+  std::vector<std::thread> th;
+  for (int t = 0; t < 4; ++t)
+    th.emplace_back([&, t] {
+      for (int rep = 0; rep < 20; ++rep)
+        for (int j = 0; j < n_stores; ++j) {
+          char *c = nullptr, *k = nullptr;
+          long long cn = 0, kn = 0;
+          const int rc = oryx_keystore_to_pem(stores[j], "oryxpass", nullptr, &c, &cn, &k, &kn);
+          if (rc != 0 || !c || !k || cn <= 0 || kn <= 0 ||
+              strncmp(c, "-----BEGIN CERTIFICATE-----", 27) != 0) {
+            fprintf(stderr, "keystore %s thread %d: rc %d (%s)\n", stores[j], t, rc,
+                    oryx_keystore_error());
+            g_errors++;
+          }
+          oryx_keystore_free(c);
+          oryx_keystore_free(k);
+          const int bad = oryx_keystore_to_pem(stores[j], "wrong", nullptr, &c, &cn, &k, &kn);
+          if (bad != 2) {
+            fprintf(stderr, "keystore %s: wrong password gave %d\n", stores[j], bad);
+            g_errors++;
+            if (bad == 0) {
+              oryx_keystore_free(c);
+              oryx_keystore_free(k);
+            }
+          }
+        }
+    });
+  for (auto& x : th) x.join();
+  // damaged copies: every prefix length (up to 4 KB) and one flipped byte per position step
+  const std::string tmp = std::string(dir) + "/damaged_store";
+  for (int j = 0; j < n_stores; ++j) {
+    FILE* f = fopen(stores[j], "rb");
+    if (!f) { g_errors++; continue; }
+    std::vector<char> b;
+    char buf[4096];
+    size_t got;
+    while ((got = fread(buf, 1, sizeof(buf), f)) > 0) b.insert(b.end(), buf, buf + got);
+    fclose(f);
+    for (size_t len = 0; len < b.size() && len < 4096; len += (len < 64 ? 1 : 37)) {
+      for (int flip = 0; flip < 2; ++flip) {
+        std::vector<char> d(b.begin(), b.begin() + (long)(flip ? b.size() : len));
+        if (flip && len < d.size()) d[len] ^= 0x5a;
+        FILE* o = fopen(tmp.c_str(), "wb");
+        if (!o) { g_errors++; return; }
+        if (!d.empty()) fwrite(d.data(), 1, d.size(), o);
+        fclose(o);
+        char *c = nullptr, *k = nullptr;
+        long long cn = 0, kn = 0;
+        const int rc = oryx_keystore_to_pem(tmp.c_str(), "oryxpass", nullptr, &c, &cn, &k, &kn);
+        if (rc == 0) {
+          oryx_keystore_free(c);
+          oryx_keystore_free(k);
+        }
+      }
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: runtime_stress2 <dir>\n");
@@ -745,6 +812,10 @@ int main(int argc, char** argv) {
   if (argc >= 4) {
     test_https(argv[2], argv[3]);
     printf("https: errors %d\n", g_errors.load());
+  }
+  if (argc >= 5) {
+    test_keystores(argv[1], (const char* const*)(argv + 4), argc - 4);
+    printf("keystores (JKS / PKCS#12, damaged copies): errors %d\n", g_errors.load());
   }
   return g_errors.load() == 0 ? 0 : 1;
 }
