@@ -291,15 +291,24 @@ class _StallWatch:
     a GIL held by a long native call, a GC pass -- shows up here, and the record lines it up
     with the slow requests and the UP applications."""
 
-    def __init__(self):
+    def __init__(self, dump_path=None):
         self.stalls = []
         self._stop = threading.Event()
         self._t = threading.Thread(target=self._run, daemon=True, name="stall-watch")
+        # faulthandler's watchdog is a C thread: armed for 20 ms on every wake-up, it dumps
+        # every Python thread's stack WITHOUT the GIL when a wake-up is that late -- the stack
+        # of whoever holds the interpreter during the stall
+        self._dump = open(dump_path, "w") if dump_path else None
 
     def _run(self):
+        import faulthandler
         last = time.perf_counter()
         while not self._stop.is_set():
+            if self._dump is not None:
+                faulthandler.dump_traceback_later(0.02, repeat=False, file=self._dump)
             time.sleep(0.001)
+            if self._dump is not None:
+                faulthandler.cancel_dump_traceback_later()
             now = time.perf_counter()
             if now - last > 0.015:
                 self.stalls.append((time.time() - (now - last), (now - last) * 1e3))
@@ -312,6 +321,8 @@ class _StallWatch:
     def stop(self):
         self._stop.set()
         self._t.join()
+        if self._dump is not None:
+            self._dump.close()
         return self.stalls
 
 
@@ -438,7 +449,8 @@ def main(argv=None) -> int:
             speed.stdin.flush()
             print("bench_traffic: mix phase", file=sys.stderr, flush=True)
             s0 = _server_side(serving)
-            sw = _StallWatch().start()
+            dump = os.path.join(work, "stall_stacks.txt")
+            sw = _StallWatch(dump).start()
             rec["mix_phase"] = run_phase(port, args, mix, args.seed + 1)
             stalls = sw.stop()
             slow = rec["mix_phase"].pop("_slow", [])
@@ -450,7 +462,9 @@ def main(argv=None) -> int:
                 "stalls": [(round(t - t_mix, 3), round(d, 1))
                            for t, d in sorted(stalls, key=lambda x: -x[1])[:20]],
                 "up_apply_ms": _stats([d for _, d, _ in applies]) if applies else None,
-                "slow_requests": _attribute_slow(slow, stalls, applies, t_mix)}
+                "slow_requests": _attribute_slow(slow, stalls, applies, t_mix),
+                # the interpreter's stacks during each stall (faulthandler, see _StallWatch)
+                "stall_stacks": open(dump).read()[:20000] if os.path.exists(dump) else None}
             rec["mix_server"] = _server_delta(s0, _server_side(serving))
             rec["mix_gc"] = gcp.take()
             speed.stdin.write("stop\n")

@@ -894,8 +894,12 @@ def _train_device(data: BinnedData, label, y, y_shift: float, S: int, classifica
         # needs 2 * (most splits in any tree) slots, not 2^(depth + 1) -- one small host read
         # per level sizes every later histogram, split search and all-reduce to the live
         # nodes (deep levels of a forest are mostly leaves)
-        live = int(is_split.sum(1).max()) if depth < max_depth else 0
-        _check_split_err(split_err, depth, ctx)
+        # (the split search's error flag comes back with the same read)
+        live_err = torch.stack([is_split.sum(1).max().to(torch.int64),
+                                split_err[0].to(torch.int64)]).tolist()
+        live = int(live_err[0]) if depth < max_depth else 0
+        if live_err[1]:
+            _check_split_err(split_err, depth, ctx)
         if ctx.is_distributed:
             # the split search above consumed this level's all-reduced histograms: a one-shot
             # all-reduce whose peer never arrived must fail the forest here, not grow trees
