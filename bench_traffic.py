@@ -417,6 +417,11 @@ def main(argv=None) -> int:
                           file=sys.stderr, flush=True)
                 time.sleep(0.02)
             rec["load_s"] = time.perf_counter() - t0
+            t_w = time.perf_counter()
+            while getattr(serving.manager, "warm_s", 0.0) is None and \
+                    time.perf_counter() - t_w < 60:
+                time.sleep(0.02)
+            rec["serving_warm_s"] = getattr(serving.manager, "warm_s", None)
             if speed is not None:
                 ld = json.loads(speed.stdout.readline())
                 rec["speed_load_s"], rec["speed_warm_s"] = ld["loaded_s"], ld["warm_s"]

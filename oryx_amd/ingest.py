@@ -152,7 +152,11 @@ class IdDict:
             if have < n:
                 new = self._fetch_keys(have, n)
                 if len(arr) < n:
-                    grown = np.empty(max(n, 2 * len(arr), 1024), dtype=object)
+                    # 1/8 headroom (at least double once filled): growing copies every key
+                    # reference with the GIL held -- at 20M keys a 30-40 ms stall of every
+                    # serving thread, which an exact-size cache paid on the first new key
+                    # after a model load (profiles/r6_traffic_20m_250_lsh03_v4.json)
+                    grown = np.empty(max(n + n // 8, 2 * len(arr), 1024), dtype=object)
                     grown[:have] = arr[:have]
                     arr = grown
                 arr[have:n] = new

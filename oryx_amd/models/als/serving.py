@@ -658,6 +658,35 @@ class ALSServingModel(ServingModel):
                 if len(a):
                     self._known[u] = a[keep[a]]
 
+    def warm(self) -> float:
+        """Take, once the model has loaded, every first-time path that the first ``UP`` rows
+        after a load would otherwise take under traffic: the known-items key cache (sized with
+        headroom), one row of each store re-written with its own value (dirty-row upload, the
+        index's incremental update, the bf16 mirror's row conversion) and a scan.  Values and
+        answers are unchanged.  Returns the seconds taken."""
+        t0 = time.perf_counter()
+        self._kdict.key_list()
+        def some_id(store):
+            for r in range(min(64, store.size())):
+                id_ = store.id_of_row(r)
+                if id_ is not None:
+                    return id_
+            return None
+        for store in (self.X, self.Y):
+            id_ = some_id(store)
+            vec = store.get_vector(id_) if id_ is not None else None
+            if vec is not None:
+                store.set_vectors([id_], vec[None])
+        if self.Y.size():
+            self.top_n(np.zeros(self.features, dtype=np.float32), 1)
+            uid = some_id(self.X)
+            u = self.get_user_vector(uid) if uid is not None else None
+            if u is not None:
+                self.top_n(u, 1, exclude=self.get_known_items(uid) or None)
+        if self.device is not None and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return time.perf_counter() - t0
+
     def get_fraction_loaded(self) -> float:
         with self._expected_lock:
             expected = len(self._expected_users) + len(self._expected_items)
@@ -805,6 +834,8 @@ class ALSServingModelManager(AbstractServingModelManager):
         # the last UP applications: (wall-clock start, ms, rows) -- what a latency record
         # correlates its slow requests with (bench_traffic.py)
         self.apply_log = collections.deque(maxlen=1024)
+        self._warmed = None          # the model last warmed (ALSServingModel.warm)
+        self.warm_s: Optional[float] = None
 
     def consume(self, updates: Iterator[KeyMessage], context=None) -> None:
         countdown = 10000
@@ -827,6 +858,7 @@ class ALSServingModelManager(AbstractServingModelManager):
                     n_up = len(batch) + drain_up_blocks(self.model, updates)
                     self.apply_log.append((t_wall, (time.perf_counter() - t0) * 1e3, n_up))
                     countdown -= n_up
+                    self._maybe_warm()
                     if countdown <= 0:
                         log.info("%s", self.model)
                         countdown = 10000
@@ -847,8 +879,10 @@ class ALSServingModelManager(AbstractServingModelManager):
                 if countdown <= 0:
                     log.info("%s", self.model)
                     countdown = 10000
+                self._maybe_warm()
             elif key in ("MODEL", "MODEL-REF"):
                 log.info("Loading new model")
+                self._warmed = None
                 pmml = pmmlu.read_pmml_from_update_key_message(key, message)
                 features = int(pmml.get_extension_value("features"))
                 implicit = pmml.get_extension_value("implicit").lower() == "true"
@@ -871,6 +905,21 @@ class ALSServingModelManager(AbstractServingModelManager):
                 log.info("Model updated: %s", self.model)
             else:
                 raise ValueError("Bad message: %r" % (km,))
+
+    def _maybe_warm(self) -> None:
+        """Warm the model (:meth:`ALSServingModel.warm`) on this consumer thread once it has
+        completely loaded: the first ``UP`` rows after a load otherwise stalled every serving
+        thread for 30-40 ms growing the 20M-key known-items cache with the GIL held
+        (profiles/r6_traffic_20m_250_lsh03_v4.json, stacks from bench_traffic's stall watch)."""
+        m = self.model
+        if m is None or self._warmed is m or m.get_fraction_loaded() < 1.0:
+            return
+        self._warmed = m
+        try:
+            self.warm_s = m.warm()
+            log.info("Serving model warmed in %.2fs", self.warm_s)
+        except Exception:   # noqa: BLE001 -- a failed warm-up only costs the first request
+            log.exception("Serving model warm-up failed")
 
     def get_model(self) -> Optional[ALSServingModel]:
         return self.model

@@ -140,6 +140,13 @@ def test_batch_layer_als_end_to_end(tmp_path):
         with urllib.request.urlopen(req) as r:
             recs = json.loads(r.read())
         assert 1 <= len(recs) <= 3 and all("id" in x and "value" in x for x in recs)
+        # the consumer warmed the loaded model (update paths taken once, answers unchanged)
+        deadline = time.time() + 30
+        while time.time() < deadline and serving.manager.warm_s is None:
+            time.sleep(0.05)
+        assert serving.manager.warm_s is not None
+        with urllib.request.urlopen(req) as r:
+            assert json.loads(r.read()) == recs
         req = urllib.request.Request("http://127.0.0.1:%d/ingest" % port, data=b"U1,I2,3\n",
                                      method="POST", headers={"Content-Type": "text/plain"})
         with urllib.request.urlopen(req) as r:
