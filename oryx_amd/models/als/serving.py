@@ -679,6 +679,10 @@ class ALSServingModel(ServingModel):
                 store.set_vectors([id_], vec[None])
         if self.Y.size():
             self.top_n(np.zeros(self.features, dtype=np.float32), 1)
+            iid = some_id(self.Y)
+            y = self.get_item_vector(iid) if iid is not None else None
+            if y is not None:
+                self.top_n(y, 1, cosine=True, exclude=[iid])      # /similarity's scan
             uid = some_id(self.X)
             u = self.get_user_vector(uid) if uid is not None else None
             if u is not None:

@@ -215,10 +215,36 @@ class ALSSpeedModel(SpeedModel):
         if self.device is not None and self.device.type == "cuda" and \
                 self.X.size() and self.Y.size():
             try:
-                self.solver_inverses()
+                inv = self.solver_inverses()
             except mathx.SingularMatrixSolverException:
-                pass           # the interval reports it, as it would have
+                inv = None     # the interval reports it, as it would have
+            if inv is not None and self.features <= 256 and native.kernels_available():
+                self._warm_foldin(inv)
         return time.perf_counter() - t0
+
+    def _warm_foldin(self, inv) -> None:
+        """One fold-in of a single event (row 0 of each store, output discarded) and the
+        formatting of its rows: the kernels' first launches -- code objects loaded, 10 ms
+        each -- happen here and not in the first micro-batch, which otherwise held the GPU
+        while the serving process beside it answered requests (r6_traffic_*_v5)."""
+        from ...ops import textfmt as tf
+        k = self.features
+        dev = self.device
+        xm, ym = self.X.device_view()[0], self.Y.device_view()[0]
+        r = torch.zeros(1, dtype=torch.int64, device=dev)
+        vals = torch.ones(1, dtype=torch.float32, device=dev)
+        new = torch.empty((2, k), dtype=torch.float32, device=dev)
+        flags = torch.empty(2, dtype=torch.uint8, device=dev)
+        xinv, yinv = inv
+        lib = native.require_kernels()
+        native.check(lib.oryx_als_foldin(
+            xm.contiguous().data_ptr(), ym.contiguous().data_ptr(), k, r.data_ptr(),
+            r.data_ptr(), vals.data_ptr(), xinv.contiguous().data_ptr(),
+            yinv.contiguous().data_ptr(), int(self.implicit), 1, new[:1].data_ptr(),
+            new[1:].data_ptr(), flags[:1].data_ptr(), flags[1:].data_ptr(),
+            native.stream_ptr(dev)), "oryx_als_foldin")
+        tf.format_rows_and(new, flags)
+        torch.cuda.synchronize(dev)
 
     def get_fraction_loaded(self) -> float:
         with self._lock:
