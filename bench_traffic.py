@@ -326,16 +326,22 @@ class _StallWatch:
         return self.stalls
 
 
-def _attribute_slow(slow, stalls, applies, t_start):
+def _attribute_slow(slow, stalls, applies, t_start, index_events=(), scans=()):
     """Per slow request (start, ms, endpoint): when it started (seconds into the phase), and
-    the serving-process stalls and UP applications whose time overlaps it."""
+    the serving-process stalls, UP applications, index refreshes / bf16 conversions and slow
+    scan batches whose time overlaps it."""
     out = []
+
+    def over(ev, t0, t1):
+        return ev[0] < t1 and ev[0] + ev[1] / 1e3 > t0
     for t0, ms, ep in slow:
         t1 = t0 + ms / 1e3
         st = [round(d, 1) for (s0, d) in stalls if s0 < t1 and s0 + d / 1e3 > t0]
         ap = [(round(d, 1), n) for (s0, d, n) in applies if s0 < t1 and s0 + d / 1e3 > t0]
+        ix = [(round(e[1], 1), e[2], e[3]) for e in index_events if over(e, t0, t1)]
+        sc = [(round(e[0] - t_start, 3), round(e[1], 1), e[2]) for e in scans if over(e, t0, t1)]
         out.append({"ms": round(ms, 1), "endpoint": ep, "at_s": round(t0 - t_start, 3),
-                    "stalls_ms": st, "up_apply": ap})
+                    "stalls_ms": st, "up_apply": ap, "index": ix, "scan_batches": sc})
     return out
 
 
@@ -467,7 +473,10 @@ def main(argv=None) -> int:
                 "stalls": [(round(t - t_mix, 3), round(d, 1))
                            for t, d in sorted(stalls, key=lambda x: -x[1])[:20]],
                 "up_apply_ms": _stats([d for _, d, _ in applies]) if applies else None,
-                "slow_requests": _attribute_slow(slow, stalls, applies, t_mix),
+                "slow_requests": _attribute_slow(
+                    slow, stalls, applies, t_mix,
+                    list(getattr(getattr(vm, "index", None), "event_log", [])),
+                    list(getattr(getattr(vm, "batcher", None), "slow_log", []))),
                 # the interpreter's stacks during each stall (faulthandler, see _StallWatch)
                 "stall_stacks": open(dump).read()[:20000] if os.path.exists(dump) else None}
             rec["mix_server"] = _server_delta(s0, _server_side(serving))

@@ -104,6 +104,7 @@ class TopNBatcher:
         self.batches = 0
         self.requests = 0
         self.inline = 0
+        self.slow_log = collections.deque(maxlen=256)
 
     def submit(self, q: "topn_ops.TopNQuery"):
         if self.max_batch <= 1:
@@ -197,6 +198,10 @@ class TopNBatcher:
         if err is None:
             try:
                 res = fin()
+                took = time.monotonic() - t_scan
+                if took > 0.01:
+                    # (wall-clock launch, ms from launch to results, queries) of slow batches
+                    self.slow_log.append((time.time() - took, took * 1e3, len(batch)))
                 for b, r in zip(batch, res):
                     b[1] = r
             except Exception as e:

@@ -23,10 +23,12 @@ passes returned -- every depth is exact.
 
 from __future__ import annotations
 
+import collections
 import ctypes
 import itertools
 import os
 import threading
+import time
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
@@ -149,6 +151,9 @@ class ItemIndex:
         self.cap = 0
         self.rebuilds = 0
         self.incremental = 0       # refreshes absorbed without a re-sort
+        # (wall-clock start, ms, what, rows) of each refresh / bf16 conversion that did work:
+        # what a latency record lines its slow requests up with (bench_traffic.py)
+        self.event_log = collections.deque(maxlen=512)
         self.delta_added = 0       # rows appended to the delta segment, ever
         self._built = False
         # bf16 scan with exact fp32 re-rank of a certified candidate pool (_launch_bf16):
@@ -177,13 +182,18 @@ class ItemIndex:
                 if self.version == st.version and self._built:
                     return
                 state = st.take_index_state(self._token)
+            t_wall, t0 = time.time(), time.perf_counter()
             ver, dirty = state
             mat, valid, _ = st.device_view()
             parts = st.device_partitions()
+            what = "incremental"
             if not self._built or dirty is None or not self._update_in_place(mat, valid, parts,
                                                                              dirty):
                 self._rebuild(mat, valid, parts)
+                what = "rebuild"
             self.version = ver
+            self.event_log.append((t_wall, (time.perf_counter() - t0) * 1e3, what,
+                                   -1 if dirty is None else len(dirty)))
 
     def _buckets(self, parts, rows):
         if parts is None:
@@ -425,6 +435,7 @@ class ItemIndex:
         if self._yb is not None and self._yb_key is not None and \
                 self._yb_key[0] == st.version and self._yb_key[1] == self._yb.shape[0]:
             return self._yb            # nothing written since the last conversion
+        t_wall, t0 = time.time(), time.perf_counter()
         ver, dirty = st.take_index_state(self._yb_token)
         mat, _ = st.device_rows()
         rows = mat.shape[0]
@@ -447,6 +458,8 @@ class ItemIndex:
                 self._max_norm = max(self._max_norm, float(norms[d].max()))
         self._yb = yb
         self._yb_key = (ver, rows)
+        self.event_log.append((t_wall, (time.perf_counter() - t0) * 1e3, "bf16",
+                               -1 if dirty is None else len(dirty)))
         return yb
 
     def _launch_bf16(self, qs: Sequence[TopNQuery]):
