@@ -338,7 +338,8 @@ def _attribute_slow(slow, stalls, applies, t_start, index_events=(), scans=()):
         t1 = t0 + ms / 1e3
         st = [round(d, 1) for (s0, d) in stalls if s0 < t1 and s0 + d / 1e3 > t0]
         ap = [(round(d, 1), n) for (s0, d, n) in applies if s0 < t1 and s0 + d / 1e3 > t0]
-        ix = [(round(e[1], 1), e[2], e[3]) for e in index_events if over(e, t0, t1)]
+        ix = [(round(e[1], 1), e[2], e[3]) + tuple(e[4:]) for e in index_events
+              if over(e, t0, t1)]
         sc = [(round(e[0] - t_start, 3), round(e[1], 1), e[2]) for e in scans if over(e, t0, t1)]
         out.append({"ms": round(ms, 1), "endpoint": ep, "at_s": round(t0 - t_start, 3),
                     "stalls_ms": st, "up_apply": ap, "index": ix, "scan_batches": sc})

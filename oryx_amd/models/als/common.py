@@ -16,6 +16,7 @@ from __future__ import annotations
 import math
 import mmap
 import threading
+import time
 from typing import Callable, Collection, Dict, Iterable, List, Optional, Sequence, Set, Tuple
 
 import numpy as np
@@ -576,6 +577,7 @@ class FeatureVectors:
                     self._dirty_all = False
                     dirty_rows = None
                 elif self._dirty:
+                    t_rf = time.perf_counter()
                     rows = np.fromiter(self._dirty, dtype=np.int64, count=len(self._dirty))
                     vals = torch.from_numpy(self._host[rows]).to(self.device, non_blocking=False)
                     if self.ld != self.k:
@@ -594,6 +596,9 @@ class FeatureVectors:
                     elif dirty_rows is not None and dirty_rows.numel():
                         self._dev_part[dirty_rows] = self.partitioner(
                             self._dev[dirty_rows][:, :self.k])
+                if dirty_rows is not None and dirty_rows.numel():
+                    # (the last dirty-row refresh's host time: latency attribution)
+                    self.last_refresh_ms = (time.perf_counter() - t_rf) * 1e3
             return self._dev[:n], self._dev_valid[:n], self._dev_norm[:n]
 
     def device_partitions(self) -> Optional[torch.Tensor]:

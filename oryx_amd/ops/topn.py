@@ -186,14 +186,18 @@ class ItemIndex:
             ver, dirty = state
             mat, valid, _ = st.device_view()
             parts = st.device_partitions()
+            t1 = time.perf_counter()
             what = "incremental"
             if not self._built or dirty is None or not self._update_in_place(mat, valid, parts,
                                                                              dirty):
                 self._rebuild(mat, valid, parts)
                 what = "rebuild"
             self.version = ver
-            self.event_log.append((t_wall, (time.perf_counter() - t0) * 1e3, what,
-                                   -1 if dirty is None else len(dirty)))
+            t2 = time.perf_counter()
+            self.event_log.append((t_wall, (t2 - t0) * 1e3, what,
+                                   -1 if dirty is None else len(dirty),
+                                   {"device_view_ms": round((t1 - t0) * 1e3, 2),
+                                    "update_ms": round((t2 - t1) * 1e3, 2)}))
 
     def _buckets(self, parts, rows):
         if parts is None:
