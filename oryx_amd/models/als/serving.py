@@ -340,6 +340,7 @@ class ALSServingModel(ServingModel):
         if device is None:
             device = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
         self.device = device
+        self.sample_rate = sample_rate
         # one GPU scans every candidate bucket at once: size the LSH for the sample rate alone
         self.lsh = LocalitySensitiveHash(sample_rate, features, num_cores=1)
         self.features = features
@@ -682,6 +683,24 @@ class ALSServingModel(ServingModel):
             vec = store.get_vector(id_) if id_ is not None else None
             if vec is not None:
                 store.set_vectors([id_], vec[None])
+        if self.index is not None and self.device.type == "cuda":
+            # a throwaway model of the same shape on the same device, whose items move between
+            # LSH buckets: the index's incremental kill / append paths launch their kernels
+            # for the first time here -- code objects are loaded on demand, ~100 ms on the
+            # first UP rows after a 20M-item load otherwise (r6_traffic_20m_250_lsh03_v6) --
+            # without a single write to this model
+            tmp = ALSServingModel(self.features, self.implicit, self.sample_rate,
+                                  device=self.device, max_batch=1)
+            g = np.random.default_rng(0)
+            ids = ["w%d" % j for j in range(512)]
+            tmp.set_item_vectors(ids, g.standard_normal((512, self.features)).astype(np.float32))
+            q = g.standard_normal(self.features).astype(np.float32)
+            tmp.top_n(q, 1)
+            tmp.set_item_vectors(ids[:64], -g.standard_normal((64, self.features))
+                                 .astype(np.float32))
+            tmp.top_n(q, 1)
+            tmp.top_n(q, 1, cosine=True, exclude=ids[:1])
+            del tmp
         if self.Y.size():
             self.top_n(np.zeros(self.features, dtype=np.float32), 1)
             iid = some_id(self.Y)
