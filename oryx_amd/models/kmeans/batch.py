@@ -163,7 +163,12 @@ class KMeansUpdate(MLUpdate):
         if sharded:
             dist.all_reduce_sum(s, ctx)
         shift = s[0] / s[1].clamp_min(1.0)
-        x = (x64 - shift).float()
+        # shifted and narrowed in row slices: (x64 - shift) whole would be another float64
+        # copy of the matrix (25.6 GB at 12.5M x 256) on top of the parse and the result
+        x = torch.empty(x64.shape, dtype=torch.float32, device=x64.device)
+        step = max(1, (1 << 27) // max(1, x64.shape[1]))
+        for lo in range(0, n, step):
+            x[lo:lo + step] = (x64[lo:lo + step] - shift).float()
         tm = self.train_phases
         if x.device.type == "cuda":
             torch.cuda.synchronize(x.device)
