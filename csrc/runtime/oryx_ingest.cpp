@@ -2621,37 +2621,20 @@ struct SpeedBatch {
   std::vector<std::deque<std::string>> owned;
   FlatIndex nu_idx, ni_idx;             // new keys -> index
   std::vector<std::string_view> nu_keys, ni_keys;
-  // aggregated pairs: rows (-1 = new), value, representative event (for the keys)
-  std::vector<int64_t> au, ai, rep;
-  std::vector<double> av;
+  // aggregated pairs: representative event (for the keys)
+  std::vector<int64_t> rep;
+  // aggregation scratch (kept for its capacity): pair hash table, per-pair first event and
+  // count, per-event pair, grouped events
+  std::vector<int32_t> tab, first, cnt, pid, start, ev;
   const char* buf = nullptr;
 
   void clear() {
     u.clear(); i.clear(); s.clear(); ts.clear(); uk.clear(); ik.clear(); owned.clear();
     uql.clear(); iql.clear();
     nu_idx.clear(); ni_idx.clear(); nu_keys.clear(); ni_keys.clear();
-    au.clear(); ai.clear(); rep.clear(); av.clear();
+    rep.clear();
   }
 };
-
-// Stable LSD radix sort of idx (initially any order) by keys[idx] (only the low `bits` bits
-// matter), 11-bit digits: a 10k-event micro-batch sorts in ~0.1 ms where std::sort's
-// mispredicted branches cost ~1 ms.
-void radix_sort_by(const std::vector<uint64_t>& keys, int bits, std::vector<uint32_t>& idx) {
-  const size_t n = idx.size();
-  std::vector<uint32_t> tmp(n);
-  constexpr int D = 11;
-  for (int shift = 0; shift < bits; shift += D) {
-    uint32_t cnt[1u << D] = {0};
-    for (size_t k = 0; k < n; ++k) ++cnt[(keys[idx[k]] >> shift) & ((1u << D) - 1)];
-    uint32_t sum = 0;
-    for (uint32_t& c : cnt) { const uint32_t t = c; c = sum; sum += t; }
-    for (size_t k = 0; k < n; ++k) tmp[cnt[(keys[idx[k]] >> shift) & ((1u << D) - 1)]++] = idx[k];
-    idx.swap(tmp);
-  }
-}
-
-int bit_width(uint64_t v) { return v ? 64 - __builtin_clzll(v) : 0; }
 
 struct SpeedChunk {
   std::vector<int64_t> u, i;
@@ -2659,8 +2642,19 @@ struct SpeedChunk {
   std::vector<double> s;
   std::vector<long long> ts;
   std::vector<std::string_view> uk, ik;
+  std::vector<uint64_t> hu, hi;         // the keys' RowMap hashes
   std::deque<std::string> owned;
+  bool has_new = false;                 // a key the stores lack
 };
+
+// splitmix64 finalizer: the aggregation's (user row, item row) pair hash
+inline uint64_t pair_mix(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
 
 }  // namespace
 
@@ -2692,7 +2686,7 @@ long long oryx_speed_parse(void* h, const char* buf, long long len, void* xm, vo
       const char* end = cut[(size_t)t + 1];
       const size_t est = (size_t)((end - p) / 20 + 1);
       c.u.reserve(est); c.i.reserve(est); c.s.reserve(est); c.ts.reserve(est);
-      c.uk.reserve(est); c.ik.reserve(est);
+      c.uk.reserve(est); c.ik.reserve(est); c.hu.reserve(est); c.hi.reserve(est);
       std::vector<std::string> toks;
       std::string field;
       std::string_view f[4];
@@ -2713,8 +2707,15 @@ long long oryx_speed_parse(void* h, const char* buf, long long len, void* xm, vo
               c.owned.emplace_back(bk);
               bk = c.owned.back();
             }
-            c.u.push_back(X->row_of(a.data(), a.size(), RowMap::hash(a.data(), a.size())));
-            c.i.push_back(Y->row_of(bk.data(), bk.size(), RowMap::hash(bk.data(), bk.size())));
+            // the row-map probes wait for the second pass: the maps of a 20M-row store are
+            // far larger than the caches, and probing as each line is parsed left one miss
+            // in flight per thread; hashed and prefetched here, the chunk's misses overlap
+            const uint64_t ha = RowMap::hash(a.data(), a.size());
+            const uint64_t hb = RowMap::hash(bk.data(), bk.size());
+            X->prefetch(ha);
+            Y->prefetch(hb);
+            c.hu.push_back(ha);
+            c.hi.push_back(hb);
             c.s.push_back(sv);
             c.ts.push_back(tv);
             c.uk.push_back(a);
@@ -2725,6 +2726,14 @@ long long oryx_speed_parse(void* h, const char* buf, long long len, void* xm, vo
         }
         p = nl ? nl + 1 : end;
       }
+      const size_t m = c.hu.size();
+      c.u.resize(m);
+      c.i.resize(m);
+      for (size_t r = 0; r < m; ++r) {
+        c.u[r] = X->row_of(c.uk[r].data(), c.uk[r].size(), c.hu[r]);
+        c.i[r] = Y->row_of(c.ik[r].data(), c.ik[r].size(), c.hi[r]);
+        c.has_new |= (c.u[r] < 0) | (c.i[r] < 0);
+      }
     }
   });
   size_t n = 0;
@@ -2732,27 +2741,30 @@ long long oryx_speed_parse(void* h, const char* buf, long long len, void* xm, vo
   b->u.reserve(n); b->i.reserve(n); b->s.reserve(n); b->ts.reserve(n);
   b->uk.reserve(n); b->ik.reserve(n); b->uql.reserve(n); b->iql.reserve(n);
   for (auto& c : ch) {
+    const size_t base = b->u.size();
+    b->u.insert(b->u.end(), c.u.begin(), c.u.end());
+    b->i.insert(b->i.end(), c.i.begin(), c.i.end());
+    b->s.insert(b->s.end(), c.s.begin(), c.s.end());
+    b->ts.insert(b->ts.end(), c.ts.begin(), c.ts.end());
+    b->uk.insert(b->uk.end(), c.uk.begin(), c.uk.end());
+    b->ik.insert(b->ik.end(), c.ik.begin(), c.ik.end());
     b->uql.insert(b->uql.end(), c.uql.begin(), c.uql.end());
     b->iql.insert(b->iql.end(), c.iql.begin(), c.iql.end());
-    for (size_t r = 0; r < c.u.size(); ++r) {
-      int64_t ur = c.u[r], ir = c.i[r];
-      bool ins;
-      if (ur < 0) {
-        const int32_t k = b->nu_idx.find_or_add(c.uk[r], (int32_t)b->nu_keys.size(), &ins);
-        if (ins) b->nu_keys.push_back(c.uk[r]);
-        ur = -(int64_t)k - 1;
+    // keys the stores lack get batch codes in first-appearance order (chunks in order)
+    if (c.has_new) {
+      for (size_t r = 0; r < c.u.size(); ++r) {
+        bool ins;
+        if (c.u[r] < 0) {
+          const int32_t k = b->nu_idx.find_or_add(c.uk[r], (int32_t)b->nu_keys.size(), &ins);
+          if (ins) b->nu_keys.push_back(c.uk[r]);
+          b->u[base + r] = -(int64_t)k - 1;
+        }
+        if (c.i[r] < 0) {
+          const int32_t k = b->ni_idx.find_or_add(c.ik[r], (int32_t)b->ni_keys.size(), &ins);
+          if (ins) b->ni_keys.push_back(c.ik[r]);
+          b->i[base + r] = -(int64_t)k - 1;
+        }
       }
-      if (ir < 0) {
-        const int32_t k = b->ni_idx.find_or_add(c.ik[r], (int32_t)b->ni_keys.size(), &ins);
-        if (ins) b->ni_keys.push_back(c.ik[r]);
-        ir = -(int64_t)k - 1;
-      }
-      b->u.push_back(ur);
-      b->i.push_back(ir);
-      b->s.push_back(c.s[r]);
-      b->ts.push_back(c.ts[r]);
-      b->uk.push_back(c.uk[r]);
-      b->ik.push_back(c.ik[r]);
     }
     b->owned.push_back(std::move(c.owned));
   }
@@ -2781,81 +2793,113 @@ long long oryx_speed_counts(void* h, long long* out) {
   out[0] = (long long)b->u.size();
   out[1] = (long long)b->nu_keys.size();
   out[2] = (long long)b->ni_keys.size();
-  out[3] = (long long)b->au.size();
+  out[3] = (long long)b->rep.size();
   return out[0];
 }
 
 // Time-ordered aggregation per (user, item) (implicit: sum after the last delete, a trailing
-// delete drops the pair; explicit: the last value, NaN drops it), pairs ordered by (user,
-// item) with new keys after the store rows.  Writes the pairs' user / item rows (-1: not in
-// the store) and values; returns the number of pairs.
+// delete drops the pair; explicit: the last value, NaN drops it), pairs in the order of their
+// first event.  Writes the pairs' user / item rows (-1: not in the store) and values; returns
+// the number of pairs.  Pairs are found through a hash table over (user, item) rather than by
+// sorting the events: a micro-batch's pairs are nearly all distinct, so one probe per event
+// and a pass over the few repeated pairs replace four radix passes (0.38 -> ~0.05 ms per
+// 10k events on the 8-core host).
 long long oryx_speed_aggregate(void* h, int implicit, long long* out_u, long long* out_i,
                                double* out_s) {
   SpeedBatch* b = static_cast<SpeedBatch*>(h);
   const size_t n = b->u.size();
-  // ordering codes: store rows first, then the batch's new keys
-  int64_t mxu = 0, mxi = 0;
+  b->rep.clear();
+  if (n == 0) return 0;
+  size_t cap = 64;
+  while (cap < 2 * n) cap <<= 1;
+  std::vector<int32_t>& tab = b->tab;
+  tab.assign(cap, -1);
+  std::vector<int32_t>& first = b->first;   // first event of each pair
+  std::vector<int32_t>& cnt = b->cnt;       // events per pair
+  std::vector<int32_t>& pid = b->pid;       // pair of each event
+  first.clear();
+  cnt.clear();
+  pid.resize(n);
+  const int64_t* U = b->u.data();
+  const int64_t* I = b->i.data();
+  const size_t msk = cap - 1;
   for (size_t r = 0; r < n; ++r) {
-    mxu = std::max(mxu, b->u[r]);
-    mxi = std::max(mxi, b->i[r]);
-  }
-  const unsigned long long nu = (unsigned long long)mxu + 1 + b->nu_keys.size();
-  const unsigned long long ni = (unsigned long long)mxi + 1 + b->ni_keys.size();
-  auto code = [](int64_t v, int64_t mx) -> unsigned long long {
-    return v >= 0 ? (unsigned long long)v : (unsigned long long)(mx + 1 + (-v - 1));
-  };
-  // order: (user, item), then time, then arrival -- stable radix sorts
-  std::vector<uint64_t> key(n), tk(n);
-  long long tmin = std::numeric_limits<long long>::max(), tmax = std::numeric_limits<long long>::min();
-  for (size_t r = 0; r < n; ++r) {
-    key[r] = code(b->u[r], mxu) * ni + code(b->i[r], mxi);
-    tmin = std::min(tmin, b->ts[r]);
-    tmax = std::max(tmax, b->ts[r]);
-  }
-  const int kb = bit_width(nu * ni), tb = n ? bit_width((uint64_t)(tmax - tmin)) : 0;
-  std::vector<uint32_t> order(n);
-  for (size_t r = 0; r < n; ++r) order[r] = (uint32_t)r;
-  if (kb + tb <= 64) {
-    for (size_t r = 0; r < n; ++r) tk[r] = (key[r] << tb) | (uint64_t)(b->ts[r] - tmin);
-    radix_sort_by(tk, kb + tb, order);
-  } else {
-    for (size_t r = 0; r < n; ++r) tk[r] = (uint64_t)(b->ts[r] - tmin);
-    radix_sort_by(tk, tb, order);
-    radix_sort_by(key, kb, order);
-  }
-  b->au.clear(); b->ai.clear(); b->av.clear(); b->rep.clear();
-  for (size_t s0 = 0; s0 < n;) {
-    size_t e = s0 + 1;
-    while (e < n && key[order[e]] == key[order[s0]]) ++e;
-    double v;
-    if (implicit) {
-      size_t from = s0;
-      for (size_t k = s0; k < e; ++k)
-        if (std::isnan(b->s[order[k]])) from = k + 1;
-      if (from == e) {
-        v = std::numeric_limits<double>::quiet_NaN();
-      } else {
-        v = 0.0;
-        for (size_t k = from; k < e; ++k) v += b->s[order[k]];
+    size_t j = (size_t)pair_mix((uint64_t)U[r] * 0x9E3779B97F4A7C15ull ^ (uint64_t)I[r]) & msk;
+    int32_t p;
+    for (;; j = (j + 1) & msk) {
+      p = tab[j];
+      if (p < 0) {
+        p = (int32_t)first.size();
+        tab[j] = p;
+        first.push_back((int32_t)r);
+        cnt.push_back(0);
+        break;
       }
-    } else {
-      v = b->s[order[e - 1]];
+      const int32_t f = first[(size_t)p];
+      if (U[f] == U[r] && I[f] == I[r]) break;
     }
-    if (!std::isnan(v)) {
-      const uint32_t r = order[s0];
-      b->au.push_back(b->u[r] >= 0 ? b->u[r] : -1);
-      b->ai.push_back(b->i[r] >= 0 ? b->i[r] : -1);
-      b->av.push_back(v);
-      b->rep.push_back((int64_t)r);
+    pid[r] = p;
+    ++cnt[(size_t)p];
+  }
+  const size_t np = first.size();
+  std::vector<int64_t>& rep = b->rep;
+  rep.resize(np);
+  size_t m = 0;
+  auto emit = [&](int64_t r, double v) {
+    if (std::isnan(v)) return;
+    out_u[m] = U[r] >= 0 ? U[r] : -1;
+    out_i[m] = I[r] >= 0 ? I[r] : -1;
+    out_s[m] = v;
+    rep[m++] = r;
+  };
+  if (np == n) {
+    // every pair has one event: its value (NaN = a delete drops the pair either way)
+    for (size_t r = 0; r < n; ++r) emit((int64_t)r, b->s[r]);
+  } else {
+    // events grouped by pair, arrival order kept (counting sort), then each repeated pair's
+    // events put in time order (stable: equal timestamps stay in arrival order)
+    std::vector<int32_t>& start = b->start;
+    std::vector<int32_t>& ev = b->ev;
+    start.resize(np + 1);
+    start[0] = 0;
+    for (size_t p = 0; p < np; ++p) start[p + 1] = start[p] + cnt[p];
+    ev.resize(n);
+    {
+      std::vector<int32_t>& at = b->cnt;   // reused as the fill cursors
+      for (size_t p = 0; p < np; ++p) at[p] = start[p];
+      for (size_t r = 0; r < n; ++r) ev[(size_t)at[(size_t)pid[r]]++] = (int32_t)r;
     }
-    s0 = e;
+    const long long* T = b->ts.data();
+    const double* S = b->s.data();
+    for (size_t p = 0; p < np; ++p) {
+      int32_t* g0 = ev.data() + start[p];
+      int32_t* g1 = ev.data() + start[p + 1];
+      if (g1 - g0 == 1) {
+        emit(*g0, S[*g0]);
+        continue;
+      }
+      bool sorted = true;
+      for (int32_t* e = g0 + 1; e < g1; ++e) sorted &= T[e[-1]] <= T[*e];
+      if (!sorted)
+        std::stable_sort(g0, g1, [&](int32_t x, int32_t y) { return T[x] < T[y]; });
+      double v;
+      if (implicit) {
+        int32_t* from = g0;
+        for (int32_t* e = g0; e < g1; ++e)
+          if (std::isnan(S[*e])) from = e + 1;
+        if (from == g1) {
+          v = std::numeric_limits<double>::quiet_NaN();
+        } else {
+          v = 0.0;
+          for (int32_t* e = from; e < g1; ++e) v += S[*e];
+        }
+      } else {
+        v = S[g1[-1]];
+      }
+      emit(*g0, v);
+    }
   }
-  const size_t m = b->au.size();
-  for (size_t k = 0; k < m; ++k) {
-    out_u[k] = b->au[k];
-    out_i[k] = b->ai[k];
-    out_s[k] = b->av[k];
-  }
+  rep.resize(m);
   return (long long)m;
 }
 

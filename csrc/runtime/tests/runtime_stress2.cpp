@@ -37,6 +37,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
+#include <random>
+#include <cmath>
+#include <algorithm>
 #include <thread>
 #include <vector>
 
@@ -84,6 +88,17 @@ long long oryx_hostbuf_quiesce(long long timeout_ms);
 long long oryx_read_file_parallel(const char* path, char* out, long long n, int threads);
 long long oryx_encode_spans(const char* base, const long long* off, const int* len, long long n,
                             long long stride, long long* codes, long long* first_row);
+void* oryx_rowmap_new();
+void oryx_rowmap_free(void* h);
+void oryx_rowmap_set(void* h, const char* blob, const long long* ends, const long long* rows,
+                     long long n);
+void* oryx_speed_new();
+void oryx_speed_free(void* h);
+long long oryx_speed_parse(void* h, const char* buf, long long len, void* xm, void* ym,
+                           long long default_ts);
+long long oryx_speed_aggregate(void* h, int implicit, long long* out_u, long long* out_i,
+                               double* out_s);
+long long oryx_speed_counts(void* h, long long* out);
 }
 
 static std::atomic<int> g_errors{0};
@@ -794,6 +809,100 @@ static void test_keystores(const char* dir, const char* const* stores, int n_sto
   }
 }
 
+// ---------------------------------------------------------------- 7. speed micro-batch
+// oryx_speed_parse (threaded parse + prefetched row-map probes) and oryx_speed_aggregate (hash
+// grouping, time order per pair) against a std::map model of the same semantics: per (user,
+// item) in (timestamp, arrival) order, implicit = sum after the last delete (a trailing delete
+// drops the pair), explicit = the last value (a delete drops it).  Batches mix repeated pairs,
+// out-of-order timestamps, deletes, quoted lines and keys the stores lack.
+
+static void add_keys(void* m, const char* pre, int n, int stride) {
+  std::string blob;
+  std::vector<long long> ends, rows;
+  for (int j = 0; j < n; ++j) {
+    blob += pre + std::to_string(j);
+    ends.push_back((long long)blob.size());
+    rows.push_back((long long)j * stride + 1);
+  }
+  oryx_rowmap_set(m, blob.data(), ends.data(), rows.data(), n);
+}
+
+static void test_speed_batch() {
+  void* xm = oryx_rowmap_new();
+  void* ym = oryx_rowmap_new();
+  add_keys(xm, "U", 3000, 3);
+  add_keys(ym, "I", 800, 2);
+  void* sb = oryx_speed_new();
+  std::mt19937_64 g(7);
+  for (int round = 0; round < 6; ++round) {
+    const int n = round < 3 ? 25000 : 400 + 3000 * round;
+    const int nu = round % 2 ? 60 : 3300, ni = round % 2 ? 20 : 900;   // dense: many repeats
+    std::string buf;
+    struct Ev { std::string u, i; double v; long long t; };
+    std::vector<Ev> evs;
+    for (int j = 0; j < n; ++j) {
+      Ev e;
+      e.u = "U" + std::to_string(g() % nu);
+      e.i = "I" + std::to_string(g() % ni);
+      const bool del = g() % 29 == 0;
+      e.v = del ? std::nan("") : (double)(g() % 400) / 8.0;
+      e.t = 1000 + (long long)(g() % 50);
+      char vb[32];
+      if (del) vb[0] = 0; else snprintf(vb, sizeof(vb), "%.3f", e.v);
+      if (g() % 11 == 0)
+        buf += "\"" + e.u + "\",\"" + e.i + "\"," + vb + "," + std::to_string(e.t) + "\n";
+      else
+        buf += e.u + "," + e.i + "," + vb + "," + std::to_string(e.t) + "\n";
+      evs.push_back(e);
+    }
+    const long long got_n = oryx_speed_parse(sb, buf.data(), (long long)buf.size(), xm, ym, 0);
+    CHECK(got_n == n);
+    for (int implicit = 0; implicit < 2; ++implicit) {
+      // model: stable sort by time, then fold per pair
+      std::vector<int> ord(evs.size());
+      for (size_t k = 0; k < ord.size(); ++k) ord[k] = (int)k;
+      std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return evs[a].t < evs[b].t; });
+      std::map<std::pair<std::string, std::string>, double> want;
+      for (int k : ord) {
+        const auto key = std::make_pair(evs[k].u, evs[k].i);
+        const double v = evs[k].v;
+        if (!implicit) { want[key] = v; continue; }
+        auto it = want.find(key);
+        if (std::isnan(v)) want[key] = std::nan("");
+        else if (it == want.end() || std::isnan(it->second)) want[key] = v;
+        else it->second += v;
+      }
+      for (auto it = want.begin(); it != want.end();)
+        it = std::isnan(it->second) ? want.erase(it) : std::next(it);
+      std::vector<long long> u(evs.size()), i(evs.size());
+      std::vector<double> v(evs.size());
+      const long long m = oryx_speed_aggregate(sb, implicit, u.data(), i.data(), v.data());
+      long long c[4];
+      oryx_speed_counts(sb, c);
+      CHECK(c[3] == m);
+      // stores hold U0..U2999 (row 3j + 1) and I0..I799 (row 2j + 1): compare the pairs the
+      // stores hold by row, and the count of the rest
+      size_t known = 0;
+      std::map<std::pair<long long, long long>, double> got;
+      for (long long k = 0; k < m; ++k)
+        if (u[k] >= 0 && i[k] >= 0) got[{u[k], i[k]}] = v[k];
+      for (const auto& kv : want) {
+        const long long uj = std::stoll(kv.first.first.substr(1)),
+                        ij = std::stoll(kv.first.second.substr(1));
+        if (uj >= 3000 || ij >= 800) continue;
+        ++known;
+        auto it = got.find({3 * uj + 1, 2 * ij + 1});
+        CHECK(it != got.end() && std::fabs(it->second - kv.second) <= 1e-9 * (1 + std::fabs(kv.second)));
+      }
+      CHECK(got.size() == known);
+      CHECK((size_t)m == want.size());
+    }
+  }
+  oryx_speed_free(sb);
+  oryx_rowmap_free(xm);
+  oryx_rowmap_free(ym);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: runtime_stress2 <dir>\n");
@@ -809,6 +918,8 @@ int main(int argc, char** argv) {
   printf("thread pool: errors %d\n", g_errors.load());
   test_hostbuf(argv[1]);
   printf("host buffers / parallel read / span encoding: errors %d\n", g_errors.load());
+  test_speed_batch();
+  printf("speed micro-batch parse / aggregate: errors %d\n", g_errors.load());
   if (argc >= 4) {
     test_https(argv[2], argv[3]);
     printf("https: errors %d\n", g_errors.load());
