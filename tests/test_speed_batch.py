@@ -216,3 +216,47 @@ def test_leaf_update_formatter_matches_json():
     want = [json.dumps([t, ids[k], m, c], separators=(",", ":"))
             for t, k, m, c in zip(trees.tolist(), idx.tolist(), means.tolist(), cnt.tolist())]
     assert list(blk) == want
+
+
+def test_publish_blocks_order_errors_and_reuse():
+    """layers.speed.publish_blocks: blocks land in order through the persistent writer, at
+    most two wait, a failing append surfaces on the caller's thread and stops the rest, and
+    the writer serves the next call afterwards."""
+    import pytest
+    from oryx_amd.api import MessageBlock
+    from oryx_amd.layers.speed import publish_blocks
+
+    class Prod:
+        def __init__(self, fail_at=None):
+            self.got, self.fail_at = [], fail_at
+
+        def send_block(self, key, b):
+            if self.fail_at is not None and len(self.got) == self.fail_at:
+                raise IOError("disk full")
+            self.got.append(list(b))
+
+        def send_many(self, pairs):
+            self.send_block("UP", [m for _, m in pairs])
+
+    def block(msgs):
+        ends = np.cumsum([len(m) + 1 for m in msgs]) - 1
+        return MessageBlock(("\n".join(msgs) + "\n").encode(), ends)
+
+    def blocks(n, made):
+        for j in range(n):
+            made.append(j)
+            msgs = ["m%d-%d" % (j, k) for k in range(3)]
+            yield block(msgs) if j % 2 else msgs
+
+    p = Prod()
+    st: dict = {}
+    assert publish_blocks(p, blocks(7, []), st) == 21
+    assert p.got == [["m%d-%d" % (j, k) for k in range(3)] for j in range(7)]
+    assert st["write_ms"] >= 0 and st["tail_ms"] >= 0
+    bad = Prod(fail_at=2)
+    made: list = []
+    with pytest.raises(IOError):
+        publish_blocks(bad, blocks(50, made), {})
+    assert len(bad.got) == 2 and len(made) < 50
+    p2 = Prod()
+    assert publish_blocks(p2, blocks(3, []), None) == 9 and len(p2.got) == 3
