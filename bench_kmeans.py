@@ -182,6 +182,7 @@ def main(argv=None) -> int:
             "init_ms": init_ms, "rescored_points_per_step": rescored,
             "speed_layer_update_ms": speed["median_ms"] if speed else None,
             "speed_layer_update_p90_ms": speed["p90_ms"] if speed else None,
+            "speed_layer_phase_ms": speed.get("phase_ms") if speed else None,
             "speed_layer_reps": speed["reps"] if speed else None,
             "speed_layer_events": args.speed_events,
             "speed_layer_messages": speed["messages"] if speed else None,

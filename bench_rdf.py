@@ -170,6 +170,7 @@ def main(argv=None) -> int:
             "nodes": sum(count_nodes(r) for r in trained.roots),
             "speed_layer_update_ms": speed_ms, "speed_layer_events": args.speed_events,
             "speed_layer_update_p90_ms": speed["p90_ms"] if speed else None,
+            "speed_layer_phase_ms": speed.get("phase_ms") if speed else None,
             "speed_layer_reps": speed["reps"] if speed else None,
             "speed_layer_messages": speed["messages"] if speed else None,
             "speed_layer_path": "RDFSpeedModelManager.build_updates + the UP messages' append "

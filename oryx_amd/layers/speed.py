@@ -119,6 +119,7 @@ def measure_intervals(manager, dataset: Dataset, producer, reps: int = 12, warmu
     per-rep times and the messages per interval (the benchmarks' speed-layer records)."""
     import numpy as np
     times = []
+    phases = []
     sent = 0
     dev = getattr(manager, "device", None)
     for rep in range(warmup + reps):
@@ -133,8 +134,10 @@ def measure_intervals(manager, dataset: Dataset, producer, reps: int = 12, warmu
         blocks = getattr(manager, "build_update_blocks", None)
         if blocks is not None:
             sent = publish_blocks(producer, blocks(dataset))
+            t1 = time.perf_counter()
         else:
             updates = manager.build_updates(dataset)
+            t1 = time.perf_counter()
             if isinstance(updates, MessageBlock):
                 producer.send_block("UP", updates)
             elif updates:
@@ -143,9 +146,14 @@ def measure_intervals(manager, dataset: Dataset, producer, reps: int = 12, warmu
         producer.flush()
         if rep >= warmup:
             times.append((time.perf_counter() - t0) * 1e3)
+            ph = dict(getattr(manager, "last_phase_ms", None) or {})
+            ph["append"] = (time.perf_counter() - t1) * 1e3
+            phases.append(ph)
     del dev
+    keys = sorted({k for p in phases for k in p})
     return {"median_ms": float(np.median(times)), "p90_ms": float(np.percentile(times, 90)),
-            "reps": reps, "times_ms": times, "messages": int(sent)}
+            "reps": reps, "times_ms": times, "messages": int(sent),
+            "phase_ms": {k: float(np.median([p.get(k, 0.0) for p in phases])) for k in keys}}
 
 
 class SpeedLayer(AbstractLayer):

@@ -60,6 +60,7 @@ class KMeansSpeedModelManager(SpeedModelManager):
     def __init__(self, config):
         self.input_schema = InputSchema(config)
         self.model: Optional[KMeansSpeedModel] = None
+        self.last_phase_ms: dict = {}
 
     def consume(self, updates, context=None) -> None:
         for km in updates:
@@ -108,7 +109,9 @@ class KMeansSpeedModelManager(SpeedModelManager):
         clusters (ClusterInfo.update's formula, vectorised), and the messages formatted
         natively (ingest.format_cluster_updates: the same bytes as text.join_json) in one
         MessageBlock."""
+        import time
         from ...textlines import TextLines
+        t0 = time.perf_counter()
         cs = self.model.clusters
         lines = new_data.values()
         if not isinstance(lines, TextLines):
@@ -119,6 +122,7 @@ class KMeansSpeedModelManager(SpeedModelManager):
         x = block.predictors(self.input_schema)
         if x.shape[0] == 0:
             return []
+        t1 = time.perf_counter()
         idx, _ = cs.nearest_batch_device(x)
         centers, _, counts = cs.device_state()
         k, d = centers.shape
@@ -135,9 +139,18 @@ class KMeansSpeedModelManager(SpeedModelManager):
         pos_h = touched.cpu().numpy()
         new_h = new_c.cpu().numpy()
         tot_h = total.cpu().numpy()
+        t2 = time.perf_counter()
         cs.set_many(pos_h.tolist(), new_h, tot_h.tolist())
         ids = np.array([cs.clusters[p].id for p in pos_h.tolist()], dtype=np.int64)
-        return ingest.format_cluster_updates(ids, new_h, tot_h)
+        t3 = time.perf_counter()
+        out = ingest.format_cluster_updates(ids, new_h, tot_h)
+        # milliseconds per phase of the last micro-batch (parse: text -> device matrix;
+        # assign_update: nearest clusters, sums, running means, results to the host;
+        # set: the model's host / device state; format: the UP messages)
+        self.last_phase_ms = {"parse": (t1 - t0) * 1e3, "assign_update": (t2 - t1) * 1e3,
+                              "set": (t3 - t2) * 1e3,
+                              "format": (time.perf_counter() - t3) * 1e3}
+        return out
 
     def close(self) -> None:
         pass
