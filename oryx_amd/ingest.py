@@ -582,7 +582,9 @@ def format_cluster_updates(ids, centers, counts):
     ends = np.empty(n, dtype=np.int64)
     cap = n * (52 + 25 * d)
     while True:
-        out = np.empty(cap, dtype=np.uint8)
+        # (a reused pinned block on a GPU host: a fresh 6 MB array faulted in its pages on
+        # every speed-layer micro-batch)
+        out = _host_buffer(cap)
         used = native.runtime().oryx_format_cluster_updates(
             _ptr(ids), _ptr(centers), _ptr(counts), n, d, _ptr(out), cap, _ptr(ends))
         if used >= 0:

@@ -140,7 +140,8 @@ class KMeansSpeedModelManager(SpeedModelManager):
         new_h = new_c.cpu().numpy()
         tot_h = total.cpu().numpy()
         t2 = time.perf_counter()
-        cs.set_many(pos_h.tolist(), new_h, tot_h.tolist())
+        cs.set_many(pos_h.tolist(), new_h, tot_h.tolist(),
+                    device_update=(touched, new_c, total))
         ids = np.array([cs.clusters[p].id for p in pos_h.tolist()], dtype=np.int64)
         t3 = time.perf_counter()
         out = ingest.format_cluster_updates(ids, new_h, tot_h)

@@ -334,22 +334,34 @@ def test_speed_manager_device_path_matches_host(cuda):
     conf = _conf(**{"oryx__input-schema__feature-names": names,
                     "oryx__input-schema__categorical-features": "[]"})
     centers = g.standard_normal((k, d)) * 3
-    pts = centers[g.integers(0, k, n)] + g.standard_normal((n, d))
-    lines = [",".join(repr(float(v)) for v in row) for row in pts]
-    outs = []
+    batches = []
+    for _ in range(3):
+        pts = centers[g.integers(0, k, n)] + g.standard_normal((n, d))
+        batches.append([",".join(repr(float(v)) for v in row) for row in pts])
+    outs, models = [], []
     for device in (torch.device(cuda), None):
         m = KMeansSpeedModelManager(conf)
         m.model = KMeansSpeedModel([ClusterInfo(10 + j, centers[j], 1 + j % 7)
                                     for j in range(k)], device)
         if device is None:
             m.model.clusters.device = None
-        outs.append([json.loads(u) for u in m.build_updates(Dataset([(None, l)
-                                                                       for l in lines]))])
-    dev, host = outs
-    assert [u[0] for u in dev] == [u[0] for u in host]
-    assert [u[2] for u in dev] == [u[2] for u in host]
-    np.testing.assert_allclose(np.array([u[1] for u in dev]), np.array([u[1] for u in host]),
-                               rtol=1e-12, atol=1e-12)
+        # consecutive micro-batches: the device path updates its device centers / counts in
+        # place after the first one
+        outs.append([[json.loads(u) for u in m.build_updates(Dataset([(None, l) for l in b]))]
+                     for b in batches])
+        models.append(m.model.clusters)
+    for dev, host in zip(*outs):
+        assert [u[0] for u in dev] == [u[0] for u in host]
+        assert [u[2] for u in dev] == [u[2] for u in host]
+        np.testing.assert_allclose(np.array([u[1] for u in dev]),
+                                   np.array([u[1] for u in host]), rtol=1e-11, atol=1e-11)
+    # the in-place device state is the state a rebuild from the host clusters gives
+    cs = models[0]
+    c, ct, cnt = cs.device_state()
+    np.testing.assert_array_equal(c.cpu().numpy(), cs.centers())
+    np.testing.assert_array_equal(ct.cpu().numpy(), cs.centers().T)
+    assert cnt.cpu().tolist() == [ci.count for ci in cs.clusters]
+    np.testing.assert_allclose(cs.centers(), models[1].centers(), rtol=1e-11, atol=1e-11)
 
 
 # ---------------------------------------------------------------- serving
