@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import ctypes
 import logging
+import os
 import threading
 import weakref
 from collections import OrderedDict
@@ -223,6 +224,11 @@ def h2d(buf: np.ndarray, off: int, nbytes: int, dst: torch.Tensor,
     # (the caching pinned allocator holds each staging block until its last copy completes)
 
 
+# average line length from which the device parse takes a wave per line instead of a thread
+# (ORYX_CSV_WIDE_MIN_BYTES; a huge value keeps the thread kernel)
+WIDE_LINE_MIN_BYTES = int(os.environ.get("ORYX_CSV_WIDE_MIN_BYTES", "192"))
+
+
 def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: InputSchema,
                   dtype: torch.dtype, device, laps: Optional[Dict[str, float]] = None
                   ) -> Optional[Tuple[torch.Tensor, Dict[int, List[str]]]]:
@@ -269,11 +275,19 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     sp_len = torch.empty((n, max(S, 1)), dtype=torch.int32, device=device)
     bad = torch.empty(n, dtype=torch.uint8, device=device)
     n_bad = torch.zeros(1, dtype=torch.int32, device=device)
-    native.check(native.require_kernels().oryx_csv_lines_to_matrix(
-        text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, is_num.data_ptr(),
-        out_col.data_ptr(), F, out.data_ptr(), int(dtype == torch.float64), sp_off.data_ptr(),
-        sp_len.data_ptr(), S, bad.data_ptr(), n_bad.data_ptr(), native.stream_ptr(device)),
-        "oryx_csv_lines_to_matrix")
+    lib = native.require_kernels()
+    if S == 0 and nbytes >= WIDE_LINE_MIN_BYTES * n:
+        # long all-numeric lines: one wave per line (csv.hip csv_wide_kernel)
+        native.check(lib.oryx_csv_wide_lines_to_matrix(
+            text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, out_col.data_ptr(),
+            F, out.data_ptr(), int(dtype == torch.float64), bad.data_ptr(), n_bad.data_ptr(),
+            native.stream_ptr(device)), "oryx_csv_wide_lines_to_matrix")
+    else:
+        native.check(lib.oryx_csv_lines_to_matrix(
+            text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, is_num.data_ptr(),
+            out_col.data_ptr(), F, out.data_ptr(), int(dtype == torch.float64),
+            sp_off.data_ptr(), sp_len.data_ptr(), S, bad.data_ptr(), n_bad.data_ptr(),
+            native.stream_ptr(device)), "oryx_csv_lines_to_matrix")
     values: Dict[int, List[str]] = {}
     bad_lines = int(n_bad.item())
     lap("kernel")

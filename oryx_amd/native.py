@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 27
+KERNELS_ABI_VERSION = 28
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -280,6 +280,8 @@ def _load_kernels():
                                          c_vp, c_vp, c_vp])
     _sig(lib, "oryx_csv_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp, c_i,
                                                 c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_csv_wide_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_i,
+                                                     c_vp, c_i, c_vp, c_vp, c_vp])
     # peer-push all-gather (ipc_allgather.hip; parallel/ipc.py IpcAllGather)
     _sig(lib, "oryx_ipc_xcd_probe", c_i, [c_vp, c_vp, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_ipc_gather_flag_bytes", c_ll, [])

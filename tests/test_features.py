@@ -93,14 +93,18 @@ def _numeric_lines(rs, n, F):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wide", [False, True])
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
-def test_device_csv_parse_matches_host_bitwise(cuda, dtype, monkeypatch):
+def test_device_csv_parse_matches_host_bitwise(cuda, dtype, wide, monkeypatch):
     """csv.hip on the device == the host parser, bitwise (NaN where empty), for numeric rows
     with signs, exponents, 17-digit values, empty fields, trailing commas and CR line ends;
-    lines outside the fast path are parsed on the host and written in (same results)."""
+    lines outside the fast path are parsed on the host and written in (same results).  Both
+    kernels: one thread per line, and one wave per line (``wide``: quoted fields and a line
+    past the wave's LDS capacity go to the host too)."""
     from oryx_amd import native
     from oryx_amd.models import features as feats
     native.require_kernels()
+    monkeypatch.setattr(feats, "WIDE_LINE_MIN_BYTES", 0 if wide else 1 << 40)
     rs = np.random.default_rng(11)
     F = 37
     schema = _numeric_schema(F)
@@ -113,6 +117,9 @@ def test_device_csv_parse_matches_host_bitwise(cuda, dtype, monkeypatch):
     for j, l in zip(range(3, 5000, 125), long):
         mixed[j] = l
     mixed[9] = "1.5E+30," + ",".join(["1"] * (F - 1))
+    mixed[11] = '"1.5",' + ",".join(["-2"] * (F - 1))                # quoted field
+    mixed[12] = "1." + "0" * 13000 + "," + ",".join(["3"] * (F - 1))  # past 12 KB
+    mixed[4999] = ",".join(["7"] * F)                                # the last line
     variants = {"plain": lines, "mixed": mixed}
     for name, ls in variants.items():
         tl = TextLines.from_strings(ls)
