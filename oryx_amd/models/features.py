@@ -322,7 +322,8 @@ def _python_block(lines: Sequence[str], schema: InputSchema, dtype: torch.dtype
     """The general parser (``parse_input_line``: quotes, escapes, JSON arrays)."""
     from ..utils import text
     F = schema.get_num_features()
-    rows = [text.parse_input_line(l) for l in lines]
+    # (a CRLF line's CR is not part of its last field, as for the native parsers)
+    rows = [text.parse_input_line(l[:-1] if l.endswith("\r") else l) for l in lines]
     rows = [r for r in rows if r is not None]
     np_dtype = np.float32 if dtype == torch.float32 else np.float64
     full = np.empty((len(rows), F), dtype=np_dtype)

@@ -69,6 +69,17 @@ def _numeric_schema(n):
     return InputSchema(conf)
 
 
+def test_general_parser_takes_crlf_lines():
+    """A block the native parser refuses (a quoted field) goes through the general parser,
+    which strips a CRLF line's CR as the native parsers do (it read '\r' as a value)."""
+    schema = _numeric_schema(3)
+    tl = TextLines.from_strings(['"1.5",2,3\r', "4,5,\r", "7,8,9"])
+    blk = parse_features(tl, schema, torch.device("cpu"), dtype=torch.float64)
+    got = blk.full.numpy()
+    assert got[0].tolist() == [1.5, 2.0, 3.0] and got[2].tolist() == [7.0, 8.0, 9.0]
+    assert got[1][:2].tolist() == [4.0, 5.0] and np.isnan(got[1][2])
+
+
 def _numeric_lines(rs, n, F):
     out = []
     for j in range(n):
@@ -99,8 +110,8 @@ def test_device_csv_parse_matches_host_bitwise(cuda, dtype, wide, monkeypatch):
     """csv.hip on the device == the host parser, bitwise (NaN where empty), for numeric rows
     with signs, exponents, 17-digit values, empty fields, trailing commas and CR line ends;
     lines outside the fast path are parsed on the host and written in (same results).  Both
-    kernels: one thread per line, and one wave per line (``wide``: quoted fields and a line
-    past the wave's LDS capacity go to the host too)."""
+    kernels: one thread per line, and one wave per line (``wide``: a line past the wave's LDS
+    capacity goes to the host too)."""
     from oryx_amd import native
     from oryx_amd.models import features as feats
     native.require_kernels()
@@ -117,7 +128,6 @@ def test_device_csv_parse_matches_host_bitwise(cuda, dtype, wide, monkeypatch):
     for j, l in zip(range(3, 5000, 125), long):
         mixed[j] = l
     mixed[9] = "1.5E+30," + ",".join(["1"] * (F - 1))
-    mixed[11] = '"1.5",' + ",".join(["-2"] * (F - 1))                # quoted field
     mixed[12] = "1." + "0" * 13000 + "," + ",".join(["3"] * (F - 1))  # past 12 KB
     mixed[4999] = ",".join(["7"] * F)                                # the last line
     variants = {"plain": lines, "mixed": mixed}
