@@ -225,8 +225,12 @@ def h2d(buf: np.ndarray, off: int, nbytes: int, dst: torch.Tensor,
 
 
 # average line length from which the device parse takes a wave per line instead of a thread
-# (ORYX_CSV_WIDE_MIN_BYTES; a huge value keeps the thread kernel)
+# (ORYX_CSV_WIDE_MIN_BYTES; a huge value keeps the thread kernel), for up to WIDE_MAX_LINES
+# lines: a speed-layer micro-batch of 10k 2.6 KB lines parses in 0.31 ms instead of 1.41 ms
+# (one thread per line fills 157 waves of the chip), but 12.5M such lines take 0.20 s against
+# the thread kernel's 0.13 s (profiles/r6_km_speed_prof_v2.json, r6_bb_kmeans_v3.json)
 WIDE_LINE_MIN_BYTES = int(os.environ.get("ORYX_CSV_WIDE_MIN_BYTES", "192"))
+WIDE_MAX_LINES = int(os.environ.get("ORYX_CSV_WIDE_MAX_LINES", str(1 << 20)))
 
 
 def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: InputSchema,
@@ -276,7 +280,7 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     bad = torch.empty(n, dtype=torch.uint8, device=device)
     n_bad = torch.zeros(1, dtype=torch.int32, device=device)
     lib = native.require_kernels()
-    if S == 0 and nbytes >= WIDE_LINE_MIN_BYTES * n:
+    if S == 0 and nbytes >= WIDE_LINE_MIN_BYTES * n and n <= WIDE_MAX_LINES:
         # long all-numeric lines: one wave per line (csv.hip csv_wide_kernel)
         native.check(lib.oryx_csv_wide_lines_to_matrix(
             text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, out_col.data_ptr(),
