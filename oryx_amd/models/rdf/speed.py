@@ -72,6 +72,10 @@ class RDFSpeedModelManager(SpeedModelManager):
         self.input_schema = InputSchema(config)
         self.model: Optional[RDFSpeedModel] = None
         self.device = _device()
+        # milliseconds per phase of the last micro-batch on the GPU path (parse: text ->
+        # encoded host rows; leaves: upload + forest traversal; counts_format: per-leaf counts
+        # or sums, results to the host, the UP messages)
+        self.last_phase_ms: dict = {}
 
     def consume(self, updates, context=None) -> None:
         for km in updates:
@@ -93,6 +97,8 @@ class RDFSpeedModelManager(SpeedModelManager):
         model = self.model
         if model is None:
             return []
+        import time
+        t0 = time.perf_counter()
         schema = self.input_schema
         values = new_data.values()
         if not len(values):
@@ -106,6 +112,7 @@ class RDFSpeedModelManager(SpeedModelManager):
             if schema.is_classification() else 0
         flat = model.flat(self.device, C)
         if self.device.type == "cuda":
+            self.last_phase_ms = {"parse": (time.perf_counter() - t0) * 1e3}
             return self._updates_device(model, flat, full, target, C)
         leaves = rdf_ops.forest_leaves(flat, torch.from_numpy(full).to(self.device)).cpu() \
             .numpy()                                             # [n, T]
@@ -148,6 +155,9 @@ class RDFSpeedModelManager(SpeedModelManager):
         """Leaves by the traversal kernel, per-(leaf, class) counts (or per-leaf sums) by one
         bincount on the device, the touched leaves' messages formatted natively
         (``ingest.format_leaf_updates``): one MessageBlock."""
+        import time
+        t0 = time.perf_counter()
+        ph = self.last_phase_ms
         dev = self.device
         X = torch.from_numpy(np.ascontiguousarray(full)).to(dev)
         leaves = rdf_ops.forest_leaves(flat, X)                      # [n, T] int64
@@ -156,6 +166,8 @@ class RDFSpeedModelManager(SpeedModelManager):
         leaves, tv = leaves[ok], tv[ok]
         if leaves.numel() == 0:
             return []
+        t1 = time.perf_counter()
+        ph["leaves"] = (t1 - t0) * 1e3
         n_nodes = len(flat.nodes)
         T = leaves.shape[1]
         if C > 0:
@@ -165,8 +177,10 @@ class RDFSpeedModelManager(SpeedModelManager):
             touched = torch.nonzero(cnt.sum(1)).flatten()
             t_h = touched.cpu().numpy()
             c_h = cnt[touched].cpu().numpy()
-            return ingest.format_leaf_updates(model.tree_of[t_h], model.id_blob,
-                                              model.id_ends, t_h, c_h, C)
+            out = ingest.format_leaf_updates(model.tree_of[t_h], model.id_blob,
+                                             model.id_ends, t_h, c_h, C)
+            ph["counts_format"] = (time.perf_counter() - t1) * 1e3
+            return out
         flat_leaf = leaves.reshape(-1)
         vals = tv[:, None].expand(-1, T).reshape(-1)
         cnt = torch.bincount(flat_leaf, minlength=n_nodes)
@@ -176,8 +190,10 @@ class RDFSpeedModelManager(SpeedModelManager):
         t_h = touched.cpu().numpy()
         n_h = cnt[touched].cpu().numpy()
         m_h = (sums[touched] / cnt[touched].to(torch.float64)).cpu().numpy()
-        return ingest.format_leaf_updates(model.tree_of[t_h], model.id_blob, model.id_ends,
-                                          t_h, n_h, 0, m_h)
+        out = ingest.format_leaf_updates(model.tree_of[t_h], model.id_blob, model.id_ends,
+                                         t_h, n_h, 0, m_h)
+        ph["counts_format"] = (time.perf_counter() - t1) * 1e3
+        return out
 
     def close(self) -> None:
         pass
