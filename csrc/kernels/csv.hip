@@ -166,8 +166,9 @@ __global__ __launch_bounds__(256) void csv_lines_kernel(const uint4* __restrict_
 // with coalesced 16-byte loads, each lane counts the commas of a 1/64 slice, a wave prefix sum
 // numbers the fields, and every lane parses the fields that start in its slice -- with the
 // thread kernel's exact number rules (same fast path, same flags), so the matrix is bitwise
-// the host parser's.  All-numeric schemas only; a line longer than kWideLineCap, or with quotes,
-// escapes, a leading '[' or a field count other than F is flagged for the host like above.
+// the host parser's; a categorical field's span goes to span_off / span_len (slot
+// span_slot[f]) and NaN to the matrix, as above.  A line longer than kWideLineCap, or with
+// quotes, escapes, a leading '[' or a field count other than F is flagged for the host.
 constexpr int kWideLineCap = 12288;
 
 // the wave's LDS writes visible to its other lanes (LDS operations of one wave stay in order;
@@ -247,6 +248,9 @@ __global__ __launch_bounds__(256) void csv_wide_kernel(const uint4* __restrict__
                                                        long long n, int F,
                                                        const int* __restrict__ out_col, int P,
                                                        T* __restrict__ out,
+                                                       const int* __restrict__ span_slot,
+                                                       long long* __restrict__ span_off,
+                                                       int* __restrict__ span_len, int S,
                                                        unsigned char* __restrict__ bad,
                                                        int* n_bad) {
   __shared__ uint4 sm[4][kWideLineCap / 16 + 1];
@@ -283,17 +287,26 @@ __global__ __launch_bounds__(256) void csv_wide_kernel(const uint4* __restrict__
       fields = __shfl(incl, 63, 64) + 1;
       if (fields == F) {
         T* o = out + i * P;
-        double v;
-        if (lane == 0) {   // field 0 starts the line
-          lane_ok &= wide_field(s, 0, L, &v);
-          if (out_col[0] >= 0) o[out_col[0]] = (T)v;
-        }
-        int f = incl - commas;   // commas before this slice
+        // field f starting at q: a number, or a categorical span (NaN in the matrix)
+        auto field = [&](int f, int q) {
+          double v;
+          const int slot = span_slot[f];
+          if (slot >= 0) {
+            int e = q;
+            while (e < L && s[e] != ',') ++e;
+            span_off[i * S + slot] = p0 + q;
+            span_len[i * S + slot] = e - q;
+            v = __builtin_nan("");
+          } else {
+            lane_ok &= wide_field(s, q, L, &v);
+          }
+          if (out_col[f] >= 0) o[out_col[f]] = (T)v;
+        };
+        if (lane == 0) field(0, 0);   // field 0 starts the line
+        int f = incl - commas;        // commas before this slice
         for (int q = a; q < b; ++q) {
           if (s[q] != ',') continue;
-          ++f;                     // field f starts after this comma
-          lane_ok &= wide_field(s, q + 1, L, &v);
-          if (out_col[f] >= 0) o[out_col[f]] = (T)v;
+          field(++f, q + 1);          // field f starts after this comma
         }
       }
     }
@@ -478,12 +491,13 @@ int oryx_csv_lines_to_matrix(const void* buf, const long long* starts, const lon
   return oryx_check_launch();
 }
 
-// All-numeric wide lines (see csv_wide_kernel): arguments as oryx_csv_lines_to_matrix without
-// the categorical spans.
+// Wide lines (see csv_wide_kernel): arguments as oryx_csv_lines_to_matrix, with span_slot[F]
+// (the span column of each categorical field, -1 for numeric ones) in place of is_num.
 int oryx_csv_wide_lines_to_matrix(const void* buf, const long long* starts,
                                   const long long* ends, long long n, int F, const int* out_col,
-                                  int P, void* out, int is_f64, unsigned char* bad, int* n_bad,
-                                  void* stream) {
+                                  int P, void* out, int is_f64, const int* span_slot,
+                                  long long* span_off, int* span_len, int S, unsigned char* bad,
+                                  int* n_bad, void* stream) {
   if (n <= 0) return ORYX_OK;
   if (F <= 0 || P <= 0 || (reinterpret_cast<uintptr_t>(buf) & 15)) return ORYX_EINVAL;
   long long blocks = (n + 3) / 4;
@@ -492,11 +506,11 @@ int oryx_csv_wide_lines_to_matrix(const void* buf, const long long* starts,
   if (is_f64)
     hipLaunchKernelGGL(csv_wide_kernel<double>, dim3((unsigned)blocks), dim3(256), 0, s,
                        static_cast<const uint4*>(buf), starts, ends, n, F, out_col, P,
-                       static_cast<double*>(out), bad, n_bad);
+                       static_cast<double*>(out), span_slot, span_off, span_len, S, bad, n_bad);
   else
     hipLaunchKernelGGL(csv_wide_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s,
                        static_cast<const uint4*>(buf), starts, ends, n, F, out_col, P,
-                       static_cast<float*>(out), bad, n_bad);
+                       static_cast<float*>(out), span_slot, span_off, span_len, S, bad, n_bad);
   return oryx_check_launch();
 }
 

@@ -280,12 +280,15 @@ def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: 
     bad = torch.empty(n, dtype=torch.uint8, device=device)
     n_bad = torch.zeros(1, dtype=torch.int32, device=device)
     lib = native.require_kernels()
-    if S == 0 and nbytes >= WIDE_LINE_MIN_BYTES * n and n <= WIDE_MAX_LINES:
-        # long all-numeric lines: one wave per line (csv.hip csv_wide_kernel)
+    if nbytes >= WIDE_LINE_MIN_BYTES * n and n <= WIDE_MAX_LINES:
+        # long lines: one wave per line (csv.hip csv_wide_kernel)
+        slot = torch.tensor([cats.index(f) if f in cats else -1 for f in range(F)],
+                            dtype=torch.int32, device=device)
         native.check(lib.oryx_csv_wide_lines_to_matrix(
             text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, out_col.data_ptr(),
-            F, out.data_ptr(), int(dtype == torch.float64), bad.data_ptr(), n_bad.data_ptr(),
-            native.stream_ptr(device)), "oryx_csv_wide_lines_to_matrix")
+            F, out.data_ptr(), int(dtype == torch.float64), slot.data_ptr(), sp_off.data_ptr(),
+            sp_len.data_ptr(), S, bad.data_ptr(), n_bad.data_ptr(), native.stream_ptr(device)),
+            "oryx_csv_wide_lines_to_matrix")
     else:
         native.check(lib.oryx_csv_lines_to_matrix(
             text.data_ptr(), d_starts.data_ptr(), d_ends.data_ptr(), n, F, is_num.data_ptr(),

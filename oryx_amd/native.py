@@ -281,7 +281,8 @@ def _load_kernels():
     _sig(lib, "oryx_csv_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp, c_i,
                                                 c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_csv_wide_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_i,
-                                                     c_vp, c_i, c_vp, c_vp, c_vp])
+                                                     c_vp, c_i, c_vp, c_vp, c_vp, c_i, c_vp,
+                                                     c_vp, c_vp])
     # peer-push all-gather (ipc_allgather.hip; parallel/ipc.py IpcAllGather)
     _sig(lib, "oryx_ipc_xcd_probe", c_i, [c_vp, c_vp, c_ll, c_vp, c_vp])
     _sig(lib, "oryx_ipc_gather_flag_bytes", c_ll, [])

@@ -146,12 +146,16 @@ def test_device_csv_parse_matches_host_bitwise(cuda, dtype, wide, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_device_csv_parse_with_categoricals_matches_host(cuda, monkeypatch):
+@pytest.mark.parametrize("wide", [False, True])
+def test_device_csv_parse_with_categoricals_matches_host(cuda, wide, monkeypatch):
     """Categorical fields through the device parser: spans on the device, codes on the host
     -- the same matrix (bitwise) and the same distinct values in first-appearance order as the
-    host parser, over several segments and through the resident history."""
+    host parser, over several segments and through the resident history; by either kernel
+    (one thread or one wave per line)."""
     from oryx_amd import native
+    from oryx_amd.models import features as feats
     native.require_kernels()
+    monkeypatch.setattr(feats, "WIDE_LINE_MIN_BYTES", 0 if wide else 1 << 40)
     rs = np.random.default_rng(5)
     schema = _schema()
     parts = []
