@@ -106,10 +106,13 @@ class RDFSpeedModelManager(SpeedModelManager):
         C = model.encodings.get_value_count(schema.get_target_feature_index()) \
             if schema.is_classification() else 0
         if self.device.type == "cuda":
+            self.last_phase_ms = {}
             got = self._parse_device(values, model)
             if got is not None:
+                t1 = time.perf_counter()
                 flat = model.flat(self.device, C)
-                self.last_phase_ms = {"parse": (time.perf_counter() - t0) * 1e3}
+                self.last_phase_ms["flat"] = (time.perf_counter() - t1) * 1e3
+                self.last_phase_ms["parse"] = (t1 - t0) * 1e3
                 return self._updates_device(model, flat, got[0], got[1], C)
         parsed = parse_csv_block(values, schema, model.encodings)
         if parsed is None:
@@ -170,8 +173,11 @@ class RDFSpeedModelManager(SpeedModelManager):
         schema = self.input_schema
         if not isinstance(values, TextLines) or not _device_ok(schema, self.device):
             return None
+        import time
+        t0 = time.perf_counter()
         blk = parse_features(values, schema, self.device, torch.float64)
         full = blk.full.to(self.device, torch.float64)
+        self.last_phase_ms["parse_text"] = (time.perf_counter() - t0) * 1e3
         if full.shape[0] != len(values):
             return None                      # (an empty line the parser skipped)
         for f, vs in (blk.values or {}).items():
