@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 import threading
 from typing import Iterable, Iterator, List, Optional, Set
 
@@ -34,6 +35,10 @@ from ...ops import als as als_ops, textfmt
 from ...utils import mathx, pmml as pmmlu, text
 from .batch import aggregate_scores
 from .common import FeatureVectors
+
+# queue the Gramian inverses on the fold-in stream before the micro-batch's host parse, so the
+# certified fp64 inverse kernel runs under it (ORYX_SPEED_PREFETCH_INV=0: after the parse)
+_PREFETCH_INV = os.environ.get("ORYX_SPEED_PREFETCH_INV", "1") != "0"
 
 __all__ = ["ALSSpeedModel", "ALSSpeedModelManager"]
 
@@ -148,9 +153,11 @@ class ALSSpeedModel(SpeedModel):
 
     def prefetch_inverses(self, stream=None) -> None:
         """Queue the device Gramians + Cholesky inverses for the current factors (on
-        ``stream``) without waiting; :meth:`solver_inverses` then only collects them.  (Not
-        called per interval: at rank 64 the ~0.6 ms of GPU work is mostly host launch time,
-        which moved into the parse phase instead of hiding -- r3_speed_profile_*.)"""
+        ``stream``) without waiting; :meth:`solver_inverses` then only collects them.  Called
+        before each GPU micro-batch's host parse (``_PREFETCH_INV``): since the inverses became
+        one fused launch (``spd_inverse_pair``, ~0.11 ms on the device) the launch is cheap; in
+        round 3 the ~0.6 ms of separate launches only moved into the parse phase
+        (r3_speed_profile_*)."""
         if self.device is None or self.device.type != "cuda":
             return
         key = (self.X.version, self.Y.version)
@@ -380,6 +387,11 @@ class ALSSpeedModelManager(SpeedModelManager):
             if self._batch is None:
                 self._batch = ingest.SpeedBatch()
             sb = self._batch
+            if _PREFETCH_INV:
+                try:
+                    model.prefetch_inverses(self._device_stream(dev))
+                except mathx.SingularMatrixSolverException:
+                    pass          # solver_inverses reports it after the parse, as before
             xm, ym = model.X.synced_rowmap(), model.Y.synced_rowmap()
             with model.X.read_lock(), model.Y.read_lock():
                 sb.parse(new_data.values(), xm, ym, default_ts=0)
