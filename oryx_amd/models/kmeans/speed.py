@@ -136,9 +136,12 @@ class KMeansSpeedModelManager(SpeedModelManager):
         mean = sums[touched] / nt[:, None].to(torch.float64)
         frac = nt.to(torch.float64) / total.to(torch.float64)
         new_c = c + frac[:, None] * (mean - c)
-        pos_h = touched.cpu().numpy()
-        new_h = new_c.cpu().numpy()
-        tot_h = total.cpu().numpy()
+        # one copy to the host: [position, center..., count] rows (integers exact in fp64)
+        packed = torch.cat([touched.to(torch.float64)[:, None], new_c,
+                            total.to(torch.float64)[:, None]], 1).cpu().numpy()
+        pos_h = packed[:, 0].astype(np.int64)
+        new_h = np.ascontiguousarray(packed[:, 1:d + 1])
+        tot_h = packed[:, d + 1].astype(np.int64)
         t2 = time.perf_counter()
         cs.set_many(pos_h.tolist(), new_h, tot_h.tolist(),
                     device_update=(touched, new_c, total))
