@@ -3148,6 +3148,61 @@ char* write_double_repr(double v, char* o) {
 
 extern "C" {
 
+// The lines of oryx_format_cluster_updates from the centers' texts already formatted into
+// 24-byte slots (slots[(j d + f) 24], lens[j d + f]: csrc/kernels/fmt64.hip on the device).
+// Returns bytes, or -(bytes needed).
+long long oryx_format_cluster_updates_slots(const long long* ids, const char* slots,
+                                            const unsigned char* lens, const long long* counts,
+                                            long long n, int d, char* out, long long cap,
+                                            long long* ends) {
+  std::vector<long long> off((size_t)n + 1, 0);
+  oryx_ff::parallel_ranges(n, 64, [&](long long lo, long long hi, int) {
+    char b[24];
+    for (long long j = lo; j < hi; ++j) {
+      long long L = 1 + snprintf(b, sizeof(b), "%lld", ids[j]) + 2 + (d > 0 ? d - 1 : 0) + 2 +
+                    snprintf(b, sizeof(b), "%lld", counts[j]) + 1;
+      const unsigned char* lj = lens + j * d;
+      for (int f = 0; f < d; ++f) L += lj[f];
+      off[(size_t)j + 1] = L + 1;   // and its '\n'
+    }
+  });
+  for (long long j = 0; j < n; ++j) off[(size_t)j + 1] += off[(size_t)j];
+  if (off[(size_t)n] > cap) return -off[(size_t)n];
+  oryx_ff::parallel_ranges(n, 64, [&](long long lo, long long hi, int) {
+    for (long long j = lo; j < hi; ++j) {
+      char* o = out + off[(size_t)j];
+      *o++ = '[';
+      o += snprintf(o, 24, "%lld", ids[j]);
+      *o++ = ',';
+      *o++ = '[';
+      for (int f = 0; f < d; ++f) {
+        if (f) *o++ = ',';
+        const long long k = j * d + f;
+        memcpy(o, slots + k * 24, lens[k]);
+        o += lens[k];
+      }
+      *o++ = ']';
+      *o++ = ',';
+      o += snprintf(o, 24, "%lld", counts[j]);
+      *o++ = ']';
+      ends[j] = (long long)(o - out);
+      *o = '\n';
+    }
+  });
+  return off[(size_t)n];
+}
+
+// Python repr of v[0..n) into 24-byte slots, lens[j] = the text's length (the reference for
+// the device formatter, csrc/kernels/fmt64.hip, and its checks).
+void oryx_format_f64_repr_host(const double* v, long long n, char* slots, unsigned char* lens) {
+  oryx_ff::parallel_ranges(n, 4096, [&](long long lo, long long hi, int) {
+    for (long long j = lo; j < hi; ++j) {
+      char* o = slots + j * 24;
+      lens[j] = (unsigned char)(write_double_repr(v[j], o) - o);
+    }
+  });
+}
+
 // n lines "[id,[c_0,...,c_{d-1}],count]" ('\n' after each) for the rows of centers [n][d];
 // ends[j] = end of line j (before its '\n').  Returns bytes, or -(bytes needed).
 long long oryx_format_cluster_updates(const long long* ids, const double* centers,

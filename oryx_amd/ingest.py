@@ -567,17 +567,57 @@ def format_leaf_updates(trees, id_blob, id_ends, idx, counts, nc: int, means=Non
         cap = -used
 
 
-def format_cluster_updates(ids, centers, counts):
+def f64_repr_slots(values):
+    """(slots uint8 [n, 24], lens uint8 [n]): Python repr text of each double of a 1-D
+    device tensor formatted on the GPU (``csrc/kernels/fmt64.hip``), or of a host array by the
+    native host formatter (the reference the device output is held to)."""
+    import torch
+    if torch.is_tensor(values) and values.is_cuda:
+        v = values.detach().to(torch.float64).contiguous().reshape(-1)
+        n = v.numel()
+        slots = torch.empty((max(n, 1), 24), dtype=torch.uint8, device=v.device)
+        lens = torch.empty(max(n, 1), dtype=torch.uint8, device=v.device)
+        native.check(native.require_kernels().oryx_format_f64_slots(
+            v.data_ptr(), n, slots.data_ptr(), lens.data_ptr(), native.stream_ptr(v.device)),
+            "oryx_format_f64_slots")
+        both = torch.cat([slots[:n].reshape(-1), lens[:n]])
+        host = torch.empty(both.numel(), dtype=torch.uint8, pin_memory=True)
+        host.copy_(both)
+        h = host.numpy()
+        return h[:24 * n].reshape(n, 24), h[24 * n:]
+    v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1)
+    n = len(v)
+    slots = np.empty((n, 24), dtype=np.uint8)
+    lens = np.empty(n, dtype=np.uint8)
+    if n:
+        native.runtime().oryx_format_f64_repr_host(_ptr(v), n, _ptr(slots), _ptr(lens))
+    return slots, lens
+
+
+def format_cluster_updates(ids, centers, counts, device_centers=None):
     """k-means speed-layer update messages ``[id,[center...],count]`` (one per row of
     ``centers`` [n, d] float64) as a :class:`~oryx_amd.api.MessageBlock`, byte-identical to
-    ``text.join_json([id, [float(v) ...], count])`` (native, threaded)."""
+    ``text.join_json([id, [float(v) ...], count])`` (native, threaded).  ``device_centers``:
+    the same values as a device tensor -- their text is then formatted on the GPU
+    (:func:`f64_repr_slots`) and only assembled on the host."""
     from .api import MessageBlock
     ids = np.ascontiguousarray(ids, dtype=np.int64)
-    centers = np.ascontiguousarray(centers, dtype=np.float64)
     counts = np.ascontiguousarray(counts, dtype=np.int64)
     n = len(ids)
     if n == 0:
         return MessageBlock(b"", np.zeros(0, dtype=np.int64))
+    if device_centers is not None and native.kernels_available():
+        d = int(device_centers.shape[1])
+        slots, lens = f64_repr_slots(device_centers)
+        ends = np.empty(n, dtype=np.int64)
+        cap = int(lens.astype(np.int64).sum()) + n * (d + 48)
+        out = _host_buffer(cap)
+        used = native.runtime().oryx_format_cluster_updates_slots(
+            _ptr(ids), _ptr(slots), _ptr(lens), _ptr(counts), n, d, _ptr(out), cap, _ptr(ends))
+        if used < 0:
+            raise RuntimeError("cluster update text larger than its bound")
+        return MessageBlock(out[:used], ends)
+    centers = np.ascontiguousarray(centers, dtype=np.float64)
     d = centers.shape[1]
     ends = np.empty(n, dtype=np.int64)
     cap = n * (52 + 25 * d)

@@ -147,7 +147,7 @@ class KMeansSpeedModelManager(SpeedModelManager):
                     device_update=(touched, new_c, total))
         ids = np.array([cs.clusters[p].id for p in pos_h.tolist()], dtype=np.int64)
         t3 = time.perf_counter()
-        out = ingest.format_cluster_updates(ids, new_h, tot_h)
+        out = ingest.format_cluster_updates(ids, new_h, tot_h, device_centers=new_c)
         # milliseconds per phase of the last micro-batch (parse: text -> device matrix;
         # assign_update: nearest clusters, sums, running means, results to the host;
         # set: the model's host / device state; format: the UP messages)

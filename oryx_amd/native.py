@@ -140,6 +140,9 @@ def _register_runtime_extras(lib):
                                                  c_vp, c_vp, c_ll, c_vp])
     _sig(lib, "oryx_format_cluster_updates", c_ll, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_ll,
                                                     c_vp])
+    _sig(lib, "oryx_format_cluster_updates_slots", c_ll, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i,
+                                                          c_vp, c_ll, c_vp])
+    _sig(lib, "oryx_format_f64_repr_host", None, [c_vp, c_ll, c_vp, c_vp])
     # nq, k, kp, max_batch, targets, cand_ptr, cand, cand_all, num_buckets, words,
     # bucket_start, n_rows, ex_ptr, ex_rows, pos_of_row, n_pos, delta_lo, delta_hi, out,
     # out_cap, info
@@ -280,6 +283,7 @@ def _load_kernels():
                                          c_vp, c_vp, c_vp])
     _sig(lib, "oryx_csv_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp, c_i,
                                                 c_vp, c_i, c_vp, c_vp, c_i, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_format_f64_slots", c_i, [c_vp, c_ll, c_vp, c_vp, c_vp])
     _sig(lib, "oryx_csv_wide_lines_to_matrix", c_i, [c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_i,
                                                      c_vp, c_i, c_vp, c_vp, c_vp, c_i, c_vp,
                                                      c_vp, c_vp])

@@ -797,3 +797,28 @@ def test_kmeans_update_evaluation_is_double_precision(tmp_path):
     x32 = x.astype(np.float32).astype(np.float64)
     d32 = ((x32[:, None, :] - cen[None, :, :]) ** 2).sum(2).min(1)
     assert abs(-d32.sum() - ev) > 1e-6 * abs(ev)      # float32 points would differ
+
+
+@pytest.mark.gpu
+def test_device_double_formatter_matches_host(cuda):
+    """fmt64.hip (Ryu on the device) writes the host formatter's bytes for every double, and
+    the cluster update block built from its slots equals the host-formatted one."""
+    from oryx_amd import ingest, native
+    native.require_kernels()
+    from tests.test_speed_batch import _double_cases
+    v = _double_cases(2_000_000, seed=11)
+    hs, hl = ingest.f64_repr_slots(v)
+    ds, dl = ingest.f64_repr_slots(torch.from_numpy(v).to(cuda))
+    assert np.array_equal(hl, dl)
+    mask = np.arange(24)[None, :] < hl[:, None].astype(np.int64)
+    assert np.array_equal(np.where(mask, hs, 0), np.where(mask, ds, 0))
+    g = np.random.default_rng(2)
+    centers = g.standard_normal((300, 256)) * 10.0 ** g.integers(-8, 8, (300, 1))
+    centers[0, :5] = [0.0, -0.0, 1.0, 1e16, 5e-324]
+    ids = g.integers(0, 10 ** 9, 300)
+    counts = g.integers(1, 10 ** 6, 300)
+    host = ingest.format_cluster_updates(ids, centers, counts)
+    dev = ingest.format_cluster_updates(ids, centers, counts,
+                                        device_centers=torch.from_numpy(centers).to(cuda))
+    assert list(host) == list(dev)
+    assert np.array_equal(host.ends, dev.ends)

@@ -260,3 +260,47 @@ def test_publish_blocks_order_errors_and_reuse():
     assert len(bad.got) == 2 and len(made) < 50
     p2 = Prod()
     assert publish_blocks(p2, blocks(3, []), None) == 9 and len(p2.got) == 3
+
+
+def _double_cases(n_random=200000, seed=7):
+    g = np.random.default_rng(seed)
+    bits = g.integers(0, 2 ** 63, n_random, dtype=np.int64).view(np.uint64)
+    bits[: n_random // 2] |= np.uint64(1) << np.uint64(63)
+    vals = [bits.view(np.float64)]
+    ints = g.integers(-2 ** 60, 2 ** 60, 20000).astype(np.float64)
+    vals += [ints, np.nextafter(ints, np.inf), g.integers(0, 10 ** 6, 20000) / 10.0 ** 3,
+             np.ldexp(1.0, np.arange(-1074, 1024)), 10.0 ** np.arange(-300, 300),
+             np.array([0.0, -0.0, np.nan, np.inf, -np.inf, 5e-324, 1.7976931348623157e308,
+                       0.1, 0.2, 0.3, 1e16, 1e15, 123456789012345680.0, 1e-5, 1e-4, 9.5e-5])]
+    return np.concatenate(vals)
+
+
+def test_f64_repr_host_matches_python_repr():
+    """The host double formatter (the reference for the device one) writes Python's repr
+    (json.dumps spelling for NaN / Infinity)."""
+    v = _double_cases(50000)
+    slots, lens = ingest.f64_repr_slots(v)
+    got = [bytes(slots[j, :lens[j]]).decode() for j in range(len(v))]
+    want = [json.dumps(float(x)) for x in v.tolist()]
+    assert got == want
+
+
+def test_ryu_formatter_matches_host_formatter(tmp_path):
+    """csrc/kernels/ryu_d2s.h (the device formatter's algorithm) compiled for the host equals
+    the runtime's formatter byte for byte over random bit patterns, integers, short decimals,
+    powers and running means (csrc/runtime/tests/ryu_check.cpp)."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        import pytest
+        pytest.skip("no g++")
+    from oryx_amd import native
+    native.runtime()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "oryx_amd", "_native")
+    exe = str(tmp_path / "ryu_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(root, "csrc", "kernels"),
+                    os.path.join(root, "csrc", "runtime", "tests", "ryu_check.cpp"),
+                    "-L", lib, "-loryx_runtime", "-Wl,-rpath," + lib, "-o", exe], check=True)
+    r = subprocess.run([exe, "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "all equal" in r.stdout, r.stdout + r.stderr
