@@ -580,9 +580,11 @@ def f64_repr_slots(values):
         native.check(native.require_kernels().oryx_format_f64_slots(
             v.data_ptr(), n, slots.data_ptr(), lens.data_ptr(), native.stream_ptr(v.device)),
             "oryx_format_f64_slots")
-        both = torch.cat([slots[:n].reshape(-1), lens[:n]])
-        host = torch.empty(both.numel(), dtype=torch.uint8, pin_memory=True)
-        host.copy_(both)
+        # both into one pinned block, one wait
+        host = torch.empty(25 * n, dtype=torch.uint8, pin_memory=True)
+        host[:24 * n].copy_(slots[:n].reshape(-1), non_blocking=True)
+        host[24 * n:].copy_(lens[:n], non_blocking=True)
+        torch.cuda.current_stream(v.device).synchronize()
         h = host.numpy()
         return h[:24 * n].reshape(n, 24), h[24 * n:]
     v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1)
@@ -610,7 +612,7 @@ def format_cluster_updates(ids, centers, counts, device_centers=None):
         d = int(device_centers.shape[1])
         slots, lens = f64_repr_slots(device_centers)
         ends = np.empty(n, dtype=np.int64)
-        cap = int(lens.astype(np.int64).sum()) + n * (d + 48)
+        cap = n * (25 * d + 48)
         out = _host_buffer(cap)
         used = native.runtime().oryx_format_cluster_updates_slots(
             _ptr(ids), _ptr(slots), _ptr(lens), _ptr(counts), n, d, _ptr(out), cap, _ptr(ends))
