@@ -15,6 +15,7 @@ namespace {
 
 constexpr int KS_THREADS = 256;
 constexpr int PT = 16;            // points per block
+constexpr int FU = 16;            // features whose center values load together
 
 __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
     const double* __restrict__ X, long long n, int d, const double* __restrict__ CT, int k,
@@ -40,8 +41,26 @@ __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
     double acc[PT];
 #pragma unroll
     for (int r = 0; r < PT; ++r) acc[r] = 0.0;
-    for (int f = 0; f < d; ++f) {
-      const double cv = CT[(long long)f * k + c];
+    // FU features' center values are loaded before they are used: one load in flight per
+    // thread left the kernel waiting on L2 latency (586 us for 10k points x 1000 centers x
+    // 256 dims, profiles/r6_km_speed_kernel_stats_v1.txt).  The sums still run over the
+    // features in order (the host scan's rounding).
+    const double* cp = CT + c;
+    int f0 = 0;
+    for (; f0 + FU <= d; f0 += FU) {
+      double cv[FU];
+#pragma unroll
+      for (int u = 0; u < FU; ++u) cv[u] = cp[(long long)(f0 + u) * k];
+#pragma unroll
+      for (int u = 0; u < FU; ++u)
+#pragma unroll
+        for (int r = 0; r < PT; ++r) {
+          const double df = xs[r * d + f0 + u] - cv[u];
+          acc[r] += df * df;
+        }
+    }
+    for (int f = f0; f < d; ++f) {
+      const double cv = cp[(long long)f * k];
 #pragma unroll
       for (int r = 0; r < PT; ++r) {
         const double df = xs[r * d + f] - cv;

@@ -226,11 +226,11 @@ def h2d(buf: np.ndarray, off: int, nbytes: int, dst: torch.Tensor,
 
 # average line length from which the device parse takes a wave per line instead of a thread
 # (ORYX_CSV_WIDE_MIN_BYTES; a huge value keeps the thread kernel), for up to WIDE_MAX_LINES
-# lines: a speed-layer micro-batch of 10k 2.6 KB lines parses in 0.31 ms instead of 1.41 ms
-# (one thread per line fills 157 waves of the chip), but 12.5M such lines take 0.20 s against
-# the thread kernel's 0.13 s (profiles/r6_km_speed_prof_v2.json, r6_bb_kmeans_v3.json)
+# lines (ORYX_CSV_WIDE_MAX_LINES).  At 256 "%.6f" values per line the wave kernel parses 10k
+# lines in 67 us and 100k in 584 us, the thread kernel in 1043 / 1834 us
+# (profiles/r6_csv_kernel_probe_v2.jsonl, scripts/csv_kernel_probe.py)
 WIDE_LINE_MIN_BYTES = int(os.environ.get("ORYX_CSV_WIDE_MIN_BYTES", "192"))
-WIDE_MAX_LINES = int(os.environ.get("ORYX_CSV_WIDE_MAX_LINES", str(1 << 20)))
+WIDE_MAX_LINES = int(os.environ.get("ORYX_CSV_WIDE_MAX_LINES", str(1 << 62)))
 
 
 def _device_block(buf: np.ndarray, off: int, nbytes: int, n_lines: int, schema: InputSchema,
