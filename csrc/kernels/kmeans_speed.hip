@@ -3,11 +3,15 @@
 // KMeansSpeedModelManager.buildUpdates ([speed-app]/kmeans/KMeansSpeedModelManager.java:
 // 88-125) assigns every point of a micro-batch to its closest cluster by Euclidean distance
 // (KMeansUtils.closestCluster: squared differences summed in double, first strictly smaller
-// distance wins).  Here one launch does a whole micro-batch: a 256-thread block holds PT
-// points in LDS and each thread runs through the clusters c = tid, tid + 256, ... reading the
-// centers from a feature-major copy (C^T [d][k]: consecutive threads read consecutive
-// centers, one coalesced line per feature); the per-point minimum is then reduced over the
-// block with the lowest index winning ties, as the sequential scan picks it.
+// distance wins).  A 256-thread block takes PT points (read by the scalar unit) and each thread runs through the
+// clusters c = c0 + tid, c0 + tid + 256, ... of the block's cluster chunk [c0, c1), reading
+// the centers from a feature-major copy (C^T [d][k]: consecutive threads read consecutive
+// centers, one coalesced line per feature); the per-point minimum is reduced over the block
+// with the lowest index winning ties, and km_nearest_merge takes the chunks in cluster order
+// with the same rule -- the sequential scan's pick.  The chunks give a 10k-point micro-batch
+// 2500 blocks instead of 625: with two resident blocks per CU the single-chunk grid ran two
+// rounds of its longest blocks (586 us for 1000 centers x 256 dims,
+// profiles/r6_km_speed_kernel_stats_v1.txt).
 
 #include "common.h"
 
@@ -15,21 +19,14 @@ namespace {
 
 constexpr int KS_THREADS = 256;
 constexpr int PT = 16;            // points per block
-constexpr int FU = 16;            // features whose center values load together
 
 __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
     const double* __restrict__ X, long long n, int d, const double* __restrict__ CT, int k,
-    long long* __restrict__ out_idx, double* __restrict__ out_dist) {
-  extern __shared__ __attribute__((aligned(16))) double xs[];      // [PT][d]
+    int kc, double* __restrict__ part_best, int* __restrict__ part_idx) {
   __shared__ double rbest[KS_THREADS / 64][PT];
   __shared__ int ridx[KS_THREADS / 64][PT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long p0 = (long long)blockIdx.x * PT;
-  for (int i = tid; i < PT * d; i += KS_THREADS) {
-    const int r = i / d, f = i - r * d;
-    xs[i] = p0 + r < n ? X[(p0 + r) * d + f] : 0.0;
-  }
-  __syncthreads();
   double best[PT];
   int bi[PT];
 #pragma unroll
@@ -37,33 +34,45 @@ __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
     best[r] = INFINITY;
     bi[r] = 0x7fffffff;
   }
-  for (int c = tid; c < k; c += KS_THREADS) {
+  // rows past the batch read the last point (their results are never written)
+  const double* xrow[PT];
+#pragma unroll
+  for (int r = 0; r < PT; ++r) xrow[r] = X + (p0 + r < n ? p0 + r : n - 1) * d;
+  const int chunk = blockIdx.y, nch = gridDim.y;
+  const int c1 = min(k, (chunk + 1) * kc);
+  for (int c = chunk * kc + tid; c < c1; c += KS_THREADS) {
     double acc[PT];
 #pragma unroll
     for (int r = 0; r < PT; ++r) acc[r] = 0.0;
-    // FU features' center values are loaded before they are used: one load in flight per
-    // thread left the kernel waiting on L2 latency (586 us for 10k points x 1000 centers x
-    // 256 dims, profiles/r6_km_speed_kernel_stats_v1.txt).  The sums still run over the
-    // features in order (the host scan's rounding).
+    // the block's points are the same for every lane: read through the scalar unit (s_load
+    // into SGPRs, an operand of each VALU op) instead of 16 broadcast LDS reads per feature,
+    // each waited on; the next feature pair's center values load under this pair's work
+    // (profiles/r6_km_speed_kernel_stats_v*.txt).  The sums run over the features in order.
     const double* cp = CT + c;
-    int f0 = 0;
-    for (; f0 + FU <= d; f0 += FU) {
-      double cv[FU];
-#pragma unroll
-      for (int u = 0; u < FU; ++u) cv[u] = cp[(long long)(f0 + u) * k];
-#pragma unroll
-      for (int u = 0; u < FU; ++u)
-#pragma unroll
-        for (int r = 0; r < PT; ++r) {
-          const double df = xs[r * d + f0 + u] - cv[u];
-          acc[r] += df * df;
-        }
-    }
-    for (int f = f0; f < d; ++f) {
-      const double cv = cp[(long long)f * k];
+    double n0 = cp[0], n1 = cp[(long long)min(1, d - 1) * k];
+    int f = 0;
+    for (; f + 2 <= d; f += 2) {
+      const double cv0 = n0, cv1 = n1;
+      n0 = cp[(long long)min(f + 2, d - 1) * k];
+      n1 = cp[(long long)min(f + 3, d - 1) * k];
+      double x0[PT], x1[PT];
 #pragma unroll
       for (int r = 0; r < PT; ++r) {
-        const double df = xs[r * d + f] - cv;
+        x0[r] = xrow[r][f];
+        x1[r] = xrow[r][f + 1];
+      }
+#pragma unroll
+      for (int r = 0; r < PT; ++r) {
+        const double df0 = x0[r] - cv0;
+        acc[r] += df0 * df0;
+        const double df1 = x1[r] - cv1;
+        acc[r] += df1 * df1;
+      }
+    }
+    if (f < d) {   // an odd feature count's last feature
+#pragma unroll
+      for (int r = 0; r < PT; ++r) {
+        const double df = xrow[r][f] - n0;
         acc[r] += df * df;
       }
     }
@@ -105,9 +114,31 @@ __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
         i = oi;
       }
     }
-    out_idx[p0 + tid] = i;
-    out_dist[p0 + tid] = sqrt(b);
+    part_best[(p0 + tid) * nch + chunk] = b;
+    part_idx[(p0 + tid) * nch + chunk] = i;
   }
+}
+
+// per point: the chunks' minima in cluster order, strictly smaller wins (ties stay with the
+// lower cluster index); a chunk with no clusters reports +inf
+__global__ __launch_bounds__(256) void km_nearest_merge(const double* __restrict__ part_best,
+                                                        const int* __restrict__ part_idx,
+                                                        long long n, int nch,
+                                                        long long* __restrict__ out_idx,
+                                                        double* __restrict__ out_dist) {
+  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= n) return;
+  double b = part_best[p * nch];
+  int i = part_idx[p * nch];
+  for (int j = 1; j < nch; ++j) {
+    const double ob = part_best[p * nch + j];
+    if (ob < b) {
+      b = ob;
+      i = part_idx[p * nch + j];
+    }
+  }
+  out_idx[p] = i;
+  out_dist[p] = sqrt(b);
 }
 
 }  // namespace
@@ -115,16 +146,32 @@ __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
 extern "C" {
 
 // X [n][d] fp64 points, CT [d][k] fp64 centers feature-major; out_idx [n] (cluster position),
-// out_dist [n] (Euclidean distance).  d <= 1024 (PT points of d doubles in LDS).
+// out_dist [n] (Euclidean distance).  part_best /
+// part_idx: scratch of n * oryx_kmeans_nearest_chunks(n, k) entries.
+int oryx_kmeans_nearest_chunks(long long n, int k) {
+  // about 2048 blocks, chunks of at least one cluster per thread
+  const long long pb = (n + PT - 1) / PT;
+  long long ch = (2048 + pb - 1) / pb;
+  const long long most = (k + KS_THREADS - 1) / KS_THREADS;
+  if (ch > most) ch = most;
+  return (int)(ch < 1 ? 1 : ch);
+}
+
 int oryx_kmeans_nearest_f64(const double* X, long long n, int d, const double* CT, int k,
-                            long long* out_idx, double* out_dist, void* stream) {
+                            long long* out_idx, double* out_dist, double* part_best,
+                            int* part_idx, void* stream) {
   if (n <= 0) return ORYX_OK;
-  if (d <= 0 || d > 1024 || k <= 0) return ORYX_EINVAL;
-  const int lds = PT * d * (int)sizeof(double);
-  if (lds > 64 * 1024 && !oryx_set_max_lds(&km_nearest_f64, lds)) return ORYX_ELAUNCH;
+  if (d <= 0 || k <= 0) return ORYX_EINVAL;
+  const int nch = oryx_kmeans_nearest_chunks(n, k);
+  const int kc = (k + nch - 1) / nch;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const unsigned blocks = (unsigned)((n + PT - 1) / PT);
-  hipLaunchKernelGGL(km_nearest_f64, dim3(blocks), dim3(KS_THREADS), lds,
-                     reinterpret_cast<hipStream_t>(stream), X, n, d, CT, k, out_idx, out_dist);
+  hipLaunchKernelGGL(km_nearest_f64, dim3(blocks, (unsigned)nch), dim3(KS_THREADS), 0, s, X,
+                     n, d, CT, k, kc, part_best, part_idx);
+  const int rc = oryx_check_launch();
+  if (rc != ORYX_OK) return rc;
+  hipLaunchKernelGGL(km_nearest_merge, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                     part_best, part_idx, n, nch, out_idx, out_dist);
   return oryx_check_launch();
 }
 

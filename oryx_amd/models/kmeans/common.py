@@ -314,9 +314,15 @@ class ClusterSet:
         n, d = x.shape
         idx = torch.empty(n, dtype=torch.int64, device=x.device)
         dist = torch.empty(n, dtype=torch.float64, device=x.device)
-        rc = native.require_kernels().oryx_kmeans_nearest_f64(
-            x.data_ptr(), n, d, ct.data_ptr(), int(ct.shape[1]), idx.data_ptr(),
-            dist.data_ptr(), native.stream_ptr(x.device))
+        lib = native.require_kernels()
+        k = int(ct.shape[1])
+        # per-point minima of each cluster chunk, merged by the kernel's second pass
+        nch = int(lib.oryx_kmeans_nearest_chunks(n, k))
+        part_b = torch.empty(max(n * nch, 1), dtype=torch.float64, device=x.device)
+        part_i = torch.empty(max(n * nch, 1), dtype=torch.int32, device=x.device)
+        rc = lib.oryx_kmeans_nearest_f64(
+            x.data_ptr(), n, d, ct.data_ptr(), k, idx.data_ptr(), dist.data_ptr(),
+            part_b.data_ptr(), part_i.data_ptr(), native.stream_ptr(x.device))
         native.check(rc, "oryx_kmeans_nearest_f64")
         return idx, dist
 

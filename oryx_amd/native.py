@@ -26,7 +26,7 @@ _kernels_error = None
 
 # must equal oryx_kernels_version() in csrc/kernels/als.hip; bump both whenever an exported
 # kernel entry point's signature or semantics change
-KERNELS_ABI_VERSION = 28
+KERNELS_ABI_VERSION = 29
 
 c_vp = ctypes.c_void_p
 c_i = ctypes.c_int
@@ -263,7 +263,9 @@ def _load_kernels():
         _sig(lib, "oryx_als_debug_gram", c_i, [c_vp, c_vp, c_vp, c_vp, c_i, c_f, c_i, c_ll,
                                                c_ll, c_vp, c_i, c_vp])
     _sig(lib, "oryx_gramian_f32", c_i, [c_vp, c_ll, c_i, c_i, c_vp, c_vp, c_vp])
-    _sig(lib, "oryx_kmeans_nearest_f64", c_i, [c_vp, c_ll, c_i, c_vp, c_i, c_vp, c_vp, c_vp])
+    _sig(lib, "oryx_kmeans_nearest_chunks", c_i, [c_ll, c_i])
+    _sig(lib, "oryx_kmeans_nearest_f64", c_i, [c_vp, c_ll, c_i, c_vp, c_i, c_vp, c_vp, c_vp, c_vp,
+                                               c_vp])
     _sig(lib, "oryx_spd_inverse_pair", c_i, [c_vp, c_vp, c_i, c_vp, c_vp, ctypes.c_double,
                                              c_vp, c_vp])
     _sig(lib, "oryx_pair_dots", c_i, [c_vp, c_vp, c_vp, c_vp, c_ll, c_i, c_vp, c_vp])

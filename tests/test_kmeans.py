@@ -822,3 +822,28 @@ def test_device_double_formatter_matches_host(cuda):
                                         device_centers=torch.from_numpy(centers).to(cuda))
     assert list(host) == list(dev)
     assert np.array_equal(host.ends, dev.ends)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k,d", [(3000, 77, 37), (1000, 600, 1), (257, 1000, 256)])
+def test_device_nearest_matches_sequential_scan(cuda, n, k, d):
+    """oryx_kmeans_nearest_f64 (cluster chunks merged in order, points through the scalar
+    unit) == the sequential scan: squared differences summed over the features in order, the
+    first strictly smaller distance winning -- the same indices, odd feature counts and
+    duplicate centers (ties) included; distances to the rounding of the kernel's fused
+    multiply-adds (the scan here rounds the square and the sum separately)."""
+    from oryx_amd.models.kmeans.common import ClusterSet
+    g = np.random.default_rng(n + k + d)
+    centers = g.standard_normal((k, d))
+    centers[k // 2] = centers[k // 3]            # a tie: the lower index must win
+    x = centers[g.integers(0, k, n)] + 0.3 * g.standard_normal((n, d))
+    cs = ClusterSet([ClusterInfo(j, centers[j], 1) for j in range(k)], torch.device(cuda))
+    idx, dist = cs.nearest_batch_device(torch.from_numpy(x).to(cuda))
+    acc = np.zeros((n, k))
+    for f in range(d):
+        df = x[:, f, None] - centers[None, :, f]
+        acc += df * df
+    want = np.argmin(acc, axis=1)                # first occurrence of the minimum
+    assert np.array_equal(idx.cpu().numpy(), want)
+    np.testing.assert_allclose(dist.cpu().numpy(), np.sqrt(acc[np.arange(n), want]),
+                               rtol=1e-14, atol=0)
