@@ -19,14 +19,20 @@ namespace {
 
 constexpr int KS_THREADS = 256;
 constexpr int PT = 16;            // points per block
+constexpr int FA = 4;             // features whose center values load ahead (even)
 
+// D > 0: the feature count at compile time (the point rows' offsets become immediates of the
+// scalar loads, sparing the SGPRs 16 row pointers); D = 0: d at run time.  n >= PT: the
+// last block starts at n - PT (it overlaps the one before it; both write the same values).
+template <int D>
 __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
-    const double* __restrict__ X, long long n, int d, const double* __restrict__ CT, int k,
+    const double* __restrict__ X, long long n, int d_rt, const double* __restrict__ CT, int k,
     int kc, double* __restrict__ part_best, int* __restrict__ part_idx) {
+  const int d = D > 0 ? D : d_rt;
   __shared__ double rbest[KS_THREADS / 64][PT];
   __shared__ int ridx[KS_THREADS / 64][PT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const long long p0 = (long long)blockIdx.x * PT;
+  const long long p0 = min((long long)blockIdx.x * PT, n - PT);
   double best[PT];
   int bi[PT];
 #pragma unroll
@@ -34,10 +40,7 @@ __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
     best[r] = INFINITY;
     bi[r] = 0x7fffffff;
   }
-  // rows past the batch read the last point (their results are never written)
-  const double* xrow[PT];
-#pragma unroll
-  for (int r = 0; r < PT; ++r) xrow[r] = X + (p0 + r < n ? p0 + r : n - 1) * d;
+  const double* xb = X + p0 * d;   // the block's PT rows, d apart
   const int chunk = blockIdx.y, nch = gridDim.y;
   const int c1 = min(k, (chunk + 1) * kc);
   for (int c = chunk * kc + tid; c < c1; c += KS_THREADS) {
@@ -46,34 +49,45 @@ __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
     for (int r = 0; r < PT; ++r) acc[r] = 0.0;
     // the block's points are the same for every lane: read through the scalar unit (s_load
     // into SGPRs, an operand of each VALU op) instead of 16 broadcast LDS reads per feature,
-    // each waited on; the next feature pair's center values load under this pair's work
+    // each waited on; the next FA features' center values load under this FA's work
     // (profiles/r6_km_speed_kernel_stats_v*.txt).  The sums run over the features in order.
     const double* cp = CT + c;
-    double n0 = cp[0], n1 = cp[(long long)min(1, d - 1) * k];
+    // center values FA features ahead (an L2 read takes longer than one feature pair's work)
+    double cur[FA], nxt[FA];
+#pragma unroll
+    for (int u = 0; u < FA; ++u) cur[u] = cp[(long long)min(u, d - 1) * k];
     int f = 0;
-    for (; f + 2 <= d; f += 2) {
-      const double cv0 = n0, cv1 = n1;
-      n0 = cp[(long long)min(f + 2, d - 1) * k];
-      n1 = cp[(long long)min(f + 3, d - 1) * k];
-      double x0[PT], x1[PT];
+    for (; f + FA <= d; f += FA) {
 #pragma unroll
-      for (int r = 0; r < PT; ++r) {
-        x0[r] = xrow[r][f];
-        x1[r] = xrow[r][f + 1];
+      for (int u = 0; u < FA; ++u) nxt[u] = cp[(long long)min(f + FA + u, d - 1) * k];
+#pragma unroll
+      for (int u = 0; u < FA; u += 2) {
+        double x0[PT], x1[PT];
+#pragma unroll
+        for (int r = 0; r < PT; ++r) {
+          x0[r] = xb[r * d + f + u];
+          x1[r] = xb[r * d + f + u + 1];
+        }
+#pragma unroll
+        for (int r = 0; r < PT; ++r) {
+          const double df0 = x0[r] - cur[u];
+          acc[r] += df0 * df0;
+          const double df1 = x1[r] - cur[u + 1];
+          acc[r] += df1 * df1;
+        }
       }
 #pragma unroll
-      for (int r = 0; r < PT; ++r) {
-        const double df0 = x0[r] - cv0;
-        acc[r] += df0 * df0;
-        const double df1 = x1[r] - cv1;
-        acc[r] += df1 * df1;
-      }
+      for (int u = 0; u < FA; ++u) cur[u] = nxt[u];
     }
-    if (f < d) {   // an odd feature count's last feature
+    // the last d % FA features (their center values are in cur)
 #pragma unroll
-      for (int r = 0; r < PT; ++r) {
-        const double df = xrow[r][f] - n0;
-        acc[r] += df * df;
+    for (int u = 0; u < FA - 1; ++u) {
+      if (f + u < d) {
+#pragma unroll
+        for (int r = 0; r < PT; ++r) {
+          const double df = xb[r * d + f + u] - cur[u];
+          acc[r] += df * df;
+        }
       }
     }
 #pragma unroll
@@ -103,7 +117,7 @@ __global__ __launch_bounds__(KS_THREADS) void km_nearest_f64(
     }
   }
   __syncthreads();
-  if (tid < PT && p0 + tid < n) {
+  if (tid < PT) {
     double b = rbest[0][tid];
     int i = ridx[0][tid];
     for (int w = 1; w < KS_THREADS / 64; ++w) {
@@ -145,7 +159,8 @@ __global__ __launch_bounds__(256) void km_nearest_merge(const double* __restrict
 
 extern "C" {
 
-// X [n][d] fp64 points, CT [d][k] fp64 centers feature-major; out_idx [n] (cluster position),
+// X [n][d] fp64 points (n >= 16), CT [d][k] fp64 centers feature-major; out_idx [n] (cluster
+// position),
 // out_dist [n] (Euclidean distance).  part_best /
 // part_idx: scratch of n * oryx_kmeans_nearest_chunks(n, k) entries.
 int oryx_kmeans_nearest_chunks(long long n, int k) {
@@ -161,13 +176,17 @@ int oryx_kmeans_nearest_f64(const double* X, long long n, int d, const double* C
                             long long* out_idx, double* out_dist, double* part_best,
                             int* part_idx, void* stream) {
   if (n <= 0) return ORYX_OK;
-  if (d <= 0 || k <= 0) return ORYX_EINVAL;
+  if (d <= 0 || k <= 0 || n < PT) return ORYX_EINVAL;   // (the caller pads to PT points)
   const int nch = oryx_kmeans_nearest_chunks(n, k);
   const int kc = (k + nch - 1) / nch;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const unsigned blocks = (unsigned)((n + PT - 1) / PT);
-  hipLaunchKernelGGL(km_nearest_f64, dim3(blocks, (unsigned)nch), dim3(KS_THREADS), 0, s, X,
-                     n, d, CT, k, kc, part_best, part_idx);
+  if (d == 256)
+    hipLaunchKernelGGL(km_nearest_f64<256>, dim3(blocks, (unsigned)nch), dim3(KS_THREADS), 0, s,
+                       X, n, d, CT, k, kc, part_best, part_idx);
+  else
+    hipLaunchKernelGGL(km_nearest_f64<0>, dim3(blocks, (unsigned)nch), dim3(KS_THREADS), 0, s,
+                       X, n, d, CT, k, kc, part_best, part_idx);
   const int rc = oryx_check_launch();
   if (rc != ORYX_OK) return rc;
   hipLaunchKernelGGL(km_nearest_merge, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,

@@ -311,6 +311,9 @@ class ClusterSet:
         from ... import native
         _, ct, _ = self.device_state()
         x = x.to(torch.float64).contiguous()
+        n0 = x.shape[0]
+        if 0 < n0 < 16:       # the kernel takes at least 16 points: repeat the last one
+            x = torch.cat([x, x[-1:].expand(16 - n0, -1)]).contiguous()
         n, d = x.shape
         idx = torch.empty(n, dtype=torch.int64, device=x.device)
         dist = torch.empty(n, dtype=torch.float64, device=x.device)
@@ -324,7 +327,7 @@ class ClusterSet:
             x.data_ptr(), n, d, ct.data_ptr(), k, idx.data_ptr(), dist.data_ptr(),
             part_b.data_ptr(), part_i.data_ptr(), native.stream_ptr(x.device))
         native.check(rc, "oryx_kmeans_nearest_f64")
-        return idx, dist
+        return idx[:n0], dist[:n0]
 
     def nearest_batch(self, x: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
         """(positions int64 [n], Euclidean distances float64 [n]) for points ``x``.
