@@ -50,16 +50,20 @@ class ClusterInfo:
         self.count = int(initial_count)
         self._lock = threading.Lock()
 
+    # instances built by _owned share this lock (update() is rare on them)
+    _lock = threading.Lock()
+
     @classmethod
-    def _owned(cls, id_: int, center: np.ndarray, count: int) -> "ClusterInfo":
-        """No validation and no copy: ``center`` is a float64 row the caller hands over (the
-        speed layer's 1k-cluster updates spent ~1 ms in the checked constructor)."""
-        self = cls.__new__(cls)
-        self.id = id_
-        self.center = center
-        self.count = count
-        self._lock = threading.Lock()
-        return self
+    def _owned_many(cls, ids, rows, counts) -> List["ClusterInfo"]:
+        """No validation and no copies: ``rows`` are float64 center rows the caller hands
+        over (the speed layer's 1k-cluster updates spent ~1 ms in the checked constructor)."""
+        new = cls.__new__
+        out = []
+        for i, row, c in zip(ids, rows, counts):
+            info = new(cls)
+            info.__dict__ = {"id": i, "center": row, "count": c}
+            out.append(info)
+        return out
 
     def get_id(self) -> int:
         return self.id
@@ -285,13 +289,16 @@ class ClusterSet:
         host ``centers`` rows are then kept without a copy."""
         with self._lock:
             owned = device_update is not None
-            for j, pos in enumerate(positions):
-                old = self.clusters[pos]
-                if owned:
-                    info = ClusterInfo._owned(old.id, centers[j], int(counts[j]))
-                else:
-                    info = ClusterInfo(old.id, centers[j], int(counts[j]))
-                self.clusters[pos] = info
+            if owned:
+                cl = self.clusters
+                infos = ClusterInfo._owned_many([cl[p].id for p in positions], list(centers),
+                                                [int(c) for c in counts])
+                for pos, info in zip(positions, infos):
+                    cl[pos] = info
+            else:
+                for j, pos in enumerate(positions):
+                    old = self.clusters[pos]
+                    self.clusters[pos] = ClusterInfo(old.id, centers[j], int(counts[j]))
             st = getattr(self, "_dev_state", None)
             current = (st is not None and st[0] == self._version and
                        self._dev_version == self._version)
