@@ -374,7 +374,7 @@ int oryx_als_batch_profile(unsigned long long* prof) {
 // 1 when the superseded kernels (tuning/als_variants.hip) are linked into this library
 int oryx_als_tuning_available() { return oryx_als_solve_variant ? 1 : 0; }
 
-int oryx_kernels_version() { return 28; }
+int oryx_kernels_version() { return 29; }
 
 int oryx_als_ws_stride(int kp) { return ws_stride(kp); }
 
