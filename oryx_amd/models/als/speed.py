@@ -39,6 +39,9 @@ from .common import FeatureVectors
 # queue the Gramian inverses on the fold-in stream before the micro-batch's host parse, so the
 # certified fp64 inverse kernel runs under it (ORYX_SPEED_PREFETCH_INV=0: after the parse)
 _PREFETCH_INV = os.environ.get("ORYX_SPEED_PREFETCH_INV", "1") != "0"
+# blocks per micro-batch on the GPU path (build_update_blocks' chunks=None): each block's row
+# text is copied to the host just before the block is handed to the publisher
+_SPEED_CHUNKS = int(os.environ.get("ORYX_SPEED_CHUNKS", "1"))
 
 __all__ = ["ALSSpeedModel", "ALSSpeedModelManager"]
 
@@ -277,6 +280,7 @@ class ALSSpeedModelManager(SpeedModelManager):
         self._stream = None
         self._dicts = None
         self._batch = None     # ingest.SpeedBatch of the GPU path (reused)
+        self._text_ws: dict = {}   # device buffer of the UP rows' text (textfmt)
         self._warmed = None    # the model last warmed (ALSSpeedModel.warm) once loaded
         self.warm_s: Optional[float] = None
         # milliseconds per phase of the last build_updates (parse_aggregate, inverses, lookup
@@ -367,7 +371,7 @@ class ALSSpeedModelManager(SpeedModelManager):
             return []
         return blocks[0] if len(blocks) == 1 else [m for b in blocks for m in b]
 
-    def build_update_blocks(self, new_data: Dataset, chunks: int = 1):
+    def build_update_blocks(self, new_data: Dataset, chunks: Optional[int] = None):
         """The interval's UP messages as a generator of blocks over consecutive event ranges
         (the same messages in the same order as :meth:`build_updates`): a publisher appends
         block j on another thread while block j + 1 is assembled
@@ -512,24 +516,29 @@ class ALSSpeedModelManager(SpeedModelManager):
             native.check(rc, "oryx_als_foldin")
             ph["foldin"] = (time.perf_counter() - t0) * 1e3
             t0 = time.perf_counter()
-            # the updated rows become JSON text on the device (csrc/kernels/textfmt.hip);
-            # only the text crosses to the host, after the row ends and the validity flags
-            # (two host round trips for the whole fold-in)
-            rows, valid = textfmt.format_rows_and(new, flags)
-        xend = int(rows.ends[n - 1])
-        xrows = textfmt.RowText(rows.blob[:xend], rows.ends[:n])
-        yrows = textfmt.RowText(rows.blob[xend:], rows.ends[n:] - xend)
+            # the updated rows become JSON text on the device (csrc/kernels/textfmt.hip); the
+            # row ends and validity flags come back first, then the text of each block's rows
+            # just before the block is handed on, so a block's append (on the publisher's
+            # thread) overlaps the next block's copy
+            rows, valid = textfmt.format_rows_device(new, flags, self._text_ws)
         ph["format_rows"] = (time.perf_counter() - t0) * 1e3
         ph["assemble"] = 0.0
         vxh, vyh = valid[:n] > 0, valid[n:] > 0
-        chunks = max(1, min(int(chunks), n // 1024 or 1))
+        chunks = max(1, min(int(chunks or _SPEED_CHUNKS), n // 1024 or 1))
+        # x rows are rows [0, n) of the formatted matrix, y rows [n, 2n): one view each over
+        # the host buffer, filled per block
+        xrows, yrows = rows.view(0, n), rows.view(n, 2 * n)
         for c in range(chunks):
+            t0 = time.perf_counter()
+            lo, hi = n * c // chunks, n * (c + 1) // chunks
+            with torch.cuda.stream(stream):
+                rows.fetch([(lo, hi), (n + lo, n + hi)])
+            ph["format_rows"] += (time.perf_counter() - t0) * 1e3
             t0 = time.perf_counter()
             # formatted by the log's writer threads straight into the update-log segment
             # when published to a native topic (ingest.DeferredUpBlock), so the assembly
             # time shows in the append
-            blk = sb.deferred(n * c // chunks, n * (c + 1) // chunks, xrows, yrows, vxh, vyh,
-                              not self.no_known_items)
+            blk = sb.deferred(lo, hi, xrows, yrows, vxh, vyh, not self.no_known_items)
             ph["assemble"] += (time.perf_counter() - t0) * 1e3
             yield blk
 

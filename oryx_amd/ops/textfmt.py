@@ -14,7 +14,7 @@ the text crosses to the host; host rows use the native formatter of
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List
+from typing import List, Optional
 
 import numpy as np
 import torch
@@ -128,6 +128,66 @@ def format_rows_and(mat: torch.Tensor, extra: torch.Tensor):
     host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
     host.copy_(ws[:total])
     return RowText(host.numpy(), small[:n]), small[n:]
+
+
+class DeviceRowText:
+    """Rows formatted by :func:`format_rows_device`: the text still on the device, its row
+    ends on the host, and a pinned host buffer of the text's size that :meth:`fetch` fills
+    range by range (so a consumer can start on the first rows while later ones copy)."""
+
+    def __init__(self, ws: torch.Tensor, ends: np.ndarray):
+        self.ws = ws
+        self.ends = ends
+        total = int(ends[-1]) if len(ends) else 0
+        self.host = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
+        self.blob = self.host.numpy()
+
+    def fetch(self, ranges) -> None:
+        """Copy the text of the row ranges [(lo, hi), ...] to the host buffer (one wait)."""
+        for lo, hi in ranges:
+            if hi <= lo:
+                continue
+            a = int(self.ends[lo - 1]) if lo else 0
+            b = int(self.ends[hi - 1])
+            if b > a:
+                self.host[a:b].copy_(self.ws[a:b], non_blocking=True)
+        torch.cuda.current_stream(self.ws.device).synchronize()
+
+    def view(self, lo: int, hi: int) -> RowText:
+        """RowText of rows [lo, hi) over the host buffer (offsets relative to row lo)."""
+        a = int(self.ends[lo - 1]) if lo else 0
+        return RowText(self.blob[a:int(self.ends[hi - 1]) if hi else a], self.ends[lo:hi] - a)
+
+
+def format_rows_device(mat: torch.Tensor, extra: torch.Tensor, cache: Optional[dict] = None):
+    """:func:`format_rows_and` without the text's copy: (DeviceRowText, extra on the host)
+    after one small round trip (row ends + ``extra``).  ``cache``: the caller's own dict for
+    the device text buffer (the text stays there while the caller fetches it, so it must not
+    share the module's buffer with other formatting threads)."""
+    m = mat.detach()
+    if m.dtype != torch.float32 or m.dim() != 2 or m.stride(1) != 1 or m.device.type != "cuda":
+        raise ValueError("need a row-contiguous 2-D float32 device matrix")
+    n, k = m.shape
+    lib = native.require_kernels()
+    dev = m.device
+    stream = native.stream_ptr(dev)
+    lens = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    if n:
+        native.check(lib.oryx_format_rows_len(m.data_ptr(), n, k, m.stride(0), lens.data_ptr(),
+                                              stream), "oryx_format_rows_len")
+    ends = torch.cumsum(lens[:n], 0, dtype=torch.int64)
+    bound = max(n * (19 * k + 2), 1)
+    wsc = cache if cache is not None else _TEXT_WS
+    ws = wsc.get(dev)
+    if ws is None or ws.numel() < bound:
+        ws = torch.empty(bound, dtype=torch.uint8, device=dev)
+        wsc[dev] = ws
+    if n:
+        native.check(lib.oryx_format_rows_text(m.data_ptr(), n, k, m.stride(0), ends.data_ptr(),
+                                               lens.data_ptr(), ws.data_ptr(), stream),
+                     "oryx_format_rows_text")
+    small = torch.cat([ends, extra.reshape(-1).to(torch.int64)]).cpu().numpy()
+    return DeviceRowText(ws, small[:n]), small[n:]
 
 
 def format_csv(mat: torch.Tensor, pinned: bool = True) -> RowText:
