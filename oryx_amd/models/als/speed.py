@@ -40,7 +40,9 @@ from .common import FeatureVectors
 # certified fp64 inverse kernel runs under it (ORYX_SPEED_PREFETCH_INV=0: after the parse)
 _PREFETCH_INV = os.environ.get("ORYX_SPEED_PREFETCH_INV", "1") != "0"
 # blocks per micro-batch on the GPU path (build_update_blocks' chunks=None): each block's row
-# text is copied to the host just before the block is handed to the publisher
+# text is copied to the host just before the block is handed to the publisher.  One block:
+# 2 and 4 blocks measured 0.3-0.9 ms slower per 10k events -- each append's fixed cost
+# outweighs the copy it overlaps (profiles/r6_speed_chunks_ab.txt)
 _SPEED_CHUNKS = int(os.environ.get("ORYX_SPEED_CHUNKS", "1"))
 
 __all__ = ["ALSSpeedModel", "ALSSpeedModelManager"]
