@@ -3,19 +3,16 @@
 // KMeansSpeedModelManager.buildUpdates ([speed-app]/kmeans/KMeansSpeedModelManager.java:
 // 88-125) assigns every point of a micro-batch to its closest cluster by Euclidean distance
 // (KMeansUtils.closestCluster: squared differences summed in double, first strictly smaller
-// distance wins).  A 256-thread block takes PT points (read by the scalar unit) and each thread runs through the
-// clusters c = c0 + tid, c0 + tid + 256, ... of the block's cluster chunk [c0, c1), reading
-// the centers from a feature-major copy (C^T [d][k]: consecutive threads read consecutive
-// centers, one coalesced line per feature); the per-point minimum is reduced over the block
-// with the lowest index winning ties, and km_nearest_merge takes the chunks in cluster order
-// with the same rule -- the sequential scan's pick.  The chunks give a 10k-point micro-batch
-// 2500 blocks instead of 625: with two resident blocks per CU the single-chunk grid ran two
-// rounds of its longest blocks (586 us for 1000 centers x 256 dims,
-// profiles/r6_km_speed_kernel_stats_v1.txt).
-
-#include "common.h"
-
-namespace {
+// distance wins).  A 256-thread block takes PT points, read by the scalar unit (SGPR operands
+// of the VALU ops: the same values for every lane), and each thread runs through the clusters
+// c = c0 + tid, c0 + tid + 256, ... of the block's cluster chunk [c0, c1), reading the centers
+// from a feature-major copy (C^T [d][k]: consecutive threads read consecutive centers, one
+// coalesced line per feature) FA features ahead; the per-point minimum is reduced over the
+// block with the lowest index winning ties, and km_nearest_merge takes the chunks in cluster
+// order with the same rule -- the sequential scan's pick.  (The squared differences are
+// accumulated with fused multiply-adds.)  At 10k points x 1000 centers x 256 dims: 264 us;
+// the first version (points broadcast from LDS, one center load in flight, one chunk) took
+// 586 us (profiles/r6_km_speed_kernel_stats_v1.txt, _v2.txt).
 
 constexpr int KS_THREADS = 256;
 constexpr int PT = 8;             // points per block (16: 326 us, 8: 264 us at 10k x 1000 x 256)
