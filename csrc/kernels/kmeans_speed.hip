@@ -14,6 +14,10 @@
 // the first version (points broadcast from LDS, one center load in flight, one chunk) took
 // 586 us (profiles/r6_km_speed_kernel_stats_v1.txt, _v2.txt).
 
+#include "common.h"
+
+namespace {
+
 constexpr int KS_THREADS = 256;
 constexpr int PT = 8;             // points per block (16: 326 us, 8: 264 us at 10k x 1000 x 256)
 constexpr int FA = 4;             // features whose center values load ahead (even)
