@@ -134,17 +134,25 @@ def test_batch_layer_als_end_to_end(tmp_path):
                         break
             except Exception:
                 time.sleep(0.2)
+        # the consumer replays both generations: wait until the second one is completely
+        # loaded and the consumer has warmed it (answers before that may come from the first)
+        xids2 = set(pmmlu.from_string(models[1]).get_extension_content("XIDs"))
+        deadline = time.time() + 30
+        mgr = serving.manager
+        while time.time() < deadline and not (
+                mgr.model is not None and mgr._warmed is mgr.model and
+                mgr.model.get_fraction_loaded() >= 1.0 and
+                xids2 <= set(mgr.model.get_all_user_ids())):
+            time.sleep(0.05)
+        assert mgr.warm_s is not None and mgr._warmed is mgr.model
         uid = sorted(xids)[0]
         req = urllib.request.Request("http://127.0.0.1:%d/recommend/%s?howMany=3" % (port, uid),
                                      headers={"Accept": "application/json"})
         with urllib.request.urlopen(req) as r:
             recs = json.loads(r.read())
         assert 1 <= len(recs) <= 3 and all("id" in x and "value" in x for x in recs)
-        # the consumer warmed the loaded model (update paths taken once, answers unchanged)
-        deadline = time.time() + 30
-        while time.time() < deadline and serving.manager.warm_s is None:
-            time.sleep(0.05)
-        assert serving.manager.warm_s is not None
+        # warming takes the model's update paths once and leaves its answers as they were
+        mgr.model.warm()
         with urllib.request.urlopen(req) as r:
             assert json.loads(r.read()) == recs
         req = urllib.request.Request("http://127.0.0.1:%d/ingest" % port, data=b"U1,I2,3\n",
