@@ -230,8 +230,10 @@ class RDFSpeedModelManager(SpeedModelManager):
             key = (leaves * C + cls[:, None]).reshape(-1)
             cnt = torch.bincount(key, minlength=n_nodes * C).view(n_nodes, C)
             touched = torch.nonzero(cnt.sum(1)).flatten()
-            t_h = touched.cpu().numpy()
-            c_h = cnt[touched].cpu().numpy()
+            # one copy to the host: [node, class counts...] rows
+            packed = torch.cat([touched[:, None], cnt[touched]], 1).cpu().numpy()
+            t_h = np.ascontiguousarray(packed[:, 0])
+            c_h = np.ascontiguousarray(packed[:, 1:])
             out = ingest.format_leaf_updates(model.tree_of[t_h], model.id_blob,
                                              model.id_ends, t_h, c_h, C)
             ph["counts_format"] = (time.perf_counter() - t1) * 1e3
@@ -242,9 +244,13 @@ class RDFSpeedModelManager(SpeedModelManager):
         sums = torch.zeros(n_nodes, dtype=torch.float64, device=dev).index_add_(0, flat_leaf,
                                                                                 vals)
         touched = torch.nonzero(cnt).flatten()
-        t_h = touched.cpu().numpy()
-        n_h = cnt[touched].cpu().numpy()
-        m_h = (sums[touched] / cnt[touched].to(torch.float64)).cpu().numpy()
+        # one copy to the host: [node, count, mean] rows (integers exact in fp64)
+        nt = cnt[touched]
+        packed = torch.stack([touched.to(torch.float64), nt.to(torch.float64),
+                              sums[touched] / nt.to(torch.float64)], 1).cpu().numpy()
+        t_h = packed[:, 0].astype(np.int64)
+        n_h = packed[:, 1].astype(np.int64)
+        m_h = np.ascontiguousarray(packed[:, 2])
         out = ingest.format_leaf_updates(model.tree_of[t_h], model.id_blob, model.id_ends,
                                          t_h, n_h, 0, m_h)
         ph["counts_format"] = (time.perf_counter() - t1) * 1e3
